@@ -1,0 +1,117 @@
+/*
+ * orbgpu.h -- C ABI of the MI355X-native ORB-SLAM3 front-end / local-BA hot path (liborbgpu.so).
+ *
+ * Plain pointers, sizes and int status codes only (no OpenCV, Eigen, torch or C++ types), so the
+ * reference's C++ (through include/orbgpu_cv.hpp) or any FFI can bind it.
+ * Each entry point names the reference interface it replaces (file:line in the reference tree).
+ *
+ * Threading (reference semantics): calls on DIFFERENT handles may run
+ * concurrently from different threads; a single handle is not thread-safe (like one
+ * ORB_SLAM3::ORBextractor object, whose mvImagePyramid is per-object state).
+ */
+#ifndef ORBGPU_H
+#define ORBGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------------------------------- */
+#define ORB_OK 0
+#define ORB_ERR_EMPTY (-1)     /* empty image: ORBextractor::operator() returns -1 (src/ORBextractor.cc:1561-1562) */
+#define ORB_ERR_ARG (-2)       /* invalid argument (null pointer, size beyond the handle's capacity, ...) */
+#define ORB_ERR_CAPACITY (-3)  /* caller's output capacity too small; the needed count is still reported */
+#define ORB_ERR_DEVICE (-4)    /* HIP runtime error (no GPU, launch failure, out of memory) */
+#define ORB_ERR_ABORTED (-5)   /* stopped through the caller's stop flag (LocalBA pbStopFlag) */
+#define ORB_ERR_INTERNAL (-6)  /* a device-side capacity guard tripped (should not happen) */
+
+/* cv::KeyPoint memory layout (28 bytes): pt.x, pt.y, size, angle, response, octave, class_id */
+typedef struct orb_keypoint {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} orb_keypoint_t;
+
+/* ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST)
+ * (include/ORBextractor.h:52-53; values from the YAML keys ORBextractor.* e.g.
+ * Examples/Monocular/EuRoC.yaml:50-56) */
+typedef struct orb_params {
+    int32_t nfeatures;
+    float scale_factor;
+    int32_t nlevels;
+    int32_t ini_th_fast;
+    int32_t min_th_fast;
+} orb_params_t;
+
+typedef struct orb_extractor_s* orb_extractor_t;
+
+/* Query the library: returns the number of visible HIP devices (0 = none), never fails. */
+int orb_device_count(void);
+/* Human readable message for the last error on this thread. */
+const char* orb_last_error(void);
+
+/* ---- ORBextractor (src/ORBextractor.cc) ------------------------------------------------------ */
+
+/* Create an extractor for frames up to max_width x max_height, batches up to max_batch frames.
+ * Replaces ORBextractor::ORBextractor (src/ORBextractor.cc:468-571).  Allocates all device
+ * buffers once; no allocation happens per call. */
+int orb_extractor_create(const orb_params_t* params, int max_width, int max_height, int max_batch,
+                         orb_extractor_t* out);
+int orb_extractor_destroy(orb_extractor_t h);
+
+/* GetLevels/GetScaleFactors/GetInverseScaleFactors/GetScaleSigmaSquares/GetInverseScaleSigmaSquares
+ * (include/ORBextractor.h:61-83) and the per-level feature budget mnFeaturesPerLevel.
+ * Each array receives nlevels values; any pointer may be NULL. */
+int orb_extractor_scales(orb_extractor_t h, float* scale, float* inv_scale, float* sigma2,
+                         float* inv_sigma2, int32_t* features_per_level);
+
+/* ORBextractor::operator()(image, mask, keypoints, descriptors, vLappingArea)
+ * (src/ORBextractor.cc:1557-1682; called from Frame::ExtractORB src/Frame.cc:513-523).
+ * Host buffers, synchronous.  image: 8-bit gray, row stride `stride` bytes.  kps/desc hold `cap`
+ * entries (desc: cap x 32 bytes).  Keypoints are placed as the reference does: those with
+ * lap_x0 <= x <= lap_x1 (level-0 coordinates) from the end backwards, the others from the front.
+ * Returns monoIndex (>= 0, the number of front-placed keypoints), ORB_ERR_EMPTY for an empty
+ * image, or another negative status.  *n_kps receives the keypoint count (also when the capacity
+ * is too small). */
+int orb_extract(orb_extractor_t h, const uint8_t* image, int width, int height, int stride,
+                int lap_x0, int lap_x1, orb_keypoint_t* kps, uint8_t* desc, int cap, int* n_kps);
+
+/* Batched, device-resident, asynchronous form (the throughput path; no reference counterpart --
+ * it runs operator() on n frames at once).  d_images: n frames, frame f at d_images + f*frame_stride,
+ * rows `stride` bytes apart.  Frame f writes d_kps[f*cap ...], d_desc[(f*cap ...)*32] and
+ * d_counts[2f] = number of keypoints, d_counts[2f+1] = monoIndex (or ORB_ERR_CAPACITY if the frame
+ * had more than cap keypoints; then d_counts[2f] still holds the count).  stream: hipStream_t
+ * (NULL = default stream).  Returns after enqueueing. */
+int orb_extract_batch_device(orb_extractor_t h, const uint8_t* d_images, int n, int width, int height,
+                             int stride, size_t frame_stride, int lap_x0, int lap_x1,
+                             orb_keypoint_t* d_kps, uint8_t* d_desc, int cap, int32_t* d_counts,
+                             void* stream);
+
+/* mvImagePyramid[level] of frame `frame` of the last call (include/ORBextractor.h:83; read by
+ * Frame::ComputeStereoMatches src/Frame.cc:1126,1249).  Gives the device address of the view
+ * (first pixel of the level image inside its 19-pixel REFLECT_101 border), its size and row pitch.
+ * The border is readable at negative offsets down to -19 rows/columns. */
+int orb_extractor_level(orb_extractor_t h, int frame, int level, const uint8_t** d_view, int* width,
+                        int* height, int* pitch);
+/* Copy the padded level plane ((w+38) x (h+38), row-major, tight) to host memory. */
+int orb_extractor_level_download(orb_extractor_t h, int frame, int level, uint8_t* host_padded);
+
+/* ---- ORBmatcher (src/ORBmatcher.cc) ---------------------------------------------------------- */
+
+/* ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:2384-2404) on host data, for ABI completeness. */
+int orb_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* Brute-force Hamming matching on device data: for each query i (n_query x 32 B) find the best and
+ * second-best train descriptor (n_train x 32 B).  Writes best_idx[i], best_dist[i], second_dist[i]
+ * (256+1 = "none").  The distance is DescriptorDistance.  Device pointers, async on `stream`. */
+int orb_hamming_knn2_device(const uint8_t* d_query, int n_query, const uint8_t* d_train, int n_train,
+                            int32_t* d_best_idx, int32_t* d_best_dist, int32_t* d_second_dist,
+                            void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ORBGPU_H */

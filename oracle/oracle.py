@@ -1,0 +1,167 @@
+"""ctypes binding of the CPU oracle (oracle/_build/liborb_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, and only as the checker / the timed CPU baseline -- never by the product package.
+"""
+from __future__ import annotations
+
+import ctypes
+import pathlib
+import subprocess
+
+import numpy as np
+
+ORACLE_DIR = pathlib.Path(__file__).resolve().parent
+LIB_PATH = ORACLE_DIR / "_build" / "liborb_oracle.so"
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+_vp, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+_PROTOS = {
+    "oracle_orb_create": (_vp, [_i, _f, _i, _i, _i]),
+    "oracle_orb_destroy": (None, [_vp]),
+    "oracle_orb_params": (None, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "oracle_orb_extract": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, ctypes.POINTER(_i)]),
+    "oracle_orb_level_dims": (None, [_vp, _i, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i),
+                                     ctypes.POINTER(_i)]),
+    "oracle_orb_level_copy": (None, [_vp, _i, _vp]),
+    "oracle_orb_level_candidates": (_i, [_vp, _i, _vp, _i]),
+    "oracle_orb_level_cell_thresholds": (_i, [_vp, _i, _vp, _i]),
+    "oracle_orb_level_keys": (_i, [_vp, _i, _vp, _i]),
+    "oracle_resize_linear_u8": (None, [_vp, _i, _i, _i, _vp, _i, _i, _i]),
+    "oracle_fast9": (_i, [_vp, _i, _i, _i, _i, _vp, _i]),
+    "oracle_distribute": (_i, [_vp, _i, _i, _i, _i, _i, _i, _vp, _i]),
+    "oracle_fast_atan2": (_f, [_f, _f]),
+    "oracle_gaussian_blur": (None, [_vp, _i, _i, _i, _vp]),
+    "oracle_descriptor_distance": (_i, [_vp, _vp]),
+}
+
+_LIB = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", str(ORACLE_DIR)], check=True)
+
+
+def load() -> ctypes.CDLL:
+    global _LIB
+    if _LIB is None:
+        if not LIB_PATH.exists():
+            build()
+        lib = ctypes.CDLL(str(LIB_PATH))
+        for name, (res, args) in _PROTOS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = lib
+    return _LIB
+
+
+class OracleExtractor:
+    """CPU restatement of ORB_SLAM3::ORBextractor (oracle/orb_extractor_oracle.cpp)."""
+
+    def __init__(self, nfeatures=1000, scaleFactor=1.2, nlevels=8, iniThFAST=20, minThFAST=7):
+        self.lib = load()
+        self.nlevels = nlevels
+        self.h = ctypes.c_void_p(self.lib.oracle_orb_create(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST))
+        self.nfeatures = nfeatures
+
+    def __del__(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            self.lib.oracle_orb_destroy(self.h)
+            self.h = None
+
+    def params(self):
+        n = self.nlevels
+        arrs = [np.zeros(n, np.float32) for _ in range(4)]
+        per = np.zeros(n, np.int32)
+        umax = np.zeros(16, np.int32)
+        self.lib.oracle_orb_params(self.h, *[a.ctypes.data for a in arrs], per.ctypes.data, umax.ctypes.data)
+        return {"scale": arrs[0], "inv_scale": arrs[1], "sigma2": arrs[2], "inv_sigma2": arrs[3],
+                "per_level": per, "umax": umax}
+
+    def __call__(self, image: np.ndarray, lapping=(0, 0)):
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        h, w = img.shape
+        cap = 4 * self.nfeatures + 256
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = ctypes.c_int()
+        rc = self.lib.oracle_orb_extract(self.h, img.ctypes.data, w, h, w, int(lapping[0]), int(lapping[1]),
+                                         kps.ctypes.data, desc.ctypes.data, cap, ctypes.byref(n))
+        if rc < -1:
+            raise RuntimeError(f"oracle extract failed {rc}")
+        k = n.value
+        return kps[:k].copy(), desc[:k].copy(), rc
+
+    def level_padded(self, level: int) -> np.ndarray:
+        w, h, pw, ph = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        self.lib.oracle_orb_level_dims(self.h, level, ctypes.byref(w), ctypes.byref(h), ctypes.byref(pw),
+                                       ctypes.byref(ph))
+        out = np.zeros((ph.value, pw.value), np.uint8)
+        self.lib.oracle_orb_level_copy(self.h, level, out.ctypes.data)
+        return out
+
+    def level_candidates(self, level: int) -> np.ndarray:
+        n = self.lib.oracle_orb_level_candidates(self.h, level, None, 0)
+        out = np.zeros(n, KEYPOINT_DTYPE)
+        self.lib.oracle_orb_level_candidates(self.h, level, out.ctypes.data, n)
+        return out
+
+    def level_cell_thresholds(self, level: int) -> np.ndarray:
+        n = self.lib.oracle_orb_level_cell_thresholds(self.h, level, None, 0)
+        out = np.zeros(n, np.int32)
+        self.lib.oracle_orb_level_cell_thresholds(self.h, level, out.ctypes.data, n)
+        return out
+
+    def level_keys(self, level: int) -> np.ndarray:
+        n = self.lib.oracle_orb_level_keys(self.h, level, None, 0)
+        out = np.zeros(n, KEYPOINT_DTYPE)
+        self.lib.oracle_orb_level_keys(self.h, level, out.ctypes.data, n)
+        return out
+
+
+def fast9(window: np.ndarray, threshold: int) -> np.ndarray:
+    lib = load()
+    win = np.ascontiguousarray(window, dtype=np.uint8)
+    h, w = win.shape
+    cap = w * h
+    out = np.zeros(cap, KEYPOINT_DTYPE)
+    n = lib.oracle_fast9(win.ctypes.data, w, w, h, threshold, out.ctypes.data, cap)
+    return out[:n].copy()
+
+
+def distribute(cand: np.ndarray, min_x: int, max_x: int, min_y: int, max_y: int, n_features: int) -> np.ndarray:
+    lib = load()
+    c = np.ascontiguousarray(cand, dtype=KEYPOINT_DTYPE)
+    cap = len(c) + 8
+    out = np.zeros(cap, KEYPOINT_DTYPE)
+    m = lib.oracle_distribute(c.ctypes.data, len(c), min_x, max_x, min_y, max_y, n_features, out.ctypes.data, cap)
+    return out[:m].copy()
+
+
+def resize_linear(src: np.ndarray, dw: int, dh: int) -> np.ndarray:
+    lib = load()
+    s = np.ascontiguousarray(src, dtype=np.uint8)
+    out = np.zeros((dh, dw), np.uint8)
+    lib.oracle_resize_linear_u8(s.ctypes.data, s.shape[1], s.shape[1], s.shape[0], out.ctypes.data, dw, dw, dh)
+    return out
+
+
+def gaussian_blur(view: np.ndarray) -> np.ndarray:
+    lib = load()
+    v = np.ascontiguousarray(view, dtype=np.uint8)
+    out = np.zeros_like(v)
+    lib.oracle_gaussian_blur(v.ctypes.data, v.shape[1], v.shape[1], v.shape[0], out.ctypes.data)
+    return out
+
+
+def fast_atan2(y: float, x: float) -> float:
+    return float(load().oracle_fast_atan2(y, x))
+
+
+def descriptor_distance(a: np.ndarray, b: np.ndarray) -> int:
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    b = np.ascontiguousarray(b, dtype=np.uint8)
+    return load().oracle_descriptor_distance(a.ctypes.data, b.ctypes.data)

@@ -1,0 +1,671 @@
+// ============================================================================================
+// ORACLE -- TEST INFRASTRUCTURE ONLY.  Never linked into, loaded by, or called from the product
+// path (orb-slam3_byzyh_amd/).  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+// leg may load liborb_oracle.so, and only as the checker / the timed CPU baseline.
+//
+// CPU restatement of ORB_SLAM3::ORBextractor (reference: src/ORBextractor.cc, include/ORBextractor.h)
+// together with the OpenCV 4.x primitives it calls, restated from their published algorithms
+// because OpenCV is absent from this image:
+//   cv::resize INTER_LINEAR 8UC1  (11-bit fixed point, 128-bit SIMD vertical pass of x86 builds)
+//   cv::copyMakeBorder BORDER_REFLECT_101
+//   cv::FAST TYPE_9_16 + nonmax suppression (FAST_t<16> / cornerScore<16>)
+//   cv::GaussianBlur 7x7 sigma 2 8U (bit-exact fixed-point path, ufixedpoint16 kernel)
+//   cv::fastAtan2 (atan_f32 polynomial, baseline build: no FMA)
+//   cvRound (round half to even), libstdc++ std::sort (used directly, as in the reference)
+//   glibc sincosf (used directly: g++ -O3 fuses the reference's cos()/sin() into sincosf)
+// The reference is compiled with -O3 -march=native (CMakeLists.txt:10-13); on an FMA machine g++
+// contracts the rBRIEF offset expressions (src/ORBextractor.cc:168) to fma(x,b,y*a)/fma(x,a,-(y*b)).
+// That is reproduced with explicit fmaf(); everything else is compiled -ffp-contract=off.
+//
+// PARITY STATUS: the reference cannot be built here (no OpenCV/Eigen), and the reference ships no
+// golden keypoints/descriptors, so this oracle is pinned only by the reference's own constants
+// (bit_pattern_31_, umax, per-level feature counts, scale tables, level sizes; tests/golden/) --
+// for the OpenCV-dependent arithmetic it is "parity unpinned" (see DESIGN.md sec. Oracle).
+// ============================================================================================
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <algorithm>
+#include <list>
+#include <utility>
+#include <vector>
+
+namespace {
+
+struct KeyPoint {  // cv::KeyPoint memory layout: pt.x, pt.y, size, angle, response, octave, class_id
+    float x, y, size, angle, response;
+    int octave, class_id;
+};
+static_assert(sizeof(KeyPoint) == 28, "cv::KeyPoint layout");
+
+constexpr int kEdge = 19;       // EDGE_THRESHOLD      src/ORBextractor.cc:78
+constexpr int kHalfPatch = 15;  // HALF_PATCH_SIZE     src/ORBextractor.cc:77
+constexpr int kPatch = 31;      // PATCH_SIZE          src/ORBextractor.cc:76
+
+const int kPattern[1024] = {
+#include "../orb-slam3_byzyh_amd/csrc/orb_pattern31.inc"
+};
+
+inline int cv_round(float v) { return (int)lrintf(v); }   // SSE2 cvtss2si: half to even
+inline int cv_round(double v) { return (int)lrint(v); }
+inline int cv_floor(float v) { int i = (int)v; return i - (i > v); }
+inline int cv_ceil(float v) { int i = (int)v; return i + (i < v); }
+inline short sat_s16(int v) { return (short)std::min(32767, std::max(-32768, v)); }
+inline uint8_t sat_u8(int v) { return (uint8_t)std::min(255, std::max(0, v)); }
+
+inline int reflect101(int p, int len) {  // cv::borderInterpolate(BORDER_REFLECT_101)
+    if (len == 1) return 0;
+    while ((unsigned)p >= (unsigned)len) p = p < 0 ? -p : 2 * len - 2 - p;
+    return p;
+}
+
+// ------------------------------------------------------------------ parameters (src:468-571)
+struct Params {
+    int nfeatures = 0, nlevels = 0, iniTh = 0, minTh = 0;
+    double scaleFactor = 0;  // double member initialised from a float argument (include/ORBextractor.h:96)
+    std::vector<float> scale, invScale, sigma2, invSigma2;
+    std::vector<int> nPerLevel, umax;
+};
+
+Params make_params(int nf, float sf, int nl, int ini, int mn) {
+    Params p;
+    p.nfeatures = nf; p.scaleFactor = sf; p.nlevels = nl; p.iniTh = ini; p.minTh = mn;
+    p.scale.assign(nl, 1.0f); p.sigma2.assign(nl, 1.0f);
+    for (int i = 1; i < nl; ++i) {
+        p.scale[i] = (float)(p.scale[i - 1] * p.scaleFactor);
+        p.sigma2[i] = p.scale[i] * p.scale[i];
+    }
+    p.invScale.resize(nl); p.invSigma2.resize(nl);
+    for (int i = 0; i < nl; ++i) { p.invScale[i] = 1.0f / p.scale[i]; p.invSigma2[i] = 1.0f / p.sigma2[i]; }
+    const float factor = (float)(1.0f / p.scaleFactor);
+    float desired = nf * (1 - factor) / (1 - (float)pow((double)factor, (double)nl));
+    int total = 0;
+    p.nPerLevel.assign(nl, 0);
+    for (int l = 0; l < nl - 1; ++l) {
+        p.nPerLevel[l] = cv_round(desired);
+        total += p.nPerLevel[l];
+        desired *= factor;
+    }
+    p.nPerLevel[nl - 1] = std::max(nf - total, 0);
+    // circular patch row extents (src:542-570)
+    p.umax.assign(kHalfPatch + 1, 0);
+    const int vmax = cv_floor(kHalfPatch * sqrtf(2.f) / 2 + 1);
+    const int vmin = cv_ceil(kHalfPatch * sqrtf(2.f) / 2);
+    const double hp2 = kHalfPatch * kHalfPatch;
+    for (int v = 0; v <= vmax; ++v) p.umax[v] = cv_round(sqrt(hp2 - v * v));
+    for (int v = kHalfPatch, v0 = 0; v >= vmin; --v) {
+        while (p.umax[v0] == p.umax[v0 + 1]) ++v0;
+        p.umax[v] = v0;
+        ++v0;
+    }
+    return p;
+}
+
+// ------------------------------------------------------------------ padded pyramid planes
+struct Plane {
+    int w = 0, h = 0;          // view (level) size
+    int pw = 0, ph = 0;        // padded size
+    std::vector<uint8_t> buf;  // padded, row stride pw
+    uint8_t* view() { return buf.data() + (size_t)kEdge * pw + kEdge; }
+    const uint8_t* view() const { return buf.data() + (size_t)kEdge * pw + kEdge; }
+    void alloc(int w_, int h_) { w = w_; h = h_; pw = w + 2 * kEdge; ph = h + 2 * kEdge; buf.assign((size_t)pw * ph, 0); }
+    void fill_border() {  // copyMakeBorder(BORDER_REFLECT_101) from the view into the 19-px frame
+        for (int py = 0; py < ph; ++py) {
+            const int sy = reflect101(py - kEdge, h);
+            for (int px = 0; px < pw; ++px) {
+                if (py >= kEdge && py < kEdge + h && px >= kEdge && px < kEdge + w) continue;
+                buf[(size_t)py * pw + px] = buf[(size_t)(sy + kEdge) * pw + reflect101(px - kEdge, w) + kEdge];
+            }
+        }
+    }
+};
+
+// cv::resize(src, dst, dsize, 0, 0, INTER_LINEAR) for 8UC1, OpenCV 4.x generic path
+// (resize.cpp: coefficient tables, HResizeLinear<uchar,int,short,2048>, VResizeLinear with
+// FixedPtCast<int,uchar,22>; the x86 build's VResizeLinearVec_32s8u handles the leading columns
+// in 16- then 8-lane blocks with the ((S>>4)*b >> 16) arithmetic, the scalar tail the rest).
+int resize_simd_end(int w) {
+    int x = 0;
+    for (; x <= w - 16; x += 16) {}
+    for (; x < w - 8; x += 8) {}
+    return x;
+}
+
+void resize_linear_u8(const uint8_t* src, int sstride, int sw, int sh, uint8_t* dst, int dstride, int dw, int dh) {
+    const double inv_sx = (double)dw / sw, inv_sy = (double)dh / sh;
+    const double scale_x = 1. / inv_sx, scale_y = 1. / inv_sy;
+    std::vector<int> xofs(dw);
+    std::vector<short> ialpha(2 * (size_t)dw);
+    for (int dx = 0; dx < dw; ++dx) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = cv_floor(fx);
+        fx -= sx;
+        if (sx < 0) { fx = 0; sx = 0; }
+        if (sx + 1 >= sw && sx >= sw - 1) { fx = 0; sx = sw - 1; }
+        xofs[dx] = sx;
+        ialpha[2 * dx] = sat_s16(cv_round((1.f - fx) * 2048));
+        ialpha[2 * dx + 1] = sat_s16(cv_round(fx * 2048));
+    }
+    std::vector<int> h0(dw), h1(dw);
+    auto hrow = [&](int sy, std::vector<int>& out) {
+        const uint8_t* S = src + (size_t)sy * sstride;
+        for (int dx = 0; dx < dw; ++dx) {
+            const int sx = xofs[dx];
+            const int sx1 = std::min(sx + 1, sw - 1);  // a1 == 0 whenever sx + 1 == sw
+            out[dx] = S[sx] * ialpha[2 * dx] + S[sx1] * ialpha[2 * dx + 1];
+        }
+    };
+    const int xv = resize_simd_end(dw);
+    for (int dy = 0; dy < dh; ++dy) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        const int sy = cv_floor(fy);
+        fy -= sy;
+        const int b0 = sat_s16(cv_round((1.f - fy) * 2048));
+        const int b1 = sat_s16(cv_round(fy * 2048));
+        const int r0 = std::min(std::max(sy, 0), sh - 1), r1 = std::min(std::max(sy + 1, 0), sh - 1);
+        hrow(r0, h0);
+        hrow(r1, h1);
+        uint8_t* D = dst + (size_t)dy * dstride;
+        for (int x = 0; x < dw; ++x) {
+            if (x < xv) {
+                const int t0 = (int16_t)std::min(32767, h0[x] >> 4), t1 = (int16_t)std::min(32767, h1[x] >> 4);
+                const int m = ((t0 * b0) >> 16) + ((t1 * b1) >> 16);   // v_mul_hi + v_add (int16)
+                D[x] = sat_u8(((int16_t)m + 2) >> 2);                   // v_rshr_pack_u<2>
+            } else {
+                D[x] = sat_u8((h0[x] * b0 + h1[x] * b1 + (1 << 21)) >> 22);
+            }
+        }
+    }
+}
+
+// ComputePyramid (src:1687-1740)
+void compute_pyramid(const Params& P, const uint8_t* img, int w, int h, int stride, std::vector<Plane>& pyr) {
+    pyr.assign(P.nlevels, Plane());
+    for (int l = 0; l < P.nlevels; ++l) {
+        const float s = P.invScale[l];
+        const int lw = cv_round((float)w * s), lh = cv_round((float)h * s);
+        pyr[l].alloc(lw, lh);
+        if (l == 0) {
+            for (int y = 0; y < h; ++y) memcpy(pyr[0].view() + (size_t)y * pyr[0].pw, img + (size_t)y * stride, w);
+        } else {
+            const Plane& prev = pyr[l - 1];
+            resize_linear_u8(prev.view(), prev.pw, prev.w, prev.h, pyr[l].view(), pyr[l].pw, lw, lh);
+        }
+        pyr[l].fill_border();
+    }
+}
+
+// ------------------------------------------------------------------ FAST-9/16 (OpenCV FAST_t<16>)
+const int kCircle[16][2] = {{0, 3}, {1, 3}, {2, 2}, {3, 1}, {3, 0}, {3, -1}, {2, -2}, {1, -3},
+                            {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
+
+int corner_score16(const uint8_t* p, const int* pix, int threshold) {  // cornerScore<16>
+    int d[25];
+    const int v = p[0];
+    for (int k = 0; k < 25; ++k) d[k] = v - p[pix[k]];
+    int a0 = threshold;
+    for (int k = 0; k < 16; k += 2) {
+        int a = std::min(d[k + 1], d[k + 2]);
+        a = std::min(a, d[k + 3]);
+        if (a <= a0) continue;
+        for (int q = 4; q <= 8; ++q) a = std::min(a, d[k + q]);
+        a0 = std::max(a0, std::min(a, d[k]));
+        a0 = std::max(a0, std::min(a, d[k + 9]));
+    }
+    int b0 = -a0;
+    for (int k = 0; k < 16; k += 2) {
+        int b = std::max(d[k + 1], d[k + 2]);
+        for (int q = 3; q <= 5; ++q) b = std::max(b, d[k + q]);
+        if (b >= b0) continue;
+        for (int q = 6; q <= 8; ++q) b = std::max(b, d[k + q]);
+        b0 = std::min(b0, std::max(b, d[k]));
+        b0 = std::min(b0, std::max(b, d[k + 9]));
+    }
+    return -b0 - 1;
+}
+
+// cv::FAST(window, kps, threshold, nonmaxSuppression=true), window given by pointer/stride/size.
+void fast9(const uint8_t* img, int stride, int cols, int rows, int threshold, std::vector<KeyPoint>& kps) {
+    kps.clear();
+    int pix[25];
+    for (int k = 0; k < 16; ++k) pix[k] = kCircle[k][0] + kCircle[k][1] * stride;
+    for (int k = 16; k < 25; ++k) pix[k] = pix[k - 16];
+    threshold = std::min(std::max(threshold, 0), 255);
+    if (cols < 7 || rows < 7) return;
+    std::vector<uint8_t> score(3 * (size_t)cols, 0);
+    std::vector<int> cpos[3];
+    auto tab = [&](int v, int x) { const int dlt = x - v; return dlt < -threshold ? 1 : dlt > threshold ? 2 : 0; };
+    for (int i = 3; i < rows - 2; ++i) {
+        uint8_t* curr = &score[(size_t)((i - 3) % 3) * cols];
+        memset(curr, 0, cols);
+        std::vector<int>& cp = cpos[(i - 3) % 3];
+        cp.clear();
+        if (i < rows - 3) {
+            for (int j = 3; j < cols - 3; ++j) {
+                const uint8_t* p = img + (size_t)i * stride + j;
+                const int v = p[0];
+                int d = tab(v, p[pix[0]]) | tab(v, p[pix[8]]);
+                if (d == 0) continue;
+                d &= tab(v, p[pix[2]]) | tab(v, p[pix[10]]);
+                d &= tab(v, p[pix[4]]) | tab(v, p[pix[12]]);
+                d &= tab(v, p[pix[6]]) | tab(v, p[pix[14]]);
+                if (d == 0) continue;
+                d &= tab(v, p[pix[1]]) | tab(v, p[pix[9]]);
+                d &= tab(v, p[pix[3]]) | tab(v, p[pix[11]]);
+                d &= tab(v, p[pix[5]]) | tab(v, p[pix[13]]);
+                d &= tab(v, p[pix[7]]) | tab(v, p[pix[15]]);
+                for (int pol = 1; pol <= 2; ++pol) {
+                    if (!(d & pol)) continue;
+                    int run = 0;
+                    for (int k = 0; k < 25; ++k) {
+                        const int x = p[pix[k]];
+                        const bool hit = pol == 1 ? x < v - threshold : x > v + threshold;
+                        if (!hit) { run = 0; continue; }
+                        if (++run > 8) {
+                            cp.push_back(j);
+                            curr[j] = (uint8_t)corner_score16(p, pix, threshold);
+                            break;
+                        }
+                    }
+                }
+            }
+        }
+        if (i == 3) continue;
+        const uint8_t* prev = &score[(size_t)((i - 1) % 3) * cols];
+        const uint8_t* pprev = &score[(size_t)((i - 2) % 3) * cols];
+        for (int j : cpos[(i - 1) % 3]) {
+            const int s = prev[j];
+            if (s > prev[j + 1] && s > prev[j - 1] && s > pprev[j - 1] && s > pprev[j] && s > pprev[j + 1] &&
+                s > curr[j - 1] && s > curr[j] && s > curr[j + 1])
+                kps.push_back({(float)j, (float)(i - 1), 7.f, -1.f, (float)s, 0, -1});
+        }
+    }
+}
+
+// ------------------------------------------------------------------ quad-tree (src:602-1057)
+struct QNode {
+    std::vector<KeyPoint> keys;
+    int ulx = 0, uly = 0, urx = 0, ury = 0, blx = 0, bly = 0, brx = 0, bry = 0;
+    std::list<QNode>::iterator self;
+    bool leaf = false;  // bNoMore
+
+    void split(QNode& a, QNode& b, QNode& c, QNode& d) const {
+        const int hx = (int)ceilf((float)(urx - ulx) / 2);
+        const int hy = (int)ceilf((float)(bry - uly) / 2);
+        a.ulx = ulx;      a.uly = uly;      a.urx = ulx + hx; a.ury = uly;
+        a.blx = ulx;      a.bly = uly + hy; a.brx = ulx + hx; a.bry = uly + hy;
+        b.ulx = a.urx;    b.uly = a.ury;    b.urx = urx;      b.ury = ury;
+        b.blx = a.brx;    b.bly = a.bry;    b.brx = urx;      b.bry = uly + hy;
+        c.ulx = a.blx;    c.uly = a.bly;    c.urx = a.brx;    c.ury = a.bry;
+        c.blx = blx;      c.bly = bly;      c.brx = a.brx;    c.bry = bly;
+        d.ulx = c.urx;    d.uly = c.ury;    d.urx = b.brx;    d.ury = b.bry;
+        d.blx = c.brx;    d.bly = c.bry;    d.brx = brx;      d.bry = bry;
+        for (const KeyPoint& k : keys) {
+            if (k.x < a.urx) (k.y < a.bry ? a : c).keys.push_back(k);
+            else (k.y < a.bry ? b : d).keys.push_back(k);
+        }
+        a.leaf = a.keys.size() == 1; b.leaf = b.keys.size() == 1;
+        c.leaf = c.keys.size() == 1; d.leaf = d.keys.size() == 1;
+    }
+};
+
+using SizeNode = std::pair<int, QNode*>;
+bool by_size_then_x(const SizeNode& e1, const SizeNode& e2) {  // compareNodes (src:676-697)
+    if (e1.first != e2.first) return e1.first < e2.first;
+    return e1.second->ulx < e2.second->ulx;
+}
+
+std::vector<KeyPoint> distribute(const std::vector<KeyPoint>& cand, int minX, int maxX, int minY, int maxY, int N) {
+    const int nRoots = (int)std::round((float)(maxX - minX) / (maxY - minY));
+    const float hx = (float)(maxX - minX) / nRoots;
+    std::list<QNode> nodes;
+    std::vector<QNode*> roots(nRoots);
+    for (int i = 0; i < nRoots; ++i) {
+        QNode n;
+        n.ulx = (int)(hx * (float)i);       n.uly = 0;
+        n.urx = (int)(hx * (float)(i + 1)); n.ury = 0;
+        n.blx = n.ulx; n.bly = maxY - minY;
+        n.brx = n.urx; n.bry = maxY - minY;
+        nodes.push_back(n);
+        roots[i] = &nodes.back();
+    }
+    for (const KeyPoint& k : cand) roots[(size_t)(k.x / hx)]->keys.push_back(k);
+    for (auto it = nodes.begin(); it != nodes.end();) {
+        if (it->keys.size() == 1) { it->leaf = true; ++it; }
+        else if (it->keys.empty()) it = nodes.erase(it);
+        else ++it;
+    }
+    // push the non-empty children of `parent` to the list front; remember the splittable ones
+    auto expand = [&](const QNode& parent, std::vector<SizeNode>& splittable, int* nToExpand) {
+        QNode ch[4];
+        parent.split(ch[0], ch[1], ch[2], ch[3]);
+        for (QNode& c : ch) {
+            if (c.keys.empty()) continue;
+            nodes.push_front(c);
+            if (c.keys.size() > 1) {
+                if (nToExpand) ++*nToExpand;
+                splittable.push_back({(int)c.keys.size(), &nodes.front()});
+                nodes.front().self = nodes.begin();
+            }
+        }
+    };
+    bool done = false;
+    std::vector<SizeNode> splittable;
+    while (!done) {
+        int prevSize = (int)nodes.size();
+        int nToExpand = 0;
+        splittable.clear();
+        for (auto it = nodes.begin(); it != nodes.end();) {
+            if (it->leaf) { ++it; continue; }
+            expand(*it, splittable, &nToExpand);
+            it = nodes.erase(it);
+        }
+        if ((int)nodes.size() >= N || (int)nodes.size() == prevSize) {
+            done = true;
+        } else if ((int)nodes.size() + nToExpand * 3 > N) {
+            while (!done) {
+                prevSize = (int)nodes.size();
+                std::vector<SizeNode> prev = splittable;
+                splittable.clear();
+                std::sort(prev.begin(), prev.end(), by_size_then_x);
+                for (int j = (int)prev.size() - 1; j >= 0; --j) {
+                    expand(*prev[j].second, splittable, nullptr);
+                    nodes.erase(prev[j].second->self);
+                    if ((int)nodes.size() >= N) break;
+                }
+                if ((int)nodes.size() >= N || (int)nodes.size() == prevSize) done = true;
+            }
+        }
+    }
+    std::vector<KeyPoint> out;
+    out.reserve(nodes.size());
+    for (const QNode& n : nodes) {
+        const KeyPoint* best = &n.keys[0];
+        for (size_t k = 1; k < n.keys.size(); ++k)
+            if (n.keys[k].response > best->response) best = &n.keys[k];
+        out.push_back(*best);
+    }
+    return out;
+}
+
+// ComputeKeyPointsOctTree cell loop (src:1061-1166) for one level.  `cand` = all FAST candidates in
+// cell-row-major then FAST emission order, coordinates relative to minBorder.
+void level_candidates(const Params& P, const Plane& L, std::vector<KeyPoint>& cand, std::vector<int>* cell_thresh) {
+    cand.clear();
+    const float W = 35;
+    const int minBX = kEdge - 3, minBY = minBX;
+    const int maxBX = L.w - kEdge + 3, maxBY = L.h - kEdge + 3;
+    const float width = (float)(maxBX - minBX), height = (float)(maxBY - minBY);
+    const int nCols = (int)(width / W), nRows = (int)(height / W);
+    const int wCell = (int)ceilf(width / nCols), hCell = (int)ceilf(height / nRows);
+    std::vector<KeyPoint> cell;
+    for (int i = 0; i < nRows; ++i) {
+        const float iniY = (float)(minBY + i * hCell);
+        float maxY = iniY + hCell + 6;
+        if (iniY >= maxBY - 3) continue;
+        if (maxY > maxBY) maxY = (float)maxBY;
+        for (int j = 0; j < nCols; ++j) {
+            const float iniX = (float)(minBX + j * wCell);
+            float maxX = iniX + wCell + 6;
+            if (iniX >= maxBX - 6) continue;
+            if (maxX > maxBX) maxX = (float)maxBX;
+            const uint8_t* win = L.view() + (size_t)(int)iniY * L.pw + (int)iniX;
+            const int wc = (int)maxX - (int)iniX, wr = (int)maxY - (int)iniY;
+            int used = P.iniTh;
+            fast9(win, L.pw, wc, wr, P.iniTh, cell);
+            if (cell.empty()) { used = P.minTh; fast9(win, L.pw, wc, wr, P.minTh, cell); }
+            if (cell_thresh) cell_thresh->push_back(used);
+            for (KeyPoint k : cell) {
+                k.x += j * wCell;
+                k.y += i * hCell;
+                cand.push_back(k);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ orientation / descriptor
+float fast_atan2_deg(float y, float x) {  // cv::fastAtan2 (atan_f32), degrees in [0, 360)
+    static const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
+    static const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
+    static const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
+    static const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
+    const float ax = std::fabs(x), ay = std::fabs(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+float ic_angle(const Plane& L, const KeyPoint& kp, const std::vector<int>& umax) {  // src:91-138
+    const uint8_t* c = L.view() + (size_t)cv_round(kp.y) * L.pw + cv_round(kp.x);
+    const int step = L.pw;
+    int m01 = 0, m10 = 0;
+    for (int u = -kHalfPatch; u <= kHalfPatch; ++u) m10 += u * c[u];
+    for (int v = 1; v <= kHalfPatch; ++v) {
+        int vs = 0;
+        const int d = umax[v];
+        for (int u = -d; u <= d; ++u) {
+            const int plus = c[u + v * step], minus = c[u - v * step];
+            vs += plus - minus;
+            m10 += u * (plus + minus);
+        }
+        m01 += v * vs;
+    }
+    return fast_atan2_deg((float)m01, (float)m10);
+}
+
+// GaussianBlur(level.clone(), 7x7, 2, 2, BORDER_REFLECT_101), OpenCV >= 4.1 bit-exact 8U path:
+// kernel = getGaussianKernelBitExact(7, 2) -> 8-fraction-bit fixed point with error diffusion
+// = {18, 34, 48, 56, 48, 34, 18}; row pass exact in 16 bits, column pass exact in 32 bits,
+// output (acc + 2^15) >> 16.
+const int kBlur[7] = {18, 34, 48, 56, 48, 34, 18};
+
+void gaussian_blur(const Plane& L, std::vector<uint8_t>& out) {
+    const int w = L.w, h = L.h;
+    std::vector<int> rowp((size_t)w * h);
+    for (int y = 0; y < h; ++y) {
+        const uint8_t* S = L.view() + (size_t)y * L.pw;
+        for (int x = 0; x < w; ++x) {
+            int acc = 0;
+            for (int k = 0; k < 7; ++k) acc += kBlur[k] * S[reflect101(x + k - 3, w)];
+            rowp[(size_t)y * w + x] = acc;
+        }
+    }
+    out.assign((size_t)w * h, 0);
+    for (int y = 0; y < h; ++y)
+        for (int x = 0; x < w; ++x) {
+            int acc = 0;
+            for (int k = 0; k < 7; ++k) acc += kBlur[k] * rowp[(size_t)reflect101(y + k - 3, h) * w + x];
+            out[(size_t)y * w + x] = sat_u8((acc + (1 << 15)) >> 16);
+        }
+}
+
+void orb_descriptor(const KeyPoint& kp, const uint8_t* img, int step, uint8_t* desc) {  // src:150-203
+    const float factorPI = (float)(M_PI / 180.f);
+    const float angle = kp.angle * factorPI;
+    float a, b;
+    sincosf(angle, &b, &a);  // (float)cos(angle), (float)sin(angle); g++ -O3 emits sincosf
+    const uint8_t* center = img + (size_t)cv_round(kp.y) * step + cv_round(kp.x);
+    auto sample = [&](int idx) {
+        const float px = (float)kPattern[2 * idx], py = (float)kPattern[2 * idx + 1];
+        const int r = cv_round(fmaf(px, b, py * a));   // g++ -march=native contraction
+        const int c = cv_round(fmaf(px, a, -(py * b)));
+        return (int)center[r * step + c];
+    };
+    for (int i = 0; i < 32; ++i) {
+        int val = 0;
+        for (int k = 0; k < 8; ++k) {
+            const int t0 = sample(16 * i + 2 * k), t1 = sample(16 * i + 2 * k + 1);
+            val |= (t0 < t1) << k;
+        }
+        desc[i] = (uint8_t)val;
+    }
+}
+
+// ------------------------------------------------------------------ whole extractor
+struct Extractor {
+    Params P;
+    std::vector<Plane> pyr;
+    std::vector<std::vector<KeyPoint>> levelKeys;   // per level, after distribution (level coords)
+    std::vector<std::vector<KeyPoint>> levelCand;   // per level, FAST candidates (relative coords)
+    std::vector<std::vector<int>> cellThresh;
+
+    int run(const uint8_t* img, int w, int h, int stride, int lap0, int lap1,
+            KeyPoint* kps, uint8_t* desc, int cap, int* n_out) {
+        if (!img || w <= 0 || h <= 0) { *n_out = 0; return -1; }
+        compute_pyramid(P, img, w, h, stride, pyr);
+        levelKeys.assign(P.nlevels, {});
+        levelCand.assign(P.nlevels, {});
+        cellThresh.assign(P.nlevels, {});
+        for (int l = 0; l < P.nlevels; ++l) {
+            const Plane& L = pyr[l];
+            level_candidates(P, L, levelCand[l], &cellThresh[l]);
+            const int minB = kEdge - 3;
+            std::vector<KeyPoint> sel = distribute(levelCand[l], minB, L.w - kEdge + 3, minB, L.h - kEdge + 3, P.nPerLevel[l]);
+            const int psize = (int)(kPatch * P.scale[l]);
+            for (KeyPoint& k : sel) { k.x += minB; k.y += minB; k.octave = l; k.size = (float)psize; }
+            for (KeyPoint& k : sel) k.angle = ic_angle(L, k, P.umax);
+            levelKeys[l] = sel;
+        }
+        int total = 0;
+        for (auto& v : levelKeys) total += (int)v.size();
+        *n_out = total;
+        if (total > cap) return -2;
+        int mono = 0, stereo = total - 1;
+        std::vector<uint8_t> blurred;
+        for (int l = 0; l < P.nlevels; ++l) {
+            std::vector<KeyPoint>& ks = levelKeys[l];
+            if (ks.empty()) continue;
+            gaussian_blur(pyr[l], blurred);
+            const float scale = P.scale[l];
+            for (KeyPoint k : ks) {
+                uint8_t d[32];
+                orb_descriptor(k, blurred.data(), pyr[l].w, d);
+                if (l != 0) { k.x *= scale; k.y *= scale; }
+                const int at = (k.x >= lap0 && k.x <= lap1) ? stereo-- : mono++;
+                kps[at] = k;
+                memcpy(desc + 32 * (size_t)at, d, 32);
+            }
+        }
+        return mono;
+    }
+};
+
+}  // namespace
+
+// ============================================================================================ C ABI
+extern "C" {
+
+typedef struct oracle_orb_s oracle_orb_t;
+
+oracle_orb_t* oracle_orb_create(int nfeatures, float scale_factor, int nlevels, int ini_th, int min_th) {
+    Extractor* e = new Extractor();
+    e->P = make_params(nfeatures, scale_factor, nlevels, ini_th, min_th);
+    return (oracle_orb_t*)e;
+}
+
+void oracle_orb_destroy(oracle_orb_t* h) { delete (Extractor*)h; }
+
+// scale tables (nlevels each) + per-level feature budget + umax[16]
+void oracle_orb_params(oracle_orb_t* h, float* scale, float* inv_scale, float* sigma2, float* inv_sigma2,
+                       int* n_per_level, int* umax) {
+    const Params& P = ((Extractor*)h)->P;
+    for (int l = 0; l < P.nlevels; ++l) {
+        scale[l] = P.scale[l]; inv_scale[l] = P.invScale[l];
+        sigma2[l] = P.sigma2[l]; inv_sigma2[l] = P.invSigma2[l];
+        n_per_level[l] = P.nPerLevel[l];
+    }
+    for (int v = 0; v <= kHalfPatch; ++v) umax[v] = P.umax[v];
+}
+
+// ORBextractor::operator() on one gray image.  kps/desc must hold `cap` entries.
+// Returns monoIndex (>= 0), -1 on empty image, -2 if cap < number of keypoints (*n_out = needed).
+int oracle_orb_extract(oracle_orb_t* h, const uint8_t* img, int w, int hgt, int stride, int lap0, int lap1,
+                       void* kps, uint8_t* desc, int cap, int* n_out) {
+    return ((Extractor*)h)->run(img, w, hgt, stride, lap0, lap1, (KeyPoint*)kps, desc, cap, n_out);
+}
+
+// ---- intermediates of the last oracle_orb_extract call (for stage-by-stage parity tests)
+void oracle_orb_level_dims(oracle_orb_t* h, int level, int* w, int* hh, int* pw, int* ph) {
+    const Plane& L = ((Extractor*)h)->pyr[level];
+    *w = L.w; *hh = L.h; *pw = L.pw; *ph = L.ph;
+}
+void oracle_orb_level_copy(oracle_orb_t* h, int level, uint8_t* out) {
+    const Plane& L = ((Extractor*)h)->pyr[level];
+    memcpy(out, L.buf.data(), L.buf.size());
+}
+int oracle_orb_level_candidates(oracle_orb_t* h, int level, void* out, int cap) {
+    const auto& v = ((Extractor*)h)->levelCand[level];
+    const int n = (int)v.size();
+    if (out) memcpy(out, v.data(), sizeof(KeyPoint) * (size_t)std::min(n, cap));
+    return n;
+}
+int oracle_orb_level_cell_thresholds(oracle_orb_t* h, int level, int* out, int cap) {
+    const auto& v = ((Extractor*)h)->cellThresh[level];
+    const int n = (int)v.size();
+    if (out) memcpy(out, v.data(), sizeof(int) * (size_t)std::min(n, cap));
+    return n;
+}
+int oracle_orb_level_keys(oracle_orb_t* h, int level, void* out, int cap) {
+    const auto& v = ((Extractor*)h)->levelKeys[level];
+    const int n = (int)v.size();
+    if (out) memcpy(out, v.data(), sizeof(KeyPoint) * (size_t)std::min(n, cap));
+    return n;
+}
+
+// ---- standalone primitives
+void oracle_resize_linear_u8(const uint8_t* src, int sstride, int sw, int sh, uint8_t* dst, int dstride, int dw, int dh) {
+    resize_linear_u8(src, sstride, sw, sh, dst, dstride, dw, dh);
+}
+int oracle_fast9(const uint8_t* img, int stride, int cols, int rows, int threshold, void* out, int cap) {
+    std::vector<KeyPoint> k;
+    fast9(img, stride, cols, rows, threshold, k);
+    const int n = (int)k.size();
+    if (out) memcpy(out, k.data(), sizeof(KeyPoint) * (size_t)std::min(n, cap));
+    return n;
+}
+// quad-tree distribution of candidates (relative coords) in a [0, maxX-minX] x [0, maxY-minY] box
+int oracle_distribute(const void* cand, int n, int minX, int maxX, int minY, int maxY, int N, void* out, int cap) {
+    std::vector<KeyPoint> c((const KeyPoint*)cand, (const KeyPoint*)cand + n);
+    std::vector<KeyPoint> r = distribute(c, minX, maxX, minY, maxY, N);
+    const int m = (int)r.size();
+    if (out) memcpy(out, r.data(), sizeof(KeyPoint) * (size_t)std::min(m, cap));
+    return m;
+}
+float oracle_fast_atan2(float y, float x) { return fast_atan2_deg(y, x); }
+void oracle_gaussian_blur(const uint8_t* view, int stride, int w, int h, uint8_t* out) {
+    Plane L;
+    L.alloc(w, h);
+    for (int y = 0; y < h; ++y) memcpy(L.view() + (size_t)y * L.pw, view + (size_t)y * stride, w);
+    std::vector<uint8_t> o;
+    gaussian_blur(L, o);
+    memcpy(out, o.data(), o.size());
+}
+
+// DescriptorDistance (reference src/ORBmatcher.cc:2384-2404): popcount of a xor b over 8 u32 words
+int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b) {
+    int dist = 0;
+    for (int i = 0; i < 8; ++i) {
+        uint32_t x, y;
+        memcpy(&x, a + 4 * i, 4);
+        memcpy(&y, b + 4 * i, 4);
+        uint32_t v = x ^ y;
+        v = v - ((v >> 1) & 0x55555555u);
+        v = (v & 0x33333333u) + ((v >> 2) & 0x33333333u);
+        dist += (int)((((v + (v >> 4)) & 0xF0F0F0Fu) * 0x1010101u) >> 24);
+    }
+    return dist;
+}
+
+}  // extern "C"

@@ -1,0 +1,12 @@
+"""MI355X-native ORB-SLAM3 front-end + local BA hot path (import name: ``orbslam3_amd``).
+
+The package directory is ``orb-slam3_byzyh_amd/`` (not a valid identifier); load it with
+``orbslam3_amd = load_package()`` from the repo root helpers (tests/conftest.py, bench.py,
+__graft_entry__.py), which register it under the import name ``orbslam3_amd``.
+"""
+from . import _lib
+from ._lib import KEYPOINT_DTYPE, OrbGpuError
+from .extractor import ORBextractor, keypoints_to_structured
+from .matcher import ORBmatcher
+
+__all__ = ["ORBextractor", "ORBmatcher", "KEYPOINT_DTYPE", "OrbGpuError", "keypoints_to_structured", "_lib"]

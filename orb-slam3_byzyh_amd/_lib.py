@@ -1,0 +1,114 @@
+"""ctypes binding of liborbgpu.so (the C ABI declared in include/orbgpu.h).
+
+The product path is the HIP library: if it is missing or cannot be loaded this module raises --
+there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import pathlib
+
+import numpy as np
+
+PKG_DIR = pathlib.Path(__file__).resolve().parent
+LIB_PATH = PKG_DIR / "lib" / "liborbgpu.so"
+
+ORB_OK = 0
+ORB_ERR_EMPTY = -1
+ORB_ERR_ARG = -2
+ORB_ERR_CAPACITY = -3
+ORB_ERR_DEVICE = -4
+ORB_ERR_ABORTED = -5
+ORB_ERR_INTERNAL = -6
+
+# cv::KeyPoint layout (28 bytes)
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+assert KEYPOINT_DTYPE.itemsize == 28
+
+
+class OrbGpuError(RuntimeError):
+    def __init__(self, code: int, where: str, msg: str = ""):
+        super().__init__(f"{where} failed with status {code}: {msg}")
+        self.code = code
+
+
+class OrbParams(ctypes.Structure):
+    _fields_ = [("nfeatures", ctypes.c_int32), ("scale_factor", ctypes.c_float), ("nlevels", ctypes.c_int32),
+                ("ini_th_fast", ctypes.c_int32), ("min_th_fast", ctypes.c_int32)]
+
+
+_vp, _i, _f, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
+_ip = ctypes.POINTER(ctypes.c_int)
+_fp = ctypes.POINTER(ctypes.c_float)
+
+# (name, restype, argtypes) for every symbol include/orbgpu.h declares
+PROTOTYPES = {
+    "orb_device_count": (_i, []),
+    "orb_last_error": (ctypes.c_char_p, []),
+    "orb_extractor_create": (_i, [ctypes.POINTER(OrbParams), _i, _i, _i, ctypes.POINTER(_vp)]),
+    "orb_extractor_destroy": (_i, [_vp]),
+    "orb_extractor_scales": (_i, [_vp, _fp, _fp, _fp, _fp, _ip]),
+    "orb_extract": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _ip]),
+    "orb_extract_batch_device": (_i, [_vp, _vp, _i, _i, _i, _i, _sz, _i, _i, _vp, _vp, _i, _vp, _vp]),
+    "orb_extractor_level": (_i, [_vp, _i, _i, ctypes.POINTER(_vp), _ip, _ip, _ip]),
+    "orb_extractor_level_download": (_i, [_vp, _i, _i, _vp]),
+    "orb_descriptor_distance": (_i, [_vp, _vp]),
+    "orb_hamming_knn2_device": (_i, [_vp, _i, _vp, _i, _vp, _vp, _vp, _vp]),
+}
+
+# parity / debugging hooks exported by the library (not part of the public header)
+DEBUG_PROTOTYPES = {
+    "orb_debug_level_candidates": (_i, [_vp, _i, _i, _vp, _i, _vp, _i]),
+    "orb_debug_level_selected": (_i, [_vp, _i, _i, _vp, _i]),
+    "orb_debug_level_blurred": (_i, [_vp, _i, _i, _vp]),
+    "orb_debug_status": (_i, [_vp]),
+}
+
+_LIB = None
+
+
+def header_symbols() -> list[str]:
+    """Function names declared in include/orbgpu.h (parsed, so the ABI test follows the header)."""
+    import re
+    hdr = (PKG_DIR.parent / "include" / "orbgpu.h").read_text()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    return sorted(set(re.findall(r"\b(orb_[a-z0-9_]+)\s*\(", hdr)))
+
+
+def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
+    """Load liborbgpu.so and declare its prototypes.  Raises if the library was not built."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = pathlib.Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise FileNotFoundError(f"{p} not found: build it with `make` (or __graft_entry__.build())")
+    lib = ctypes.CDLL(str(p))
+    for name, (res, args) in {**PROTOTYPES, **DEBUG_PROTOTYPES}.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _LIB = lib
+    return lib
+
+
+def last_error() -> str:
+    return load().orb_last_error().decode(errors="replace")
+
+
+def check(code: int, where: str) -> int:
+    if code < 0:
+        raise OrbGpuError(code, where, last_error())
+    return code
+
+
+def device_count() -> int:
+    return load().orb_device_count()
+
+
+def require_device() -> None:
+    if device_count() <= 0:
+        raise OrbGpuError(ORB_ERR_DEVICE, "liborbgpu", "no HIP device visible (the HIP path has no CPU fallback)")

@@ -1,0 +1,162 @@
+"""GPU parity of the HIP ORB extractor against the CPU oracle, stage by stage and end to end.
+
+Bar: bit-exact (pyramid bytes, blurred bytes, FAST candidates + per-cell thresholds, quad-tree
+selection order, keypoint structs, descriptors, monoIndex).  Runs on the MI355X box (-m gpu).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames(synth):
+    left, right, _ = synth.stereo_pair(752, 480, seed=200)
+    return {
+        "poly640": (synth.polygon_frame(640, 480, seed=1), 1000, (0, 1000)),
+        "noise640": (synth.blurred_noise_frame(640, 480, seed=2), 1000, (0, 0)),
+        "stereoL752": (left, 1200, (0, 0)),
+        "stereoR752": (right, 1200, (0, 0)),
+        "poly1280": (synth.polygon_frame(1280, 720, seed=5), 1000, (0, 1000)),
+        "init5000": (synth.polygon_frame(640, 480, seed=11), 5000, (0, 1000)),
+        "odd_size": (synth.polygon_frame(643, 397, seed=13), 800, (100, 400)),
+        "noise1280": (synth.blurred_noise_frame(1280, 720, seed=3), 1000, (0, 1000)),
+    }
+
+
+CASES = ["poly640", "noise640", "stereoL752", "stereoR752", "poly1280", "init5000", "odd_size", "noise1280"]
+
+
+@pytest.fixture(scope="module")
+def frames(synth):
+    return _frames(synth)
+
+
+def _decode(keys: np.ndarray):
+    keys = keys.astype(np.uint64)
+    return np.stack([(keys >> 8) & 0xFFF, keys >> 20, keys & 0xFF], axis=1).astype(np.int64)
+
+
+def _first_diff(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    if a.shape != b.shape:
+        return f"shape {a.shape} vs {b.shape}"
+    idx = np.argwhere(a != b)
+    return f"{len(idx)} diffs, first at {idx[0].tolist()}: {a[tuple(idx[0])]} vs {b[tuple(idx[0])]}" if len(idx) else ""
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_extract_parity(pkg, oracle, frames, case):
+    img, nf, lap = frames[case]
+    h, w = img.shape
+    ex = pkg.ORBextractor(nf, 1.2, 8, 20, 7, max_width=1280, max_height=720)
+    ref = oracle.OracleExtractor(nf, 1.2, 8, 20, 7)
+    kps, desc, mono = ex(img, None, lap)
+    rkps, rdesc, rmono = ref(img, lap)
+    lib = ex._lib
+    for l in range(8):
+        # 1. pyramid (padded planes incl. the REFLECT_101 frame)
+        gp, rp = ex.level_padded(l), ref.level_padded(l)
+        assert np.array_equal(gp, rp), f"{case} level {l} pyramid: {_first_diff(gp, rp)}"
+        # 2. blurred level == GaussianBlur(level.clone(), 7x7, 2) of the oracle's level
+        lw, lh = rp.shape[1] - 38, rp.shape[0] - 38
+        gb = np.zeros((lh, lw), np.uint8)
+        assert lib.orb_debug_level_blurred(ex._h, 0, l, gb.ctypes.data) == 0
+        rb = oracle.gaussian_blur(rp[19:-19, 19:-19])
+        assert np.array_equal(gb, rb), f"{case} level {l} blur: {_first_diff(gb, rb)}"
+        # 3. FAST candidates in cell order + per-cell threshold choice
+        rc = ref.level_candidates(l)
+        rthr = ref.level_cell_thresholds(l)
+        cap = max(1, len(rc) + 64)
+        buf = np.zeros(cap, np.uint32)
+        thr = np.zeros(len(rthr) + 1, np.uint8)
+        n = lib.orb_debug_level_candidates(ex._h, 0, l, buf.ctypes.data, cap, thr.ctypes.data, len(thr))
+        assert n == len(rc), f"{case} level {l}: {n} candidates vs oracle {len(rc)}"
+        got = _decode(buf[:n])
+        exp = np.stack([rc["x"], rc["y"], rc["response"]], axis=1).astype(np.int64)
+        assert np.array_equal(got, exp), f"{case} level {l} candidates: {_first_diff(got, exp)}"
+        assert np.array_equal(thr[:len(rthr)].astype(np.int32), rthr), f"{case} level {l} thresholds"
+        # 4. quad-tree selection, in list order (level coordinates)
+        rk = ref.level_keys(l)
+        sbuf = np.zeros(len(rk) + 64, np.uint32)
+        ns = lib.orb_debug_level_selected(ex._h, 0, l, sbuf.ctypes.data, len(sbuf))
+        assert ns == len(rk), f"{case} level {l}: {ns} selected vs oracle {len(rk)}"
+        sel = _decode(sbuf[:ns]) + np.array([16, 16, 0])
+        exp = np.stack([rk["x"], rk["y"], rk["response"]], axis=1).astype(np.int64)
+        assert np.array_equal(sel, exp), f"{case} level {l} selection: {_first_diff(sel, exp)}"
+    assert lib.orb_debug_status(ex._h) == 0
+    # 5. end to end: keypoints (bitwise), descriptors, monoIndex
+    assert mono == rmono
+    assert len(kps) == len(rkps)
+    assert np.array_equal(kps.view(np.uint8), rkps.view(np.uint8)), \
+        f"{case} keypoints: {_first_diff(kps.view(np.uint32).reshape(-1, 7), rkps.view(np.uint32).reshape(-1, 7))}"
+    assert np.array_equal(desc, rdesc), f"{case} descriptors: {_first_diff(desc, rdesc)}"
+
+
+def test_batch_equals_single_calls(pkg, oracle, synth):
+    import torch
+    frames = synth.frame_batch(6, 640, 480, seed0=300)
+    ex = pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=640, max_height=480, max_batch=8)
+    imgs = torch.from_numpy(frames).cuda()
+    kps, desc, counts = ex.extract_batch_device(imgs, (0, 1000))
+    torch.cuda.synchronize()
+    counts = counts.cpu().numpy()
+    ref = oracle.OracleExtractor(1000, 1.2, 8, 20, 7)
+    for f in range(len(frames)):
+        rk, rd, rm = ref(frames[f], (0, 1000))
+        n = int(counts[f, 0])
+        assert n == len(rk) and int(counts[f, 1]) == rm
+        gk = pkg.keypoints_to_structured(kps[f], n)
+        assert np.array_equal(gk.view(np.uint8), rk.view(np.uint8)), f"frame {f} keypoints"
+        assert np.array_equal(desc[f, :n].cpu().numpy(), rd), f"frame {f} descriptors"
+
+
+def test_empty_image_and_capacity(pkg):
+    ex = pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=640, max_height=480)
+    k, d, m = ex(np.zeros((0, 0), np.uint8))
+    assert m == -1 and len(k) == 0 and d is None
+    # a flat image has no corners at all
+    k, d, m = ex(np.full((480, 640), 128, np.uint8), None, (0, 1000))
+    assert len(k) == 0 and m == 0
+    with pytest.raises(Exception):
+        ex(np.zeros((800, 900), np.uint8))  # larger than the handle was created for
+
+
+def test_mv_image_pyramid_and_getters(pkg, oracle, synth):
+    img = synth.polygon_frame(640, 480, seed=21)
+    ex = pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=640, max_height=480)
+    ex(img, None, (0, 0))
+    pyr = ex.mvImagePyramid
+    assert [p.shape for p in pyr] == [(480, 640), (400, 533), (333, 444), (278, 370), (231, 309), (193, 257),
+                                      (161, 214), (134, 179)]
+    assert np.array_equal(pyr[0], img)
+    p = oracle.OracleExtractor(1000, 1.2, 8, 20, 7).params()
+    assert ex.GetLevels() == 8
+    assert np.array_equal(np.float32(ex.GetScaleFactors()), p["scale"])
+    assert np.array_equal(np.float32(ex.GetInverseScaleSigmaSquares()), p["inv_sigma2"])
+    assert ex.mnFeaturesPerLevel == list(p["per_level"])
+
+
+def test_hamming_knn2(pkg, oracle):
+    import torch
+    rng = np.random.default_rng(9)
+    q = rng.integers(0, 256, (700, 32), dtype=np.uint8)
+    t = rng.integers(0, 256, (1300, 32), dtype=np.uint8)
+    t[5] = q[3]
+    t[17] = q[3]  # a tie at distance 0: the first index wins
+    idx, d1, d2 = pkg.ORBmatcher.knn2_device(torch.from_numpy(q).cuda(), torch.from_numpy(t).cuda())
+    idx, d1, d2 = idx.cpu().numpy(), d1.cpu().numpy(), d2.cpu().numpy()
+    D = np.unpackbits(q[:, None, :] ^ t[None, :, :], axis=2).sum(axis=2)
+    for i in range(len(q)):
+        best, second, bi = 257, 257, -1
+        for j in range(len(t)):
+            d = D[i, j]
+            if d < best:
+                second, best, bi = best, d, j
+            elif d < second:
+                second = d
+        assert (idx[i], d1[i], d2[i]) == (bi, best, second)
+    assert idx[3] == 5 and d1[3] == 0 and d2[3] == 0
