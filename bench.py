@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X ORB front-end hot path (BASELINE.json metric, config C2 at N=1).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+
+One "step" = ORBextractor::operator() on one batch of 64 synthetic 640x480 frames (nFeatures 1000,
+8 levels, scale 1.2, FAST 20/7), device-resident inputs and outputs, on each rank's GPU.  Frames are
+independent units: each rank extracts its own batch (weak scaling, no data-path collective).
+`value` = keypoints extracted+described by all ranks per ms of the max-over-ranks timed region.
+
+Extra fields: `roofline` for the dominant kernel (HIP-event time on the launch stream, algorithmic
+bytes per DESIGN.md), `cpu_baseline` (the CPU oracle -- a restatement of the reference -- timed on
+this host's cores on a bounded sample), `stages_ms` (per-stage HIP-event ms per step).
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import importlib.util
+import json
+import os
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+FRAMES, WIDTH, HEIGHT, NFEAT, NLEVELS = 64, 640, 480, 1000, 8
+
+
+def load_package():
+    if "orbslam3_amd" in sys.modules:
+        return sys.modules["orbslam3_amd"]
+    pkg_dir = ROOT / "orb-slam3_byzyh_amd"
+    spec = importlib.util.spec_from_file_location("orbslam3_amd", pkg_dir / "__init__.py",
+                                                  submodule_search_locations=[str(pkg_dir)])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["orbslam3_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def level_sizes(w, h, n=NLEVELS, s=1.2):
+    import numpy as np
+    out, f = [], np.float32(1.0)
+    for l in range(n):
+        if l:
+            f = np.float32(float(f) * float(np.float32(s)))
+        inv = np.float32(1.0) / f
+        out.append((int(np.rint(np.float32(w) * inv)), int(np.rint(np.float32(h) * inv))))
+    return out
+
+
+def algorithmic_bytes_per_frame(w, h, nkp):
+    """Per-frame algorithmic bytes of each stage (DESIGN.md sec. Measurement)."""
+    sizes = level_sizes(w, h)
+    px = [a * b for a, b in sizes]
+    pad = [(a + 38) * (b + 38) for a, b in sizes]
+    return {
+        # read L0 + read levels 0..6 to resize; write every padded plane and every blurred level
+        "pyramid": w * h + sum(px[:-1]) + sum(pad) + sum(px),
+        # read every level once; candidates are ~1% of pixels (not counted)
+        "fast": sum(px),
+        # candidates in, selected keys out (small); counted as one level read equivalent of 4 B/cand
+        "quadtree": 0,
+        "place": 0,
+        # per keypoint: 749-px disc + 512 samples in, 28 + 32 B out
+        "describe": nkp * (749 + 512 + 60),
+        # SURVEY.md sec. 8(d) whole-path figure: L0 read + levels 1..7 written and read + kps/descs out
+        "path": w * h + 2 * sum(px[1:]) + nkp * 60,
+    }
+
+
+def cpu_baseline(oracle_mod, frames, budget_s=10.0):
+    """Oracle (CPU restatement of ORBextractor) on a thread pool, one frame per thread at a time."""
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))
+    ex = [oracle_mod.OracleExtractor(NFEAT, 1.2, NLEVELS, 20, 7) for _ in range(cores)]
+    t0 = time.perf_counter()
+    done = [0] * cores
+    feats = [0] * cores
+
+    def worker(i):
+        j = i
+        while time.perf_counter() - t0 < budget_s:
+            k, _, _ = ex[i](frames[j % len(frames)], (0, 1000))
+            feats[i] += len(k)
+            done[i] += 1
+            j += cores
+
+    with cf.ThreadPoolExecutor(cores) as pool:
+        list(pool.map(worker, range(cores)))
+    dt = time.perf_counter() - t0
+    nf = sum(done)
+    return {"value": round(sum(feats) / (dt * 1e3), 3), "unit": "features/ms", "cores": cores, "kind": "port",
+            "sample": f"{nf} frames of the C2 set (640x480, nFeatures 1000) in {dt:.1f} s on {cores} threads, "
+                      "oracle/orb_extractor_oracle.cpp -O2"}
+
+
+def pmc_traffic():
+    p = ROOT / "profiles" / "pmc_latest.json"
+    if p.exists():
+        try:
+            return json.loads(p.read_text())
+        except Exception:
+            return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=FRAMES)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    pkg = load_package()
+    from orbslam3_amd import synth
+
+    nfr = args.frames
+    frames = np.stack([synth.polygon_frame(WIDTH, HEIGHT, seed=100 + i) for i in range(nfr)])
+    imgs = torch.from_numpy(frames).to(dev)
+    ex = pkg.ORBextractor(NFEAT, 1.2, NLEVELS, 20, 7, max_width=WIDTH, max_height=HEIGHT, max_batch=nfr)
+    cap = NFEAT + 16 * NLEVELS
+    out = (torch.empty((nfr, cap, 7), dtype=torch.float32, device=dev),
+           torch.empty((nfr, cap, 32), dtype=torch.uint8, device=dev),
+           torch.empty((nfr, 2), dtype=torch.int32, device=dev))
+    stream = torch.cuda.current_stream(dev)
+    for _ in range(args.warmup):
+        ex.extract_batch_device(imgs, (0, 1000), cap=cap, out=out, stream=stream)
+    torch.cuda.synchronize(dev)
+    counts = out[2].cpu().numpy()
+    feats_per_step = int(counts[:, 0].sum())
+    if (counts[:, 1] < 0).any():
+        raise RuntimeError("a frame exceeded the keypoint capacity")
+
+    ex.profile(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ex.extract_batch_device(imgs, (0, 1000), cap=cap, out=out, stream=stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed_ms = (time.perf_counter() - t0) * 1e3
+    stage_ms, launches, _ = ex.stage_ms()
+    ex.profile(False)
+
+    total_feats = feats_per_step * args.steps
+    if world > 1:
+        t = torch.tensor([elapsed_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed_ms = float(t.item())
+        f = torch.tensor([total_feats], dtype=torch.int64, device=dev)
+        dist.all_reduce(f, op=dist.ReduceOp.SUM)
+        total_feats = int(f.item())
+
+    if rank == 0:
+        per_step = {k: v / max(1, launches) for k, v in stage_ms.items()}
+        dom = max(per_step, key=per_step.get)
+        nkp_frame = feats_per_step / nfr
+        alg = algorithmic_bytes_per_frame(WIDTH, HEIGHT, nkp_frame)
+        dom_bytes = alg[dom] * nfr
+        achieved = dom_bytes / (per_step[dom] * 1e-3) / 1e9 if per_step[dom] > 0 else 0.0
+        pmc = pmc_traffic()
+        traffic = None
+        if pmc and pmc.get("kernel_stage") == dom and pmc.get("frames_per_launch") == nfr:
+            traffic = pmc.get("hbm_bytes_per_launch")
+        result = {
+            "metric": "ORB features/ms (640x480, 8-level) + LocalBA iter ms @1/2/4/8 GPU",
+            "value": round(total_feats / elapsed_ms, 3),
+            "unit": "features/ms",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed_ms / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (polygon frames, seeds 100..163; no EuRoC images ship with the reference)",
+            "config": {"workload": "C2: batch of 64 synthetic 640x480 frames per GPU, nFeatures=1000, 8 levels, "
+                                   "extraction+description (ORBextractor::operator())",
+                       "frames_per_gpu": nfr, "width": WIDTH, "height": HEIGHT, "nfeatures": NFEAT,
+                       "nlevels": NLEVELS, "features_per_step_per_gpu": feats_per_step,
+                       "parallelism": f"frame-sharded x{world}"},
+            "stages_ms": {k: round(v, 4) for k, v in per_step.items()},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "algorithmic_bytes_per_launch": int(dom_bytes)},
+            "localba_iter_ms": None,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            from oracle import oracle as oracle_mod
+            result["cpu_baseline"] = cpu_baseline(oracle_mod, frames[: min(nfr, 32)], args.cpu_budget)
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -64,7 +64,11 @@ DEBUG_PROTOTYPES = {
     "orb_debug_level_selected": (_i, [_vp, _i, _i, _vp, _i]),
     "orb_debug_level_blurred": (_i, [_vp, _i, _i, _vp]),
     "orb_debug_status": (_i, [_vp]),
+    "orb_extractor_profile": (_i, [_vp, _i]),
+    "orb_extractor_stage_ms": (_i, [_vp, _fp, _ip, ctypes.POINTER(ctypes.c_longlong)]),
 }
+
+STAGES = ("pyramid", "fast", "quadtree", "place", "describe")
 
 _LIB = None
 
@@ -83,6 +87,13 @@ def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     if _LIB is not None and path is None:
         return _LIB
     p = pathlib.Path(path) if path else LIB_PATH
+    # One HIP runtime per process: torch wheels bundle their own libamdhip64/libhsa-runtime64 (same
+    # sonames as /opt/rocm's).  Importing torch first makes liborbgpu.so bind to that already-loaded
+    # copy instead of pulling in a second ROCr instance, which would fail to open the device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not p.exists():
         raise FileNotFoundError(f"{p} not found: build it with `make` (or __graft_entry__.build())")
     lib = ctypes.CDLL(str(p))

@@ -799,6 +799,11 @@ struct Extractor {
     hipStream_t stream = nullptr;
     int last_n = 0;
     int qt_lds = 0;
+    // optional per-stage timing: HIP events recorded on the launch stream between the stages
+    bool profile = false;
+    std::vector<hipEvent_t> events;   // kStages + 1 per profiled launch
+    int ev_used = 0;                  // launches recorded since the last read
+    long long frames_profiled = 0;
 };
 
 }  // namespace orbgpu
@@ -855,7 +860,21 @@ int launch_batch(Extractor* e, const uint8_t* d_images, int n, int w, int h, int
                  hipStream_t st) {
     const orbgpu::Geometry& G = e->geo;
     const orbgpu::KernelGeom& k = G.k;
+    hipEvent_t* ev = nullptr;
+    if (e->profile) {
+        const size_t need = (size_t)(e->ev_used + 1) * (orbgpu::kStages + 1);
+        while (e->events.size() < need) {
+            hipEvent_t x;
+            if (hipEventCreate(&x) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "hipEventCreate failed");
+            e->events.push_back(x);
+        }
+        ev = &e->events[(size_t)e->ev_used * (orbgpu::kStages + 1)];
+        e->ev_used++;
+        e->frames_profiled += n;
+    }
+    auto mark = [&](int i) { if (ev) hipEventRecord(ev[i], st); };
     hipMemsetAsync(e->d_status, 0, sizeof(int), st);
+    mark(0);
     for (int l = 0; l < k.nlevels; ++l) {
         const orbgpu::LevelGeom& L = k.lv[l];
         dim3 grid((L.pw + kTileW - 1) / kTileW, (L.ph + kTileH - 1) / kTileH, n);
@@ -866,15 +885,20 @@ int launch_batch(Extractor* e, const uint8_t* d_images, int n, int w, int h, int
             hipLaunchKernelGGL(k_pyramid_level<false>, grid, dim3(256), 0, st, k, l, nullptr, 0LL, 0, e->d_pyr,
                                e->d_blur, e->d_xtab, e->d_ytab);
     }
+    mark(1);
     const int win_cap = (G.max_win + 15) & ~15;
     hipLaunchKernelGGL(k_fast_cells, dim3((k.ncells + 3) / 4, n), dim3(256), 4 * 2 * win_cap, st, k, e->d_cells,
                        win_cap, e->d_pyr, e->d_cand, e->d_cell_count, e->d_cell_thr);
+    mark(2);
     hipLaunchKernelGGL(k_quadtree, dim3(k.nlevels, n), dim3(64), e->qt_lds, st, k, e->d_cells, e->d_cand,
                        e->d_cell_count, e->d_scratch, e->d_sel, e->d_sel_count, e->qt_lds, e->d_status);
+    mark(3);
     hipLaunchKernelGGL(k_place, dim3(n), dim3(64), 0, st, k, e->d_sel, e->d_sel_count, e->d_dst, lap0, lap1, cap,
                        d_counts);
+    mark(4);
     hipLaunchKernelGGL(k_describe, dim3((G.max_sel + 3) / 4, k.nlevels, n), dim3(256), 0, st, k, e->d_pyr, e->d_blur,
                        e->d_sel, e->d_sel_count, e->d_dst, d_counts, cap, d_kps, d_desc);
+    mark(5);
     if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "kernel launch failed");
     e->last_n = n;
     return ORB_OK;
@@ -916,6 +940,7 @@ int orb_extractor_destroy(orb_extractor_t h) {
                     e->d_img, e->d_kps, e->d_desc, e->d_counts};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
+    for (hipEvent_t x : e->events) (void)hipEventDestroy(x);
     if (e->stream) hipStreamDestroy(e->stream);
     delete e;
     return ORB_OK;
@@ -1075,6 +1100,36 @@ int orb_debug_level_blurred(orb_extractor_t h, int frame, int level, uint8_t* ho
     hipDeviceSynchronize();
     if (hipMemcpy2D(host_view, L.w, src, L.pitch, L.w, L.h, hipMemcpyDeviceToHost) != hipSuccess)
         return orbgpu_fail(ORB_ERR_DEVICE, "download failed");
+    return ORB_OK;
+}
+
+// Per-stage timing (HIP events on the launch stream).  enable != 0 starts recording (and clears
+// what was recorded); orb_extractor_stage_ms waits for the recorded launches and returns the summed
+// milliseconds of [pyramid, fast, quadtree, place, describe] and the number of launches / frames.
+int orb_extractor_profile(orb_extractor_t h, int enable) {
+    Extractor* e = reinterpret_cast<Extractor*>(h);
+    if (!e) return ORB_ERR_ARG;
+    e->profile = enable != 0;
+    e->ev_used = 0;
+    e->frames_profiled = 0;
+    return ORB_OK;
+}
+
+int orb_extractor_stage_ms(orb_extractor_t h, float* ms, int* launches, long long* frames) {
+    Extractor* e = reinterpret_cast<Extractor*>(h);
+    if (!e || !ms) return ORB_ERR_ARG;
+    for (int s = 0; s < orbgpu::kStages; ++s) ms[s] = 0.f;
+    for (int i = 0; i < e->ev_used; ++i) {
+        hipEvent_t* ev = &e->events[(size_t)i * (orbgpu::kStages + 1)];
+        if (hipEventSynchronize(ev[orbgpu::kStages]) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "event sync");
+        for (int s = 0; s < orbgpu::kStages; ++s) {
+            float t = 0.f;
+            hipEventElapsedTime(&t, ev[s], ev[s + 1]);
+            ms[s] += t;
+        }
+    }
+    if (launches) *launches = e->ev_used;
+    if (frames) *frames = e->frames_profiled;
     return ORB_OK;
 }
 

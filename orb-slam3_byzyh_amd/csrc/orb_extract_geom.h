@@ -15,6 +15,7 @@ constexpr int kHalfPatch = 15;  // HALF_PATCH_SIZE, src/ORBextractor.cc:77
 constexpr int kPatchSize = 31;  // PATCH_SIZE, src/ORBextractor.cc:76
 constexpr int kCellW = 35;      // W, src/ORBextractor.cc:1069
 constexpr int kMaxRoots = 8;
+constexpr int kStages = 5;      // timed stages of one extraction launch
 
 // per level, passed to kernels by value (inside KernelGeom)
 struct LevelGeom {

@@ -131,6 +131,18 @@ class ORBextractor:
         self._last_frames = b
         return kps, desc, counts
 
+    # ---- per-stage timing (HIP events on the launch stream)
+    def profile(self, enable: bool = True) -> None:
+        check(self._lib.orb_extractor_profile(self._h, 1 if enable else 0), "orb_extractor_profile")
+
+    def stage_ms(self):
+        """Summed ms per stage since profile(True), the number of launches and frames recorded."""
+        ms = (ctypes.c_float * len(_lib.STAGES))()
+        n = ctypes.c_int()
+        fr = ctypes.c_longlong()
+        check(self._lib.orb_extractor_stage_ms(self._h, ms, ctypes.byref(n), ctypes.byref(fr)), "orb_extractor_stage_ms")
+        return dict(zip(_lib.STAGES, (float(v) for v in ms))), n.value, fr.value
+
     # ---- public pyramid, include/ORBextractor.h:83
     def level_padded(self, level: int, frame: int = 0) -> np.ndarray:
         """Padded plane ((h+38) x (w+38)) of level `level` of frame `frame` of the last call."""
