@@ -47,10 +47,11 @@ __device__ __forceinline__ int blur_tap(int k) {
     return k == 3 ? 56 : (k == 2 || k == 4) ? 48 : (k == 1 || k == 5) ? 34 : 18;
 }
 
+// BORDER_REFLECT_101 index for offsets at most len-1 outside [0, len): one reflection, branch-free.
+// Callers stay within the 19-px frame + 3-px blur halo and build_geometry requires len >= 38.
 __device__ __forceinline__ int reflect101(int p, int len) {
-    if (len == 1) return 0;
-    while ((unsigned)p >= (unsigned)len) p = p < 0 ? -p : 2 * len - 2 - p;
-    return p;
+    p = p < 0 ? -p : p;
+    return p >= len ? 2 * len - 2 - p : p;
 }
 
 __device__ __forceinline__ void wave_sync() {
@@ -74,113 +75,181 @@ __device__ __forceinline__ int wave_sum(int v) {
 // ================================================================================================
 // 1. pyramid level: padded plane + blurred view, src:1687-1740 and src:1629-1637
 // ================================================================================================
-constexpr int kTileW = 64, kTileH = 16, kHalo = 3;
-constexpr int kLW = kTileW + 2 * kHalo, kLH = kTileH + 2 * kHalo;  // 70 x 22
+constexpr int kTileW = 128, kTileH = 16, kHalo = 3;  // 128-byte rows: every store fills whole cache lines
+constexpr int kLW = kTileW + 2 * kHalo, kLH = kTileH + 2 * kHalo;  // 134 x 22
+constexpr int kBoxW = 2 * kLW + 4, kBoxH = 2 * kLH + 4;           // source box for scale factors <= 2
 
-// cv::resize INTER_LINEAR 8U value of level pixel (vx, vy) from the previous level view S
-__device__ __forceinline__ int resize_px(const uint8_t* __restrict__ S, int sstride, int sw, int vx, int vy,
-                                         const int2* __restrict__ xt, const int4* __restrict__ yt, int simd_end) {
-    const int2 X = xt[vx];
-    const int4 Y = yt[vy];
-    const int sx = X.x, sx1 = min(sx + 1, sw - 1);
-    const int a0 = X.y & 0xffff, a1 = X.y >> 16;
-    const uint8_t* R0 = S + (size_t)Y.x * sstride;
-    const uint8_t* R1 = S + (size_t)Y.y * sstride;
-    const int h0 = R0[sx] * a0 + R0[sx1] * a1;
-    const int h1 = R1[sx] * a0 + R1[sx1] * a1;
-    int v;
-    if (vx < simd_end) {  // VResizeLinearVec_32s8u: v_mul_hi on (S >> 4), then rounding shift by 2
-        const int t0 = min(h0 >> 4, 32767), t1 = min(h1 >> 4, 32767);
-        v = (((t0 * Y.z) >> 16) + ((t1 * Y.w) >> 16) + 2) >> 2;
-    } else {              // FixedPtCast<int, uchar, 22>
-        v = (h0 * Y.z + h1 * Y.w + (1 << 21)) >> 22;
-    }
-    return min(max(v, 0), 255);
+// 8 bytes from a 4-byte-aligned LDS row at any byte offset, as aligned dword reads + v_alignbyte.
+// (Adjacent byte reads would otherwise be merged by the compiler into unaligned ds_read_u16/b64,
+// which gfx950 replays: SQ_LDS_UNALIGNED_STALL.)
+__device__ __forceinline__ unsigned long long lds_bytes8(const uint8_t* row, int off) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(row) + (off >> 2);
+    const unsigned sh = (unsigned)(off & 3);
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+    const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+    return lo | ((unsigned long long)hi << 32);
 }
 
+// range of reflect101(p) over p in [a, b] (view coordinates), len >= 38
+__device__ __forceinline__ void reflect_range(int a, int b, int len, int& lo, int& hi) {
+    lo = 1 << 30; hi = -1;
+    if (a < 0) { const int e = min(b, -1); lo = min(lo, -e); hi = max(hi, -a); }
+    if (b >= 0 && a < len) { lo = min(lo, max(a, 0)); hi = max(hi, min(b, len - 1)); }
+    if (b >= len) { const int s0 = max(a, len); lo = min(lo, 2 * len - 2 - b); hi = max(hi, 2 * len - 2 - s0); }
+}
+
+// cv::resize INTER_LINEAR source index of destination coordinate d (resize.cpp coefficient loop)
+__device__ __forceinline__ int resize_src_index(int d, double scale, int slen) {
+    const float f = (float)((d + 0.5) * scale - 0.5);
+    int s = (int)f;
+    s -= (s > f);
+    return min(max(s, 0), slen - 1);
+}
+
+// One workgroup = one 64 x 32 tile of a padded level plane (+3-px halo for the blur).
+// Level 0 copies the input; level l > 0 resizes the previous level view.  The source pixels the tile
+// needs are staged in LDS (one round of independent loads), the interpolation reads LDS only.
 template <bool kLevel0>
-__global__ __launch_bounds__(256) void k_pyramid_level(KernelGeom g, int level, const uint8_t* __restrict__ in,
-                                                       long long in_frame_stride, int in_stride,
-                                                       uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
-                                                       const int2* __restrict__ xtab, const int4* __restrict__ ytab) {
-    __shared__ uint8_t tile[kLH][kLW + 2];
+__global__ __launch_bounds__(256) void k_pyramid_level(const KernelGeom* __restrict__ gp, int level,
+                                                       const uint8_t* __restrict__ in, long long in_frame_stride,
+                                                       int in_stride, uint8_t* __restrict__ pyr,
+                                                       uint8_t* __restrict__ blur, const int2* __restrict__ xtab,
+                                                       const int4* __restrict__ ytab) {
+    const KernelGeom& g = *gp;
+    __shared__ __attribute__((aligned(16))) uint8_t box[kBoxH * kBoxW];
+    __shared__ __attribute__((aligned(16))) uint8_t tile[kLH][kLW + 2 + 8];  // rows 4-aligned, +8 readable slack
     __shared__ int hsum[kLH][kTileW];
-    const int f = blockIdx.z;
+    __shared__ int2 xs[kLW];
+    __shared__ int4 ys[kLH];
+    const int f = blockIdx.z, tid = threadIdx.x;
     const LevelGeom& L = g.lv[level];
     const int X0 = blockIdx.x * kTileW, Y0 = blockIdx.y * kTileH;
     uint8_t* plane = pyr + (size_t)f * g.pyr_frame_bytes + L.plane_off;
     uint8_t* bplane = blur + (size_t)f * g.pyr_frame_bytes + L.plane_off;
+    // view-coordinate ranges this tile (+halo) reads
+    int vx0, vx1, vy0, vy1;
+    reflect_range(X0 - kHalo - kEdge, X0 + kTileW + kHalo - 1 - kEdge, L.w, vx0, vx1);
+    reflect_range(Y0 - kHalo - kEdge, Y0 + kTileH + kHalo - 1 - kEdge, L.h, vy0, vy1);
     const uint8_t* src;
-    int sstride, sw = 0;
+    int sstride, bx0, by0, bw, bh;
     if (kLevel0) {
         src = in + (size_t)f * in_frame_stride;
         sstride = in_stride;
+        bx0 = vx0; by0 = vy0; bw = vx1 - vx0 + 1; bh = vy1 - vy0 + 1;
     } else {
         const LevelGeom& P = g.lv[level - 1];
         src = pyr + (size_t)f * g.pyr_frame_bytes + P.plane_off + (size_t)kEdge * P.pitch + kEdge;
         sstride = P.pitch;
-        sw = P.w;
+        const double scx = 1. / ((double)L.w / P.w), scy = 1. / ((double)L.h / P.h);
+        bx0 = resize_src_index(vx0, scx, P.w);
+        by0 = resize_src_index(vy0, scy, P.h);
+        bw = min(resize_src_index(vx1, scx, P.w) + 1, P.w - 1) - bx0 + 1;
+        bh = min(resize_src_index(vy1, scy, P.h) + 1, P.h - 1) - by0 + 1;
+        // coefficient tables of the tile's columns / rows
+        if (tid < kLW) xs[tid] = xtab[L.xtab_off + reflect101(X0 - kHalo + tid - kEdge, L.w)];
+        else if (tid >= 192 && tid < 192 + kLH) ys[tid - 192] = ytab[L.ytab_off + reflect101(Y0 - kHalo + (tid - 192) - kEdge, L.h)];
     }
-    const int2* xt = xtab + (kLevel0 ? 0 : L.xtab_off);
-    const int4* yt = ytab + (kLevel0 ? 0 : L.ytab_off);
-    for (int i = threadIdx.x; i < kLH * kLW; i += 256) {
+    // stage the source box: 8 independent byte loads per thread per round
+    const int nbox = bw * bh;
+    for (int i0 = 0; i0 < nbox; i0 += 256 * 8) {
+        uint8_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = i0 + k * 256 + tid;
+            const int r = i / bw, c = i - (i / bw) * bw;
+            v[k] = i < nbox ? src[(size_t)(by0 + r) * sstride + bx0 + c] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = i0 + k * 256 + tid;
+            if (i < nbox) box[(i / bw) * kBoxW + (i - (i / bw) * bw)] = v[k];
+        }
+    }
+    __syncthreads();
+    // tile (+halo) values
+    for (int i = tid; i < kLH * kLW; i += 256) {
         const int ty = i / kLW, tx = i - ty * kLW;
-        const int vx = reflect101(X0 - kHalo + tx - kEdge, L.w);
-        const int vy = reflect101(Y0 - kHalo + ty - kEdge, L.h);
         int v;
-        if (kLevel0) v = src[(size_t)vy * sstride + vx];
-        else v = resize_px(src, sstride, sw, vx, vy, xt, yt, L.simd_end);
+        if (kLevel0) {
+            const int vx = reflect101(X0 - kHalo + tx - kEdge, L.w), vy = reflect101(Y0 - kHalo + ty - kEdge, L.h);
+            v = box[(vy - by0) * kBoxW + (vx - bx0)];
+        } else {
+            const int2 X = xs[tx];
+            const int4 Y = ys[ty];
+            const int sx = X.x - bx0, sx1 = min(X.x + 1, bx0 + bw - 1) - bx0;
+            const int a0 = X.y & 0xffff, a1 = X.y >> 16;
+            const uint8_t* R0 = box + (Y.x - by0) * kBoxW;
+            const uint8_t* R1 = box + (Y.y - by0) * kBoxW;
+            const int h0 = R0[sx] * a0 + R0[sx1] * a1, h1 = R1[sx] * a0 + R1[sx1] * a1;
+            const int vx = reflect101(X0 - kHalo + tx - kEdge, L.w);
+            if (vx < L.simd_end) {  // VResizeLinearVec_32s8u: v_mul_hi on (S >> 4), rounding shift by 2
+                const int t0 = min(h0 >> 4, 32767), t1 = min(h1 >> 4, 32767);
+                v = (((t0 * Y.z) >> 16) + ((t1 * Y.w) >> 16) + 2) >> 2;
+            } else {                // FixedPtCast<int, uchar, 22>
+                v = (h0 * Y.z + h1 * Y.w + (1 << 21)) >> 22;
+            }
+            v = min(max(v, 0), 255);
+        }
         tile[ty][tx] = (uint8_t)v;
     }
     __syncthreads();
-    // padded plane: 4 consecutive pixels per thread
+    // padded plane: 8 consecutive pixels per thread
+    const int r = tid >> 4, c = (tid & 15) * 8;
     {
-        const int r = threadIdx.x >> 4, c = (threadIdx.x & 15) * 4;
         const int py = Y0 + r, px = X0 + c;
         if (py < L.ph) {
             uint8_t* dst = plane + (size_t)py * L.pitch + px;
-            if (px + 3 < L.pw) {
-                const uint32_t w = tile[r + kHalo][c + kHalo] | (tile[r + kHalo][c + kHalo + 1] << 8) |
-                                   (tile[r + kHalo][c + kHalo + 2] << 16) | ((uint32_t)tile[r + kHalo][c + kHalo + 3] << 24);
-                *reinterpret_cast<uint32_t*>(dst) = w;
+            if (px + 7 < L.pw) {
+                *reinterpret_cast<unsigned long long*>(dst) = lds_bytes8(tile[r + kHalo], c + kHalo);
             } else {
-                for (int k = 0; k < 4 && px + k < L.pw; ++k) dst[k] = tile[r + kHalo][c + kHalo + k];
+                for (int k = 0; k < 8 && px + k < L.pw; ++k) dst[k] = tile[r + kHalo][c + kHalo + k];
             }
         }
     }
     // does this tile touch the view at all?
     if (X0 + kTileW <= kEdge || X0 >= kEdge + L.w || Y0 + kTileH <= kEdge || Y0 >= kEdge + L.h) return;
-    // horizontal 7-tap pass over all 22 rows (exact in 16 bits, kept as int)
-    for (int i = threadIdx.x; i < kLH * kTileW; i += 256) {
-        const int ty = i / kTileW, tx = i - ty * kTileW;
-        int acc = 0;
+    // GaussianBlur 7x7 sigma 2: horizontal pass (exact in 16 bits, kept as int), then vertical
+    for (int i = tid; i < kLH * kTileW / 4; i += 256) {  // 4 outputs per item from 3 aligned dwords
+        const int ty = i / (kTileW / 4), tx = (i - ty * (kTileW / 4)) * 4;
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(tile[ty]) + (tx >> 2);
+        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+        int px[12];
 #pragma unroll
-        for (int k = 0; k < 7; ++k) acc += blur_tap(k) * tile[ty][tx + k];
-        hsum[ty][tx] = acc;
+        for (int k = 0; k < 4; ++k) {
+            px[k] = (w0 >> (8 * k)) & 0xff;
+            px[4 + k] = (w1 >> (8 * k)) & 0xff;
+            px[8 + k] = (w2 >> (8 * k)) & 0xff;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            int acc = 0;
+#pragma unroll
+            for (int k = 0; k < 7; ++k) acc += blur_tap(k) * px[q + k];
+            hsum[ty][tx + q] = acc;
+        }
     }
     __syncthreads();
     {
-        const int r = threadIdx.x >> 4, c = (threadIdx.x & 15) * 4;
-        const int py = Y0 + r;
-        const int vy = py - kEdge;
+        const int py = Y0 + r, vy = py - kEdge;
         if (vy >= 0 && vy < L.h) {
-            uint32_t word = 0;
-            int acc4[4];
+            unsigned long long w = 0;
+            int outv[8];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < 8; ++q) {
                 int acc = 0;
 #pragma unroll
                 for (int k = 0; k < 7; ++k) acc += blur_tap(k) * hsum[r + k][c + q];
-                acc4[q] = min((acc + (1 << 15)) >> 16, 255);
-                word |= (uint32_t)acc4[q] << (8 * q);
+                outv[q] = min((acc + (1 << 15)) >> 16, 255);
+                w |= (unsigned long long)outv[q] << (8 * q);
             }
             const int px = X0 + c;
             uint8_t* dst = bplane + (size_t)py * L.pitch + px;
-            if (px >= kEdge && px + 3 < kEdge + L.w) {
-                *reinterpret_cast<uint32_t*>(dst) = word;
+            if (px >= kEdge && px + 7 < kEdge + L.w) {
+                *reinterpret_cast<unsigned long long*>(dst) = w;
             } else {
-                for (int q = 0; q < 4; ++q)
-                    if (px + q >= kEdge && px + q < kEdge + L.w) dst[q] = (uint8_t)acc4[q];
+                for (int q = 0; q < 8; ++q)
+                    if (px + q >= kEdge && px + q < kEdge + L.w) dst[q] = (uint8_t)outv[q];
             }
         }
     }
@@ -228,9 +297,36 @@ __device__ __forceinline__ int key_x(uint32_t k) { return (int)((k >> 8) & 0xfff
 __device__ __forceinline__ int key_y(uint32_t k) { return (int)(k >> 20); }
 __device__ __forceinline__ int key_score(uint32_t k) { return (int)(k & 0xff); }
 
-__global__ __launch_bounds__(256) void k_fast_cells(KernelGeom g, const CellDesc* __restrict__ cells, int win_cap,
+// corner(t) for the pixel at p: a run of >= 9 contiguous circle pixels all brighter than v+t or all
+// darker than v-t (FAST_t<16>, OpenCV fast.cpp).  Bit k of the 16-bit masks = circle pixel k.
+__device__ __forceinline__ bool has_run9(unsigned m) {
+    const unsigned m2 = m | (m << 16);  // circular
+    unsigned r = m2 & (m2 >> 1);        // runs of 2
+    r &= r >> 2;                        // 4
+    r &= r >> 4;                        // 8
+    r &= m2 >> 8;                       // 9
+    return (r & 0xFFFFu) != 0;
+}
+
+__device__ __forceinline__ bool fast_corner(const uint8_t* __restrict__ p, const int (&off)[16], int t) {
+    const int v = p[0], hi = v + t, lo = v - t;
+    unsigned bm = 0, dm = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int x = p[off[k]];
+        bm |= (unsigned)(x > hi) << k;
+        dm |= (unsigned)(x < lo) << k;
+    }
+    return has_run9(bm) || has_run9(dm);
+}
+
+// One wave per FAST cell.  LDS per wave: window | score map | candidate list (u16 pixel indices).
+// Pixels with score < minTh can neither be emitted nor beat an emitted neighbour, so the exact score
+// is computed only for the pixels that are corners at minTh (compacted list, no divergence).
+__global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict__ gp, const CellDesc* __restrict__ cells, int win_cap,
                                                     const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
                                                     int32_t* __restrict__ cell_count, uint8_t* __restrict__ cell_thr) {
+    const KernelGeom& g = *gp;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int cid = blockIdx.x * 4 + wave;
@@ -239,17 +335,25 @@ __global__ __launch_bounds__(256) void k_fast_cells(KernelGeom g, const CellDesc
     const CellDesc C = cells[cid];
     const LevelGeom& L = g.lv[C.level];
     const uint8_t* view = pyr + (size_t)f * g.pyr_frame_bytes + L.plane_off + (size_t)kEdge * L.pitch + kEdge;
-    uint8_t* win = smem + (size_t)wave * 2 * win_cap;
+    uint8_t* win = smem + (size_t)wave * 4 * win_cap;
     uint8_t* sc = win + win_cap;
+    uint16_t* cl = reinterpret_cast<uint16_t*>(sc + win_cap);
     const int ww = C.win_w, wh = C.win_h, n = ww * wh;
     const uint8_t* src = view + (size_t)C.ini_y * L.pitch + C.ini_x;
-    for (int i = lane; i < n; i += 64) {
-        const int r = i / ww, c = i - r * ww;
-        win[i] = src[(size_t)r * L.pitch + c];
-        sc[i] = 0;
+    for (int i = lane; i < n; i += 64) sc[i] = 0;
+    for (int c = lane; c < ww; c += 64) {
+        for (int r0 = 0; r0 < wh; r0 += 8) {  // 8 independent loads in flight per lane
+            uint8_t v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = r0 + k < wh ? src[(size_t)(r0 + k) * L.pitch + c] : 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (r0 + k < wh) win[(r0 + k) * ww + c] = v[k];
+        }
     }
     wave_sync();
-    const int dw = ww - 6, dh = wh - 6, nd = max(dw, 0) * max(dh, 0);
+    const int dw = ww - 6, dh = wh - 6;
+    const int nd = (dw > 0 && dh > 0) ? dw * dh : 0;
     int off[16];
     {
         const int cx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
@@ -257,36 +361,79 @@ __global__ __launch_bounds__(256) void k_fast_cells(KernelGeom g, const CellDesc
 #pragma unroll
         for (int k = 0; k < 16; ++k) off[k] = cx[k] + cy[k] * ww;
     }
-    for (int i = lane; i < nd; i += 64) {
-        const int r = 3 + i / dw, c = 3 + (i - (i / dw) * dw);
-        const int s = fast_score(win + r * ww + c, off);
-        sc[r * ww + c] = (uint8_t)min(max(s, 0), 255);
+    const int ini = g.ini_th, mint = g.min_th;
+    // 1a. compass filter at minTh: a 9-pixel arc always contains two circle pixels 4 apart among
+    //     {0, 4, 8, 12}, so only pixels with such a bright or dark pair can be corners.  Passing
+    //     pixels are compacted (row-major) into cl[].
+    int nlist = 0;
+    if (nd > 0) {
+        const int dr = 64 / dw, dc = 64 - dr * dw;
+        int r = lane / dw, c = lane - (lane / dw) * dw;
+        for (int i0 = 0; i0 < nd; i0 += 64) {
+            bool pass = false;
+            int idx = 0;
+            if (i0 + lane < nd) {
+                idx = (r + 3) * ww + (c + 3);
+                const uint8_t* q = win + idx;
+                const int v = q[0], hi = v + mint, lo = v - mint;
+                const int p0 = q[off[0]], p4 = q[off[4]], p8 = q[off[8]], p12 = q[off[12]];
+                const bool b0 = p0 > hi, b4 = p4 > hi, b8 = p8 > hi, b12 = p12 > hi;
+                const bool d0 = p0 < lo, d4 = p4 < lo, d8 = p8 < lo, d12 = p12 < lo;
+                pass = (b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0) | (d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0);
+            }
+            const unsigned long long m = ballot(pass);
+            if (pass) cl[nlist + rank_in(m)] = (uint16_t)idx;
+            nlist += __popcll(m);
+            c += dc;
+            r += dr;
+            if (c >= dw) { c -= dw; r++; }
+        }
     }
     wave_sync();
-    const int ini = g.ini_th, mint = g.min_th;
+    // 1b. full 9-arc test at minTh on the filtered pixels; in-place compaction keeps row-major order
+    int ncand = 0;
+    for (int j0 = 0; j0 < nlist; j0 += 64) {
+        const int j = j0 + lane;
+        int idx = 0;
+        bool is_c = false;
+        if (j < nlist) {
+            idx = cl[j];
+            is_c = fast_corner(win + idx, off, mint);
+        }
+        const unsigned long long m = ballot(is_c);
+        if (is_c) cl[ncand + rank_in(m)] = (uint16_t)idx;
+        ncand += __popcll(m);
+    }
+    wave_sync();
+    // 2. exact score of the candidates
+    for (int j = lane; j < ncand; j += 64) {
+        const int idx = cl[j];
+        sc[idx] = (uint8_t)min(max(fast_score(win + idx, off), 0), 255);
+    }
+    wave_sync();
+    // 3. iniTh first; minTh only if the cell has no corner at iniTh (src:1135-1148)
     bool any = false;
-    for (int i = lane; i < nd; i += 64) {
-        const int r = 3 + i / dw, c = 3 + (i - (i / dw) * dw);
-        const int idx = r * ww + c, s = sc[idx];
+    for (int j = lane; j < ncand; j += 64) {
+        const int idx = cl[j], s = sc[idx];
         any |= (s >= ini) && is_local_max(sc, ww, idx, s);
     }
     const int t = ballot(any) ? ini : mint;
+    // 4. emission in row-major order (the candidate list is row-major)
     uint32_t* out = cand + (size_t)f * g.cand_frame_cap + L.cand_off + C.slot;
     int count = 0;
-    for (int i0 = 0; i0 < nd; i0 += 64) {
-        const int i = i0 + lane;
+    for (int j0 = 0; j0 < ncand; j0 += 64) {
+        const int j = j0 + lane;
         bool keep = false;
-        int r = 0, c = 0, s = 0;
-        if (i < nd) {
-            r = 3 + i / dw;
-            c = 3 + (i - (i / dw) * dw);
-            const int idx = r * ww + c;
+        int idx = 0, s = 0;
+        if (j < ncand) {
+            idx = cl[j];
             s = sc[idx];
             keep = (s >= t) && is_local_max(sc, ww, idx, s);
         }
         const unsigned long long m = ballot(keep);
         if (keep) {
             const int pos = count + rank_in(m);
+            const int r = idx / ww, c = idx - (idx / ww) * ww;
             if (pos < C.cap) out[pos] = pack_key(C.off_x + c, C.off_y + r, s);
         }
         count += __popcll(m);
@@ -302,86 +449,116 @@ __global__ __launch_bounds__(256) void k_fast_cells(KernelGeom g, const CellDesc
 // ================================================================================================
 // The reference keeps the nodes in a std::list: every non-leaf node is divided and its non-empty
 // children pushed to the FRONT in the order n1..n4, the parent erased.  A pass therefore yields
-// list = reverse(children in push order) ++ (leaf nodes in old order).  In the "careful" phase the
-// children of the last pass are std::sort-ed with compareNodes and divided from the largest until
-// the list reaches N; parents are erased from wherever they are.  We keep the list as an array that
-// is re-materialised after every pass / careful round, node keys as contiguous ranges of packed
-// keys that are stably 4-way partitioned between two buffers on every division, and port the
-// libstdc++ introsort exactly (orb_hd.h) because compareNodes has ties.
-struct QTree {
-    uint32_t* keys[2];
-    // node arrays (NCAP)
+//   list' = reverse(children in push order) ++ (leaf nodes in old order).
+// In the "careful" phase the splittable children of the last pass are std::sort-ed with
+// compareNodes and divided from the largest until the list reaches N; parents are erased wherever
+// they are, so a round yields list' = reverse(children in push order) ++ (old list minus divided).
+//
+// Here node records live in list order in two generations (current / next).  A pass is computed
+// in parallel: per node child counts (wave-cooperative for big nodes, one lane per node for small
+// ones), wave scans for the positions of children / survivors / splittable children, and a stable
+// 4-way partition of each divided node's keys into the other key buffer.  The careful phase finds
+// its stopping division with a scan over the sorted order.  The sort itself is the exact libstdc++
+// introsort port (orb_hd.h), run by one lane, because compareNodes has ties.
+constexpr int kBigNode = 48;  // nodes with more keys are partitioned by the whole wave
+
+struct QGen {
     int16_t *x0, *y0, *x1, *y1;
-    int32_t *kstart, *kcount;
-    uint8_t *kbuf, *leaf, *erased;
-    uint16_t* freelist;
-    // list arrays (LCAP)
-    uint16_t *list, *list2, *stack, *surv, *split, *prev, *pending;
-    int ncap, lcap;
+    int32_t *ks, *kn;
+    uint8_t *kb, *leaf;
 };
 
-__device__ __forceinline__ size_t qt_node_bytes(int ncap) { return (size_t)ncap * (4 * 2 + 2 * 4 + 3 + 2); }
-__device__ __forceinline__ size_t qt_list_bytes(int lcap) { return (size_t)lcap * 2 * 7; }
+struct QTree {
+    uint32_t *keys0, *keys1;
+    QGen g0, g1;
+    int32_t* cnt;        // [4][lcap] child counts of the current generation's nodes
+    uint16_t *split, *prev;
+    uint8_t* divided;
+    int* sort_ws;        // introsort stack (kOrbSortStack * 3 ints)
+    int lcap;
+};
 
-__device__ inline void qt_carve(QTree& t, uint8_t* p, int ncap, int lcap) {
-    t.ncap = ncap; t.lcap = lcap;
-    t.kstart = (int32_t*)p; p += 4 * ncap;
-    t.kcount = (int32_t*)p; p += 4 * ncap;
-    t.x0 = (int16_t*)p; p += 2 * ncap;
-    t.y0 = (int16_t*)p; p += 2 * ncap;
-    t.x1 = (int16_t*)p; p += 2 * ncap;
-    t.y1 = (int16_t*)p; p += 2 * ncap;
-    t.freelist = (uint16_t*)p; p += 2 * ncap;
-    t.list = (uint16_t*)p; p += 2 * lcap;
-    t.list2 = (uint16_t*)p; p += 2 * lcap;
-    t.stack = (uint16_t*)p; p += 2 * lcap;
-    t.surv = (uint16_t*)p; p += 2 * lcap;
-    t.split = (uint16_t*)p; p += 2 * lcap;
-    t.prev = (uint16_t*)p; p += 2 * lcap;
-    t.pending = (uint16_t*)p; p += 2 * lcap;
-    t.kbuf = p; p += ncap;
-    t.leaf = p; p += ncap;
-    t.erased = p; p += ncap;
+__device__ inline size_t qt_meta_bytes(int lcap) {
+    return (size_t)lcap * (2 * (4 * 2 + 4 * 2 + 2) + 4 * 4 + 2 * 2 + 1) + 64 + kOrbSortStack * 12;
 }
 
-struct QState {  // wave-uniform scalars (every lane holds the same values)
-    int nfree;
-    int nstack, nsplit;
-    int npending;     // parents divided in a careful round; recycled after the list is rebuilt
-    bool overflow;
-};
-
-// Divide `node`: stable 4-way partition of its keys into the other buffer, children pushed to
-// `stack` (order n1, n2, n3, n4), the splittable ones (> 1 key) appended to `split`.
-// Returns the number of children created.
-__device__ inline int qt_divide(QTree& t, QState& s, int node, int lane, bool defer_free) {
-    const int x0 = t.x0[node], y0 = t.y0[node], x1 = t.x1[node], y1 = t.y1[node];
-    const int ks = uniform(t.kstart[node]), kn = uniform(t.kcount[node]), kb = uniform(t.kbuf[node]);
-    const int hx = (x1 - x0 + 1) >> 1, hy = (y1 - y0 + 1) >> 1;  // ceil((float)(d)/2), src:608-609
-    const int sx = x0 + hx, sy = y0 + hy;
-    const uint32_t* src = t.keys[kb] + ks;
-    uint32_t* dst = t.keys[kb ^ 1] + ks;
-    int cnt[4] = {0, 0, 0, 0};
-    for (int b = 0; b < kn; b += 64) {
-        const int i = b + lane;
-        int q = -1;
-        if (i < kn) {
-            const uint32_t k = src[i];
-            q = (key_x(k) >= sx ? 1 : 0) + (key_y(k) >= sy ? 2 : 0);  // src:651-661
-        }
+__device__ inline void qt_carve(QTree& t, uint8_t* p, int lcap) {
+    t.lcap = lcap;
+    t.sort_ws = (int*)p;
+    p += kOrbSortStack * 12;
+    QGen* gens[2] = {&t.g0, &t.g1};
 #pragma unroll
-        for (int qq = 0; qq < 4; ++qq) cnt[qq] += __popcll(ballot(q == qq));
+    for (int g = 0; g < 2; ++g) {
+        gens[g]->ks = (int32_t*)p; p += 4 * lcap;
+        gens[g]->kn = (int32_t*)p; p += 4 * lcap;
     }
-    int base[4];
-    base[0] = 0; base[1] = cnt[0]; base[2] = cnt[0] + cnt[1]; base[3] = base[2] + cnt[2];
+    t.cnt = (int32_t*)p; p += 16 * lcap;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        gens[g]->x0 = (int16_t*)p; p += 2 * lcap;
+        gens[g]->y0 = (int16_t*)p; p += 2 * lcap;
+        gens[g]->x1 = (int16_t*)p; p += 2 * lcap;
+        gens[g]->y1 = (int16_t*)p; p += 2 * lcap;
+    }
+    t.split = (uint16_t*)p; p += 2 * lcap;
+    t.prev = (uint16_t*)p; p += 2 * lcap;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        gens[g]->kb = p; p += lcap;
+        gens[g]->leaf = p; p += lcap;
+    }
+    t.divided = p;
+}
+
+__device__ __forceinline__ uint32_t* key_buf(const QTree& t, int b) { return b ? t.keys1 : t.keys0; }
+
+__device__ __forceinline__ int quadrant(uint32_t k, int sx, int sy) {  // n1 n2 / n3 n4, src:651-661
+    return (key_x(k) >= sx ? 1 : 0) + (key_y(k) >= sy ? 2 : 0);
+}
+
+__device__ __forceinline__ void split_point(const QGen& G, int p, int& sx, int& sy) {
+    const int x0 = G.x0[p], y0 = G.y0[p], x1 = G.x1[p], y1 = G.y1[p];
+    sx = x0 + ((x1 - x0 + 1) >> 1);  // UL.x + ceil((float)(UR.x-UL.x)/2), src:608
+    sy = y0 + ((y1 - y0 + 1) >> 1);
+}
+
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// child counts of node p of generation G; the whole wave cooperates (result uniform)
+__device__ inline void coop_count(const QTree& t, const QGen& G, int p, int lane, int c[4]) {
+    int sx, sy;
+    split_point(G, p, sx, sy);
+    const uint32_t* src = key_buf(t, G.kb[p]) + G.ks[p];
+    const int kn = uniform(G.kn[p]);
+    c[0] = c[1] = c[2] = c[3] = 0;
     for (int b = 0; b < kn; b += 64) {
         const int i = b + lane;
-        int q = -1;
+        const int q = i < kn ? quadrant(src[i], sx, sy) : -1;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) c[qq] += __popcll(ballot(q == qq));
+    }
+}
+
+__device__ inline void coop_scatter(const QTree& t, const QGen& G, int p, int lane, const int c[4]) {
+    int sx, sy;
+    split_point(G, p, sx, sy);
+    const int kb = G.kb[p], ks = G.ks[p];
+    const uint32_t* src = key_buf(t, kb) + ks;
+    uint32_t* dst = key_buf(t, kb ^ 1) + ks;
+    const int kn = uniform(G.kn[p]);
+    int base[4] = {0, c[0], c[0] + c[1], c[0] + c[1] + c[2]};
+    for (int b = 0; b < kn; b += 64) {
+        const int i = b + lane;
         uint32_t k = 0;
-        if (i < kn) {
-            k = src[i];
-            q = (key_x(k) >= sx ? 1 : 0) + (key_y(k) >= sy ? 2 : 0);
-        }
+        int q = -1;
+        if (i < kn) { k = src[i]; q = quadrant(k, sx, sy); }
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
             const unsigned long long m = ballot(q == qq);
@@ -389,120 +566,191 @@ __device__ inline int qt_divide(QTree& t, QState& s, int node, int lane, bool de
             base[qq] += __popcll(m);
         }
     }
-    // children rectangles, src:614-640
-    const int cx0[4] = {x0, sx, x0, sx}, cy0[4] = {y0, y0, sy, sy};
-    const int cx1[4] = {sx, x1, sx, x1}, cy1[4] = {sy, sy, y1, y1};
-    int start = ks, made = 0;
-    // the parent's id is recycled after its children are allocated (it is no longer referenced)
-    for (int qq = 0; qq < 4; ++qq) {
-        const int n = cnt[qq];
-        if (n > 0) {
-            if (s.nfree == 0 || s.nstack >= t.lcap) { s.overflow = true; return made; }
-            const int id = t.freelist[--s.nfree];
-            if (lane == 0) {
-                t.x0[id] = (int16_t)cx0[qq]; t.y0[id] = (int16_t)cy0[qq];
-                t.x1[id] = (int16_t)cx1[qq]; t.y1[id] = (int16_t)cy1[qq];
-                t.kstart[id] = start; t.kcount[id] = n;
-                t.kbuf[id] = (uint8_t)(kb ^ 1);
-                t.leaf[id] = n == 1;
-                t.erased[id] = 0;
-                t.stack[s.nstack] = (uint16_t)id;
-                if (n > 1) t.split[s.nsplit] = (uint16_t)id;
-            }
-            s.nstack++;
-            if (n > 1) {
-                if (s.nsplit >= t.lcap) { s.overflow = true; return made; }
-                s.nsplit++;
-            }
-            made++;
-        }
-        start += n;
+}
+
+__device__ inline void serial_count(const QTree& t, const QGen& G, int p, int c[4]) {
+    int sx, sy;
+    split_point(G, p, sx, sy);
+    const uint32_t* src = key_buf(t, G.kb[p]) + G.ks[p];
+    const int kn = G.kn[p];
+    c[0] = c[1] = c[2] = c[3] = 0;
+    for (int i = 0; i < kn; ++i) {
+        const int q = quadrant(src[i], sx, sy);
+        c[0] += q == 0; c[1] += q == 1; c[2] += q == 2; c[3] += q == 3;
     }
-    // a careful round still scans the old list (and its erased flags) after this division, so the
-    // parent's id must not be handed out again before the list is rebuilt
-    if (defer_free) {
-        if (lane == 0) { t.pending[s.npending] = (uint16_t)node; t.erased[node] = 1; }
-        s.npending++;
-    } else {
-        if (lane == 0) t.freelist[s.nfree] = (uint16_t)node;
-        s.nfree++;
+}
+
+__device__ inline void serial_scatter(const QTree& t, const QGen& G, int p, const int c[4]) {
+    int sx, sy;
+    split_point(G, p, sx, sy);
+    const int kb = G.kb[p], ks = G.ks[p];
+    const uint32_t* src = key_buf(t, kb) + ks;
+    uint32_t* dst = key_buf(t, kb ^ 1) + ks;
+    const int kn = G.kn[p];
+    int base[4] = {0, c[0], c[0] + c[1], c[0] + c[1] + c[2]};
+    for (int i = 0; i < kn; ++i) {
+        const uint32_t k = src[i];
+        const int q = quadrant(k, sx, sy);
+        const int o = q == 0 ? base[0]++ : q == 1 ? base[1]++ : q == 2 ? base[2]++ : base[3]++;
+        dst[o] = k;
+    }
+}
+
+// Child counts for the nodes at positions pos(i), i < n (pos == nullptr: identity, skipping leaves).
+__device__ inline void qt_count_children(QTree& t, const QGen& G, const uint16_t* pos, int n, int lane) {
+    for (int b = 0; b < n; b += 64) {
+        const int i = b + lane;
+        int p = 0;
+        bool big = false;
+        if (i < n) {
+            p = pos ? pos[i] : i;
+            big = !G.leaf[p] && G.kn[p] > kBigNode;
+        }
+        unsigned long long m = ballot(big);
+        while (m) {
+            const int bit = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            const int pp = uniform(pos ? pos[b + bit] : b + bit);
+            int c[4];
+            coop_count(t, G, pp, lane, c);
+            if (lane == 0) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) t.cnt[q * t.lcap + pp] = c[q];
+            }
+        }
+        if (i < n && !G.leaf[p] && !big) {
+            int c[4];
+            serial_count(t, G, p, c);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) t.cnt[q * t.lcap + p] = c[q];
+        }
     }
     wave_sync();
-    return made;
+}
+
+__device__ inline void qt_partition(QTree& t, const QGen& G, const uint16_t* pos, int n, int lane) {
+    for (int b = 0; b < n; b += 64) {
+        const int i = b + lane;
+        int p = 0;
+        bool big = false;
+        if (i < n) {
+            p = pos ? pos[i] : i;
+            big = !G.leaf[p] && G.kn[p] > kBigNode;
+        }
+        unsigned long long m = ballot(big);
+        while (m) {
+            const int bit = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            const int pp = uniform(pos ? pos[b + bit] : b + bit);
+            int c[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) c[q] = uniform(t.cnt[q * t.lcap + pp]);
+            coop_scatter(t, G, pp, lane, c);
+        }
+        if (i < n && !G.leaf[p] && !big) {
+            int c[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) c[q] = t.cnt[q * t.lcap + p];
+            serial_scatter(t, G, p, c);
+        }
+    }
+    wave_sync();
+}
+
+// write child q of node p (generation A) to position `to` of generation B
+__device__ __forceinline__ void qt_write_child(QTree& t, const QGen& A, QGen& B, int p, int q, int n, int to) {
+    int sx, sy;
+    split_point(A, p, sx, sy);
+    const int x0 = A.x0[p], y0 = A.y0[p], x1 = A.x1[p], y1 = A.y1[p];
+    int off = 0;
+    for (int qq = 0; qq < q; ++qq) off += t.cnt[qq * t.lcap + p];
+    B.x0[to] = (int16_t)((q & 1) ? sx : x0);
+    B.x1[to] = (int16_t)((q & 1) ? x1 : sx);
+    B.y0[to] = (int16_t)((q & 2) ? sy : y0);
+    B.y1[to] = (int16_t)((q & 2) ? y1 : sy);
+    B.ks[to] = A.ks[p] + off;
+    B.kn[to] = n;
+    B.kb[to] = (uint8_t)(A.kb[p] ^ 1);
+    B.leaf[to] = n == 1;
+}
+
+__device__ __forceinline__ void qt_copy_node(const QGen& A, QGen& B, int p, int to) {
+    B.x0[to] = A.x0[p]; B.y0[to] = A.y0[p]; B.x1[to] = A.x1[p]; B.y1[to] = A.y1[p];
+    B.ks[to] = A.ks[p]; B.kn[to] = A.kn[p]; B.kb[to] = A.kb[p]; B.leaf[to] = A.leaf[p];
 }
 
 template <bool kKeysInLds>
-__device__ void qt_run(QTree& t, int K, int N, int nroots, float root_w, int span_x, int span_y,
+__device__ void qt_run(QTree& t, int K, int N, int nroots, float root_w, int span_y,
                        const uint32_t* __restrict__ cand_level, const CellDesc* __restrict__ cells, int cell_begin,
                        int cell_count, const int32_t* __restrict__ ccount, uint32_t* __restrict__ sel_out,
                        int sel_cap, int* n_sel, int* status) {
     const int lane = lane_id();
-    QState s{};
-    s.nfree = 0;
-    // free list: ids ncap-1 .. 0 so that allocation order is 0, 1, 2, ...
-    for (int i = lane; i < t.ncap; i += 64) t.freelist[i] = (uint16_t)(t.ncap - 1 - i);
-    s.nfree = t.ncap;
-    // ---- gather candidates in cell order into keys[1], counting per root (src:756-764)
+    bool overflow = false;
+    // ---- gather candidates in cell order into keys[1], counting per root (src:756-764).
+    // One lane per cell (cells in chunks of 64); destinations from a wave scan of the cell counts.
     int rcount[kMaxRoots];
 #pragma unroll
     for (int r = 0; r < kMaxRoots; ++r) rcount[r] = 0;
     {
-        int pos = 0;
-        for (int c = 0; c < cell_count; ++c) {
-            const int n = uniform(ccount[c]);
-            const uint32_t* src = cand_level + cells[cell_begin + c].slot;
-            for (int b = 0; b < n; b += 64) {
-                const int i = b + lane;
-                int root = -1;
-                if (i < n) {
-                    const uint32_t k = src[i];
-                    t.keys[1][pos + i] = k;
-                    root = (int)((float)key_x(k) / root_w);
-                }
+        int carry = 0;
+        for (int cb = 0; cb < cell_count; cb += 64) {
+            const int c = cb + lane;
+            int n = 0, slot = 0;
+            if (c < cell_count) { n = ccount[c]; slot = cells[cell_begin + c].slot; }
+            const int incl = wave_incl_scan(n, lane);
+            const int start = carry + incl - n;
+            const uint32_t* src = cand_level + slot;
+            for (int i0 = 0; i0 < n; i0 += 8) {
+                uint32_t kk[8];
 #pragma unroll
-                for (int r = 0; r < kMaxRoots; ++r)
-                    if (r < nroots) rcount[r] += __popcll(ballot(root == r));
+                for (int j = 0; j < 8; ++j) kk[j] = i0 + j < n ? src[i0 + j] : 0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    if (i0 + j >= n) break;
+                    t.keys1[start + i0 + j] = kk[j];
+                    const int root = (int)((float)key_x(kk[j]) / root_w);
+#pragma unroll
+                    for (int r = 0; r < kMaxRoots; ++r) rcount[r] += root == r;
+                }
             }
-            pos += n;
+            carry += __shfl(incl, 63, 64);
         }
+#pragma unroll
+        for (int r = 0; r < kMaxRoots; ++r) rcount[r] = uniform(wave_sum(rcount[r]));
     }
     wave_sync();
-    // stable partition by root into keys[0]
-    {
+    {   // stable partition by root into keys[0]
         int base[kMaxRoots];
         int acc = 0;
 #pragma unroll
-        for (int r = 0; r < kMaxRoots; ++r) { base[r] = acc; acc += r < nroots ? rcount[r] : 0; }
+        for (int r = 0; r < kMaxRoots; ++r) { base[r] = acc; acc += rcount[r]; }
         for (int b = 0; b < K; b += 64) {
             const int i = b + lane;
             int root = -1;
             uint32_t k = 0;
-            if (i < K) { k = t.keys[1][i]; root = (int)((float)key_x(k) / root_w); }
+            if (i < K) { k = t.keys1[i]; root = (int)((float)key_x(k) / root_w); }
 #pragma unroll
             for (int r = 0; r < kMaxRoots; ++r) {
-                if (r >= nroots) break;
                 const unsigned long long m = ballot(root == r);
-                if (root == r) t.keys[0][base[r] + rank_in(m)] = k;
+                if (root == r) t.keys0[base[r] + rank_in(m)] = k;
                 base[r] += __popcll(m);
             }
         }
     }
     // ---- roots (src:733-786): empty roots erased, single-key roots are leaves
+    QGen A = t.g0, B = t.g1;  // current / next generation, swapped after every pass
     int nlist = 0;
     {
         int start = 0;
         for (int r = 0; r < nroots; ++r) {
             const int n = rcount[r];
             if (n > 0) {
-                const int id = t.freelist[--s.nfree];
                 if (lane == 0) {
-                    t.x0[id] = (int16_t)(int)(root_w * (float)r);
-                    t.x1[id] = (int16_t)(int)(root_w * (float)(r + 1));
-                    t.y0[id] = 0;
-                    t.y1[id] = (int16_t)span_y;
-                    t.kstart[id] = start; t.kcount[id] = n; t.kbuf[id] = 0;
-                    t.leaf[id] = n == 1; t.erased[id] = 0;
-                    t.list[nlist] = (uint16_t)id;
+                    A.x0[nlist] = (int16_t)(int)(root_w * (float)r);
+                    A.x1[nlist] = (int16_t)(int)(root_w * (float)(r + 1));
+                    A.y0[nlist] = 0;
+                    A.y1[nlist] = (int16_t)span_y;
+                    A.ks[nlist] = start; A.kn[nlist] = n; A.kb[nlist] = 0; A.leaf[nlist] = n == 1;
                 }
                 nlist++;
             }
@@ -510,98 +758,170 @@ __device__ void qt_run(QTree& t, int K, int N, int nroots, float root_w, int spa
         }
     }
     wave_sync();
-    (void)span_x;
+    int nsplit = 0;
     bool done = false;
-    while (!done && !s.overflow) {
+    while (!done && !overflow) {
         // ---------------- regular pass (src:802-918)
         const int prev_size = nlist;
-        int nsurv = 0, to_expand = 0;
-        s.nstack = 0;
-        s.nsplit = 0;
-        for (int i = 0; i < nlist && !s.overflow; ++i) {
-            const int node = uniform(t.list[i]);
-            if (t.leaf[node]) {
-                if (lane == 0) t.surv[nsurv] = (uint16_t)node;
-                nsurv++;
-                continue;
+        qt_count_children(t, A, nullptr, nlist, lane);
+        int total_children = 0, total_surv = 0;
+        for (int b = 0; b < nlist; b += 64) {
+            const int i = b + lane;
+            int nc = 0, sv = 0;
+            if (i < nlist) {
+                if (A.leaf[i]) sv = 1;
+                else for (int q = 0; q < 4; ++q) nc += t.cnt[q * t.lcap + i] > 0;
             }
-            const int before = s.nsplit;
-            qt_divide(t, s, node, lane, false);
-            to_expand += s.nsplit - before;
+            total_children += wave_sum(nc);
+            total_surv += wave_sum(sv);
         }
-        if (s.overflow) break;
-        wave_sync();
-        nlist = s.nstack + nsurv;
-        if (nlist > t.lcap) { s.overflow = true; break; }
-        for (int i = lane; i < nlist; i += 64)
-            t.list2[i] = i < s.nstack ? t.stack[s.nstack - 1 - i] : t.surv[i - s.nstack];
-        wave_sync();
-        for (int i = lane; i < nlist; i += 64) t.list[i] = t.list2[i];
-        wave_sync();
+        total_children = uniform(total_children);
+        total_surv = uniform(total_surv);
+        const int new_size = total_children + total_surv;
+        if (new_size > t.lcap) { overflow = true; break; }
+        int carry_c = 0, carry_s = 0, carry_p = 0;
+        for (int b = 0; b < nlist; b += 64) {
+            const int i = b + lane;
+            int nc = 0, sv = 0, ns = 0, c[4] = {0, 0, 0, 0};
+            if (i < nlist) {
+                if (A.leaf[i]) sv = 1;
+                else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) { c[q] = t.cnt[q * t.lcap + i]; nc += c[q] > 0; ns += c[q] > 1; }
+                }
+            }
+            const int ic = wave_incl_scan(nc, lane), is = wave_incl_scan(sv, lane), ip = wave_incl_scan(ns, lane);
+            if (i < nlist) {
+                if (sv) {
+                    qt_copy_node(A, B, i, total_children + carry_s + is - 1);
+                } else {
+                    int r = 0, r2 = 0;
+                    const int stackpos = carry_c + ic - nc, splitpos = carry_p + ip - ns;
+                    for (int q = 0; q < 4; ++q) {
+                        if (c[q] == 0) continue;
+                        const int to = total_children - 1 - (stackpos + r);
+                        qt_write_child(t, A, B, i, q, c[q], to);
+                        if (c[q] > 1) t.split[splitpos + r2++] = (uint16_t)to;
+                        r++;
+                    }
+                }
+            }
+            carry_c += __shfl(ic, 63, 64);
+            carry_s += __shfl(is, 63, 64);
+            carry_p += __shfl(ip, 63, 64);
+        }
+        nsplit = carry_p;
+        qt_partition(t, A, nullptr, nlist, lane);
+        { const QGen tmp = A; A = B; B = tmp; }
+        nlist = new_size;
+        const int to_expand = nsplit;
         if (nlist >= N || nlist == prev_size) {
             done = true;
         } else if (nlist + to_expand * 3 > N) {
             // ---------------- careful rounds (src:932-1016)
-            while (!done && !s.overflow) {
+            while (!done && !overflow) {
+                QGen& A2 = A;
+                QGen& B2 = B;
                 const int round_prev = nlist;
-                const int nprev = s.nsplit;
-                for (int i = lane; i < nprev; i += 64) t.prev[i] = t.split[i];
+                const int np = nsplit;
+                for (int i = lane; i < np; i += 64) t.prev[i] = t.split[i];
                 wave_sync();
                 if (lane == 0) {
-                    const int16_t* x0a = t.x0;
-                    const int32_t* kc = t.kcount;
-                    orb_std_sort(t.prev, nprev, [&](uint16_t a, uint16_t b) {
+                    const int16_t* x0a = A2.x0;
+                    const int32_t* kc = A2.kn;
+                    orb_std_sort(t.prev, np, [&](uint16_t a, uint16_t b) {
                         const int ca = kc[a], cb = kc[b];
                         return ca < cb || (ca == cb && x0a[a] < x0a[b]);
-                    });
+                    }, t.sort_ws);
                 }
                 wave_sync();
-                s.nstack = 0;
-                s.nsplit = 0;
-                s.npending = 0;
-                int size = nlist;
-                for (int j = nprev - 1; j >= 0; --j) {
-                    const int node = uniform(t.prev[j]);
-                    const int made = qt_divide(t, s, node, lane, true);
-                    if (s.overflow) break;
-                    size += made - 1;
-                    if (size >= N) break;
+                qt_count_children(t, A2, t.prev, np, lane);
+                // division order o = 0.. is prev[np-1-o]; stop once the list reaches N (src:1006)
+                int ndiv = np, carry = 0;
+                for (int b = 0; b < np; b += 64) {
+                    const int o = b + lane;
+                    int d = 0;
+                    if (o < np) {
+                        const int p = t.prev[np - 1 - o];
+                        for (int q = 0; q < 4; ++q) d += t.cnt[q * t.lcap + p] > 0;
+                        d -= 1;
+                    }
+                    const int inc = wave_incl_scan(d, lane);
+                    const unsigned long long hit = ballot(o < np && nlist + carry + inc >= N);
+                    if (hit) { ndiv = b + __ffsll((long long)hit); break; }
+                    carry += __shfl(inc, 63, 64);
                 }
-                if (s.overflow) break;
+                ndiv = uniform(ndiv);
+                for (int i = lane; i < nlist; i += 64) t.divided[i] = 0;
                 wave_sync();
-                // list = reverse(stack) ++ (old list minus erased)
-                int w = s.nstack;
+                for (int o = lane; o < ndiv; o += 64) t.divided[t.prev[np - 1 - o]] = 1;
+                wave_sync();
+                // children of the divided nodes, in push order
+                int total_children = 0;
+                for (int b = 0; b < ndiv; b += 64) {
+                    const int o = b + lane;
+                    int nc = 0;
+                    if (o < ndiv) {
+                        const int p = t.prev[np - 1 - o];
+                        for (int q = 0; q < 4; ++q) nc += t.cnt[q * t.lcap + p] > 0;
+                    }
+                    total_children += wave_sum(nc);
+                }
+                total_children = uniform(total_children);
+                int kept = 0;
+                for (int b = 0; b < nlist; b += 64) kept += __popcll(ballot(b + lane < nlist && !t.divided[b + lane]));
+                const int new_size = total_children + kept;
+                if (new_size > t.lcap) { overflow = true; break; }
+                int carry_c = 0, carry_p = 0;
+                for (int b = 0; b < ndiv; b += 64) {
+                    const int o = b + lane;
+                    int nc = 0, ns = 0, c[4] = {0, 0, 0, 0}, p = 0;
+                    if (o < ndiv) {
+                        p = t.prev[np - 1 - o];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) { c[q] = t.cnt[q * t.lcap + p]; nc += c[q] > 0; ns += c[q] > 1; }
+                    }
+                    const int ic = wave_incl_scan(nc, lane), ip = wave_incl_scan(ns, lane);
+                    if (o < ndiv) {
+                        int r = 0, r2 = 0;
+                        const int stackpos = carry_c + ic - nc, splitpos = carry_p + ip - ns;
+                        for (int q = 0; q < 4; ++q) {
+                            if (c[q] == 0) continue;
+                            const int to = total_children - 1 - (stackpos + r);
+                            qt_write_child(t, A2, B2, p, q, c[q], to);
+                            if (c[q] > 1) t.split[splitpos + r2++] = (uint16_t)to;
+                            r++;
+                        }
+                    }
+                    carry_c += __shfl(ic, 63, 64);
+                    carry_p += __shfl(ip, 63, 64);
+                }
+                nsplit = carry_p;
+                int carry_k = 0;
                 for (int b = 0; b < nlist; b += 64) {
                     const int i = b + lane;
-                    bool keep = false;
-                    int id = 0;
-                    if (i < nlist) { id = t.list[i]; keep = !t.erased[id]; }
+                    const bool keep = i < nlist && !t.divided[i];
                     const unsigned long long m = ballot(keep);
-                    if (keep && w + rank_in(m) < t.lcap) t.list2[w + rank_in(m)] = (uint16_t)id;
-                    w += __popcll(m);
+                    if (keep) qt_copy_node(A2, B2, i, total_children + carry_k + rank_in(m));
+                    carry_k += __popcll(m);
                 }
-                if (w > t.lcap) { s.overflow = true; break; }
-                for (int i = lane; i < s.nstack; i += 64) t.list2[i] = t.stack[s.nstack - 1 - i];
-                wave_sync();
-                nlist = w;
-                for (int i = lane; i < nlist; i += 64) t.list[i] = t.list2[i];
-                for (int i = lane; i < s.npending; i += 64) t.freelist[s.nfree + i] = t.pending[i];
-                s.nfree += s.npending;
-                s.npending = 0;
-                wave_sync();
+                // key partition of the divided nodes (prev[np-ndiv .. np-1])
+                qt_partition(t, A2, t.prev + (np - ndiv), ndiv, lane);
+                { const QGen tmp = A; A = B; B = tmp; }
+                nlist = new_size;
                 if (nlist >= N || nlist == round_prev) done = true;
             }
         }
     }
-    if (s.overflow || nlist > sel_cap) {
+    if (overflow || nlist > sel_cap) {
         if (lane == 0) { *n_sel = 0; atomicMax(status, 1); }
         return;
     }
     // ---- keep the first max-response key of every node, in list order (src:1028-1053)
+    const QGen& F = A;
     for (int i = lane; i < nlist; i += 64) {
-        const int id = t.list[i];
-        const uint32_t* kk = t.keys[t.kbuf[id]] + t.kstart[id];
-        const int n = t.kcount[id];
+        const uint32_t* kk = key_buf(t, F.kb[i]) + F.ks[i];
+        const int n = F.kn[i];
         uint32_t best = kk[0];
         for (int q = 1; q < n; ++q)
             if (key_score(kk[q]) > key_score(best)) best = kk[q];
@@ -610,55 +930,59 @@ __device__ void qt_run(QTree& t, int K, int N, int nroots, float root_w, int spa
     if (lane == 0) *n_sel = nlist;
 }
 
-__global__ __launch_bounds__(64) void k_quadtree(KernelGeom g, const CellDesc* __restrict__ cells,
+__global__ __launch_bounds__(64) void k_quadtree(const KernelGeom* __restrict__ gp, const CellDesc* __restrict__ cells,
                                                  const uint32_t* __restrict__ cand, const int32_t* __restrict__ cell_count,
                                                  uint32_t* __restrict__ key_scratch, uint32_t* __restrict__ sel,
                                                  int32_t* __restrict__ sel_count, int lds_bytes, int* __restrict__ status) {
+    const KernelGeom& g = *gp;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int level = blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
     const LevelGeom& L = g.lv[level];
     const int32_t* cc = cell_count + (size_t)f * g.ncells + L.cell_begin;
     int K = 0;
     for (int c = lane; c < L.cell_count; c += 64) K += cc[c];
-    K = wave_sum(K);
-    K = uniform(K);
+    K = uniform(wave_sum(K));
     const int N = L.nfeat;
-    const int lcap = L.sel_cap + 64, ncap = 2 * lcap + 8;
+    const int lcap = L.sel_cap + 64;
     QTree t;
-    size_t meta = qt_node_bytes(ncap) + qt_list_bytes(lcap);
-    meta = (meta + 15) & ~(size_t)15;
-    qt_carve(t, smem, ncap, lcap);
+    size_t meta = (qt_meta_bytes(lcap) + 15) & ~(size_t)15;
+    qt_carve(t, smem, lcap);
     uint32_t* sel_out = sel + (size_t)f * g.sel_frame_cap + L.sel_off;
     int32_t* n_sel = sel_count + (size_t)f * g.nlevels + level;
     const uint32_t* cand_level = cand + (size_t)f * g.cand_frame_cap + L.cand_off;
+    if (meta > (size_t)lds_bytes) {
+        if (lane == 0) { *n_sel = 0; atomicMax(status, 2); }
+        return;
+    }
     const size_t key_bytes = (size_t)K * 4 * 2;
     if (meta + key_bytes <= (size_t)lds_bytes) {
-        t.keys[0] = (uint32_t*)(smem + meta);
-        t.keys[1] = t.keys[0] + K;
-        qt_run<true>(t, K, N, L.n_roots, L.root_w, L.maxBX - L.minB, L.maxBY - L.minB, cand_level, cells,
-                     L.cell_begin, L.cell_count, cc, sel_out, L.sel_cap, n_sel, status);
+        t.keys0 = (uint32_t*)(smem + meta);
+        t.keys1 = t.keys0 + K;
+        qt_run<true>(t, K, N, L.n_roots, L.root_w, L.maxBY - L.minB, cand_level, cells, L.cell_begin,
+                     L.cell_count, cc, sel_out, L.sel_cap, n_sel, status);
     } else {
         uint32_t* scratch = key_scratch + ((size_t)f * g.cand_frame_cap + L.cand_off) * 2;
-        t.keys[0] = scratch;
-        t.keys[1] = scratch + L.cand_cap;
-        qt_run<false>(t, K, N, L.n_roots, L.root_w, L.maxBX - L.minB, L.maxBY - L.minB, cand_level, cells,
-                      L.cell_begin, L.cell_count, cc, sel_out, L.sel_cap, n_sel, status);
+        t.keys0 = scratch;
+        t.keys1 = scratch + L.cand_cap;
+        qt_run<false>(t, K, N, L.n_roots, L.root_w, L.maxBY - L.minB, cand_level, cells, L.cell_begin,
+                      L.cell_count, cc, sel_out, L.sel_cap, n_sel, status);
     }
 }
 
 // ================================================================================================
 // 4. output placement by vLappingArea, src:1613-1681
 // ================================================================================================
-__global__ __launch_bounds__(64) void k_place(KernelGeom g, const uint32_t* __restrict__ sel,
+__global__ __launch_bounds__(64) void k_place(const KernelGeom* __restrict__ gp, const uint32_t* __restrict__ sel,
                                               const int32_t* __restrict__ sel_count, int32_t* __restrict__ dst_index,
                                               int lap0, int lap1, int cap, int32_t* __restrict__ counts) {
+    const KernelGeom& g = *gp;
     const int f = blockIdx.x, lane = threadIdx.x;
-    int total = 0;
-    for (int l = 0; l < g.nlevels; ++l) total += sel_count[(size_t)f * g.nlevels + l];
+    const int my_count = lane < g.nlevels ? sel_count[(size_t)f * g.nlevels + lane] : 0;
+    const int total = wave_sum(my_count);
     int mono = 0, stereo = 0;
     for (int l = 0; l < g.nlevels; ++l) {
         const LevelGeom& L = g.lv[l];
-        const int n = sel_count[(size_t)f * g.nlevels + l];
+        const int n = __shfl(my_count, l, 64);
         const uint32_t* s = sel + (size_t)f * g.sel_frame_cap + L.sel_off;
         int32_t* d = dst_index + (size_t)f * g.sel_frame_cap + L.sel_off;
         for (int b = 0; b < n; b += 64) {
@@ -696,63 +1020,76 @@ __device__ __forceinline__ void steer_sincos(float ang, float* s, float* c) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_describe(KernelGeom g, const uint8_t* __restrict__ pyr,
+// Two keypoints per wave (one per 32-lane half): lane u = -15..15 of the IC_Angle disc columns,
+// then 8 of the 256 BRIEF tests per lane; every lane's loads are independent and issued together.
+constexpr int kDescKpPerBlock = 8;
+
+__global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__ gp, const uint8_t* __restrict__ pyr,
                                                   const uint8_t* __restrict__ blur, const uint32_t* __restrict__ sel,
                                                   const int32_t* __restrict__ sel_count,
                                                   const int32_t* __restrict__ dst_index, const int32_t* __restrict__ counts,
                                                   int cap, orb_keypoint_t* __restrict__ kps, uint8_t* __restrict__ desc) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int slot = blockIdx.x * 4 + wave, level = blockIdx.y, f = blockIdx.z;
+    const KernelGeom& g = *gp;
+    const int half = threadIdx.x >> 5, hl = threadIdx.x & 31;
+    const int slot = blockIdx.x * kDescKpPerBlock + half, level = blockIdx.y, f = blockIdx.z;
     const int n = sel_count[(size_t)f * g.nlevels + level];
-    if (slot >= n) return;
-    if (counts[2 * f + 1] < 0) return;  // frame exceeded the caller's capacity
+    if (blockIdx.x * kDescKpPerBlock >= n) return;           // whole block idle
+    const bool active = slot < n && counts[2 * f + 1] >= 0;  // frame within the caller's capacity
     const LevelGeom& L = g.lv[level];
-    const uint32_t key = sel[(size_t)f * g.sel_frame_cap + L.sel_off + slot];
+    const uint32_t key = active ? sel[(size_t)f * g.sel_frame_cap + L.sel_off + slot] : 0;
     const int x = key_x(key) + L.minB, y = key_y(key) + L.minB;
-    // ---- IC_Angle on the unblurred level: lane = (side, u); side 0 rows +v, side 1 rows -v
+    // ---- IC_Angle on the unblurred level (src:91-138)
     const uint8_t* center = pyr + (size_t)f * g.pyr_frame_bytes + L.plane_off + (size_t)(y + kEdge) * L.pitch + (x + kEdge);
-    const int side = lane >> 5, u = (lane & 31) - kHalfPatch;
-    const bool col_ok = (lane & 31) < 2 * kHalfPatch + 1;
+    const int u = hl - kHalfPatch;
     int m10 = 0, m01 = 0;
-    if (col_ok && side == 0) m10 += u * center[u];
+    if (active && hl < 2 * kHalfPatch + 1) {
+        int val[2 * kHalfPatch + 1];
 #pragma unroll
-    for (int v = 1; v <= kHalfPatch; ++v) {
-        const int d = g.umax[v];
-        if (col_ok && u >= -d && u <= d) {
-            const int sv = side ? -v : v;
-            const int val = center[u + sv * L.pitch];
-            m10 += u * val;
-            m01 += sv * val;
+        for (int v = -kHalfPatch; v <= kHalfPatch; ++v) {
+            const int d = g.umax[v < 0 ? -v : v];
+            val[v + kHalfPatch] = (u >= -d && u <= d) ? center[u + v * L.pitch] : 0;
+        }
+#pragma unroll
+        for (int v = -kHalfPatch; v <= kHalfPatch; ++v) {
+            m10 += u * val[v + kHalfPatch];
+            m01 += v * val[v + kHalfPatch];
         }
     }
-    m10 = wave_sum(m10);
-    m01 = wave_sum(m01);
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {  // stays inside the 32-lane half
+        m10 += __shfl_xor(m10, o, 64);
+        m01 += __shfl_xor(m01, o, 64);
+    }
     const float angle = orb_fast_atan2((float)m01, (float)m10);
-    // ---- steered BRIEF on the blurred level
+    // ---- steered BRIEF on the blurred level (src:150-203)
     const float ang = angle * (float)(3.14159265358979323846 / 180.f);
     float a, b;
     steer_sincos(ang, &b, &a);  // a = cos, b = sin
     const uint8_t* bc = blur + (size_t)f * g.pyr_frame_bytes + L.plane_off + (size_t)(y + kEdge) * L.pitch + (x + kEdge);
-    unsigned long long words[4];
+    int t0[8], t1[8];
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        const int j = 64 * m + lane;  // test j = byte j/8, bit j%8 (src:173-199)
-        int t[2];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const float px = (float)c_pattern[4 * j + 2 * e], py = (float)c_pattern[4 * j + 2 * e + 1];
-            const int r = (int)__builtin_rintf(__builtin_fmaf(px, b, py * a));
-            const int c = (int)__builtin_rintf(__builtin_fmaf(px, a, -(py * b)));
-            t[e] = bc[r * L.pitch + c];
-        }
-        words[m] = ballot(t[0] < t[1]);
+    for (int m = 0; m < 8; ++m) {
+        const int j = 32 * m + hl;  // test j -> byte j/8, bit j%8 (src:173-199)
+        const float px0 = (float)c_pattern[4 * j], py0 = (float)c_pattern[4 * j + 1];
+        const float px1 = (float)c_pattern[4 * j + 2], py1 = (float)c_pattern[4 * j + 3];
+        const int r0 = (int)__builtin_rintf(__builtin_fmaf(px0, b, py0 * a));
+        const int c0 = (int)__builtin_rintf(__builtin_fmaf(px0, a, -(py0 * b)));
+        const int r1 = (int)__builtin_rintf(__builtin_fmaf(px1, b, py1 * a));
+        const int c1 = (int)__builtin_rintf(__builtin_fmaf(px1, a, -(py1 * b)));
+        t0[m] = active ? bc[r0 * L.pitch + c0] : 0;
+        t1[m] = active ? bc[r1 * L.pitch + c1] : 0;
     }
+    uint32_t words[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) words[m] = (uint32_t)(ballot(t0[m] < t1[m]) >> (32 * (half & 1)));
+    if (!active) return;
     const int dst = dst_index[(size_t)f * g.sel_frame_cap + L.sel_off + slot];
-    if (lane < 4) {
-        unsigned long long* dd = reinterpret_cast<unsigned long long*>(desc + ((size_t)f * cap + dst) * 32);
-        dd[lane] = words[lane == 0 ? 0 : lane == 1 ? 1 : lane == 2 ? 2 : 3];
-    }
-    if (lane == 0) {
+    if (hl < 8) {
+        uint32_t w = words[0];
+#pragma unroll
+        for (int m = 1; m < 8; ++m) if (hl == m) w = words[m];
+        reinterpret_cast<uint32_t*>(desc + ((size_t)f * cap + dst) * 32)[hl] = w;
+    } else if (hl == 8) {
         orb_keypoint_t k;
         float fx = (float)x, fy = (float)y;
         if (level != 0) { fx = fx * L.scale; fy = fy * L.scale; }
@@ -780,6 +1117,7 @@ struct Extractor {
     Geometry geo;
     bool geo_ok = false;
     // device buffers
+    orbgpu::KernelGeom* d_geom = nullptr;  // kernel geometry in device memory (read by every kernel)
     CellDesc* d_cells = nullptr; size_t cells_cap = 0;
     int2* d_xtab = nullptr; size_t xtab_cap = 0;
     int4* d_ytab = nullptr; size_t ytab_cap = 0;
@@ -826,6 +1164,8 @@ int grow(T*& p, size_t& cap, size_t need) {
 
 int prepare(Extractor* e, int w, int h, int n) {
     if (w != e->cur_w || h != e->cur_h) {
+        // the tables below are read by in-flight launches of the previous frame size
+        if (e->cur_w >= 0 && hipDeviceSynchronize() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "sync failed");
         orbgpu::Geometry g;
         if (!orbgpu::build_geometry(e->P, w, h, g)) return orbgpu_fail(ORB_ERR_ARG, "image too small for the pyramid/cell grid");
         e->geo = g;
@@ -835,7 +1175,10 @@ int prepare(Extractor* e, int w, int h, int n) {
         if ((rc = grow(e->d_cells, e->cells_cap, g.cells.size())) != ORB_OK) return rc;
         if ((rc = grow(e->d_xtab, e->xtab_cap, std::max<size_t>(1, g.xtab.size() / 2))) != ORB_OK) return rc;
         if ((rc = grow(e->d_ytab, e->ytab_cap, std::max<size_t>(1, g.ytab.size() / 4))) != ORB_OK) return rc;
-        if (hipMemcpy(e->d_cells, g.cells.data(), g.cells.size() * sizeof(orbgpu::CellDesc), hipMemcpyHostToDevice) != hipSuccess ||
+        if (!e->d_geom && hipMalloc(&e->d_geom, sizeof(orbgpu::KernelGeom)) != hipSuccess)
+            return orbgpu_fail(ORB_ERR_DEVICE, "hipMalloc failed");
+        if (hipMemcpy(e->d_geom, &g.k, sizeof(orbgpu::KernelGeom), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(e->d_cells, g.cells.data(), g.cells.size() * sizeof(orbgpu::CellDesc), hipMemcpyHostToDevice) != hipSuccess ||
             (!g.xtab.empty() && hipMemcpy(e->d_xtab, g.xtab.data(), g.xtab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) ||
             (!g.ytab.empty() && hipMemcpy(e->d_ytab, g.ytab.data(), g.ytab.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
             return orbgpu_fail(ORB_ERR_DEVICE, "table upload failed");
@@ -879,24 +1222,24 @@ int launch_batch(Extractor* e, const uint8_t* d_images, int n, int w, int h, int
         const orbgpu::LevelGeom& L = k.lv[l];
         dim3 grid((L.pw + kTileW - 1) / kTileW, (L.ph + kTileH - 1) / kTileH, n);
         if (l == 0)
-            hipLaunchKernelGGL(k_pyramid_level<true>, grid, dim3(256), 0, st, k, 0, d_images, (long long)frame_stride,
+            hipLaunchKernelGGL(k_pyramid_level<true>, grid, dim3(256), 0, st, e->d_geom, 0, d_images, (long long)frame_stride,
                                stride, e->d_pyr, e->d_blur, e->d_xtab, e->d_ytab);
         else
-            hipLaunchKernelGGL(k_pyramid_level<false>, grid, dim3(256), 0, st, k, l, nullptr, 0LL, 0, e->d_pyr,
+            hipLaunchKernelGGL(k_pyramid_level<false>, grid, dim3(256), 0, st, e->d_geom, l, nullptr, 0LL, 0, e->d_pyr,
                                e->d_blur, e->d_xtab, e->d_ytab);
     }
     mark(1);
     const int win_cap = (G.max_win + 15) & ~15;
-    hipLaunchKernelGGL(k_fast_cells, dim3((k.ncells + 3) / 4, n), dim3(256), 4 * 2 * win_cap, st, k, e->d_cells,
+    hipLaunchKernelGGL(k_fast_cells, dim3((k.ncells + 3) / 4, n), dim3(256), 4 * 4 * win_cap, st, e->d_geom, e->d_cells,
                        win_cap, e->d_pyr, e->d_cand, e->d_cell_count, e->d_cell_thr);
     mark(2);
-    hipLaunchKernelGGL(k_quadtree, dim3(k.nlevels, n), dim3(64), e->qt_lds, st, k, e->d_cells, e->d_cand,
+    hipLaunchKernelGGL(k_quadtree, dim3(k.nlevels, n), dim3(64), e->qt_lds, st, e->d_geom, e->d_cells, e->d_cand,
                        e->d_cell_count, e->d_scratch, e->d_sel, e->d_sel_count, e->qt_lds, e->d_status);
     mark(3);
-    hipLaunchKernelGGL(k_place, dim3(n), dim3(64), 0, st, k, e->d_sel, e->d_sel_count, e->d_dst, lap0, lap1, cap,
+    hipLaunchKernelGGL(k_place, dim3(n), dim3(64), 0, st, e->d_geom, e->d_sel, e->d_sel_count, e->d_dst, lap0, lap1, cap,
                        d_counts);
     mark(4);
-    hipLaunchKernelGGL(k_describe, dim3((G.max_sel + 3) / 4, k.nlevels, n), dim3(256), 0, st, k, e->d_pyr, e->d_blur,
+    hipLaunchKernelGGL(k_describe, dim3((G.max_sel + kDescKpPerBlock - 1) / kDescKpPerBlock, k.nlevels, n), dim3(256), 0, st, e->d_geom, e->d_pyr, e->d_blur,
                        e->d_sel, e->d_sel_count, e->d_dst, d_counts, cap, d_kps, d_desc);
     mark(5);
     if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "kernel launch failed");
@@ -935,7 +1278,7 @@ int orb_extractor_destroy(orb_extractor_t h) {
     Extractor* e = reinterpret_cast<Extractor*>(h);
     if (!e) return ORB_ERR_ARG;
     if (e->stream) hipStreamSynchronize(e->stream);
-    void* bufs[] = {e->d_cells, e->d_xtab, e->d_ytab, e->d_pyr, e->d_blur, e->d_cand, e->d_scratch,
+    void* bufs[] = {e->d_geom, e->d_cells, e->d_xtab, e->d_ytab, e->d_pyr, e->d_blur, e->d_cand, e->d_scratch,
                     e->d_cell_count, e->d_cell_thr, e->d_sel, e->d_dst, e->d_sel_count, e->d_status,
                     e->d_img, e->d_kps, e->d_desc, e->d_counts};
     for (void* b : bufs)

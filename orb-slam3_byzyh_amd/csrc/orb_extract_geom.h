@@ -162,7 +162,7 @@ inline bool build_geometry(const Params& P, int width, int height, Geometry& g) 
         if (L.w < 2 * kEdge || L.h < 2 * kEdge) return false;
         L.pw = L.w + 2 * kEdge;
         L.ph = L.h + 2 * kEdge;
-        L.pitch = align_up(L.pw, 64);
+        L.pitch = align_up(L.pw, 128);
         L.plane_off = plane_off;
         plane_off += (long long)L.pitch * L.ph;
         plane_off = (plane_off + 255) / 256 * 256;

@@ -138,14 +138,17 @@ ORB_HD static inline int orb_unguarded_partition(uint16_t* a, int first, int las
     }
 }
 
+// `ws` = workspace of kOrbSortStack * 3 ints for the explicit introsort stack (LDS on the device)
+constexpr int kOrbSortStack = 40;  // one pending right part per partition level; depth <= 2*lg(n) <= 32
+
 template <class Less>
-ORB_HD static inline void orb_std_sort(uint16_t* a, int n, Less less) {
+ORB_HD static inline void orb_std_sort(uint16_t* a, int n, Less less, int* ws) {
     if (n <= 1) return;
     int lg = 0;
     for (int m = n; m > 1; m >>= 1) ++lg;
     // __introsort_loop with an explicit stack (the recursion is on the right part, loop on the left)
     struct Range { int first, last, depth; };
-    Range stack[40];  // one pending right part per partition level; depth <= 2*lg(n) <= 32
+    Range* stack = reinterpret_cast<Range*>(ws);
     int sp = 0;
     stack[sp++] = {0, n, 2 * lg};
     while (sp > 0) {
@@ -171,4 +174,10 @@ ORB_HD static inline void orb_std_sort(uint16_t* a, int n, Less less) {
     } else {
         orb_insertion_sort(a, 0, n, less);
     }
+}
+
+template <class Less>
+ORB_HD static inline void orb_std_sort(uint16_t* a, int n, Less less) {
+    int ws[kOrbSortStack * 3];
+    orb_std_sort(a, n, less, ws);
 }
