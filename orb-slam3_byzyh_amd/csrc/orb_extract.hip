@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -475,17 +476,21 @@ struct QTree {
     uint16_t *split, *prev;
     uint8_t* divided;
     int* sort_ws;        // introsort stack (kOrbSortStack * 3 ints)
+    unsigned long long *sel_el, *sel_tmp;  // sort elements: (count << 16 | UL.x) << 16 | position
+    uint16_t *posA, *posB, *bend;          // partition stop lists, leaf-block ends
     int lcap;
 };
 
-__device__ inline size_t qt_meta_bytes(int lcap) {
-    return (size_t)lcap * (2 * (4 * 2 + 4 * 2 + 2) + 4 * 4 + 2 * 2 + 1) + 64 + kOrbSortStack * 12;
+__host__ __device__ inline size_t qt_meta_bytes(int lcap) {
+    return (size_t)lcap * (2 * (4 * 2 + 4 * 2 + 2) + 4 * 4 + 2 * 2 + 1 + 16 + 6) + 64 + kOrbSortStack * 12;
 }
 
 __device__ inline void qt_carve(QTree& t, uint8_t* p, int lcap) {
     t.lcap = lcap;
     t.sort_ws = (int*)p;
-    p += kOrbSortStack * 12;
+    p += kOrbSortStack * 12;  // 480 bytes: keeps the u64 arrays 8-aligned
+    t.sel_el = (unsigned long long*)p; p += 8 * lcap;
+    t.sel_tmp = (unsigned long long*)p; p += 8 * lcap;
     QGen* gens[2] = {&t.g0, &t.g1};
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
@@ -502,6 +507,9 @@ __device__ inline void qt_carve(QTree& t, uint8_t* p, int lcap) {
     }
     t.split = (uint16_t*)p; p += 2 * lcap;
     t.prev = (uint16_t*)p; p += 2 * lcap;
+    t.posA = (uint16_t*)p; p += 2 * lcap;
+    t.posB = (uint16_t*)p; p += 2 * lcap;
+    t.bend = (uint16_t*)p; p += 2 * lcap;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
         gens[g]->kb = p; p += lcap;
@@ -679,11 +687,126 @@ __device__ __forceinline__ void qt_copy_node(const QGen& A, QGen& B, int p, int 
     B.ks[to] = A.ks[p]; B.kn[to] = A.kn[p]; B.kb[to] = A.kb[p]; B.leaf[to] = A.leaf[p];
 }
 
+__device__ __forceinline__ int wave_incl_max(int v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(v, o, 64);
+        if (lane >= o) v = max(v, t);
+    }
+    return v;
+}
+
+// std::sort(vPrevSizeAndPointerToNode, compareNodes) (src:950) on t.prev[0..n), emulated exactly and
+// wave-parallel.  Each libstdc++ partition step (median-of-3 to first, unguarded Hoare partition) is
+// computed from two ballot-built stop lists: A = ascending positions with !(a < pivot), B = descending
+// positions with !(pivot < a); pairs (A_k, B_k) are swapped while A_k < B_k and the cut is
+// min(A_K*, B_K*-1) (tests/native/sort_port_check.cpp checks this against libstdc++).  The final
+// insertion sort is stable, so it is a stable rank sort inside each leaf block (<= 16 elements, or
+// a heap-sorted range when the depth limit hits, which is then already sorted).
+__device__ void qt_sort(QTree& t, const QGen& A, int n, int lane) {
+    unsigned long long* el = t.sel_el;
+    auto less64 = [](unsigned long long x, unsigned long long y) { return (x >> 16) < (y >> 16); };
+    for (int i = lane; i < n; i += 64) {
+        const int id = t.prev[i];
+        const uint32_t key = ((uint32_t)A.kn[id] << 16) | (uint16_t)A.x0[id];
+        el[i] = ((unsigned long long)key << 16) | (unsigned)id;
+        t.bend[i] = 0;
+    }
+    wave_sync();
+    if (n <= 1) return;
+    if (n > 16) {
+        int lg = 0;
+        for (int m = n; m > 1; m >>= 1) ++lg;
+        int* st = t.sort_ws;
+        if (lane == 0) { st[0] = 0; st[1] = n; st[2] = 2 * lg; }
+        int sp = 1;
+        wave_sync();
+        while (sp > 0) {
+            --sp;
+            const int first = uniform(st[3 * sp]);
+            int last = uniform(st[3 * sp + 1]), depth = uniform(st[3 * sp + 2]);
+            while (last - first > 16) {
+                if (depth == 0) {  // __partial_sort fallback: heap sort, serial (practically never taken)
+                    if (lane == 0) orb_heap_sort(el, first, last, less64);
+                    wave_sync();
+                    break;
+                }
+                --depth;
+                const int mid = first + (last - first) / 2;
+                if (lane == 0) orb_move_median_to_first(el, first, first + 1, mid, last - 1, less64);
+                wave_sync();
+                const unsigned long long p = el[first] >> 16;
+                int nA = 0, nB = 0;
+                for (int b = first + 1; b < last; b += 64) {
+                    const int i = b + lane;
+                    const bool fa = i < last && !((el[i] >> 16) < p);
+                    const unsigned long long m = ballot(fa);
+                    if (fa) t.posA[nA + rank_in(m)] = (uint16_t)i;
+                    nA += __popcll(m);
+                }
+                for (int b = last - 1; b > first; b -= 64) {
+                    const int j = b - lane;
+                    const bool fb = j > first && !(p < (el[j] >> 16));
+                    const unsigned long long m = ballot(fb);
+                    if (fb) t.posB[nB + rank_in(m)] = (uint16_t)j;
+                    nB += __popcll(m);
+                }
+                wave_sync();
+                const int lim = min(nA, nB);
+                int ks = lim;
+                for (int b = 0; b < lim; b += 64) {
+                    const int k = b + lane;
+                    const unsigned long long m = ballot(k < lim && t.posA[k] >= t.posB[k]);
+                    if (m) { ks = b + __ffsll((long long)m) - 1; break; }
+                }
+                ks = uniform(ks);
+                const int cut = uniform(min(ks < nA ? (int)t.posA[ks] : 1 << 30, ks > 0 ? (int)t.posB[ks - 1] : 1 << 30));
+                for (int k = lane; k < ks; k += 64) {  // disjoint (nested) pairs: no cross-lane hazards
+                    const int ia = t.posA[k], ib = t.posB[k];
+                    const unsigned long long ea = el[ia], eb = el[ib];
+                    el[ia] = eb;
+                    el[ib] = ea;
+                }
+                if (lane == 0) { st[3 * sp] = cut; st[3 * sp + 1] = last; st[3 * sp + 2] = depth; }
+                sp++;
+                wave_sync();
+                last = cut;
+            }
+            if (lane == 0) t.bend[first] = (uint16_t)last;  // leaf block [first, last)
+            wave_sync();
+        }
+    } else {
+        if (lane == 0) t.bend[0] = (uint16_t)n;
+        wave_sync();
+    }
+    // __final_insertion_sort == stable sort; elements never leave their leaf block
+    int carry = -1;
+    for (int b = 0; b < n; b += 64) {
+        const int i = b + lane;
+        int v = (i < n && t.bend[i] != 0) ? i : -1;
+        v = max(wave_incl_max(v, lane), carry);
+        if (i < n) {
+            const int s0 = v, e0 = t.bend[v];
+            const unsigned long long ki = el[i] >> 16;
+            int r = s0;
+            for (int j = s0; j < e0; ++j) {
+                const unsigned long long kj = el[j] >> 16;
+                r += (kj < ki) || (kj == ki && j < i);
+            }
+            t.sel_tmp[r] = el[i];
+        }
+        carry = __shfl(v, 63, 64);
+    }
+    wave_sync();
+    for (int i = lane; i < n; i += 64) t.prev[i] = (uint16_t)(t.sel_tmp[i] & 0xffff);
+    wave_sync();
+}
+
 template <bool kKeysInLds>
 __device__ void qt_run(QTree& t, int K, int N, int nroots, float root_w, int span_y,
                        const uint32_t* __restrict__ cand_level, const CellDesc* __restrict__ cells, int cell_begin,
                        int cell_count, const int32_t* __restrict__ ccount, uint32_t* __restrict__ sel_out,
-                       int sel_cap, int* n_sel, int* status) {
+                       int sel_cap, int* n_sel, int* status, int debug_flags) {
     const int lane = lane_id();
     bool overflow = false;
     // ---- gather candidates in cell order into keys[1], counting per root (src:756-764).
@@ -826,15 +949,19 @@ __device__ void qt_run(QTree& t, int K, int N, int nroots, float root_w, int spa
                 const int np = nsplit;
                 for (int i = lane; i < np; i += 64) t.prev[i] = t.split[i];
                 wave_sync();
-                if (lane == 0) {
-                    const int16_t* x0a = A2.x0;
-                    const int32_t* kc = A2.kn;
-                    orb_std_sort(t.prev, np, [&](uint16_t a, uint16_t b) {
-                        const int ca = kc[a], cb = kc[b];
-                        return ca < cb || (ca == cb && x0a[a] < x0a[b]);
-                    }, t.sort_ws);
+                if (debug_flags & 2) {  // reference single-lane port (A/B check)
+                    if (lane == 0) {
+                        const int16_t* x0a = A2.x0;
+                        const int32_t* kc = A2.kn;
+                        orb_std_sort(t.prev, np, [&](uint16_t a, uint16_t b) {
+                            const int ca = kc[a], cb = kc[b];
+                            return ca < cb || (ca == cb && x0a[a] < x0a[b]);
+                        }, t.sort_ws);
+                    }
+                    wave_sync();
+                } else {
+                    qt_sort(t, A2, np, lane);
                 }
-                wave_sync();
                 qt_count_children(t, A2, t.prev, np, lane);
                 // division order o = 0.. is prev[np-1-o]; stop once the list reaches N (src:1006)
                 int ndiv = np, carry = 0;
@@ -959,13 +1086,13 @@ __global__ __launch_bounds__(64) void k_quadtree(const KernelGeom* __restrict__ 
         t.keys0 = (uint32_t*)(smem + meta);
         t.keys1 = t.keys0 + K;
         qt_run<true>(t, K, N, L.n_roots, L.root_w, L.maxBY - L.minB, cand_level, cells, L.cell_begin,
-                     L.cell_count, cc, sel_out, L.sel_cap, n_sel, status);
+                     L.cell_count, cc, sel_out, L.sel_cap, n_sel, status, g.debug_flags);
     } else {
         uint32_t* scratch = key_scratch + ((size_t)f * g.cand_frame_cap + L.cand_off) * 2;
         t.keys0 = scratch;
         t.keys1 = scratch + L.cand_cap;
         qt_run<false>(t, K, N, L.n_roots, L.root_w, L.maxBY - L.minB, cand_level, cells, L.cell_begin,
-                      L.cell_count, cc, sel_out, L.sel_cap, n_sel, status);
+                      L.cell_count, cc, sel_out, L.sel_cap, n_sel, status, g.debug_flags);
     }
 }
 
@@ -1138,8 +1265,14 @@ struct Extractor {
     int last_n = 0;
     int qt_lds = 0;
     // optional per-stage timing: HIP events recorded on the launch stream between the stages
+    // sub-batching over internal streams
+    static constexpr int kMaxStreams = 4;
+    int chunk = 1 << 30, nstreams = 1;  // off by default: measured slower (streams did not overlap)
+    hipStream_t sub[kMaxStreams] = {};
+    hipEvent_t fork_ev = nullptr, join_ev[kMaxStreams] = {};
+    long long batches = 0;
     bool profile = false;
-    std::vector<hipEvent_t> events;   // kStages + 1 per profiled launch
+    std::vector<hipEvent_t> events;   // kStages + 1 per profiled sub-batch launch
     int ev_used = 0;                  // launches recorded since the last read
     long long frames_profiled = 0;
 };
@@ -1183,6 +1316,15 @@ int prepare(Extractor* e, int w, int h, int n) {
             (!g.ytab.empty() && hipMemcpy(e->d_ytab, g.ytab.data(), g.ytab.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
             return orbgpu_fail(ORB_ERR_DEVICE, "table upload failed");
         e->geo_ok = true;
+        // quad-tree LDS: node metadata of the largest level + room for ~7k keys (80 KB: two
+        // workgroups per CU); larger feature budgets (e.g. the 5x monocular-init extractor) get more
+        size_t meta = 0;
+        for (int l = 0; l < g.k.nlevels; ++l) meta = std::max(meta, (qt_meta_bytes(g.k.lv[l].sel_cap + 64) + 15) & ~(size_t)15);
+        const size_t want = std::max<size_t>(80 * 1024, meta + 32 * 1024);
+        if (meta > 160 * 1024) return orbgpu_fail(ORB_ERR_ARG, "nfeatures too large for the quad-tree LDS budget");
+        e->qt_lds = (int)std::min<size_t>(want, 160 * 1024);
+        if (hipFuncSetAttribute((const void*)k_quadtree, hipFuncAttributeMaxDynamicSharedMemorySize, e->qt_lds) != hipSuccess)
+            return orbgpu_fail(ORB_ERR_DEVICE, "cannot raise the quad-tree LDS limit");
     }
     const orbgpu::KernelGeom& k = e->geo.k;
     int rc;
@@ -1198,9 +1340,9 @@ int prepare(Extractor* e, int w, int h, int n) {
     return ORB_OK;
 }
 
-int launch_batch(Extractor* e, const uint8_t* d_images, int n, int w, int h, int stride, size_t frame_stride,
-                 int lap0, int lap1, orb_keypoint_t* d_kps, uint8_t* d_desc, int cap, int32_t* d_counts,
-                 hipStream_t st) {
+// Enqueue the five stages for frames [f0, f0 + n) of the handle's buffers on stream st.
+int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int stride, size_t frame_stride, int lap0,
+                 int lap1, orb_keypoint_t* d_kps, uint8_t* d_desc, int cap, int32_t* d_counts, hipStream_t st) {
     const orbgpu::Geometry& G = e->geo;
     const orbgpu::KernelGeom& k = G.k;
     hipEvent_t* ev = nullptr;
@@ -1216,33 +1358,74 @@ int launch_batch(Extractor* e, const uint8_t* d_images, int n, int w, int h, int
         e->frames_profiled += n;
     }
     auto mark = [&](int i) { if (ev) hipEventRecord(ev[i], st); };
-    hipMemsetAsync(e->d_status, 0, sizeof(int), st);
+    uint8_t* pyr = e->d_pyr + (size_t)f0 * k.pyr_frame_bytes;
+    uint8_t* blr = e->d_blur + (size_t)f0 * k.pyr_frame_bytes;
+    uint32_t* cand = e->d_cand + (size_t)f0 * k.cand_frame_cap;
+    uint32_t* scratch = e->d_scratch + (size_t)f0 * k.cand_frame_cap * 2;
+    int32_t* ccount = e->d_cell_count + (size_t)f0 * k.ncells;
+    uint8_t* cthr = e->d_cell_thr + (size_t)f0 * k.ncells;
+    uint32_t* sel = e->d_sel + (size_t)f0 * k.sel_frame_cap;
+    int32_t* dst = e->d_dst + (size_t)f0 * k.sel_frame_cap;
+    int32_t* scount = e->d_sel_count + (size_t)f0 * k.nlevels;
+    const uint8_t* imgs = d_images + (size_t)f0 * frame_stride;
+    orb_keypoint_t* kps = d_kps + (size_t)f0 * cap;
+    uint8_t* desc = d_desc + (size_t)f0 * cap * 32;
+    int32_t* counts = d_counts + 2 * (size_t)f0;
     mark(0);
     for (int l = 0; l < k.nlevels; ++l) {
         const orbgpu::LevelGeom& L = k.lv[l];
         dim3 grid((L.pw + kTileW - 1) / kTileW, (L.ph + kTileH - 1) / kTileH, n);
         if (l == 0)
-            hipLaunchKernelGGL(k_pyramid_level<true>, grid, dim3(256), 0, st, e->d_geom, 0, d_images, (long long)frame_stride,
-                               stride, e->d_pyr, e->d_blur, e->d_xtab, e->d_ytab);
+            hipLaunchKernelGGL(k_pyramid_level<true>, grid, dim3(256), 0, st, e->d_geom, 0, imgs, (long long)frame_stride,
+                               stride, pyr, blr, e->d_xtab, e->d_ytab);
         else
-            hipLaunchKernelGGL(k_pyramid_level<false>, grid, dim3(256), 0, st, e->d_geom, l, nullptr, 0LL, 0, e->d_pyr,
-                               e->d_blur, e->d_xtab, e->d_ytab);
+            hipLaunchKernelGGL(k_pyramid_level<false>, grid, dim3(256), 0, st, e->d_geom, l, nullptr, 0LL, 0, pyr, blr,
+                               e->d_xtab, e->d_ytab);
     }
     mark(1);
     const int win_cap = (G.max_win + 15) & ~15;
     hipLaunchKernelGGL(k_fast_cells, dim3((k.ncells + 3) / 4, n), dim3(256), 4 * 4 * win_cap, st, e->d_geom, e->d_cells,
-                       win_cap, e->d_pyr, e->d_cand, e->d_cell_count, e->d_cell_thr);
+                       win_cap, pyr, cand, ccount, cthr);
     mark(2);
-    hipLaunchKernelGGL(k_quadtree, dim3(k.nlevels, n), dim3(64), e->qt_lds, st, e->d_geom, e->d_cells, e->d_cand,
-                       e->d_cell_count, e->d_scratch, e->d_sel, e->d_sel_count, e->qt_lds, e->d_status);
+    hipLaunchKernelGGL(k_quadtree, dim3(k.nlevels, n), dim3(64), e->qt_lds, st, e->d_geom, e->d_cells, cand, ccount,
+                       scratch, sel, scount, e->qt_lds, e->d_status);
     mark(3);
-    hipLaunchKernelGGL(k_place, dim3(n), dim3(64), 0, st, e->d_geom, e->d_sel, e->d_sel_count, e->d_dst, lap0, lap1, cap,
-                       d_counts);
+    hipLaunchKernelGGL(k_place, dim3(n), dim3(64), 0, st, e->d_geom, sel, scount, dst, lap0, lap1, cap, counts);
     mark(4);
-    hipLaunchKernelGGL(k_describe, dim3((G.max_sel + kDescKpPerBlock - 1) / kDescKpPerBlock, k.nlevels, n), dim3(256), 0, st, e->d_geom, e->d_pyr, e->d_blur,
-                       e->d_sel, e->d_sel_count, e->d_dst, d_counts, cap, d_kps, d_desc);
+    hipLaunchKernelGGL(k_describe, dim3((G.max_sel + kDescKpPerBlock - 1) / kDescKpPerBlock, k.nlevels, n), dim3(256), 0,
+                       st, e->d_geom, pyr, blr, sel, scount, dst, counts, cap, kps, desc);
     mark(5);
     if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "kernel launch failed");
+    return ORB_OK;
+}
+
+// A batch is split into sub-batches of e->chunk frames on the handle's internal streams (fork/join
+// with events against the caller's stream), so the latency-bound stages of one sub-batch (quad-tree,
+// descriptors) overlap the compute-bound stages (pyramid, FAST) of another.
+int launch_batch(Extractor* e, const uint8_t* d_images, int n, int w, int h, int stride, size_t frame_stride,
+                 int lap0, int lap1, orb_keypoint_t* d_kps, uint8_t* d_desc, int cap, int32_t* d_counts,
+                 hipStream_t st) {
+    (void)w; (void)h;
+    hipMemsetAsync(e->d_status, 0, sizeof(int), st);
+    const int nchunks = (n + e->chunk - 1) / e->chunk;
+    if (nchunks <= 1 || e->nstreams <= 1) {
+        const int rc = launch_chunk(e, 0, d_images, n, stride, frame_stride, lap0, lap1, d_kps, d_desc, cap, d_counts, st);
+        if (rc != ORB_OK) return rc;
+    } else {
+        hipEventRecord(e->fork_ev, st);
+        for (int s = 0; s < e->nstreams; ++s) hipStreamWaitEvent(e->sub[s], e->fork_ev, 0);
+        for (int c = 0; c < nchunks; ++c) {
+            const int f0 = c * e->chunk, m = std::min(e->chunk, n - f0);
+            const int rc = launch_chunk(e, f0, d_images, m, stride, frame_stride, lap0, lap1, d_kps, d_desc, cap, d_counts,
+                                        e->sub[c % e->nstreams]);
+            if (rc != ORB_OK) return rc;
+        }
+        for (int s = 0; s < e->nstreams; ++s) {
+            hipEventRecord(e->join_ev[s], e->sub[s]);
+            hipStreamWaitEvent(st, e->join_ev[s], 0);
+        }
+    }
+    e->batches++;
     e->last_n = n;
     return ORB_OK;
 }
@@ -1270,6 +1453,16 @@ int orb_extractor_create(const orb_params_t* p, int max_width, int max_height, i
         return orbgpu_fail(ORB_ERR_DEVICE, "stream/status allocation failed");
     }
     hipFuncSetAttribute((const void*)k_quadtree, hipFuncAttributeMaxDynamicSharedMemorySize, e->qt_lds);
+    if (const char* c = getenv("ORBGPU_CHUNK")) e->chunk = std::max(1, atoi(c));
+    if (const char* c = getenv("ORBGPU_STREAMS")) e->nstreams = std::min(Extractor::kMaxStreams, std::max(1, atoi(c)));
+    bool ok = hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) == hipSuccess;
+    for (int s = 0; s < Extractor::kMaxStreams && ok; ++s)
+        ok = hipStreamCreateWithFlags(&e->sub[s], hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&e->join_ev[s], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        orb_extractor_destroy(reinterpret_cast<orb_extractor_t>(e));
+        return orbgpu_fail(ORB_ERR_DEVICE, "stream/event creation failed");
+    }
     *out = reinterpret_cast<orb_extractor_t>(e);
     return ORB_OK;
 }
@@ -1284,6 +1477,11 @@ int orb_extractor_destroy(orb_extractor_t h) {
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t x : e->events) (void)hipEventDestroy(x);
+    for (int s = 0; s < Extractor::kMaxStreams; ++s) {
+        if (e->sub[s]) { hipStreamSynchronize(e->sub[s]); hipStreamDestroy(e->sub[s]); }
+        if (e->join_ev[s]) hipEventDestroy(e->join_ev[s]);
+    }
+    if (e->fork_ev) hipEventDestroy(e->fork_ev);
     if (e->stream) hipStreamDestroy(e->stream);
     delete e;
     return ORB_OK;
@@ -1455,6 +1653,7 @@ int orb_extractor_profile(orb_extractor_t h, int enable) {
     e->profile = enable != 0;
     e->ev_used = 0;
     e->frames_profiled = 0;
+    e->batches = 0;
     return ORB_OK;
 }
 
@@ -1471,7 +1670,7 @@ int orb_extractor_stage_ms(orb_extractor_t h, float* ms, int* launches, long lon
             ms[s] += t;
         }
     }
-    if (launches) *launches = e->ev_used;
+    if (launches) *launches = (int)e->batches;  // batch calls (each may be several sub-batch launches)
     if (frames) *frames = e->frames_profiled;
     return ORB_OK;
 }

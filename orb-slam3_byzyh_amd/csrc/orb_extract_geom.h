@@ -4,6 +4,7 @@
 // derives it (file:line cited per item) so the kernels only have to index tables.
 #pragma once
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 #include <vector>
 
@@ -43,6 +44,7 @@ struct KernelGeom {
     int cand_frame_cap;          // candidate slots per frame
     int sel_frame_cap;           // selected-keypoint slots per frame
     int umax[kHalfPatch + 1];
+    int debug_flags;             // timing experiments only (ORBGPU_DEBUG_FLAGS); 0 in production
     LevelGeom lv[kMaxLevels];
 };
 
@@ -151,6 +153,8 @@ inline bool build_geometry(const Params& P, int width, int height, Geometry& g) 
     k.nlevels = P.nlevels;
     k.ini_th = std::min(std::max(P.ini_th, 0), 255);
     k.min_th = std::min(std::max(P.min_th, 0), 255);
+    k.debug_flags = 0;
+    if (const char* d = getenv("ORBGPU_DEBUG_FLAGS")) k.debug_flags = atoi(d);
     for (int v = 0; v <= kHalfPatch; ++v) k.umax[v] = P.umax[v];
     long long plane_off = 0;
     int cand_off = 0, sel_off = 0;

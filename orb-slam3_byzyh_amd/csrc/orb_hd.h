@@ -42,20 +42,20 @@ ORB_HD static inline float orb_fast_atan2(float y, float x) {
 // 676-697, 950), which has ties (equal count and equal UL.x); the resulting order, and hence the
 // selected keypoints, depends on this exact algorithm.  Run by ONE lane.
 // ---------------------------------------------------------------------------------------------
-template <class Less>
-ORB_HD static inline void orb_unguarded_linear_insert(uint16_t* a, int last, Less less) {
-    const uint16_t val = a[last];
+template <class T, class Less>
+ORB_HD static inline void orb_unguarded_linear_insert(T* a, int last, Less less) {
+    const T val = a[last];
     int next = last - 1;
     while (less(val, a[next])) { a[last] = a[next]; last = next; --next; }
     a[last] = val;
 }
 
-template <class Less>
-ORB_HD static inline void orb_insertion_sort(uint16_t* a, int first, int last, Less less) {
+template <class T, class Less>
+ORB_HD static inline void orb_insertion_sort(T* a, int first, int last, Less less) {
     if (first == last) return;
     for (int i = first + 1; i != last; ++i) {
         if (less(a[i], a[first])) {
-            const uint16_t val = a[i];
+            const T val = a[i];
             for (int k = i; k > first; --k) a[k] = a[k - 1];
             a[first] = val;
         } else {
@@ -64,8 +64,8 @@ ORB_HD static inline void orb_insertion_sort(uint16_t* a, int first, int last, L
     }
 }
 
-template <class Less>
-ORB_HD static inline void orb_push_heap(uint16_t* a, int first, int hole, int top, uint16_t val, Less less) {
+template <class T, class Less>
+ORB_HD static inline void orb_push_heap(T* a, int first, int hole, int top, T val, Less less) {
     int parent = (hole - 1) / 2;
     while (hole > top && less(a[first + parent], val)) {
         a[first + hole] = a[first + parent];
@@ -75,8 +75,8 @@ ORB_HD static inline void orb_push_heap(uint16_t* a, int first, int hole, int to
     a[first + hole] = val;
 }
 
-template <class Less>
-ORB_HD static inline void orb_adjust_heap(uint16_t* a, int first, int hole, int len, uint16_t val, Less less) {
+template <class T, class Less>
+ORB_HD static inline void orb_adjust_heap(T* a, int first, int hole, int len, T val, Less less) {
     const int top = hole;
     int child = hole;
     while (child < (len - 1) / 2) {
@@ -93,8 +93,8 @@ ORB_HD static inline void orb_adjust_heap(uint16_t* a, int first, int hole, int 
     orb_push_heap(a, first, hole, top, val, less);
 }
 
-template <class Less>
-ORB_HD static inline void orb_heap_sort(uint16_t* a, int first, int last, Less less) {
+template <class T, class Less>
+ORB_HD static inline void orb_heap_sort(T* a, int first, int last, Less less) {
     const int len = last - first;
     if (len >= 2) {  // __make_heap
         int parent = (len - 2) / 2;
@@ -107,14 +107,14 @@ ORB_HD static inline void orb_heap_sort(uint16_t* a, int first, int last, Less l
     // __heap_select over [first, last, last) adds nothing; then __sort_heap
     while (last - first > 1) {
         --last;
-        const uint16_t val = a[last];
+        const T val = a[last];
         a[last] = a[first];
         orb_adjust_heap(a, first, 0, last - first, val, less);
     }
 }
 
-template <class Less>
-ORB_HD static inline void orb_move_median_to_first(uint16_t* a, int result, int x, int y, int z, Less less) {
+template <class T, class Less>
+ORB_HD static inline void orb_move_median_to_first(T* a, int result, int x, int y, int z, Less less) {
     int pick;
     if (less(a[x], a[y])) {
         if (less(a[y], a[z])) pick = y;
@@ -123,17 +123,17 @@ ORB_HD static inline void orb_move_median_to_first(uint16_t* a, int result, int 
     } else if (less(a[x], a[z])) pick = x;
     else if (less(a[y], a[z])) pick = z;
     else pick = y;
-    const uint16_t t = a[result]; a[result] = a[pick]; a[pick] = t;
+    const T t = a[result]; a[result] = a[pick]; a[pick] = t;
 }
 
-template <class Less>
-ORB_HD static inline int orb_unguarded_partition(uint16_t* a, int first, int last, int pivot, Less less) {
+template <class T, class Less>
+ORB_HD static inline int orb_unguarded_partition(T* a, int first, int last, int pivot, Less less) {
     while (true) {
         while (less(a[first], a[pivot])) ++first;
         --last;
         while (less(a[pivot], a[last])) --last;
         if (!(first < last)) return first;
-        const uint16_t t = a[first]; a[first] = a[last]; a[last] = t;
+        const T t = a[first]; a[first] = a[last]; a[last] = t;
         ++first;
     }
 }
@@ -141,8 +141,8 @@ ORB_HD static inline int orb_unguarded_partition(uint16_t* a, int first, int las
 // `ws` = workspace of kOrbSortStack * 3 ints for the explicit introsort stack (LDS on the device)
 constexpr int kOrbSortStack = 40;  // one pending right part per partition level; depth <= 2*lg(n) <= 32
 
-template <class Less>
-ORB_HD static inline void orb_std_sort(uint16_t* a, int n, Less less, int* ws) {
+template <class T, class Less>
+ORB_HD static inline void orb_std_sort(T* a, int n, Less less, int* ws) {
     if (n <= 1) return;
     int lg = 0;
     for (int m = n; m > 1; m >>= 1) ++lg;
@@ -176,8 +176,8 @@ ORB_HD static inline void orb_std_sort(uint16_t* a, int n, Less less, int* ws) {
     }
 }
 
-template <class Less>
-ORB_HD static inline void orb_std_sort(uint16_t* a, int n, Less less) {
+template <class T, class Less>
+ORB_HD static inline void orb_std_sort(T* a, int n, Less less) {
     int ws[kOrbSortStack * 3];
     orb_std_sort(a, n, less, ws);
 }

@@ -18,8 +18,48 @@ static bool compareNodes(std::pair<int, Node*>& e1, std::pair<int, Node*>& e2) {
     return e1.second->ulx < e2.second->ulx;
 }
 
+// The wave-parallel emulation used on the GPU (k_quadtree, qt_sort): libstdc++'s unguarded Hoare
+// partition of [first+1, last) around a[first] expressed through two "stop lists":
+//   A = ascending positions with !(a[i] < p), B = descending positions with !(p < a[i]);
+//   pairs (A_k, B_k) are swapped while A_k < B_k; with K* the first k where A_k >= B_k (A past its end
+//   = +inf, B past its end = -inf) the cut is min(A_K*, B_{K*-1}) (B_{-1} = +inf).
+// Checked against orb_unguarded_partition, which test 1 checks against std::sort itself.
+template <class T, class Less>
+static int stoplist_partition(T* a, int first, int last, Less less) {
+    const T p = a[first];
+    std::vector<int> A, B;
+    for (int i = first + 1; i < last; ++i) if (!less(a[i], p)) A.push_back(i);
+    for (int i = last - 1; i > first; --i) if (!less(p, a[i])) B.push_back(i);
+    const int lim = (int)std::min(A.size(), B.size());
+    int ks = lim;
+    for (int k = 0; k < lim; ++k) if (A[k] >= B[k]) { ks = k; break; }
+    const long inf = 1L << 40;
+    const long ak = ks < (int)A.size() ? A[ks] : inf;
+    const long bprev = ks > 0 ? B[ks - 1] : inf;
+    for (int k = 0; k < ks; ++k) std::swap(a[A[k]], a[B[k]]);
+    return (int)std::min(ak, bprev);
+}
+
 int main() {
     std::mt19937 rng(12345);
+    {
+        int cases = 0;
+        for (int n : {17, 18, 19, 33, 40, 100, 500, 1200}) {  // partitions only run on ranges > 16
+            for (int rep = 0; rep < 400; ++rep, ++cases) {
+                std::vector<int> v(n), w;
+                const int kv = 1 + (int)(rng() % (rep % 4 == 0 ? 2 : 20));
+                for (int i = 0; i < n; ++i) v[i] = (int)(rng() % kv) * 16 + i % 16;  // payload in low bits
+                auto less = [](int x, int y) { return (x >> 4) < (y >> 4); };
+                const int mid = n / 2;
+                orb_move_median_to_first(v.data(), 0, 1, mid, n - 1, less);
+                w = v;
+                const int c1 = orb_unguarded_partition(v.data(), 1, n, 0, less);
+                const int c2 = stoplist_partition(w.data(), 0, n, less);
+                if (c1 != c2 || v != w) { printf("STOPLIST MISMATCH n=%d rep=%d cut %d vs %d\n", n, rep, c1, c2); return 1; }
+            }
+        }
+        printf("stoplist ok %d\n", cases);
+    }
     int cases = 0;
     for (int n : {0, 1, 2, 5, 15, 16, 17, 18, 31, 33, 64, 100, 257, 600, 1500, 4000}) {
         for (int rep = 0; rep < 60; ++rep, ++cases) {
