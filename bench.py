@@ -154,7 +154,8 @@ def main():
     if (counts[:, 1] < 0).any():
         raise RuntimeError("a frame exceeded the keypoint capacity")
 
-    ex.profile(True)
+    stage_timing = os.environ.get("BENCH_NO_STAGE_TIMING", "0") != "1"
+    ex.profile(stage_timing)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)

@@ -78,7 +78,9 @@ __device__ __forceinline__ int wave_sum(int v) {
 // ================================================================================================
 constexpr int kTileW = 128, kTileH = 16, kHalo = 3;  // 128-byte rows: every store fills whole cache lines
 constexpr int kLW = kTileW + 2 * kHalo, kLH = kTileH + 2 * kHalo;  // 134 x 22
-constexpr int kBoxW = 2 * kLW + 4, kBoxH = 2 * kLH + 4;           // source box for scale factors <= 2
+constexpr int kBoxW = 288, kBoxH = 2 * kLH + 4;  // source box (bytes) for scale factors <= 2
+constexpr int kBoxWords = kBoxW / 4;
+static_assert(kBoxW >= 3 + 2 * kLW + 2, "box too narrow");
 
 // 8 bytes from a 4-byte-aligned LDS row at any byte offset, as aligned dword reads + v_alignbyte.
 // (Adjacent byte reads would otherwise be merged by the compiler into unaligned ds_read_u16/b64,
@@ -132,69 +134,92 @@ __global__ __launch_bounds__(256) void k_pyramid_level(const KernelGeom* __restr
     int vx0, vx1, vy0, vy1;
     reflect_range(X0 - kHalo - kEdge, X0 + kTileW + kHalo - 1 - kEdge, L.w, vx0, vx1);
     reflect_range(Y0 - kHalo - kEdge, Y0 + kTileH + kHalo - 1 - kEdge, L.h, vy0, vy1);
-    const uint8_t* src;
-    int sstride, bx0, by0, bw, bh;
     if (kLevel0) {
-        src = in + (size_t)f * in_frame_stride;
-        sstride = in_stride;
-        bx0 = vx0; by0 = vy0; bw = vx1 - vx0 + 1; bh = vy1 - vy0 + 1;
+        // level 0: tile (+halo) straight from the input with reflected indices; 2 rows x 128 columns
+        // per pass, 4 passes (8 loads per thread) in flight
+        const uint8_t* src = in + (size_t)f * in_frame_stride;
+        const int c0 = tid & 127, rg = tid >> 7;
+        for (int ty0 = 0; ty0 < kLH; ty0 += 8) {
+            int v[4][2];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int ty = ty0 + 2 * q + rg;
+                const int vy = reflect101(Y0 - kHalo + min(ty, kLH - 1) - kEdge, L.h);
+#pragma unroll
+                for (int hx = 0; hx < 2; ++hx) {
+                    const int tx = c0 + 128 * hx;
+                    const int vx = reflect101(X0 - kHalo + min(tx, kLW - 1) - kEdge, L.w);
+                    v[q][hx] = (ty < kLH && tx < kLW) ? src[(size_t)vy * in_stride + vx] : 0;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int hx = 0; hx < 2; ++hx) {
+                    const int ty = ty0 + 2 * q + rg, tx = c0 + 128 * hx;
+                    if (ty < kLH && tx < kLW) tile[ty][tx] = (uint8_t)v[q][hx];
+                }
+        }
+        __syncthreads();
     } else {
         const LevelGeom& P = g.lv[level - 1];
-        src = pyr + (size_t)f * g.pyr_frame_bytes + P.plane_off + (size_t)kEdge * P.pitch + kEdge;
-        sstride = P.pitch;
+        const uint8_t* src = pyr + (size_t)f * g.pyr_frame_bytes + P.plane_off + (size_t)kEdge * P.pitch + kEdge;
+        const int sstride = P.pitch;  // multiple of 128: every box row has the same alignment
         const double scx = 1. / ((double)L.w / P.w), scy = 1. / ((double)L.h / P.h);
-        bx0 = resize_src_index(vx0, scx, P.w);
-        by0 = resize_src_index(vy0, scy, P.h);
-        bw = min(resize_src_index(vx1, scx, P.w) + 1, P.w - 1) - bx0 + 1;
-        bh = min(resize_src_index(vy1, scy, P.h) + 1, P.h - 1) - by0 + 1;
+        const int bx0 = resize_src_index(vx0, scx, P.w);
+        const int by0 = resize_src_index(vy0, scy, P.h);
+        const int bw = min(resize_src_index(vx1, scx, P.w) + 1, P.w - 1) - bx0 + 1;
+        const int bh = min(resize_src_index(vy1, scy, P.h) + 1, P.h - 1) - by0 + 1;
         // coefficient tables of the tile's columns / rows
         if (tid < kLW) xs[tid] = xtab[L.xtab_off + reflect101(X0 - kHalo + tid - kEdge, L.w)];
         else if (tid >= 192 && tid < 192 + kLH) ys[tid - 192] = ytab[L.ytab_off + reflect101(Y0 - kHalo + (tid - 192) - kEdge, L.h)];
-    }
-    // stage the source box: 8 independent byte loads per thread per round
-    const int nbox = bw * bh;
-    for (int i0 = 0; i0 < nbox; i0 += 256 * 8) {
-        uint8_t v[8];
+        // source box as aligned dwords (over-reads stay inside the previous level's 19-px frame)
+        const uint8_t* row0 = src + (size_t)by0 * sstride + bx0;
+        const int shift = (int)((uintptr_t)row0 & 3);
+        const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(row0 - shift);
+        const int nw = (shift + bw + 3) >> 2;
+        uint32_t* boxw = reinterpret_cast<uint32_t*>(box);
+        const int wl = tid & 63, rg = tid >> 6;
+        for (int r0 = 0; r0 < bh; r0 += 8) {
+            uint32_t v[2][2];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int i = i0 + k * 256 + tid;
-            const int r = i / bw, c = i - (i / bw) * bw;
-            v[k] = i < nbox ? src[(size_t)(by0 + r) * sstride + bx0 + c] : 0;
-        }
+            for (int q = 0; q < 2; ++q)
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int i = i0 + k * 256 + tid;
-            if (i < nbox) box[(i / bw) * kBoxW + (i - (i / bw) * bw)] = v[k];
+                for (int hx = 0; hx < 2; ++hx) {
+                    const int r = r0 + 4 * q + rg, w = wl + 64 * hx;
+                    v[q][hx] = (r < bh && w < nw) ? wsrc[(size_t)r * (sstride >> 2) + w] : 0u;
+                }
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+#pragma unroll
+                for (int hx = 0; hx < 2; ++hx) {
+                    const int r = r0 + 4 * q + rg, w = wl + 64 * hx;
+                    if (r < bh && w < nw) boxw[r * kBoxWords + w] = v[q][hx];
+                }
         }
-    }
-    __syncthreads();
-    // tile (+halo) values
-    for (int i = tid; i < kLH * kLW; i += 256) {
-        const int ty = i / kLW, tx = i - ty * kLW;
-        int v;
-        if (kLevel0) {
-            const int vx = reflect101(X0 - kHalo + tx - kEdge, L.w), vy = reflect101(Y0 - kHalo + ty - kEdge, L.h);
-            v = box[(vy - by0) * kBoxW + (vx - bx0)];
-        } else {
+        __syncthreads();
+        // tile (+halo) values, INTER_LINEAR from the box
+        for (int i = tid; i < kLH * kLW; i += 256) {
+            const int ty = i / kLW, tx = i - ty * kLW;
             const int2 X = xs[tx];
             const int4 Y = ys[ty];
-            const int sx = X.x - bx0, sx1 = min(X.x + 1, bx0 + bw - 1) - bx0;
+            const int sx = X.x - bx0 + shift, sx1 = min(X.x + 1, bx0 + bw - 1) - bx0 + shift;
             const int a0 = X.y & 0xffff, a1 = X.y >> 16;
             const uint8_t* R0 = box + (Y.x - by0) * kBoxW;
             const uint8_t* R1 = box + (Y.y - by0) * kBoxW;
             const int h0 = R0[sx] * a0 + R0[sx1] * a1, h1 = R1[sx] * a0 + R1[sx1] * a1;
             const int vx = reflect101(X0 - kHalo + tx - kEdge, L.w);
+            int v;
             if (vx < L.simd_end) {  // VResizeLinearVec_32s8u: v_mul_hi on (S >> 4), rounding shift by 2
                 const int t0 = min(h0 >> 4, 32767), t1 = min(h1 >> 4, 32767);
                 v = (((t0 * Y.z) >> 16) + ((t1 * Y.w) >> 16) + 2) >> 2;
             } else {                // FixedPtCast<int, uchar, 22>
                 v = (h0 * Y.z + h1 * Y.w + (1 << 21)) >> 22;
             }
-            v = min(max(v, 0), 255);
+            tile[ty][tx] = (uint8_t)min(max(v, 0), 255);
         }
-        tile[ty][tx] = (uint8_t)v;
+        __syncthreads();
     }
-    __syncthreads();
     // padded plane: 8 consecutive pixels per thread
     const int r = tid >> 4, c = (tid & 15) * 8;
     {
