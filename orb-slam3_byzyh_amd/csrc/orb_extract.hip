@@ -366,18 +366,34 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
     uint16_t* cl = reinterpret_cast<uint16_t*>(sc + win_cap);
     const int ww = C.win_w, wh = C.win_h, n = ww * wh;
     const uint8_t* src = view + (size_t)C.ini_y * L.pitch + C.ini_x;
-    for (int i = lane; i < n; i += 64) sc[i] = 0;
-    for (int c = lane; c < ww; c += 64) {
-        for (int r0 = 0; r0 < wh; r0 += 8) {  // 8 independent loads in flight per lane
-            uint8_t v[8];
+    // window rows as aligned dwords into an LDS image whose rows start `shift` bytes in (the level's
+    // 19-px frame keeps the over-read inside the plane); row stride ws = roundup(shift + ww, 4)
+    const int shift = (int)((uintptr_t)src & 3);
+    const int ws = (shift + ww + 3) & ~3, nwr = ws >> 2;
+    const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(src - shift);
+    uint32_t* win32 = reinterpret_cast<uint32_t*>(win);
+    uint32_t* sc32 = reinterpret_cast<uint32_t*>(sc);
+    // lanes = 4 rows x 16 dwords (a second column pass only for windows wider than 16 dwords)
+    const int lr = lane >> 4, lw = lane & 15;
+    for (int w0 = 0; w0 < nwr; w0 += 16) {
+        const int w = w0 + lw;
+        for (int r0 = 0; r0 < wh; r0 += 16) {
+            uint32_t v[4];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = r0 + k < wh ? src[(size_t)(r0 + k) * L.pitch + c] : 0;
+            for (int k = 0; k < 4; ++k) {
+                const int r = r0 + 4 * k + lr;
+                v[k] = (r < wh && w < nwr) ? wsrc[(size_t)r * (L.pitch >> 2) + w] : 0u;
+            }
 #pragma unroll
-            for (int k = 0; k < 8; ++k)
-                if (r0 + k < wh) win[(r0 + k) * ww + c] = v[k];
+            for (int k = 0; k < 4; ++k) {
+                const int r = r0 + 4 * k + lr;
+                if (r < wh && w < nwr) { win32[r * nwr + w] = v[k]; sc32[r * nwr + w] = 0u; }
+            }
         }
     }
     wave_sync();
+    win += shift;  // window pixel (r, c) is at win[r * ws + c]; same layout for the score map
+    sc += shift;
     const int dw = ww - 6, dh = wh - 6;
     const int nd = (dw > 0 && dh > 0) ? dw * dh : 0;
     int off[16];
@@ -385,7 +401,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
         const int cx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
         const int cy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
 #pragma unroll
-        for (int k = 0; k < 16; ++k) off[k] = cx[k] + cy[k] * ww;
+        for (int k = 0; k < 16; ++k) off[k] = cx[k] + cy[k] * ws;
     }
     const int ini = g.ini_th, mint = g.min_th;
     // 1a. compass filter at minTh: a 9-pixel arc always contains two circle pixels 4 apart among
@@ -399,7 +415,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
             bool pass = false;
             int idx = 0;
             if (i0 + lane < nd) {
-                idx = (r + 3) * ww + (c + 3);
+                idx = (r + 3) * ws + (c + 3);
                 const uint8_t* q = win + idx;
                 const int v = q[0], hi = v + mint, lo = v - mint;
                 const int p0 = q[off[0]], p4 = q[off[4]], p8 = q[off[8]], p12 = q[off[12]];
@@ -441,7 +457,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
     bool any = false;
     for (int j = lane; j < ncand; j += 64) {
         const int idx = cl[j], s = sc[idx];
-        any |= (s >= ini) && is_local_max(sc, ww, idx, s);
+        any |= (s >= ini) && is_local_max(sc, ws, idx, s);
     }
     const int t = ballot(any) ? ini : mint;
     // 4. emission in row-major order (the candidate list is row-major)
@@ -454,12 +470,12 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
         if (j < ncand) {
             idx = cl[j];
             s = sc[idx];
-            keep = (s >= t) && is_local_max(sc, ww, idx, s);
+            keep = (s >= t) && is_local_max(sc, ws, idx, s);
         }
         const unsigned long long m = ballot(keep);
         if (keep) {
             const int pos = count + rank_in(m);
-            const int r = idx / ww, c = idx - (idx / ww) * ww;
+            const int r = idx / ws, c = idx - (idx / ws) * ws;
             if (pos < C.cap) out[pos] = pack_key(C.off_x + c, C.off_y + r, s);
         }
         count += __popcll(m);
@@ -1172,9 +1188,13 @@ __device__ __forceinline__ void steer_sincos(float ang, float* s, float* c) {
     }
 }
 
-// Two keypoints per wave (one per 32-lane half): lane u = -15..15 of the IC_Angle disc columns,
-// then 8 of the 256 BRIEF tests per lane; every lane's loads are independent and issued together.
+// One keypoint per 32-lane half-wave, 8 per block.  The keypoint's 37x37 blurred patch (rBRIEF reaches
+// round(13*sqrt(2)) = 18 px) and 31x31 unblurred disc box are staged in LDS with one round of dword
+// loads, so the dependent memory phases are: key -> patches -> stores.
 constexpr int kDescKpPerBlock = 8;
+constexpr int kPB = 37, kPBW = 10;  // blurred patch rows, dwords per row
+constexpr int kPU = 31, kPUW = 9;   // disc box rows, dwords per row
+constexpr int kDescLds = kPB * kPBW * 4 + kPU * kPUW * 4;  // 2596 bytes per keypoint
 
 __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__ gp, const uint8_t* __restrict__ pyr,
                                                   const uint8_t* __restrict__ blur, const uint32_t* __restrict__ sel,
@@ -1182,6 +1202,7 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
                                                   const int32_t* __restrict__ dst_index, const int32_t* __restrict__ counts,
                                                   int cap, orb_keypoint_t* __restrict__ kps, uint8_t* __restrict__ desc) {
     const KernelGeom& g = *gp;
+    __shared__ __attribute__((aligned(16))) uint32_t patch[kDescKpPerBlock][(kDescLds + 15) / 16 * 4];
     const int half = threadIdx.x >> 5, hl = threadIdx.x & 31;
     const int slot = blockIdx.x * kDescKpPerBlock + half, level = blockIdx.y, f = blockIdx.z;
     const int n = sel_count[(size_t)f * g.nlevels + level];
@@ -1190,21 +1211,51 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
     const LevelGeom& L = g.lv[level];
     const uint32_t key = active ? sel[(size_t)f * g.sel_frame_cap + L.sel_off + slot] : 0;
     const int x = key_x(key) + L.minB, y = key_y(key) + L.minB;
-    // ---- IC_Angle on the unblurred level (src:91-138)
-    const uint8_t* center = pyr + (size_t)f * g.pyr_frame_bytes + L.plane_off + (size_t)(y + kEdge) * L.pitch + (x + kEdge);
+    const size_t cofs = (size_t)f * g.pyr_frame_bytes + L.plane_off + (size_t)(y + kEdge) * L.pitch + (x + kEdge);
+    // ---- stage both patches (over-reads stay inside the padded planes)
+    const uint8_t* b0 = blur + cofs - (size_t)18 * L.pitch - 18;
+    const uint8_t* u0 = pyr + cofs - (size_t)kHalfPatch * L.pitch - kHalfPatch;
+    const int bsh = (int)((uintptr_t)b0 & 3), ush = (int)((uintptr_t)u0 & 3);
+    const uint32_t* bw = reinterpret_cast<const uint32_t*>(b0 - bsh);
+    const uint32_t* uw = reinterpret_cast<const uint32_t*>(u0 - ush);
+    const int pw = L.pitch >> 2;
+    uint32_t* P = patch[half];
+    uint32_t vb[(kPB * kPBW + 31) / 32], vu[(kPU * kPUW + 31) / 32];
+    if (active) {
+#pragma unroll
+        for (int k = 0; k < (kPB * kPBW + 31) / 32; ++k) {
+            const int i = 32 * k + hl;
+            vb[k] = i < kPB * kPBW ? bw[(size_t)(i / kPBW) * pw + i % kPBW] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < (kPU * kPUW + 31) / 32; ++k) {
+            const int i = 32 * k + hl;
+            vu[k] = i < kPU * kPUW ? uw[(size_t)(i / kPUW) * pw + i % kPUW] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < (kPB * kPBW + 31) / 32; ++k) {
+            const int i = 32 * k + hl;
+            if (i < kPB * kPBW) P[i] = vb[k];
+        }
+#pragma unroll
+        for (int k = 0; k < (kPU * kPUW + 31) / 32; ++k) {
+            const int i = 32 * k + hl;
+            if (i < kPU * kPUW) P[kPB * kPBW + i] = vu[k];
+        }
+    }
+    __syncthreads();
+    const uint8_t* PB = reinterpret_cast<const uint8_t*>(P) + bsh + 18 * (kPBW * 4) + 18;  // blurred centre
+    const uint8_t* PU = reinterpret_cast<const uint8_t*>(P + kPB * kPBW) + ush + kHalfPatch * (kPUW * 4) + kHalfPatch;
+    // ---- IC_Angle on the unblurred level (src:91-138): lane = disc column u
     const int u = hl - kHalfPatch;
     int m10 = 0, m01 = 0;
     if (active && hl < 2 * kHalfPatch + 1) {
-        int val[2 * kHalfPatch + 1];
 #pragma unroll
         for (int v = -kHalfPatch; v <= kHalfPatch; ++v) {
             const int d = g.umax[v < 0 ? -v : v];
-            val[v + kHalfPatch] = (u >= -d && u <= d) ? center[u + v * L.pitch] : 0;
-        }
-#pragma unroll
-        for (int v = -kHalfPatch; v <= kHalfPatch; ++v) {
-            m10 += u * val[v + kHalfPatch];
-            m01 += v * val[v + kHalfPatch];
+            const int val = (u >= -d && u <= d) ? PU[v * (kPUW * 4) + u] : 0;
+            m10 += u * val;
+            m01 += v * val;
         }
     }
 #pragma unroll
@@ -1217,7 +1268,6 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
     const float ang = angle * (float)(3.14159265358979323846 / 180.f);
     float a, b;
     steer_sincos(ang, &b, &a);  // a = cos, b = sin
-    const uint8_t* bc = blur + (size_t)f * g.pyr_frame_bytes + L.plane_off + (size_t)(y + kEdge) * L.pitch + (x + kEdge);
     int t0[8], t1[8];
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
@@ -1228,8 +1278,8 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
         const int c0 = (int)__builtin_rintf(__builtin_fmaf(px0, a, -(py0 * b)));
         const int r1 = (int)__builtin_rintf(__builtin_fmaf(px1, b, py1 * a));
         const int c1 = (int)__builtin_rintf(__builtin_fmaf(px1, a, -(py1 * b)));
-        t0[m] = active ? bc[r0 * L.pitch + c0] : 0;
-        t1[m] = active ? bc[r1 * L.pitch + c1] : 0;
+        t0[m] = PB[r0 * (kPBW * 4) + c0];
+        t1[m] = PB[r1 * (kPBW * 4) + c1];
     }
     uint32_t words[8];
 #pragma unroll

@@ -207,7 +207,7 @@ inline bool build_geometry(const Params& P, int width, int height, Geometry& g) 
                 c.cap = ((dw + 1) / 2) * ((dh + 1) / 2);
                 c.slot = level_cap;
                 level_cap += c.cap;
-                g.max_win = std::max(g.max_win, (int)c.win_w * c.win_h);
+                g.max_win = std::max(g.max_win, ((int)c.win_w + 6) * c.win_h);  // dword-aligned rows
                 g.cells.push_back(c);
             }
         }
