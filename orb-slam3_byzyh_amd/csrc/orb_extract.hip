@@ -5,8 +5,8 @@
 //                    REFLECT_101 frame) + its 7x7 sigma-2 Gaussian (for rBRIEF), one LDS tile pass
 //   k_fast_cells     one wave per (frame, FAST cell): threshold-independent FAST-9 score, 3x3 NMS
 //                    inside the cell window, iniTh/minTh choice, row-major candidate emission
-//   k_quadtree       one wave per (frame, level): DistributeOctTree, exact list/sort semantics
-//   k_place          one wave per frame: level-0 scaling and vLappingArea output placement
+//   k_quadtree       one wave per (frame, level): DistributeOctTree, exact list/sort semantics, plus the
+//                    keypoint's vLappingArea class rank (level-0 scaling, src:1656-1676)
 //   k_describe       one wave per keypoint: IC_Angle (31-px disc) + steered rBRIEF (256 tests)
 //
 // No MFMA anywhere: this is byte / integer / popcount work.  All float arithmetic that reaches an
@@ -843,13 +843,30 @@ __device__ void qt_sort(QTree& t, const QGen& A, int n, int lane) {
     wave_sync();
 }
 
+constexpr int kQtStamps = 12;
+
+struct QPlace {  // vLappingArea classification of the selected keys
+    int level, minB, lap0, lap1;
+    float scale;
+    int32_t* rank_out;
+    int32_t* n_lap;
+};
+
 template <bool kKeysInLds>
 __device__ void qt_run(QTree& t, int K, int N, int nroots, float root_w, int span_y,
                        const uint32_t* __restrict__ cand_level, const CellDesc* __restrict__ cells, int cell_begin,
                        int cell_count, const int32_t* __restrict__ ccount, uint32_t* __restrict__ sel_out,
-                       int sel_cap, int* n_sel, int* status, int debug_flags) {
+                       int sel_cap, int* n_sel, int* status, int debug_flags, unsigned long long* stamps,
+                       const QPlace& place) {
     const int lane = lane_id();
     bool overflow = false;
+    // diagnostic phase timers (debug_flags & 4): gather, reg count, reg scan+write, reg partition, sort,
+    // careful count, careful scan+write, careful partition, final, #regular passes, #careful rounds, K
+    unsigned long long tm[kQtStamps] = {};
+    unsigned long long t_last = (debug_flags & 4) ? __builtin_amdgcn_s_memtime() : 0;
+    auto stamp = [&](int i) {
+        if (debug_flags & 4) { const unsigned long long now = __builtin_amdgcn_s_memtime(); tm[i] += now - t_last; t_last = now; }
+    };
     // ---- gather candidates in cell order into keys[1], counting per root (src:756-764).
     // One lane per cell (cells in chunks of 64); destinations from a wave scan of the cell counts.
     int rcount[kMaxRoots];
@@ -901,6 +918,7 @@ __device__ void qt_run(QTree& t, int K, int N, int nroots, float root_w, int spa
             }
         }
     }
+    stamp(0);
     // ---- roots (src:733-786): empty roots erased, single-key roots are leaves
     QGen A = t.g0, B = t.g1;  // current / next generation, swapped after every pass
     int nlist = 0;
@@ -928,6 +946,7 @@ __device__ void qt_run(QTree& t, int K, int N, int nroots, float root_w, int spa
         // ---------------- regular pass (src:802-918)
         const int prev_size = nlist;
         qt_count_children(t, A, nullptr, nlist, lane);
+        stamp(1);
         int total_children = 0, total_surv = 0;
         for (int b = 0; b < nlist; b += 64) {
             const int i = b + lane;
@@ -975,10 +994,13 @@ __device__ void qt_run(QTree& t, int K, int N, int nroots, float root_w, int spa
             carry_p += __shfl(ip, 63, 64);
         }
         nsplit = carry_p;
+        stamp(2);
         qt_partition(t, A, nullptr, nlist, lane);
         { const QGen tmp = A; A = B; B = tmp; }
         nlist = new_size;
         const int to_expand = nsplit;
+        stamp(3);
+        tm[9]++;
         if (nlist >= N || nlist == prev_size) {
             done = true;
         } else if (nlist + to_expand * 3 > N) {
@@ -1003,7 +1025,10 @@ __device__ void qt_run(QTree& t, int K, int N, int nroots, float root_w, int spa
                 } else {
                     qt_sort(t, A2, np, lane);
                 }
+                stamp(4);
+                tm[10]++;
                 qt_count_children(t, A2, t.prev, np, lane);
+                stamp(5);
                 // division order o = 0.. is prev[np-1-o]; stop once the list reaches N (src:1006)
                 int ndiv = np, carry = 0;
                 for (int b = 0; b < np; b += 64) {
@@ -1073,10 +1098,12 @@ __device__ void qt_run(QTree& t, int K, int N, int nroots, float root_w, int spa
                     if (keep) qt_copy_node(A2, B2, i, total_children + carry_k + rank_in(m));
                     carry_k += __popcll(m);
                 }
+                stamp(6);
                 // key partition of the divided nodes (prev[np-ndiv .. np-1])
                 qt_partition(t, A2, t.prev + (np - ndiv), ndiv, lane);
                 { const QGen tmp = A; A = B; B = tmp; }
                 nlist = new_size;
+                stamp(7);
                 if (nlist >= N || nlist == round_prev) done = true;
             }
         }
@@ -1085,23 +1112,44 @@ __device__ void qt_run(QTree& t, int K, int N, int nroots, float root_w, int spa
         if (lane == 0) { *n_sel = 0; atomicMax(status, 1); }
         return;
     }
-    // ---- keep the first max-response key of every node, in list order (src:1028-1053)
+    // ---- keep the first max-response key of every node, in list order (src:1028-1053), and rank it
+    // within its vLappingArea class (src:1656-1676): rank_out = rank among non-lapping keys, or
+    // -(1 + rank among lapping keys); k_describe turns that into the output slot
     const QGen& F = A;
-    for (int i = lane; i < nlist; i += 64) {
-        const uint32_t* kk = key_buf(t, F.kb[i]) + F.ks[i];
-        const int n = F.kn[i];
-        uint32_t best = kk[0];
-        for (int q = 1; q < n; ++q)
-            if (key_score(kk[q]) > key_score(best)) best = kk[q];
-        sel_out[i] = best;
+    int carry_lap = 0, carry_mono = 0;
+    for (int b = 0; b < nlist; b += 64) {
+        const int i = b + lane;
+        bool lap = false;
+        if (i < nlist) {
+            const uint32_t* kk = key_buf(t, F.kb[i]) + F.ks[i];
+            const int n = F.kn[i];
+            uint32_t best = kk[0];
+            for (int q = 1; q < n; ++q)
+                if (key_score(kk[q]) > key_score(best)) best = kk[q];
+            sel_out[i] = best;
+            float x = (float)(key_x(best) + place.minB);
+            if (place.level != 0) x = x * place.scale;
+            lap = x >= (float)place.lap0 && x <= (float)place.lap1;
+        }
+        const unsigned long long ml = ballot(i < nlist && lap), mm = ballot(i < nlist && !lap);
+        if (i < nlist) place.rank_out[i] = lap ? -(1 + carry_lap + rank_in(ml)) : carry_mono + rank_in(mm);
+        carry_lap += __popcll(ml);
+        carry_mono += __popcll(mm);
     }
-    if (lane == 0) *n_sel = nlist;
+    if (lane == 0) { *n_sel = nlist; *place.n_lap = carry_lap; }
+    stamp(8);
+    if ((debug_flags & 4) && stamps && lane == 0) {
+        tm[11] = (unsigned long long)K;
+        for (int i = 0; i < kQtStamps; ++i) stamps[i] = tm[i];
+    }
 }
 
 __global__ __launch_bounds__(64) void k_quadtree(const KernelGeom* __restrict__ gp, const CellDesc* __restrict__ cells,
                                                  const uint32_t* __restrict__ cand, const int32_t* __restrict__ cell_count,
                                                  uint32_t* __restrict__ key_scratch, uint32_t* __restrict__ sel,
-                                                 int32_t* __restrict__ sel_count, int lds_bytes, int* __restrict__ status) {
+                                                 int32_t* __restrict__ sel_count, int lds_bytes, int* __restrict__ status,
+                                                 unsigned long long* __restrict__ stamps, int lap0, int lap1,
+                                                 int32_t* __restrict__ rank_out, int32_t* __restrict__ lap_count) {
     const KernelGeom& g = *gp;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int level = blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
@@ -1118,6 +1166,8 @@ __global__ __launch_bounds__(64) void k_quadtree(const KernelGeom* __restrict__ 
     uint32_t* sel_out = sel + (size_t)f * g.sel_frame_cap + L.sel_off;
     int32_t* n_sel = sel_count + (size_t)f * g.nlevels + level;
     const uint32_t* cand_level = cand + (size_t)f * g.cand_frame_cap + L.cand_off;
+    QPlace place{level, L.minB, lap0, lap1, L.scale, rank_out + (size_t)f * g.sel_frame_cap + L.sel_off,
+                 lap_count + (size_t)f * g.nlevels + level};
     if (meta > (size_t)lds_bytes) {
         if (lane == 0) { *n_sel = 0; atomicMax(status, 2); }
         return;
@@ -1127,49 +1177,15 @@ __global__ __launch_bounds__(64) void k_quadtree(const KernelGeom* __restrict__ 
         t.keys0 = (uint32_t*)(smem + meta);
         t.keys1 = t.keys0 + K;
         qt_run<true>(t, K, N, L.n_roots, L.root_w, L.maxBY - L.minB, cand_level, cells, L.cell_begin,
-                     L.cell_count, cc, sel_out, L.sel_cap, n_sel, status, g.debug_flags);
+                     L.cell_count, cc, sel_out, L.sel_cap, n_sel, status, g.debug_flags,
+                     stamps ? stamps + ((size_t)f * g.nlevels + level) * kQtStamps : nullptr, place);
     } else {
         uint32_t* scratch = key_scratch + ((size_t)f * g.cand_frame_cap + L.cand_off) * 2;
         t.keys0 = scratch;
         t.keys1 = scratch + L.cand_cap;
         qt_run<false>(t, K, N, L.n_roots, L.root_w, L.maxBY - L.minB, cand_level, cells, L.cell_begin,
-                      L.cell_count, cc, sel_out, L.sel_cap, n_sel, status, g.debug_flags);
-    }
-}
-
-// ================================================================================================
-// 4. output placement by vLappingArea, src:1613-1681
-// ================================================================================================
-__global__ __launch_bounds__(64) void k_place(const KernelGeom* __restrict__ gp, const uint32_t* __restrict__ sel,
-                                              const int32_t* __restrict__ sel_count, int32_t* __restrict__ dst_index,
-                                              int lap0, int lap1, int cap, int32_t* __restrict__ counts) {
-    const KernelGeom& g = *gp;
-    const int f = blockIdx.x, lane = threadIdx.x;
-    const int my_count = lane < g.nlevels ? sel_count[(size_t)f * g.nlevels + lane] : 0;
-    const int total = wave_sum(my_count);
-    int mono = 0, stereo = 0;
-    for (int l = 0; l < g.nlevels; ++l) {
-        const LevelGeom& L = g.lv[l];
-        const int n = __shfl(my_count, l, 64);
-        const uint32_t* s = sel + (size_t)f * g.sel_frame_cap + L.sel_off;
-        int32_t* d = dst_index + (size_t)f * g.sel_frame_cap + L.sel_off;
-        for (int b = 0; b < n; b += 64) {
-            const int i = b + lane;
-            bool valid = i < n, lap = false;
-            if (valid) {
-                float x = (float)(key_x(s[i]) + L.minB);
-                if (l != 0) x = x * L.scale;
-                lap = x >= (float)lap0 && x <= (float)lap1;
-            }
-            const unsigned long long ml = ballot(valid && lap), mm = ballot(valid && !lap);
-            if (valid) d[i] = lap ? total - 1 - (stereo + rank_in(ml)) : mono + rank_in(mm);
-            stereo += __popcll(ml);
-            mono += __popcll(mm);
-        }
-    }
-    if (lane == 0) {
-        counts[2 * f] = total;
-        counts[2 * f + 1] = total > cap ? ORB_ERR_CAPACITY : mono;
+                      L.cell_count, cc, sel_out, L.sel_cap, n_sel, status, g.debug_flags,
+                     stamps ? stamps + ((size_t)f * g.nlevels + level) * kQtStamps : nullptr, place);
     }
 }
 
@@ -1199,15 +1215,34 @@ constexpr int kDescLds = kPB * kPBW * 4 + kPU * kPUW * 4;  // 2596 bytes per key
 __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__ gp, const uint8_t* __restrict__ pyr,
                                                   const uint8_t* __restrict__ blur, const uint32_t* __restrict__ sel,
                                                   const int32_t* __restrict__ sel_count,
-                                                  const int32_t* __restrict__ dst_index, const int32_t* __restrict__ counts,
-                                                  int cap, orb_keypoint_t* __restrict__ kps, uint8_t* __restrict__ desc) {
+                                                  const int32_t* __restrict__ rank_in_class, const int32_t* __restrict__ lap_count,
+                                                  int cap, orb_keypoint_t* __restrict__ kps, uint8_t* __restrict__ desc,
+                                                  int32_t* __restrict__ counts) {
     const KernelGeom& g = *gp;
     __shared__ __attribute__((aligned(16))) uint32_t patch[kDescKpPerBlock][(kDescLds + 15) / 16 * 4];
     const int half = threadIdx.x >> 5, hl = threadIdx.x & 31;
     const int slot = blockIdx.x * kDescKpPerBlock + half, level = blockIdx.y, f = blockIdx.z;
-    const int n = sel_count[(size_t)f * g.nlevels + level];
+    // per-frame totals over the levels (src:1586-1591) and this level's class bases (src:1613-1676)
+    const int li = hl & 15;
+    const int cnt_l = li < g.nlevels ? sel_count[(size_t)f * g.nlevels + li] : 0;
+    const int lap_l = li < g.nlevels ? lap_count[(size_t)f * g.nlevels + li] : 0;
+    int total = cnt_l, lap_before = li < level ? lap_l : 0, mono_before = li < level ? cnt_l - lap_l : 0;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {  // within each 16-lane group
+        total += __shfl_xor(total, o, 64);
+        lap_before += __shfl_xor(lap_before, o, 64);
+        mono_before += __shfl_xor(mono_before, o, 64);
+    }
+    const int n = __shfl(cnt_l, (threadIdx.x & ~15) + level, 64);
+    if (blockIdx.x == 0 && level == 0 && threadIdx.x == 0) {
+        int mono = 0;
+        for (int l = 0; l < g.nlevels; ++l)
+            mono += sel_count[(size_t)f * g.nlevels + l] - lap_count[(size_t)f * g.nlevels + l];
+        counts[2 * f] = total;
+        counts[2 * f + 1] = total > cap ? ORB_ERR_CAPACITY : mono;
+    }
     if (blockIdx.x * kDescKpPerBlock >= n) return;           // whole block idle
-    const bool active = slot < n && counts[2 * f + 1] >= 0;  // frame within the caller's capacity
+    const bool active = slot < n && total <= cap;            // frame within the caller's capacity
     const LevelGeom& L = g.lv[level];
     const uint32_t key = active ? sel[(size_t)f * g.sel_frame_cap + L.sel_off + slot] : 0;
     const int x = key_x(key) + L.minB, y = key_y(key) + L.minB;
@@ -1285,7 +1320,8 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
 #pragma unroll
     for (int m = 0; m < 8; ++m) words[m] = (uint32_t)(ballot(t0[m] < t1[m]) >> (32 * (half & 1)));
     if (!active) return;
-    const int dst = dst_index[(size_t)f * g.sel_frame_cap + L.sel_off + slot];
+    const int rk = rank_in_class[(size_t)f * g.sel_frame_cap + L.sel_off + slot];
+    const int dst = rk < 0 ? total - 1 - (lap_before + (-rk - 1)) : mono_before + rk;
     if (hl < 8) {
         uint32_t w = words[0];
 #pragma unroll
@@ -1332,6 +1368,7 @@ struct Extractor {
     uint32_t* d_sel = nullptr; size_t sel_cap = 0;
     int32_t* d_dst = nullptr; size_t dst_cap = 0;
     int32_t* d_sel_count = nullptr; size_t selcount_cap = 0;
+    int32_t* d_lap_count = nullptr; size_t lapcount_cap = 0;
     int* d_status = nullptr;
     // synchronous path staging
     uint8_t* d_img = nullptr; size_t img_cap = 0;
@@ -1350,6 +1387,8 @@ struct Extractor {
     std::vector<hipEvent_t> events;   // kStages + 1 per profiled sub-batch launch
     int ev_used = 0;                  // launches recorded since the last read
     long long frames_profiled = 0;
+    unsigned long long* d_stamps = nullptr;  // quad-tree phase timers (ORBGPU_DEBUG_FLAGS & 4)
+    size_t stamps_cap = 0;
 };
 
 }  // namespace orbgpu
@@ -1412,6 +1451,8 @@ int prepare(Extractor* e, int w, int h, int n) {
     if ((rc = grow(e->d_sel, e->sel_cap, (size_t)k.sel_frame_cap * n)) != ORB_OK) return rc;
     if ((rc = grow(e->d_dst, e->dst_cap, (size_t)k.sel_frame_cap * n)) != ORB_OK) return rc;
     if ((rc = grow(e->d_sel_count, e->selcount_cap, (size_t)k.nlevels * n)) != ORB_OK) return rc;
+    if ((rc = grow(e->d_lap_count, e->lapcount_cap, (size_t)k.nlevels * n)) != ORB_OK) return rc;
+    if ((k.debug_flags & 4) && (rc = grow(e->d_stamps, e->stamps_cap, (size_t)k.nlevels * n * kQtStamps)) != ORB_OK) return rc;
     return ORB_OK;
 }
 
@@ -1442,6 +1483,7 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     uint32_t* sel = e->d_sel + (size_t)f0 * k.sel_frame_cap;
     int32_t* dst = e->d_dst + (size_t)f0 * k.sel_frame_cap;
     int32_t* scount = e->d_sel_count + (size_t)f0 * k.nlevels;
+    int32_t* lapc = e->d_lap_count + (size_t)f0 * k.nlevels;
     const uint8_t* imgs = d_images + (size_t)f0 * frame_stride;
     orb_keypoint_t* kps = d_kps + (size_t)f0 * cap;
     uint8_t* desc = d_desc + (size_t)f0 * cap * 32;
@@ -1463,12 +1505,12 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
                        win_cap, pyr, cand, ccount, cthr);
     mark(2);
     hipLaunchKernelGGL(k_quadtree, dim3(k.nlevels, n), dim3(64), e->qt_lds, st, e->d_geom, e->d_cells, cand, ccount,
-                       scratch, sel, scount, e->qt_lds, e->d_status);
+                       scratch, sel, scount, e->qt_lds, e->d_status,
+                       e->d_stamps ? e->d_stamps + (size_t)f0 * k.nlevels * kQtStamps : nullptr, lap0, lap1, dst, lapc);
     mark(3);
-    hipLaunchKernelGGL(k_place, dim3(n), dim3(64), 0, st, e->d_geom, sel, scount, dst, lap0, lap1, cap, counts);
     mark(4);
     hipLaunchKernelGGL(k_describe, dim3((G.max_sel + kDescKpPerBlock - 1) / kDescKpPerBlock, k.nlevels, n), dim3(256), 0,
-                       st, e->d_geom, pyr, blr, sel, scount, dst, counts, cap, kps, desc);
+                       st, e->d_geom, pyr, blr, sel, scount, dst, lapc, cap, kps, desc, counts);
     mark(5);
     if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "kernel launch failed");
     return ORB_OK;
@@ -1546,8 +1588,8 @@ int orb_extractor_destroy(orb_extractor_t h) {
     Extractor* e = reinterpret_cast<Extractor*>(h);
     if (!e) return ORB_ERR_ARG;
     if (e->stream) hipStreamSynchronize(e->stream);
-    void* bufs[] = {e->d_geom, e->d_cells, e->d_xtab, e->d_ytab, e->d_pyr, e->d_blur, e->d_cand, e->d_scratch,
-                    e->d_cell_count, e->d_cell_thr, e->d_sel, e->d_dst, e->d_sel_count, e->d_status,
+    void* bufs[] = {e->d_stamps, e->d_geom, e->d_cells, e->d_xtab, e->d_ytab, e->d_pyr, e->d_blur, e->d_cand, e->d_scratch,
+                    e->d_cell_count, e->d_cell_thr, e->d_sel, e->d_dst, e->d_sel_count, e->d_lap_count, e->d_status,
                     e->d_img, e->d_kps, e->d_desc, e->d_counts};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -1748,6 +1790,15 @@ int orb_extractor_stage_ms(orb_extractor_t h, float* ms, int* launches, long lon
     if (launches) *launches = (int)e->batches;  // batch calls (each may be several sub-batch launches)
     if (frames) *frames = e->frames_profiled;
     return ORB_OK;
+}
+
+int orb_debug_qt_stamps(orb_extractor_t h, unsigned long long* out, int n) {
+    Extractor* e = reinterpret_cast<Extractor*>(h);
+    if (!e || !e->d_stamps) return ORB_ERR_ARG;
+    hipDeviceSynchronize();
+    const int m = std::min<int>(n, (int)e->stamps_cap);
+    hipMemcpy(out, e->d_stamps, sizeof(unsigned long long) * m, hipMemcpyDeviceToHost);
+    return m;
 }
 
 int orb_debug_status(orb_extractor_t h) {
