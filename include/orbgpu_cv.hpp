@@ -1,0 +1,118 @@
+/*
+ * orbgpu_cv.hpp -- header-only C++ drop-in for ORB_SLAM3::ORBextractor on top of the C ABI
+ * (orbgpu.h).  Same public interface as the reference class (include/ORBextractor.h:43-109):
+ * constructor (nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST), operator()(image, mask,
+ * keypoints, descriptors, vLappingArea) returning monoIndex, the scale getters and the public
+ * mvImagePyramid.  Include it instead of ORBextractor.h and alias the type:
+ *
+ *     #include "orbgpu_cv.hpp"
+ *     namespace ORB_SLAM3 { using ORBextractor = orbgpu::ORBextractor; }
+ *
+ * Needs OpenCV (core) and liborbgpu.so at link time.  mvImagePyramid is filled on demand
+ * (SyncPyramid()) because only Frame::ComputeStereoMatches reads it (src/Frame.cc:1126,1249);
+ * the levels are views into padded planes, like the reference's (src/ORBextractor.cc:1695-1697),
+ * so the 19-pixel border stays readable.
+ */
+#ifndef ORBGPU_CV_HPP
+#define ORBGPU_CV_HPP
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include <opencv2/core/core.hpp>
+
+#include "orbgpu.h"
+
+namespace orbgpu {
+
+class ORBextractor {
+public:
+    enum { HARRIS_SCORE = 0, FAST_SCORE = 1 };
+
+    ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST,
+                 int maxWidth = 1280, int maxHeight = 720)
+        : nfeatures_(nfeatures), scaleFactor_(scaleFactor), nlevels_(nlevels) {
+        orb_params_t p{nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST};
+        if (orb_extractor_create(&p, maxWidth, maxHeight, 1, &h_) != ORB_OK)
+            throw std::runtime_error(std::string("orb_extractor_create: ") + orb_last_error());
+        mvScaleFactor_.resize(nlevels);
+        mvInvScaleFactor_.resize(nlevels);
+        mvLevelSigma2_.resize(nlevels);
+        mvInvLevelSigma2_.resize(nlevels);
+        std::vector<int32_t> per(nlevels);
+        orb_extractor_scales(h_, mvScaleFactor_.data(), mvInvScaleFactor_.data(), mvLevelSigma2_.data(),
+                             mvInvLevelSigma2_.data(), per.data());
+        mvImagePyramid.resize(nlevels);
+    }
+    ~ORBextractor() { orb_extractor_destroy(h_); }
+    ORBextractor(const ORBextractor&) = delete;
+    ORBextractor& operator=(const ORBextractor&) = delete;
+
+    // src/ORBextractor.cc:1557-1682.  Returns monoIndex, or -1 for an empty image.
+    int operator()(cv::InputArray _image, cv::InputArray /*_mask (ignored upstream)*/,
+                   std::vector<cv::KeyPoint>& _keypoints, cv::OutputArray _descriptors,
+                   std::vector<int>& vLappingArea) {
+        if (_image.empty()) return -1;
+        cv::Mat image = _image.getMat();
+        CV_Assert(image.type() == CV_8UC1);
+        int cap = 2 * nfeatures_ + 64 * nlevels_;
+        for (int attempt = 0; attempt < 2; ++attempt) {
+            kps_.resize(cap);
+            desc_.create(cap, 32, CV_8U);
+            int n = 0;
+            int rc = orb_extract(h_, image.data, image.cols, image.rows, (int)image.step, vLappingArea[0],
+                                 vLappingArea[1], kps_.data(), desc_.data, cap, &n);
+            if (rc == ORB_ERR_CAPACITY) { cap = n; continue; }
+            if (rc < 0) throw std::runtime_error(std::string("orb_extract: ") + orb_last_error());
+            _keypoints.resize(n);
+            for (int i = 0; i < n; ++i) {
+                const orb_keypoint_t& k = kps_[i];
+                _keypoints[i] = cv::KeyPoint(k.x, k.y, k.size, k.angle, k.response, k.octave, k.class_id);
+            }
+            if (n == 0) _descriptors.release();
+            else desc_.rowRange(0, n).copyTo(_descriptors);
+            pyramidStale_ = true;
+            return rc;
+        }
+        throw std::runtime_error("orb_extract: capacity retry failed");
+    }
+
+    int inline GetLevels() { return nlevels_; }
+    float inline GetScaleFactor() { return (float)scaleFactor_; }
+    std::vector<float> inline GetScaleFactors() { return mvScaleFactor_; }
+    std::vector<float> inline GetInverseScaleFactors() { return mvInvScaleFactor_; }
+    std::vector<float> inline GetScaleSigmaSquares() { return mvLevelSigma2_; }
+    std::vector<float> inline GetInverseScaleSigmaSquares() { return mvInvLevelSigma2_; }
+
+    // Download the pyramid of the last frame into mvImagePyramid (call before reading it).
+    void SyncPyramid() {
+        if (!pyramidStale_) return;
+        for (int l = 0; l < nlevels_; ++l) {
+            int w = 0, h = 0, pitch = 0;
+            if (orb_extractor_level(h_, 0, l, nullptr, &w, &h, &pitch) != ORB_OK)
+                throw std::runtime_error(std::string("orb_extractor_level: ") + orb_last_error());
+            padded_[l].create(h + 38, w + 38, CV_8U);
+            orb_extractor_level_download(h_, 0, l, padded_[l].data);
+            mvImagePyramid[l] = padded_[l](cv::Rect(19, 19, w, h));
+        }
+        pyramidStale_ = false;
+    }
+
+    std::vector<cv::Mat> mvImagePyramid;
+
+private:
+    orb_extractor_t h_ = nullptr;
+    int nfeatures_;
+    double scaleFactor_;
+    int nlevels_;
+    bool pyramidStale_ = true;
+    std::vector<orb_keypoint_t> kps_;
+    cv::Mat desc_;
+    cv::Mat padded_[12];
+    std::vector<float> mvScaleFactor_, mvInvScaleFactor_, mvLevelSigma2_, mvInvLevelSigma2_;
+};
+
+}  // namespace orbgpu
+
+#endif  // ORBGPU_CV_HPP
