@@ -110,6 +110,57 @@ int orb_hamming_knn2_device(const uint8_t* d_query, int n_query, const uint8_t* 
                             int32_t* d_best_idx, int32_t* d_best_dist, int32_t* d_second_dist,
                             void* stream);
 
+/* ---- ORBmatcher::SearchForTriangulation (src/ORBmatcher.cc:1046-1324) ------------------------- */
+
+/* Flat view of the KeyFrame fields SearchForTriangulation reads (host memory).  Pinhole camera,
+ * no second camera (mpCamera2 == NULL, NLeft == -1): the configuration LocalMapping runs for
+ * monocular / stereo / RGB-D pinhole rigs. */
+typedef struct orb_kf_view {
+    int32_t n;                     /* KeyFrame::N */
+    const orb_keypoint_t* kps_un;  /* mvKeysUn (n) */
+    const uint8_t* desc;           /* mDescriptors, n x 32 bytes, row-major */
+    const float* u_right;          /* mvuRight (n); NULL = monocular (every entry -1) */
+    const uint8_t* has_mappoint;   /* n flags, 1 = GetMapPoint(i) != NULL; NULL = no map points */
+    int32_t n_nodes;               /* mFeatVec.size() (DBoW2::FeatureVector, a std::map) */
+    const uint32_t* fv_node;       /* node ids, strictly ascending (map order) */
+    const int32_t* fv_offset;      /* n_nodes + 1 CSR offsets into fv_index */
+    const int32_t* fv_index;       /* feature indices, each node's vector in its order */
+    float fx, fy, cx, cy;          /* mpCamera->mvParameters (Pinhole::toK_, src/CameraModels/Pinhole.cpp:168-173) */
+    int32_t nlevels;               /* <= 12 */
+    const float* scale_factors;    /* mvScaleFactors (nlevels) */
+    const float* level_sigma2;     /* mvLevelSigma2 (nlevels) */
+} orb_kf_view_t;
+
+/* Per-pair geometry SearchForTriangulation derives from the two poses (src/ORBmatcher.cc:1063-1090):
+ * T12 = T1w * Tw2 (R12 row-major, t12) and the epipole ep = pKF2->mpCamera->project(T2w * Cw1).
+ * A C++ caller fills it with Sophus exactly as the reference does; orb_kf_pair_geometry computes
+ * it from two 3x4 [R|t] poses for callers without Sophus. */
+typedef struct orb_kf_pair_geom {
+    float R12[9];
+    float t12[3];
+    float ep[2];
+} orb_kf_pair_geom_t;
+
+typedef struct orb_matcher_s* orb_matcher_t;
+
+/* ORBmatcher(float nnratio, bool checkOri) (include/ORBmatcher.h:40).  The handle owns device
+ * staging buffers and a stream; one handle per thread (like one ORBmatcher object). */
+int orb_matcher_create(float nnratio, int check_orientation, orb_matcher_t* out);
+int orb_matcher_destroy(orb_matcher_t m);
+
+/* T1w, T2w: 3x4 row-major [R|t] world->camera poses (float); fx..cy: camera of KF2. */
+int orb_kf_pair_geometry(const float T1w[12], const float T2w[12], float fx2, float fy2, float cx2, float cy2,
+                         orb_kf_pair_geom_t* out);
+
+/* SearchForTriangulation(pKF1, pKF2[p], vMatchedPairs, bOnlyStereo, bCoarse) for n_pairs
+ * neighbours of one keyframe in one launch (LocalMapping::CreateNewMapPoints calls it once per
+ * covisible KF, src/LocalMapping.cc:610).  Host memory, synchronous.  Writes
+ * matches12[p * kf1->n + i] = matched index in kf2s[p] or -1 (vMatchedPairs is the list of
+ * (i, matches12[i]) with matches12[i] >= 0 in increasing i) and n_matches[p] (the return value). */
+int orb_search_for_triangulation(orb_matcher_t m, const orb_kf_view_t* kf1, const orb_kf_view_t* kf2s,
+                                 const orb_kf_pair_geom_t* geoms, int n_pairs, int only_stereo, int coarse,
+                                 int32_t* matches12, int32_t* n_matches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -35,6 +35,7 @@ _PROTOS = {
     "oracle_fast_atan2": (_f, [_f, _f]),
     "oracle_gaussian_blur": (None, [_vp, _i, _i, _i, _vp]),
     "oracle_descriptor_distance": (_i, [_vp, _vp]),
+    "oracle_search_for_triangulation": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp]),
 }
 
 _LIB = None
@@ -165,3 +166,14 @@ def descriptor_distance(a: np.ndarray, b: np.ndarray) -> int:
     a = np.ascontiguousarray(a, dtype=np.uint8)
     b = np.ascontiguousarray(b, dtype=np.uint8)
     return load().oracle_descriptor_distance(a.ctypes.data, b.ctypes.data)
+
+
+def search_for_triangulation(kf1, kf2, geom, only_stereo: bool, coarse: bool, check_ori: bool):
+    """Oracle SearchForTriangulation for one pair.  kf1/kf2: objects with .view() returning an
+    orb_kf_view_t ctypes struct (the product's KeyFrame, used here as plain data); geom: the
+    orb_kf_pair_geom_t struct.  Returns (nmatches, vMatches12 int32[N1])."""
+    m = np.full(max(kf1.N, 1), -1, np.int32)
+    n = load().oracle_search_for_triangulation(ctypes.byref(kf1.view()), ctypes.byref(kf2.view()),
+                                               ctypes.byref(geom), int(only_stereo), int(coarse), int(check_ori),
+                                               m.ctypes.data)
+    return n, m[:kf1.N]

@@ -7,6 +7,7 @@ __graft_entry__.py), which register it under the import name ``orbslam3_amd``.
 from . import _lib
 from ._lib import KEYPOINT_DTYPE, OrbGpuError
 from .extractor import ORBextractor, keypoints_to_structured
+from .keyframe import KeyFrame
 from .matcher import ORBmatcher
 
-__all__ = ["ORBextractor", "ORBmatcher", "KEYPOINT_DTYPE", "OrbGpuError", "keypoints_to_structured", "_lib"]
+__all__ = ["ORBextractor", "ORBmatcher", "KeyFrame", "KEYPOINT_DTYPE", "OrbGpuError", "keypoints_to_structured", "_lib"]

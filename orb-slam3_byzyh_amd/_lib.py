@@ -56,6 +56,10 @@ PROTOTYPES = {
     "orb_extractor_level_download": (_i, [_vp, _i, _i, _vp]),
     "orb_descriptor_distance": (_i, [_vp, _vp]),
     "orb_hamming_knn2_device": (_i, [_vp, _i, _vp, _i, _vp, _vp, _vp, _vp]),
+    "orb_matcher_create": (_i, [_f, _i, ctypes.POINTER(_vp)]),
+    "orb_matcher_destroy": (_i, [_vp]),
+    "orb_kf_pair_geometry": (_i, [_vp, _vp, _f, _f, _f, _f, _vp]),
+    "orb_search_for_triangulation": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
 }
 
 # parity / debugging hooks exported by the library (not part of the public header)

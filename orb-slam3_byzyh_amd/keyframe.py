@@ -1,0 +1,69 @@
+"""Flat keyframe view for the matcher ABI (orb_kf_view_t in include/orbgpu.h).
+
+Holds the KeyFrame fields ORBmatcher::SearchForTriangulation reads (reference
+src/ORBmatcher.cc:1046-1324): mvKeysUn, mDescriptors, mvuRight, the map-point slots (as flags),
+mFeatVec (DBoW2::FeatureVector, a std::map node id -> feature indices) as CSR arrays, the pose
+Tcw and the pinhole intrinsics, mvScaleFactors and mvLevelSigma2.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from ._lib import KEYPOINT_DTYPE
+
+
+class KfView(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("kps_un", ctypes.c_void_p), ("desc", ctypes.c_void_p),
+                ("u_right", ctypes.c_void_p), ("has_mappoint", ctypes.c_void_p), ("n_nodes", ctypes.c_int32),
+                ("fv_node", ctypes.c_void_p), ("fv_offset", ctypes.c_void_p), ("fv_index", ctypes.c_void_p),
+                ("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),
+                ("nlevels", ctypes.c_int32), ("scale_factors", ctypes.c_void_p), ("level_sigma2", ctypes.c_void_p)]
+
+
+class PairGeom(ctypes.Structure):
+    _fields_ = [("R12", ctypes.c_float * 9), ("t12", ctypes.c_float * 3), ("ep", ctypes.c_float * 2)]
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+class KeyFrame:
+    """Keyframe data for the matcher.  feat_vec: dict node_id -> list of feature indices."""
+
+    def __init__(self, keys_un, descriptors, Tcw, camera, scale_factors, level_sigma2, u_right=None,
+                 has_mappoint=None, feat_vec=None):
+        self.mvKeysUn = np.ascontiguousarray(keys_un, dtype=KEYPOINT_DTYPE)
+        self.N = len(self.mvKeysUn)
+        self.mDescriptors = np.ascontiguousarray(descriptors, dtype=np.uint8).reshape(self.N, 32)
+        self.Tcw = np.ascontiguousarray(Tcw, dtype=np.float32).reshape(3, 4)
+        self.fx, self.fy, self.cx, self.cy = (float(np.float32(v)) for v in camera)
+        self.mvScaleFactors = np.ascontiguousarray(scale_factors, dtype=np.float32)
+        self.mvLevelSigma2 = np.ascontiguousarray(level_sigma2, dtype=np.float32)
+        self.mvuRight = None if u_right is None else np.ascontiguousarray(u_right, dtype=np.float32)
+        self.has_mappoint = None if has_mappoint is None else np.ascontiguousarray(has_mappoint, dtype=np.uint8)
+        feat_vec = feat_vec or {}
+        nodes = sorted(feat_vec)
+        self.fv_node = np.asarray(nodes, dtype=np.uint32)
+        self.fv_offset = np.zeros(len(nodes) + 1, np.int32)
+        idx = []
+        for i, k in enumerate(nodes):
+            idx.extend(feat_vec[k])
+            self.fv_offset[i + 1] = len(idx)
+        self.fv_index = np.asarray(idx, dtype=np.int32)
+        self._view = None
+
+    @property
+    def mFeatVec(self) -> dict:
+        return {int(k): self.fv_index[self.fv_offset[i]:self.fv_offset[i + 1]].tolist()
+                for i, k in enumerate(self.fv_node)}
+
+    def view(self) -> KfView:
+        if self._view is None:
+            self._view = KfView(self.N, _ptr(self.mvKeysUn), _ptr(self.mDescriptors), _ptr(self.mvuRight),
+                                _ptr(self.has_mappoint), len(self.fv_node), _ptr(self.fv_node), _ptr(self.fv_offset),
+                                _ptr(self.fv_index), self.fx, self.fy, self.cx, self.cy, len(self.mvScaleFactors),
+                                _ptr(self.mvScaleFactors), _ptr(self.mvLevelSigma2))
+        return self._view

@@ -7,6 +7,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import check
+from .keyframe import KeyFrame, KfView, PairGeom
 
 TH_HIGH = 100  # src/ORBmatcher.cc:36
 TH_LOW = 50    # src/ORBmatcher.cc:37
@@ -21,6 +22,58 @@ class ORBmatcher:
     def __init__(self, nnratio: float = 0.6, checkOri: bool = True):
         self.mfNNratio = float(nnratio)
         self.mbCheckOrientation = bool(checkOri)
+        self._h = None
+
+    def _handle(self):
+        if self._h is None:
+            lib = _lib.load()
+            h = ctypes.c_void_p()
+            check(lib.orb_matcher_create(self.mfNNratio, int(self.mbCheckOrientation), ctypes.byref(h)),
+                  "orb_matcher_create")
+            self._h = h
+        return self._h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _lib.load().orb_matcher_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    @staticmethod
+    def pair_geometry(pKF1: KeyFrame, pKF2: KeyFrame) -> PairGeom:
+        """R12, t12 of T12 = T1w * Tw2 and the epipole of KF1's centre in KF2 (src/ORBmatcher.cc:1063-1090)."""
+        g = PairGeom()
+        check(_lib.load().orb_kf_pair_geometry(pKF1.Tcw.ctypes.data, pKF2.Tcw.ctypes.data, pKF2.fx, pKF2.fy,
+                                               pKF2.cx, pKF2.cy, ctypes.byref(g)), "orb_kf_pair_geometry")
+        return g
+
+    def SearchForTriangulation(self, pKF1: KeyFrame, pKF2: KeyFrame, bOnlyStereo: bool, bCoarse: bool = False):
+        """src/ORBmatcher.cc:1046-1324.  Returns (nmatches, vMatchedPairs as a list of (idx1, idx2))."""
+        (n, m12), = self.SearchForTriangulationMany(pKF1, [pKF2], bOnlyStereo, bCoarse)
+        pairs = [(int(i), int(m12[i])) for i in np.flatnonzero(m12 >= 0)]
+        return n, pairs
+
+    def SearchForTriangulationMany(self, pKF1: KeyFrame, neighbours, bOnlyStereo: bool, bCoarse: bool = False,
+                                   geoms=None):
+        """SearchForTriangulation of pKF1 against every keyframe in `neighbours` in one device launch
+        (the loop of LocalMapping::CreateNewMapPoints).  Returns [(nmatches, vMatches12 int32[N1])]."""
+        neighbours = list(neighbours)
+        p = len(neighbours)
+        if p == 0:
+            return []
+        views = (KfView * p)(*[k.view() for k in neighbours])
+        if geoms is None:
+            geoms = [self.pair_geometry(pKF1, k) for k in neighbours]
+        garr = (PairGeom * p)(*geoms)
+        m12 = np.full((p, max(pKF1.N, 1)), -1, np.int32)
+        cnt = np.zeros(p, np.int32)
+        check(_lib.load().orb_search_for_triangulation(self._handle(), ctypes.byref(pKF1.view()), views, garr, p,
+                                                       int(bOnlyStereo), int(bCoarse), m12.ctypes.data,
+                                                       cnt.ctypes.data), "orb_search_for_triangulation")
+        return [(int(cnt[i]), m12[i, :pKF1.N]) for i in range(p)]
 
     @staticmethod
     def DescriptorDistance(a, b) -> int:

@@ -70,3 +70,118 @@ def stereo_pair(width: int = 752, height: int = 480, seed: int = 200, dmin: int 
 
 def frame_batch(n: int, width: int = 640, height: int = 480, seed0: int = 100) -> np.ndarray:
     return np.stack([polygon_frame(width, height, seed=seed0 + i) for i in range(n)])
+
+
+# ---- keyframes for the matcher ------------------------------------------
+
+EUROC_K = (458.654, 457.296, 367.215, 248.375)  # Examples/Stereo/EuRoC.yaml camera (left)
+EUROC_BF = 47.90639384423901                     # fx * baseline (0.110074 m)
+
+
+def scale_tables(nlevels: int = 8, scale: float = 1.2):
+    """mvScaleFactors / mvLevelSigma2 as the extractor computes them (float32 chain)."""
+    s = np.zeros(nlevels, np.float32)
+    s[0] = 1.0
+    for l in range(1, nlevels):
+        s[l] = np.float32(float(s[l - 1]) * float(np.float32(scale)))
+    return s, (s * s).astype(np.float32)
+
+
+class SyntheticVocabulary:
+    """k=10, two-level synthetic DBoW2-like tree: a feature's node is the level-2 word reached by
+    greedy Hamming argmin (first minimum) -- node ids 11..110 as DBoW2 numbers a 10-ary tree.
+    Stands in for ORBvoc.txt (absent: .MISSING_LARGE_BLOBS) to build FeatureVectors."""
+
+    def __init__(self, seed: int = 201, k: int = 10):
+        rng = np.random.default_rng(seed)
+        self.k = k
+        self.l1 = rng.integers(0, 256, (k, 32), dtype=np.uint8)
+        # children are perturbations of their parent so the tree is coherent
+        flips = rng.random((k, k, 256)) < 0.25
+        bits = np.unpackbits(self.l1, axis=1)[:, None, :] ^ flips
+        self.l2 = np.packbits(bits.astype(np.uint8), axis=2)
+
+    @staticmethod
+    def _ham(d, c):
+        return np.unpackbits(d[:, None, :] ^ c[None, :, :], axis=2).sum(axis=2)
+
+    def transform(self, desc: np.ndarray) -> dict:
+        a = np.argmin(self._ham(desc, self.l1), axis=1)
+        fv: dict = {}
+        for i in range(len(desc)):
+            b = int(np.argmin(self._ham(desc[i:i + 1], self.l2[a[i]])[0]))
+            fv.setdefault(1 + self.k + self.k * int(a[i]) + b, []).append(i)
+        return fv
+
+
+def _rot_yaw_pitch(yaw, pitch):
+    cy, sy, cp, sp = np.cos(yaw), np.sin(yaw), np.cos(pitch), np.sin(pitch)
+    Ry = np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]])
+    Rx = np.array([[1, 0, 0], [0, cp, -sp], [0, sp, cp]])
+    return Ry @ Rx
+
+
+def keyframe_scene(n_kf: int = 4, n_points: int = 1500, seed: int = 201, width: int = 752, height: int = 480,
+                   stereo_frac: float = 0.5, mappoint_frac: float = 0.3, clutter: int = 250, nlevels: int = 8,
+                   baseline: float = 0.2, yaw_deg: float = 3.0, pixel_noise: float = 0.7):
+    """Keyframes observing one random point cloud (depth 2..10 m) from poses along a 0.2 m-step arc.
+
+    Each visible point gives a keypoint with a random octave, noisy projection, an angle shared by the
+    point (+ noise) and the point's base descriptor with 0..40 flipped bits; plus random clutter
+    keypoints; a fraction has a stereo coordinate (mvuRight = u - bf/z) and a fraction already has a
+    MapPoint.  FeatureVectors come from SyntheticVocabulary.  Returns a list of dicts of KeyFrame
+    fields (keys_un, descriptors, Tcw, camera, scale_factors, level_sigma2, u_right, has_mappoint,
+    feat_vec)."""
+    from ._lib import KEYPOINT_DTYPE
+    rng = np.random.default_rng(seed)
+    voc = SyntheticVocabulary(seed)
+    fx, fy, cx, cy = EUROC_K
+    scale, sigma2 = scale_tables(nlevels)
+    P = np.stack([rng.uniform(-4, 4, n_points), rng.uniform(-2.5, 2.5, n_points), rng.uniform(2, 10, n_points)], 1)
+    base = rng.integers(0, 256, (n_points, 32), dtype=np.uint8)
+    ang0 = rng.uniform(0, 360, n_points)
+    out = []
+    for k in range(n_kf):
+        R = _rot_yaw_pitch(np.deg2rad(yaw_deg * k), np.deg2rad(0.5 * k))
+        C = np.array([baseline * k, 0.02 * k, 0.05 * k])  # camera centre
+        t = -R @ C
+        Xc = P @ R.T + t
+        z = Xc[:, 2]
+        u = fx * Xc[:, 0] / z + cx
+        v = fy * Xc[:, 1] / z + cy
+        vis = np.flatnonzero((z > 0.5) & (u >= 20) & (u < width - 20) & (v >= 20) & (v < height - 20))
+        nv = len(vis)
+        n = nv + clutter
+        kps = np.zeros(n, KEYPOINT_DTYPE)
+        octv = rng.integers(0, nlevels, n)
+        kps["octave"] = octv
+        kps["x"][:nv] = u[vis] + rng.normal(0, pixel_noise, nv) * scale[octv[:nv]]
+        kps["y"][:nv] = v[vis] + rng.normal(0, pixel_noise, nv) * scale[octv[:nv]]
+        kps["x"][nv:] = rng.uniform(20, width - 20, clutter)
+        kps["y"][nv:] = rng.uniform(20, height - 20, clutter)
+        kps["angle"][:nv] = np.mod(ang0[vis] + rng.normal(0, 4, nv) + 2.0 * k, 360)
+        kps["angle"][nv:] = rng.uniform(0, 360, clutter)
+        kps["size"] = 31 * scale[octv]
+        kps["response"] = rng.integers(7, 120, n)
+        kps["class_id"] = -1
+        desc = np.empty((n, 32), np.uint8)
+        bits = np.unpackbits(base[vis], axis=1)
+        nflip = rng.integers(0, 41, nv)
+        for i in range(nv):
+            bits[i, rng.choice(256, nflip[i], replace=False)] ^= 1
+        desc[:nv] = np.packbits(bits, axis=1)
+        desc[nv:] = rng.integers(0, 256, (clutter, 32), dtype=np.uint8)
+        # a few exact duplicates so that distance ties occur inside nodes
+        dup = rng.choice(n, size=min(20, n // 2), replace=False)
+        desc[dup[1::2]] = desc[dup[0::2]]
+        ur = np.full(n, -1.0, np.float32)
+        st = rng.random(nv) < stereo_frac
+        ur[:nv][st] = (kps["x"][:nv][st] - EUROC_BF / z[vis][st]).astype(np.float32)
+        perm = rng.permutation(n)
+        kps, desc, ur = kps[perm], desc[perm], ur[perm]
+        Tcw = np.concatenate([R, t[:, None]], 1).astype(np.float32)
+        out.append(dict(keys_un=kps, descriptors=desc, Tcw=Tcw, camera=EUROC_K, scale_factors=scale,
+                        level_sigma2=sigma2, u_right=ur,
+                        has_mappoint=(rng.random(n) < mappoint_frac).astype(np.uint8),
+                        feat_vec=voc.transform(desc)))
+    return out
