@@ -161,6 +161,64 @@ int orb_search_for_triangulation(orb_matcher_t m, const orb_kf_view_t* kf1, cons
                                  const orb_kf_pair_geom_t* geoms, int n_pairs, int only_stereo, int coarse,
                                  int32_t* matches12, int32_t* n_matches);
 
+/* ---- Optimizer::LocalBundleAdjustment (src/Optimizer.cc:1740-2188) ----------------------------- */
+/* The shim keeps the reference's graph gather (B1, src/Optimizer.cc:1744-1855) and the culling /
+ * write-back (B10, :2107-2185) on the host and hands the flattened g2o problem across this ABI; the
+ * library runs g2o's Levenberg-Marquardt (optimization_algorithm_levenberg.cpp:61-169) with the
+ * BlockSolver_6_3 Schur complement (block_solver.hpp:354-486) on the GPU, FP64 throughout. */
+
+typedef struct orb_ba_camera {  /* per keyframe: pKFi->fx, fy, cx, cy, mbf (floats upstream) */
+    float fx, fy, cx, cy, bf;
+} orb_ba_camera_t;
+
+typedef struct orb_ba_edge {
+    int32_t point;      /* index into the point arrays (vertex 0 of the g2o edge) */
+    int32_t pose;       /* index into the pose arrays (vertex 1) */
+    int32_t stereo;     /* 0: ORB_SLAM3::EdgeSE3ProjectXYZ (u, v), Huber sqrt(5.991);
+                           1: g2o::EdgeStereoSE3ProjectXYZ (u, v, u_right), Huber sqrt(7.815) */
+    float inv_sigma2;   /* pKFi->mvInvLevelSigma2[kpUn.octave]: information = I * inv_sigma2 */
+    double obs[3];      /* measurement (obs[2] unused for mono edges) */
+} orb_ba_edge_t;
+
+typedef struct orb_ba_problem {
+    int32_t n_poses, n_points, n_edges;
+    double* pose;                         /* n_poses x 7, in/out: g2o::SE3Quat::toVector (tx ty tz qx qy qz qw) of Tcw */
+    const int64_t* pose_id;               /* vertex ids (KeyFrame::mnId), unique */
+    const uint8_t* pose_fixed;            /* 1 = setFixed(true) (the map's init KF and the fixed covisible KFs) */
+    const orb_ba_camera_t* pose_camera;   /* n_poses */
+    double* point;                        /* n_points x 3, in/out: world position */
+    const int64_t* point_id;              /* vertex ids (MapPoint::mnId + maxKFid + 1), above every pose id */
+    const orb_ba_edge_t* edges;           /* n_edges, in insertion (edge id) order */
+} orb_ba_problem_t;
+
+typedef struct orb_ba_options {
+    int32_t iterations;                   /* optimizer.optimize(10) (src/Optimizer.cc:2101) */
+    double user_lambda_init;              /* 0: tau * max diag(H) (tau = 1e-5); >0: setUserLambdaInit */
+    const volatile int32_t* stop_flag;    /* pbStopFlag (polled between iterations and trials), may be NULL */
+} orb_ba_options_t;
+
+typedef struct orb_ba_result {
+    int32_t iterations;       /* iterations run (SparseOptimizer::optimize's return value) */
+    int32_t trials;           /* LM trials (linear solves) over all iterations */
+    int32_t terminated;       /* 1 if the algorithm returned Terminate (no progress / 3 bad steps) */
+    int32_t stopped;          /* 1 if the stop flag ended the run */
+    double initial_chi2;      /* robust chi2 before the first update */
+    double final_chi2;        /* robust chi2 of the accepted state */
+    double lambda;            /* final LM damping */
+} orb_ba_result_t;
+
+typedef struct orb_ba_s* orb_ba_t;
+
+int orb_ba_create(orb_ba_t* out);
+int orb_ba_destroy(orb_ba_t h);
+
+/* Optimise `problem` in place (poses and points).  edge_chi2[e] receives e->chi2() as the culling
+ * pass reads it after optimize() (the error of the last evaluated state, robust kernel not applied)
+ * and edge_depth_ok[e] e->isDepthPositive() for the final estimates (either may be NULL).
+ * Returns ORB_OK, ORB_ERR_ABORTED if the stop flag was set before the first iteration, or an error. */
+int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* problem, const orb_ba_options_t* options, double* edge_chi2,
+                    uint8_t* edge_depth_ok, orb_ba_result_t* result);
+
 #ifdef __cplusplus
 }
 #endif

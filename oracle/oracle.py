@@ -36,6 +36,7 @@ _PROTOS = {
     "oracle_gaussian_blur": (None, [_vp, _i, _i, _i, _vp]),
     "oracle_descriptor_distance": (_i, [_vp, _vp]),
     "oracle_search_for_triangulation": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp]),
+    "oracle_local_ba": (_i, [_vp, _vp, _vp, _vp, _vp]),
 }
 
 _LIB = None
@@ -177,3 +178,44 @@ def search_for_triangulation(kf1, kf2, geom, only_stereo: bool, coarse: bool, ch
                                                ctypes.byref(geom), int(only_stereo), int(coarse), int(check_ori),
                                                m.ctypes.data)
     return n, m[:kf1.N]
+
+
+class _BaProblem(ctypes.Structure):
+    _fields_ = [("n_poses", ctypes.c_int32), ("n_points", ctypes.c_int32), ("n_edges", ctypes.c_int32),
+                ("pose", _vp), ("pose_id", _vp), ("pose_fixed", _vp), ("pose_camera", _vp), ("point", _vp),
+                ("point_id", _vp), ("edges", _vp)]
+
+
+class _BaOptions(ctypes.Structure):
+    _fields_ = [("iterations", ctypes.c_int32), ("user_lambda_init", ctypes.c_double), ("stop_flag", _vp)]
+
+
+class _BaResult(ctypes.Structure):
+    _fields_ = [("iterations", ctypes.c_int32), ("trials", ctypes.c_int32), ("terminated", ctypes.c_int32),
+                ("stopped", ctypes.c_int32), ("initial_chi2", ctypes.c_double), ("final_chi2", ctypes.c_double),
+                ("lambda_", ctypes.c_double)]
+
+
+def local_ba(prob: dict, iterations: int = 10, user_lambda_init: float = 0.0, stop_flag=None):
+    """Oracle g2o LM/Schur solve of a flattened LocalBundleAdjustment graph (see oracle/orb_ba_oracle.cpp).
+    prob: dict of arrays (pose [n,7] t+q, pose_id, pose_fixed, pose_camera (5 x f4 records), point [m,3],
+    point_id, edges (40-byte records)).  Returns (pose, point, edge_chi2, depth_ok, result dict)."""
+    pose = np.ascontiguousarray(prob["pose"], dtype=np.float64).copy()
+    point = np.ascontiguousarray(prob["point"], dtype=np.float64).copy()
+    pid = np.ascontiguousarray(prob["pose_id"], dtype=np.int64)
+    pfx = np.ascontiguousarray(prob["pose_fixed"], dtype=np.uint8)
+    cam = np.ascontiguousarray(prob["pose_camera"])
+    qid = np.ascontiguousarray(prob["point_id"], dtype=np.int64)
+    edges = np.ascontiguousarray(prob["edges"])
+    assert cam.dtype.itemsize == 20 and edges.dtype.itemsize == 40
+    s = _BaProblem(len(pose), len(point), len(edges), pose.ctypes.data, pid.ctypes.data, pfx.ctypes.data,
+                   cam.ctypes.data, point.ctypes.data, qid.ctypes.data, edges.ctypes.data)
+    flag = None if stop_flag is None else np.ascontiguousarray(stop_flag, dtype=np.int32)
+    o = _BaOptions(int(iterations), float(user_lambda_init), None if flag is None else flag.ctypes.data)
+    chi2 = np.zeros(len(edges))
+    depth = np.zeros(len(edges), np.uint8)
+    r = _BaResult()
+    load().oracle_local_ba(ctypes.byref(s), ctypes.byref(o), chi2.ctypes.data, depth.ctypes.data, ctypes.byref(r))
+    res = {"iterations": r.iterations, "trials": r.trials, "terminated": r.terminated, "stopped": r.stopped,
+           "initial_chi2": r.initial_chi2, "final_chi2": r.final_chi2, "lambda": r.lambda_}
+    return pose, point, chi2, depth.astype(bool), res

@@ -9,5 +9,6 @@ from ._lib import KEYPOINT_DTYPE, OrbGpuError
 from .extractor import ORBextractor, keypoints_to_structured
 from .keyframe import KeyFrame
 from .matcher import ORBmatcher
+from .optimizer import LocalBA, local_bundle_adjustment
 
-__all__ = ["ORBextractor", "ORBmatcher", "KeyFrame", "KEYPOINT_DTYPE", "OrbGpuError", "keypoints_to_structured", "_lib"]
+__all__ = ["ORBextractor", "ORBmatcher", "KeyFrame", "LocalBA", "local_bundle_adjustment", "KEYPOINT_DTYPE", "OrbGpuError", "keypoints_to_structured", "_lib"]

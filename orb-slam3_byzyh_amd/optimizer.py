@@ -1,0 +1,108 @@
+"""Optimizer::LocalBundleAdjustment's solve on the MI355X (reference src/Optimizer.cc:1740-2188).
+
+The reference gathers the local window from its map (B1, :1744-1855), builds a g2o graph, runs
+optimizer.optimize(10) (:2101), then culls edges by chi2 / depth and writes the estimates back
+(B10, :2107-2185).  This module takes the flattened graph (poses as g2o::SE3Quat vectors, points,
+edges with their measurements, information and camera) and runs the g2o Levenberg-Marquardt /
+Schur solve on the GPU through orb_ba_optimize (include/orbgpu.h).  `local_bundle_adjustment`
+then applies the reference's culling thresholds (5.991 mono, 7.815 stereo) and reports the
+observations LocalBundleAdjustment would erase.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check
+
+CHI2_MONO = 5.991    # src/Optimizer.cc:2115
+CHI2_STEREO = 7.815  # src/Optimizer.cc:2145
+
+_p = ctypes.c_void_p
+
+
+class BaProblem(ctypes.Structure):
+    _fields_ = [("n_poses", ctypes.c_int32), ("n_points", ctypes.c_int32), ("n_edges", ctypes.c_int32),
+                ("pose", _p), ("pose_id", _p), ("pose_fixed", _p), ("pose_camera", _p), ("point", _p),
+                ("point_id", _p), ("edges", _p)]
+
+
+class BaOptions(ctypes.Structure):
+    _fields_ = [("iterations", ctypes.c_int32), ("user_lambda_init", ctypes.c_double), ("stop_flag", _p)]
+
+
+class BaResult(ctypes.Structure):
+    _fields_ = [("iterations", ctypes.c_int32), ("trials", ctypes.c_int32), ("terminated", ctypes.c_int32),
+                ("stopped", ctypes.c_int32), ("initial_chi2", ctypes.c_double), ("final_chi2", ctypes.c_double),
+                ("lambda_", ctypes.c_double)]
+
+    def as_dict(self):
+        return {"iterations": self.iterations, "trials": self.trials, "terminated": self.terminated,
+                "stopped": self.stopped, "initial_chi2": self.initial_chi2, "final_chi2": self.final_chi2,
+                "lambda": self.lambda_}
+
+
+def make_problem_struct(prob: dict) -> tuple[BaProblem, dict]:
+    """Contiguous copies of the problem arrays (pose and point are optimised in place) + the struct."""
+    from .synth import BA_CAMERA_DTYPE, BA_EDGE_DTYPE
+    arrs = {
+        "pose": np.ascontiguousarray(prob["pose"], dtype=np.float64).copy(),
+        "pose_id": np.ascontiguousarray(prob["pose_id"], dtype=np.int64),
+        "pose_fixed": np.ascontiguousarray(prob["pose_fixed"], dtype=np.uint8),
+        "pose_camera": np.ascontiguousarray(prob["pose_camera"], dtype=BA_CAMERA_DTYPE),
+        "point": np.ascontiguousarray(prob["point"], dtype=np.float64).copy(),
+        "point_id": np.ascontiguousarray(prob["point_id"], dtype=np.int64),
+        "edges": np.ascontiguousarray(prob["edges"], dtype=BA_EDGE_DTYPE),
+    }
+    s = BaProblem(len(arrs["pose"]), len(arrs["point"]), len(arrs["edges"]), arrs["pose"].ctypes.data,
+                  arrs["pose_id"].ctypes.data, arrs["pose_fixed"].ctypes.data, arrs["pose_camera"].ctypes.data,
+                  arrs["point"].ctypes.data, arrs["point_id"].ctypes.data, arrs["edges"].ctypes.data)
+    return s, arrs
+
+
+class LocalBA:
+    """A device handle for repeated local BA solves (one per LocalMapping thread)."""
+
+    def __init__(self):
+        lib = _lib.load()
+        _lib.require_device()
+        h = ctypes.c_void_p()
+        check(lib.orb_ba_create(ctypes.byref(h)), "orb_ba_create")
+        self._h = h
+        self._lib = lib
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                self._lib.orb_ba_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def optimize(self, prob: dict, iterations: int = 10, user_lambda_init: float = 0.0, stop_flag=None):
+        """Run optimize(iterations) on a copy of `prob`.  Returns (pose, point, edge_chi2, depth_ok, result)."""
+        s, arrs = make_problem_struct(prob)
+        flag = None if stop_flag is None else np.ascontiguousarray(stop_flag, dtype=np.int32)
+        opt = BaOptions(int(iterations), float(user_lambda_init), None if flag is None else flag.ctypes.data)
+        ne = len(arrs["edges"])
+        chi2 = np.zeros(ne, np.float64)
+        depth = np.zeros(ne, np.uint8)
+        res = BaResult()
+        rc = self._lib.orb_ba_optimize(self._h, ctypes.byref(s), ctypes.byref(opt), chi2.ctypes.data,
+                                       depth.ctypes.data, ctypes.byref(res))
+        if rc != _lib.ORB_ERR_ABORTED:
+            check(rc, "orb_ba_optimize")
+        return arrs["pose"], arrs["point"], chi2, depth.astype(bool), res.as_dict()
+
+
+def local_bundle_adjustment(prob: dict, iterations: int = 10, solver: LocalBA | None = None):
+    """optimize(10) and the reference's culling pass (src/Optimizer.cc:2107-2160): returns
+    (pose, point, erase_mask over edges, result)."""
+    solver = solver or LocalBA()
+    pose, point, chi2, depth, res = solver.optimize(prob, iterations)
+    stereo = np.asarray(prob["edges"]["stereo"]) != 0
+    erase = np.where(stereo, chi2 > CHI2_STEREO, chi2 > CHI2_MONO) | ~depth
+    return pose, point, erase, res

@@ -185,3 +185,118 @@ def keyframe_scene(n_kf: int = 4, n_points: int = 1500, seed: int = 201, width: 
                         has_mappoint=(rng.random(n) < mappoint_frac).astype(np.uint8),
                         feat_vec=voc.transform(desc)))
     return out
+
+
+# ---- local bundle adjustment problems ----------------------------------
+
+BA_EDGE_DTYPE = np.dtype([("point", "<i4"), ("pose", "<i4"), ("stereo", "<i4"), ("inv_sigma2", "<f4"),
+                          ("obs", "<f8", (3,))])
+BA_CAMERA_DTYPE = np.dtype([("fx", "<f4"), ("fy", "<f4"), ("cx", "<f4"), ("cy", "<f4"), ("bf", "<f4")])
+
+
+def rot_to_quat(R):
+    """Rotation matrix -> quaternion (x, y, z, w) with w >= 0."""
+    R = np.asarray(R, np.float64)
+    t = np.trace(R)
+    if t > 0:
+        s = np.sqrt(t + 1.0) * 2
+        q = np.array([(R[2, 1] - R[1, 2]) / s, (R[0, 2] - R[2, 0]) / s, (R[1, 0] - R[0, 1]) / s, 0.25 * s])
+    else:
+        i = int(np.argmax(np.diag(R)))
+        j, k = (i + 1) % 3, (i + 2) % 3
+        s = np.sqrt(R[i, i] - R[j, j] - R[k, k] + 1.0) * 2
+        q = np.zeros(4)
+        q[i] = 0.25 * s
+        q[3] = (R[k, j] - R[j, k]) / s
+        q[j] = (R[j, i] + R[i, j]) / s
+        q[k] = (R[k, i] + R[i, k]) / s
+    q /= np.linalg.norm(q)
+    return q if q[3] >= 0 else -q
+
+
+def quat_to_rot(q):
+    x, y, z, w = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+def _small_rot(rng, sigma):
+    w = rng.normal(0, sigma, 3)
+    th = np.linalg.norm(w)
+    if th < 1e-12:
+        return np.eye(3)
+    k = w / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+
+
+def local_ba_problem(n_kf: int = 50, n_points: int = 2000, obs_per_point: int = 6, stereo_frac: float = 0.0,
+                     n_fixed: int = 2, seed: int = 7, outlier_frac: float = 0.05, width: int = 752, height: int = 480,
+                     nlevels: int = 8):
+    """C5: keyframes along a 10 m arc facing a point cloud 2-10 m deep; each point observed by ~6
+    keyframes (~12k edges for 2000 points); octave U{0..7}, information 1/1.44^octave, pixel noise
+    N(0, 1)*scale, 5 % outliers (+-20 px), poses perturbed by 0.01 rad / 0.02 m and points by
+    0.05 m, `n_fixed` fixed keyframes, EuRoC pinhole intrinsics.  Returns a dict of the arrays of
+    orb_ba_problem_t plus the ground truth."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = EUROC_K
+    scale, sigma2 = scale_tables(nlevels)
+    inv_sigma2 = (np.float32(1.0) / sigma2).astype(np.float32)
+    # ground truth: camera centres on an arc, looking roughly at the cloud centre (0, 0, 8)
+    phis = np.linspace(-0.5, 0.5, n_kf)
+    Rs, ts = [], []
+    for k, ph in enumerate(phis):
+        C = np.array([10.0 * np.sin(ph) * 0.5, 0.3 * np.sin(3 * ph), -10.0 * (1 - np.cos(ph)) * 0.5])
+        yaw = -ph * 0.5
+        Rwc = np.array([[np.cos(yaw), 0, np.sin(yaw)], [0, 1, 0], [-np.sin(yaw), 0, np.cos(yaw)]])
+        Rcw = Rwc.T
+        Rs.append(Rcw)
+        ts.append(-Rcw @ C)
+    P = np.stack([rng.uniform(-5, 5, n_points), rng.uniform(-2.5, 2.5, n_points), rng.uniform(4, 12, n_points)], 1)
+    edges = []
+    for p in range(n_points):
+        vis = []
+        for k in range(n_kf):
+            Xc = Rs[k] @ P[p] + ts[k]
+            if Xc[2] < 1.0:
+                continue
+            u, v = fx * Xc[0] / Xc[2] + cx, fy * Xc[1] / Xc[2] + cy
+            if 10 <= u < width - 10 and 10 <= v < height - 10:
+                vis.append((k, u, v, Xc[2]))
+        if not vis:
+            continue
+        sel = rng.choice(len(vis), size=min(obs_per_point, len(vis)), replace=False)
+        for s in sorted(sel, key=lambda i: vis[i][0]):
+            k, u, v, z = vis[s]
+            octv = int(rng.integers(0, nlevels))
+            sc = float(scale[octv])
+            uo, vo = u + rng.normal(0, 1.0) * sc, v + rng.normal(0, 1.0) * sc
+            if rng.random() < outlier_frac:
+                uo += rng.uniform(-20, 20)
+                vo += rng.uniform(-20, 20)
+            st = rng.random() < stereo_frac
+            ur = uo - EUROC_BF / z + rng.normal(0, 1.0) * sc if st else 0.0
+            edges.append((p, k, int(st), inv_sigma2[octv], (uo, vo, ur)))
+    E = np.zeros(len(edges), BA_EDGE_DTYPE)
+    for i, (p, k, st, info, obs) in enumerate(edges):
+        E[i] = (p, k, st, info, obs)
+    pose_gt = np.zeros((n_kf, 7))
+    pose0 = np.zeros((n_kf, 7))
+    fixed = np.zeros(n_kf, np.uint8)
+    fixed[:n_fixed] = 1
+    for k in range(n_kf):
+        pose_gt[k, :3] = ts[k]
+        pose_gt[k, 3:] = rot_to_quat(Rs[k])
+        if fixed[k]:
+            pose0[k] = pose_gt[k]
+        else:
+            Rp = _small_rot(rng, 0.01) @ Rs[k]
+            pose0[k, :3] = ts[k] + rng.normal(0, 0.02, 3)
+            pose0[k, 3:] = rot_to_quat(Rp)
+    cams = np.zeros(n_kf, BA_CAMERA_DTYPE)
+    cams[:] = (fx, fy, cx, cy, EUROC_BF)
+    point0 = P + rng.normal(0, 0.05, P.shape)
+    return dict(pose=pose0, pose_id=np.arange(n_kf, dtype=np.int64), pose_fixed=fixed, pose_camera=cams,
+                point=point0, point_id=np.arange(n_points, dtype=np.int64) + n_kf + 1, edges=E,
+                pose_gt=pose_gt, point_gt=P)
