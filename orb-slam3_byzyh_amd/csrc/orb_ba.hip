@@ -14,8 +14,8 @@
 //
 // One LM iteration = k_ba_build (per edge: error, Huber weight, Jacobians, quadratic form parts)
 // -> k_ba_reduce_land / k_ba_reduce_pose (fixed-order reductions) -> per trial:
-// k_ba_schur_land (Dinv, Z, Hpl*db) -> k_ba_schur_blocks (S = Hpp + lambda I - sum Z Hpl^T, one
-// wave per 6x6 block) -> k_ba_schur_rhs -> k_ba_chol (single-workgroup blocked Cholesky + both
+// k_ba_schur_edges (Dinv, Z, Hpl*db per edge) -> k_ba_schur_blocks (S = Hpp + lambda I - sum Z Hpl^T,
+// one wave per 6x6 block) -> k_ba_schur_rhs -> k_ba_chol (single-workgroup blocked Cholesky + both
 // triangular solves) -> k_ba_backsub (x_l) -> k_ba_update (push + oplus) -> k_ba_error -> k_ba_sums
 // (robust chi2 and g2o's computeScale).  The host reads two scalars per trial and runs g2o's
 // accept / reject logic (rejection restores the backup, like g2o's pop()).
@@ -23,11 +23,14 @@
 // Reductions run in a fixed order, so results are deterministic; they differ from g2o's serial
 // sums by rounding only (parity bar: 1e-6 RMSE on poses).  S is factored with Cholesky; Eigen's
 // SimplicialLDLT differs only by rounding on the SPD matrices LM produces (H PSD, lambda > 0).
+#include <hip/hip_cooperative_groups.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <numeric>
@@ -36,10 +39,14 @@
 #include "orbgpu.h"
 #include "orbgpu_internal.h"
 
+// The BA path is judged at 1e-6 RMSE (not bitwise like the extractor): let products and sums
+// contract into FMAs in this file despite the library-wide -ffp-contract=off.
+#pragma clang fp contract(fast)
+
 namespace {
 
 constexpr int kT = 256;
-constexpr int kCholThreads = 1024;
+constexpr int kCholThreads = 512;
 
 struct EdgeDev {  // == orb_ba_edge_t
     int32_t point, pose, stereo;
@@ -85,19 +92,27 @@ __device__ void qfrom_matrix(const double m[9], double q[4]) {  // Eigen Quatern
         q[0] = (m[7] - m[5]) * t;
         q[1] = (m[2] - m[6]) * t;
         q[2] = (m[3] - m[1]) * t;
-    } else {
-        int i = 0;
-        if (m[4] > m[0]) i = 1;
-        if (m[8] > m[4 * i]) i = 2;
-        const int j = (i + 1) % 3, k = (j + 1) % 3;
-        t = sqrt(m[4 * i] - m[4 * j] - m[4 * k] + 1.0);
-        double c[3];
-        c[i] = 0.5 * t;
+    } else if (m[4] <= m[0] && m[8] <= m[0]) {  // i = 0, j = 1, k = 2
+        t = sqrt(m[0] - m[4] - m[8] + 1.0);
+        q[0] = 0.5 * t;
         t = 0.5 / t;
-        q[3] = (m[3 * k + j] - m[3 * j + k]) * t;
-        c[j] = (m[3 * j + i] + m[3 * i + j]) * t;
-        c[k] = (m[3 * k + i] + m[3 * i + k]) * t;
-        q[0] = c[0]; q[1] = c[1]; q[2] = c[2];
+        q[3] = (m[7] - m[5]) * t;
+        q[1] = (m[3] + m[1]) * t;
+        q[2] = (m[6] + m[2]) * t;
+    } else if (m[8] <= m[4]) {  // i = 1, j = 2, k = 0
+        t = sqrt(m[4] - m[8] - m[0] + 1.0);
+        q[1] = 0.5 * t;
+        t = 0.5 / t;
+        q[3] = (m[2] - m[6]) * t;
+        q[2] = (m[7] + m[5]) * t;
+        q[0] = (m[1] + m[3]) * t;
+    } else {  // i = 2, j = 0, k = 1
+        t = sqrt(m[8] - m[0] - m[4] + 1.0);
+        q[2] = 0.5 * t;
+        t = 0.5 / t;
+        q[3] = (m[3] - m[1]) * t;
+        q[0] = (m[2] + m[6]) * t;
+        q[1] = (m[5] + m[7]) * t;
     }
 }
 
@@ -207,7 +222,7 @@ __global__ __launch_bounds__(kT) void k_ba_edges(int ne, const EdgeDev* __restri
     qmatrix(q, R);
     const double x = Xc[0], y = Xc[1], z = Xc[2];
     const double fx = cam.fx, fy = cam.fy;
-    const int D = E.stereo ? 3 : 2;
+    constexpr int D = 3;  // mono edges have a zero third row and omega_r[2] = 0: adding +0.0 is exact
     double A[9], B[18];
     if (!E.stereo) {  // src/OptimizableTypes.cpp:175-197 with -Pinhole::projectJac
         const double j00 = -(fx / z), j02 = -(-fx * x / (z * z)), j11 = -(fy / z), j12 = -(-fy * y / (z * z));
@@ -335,56 +350,73 @@ __device__ __forceinline__ void inverse3(const double m[9], double o[9]) {  // E
         for (int j = 0; j < 3; ++j) o[3 * i + j] = cof(j, i) * invdet;
 }
 
-// per landmark: Dinv = (Hll + lambda I)^-1, db = Dinv b_l, Z_e = Hpl_e Dinv, cb_e = Hpl_e db
-__global__ __launch_bounds__(kT) void k_ba_schur_land(int nl, double lambda, const int32_t* __restrict__ off,
-                                                      const int32_t* __restrict__ eidx, const double* __restrict__ hll,
-                                                      const double* __restrict__ bl, const double* __restrict__ hpl,
-                                                      double* __restrict__ dinv, double* __restrict__ z,
-                                                      double* __restrict__ cb) {
-    const int l = blockIdx.x * kT + threadIdx.x;
-    if (l >= nl) return;
-    double D[9], Di[9];
+// Dinv = (Hll_l + lambda I)^-1 (BlockSolver::solve: D->inverse() of the damped landmark block)
+__device__ __forceinline__ void land_dinv(const double* __restrict__ hll, int l, double lambda, double Di[9]) {
+    double D[9];
     for (int i = 0; i < 9; ++i) D[i] = hll[9 * (size_t)l + i] + (i % 4 == 0 ? lambda : 0.0);
     inverse3(D, Di);
-    for (int i = 0; i < 9; ++i) dinv[9 * (size_t)l + i] = Di[i];
+}
+
+// per free edge e of landmark l: Z_e = Hpl_e Dinv_l, cb_e = Hpl_e (Dinv_l b_l) (one thread per edge)
+__global__ __launch_bounds__(kT) void k_ba_schur_edges(int nfe, double lambda, const int32_t* __restrict__ fedge,
+                                                       const int32_t* __restrict__ fland, const double* __restrict__ hll,
+                                                       const double* __restrict__ bl, const double* __restrict__ hpl,
+                                                       double* __restrict__ z, double* __restrict__ cb) {
+    const int t = blockIdx.x * kT + threadIdx.x;
+    if (t >= nfe) return;
+    const int e = fedge[t], l = fland[t];
+    double Di[9];
+    land_dinv(hll, l, lambda, Di);
     const double b0 = bl[3 * (size_t)l], b1 = bl[3 * (size_t)l + 1], b2 = bl[3 * (size_t)l + 2];
     double db[3];
     for (int r = 0; r < 3; ++r) db[r] = Di[3 * r] * b0 + Di[3 * r + 1] * b1 + Di[3 * r + 2] * b2;
-    for (int k = off[l]; k < off[l + 1]; ++k) {
-        const int e = eidx[k];
-        const double* H = hpl + 18 * (size_t)e;
-        double* Z = z + 18 * (size_t)e;
-        double* C = cb + 6 * (size_t)e;
-        for (int r = 0; r < 6; ++r) {
-            const double h0 = H[3 * r], h1 = H[3 * r + 1], h2 = H[3 * r + 2];
-            for (int c = 0; c < 3; ++c) Z[3 * r + c] = h0 * Di[c] + h1 * Di[3 + c] + h2 * Di[6 + c];
-            C[r] = h0 * db[0] + h1 * db[1] + h2 * db[2];
-        }
+    const double* H = hpl + 18 * (size_t)e;
+    double* Z = z + 18 * (size_t)e;
+    double* C = cb + 6 * (size_t)e;
+    for (int r = 0; r < 6; ++r) {
+        const double h0 = H[3 * r], h1 = H[3 * r + 1], h2 = H[3 * r + 2];
+        for (int c = 0; c < 3; ++c) Z[3 * r + c] = h0 * Di[c] + h1 * Di[3 + c] + h2 * Di[6 + c];
+        C[r] = h0 * db[0] + h1 * db[1] + h2 * db[2];
     }
 }
 
-// S block (bi, bj), bi <= bj: one wave, lane = 6*r + c (36 lanes); S = [Hpp + lambda I] - sum Z_a Hpl_b^T
-__global__ __launch_bounds__(256) void k_ba_schur_blocks(int nblk, int n, double lambda, const int32_t* __restrict__ bi,
-                                                         const int32_t* __restrict__ bj, const int32_t* __restrict__ off,
-                                                         const int32_t* __restrict__ pa, const int32_t* __restrict__ pb,
-                                                         const double* __restrict__ z, const double* __restrict__ hpl,
-                                                         const double* __restrict__ hpp, double* __restrict__ S) {
-    const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (blk >= nblk || lane >= 36) return;
+// S block (bi, bj), bi <= bj, one wave: lanes split the block's (Z_a, Hpl_b) products, each
+// accumulating the full 6x6 partial sum; lane e < 36 then adds the 64 partials in lane order.
+// S = [Hpp + lambda I] - sum Z_a Hpl_b^T; written to both triangles.
+__global__ __launch_bounds__(64) void k_ba_schur_blocks(int n, double lambda, const int32_t* __restrict__ bi,
+                                                        const int32_t* __restrict__ bj, const int32_t* __restrict__ off,
+                                                        const int32_t* __restrict__ pa, const int32_t* __restrict__ pb,
+                                                        const double* __restrict__ z, const double* __restrict__ hpl,
+                                                        const double* __restrict__ hpp, double* __restrict__ S) {
+    __shared__ double red[36][65];
+    const int blk = blockIdx.x, lane = threadIdx.x;
+    double acc[36];
+#pragma unroll
+    for (int k = 0; k < 36; ++k) acc[k] = 0;
+    for (int k = off[blk] + lane; k < off[blk + 1]; k += 64) {
+        const double* Z = z + 18 * (size_t)pa[k];
+        const double* H = hpl + 18 * (size_t)pb[k];
+        double zr[18], hr[18];
+#pragma unroll
+        for (int q = 0; q < 18; ++q) { zr[q] = Z[q]; hr[q] = H[q]; }
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int c = 0; c < 6; ++c)
+                acc[6 * r + c] += zr[3 * r] * hr[3 * c] + zr[3 * r + 1] * hr[3 * c + 1] + zr[3 * r + 2] * hr[3 * c + 2];
+    }
+#pragma unroll
+    for (int k = 0; k < 36; ++k) red[k][lane] = acc[k];
+    __syncthreads();
+    if (lane >= 36) return;
+    double sum = 0;
+    for (int q = 0; q < 64; ++q) sum += red[lane][q];
     const int r = lane / 6, c = lane % 6;
     const int i = bi[blk], j = bj[blk];
-    double s = 0;
-    if (i == j) s = hpp[36 * (size_t)i + 6 * r + c] + (r == c ? lambda : 0.0);
-    double acc = 0;
-    for (int k = off[blk]; k < off[blk + 1]; ++k) {
-        const double* Z = z + 18 * (size_t)pa[k] + 3 * r;
-        const double* H = hpl + 18 * (size_t)pb[k] + 3 * c;
-        acc += Z[0] * H[0] + Z[1] * H[1] + Z[2] * H[2];
-    }
-    s -= acc;
-    S[(size_t)(6 * i + r) * n + 6 * j + c] = s;
-    S[(size_t)(6 * j + c) * n + 6 * i + r] = s;
+    double v = -sum;
+    if (i == j) v = (hpp[36 * (size_t)i + 6 * r + c] + (r == c ? lambda : 0.0)) - sum;
+    S[(size_t)(6 * i + r) * n + 6 * j + c] = v;
+    S[(size_t)(6 * j + c) * n + 6 * i + r] = v;
 }
 
 // b_S = b_p - sum over the pose's edges of Hpl_e db (one wave per free pose)
@@ -415,33 +447,72 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     return __longlong_as_double(((uint64_t)hi << 32) | lo);
 }
 
-// Dense Cholesky S = L L^T (lower, in place) and the solves L y = b, L^T x = y, one workgroup.
-// Right-looking, panel width NB: wave 0 factors the NB x NB diagonal block in registers (lane r =
-// row r, cross-lane reads through v_readlane), all threads solve the panel rows against it and
-// apply the trailing update from the LDS-staged panel (4x4 register tiles).
+// Dense Cholesky S = L L^T and the solves L y = b, L^T x = y in one workgroup (512 threads).
+// Left-looking by panels of NB columns: the panel S[k0:n, k0:k0+NB] is staged in LDS and updated
+// with the L rows computed so far (L is kept transposed, LT[j*n + i] = L[i][j], so that column j
+// of L -- what every panel update streams -- is contiguous and the loads coalesce over rows);
+// wave 0 factors the NB x NB diagonal block in registers (lane r = row r, cross-lane reads through
+// v_readlane); all threads then solve the panel rows against it.  LDS: the NB rows of L above
+// the panel (NB x n), the panel (n x (NB+1)) and y (n).
 template <int NB>
-__global__ __launch_bounds__(kCholThreads) void k_ba_chol(int n, double* __restrict__ S, const double* __restrict__ b,
-                                                          double* __restrict__ x, int32_t* __restrict__ status) {
+__global__ __launch_bounds__(kCholThreads) void k_ba_chol(int n, const double* __restrict__ S, double* __restrict__ LT,
+                                                          const double* __restrict__ b, double* __restrict__ x,
+                                                          int32_t* __restrict__ status) {
     extern __shared__ double lds[];
-    double* P = lds;                              // panel rows [m][NB + 1]
-    double* y = lds + (size_t)n * (NB + 1);       // rhs / solution (n)
+    double* Lk = lds;                      // [NB][n]: Lk[c*n + j] = L[k0 + c][j], j < k0
+    double* A = Lk + (size_t)NB * n;       // [n][NB + 1]: panel rows
+    double* y = A + (size_t)n * (NB + 1);  // [n]
     __shared__ double Lkk[NB][NB + 1];
-    __shared__ double yblk[NB];
     __shared__ int fail;
     const int tid = threadIdx.x;
     for (int i = tid; i < n; i += kCholThreads) y[i] = b[i];
     if (tid == 0) fail = 0;
-    __syncthreads();
     for (int k0 = 0; k0 < n; k0 += NB) {
-        const int kb = min(NB, n - k0);
-        const int k1 = k0 + kb;
+        const int kb = min(NB, n - k0), m = n - k0;
+        __syncthreads();
+        for (int t = tid; t < NB * k0; t += kCholThreads) {
+            const int c = t % NB, j = t / NB;
+            Lk[(size_t)c * n + j] = c < kb ? LT[(size_t)j * n + k0 + c] : 0.0;
+        }
+        for (int t = tid; t < m * NB; t += kCholThreads) {
+            const int c = t % NB, i = t / NB;
+            A[(size_t)i * (NB + 1) + c] = c < kb ? S[(size_t)(k0 + i) * n + k0 + c] : 0.0;
+        }
+        __syncthreads();
+        // ---- panel update: A[i][c] -= sum_{j < k0} L[k0 + i][j] L[k0 + c][j]; 2 rows x 4 columns per item
+        const int npair = (m + 1) / 2;
+        for (int t = tid; t < npair * (NB / 4); t += kCholThreads) {
+            const int rp = t % npair, cg = t / npair;
+            const int i0 = 2 * rp, c0 = 4 * cg;
+            const bool two = i0 + 1 < m;
+            double acc[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+            const double* col = LT + k0 + i0;
+            const double* l0 = Lk + (size_t)c0 * n;
+#pragma unroll 16
+            for (int j = 0; j < k0; ++j) {
+                const double a0 = col[(size_t)j * n];
+                const double a1 = two ? col[(size_t)j * n + 1] : 0.0;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const double l = l0[(size_t)c * n + j];
+                    acc[0][c] += a0 * l;
+                    acc[1][c] += a1 * l;
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                A[(size_t)i0 * (NB + 1) + c0 + c] -= acc[0][c];
+                if (two) A[(size_t)(i0 + 1) * (NB + 1) + c0 + c] -= acc[1][c];
+            }
+        }
+        __syncthreads();
+        // ---- diagonal block (wave 0): lane r holds row r, identity padding beyond kb
         if (tid < 64) {
-            // ---- diagonal block: lane r holds row r (identity padding beyond kb)
             const int r = tid;
             double row[NB];
 #pragma unroll
             for (int c = 0; c < NB; ++c)
-                row[c] = (r < kb && c < kb) ? S[(size_t)(k0 + r) * n + k0 + c] : (r == c ? 1.0 : 0.0);
+                row[c] = (r < kb && c < kb) ? A[(size_t)r * (NB + 1) + c] : (r == c ? 1.0 : 0.0);
             bool bad = false;
 #pragma unroll
             for (int c = 0; c < NB; ++c) {
@@ -456,116 +527,88 @@ __global__ __launch_bounds__(kCholThreads) void k_ba_chol(int n, double* __restr
                     if (r >= j) row[j] -= row[c] * ljc;
                 }
             }
-            // forward solve of this block of y: yb_c = (y_c - sum_{k<c} L_ck yb_k) / L_cc
-            double yy = (r < kb) ? y[k0 + r] : 0.0;
-#pragma unroll
-            for (int c = 0; c < NB; ++c) {
-                const double yc = readlane_d(yy, c) / readlane_d(row[c], c);
-                if (r == c) yy = yc;
-                else if (r > c) yy -= row[c] * yc;
-            }
             if (r < NB) {
 #pragma unroll
-                for (int c = 0; c < NB; ++c) Lkk[r][c] = row[c];
-                yblk[r] = yy;
-            }
-            if (r < kb) {
-                y[k0 + r] = yy;
-#pragma unroll
-                for (int c = 0; c < NB; ++c)
-                    if (c <= r && c < kb) S[(size_t)(k0 + r) * n + k0 + c] = row[c];
+                for (int c = 0; c < NB; ++c) {
+                    Lkk[r][c] = c <= r ? row[c] : 0.0;
+                    A[(size_t)r * (NB + 1) + c] = c <= r ? row[c] : 0.0;
+                }
             }
             if (r == 0 && bad) fail = 1;
         }
         __syncthreads();
-        // ---- panel: rows i >= k1 solve L[i, k0:k1] L_kk^T = S[i, k0:k1]; update y[i]
-        const int m = n - k1;
-        for (int t = tid; t < m; t += kCholThreads) {
-            const int i = k1 + t;
+        // ---- panel rows below the diagonal block: solve x L_kk^T = a
+        for (int i = kb + tid; i < m; i += kCholThreads) {
+            asm volatile("" ::: "memory");  // keep the L_kk reads inside the loop (no LICM into 136 registers)
             double v[NB];
 #pragma unroll
-            for (int c = 0; c < NB; ++c) v[c] = c < kb ? S[(size_t)i * n + k0 + c] : 0.0;
-            double yi = y[i];
+            for (int c = 0; c < NB; ++c) v[c] = A[(size_t)i * (NB + 1) + c];
 #pragma unroll
             for (int c = 0; c < NB; ++c) {
                 double s = v[c];
 #pragma unroll
                 for (int k = 0; k < c; ++k) s -= v[k] * Lkk[c][k];
-                v[c] = s / Lkk[c][c];
-                yi -= v[c] * yblk[c];
+                v[c] = c < kb ? s / Lkk[c][c] : 0.0;
             }
-            y[i] = yi;
 #pragma unroll
-            for (int c = 0; c < NB; ++c) {
-                P[(size_t)t * (NB + 1) + c] = v[c];
-                if (c < kb) S[(size_t)i * n + k0 + c] = v[c];
-            }
+            for (int c = 0; c < NB; ++c) A[(size_t)i * (NB + 1) + c] = v[c];
         }
         __syncthreads();
-        // ---- trailing update of the lower triangle S[k1:n, k1:n] -= P P^T, 4x4 tiles
-        const int nt = (m + 3) / 4;
-        const int ntiles = nt * (nt + 1) / 2;
-        for (int tt = tid; tt < ntiles; tt += kCholThreads) {
-            // tile (ti, tj), tj <= ti, enumerated row by row
-            int ti = (int)((sqrt(8.0 * tt + 1.0) - 1.0) * 0.5);
-            while ((ti + 1) * (ti + 2) / 2 <= tt) ++ti;
-            while (ti * (ti + 1) / 2 > tt) --ti;
-            const int tj = tt - ti * (ti + 1) / 2;
-            double acc[4][4];
+        // ---- write the panel: LT[(k0 + c) * n + k0 + i] = L[k0 + i][k0 + c]
+        for (int t = tid; t < m * kb; t += kCholThreads) {
+            const int i = t % m, c = t / m;
+            LT[(size_t)(k0 + c) * n + k0 + i] = A[(size_t)i * (NB + 1) + c];
+        }
+    }
+    __syncthreads();
+    // ---- forward: L y = b
+    for (int k0 = 0; k0 < n; k0 += NB) {
+        const int kb = min(NB, n - k0);
+        if (tid < 64) {
+            const int r = tid;
+            double lrow[NB];
 #pragma unroll
-            for (int a = 0; a < 4; ++a)
+            for (int c = 0; c < NB; ++c)
+                lrow[c] = (r < kb && c < kb && c <= r) ? LT[(size_t)(k0 + c) * n + k0 + r] : (r == c ? 1.0 : 0.0);
+            double yy = r < kb ? y[k0 + r] : 0.0;
 #pragma unroll
-                for (int c = 0; c < 4; ++c) acc[a][c] = 0;
-            const int ia = 4 * ti, ja = 4 * tj;
-#pragma unroll 4
-            for (int k = 0; k < NB; ++k) {
-                double pi[4], pj[4];
-#pragma unroll
-                for (int a = 0; a < 4; ++a) {
-                    pi[a] = (ia + a < m) ? P[(size_t)(ia + a) * (NB + 1) + k] : 0.0;
-                    pj[a] = (ja + a < m) ? P[(size_t)(ja + a) * (NB + 1) + k] : 0.0;
-                }
-#pragma unroll
-                for (int a = 0; a < 4; ++a)
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) acc[a][c] += pi[a] * pj[c];
+            for (int c = 0; c < NB; ++c) {
+                const double yc = readlane_d(yy, c) / readlane_d(lrow[c], c);
+                if (r == c) yy = yc;
+                else if (r > c) yy -= lrow[c] * yc;
             }
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const int i = ia + a, j = ja + c;
-                    if (i < m && j <= i) S[(size_t)(k1 + i) * n + k1 + j] -= acc[a][c];
-                }
+            if (r < kb) y[k0 + r] = yy;
+        }
+        __syncthreads();
+        for (int i = k0 + kb + tid; i < n; i += kCholThreads) {
+            double s = 0;
+            for (int c = 0; c < kb; ++c) s += LT[(size_t)(k0 + c) * n + i] * y[k0 + c];
+            y[i] -= s;
         }
         __syncthreads();
     }
-    // ---- backward: L^T x = y, block by block from the bottom
+    // ---- backward: L^T x = y
     for (int k0 = ((n - 1) / NB) * NB; k0 >= 0; k0 -= NB) {
         const int kb = min(NB, n - k0);
         if (tid < 64) {
-            const int c = tid;  // lane c holds column c of L_kk: L[k0 + r][k0 + c], r >= c
+            const int c = tid;  // lane c holds column c of L_kk
             double col[NB];
 #pragma unroll
             for (int r = 0; r < NB; ++r)
-                col[r] = (r < kb && c < kb && r >= c) ? S[(size_t)(k0 + r) * n + k0 + c] : (r == c ? 1.0 : 0.0);
-            double yy = (c < kb) ? y[k0 + c] : 0.0;
+                col[r] = (r < kb && c < kb && r >= c) ? LT[(size_t)(k0 + c) * n + k0 + r] : (r == c ? 1.0 : 0.0);
+            double yy = c < kb ? y[k0 + c] : 0.0;
 #pragma unroll
             for (int r = NB - 1; r >= 0; --r) {
                 const double xr = readlane_d(yy, r) / readlane_d(col[r], r);
                 if (c == r) yy = xr;
                 else if (c < r) yy -= col[r] * xr;
             }
-            if (c < kb) {
-                y[k0 + c] = yy;
-                yblk[c] = yy;
-            }
+            if (c < kb) y[k0 + c] = yy;
         }
         __syncthreads();
-        // y[j] -= sum_c L[k0 + c][j] x_c for j < k0
         for (int j = tid; j < k0; j += kCholThreads) {
             double s = 0;
-            for (int c = 0; c < kb; ++c) s += S[(size_t)(k0 + c) * n + j] * yblk[c];
+            for (int c = 0; c < kb; ++c) s += LT[(size_t)j * n + k0 + c] * y[k0 + c];
             y[j] -= s;
         }
         __syncthreads();
@@ -574,11 +617,268 @@ __global__ __launch_bounds__(kCholThreads) void k_ba_chol(int n, double* __restr
     if (tid == 0) *status = fail;
 }
 
+// Cooperative multi-workgroup Cholesky + solve (the fast path for n <= 560 / 1100).
+// Right-looking by block columns of NB: workgroup w < nbc keeps block column w (rows j0..n) in LDS
+// for the whole factorisation; workgroup nbc owns the right-hand side.  Step k: the owner of
+// column k factors its diagonal block (wave 0, registers + v_readlane) and its panel rows and
+// publishes the panel to Lg (row-major L); after a grid barrier every later column applies the
+// panel's update to itself and the rhs owner runs the forward substitution of block k.  The rhs
+// owner finishes with the backward substitution L^T x = y from Lg.  One grid barrier per block
+// column; the matrix never makes a round trip through HBM between steps.
+constexpr int kCoopThreads = 256;
+
+// Cooperative multi-workgroup Cholesky + solve (n <= ~560 with NB = 32).  Workgroup w < nbc keeps
+// block column w (rows j0..n, NB columns) in LDS for the whole factorisation; workgroup nbc owns
+// the right-hand side.  Right-looking with a one-step look-ahead: after panel k is published, the
+// owner of column k+1 "finalizes" (applies panel k, factors its NB x NB diagonal block with a
+// one-wave LDS chain, inverts it, turns its panel rows into L rows with two GEMM passes, publishes
+// L and L_kk^-1), while every later column applies panel k and the rhs owner runs forward block k
+// as matrix-vector products with L_kk^-1.  One grid barrier per block column.
+template <int NB>
+struct CoopShared {
+    double Lkj[NB][NB + 1];   // rows of the current panel that fall in this block column
+    double Linv[NB][NB + 1];  // L_kk^-1 (lower)
+    double yb[NB];
+};
+
+// A[r][c] -= sum_q L[j0 + r][k0 + q] * Lkj[c][q] for r in [r_begin, rows), all NB columns; L rows
+// streamed from Lg (32 loads in flight per item), Lkj from LDS.  Items: (row, half of the columns).
+template <int NB>
+__device__ __forceinline__ void apply_panel(double* __restrict__ A, const double* __restrict__ Lg, int n, int j0,
+                                            int k0, int r_begin, int rows, const CoopShared<NB>& sh) {
+    constexpr int H = NB / 2;
+    const int items = (rows - r_begin) * 2;
+    for (int t = threadIdx.x; t < items; t += kCoopThreads) {
+        asm volatile("" ::: "memory");  // no LICM of the Lkj reads across items
+        const int r = r_begin + t / 2, c0 = H * (t % 2);
+        const double* lrow = Lg + (size_t)(j0 + r) * n + k0;
+        double l[NB];
+#pragma unroll
+        for (int q = 0; q < NB; ++q) l[q] = lrow[q];
+        double acc[H];
+#pragma unroll
+        for (int c = 0; c < H; ++c) acc[c] = 0;
+#pragma unroll
+        for (int q = 0; q < NB; ++q)
+#pragma unroll
+            for (int c = 0; c < H; ++c) acc[c] += l[q] * sh.Lkj[c0 + c][q];
+#pragma unroll
+        for (int c = 0; c < H; ++c) A[(size_t)r * (NB + 1) + c0 + c] -= acc[c];
+    }
+}
+
+template <int NB>
+__device__ __forceinline__ void coop_finalize(double* __restrict__ A, double* __restrict__ Lg, double* __restrict__ Linvg, int n,
+                              int w, int j0, int jb, int rows, CoopShared<NB>& sh, int32_t* __restrict__ status,
+                              int64_t* __restrict__ ft) {
+    const int tid = threadIdx.x;
+#define FT(i) if (ft && tid == 0) ft[i] = wall_clock64();
+    FT(0)
+    if (w > 0) {
+        const int k0 = j0 - NB;  // previous panel (always NB wide)
+        for (int t = tid; t < NB * NB; t += kCoopThreads) {
+            const int c = t / NB, q = t % NB;
+            sh.Lkj[c][q] = c < jb ? Lg[(size_t)(j0 + c) * n + k0 + q] : 0.0;
+        }
+        __syncthreads();
+        for (int t = tid; t < jb * jb; t += kCoopThreads) {  // diagonal block (lower)
+            const int r = t / jb, c = t % jb;
+            if (c > r) continue;
+            double acc = 0;
+#pragma unroll 8
+            for (int q = 0; q < NB; ++q) acc += sh.Lkj[r][q] * sh.Lkj[c][q];
+            A[(size_t)r * (NB + 1) + c] -= acc;
+        }
+        __syncthreads();
+    }
+    FT(1)
+    // ---- left-looking Cholesky of the diagonal block, one wave, lane i = row i
+    if (tid < 64) {
+        const int i = tid;
+        double Lrow[NB];
+        bool bad = false;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            Lrow[j] = 0.0;
+            if (j < jb) {
+                double d = A[(size_t)j * (NB + 1) + j], s = (i > j && i < jb) ? A[(size_t)i * (NB + 1) + j] : 0.0;
+#pragma unroll
+                for (int k = 0; k < j; ++k) {
+                    const double ljk = A[(size_t)j * (NB + 1) + k];
+                    d -= ljk * ljk;
+                    s -= Lrow[k] * ljk;
+                }
+                bad |= !(d > 0.0);
+                const double lj = sqrt(d), rl = 1.0 / lj;
+                if (i == j) {
+                    Lrow[j] = lj;
+                    A[(size_t)i * (NB + 1) + j] = lj;
+                } else if (i > j && i < jb) {
+                    Lrow[j] = s * rl;
+                    A[(size_t)i * (NB + 1) + j] = Lrow[j];
+                }
+                __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the row is visible to the next step
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        if (i == 0 && bad) atomicOr(status, 1);
+        FT(2)
+        // ---- L_kk^-1: lane c solves L x = e_c (x_r = 0 for r < c)
+        const int c = i;
+        double xcol[NB];
+#pragma unroll
+        for (int r = 0; r < NB; ++r) {
+            double v = 0.0;
+            if (c < jb && r < jb && r >= c) {
+                double acc = (r == c) ? 1.0 : 0.0;
+#pragma unroll
+                for (int k = 0; k < r; ++k)
+                    if (k >= c) acc -= A[(size_t)r * (NB + 1) + k] * xcol[k];
+                v = acc / A[(size_t)r * (NB + 1) + r];
+            }
+            xcol[r] = v;
+        }
+        if (c < NB) {
+#pragma unroll
+            for (int r = 0; r < NB; ++r) sh.Linv[r][c] = xcol[r];
+        }
+    }
+    __syncthreads();
+    FT(3)
+    // ---- panel rows: apply the pending panel, then X = A L_kk^-T (two GEMM passes)
+    if (w > 0) {
+        apply_panel<NB>(A, Lg, n, j0, j0 - NB, jb, rows, sh);
+        __syncthreads();
+    }
+    FT(4)
+    for (int r = jb + tid; r < rows; r += kCoopThreads) {  // one row per thread: X[r] = A[r] L_kk^-T
+        asm volatile("" ::: "memory");
+        double a[NB];
+#pragma unroll
+        for (int q = 0; q < NB; ++q) a[q] = A[(size_t)r * (NB + 1) + q];
+#pragma unroll
+        for (int c = 0; c < NB; ++c) {
+            double acc = 0;
+#pragma unroll
+            for (int q = 0; q <= c; ++q) acc += a[q] * sh.Linv[c][q];
+            A[(size_t)r * (NB + 1) + c] = acc;
+        }
+    }
+    __syncthreads();
+    FT(5)
+    // ---- publish L rows of this block column and L_kk^-1
+    for (int t = tid; t < rows * jb; t += kCoopThreads) {
+        const int r = t / jb, c = t % jb;
+        Lg[(size_t)(j0 + r) * n + j0 + c] = (r < jb && c > r) ? 0.0 : A[(size_t)r * (NB + 1) + c];
+    }
+    for (int t = tid; t < NB * NB; t += kCoopThreads) Linvg[(size_t)w * NB * NB + t] = sh.Linv[t / NB][t % NB];
+    __threadfence();
+    FT(6)
+#undef FT
+}
+
+template <int NB>
+__global__ __launch_bounds__(kCoopThreads) void k_ba_chol_coop(int n, const double* __restrict__ S,
+                                                                double* __restrict__ Lg, double* __restrict__ Linvg,
+                                                                const double* __restrict__ b, double* __restrict__ x,
+                                                                int32_t* __restrict__ status, int64_t* __restrict__ trace) {
+    namespace cg = cooperative_groups;
+    cg::grid_group grid = cg::this_grid();
+    extern __shared__ double lds[];
+    __shared__ CoopShared<NB> sh;
+    const int tid = threadIdx.x, w = blockIdx.x;
+    const int nbc = (n + NB - 1) / NB;
+    const bool rhs = (w == nbc);
+    const int j0 = w * NB, jb = rhs ? 0 : min(NB, n - j0), rows = rhs ? 0 : n - j0;
+    double* A = lds;  // column owner: [rows][NB + 1]; rhs owner: y [n]
+    if (!rhs) {
+        for (int t = tid; t < rows * NB; t += kCoopThreads) {
+            const int r = t / NB, c = t % NB;
+            A[(size_t)r * (NB + 1) + c] = c < jb ? S[(size_t)(j0 + r) * n + j0 + c] : 0.0;
+        }
+    } else {
+        for (int i = tid; i < n; i += kCoopThreads) A[i] = b[i];
+    }
+    __syncthreads();
+    if (trace && tid == 0 && w == 0) { trace[200] = wall_clock64(); trace[201] = clock64(); }
+    if (w == 0) coop_finalize<NB>(A, Lg, Linvg, n, 0, j0, jb, rows, sh, status, trace ? trace + 64 : nullptr);
+    if (trace && tid == 0 && w == 0) { trace[202] = wall_clock64(); trace[203] = clock64(); }
+    if (trace && tid == 0 && w == 0) trace[0] = wall_clock64();
+    for (int k = 0; k < nbc; ++k) {
+        const int k0 = k * NB, kb = min(NB, n - k0);
+        grid.sync();  // panel k and L_kk^-1 are published
+        if (trace && tid == 0 && w == k + 1) trace[1 + 2 * k] = wall_clock64();
+        if (w == k + 1 && !rhs) {
+            coop_finalize<NB>(A, Lg, Linvg, n, w, j0, jb, rows, sh, status, trace ? trace + 64 + 8 * w : nullptr);
+            if (trace && tid == 0) trace[2 + 2 * k] = wall_clock64();
+        } else if (w > k + 1 && !rhs) {
+            for (int t = tid; t < NB * NB; t += kCoopThreads) {
+                const int c = t / NB, q = t % NB;
+                sh.Lkj[c][q] = (c < jb && q < kb) ? Lg[(size_t)(j0 + c) * n + k0 + q] : 0.0;
+            }
+            __syncthreads();
+            apply_panel<NB>(A, Lg, n, j0, k0, 0, rows, sh);
+            __syncthreads();
+        } else if (rhs) {
+            // forward block k: y_k = L_kk^-1 y_k; y_i -= L[i][k0:k1] y_k for i >= k1
+            for (int t = tid; t < NB * NB; t += kCoopThreads) sh.Linv[t / NB][t % NB] = Linvg[(size_t)k * NB * NB + t];
+            __syncthreads();
+            if (tid < NB) {
+                double acc = 0;
+#pragma unroll 8
+                for (int q = 0; q < NB; ++q) acc += sh.Linv[tid][q] * (q < kb ? A[k0 + q] : 0.0);
+                sh.yb[tid] = tid < kb ? acc : 0.0;
+            }
+            __syncthreads();
+            if (tid < kb) A[k0 + tid] = sh.yb[tid];
+            for (int i = k0 + kb + tid; i < n; i += kCoopThreads) {
+                const double* lrow = Lg + (size_t)i * n + k0;
+                double l[NB];
+#pragma unroll
+                for (int q = 0; q < NB; ++q) l[q] = q < kb ? lrow[q] : 0.0;
+                double s2 = 0;
+#pragma unroll
+                for (int q = 0; q < NB; ++q) s2 += l[q] * sh.yb[q];
+                A[i] -= s2;
+            }
+            __syncthreads();
+        }
+    }
+    if (!rhs) return;
+    if (trace && tid == 0) trace[2 * nbc + 1] = wall_clock64();
+    // backward: L^T x = y, block by block from the bottom, with L_kk^-T
+    for (int k = nbc - 1; k >= 0; --k) {
+        const int k0 = k * NB, kb = min(NB, n - k0);
+        for (int t = tid; t < NB * NB; t += kCoopThreads) sh.Linv[t / NB][t % NB] = Linvg[(size_t)k * NB * NB + t];
+        __syncthreads();
+        if (tid < NB) {  // x_c = sum_r Linv[r][c] y_r
+            double acc = 0;
+#pragma unroll 8
+            for (int r = 0; r < NB; ++r) acc += sh.Linv[r][tid] * (r < kb ? A[k0 + r] : 0.0);
+            sh.yb[tid] = tid < kb ? acc : 0.0;
+        }
+        __syncthreads();
+        if (tid < kb) A[k0 + tid] = sh.yb[tid];
+        for (int j = tid; j < k0; j += kCoopThreads) {
+            double l[NB];
+#pragma unroll
+            for (int c = 0; c < NB; ++c) l[c] = c < kb ? Lg[(size_t)(k0 + c) * n + j] : 0.0;
+            double s2 = 0;
+#pragma unroll
+            for (int c = 0; c < NB; ++c) s2 += l[c] * sh.yb[c];
+            A[j] -= s2;
+        }
+        __syncthreads();
+    }
+    for (int i = tid; i < n; i += kCoopThreads) x[i] = A[i];
+    if (trace && tid == 0) trace[2 * nbc + 2] = wall_clock64();
+}
+
 // x_l = Dinv (b_l - sum_e Hpl_e^T x_pose(e))
-__global__ __launch_bounds__(kT) void k_ba_backsub(int nl, int n, const int32_t* __restrict__ off,
+__global__ __launch_bounds__(kT) void k_ba_backsub(int nl, int n, double lambda, const int32_t* __restrict__ off,
                                                    const int32_t* __restrict__ eidx, const EdgeDev* __restrict__ edges,
                                                    const int32_t* __restrict__ pose_h, const double* __restrict__ hpl,
-                                                   const double* __restrict__ bl, const double* __restrict__ dinv,
+                                                   const double* __restrict__ bl, const double* __restrict__ hll,
                                                    double* __restrict__ x) {
     const int l = blockIdx.x * kT + threadIdx.x;
     if (l >= nl) return;
@@ -590,7 +890,8 @@ __global__ __launch_bounds__(kT) void k_ba_backsub(int nl, int n, const int32_t*
         for (int c = 0; c < 3; ++c)
             for (int r = 0; r < 6; ++r) cl[c] += H[3 * r + c] * -xp[r];
     }
-    const double* Di = dinv + 9 * (size_t)l;
+    double Di[9];
+    land_dinv(hll, l, lambda, Di);
     for (int r = 0; r < 3; ++r) x[n + 3 * (size_t)l + r] = Di[3 * r] * cl[0] + Di[3 * r + 1] * cl[1] + Di[3 * r + 2] * cl[2];
 }
 
@@ -699,22 +1000,22 @@ struct DevBuf {
 
 struct orb_ba_s {
     hipStream_t stream = nullptr;
-    DevBuf<double> pose, pose_bak, point, point_bak, err, rho0, ecl, hpl, ecp, hpp, hll, b, dinv, z, cb, S, bs, x, scal;
+    DevBuf<double> pose, pose_bak, point, point_bak, err, rho0, ecl, hpl, ecp, hpp, hll, b, z, cb, S, LT, Linv, bs, x, scal;
     DevBuf<EdgeDev> edges;
     DevBuf<orb_ba_camera_t> cams;
-    DevBuf<int32_t> pose_h, free_pose, land_point, land_off, land_edge, landf_off, landf_edge, pose_off, pose_edge,
+    DevBuf<int32_t> pose_h, free_pose, land_point, land_off, land_edge, landf_off, landf_edge, fland, pose_off, pose_edge,
         blk_i, blk_j, blk_off, pair_a, pair_b, status;
     DevBuf<uint8_t> depth;
     double* h_scal = nullptr;  // pinned: [0] chi2, [1] scale, [2] status, [3] maxdiag
     float ms_total = 0;
 
     void release() {
-        for (auto* d : {&pose, &pose_bak, &point, &point_bak, &err, &rho0, &ecl, &hpl, &ecp, &hpp, &hll, &b, &dinv, &z,
-                        &cb, &S, &bs, &x, &scal})
+        for (auto* d : {&pose, &pose_bak, &point, &point_bak, &err, &rho0, &ecl, &hpl, &ecp, &hpp, &hll, &b, &z,
+                        &cb, &S, &LT, &Linv, &bs, &x, &scal})
             d->release();
         edges.release();
         cams.release();
-        for (auto* d : {&pose_h, &free_pose, &land_point, &land_off, &land_edge, &landf_off, &landf_edge, &pose_off,
+        for (auto* d : {&pose_h, &free_pose, &land_point, &land_off, &land_edge, &landf_off, &landf_edge, &fland, &pose_off,
                         &pose_edge, &blk_i, &blk_j, &blk_off, &pair_a, &pair_b, &status})
             d->release();
         depth.release();
@@ -808,8 +1109,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     }
     if (stop()) { res->stopped = 1; return ORB_ERR_ABORTED; }
     const int n = 6 * nf, m = 3 * nl;
-    if (n > 6 * 300) return orbgpu_fail(ORB_ERR_ARG, "more than 300 free keyframes in one local BA");
-
+    
     // landmark -> all edges (edge order), landmark -> free-pose edges (pose row ascending), pose -> edges
     std::vector<int32_t> land_off(nl + 1, 0), land_edge(ne), landf_off(nl + 1, 0), landf_edge, pose_off(nf + 1, 0),
         pose_edge;
@@ -839,6 +1139,10 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     for (int l = 0; l < nl; ++l)
         std::stable_sort(landf_edge.begin() + landf_off[l], landf_edge.begin() + landf_off[l + 1],
                          [&](int a, int b) { return pose_h[pr->edges[a].pose] < pose_h[pr->edges[b].pose]; });
+    const int nfe = (int)landf_edge.size();
+    std::vector<int32_t> fland(nfe);
+    for (int l = 0; l < nl; ++l)
+        for (int k = landf_off[l]; k < landf_off[l + 1]; ++k) fland[k] = l;
     // Schur block pattern: (row_a <= row_b) products per landmark, in landmark order
     std::vector<int32_t> blk_id((size_t)nf * nf, -1), blk_i, blk_j;
     std::vector<int32_t> cnt;
@@ -881,14 +1185,14 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
               upload(h->cams, pr->pose_camera, np, s) && upload(h->pose_h, pose_h, s) &&
               upload(h->free_pose, free_pose, s) && upload(h->land_point, land_point, s) &&
               upload(h->land_off, land_off, s) && upload(h->land_edge, land_edge, s) &&
-              upload(h->landf_off, landf_off, s) && upload(h->landf_edge, landf_edge, s) &&
+              upload(h->landf_off, landf_off, s) && upload(h->landf_edge, landf_edge, s) && upload(h->fland, fland, s) &&
               upload(h->pose_off, pose_off, s) && upload(h->pose_edge, pose_edge, s) && upload(h->blk_i, blk_i, s) &&
               upload(h->blk_j, blk_j, s) && upload(h->blk_off, blk_off, s) && upload(h->pair_a, pair_a, s) &&
               upload(h->pair_b, pair_b, s) && h->err.grow(3 * (size_t)ne) && h->rho0.grow(ne) &&
               h->ecl.grow(12 * (size_t)ne) && h->hpl.grow(18 * (size_t)ne) && h->ecp.grow(42 * (size_t)ne) &&
               h->hpp.grow(36 * (size_t)nf) && h->hll.grow(9 * (size_t)nl) && h->b.grow(n + m) &&
-              h->dinv.grow(9 * (size_t)nl) && h->z.grow(18 * (size_t)ne) && h->cb.grow(6 * (size_t)ne) &&
-              h->S.grow((size_t)n * n) && h->bs.grow(n) && h->x.grow(n + m) && h->scal.grow(8) && h->status.grow(1) &&
+h->z.grow(18 * (size_t)ne) && h->cb.grow(6 * (size_t)ne) &&
+              h->S.grow((size_t)n * n) && h->LT.grow((size_t)n * n) && h->Linv.grow((size_t)n * 32 + 32 * 32) && h->bs.grow(n) && h->x.grow(n + m) && h->scal.grow(8) && h->status.grow(1) &&
               h->depth.grow(ne);
     if (!ok) return orbgpu_fail(ORB_ERR_DEVICE, "BA device allocation / upload");
     hipMemsetAsync(h->x.p, 0, sizeof(double) * (n + m), s);  // g2o's _x starts zeroed
@@ -896,15 +1200,35 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     const float dm = (float)std::sqrt(5.991), ds = (float)std::sqrt(7.815);  // src/Optimizer.cc:1957-1958
     const Huber2 hub{(double)dm, (double)ds, (float)((double)dm * (double)dm), (float)((double)ds * (double)ds)};
     // dynamic LDS of the Cholesky kernel: panel rows (n x (NB + 1)) + y (n)
-    int nb = 32;
-    size_t chol_lds = sizeof(double) * ((size_t)n * (nb + 1) + n);
-    if (chol_lds > 150 * 1024) { nb = 16; chol_lds = sizeof(double) * ((size_t)n * (nb + 1) + n); }
-    if (chol_lds > 150 * 1024) { nb = 8; chol_lds = sizeof(double) * ((size_t)n * (nb + 1) + n); }
+    // cooperative path: block column rows x (NB + 1) doubles per workgroup (rhs owner: n doubles)
+    auto coop_bytes = [&](int b) { return sizeof(double) * (size_t)n * (b + 1); };
+    int coop_nb = 0;
+    if (coop_bytes(32) <= 136 * 1024) coop_nb = 32;
+    else if (coop_bytes(16) <= 136 * 1024) coop_nb = 16;
+    {
+        static int coop_ok = -1;
+        if (coop_ok < 0) {
+            int dev = 0, v = 0;
+            hipGetDevice(&dev);
+            coop_ok = (hipDeviceGetAttribute(&v, hipDeviceAttributeCooperativeLaunch, dev) == hipSuccess && v) ? 1 : 0;
+            hipFuncSetAttribute((const void*)k_ba_chol_coop<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 136 * 1024);
+            hipFuncSetAttribute((const void*)k_ba_chol_coop<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 136 * 1024);
+            (void)hipGetLastError();
+        }
+        if (!coop_ok || !getenv("ORBGPU_BA_COOP")) coop_nb = 0;  // the single-workgroup kernel is the default
+    }
+    const size_t coop_lds = coop_nb ? coop_bytes(coop_nb) : 0;
+    int nb = 16;
+    auto lds_bytes = [&](int b) { return sizeof(double) * ((size_t)b * n + (size_t)n * (b + 1) + n); };
+    if (lds_bytes(nb) > 150 * 1024) nb = 8;
+    const size_t chol_lds = lds_bytes(nb);
+    if (chol_lds > 150 * 1024 && !coop_nb)
+        return orbgpu_fail(ORB_ERR_ARG, "too many free keyframes for the on-chip Cholesky");
     static bool attr_set = false;
     if (!attr_set) {
-        hipFuncSetAttribute((const void*)k_ba_chol<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
         hipFuncSetAttribute((const void*)k_ba_chol<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
         hipFuncSetAttribute((const void*)k_ba_chol<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+        (void)hipGetLastError();
         attr_set = true;
     }
     double* bl = h->b.p + n;
@@ -950,29 +1274,70 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         int qmax = 0;
         do {
             // setLambda + BlockSolver::solve
-            hipLaunchKernelGGL(k_ba_schur_land, dim3(grid(nl)), dim3(kT), 0, s, nl, lambda, h->landf_off.p,
-                               h->landf_edge.p, h->hll.p, bl, h->hpl.p, h->dinv.p, h->z.p, h->cb.p);
+            if (nfe)
+                hipLaunchKernelGGL(k_ba_schur_edges, dim3(grid(nfe)), dim3(kT), 0, s, nfe, lambda, h->landf_edge.p,
+                                   h->fland.p, h->hll.p, bl, h->hpl.p, h->z.p, h->cb.p);
             if (nf) {
                 hipMemsetAsync(h->S.p, 0, sizeof(double) * (size_t)n * n, s);
-                hipLaunchKernelGGL(k_ba_schur_blocks, dim3((nblk + 3) / 4), dim3(256), 0, s, nblk, n, lambda,
-                                   h->blk_i.p, h->blk_j.p, h->blk_off.p, h->pair_a.p, h->pair_b.p, h->z.p, h->hpl.p,
-                                   h->hpp.p, h->S.p);
+                hipLaunchKernelGGL(k_ba_schur_blocks, dim3(nblk), dim3(64), 0, s, n, lambda, h->blk_i.p, h->blk_j.p,
+                                   h->blk_off.p, h->pair_a.p, h->pair_b.p, h->z.p, h->hpl.p, h->hpp.p, h->S.p);
                 hipLaunchKernelGGL(k_ba_schur_rhs, dim3(nf), dim3(64), 0, s, h->pose_off.p, h->pose_edge.p, h->cb.p,
                                    h->b.p, h->bs.p);
-                if (nb == 32)
-                    hipLaunchKernelGGL(k_ba_chol<32>, dim3(1), dim3(kCholThreads), chol_lds, s, n, h->S.p, h->bs.p,
-                                       h->x.p, h->status.p);
-                else if (nb == 16)
-                    hipLaunchKernelGGL(k_ba_chol<16>, dim3(1), dim3(kCholThreads), chol_lds, s, n, h->S.p, h->bs.p,
-                                       h->x.p, h->status.p);
+                if (coop_nb) {
+                    hipMemsetAsync(h->status.p, 0, sizeof(int32_t), s);
+                    int nn = n;
+                    double* Sp = h->S.p;
+                    double* Lp = h->LT.p;
+                    double* bp = h->bs.p;
+                    double* xp = h->x.p;
+                    int32_t* stp = h->status.p;
+                    static int64_t* d_trace = nullptr;
+                    static const bool tracing = getenv("ORBGPU_BA_TRACE") != nullptr;
+                    if (tracing && !d_trace) hipMalloc(&d_trace, 8 * 1024 * sizeof(int64_t));
+                    int64_t* trp = tracing ? d_trace : nullptr;
+                    double* Lip = h->Linv.p;
+                    void* args[] = {&nn, &Sp, &Lp, &Lip, &bp, &xp, &stp, &trp};
+                    const dim3 g((n + coop_nb - 1) / coop_nb + 1);
+                    const hipError_t le =
+                        coop_nb == 32
+                            ? hipLaunchCooperativeKernel((const void*)k_ba_chol_coop<32>, g, dim3(kCoopThreads), args,
+                                                         (unsigned)coop_lds, s)
+                            : hipLaunchCooperativeKernel((const void*)k_ba_chol_coop<16>, g, dim3(kCoopThreads), args,
+                                                         (unsigned)coop_lds, s);
+                    if (le != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "cooperative Cholesky launch failed");
+                    if (tracing) {
+                        const int nbc = (n + coop_nb - 1) / coop_nb;
+                        std::vector<int64_t> tr(2 * nbc + 3);
+                        hipMemcpyAsync(tr.data(), d_trace, tr.size() * 8, hipMemcpyDeviceToHost, s);
+                        hipStreamSynchronize(s);
+                        for (int k = 0; k + 1 < nbc; ++k)
+                            fprintf(stderr, "k=%d sync seen %.2f finalize(k+1) done %.2f us\n", k,
+                                    (tr[1 + 2 * k] - tr[0]) / 100.0, (tr[2 + 2 * k] - tr[0]) / 100.0);
+                        fprintf(stderr, "backward start %.2f end %.2f us\n", (tr[2 * nbc + 1] - tr[0]) / 100.0,
+                                (tr[2 * nbc + 2] - tr[0]) / 100.0);
+                        std::vector<int64_t> clk(4);
+                        hipMemcpy(clk.data(), d_trace + 200, 32, hipMemcpyDeviceToHost);
+                        fprintf(stderr, "shader clock estimate: %.1f MHz\n",
+                                100.0 * (double)(clk[3] - clk[1]) / (double)(clk[2] - clk[0]));
+                        std::vector<int64_t> ft(8 * nbc);
+                        hipMemcpy(ft.data(), d_trace + 64, ft.size() * 8, hipMemcpyDeviceToHost);
+                        for (int w = 0; w < nbc; ++w)
+                            fprintf(stderr, "finalize w=%d: diag-upd %.2f chain %.2f inv %.2f apply %.2f gemm %.2f pub %.2f us\n", w,
+                                    (ft[8 * w + 1] - ft[8 * w]) / 100.0, (ft[8 * w + 2] - ft[8 * w + 1]) / 100.0,
+                                    (ft[8 * w + 3] - ft[8 * w + 2]) / 100.0, (ft[8 * w + 4] - ft[8 * w + 3]) / 100.0,
+                                    (ft[8 * w + 5] - ft[8 * w + 4]) / 100.0, (ft[8 * w + 6] - ft[8 * w + 5]) / 100.0);
+                    }
+                } else if (nb == 16)
+                    hipLaunchKernelGGL(k_ba_chol<16>, dim3(1), dim3(kCholThreads), chol_lds, s, n, h->S.p, h->LT.p,
+                                       h->bs.p, h->x.p, h->status.p);
                 else
-                    hipLaunchKernelGGL(k_ba_chol<8>, dim3(1), dim3(kCholThreads), chol_lds, s, n, h->S.p, h->bs.p,
-                                       h->x.p, h->status.p);
+                    hipLaunchKernelGGL(k_ba_chol<8>, dim3(1), dim3(kCholThreads), chol_lds, s, n, h->S.p, h->LT.p,
+                                       h->bs.p, h->x.p, h->status.p);
             } else {
                 hipMemsetAsync(h->status.p, 0, sizeof(int32_t), s);
             }
-            hipLaunchKernelGGL(k_ba_backsub, dim3(grid(nl)), dim3(kT), 0, s, nl, n, h->landf_off.p, h->landf_edge.p,
-                               h->edges.p, h->pose_h.p, h->hpl.p, bl, h->dinv.p, h->x.p);
+            hipLaunchKernelGGL(k_ba_backsub, dim3(grid(nl)), dim3(kT), 0, s, nl, n, lambda, h->landf_off.p,
+                               h->landf_edge.p, h->edges.p, h->pose_h.p, h->hpl.p, bl, h->hll.p, h->x.p);
             // SparseOptimizer::update (push first), then computeActiveErrors
             hipLaunchKernelGGL(k_ba_update, dim3(grid(nf + nl)), dim3(kT), 0, s, nf, nl, n, h->free_pose.p,
                                h->land_point.p, h->x.p, h->pose.p, h->pose_bak.p, h->point.p, h->point_bak.p);
