@@ -102,6 +102,79 @@ def cpu_baseline(oracle_mod, frames, budget_s=10.0):
                       "oracle/orb_extractor_oracle.cpp -O2"}
 
 
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (= FP64 matrix) peak, AMD spec; not listed in MI355X_MICROARCH.md
+
+
+def ba_flops_per_iteration(prob):
+    """Algorithmic FP64 FLOPs of one LM iteration with one trial."""
+    import numpy as np
+    e = prob["edges"]
+    ne = len(e)
+    free = np.asarray(prob["pose_fixed"]) == 0
+    nfree = int(free.sum())
+    fe = free[e["pose"]]
+    per_point = np.bincount(e["point"][fe], minlength=len(prob["point"]))
+    pairs = int((per_point * (per_point + 1) // 2).sum())
+    n = 6 * nfree
+    return (ne * 450            # error, Jacobians, Huber weight, quadratic-form parts
+            + 2 * ne * 30       # the trial's error re-evaluation + chi2
+            + int(fe.sum()) * (150 + 36)   # Z = Hpl Dinv, Hpl db, back-substitution
+            + pairs * 216       # Schur block products
+            + n ** 3 // 3 + 4 * n * n)     # Cholesky + two triangular solves
+
+
+def bench_local_ba(pkg, synth, world, dev, steps, cpu_baseline_on):
+    """C5: LocalBundleAdjustment's optimize(10) on 50 KF / 2000 MP / ~12k edges, one independent
+    problem per rank (replicas).  Returns the localba object of the JSON line (rank 0)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    prob = synth.local_ba_problem(n_kf=50, n_points=2000, obs_per_point=6, stereo_frac=0.0, seed=7)
+    ba = pkg.LocalBA()
+    for _ in range(2):
+        ba.optimize(prob, 10)
+    reps = max(3, min(steps, 20))
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    iters = 0
+    res = None
+    for _ in range(reps):
+        _, _, _, _, res = ba.optimize(prob, 10)
+        iters += res["iterations"]
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) * 1e3
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    iter_ms = dt / iters
+    flops = ba_flops_per_iteration(prob)
+    achieved = flops / (iter_ms * 1e-3) / 1e12
+    out = {"config": "C5: 50 keyframes (2 fixed) / 2000 map points / %d mono edges, optimize(10), "
+                     "one independent problem per GPU (replicas)" % len(prob["edges"]),
+           "iter_ms": round(iter_ms, 4), "solve_ms": round(dt / reps, 4), "iterations": res["iterations"],
+           "trials": res["trials"], "dtype": "f64",
+           "roofline": {"bound": "fp64", "achieved": round(achieved, 5), "peak": FP64_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 7),
+                        "flops_per_iteration": int(flops)}}
+    if cpu_baseline_on:
+        from oracle import oracle as oracle_mod
+        t0 = time.perf_counter()
+        nrep = 0
+        it_cpu = 0
+        while time.perf_counter() - t0 < 3.0 or nrep < 2:
+            _, _, _, _, r = oracle_mod.local_ba(prob, 10)
+            it_cpu += r["iterations"]
+            nrep += 1
+        cdt = (time.perf_counter() - t0) * 1e3
+        out["cpu_baseline"] = {"value": round(cdt / it_cpu, 4), "unit": "ms/iteration", "cores": 1, "kind": "port",
+                               "sample": f"{nrep} solves of the same C5 problem, oracle/orb_ba_oracle.cpp -O2, "
+                                         "one thread (g2o is built without OpenMP)"}
+    return out
+
+
 def pmc_traffic():
     p = ROOT / "profiles" / "pmc_latest.json"
     if p.exists():
@@ -120,6 +193,7 @@ def main():
     ap.add_argument("--frames", type=int, default=FRAMES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-ba", action="store_true", help="skip the LocalBA (C5) measurement")
     args = ap.parse_args()
 
     import numpy as np
@@ -211,11 +285,16 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "algorithmic_bytes_per_launch": int(dom_bytes)},
-            "localba_iter_ms": None,
         }
         if not args.no_cpu_baseline and world == 1:
             from oracle import oracle as oracle_mod
             result["cpu_baseline"] = cpu_baseline(oracle_mod, frames[: min(nfr, 32)], args.cpu_budget)
+    localba = None
+    if not args.no_ba:
+        localba = bench_local_ba(pkg, synth, world, dev, args.steps, rank == 0 and world == 1 and not args.no_cpu_baseline)
+    if rank == 0:
+        result["localba_iter_ms"] = localba["iter_ms"] if localba else None
+        result["localba"] = localba
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Turn rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py into profiles/pmc_latest.json.
+
+FETCH_SIZE and WRITE_SIZE are in KiB per dispatch.  Per MI355X_MICROARCH.md (HBM section) gfx950's
+FETCH_SIZE counts half the bytes of wide coalesced reads, so it is doubled.  Totals are per step of
+the stage, summed over the stage's launches, to match bench.py's roofline.achieved.
+"""
+import collections
+import csv
+import glob
+import json
+import re
+import sys
+
+STAGE_KERNELS = {"pyramid": ["k_pyramid_level"], "fast": ["k_fast_cells"], "quadtree": ["k_quadtree"],
+                 "describe": ["k_describe"]}
+
+
+def main(d, out, frames=64):
+    per = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(float)))
+    for f in sorted(glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)):
+        for row in csv.DictReader(open(f)):
+            m = re.search(r"(k_[a-z0-9_]+)", row["Kernel_Name"])
+            if not m:
+                continue
+            per[m.group(1)][row["Counter_Name"]][int(row["Dispatch_Id"])] += float(row["Counter_Value"])
+    res = {"frames_per_launch": frames, "unit_note": "bytes per step of the stage (all its launches); "
+           "FETCH_SIZE doubled for the gfx950 half-count of wide reads", "stages": {}}
+    for stage, ks in STAGE_KERNELS.items():
+        fetch = write = 0.0
+        launches = 0
+        for k in ks:
+            cs = per.get(k, {})
+            fd = cs.get("FETCH_SIZE", {})
+            wd = cs.get("WRITE_SIZE", {})
+            if not fd:
+                continue
+            # per-dispatch averages x launches per step (pyramid: 8 launches per step)
+            nper = 8 if stage == "pyramid" else 1
+            fetch += 2 * 1024 * sum(fd.values()) / len(fd) * nper
+            if wd:
+                write += 1024 * sum(wd.values()) / len(wd) * nper
+            launches = nper
+        if launches:
+            res["stages"][stage] = {"fetch_bytes": fetch, "write_bytes": write, "hbm_bytes": fetch + write}
+    dom = max(res["stages"], key=lambda s: res["stages"][s]["hbm_bytes"]) if res["stages"] else None
+    res["kernel_stage"] = "pyramid" if "pyramid" in res["stages"] else dom
+    if res["kernel_stage"]:
+        res["hbm_bytes_per_launch"] = res["stages"][res["kernel_stage"]]["hbm_bytes"]
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

@@ -3,7 +3,7 @@
 # bench's kernels.  Usage (on the GPU box): tools/pmc_run.sh OUTDIR "bench args"
 set -u
 OUT=${1:-gpurun_out/pmc}
-ARGS=${2:---steps 3 --warmup 1 --no-cpu-baseline}
+ARGS=${2:---steps 3 --warmup 1 --no-cpu-baseline --no-ba}
 export TMPDIR=/tmp
 mkdir -p "$OUT"
 i=0
@@ -12,8 +12,8 @@ while read -r line; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $line --kernel-trace --output-format csv -d "$OUT" -o "pass$i" -- python3 bench.py $ARGS > "$OUT/pass$i.log" 2>&1 || { echo "pass $i failed"; exit 1; }
 done <<'PASSES'
-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE
-SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES
+
+
 FETCH_SIZE
 WRITE_SIZE
 PASSES
