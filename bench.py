@@ -203,8 +203,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")  # "gloo": multi-rank rehearsal on one GPU
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group(backend, init_method="env://")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -220,10 +222,25 @@ def main():
            torch.empty((nfr, cap, 32), dtype=torch.uint8, device=dev),
            torch.empty((nfr, 2), dtype=torch.int32, device=dev))
     stream = torch.cuda.current_stream(dev)
+    sharded = None
+    if world > 1:
+        # C4 data path: every step all-gathers the features of all ranks' frames (RCCL over xGMI),
+        # asynchronously and double-buffered so it overlaps the next step's extraction
+        from orbslam3_amd.distributed import ShardedExtractor
+        sharded = ShardedExtractor(ex, nfr, cap)
+
+    def step():
+        if sharded is None:
+            ex.extract_batch_device(imgs, (0, 1000), cap=cap, out=out, stream=stream)
+        else:
+            sharded.step(imgs, (0, 1000), stream=stream)
+
     for _ in range(args.warmup):
-        ex.extract_batch_device(imgs, (0, 1000), cap=cap, out=out, stream=stream)
+        step()
+    if sharded is not None:
+        sharded.finish()
     torch.cuda.synchronize(dev)
-    counts = out[2].cpu().numpy()
+    counts = (out[2] if sharded is None else sharded.local.counts[(args.warmup - 1) % 2]).cpu().numpy()
     feats_per_step = int(counts[:, 0].sum())
     if (counts[:, 1] < 0).any():
         raise RuntimeError("a frame exceeded the keypoint capacity")
@@ -235,7 +252,9 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        ex.extract_batch_device(imgs, (0, 1000), cap=cap, out=out, stream=stream)
+        step()
+    if sharded is not None:
+        sharded.finish()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -280,7 +299,8 @@ def main():
                                    "extraction+description (ORBextractor::operator())",
                        "frames_per_gpu": nfr, "width": WIDTH, "height": HEIGHT, "nfeatures": NFEAT,
                        "nlevels": NLEVELS, "features_per_step_per_gpu": feats_per_step,
-                       "parallelism": f"frame-sharded x{world}"},
+                       "parallelism": f"frame-sharded x{world}" + (
+                           f", all-gather of descriptors+keypoints ({backend})" if world > 1 else "")},
             "stages_ms": {k: round(v, 4) for k, v in per_step.items()},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,

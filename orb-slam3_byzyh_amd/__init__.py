@@ -10,5 +10,6 @@ from .extractor import ORBextractor, keypoints_to_structured
 from .keyframe import KeyFrame
 from .matcher import ORBmatcher
 from .optimizer import LocalBA, local_bundle_adjustment
+from . import distributed
 
 __all__ = ["ORBextractor", "ORBmatcher", "KeyFrame", "LocalBA", "local_bundle_adjustment", "KEYPOINT_DTYPE", "OrbGpuError", "keypoints_to_structured", "_lib"]

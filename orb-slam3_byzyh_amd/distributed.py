@@ -1,0 +1,99 @@
+"""Frame-sharded batch extraction across GPUs with an all-gather of the features (C4).
+
+One process per GPU (torch.distributed, backend "nccl" = RCCL on ROCm; "gloo" on CPU for tests).
+Frames are independent units.  Rank r extracts frames [r*B, (r+1)*B) of the global batch into
+fixed-capacity blocks, then a single all-gather over xGMI gives every rank the features of all
+frames: descriptors [W*B, cap, 32] u8, keypoints [W*B, cap, 7] (cv::KeyPoint layout) and counts
+[W*B, 2].  Cross-frame matching then runs locally against the gathered set (knn2 of a frame's
+descriptors vs. the other frames', src/ORBmatcher.cc DescriptorDistance).
+
+The all-gather is the only data-path collective.  It is issued asynchronously on RCCL's stream
+and double-buffered, so step i's exchange overlaps step i+1's extraction.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(n_total: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous frame range of `rank` (the first n_total % world ranks take one extra frame)."""
+    base, extra = divmod(n_total, world)
+    begin = rank * base + min(rank, extra)
+    return begin, begin + base + (1 if rank < extra else 0)
+
+
+class FeatureBlocks:
+    """Fixed-capacity per-frame feature blocks (the extractor's device output layout)."""
+
+    def __init__(self, frames: int, cap: int, device, count: int = 1):
+        self.frames, self.cap = frames, cap
+        self.kps = torch.empty((count, frames, cap, 7), dtype=torch.float32, device=device)
+        self.desc = torch.empty((count, frames, cap, 32), dtype=torch.uint8, device=device)
+        self.counts = torch.empty((count, frames, 2), dtype=torch.int32, device=device)
+
+    def view(self, i: int = 0):
+        return self.kps[i], self.desc[i], self.counts[i]
+
+
+def all_gather_features(kps, desc, counts, group=None, async_op: bool = False):
+    """All-gather one rank's feature blocks; returns (gathered kps, desc, counts[, work handles]).
+    With the gloo backend (CPU tests, single-GPU rehearsals) device tensors are staged on the host."""
+    world = dist.get_world_size(group)
+    if dist.get_backend(group) == "gloo" and kps.is_cuda:
+        out = all_gather_features(kps.cpu(), desc.cpu(), counts.cpu(), group, False)
+        out = tuple(t.to(kps.device) for t in out)
+        return out + ([],) if async_op else out
+    g_kps = torch.empty((world * kps.shape[0],) + tuple(kps.shape[1:]), dtype=kps.dtype, device=kps.device)
+    g_desc = torch.empty((world * desc.shape[0],) + tuple(desc.shape[1:]), dtype=desc.dtype, device=desc.device)
+    g_cnt = torch.empty((world * counts.shape[0],) + tuple(counts.shape[1:]), dtype=counts.dtype,
+                        device=counts.device)
+    works = [dist.all_gather_into_tensor(g_desc, desc.contiguous(), group=group, async_op=async_op),
+             dist.all_gather_into_tensor(g_kps, kps.contiguous(), group=group, async_op=async_op),
+             dist.all_gather_into_tensor(g_cnt, counts.contiguous(), group=group, async_op=async_op)]
+    if async_op:
+        return g_kps, g_desc, g_cnt, works
+    return g_kps, g_desc, g_cnt
+
+
+class ShardedExtractor:
+    """ORB extraction of a global frame batch sharded over the ranks of a process group."""
+
+    def __init__(self, extractor, frames_per_rank: int, cap: int | None = None, group=None):
+        self.ex = extractor
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.frames = frames_per_rank
+        self.cap = cap or (extractor.nfeatures + 16 * extractor.nlevels)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.local = FeatureBlocks(frames_per_rank, self.cap, dev, count=2)
+        self._i = 0
+        self._pending = None
+
+    def step(self, images, vLappingArea=(0, 0), stream=None):
+        """Extract this rank's frames (uint8 [B, H, W] on the GPU) and start the all-gather.
+        Returns the previous step's gathered blocks (or None on the first call)."""
+        buf = self._i % 2
+        out = self.local.view(buf)
+        self.ex.extract_batch_device(images, vLappingArea, cap=self.cap, out=out, stream=stream)
+        prev = self.finish()
+        self._pending = all_gather_features(*out, group=self.group, async_op=True)
+        self._i += 1
+        return prev
+
+    def finish(self):
+        """Wait for the in-flight all-gather and return its (kps, desc, counts)."""
+        if self._pending is None:
+            return None
+        g_kps, g_desc, g_cnt, works = self._pending
+        for w in works:
+            w.wait()
+        self._pending = None
+        return g_kps, g_desc, g_cnt
+
+
+def frame_descriptors(g_desc, g_cnt, frame: int):
+    """Descriptors of global frame `frame` from the gathered blocks (a view, count rows)."""
+    n = int(g_cnt[frame, 0])
+    return g_desc[frame, :n]

@@ -1,0 +1,54 @@
+"""GPU check of the sharded extractor's data path on one rank (RCCL group of size 1).
+
+The gathered blocks must equal a direct batched extraction of the same frames, and the cross-frame
+knn2 on the gathered descriptors must run on the device.  World sizes > 1 are covered by the gloo
+tests in test_distributed_cpu.py and by bench.py --gpus N.
+"""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_sharded_extractor_single_rank(pkg, synth):
+    import torch
+    import torch.distributed as dist
+    from orbslam3_amd import distributed as D
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        frames = torch.from_numpy(synth.frame_batch(4, 640, 480, seed0=500)).cuda()
+        ex = pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=640, max_height=480, max_batch=4)
+        sh = D.ShardedExtractor(ex, 4)
+        assert sh.step(frames, (0, 1000)) is None
+        g_kps, g_desc, g_cnt = sh.finish()
+        kps, desc, cnt = ex.extract_batch_device(frames, (0, 1000), cap=sh.cap)
+        torch.cuda.synchronize()
+        assert torch.equal(g_cnt, cnt)
+        for f in range(4):
+            n = int(cnt[f, 0])
+            assert torch.equal(g_desc[f, :n], desc[f, :n])
+            # int fields (octave, class_id = -1) are punned into the float rows: compare bits
+            assert torch.equal(g_kps[f, :n].view(torch.int32), kps[f, :n].view(torch.int32))
+        # cross-frame matching against the gathered set: frame 0 vs frame 1
+        q = D.frame_descriptors(g_desc, g_cnt, 0).contiguous()
+        t = D.frame_descriptors(g_desc, g_cnt, 1).contiguous()
+        idx, d1, d2 = pkg.ORBmatcher.knn2_device(q, t)
+        qa, ta = q.cpu().numpy(), t.cpu().numpy()
+        D_ = np.unpackbits(qa[:16, None, :] ^ ta[None, :, :], axis=2).sum(axis=2)
+        assert np.array_equal(d1.cpu().numpy()[:16], D_.min(axis=1))
+    finally:
+        dist.destroy_process_group()
