@@ -79,8 +79,10 @@ __device__ __forceinline__ int wave_sum(int v) {
 constexpr int kTileW = 128, kTileH = 16, kHalo = 3;  // 128-byte rows: every store fills whole cache lines
 constexpr int kLW = kTileW + 2 * kHalo, kLH = kTileH + 2 * kHalo;  // 134 x 22
 constexpr int kBoxW = 288, kBoxH = 2 * kLH + 4;  // source box (bytes) for scale factors <= 2
-constexpr int kBoxWords = kBoxW / 4;
 static_assert(kBoxW >= 3 + 2 * kLW + 2, "box too narrow");
+// box for level ratios <= 1.25 (the usual 1.2): 133 * 1.25 + 2 columns + 3 alignment bytes, 21 * 1.25 + 2 rows
+constexpr int kSmallBoxW = 176, kSmallBoxH = 32;
+static_assert(kSmallBoxW >= 3 + (kLW - 1) * 5 / 4 + 3 && kSmallBoxH >= (kLH - 1) * 5 / 4 + 3, "small box too small");
 
 // 8 bytes from a 4-byte-aligned LDS row at any byte offset, as aligned dword reads + v_alignbyte.
 // (Adjacent byte reads would otherwise be merged by the compiler into unaligned ds_read_u16/b64,
@@ -113,16 +115,17 @@ __device__ __forceinline__ int resize_src_index(int d, double scale, int slen) {
 // One workgroup = one 64 x 32 tile of a padded level plane (+3-px halo for the blur).
 // Level 0 copies the input; level l > 0 resizes the previous level view.  The source pixels the tile
 // needs are staged in LDS (one round of independent loads), the interpolation reads LDS only.
-template <bool kLevel0>
+template <bool kLevel0, int kBH = kSmallBoxH, int kBW = kSmallBoxW>
 __global__ __launch_bounds__(256) void k_pyramid_level(const KernelGeom* __restrict__ gp, int level,
                                                        const uint8_t* __restrict__ in, long long in_frame_stride,
                                                        int in_stride, uint8_t* __restrict__ pyr,
                                                        uint8_t* __restrict__ blur, const int2* __restrict__ xtab,
                                                        const int4* __restrict__ ytab) {
     const KernelGeom& g = *gp;
-    __shared__ __attribute__((aligned(16))) uint8_t box[kBoxH * kBoxW];
+    constexpr int kBoxWords = kBW / 4;
+    __shared__ __attribute__((aligned(16))) uint8_t box[kLevel0 ? 4 : kBH * kBW];
     __shared__ __attribute__((aligned(16))) uint8_t tile[kLH][kLW + 2 + 8];  // rows 4-aligned, +8 readable slack
-    __shared__ int hsum[kLH][kTileW];
+    __shared__ uint16_t hsum[kLH][kTileW];  // <= 255 * 256: exact in 16 bits
     __shared__ int2 xs[kLW];
     __shared__ int4 ys[kLH];
     const int f = blockIdx.z, tid = threadIdx.x;
@@ -205,8 +208,8 @@ __global__ __launch_bounds__(256) void k_pyramid_level(const KernelGeom* __restr
             const int4 Y = ys[ty];
             const int sx = X.x - bx0 + shift, sx1 = min(X.x + 1, bx0 + bw - 1) - bx0 + shift;
             const int a0 = X.y & 0xffff, a1 = X.y >> 16;
-            const uint8_t* R0 = box + (Y.x - by0) * kBoxW;
-            const uint8_t* R1 = box + (Y.y - by0) * kBoxW;
+            const uint8_t* R0 = box + (Y.x - by0) * kBW;
+            const uint8_t* R1 = box + (Y.y - by0) * kBW;
             const int h0 = R0[sx] * a0 + R0[sx1] * a1, h1 = R1[sx] * a0 + R1[sx1] * a1;
             const int vx = reflect101(X0 - kHalo + tx - kEdge, L.w);
             int v;
@@ -252,7 +255,7 @@ __global__ __launch_bounds__(256) void k_pyramid_level(const KernelGeom* __restr
             int acc = 0;
 #pragma unroll
             for (int k = 0; k < 7; ++k) acc += blur_tap(k) * px[q + k];
-            hsum[ty][tx + q] = acc;
+            hsum[ty][tx + q] = (uint16_t)acc;
         }
     }
     __syncthreads();
@@ -351,13 +354,14 @@ __device__ __forceinline__ bool fast_corner(const uint8_t* __restrict__ p, const
 // is computed only for the pixels that are corners at minTh (compacted list, no divergence).
 __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict__ gp, const CellDesc* __restrict__ cells, int win_cap,
                                                     const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
-                                                    int32_t* __restrict__ cell_count, uint8_t* __restrict__ cell_thr) {
+                                                    int32_t* __restrict__ cell_count, uint8_t* __restrict__ cell_thr,
+                                                    int cell0, int cell_end) {
     const KernelGeom& g = *gp;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int cid = blockIdx.x * 4 + wave;
+    const int cid = cell0 + blockIdx.x * 4 + wave;
     const int f = blockIdx.y;
-    if (cid >= g.ncells) return;
+    if (cid >= cell_end) return;
     const CellDesc C = cells[cid];
     const LevelGeom& L = g.lv[C.level];
     const uint8_t* view = pyr + (size_t)f * g.pyr_frame_bytes + L.plane_off + (size_t)kEdge * L.pitch + kEdge;
@@ -1380,6 +1384,9 @@ struct Extractor {
     // sub-batching over internal streams
     static constexpr int kMaxStreams = 4;
     int chunk = 1 << 30, nstreams = 1;  // off by default: measured slower (streams did not overlap)
+    int fast_split = 3;                 // FAST on levels [0, fast_split) overlaps the small pyramid levels
+    hipStream_t side = nullptr;
+    hipEvent_t split_ev[2] = {};
     hipStream_t sub[kMaxStreams] = {};
     hipEvent_t fork_ev = nullptr, join_ev[kMaxStreams] = {};
     long long batches = 0;
@@ -1489,20 +1496,38 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     uint8_t* desc = d_desc + (size_t)f0 * cap * 32;
     int32_t* counts = d_counts + 2 * (size_t)f0;
     mark(0);
+    // FAST on the first `split` levels runs on a side stream as soon as those pyramid levels exist,
+    // overlapping the latency-bound launches of the small levels (k.lv[split..] ) on `st`.
+    const int split = (e->fast_split > 0 && e->fast_split < k.nlevels) ? e->fast_split : 0;
+    const int win_cap = (G.max_win + 15) & ~15;
+    auto launch_fast = [&](int l0, int l1, hipStream_t s2) {
+        const int c0 = k.lv[l0].cell_begin, c1 = k.lv[l1 - 1].cell_begin + k.lv[l1 - 1].cell_count;
+        if (c1 > c0)
+            hipLaunchKernelGGL(k_fast_cells, dim3((c1 - c0 + 3) / 4, n), dim3(256), 4 * 4 * win_cap, s2, e->d_geom,
+                               e->d_cells, win_cap, pyr, cand, ccount, cthr, c0, c1);
+    };
     for (int l = 0; l < k.nlevels; ++l) {
         const orbgpu::LevelGeom& L = k.lv[l];
         dim3 grid((L.pw + kTileW - 1) / kTileW, (L.ph + kTileH - 1) / kTileH, n);
         if (l == 0)
             hipLaunchKernelGGL(k_pyramid_level<true>, grid, dim3(256), 0, st, e->d_geom, 0, imgs, (long long)frame_stride,
                                stride, pyr, blr, e->d_xtab, e->d_ytab);
+        else if (4 * k.lv[l - 1].w <= 5 * L.w && 4 * k.lv[l - 1].h <= 5 * L.h)  // level ratio <= 1.25
+            hipLaunchKernelGGL((k_pyramid_level<false, kSmallBoxH, kSmallBoxW>), grid, dim3(256), 0, st, e->d_geom, l,
+                               nullptr, 0LL, 0, pyr, blr, e->d_xtab, e->d_ytab);
         else
-            hipLaunchKernelGGL(k_pyramid_level<false>, grid, dim3(256), 0, st, e->d_geom, l, nullptr, 0LL, 0, pyr, blr,
-                               e->d_xtab, e->d_ytab);
+            hipLaunchKernelGGL((k_pyramid_level<false, kBoxH, kBoxW>), grid, dim3(256), 0, st, e->d_geom, l, nullptr, 0LL,
+                               0, pyr, blr, e->d_xtab, e->d_ytab);
+        if (split && l == split - 1) {
+            hipEventRecord(e->split_ev[0], st);
+            hipStreamWaitEvent(e->side, e->split_ev[0], 0);
+            launch_fast(0, split, e->side);
+            hipEventRecord(e->split_ev[1], e->side);
+        }
     }
     mark(1);
-    const int win_cap = (G.max_win + 15) & ~15;
-    hipLaunchKernelGGL(k_fast_cells, dim3((k.ncells + 3) / 4, n), dim3(256), 4 * 4 * win_cap, st, e->d_geom, e->d_cells,
-                       win_cap, pyr, cand, ccount, cthr);
+    launch_fast(split, k.nlevels, st);
+    if (split) hipStreamWaitEvent(st, e->split_ev[1], 0);
     mark(2);
     hipLaunchKernelGGL(k_quadtree, dim3(k.nlevels, n), dim3(64), e->qt_lds, st, e->d_geom, e->d_cells, cand, ccount,
                        scratch, sel, scount, e->qt_lds, e->d_status,
@@ -1572,7 +1597,11 @@ int orb_extractor_create(const orb_params_t* p, int max_width, int max_height, i
     hipFuncSetAttribute((const void*)k_quadtree, hipFuncAttributeMaxDynamicSharedMemorySize, e->qt_lds);
     if (const char* c = getenv("ORBGPU_CHUNK")) e->chunk = std::max(1, atoi(c));
     if (const char* c = getenv("ORBGPU_STREAMS")) e->nstreams = std::min(Extractor::kMaxStreams, std::max(1, atoi(c)));
-    bool ok = hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) == hipSuccess;
+    if (const char* c = getenv("ORBGPU_FAST_SPLIT")) e->fast_split = atoi(c);
+    bool ok = hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) == hipSuccess &&
+              hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&e->split_ev[0], hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&e->split_ev[1], hipEventDisableTiming) == hipSuccess;
     for (int s = 0; s < Extractor::kMaxStreams && ok; ++s)
         ok = hipStreamCreateWithFlags(&e->sub[s], hipStreamNonBlocking) == hipSuccess &&
              hipEventCreateWithFlags(&e->join_ev[s], hipEventDisableTiming) == hipSuccess;
@@ -1594,6 +1623,9 @@ int orb_extractor_destroy(orb_extractor_t h) {
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t x : e->events) (void)hipEventDestroy(x);
+    if (e->side) { hipStreamSynchronize(e->side); hipStreamDestroy(e->side); }
+    for (int k2 = 0; k2 < 2; ++k2)
+        if (e->split_ev[k2]) hipEventDestroy(e->split_ev[k2]);
     for (int s = 0; s < Extractor::kMaxStreams; ++s) {
         if (e->sub[s]) { hipStreamSynchronize(e->sub[s]); hipStreamDestroy(e->sub[s]); }
         if (e->join_ev[s]) hipEventDestroy(e->join_ev[s]);
