@@ -1153,10 +1153,11 @@ __global__ __launch_bounds__(64) void k_quadtree(const KernelGeom* __restrict__ 
                                                  uint32_t* __restrict__ key_scratch, uint32_t* __restrict__ sel,
                                                  int32_t* __restrict__ sel_count, int lds_bytes, int* __restrict__ status,
                                                  unsigned long long* __restrict__ stamps, int lap0, int lap1,
-                                                 int32_t* __restrict__ rank_out, int32_t* __restrict__ lap_count) {
+                                                 int32_t* __restrict__ rank_out, int32_t* __restrict__ lap_count,
+                                                 int level0) {
     const KernelGeom& g = *gp;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int level = blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
+    const int level = level0 + blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
     const LevelGeom& L = g.lv[level];
     const int32_t* cc = cell_count + (size_t)f * g.ncells + L.cell_begin;
     int K = 0;
@@ -1506,6 +1507,14 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
             hipLaunchKernelGGL(k_fast_cells, dim3((c1 - c0 + 3) / 4, n), dim3(256), 4 * 4 * win_cap, s2, e->d_geom,
                                e->d_cells, win_cap, pyr, cand, ccount, cthr, c0, c1);
     };
+    // quad-tree of levels [l0, l1): one wave per (level, frame)
+    auto launch_qt = [&](int l0, int l1, hipStream_t s2) {
+        if (l1 > l0)
+            hipLaunchKernelGGL(k_quadtree, dim3(l1 - l0, n), dim3(64), e->qt_lds, s2, e->d_geom, e->d_cells, cand, ccount,
+                               scratch, sel, scount, e->qt_lds, e->d_status,
+                               e->d_stamps ? e->d_stamps + (size_t)f0 * k.nlevels * kQtStamps : nullptr, lap0, lap1, dst,
+                               lapc, l0);
+    };
     for (int l = 0; l < k.nlevels; ++l) {
         const orbgpu::LevelGeom& L = k.lv[l];
         dim3 grid((L.pw + kTileW - 1) / kTileW, (L.ph + kTileH - 1) / kTileH, n);
@@ -1529,9 +1538,9 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     launch_fast(split, k.nlevels, st);
     if (split) hipStreamWaitEvent(st, e->split_ev[1], 0);
     mark(2);
-    hipLaunchKernelGGL(k_quadtree, dim3(k.nlevels, n), dim3(64), e->qt_lds, st, e->d_geom, e->d_cells, cand, ccount,
-                       scratch, sel, scount, e->qt_lds, e->d_status,
-                       e->d_stamps ? e->d_stamps + (size_t)f0 * k.nlevels * kQtStamps : nullptr, lap0, lap1, dst, lapc);
+    // (running the quad-tree of the early levels on the side stream was measured slower: its
+    // 80 KB-LDS waves crowd out the FAST work of the late levels)
+    launch_qt(0, k.nlevels, st);
     mark(3);
     mark(4);
     hipLaunchKernelGGL(k_describe, dim3((G.max_sel + kDescKpPerBlock - 1) / kDescKpPerBlock, k.nlevels, n), dim3(256), 0,
