@@ -1386,12 +1386,14 @@ struct Extractor {
     static constexpr int kMaxStreams = 4;
     int chunk = 1 << 30, nstreams = 1;  // off by default: measured slower (streams did not overlap)
     int fast_split = 3;                 // FAST on levels [0, fast_split) overlaps the small pyramid levels
-    hipStream_t side = nullptr;
-    hipEvent_t split_ev[2] = {};
+    int fast_per_level = 0;             // 1: FAST of each later level right after its pyramid level (side2); measured slower
+    hipStream_t side = nullptr, side2 = nullptr;
+    hipEvent_t split_ev[3] = {};
+    hipEvent_t lvl_ev[orbgpu::kMaxLevels] = {};
     hipStream_t sub[kMaxStreams] = {};
     hipEvent_t fork_ev = nullptr, join_ev[kMaxStreams] = {};
     long long batches = 0;
-    bool profile = false;
+    int profile = 0;  // 0 off, 1 every stage boundary, 2 only the pyramid stage (marks 0 and 1)
     std::vector<hipEvent_t> events;   // kStages + 1 per profiled sub-batch launch
     int ev_used = 0;                  // launches recorded since the last read
     long long frames_profiled = 0;
@@ -1481,7 +1483,9 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
         e->ev_used++;
         e->frames_profiled += n;
     }
-    auto mark = [&](int i) { if (ev) hipEventRecord(ev[i], st); };
+    auto mark = [&](int i) {
+        if (ev && (e->profile == 1 || i <= 1)) hipEventRecord(ev[i], st);
+    };
     uint8_t* pyr = e->d_pyr + (size_t)f0 * k.pyr_frame_bytes;
     uint8_t* blr = e->d_blur + (size_t)f0 * k.pyr_frame_bytes;
     uint32_t* cand = e->d_cand + (size_t)f0 * k.cand_frame_cap;
@@ -1532,10 +1536,20 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
             hipStreamWaitEvent(e->side, e->split_ev[0], 0);
             launch_fast(0, split, e->side);
             hipEventRecord(e->split_ev[1], e->side);
+        } else if (split && l >= split && e->fast_per_level) {
+            // later (small) levels: FAST as soon as the level exists, on a second side stream
+            hipEventRecord(e->lvl_ev[l], st);
+            hipStreamWaitEvent(e->side2, e->lvl_ev[l], 0);
+            launch_fast(l, l + 1, e->side2);
         }
     }
     mark(1);
-    launch_fast(split, k.nlevels, st);
+    if (split && e->fast_per_level) {
+        hipEventRecord(e->split_ev[2], e->side2);
+        hipStreamWaitEvent(st, e->split_ev[2], 0);
+    } else {
+        launch_fast(split, k.nlevels, st);
+    }
     if (split) hipStreamWaitEvent(st, e->split_ev[1], 0);
     mark(2);
     // (running the quad-tree of the early levels on the side stream was measured slower: its
@@ -1609,8 +1623,11 @@ int orb_extractor_create(const orb_params_t* p, int max_width, int max_height, i
     if (const char* c = getenv("ORBGPU_FAST_SPLIT")) e->fast_split = atoi(c);
     bool ok = hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) == hipSuccess &&
               hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) == hipSuccess &&
-              hipEventCreateWithFlags(&e->split_ev[0], hipEventDisableTiming) == hipSuccess &&
-              hipEventCreateWithFlags(&e->split_ev[1], hipEventDisableTiming) == hipSuccess;
+              hipStreamCreateWithFlags(&e->side2, hipStreamNonBlocking) == hipSuccess;
+    for (int k2 = 0; k2 < 3 && ok; ++k2) ok = hipEventCreateWithFlags(&e->split_ev[k2], hipEventDisableTiming) == hipSuccess;
+    for (int k2 = 0; k2 < orbgpu::kMaxLevels && ok; ++k2)
+        ok = hipEventCreateWithFlags(&e->lvl_ev[k2], hipEventDisableTiming) == hipSuccess;
+    if (const char* c = getenv("ORBGPU_FAST_PER_LEVEL")) e->fast_per_level = atoi(c);
     for (int s = 0; s < Extractor::kMaxStreams && ok; ++s)
         ok = hipStreamCreateWithFlags(&e->sub[s], hipStreamNonBlocking) == hipSuccess &&
              hipEventCreateWithFlags(&e->join_ev[s], hipEventDisableTiming) == hipSuccess;
@@ -1633,8 +1650,11 @@ int orb_extractor_destroy(orb_extractor_t h) {
         if (b) (void)hipFree(b);
     for (hipEvent_t x : e->events) (void)hipEventDestroy(x);
     if (e->side) { hipStreamSynchronize(e->side); hipStreamDestroy(e->side); }
-    for (int k2 = 0; k2 < 2; ++k2)
+    if (e->side2) { hipStreamSynchronize(e->side2); hipStreamDestroy(e->side2); }
+    for (int k2 = 0; k2 < 3; ++k2)
         if (e->split_ev[k2]) hipEventDestroy(e->split_ev[k2]);
+    for (int k2 = 0; k2 < orbgpu::kMaxLevels; ++k2)
+        if (e->lvl_ev[k2]) hipEventDestroy(e->lvl_ev[k2]);
     for (int s = 0; s < Extractor::kMaxStreams; ++s) {
         if (e->sub[s]) { hipStreamSynchronize(e->sub[s]); hipStreamDestroy(e->sub[s]); }
         if (e->join_ev[s]) hipEventDestroy(e->join_ev[s]);
@@ -1808,7 +1828,7 @@ int orb_debug_level_blurred(orb_extractor_t h, int frame, int level, uint8_t* ho
 int orb_extractor_profile(orb_extractor_t h, int enable) {
     Extractor* e = reinterpret_cast<Extractor*>(h);
     if (!e) return ORB_ERR_ARG;
-    e->profile = enable != 0;
+    e->profile = enable == 2 ? 2 : (enable != 0 ? 1 : 0);
     e->ev_used = 0;
     e->frames_profiled = 0;
     e->batches = 0;
@@ -1821,8 +1841,9 @@ int orb_extractor_stage_ms(orb_extractor_t h, float* ms, int* launches, long lon
     for (int s = 0; s < orbgpu::kStages; ++s) ms[s] = 0.f;
     for (int i = 0; i < e->ev_used; ++i) {
         hipEvent_t* ev = &e->events[(size_t)i * (orbgpu::kStages + 1)];
-        if (hipEventSynchronize(ev[orbgpu::kStages]) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "event sync");
-        for (int s = 0; s < orbgpu::kStages; ++s) {
+        const int last = e->profile == 2 ? 1 : orbgpu::kStages;
+        if (hipEventSynchronize(ev[last]) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "event sync");
+        for (int s = 0; s < last; ++s) {
             float t = 0.f;
             hipEventElapsedTime(&t, ev[s], ev[s + 1]);
             ms[s] += t;

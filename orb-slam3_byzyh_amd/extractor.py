@@ -132,8 +132,11 @@ class ORBextractor:
         return kps, desc, counts
 
     # ---- per-stage timing (HIP events on the launch stream)
-    def profile(self, enable: bool = True) -> None:
-        check(self._lib.orb_extractor_profile(self._h, 1 if enable else 0), "orb_extractor_profile")
+    def profile(self, enable: bool | str = True) -> None:
+        """Record HIP events at stage boundaries: True = every stage, "pyramid" = only around the
+        pyramid stage (2 events per call, for timed regions), False = off."""
+        mode = 2 if enable == "pyramid" else (1 if enable else 0)
+        check(self._lib.orb_extractor_profile(self._h, mode), "orb_extractor_profile")
 
     def stage_ms(self):
         """Summed ms per stage since profile(True), the number of launches and frames recorded."""
