@@ -161,6 +161,43 @@ int orb_search_for_triangulation(orb_matcher_t m, const orb_kf_view_t* kf1, cons
                                  const orb_kf_pair_geom_t* geoms, int n_pairs, int only_stereo, int coarse,
                                  int32_t* matches12, int32_t* n_matches);
 
+/* ---- ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono) (src/ORBmatcher.cc:1951-2185)
+ * Pinhole frames without a second camera (Nleft == -1). */
+
+/* The current frame: keypoints, descriptors, the feature grid bounds (Frame::mnMinX.., the grid
+ * element inverse sizes; FRAME_GRID_COLS x ROWS = 64 x 48, include/Frame.h:44-45) and its pose. */
+typedef struct orb_frame_view {
+    int32_t n;
+    const orb_keypoint_t* kps_un;   /* mvKeysUn */
+    const uint8_t* desc;            /* mDescriptors, n x 32 */
+    const float* u_right;           /* mvuRight (n); NULL = monocular */
+    float min_x, max_x, min_y, max_y;       /* mnMinX, mnMaxX, mnMinY, mnMaxY */
+    float grid_inv_w, grid_inv_h;           /* mfGridElementWidthInv, mfGridElementHeightInv */
+    float fx, fy, cx, cy;                   /* mpCamera parameters */
+    float bf, b;                            /* mbf, mb */
+    int32_t nlevels;
+    const float* scale_factors;             /* mvScaleFactors (nlevels) */
+    float Tcw[12];                          /* GetPose(), 3x4 row-major [R|t] */
+} orb_frame_view_t;
+
+/* The last frame's tracked map points, indexed like LastFrame's keypoints. */
+typedef struct orb_last_points {
+    int32_t n;                      /* LastFrame.N */
+    const uint8_t* valid;           /* mvpMapPoints[i] != NULL && !mvbOutlier[i] */
+    const uint8_t* observed;        /* mvpMapPoints[i]->Observations() > 0 */
+    const float* xyz;               /* mvpMapPoints[i]->GetWorldPos(), n x 3 */
+    const uint8_t* desc;            /* mvpMapPoints[i]->GetDescriptor(), n x 32 */
+    const orb_keypoint_t* kps_un;   /* LastFrame.mvKeysUn (octave and angle) */
+    float Tcw[12];                  /* LastFrame.GetPose() */
+} orb_last_points_t;
+
+/* match[i2] receives the LastFrame index whose map point was assigned to current keypoint i2 (-1:
+ * none).  Like the reference, points are processed in index order and a keypoint already holding
+ * a map point with observations is skipped by later points; `check_ori` comes from the matcher
+ * handle.  Returns the number of matches in *n_matches.  Host memory, synchronous. */
+int orb_search_by_projection_frame(orb_matcher_t m, const orb_frame_view_t* cur, const orb_last_points_t* last,
+                                   float th, int mono, int32_t* match, int32_t* n_matches);
+
 /* ---- Optimizer::LocalBundleAdjustment (src/Optimizer.cc:1740-2188) ----------------------------- */
 /* The shim keeps the reference's graph gather (B1, src/Optimizer.cc:1744-1855) and the culling /
  * write-back (B10, :2107-2185) on the host and hands the flattened g2o problem across this ABI; the

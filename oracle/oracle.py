@@ -37,6 +37,7 @@ _PROTOS = {
     "oracle_descriptor_distance": (_i, [_vp, _vp]),
     "oracle_search_for_triangulation": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp]),
     "oracle_local_ba": (_i, [_vp, _vp, _vp, _vp, _vp]),
+    "oracle_search_by_projection_frame": (_i, [_vp, _vp, _f, _i, _i, _vp]),
 }
 
 _LIB = None
@@ -219,3 +220,12 @@ def local_ba(prob: dict, iterations: int = 10, user_lambda_init: float = 0.0, st
     res = {"iterations": r.iterations, "trials": r.trials, "terminated": r.terminated, "stopped": r.stopped,
            "initial_chi2": r.initial_chi2, "final_chi2": r.final_chi2, "lambda": r.lambda_}
     return pose, point, chi2, depth.astype(bool), res
+
+
+def search_by_projection_frame(cur, last, th: float, mono: bool, check_ori: bool):
+    """Oracle SearchByProjection(CurrentFrame, LastFrame, th, bMono).  cur/last: objects with .view() /
+    .last_points() returning the orb_frame_view_t / orb_last_points_t ctypes structs (plain data)."""
+    m = np.full(max(cur.N, 1), -1, np.int32)
+    n = load().oracle_search_by_projection_frame(ctypes.byref(cur.view()), ctypes.byref(last.last_points()),
+                                                 float(th), int(mono), int(check_ori), m.ctypes.data)
+    return n, m[:cur.N]

@@ -296,6 +296,17 @@ struct orb_matcher_s {
     }
 };
 
+// Staging buffers of a matcher handle for the other matcher entry points (orb_projection.hip).
+int orbgpu_matcher_reserve(orb_matcher_t m, size_t bytes, char** d_buf, char** h_buf, hipStream_t* stream,
+                           int* check_ori) {
+    if (int rc = m->reserve(bytes)) return rc;
+    *d_buf = m->d_buf;
+    *h_buf = m->h_buf;
+    *stream = m->stream;
+    *check_ori = m->check_ori;
+    return ORB_OK;
+}
+
 extern "C" {
 
 int orb_matcher_create(float nnratio, int check_orientation, orb_matcher_t* out) {

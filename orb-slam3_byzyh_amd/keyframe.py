@@ -67,3 +67,63 @@ class KeyFrame:
                                 _ptr(self.fv_index), self.fx, self.fy, self.cx, self.cy, len(self.mvScaleFactors),
                                 _ptr(self.mvScaleFactors), _ptr(self.mvLevelSigma2))
         return self._view
+
+
+class FrameView(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("kps_un", ctypes.c_void_p), ("desc", ctypes.c_void_p),
+                ("u_right", ctypes.c_void_p), ("min_x", ctypes.c_float), ("max_x", ctypes.c_float),
+                ("min_y", ctypes.c_float), ("max_y", ctypes.c_float), ("grid_inv_w", ctypes.c_float),
+                ("grid_inv_h", ctypes.c_float), ("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float),
+                ("cy", ctypes.c_float), ("bf", ctypes.c_float), ("b", ctypes.c_float), ("nlevels", ctypes.c_int32),
+                ("scale_factors", ctypes.c_void_p), ("Tcw", ctypes.c_float * 12)]
+
+
+class LastPoints(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("valid", ctypes.c_void_p), ("observed", ctypes.c_void_p),
+                ("xyz", ctypes.c_void_p), ("desc", ctypes.c_void_p), ("kps_un", ctypes.c_void_p),
+                ("Tcw", ctypes.c_float * 12)]
+
+
+FRAME_GRID_COLS, FRAME_GRID_ROWS = 64, 48  # include/Frame.h:44-45
+
+
+class Frame:
+    """The Frame fields SearchByProjection reads (src/Frame.cc; pinhole, no second camera)."""
+
+    def __init__(self, keys_un, descriptors, Tcw, camera, scale_factors, width, height, bf=0.0, u_right=None,
+                 map_points=None):
+        self.mvKeysUn = np.ascontiguousarray(keys_un, dtype=KEYPOINT_DTYPE)
+        self.N = len(self.mvKeysUn)
+        self.mDescriptors = np.ascontiguousarray(descriptors, dtype=np.uint8).reshape(self.N, 32)
+        self.Tcw = np.ascontiguousarray(Tcw, dtype=np.float32).reshape(3, 4)
+        self.fx, self.fy, self.cx, self.cy = (float(np.float32(v)) for v in camera)
+        self.mvScaleFactors = np.ascontiguousarray(scale_factors, dtype=np.float32)
+        self.mbf = float(np.float32(bf))
+        self.mb = float(np.float32(np.float32(bf) / np.float32(self.fx))) if bf else 0.0
+        self.mvuRight = None if u_right is None else np.ascontiguousarray(u_right, dtype=np.float32)
+        # undistorted image bounds (no distortion: the image rectangle, Frame::ComputeImageBounds)
+        self.mnMinX, self.mnMaxX, self.mnMinY, self.mnMaxY = 0.0, float(width), 0.0, float(height)
+        self.mfGridElementWidthInv = float(np.float32(FRAME_GRID_COLS) / np.float32(self.mnMaxX - self.mnMinX))
+        self.mfGridElementHeightInv = float(np.float32(FRAME_GRID_ROWS) / np.float32(self.mnMaxY - self.mnMinY))
+        # tracked map points, for use as a LastFrame: dict with valid, observed, xyz, desc arrays
+        self.map_points = map_points
+
+    def view(self) -> FrameView:
+        v = FrameView(self.N, _ptr(self.mvKeysUn), _ptr(self.mDescriptors), _ptr(self.mvuRight), self.mnMinX,
+                      self.mnMaxX, self.mnMinY, self.mnMaxY, self.mfGridElementWidthInv, self.mfGridElementHeightInv,
+                      self.fx, self.fy, self.cx, self.cy, self.mbf, self.mb, len(self.mvScaleFactors),
+                      _ptr(self.mvScaleFactors))
+        v.Tcw[:] = [float(x) for x in self.Tcw.reshape(-1)]
+        self._keep = v
+        return v
+
+    def last_points(self) -> LastPoints:
+        mp = self.map_points
+        self._mp_arrays = {k: np.ascontiguousarray(mp[k], dtype=dt) for k, dt in
+                           (("valid", np.uint8), ("observed", np.uint8), ("xyz", np.float32), ("desc", np.uint8))}
+        a = self._mp_arrays
+        v = LastPoints(self.N, _ptr(a["valid"]), _ptr(a["observed"]), _ptr(a["xyz"]), _ptr(a["desc"]),
+                       _ptr(self.mvKeysUn))
+        v.Tcw[:] = [float(x) for x in self.Tcw.reshape(-1)]
+        self._keep_last = v
+        return v

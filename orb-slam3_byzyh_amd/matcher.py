@@ -7,7 +7,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import check
-from .keyframe import KeyFrame, KfView, PairGeom
+from .keyframe import Frame, KeyFrame, KfView, PairGeom
 
 TH_HIGH = 100  # src/ORBmatcher.cc:36
 TH_LOW = 50    # src/ORBmatcher.cc:37
@@ -97,3 +97,15 @@ class ORBmatcher:
                                                   d1.data_ptr(), d2.data_ptr(), ctypes.c_void_p(st.cuda_stream)),
               "orb_hamming_knn2_device")
         return idx, d1, d2
+
+    def SearchByProjectionFrame(self, CurrentFrame: Frame, LastFrame: Frame, th: float, bMono: bool):
+        """SearchByProjection(Frame &CurrentFrame, const Frame &LastFrame, th, bMono)
+        (src/ORBmatcher.cc:1951-2185).  Returns (nmatches, match) with match[i2] = the LastFrame index
+        whose map point CurrentFrame.mvpMapPoints[i2] receives (-1: none)."""
+        m = np.full(max(CurrentFrame.N, 1), -1, np.int32)
+        n = ctypes.c_int32()
+        check(_lib.load().orb_search_by_projection_frame(self._handle(), ctypes.byref(CurrentFrame.view()),
+                                                         ctypes.byref(LastFrame.last_points()), float(th),
+                                                         int(bMono), m.ctypes.data, ctypes.byref(n)),
+              "orb_search_by_projection_frame")
+        return n.value, m[:CurrentFrame.N]

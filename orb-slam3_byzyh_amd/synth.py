@@ -300,3 +300,76 @@ def local_ba_problem(n_kf: int = 50, n_points: int = 2000, obs_per_point: int = 
     return dict(pose=pose0, pose_id=np.arange(n_kf, dtype=np.int64), pose_fixed=fixed, pose_camera=cams,
                 point=point0, point_id=np.arange(n_points, dtype=np.int64) + n_kf + 1, edges=E,
                 pose_gt=pose_gt, point_gt=P)
+
+
+def tracking_pair(n_points: int = 1200, seed: int = 31, width: int = 752, height: int = 480, stereo: bool = True,
+                  clutter: int = 300, outlier_frac: float = 0.05, unobserved_frac: float = 0.15, dup_frac: float = 0.05,
+                  forward: float = 0.02, nlevels: int = 8):
+    """Two consecutive frames for SearchByProjection(CurrentFrame, LastFrame): the last frame tracks
+    map points (xyz, descriptor, observed flag, a few outliers); the current frame sees them again
+    after a small motion, with noisy keypoints, perturbed descriptors, stereo u_right and clutter.
+    A few map points share descriptors and nearby positions so that current keypoints are contested
+    (exercises the in-order 'already matched' rule).  Returns dicts for Frame(**cur), Frame(**last)."""
+    from ._lib import KEYPOINT_DTYPE
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = EUROC_K
+    scale, _ = scale_tables(nlevels)
+    P = np.stack([rng.uniform(-4, 4, n_points), rng.uniform(-2.5, 2.5, n_points), rng.uniform(2, 12, n_points)], 1)
+    base = rng.integers(0, 256, (n_points, 32), dtype=np.uint8)
+    ndup = int(dup_frac * n_points)
+    src = rng.choice(n_points, ndup, replace=False)
+    dst = rng.choice(n_points, ndup, replace=False)
+    P[dst] = P[src] + rng.normal(0, 0.004, (ndup, 3))
+    base[dst] = base[src]
+    ang = rng.uniform(0, 360, n_points)
+    octv = rng.integers(0, nlevels, n_points)
+
+    def frame(R, t, noise, flips):
+        Xc = P @ R.T + t
+        z = Xc[:, 2]
+        u = fx * Xc[:, 0] / z + cx
+        v = fy * Xc[:, 1] / z + cy
+        vis = np.flatnonzero((z > 0.3) & (u >= 0) & (u < width) & (v >= 0) & (v < height))
+        nv = len(vis)
+        kps = np.zeros(nv + clutter, KEYPOINT_DTYPE)
+        o = octv[vis].copy()
+        o = np.clip(o + rng.integers(-1, 2, nv), 0, nlevels - 1)
+        kps["octave"][:nv] = o
+        kps["x"][:nv] = np.clip(u[vis] + rng.normal(0, noise, nv) * scale[o], 0, width - 1)
+        kps["y"][:nv] = np.clip(v[vis] + rng.normal(0, noise, nv) * scale[o], 0, height - 1)
+        kps["angle"][:nv] = np.mod(ang[vis] + rng.normal(0, 3, nv), 360)
+        kps["x"][nv:] = rng.uniform(0, width - 1, clutter)
+        kps["y"][nv:] = rng.uniform(0, height - 1, clutter)
+        kps["octave"][nv:] = rng.integers(0, nlevels, clutter)
+        kps["angle"][nv:] = rng.uniform(0, 360, clutter)
+        kps["size"] = 31 * scale[kps["octave"]]
+        kps["class_id"] = -1
+        bits = np.unpackbits(base[vis], axis=1)
+        for i in range(nv):
+            bits[i, rng.choice(256, int(rng.integers(0, flips)), replace=False)] ^= 1
+        desc = np.concatenate([np.packbits(bits, axis=1), rng.integers(0, 256, (clutter, 32), dtype=np.uint8)])
+        ur = np.full(nv + clutter, -1.0, np.float32)
+        if stereo:
+            st = rng.random(nv) < 0.6
+            ur[:nv][st] = (kps["x"][:nv][st] - EUROC_BF / z[vis][st] + rng.normal(0, 0.5, st.sum())).astype(np.float32)
+        perm = rng.permutation(nv + clutter)
+        ids = np.concatenate([vis, np.full(clutter, -1)])[perm]
+        Tcw = np.concatenate([R, t[:, None]], 1).astype(np.float32)
+        return kps[perm], desc[perm], ur[perm], ids, Tcw
+
+    R0, t0 = np.eye(3), np.zeros(3)
+    R1 = _rot_yaw_pitch(np.deg2rad(0.8), np.deg2rad(0.3))
+    t1 = np.array([0.03, -0.01, -forward])
+    lk, ld, lur, lids, lT = frame(R0, t0, 0.3, 12)
+    ck, cd, cur_, cids, cT = frame(R1, t1, 0.5, 30)
+    valid = (lids >= 0) & (rng.random(len(lids)) > outlier_frac)
+    xyz = np.zeros((len(lids), 3), np.float32)
+    mdesc = np.zeros((len(lids), 32), np.uint8)
+    xyz[lids >= 0] = P[lids[lids >= 0]] + rng.normal(0, 0.01, ((lids >= 0).sum(), 3))
+    mdesc[lids >= 0] = base[lids[lids >= 0]]
+    observed = (rng.random(len(lids)) > unobserved_frac).astype(np.uint8)
+    common = dict(camera=EUROC_K, scale_factors=scale, width=width, height=height, bf=EUROC_BF if stereo else 0.0)
+    last = dict(keys_un=lk, descriptors=ld, Tcw=lT, u_right=lur if stereo else None,
+                map_points=dict(valid=valid.astype(np.uint8), observed=observed, xyz=xyz, desc=mdesc), **common)
+    cur = dict(keys_un=ck, descriptors=cd, Tcw=cT, u_right=cur_ if stereo else None, **common)
+    return cur, last
