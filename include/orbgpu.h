@@ -198,6 +198,28 @@ typedef struct orb_last_points {
 int orb_search_by_projection_frame(orb_matcher_t m, const orb_frame_view_t* cur, const orb_last_points_t* last,
                                    float th, int mono, int32_t* match, int32_t* n_matches);
 
+/* ---- ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th, bFarPoints, thFarPoints)
+ * (src/ORBmatcher.cc:46-240, called from Tracking::SearchLocalPoints).  The local map points with the
+ * tracking fields Frame::isInFrustum wrote into them (src/Frame.cc:667-773). */
+typedef struct orb_local_points {
+    int32_t n;                      /* vpMapPoints.size() */
+    const uint8_t* track_in_view;   /* mbTrackInView */
+    const uint8_t* is_bad;          /* isBad() */
+    const uint8_t* observed;        /* Observations() > 0 */
+    const float* track_proj;        /* n x 3: mTrackProjX, mTrackProjY, mTrackProjXR */
+    const float* track_view_cos;    /* mTrackViewCos */
+    const float* track_depth;       /* mTrackDepth */
+    const int32_t* track_level;     /* mnTrackScaleLevel */
+    const uint8_t* desc;            /* GetDescriptor(), n x 32 */
+} orb_local_points_t;
+
+/* frame_taken[i]: F.mvpMapPoints[i] != NULL && ->Observations() > 0 before the call (NULL: none).
+ * match[i] receives the index into vpMapPoints of the map point assigned to keypoint i by this
+ * call (-1: none); points are processed in order and the ratio test uses the handle's nnratio. */
+int orb_search_by_projection_local(orb_matcher_t m, const orb_frame_view_t* frame, const uint8_t* frame_taken,
+                                   const orb_local_points_t* pts, float th, int far_points, float th_far_points,
+                                   int32_t* match, int32_t* n_matches);
+
 /* ---- Optimizer::LocalBundleAdjustment (src/Optimizer.cc:1740-2188) ----------------------------- */
 /* The shim keeps the reference's graph gather (B1, src/Optimizer.cc:1744-1855) and the culling /
  * write-back (B10, :2107-2185) on the host and hands the flattened g2o problem across this ABI; the

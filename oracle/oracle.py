@@ -38,6 +38,7 @@ _PROTOS = {
     "oracle_search_for_triangulation": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp]),
     "oracle_local_ba": (_i, [_vp, _vp, _vp, _vp, _vp]),
     "oracle_search_by_projection_frame": (_i, [_vp, _vp, _f, _i, _i, _vp]),
+    "oracle_search_by_projection_local": (_i, [_vp, _vp, _vp, _f, _i, _f, _f, _vp]),
 }
 
 _LIB = None
@@ -229,3 +230,13 @@ def search_by_projection_frame(cur, last, th: float, mono: bool, check_ori: bool
     n = load().oracle_search_by_projection_frame(ctypes.byref(cur.view()), ctypes.byref(last.last_points()),
                                                  float(th), int(mono), int(check_ori), m.ctypes.data)
     return n, m[:cur.N]
+
+
+def search_by_projection_local(frame, points, th: float, far: bool, th_far: float, nnratio: float, frame_taken=None):
+    """Oracle SearchByProjection(Frame, vector<MapPoint*>, th, bFarPoints, thFarPoints)."""
+    m = np.full(max(frame.N, 1), -1, np.int32)
+    tk = None if frame_taken is None else np.ascontiguousarray(frame_taken, dtype=np.uint8)
+    n = load().oracle_search_by_projection_local(ctypes.byref(frame.view()), None if tk is None else tk.ctypes.data,
+                                                 ctypes.byref(points.view()), float(th), int(far), float(th_far),
+                                                 float(nnratio), m.ctypes.data)
+    return n, m[:frame.N]

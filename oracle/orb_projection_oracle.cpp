@@ -176,3 +176,61 @@ extern "C" int oracle_search_by_projection_frame(const orb_frame_view_t* cur, co
     delete G;
     return nmatches;
 }
+
+// ORBmatcher::SearchByProjection(Frame &F, const vector<MapPoint*> &vpMapPoints, th, bFarPoints,
+// thFarPoints), src/ORBmatcher.cc:46-240 (Nleft == -1), with RadiusByViewingCos (src:243-250).
+extern "C" int oracle_search_by_projection_local(const orb_frame_view_t* Fv, const uint8_t* frame_taken,
+                                                 const orb_local_points_t* pts, float th, int bFarPoints,
+                                                 float thFarPoints, float mfNNratio, int32_t* match_out) {
+    const orb_frame_view_t& F = *Fv;
+    Grid* G = new Grid();
+    build_grid(F, *G);
+    std::vector<int> owner_obs(F.n, 0), match(F.n, -1);
+    if (frame_taken)
+        for (int i = 0; i < F.n; ++i) owner_obs[i] = frame_taken[i];
+    int nmatches = 0;
+    const bool bFactor = th != 1.0;
+    for (int iMP = 0; iMP < pts->n; iMP++) {
+        if (!pts->track_in_view[iMP]) continue;
+        if (bFarPoints && pts->track_depth[iMP] > thFarPoints) continue;
+        if (pts->is_bad[iMP]) continue;
+        const int nPredictedLevel = pts->track_level[iMP];
+        float r = (pts->track_view_cos[iMP] > 0.998) ? 2.5 : 4.0;
+        if (bFactor) r *= th;
+        const std::vector<int> vIndices =
+            features_in_area(F, *G, pts->track_proj[3 * iMP], pts->track_proj[3 * iMP + 1],
+                             r * F.scale_factors[nPredictedLevel], nPredictedLevel - 1, nPredictedLevel);
+        if (vIndices.empty()) continue;
+        const uint8_t* MPdescriptor = pts->desc + 32 * iMP;
+        int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+        for (int idx : vIndices) {
+            if (owner_obs[idx]) continue;  // F.mvpMapPoints[idx] && ->Observations() > 0
+            if (F.u_right && F.u_right[idx] > 0) {
+                const float er = std::fabs(pts->track_proj[3 * iMP + 2] - F.u_right[idx]);
+                if (er > r * F.scale_factors[nPredictedLevel]) continue;
+            }
+            const int dist = dist256(MPdescriptor, F.desc + 32 * idx);
+            if (dist < bestDist) {
+                bestDist2 = bestDist;
+                bestDist = dist;
+                bestLevel2 = bestLevel;
+                bestLevel = F.kps_un[idx].octave;
+                bestIdx = idx;
+            } else if (dist < bestDist2) {
+                bestLevel2 = F.kps_un[idx].octave;
+                bestDist2 = dist;
+            }
+        }
+        if (bestDist <= TH_HIGH) {
+            if (bestLevel == bestLevel2 && bestDist > mfNNratio * bestDist2) continue;
+            if (bestLevel != bestLevel2 || bestDist <= mfNNratio * bestDist2) {
+                match[bestIdx] = iMP;
+                owner_obs[bestIdx] = pts->observed[iMP];
+                nmatches++;
+            }
+        }
+    }
+    for (int i = 0; i < F.n; ++i) match_out[i] = match[i];
+    delete G;
+    return nmatches;
+}

@@ -7,9 +7,9 @@ __graft_entry__.py), which register it under the import name ``orbslam3_amd``.
 from . import _lib
 from ._lib import KEYPOINT_DTYPE, OrbGpuError
 from .extractor import ORBextractor, keypoints_to_structured
-from .keyframe import Frame, KeyFrame
+from .keyframe import Frame, KeyFrame, LocalMapPoints
 from .matcher import ORBmatcher
 from .optimizer import LocalBA, local_bundle_adjustment
 from . import distributed
 
-__all__ = ["ORBextractor", "ORBmatcher", "KeyFrame", "Frame", "LocalBA", "local_bundle_adjustment", "KEYPOINT_DTYPE", "OrbGpuError", "keypoints_to_structured", "_lib"]
+__all__ = ["ORBextractor", "ORBmatcher", "KeyFrame", "Frame", "LocalMapPoints", "LocalBA", "local_bundle_adjustment", "KEYPOINT_DTYPE", "OrbGpuError", "keypoints_to_structured", "_lib"]

@@ -307,6 +307,8 @@ int orbgpu_matcher_reserve(orb_matcher_t m, size_t bytes, char** d_buf, char** h
     return ORB_OK;
 }
 
+float orbgpu_matcher_nnratio(orb_matcher_t m) { return m->nnratio; }
+
 extern "C" {
 
 int orb_matcher_create(float nnratio, int check_orientation, orb_matcher_t* out) {

@@ -127,3 +127,26 @@ class Frame:
         v.Tcw[:] = [float(x) for x in self.Tcw.reshape(-1)]
         self._keep_last = v
         return v
+
+
+class LocalPointsView(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("track_in_view", ctypes.c_void_p), ("is_bad", ctypes.c_void_p),
+                ("observed", ctypes.c_void_p), ("track_proj", ctypes.c_void_p), ("track_view_cos", ctypes.c_void_p),
+                ("track_depth", ctypes.c_void_p), ("track_level", ctypes.c_void_p), ("desc", ctypes.c_void_p)]
+
+
+class LocalMapPoints:
+    """Local map points with the tracking fields Frame::isInFrustum sets (src/Frame.cc:667-773)."""
+
+    _fields = (("track_in_view", np.uint8), ("is_bad", np.uint8), ("observed", np.uint8), ("track_proj", np.float32),
+               ("track_view_cos", np.float32), ("track_depth", np.float32), ("track_level", np.int32),
+               ("desc", np.uint8))
+
+    def __init__(self, **arrays):
+        for k, dt in self._fields:
+            setattr(self, k, np.ascontiguousarray(arrays[k], dtype=dt))
+        self.n = len(self.track_in_view)
+
+    def view(self) -> LocalPointsView:
+        self._v = LocalPointsView(self.n, *[_ptr(getattr(self, k)) for k, _ in self._fields])
+        return self._v

@@ -7,7 +7,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import check
-from .keyframe import Frame, KeyFrame, KfView, PairGeom
+from .keyframe import Frame, KeyFrame, KfView, LocalMapPoints, PairGeom
 
 TH_HIGH = 100  # src/ORBmatcher.cc:36
 TH_LOW = 50    # src/ORBmatcher.cc:37
@@ -109,3 +109,18 @@ class ORBmatcher:
                                                          int(bMono), m.ctypes.data, ctypes.byref(n)),
               "orb_search_by_projection_frame")
         return n.value, m[:CurrentFrame.N]
+
+    def SearchByProjection(self, F: Frame, vpMapPoints: LocalMapPoints, th: float = 3, bFarPoints: bool = False,
+                           thFarPoints: float = 50.0, frame_taken=None):
+        """SearchByProjection(Frame &F, const vector<MapPoint*> &vpMapPoints, th, bFarPoints, thFarPoints)
+        (src/ORBmatcher.cc:46-240).  frame_taken[i]: keypoint i already holds a map point with
+        observations.  Returns (nmatches, match) with match[i] = index of the map point assigned."""
+        m = np.full(max(F.N, 1), -1, np.int32)
+        n = ctypes.c_int32()
+        tk = None if frame_taken is None else np.ascontiguousarray(frame_taken, dtype=np.uint8)
+        check(_lib.load().orb_search_by_projection_local(self._handle(), ctypes.byref(F.view()),
+                                                         None if tk is None else tk.ctypes.data,
+                                                         ctypes.byref(vpMapPoints.view()), float(th), int(bFarPoints),
+                                                         float(thFarPoints), m.ctypes.data, ctypes.byref(n)),
+              "orb_search_by_projection_local")
+        return n.value, m[:F.N]

@@ -373,3 +373,33 @@ def tracking_pair(n_points: int = 1200, seed: int = 31, width: int = 752, height
                 map_points=dict(valid=valid.astype(np.uint8), observed=observed, xyz=xyz, desc=mdesc), **common)
     cur = dict(keys_un=ck, descriptors=cd, Tcw=cT, u_right=cur_ if stereo else None, **common)
     return cur, last
+
+
+def local_map_points(cur: dict, n_points: int = 1500, seed: int = 51, width: int = 752, height: int = 480,
+                     nlevels: int = 8, bad_frac: float = 0.03, unobserved_frac: float = 0.1, dup_frac: float = 0.05):
+    """Local map points for SearchByProjection(Frame, vector<MapPoint*>): the tracking fields
+    isInFrustum would write for the current frame `cur` (from tracking_pair): projection (u, v, u_R),
+    view cosine, depth and predicted level; descriptors close to the frame's keypoints for most
+    points; a few bad / unobserved / duplicated points."""
+    rng = np.random.default_rng(seed)
+    kps = cur["keys_un"]
+    desc = cur["descriptors"]
+    n = n_points
+    pick = rng.integers(0, len(kps), n)
+    proj = np.zeros((n, 3), np.float32)
+    proj[:, 0] = np.clip(kps["x"][pick] + rng.normal(0, 2.0, n), 0, width - 1)
+    proj[:, 1] = np.clip(kps["y"][pick] + rng.normal(0, 2.0, n), 0, height - 1)
+    depth = rng.uniform(1.5, 15, n).astype(np.float32)
+    proj[:, 2] = proj[:, 0] - np.float32(EUROC_BF) / depth
+    lvl = np.clip(kps["octave"][pick] + rng.integers(-1, 2, n), 0, nlevels - 1).astype(np.int32)
+    bits = np.unpackbits(desc[pick], axis=1)
+    for i in range(n):
+        bits[i, rng.choice(256, int(rng.integers(0, 45)), replace=False)] ^= 1
+    mdesc = np.packbits(bits, axis=1)
+    ndup = int(dup_frac * n)
+    a, b = rng.choice(n, ndup, replace=False), rng.choice(n, ndup, replace=False)
+    mdesc[b], proj[b], lvl[b] = mdesc[a], proj[a], lvl[a]
+    return dict(track_in_view=(rng.random(n) > 0.1).astype(np.uint8), is_bad=(rng.random(n) < bad_frac).astype(np.uint8),
+                observed=(rng.random(n) > unobserved_frac).astype(np.uint8), track_proj=proj,
+                track_view_cos=rng.choice(np.array([0.999, 0.99], np.float32), n), track_depth=depth,
+                track_level=lvl, desc=mdesc)

@@ -117,3 +117,68 @@ def test_projection_oracle_matches_python(pkg, oracle, synth, th, mono, ori, ste
     pn, pm = py_search(C, L, th, mono, ori)
     assert n == pn and np.array_equal(m, pm), f"{int((m != pm).sum())} differences"
     assert n > 100
+
+
+def py_search_local(F, P, th, far, th_far, ratio, taken=None):
+    grid = {}
+    for i, kp in enumerate(F.mvKeysUn):
+        px = int(np.round(f32(f32(kp["x"] - f32(F.mnMinX)) * f32(F.mfGridElementWidthInv))))
+        py = int(np.round(f32(f32(kp["y"] - f32(F.mnMinY)) * f32(F.mfGridElementHeightInv))))
+        if 0 <= px < 64 and 0 <= py < 48:
+            grid.setdefault((px, py), []).append(i)
+    D = np.unpackbits(P.desc[:, None, :] ^ F.mDescriptors[None, :, :], axis=2).sum(axis=2)
+    owner = np.zeros(F.N, bool) if taken is None else taken.astype(bool).copy()
+    match = np.full(F.N, -1)
+    n = 0
+    for i in range(P.n):
+        if not P.track_in_view[i] or (far and P.track_depth[i] > f32(th_far)) or P.is_bad[i]:
+            continue
+        lvl = int(P.track_level[i])
+        r = f32(2.5) if float(P.track_view_cos[i]) > 0.998 else f32(4.0)
+        if f32(th) != f32(1.0):
+            r = f32(r * f32(th))
+        rad = f32(r * F.mvScaleFactors[lvl])
+        x, y, xr = (f32(v) for v in P.track_proj[i])
+        x0 = max(0, math.floor(f32(f32(f32(x - f32(F.mnMinX)) - rad) * f32(F.mfGridElementWidthInv))))
+        x1 = min(63, math.ceil(f32(f32(f32(x - f32(F.mnMinX)) + rad) * f32(F.mfGridElementWidthInv))))
+        y0 = max(0, math.floor(f32(f32(f32(y - f32(F.mnMinY)) - rad) * f32(F.mfGridElementHeightInv))))
+        y1 = min(47, math.ceil(f32(f32(f32(y - f32(F.mnMinY)) + rad) * f32(F.mfGridElementHeightInv))))
+        if x0 >= 64 or x1 < 0 or y0 >= 48 or y1 < 0:
+            continue
+        b1, l1, b2, l2, bi = 256, -1, 256, -1, -1
+        for ix in range(x0, x1 + 1):
+            for iy in range(y0, y1 + 1):
+                for j in grid.get((ix, iy), []):
+                    kp = F.mvKeysUn[j]
+                    if kp["octave"] < lvl - 1 or kp["octave"] > lvl:
+                        continue
+                    if not (abs(f32(kp["x"] - x)) < rad and abs(f32(kp["y"] - y)) < rad):
+                        continue
+                    if owner[j]:
+                        continue
+                    if F.mvuRight is not None and F.mvuRight[j] > 0 and abs(f32(xr - F.mvuRight[j])) > rad:
+                        continue
+                    d = int(D[i, j])
+                    if d < b1:
+                        b2, l2, b1, l1, bi = b1, l1, d, int(kp["octave"]), j
+                    elif d < b2:
+                        b2, l2 = d, int(kp["octave"])
+        if b1 <= 100:
+            if l1 == l2 and f32(b1) > f32(f32(ratio) * f32(b2)):
+                continue
+            match[bi] = i
+            owner[bi] = bool(P.observed[i])
+            n += 1
+    return n, match
+
+
+@pytest.mark.parametrize("th,far", [(1, False), (3, False), (5, True)])
+def test_local_projection_oracle_matches_python(pkg, oracle, synth, th, far):
+    cur, _ = synth.tracking_pair(n_points=400, clutter=100, seed=43)
+    F = pkg.Frame(**cur)
+    P = pkg.LocalMapPoints(**synth.local_map_points(cur, n_points=500, seed=44))
+    taken = (np.random.default_rng(3).random(F.N) < 0.05).astype(np.uint8)
+    n, m = oracle.search_by_projection_local(F, P, th, far, 10.0, 0.8, taken)
+    pn, pm = py_search_local(F, P, th, far, 10.0, 0.8, taken)
+    assert n == pn and np.array_equal(m, pm), f"{int((m != pm).sum())} differences"
+    assert n > 50

@@ -37,3 +37,18 @@ def test_search_by_projection_frame_edge_cases(pkg, oracle, synth):
     n, got = m.SearchByProjectionFrame(C, L, 60, False)
     rn, exp = oracle.search_by_projection_frame(C, L, 60, False, True)
     assert n == rn and np.array_equal(got, exp)
+
+
+@pytest.mark.parametrize("seed,th,far,ratio,taken_frac", [(51, 1, False, 0.8, 0.0), (52, 3, False, 0.9, 0.05),
+                                                           (53, 5, True, 0.6, 0.1), (54, 10, False, 0.8, 0.0)])
+def test_search_by_projection_local_parity(pkg, oracle, synth, seed, th, far, ratio, taken_frac):
+    cur, _ = synth.tracking_pair(seed=seed)
+    F = pkg.Frame(**cur)
+    P = pkg.LocalMapPoints(**synth.local_map_points(cur, seed=seed + 100))
+    taken = (np.random.default_rng(seed).random(F.N) < taken_frac).astype(np.uint8)
+    m = pkg.ORBmatcher(ratio, True)
+    n, got = m.SearchByProjection(F, P, th, far, 10.0, taken)
+    rn, exp = oracle.search_by_projection_local(F, P, th, far, 10.0, ratio, taken)
+    assert n == rn, f"{n} vs oracle {rn}"
+    assert np.array_equal(got, exp), f"{int((got != exp).sum())} differing assignments"
+    assert n > 50
