@@ -278,6 +278,23 @@ int orb_ba_destroy(orb_ba_t h);
 int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* problem, const orb_ba_options_t* options, double* edge_chi2,
                     uint8_t* edge_depth_ok, orb_ba_result_t* result);
 
+/* ---- multi-GPU local BA: one process per GPU, every rank passes the same
+ * problem; rank r owns a contiguous, edge-balanced range of the landmarks and their edges, and
+ * the ranks all-reduce the partial Hpp/b_p, the partial reduced camera system (S, b_S) of each LM
+ * trial and the chi2 / scale partials.  Every rank factors S and updates the poses identically,
+ * and the results of all ranks are identical. */
+#define ORB_BA_SUM 0
+#define ORB_BA_MAX 1
+/* In-place all-reduce of n doubles in host memory across the ranks; returns 0 on success. */
+typedef int (*orb_ba_host_reduce_fn)(void* ctx, double* host_buf, size_t n, int op);
+
+/* ncclGetUniqueId of the RCCL loaded in the process (librccl.so.1); 128 bytes. */
+int orb_ba_dist_unique_id(uint8_t id[128]);
+/* Attach an RCCL communicator (ncclCommInitRank over `id`) to the handle: device all-reduces. */
+int orb_ba_dist_init_rccl(orb_ba_t h, const uint8_t id[128], int world, int rank);
+/* Attach a host-memory reducer instead (e.g. an MPI or gloo all-reduce). */
+int orb_ba_dist_init_host(orb_ba_t h, orb_ba_host_reduce_fn fn, void* ctx, int world, int rank);
+
 #ifdef __cplusplus
 }
 #endif

@@ -65,6 +65,9 @@ PROTOTYPES = {
     "orb_ba_create": (_i, [ctypes.POINTER(_vp)]),
     "orb_ba_destroy": (_i, [_vp]),
     "orb_ba_optimize": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "orb_ba_dist_unique_id": (_i, [_vp]),
+    "orb_ba_dist_init_rccl": (_i, [_vp, _vp, _i, _i]),
+    "orb_ba_dist_init_host": (_i, [_vp, _vp, _vp, _i, _i]),
 }
 
 # parity / debugging hooks exported by the library (not part of the public header)

@@ -23,6 +23,7 @@
 // Reductions run in a fixed order, so results are deterministic; they differ from g2o's serial
 // sums by rounding only (parity bar: 1e-6 RMSE on poses).  S is factored with Cholesky; Eigen's
 // SimplicialLDLT differs only by rounding on the SPD matrices LM produces (H PSD, lambda > 0).
+#include <dlfcn.h>
 #include <hip/hip_cooperative_groups.h>
 #include <hip/hip_runtime.h>
 
@@ -383,7 +384,7 @@ __global__ __launch_bounds__(kT) void k_ba_schur_edges(int nfe, double lambda, c
 // S block (bi, bj), bi <= bj, one wave: lanes split the block's (Z_a, Hpl_b) products, each
 // accumulating the full 6x6 partial sum; lane e < 36 then adds the 64 partials in lane order.
 // S = [Hpp + lambda I] - sum Z_a Hpl_b^T; written to both triangles.
-__global__ __launch_bounds__(64) void k_ba_schur_blocks(int n, double lambda, const int32_t* __restrict__ bi,
+__global__ __launch_bounds__(64) void k_ba_schur_blocks(int n, double lambda, int add_diag, const int32_t* __restrict__ bi,
                                                         const int32_t* __restrict__ bj, const int32_t* __restrict__ off,
                                                         const int32_t* __restrict__ pa, const int32_t* __restrict__ pb,
                                                         const double* __restrict__ z, const double* __restrict__ hpl,
@@ -414,7 +415,7 @@ __global__ __launch_bounds__(64) void k_ba_schur_blocks(int n, double lambda, co
     const int r = lane / 6, c = lane % 6;
     const int i = bi[blk], j = bj[blk];
     double v = -sum;
-    if (i == j) v = (hpp[36 * (size_t)i + 6 * r + c] + (r == c ? lambda : 0.0)) - sum;
+    if (i == j && add_diag) v = (hpp[36 * (size_t)i + 6 * r + c] + (r == c ? lambda : 0.0)) - sum;
     S[(size_t)(6 * i + r) * n + 6 * j + c] = v;
     S[(size_t)(6 * j + c) * n + 6 * i + r] = v;
 }
@@ -422,7 +423,7 @@ __global__ __launch_bounds__(64) void k_ba_schur_blocks(int n, double lambda, co
 // b_S = b_p - sum over the pose's edges of Hpl_e db (one wave per free pose)
 __global__ __launch_bounds__(64) void k_ba_schur_rhs(const int32_t* __restrict__ off, const int32_t* __restrict__ eidx,
                                                      const double* __restrict__ cb, const double* __restrict__ bp,
-                                                     double* __restrict__ bs) {
+                                                     int use_bp, double* __restrict__ bs) {
     __shared__ double red[6][65];
     const int p = blockIdx.x, lane = threadIdx.x;
     double s[6] = {0, 0, 0, 0, 0, 0};
@@ -437,7 +438,7 @@ __global__ __launch_bounds__(64) void k_ba_schur_rhs(const int32_t* __restrict__
             for (int i = 0; i < 6; ++i) red[i][lane] += red[i][lane + w];
         __syncthreads();
     }
-    if (lane < 6) bs[6 * (size_t)p + lane] = bp[6 * (size_t)p + lane] - red[lane][0];
+    if (lane < 6) bs[6 * (size_t)p + lane] = (use_bp ? bp[6 * (size_t)p + lane] : 0.0) - red[lane][0];
 }
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
@@ -934,14 +935,14 @@ __global__ __launch_bounds__(kT) void k_ba_restore(int nf, int nl, const int32_t
 }
 
 // out[0] = sum rho0 (activeRobustChi2), out[1] = sum x (lambda x + b) (computeScale, before +1e-3)
-__global__ __launch_bounds__(1024) void k_ba_sums(int ne, const double* __restrict__ rho0, int nx, double lambda,
+__global__ __launch_bounds__(1024) void k_ba_sums(int ne, const double* __restrict__ rho0, int x0, int nx, double lambda,
                                                   const double* __restrict__ x, const double* __restrict__ b,
                                                   double* __restrict__ out) {
     __shared__ double r0[1024], r1[1024];
     double a = 0, c = 0;
     for (int i = threadIdx.x; i < ne; i += 1024) a += rho0[i];
     if (x)
-        for (int i = threadIdx.x; i < nx; i += 1024) c += x[i] * (lambda * x[i] + b[i]);
+        for (int i = x0 + threadIdx.x; i < nx; i += 1024) c += x[i] * (lambda * x[i] + b[i]);
     r0[threadIdx.x] = a;
     r1[threadIdx.x] = c;
     __syncthreads();
@@ -1006,8 +1007,16 @@ struct orb_ba_s {
     DevBuf<int32_t> pose_h, free_pose, land_point, land_off, land_edge, landf_off, landf_edge, fland, pose_off, pose_edge,
         blk_i, blk_j, blk_off, pair_a, pair_b, status;
     DevBuf<uint8_t> depth;
-    double* h_scal = nullptr;  // pinned: [0] chi2, [1] scale, [2] status, [3] maxdiag
+    double* h_scal = nullptr;  // pinned: [0] chi2, [1] scale, [2] status, [3] maxdiag, [4] stop
     float ms_total = 0;
+    // multi-GPU: ranks own landmark ranges; partial sums are all-reduced
+    int world = 1, rank = 0;
+    orb_ba_host_reduce_fn host_fn = nullptr;
+    void* host_ctx = nullptr;
+    void* nccl_comm = nullptr;
+    double* h_red = nullptr;  // pinned staging of the host reducer
+    size_t h_red_cap = 0;
+    DevBuf<double> red_buf;
 
     void release() {
         for (auto* d : {&pose, &pose_bak, &point, &point_bak, &err, &rho0, &ecl, &hpl, &ecp, &hpp, &hll, &b, &z,
@@ -1063,9 +1072,95 @@ int orb_ba_destroy(orb_ba_t h) {
     if (!h) return ORB_OK;
     hipStreamSynchronize(h->stream);
     h->release();
+    h->red_buf.release();
     if (h->h_scal) hipHostFree(h->h_scal);
+    if (h->h_red) hipHostFree(h->h_red);
     hipStreamDestroy(h->stream);
     delete h;
+    return ORB_OK;
+}
+
+// ---- collectives of the sharded solve -------------------------------------------------------------
+namespace {
+
+// RCCL entry points, resolved from the librccl.so.1 already loaded in the process (torch's) or from
+// /opt/rocm/lib: no link-time dependency, one RCCL instance per process.
+struct Rccl {
+    typedef int (*GetUniqueId)(void*);
+    typedef int (*CommInitRank)(void**, int, const void*, int);
+    typedef int (*AllReduce)(const void*, void*, size_t, int, int, void*, hipStream_t);
+    typedef int (*CommDestroy)(void*);
+    GetUniqueId get_id = nullptr;
+    CommInitRank init = nullptr;
+    AllReduce all_reduce = nullptr;
+    CommDestroy destroy = nullptr;
+    bool load() {
+        if (all_reduce) return true;
+        void* lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+        if (!lib) lib = dlopen("librccl.so.1", RTLD_NOW);
+        if (!lib) lib = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW);
+        if (!lib) return false;
+        get_id = (GetUniqueId)dlsym(lib, "ncclGetUniqueId");
+        init = (CommInitRank)dlsym(lib, "ncclCommInitRank");
+        all_reduce = (AllReduce)dlsym(lib, "ncclAllReduce");
+        destroy = (CommDestroy)dlsym(lib, "ncclCommDestroy");
+        return get_id && init && all_reduce && destroy;
+    }
+};
+Rccl g_rccl;
+constexpr int kNcclDouble = 8, kNcclSum = 0, kNcclMax = 2;  // ncclDataType_t / ncclRedOp_t values
+
+// In-place all-reduce of n doubles at device address d (stream-ordered); no-op on one rank.
+bool dev_reduce(orb_ba_s* h, double* d, size_t n, int op) {
+    if (h->world <= 1 || n == 0) return true;
+    if (h->nccl_comm)
+        return g_rccl.all_reduce(d, d, n, kNcclDouble, op == ORB_BA_MAX ? kNcclMax : kNcclSum, h->nccl_comm,
+                                 h->stream) == 0;
+    if (n > h->h_red_cap) {
+        if (h->h_red) hipHostFree(h->h_red);
+        h->h_red = nullptr;
+        h->h_red_cap = 0;
+        if (hipHostMalloc(&h->h_red, n * sizeof(double), hipHostMallocDefault) != hipSuccess) return false;
+        h->h_red_cap = n;
+    }
+    if (hipMemcpyAsync(h->h_red, d, n * sizeof(double), hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+        hipStreamSynchronize(h->stream) != hipSuccess)
+        return false;
+    if (h->host_fn(h->host_ctx, h->h_red, n, op) != 0) return false;
+    return hipMemcpyAsync(d, h->h_red, n * sizeof(double), hipMemcpyHostToDevice, h->stream) == hipSuccess;
+}
+
+}  // namespace
+
+int orb_ba_dist_unique_id(uint8_t id[128]) {
+    if (!id) return orbgpu_fail(ORB_ERR_ARG, "null id");
+    if (!g_rccl.load()) return orbgpu_fail(ORB_ERR_DEVICE, "librccl.so.1 not found");
+    if (g_rccl.get_id(id) != 0) return orbgpu_fail(ORB_ERR_DEVICE, "ncclGetUniqueId failed");
+    return ORB_OK;
+}
+
+int orb_ba_dist_init_rccl(orb_ba_t h, const uint8_t id[128], int world, int rank) {
+    if (!h || !id || world < 1 || rank < 0 || rank >= world) return orbgpu_fail(ORB_ERR_ARG, "bad RCCL arguments");
+    if (!g_rccl.load()) return orbgpu_fail(ORB_ERR_DEVICE, "librccl.so.1 not found");
+    if (h->nccl_comm) g_rccl.destroy(h->nccl_comm);
+    h->nccl_comm = nullptr;
+    if (world > 1 && g_rccl.init(&h->nccl_comm, world, id, rank) != 0)
+        return orbgpu_fail(ORB_ERR_DEVICE, "ncclCommInitRank failed");
+    h->world = world;
+    h->rank = rank;
+    h->host_fn = nullptr;
+    return ORB_OK;
+}
+
+int orb_ba_dist_init_host(orb_ba_t h, orb_ba_host_reduce_fn fn, void* ctx, int world, int rank) {
+    if (!h || (world > 1 && !fn) || world < 1 || rank < 0 || rank >= world)
+        return orbgpu_fail(ORB_ERR_ARG, "bad host reducer arguments");
+    if (h->nccl_comm) g_rccl.destroy(h->nccl_comm);
+    h->nccl_comm = nullptr;
+    h->host_fn = fn;
+    h->host_ctx = ctx;
+    h->world = world;
+    h->rank = rank;
     return ORB_OK;
 }
 
@@ -1073,20 +1168,34 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                     uint8_t* edge_depth_ok, orb_ba_result_t* res) {
     if (!h || !pr || !opt || !res) return orbgpu_fail(ORB_ERR_ARG, "null BA argument");
     memset(res, 0, sizeof(*res));
-    const int np = pr->n_poses, nq = pr->n_points, ne = pr->n_edges;
-    if (np < 0 || nq < 0 || ne < 0 || (np && (!pr->pose || !pr->pose_id || !pr->pose_fixed || !pr->pose_camera)) ||
-        (nq && (!pr->point || !pr->point_id)) || (ne && !pr->edges) || opt->iterations < 0)
+    const int np = pr->n_poses, nq = pr->n_points, ne_all = pr->n_edges;
+    if (np < 0 || nq < 0 || ne_all < 0 || (np && (!pr->pose || !pr->pose_id || !pr->pose_fixed || !pr->pose_camera)) ||
+        (nq && (!pr->point || !pr->point_id)) || (ne_all && !pr->edges) || opt->iterations < 0)
         return orbgpu_fail(ORB_ERR_ARG, "invalid BA problem");
-    for (int e = 0; e < ne; ++e) {
+    for (int e = 0; e < ne_all; ++e) {
         const orb_ba_edge_t& E = pr->edges[e];
         if (E.point < 0 || E.point >= nq || E.pose < 0 || E.pose >= np || (E.stereo != 0 && E.stereo != 1))
             return orbgpu_fail(ORB_ERR_ARG, "BA edge references a missing vertex");
     }
-    auto stop = [&]() { return opt->stop_flag && *opt->stop_flag; };
+    const bool dist = h->world > 1;
+    const bool primary = h->rank == 0;
+    hipStream_t s = h->stream;
+    if (!h->scal.grow(8)) return orbgpu_fail(ORB_ERR_DEVICE, "BA scalar buffer");
+    // the stop flag, agreed across the ranks (MAX) so that every rank takes the same path
+    auto stop = [&]() -> bool {
+        double f = (opt->stop_flag && *opt->stop_flag) ? 1.0 : 0.0;
+        if (!dist) return f != 0.0;
+        h->h_scal[4] = f;
+        hipMemcpyAsync(h->scal.p + 4, &h->h_scal[4], sizeof(double), hipMemcpyHostToDevice, s);
+        dev_reduce(h, h->scal.p + 4, 1, ORB_BA_MAX);
+        hipMemcpyAsync(&h->h_scal[4], h->scal.p + 4, sizeof(double), hipMemcpyDeviceToHost, s);
+        hipStreamSynchronize(s);
+        return h->h_scal[4] != 0.0;
+    };
 
-    // ---- structure (initializeOptimization + BlockSolver::buildStructure)
+    // ---- structure (initializeOptimization + BlockSolver::buildStructure), from the whole problem
     std::vector<int> pdeg(np, 0), qdeg(nq, 0);
-    for (int e = 0; e < ne; ++e) { pdeg[pr->edges[e].pose]++; qdeg[pr->edges[e].point]++; }
+    for (int e = 0; e < ne_all; ++e) { pdeg[pr->edges[e].pose]++; qdeg[pr->edges[e].point]++; }
     std::vector<int> order(np);
     std::iota(order.begin(), order.end(), 0);
     std::sort(order.begin(), order.end(), [&](int a, int b) { return pr->pose_id[a] < pr->pose_id[b]; });
@@ -1096,28 +1205,48 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     std::vector<int> qorder(nq);
     std::iota(qorder.begin(), qorder.end(), 0);
     std::sort(qorder.begin(), qorder.end(), [&](int a, int b) { return pr->point_id[a] < pr->point_id[b]; });
-    std::vector<int32_t> point_l(nq, -1), land_point;
+    std::vector<int> all_land;
     for (int i : qorder)
-        if (qdeg[i]) { point_l[i] = (int32_t)land_point.size(); land_point.push_back(i); }
-    const int nf = (int)free_pose.size(), nl = (int)land_point.size();
-    if (ne == 0 || nf + nl == 0) {  // SparseOptimizer::optimize returns -1: nothing to do
-        for (int e = 0; e < ne; ++e) {
+        if (qdeg[i]) all_land.push_back(i);
+    const int nf = (int)free_pose.size(), nl_all = (int)all_land.size();
+    if (ne_all == 0 || nf + nl_all == 0) {  // SparseOptimizer::optimize returns -1: nothing to do
+        for (int e = 0; e < ne_all; ++e) {
             if (edge_chi2) edge_chi2[e] = 0;
             if (edge_depth_ok) edge_depth_ok[e] = 0;
         }
         return ORB_OK;
     }
     if (stop()) { res->stopped = 1; return ORB_ERR_ABORTED; }
+    // this rank's landmarks: a contiguous range of the landmark order with about 1/world of the edges
+    int l_begin = 0, l_end = nl_all;
+    if (dist) {
+        std::vector<long long> cum(nl_all + 1, 0);
+        for (int l = 0; l < nl_all; ++l) cum[l + 1] = cum[l] + qdeg[all_land[l]];
+        auto cut = [&](int r) {
+            const long long target = cum[nl_all] * r / h->world;
+            return (int)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
+        };
+        l_begin = h->rank == 0 ? 0 : cut(h->rank);
+        l_end = h->rank == h->world - 1 ? nl_all : cut(h->rank + 1);
+    }
+    std::vector<int32_t> point_l(nq, -1), land_point(all_land.begin() + l_begin, all_land.begin() + l_end);
+    for (int l = 0; l < (int)land_point.size(); ++l) point_l[land_point[l]] = l;
+    std::vector<int32_t> lmap;  // local edge -> problem edge (problem order kept)
+    for (int e = 0; e < ne_all; ++e)
+        if (point_l[pr->edges[e].point] >= 0) lmap.push_back(e);
+    std::vector<EdgeDev> ledges(lmap.size());
+    for (size_t k = 0; k < lmap.size(); ++k) memcpy(&ledges[k], &pr->edges[lmap[k]], sizeof(EdgeDev));
+    const int ne = (int)lmap.size(), nl = (int)land_point.size();
     const int n = 6 * nf, m = 3 * nl;
-    
+
     // landmark -> all edges (edge order), landmark -> free-pose edges (pose row ascending), pose -> edges
     std::vector<int32_t> land_off(nl + 1, 0), land_edge(ne), landf_off(nl + 1, 0), landf_edge, pose_off(nf + 1, 0),
         pose_edge;
     for (int e = 0; e < ne; ++e) {
-        land_off[point_l[pr->edges[e].point] + 1]++;
-        if (pose_h[pr->edges[e].pose] >= 0) {
-            landf_off[point_l[pr->edges[e].point] + 1]++;
-            pose_off[pose_h[pr->edges[e].pose] + 1]++;
+        land_off[point_l[ledges[e].point] + 1]++;
+        if (pose_h[ledges[e].pose] >= 0) {
+            landf_off[point_l[ledges[e].point] + 1]++;
+            pose_off[pose_h[ledges[e].pose] + 1]++;
         }
     }
     for (int l = 0; l < nl; ++l) { land_off[l + 1] += land_off[l]; landf_off[l + 1] += landf_off[l]; }
@@ -1128,7 +1257,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         std::vector<int32_t> c1(land_off.begin(), land_off.end() - 1), c2(landf_off.begin(), landf_off.end() - 1),
             c3(pose_off.begin(), pose_off.end() - 1);
         for (int e = 0; e < ne; ++e) {
-            const int l = point_l[pr->edges[e].point], p = pose_h[pr->edges[e].pose];
+            const int l = point_l[ledges[e].point], p = pose_h[ledges[e].pose];
             land_edge[c1[l]++] = e;
             if (p >= 0) {
                 landf_edge[c2[l]++] = e;
@@ -1138,18 +1267,24 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     }
     for (int l = 0; l < nl; ++l)
         std::stable_sort(landf_edge.begin() + landf_off[l], landf_edge.begin() + landf_off[l + 1],
-                         [&](int a, int b) { return pose_h[pr->edges[a].pose] < pose_h[pr->edges[b].pose]; });
+                         [&](int a, int b) { return pose_h[ledges[a].pose] < pose_h[ledges[b].pose]; });
     const int nfe = (int)landf_edge.size();
     std::vector<int32_t> fland(nfe);
     for (int l = 0; l < nl; ++l)
         for (int k = landf_off[l]; k < landf_off[l + 1]; ++k) fland[k] = l;
-    // Schur block pattern: (row_a <= row_b) products per landmark, in landmark order
+    // Schur block pattern: every diagonal block, then the (row_a <= row_b) products per landmark
     std::vector<int32_t> blk_id((size_t)nf * nf, -1), blk_i, blk_j;
     std::vector<int32_t> cnt;
+    for (int i = 0; i < nf; ++i) {
+        blk_id[(size_t)i * nf + i] = (int32_t)blk_i.size();
+        blk_i.push_back(i);
+        blk_j.push_back(i);
+        cnt.push_back(0);
+    }
     for (int l = 0; l < nl; ++l)
         for (int a = landf_off[l]; a < landf_off[l + 1]; ++a)
             for (int b2 = a; b2 < landf_off[l + 1]; ++b2) {
-                const int i = pose_h[pr->edges[landf_edge[a]].pose], j = pose_h[pr->edges[landf_edge[b2]].pose];
+                const int i = pose_h[ledges[landf_edge[a]].pose], j = pose_h[ledges[landf_edge[b2]].pose];
                 int32_t& id = blk_id[(size_t)i * nf + j];
                 if (id < 0) { id = (int32_t)blk_i.size(); blk_i.push_back(i); blk_j.push_back(j); cnt.push_back(0); }
                 cnt[id]++;
@@ -1163,7 +1298,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         for (int l = 0; l < nl; ++l)
             for (int a = landf_off[l]; a < landf_off[l + 1]; ++a)
                 for (int b2 = a; b2 < landf_off[l + 1]; ++b2) {
-                    const int i = pose_h[pr->edges[landf_edge[a]].pose], j = pose_h[pr->edges[landf_edge[b2]].pose];
+                    const int i = pose_h[ledges[landf_edge[a]].pose], j = pose_h[ledges[landf_edge[b2]].pose];
                     const int id = blk_id[(size_t)i * nf + j];
                     pair_a[c[id]] = landf_edge[a];
                     pair_b[c[id]++] = landf_edge[b2];
@@ -1178,29 +1313,26 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         if (nn > 0) for (int k = 0; k < 4; ++k) q[k] /= nn;
     }
 
-    hipStream_t s = h->stream;
+    const size_t ne1 = std::max(ne, 1);
     bool ok = upload(h->pose, pose, s) && h->pose_bak.grow(7 * (size_t)np) &&
               upload(h->point, pr->point, 3 * (size_t)nq, s) && h->point_bak.grow(3 * (size_t)nq) &&
-              upload(h->edges, reinterpret_cast<const EdgeDev*>(pr->edges), ne, s) &&
-              upload(h->cams, pr->pose_camera, np, s) && upload(h->pose_h, pose_h, s) &&
+              upload(h->edges, ledges, s) && upload(h->cams, pr->pose_camera, np, s) && upload(h->pose_h, pose_h, s) &&
               upload(h->free_pose, free_pose, s) && upload(h->land_point, land_point, s) &&
               upload(h->land_off, land_off, s) && upload(h->land_edge, land_edge, s) &&
               upload(h->landf_off, landf_off, s) && upload(h->landf_edge, landf_edge, s) && upload(h->fland, fland, s) &&
               upload(h->pose_off, pose_off, s) && upload(h->pose_edge, pose_edge, s) && upload(h->blk_i, blk_i, s) &&
               upload(h->blk_j, blk_j, s) && upload(h->blk_off, blk_off, s) && upload(h->pair_a, pair_a, s) &&
-              upload(h->pair_b, pair_b, s) && h->err.grow(3 * (size_t)ne) && h->rho0.grow(ne) &&
-              h->ecl.grow(12 * (size_t)ne) && h->hpl.grow(18 * (size_t)ne) && h->ecp.grow(42 * (size_t)ne) &&
-              h->hpp.grow(36 * (size_t)nf) && h->hll.grow(9 * (size_t)nl) && h->b.grow(n + m) &&
-h->z.grow(18 * (size_t)ne) && h->cb.grow(6 * (size_t)ne) &&
-              h->S.grow((size_t)n * n) && h->LT.grow((size_t)n * n) && h->Linv.grow((size_t)n * 32 + 32 * 32) && h->bs.grow(n) && h->x.grow(n + m) && h->scal.grow(8) && h->status.grow(1) &&
-              h->depth.grow(ne);
+              upload(h->pair_b, pair_b, s) && h->err.grow(3 * ne1) && h->rho0.grow(ne1) && h->ecl.grow(12 * ne1) &&
+              h->hpl.grow(18 * ne1) && h->ecp.grow(42 * ne1) && h->hpp.grow(36 * (size_t)nf) &&
+              h->hll.grow(9 * (size_t)nl) && h->b.grow(n + m) && h->z.grow(18 * ne1) && h->cb.grow(6 * ne1) &&
+              h->S.grow((size_t)n * n) && h->LT.grow((size_t)n * n) && h->Linv.grow((size_t)n * 32 + 32 * 32) &&
+              h->bs.grow(n) && h->x.grow(n + m) && h->status.grow(1) && h->depth.grow(ne1);
     if (!ok) return orbgpu_fail(ORB_ERR_DEVICE, "BA device allocation / upload");
     hipMemsetAsync(h->x.p, 0, sizeof(double) * (n + m), s);  // g2o's _x starts zeroed
 
     const float dm = (float)std::sqrt(5.991), ds = (float)std::sqrt(7.815);  // src/Optimizer.cc:1957-1958
     const Huber2 hub{(double)dm, (double)ds, (float)((double)dm * (double)dm), (float)((double)ds * (double)ds)};
-    // dynamic LDS of the Cholesky kernel: panel rows (n x (NB + 1)) + y (n)
-    // cooperative path: block column rows x (NB + 1) doubles per workgroup (rhs owner: n doubles)
+    // cooperative path (optional): block column rows x (NB + 1) doubles per workgroup
     auto coop_bytes = [&](int b) { return sizeof(double) * (size_t)n * (b + 1); };
     int coop_nb = 0;
     if (coop_bytes(32) <= 136 * 1024) coop_nb = 32;
@@ -1233,6 +1365,7 @@ h->z.grow(18 * (size_t)ne) && h->cb.grow(6 * (size_t)ne) &&
     }
     double* bl = h->b.p + n;
     auto launch_edges = [&](bool build) {
+        if (ne == 0) return;
         if (build)
             hipLaunchKernelGGL(k_ba_edges<true>, dim3(grid(ne)), dim3(kT), 0, s, ne, h->edges.p, h->cams.p, h->pose.p,
                                h->point.p, h->pose_h.p, hub, h->err.p, h->rho0.p, h->ecl.p, h->hpl.p, h->ecp.p);
@@ -1240,9 +1373,12 @@ h->z.grow(18 * (size_t)ne) && h->cb.grow(6 * (size_t)ne) &&
             hipLaunchKernelGGL(k_ba_edges<false>, dim3(grid(ne)), dim3(kT), 0, s, ne, h->edges.p, h->cams.p, h->pose.p,
                                h->point.p, h->pose_h.p, hub, h->err.p, h->rho0.p, h->ecl.p, h->hpl.p, h->ecp.p);
     };
+    // [0] robust chi2 (sum over the ranks' edges), [1] computeScale (pose part counted by rank 0),
+    // [2] factorisation status (identical on every rank), [3] max diag (max over the ranks)
     auto read_scalars = [&](double lambda, bool with_x) -> bool {
-        hipLaunchKernelGGL(k_ba_sums, dim3(1), dim3(1024), 0, s, ne, h->rho0.p, n + m, lambda,
+        hipLaunchKernelGGL(k_ba_sums, dim3(1), dim3(1024), 0, s, ne, h->rho0.p, primary ? 0 : n, n + m, lambda,
                            with_x ? h->x.p : nullptr, h->b.p, h->scal.p);
+        if (!dev_reduce(h, h->scal.p, 2, ORB_BA_SUM) || !dev_reduce(h, h->scal.p + 3, 1, ORB_BA_MAX)) return false;
         hipMemcpyAsync(h->scal.p + 2, h->status.p, sizeof(int32_t), hipMemcpyDeviceToDevice, s);
         hipMemcpyAsync(h->h_scal, h->scal.p, 4 * sizeof(double), hipMemcpyDeviceToHost, s);
         return hipStreamSynchronize(s) == hipSuccess;
@@ -1251,14 +1387,19 @@ h->z.grow(18 * (size_t)ne) && h->cb.grow(6 * (size_t)ne) &&
     double lambda = 0, ni = 2;
     int nBad = 0, it = 0;
     const double tau = 1e-5;
+    hipMemsetAsync(h->scal.p, 0, 8 * sizeof(double), s);
     for (; it < opt->iterations && !stop(); ++it) {
         // computeActiveErrors + activeRobustChi2 + buildSystem
         launch_edges(true);
-        hipLaunchKernelGGL(k_ba_reduce_land, dim3(grid(nl)), dim3(kT), 0, s, nl, h->land_off.p, h->land_edge.p,
-                           h->ecl.p, h->hll.p, bl);
-        if (nf)
+        if (nl)
+            hipLaunchKernelGGL(k_ba_reduce_land, dim3(grid(nl)), dim3(kT), 0, s, nl, h->land_off.p, h->land_edge.p,
+                               h->ecl.p, h->hll.p, bl);
+        if (nf) {
             hipLaunchKernelGGL(k_ba_reduce_pose, dim3(nf), dim3(64), 0, s, h->pose_off.p, h->pose_edge.p, h->ecp.p,
                                h->hpp.p, h->b.p);
+            if (!dev_reduce(h, h->hpp.p, 36 * (size_t)nf, ORB_BA_SUM) || !dev_reduce(h, h->b.p, n, ORB_BA_SUM))
+                return orbgpu_fail(ORB_ERR_DEVICE, "BA all-reduce (Hpp, b_p) failed");
+        }
         if (it == 0)
             hipLaunchKernelGGL(k_ba_maxdiag, dim3(1), dim3(kT), 0, s, nf, nl, h->hpp.p, h->hll.p, h->scal.p + 3);
         if (!read_scalars(0.0, false)) return orbgpu_fail(ORB_ERR_DEVICE, "BA build failed");
@@ -1273,16 +1414,18 @@ h->z.grow(18 * (size_t)ne) && h->cb.grow(6 * (size_t)ne) &&
         double rho = 0;
         int qmax = 0;
         do {
-            // setLambda + BlockSolver::solve
+            // setLambda + BlockSolver::solve (partial S, b_S per rank, then all-reduced)
             if (nfe)
                 hipLaunchKernelGGL(k_ba_schur_edges, dim3(grid(nfe)), dim3(kT), 0, s, nfe, lambda, h->landf_edge.p,
                                    h->fland.p, h->hll.p, bl, h->hpl.p, h->z.p, h->cb.p);
             if (nf) {
                 hipMemsetAsync(h->S.p, 0, sizeof(double) * (size_t)n * n, s);
-                hipLaunchKernelGGL(k_ba_schur_blocks, dim3(nblk), dim3(64), 0, s, n, lambda, h->blk_i.p, h->blk_j.p,
-                                   h->blk_off.p, h->pair_a.p, h->pair_b.p, h->z.p, h->hpl.p, h->hpp.p, h->S.p);
+                hipLaunchKernelGGL(k_ba_schur_blocks, dim3(nblk), dim3(64), 0, s, n, lambda, primary ? 1 : 0, h->blk_i.p,
+                                   h->blk_j.p, h->blk_off.p, h->pair_a.p, h->pair_b.p, h->z.p, h->hpl.p, h->hpp.p, h->S.p);
                 hipLaunchKernelGGL(k_ba_schur_rhs, dim3(nf), dim3(64), 0, s, h->pose_off.p, h->pose_edge.p, h->cb.p,
-                                   h->b.p, h->bs.p);
+                                   h->b.p, primary ? 1 : 0, h->bs.p);
+                if (!dev_reduce(h, h->S.p, (size_t)n * n, ORB_BA_SUM) || !dev_reduce(h, h->bs.p, n, ORB_BA_SUM))
+                    return orbgpu_fail(ORB_ERR_DEVICE, "BA all-reduce (S, b_S) failed");
                 if (coop_nb) {
                     hipMemsetAsync(h->status.p, 0, sizeof(int32_t), s);
                     int nn = n;
@@ -1291,10 +1434,7 @@ h->z.grow(18 * (size_t)ne) && h->cb.grow(6 * (size_t)ne) &&
                     double* bp = h->bs.p;
                     double* xp = h->x.p;
                     int32_t* stp = h->status.p;
-                    static int64_t* d_trace = nullptr;
-                    static const bool tracing = getenv("ORBGPU_BA_TRACE") != nullptr;
-                    if (tracing && !d_trace) hipMalloc(&d_trace, 8 * 1024 * sizeof(int64_t));
-                    int64_t* trp = tracing ? d_trace : nullptr;
+                    int64_t* trp = nullptr;
                     double* Lip = h->Linv.p;
                     void* args[] = {&nn, &Sp, &Lp, &Lip, &bp, &xp, &stp, &trp};
                     const dim3 g((n + coop_nb - 1) / coop_nb + 1);
@@ -1305,28 +1445,6 @@ h->z.grow(18 * (size_t)ne) && h->cb.grow(6 * (size_t)ne) &&
                             : hipLaunchCooperativeKernel((const void*)k_ba_chol_coop<16>, g, dim3(kCoopThreads), args,
                                                          (unsigned)coop_lds, s);
                     if (le != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "cooperative Cholesky launch failed");
-                    if (tracing) {
-                        const int nbc = (n + coop_nb - 1) / coop_nb;
-                        std::vector<int64_t> tr(2 * nbc + 3);
-                        hipMemcpyAsync(tr.data(), d_trace, tr.size() * 8, hipMemcpyDeviceToHost, s);
-                        hipStreamSynchronize(s);
-                        for (int k = 0; k + 1 < nbc; ++k)
-                            fprintf(stderr, "k=%d sync seen %.2f finalize(k+1) done %.2f us\n", k,
-                                    (tr[1 + 2 * k] - tr[0]) / 100.0, (tr[2 + 2 * k] - tr[0]) / 100.0);
-                        fprintf(stderr, "backward start %.2f end %.2f us\n", (tr[2 * nbc + 1] - tr[0]) / 100.0,
-                                (tr[2 * nbc + 2] - tr[0]) / 100.0);
-                        std::vector<int64_t> clk(4);
-                        hipMemcpy(clk.data(), d_trace + 200, 32, hipMemcpyDeviceToHost);
-                        fprintf(stderr, "shader clock estimate: %.1f MHz\n",
-                                100.0 * (double)(clk[3] - clk[1]) / (double)(clk[2] - clk[0]));
-                        std::vector<int64_t> ft(8 * nbc);
-                        hipMemcpy(ft.data(), d_trace + 64, ft.size() * 8, hipMemcpyDeviceToHost);
-                        for (int w = 0; w < nbc; ++w)
-                            fprintf(stderr, "finalize w=%d: diag-upd %.2f chain %.2f inv %.2f apply %.2f gemm %.2f pub %.2f us\n", w,
-                                    (ft[8 * w + 1] - ft[8 * w]) / 100.0, (ft[8 * w + 2] - ft[8 * w + 1]) / 100.0,
-                                    (ft[8 * w + 3] - ft[8 * w + 2]) / 100.0, (ft[8 * w + 4] - ft[8 * w + 3]) / 100.0,
-                                    (ft[8 * w + 5] - ft[8 * w + 4]) / 100.0, (ft[8 * w + 6] - ft[8 * w + 5]) / 100.0);
-                    }
                 } else if (nb == 16)
                     hipLaunchKernelGGL(k_ba_chol<16>, dim3(1), dim3(kCholThreads), chol_lds, s, n, h->S.p, h->LT.p,
                                        h->bs.p, h->x.p, h->status.p);
@@ -1336,8 +1454,9 @@ h->z.grow(18 * (size_t)ne) && h->cb.grow(6 * (size_t)ne) &&
             } else {
                 hipMemsetAsync(h->status.p, 0, sizeof(int32_t), s);
             }
-            hipLaunchKernelGGL(k_ba_backsub, dim3(grid(nl)), dim3(kT), 0, s, nl, n, lambda, h->landf_off.p,
-                               h->landf_edge.p, h->edges.p, h->pose_h.p, h->hpl.p, bl, h->hll.p, h->x.p);
+            if (nl)
+                hipLaunchKernelGGL(k_ba_backsub, dim3(grid(nl)), dim3(kT), 0, s, nl, n, lambda, h->landf_off.p,
+                                   h->landf_edge.p, h->edges.p, h->pose_h.p, h->hpl.p, bl, h->hll.p, h->x.p);
             // SparseOptimizer::update (push first), then computeActiveErrors
             hipLaunchKernelGGL(k_ba_update, dim3(grid(nf + nl)), dim3(kT), 0, s, nf, nl, n, h->free_pose.p,
                                h->land_point.p, h->x.p, h->pose.p, h->pose_bak.p, h->point.p, h->point_bak.p);
@@ -1374,14 +1493,48 @@ h->z.grow(18 * (size_t)ne) && h->cb.grow(6 * (size_t)ne) &&
     res->iterations = it;
     res->lambda = lambda;
     res->stopped = stop() ? 1 : 0;
-    hipLaunchKernelGGL(k_ba_final, dim3(grid(ne)), dim3(kT), 0, s, ne, h->edges.p, h->pose.p, h->point.p, h->err.p,
-                       h->rho0.p, h->depth.p);
+    if (ne)
+        hipLaunchKernelGGL(k_ba_final, dim3(grid(ne)), dim3(kT), 0, s, ne, h->edges.p, h->pose.p, h->point.p, h->err.p,
+                           h->rho0.p, h->depth.p);
     hipMemcpyAsync(pr->pose, h->pose.p, sizeof(double) * 7 * (size_t)np, hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(pr->point, h->point.p, sizeof(double) * 3 * (size_t)nq, hipMemcpyDeviceToHost, s);
-    if (edge_chi2) hipMemcpyAsync(edge_chi2, h->rho0.p, sizeof(double) * ne, hipMemcpyDeviceToHost, s);
-    if (edge_depth_ok) hipMemcpyAsync(edge_depth_ok, h->depth.p, ne, hipMemcpyDeviceToHost, s);
-    if (hipStreamSynchronize(s) != hipSuccess || hipGetLastError() != hipSuccess)
-        return orbgpu_fail(ORB_ERR_DEVICE, "BA device error");
+    std::vector<double> pts(3 * (size_t)nq), lchi(ne1);
+    std::vector<uint8_t> ldep(ne1);
+    hipMemcpyAsync(pts.data(), h->point.p, sizeof(double) * 3 * (size_t)nq, hipMemcpyDeviceToHost, s);
+    if (ne) {
+        hipMemcpyAsync(lchi.data(), h->rho0.p, sizeof(double) * ne, hipMemcpyDeviceToHost, s);
+        hipMemcpyAsync(ldep.data(), h->depth.p, ne, hipMemcpyDeviceToHost, s);
+    }
+    if (hipStreamSynchronize(s) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "BA device error");
+    if (!dist) {
+        memcpy(pr->point, pts.data(), sizeof(double) * 3 * (size_t)nq);
+        for (int e = 0; e < ne; ++e) {
+            if (edge_chi2) edge_chi2[e] = lchi[e];
+            if (edge_depth_ok) edge_depth_ok[e] = ldep[e];
+        }
+        return ORB_OK;
+    }
+    // gather: each rank contributes its landmarks (rank 0 also the points without edges) and its
+    // edges' chi2 / depth flags; one SUM all-reduce of the zero-padded arrays
+    const size_t nred = 3 * (size_t)nq + 2 * (size_t)ne_all;
+    std::vector<double> contrib(nred, 0.0);
+    for (int q = 0; q < nq; ++q)
+        if (point_l[q] >= 0 || (primary && qdeg[q] == 0))
+            for (int k = 0; k < 3; ++k) contrib[3 * (size_t)q + k] = pts[3 * (size_t)q + k];
+    for (int e = 0; e < ne; ++e) {
+        contrib[3 * (size_t)nq + lmap[e]] = lchi[e];
+        contrib[3 * (size_t)nq + ne_all + lmap[e]] = ldep[e] ? 1.0 : 0.0;
+    }
+    if (!h->red_buf.grow(nred) ||
+        hipMemcpyAsync(h->red_buf.p, contrib.data(), nred * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess ||
+        !dev_reduce(h, h->red_buf.p, nred, ORB_BA_SUM) ||
+        hipMemcpyAsync(contrib.data(), h->red_buf.p, nred * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "BA result all-reduce failed");
+    memcpy(pr->point, contrib.data(), sizeof(double) * 3 * (size_t)nq);
+    for (int e = 0; e < ne_all; ++e) {
+        if (edge_chi2) edge_chi2[e] = contrib[3 * (size_t)nq + e];
+        if (edge_depth_ok) edge_depth_ok[e] = contrib[3 * (size_t)nq + ne_all + e] != 0.0;
+    }
     return ORB_OK;
 }
 

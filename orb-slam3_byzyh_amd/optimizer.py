@@ -62,8 +62,38 @@ def make_problem_struct(prob: dict) -> tuple[BaProblem, dict]:
     return s, arrs
 
 
+# orb_ba_host_reduce_fn (include/orbgpu.h): in-place all-reduce of n doubles, op 0 = SUM, 1 = MAX
+HOST_REDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_size_t,
+                                  ctypes.c_int)
+BA_SUM, BA_MAX = 0, 1
+
+
+def make_host_reducer(group=None):
+    """An orb_ba_host_reduce_fn that all-reduces the library's host buffer with the group's own
+    all_reduce (in place, float64).  Returns nonzero to the library when the collective raises."""
+    import torch
+    import torch.distributed as dist
+    ops = {BA_SUM: dist.ReduceOp.SUM, BA_MAX: dist.ReduceOp.MAX}
+
+    def reduce_cb(_ctx, buf, n, op):
+        try:
+            t = torch.from_numpy(np.ctypeslib.as_array(buf, shape=(n,)))
+            dist.all_reduce(t, op=ops[op], group=group)
+            return 0
+        except Exception:  # noqa: BLE001 -- reported to the library as a failed collective
+            return -1
+
+    return HOST_REDUCE_FN(reduce_cb)
+
+
 class LocalBA:
-    """A device handle for repeated local BA solves (one per LocalMapping thread)."""
+    """A device handle for repeated local BA solves (one per LocalMapping thread).
+
+    attach() shards each solve's landmarks over the ranks of a torch.distributed group (DESIGN.md
+    sec. 5): every rank passes the SAME problem; each builds the Schur complement of its landmark
+    range and the partial systems are all-reduced (RCCL for an nccl group, the group's own
+    all_reduce on host buffers for gloo).  Results are identical on every rank.
+    """
 
     def __init__(self):
         lib = _lib.load()
@@ -72,6 +102,37 @@ class LocalBA:
         check(lib.orb_ba_create(ctypes.byref(h)), "orb_ba_create")
         self._h = h
         self._lib = lib
+
+    def attach(self, group=None, transport: str | None = None):
+        """Join the ranks of `group` (default: the world group) for sharded solves.
+
+        transport: "rccl" (device all-reduce inside the library, needs one GPU per rank) or "host"
+        (the group's all_reduce on CPU tensors through a callback).  Default: "rccl" when the
+        group's backend is nccl, else "host"."""
+        import torch
+        import torch.distributed as dist
+        world = dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        if transport is None:
+            transport = "rccl" if dist.get_backend(group) == "nccl" else "host"
+        if transport == "rccl":
+            uid = (ctypes.c_uint8 * 128)()
+            if rank == 0:
+                check(self._lib.orb_ba_dist_unique_id(uid), "orb_ba_dist_unique_id")
+            box = [bytes(uid)]
+            dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                                       group=group)
+            uid = (ctypes.c_uint8 * 128).from_buffer_copy(box[0])
+            check(self._lib.orb_ba_dist_init_rccl(self._h, uid, world, rank), "orb_ba_dist_init_rccl")
+            self._reduce_cb = None
+        elif transport == "host":
+            self._reduce_cb = make_host_reducer(group)  # kept alive with the handle
+            check(self._lib.orb_ba_dist_init_host(self._h, self._reduce_cb, None, world, rank),
+                  "orb_ba_dist_init_host")
+        else:
+            raise ValueError(f"unknown transport {transport!r}")
+        self.world, self.rank, self.transport = world, rank, transport
+        return self
 
     def __del__(self):
         h = getattr(self, "_h", None)

@@ -1,0 +1,84 @@
+"""GPU check of the landmark-sharded LocalBA (orb_ba_dist_init_host + orb_ba_optimize).
+
+W processes share the one GPU of the box, each attached to a gloo group with the host reducer;
+every rank solves the SAME problem with 1/W of the landmarks and the partial Schur systems are
+all-reduced.  The bar is the single-GPU bar against the oracle: same LM path (iterations, trials,
+termination), poses and points within 1e-6 RMSE, edge chi2 and the culling decisions equal; and
+all ranks return the same state.  The RCCL transport needs one GPU per rank and runs in
+bench.py --gpus N.
+"""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, kw, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from conftest import load_package
+        pkg = load_package()
+        from orbslam3_amd import synth
+        prob = synth.local_ba_problem(**kw)
+        ba = pkg.LocalBA().attach(transport="host")
+        pose, point, chi2, depth, res = ba.optimize(prob, 10)
+        q.put((rank, (pose, point, chi2, depth, res)))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, kw):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kw, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r, v in out.items():
+        assert not isinstance(v, str), f"rank {r}: {v}"
+    return out
+
+
+def _rmse(a, b):
+    return float(np.sqrt(np.mean((np.asarray(a) - np.asarray(b)) ** 2)))
+
+
+@pytest.mark.parametrize("world,stereo_frac,seed", [(2, 0.0, 7), (3, 0.0, 11), (2, 0.5, 8)])
+def test_sharded_local_ba_matches_oracle(oracle, synth, world, stereo_frac, seed):
+    kw = dict(n_kf=20, n_points=800, obs_per_point=5, stereo_frac=stereo_frac, seed=seed)
+    out = _run(world, kw)
+    prob = synth.local_ba_problem(**kw)
+    rpose, rpoint, rchi2, rdepth, rres = oracle.local_ba(prob, 10)
+    for r in range(world):
+        pose, point, chi2, depth, res = out[r]
+        for k in ("iterations", "trials", "terminated", "stopped"):
+            assert res[k] == rres[k], f"rank {r} {k}: {res[k]} vs oracle {rres[k]}"
+        assert _rmse(pose[:, :3], rpose[:, :3]) < 1e-6
+        assert _rmse(point, rpoint) < 1e-6
+        tol = dict(rtol=1e-9, atol=1e-12) if stereo_frac == 0 else dict(rtol=1e-6, atol=1e-3)
+        assert np.allclose(chi2, rchi2, **tol)
+        assert np.array_equal(depth, rdepth)
+        # every rank holds the same result
+        assert np.array_equal(pose, out[0][0]) and np.array_equal(point, out[0][1])
+        assert np.array_equal(chi2, out[0][2])

@@ -88,3 +88,41 @@ def test_shard_range(pkg):
                 assert 0 <= e - b <= -(-total // world)
                 seen.extend(range(b, e))
             assert seen == list(range(total))
+
+
+def _reducer_worker(rank, world, port, q):
+    import ctypes
+
+    import numpy as np
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from conftest import load_package
+        load_package()
+        from orbslam3_amd import optimizer as O
+        cb = O.make_host_reducer()
+        a = np.arange(5, dtype=np.float64) * (rank + 1)
+        rc1 = cb(None, a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), 5, O.BA_SUM)
+        b = np.array([rank, -rank, 0.5], dtype=np.float64)
+        rc2 = cb(None, b.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), 3, O.BA_MAX)
+        s = sum(r + 1 for r in range(world))
+        ok = rc1 == 0 and rc2 == 0 and np.array_equal(a, np.arange(5) * s) and \
+            np.array_equal(b, [world - 1, 0, 0.5])
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ba_host_reducer_gloo_world2(pkg):
+    """The orb_ba_host_reduce_fn callback the sharded LocalBA uses on gloo groups: in-place SUM and
+    MAX of the library's float64 host buffer, called through ctypes as the library calls it."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_reducer_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}

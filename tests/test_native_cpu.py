@@ -74,4 +74,4 @@ def test_sincos_exception_table_exhaustive():
     """All 1,135,869,952 float angles in [0, 360): deterministic sincos + table == glibc offsets."""
     exe = _compile(ROOT / "tools" / "gen_sincos_exceptions.cpp", BUILD / "sincos_check", ("-DORB_CHECK_TABLE",))
     r = subprocess.run([str(exe), "--check"], capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0 and "\nOK " in "\n" + r.stdout, r.stdout + r.stderr
+    assert r.returncode == 0 and "\nOK: " in "\n" + r.stdout, r.stdout + r.stderr
