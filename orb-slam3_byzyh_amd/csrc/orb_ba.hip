@@ -618,6 +618,262 @@ __global__ __launch_bounds__(kCholThreads) void k_ba_chol(int n, const double* _
     if (tid == 0) *status = fail;
 }
 
+// ---- register-resident MFMA Cholesky + solve (n <= 288, one workgroup of 8 waves) ------------------
+// The lower triangle of S is cut into 16x16 tiles that live in the waves' registers for the whole
+// factorisation.  Each tile holds M in the operand layout O(M) of v_mfma_f64_16x16x4_f64: lane l,
+// register q = M[l & 15][(l >> 4) + 4q].  That is the C/D layout of M^T, so with tiles kept
+// transposed every product below takes its operands straight from registers or from one
+// lane-linear LDS read:
+//   trailing update  M_ij^T -= L_jk L_ik^T      A = O(L_jk) negated (blgp = neg A), B = O(L_ik)
+//   panel            L_ik^T  = L_kk^-1 A_ik^T   A = O(L_kk^-1), B = the tile itself
+// Right-looking over the 16-column block steps k.  The owner of tile (k, k) factors it in one
+// wave (lane r = row r, cross-lane reads through v_readlane) and inverts L_kk, with a look-ahead:
+// it updates tile (k+1, k+1) first in step k and factors it while the other waves finish their
+// updates.  The forward solve is folded in (y_k = L_kk^-1 b_k, then b_i -= L_ik y_k by the panel
+// owners); the backward solve walks the tile rows kept in registers.  Tiles are dealt round-robin
+// in order of decreasing column, so the active tiles of every step are a prefix of each wave's
+// slots and the load stays balanced as the trailing matrix shrinks.  Every sum has a fixed order.
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+constexpr int kMfTileWaves = 7, kMfMaxNT = 18;
+constexpr size_t kMfLds = sizeof(double) * (2 * (size_t)kMfMaxNT * 256 + 16 * 17 + 2 * 16 * kMfMaxNT);
+
+template <int N>
+__device__ __forceinline__ double dpp_row_shr(double v) {  // lane l <- lane l - N of its 16-lane row, 0 at the edge
+    const uint64_t u = __double_as_longlong(v);
+    const uint32_t lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, 0x110 + N, 0xf, 0xf, true);
+    const uint32_t hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), 0x110 + N, 0xf, 0xf, true);
+    return __longlong_as_double(((uint64_t)hi << 32) | lo);
+}
+
+// Sum over the 16 lanes of each DPP row (valid in lane 15 of the row), in a fixed order.
+__device__ __forceinline__ double row16_sum(double v) {
+    v += dpp_row_shr<1>(v);
+    v += dpp_row_shr<2>(v);
+    v += dpp_row_shr<4>(v);
+    v += dpp_row_shr<8>(v);
+    return v;
+}
+
+__device__ __forceinline__ void mf_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One wave: factor the 16x16 block in dk (row-major, stride 17), write L_kk^-1 in operand layout
+// to linv_k and replace yv[16k .. 16k + 16) (= b_k, already reduced by the earlier panels) by
+// y_k = L_kk^-1 b_k.
+__device__ __forceinline__ void mf_diag(double* __restrict__ dk, double* __restrict__ linv_k,
+                                        double* __restrict__ yk, int lane, int* fail) {
+    const int r = lane & 15;
+    double row[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) row[c] = dk[r * 17 + c];
+    bool bad = false;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        const double piv = readlane_d(row[c], c);
+        bad |= !(piv > 0.0);
+        const double lcc = sqrt(piv);
+        if (r == c) row[c] = lcc;
+        else if (r > c) row[c] = row[c] / lcc;
+#pragma unroll
+        for (int j = c + 1; j < 16; ++j) {
+            const double ljc = readlane_d(row[c], j);
+            if (r >= j) row[j] -= row[c] * ljc;
+        }
+    }
+    if (lane < 16) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) dk[r * 17 + c] = c <= r ? row[c] : 0.0;
+        dk[r * 17 + 16] = 1.0 / row[r];
+    }
+    if (lane == 0 && bad) *fail = 1;
+    mf_wave_sync();
+    // column c = lane & 15 of L^-1 by forward substitution (L rows are LDS broadcasts)
+    const int c = lane & 15;
+    double xc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        double s = i == c ? 1.0 : 0.0;
+#pragma unroll
+        for (int j = 0; j < i; ++j) s -= dk[i * 17 + j] * xc[j];
+        xc[i] = s * dk[i * 17 + 16];
+    }
+    if (lane < 16) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) linv_k[(c >> 2) * 64 + i + 16 * (c & 3)] = xc[i];  // O layout
+    }
+    mf_wave_sync();
+    // y_k row r = sum_c L^-1[r][c] b_k[c]
+    double y = 0.0;
+#pragma unroll
+    for (int cc = 0; cc < 16; ++cc) y += linv_k[(cc >> 2) * 64 + r + 16 * (cc & 3)] * yk[cc];
+    mf_wave_sync();
+    if (lane < 16) yk[r] = y;
+}
+
+template <int W>  // W tile waves + one wave for the diagonal blocks
+__global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mfma(int n, const double* __restrict__ S,
+                                                               const double* __restrict__ b, double* __restrict__ x,
+                                                               int32_t* __restrict__ status) {
+    constexpr int SL = (kMfMaxNT * (kMfMaxNT + 1) / 2 + W - 1) / W;
+    extern __shared__ double lds[];
+    double* pan = lds;                    // [NT][4][64] panel tiles O(L_ik)
+    double* linv = pan + kMfMaxNT * 256;  // [NT][4][64] O(L_kk^-1)
+    double* dk = linv + kMfMaxNT * 256;   // [16][17] diagonal block scratch (+ 1/L_rr)
+    double* yv = dk + 16 * 17;            // [16 NT] b -> y (forward) -> updated y (backward)
+    double* xv = yv + 16 * kMfMaxNT;      // [16 NT] x
+    __shared__ int fail, ready;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int NT = (n + 15) >> 4, ntt = NT * (NT + 1) / 2;
+    const int r16 = lane & 15, g4 = lane >> 4;
+    if (w == W) {
+        // ---- the diagonal wave: b -> yv, block (0, 0), then block k + 1 during step k's updates
+        for (int i = lane; i < 16 * NT; i += 64) yv[i] = i < n ? b[i] : 0.0;
+        for (int t = lane; t < 256; t += 64) {
+            const int r = t >> 4, c = t & 15;
+            dk[r * 17 + c] = (r < n && c < n) ? S[(size_t)r * n + c] : (r == c ? 1.0 : 0.0);
+        }
+        if (lane == 0) {
+            fail = 0;
+            ready = 0;
+        }
+        mf_wave_sync();
+        mf_diag(dk, linv, yv, lane, &fail);
+        __syncthreads();  // S0
+        for (int k = 0; k + 1 < NT; ++k) {
+            __syncthreads();  // S1(k): panel k applied to yv
+            for (int spin = 0; __hip_atomic_load(&ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < k + 1;
+                 ++spin) {
+                if (spin > (1 << 22)) {  // bounded: a missing hand-off fails the solve instead of hanging
+                    if (lane == 0) fail = 2;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            mf_diag(dk, linv + (k + 1) * 256, yv + 16 * (k + 1), lane, &fail);
+            __syncthreads();  // S2(k)
+        }
+        __syncthreads();  // S1(NT - 1)
+        __syncthreads();  // S2(NT - 1)
+        for (int k = NT - 1; k >= 0; --k) {
+            const double* lk = linv + k * 256;
+            double v = 0.0;
+#pragma unroll
+            for (int rr = 0; rr < 16; ++rr) v += lk[(r16 >> 2) * 64 + rr + 16 * (r16 & 3)] * yv[16 * k + rr];
+            if (lane < 16) xv[16 * k + r16] = v;  // x_k = L_kk^-T y_k
+            __syncthreads();  // B1(k)
+            if (k == 0) break;
+            __syncthreads();  // B2(k)
+        }
+    } else {
+        // ---- tile waves: slot s holds tile t = s W + w (packed i | j << 8), -1 when empty
+        int tij[SL];
+        f64x4 T[SL];
+#pragma unroll
+        for (int s = 0; s < SL; ++s) {
+            const int t = s * W + w;
+            tij[s] = -1;
+            T[s] = f64x4{0.0, 0.0, 0.0, 0.0};
+            if (t < ntt) {
+                int c = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+                while ((c + 1) * (c + 2) / 2 <= t) ++c;
+                while (c * (c + 1) / 2 > t) --c;
+                const int j = NT - 1 - c, i = j + (t - c * (c + 1) / 2);
+                tij[s] = i | (j << 8);
+                double e[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {  // S symmetric: read as S[col block][row block], coalesced
+                    const int row = 16 * j + g4 + 4 * q, col = 16 * i + r16;
+                    const double v = S[(size_t)min(row, n - 1) * n + min(col, n - 1)];  // branch-free
+                    e[q] = (row < n && col < n) ? v : (row == col ? 1.0 : 0.0);
+                }
+                T[s] = f64x4{e[0], e[1], e[2], e[3]};
+            }
+        }
+        __syncthreads();  // S0
+        for (int k = 0; k < NT; ++k) {
+            // ---- panel: L_ik = A_ik L_kk^-T for the tiles (i > k, k); forward b_i -= L_ik y_k
+            const double* lk = linv + k * 256;
+#pragma unroll
+            for (int s = 0; s < SL; ++s) {
+                int v = tij[s];
+                asm volatile("" : "+s"(v)::"memory");  // no per-slot addresses hoisted out of the k loop
+                const int i = v & 255, j = v >> 8;
+                if (v >= 0 && j == k && i > k) {
+                    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(lk[q * 64 + lane], T[s][q], acc, 0, 0, 0);
+                    T[s] = acc;
+                    double part = 0.0;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        pan[i * 256 + q * 64 + lane] = acc[q];
+                        part += acc[q] * yv[16 * k + g4 + 4 * q];
+                    }
+                    part += __shfl_xor(part, 16);
+                    part += __shfl_xor(part, 32);
+                    if (lane < 16) yv[16 * i + lane] -= part;
+                }
+            }
+            __syncthreads();  // S1(k)
+            // (no early exit at k = NT - 1: a break here keeps a second copy of every tile live)
+            // ---- trailing update of the tiles (i, j), j > k; tile (k+1, k+1) first, handed to the diagonal wave
+#pragma unroll
+            for (int s = 0; s < SL; ++s)
+                if (tij[s] == ((k + 1) | ((k + 1) << 8))) {  // (the one slot that matches)
+                    const double* pk = pan + (k + 1) * 256;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        T[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(pk[q * 64 + lane], pk[q * 64 + lane], T[s], 0, 0, 1);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) dk[r16 * 17 + g4 + 4 * q] = T[s][q];
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    if (lane == 0) __hip_atomic_store(&ready, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+#pragma unroll
+            for (int s = 0; s < SL; ++s) {
+                int v = tij[s];
+                asm volatile("" : "+s"(v)::"memory");  // no per-slot addresses hoisted out of the k loop
+                const int i = v & 255, j = v >> 8;
+                if (v >= 0 && j > k && !(i == k + 1 && j == k + 1)) {
+                    const double* pi = pan + i * 256;
+                    const double* pj = pan + j * 256;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        T[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(pj[q * 64 + lane], pi[q * 64 + lane], T[s], 0, 0, 1);
+                }
+            }
+            __syncthreads();  // S2(k)
+        }
+        // ---- backward: y_j -= L_kj^T x_k for the tiles (k, j < k) of row k
+        for (int k = NT - 1; k >= 0; --k) {
+            __syncthreads();  // B1(k): x_k published
+            if (k == 0) break;
+#pragma unroll
+            for (int s = 0; s < SL; ++s) {
+                int v = tij[s];
+                asm volatile("" : "+s"(v)::"memory");  // no per-slot addresses hoisted out of the k loop
+                const int i = v & 255, j = v >> 8;
+                if (v >= 0 && i == k && j < k) {
+                    const double xr = xv[16 * k + r16];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const double o = row16_sum(T[s][q] * xr);  // sum_r L_kj[r][c] x_k[r], c = g4 + 4q
+                        if (r16 == 15) yv[16 * j + g4 + 4 * q] -= o;
+                    }
+                }
+            }
+            __syncthreads();  // B2(k)
+        }
+    }
+    for (int i = threadIdx.x; i < n; i += (W + 1) * 64) x[i] = xv[i];
+    if (threadIdx.x == 0) *status = fail;
+}
+
 // Cooperative multi-workgroup Cholesky + solve (the fast path for n <= 560 / 1100).
 // Right-looking by block columns of NB: workgroup w < nbc keeps block column w (rows j0..n) in LDS
 // for the whole factorisation; workgroup nbc owns the right-hand side.  Step k: the owner of
@@ -1354,10 +1610,12 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     auto lds_bytes = [&](int b) { return sizeof(double) * ((size_t)b * n + (size_t)n * (b + 1) + n); };
     if (lds_bytes(nb) > 150 * 1024) nb = 8;
     const size_t chol_lds = lds_bytes(nb);
-    if (chol_lds > 150 * 1024 && !coop_nb)
+    if (chol_lds > 150 * 1024 && !coop_nb && n > 16 * kMfMaxNT)
         return orbgpu_fail(ORB_ERR_ARG, "too many free keyframes for the on-chip Cholesky");
+    const bool use_mf = !coop_nb && n <= 16 * kMfMaxNT && !getenv("ORBGPU_BA_CHOL_LDS");
     static bool attr_set = false;
     if (!attr_set) {
+        hipFuncSetAttribute((const void*)k_ba_chol_mfma<kMfTileWaves>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMfLds);
         hipFuncSetAttribute((const void*)k_ba_chol<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
         hipFuncSetAttribute((const void*)k_ba_chol<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
         (void)hipGetLastError();
@@ -1445,7 +1703,10 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                             : hipLaunchCooperativeKernel((const void*)k_ba_chol_coop<16>, g, dim3(kCoopThreads), args,
                                                          (unsigned)coop_lds, s);
                     if (le != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "cooperative Cholesky launch failed");
-                } else if (nb == 16)
+                } else if (use_mf)
+                    hipLaunchKernelGGL(k_ba_chol_mfma<kMfTileWaves>, dim3(1), dim3((kMfTileWaves + 1) * 64), kMfLds, s, n, h->S.p, h->bs.p,
+                                       h->x.p, h->status.p);
+                else if (nb == 16)
                     hipLaunchKernelGGL(k_ba_chol<16>, dim3(1), dim3(kCholThreads), chol_lds, s, n, h->S.p, h->LT.p,
                                        h->bs.p, h->x.p, h->status.p);
                 else
