@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -173,18 +174,41 @@ struct Huber2 {
     float dsqr_mono, dsqr_stereo;
 };
 
+// ---- Levenberg-Marquardt state of the device-driven solve -----------------------------------------
+// One process: the per-trial kernels read it to decide whether to run (the build only at the start
+// of an iteration, nothing once the solve has ended); k_lm_build_done / k_lm_trial_done update it
+// exactly as g2o's OptimizationAlgorithmLevenberg::solve does on the host.
+struct LmState {
+    double lambda, ni, current_chi, ini_chi, final_chi, initial_chi, user_lambda, tau;
+    int32_t it, qmax, nbad, phase, done, reject, terminated, trials, iterations, pad;
+};
+// what the host reads after each unit (pinned)
+struct LmProgress {
+    double final_chi, initial_chi, lambda;
+    int32_t done, it, trials, terminated;
+};
+enum { kGateBuild = 0, kGateBuild0 = 1, kGateTrial = 2, kGateRestore = 3 };
+
+__device__ __forceinline__ bool lm_skip(const LmState* st, int kind) {
+    if (!st) return false;
+    if (kind == kGateRestore) return !st->reject;
+    if (st->done) return true;
+    if (kind == kGateBuild) return st->phase != 0;
+    if (kind == kGateBuild0) return st->phase != 0 || st->it != 0;
+    return false;
+}
+
 // ---- per-edge error / linearisation ------------------------------------------------------------
 
 template <bool kBuild>
-__global__ __launch_bounds__(kT) void k_ba_edges(int ne, const EdgeDev* __restrict__ edges,
+__device__ __forceinline__ double ba_edge(int e, const EdgeDev* __restrict__ edges,
                                                  const orb_ba_camera_t* __restrict__ cams,
                                                  const double* __restrict__ pose, const double* __restrict__ point,
                                                  const int32_t* __restrict__ pose_h, Huber2 hub,
                                                  double* __restrict__ err, double* __restrict__ rho0_out,
                                                  double* __restrict__ ecl, double* __restrict__ hpl,
-                                                 double* __restrict__ ecp) {
-    const int e = blockIdx.x * kT + threadIdx.x;
-    if (e >= ne) return;
+                                                 double* __restrict__ ecp,
+        int) {
     const EdgeDev E = edges[e];
     const orb_ba_camera_t cam = cams[E.pose];
     double T[7], X[3], Xc[3];
@@ -216,7 +240,7 @@ __global__ __launch_bounds__(kT) void k_ba_edges(int ne, const EdgeDev* __restri
     err[3 * (size_t)e + 1] = er[1];
     err[3 * (size_t)e + 2] = er[2];
     rho0_out[e] = rho0;
-    if (!kBuild) return;
+    if (!kBuild) return rho0;
 
     // Jacobians: A = d e / d point (D x 3), B = d e / d pose (D x 6, rotation first)
     double R[9];
@@ -265,7 +289,7 @@ __global__ __launch_bounds__(kT) void k_ba_edges(int ne, const EdgeDev* __restri
         for (int r = 0; r < D; ++r) bs += A[3 * r + i] * omr[r];
         pl[9 + i] = bs;
     }
-    if (pose_h[E.pose] < 0) return;
+    if (pose_h[E.pose] < 0) return rho0;
     double* hx = hpl + 18 * (size_t)e;  // B^T W A (6 x 3)
     for (int i = 0; i < 6; ++i)
         for (int j = 0; j < 3; ++j) {
@@ -284,14 +308,26 @@ __global__ __launch_bounds__(kT) void k_ba_edges(int ne, const EdgeDev* __restri
         for (int r = 0; r < D; ++r) bs += B[6 * r + i] * omr[r];
         pp[36 + i] = bs;
     }
+    return rho0;
+}
+
+template <bool kBuild>
+__global__ __launch_bounds__(kT) void k_ba_edges(int ne, const EdgeDev* __restrict__ edges,
+                                                 const orb_ba_camera_t* __restrict__ cams,
+                                                 const double* __restrict__ pose, const double* __restrict__ point,
+                                                 const int32_t* __restrict__ pose_h, Huber2 hub,
+                                                 double* __restrict__ err, double* __restrict__ rho0_out,
+                                                 double* __restrict__ ecl, double* __restrict__ hpl,
+                                                 double* __restrict__ ecp, const LmState* __restrict__ lm_st, int lm_gk) {
+    if (lm_skip(lm_st, lm_gk)) return;
+    const int e = blockIdx.x * kT + threadIdx.x;
+    if (e < ne) ba_edge<kBuild>(e, edges, cams, pose, point, pose_h, hub, err, rho0_out, ecl, hpl, ecp, 0);
 }
 
 // Hll and b_l per landmark: sum of its edges in edge order (g2o accumulates in edge id order)
-__global__ __launch_bounds__(kT) void k_ba_reduce_land(int nl, const int32_t* __restrict__ off,
-                                                       const int32_t* __restrict__ eidx, const double* __restrict__ ecl,
-                                                       double* __restrict__ hll, double* __restrict__ bl) {
-    const int l = blockIdx.x * kT + threadIdx.x;
-    if (l >= nl) return;
+__device__ __forceinline__ void ba_reduce_land(int l, const int32_t* __restrict__ off, const int32_t* __restrict__ eidx,
+                                               const double* __restrict__ ecl, double* __restrict__ hll,
+                                               double* __restrict__ bl) {
     double s[12] = {0};
     for (int k = off[l]; k < off[l + 1]; ++k) {
         const double* p = ecl + 12 * (size_t)eidx[k];
@@ -301,12 +337,20 @@ __global__ __launch_bounds__(kT) void k_ba_reduce_land(int nl, const int32_t* __
     for (int i = 0; i < 3; ++i) bl[3 * (size_t)l + i] = s[9 + i];
 }
 
+__global__ __launch_bounds__(kT) void k_ba_reduce_land(int nl, const int32_t* __restrict__ off,
+                                                       const int32_t* __restrict__ eidx, const double* __restrict__ ecl,
+                                                       double* __restrict__ hll, double* __restrict__ bl,
+                                                       const LmState* __restrict__ lm_st, int lm_gk) {
+    if (lm_skip(lm_st, lm_gk)) return;
+    const int l = blockIdx.x * kT + threadIdx.x;
+    if (l < nl) ba_reduce_land(l, off, eidx, ecl, hll, bl);
+}
+
 // Hpp and b_p per free pose: one wave, lanes stride the pose's edges, fixed-order tree in LDS
-__global__ __launch_bounds__(64) void k_ba_reduce_pose(const int32_t* __restrict__ off, const int32_t* __restrict__ eidx,
-                                                       const double* __restrict__ ecp, double* __restrict__ hpp,
-                                                       double* __restrict__ bp) {
+__device__ __forceinline__ void ba_reduce_pose(int p, int lane, const int32_t* __restrict__ off,
+                                               const int32_t* __restrict__ eidx, const double* __restrict__ ecp,
+                                               double* __restrict__ hpp, double* __restrict__ bp) {
     __shared__ double red[42][65];
-    const int p = blockIdx.x, lane = threadIdx.x;
     double s[42];
     for (int i = 0; i < 42; ++i) s[i] = 0;
     for (int k = off[p] + lane; k < off[p + 1]; k += 64) {
@@ -324,9 +368,19 @@ __global__ __launch_bounds__(64) void k_ba_reduce_pose(const int32_t* __restrict
     else if (lane < 42) bp[6 * (size_t)p + lane - 36] = red[lane][0];
 }
 
+__global__ __launch_bounds__(64) void k_ba_reduce_pose(const int32_t* __restrict__ off, const int32_t* __restrict__ eidx,
+                                                       const double* __restrict__ ecp, double* __restrict__ hpp,
+                                                       double* __restrict__ bp, const LmState* __restrict__ lm_st,
+                                                       int lm_gk) {
+    if (lm_skip(lm_st, lm_gk)) return;
+    ba_reduce_pose(blockIdx.x, threadIdx.x, off, eidx, ecp, hpp, bp);
+}
+
 // max |diag| over the free vertices' Hessian blocks (computeLambdaInit)
 __global__ __launch_bounds__(kT) void k_ba_maxdiag(int nf, int nl, const double* __restrict__ hpp,
-                                                   const double* __restrict__ hll, double* __restrict__ out) {
+                                                   const double* __restrict__ hll, double* __restrict__ out,
+        const LmState* __restrict__ lm_st, int lm_gk) {
+    if (lm_skip(lm_st, lm_gk)) return;
     __shared__ double red[kT];
     double m = 0;
     for (int i = threadIdx.x; i < 6 * nf; i += kT) m = fmax(m, fabs(hpp[36 * (size_t)(i / 6) + 7 * (i % 6)]));
@@ -359,10 +413,13 @@ __device__ __forceinline__ void land_dinv(const double* __restrict__ hll, int l,
 }
 
 // per free edge e of landmark l: Z_e = Hpl_e Dinv_l, cb_e = Hpl_e (Dinv_l b_l) (one thread per edge)
-__global__ __launch_bounds__(kT) void k_ba_schur_edges(int nfe, double lambda, const int32_t* __restrict__ fedge,
+__global__ __launch_bounds__(kT) void k_ba_schur_edges(int nfe, const double* __restrict__ lam, const int32_t* __restrict__ fedge,
                                                        const int32_t* __restrict__ fland, const double* __restrict__ hll,
                                                        const double* __restrict__ bl, const double* __restrict__ hpl,
-                                                       double* __restrict__ z, double* __restrict__ cb) {
+                                                       double* __restrict__ z, double* __restrict__ cb,
+        const LmState* __restrict__ lm_st, int lm_gk) {
+    if (lm_skip(lm_st, lm_gk)) return;
+    const double lambda = *lam;
     const int t = blockIdx.x * kT + threadIdx.x;
     if (t >= nfe) return;
     const int e = fedge[t], l = fland[t];
@@ -384,13 +441,13 @@ __global__ __launch_bounds__(kT) void k_ba_schur_edges(int nfe, double lambda, c
 // S block (bi, bj), bi <= bj, one wave: lanes split the block's (Z_a, Hpl_b) products, each
 // accumulating the full 6x6 partial sum; lane e < 36 then adds the 64 partials in lane order.
 // S = [Hpp + lambda I] - sum Z_a Hpl_b^T; written to both triangles.
-__global__ __launch_bounds__(64) void k_ba_schur_blocks(int n, double lambda, int add_diag, const int32_t* __restrict__ bi,
-                                                        const int32_t* __restrict__ bj, const int32_t* __restrict__ off,
-                                                        const int32_t* __restrict__ pa, const int32_t* __restrict__ pb,
-                                                        const double* __restrict__ z, const double* __restrict__ hpl,
-                                                        const double* __restrict__ hpp, double* __restrict__ S) {
+__device__ __forceinline__ void ba_schur_block(int blk, int lane, int n, double lambda, int add_diag,
+                                               const int32_t* __restrict__ bi, const int32_t* __restrict__ bj,
+                                               const int32_t* __restrict__ off, const int32_t* __restrict__ pa,
+                                               const int32_t* __restrict__ pb, const double* __restrict__ z,
+                                               const double* __restrict__ hpl, const double* __restrict__ hpp,
+                                               double* __restrict__ S) {
     __shared__ double red[36][65];
-    const int blk = blockIdx.x, lane = threadIdx.x;
     double acc[36];
 #pragma unroll
     for (int k = 0; k < 36; ++k) acc[k] = 0;
@@ -420,12 +477,23 @@ __global__ __launch_bounds__(64) void k_ba_schur_blocks(int n, double lambda, in
     S[(size_t)(6 * j + c) * n + 6 * i + r] = v;
 }
 
+
+__global__ __launch_bounds__(64) void k_ba_schur_blocks(int n, const double* __restrict__ lam, int add_diag,
+                                                        const int32_t* __restrict__ bi, const int32_t* __restrict__ bj,
+                                                        const int32_t* __restrict__ off, const int32_t* __restrict__ pa,
+                                                        const int32_t* __restrict__ pb, const double* __restrict__ z,
+                                                        const double* __restrict__ hpl, const double* __restrict__ hpp,
+                                                        double* __restrict__ S, const LmState* __restrict__ lm_st,
+                                                        int lm_gk) {
+    if (lm_skip(lm_st, lm_gk)) return;
+    ba_schur_block(blockIdx.x, threadIdx.x, n, *lam, add_diag, bi, bj, off, pa, pb, z, hpl, hpp, S);
+}
+
 // b_S = b_p - sum over the pose's edges of Hpl_e db (one wave per free pose)
-__global__ __launch_bounds__(64) void k_ba_schur_rhs(const int32_t* __restrict__ off, const int32_t* __restrict__ eidx,
-                                                     const double* __restrict__ cb, const double* __restrict__ bp,
-                                                     int use_bp, double* __restrict__ bs) {
+__device__ __forceinline__ void ba_schur_rhs(int p, int lane, const int32_t* __restrict__ off,
+                                             const int32_t* __restrict__ eidx, const double* __restrict__ cb,
+                                             const double* __restrict__ bp, int use_bp, double* __restrict__ bs) {
     __shared__ double red[6][65];
-    const int p = blockIdx.x, lane = threadIdx.x;
     double s[6] = {0, 0, 0, 0, 0, 0};
     for (int k = off[p] + lane; k < off[p + 1]; k += 64) {
         const double* q = cb + 6 * (size_t)eidx[k];
@@ -439,6 +507,14 @@ __global__ __launch_bounds__(64) void k_ba_schur_rhs(const int32_t* __restrict__
         __syncthreads();
     }
     if (lane < 6) bs[6 * (size_t)p + lane] = (use_bp ? bp[6 * (size_t)p + lane] : 0.0) - red[lane][0];
+}
+
+__global__ __launch_bounds__(64) void k_ba_schur_rhs(const int32_t* __restrict__ off, const int32_t* __restrict__ eidx,
+                                                     const double* __restrict__ cb, const double* __restrict__ bp,
+                                                     int use_bp, double* __restrict__ bs, const LmState* __restrict__ lm_st,
+                                                     int lm_gk) {
+    if (lm_skip(lm_st, lm_gk)) return;
+    ba_schur_rhs(blockIdx.x, threadIdx.x, off, eidx, cb, bp, use_bp, bs);
 }
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
@@ -630,12 +706,14 @@ __global__ __launch_bounds__(kCholThreads) void k_ba_chol(int n, const double* _
 // wave (lane r = row r, cross-lane reads through v_readlane) and inverts L_kk, with a look-ahead:
 // it updates tile (k+1, k+1) first in step k and factors it while the other waves finish their
 // updates.  The forward solve is folded in (y_k = L_kk^-1 b_k, then b_i -= L_ik y_k by the panel
-// owners); the backward solve walks the tile rows kept in registers.  Tiles are dealt round-robin
+// owners); the backward solve walks the tile rows kept in registers, pipelined through LDS
+// flags: the diagonal wave publishes x_k once every L_kj^T x_j contribution has landed.  Tiles are dealt round-robin
 // in order of decreasing column, so the active tiles of every step are a prefix of each wave's
 // slots and the load stays balanced as the trailing matrix shrinks.  Every sum has a fixed order.
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 constexpr int kMfTileWaves = 7, kMfMaxNT = 18;
-constexpr size_t kMfLds = sizeof(double) * (2 * (size_t)kMfMaxNT * 256 + 16 * 17 + 2 * 16 * kMfMaxNT);
+constexpr size_t kMfLds =
+    sizeof(double) * (2 * (size_t)kMfMaxNT * 256 + 16 * 17 + 2 * 16 * kMfMaxNT + 16 * kMfMaxNT * (kMfMaxNT - 1) / 2);
 
 template <int N>
 __device__ __forceinline__ double dpp_row_shr(double v) {  // lane l <- lane l - N of its 16-lane row, 0 at the edge
@@ -660,63 +738,75 @@ __device__ __forceinline__ void mf_wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// One wave: factor the 16x16 block in dk (row-major, stride 17), write L_kk^-1 in operand layout
-// to linv_k and replace yv[16k .. 16k + 16) (= b_k, already reduced by the earlier panels) by
-// y_k = L_kk^-1 b_k.
+// 1/sqrt(x): v_rsq_f64 and two Newton steps (about 1 ulp; the factor need not be correctly rounded)
+__device__ __forceinline__ double rsqrt_nr(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    const double h = 0.5 * x;
+    y = y * __builtin_fma(-h, y * y, 1.5);
+    y = y * __builtin_fma(-h, y * y, 1.5);
+    return y;
+}
+
+// One wave: factor the 16x16 block in dk (row-major, stride 17) and write L_kk^-1 in operand layout
+// to linv_k; replace yk[0 .. 16) (= b_k, already reduced by the earlier panels) by y_k = L_kk^-1 b_k.
+// Lane r holds row r of the block and column r of L^-1.  Column step c: one rsqrt, then the values
+// L[j][c] (j > c) are broadcast once (v_readlane) and feed both the rank-1 update of the block and
+// the substitution step of L^-1 (x_i -= L[i][c] x_c).  The updates run unconditionally: entries
+// above the diagonal collect garbage that is never read.
 __device__ __forceinline__ void mf_diag(double* __restrict__ dk, double* __restrict__ linv_k,
-                                        double* __restrict__ yk, int lane, int* fail) {
+                                        double* __restrict__ yk, int lane, int* fail, int64_t* tr = nullptr) {
+    if (tr && lane == 0) tr[0] = clock64();
     const int r = lane & 15;
-    double row[16];
+    double row[16], xc[16];
 #pragma unroll
-    for (int c = 0; c < 16; ++c) row[c] = dk[r * 17 + c];
+    for (int c = 0; c < 16; ++c) {
+        row[c] = dk[r * 17 + c];
+        xc[c] = c == r ? 1.0 : 0.0;
+    }
     bool bad = false;
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
         const double piv = readlane_d(row[c], c);
         bad |= !(piv > 0.0);
-        const double lcc = sqrt(piv);
-        if (r == c) row[c] = lcc;
-        else if (r > c) row[c] = row[c] / lcc;
+        const double inv = rsqrt_nr(piv);  // 1 / L[c][c]
+        const double lrc = row[c] * inv;    // L[r][c] for r > c
+        xc[c] *= inv;                       // x_c of column r of L^-1
 #pragma unroll
         for (int j = c + 1; j < 16; ++j) {
-            const double ljc = readlane_d(row[c], j);
-            if (r >= j) row[j] -= row[c] * ljc;
+            const double ljc = readlane_d(lrc, j);
+            row[j] = __builtin_fma(-lrc, ljc, row[j]);
+            xc[j] = __builtin_fma(-ljc, xc[c], xc[j]);
         }
     }
-    if (lane < 16) {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) dk[r * 17 + c] = c <= r ? row[c] : 0.0;
-        dk[r * 17 + 16] = 1.0 / row[r];
-    }
     if (lane == 0 && bad) *fail = 1;
-    mf_wave_sync();
-    // column c = lane & 15 of L^-1 by forward substitution (L rows are LDS broadcasts)
-    const int c = lane & 15;
-    double xc[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        double s = i == c ? 1.0 : 0.0;
-#pragma unroll
-        for (int j = 0; j < i; ++j) s -= dk[i * 17 + j] * xc[j];
-        xc[i] = s * dk[i * 17 + 16];
-    }
+    if (tr && lane == 0) tr[1] = clock64();
     if (lane < 16) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) linv_k[(c >> 2) * 64 + i + 16 * (c & 3)] = xc[i];  // O layout
+        for (int i = 0; i < 16; ++i) linv_k[(r >> 2) * 64 + i + 16 * (r & 3)] = xc[i];  // L^-1[i][r], O layout
     }
     mf_wave_sync();
-    // y_k row r = sum_c L^-1[r][c] b_k[c]
-    double y = 0.0;
+    if (tr && lane == 0) tr[2] = clock64();
+    // y_k row r = sum_c L^-1[r][c] b_k[c] (four partial sums)
+    double y4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int cc = 0; cc < 16; ++cc) y += linv_k[(cc >> 2) * 64 + r + 16 * (cc & 3)] * yk[cc];
+    for (int cc = 0; cc < 16; ++cc)
+        y4[cc & 3] = __builtin_fma(linv_k[(cc >> 2) * 64 + r + 16 * (cc & 3)], yk[cc], y4[cc & 3]);
+    const double y = (y4[0] + y4[1]) + (y4[2] + y4[3]);
     mf_wave_sync();
     if (lane < 16) yk[r] = y;
+    if (tr && lane == 0) tr[3] = clock64();
 }
 
 template <int W>  // W tile waves + one wave for the diagonal blocks
 __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mfma(int n, const double* __restrict__ S,
                                                                const double* __restrict__ b, double* __restrict__ x,
-                                                               int32_t* __restrict__ status) {
+                                                               int32_t* __restrict__ status,
+                                                               int64_t* __restrict__ trace,
+        const LmState* __restrict__ lm_st, int lm_gk) {
+    if (lm_skip(lm_st, lm_gk)) return;
+    // trace (debug, ORBGPU_BA_TRACE): clock64 stamps [(k * 8 + wave) * 4 + point], backward at [600 + k]
+#define MF_STAMP(k_, pt_) \
+    if (trace && lane == 0) trace[((k_) * 8 + w) * 4 + (pt_)] = clock64()
     constexpr int SL = (kMfMaxNT * (kMfMaxNT + 1) / 2 + W - 1) / W;
     extern __shared__ double lds[];
     double* pan = lds;                    // [NT][4][64] panel tiles O(L_ik)
@@ -724,7 +814,8 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mfma(int n, const doub
     double* dk = linv + kMfMaxNT * 256;   // [16][17] diagonal block scratch (+ 1/L_rr)
     double* yv = dk + 16 * 17;            // [16 NT] b -> y (forward) -> updated y (backward)
     double* xv = yv + 16 * kMfMaxNT;      // [16 NT] x
-    __shared__ int fail, ready;
+    double* contrib = xv + 16 * kMfMaxNT;  // [k (k - 1) / 2 + j][16]: L_kj^T x_k, one slot per tile (k > j)
+    __shared__ int fail, ready, xready, cnt[kMfMaxNT];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int NT = (n + 15) >> 4, ntt = NT * (NT + 1) / 2;
@@ -739,12 +830,15 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mfma(int n, const doub
         if (lane == 0) {
             fail = 0;
             ready = 0;
+            xready = NT;
         }
+        if (lane < kMfMaxNT) cnt[lane] = 0;
         mf_wave_sync();
         mf_diag(dk, linv, yv, lane, &fail);
         __syncthreads();  // S0
         for (int k = 0; k + 1 < NT; ++k) {
             __syncthreads();  // S1(k): panel k applied to yv
+            MF_STAMP(k, 1);
             for (int spin = 0; __hip_atomic_load(&ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < k + 1;
                  ++spin) {
                 if (spin > (1 << 22)) {  // bounded: a missing hand-off fails the solve instead of hanging
@@ -753,20 +847,37 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mfma(int n, const doub
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
-            mf_diag(dk, linv + (k + 1) * 256, yv + 16 * (k + 1), lane, &fail);
+            MF_STAMP(k, 2);
+            mf_diag(dk, linv + (k + 1) * 256, yv + 16 * (k + 1), lane, &fail, trace ? trace + 700 + 4 * k : nullptr);
+            MF_STAMP(k, 3);
             __syncthreads();  // S2(k)
         }
         __syncthreads();  // S1(NT - 1)
         __syncthreads();  // S2(NT - 1)
-        for (int k = NT - 1; k >= 0; --k) {
-            const double* lk = linv + k * 256;
-            double v = 0.0;
+        // ---- backward, producer side: x_j once all L_kj^T x_k (k > j) have landed, summed in fixed order
+        for (int j = NT - 1; j >= 0; --j) {
+            if (trace && lane == 0) trace[600 + j] = clock64();
+            for (int spin = 0; __hip_atomic_load(&cnt[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NT - 1 - j;
+                 ++spin) {
+                if (spin > (1 << 22)) {
+                    if (lane == 0) fail = 3;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            double yj = yv[16 * j + r16];
+            for (int kk = NT - 1; kk > j; --kk) yj -= contrib[(kk * (kk - 1) / 2 + j) * 16 + r16];
+            mf_wave_sync();
+            if (lane < 16) yv[16 * j + r16] = yj;
+            mf_wave_sync();
+            const double* lj = linv + j * 256;
+            double v4[4] = {0.0, 0.0, 0.0, 0.0};  // x_j[c] = sum_r L^-1[r][c] y_j[r], c = lane & 15
 #pragma unroll
-            for (int rr = 0; rr < 16; ++rr) v += lk[(r16 >> 2) * 64 + rr + 16 * (r16 & 3)] * yv[16 * k + rr];
-            if (lane < 16) xv[16 * k + r16] = v;  // x_k = L_kk^-T y_k
-            __syncthreads();  // B1(k)
-            if (k == 0) break;
-            __syncthreads();  // B2(k)
+            for (int rr = 0; rr < 16; ++rr)
+                v4[rr & 3] = __builtin_fma(lj[(r16 >> 2) * 64 + rr + 16 * (r16 & 3)], yv[16 * j + rr], v4[rr & 3]);
+            if (lane < 16) xv[16 * j + r16] = (v4[0] + v4[1]) + (v4[2] + v4[3]);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) __hip_atomic_store(&xready, j, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     } else {
         // ---- tile waves: slot s holds tile t = s W + w (packed i | j << 8), -1 when empty
@@ -795,12 +906,13 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mfma(int n, const doub
         }
         __syncthreads();  // S0
         for (int k = 0; k < NT; ++k) {
+            MF_STAMP(k, 0);
             // ---- panel: L_ik = A_ik L_kk^-T for the tiles (i > k, k); forward b_i -= L_ik y_k
             const double* lk = linv + k * 256;
 #pragma unroll
             for (int s = 0; s < SL; ++s) {
                 int v = tij[s];
-                asm volatile("" : "+s"(v)::"memory");  // no per-slot addresses hoisted out of the k loop
+                asm volatile("" : "+s"(v));  // no per-slot addresses hoisted out of the k loop
                 const int i = v & 255, j = v >> 8;
                 if (v >= 0 && j == k && i > k) {
                     f64x4 acc = {0.0, 0.0, 0.0, 0.0};
@@ -808,11 +920,11 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mfma(int n, const doub
                     for (int q = 0; q < 4; ++q)
                         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(lk[q * 64 + lane], T[s][q], acc, 0, 0, 0);
                     T[s] = acc;
-                    double part = 0.0;
+                    double part = 0.0;  // forward: b_i -= L_ik y_k (this tile is the only writer of b_i in step k)
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         pan[i * 256 + q * 64 + lane] = acc[q];
-                        part += acc[q] * yv[16 * k + g4 + 4 * q];
+                        part = __builtin_fma(acc[q], yv[16 * k + g4 + 4 * q], part);
                     }
                     part += __shfl_xor(part, 16);
                     part += __shfl_xor(part, 32);
@@ -820,6 +932,7 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mfma(int n, const doub
                 }
             }
             __syncthreads();  // S1(k)
+            MF_STAMP(k, 1);
             // (no early exit at k = NT - 1: a break here keeps a second copy of every tile live)
             // ---- trailing update of the tiles (i, j), j > k; tile (k+1, k+1) first, handed to the diagonal wave
 #pragma unroll
@@ -837,7 +950,7 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mfma(int n, const doub
 #pragma unroll
             for (int s = 0; s < SL; ++s) {
                 int v = tij[s];
-                asm volatile("" : "+s"(v)::"memory");  // no per-slot addresses hoisted out of the k loop
+                asm volatile("" : "+s"(v));  // no per-slot addresses hoisted out of the k loop
                 const int i = v & 255, j = v >> 8;
                 if (v >= 0 && j > k && !(i == k + 1 && j == k + 1)) {
                     const double* pi = pan + i * 256;
@@ -847,31 +960,44 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mfma(int n, const doub
                         T[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(pj[q * 64 + lane], pi[q * 64 + lane], T[s], 0, 0, 1);
                 }
             }
+            MF_STAMP(k, 3);
             __syncthreads();  // S2(k)
         }
-        // ---- backward: y_j -= L_kj^T x_k for the tiles (k, j < k) of row k
-        for (int k = NT - 1; k >= 0; --k) {
-            __syncthreads();  // B1(k): x_k published
-            if (k == 0) break;
+        // ---- backward, consumer side: row k's tiles contribute L_kj^T x_k as soon as x_k is out
+        for (int k = NT - 1; k >= 1; --k) {
+            bool mine = false;
+#pragma unroll
+            for (int s = 0; s < SL; ++s) mine |= tij[s] >= 0 && (tij[s] & 255) == k && (tij[s] >> 8) < k;
+            if (!mine) continue;
+            for (int spin = 0; __hip_atomic_load(&xready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) > k;
+                 ++spin) {
+                if (spin > (1 << 22)) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            const double xr = xv[16 * k + r16];
 #pragma unroll
             for (int s = 0; s < SL; ++s) {
                 int v = tij[s];
-                asm volatile("" : "+s"(v)::"memory");  // no per-slot addresses hoisted out of the k loop
+                asm volatile("" : "+s"(v));
                 const int i = v & 255, j = v >> 8;
                 if (v >= 0 && i == k && j < k) {
-                    const double xr = xv[16 * k + r16];
+                    double* cs = contrib + (k * (k - 1) / 2 + j) * 16;
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         const double o = row16_sum(T[s][q] * xr);  // sum_r L_kj[r][c] x_k[r], c = g4 + 4q
-                        if (r16 == 15) yv[16 * j + g4 + 4 * q] -= o;
+                        if (r16 == 15) cs[g4 + 4 * q] = o;
                     }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    if (lane == 0) __hip_atomic_fetch_add(&cnt[j], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
-            __syncthreads();  // B2(k)
         }
     }
+    __syncthreads();  // x complete
     for (int i = threadIdx.x; i < n; i += (W + 1) * 64) x[i] = xv[i];
     if (threadIdx.x == 0) *status = fail;
+    if (trace && threadIdx.x == 0) trace[640] = clock64();
+#undef MF_STAMP
 }
 
 // Cooperative multi-workgroup Cholesky + solve (the fast path for n <= 560 / 1100).
@@ -1132,13 +1258,11 @@ __global__ __launch_bounds__(kCoopThreads) void k_ba_chol_coop(int n, const doub
 }
 
 // x_l = Dinv (b_l - sum_e Hpl_e^T x_pose(e))
-__global__ __launch_bounds__(kT) void k_ba_backsub(int nl, int n, double lambda, const int32_t* __restrict__ off,
-                                                   const int32_t* __restrict__ eidx, const EdgeDev* __restrict__ edges,
-                                                   const int32_t* __restrict__ pose_h, const double* __restrict__ hpl,
-                                                   const double* __restrict__ bl, const double* __restrict__ hll,
-                                                   double* __restrict__ x) {
-    const int l = blockIdx.x * kT + threadIdx.x;
-    if (l >= nl) return;
+__device__ __forceinline__ void ba_backsub(int l, int n, double lambda, const int32_t* __restrict__ off,
+                                           const int32_t* __restrict__ eidx, const EdgeDev* __restrict__ edges,
+                                           const int32_t* __restrict__ pose_h, const double* __restrict__ hpl,
+                                           const double* __restrict__ bl, const double* __restrict__ hll,
+                                           double* __restrict__ x) {
     double cl[3] = {bl[3 * (size_t)l], bl[3 * (size_t)l + 1], bl[3 * (size_t)l + 2]};
     for (int k = off[l]; k < off[l + 1]; ++k) {
         const int e = eidx[k];
@@ -1152,17 +1276,33 @@ __global__ __launch_bounds__(kT) void k_ba_backsub(int nl, int n, double lambda,
     for (int r = 0; r < 3; ++r) x[n + 3 * (size_t)l + r] = Di[3 * r] * cl[0] + Di[3 * r + 1] * cl[1] + Di[3 * r + 2] * cl[2];
 }
 
+__global__ __launch_bounds__(kT) void k_ba_backsub(int nl, int n, const double* __restrict__ lam,
+                                                   const int32_t* __restrict__ off, const int32_t* __restrict__ eidx,
+                                                   const EdgeDev* __restrict__ edges, const int32_t* __restrict__ pose_h,
+                                                   const double* __restrict__ hpl, const double* __restrict__ bl,
+                                                   const double* __restrict__ hll, double* __restrict__ x,
+                                                   const LmState* __restrict__ lm_st, int lm_gk) {
+    if (lm_skip(lm_st, lm_gk)) return;
+    const int l = blockIdx.x * kT + threadIdx.x;
+    if (l < nl) ba_backsub(l, n, *lam, off, eidx, edges, pose_h, hpl, bl, hll, x);
+}
+
 // push + oplus for every free vertex: threads [0, nf) poses, [nf, nf + nl) landmarks
-__global__ __launch_bounds__(kT) void k_ba_update(int nf, int nl, int n, const int32_t* __restrict__ free_pose,
-                                                  const int32_t* __restrict__ land_point, const double* __restrict__ x,
-                                                  double* __restrict__ pose, double* __restrict__ pose_bak,
-                                                  double* __restrict__ point, double* __restrict__ point_bak) {
-    const int t = blockIdx.x * kT + threadIdx.x;
+// push + oplus for vertex t (poses first, then landmarks).  from_bak: the previous trial was
+// rejected and not restored yet (device-driven loop): start from the backup and keep it.
+__device__ __forceinline__ void ba_update(int t, int nf, int nl, int n, bool from_bak,
+                                          const int32_t* __restrict__ free_pose, const int32_t* __restrict__ land_point,
+                                          const double* __restrict__ x, double* __restrict__ pose,
+                                          double* __restrict__ pose_bak, double* __restrict__ point,
+                                          double* __restrict__ point_bak) {
     if (t < nf) {
         double* T = pose + 7 * (size_t)free_pose[t];
         double* Tb = pose_bak + 7 * (size_t)free_pose[t];
         double v[7], u[6];
-        for (int i = 0; i < 7; ++i) Tb[i] = v[i] = T[i];
+        for (int i = 0; i < 7; ++i) {
+            v[i] = from_bak ? Tb[i] : T[i];
+            Tb[i] = v[i];
+        }
         for (int i = 0; i < 6; ++i) u[i] = x[6 * (size_t)t + i];
         se3_oplus(v, u);
         for (int i = 0; i < 7; ++i) T[i] = v[i];
@@ -1171,16 +1311,29 @@ __global__ __launch_bounds__(kT) void k_ba_update(int nf, int nl, int n, const i
         double* X = point + 3 * (size_t)land_point[l];
         double* Xb = point_bak + 3 * (size_t)land_point[l];
         for (int i = 0; i < 3; ++i) {
-            Xb[i] = X[i];
-            X[i] += x[n + 3 * (size_t)l + i];
+            const double v = from_bak ? Xb[i] : X[i];
+            Xb[i] = v;
+            X[i] = v + x[n + 3 * (size_t)l + i];
         }
     }
+}
+
+__global__ __launch_bounds__(kT) void k_ba_update(int nf, int nl, int n, const int32_t* __restrict__ free_pose,
+                                                  const int32_t* __restrict__ land_point, const double* __restrict__ x,
+                                                  double* __restrict__ pose, double* __restrict__ pose_bak,
+                                                  double* __restrict__ point, double* __restrict__ point_bak,
+                                                  const LmState* __restrict__ lm_st, int lm_gk) {
+    if (lm_skip(lm_st, lm_gk)) return;
+    ba_update(blockIdx.x * kT + threadIdx.x, nf, nl, n, false, free_pose, land_point, x, pose, pose_bak, point,
+              point_bak);
 }
 
 __global__ __launch_bounds__(kT) void k_ba_restore(int nf, int nl, const int32_t* __restrict__ free_pose,
                                                    const int32_t* __restrict__ land_point, double* __restrict__ pose,
                                                    const double* __restrict__ pose_bak, double* __restrict__ point,
-                                                   const double* __restrict__ point_bak) {
+                                                   const double* __restrict__ point_bak,
+        const LmState* __restrict__ lm_st, int lm_gk) {
+    if (lm_skip(lm_st, lm_gk)) return;
     const int t = blockIdx.x * kT + threadIdx.x;
     if (t < nf) {
         for (int i = 0; i < 7; ++i) pose[7 * (size_t)free_pose[t] + i] = pose_bak[7 * (size_t)free_pose[t] + i];
@@ -1191,9 +1344,16 @@ __global__ __launch_bounds__(kT) void k_ba_restore(int nf, int nl, const int32_t
 }
 
 // out[0] = sum rho0 (activeRobustChi2), out[1] = sum x (lambda x + b) (computeScale, before +1e-3)
-__global__ __launch_bounds__(1024) void k_ba_sums(int ne, const double* __restrict__ rho0, int x0, int nx, double lambda,
+// out: [0] robust chi2, [1] computeScale part, [2] factorisation status (as a double), [3] max diag
+// (written earlier by k_ba_maxdiag).  host: optional pinned copy of out[0..3] (one process: the
+// host reads it after the stream sync, no copy launches).
+__global__ __launch_bounds__(1024) void k_ba_sums(int ne, const double* __restrict__ rho0, int x0, int nx, const double* __restrict__ lam,
                                                   const double* __restrict__ x, const double* __restrict__ b,
-                                                  double* __restrict__ out) {
+                                                  const int32_t* __restrict__ status, double* __restrict__ out,
+                                                  double* __restrict__ host,
+        const LmState* __restrict__ lm_st, int lm_gk) {
+    if (lm_skip(lm_st, lm_gk)) return;
+    const double lambda = *lam;
     __shared__ double r0[1024], r1[1024];
     double a = 0, c = 0;
     for (int i = threadIdx.x; i < ne; i += 1024) a += rho0[i];
@@ -1212,6 +1372,14 @@ __global__ __launch_bounds__(1024) void k_ba_sums(int ne, const double* __restri
     if (threadIdx.x == 0) {
         out[0] = r0[0];
         out[1] = r1[0];
+        out[2] = (x && *status) ? 1.0 : 0.0;
+        if (host) {
+            host[0] = r0[0];
+            host[1] = r1[0];
+            host[2] = out[2];
+            host[3] = out[3];
+            __threadfence_system();
+        }
     }
 }
 
@@ -1231,6 +1399,236 @@ __global__ __launch_bounds__(kT) void k_ba_final(int ne, const EdgeDev* __restri
     double Xc[3];
     qrotate(q, point + 3 * (size_t)E.point, Xc);
     depth_ok[e] = (Xc[2] + T[2]) > 0.0;
+}
+
+// ---- LM controllers (one thread), g2o OptimizationAlgorithmLevenberg::solve ---------------------
+// after the build: currentChi, iniChi; at iteration 0 the initial lambda (tau * max diag, or the
+// user's)
+__device__ void lm_build_done(LmState* st, double chi, double maxdiag) {
+    st->current_chi = chi;
+    st->ini_chi = chi;
+    if (st->it == 0) {
+        st->initial_chi = chi;
+        st->lambda = st->user_lambda > 0 ? st->user_lambda : st->tau * maxdiag;
+        st->ni = 2;
+        st->nbad = 0;
+    }
+    st->qmax = 0;
+    st->phase = 1;
+}
+
+// after a trial: accept (lambda shrinks) or reject (lambda grows; the next update starts from the
+// backup, and a final restore launch undoes a rejected last trial); at the end of the trial loop
+// the termination tests
+__device__ void lm_trial_done(LmState* st, double chi, double scale_part, bool failed, LmProgress* prog) {
+    double tempChi = chi;
+    if (failed) tempChi = DBL_MAX;
+    double rho = st->current_chi - tempChi;
+    const double scale = scale_part + 1e-3;
+    rho /= scale;
+    if (rho > 0 && isfinite(tempChi)) {
+        double alpha = 1. - pow(2 * rho - 1, 3.0);
+        alpha = fmin(alpha, 2. / 3.);
+        st->lambda *= fmax(1. / 3., alpha);
+        st->ni = 2;
+        st->current_chi = tempChi;
+        st->reject = 0;
+    } else {
+        st->lambda *= st->ni;
+        st->ni *= 2;
+        st->reject = 1;
+    }
+    st->qmax++;
+    st->trials++;
+    if (!(rho < 0 && st->qmax < 10)) {  // the trial loop is over
+        st->final_chi = st->current_chi;
+        if (st->qmax == 10 || rho == 0) {
+            st->terminated = 1;
+            st->it++;
+            st->done = 1;
+        } else {
+            if ((st->ini_chi - st->current_chi) * 1e3 < st->ini_chi) st->nbad++;
+            else st->nbad = 0;
+            st->it++;
+            if (st->nbad >= 3) {
+                st->terminated = 1;
+                st->done = 1;
+            } else {
+                st->phase = 0;
+                if (st->it >= st->iterations) st->done = 1;
+            }
+        }
+    }
+    prog->final_chi = st->final_chi;
+    prog->initial_chi = st->initial_chi;
+    prog->lambda = st->lambda;
+    prog->it = st->it;
+    prog->trials = st->trials;
+    prog->terminated = st->terminated;
+    prog->done = st->done;
+    __threadfence_system();
+}
+
+// ---- fused kernels of the device-driven unit ------------------------------------------------------
+// fixed-order block sum of one value per thread (blockDim = NT); the result is valid in every thread
+template <int NT>
+__device__ __forceinline__ double block_sum(double v) {
+    __shared__ double red[NT];
+    __syncthreads();
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int w = NT / 2; w >= 1; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    return red[0];
+}
+
+// true in the last block to finish (its predecessors' global writes are visible to it)
+__device__ __forceinline__ bool last_block(unsigned* counter) {
+    __shared__ bool last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(counter, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (last) __threadfence();
+    return last;
+}
+
+// unit step 1 (build): linearise every edge; per-block robust chi2 partials
+__global__ __launch_bounds__(kT) void k_u_edges_build(int ne, const EdgeDev* __restrict__ edges,
+                                                      const orb_ba_camera_t* __restrict__ cams,
+                                                      const double* __restrict__ pose, const double* __restrict__ point,
+                                                      const int32_t* __restrict__ pose_h, Huber2 hub,
+                                                      double* __restrict__ err, double* __restrict__ rho0_out,
+                                                      double* __restrict__ ecl, double* __restrict__ hpl,
+                                                      double* __restrict__ ecp, double* __restrict__ part,
+                                                      const LmState* __restrict__ st) {
+    if (lm_skip(st, kGateBuild)) return;
+    const int e = blockIdx.x * kT + threadIdx.x;
+    double r = 0.0;
+    if (e < ne) r = ba_edge<true>(e, edges, cams, pose, point, pose_h, hub, err, rho0_out, ecl, hpl, ecp, 0);
+    const double bsum = block_sum<kT>(r);
+    if (threadIdx.x == 0) part[blockIdx.x] = bsum;
+}
+
+// unit step 2 (build): Hpp/b_p (blocks [0, nf)), Hll/b_l (64 landmarks per block); the last block
+// sums chi2, takes max diag at iteration 0 and runs the build controller
+__global__ __launch_bounds__(64) void k_u_reduce_build(int nf, int nl, const int32_t* __restrict__ pose_off,
+                                                       const int32_t* __restrict__ pose_edge, const double* __restrict__ ecp,
+                                                       double* __restrict__ hpp, double* __restrict__ bp,
+                                                       const int32_t* __restrict__ land_off,
+                                                       const int32_t* __restrict__ land_edge,
+                                                       const double* __restrict__ ecl, double* __restrict__ hll,
+                                                       double* __restrict__ bl, const double* __restrict__ part,
+                                                       int nparts, unsigned* counter, double* __restrict__ scal,
+                                                       LmState* st) {
+    if (lm_skip(st, kGateBuild)) return;
+    const int b = blockIdx.x, lane = threadIdx.x;
+    if (b < nf) {
+        ba_reduce_pose(b, lane, pose_off, pose_edge, ecp, hpp, bp);
+    } else {
+        const int l = (b - nf) * 64 + lane;
+        if (l < nl) ba_reduce_land(l, land_off, land_edge, ecl, hll, bl);
+    }
+    if (!last_block(counter)) return;
+    double c = 0.0;
+    for (int i = lane; i < nparts; i += 64) c += part[i];
+    const double chi = block_sum<64>(c);
+    double md = 0.0;
+    if (st->it == 0) {
+        double m = 0;
+        for (int i = lane; i < 6 * nf; i += 64) m = fmax(m, fabs(hpp[36 * (size_t)(i / 6) + 7 * (i % 6)]));
+        for (int i = lane; i < 3 * nl; i += 64) m = fmax(m, fabs(hll[9 * (size_t)(i / 3) + 4 * (i % 3)]));
+        __shared__ double mx[64];
+        mx[lane] = m;
+        __syncthreads();
+        for (int w = 32; w >= 1; w >>= 1) {
+            if (lane < w) mx[lane] = fmax(mx[lane], mx[lane + w]);
+            __syncthreads();
+        }
+        md = mx[0];
+    }
+    if (lane == 0) {
+        scal[0] = chi;
+        scal[3] = md;
+        lm_build_done(st, chi, md);
+        *counter = 0;
+    }
+}
+
+// unit step 4 (trial): S blocks (blocks [0, nblk)) and b_S (one block per free pose)
+__global__ __launch_bounds__(64) void k_u_schur(int n, int nblk, const double* __restrict__ lam,
+                                                const int32_t* __restrict__ bi, const int32_t* __restrict__ bj,
+                                                const int32_t* __restrict__ off, const int32_t* __restrict__ pa,
+                                                const int32_t* __restrict__ pb, const double* __restrict__ z,
+                                                const double* __restrict__ hpl, const double* __restrict__ hpp,
+                                                double* __restrict__ S, const int32_t* __restrict__ pose_off,
+                                                const int32_t* __restrict__ pose_edge, const double* __restrict__ cb,
+                                                const double* __restrict__ bp, double* __restrict__ bs,
+                                                const LmState* __restrict__ st) {
+    if (lm_skip(st, kGateTrial)) return;
+    if ((int)blockIdx.x < nblk)
+        ba_schur_block(blockIdx.x, threadIdx.x, n, *lam, 1, bi, bj, off, pa, pb, z, hpl, hpp, S);
+    else
+        ba_schur_rhs(blockIdx.x - nblk, threadIdx.x, pose_off, pose_edge, cb, bp, 1, bs);
+}
+
+// unit step 6 (trial): x_l per landmark and its update, then the pose updates; a rejected previous
+// trial is undone here (from the backup) instead of by a restore launch
+__global__ __launch_bounds__(kT) void k_u_backsub_update(int nl, int nf, int n, const double* __restrict__ lam,
+                                                         const int32_t* __restrict__ off, const int32_t* __restrict__ eidx,
+                                                         const EdgeDev* __restrict__ edges,
+                                                         const int32_t* __restrict__ pose_h, const double* __restrict__ hpl,
+                                                         const double* __restrict__ bl, const double* __restrict__ hll,
+                                                         double* __restrict__ x, const int32_t* __restrict__ free_pose,
+                                                         const int32_t* __restrict__ land_point, double* __restrict__ pose,
+                                                         double* __restrict__ pose_bak, double* __restrict__ point,
+                                                         double* __restrict__ point_bak, const LmState* __restrict__ st) {
+    if (lm_skip(st, kGateTrial)) return;
+    const bool rej = st->reject != 0;
+    const int t = blockIdx.x * kT + threadIdx.x;
+    if (t < nl) {
+        ba_backsub(t, n, *lam, off, eidx, edges, pose_h, hpl, bl, hll, x);
+        ba_update(nf + t, nf, nl, n, rej, free_pose, land_point, x, pose, pose_bak, point, point_bak);
+    } else if (t < nl + nf) {
+        ba_update(t - nl, nf, nl, n, rej, free_pose, land_point, x, pose, pose_bak, point, point_bak);
+    }
+}
+
+// unit step 7 (trial): errors at the new estimate; the last block sums chi2 and computeScale and
+// runs the trial controller
+__global__ __launch_bounds__(kT) void k_u_edges_trial(int ne, const EdgeDev* __restrict__ edges,
+                                                      const orb_ba_camera_t* __restrict__ cams,
+                                                      const double* __restrict__ pose, const double* __restrict__ point,
+                                                      const int32_t* __restrict__ pose_h, Huber2 hub,
+                                                      double* __restrict__ err, double* __restrict__ rho0_out,
+                                                      double* __restrict__ part, unsigned* counter, int nx,
+                                                      const double* __restrict__ x, const double* __restrict__ b,
+                                                      const int32_t* __restrict__ status, double* __restrict__ scal,
+                                                      LmState* st, LmProgress* prog) {
+    if (lm_skip(st, kGateTrial)) return;
+    const int e = blockIdx.x * kT + threadIdx.x;
+    double r = 0.0;
+    if (e < ne) r = ba_edge<false>(e, edges, cams, pose, point, pose_h, hub, err, rho0_out, nullptr, nullptr, nullptr, 0);
+    const double bsum = block_sum<kT>(r);
+    if (threadIdx.x == 0) part[blockIdx.x] = bsum;
+    if (!last_block(counter)) return;
+    double c = 0.0;
+    for (int i = threadIdx.x; i < (int)gridDim.x; i += kT) c += part[i];
+    const double chi = block_sum<kT>(c);
+    const double lambda = st->lambda;
+    double sc = 0.0;
+    for (int i = threadIdx.x; i < nx; i += kT) sc += x[i] * (lambda * x[i] + b[i]);
+    const double scale = block_sum<kT>(sc);
+    if (threadIdx.x == 0) {
+        const bool failed = *status != 0;
+        scal[0] = chi;
+        scal[1] = scale;
+        scal[2] = failed ? 1.0 : 0.0;
+        lm_trial_done(st, chi, scale, failed, prog);
+        *counter = 0;
+    }
 }
 
 template <typename T>
@@ -1255,6 +1653,41 @@ struct DevBuf {
 
 }  // namespace
 
+// All per-solve inputs travel in one pinned staging buffer: one H2D copy, then k_ba_scatter moves
+// every array to its device buffer (one launch instead of one copy per array).
+struct ScatterItem {
+    uint64_t dst, off, bytes;
+};
+
+__global__ __launch_bounds__(256) void k_ba_scatter(const uint8_t* __restrict__ src, const ScatterItem* __restrict__ items) {
+    const ScatterItem it = items[blockIdx.y];
+    uint8_t* dst = reinterpret_cast<uint8_t*>(it.dst);
+    const uint8_t* sp = src + it.off;
+    const size_t n16 = it.bytes / 16;
+    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256)
+        reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(sp)[i];
+    if (blockIdx.x == 0 && threadIdx.x < it.bytes % 16) dst[n16 * 16 + threadIdx.x] = sp[n16 * 16 + threadIdx.x];
+}
+
+struct Stager {
+    std::vector<uint8_t> host;
+    std::vector<ScatterItem> items;
+    template <typename T>
+    bool add(DevBuf<T>& d, const T* src, size_t n) {
+        if (!d.grow(n)) return false;
+        if (n == 0) return true;
+        const size_t off = (host.size() + 15) & ~size_t(15);
+        host.resize(off + n * sizeof(T));
+        memcpy(host.data() + off, src, n * sizeof(T));
+        items.push_back({(uint64_t)(uintptr_t)d.p, off, n * sizeof(T)});
+        return true;
+    }
+    template <typename T>
+    bool add(DevBuf<T>& d, const std::vector<T>& v) {
+        return add(d, v.data(), v.size());
+    }
+};
+
 struct orb_ba_s {
     hipStream_t stream = nullptr;
     DevBuf<double> pose, pose_bak, point, point_bak, err, rho0, ecl, hpl, ecp, hpp, hll, b, z, cb, S, LT, Linv, bs, x, scal;
@@ -1263,7 +1696,16 @@ struct orb_ba_s {
     DevBuf<int32_t> pose_h, free_pose, land_point, land_off, land_edge, landf_off, landf_edge, fland, pose_off, pose_edge,
         blk_i, blk_j, blk_off, pair_a, pair_b, status;
     DevBuf<uint8_t> depth;
-    double* h_scal = nullptr;  // pinned: [0] chi2, [1] scale, [2] status, [3] maxdiag, [4] stop
+    double* h_scal = nullptr;  // pinned: [0] chi2, [1] scale, [2] status, [3] maxdiag, [4] stop, [5] lambda
+    DevBuf<LmState> lm;        // device-driven LM state
+    DevBuf<double> part;       // per-block chi2 partials of the fused unit kernels
+    DevBuf<unsigned> counters;  // last-block counters of the fused unit kernels
+    uint8_t* h_stage = nullptr;  // pinned staging of the per-solve inputs
+    size_t h_stage_cap = 0;
+    DevBuf<uint8_t> d_stage;
+    LmState* h_lm = nullptr;   // pinned staging of the initial state
+    LmProgress* h_prog = nullptr;  // pinned, written by k_lm_trial_done
+    hipEvent_t unit_ev[2] = {nullptr, nullptr};
     float ms_total = 0;
     // multi-GPU: ranks own landmark ranges; partial sums are all-reduced
     int world = 1, rank = 0;
@@ -1273,6 +1715,7 @@ struct orb_ba_s {
     double* h_red = nullptr;  // pinned staging of the host reducer
     size_t h_red_cap = 0;
     DevBuf<double> red_buf;
+    DevBuf<int64_t> trace;  // ORBGPU_BA_TRACE stamps (debug)
 
     void release() {
         for (auto* d : {&pose, &pose_bak, &point, &point_bak, &err, &rho0, &ecl, &hpl, &ecp, &hpp, &hll, &b, &z,
@@ -1316,7 +1759,11 @@ int orb_ba_create(orb_ba_t* out) {
     }
     auto* h = new orb_ba_s();
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc(&h->h_scal, 8 * sizeof(double), hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc(&h->h_scal, 8 * sizeof(double), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&h->h_lm, sizeof(LmState), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&h->h_prog, sizeof(LmProgress), hipHostMallocDefault) != hipSuccess || !h->lm.grow(1) ||
+        hipEventCreateWithFlags(&h->unit_ev[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->unit_ev[1], hipEventDisableTiming) != hipSuccess) {
         delete h;
         return orbgpu_fail(ORB_ERR_DEVICE, "BA handle allocation");
     }
@@ -1329,11 +1776,40 @@ int orb_ba_destroy(orb_ba_t h) {
     hipStreamSynchronize(h->stream);
     h->release();
     h->red_buf.release();
+    h->lm.release();
+    h->part.release();
+    h->counters.release();
+    h->d_stage.release();
+    if (h->h_stage) hipHostFree(h->h_stage);
+    if (h->h_lm) hipHostFree(h->h_lm);
+    if (h->h_prog) hipHostFree(h->h_prog);
+    for (hipEvent_t e : h->unit_ev)
+        if (e) hipEventDestroy(e);
+    h->trace.release();
     if (h->h_scal) hipHostFree(h->h_scal);
     if (h->h_red) hipHostFree(h->h_red);
     hipStreamDestroy(h->stream);
     delete h;
     return ORB_OK;
+}
+
+// ORBGPU_BA_TRACE: print the MFMA Cholesky's phase stamps (debug)
+void dump_chol_trace(const int64_t* tr, int n, hipStream_t s) {
+    std::vector<int64_t> ht(1024);
+    hipMemcpyAsync(ht.data(), tr, 1024 * sizeof(int64_t), hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    const int64_t t0 = ht[0];
+    const int NT = (n + 15) / 16;
+    auto rel = [&](int i) { return (long long)(ht[i] ? ht[i] - t0 : -1); };
+    for (int k = 0; k < NT; ++k)
+        for (int w = 0; w <= kMfTileWaves; ++w)
+            fprintf(stderr, "MFTRACE k=%d w=%d %lld %lld %lld %lld\n", k, w, rel((k * 8 + w) * 4),
+                    rel((k * 8 + w) * 4 + 1), rel((k * 8 + w) * 4 + 2), rel((k * 8 + w) * 4 + 3));
+    for (int k = NT - 1; k >= 0; --k) fprintf(stderr, "MFTRACE back k=%d %lld\n", k, rel(600 + k));
+    fprintf(stderr, "MFTRACE end %lld\n", rel(640));
+    for (int k = 0; k + 1 < NT; ++k)
+        fprintf(stderr, "MFTRACE diag k=%d factor %lld linv %lld y %lld\n", k, (long long)(ht[701 + 4 * k] - ht[700 + 4 * k]),
+                (long long)(ht[702 + 4 * k] - ht[701 + 4 * k]), (long long)(ht[703 + 4 * k] - ht[702 + 4 * k]));
 }
 
 // ---- collectives of the sharded solve -------------------------------------------------------------
@@ -1570,21 +2046,46 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     }
 
     const size_t ne1 = std::max(ne, 1);
-    bool ok = upload(h->pose, pose, s) && h->pose_bak.grow(7 * (size_t)np) &&
-              upload(h->point, pr->point, 3 * (size_t)nq, s) && h->point_bak.grow(3 * (size_t)nq) &&
-              upload(h->edges, ledges, s) && upload(h->cams, pr->pose_camera, np, s) && upload(h->pose_h, pose_h, s) &&
-              upload(h->free_pose, free_pose, s) && upload(h->land_point, land_point, s) &&
-              upload(h->land_off, land_off, s) && upload(h->land_edge, land_edge, s) &&
-              upload(h->landf_off, landf_off, s) && upload(h->landf_edge, landf_edge, s) && upload(h->fland, fland, s) &&
-              upload(h->pose_off, pose_off, s) && upload(h->pose_edge, pose_edge, s) && upload(h->blk_i, blk_i, s) &&
-              upload(h->blk_j, blk_j, s) && upload(h->blk_off, blk_off, s) && upload(h->pair_a, pair_a, s) &&
-              upload(h->pair_b, pair_b, s) && h->err.grow(3 * ne1) && h->rho0.grow(ne1) && h->ecl.grow(12 * ne1) &&
-              h->hpl.grow(18 * ne1) && h->ecp.grow(42 * ne1) && h->hpp.grow(36 * (size_t)nf) &&
-              h->hll.grow(9 * (size_t)nl) && h->b.grow(n + m) && h->z.grow(18 * ne1) && h->cb.grow(6 * ne1) &&
-              h->S.grow((size_t)n * n) && h->LT.grow((size_t)n * n) && h->Linv.grow((size_t)n * 32 + 32 * 32) &&
-              h->bs.grow(n) && h->x.grow(n + m) && h->status.grow(1) && h->depth.grow(ne1);
+    Stager st;
+    bool ok = st.add(h->pose, pose) && h->pose_bak.grow(7 * (size_t)np) && st.add(h->point, pr->point, 3 * (size_t)nq) &&
+              h->point_bak.grow(3 * (size_t)nq) && st.add(h->edges, ledges) && st.add(h->cams, pr->pose_camera, np) &&
+              st.add(h->pose_h, pose_h) && st.add(h->free_pose, free_pose) && st.add(h->land_point, land_point) &&
+              st.add(h->land_off, land_off) && st.add(h->land_edge, land_edge) && st.add(h->landf_off, landf_off) &&
+              st.add(h->landf_edge, landf_edge) && st.add(h->fland, fland) && st.add(h->pose_off, pose_off) &&
+              st.add(h->pose_edge, pose_edge) && st.add(h->blk_i, blk_i) && st.add(h->blk_j, blk_j) &&
+              st.add(h->blk_off, blk_off) && st.add(h->pair_a, pair_a) && st.add(h->pair_b, pair_b) &&
+              h->err.grow(3 * ne1) && h->rho0.grow(ne1) && h->ecl.grow(12 * ne1) && h->hpl.grow(18 * ne1) &&
+              h->ecp.grow(42 * ne1) && h->hpp.grow(36 * (size_t)nf) && h->hll.grow(9 * (size_t)nl) && h->b.grow(n + m) &&
+              h->z.grow(18 * ne1) && h->cb.grow(6 * ne1) && h->S.grow((size_t)n * n) && h->LT.grow((size_t)n * n) &&
+              h->Linv.grow((size_t)n * 32 + 32 * 32) && h->bs.grow(n) && h->x.grow(n + m) && h->status.grow(1) &&
+              h->depth.grow(ne1);
+    if (ok && !st.items.empty()) {
+        // [items table | data], one pinned buffer, one copy, one scatter launch
+        const size_t tbl = st.items.size() * sizeof(ScatterItem), data_off = (tbl + 255) & ~size_t(255);
+        const size_t total = data_off + st.host.size();
+        if (total > h->h_stage_cap) {
+            if (h->h_stage) hipHostFree(h->h_stage);
+            h->h_stage = nullptr;
+            h->h_stage_cap = 0;
+            ok = hipHostMalloc(&h->h_stage, total, hipHostMallocDefault) == hipSuccess;
+            if (ok) h->h_stage_cap = total;
+        }
+        ok = ok && h->d_stage.grow(total);
+        if (ok) {
+            memcpy(h->h_stage, st.items.data(), tbl);
+            memcpy(h->h_stage + data_off, st.host.data(), st.host.size());
+            ok = hipMemcpyAsync(h->d_stage.p, h->h_stage, total, hipMemcpyHostToDevice, s) == hipSuccess;
+            size_t maxb = 0;
+            for (const ScatterItem& it : st.items) maxb = std::max<size_t>(maxb, it.bytes);
+            const unsigned gx = (unsigned)std::min<size_t>(64, std::max<size_t>(1, (maxb / 16 + 255) / 256));
+            hipLaunchKernelGGL(k_ba_scatter, dim3(gx, (unsigned)st.items.size()), dim3(256), 0, s,
+                               h->d_stage.p + data_off, (const ScatterItem*)h->d_stage.p);
+        }
+    }
     if (!ok) return orbgpu_fail(ORB_ERR_DEVICE, "BA device allocation / upload");
     hipMemsetAsync(h->x.p, 0, sizeof(double) * (n + m), s);  // g2o's _x starts zeroed
+    // S: the block pattern is fixed for the solve, so the blocks outside it are zeroed once here
+    if (n) hipMemsetAsync(h->S.p, 0, sizeof(double) * (size_t)n * n, s);
 
     const float dm = (float)std::sqrt(5.991), ds = (float)std::sqrt(7.815);  // src/Optimizer.cc:1957-1958
     const Huber2 hub{(double)dm, (double)ds, (float)((double)dm * (double)dm), (float)((double)ds * (double)ds)};
@@ -1622,137 +2123,246 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         attr_set = true;
     }
     double* bl = h->b.p + n;
-    auto launch_edges = [&](bool build) {
-        if (ne == 0) return;
-        if (build)
+    // The device-driven LM loop (one process, the MFMA Cholesky): no host round trip per trial.
+    const bool dev_lm = !dist && use_mf && !getenv("ORBGPU_BA_HOST_LM");
+    const LmState* G = dev_lm ? h->lm.p : nullptr;            // gate source for every per-trial kernel
+    const double* lam = dev_lm ? &h->lm.p->lambda : h->h_scal + 5;  // the trial's lambda (device / pinned)
+    // ---- computeActiveErrors + activeRobustChi2 + buildSystem
+    auto launch_build = [&](bool first) -> bool {
+        if (ne)
             hipLaunchKernelGGL(k_ba_edges<true>, dim3(grid(ne)), dim3(kT), 0, s, ne, h->edges.p, h->cams.p, h->pose.p,
-                               h->point.p, h->pose_h.p, hub, h->err.p, h->rho0.p, h->ecl.p, h->hpl.p, h->ecp.p);
-        else
-            hipLaunchKernelGGL(k_ba_edges<false>, dim3(grid(ne)), dim3(kT), 0, s, ne, h->edges.p, h->cams.p, h->pose.p,
-                               h->point.p, h->pose_h.p, hub, h->err.p, h->rho0.p, h->ecl.p, h->hpl.p, h->ecp.p);
+                               h->point.p, h->pose_h.p, hub, h->err.p, h->rho0.p, h->ecl.p, h->hpl.p, h->ecp.p, G,
+                               (int)kGateBuild);
+        if (nl)
+            hipLaunchKernelGGL(k_ba_reduce_land, dim3(grid(nl)), dim3(kT), 0, s, nl, h->land_off.p, h->land_edge.p,
+                               h->ecl.p, h->hll.p, bl, G, (int)kGateBuild);
+        if (nf) {
+            hipLaunchKernelGGL(k_ba_reduce_pose, dim3(nf), dim3(64), 0, s, h->pose_off.p, h->pose_edge.p, h->ecp.p,
+                               h->hpp.p, h->b.p, G, (int)kGateBuild);
+            if (!dev_reduce(h, h->hpp.p, 36 * (size_t)nf, ORB_BA_SUM) || !dev_reduce(h, h->b.p, n, ORB_BA_SUM))
+                return false;
+        }
+        if (first)  // (on the device path the gate limits it to iteration 0)
+            hipLaunchKernelGGL(k_ba_maxdiag, dim3(1), dim3(kT), 0, s, nf, nl, h->hpp.p, h->hll.p, h->scal.p + 3, G,
+                               (int)kGateBuild0);
+        hipLaunchKernelGGL(k_ba_sums, dim3(1), dim3(1024), 0, s, ne, h->rho0.p, primary ? 0 : n, n + m, lam,
+                           (const double*)nullptr, h->b.p, h->status.p, h->scal.p, dev_lm || dist ? nullptr : h->h_scal,
+                           G, (int)kGateBuild);
+        return true;
     };
-    // [0] robust chi2 (sum over the ranks' edges), [1] computeScale (pose part counted by rank 0),
-    // [2] factorisation status (identical on every rank), [3] max diag (max over the ranks)
-    auto read_scalars = [&](double lambda, bool with_x) -> bool {
-        hipLaunchKernelGGL(k_ba_sums, dim3(1), dim3(1024), 0, s, ne, h->rho0.p, primary ? 0 : n, n + m, lambda,
-                           with_x ? h->x.p : nullptr, h->b.p, h->scal.p);
-        if (!dev_reduce(h, h->scal.p, 2, ORB_BA_SUM) || !dev_reduce(h, h->scal.p + 3, 1, ORB_BA_MAX)) return false;
-        hipMemcpyAsync(h->scal.p + 2, h->status.p, sizeof(int32_t), hipMemcpyDeviceToDevice, s);
-        hipMemcpyAsync(h->h_scal, h->scal.p, 4 * sizeof(double), hipMemcpyDeviceToHost, s);
+    // ---- setLambda + BlockSolver::solve + SparseOptimizer::update + computeActiveErrors + computeScale
+    auto launch_trial = [&]() -> bool {
+        if (nfe)
+            hipLaunchKernelGGL(k_ba_schur_edges, dim3(grid(nfe)), dim3(kT), 0, s, nfe, lam, h->landf_edge.p, h->fland.p,
+                               h->hll.p, bl, h->hpl.p, h->z.p, h->cb.p, G, (int)kGateTrial);
+        if (nf) {
+            hipLaunchKernelGGL(k_ba_schur_blocks, dim3(nblk), dim3(64), 0, s, n, lam, primary ? 1 : 0, h->blk_i.p,
+                               h->blk_j.p, h->blk_off.p, h->pair_a.p, h->pair_b.p, h->z.p, h->hpl.p, h->hpp.p, h->S.p, G,
+                               (int)kGateTrial);
+            hipLaunchKernelGGL(k_ba_schur_rhs, dim3(nf), dim3(64), 0, s, h->pose_off.p, h->pose_edge.p, h->cb.p, h->b.p,
+                               primary ? 1 : 0, h->bs.p, G, (int)kGateTrial);
+            if (!dev_reduce(h, h->S.p, (size_t)n * n, ORB_BA_SUM) || !dev_reduce(h, h->bs.p, n, ORB_BA_SUM))
+                return false;
+            if (coop_nb) {
+                hipMemsetAsync(h->status.p, 0, sizeof(int32_t), s);
+                int nn = n;
+                double* Sp = h->S.p;
+                double* Lp = h->LT.p;
+                double* bp = h->bs.p;
+                double* xp = h->x.p;
+                int32_t* stp = h->status.p;
+                int64_t* trp = nullptr;
+                double* Lip = h->Linv.p;
+                void* args[] = {&nn, &Sp, &Lp, &Lip, &bp, &xp, &stp, &trp};
+                const dim3 g((n + coop_nb - 1) / coop_nb + 1);
+                const hipError_t le =
+                    coop_nb == 32 ? hipLaunchCooperativeKernel((const void*)k_ba_chol_coop<32>, g, dim3(kCoopThreads),
+                                                               args, (unsigned)coop_lds, s)
+                                  : hipLaunchCooperativeKernel((const void*)k_ba_chol_coop<16>, g, dim3(kCoopThreads),
+                                                               args, (unsigned)coop_lds, s);
+                if (le != hipSuccess) return false;
+            } else if (use_mf) {
+                int64_t* tr = nullptr;
+                static int trace_left = getenv("ORBGPU_BA_TRACE") ? 1 : 0;
+                if (trace_left && h->trace.grow(1024)) {
+                    hipMemsetAsync(h->trace.p, 0, 1024 * sizeof(int64_t), s);
+                    tr = h->trace.p;
+                }
+                hipLaunchKernelGGL(k_ba_chol_mfma<kMfTileWaves>, dim3(1), dim3((kMfTileWaves + 1) * 64), kMfLds, s, n,
+                                   h->S.p, h->bs.p, h->x.p, h->status.p, tr, G, (int)kGateTrial);
+                if (tr) {
+                    trace_left = 0;
+                    dump_chol_trace(tr, n, s);
+                }
+            } else if (nb == 16)
+                hipLaunchKernelGGL(k_ba_chol<16>, dim3(1), dim3(kCholThreads), chol_lds, s, n, h->S.p, h->LT.p, h->bs.p,
+                                   h->x.p, h->status.p);
+            else
+                hipLaunchKernelGGL(k_ba_chol<8>, dim3(1), dim3(kCholThreads), chol_lds, s, n, h->S.p, h->LT.p, h->bs.p,
+                                   h->x.p, h->status.p);
+        } else if (!dev_lm) {
+            hipMemsetAsync(h->status.p, 0, sizeof(int32_t), s);
+        }
+        if (nl)
+            hipLaunchKernelGGL(k_ba_backsub, dim3(grid(nl)), dim3(kT), 0, s, nl, n, lam, h->landf_off.p, h->landf_edge.p,
+                               h->edges.p, h->pose_h.p, h->hpl.p, bl, h->hll.p, h->x.p, G, (int)kGateTrial);
+        hipLaunchKernelGGL(k_ba_update, dim3(grid(nf + nl)), dim3(kT), 0, s, nf, nl, n, h->free_pose.p, h->land_point.p,
+                           h->x.p, h->pose.p, h->pose_bak.p, h->point.p, h->point_bak.p, G, (int)kGateTrial);
+        if (ne)
+            hipLaunchKernelGGL(k_ba_edges<false>, dim3(grid(ne)), dim3(kT), 0, s, ne, h->edges.p, h->cams.p, h->pose.p,
+                               h->point.p, h->pose_h.p, hub, h->err.p, h->rho0.p, h->ecl.p, h->hpl.p, h->ecp.p, G,
+                               (int)kGateTrial);
+        hipLaunchKernelGGL(k_ba_sums, dim3(1), dim3(1024), 0, s, ne, h->rho0.p, primary ? 0 : n, n + m, lam,
+                           (const double*)h->x.p, h->b.p, h->status.p, h->scal.p,
+                           dev_lm || dist ? nullptr : h->h_scal, G, (int)kGateTrial);
+        return true;
+    };
+    auto launch_restore = [&]() {
+        hipLaunchKernelGGL(k_ba_restore, dim3(grid(nf + nl)), dim3(kT), 0, s, nf, nl, h->free_pose.p, h->land_point.p,
+                           h->pose.p, h->pose_bak.p, h->point.p, h->point_bak.p, G, (int)kGateRestore);
+    };
+    // the host loop reads [0] chi2, [1] computeScale, [2] status, [3] max diag (reduced over the ranks)
+    auto read_scalars = [&]() -> bool {
+        if (dist) {
+            if (!dev_reduce(h, h->scal.p, 2, ORB_BA_SUM) || !dev_reduce(h, h->scal.p + 3, 1, ORB_BA_MAX)) return false;
+            hipMemcpyAsync(h->h_scal, h->scal.p, 4 * sizeof(double), hipMemcpyDeviceToHost, s);
+        }
         return hipStreamSynchronize(s) == hipSuccess;
     };
 
-    double lambda = 0, ni = 2;
-    int nBad = 0, it = 0;
     const double tau = 1e-5;
     hipMemsetAsync(h->scal.p, 0, 8 * sizeof(double), s);
-    for (; it < opt->iterations && !stop(); ++it) {
-        // computeActiveErrors + activeRobustChi2 + buildSystem
-        launch_edges(true);
-        if (nl)
-            hipLaunchKernelGGL(k_ba_reduce_land, dim3(grid(nl)), dim3(kT), 0, s, nl, h->land_off.p, h->land_edge.p,
-                               h->ecl.p, h->hll.p, bl);
-        if (nf) {
-            hipLaunchKernelGGL(k_ba_reduce_pose, dim3(nf), dim3(64), 0, s, h->pose_off.p, h->pose_edge.p, h->ecp.p,
-                               h->hpp.p, h->b.p);
-            if (!dev_reduce(h, h->hpp.p, 36 * (size_t)nf, ORB_BA_SUM) || !dev_reduce(h, h->b.p, n, ORB_BA_SUM))
-                return orbgpu_fail(ORB_ERR_DEVICE, "BA all-reduce (Hpp, b_p) failed");
-        }
-        if (it == 0)
-            hipLaunchKernelGGL(k_ba_maxdiag, dim3(1), dim3(kT), 0, s, nf, nl, h->hpp.p, h->hll.p, h->scal.p + 3);
-        if (!read_scalars(0.0, false)) return orbgpu_fail(ORB_ERR_DEVICE, "BA build failed");
-        double currentChi = h->h_scal[0];
-        const double iniChi = currentChi;
-        if (it == 0) {
-            res->initial_chi2 = currentChi;
-            lambda = opt->user_lambda_init > 0 ? opt->user_lambda_init : tau * h->h_scal[3];
-            ni = 2;
-            nBad = 0;
-        }
-        double rho = 0;
-        int qmax = 0;
-        do {
-            // setLambda + BlockSolver::solve (partial S, b_S per rank, then all-reduced)
+    if (dev_lm) {
+        // One unit per trial: build (gated to the start of an iteration), the build controller, the
+        // trial, the trial controller, restore on reject.  The host keeps one unit queued behind the
+        // running one and reads the pinned progress after each unit's event; once the solve is done
+        // the queued unit is a run of no-op launches.
+        LmState init{};
+        init.ni = 2;
+        init.user_lambda = opt->user_lambda_init;
+        init.tau = tau;
+        init.iterations = opt->iterations;
+        init.done = opt->iterations <= 0;
+        *h->h_lm = init;
+        hipMemcpyAsync(h->lm.p, h->h_lm, sizeof(LmState), hipMemcpyHostToDevice, s);
+        memset(h->h_prog, 0, sizeof(LmProgress));
+        const int nparts = (int)grid(ne);
+        if (!h->part.grow(nparts) || !h->counters.grow(2)) return orbgpu_fail(ORB_ERR_DEVICE, "BA unit buffers");
+        hipMemsetAsync(h->counters.p, 0, 2 * sizeof(unsigned), s);
+        hipMemsetAsync(h->status.p, 0, sizeof(int32_t), s);
+        LmState* L = h->lm.p;
+        // one unit = 7 launches: edges+linearise, reductions (+ chi2, max diag, build controller),
+        // Schur edges, Schur blocks + rhs, Cholesky + solves, back-substitution + update, errors at
+        // the new estimate (+ chi2, computeScale, trial controller)
+        auto unit = [&](int u) -> bool {
+            hipLaunchKernelGGL(k_u_edges_build, dim3(nparts), dim3(kT), 0, s, ne, h->edges.p, h->cams.p, h->pose.p,
+                               h->point.p, h->pose_h.p, hub, h->err.p, h->rho0.p, h->ecl.p, h->hpl.p, h->ecp.p,
+                               h->part.p, (const LmState*)L);
+            hipLaunchKernelGGL(k_u_reduce_build, dim3(nf + (nl + 63) / 64), dim3(64), 0, s, nf, nl, h->pose_off.p,
+                               h->pose_edge.p, h->ecp.p, h->hpp.p, h->b.p, h->land_off.p, h->land_edge.p, h->ecl.p,
+                               h->hll.p, bl, h->part.p, nparts, h->counters.p, h->scal.p, L);
             if (nfe)
-                hipLaunchKernelGGL(k_ba_schur_edges, dim3(grid(nfe)), dim3(kT), 0, s, nfe, lambda, h->landf_edge.p,
-                                   h->fland.p, h->hll.p, bl, h->hpl.p, h->z.p, h->cb.p);
+                hipLaunchKernelGGL(k_ba_schur_edges, dim3(grid(nfe)), dim3(kT), 0, s, nfe, lam, h->landf_edge.p,
+                                   h->fland.p, h->hll.p, bl, h->hpl.p, h->z.p, h->cb.p, (const LmState*)L,
+                                   (int)kGateTrial);
             if (nf) {
-                hipMemsetAsync(h->S.p, 0, sizeof(double) * (size_t)n * n, s);
-                hipLaunchKernelGGL(k_ba_schur_blocks, dim3(nblk), dim3(64), 0, s, n, lambda, primary ? 1 : 0, h->blk_i.p,
-                                   h->blk_j.p, h->blk_off.p, h->pair_a.p, h->pair_b.p, h->z.p, h->hpl.p, h->hpp.p, h->S.p);
-                hipLaunchKernelGGL(k_ba_schur_rhs, dim3(nf), dim3(64), 0, s, h->pose_off.p, h->pose_edge.p, h->cb.p,
-                                   h->b.p, primary ? 1 : 0, h->bs.p);
-                if (!dev_reduce(h, h->S.p, (size_t)n * n, ORB_BA_SUM) || !dev_reduce(h, h->bs.p, n, ORB_BA_SUM))
-                    return orbgpu_fail(ORB_ERR_DEVICE, "BA all-reduce (S, b_S) failed");
-                if (coop_nb) {
-                    hipMemsetAsync(h->status.p, 0, sizeof(int32_t), s);
-                    int nn = n;
-                    double* Sp = h->S.p;
-                    double* Lp = h->LT.p;
-                    double* bp = h->bs.p;
-                    double* xp = h->x.p;
-                    int32_t* stp = h->status.p;
-                    int64_t* trp = nullptr;
-                    double* Lip = h->Linv.p;
-                    void* args[] = {&nn, &Sp, &Lp, &Lip, &bp, &xp, &stp, &trp};
-                    const dim3 g((n + coop_nb - 1) / coop_nb + 1);
-                    const hipError_t le =
-                        coop_nb == 32
-                            ? hipLaunchCooperativeKernel((const void*)k_ba_chol_coop<32>, g, dim3(kCoopThreads), args,
-                                                         (unsigned)coop_lds, s)
-                            : hipLaunchCooperativeKernel((const void*)k_ba_chol_coop<16>, g, dim3(kCoopThreads), args,
-                                                         (unsigned)coop_lds, s);
-                    if (le != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "cooperative Cholesky launch failed");
-                } else if (use_mf)
-                    hipLaunchKernelGGL(k_ba_chol_mfma<kMfTileWaves>, dim3(1), dim3((kMfTileWaves + 1) * 64), kMfLds, s, n, h->S.p, h->bs.p,
-                                       h->x.p, h->status.p);
-                else if (nb == 16)
-                    hipLaunchKernelGGL(k_ba_chol<16>, dim3(1), dim3(kCholThreads), chol_lds, s, n, h->S.p, h->LT.p,
-                                       h->bs.p, h->x.p, h->status.p);
-                else
-                    hipLaunchKernelGGL(k_ba_chol<8>, dim3(1), dim3(kCholThreads), chol_lds, s, n, h->S.p, h->LT.p,
-                                       h->bs.p, h->x.p, h->status.p);
-            } else {
-                hipMemsetAsync(h->status.p, 0, sizeof(int32_t), s);
+                hipLaunchKernelGGL(k_u_schur, dim3(nblk + nf), dim3(64), 0, s, n, nblk, lam, h->blk_i.p, h->blk_j.p,
+                                   h->blk_off.p, h->pair_a.p, h->pair_b.p, h->z.p, h->hpl.p, h->hpp.p, h->S.p,
+                                   h->pose_off.p, h->pose_edge.p, h->cb.p, h->b.p, h->bs.p, (const LmState*)L);
+                int64_t* tr = nullptr;
+                static int trace_left_u = getenv("ORBGPU_BA_TRACE") ? 1 : 0;
+                if (trace_left_u && h->trace.grow(1024)) {
+                    hipMemsetAsync(h->trace.p, 0, 1024 * sizeof(int64_t), s);
+                    tr = h->trace.p;
+                }
+                hipLaunchKernelGGL(k_ba_chol_mfma<kMfTileWaves>, dim3(1), dim3((kMfTileWaves + 1) * 64), kMfLds, s, n,
+                                   h->S.p, h->bs.p, h->x.p, h->status.p, tr, (const LmState*)L, (int)kGateTrial);
+                if (tr) {
+                    trace_left_u = 0;
+                    dump_chol_trace(tr, n, s);
+                }
             }
-            if (nl)
-                hipLaunchKernelGGL(k_ba_backsub, dim3(grid(nl)), dim3(kT), 0, s, nl, n, lambda, h->landf_off.p,
-                                   h->landf_edge.p, h->edges.p, h->pose_h.p, h->hpl.p, bl, h->hll.p, h->x.p);
-            // SparseOptimizer::update (push first), then computeActiveErrors
-            hipLaunchKernelGGL(k_ba_update, dim3(grid(nf + nl)), dim3(kT), 0, s, nf, nl, n, h->free_pose.p,
-                               h->land_point.p, h->x.p, h->pose.p, h->pose_bak.p, h->point.p, h->point_bak.p);
-            launch_edges(false);
-            if (!read_scalars(lambda, true)) return orbgpu_fail(ORB_ERR_DEVICE, "BA trial failed");
-            res->trials++;
-            int32_t st;
-            memcpy(&st, &h->h_scal[2], sizeof(st));
-            double tempChi = h->h_scal[0];
-            if (st) tempChi = std::numeric_limits<double>::max();  // solve failed (not positive definite)
-            rho = currentChi - tempChi;
-            double scale = h->h_scal[1] + 1e-3;
-            rho /= scale;
-            if (rho > 0 && std::isfinite(tempChi)) {
-                double alpha = 1. - std::pow((2 * rho - 1), 3);
-                alpha = std::min(alpha, 2. / 3.);
-                lambda *= std::max(1. / 3., alpha);
+            hipLaunchKernelGGL(k_u_backsub_update, dim3(grid(nl + nf)), dim3(kT), 0, s, nl, nf, n, lam, h->landf_off.p,
+                               h->landf_edge.p, h->edges.p, h->pose_h.p, h->hpl.p, bl, h->hll.p, h->x.p, h->free_pose.p,
+                               h->land_point.p, h->pose.p, h->pose_bak.p, h->point.p, h->point_bak.p,
+                               (const LmState*)L);
+            hipLaunchKernelGGL(k_u_edges_trial, dim3(nparts), dim3(kT), 0, s, ne, h->edges.p, h->cams.p, h->pose.p,
+                               h->point.p, h->pose_h.p, hub, h->err.p, h->rho0.p, h->part.p, h->counters.p + 1, n + m,
+                               h->x.p, h->b.p, h->status.p, h->scal.p, L, h->h_prog);
+            return hipEventRecord(h->unit_ev[u & 1], s) == hipSuccess;
+        };
+        const int max_units = std::max(0, opt->iterations) * 10;
+        bool stopped_mid = false;
+        if (max_units > 0) {
+            if (!unit(0)) return orbgpu_fail(ORB_ERR_DEVICE, "BA launch failed");
+            for (int u = 1;; ++u) {
+                const bool more = u < max_units;
+                if (more && !unit(u)) return orbgpu_fail(ORB_ERR_DEVICE, "BA launch failed");
+                if (hipEventSynchronize(h->unit_ev[(u - 1) & 1]) != hipSuccess)
+                    return orbgpu_fail(ORB_ERR_DEVICE, "BA device error");
+                if (h->h_prog->done || !more) break;
+                if (opt->stop_flag && *opt->stop_flag) {
+                    stopped_mid = true;
+                    break;
+                }
+            }
+        }
+        launch_restore();  // undo a rejected last trial (gated on the device state)
+        if (hipStreamSynchronize(s) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "BA device error");
+        (void)stopped_mid;
+        const LmProgress pg = *h->h_prog;
+        res->iterations = pg.it;
+        res->trials = pg.trials;
+        res->terminated = pg.terminated;
+        res->initial_chi2 = pg.initial_chi;
+        res->final_chi2 = pg.final_chi;
+        res->lambda = pg.lambda;
+    } else {
+        double lambda = 0, ni = 2;
+        int nBad = 0, it = 0;
+        for (; it < opt->iterations && !stop(); ++it) {
+            if (!launch_build(it == 0) || !read_scalars()) return orbgpu_fail(ORB_ERR_DEVICE, "BA build failed");
+            double currentChi = h->h_scal[0];
+            const double iniChi = currentChi;
+            if (it == 0) {
+                res->initial_chi2 = currentChi;
+                lambda = opt->user_lambda_init > 0 ? opt->user_lambda_init : tau * h->h_scal[3];
                 ni = 2;
-                currentChi = tempChi;
-            } else {
-                lambda *= ni;
-                ni *= 2;
-                hipLaunchKernelGGL(k_ba_restore, dim3(grid(nf + nl)), dim3(kT), 0, s, nf, nl, h->free_pose.p,
-                                   h->land_point.p, h->pose.p, h->pose_bak.p, h->point.p, h->point_bak.p);
+                nBad = 0;
             }
-            qmax++;
-        } while (rho < 0 && qmax < 10 && !stop());
-        res->final_chi2 = currentChi;
-        if (qmax == 10 || rho == 0) { res->terminated = 1; ++it; break; }
-        if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
-        else nBad = 0;
-        if (nBad >= 3) { res->terminated = 1; ++it; break; }
+            double rho = 0;
+            int qmax = 0;
+            do {
+                h->h_scal[5] = lambda;  // read by the trial kernels (the stream is idle here)
+                if (!launch_trial() || !read_scalars()) return orbgpu_fail(ORB_ERR_DEVICE, "BA trial failed");
+                res->trials++;
+                double tempChi = h->h_scal[0];
+                if (h->h_scal[2] != 0.0) tempChi = std::numeric_limits<double>::max();  // not positive definite
+                rho = currentChi - tempChi;
+                double scale = h->h_scal[1] + 1e-3;
+                rho /= scale;
+                if (rho > 0 && std::isfinite(tempChi)) {
+                    double alpha = 1. - std::pow((2 * rho - 1), 3);
+                    alpha = std::min(alpha, 2. / 3.);
+                    lambda *= std::max(1. / 3., alpha);
+                    ni = 2;
+                    currentChi = tempChi;
+                } else {
+                    lambda *= ni;
+                    ni *= 2;
+                    launch_restore();
+                }
+                qmax++;
+            } while (rho < 0 && qmax < 10 && !stop());
+            res->final_chi2 = currentChi;
+            if (qmax == 10 || rho == 0) { res->terminated = 1; ++it; break; }
+            if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
+            else nBad = 0;
+            if (nBad >= 3) { res->terminated = 1; ++it; break; }
+        }
+        res->iterations = it;
+        res->lambda = lambda;
     }
-    res->iterations = it;
-    res->lambda = lambda;
     res->stopped = stop() ? 1 : 0;
     if (ne)
         hipLaunchKernelGGL(k_ba_final, dim3(grid(ne)), dim3(kT), 0, s, ne, h->edges.p, h->pose.p, h->point.p, h->err.p,

@@ -1,0 +1,25 @@
+"""Per-unit timeline of the BA solve from a rocprofv3 kernel-trace db: kernel durations and the
+idle gaps between consecutive dispatches (one representative unit, the median over units)."""
+import sqlite3
+import sys
+from collections import defaultdict
+from statistics import median
+
+c = sqlite3.connect(sys.argv[1])
+rows = c.execute("select s.kernel_name, d.start, d.end from rocpd_kernel_dispatch d join rocpd_info_kernel_symbol s "
+                 "on d.kernel_id=s.id order by d.start").fetchall()
+dur = defaultdict(list)
+gap = defaultdict(list)
+prev_end = None
+for name, st, en in rows:
+    short = name.split("(")[0].replace("_ZN12_GLOBAL__N_1", "")[:40]
+    dur[short].append((en - st) / 1e3)
+    if prev_end is not None and 0 <= st - prev_end < 200e3:
+        gap[short].append((st - prev_end) / 1e3)
+    prev_end = en
+print(f"{'kernel':42s} {'n':>5s} {'dur_med':>8s} {'gap_before_med':>15s}")
+tot_d = tot_g = 0.0
+for k in dur:
+    d = median(dur[k])
+    g = median(gap[k]) if gap[k] else 0.0
+    print(f"{k:42s} {len(dur[k]):5d} {d:8.2f} {g:15.2f}")
