@@ -1000,6 +1000,294 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mfma(int n, const doub
 #undef MF_STAMP
 }
 
+// ---- v2: the diagonal wave carries the whole critical chain ----------------------------------------
+// Same tiles, layouts and arithmetic as k_ba_chol_mfma, rescheduled so that the sequential part
+// of every step runs in one wave without workgroup barriers:
+//   diagonal wave, step k: wait for the "pre" tiles A_{k+1,k}, P_{k+1,k+1} (updated through panel
+//   k-1, published by their owners in LDS); L_{k+1,k} = A L_kk^-T (4 MFMAs), b_{k+1} -= L y_k,
+//   P -= L L^T (4 MFMAs), factor P (mf_diag), publish L_{k+1,k+1}^-1 and y_{k+1} (flag lk).
+//   tile waves, step k: wait for lk >= k; panel tiles (i > k, k) into the double-buffered panel;
+//   b_i -= L_ik y_k for i > k + 1; tile-wave barrier (LDS counter); trailing update, the next
+//   step's two pre tiles first.  The diagonal tile (k+1, k+1) is left to the diagonal wave.
+// Backward: the diagonal wave keeps every L_{k+1,k} (sub-diagonal tile) in LDS, so the chain
+// x_{k+1} -> x_k never leaves it; the tile waves add the other rows' L_kj^T x_k contributions into
+// per-tile slots (the panel buffers, free by then), summed in a fixed order.
+constexpr size_t kMf2Lds = sizeof(double) * ((2 + 1) * (size_t)kMfMaxNT * 256 + (kMfMaxNT - 1) * 256 + 4 * 256 +
+                                             16 * 17 + 2 * 16 * kMfMaxNT);
+
+__device__ __forceinline__ void lds_flag_wait(int* f, int target, int lane, int* fail, int code) {
+    for (int spin = 0; __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target; ++spin) {
+        if (spin > (1 << 22)) {  // bounded: a missing hand-off fails the solve instead of hanging
+            if (lane == 0) *fail = code;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const double* __restrict__ S,
+                                                              const double* __restrict__ b, double* __restrict__ x,
+                                                              int32_t* __restrict__ status, int64_t* __restrict__ trace,
+                                                              const LmState* __restrict__ lm_st, int lm_gk) {
+    if (lm_skip(lm_st, lm_gk)) return;
+    constexpr int SL = (kMfMaxNT * (kMfMaxNT + 1) / 2 + W - 1) / W;
+    static_assert(SL <= 32, "slot dispatch covers 32 slots");
+    extern __shared__ double lds[];
+    double* pan = lds;                        // [2][NT][256] panel tiles O(L_ik), by step parity
+    double* contrib = lds;                    // backward: [k (k - 1) / 2 + j][16] (aliases pan)
+    double* linv = pan + 2 * kMfMaxNT * 256;  // [NT][256] O(L_kk^-1)
+    double* sub = linv + kMfMaxNT * 256;      // [NT - 1][256] O(L_{k+1,k})
+    double* pre = sub + (kMfMaxNT - 1) * 256;  // [2][2][256] A_{k+1,k}, P_{k+1,k+1} by step parity
+    double* dk = pre + 4 * 256;               // [16][17]
+    double* yv = dk + 16 * 17;                // [16 NT]
+    double* xv = yv + 16 * kMfMaxNT;          // [16 NT]
+    __shared__ int fail, lk, tbar, xready, pre_ready[kMfMaxNT], cnt[kMfMaxNT];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int NT = (n + 15) >> 4, ntt = NT * (NT + 1) / 2;
+    const int r16 = lane & 15, g4 = lane >> 4;
+    if (threadIdx.x == 0) {
+        fail = 0;
+        lk = -1;
+        tbar = 0;
+        xready = 0;  // number of x blocks published (x_{NT-1} first)
+    }
+    if (threadIdx.x < kMfMaxNT) {
+        pre_ready[threadIdx.x] = 0;
+        cnt[threadIdx.x] = 0;
+    }
+    for (int i = threadIdx.x; i < 16 * NT; i += (W + 1) * 64) yv[i] = i < n ? b[i] : 0.0;
+    __syncthreads();  // the only workgroup barrier before the end
+    if (w == W) {
+        // ---------------- diagonal wave ----------------
+        for (int t = lane; t < 256; t += 64) {
+            const int r = t >> 4, c = t & 15;
+            dk[r * 17 + c] = (r < n && c < n) ? S[(size_t)r * n + c] : (r == c ? 1.0 : 0.0);
+        }
+        mf_wave_sync();
+        mf_diag(dk, linv, yv, lane, &fail);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&lk, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (int k = 0; k + 1 < NT; ++k) {
+            if (trace && lane == 0) trace[(k * 8 + W) * 4 + 1] = clock64();
+            lds_flag_wait(&pre_ready[k], 2, lane, &fail, 2);
+            if (trace && lane == 0) trace[(k * 8 + W) * 4 + 2] = clock64();
+            const double* A = pre + (k & 1) * 512;
+            const double* P = A + 256;
+            const double* lkk = linv + k * 256;
+            f64x4 L = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) L = __builtin_amdgcn_mfma_f64_16x16x4f64(lkk[q * 64 + lane], A[q * 64 + lane], L, 0, 0, 0);
+            f64x4 Pm = {P[lane], P[64 + lane], P[128 + lane], P[192 + lane]};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) Pm = __builtin_amdgcn_mfma_f64_16x16x4f64(L[q], L[q], Pm, 0, 0, 1);
+            double part = 0.0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                sub[k * 256 + q * 64 + lane] = L[q];
+                part = __builtin_fma(L[q], yv[16 * k + g4 + 4 * q], part);
+                dk[r16 * 17 + g4 + 4 * q] = Pm[q];
+            }
+            part += __shfl_xor(part, 16);
+            part += __shfl_xor(part, 32);
+            if (lane < 16) yv[16 * (k + 1) + lane] -= part;  // b_{k+1} -= L_{k+1,k} y_k
+            mf_wave_sync();
+            mf_diag(dk, linv + (k + 1) * 256, yv + 16 * (k + 1), lane, &fail, trace ? trace + 700 + 4 * k : nullptr);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) __hip_atomic_store(&lk, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (trace && lane == 0) trace[(k * 8 + W) * 4 + 3] = clock64();
+        }
+        // backward: x_j = L_jj^-T (y_j - sum_{k >= j+2} c_kj - L_{j+1,j}^T x_{j+1})
+        for (int j = NT - 1; j >= 0; --j) {
+            if (trace && lane == 0) trace[600 + j] = clock64();
+            lds_flag_wait(&cnt[j], NT - 2 - j, lane, &fail, 3);
+            double yj = yv[16 * j + r16];
+            for (int kk = NT - 1; kk >= j + 2; --kk) yj -= contrib[(kk * (kk - 1) / 2 + j) * 16 + r16];
+            if (j + 1 < NT) {
+                const double* L = sub + j * 256;  // L_{j+1,j}[r][c] at [(c >> 2) * 64 + r + 16 (c & 3)]
+                double t4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int rr = 0; rr < 16; ++rr)
+                    t4[rr & 3] = __builtin_fma(L[(r16 >> 2) * 64 + rr + 16 * (r16 & 3)], xv[16 * (j + 1) + rr], t4[rr & 3]);
+                yj -= (t4[0] + t4[1]) + (t4[2] + t4[3]);
+            }
+            mf_wave_sync();
+            if (lane < 16) yv[16 * j + r16] = yj;
+            mf_wave_sync();
+            const double* lj = linv + j * 256;
+            double v4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int rr = 0; rr < 16; ++rr)
+                v4[rr & 3] = __builtin_fma(lj[(r16 >> 2) * 64 + rr + 16 * (r16 & 3)], yv[16 * j + rr], v4[rr & 3]);
+            if (lane < 16) xv[16 * j + r16] = (v4[0] + v4[1]) + (v4[2] + v4[3]);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) __hip_atomic_store(&xready, NT - j, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    } else {
+        // ---------------- tile waves: slot s holds tile t = s W + w (packed i | j << 8) ----------------
+        int tij[SL];
+        f64x4 T[SL];
+#pragma unroll
+        for (int s = 0; s < SL; ++s) {
+            const int t = s * W + w;
+            tij[s] = -1;
+            T[s] = f64x4{0.0, 0.0, 0.0, 0.0};
+            if (t < ntt) {
+                int c = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+                while ((c + 1) * (c + 2) / 2 <= t) ++c;
+                while (c * (c + 1) / 2 > t) --c;
+                const int j = NT - 1 - c, i = j + (t - c * (c + 1) / 2);
+                tij[s] = i | (j << 8);
+                double e[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {  // S symmetric: read as S[col block][row block], coalesced
+                    const int row = 16 * j + g4 + 4 * q, col = 16 * i + r16;
+                    const double v = S[(size_t)min(row, n - 1) * n + min(col, n - 1)];
+                    e[q] = (row < n && col < n) ? v : (row == col ? 1.0 : 0.0);
+                }
+                T[s] = f64x4{e[0], e[1], e[2], e[3]};
+                if (NT > 1 && (tij[s] == (1 | (0 << 8)) || tij[s] == (1 | (1 << 8)))) {  // pre tiles of step 0
+                    double* dst = pre + (tij[s] == 1 ? 0 : 256);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) dst[q * 64 + lane] = e[q];
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    if (lane == 0) __hip_atomic_fetch_add(&pre_ready[0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+        }
+        // (range checks use `continue`, not `break`: a runtime exit stops the full unrolling that keeps
+        // T[] in registers)
+        // tiles are numbered by decreasing column: tiles with j > k are t < Tc(k) = (NT-1-k)(NT-k)/2,
+        // column k is t in [Tc(k), Tc(k) + NT - k) (its first tile is the diagonal one); this
+        // wave's slot s holds t = s W + w, so every phase below is a contiguous slot range
+        auto Tc = [&](int k) { return (NT - 1 - k) * (NT - k) / 2; };
+        auto slot_lo = [&](int t) { return t <= w ? 0 : (t - w + W - 1) / W; };  // first s with s W + w >= t
+        for (int k = 0; k + 1 < NT; ++k) {
+            if (trace && lane == 0) trace[(k * 8 + w) * 4] = clock64();
+            lds_flag_wait(&lk, k, lane, &fail, 4);
+            double* pk = pan + (k & 1) * kMfMaxNT * 256;
+            const double* lkk = linv + k * 256;
+            const int t_upd = Tc(k), s_upd = slot_lo(t_upd);  // update: s < s_upd
+            const int s_pan_end = slot_lo(t_upd + NT - k);     // panel: s_upd <= s < s_pan_end
+            // ---- panel: L_ik = A_ik L_kk^-T, i > k; forward b_i -= L_ik y_k for i > k + 1
+#pragma unroll
+            for (int s = 0; s < SL; ++s) {
+                if (s < s_upd) continue;
+                if (s >= s_pan_end) continue;
+                const int i = tij[s] & 255;
+                if (i > k) {
+                    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(lkk[q * 64 + lane], T[s][q], acc, 0, 0, 0);
+                    T[s] = acc;
+                    double part = 0.0;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        pk[i * 256 + q * 64 + lane] = acc[q];
+                        part = __builtin_fma(acc[q], yv[16 * k + g4 + 4 * q], part);
+                    }
+                    if (i > k + 1) {
+                        part += __shfl_xor(part, 16);
+                        part += __shfl_xor(part, 32);
+                        if (lane < 16) yv[16 * i + lane] -= part;
+                    }
+                }
+            }
+            // ---- tile-wave barrier (the diagonal wave does not take part)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) __hip_atomic_fetch_add(&tbar, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            lds_flag_wait(&tbar, W * (k + 1), lane, &fail, 5);
+            if (trace && lane == 0) trace[(k * 8 + w) * 4 + 1] = clock64();
+            // ---- trailing update with panel k.  The next step's pre tiles first: A = (k+2, k+1) is
+            // t = Tc(k+1) + 1, P = (k+2, k+2) is t = Tc(k+2); the diagonal wave takes (k+1, k+1) = Tc(k+1).
+            const int t_diag = Tc(k + 1);
+            const int t_pa = k + 2 < NT ? Tc(k + 1) + 1 : -1, t_pp = k + 2 < NT ? Tc(k + 2) : -1;
+            const int s_pre_end = k + 2 < NT ? slot_lo(t_pa + 1) : 0;
+#pragma unroll
+            for (int s = 0; s < SL; ++s) {
+                if (s >= s_pre_end) continue;
+                const int t = s * W + w;
+                if (t == t_pa || t == t_pp) {
+                    const int i = tij[s] & 255, j = tij[s] >> 8;
+                    const double* pi = pk + i * 256;
+                    const double* pj = pk + j * 256;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        T[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(pj[q * 64 + lane], pi[q * 64 + lane], T[s], 0, 0, 1);
+                    double* dst = pre + ((k + 1) & 1) * 512 + (t == t_pp ? 256 : 0);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) dst[q * 64 + lane] = T[s][q];
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    if (lane == 0) __hip_atomic_fetch_add(&pre_ready[k + 1], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < SL; ++s) {
+                if (s >= s_upd) continue;
+                const int t = s * W + w;
+                if (t != t_diag && t != t_pa && t != t_pp) {
+                    const int i = tij[s] & 255, j = tij[s] >> 8;
+                    const double* pi = pk + i * 256;
+                    const double* pj = pk + j * 256;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        T[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(pj[q * 64 + lane], pi[q * 64 + lane], T[s], 0, 0, 1);
+                }
+            }
+            if (trace && lane == 0) trace[(k * 8 + w) * 4 + 3] = clock64();
+        }
+        // every tile wave is past its last read of the panel buffers before contributions land there
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_fetch_add(&tbar, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        lds_flag_wait(&tbar, W * NT, lane, &fail, 6);
+        // ---- backward: row k's tiles (k, j <= k - 2) contribute L_kj^T x_k; tile (k, j) is
+        // t = Tc(j) + (k - j), so the wave finds its own by arithmetic and dispatches to the slot
+        auto contribute = [&](const f64x4& Tv, int k, int j, double xr) {
+            double* cs = contrib + (k * (k - 1) / 2 + j) * 16;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const double o = row16_sum(Tv[q] * xr);  // sum_r L_kj[r][c] x_k[r], c = g4 + 4q
+                if (r16 == 15) cs[g4 + 4 * q] = o;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) __hip_atomic_fetch_add(&cnt[j], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        };
+        for (int k = NT - 1; k >= 2; --k) {
+            bool waited = false;
+            double xr = 0.0;
+            for (int j = 0; j + 2 <= k; ++j) {
+                const int t = Tc(j) + (k - j);
+                if (t % W != w) continue;
+                if (!waited) {
+                    lds_flag_wait(&xready, NT - k, lane, &fail, 7);  // x_k published
+                    xr = xv[16 * k + r16];
+                    waited = true;
+                }
+                switch (t / W) {
+#define MF_SLOT(S)                                                                            \
+    case S:                                                                                   \
+        if constexpr (S < SL) {                                                               \
+            asm volatile("; slot " #S); /* distinct cases: keeps T in registers (no merging) */ \
+            contribute(T[S], k, j, xr);                                                       \
+        }                                                                                     \
+        break;
+                    MF_SLOT(0) MF_SLOT(1) MF_SLOT(2) MF_SLOT(3) MF_SLOT(4) MF_SLOT(5) MF_SLOT(6) MF_SLOT(7)
+                    MF_SLOT(8) MF_SLOT(9) MF_SLOT(10) MF_SLOT(11) MF_SLOT(12) MF_SLOT(13) MF_SLOT(14) MF_SLOT(15)
+                    MF_SLOT(16) MF_SLOT(17) MF_SLOT(18) MF_SLOT(19) MF_SLOT(20) MF_SLOT(21) MF_SLOT(22) MF_SLOT(23)
+                    MF_SLOT(24) MF_SLOT(25) MF_SLOT(26) MF_SLOT(27) MF_SLOT(28) MF_SLOT(29) MF_SLOT(30) MF_SLOT(31)
+#undef MF_SLOT
+                    default: break;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += (W + 1) * 64) x[i] = xv[i];
+    if (threadIdx.x == 0) *status = fail;
+}
+
 // Cooperative multi-workgroup Cholesky + solve (the fast path for n <= 560 / 1100).
 // Right-looking by block columns of NB: workgroup w < nbc keeps block column w (rows j0..n) in LDS
 // for the whole factorisation; workgroup nbc owns the right-hand side.  Step k: the owner of
@@ -2114,9 +2402,11 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     if (chol_lds > 150 * 1024 && !coop_nb && n > 16 * kMfMaxNT)
         return orbgpu_fail(ORB_ERR_ARG, "too many free keyframes for the on-chip Cholesky");
     const bool use_mf = !coop_nb && n <= 16 * kMfMaxNT && !getenv("ORBGPU_BA_CHOL_LDS");
+    const bool chol_v1 = getenv("ORBGPU_BA_CHOL_V1") != nullptr;
     static bool attr_set = false;
     if (!attr_set) {
         hipFuncSetAttribute((const void*)k_ba_chol_mfma<kMfTileWaves>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMfLds);
+        hipFuncSetAttribute((const void*)k_ba_chol_mf2<kMfTileWaves>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMf2Lds);
         hipFuncSetAttribute((const void*)k_ba_chol<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
         hipFuncSetAttribute((const void*)k_ba_chol<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
         (void)hipGetLastError();
@@ -2188,8 +2478,12 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                     hipMemsetAsync(h->trace.p, 0, 1024 * sizeof(int64_t), s);
                     tr = h->trace.p;
                 }
-                hipLaunchKernelGGL(k_ba_chol_mfma<kMfTileWaves>, dim3(1), dim3((kMfTileWaves + 1) * 64), kMfLds, s, n,
-                                   h->S.p, h->bs.p, h->x.p, h->status.p, tr, G, (int)kGateTrial);
+                if (chol_v1)
+                    hipLaunchKernelGGL(k_ba_chol_mfma<kMfTileWaves>, dim3(1), dim3((kMfTileWaves + 1) * 64), kMfLds, s,
+                                       n, h->S.p, h->bs.p, h->x.p, h->status.p, tr, G, (int)kGateTrial);
+                else
+                    hipLaunchKernelGGL(k_ba_chol_mf2<kMfTileWaves>, dim3(1), dim3((kMfTileWaves + 1) * 64), kMf2Lds, s,
+                                       n, h->S.p, h->bs.p, h->x.p, h->status.p, tr, G, (int)kGateTrial);
                 if (tr) {
                     trace_left = 0;
                     dump_chol_trace(tr, n, s);
@@ -2275,8 +2569,12 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                     hipMemsetAsync(h->trace.p, 0, 1024 * sizeof(int64_t), s);
                     tr = h->trace.p;
                 }
-                hipLaunchKernelGGL(k_ba_chol_mfma<kMfTileWaves>, dim3(1), dim3((kMfTileWaves + 1) * 64), kMfLds, s, n,
-                                   h->S.p, h->bs.p, h->x.p, h->status.p, tr, (const LmState*)L, (int)kGateTrial);
+                if (chol_v1)
+                    hipLaunchKernelGGL(k_ba_chol_mfma<kMfTileWaves>, dim3(1), dim3((kMfTileWaves + 1) * 64), kMfLds, s,
+                                       n, h->S.p, h->bs.p, h->x.p, h->status.p, tr, (const LmState*)L, (int)kGateTrial);
+                else
+                    hipLaunchKernelGGL(k_ba_chol_mf2<kMfTileWaves>, dim3(1), dim3((kMfTileWaves + 1) * 64), kMf2Lds, s,
+                                       n, h->S.p, h->bs.p, h->x.p, h->status.p, tr, (const LmState*)L, (int)kGateTrial);
                 if (tr) {
                     trace_left_u = 0;
                     dump_chol_trace(tr, n, s);
