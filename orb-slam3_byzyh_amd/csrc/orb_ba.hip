@@ -753,6 +753,9 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
 // L[j][c] (j > c) are broadcast once (v_readlane) and feed both the rank-1 update of the block and
 // the substitution step of L^-1 (x_i -= L[i][c] x_c).  The updates run unconditionally: entries
 // above the diagonal collect garbage that is never read.
+// kColMajor: L^-1 stored column-major with stride 17 (L^-1[i][c] at c * 17 + i: conflict-free for the
+// writes here and for every reader); otherwise in the MFMA operand layout.
+template <bool kColMajor = false>
 __device__ __forceinline__ void mf_diag(double* __restrict__ dk, double* __restrict__ linv_k,
                                         double* __restrict__ yk, int lane, int* fail, int64_t* tr = nullptr) {
     if (tr && lane == 0) tr[0] = clock64();
@@ -782,7 +785,8 @@ __device__ __forceinline__ void mf_diag(double* __restrict__ dk, double* __restr
     if (tr && lane == 0) tr[1] = clock64();
     if (lane < 16) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) linv_k[(r >> 2) * 64 + i + 16 * (r & 3)] = xc[i];  // L^-1[i][r], O layout
+        for (int i = 0; i < 16; ++i)  // L^-1[i][r]
+            linv_k[kColMajor ? r * 17 + i : (r >> 2) * 64 + i + 16 * (r & 3)] = xc[i];
     }
     mf_wave_sync();
     if (tr && lane == 0) tr[2] = clock64();
@@ -790,7 +794,8 @@ __device__ __forceinline__ void mf_diag(double* __restrict__ dk, double* __restr
     double y4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int cc = 0; cc < 16; ++cc)
-        y4[cc & 3] = __builtin_fma(linv_k[(cc >> 2) * 64 + r + 16 * (cc & 3)], yk[cc], y4[cc & 3]);
+        y4[cc & 3] = __builtin_fma(linv_k[kColMajor ? cc * 17 + r : (cc >> 2) * 64 + r + 16 * (cc & 3)], yk[cc],
+                                   y4[cc & 3]);
     const double y = (y4[0] + y4[1]) + (y4[2] + y4[3]);
     mf_wave_sync();
     if (lane < 16) yk[r] = y;
@@ -1012,8 +1017,8 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mfma(int n, const doub
 // Backward: the diagonal wave keeps every L_{k+1,k} (sub-diagonal tile) in LDS, so the chain
 // x_{k+1} -> x_k never leaves it; the tile waves add the other rows' L_kj^T x_k contributions into
 // per-tile slots (the panel buffers, free by then), summed in a fixed order.
-constexpr size_t kMf2Lds = sizeof(double) * ((2 + 1) * (size_t)kMfMaxNT * 256 + (kMfMaxNT - 1) * 256 + 4 * 256 +
-                                             16 * 17 + 2 * 16 * kMfMaxNT);
+constexpr size_t kMf2Lds = sizeof(double) * (2 * (size_t)kMfMaxNT * 256 + (size_t)kMfMaxNT * 272 +
+                                             (kMfMaxNT - 1) * 256 + 4 * 256 + 16 * 17 + 2 * 16 * kMfMaxNT);
 
 __device__ __forceinline__ void lds_flag_wait(int* f, int target, int lane, int* fail, int code) {
     for (int spin = 0; __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target; ++spin) {
@@ -1036,8 +1041,8 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
     extern __shared__ double lds[];
     double* pan = lds;                        // [2][NT][256] panel tiles O(L_ik), by step parity
     double* contrib = lds;                    // backward: [k (k - 1) / 2 + j][16] (aliases pan)
-    double* linv = pan + 2 * kMfMaxNT * 256;  // [NT][256] O(L_kk^-1)
-    double* sub = linv + kMfMaxNT * 256;      // [NT - 1][256] O(L_{k+1,k})
+    double* linv = pan + 2 * kMfMaxNT * 256;  // [NT][272] L_kk^-1 column-major, stride 17
+    double* sub = linv + kMfMaxNT * 272;      // [NT - 1][256] O(L_{k+1,k})
     double* pre = sub + (kMfMaxNT - 1) * 256;  // [2][2][256] A_{k+1,k}, P_{k+1,k+1} by step parity
     double* dk = pre + 4 * 256;               // [16][17]
     double* yv = dk + 16 * 17;                // [16 NT]
@@ -1066,7 +1071,7 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
             dk[r * 17 + c] = (r < n && c < n) ? S[(size_t)r * n + c] : (r == c ? 1.0 : 0.0);
         }
         mf_wave_sync();
-        mf_diag(dk, linv, yv, lane, &fail);
+        mf_diag<true>(dk, linv, yv, lane, &fail);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) __hip_atomic_store(&lk, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         for (int k = 0; k + 1 < NT; ++k) {
@@ -1075,10 +1080,11 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
             if (trace && lane == 0) trace[(k * 8 + W) * 4 + 2] = clock64();
             const double* A = pre + (k & 1) * 512;
             const double* P = A + 256;
-            const double* lkk = linv + k * 256;
+            const double* lkk = linv + k * 272;
             f64x4 L = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int q = 0; q < 4; ++q) L = __builtin_amdgcn_mfma_f64_16x16x4f64(lkk[q * 64 + lane], A[q * 64 + lane], L, 0, 0, 0);
+            for (int q = 0; q < 4; ++q)  // A operand O(L^-1): L^-1[r16][g4 + 4q]
+                L = __builtin_amdgcn_mfma_f64_16x16x4f64(lkk[(g4 + 4 * q) * 17 + r16], A[q * 64 + lane], L, 0, 0, 0);
             f64x4 Pm = {P[lane], P[64 + lane], P[128 + lane], P[192 + lane]};
 #pragma unroll
             for (int q = 0; q < 4; ++q) Pm = __builtin_amdgcn_mfma_f64_16x16x4f64(L[q], L[q], Pm, 0, 0, 1);
@@ -1093,7 +1099,7 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
             part += __shfl_xor(part, 32);
             if (lane < 16) yv[16 * (k + 1) + lane] -= part;  // b_{k+1} -= L_{k+1,k} y_k
             mf_wave_sync();
-            mf_diag(dk, linv + (k + 1) * 256, yv + 16 * (k + 1), lane, &fail, trace ? trace + 700 + 4 * k : nullptr);
+            mf_diag<true>(dk, linv + (k + 1) * 272, yv + 16 * (k + 1), lane, &fail, trace ? trace + 700 + 4 * k : nullptr);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_store(&lk, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (trace && lane == 0) trace[(k * 8 + W) * 4 + 3] = clock64();
@@ -1115,11 +1121,10 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
             mf_wave_sync();
             if (lane < 16) yv[16 * j + r16] = yj;
             mf_wave_sync();
-            const double* lj = linv + j * 256;
+            const double* lj = linv + j * 272;
             double v4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int rr = 0; rr < 16; ++rr)
-                v4[rr & 3] = __builtin_fma(lj[(r16 >> 2) * 64 + rr + 16 * (r16 & 3)], yv[16 * j + rr], v4[rr & 3]);
+            for (int rr = 0; rr < 16; ++rr) v4[rr & 3] = __builtin_fma(lj[r16 * 17 + rr], yv[16 * j + rr], v4[rr & 3]);
             if (lane < 16) xv[16 * j + r16] = (v4[0] + v4[1]) + (v4[2] + v4[3]);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_store(&xready, NT - j, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1167,7 +1172,7 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
             if (trace && lane == 0) trace[(k * 8 + w) * 4] = clock64();
             lds_flag_wait(&lk, k, lane, &fail, 4);
             double* pk = pan + (k & 1) * kMfMaxNT * 256;
-            const double* lkk = linv + k * 256;
+            const double* lkk = linv + k * 272;
             const int t_upd = Tc(k), s_upd = slot_lo(t_upd);  // update: s < s_upd
             const int s_pan_end = slot_lo(t_upd + NT - k);     // panel: s_upd <= s < s_pan_end
             // ---- panel: L_ik = A_ik L_kk^-T, i > k; forward b_i -= L_ik y_k for i > k + 1
@@ -1180,7 +1185,7 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
                     f64x4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
                     for (int q = 0; q < 4; ++q)
-                        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(lkk[q * 64 + lane], T[s][q], acc, 0, 0, 0);
+                        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(lkk[(g4 + 4 * q) * 17 + r16], T[s][q], acc, 0, 0, 0);
                     T[s] = acc;
                     double part = 0.0;
 #pragma unroll
