@@ -285,6 +285,336 @@ __global__ __launch_bounds__(256) void k_pyramid_level(const KernelGeom* __restr
 }
 
 // ================================================================================================
+// 1b. whole pyramid in one launch: one workgroup per (frame, horizontal band)
+// ================================================================================================
+// The per-level launches above are latency-bound (a level's tiles cannot start before the previous
+// level exists, and the small levels cannot fill the chip).  Here one 1024-thread workgroup owns a
+// horizontal band of one frame and walks all levels itself: it computes, level by level, every view
+// row its band needs -- its own rows, +-3 rows for the blur, and the source rows of the next
+// level's computed rows -- so it never waits for another workgroup.  Rows computed by two bands
+// (the margins) are written twice with identical bytes.  Per chunk of R rows (a "task"):
+//   P1  resize (level 0: copy) the staged source rows S -> padded rows V (REFLECT_101 columns);
+//       vertical blur of the rows the previous task completed (hsum ring H -> blurred plane)
+//   P2  padded rows V -> pyramid plane (+ the reflected border rows); horizontal blur V -> H;
+//       store the next task's source rows, prefetched into registers during P1, into S
+// Two workgroup barriers per task; the next task's global loads overlap this task's P1.
+struct BandTask {
+    int level, late;  // late: sources written by the previous task, staged after its barrier
+    int a, b;         // view rows [a, b) of `level`
+    int s_lo, s_n;    // staged source rows: previous level view rows (level 0: input rows)
+    int e0, e1;       // blurred view rows completed by this task (emitted during the next P1)
+};
+static_assert(sizeof(BandTask) == 32, "BandTask layout");
+
+constexpr int kBandThreads = 1024;
+constexpr int kBandGranules = 3;  // 16-byte source granules per thread per task
+
+struct BandArgs {  // scalars only: the pointers are __restrict__ kernel parameters (scalar loads)
+    int max_tasks;
+    long long in_frame_stride;
+    int in_stride, in_vec;  // in_vec: 16-byte aligned input rows with width % 16 == 0
+    int xt_total;            // INTER_LINEAR column entries of levels >= 1 (all staged in LDS)
+    int R, ring, s_rows, sp, vp, hp;  // LDS geometry (bytes; hp in uint16)
+};
+
+__device__ __forceinline__ int blur_hsum_end(int w) { return (w + kEdge + 7) & ~7; }  // padded cols [16, end)
+
+// Row entry of cv::resize INTER_LINEAR (source rows r0, r1 and 11-bit weights b0, b1) for
+// destination row dy of dh rows from sh: the same operations as the host table (resize_tables in
+// orb_extract_geom.h), IEEE double / float with no contraction, so the result is bit-identical.
+__device__ __forceinline__ int4 resize_row_coef(int dy, int dh, int sh) {
+    const double scale_y = 1. / ((double)dh / sh);
+    float fy = (float)((dy + 0.5) * scale_y - 0.5);
+    int sy = (int)fy;
+    sy -= (sy > fy);
+    fy -= sy;
+    const int b0 = min(max((int)__builtin_rintf((1.f - fy) * 2048), -32768), 32767);
+    const int b1 = min(max((int)__builtin_rintf(fy * 2048), -32768), 32767);
+    return make_int4(min(max(sy, 0), sh - 1), min(max(sy + 1, 0), sh - 1), b0, b1);
+}
+
+// kOcc = waves per SIMD the register budget must allow: 4 (one workgroup per CU) or 8 (two)
+template <int kOcc>
+__global__ __launch_bounds__(kBandThreads, kOcc) void k_pyramid_band(
+    const KernelGeom* __restrict__ gp, const BandTask* __restrict__ tasks, const int* __restrict__ ntasks,
+    const uint8_t* __restrict__ in, uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+    const int2* __restrict__ xtab, const int4* __restrict__ ytab, unsigned long long* __restrict__ stamps,
+    BandArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const KernelGeom& g = *gp;
+    const int tid = threadIdx.x, band = blockIdx.x, f = blockIdx.y;
+    uint8_t* S = lds;
+    uint8_t* V = S + A.s_rows * A.sp;
+    uint16_t* H = reinterpret_cast<uint16_t*>(V + A.R * A.vp);
+    int2* X = reinterpret_cast<int2*>(H + A.ring * A.hp);
+    const int ring_mask = A.ring - 1;                    // ring: power of two
+    const int nt = ntasks[band];
+    const BandTask* T = tasks + (size_t)band * A.max_tasks;
+    uint8_t* const pyr_f = pyr + (size_t)f * g.pyr_frame_bytes;
+    uint8_t* const blur_f = blur + (size_t)f * g.pyr_frame_bytes;
+    const uint8_t* const in_f = in + (size_t)f * A.in_frame_stride;
+    for (int i = tid; i < A.xt_total; i += kBandThreads) X[i] = xtab[i];
+
+    // rows x ncols items: each thread keeps one column and strides over rows (ncols <= 1024; one
+    // integer division per phase instead of one per item)
+#define BAND_FOR(ncols, rows, r, c)                                                   \
+    for (int c = tid % (ncols), r = tid / (ncols), _step = kBandThreads / (ncols);    \
+         r < (rows) && tid < _step * (ncols); r += _step)
+
+    // 16-byte granules of a task's source rows: level 0 from the input, else the previous level's
+    // padded plane from column 16 (view column c lands at S column c + 3)
+    auto granules = [&](const BandTask& t, int& gpr) {
+        gpr = t.level == 0 ? g.lv[0].w >> 4 : (g.lv[t.level - 1].w + 4 + 15) >> 4;
+        return t.s_n * gpr;
+    };
+    auto gsrc = [&](const BandTask& t, int r) -> const uint8_t* {
+        if (t.level == 0) return in_f + (size_t)(t.s_lo + r) * A.in_stride;
+        const LevelGeom& P = g.lv[t.level - 1];
+        return pyr_f + P.plane_off + (size_t)(t.s_lo + r + kEdge) * P.pitch + 16;
+    };
+    static_assert(kBandGranules == 3, "staging registers below");
+    struct Staged { uint4 r0, r1, r2; };  // the next task's source granules
+    auto issue = [&](const BandTask& t, Staged& q) {
+        int gpr;
+        const int n = granules(t, gpr);
+        // unconditional loads (granule index clamped into the task) so that the loads stay in
+        // flight together; commit() stores only the valid ones
+        auto ld = [&](int gi) {
+            gi = min(gi, n - 1);
+            const int r = gi / gpr, j = gi - r * gpr;
+            return *reinterpret_cast<const uint4*>(gsrc(t, r) + 16 * j);
+        };
+        q.r0 = ld(tid);
+        q.r1 = ld(tid + kBandThreads);
+        q.r2 = ld(tid + 2 * kBandThreads);
+    };
+    auto commit = [&](const BandTask& t, const Staged& q, bool keep) {
+        // consume the registers on every path, so that the wait for them sits here and nowhere
+        // else (a wait at the next issue() would also drain every store issued since)
+        if ((q.r0.x ^ q.r1.y ^ q.r2.z) == 0x9e3779b9u && A.in_stride < 0) S[0] = 0;
+        if (!keep) return;
+        int gpr;
+        const int n = granules(t, gpr);
+        auto st = [&](int gi, const uint4& v) {
+            const int r = gi / gpr, j = gi - r * gpr;
+            *reinterpret_cast<uint4*>(S + r * A.sp + 16 * j) = v;
+        };
+        if (tid < n) st(tid, q.r0);
+        if (tid + kBandThreads < n) st(tid + kBandThreads, q.r1);
+        if (tid + 2 * kBandThreads < n) st(tid + 2 * kBandThreads, q.r2);
+    };
+    auto stage_now = [&](const BandTask& t) {
+        if (t.level == 0 && !A.in_vec) {  // unaligned input: byte loads
+            const int w = g.lv[0].w;
+            for (int i = tid; i < t.s_n * w; i += kBandThreads) {
+                const int r = i / w, x = i - r * w;
+                S[r * A.sp + x] = gsrc(t, r)[x];
+            }
+        } else {
+            Staged q;
+            issue(t, q);
+            commit(t, q, true);
+        }
+    };
+    auto is_late = [&](const BandTask& t) { return t.late || (t.level == 0 && !A.in_vec); };
+
+    // P1 (level >= 1): INTER_LINEAR rows [a, b) in padded columns, 4 pixels per item
+    auto resize_rows = [&](const BandTask& t) {
+        const LevelGeom& L = g.lv[t.level];
+        const LevelGeom& P = g.lv[t.level - 1];
+        const int ngr = (L.pw + 3) >> 2;
+        const int2* XL = X + (L.xtab_off - g.lv[1].xtab_off);
+        BAND_FOR(ngr, t.b - t.a, r, gq) {
+            const int px0 = gq * 4;
+            const int4 Y = resize_row_coef(t.a + r, L.h, P.h);
+            const uint8_t* R0 = S + (Y.x - t.s_lo) * A.sp;
+            const uint8_t* R1 = S + (Y.y - t.s_lo) * A.sp;
+            int vx[4];
+            int2 Xk[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                vx[k] = reflect101(min(px0 + k, L.pw - 1) - kEdge, L.w);
+                Xk[k] = XL[vx[k]];
+            }
+            int p0[4], p0n[4], p1[4], p1n[4];
+            if (px0 >= kEdge && px0 + 3 <= L.w + kEdge - 1 && Xk[3].x + 1 - Xk[0].x <= 7) {
+                const unsigned long long q0 = lds_bytes8(R0, Xk[0].x + 3), q1 = lds_bytes8(R1, Xk[0].x + 3);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int d = 8 * (Xk[k].x - Xk[0].x);
+                    p0[k] = (int)((q0 >> d) & 0xff); p0n[k] = (int)((q0 >> (d + 8)) & 0xff);
+                    p1[k] = (int)((q1 >> d) & 0xff); p1n[k] = (int)((q1 >> (d + 8)) & 0xff);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int s = Xk[k].x + 3;
+                    p0[k] = R0[s]; p0n[k] = R0[s + 1]; p1[k] = R1[s]; p1n[k] = R1[s + 1];
+                }
+            }
+            uint32_t packed = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int a0 = Xk[k].y & 0xffff, a1 = Xk[k].y >> 16;
+                const int h0 = p0[k] * a0 + p0n[k] * a1, h1 = p1[k] * a0 + p1n[k] * a1;
+                int v;
+                if (vx[k] < L.simd_end) {  // VResizeLinearVec_32s8u (see k_pyramid_level)
+                    const int t0 = min(h0 >> 4, 32767), t1 = min(h1 >> 4, 32767);
+                    v = (((t0 * Y.z) >> 16) + ((t1 * Y.w) >> 16) + 2) >> 2;
+                } else {
+                    v = (h0 * Y.z + h1 * Y.w + (1 << 21)) >> 22;
+                }
+                packed |= (uint32_t)min(max(v, 0), 255) << (8 * k);
+            }
+            *reinterpret_cast<uint32_t*>(V + r * A.vp + px0) = packed;
+        }
+    };
+    // P1 (level 0): padded rows straight from the staged input rows
+    auto copy_rows = [&](const BandTask& t) {
+        const LevelGeom& L = g.lv[0];
+        const int ngr = (L.pw + 3) >> 2;
+        BAND_FOR(ngr, t.b - t.a, r, gq) {
+            const int px0 = gq * 4;
+            const uint8_t* row = S + r * A.sp;
+            uint32_t packed;
+            if (px0 >= kEdge && px0 + 3 <= L.w + kEdge - 1) {
+                packed = (uint32_t)lds_bytes8(row, px0 - kEdge);
+            } else {
+                packed = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    packed |= (uint32_t)row[reflect101(min(px0 + k, L.pw - 1) - kEdge, L.w)] << (8 * k);
+            }
+            *reinterpret_cast<uint32_t*>(V + r * A.vp + px0) = packed;
+        }
+    };
+    // P2: padded rows to the plane (+ REFLECT_101 border rows 19 - y and 2h + 17 - y)
+    auto write_rows = [&](const BandTask& t) {
+        const LevelGeom& L = g.lv[t.level];
+        uint8_t* plane = pyr_f + L.plane_off;
+        const int n8 = (L.pw + 7) >> 3;
+        BAND_FOR(n8, t.b - t.a, r, c8) {
+            const int px = c8 * 8, y = t.a + r;
+            const unsigned long long v = *reinterpret_cast<const unsigned long long*>(V + r * A.vp + px);
+            const int top = (y >= 1 && y <= kEdge) ? kEdge - y : -1;
+            const int bot = (y >= L.h - kEdge - 1 && y <= L.h - 2) ? 2 * L.h + kEdge - 2 - y : -1;
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                const int row = d == 0 ? y + kEdge : d == 1 ? top : bot;
+                if (row < 0) continue;
+                uint8_t* o = plane + (size_t)row * L.pitch + px;
+                if (px + 8 <= L.pw) {
+                    *reinterpret_cast<unsigned long long*>(o) = v;
+                } else {
+                    for (int k = 0; k < 8 && px + k < L.pw; ++k) o[k] = (uint8_t)(v >> (8 * k));
+                }
+            }
+        }
+    };
+    // P2: horizontal 7-tap pass of rows [a, b) into the hsum ring (padded columns [16, end))
+    auto hblur_rows = [&](const BandTask& t) {
+        const LevelGeom& L = g.lv[t.level];
+        const int n4 = (blur_hsum_end(L.w) - 16) >> 2;
+        BAND_FOR(n4, t.b - t.a, r, c4) {
+            const int px = 16 + c4 * 4;
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(V + r * A.vp) + (px >> 2) - 1;
+            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+            int pv[12];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                pv[k] = (w0 >> (8 * k)) & 0xff;
+                pv[4 + k] = (w1 >> (8 * k)) & 0xff;
+                pv[8 + k] = (w2 >> (8 * k)) & 0xff;
+            }
+            unsigned long long out = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                int acc = 0;
+#pragma unroll
+                for (int k = 0; k < 7; ++k) acc += blur_tap(k) * pv[1 + q + k];
+                out |= (unsigned long long)acc << (16 * q);
+            }
+            *reinterpret_cast<unsigned long long*>(H + ((t.a + r) & ring_mask) * A.hp + px) = out;
+        }
+    };
+    // P1 of the next task: vertical 7-tap pass of the completed rows [e0, e1) -> blurred plane
+    auto vblur_rows = [&](const BandTask& t) {
+        if (t.e1 <= t.e0) return;
+        const LevelGeom& L = g.lv[t.level];
+        uint8_t* plane = blur_f + L.plane_off;
+        const int xe = L.w + kEdge, n8 = (blur_hsum_end(L.w) - 16) >> 3;
+        BAND_FOR(n8, t.e1 - t.e0, r, c8) {
+            const int px = 16 + c8 * 8, y = t.e0 + r;
+            int acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+            for (int k = 0; k < 7; ++k) {
+                const int yy = reflect101(y - 3 + k, L.h);
+                const uint4 q = *reinterpret_cast<const uint4*>(H + (yy & ring_mask) * A.hp + px);
+                const uint32_t qq[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc[2 * j] += blur_tap(k) * (int)(qq[j] & 0xffff);
+                    acc[2 * j + 1] += blur_tap(k) * (int)(qq[j] >> 16);
+                }
+            }
+            unsigned long long w = 0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) w |= (unsigned long long)min((acc[q] + (1 << 15)) >> 16, 255) << (8 * q);
+            uint8_t* o = plane + (size_t)(y + kEdge) * L.pitch + px;
+            if (px >= kEdge && px + 8 <= xe) {
+                *reinterpret_cast<unsigned long long*>(o) = w;
+            } else {
+                for (int q = 0; q < 8; ++q)
+                    if (px + q >= kEdge && px + q < xe) o[q] = (uint8_t)(w >> (8 * q));
+            }
+        }
+    };
+#undef BAND_FOR
+
+    BandTask prev;
+    prev.e0 = prev.e1 = 0;
+    prev.level = 0;
+    // debug trace (ORBGPU_BAND_TRACE): wall clock of band 0 / frame 0 at each phase boundary
+    const bool trace = stamps && band == 0 && f == 0 && tid == 0;
+    constexpr int kTr = 10;
+#define BAND_STAMP(k) \
+    if (trace) stamps[kTr * i + (k)] = wall_clock64()
+    for (int i = 0; i < nt; ++i) {
+        const BandTask t = T[i];
+        BAND_STAMP(0);
+        if (i == 0 || is_late(t)) {
+            stage_now(t);
+            __syncthreads();
+        }
+        BAND_STAMP(1);
+        // order: stores of the previous blur rows, then the next task's loads, then the resize;
+        // after the barrier the commit waits for those loads (and the older stores) only
+        const BandTask tn = T[min(i + 1, nt - 1)];
+        const bool pre = i + 1 < nt && !is_late(tn);
+        vblur_rows(prev);
+        BAND_STAMP(2);
+        Staged q;
+        issue(pre ? tn : t, q);  // without a prefetch: a harmless reload, so the wait stays unconditional
+        BAND_STAMP(3);
+        if (t.level == 0) copy_rows(t); else resize_rows(t);
+        BAND_STAMP(4);
+        __syncthreads();
+        BAND_STAMP(5);
+        commit(tn, q, pre);
+        BAND_STAMP(6);
+        write_rows(t);
+        BAND_STAMP(7);
+        hblur_rows(t);
+        BAND_STAMP(8);
+        __syncthreads();
+        BAND_STAMP(9);
+        prev = t;
+    }
+#undef BAND_STAMP
+    vblur_rows(prev);
+}
+
+// ================================================================================================
 // 2. FAST cells: src:1098-1166 (cell loop) + OpenCV FAST_t<16>/cornerScore<16> semantics
 // ================================================================================================
 // score(p) = max over the 16 9-pixel arcs and both polarities of the arc minimum of |I(p)-I(q)|,
@@ -1399,6 +1729,20 @@ struct Extractor {
     long long frames_profiled = 0;
     unsigned long long* d_stamps = nullptr;  // quad-tree phase timers (ORBGPU_DEBUG_FLAGS & 4)
     size_t stamps_cap = 0;
+    // whole-pyramid band kernel (k_pyramid_band): plan for the current geometry and band count
+    // off by default: measured slower than the per-level launches (DESIGN.md sec. 4, round 1:
+    // 0.694 ms/step all levels, 0.626 ms from level 3, against 0.610 ms)
+    int band_mode = 0;         // ORBGPU_PYR_BAND=1 enables it
+    int band_wg_per_cu = 1;    // target workgroups per CU (ORBGPU_PYR_WG_PER_CU)
+    int band_from = 0;         // first level built by the band kernel (ORBGPU_PYR_BAND_FROM); earlier: per-level
+    int band_r = 16;           // rows per task (ORBGPU_PYR_BAND_R)
+    int num_cus = 0;
+    int plan_nb = -1;          // band count the device plan was built for (-1: none)
+    bool plan_ok = false;
+    int plan_max_tasks = 0, plan_R = 0, plan_ring = 0, plan_s_rows = 0, plan_sp = 0, plan_vp = 0, plan_hp = 0;
+    size_t plan_lds = 0;
+    BandTask* d_tasks = nullptr; size_t tasks_cap = 0;
+    int* d_ntasks = nullptr; size_t ntasks_cap = 0;
 };
 
 }  // namespace orbgpu
@@ -1428,6 +1772,8 @@ int prepare(Extractor* e, int w, int h, int n) {
         e->geo = g;
         e->cur_w = w;
         e->cur_h = h;
+        e->plan_nb = -1;
+        e->plan_ok = false;
         int rc;
         if ((rc = grow(e->d_cells, e->cells_cap, g.cells.size())) != ORB_OK) return rc;
         if ((rc = grow(e->d_xtab, e->xtab_cap, std::max<size_t>(1, g.xtab.size() / 2))) != ORB_OK) return rc;
@@ -1464,6 +1810,140 @@ int prepare(Extractor* e, int w, int h, int n) {
     if ((rc = grow(e->d_lap_count, e->lapcount_cap, (size_t)k.nlevels * n)) != ORB_OK) return rc;
     if ((k.debug_flags & 4) && (rc = grow(e->d_stamps, e->stamps_cap, (size_t)k.nlevels * n * kQtStamps)) != ORB_OK) return rc;
     return ORB_OK;
+}
+
+// Band plan of k_pyramid_band for nb bands (host, once per geometry and band count).  Own rows
+// of band b at level l: [b*h/nb, (b+1)*h/nb).  Computed rows C_l, from the top level down: own rows
+// +-3 (blur), and the source rows of C_{l+1}.  Tasks are chunks of R rows of C_l, level by level.
+// Returns false when the plan does not fit (LDS, staging registers, hsum ring): per-level path.
+bool build_band_plan(const orbgpu::Geometry& G, int nb, int R, int ring, int lfirst, std::vector<BandTask>& tasks,
+                     std::vector<int>& counts, int& max_tasks, int& s_rows) {
+    const orbgpu::KernelGeom& k = G.k;
+    const int L = k.nlevels;
+    std::vector<std::vector<BandTask>> per(nb);
+    s_rows = R;
+    auto yt = [&](int l, int y) { return &G.ytab[4 * ((size_t)k.lv[l].ytab_off + y)]; };
+    for (int b = 0; b < nb; ++b) {
+        std::vector<int> c0(L), c1(L), o0(L), o1(L);
+        for (int l = L - 1; l >= lfirst; --l) {
+            const int h = k.lv[l].h;
+            o0[l] = (int)((long long)b * h / nb);
+            o1[l] = (int)((long long)(b + 1) * h / nb);
+            int lo = std::max(o0[l] - 3, 0), hi = std::min(o1[l] + 3, h);
+            if (l + 1 < L && c1[l + 1] > c0[l + 1]) {
+                lo = std::min(lo, yt(l + 1, c0[l + 1])[0]);
+                hi = std::max(hi, yt(l + 1, c1[l + 1] - 1)[1] + 1);
+            }
+            c0[l] = lo;
+            c1[l] = hi;
+        }
+        std::vector<BandTask>& T = per[b];
+        std::vector<int> first(L, 0);
+        for (int l = lfirst; l < L; ++l) {
+            const int h = k.lv[l].h;
+            first[l] = (int)T.size();
+            int e_next = o0[l];
+            for (int a = c0[l]; a < c1[l]; a += R) {
+                BandTask t{};
+                t.level = l;
+                t.a = a;
+                t.b = std::min(a + R, c1[l]);
+                if (l == 0) {
+                    t.s_lo = t.a;
+                    t.s_n = t.b - t.a;
+                } else {
+                    t.s_lo = yt(l, t.a)[0];
+                    t.s_n = yt(l, t.b - 1)[1] - t.s_lo + 1;
+                    // producer of the last source row (level l-1 chunks are consecutive from first[l-1]);
+                    // level lfirst reads a level written by an earlier launch
+                    if (l > lfirst) {
+                        const int p = first[l - 1] + (yt(l, t.b - 1)[1] - c0[l - 1]) / R;
+                        t.late = p >= (int)T.size() - 1;
+                        if (yt(l, t.a)[0] < c0[l - 1] || yt(l, t.b - 1)[1] >= c1[l - 1]) return false;
+                    }
+                }
+                s_rows = std::max(s_rows, t.s_n);
+                t.e0 = e_next;
+                t.e1 = std::max(e_next, std::min(o1[l], t.b == h ? h : t.b - 3));
+                // every hsum row the emitted rows read must still be in the ring
+                for (int y = t.e0; y < t.e1; ++y)
+                    for (int d = -3; d <= 3; ++d) {
+                        int yy = y + d;
+                        yy = yy < 0 ? -yy : yy >= h ? 2 * h - 2 - yy : yy;
+                        if (yy >= t.b || yy < t.b - ring || yy < c0[l]) return false;
+                    }
+                e_next = t.e1;
+                T.push_back(t);
+            }
+            if (e_next != o1[l]) return false;
+        }
+    }
+    max_tasks = 0;
+    for (auto& T : per) max_tasks = std::max(max_tasks, (int)T.size());
+    tasks.assign((size_t)nb * max_tasks, BandTask{});
+    counts.assign(nb, 0);
+    for (int b = 0; b < nb; ++b) {
+        counts[b] = (int)per[b].size();
+        std::copy(per[b].begin(), per[b].end(), tasks.begin() + (size_t)b * max_tasks);
+    }
+    return true;
+}
+
+// Prepare (or reuse) the band plan for a batch of n frames; false: use the per-level launches.
+bool ensure_band_plan(Extractor* e, int n) {
+    if (!e->band_mode) return false;
+    const orbgpu::Geometry& G = e->geo;
+    const orbgpu::KernelGeom& k = G.k;
+    if (e->num_cus <= 0) {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        e->num_cus = std::max(1, cus);
+    }
+    const int lfirst = std::min(std::max(e->band_from, 0), k.nlevels - 1);
+    const int max_nb = std::max(1, k.lv[k.nlevels - 1].h / 8);
+    const int nb = std::min(max_nb, std::max(1, (e->num_cus * e->band_wg_per_cu + n - 1) / n));
+    if (nb == e->plan_nb) return e->plan_ok;
+    if (e->plan_nb >= 0 && hipDeviceSynchronize() != hipSuccess) return false;  // old plan may be in flight
+    e->plan_nb = nb;
+    e->plan_ok = false;
+    // widest level the kernel touches: the source of level lfirst (or lfirst itself for level 0)
+    const int w0 = k.lv[lfirst > 0 ? lfirst - 1 : 0].w, pw0 = k.lv[lfirst].pw;
+    const int sp = (w0 + 16 + 15) & ~15, vp = (pw0 + 8 + 15) & ~15, hp = (k.lv[lfirst].w + 34 + 7) & ~7;
+    const size_t xt = G.xtab.size() / 2;
+    if ((pw0 + 3) / 4 > kBandThreads) return false;
+    for (int R = e->band_r; R >= 4; R /= 2) {
+        int ring = 1;
+        while (ring < R + 8) ring *= 2;
+        std::vector<BandTask> tasks;
+        std::vector<int> counts;
+        int max_tasks = 0, s_rows = 0;
+        if (!build_band_plan(G, nb, R, ring, lfirst, tasks, counts, max_tasks, s_rows)) continue;
+        const size_t lds = (size_t)s_rows * sp + (size_t)R * vp + (size_t)ring * hp * 2 + xt * 8;
+        if (lds > 160 * 1024) continue;
+        // staged source granules per task must fit kBandGranules per thread
+        const int gmax = std::max(s_rows * ((w0 + 4 + 15) >> 4), R * (k.lv[0].w >> 4));
+        if (gmax > kBandGranules * kBandThreads) continue;
+        if (grow(e->d_tasks, e->tasks_cap, tasks.size()) != ORB_OK || grow(e->d_ntasks, e->ntasks_cap, counts.size()) != ORB_OK)
+            return false;
+        if (hipMemcpy(e->d_tasks, tasks.data(), tasks.size() * sizeof(BandTask), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(e->d_ntasks, counts.data(), counts.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
+            return false;
+        if (hipFuncSetAttribute((const void*)k_pyramid_band<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess ||
+            hipFuncSetAttribute((const void*)k_pyramid_band<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return false;
+        e->plan_max_tasks = max_tasks;
+        e->plan_R = R;
+        e->plan_ring = ring;
+        e->plan_s_rows = s_rows;
+        e->plan_sp = sp;
+        e->plan_vp = vp;
+        e->plan_hp = hp;
+        e->plan_lds = lds;
+        e->plan_ok = true;
+        return true;
+    }
+    return false;
 }
 
 // Enqueue the five stages for frames [f0, f0 + n) of the handle's buffers on stream st.
@@ -1519,7 +1999,50 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
                                e->d_stamps ? e->d_stamps + (size_t)f0 * k.nlevels * kQtStamps : nullptr, lap0, lap1, dst,
                                lapc, l0);
     };
-    for (int l = 0; l < k.nlevels; ++l) {
+    // levels [0, lfirst): per-level launches; [lfirst, L): one band launch (k_pyramid_band)
+    const bool band = ensure_band_plan(e, n);
+    const int lfirst = band ? std::min(std::max(e->band_from, 0), k.nlevels - 1) : k.nlevels;
+    auto launch_band = [&]() {
+        BandArgs A;
+        A.max_tasks = e->plan_max_tasks;
+        A.in_frame_stride = (long long)frame_stride;
+        A.in_stride = stride;
+        A.in_vec = ((uintptr_t)imgs % 16 == 0 && stride % 16 == 0 && frame_stride % 16 == 0 && k.lv[0].w % 16 == 0) ? 1 : 0;
+        A.xt_total = (int)(G.xtab.size() / 2);
+        A.R = e->plan_R;
+        A.ring = e->plan_ring;
+        A.s_rows = e->plan_s_rows;
+        A.sp = e->plan_sp;
+        A.vp = e->plan_vp;
+        A.hp = e->plan_hp;
+        static const bool trace = getenv("ORBGPU_BAND_TRACE") != nullptr;
+        unsigned long long* stamps = nullptr;
+        if (trace) (void)hipMalloc(&stamps, sizeof(unsigned long long) * 10 * e->plan_max_tasks);
+        if (e->band_wg_per_cu >= 2 && 2 * e->plan_lds <= 160 * 1024)
+            hipLaunchKernelGGL(k_pyramid_band<8>, dim3(e->plan_nb, n), dim3(kBandThreads), e->plan_lds, st, e->d_geom,
+                               e->d_tasks, e->d_ntasks, imgs, pyr, blr, e->d_xtab, e->d_ytab, stamps, A);
+        else
+            hipLaunchKernelGGL(k_pyramid_band<4>, dim3(e->plan_nb, n), dim3(kBandThreads), e->plan_lds, st, e->d_geom,
+                               e->d_tasks, e->d_ntasks, imgs, pyr, blr, e->d_xtab, e->d_ytab, stamps, A);
+        if (stamps) {  // debug: per-task phase times of band 0, frame 0 (wave 0's view)
+            std::vector<unsigned long long> h(10 * e->plan_max_tasks);
+            std::vector<BandTask> tk(e->plan_max_tasks);
+            int nt0 = 0;
+            (void)hipStreamSynchronize(st);
+            (void)hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost);
+            (void)hipMemcpy(tk.data(), e->d_tasks, tk.size() * sizeof(BandTask), hipMemcpyDeviceToHost);
+            (void)hipMemcpy(&nt0, e->d_ntasks, sizeof(int), hipMemcpyDeviceToHost);
+            for (int i = 0; i < nt0; ++i) {
+                fprintf(stderr, "band-trace task %2d L%d rows [%3d,%3d) late %d |", i, tk[i].level, tk[i].a, tk[i].b, tk[i].late);
+                for (int k = 1; k < 10; ++k) fprintf(stderr, " %5.2f", (h[10 * i + k] - h[10 * i + k - 1]) * 0.01);
+                fprintf(stderr, "\n");
+            }
+            fprintf(stderr, "band-trace (stage vblur issue resize bar1 commit write hblur bar2) total %.2f us, %d tasks, nb %d, R %d\n",
+                    (h[10 * (nt0 - 1) + 9] - h[0]) * 0.01, nt0, e->plan_nb, e->plan_R);
+            (void)hipFree(stamps);
+        }
+    };
+    for (int l = 0; l < lfirst; ++l) {
         const orbgpu::LevelGeom& L = k.lv[l];
         dim3 grid((L.pw + kTileW - 1) / kTileW, (L.ph + kTileH - 1) / kTileH, n);
         if (l == 0)
@@ -1543,14 +2066,17 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
             launch_fast(l, l + 1, e->side2);
         }
     }
+    if (band) launch_band();
     mark(1);
-    if (split && e->fast_per_level) {
+    if (band && (split == 0 || split > lfirst)) {
+        launch_fast(0, k.nlevels, st);
+    } else if (split && e->fast_per_level && !band) {
         hipEventRecord(e->split_ev[2], e->side2);
         hipStreamWaitEvent(st, e->split_ev[2], 0);
     } else {
         launch_fast(split, k.nlevels, st);
     }
-    if (split) hipStreamWaitEvent(st, e->split_ev[1], 0);
+    if (split && (!band || split <= lfirst)) hipStreamWaitEvent(st, e->split_ev[1], 0);
     mark(2);
     // (running the quad-tree of the early levels on the side stream was measured slower: its
     // 80 KB-LDS waves crowd out the FAST work of the late levels)
@@ -1628,6 +2154,10 @@ int orb_extractor_create(const orb_params_t* p, int max_width, int max_height, i
     for (int k2 = 0; k2 < orbgpu::kMaxLevels && ok; ++k2)
         ok = hipEventCreateWithFlags(&e->lvl_ev[k2], hipEventDisableTiming) == hipSuccess;
     if (const char* c = getenv("ORBGPU_FAST_PER_LEVEL")) e->fast_per_level = atoi(c);
+    if (const char* c = getenv("ORBGPU_PYR_BAND")) e->band_mode = atoi(c);
+    if (const char* c = getenv("ORBGPU_PYR_WG_PER_CU")) e->band_wg_per_cu = std::max(1, atoi(c));
+    if (const char* c = getenv("ORBGPU_PYR_BAND_FROM")) e->band_from = std::max(0, atoi(c));
+    if (const char* c = getenv("ORBGPU_PYR_BAND_R")) e->band_r = std::min(16, std::max(4, atoi(c)));
     for (int s = 0; s < Extractor::kMaxStreams && ok; ++s)
         ok = hipStreamCreateWithFlags(&e->sub[s], hipStreamNonBlocking) == hipSuccess &&
              hipEventCreateWithFlags(&e->join_ev[s], hipEventDisableTiming) == hipSuccess;
@@ -1643,7 +2173,7 @@ int orb_extractor_destroy(orb_extractor_t h) {
     Extractor* e = reinterpret_cast<Extractor*>(h);
     if (!e) return ORB_ERR_ARG;
     if (e->stream) hipStreamSynchronize(e->stream);
-    void* bufs[] = {e->d_stamps, e->d_geom, e->d_cells, e->d_xtab, e->d_ytab, e->d_pyr, e->d_blur, e->d_cand, e->d_scratch,
+    void* bufs[] = {e->d_tasks, e->d_ntasks, e->d_stamps, e->d_geom, e->d_cells, e->d_xtab, e->d_ytab, e->d_pyr, e->d_blur, e->d_cand, e->d_scratch,
                     e->d_cell_count, e->d_cell_thr, e->d_sel, e->d_dst, e->d_sel_count, e->d_lap_count, e->d_status,
                     e->d_img, e->d_kps, e->d_desc, e->d_counts};
     for (void* b : bufs)

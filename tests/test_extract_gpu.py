@@ -160,3 +160,31 @@ def test_hamming_knn2(pkg, oracle):
                 second = d
         assert (idx[i], d1[i], d2[i]) == (bi, best, second)
     assert idx[3] == 5 and d1[3] == 0 and d2[3] == 0
+
+
+@pytest.mark.parametrize("band_from", ["0", "3"])
+def test_band_pyramid_path_parity(pkg, oracle, frames, synth, monkeypatch, band_from):
+    """The optional whole-pyramid band kernel (ORBGPU_PYR_BAND=1, off by default) stays bit-exact:
+    single frames (aligned 752, unaligned 643 -> byte staging path) and a device batch."""
+    import torch
+    monkeypatch.setenv("ORBGPU_PYR_BAND", "1")
+    monkeypatch.setenv("ORBGPU_PYR_BAND_FROM", band_from)
+    for case in ["stereoL752", "odd_size"]:
+        img, nf, lap = frames[case]
+        ex = pkg.ORBextractor(nf, 1.2, 8, 20, 7, max_width=1280, max_height=720)
+        kps, desc, mono = ex(img, None, lap)
+        rkps, rdesc, rmono = oracle.OracleExtractor(nf, 1.2, 8, 20, 7)(img, lap)
+        assert mono == rmono and np.array_equal(kps.view(np.uint8), rkps.view(np.uint8)), case
+        assert np.array_equal(desc, rdesc), case
+    batch = synth.frame_batch(5, 640, 480, seed0=900)
+    ex = pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=640, max_height=480, max_batch=8)
+    kps, desc, counts = ex.extract_batch_device(torch.from_numpy(batch).cuda(), (0, 1000))
+    torch.cuda.synchronize()
+    counts = counts.cpu().numpy()
+    ref = oracle.OracleExtractor(1000, 1.2, 8, 20, 7)
+    for f in range(len(batch)):
+        rk, rd, rm = ref(batch[f], (0, 1000))
+        n = int(counts[f, 0])
+        assert n == len(rk) and int(counts[f, 1]) == rm
+        assert np.array_equal(pkg.keypoints_to_structured(kps[f], n).view(np.uint8), rk.view(np.uint8)), f
+        assert np.array_equal(desc[f, :n].cpu().numpy(), rd), f
