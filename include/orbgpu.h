@@ -220,6 +220,32 @@ int orb_search_by_projection_local(orb_matcher_t m, const orb_frame_view_t* fram
                                    const orb_local_points_t* pts, float th, int far_points, float th_far_points,
                                    int32_t* match, int32_t* n_matches);
 
+/* ---- Frame::ComputeStereoMatches (src/Frame.cc:1102-1358) ------------------------------------ */
+
+/* Stereo matching of a rectified pair, on the two extractors' device pyramids (mvImagePyramid of
+ * mpORBextractorLeft / mpORBextractorRight, src/Frame.cc:1241,1262) and their keypoints /
+ * descriptors: per left keypoint the row-band Hamming search (TH_HIGH start, octave +-1, u range
+ * [uL - bf/b, uL], accept < (TH_HIGH+TH_LOW)/2), the 11x11 SAD over +-5 px at the keypoint's
+ * level, the parabola sub-pixel fit, the disparity test, then the median cull
+ * (SAD >= 1.5*1.4*median dropped).  Writes mvuRight / mvDepth (-1 = no match) for the left
+ * keypoints.  `left` and `right` must have extracted frames of the same size with the same
+ * parameters; the pyramids of their last extraction are read.
+ *
+ * Host arrays, frame 0 of each handle (after orb_extract): returns the number of keypoints kept
+ * (>= 0) or a negative status.  Synchronous. */
+int orb_compute_stereo_matches(orb_extractor_t left, orb_extractor_t right, const orb_keypoint_t* kps_l, int n_l,
+                               const uint8_t* desc_l, const orb_keypoint_t* kps_r, int n_r, const uint8_t* desc_r,
+                               float bf, float b, float* u_right, float* depth);
+/* Device batch: frames 0..n-1 of both handles (after orb_extract_batch_device), keypoints
+ * [n][cap] and counts [n][2] (element 0 = keypoint count) exactly as orb_extract_batch_device wrote
+ * them.  Writes u_right / depth [n][cap_l] and kept[n].  Async on `stream`. */
+int orb_compute_stereo_matches_batch_device(orb_extractor_t left, orb_extractor_t right, int n,
+                                            const orb_keypoint_t* d_kps_l, const int32_t* d_counts_l,
+                                            const uint8_t* d_desc_l, int cap_l, const orb_keypoint_t* d_kps_r,
+                                            const int32_t* d_counts_r, const uint8_t* d_desc_r, int cap_r,
+                                            float bf, float b, float* d_u_right, float* d_depth, int32_t* d_kept,
+                                            void* stream);
+
 /* ---- Optimizer::LocalBundleAdjustment (src/Optimizer.cc:1740-2188) ----------------------------- */
 /* The shim keeps the reference's graph gather (B1, src/Optimizer.cc:1744-1855) and the culling /
  * write-back (B10, :2107-2185) on the host and hands the flattened g2o problem across this ABI; the

@@ -39,6 +39,8 @@ _PROTOS = {
     "oracle_local_ba": (_i, [_vp, _vp, _vp, _vp, _vp]),
     "oracle_search_by_projection_frame": (_i, [_vp, _vp, _f, _i, _i, _vp]),
     "oracle_search_by_projection_local": (_i, [_vp, _vp, _vp, _f, _i, _f, _f, _vp]),
+    "oracle_compute_stereo_matches": (_i, [_vp, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _f, _f,
+                                           _vp, _vp]),
 }
 
 _LIB = None
@@ -240,3 +242,30 @@ def search_by_projection_local(frame, points, th: float, far: bool, th_far: floa
                                                  ctypes.byref(points.view()), float(th), int(far), float(th_far),
                                                  float(nnratio), m.ctypes.data)
     return n, m[:frame.N]
+
+
+def compute_stereo_matches(kps_l, desc_l, kps_r, desc_r, planes_l, planes_r, scale, inv_scale, bf, b):
+    """Frame::ComputeStereoMatches (oracle/orb_stereo_oracle.cpp).  planes_*: per level, the padded
+    plane ((h+38) x (w+38) uint8) of the left / right extractor.  Returns (mvuRight, mvDepth, kept)."""
+    lib = load()
+    kl = np.ascontiguousarray(kps_l, KEYPOINT_DTYPE)
+    kr = np.ascontiguousarray(kps_r, KEYPOINT_DTYPE)
+    dl = np.ascontiguousarray(desc_l, np.uint8).reshape(-1, 32)
+    dr = np.ascontiguousarray(desc_r, np.uint8).reshape(-1, 32)
+    n = len(planes_l)
+    pl = [np.ascontiguousarray(p, np.uint8) for p in planes_l]
+    pr = [np.ascontiguousarray(p, np.uint8) for p in planes_r]
+    ptr_l = (ctypes.c_void_p * n)(*[p.ctypes.data for p in pl])
+    ptr_r = (ctypes.c_void_p * n)(*[p.ctypes.data for p in pr])
+    pitch = np.array([p.shape[1] for p in pl], np.int32)
+    w = pitch - 38
+    h = np.array([p.shape[0] - 38 for p in pl], np.int32)
+    sc = np.ascontiguousarray(scale, np.float32)
+    isc = np.ascontiguousarray(inv_scale, np.float32)
+    ur = np.zeros(len(kl), np.float32)
+    dp = np.zeros(len(kl), np.float32)
+    kept = lib.oracle_compute_stereo_matches(kl.ctypes.data, len(kl), dl.ctypes.data, kr.ctypes.data, len(kr),
+                                             dr.ctypes.data, ptr_l, ptr_r, pitch.ctypes.data, w.ctypes.data,
+                                             h.ctypes.data, n, sc.ctypes.data, isc.ctypes.data, float(bf), float(b),
+                                             ur.ctypes.data, dp.ctypes.data)
+    return ur, dp, kept

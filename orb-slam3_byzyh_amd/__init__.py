@@ -11,5 +11,6 @@ from .keyframe import Frame, KeyFrame, LocalMapPoints
 from .matcher import ORBmatcher
 from .optimizer import LocalBA, local_bundle_adjustment
 from . import distributed
+from .stereo import compute_stereo_matches, compute_stereo_matches_batch_device
 
-__all__ = ["ORBextractor", "ORBmatcher", "KeyFrame", "Frame", "LocalMapPoints", "LocalBA", "local_bundle_adjustment", "KEYPOINT_DTYPE", "OrbGpuError", "keypoints_to_structured", "_lib"]
+__all__ = ["ORBextractor", "ORBmatcher", "KeyFrame", "Frame", "LocalMapPoints", "LocalBA", "local_bundle_adjustment", "compute_stereo_matches", "compute_stereo_matches_batch_device", "KEYPOINT_DTYPE", "OrbGpuError", "keypoints_to_structured", "_lib"]

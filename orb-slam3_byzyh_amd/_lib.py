@@ -62,6 +62,9 @@ PROTOTYPES = {
     "orb_search_for_triangulation": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
     "orb_search_by_projection_frame": (_i, [_vp, _vp, _vp, _f, _i, _vp, _vp]),
     "orb_search_by_projection_local": (_i, [_vp, _vp, _vp, _vp, _f, _i, _f, _vp, _vp]),
+    "orb_compute_stereo_matches": (_i, [_vp, _vp, _vp, _i, _vp, _vp, _i, _vp, _f, _f, _vp, _vp]),
+    "orb_compute_stereo_matches_batch_device": (_i, [_vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _i, _f, _f, _vp,
+                                                     _vp, _vp, _vp]),
     "orb_ba_create": (_i, [ctypes.POINTER(_vp)]),
     "orb_ba_destroy": (_i, [_vp]),
     "orb_ba_optimize": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),

@@ -2169,6 +2169,28 @@ int orb_extractor_create(const orb_params_t* p, int max_width, int max_height, i
     return ORB_OK;
 }
 
+int orbgpu_extractor_pyramid(orb_extractor_t h, OrbPyramidView* out) {
+    Extractor* e = reinterpret_cast<Extractor*>(h);
+    if (!e || !out) return orbgpu_fail(ORB_ERR_ARG, "null handle");
+    if (!e->geo_ok || e->last_n <= 0) return orbgpu_fail(ORB_ERR_ARG, "the extractor has not run yet");
+    const orbgpu::KernelGeom& k = e->geo.k;
+    *out = OrbPyramidView{};
+    out->base = e->d_pyr;
+    out->frame_bytes = k.pyr_frame_bytes;
+    out->nframes = e->last_n;
+    out->nlevels = k.nlevels;
+    for (int l = 0; l < k.nlevels; ++l) {
+        out->plane_off[l] = k.lv[l].plane_off;
+        out->pitch[l] = k.lv[l].pitch;
+        out->w[l] = k.lv[l].w;
+        out->h[l] = k.lv[l].h;
+        out->scale[l] = e->P.scale[l];
+        out->inv_scale[l] = e->P.inv_scale[l];
+    }
+    out->stream = e->stream;
+    return ORB_OK;
+}
+
 int orb_extractor_destroy(orb_extractor_t h) {
     Extractor* e = reinterpret_cast<Extractor*>(h);
     if (!e) return ORB_ERR_ARG;

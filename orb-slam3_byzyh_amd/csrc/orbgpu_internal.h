@@ -1,5 +1,22 @@
 // Internal helpers shared by the liborbgpu.so translation units (not part of the C ABI).
 #pragma once
+#include <cstdint>
+
+#include "orbgpu.h"
 
 // Record `msg` as this thread's last error (orb_last_error) and return `code`.
 int orbgpu_fail(int code, const char* msg);
+
+// Device view of an extractor handle's image pyramids (the padded planes of its last batch), for
+// kernels that read mvImagePyramid (Frame::ComputeStereoMatches).
+struct OrbPyramidView {
+    const uint8_t* base;    // frame 0's padded pyramid block (device)
+    long long frame_bytes;  // stride between frames' blocks
+    int nframes;            // frames extracted by the last launch
+    int nlevels;
+    long long plane_off[12];
+    int pitch[12], w[12], h[12];  // padded-plane pitch, level (view) size
+    float scale[12], inv_scale[12];
+    void* stream;           // the handle's stream (orb_extract's synchronous path runs on it)
+};
+extern "C" int orbgpu_extractor_pyramid(orb_extractor_t h, OrbPyramidView* out);
