@@ -181,6 +181,73 @@ def bench_local_ba(pkg, synth, world, dev, steps, cpu_baseline_on):
     return out
 
 
+def bench_stereo(pkg, synth, dev, steps, cpu_baseline_on, n_pairs=32):
+    """C3 stereo stream (752x480, nFeatures 1200, EuRoC bf/b): one step = extract the left and the
+    right batch of n_pairs frames + Frame::ComputeStereoMatches on the device pyramids.  Reports
+    stereo frames per ms, the matching kernels' share, and the CPU oracle on a bounded sample."""
+    import numpy as np
+    import torch
+    bf, b = 47.90639384423901, 0.110074
+    pairs = [synth.stereo_pair(752, 480, seed=2000 + i) for i in range(n_pairs)]
+    L = torch.from_numpy(np.stack([p[0] for p in pairs])).to(dev)
+    R = torch.from_numpy(np.stack([p[1] for p in pairs])).to(dev)
+    exl = pkg.ORBextractor(1200, 1.2, 8, 20, 7, max_width=752, max_height=480, max_batch=n_pairs)
+    exr = pkg.ORBextractor(1200, 1.2, 8, 20, 7, max_width=752, max_height=480, max_batch=n_pairs)
+    cap = 1200 + 16 * 8
+    st = torch.cuda.current_stream(dev)
+    mk = lambda: (torch.empty((n_pairs, cap, 7), dtype=torch.float32, device=dev),
+                  torch.empty((n_pairs, cap, 32), dtype=torch.uint8, device=dev),
+                  torch.empty((n_pairs, 2), dtype=torch.int32, device=dev))
+    out_l, out_r = mk(), mk()
+
+    def step():
+        exl.extract_batch_device(L, (0, 0), cap=cap, out=out_l, stream=st)
+        exr.extract_batch_device(R, (0, 0), cap=cap, out=out_r, stream=st)
+        return pkg.compute_stereo_matches_batch_device(exl, exr, out_l, out_r, bf, b, stream=st)
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize(dev)
+    reps = max(5, min(steps, 20))
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    t0 = time.perf_counter()
+    for i in range(reps):
+        exl.extract_batch_device(L, (0, 0), cap=cap, out=out_l, stream=st)
+        exr.extract_batch_device(R, (0, 0), cap=cap, out=out_r, stream=st)
+        ev[i][0].record(st)
+        _, _, kept = pkg.compute_stereo_matches_batch_device(exl, exr, out_l, out_r, bf, b, stream=st)
+        ev[i][1].record(st)
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) * 1e3
+    match_ms = sum(a.elapsed_time(z) for a, z in ev)
+    kept = kept.cpu().numpy()
+    out = {"config": f"C3: {n_pairs} stereo pairs 752x480 per step (synthetic EuRoC-shaped, disparity 4-48 px), "
+                     "nFeatures 1200, extract left + right + Frame::ComputeStereoMatches, one GPU",
+           "stereo_frames_per_ms": round(n_pairs * reps / dt, 4), "ms_per_step": round(dt / reps, 4),
+           "match_ms_per_step": round(match_ms / reps, 4),
+           "matches_per_frame": round(float(kept.mean()), 1)}
+    if cpu_baseline_on:
+        from oracle import oracle as oracle_mod
+        import concurrent.futures as cf
+        exo = [oracle_mod.OracleExtractor(1200, 1.2, 8, 20, 7) for _ in range(2)]
+        sc = exo[0].params()
+        t0 = time.perf_counter()
+        nfr = 0
+        with cf.ThreadPoolExecutor(2) as pool:  # left || right, as Frame.cc:136-141
+            while time.perf_counter() - t0 < 3.0 or nfr < 2:
+                lft, rgt, _ = pairs[nfr % n_pairs]
+                (kl, dl, _), (kr, dr, _) = pool.map(lambda a: a[0](a[1], (0, 0)), [(exo[0], lft), (exo[1], rgt)])
+                oracle_mod.compute_stereo_matches(kl, dl, kr, dr, [exo[0].level_padded(l) for l in range(8)],
+                                                  [exo[1].level_padded(l) for l in range(8)], sc["scale"],
+                                                  sc["inv_scale"], bf, b)
+                nfr += 1
+        cdt = (time.perf_counter() - t0) * 1e3
+        out["cpu_baseline"] = {"value": round(nfr / cdt, 5), "unit": "stereo frames/ms", "cores": 2, "kind": "port",
+                               "sample": f"{nfr} stereo frames of the C3 set in {cdt / 1e3:.1f} s, left and right "
+                                         "extraction on 2 threads + the stereo oracle"}
+    return out
+
+
 def pmc_traffic():
     p = ROOT / "profiles" / "pmc_latest.json"
     if p.exists():
@@ -200,6 +267,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-ba", action="store_true", help="skip the LocalBA (C5) measurement")
+    ap.add_argument("--no-stereo", action="store_true", help="skip the stereo stream (C3) measurement")
     args = ap.parse_args()
 
     import numpy as np
@@ -333,9 +401,17 @@ def main():
                                      rank == 0 and world == 1 and not args.no_cpu_baseline)
         except Exception as e:  # noqa: BLE001 -- the extraction line is still reported
             localba = {"error": repr(e)}
+    stereo = None
+    if not args.no_stereo and world == 1:
+        try:
+            stereo = bench_stereo(pkg, synth, dev, args.steps, not args.no_cpu_baseline)
+        except Exception as e:  # noqa: BLE001
+            stereo = {"error": repr(e)}
     if rank == 0:
         result["localba_iter_ms"] = localba.get("iter_ms") if localba else None
         result["localba"] = localba
+        if stereo is not None:
+            result["stereo"] = stereo
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
