@@ -101,6 +101,9 @@ public:
 
     std::vector<cv::Mat> mvImagePyramid;
 
+    // the underlying handle, for the device-side consumers of the pyramid (orb_compute_stereo_matches)
+    orb_extractor_t handle() const { return h_; }
+
 private:
     orb_extractor_t h_ = nullptr;
     int nfeatures_;
