@@ -139,30 +139,29 @@ __global__ __launch_bounds__(256) void k_pyramid_level(const KernelGeom* __restr
     reflect_range(Y0 - kHalo - kEdge, Y0 + kTileH + kHalo - 1 - kEdge, L.h, vy0, vy1);
     if (kLevel0) {
         // level 0: tile (+halo) straight from the input with reflected indices; 2 rows x 128 columns
-        // per pass, 4 passes (8 loads per thread) in flight
+        // per pass, all 22 loads per thread issued before the first LDS store (one round trip)
         const uint8_t* src = in + (size_t)f * in_frame_stride;
         const int c0 = tid & 127, rg = tid >> 7;
-        for (int ty0 = 0; ty0 < kLH; ty0 += 8) {
-            int v[4][2];
+        constexpr int kPass = (kLH + 1) / 2;
+        int v[kPass][2];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int ty = ty0 + 2 * q + rg;
-                const int vy = reflect101(Y0 - kHalo + min(ty, kLH - 1) - kEdge, L.h);
+        for (int q = 0; q < kPass; ++q) {
+            const int ty = 2 * q + rg;
+            const int vy = reflect101(Y0 - kHalo + min(ty, kLH - 1) - kEdge, L.h);
 #pragma unroll
-                for (int hx = 0; hx < 2; ++hx) {
-                    const int tx = c0 + 128 * hx;
-                    const int vx = reflect101(X0 - kHalo + min(tx, kLW - 1) - kEdge, L.w);
-                    v[q][hx] = (ty < kLH && tx < kLW) ? src[(size_t)vy * in_stride + vx] : 0;
-                }
+            for (int hx = 0; hx < 2; ++hx) {
+                const int tx = c0 + 128 * hx;
+                const int vx = reflect101(X0 - kHalo + min(tx, kLW - 1) - kEdge, L.w);
+                v[q][hx] = (ty < kLH && tx < kLW) ? src[(size_t)vy * in_stride + vx] : 0;
             }
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-#pragma unroll
-                for (int hx = 0; hx < 2; ++hx) {
-                    const int ty = ty0 + 2 * q + rg, tx = c0 + 128 * hx;
-                    if (ty < kLH && tx < kLW) tile[ty][tx] = (uint8_t)v[q][hx];
-                }
         }
+#pragma unroll
+        for (int q = 0; q < kPass; ++q)
+#pragma unroll
+            for (int hx = 0; hx < 2; ++hx) {
+                const int ty = 2 * q + rg, tx = c0 + 128 * hx;
+                if (ty < kLH && tx < kLW) tile[ty][tx] = (uint8_t)v[q][hx];
+            }
         __syncthreads();
     } else {
         const LevelGeom& P = g.lv[level - 1];
@@ -183,23 +182,23 @@ __global__ __launch_bounds__(256) void k_pyramid_level(const KernelGeom* __restr
         const int nw = (shift + bw + 3) >> 2;
         uint32_t* boxw = reinterpret_cast<uint32_t*>(box);
         const int wl = tid & 63, rg = tid >> 6;
-        for (int r0 = 0; r0 < bh; r0 += 8) {
-            uint32_t v[2][2];
+        // every load of the box issued before the first LDS store (one round trip per block)
+        constexpr int kRowPass = kBH / 4, kWordPass = (kBoxWords + 63) / 64;
+        uint32_t v[kRowPass][kWordPass];
 #pragma unroll
-            for (int q = 0; q < 2; ++q)
+        for (int q = 0; q < kRowPass; ++q)
 #pragma unroll
-                for (int hx = 0; hx < 2; ++hx) {
-                    const int r = r0 + 4 * q + rg, w = wl + 64 * hx;
-                    v[q][hx] = (r < bh && w < nw) ? wsrc[(size_t)r * (sstride >> 2) + w] : 0u;
-                }
+            for (int hx = 0; hx < kWordPass; ++hx) {
+                const int r = 4 * q + rg, w = wl + 64 * hx;
+                v[q][hx] = (r < bh && w < nw) ? wsrc[(size_t)r * (sstride >> 2) + w] : 0u;
+            }
 #pragma unroll
-            for (int q = 0; q < 2; ++q)
+        for (int q = 0; q < kRowPass; ++q)
 #pragma unroll
-                for (int hx = 0; hx < 2; ++hx) {
-                    const int r = r0 + 4 * q + rg, w = wl + 64 * hx;
-                    if (r < bh && w < nw) boxw[r * kBoxWords + w] = v[q][hx];
-                }
-        }
+            for (int hx = 0; hx < kWordPass; ++hx) {
+                const int r = 4 * q + rg, w = wl + 64 * hx;
+                if (r < bh && w < nw) boxw[r * kBoxWords + w] = v[q][hx];
+            }
         __syncthreads();
         // tile (+halo) values, INTER_LINEAR from the box
         for (int i = tid; i < kLH * kLW; i += 256) {
