@@ -708,6 +708,20 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
     uint32_t* sc32 = reinterpret_cast<uint32_t*>(sc);
     // lanes = 4 rows x 16 dwords (a second column pass only for windows wider than 16 dwords)
     const int lr = lane >> 4, lw = lane & 15;
+    if (nwr <= 16 && wh <= 48) {
+        // the usual cell window (<= 64 bytes x 48 rows): every load issued before any LDS store
+        uint32_t v[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+            const int r = 4 * k + lr;
+            v[k] = (r < wh && lw < nwr) ? wsrc[(size_t)r * (L.pitch >> 2) + lw] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+            const int r = 4 * k + lr;
+            if (r < wh && lw < nwr) { win32[r * nwr + lw] = v[k]; sc32[r * nwr + lw] = 0u; }
+        }
+    } else
     for (int w0 = 0; w0 < nwr; w0 += 16) {
         const int w = w0 + lw;
         for (int r0 = 0; r0 < wh; r0 += 16) {
