@@ -304,6 +304,40 @@ int orb_ba_destroy(orb_ba_t h);
 int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* problem, const orb_ba_options_t* options, double* edge_chi2,
                     uint8_t* edge_depth_ok, orb_ba_result_t* result);
 
+/* ---- Optimizer::PoseOptimization (src/Optimizer.cc:55-415) ------------------------------------ */
+/* Motion-only BA of tracking, batched over frames.  Per frame: one g2o::VertexSE3Expmap (Tcw) and a
+ * unary edge per matched MapPoint -- ORB_SLAM3::EdgeSE3ProjectXYZOnlyPose (mono, Huber sqrt(5.991))
+ * or g2o::EdgeStereoSE3ProjectXYZOnlyPose (mvuRight >= 0, Huber sqrt(7.815)) -- then 4 rounds of
+ * optimize(10) with g2o's Levenberg-Marquardt and LinearSolverDense, each round restarting from the
+ * frame's pose, re-classifying every edge by chi2 > 5.991 / 7.815 (the error of the last evaluated
+ * state for active edges, recomputed for outliers), the robust kernels removed after round 2, and
+ * the early exit when the frame has fewer than 10 edges.  Pinhole, single camera (mpCamera2 ==
+ * NULL); the fisheye two-camera edge (EdgeSE3ProjectXYZOnlyPoseToBody) is not covered. */
+
+typedef struct orb_pose_edge {
+    double xw[3];        /* pMP->GetWorldPos().cast<double>() */
+    double obs[3];       /* kpUn.pt.x, kpUn.pt.y, mvuRight[i] (stereo only) */
+    float inv_sigma2;    /* mvInvLevelSigma2[kpUn.octave] */
+    int32_t stereo;      /* mvuRight[i] >= 0 */
+} orb_pose_edge_t;
+
+typedef struct orb_pose_frame {
+    double pose[7];          /* Tcw as g2o::SE3Quat::toVector (tx ty tz qx qy qz qw), in */
+    orb_ba_camera_t cam;     /* fx, fy, cx, cy, mbf */
+    int32_t edge_begin;      /* this frame's edges: edges[edge_begin, edge_begin + n_edges) */
+    int32_t n_edges;         /* = nInitialCorrespondences */
+} orb_pose_frame_t;
+
+/* Host arrays, synchronous.  pose_out[7 f]: the optimised Tcw (unchanged when the frame has fewer
+ * than 3 edges); outlier[e]: mvbOutlier of edge e after the last round; inliers[f]: the return value
+ * of PoseOptimization (nInitialCorrespondences - nBad, 0 below 3 correspondences). */
+int orb_pose_optimization(int n_frames, const orb_pose_frame_t* frames, int n_edges, const orb_pose_edge_t* edges,
+                          double* pose_out, uint8_t* outlier, int32_t* inliers);
+/* The same on device arrays, asynchronous on `stream` (one workgroup per frame). */
+int orb_pose_optimization_device(int n_frames, const orb_pose_frame_t* d_frames, int n_edges,
+                                 const orb_pose_edge_t* d_edges, double* d_pose_out, uint8_t* d_outlier,
+                                 int32_t* d_inliers, void* stream);
+
 /* ---- multi-GPU local BA: one process per GPU, every rank passes the same
  * problem; rank r owns a contiguous, edge-balanced range of the landmarks and their edges, and
  * the ranks all-reduce the partial Hpp/b_p, the partial reduced camera system (S, b_S) of each LM

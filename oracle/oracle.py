@@ -39,6 +39,7 @@ _PROTOS = {
     "oracle_local_ba": (_i, [_vp, _vp, _vp, _vp, _vp]),
     "oracle_search_by_projection_frame": (_i, [_vp, _vp, _f, _i, _i, _vp]),
     "oracle_search_by_projection_local": (_i, [_vp, _vp, _vp, _f, _i, _f, _f, _vp]),
+    "oracle_pose_optimization": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
     "oracle_compute_stereo_matches": (_i, [_vp, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _f, _f,
                                            _vp, _vp]),
 }
@@ -269,3 +270,18 @@ def compute_stereo_matches(kps_l, desc_l, kps_r, desc_r, planes_l, planes_r, sca
                                              h.ctypes.data, n, sc.ctypes.data, isc.ctypes.data, float(bf), float(b),
                                              ur.ctypes.data, dp.ctypes.data)
     return ur, dp, kept
+
+
+def pose_optimization(frames, edges):
+    """Oracle Optimizer::PoseOptimization over a batch (oracle/orb_pose_oracle.cpp).  frames / edges:
+    orb_pose_frame_t / orb_pose_edge_t records (88 / 56 bytes).  Returns (poses [n, 7], outlier
+    flags per edge (bool), inliers per frame)."""
+    fr = np.ascontiguousarray(frames)
+    ed = np.ascontiguousarray(edges)
+    assert fr.dtype.itemsize == 88 and ed.dtype.itemsize == 56
+    poses = np.zeros((len(fr), 7))
+    outl = np.zeros(max(len(ed), 1), np.uint8)
+    inl = np.zeros(max(len(fr), 1), np.int32)
+    load().oracle_pose_optimization(len(fr), fr.ctypes.data, ed.ctypes.data, poses.ctypes.data, outl.ctypes.data,
+                                    inl.ctypes.data)
+    return poses, outl[:len(ed)].astype(bool), inl[:len(fr)]

@@ -5,12 +5,12 @@ The package directory is ``orb-slam3_byzyh_amd/`` (not a valid identifier); load
 __graft_entry__.py), which register it under the import name ``orbslam3_amd``.
 """
 from . import _lib
-from ._lib import KEYPOINT_DTYPE, OrbGpuError
+from ._lib import KEYPOINT_DTYPE, POSE_EDGE_DTYPE, POSE_FRAME_DTYPE, OrbGpuError
 from .extractor import ORBextractor, keypoints_to_structured
 from .keyframe import Frame, KeyFrame, LocalMapPoints
 from .matcher import ORBmatcher
-from .optimizer import LocalBA, local_bundle_adjustment
+from .optimizer import LocalBA, local_bundle_adjustment, pose_optimization
 from . import distributed
 from .stereo import compute_stereo_matches, compute_stereo_matches_batch_device
 
-__all__ = ["ORBextractor", "ORBmatcher", "KeyFrame", "Frame", "LocalMapPoints", "LocalBA", "local_bundle_adjustment", "compute_stereo_matches", "compute_stereo_matches_batch_device", "KEYPOINT_DTYPE", "OrbGpuError", "keypoints_to_structured", "_lib"]
+__all__ = ["ORBextractor", "ORBmatcher", "KeyFrame", "Frame", "LocalMapPoints", "LocalBA", "local_bundle_adjustment", "pose_optimization", "compute_stereo_matches", "compute_stereo_matches_batch_device", "KEYPOINT_DTYPE", "OrbGpuError", "keypoints_to_structured", "_lib"]

@@ -28,6 +28,15 @@ KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle"
 assert KEYPOINT_DTYPE.itemsize == 28
 
 
+# orb_pose_edge_t (56 bytes) / orb_pose_frame_t (88 bytes, 8-byte aligned) of include/orbgpu.h
+POSE_EDGE_DTYPE = np.dtype([("xw", "<f8", 3), ("obs", "<f8", 3), ("inv_sigma2", "<f4"), ("stereo", "<i4")])
+POSE_CAMERA_DTYPE = np.dtype([("fx", "<f4"), ("fy", "<f4"), ("cx", "<f4"), ("cy", "<f4"), ("bf", "<f4")])
+POSE_FRAME_DTYPE = np.dtype({"names": ["pose", "cam", "edge_begin", "n_edges"],
+                             "formats": [("<f8", 7), POSE_CAMERA_DTYPE, "<i4", "<i4"],
+                             "offsets": [0, 56, 76, 80], "itemsize": 88})
+assert POSE_EDGE_DTYPE.itemsize == 56
+
+
 class OrbGpuError(RuntimeError):
     def __init__(self, code: int, where: str, msg: str = ""):
         super().__init__(f"{where} failed with status {code}: {msg}")
@@ -65,6 +74,8 @@ PROTOTYPES = {
     "orb_compute_stereo_matches": (_i, [_vp, _vp, _vp, _i, _vp, _vp, _i, _vp, _f, _f, _vp, _vp]),
     "orb_compute_stereo_matches_batch_device": (_i, [_vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _i, _f, _f, _vp,
                                                      _vp, _vp, _vp]),
+    "orb_pose_optimization": (_i, [_i, _vp, _i, _vp, _vp, _vp, _vp]),
+    "orb_pose_optimization_device": (_i, [_i, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
     "orb_ba_create": (_i, [ctypes.POINTER(_vp)]),
     "orb_ba_destroy": (_i, [_vp]),
     "orb_ba_optimize": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),

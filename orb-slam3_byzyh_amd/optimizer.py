@@ -167,3 +167,21 @@ def local_bundle_adjustment(prob: dict, iterations: int = 10, solver: LocalBA | 
     stereo = np.asarray(prob["edges"]["stereo"]) != 0
     erase = np.where(stereo, chi2 > CHI2_STEREO, chi2 > CHI2_MONO) | ~depth
     return pose, point, erase, res
+
+
+def pose_optimization(frames, edges):
+    """Optimizer::PoseOptimization (src/Optimizer.cc:55-415) on a batch of frames, on the GPU.
+
+    frames: POSE_FRAME_DTYPE records (Tcw as SE3Quat vector, camera, the frame's edge range);
+    edges: POSE_EDGE_DTYPE records (MapPoint position, observation, information, stereo flag).
+    Returns (poses [n, 7], mvbOutlier per edge (bool), inliers per frame = the reference's return
+    value).  The reference's Frame writes (SetPose, mvbOutlier) are the caller's."""
+    from ._lib import POSE_EDGE_DTYPE, POSE_FRAME_DTYPE
+    fr = np.ascontiguousarray(frames, POSE_FRAME_DTYPE)
+    ed = np.ascontiguousarray(edges, POSE_EDGE_DTYPE)
+    poses = np.zeros((len(fr), 7), np.float64)
+    outl = np.zeros(max(len(ed), 1), np.uint8)
+    inl = np.zeros(max(len(fr), 1), np.int32)
+    check(_lib.load().orb_pose_optimization(len(fr), fr.ctypes.data, len(ed), ed.ctypes.data, poses.ctypes.data,
+                                            outl.ctypes.data, inl.ctypes.data), "orb_pose_optimization")
+    return poses, outl[:len(ed)].astype(bool), inl[:len(fr)]

@@ -403,3 +403,53 @@ def local_map_points(cur: dict, n_points: int = 1500, seed: int = 51, width: int
                 observed=(rng.random(n) > unobserved_frac).astype(np.uint8), track_proj=proj,
                 track_view_cos=rng.choice(np.array([0.999, 0.99], np.float32), n), track_depth=depth,
                 track_level=lvl, desc=mdesc)
+
+
+def pose_opt_batch(n_frames: int = 64, n_points: int = 600, stereo_frac: float = 0.5, outlier_frac: float = 0.08,
+                   seed: int = 41, width: int = 752, height: int = 480, nlevels: int = 8, rot_err: float = 0.01,
+                   trans_err: float = 0.03, points_per_frame=None):
+    """Tracking frames for Optimizer::PoseOptimization: per frame a true pose, ~n_points matched map
+    points 1.5-12 m in front, observations at octave U{0..7} with N(0, 1)*scale pixel noise, stereo
+    u_right for `stereo_frac` of them, `outlier_frac` gross outliers (+-15..60 px), and the initial
+    pose (the motion model's prediction) off by ~rot_err rad / trans_err m.  EuRoC intrinsics.
+    Returns (frames POSE_FRAME_DTYPE, edges POSE_EDGE_DTYPE, true poses [n, 7])."""
+    from ._lib import POSE_EDGE_DTYPE, POSE_FRAME_DTYPE
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = EUROC_K
+    scale, sigma2 = scale_tables(nlevels)
+    inv_sigma2 = (np.float32(1.0) / sigma2).astype(np.float32)
+    frames = np.zeros(n_frames, POSE_FRAME_DTYPE)
+    all_edges = []
+    truth = np.zeros((n_frames, 7))
+    for f in range(n_frames):
+        yaw, pitch = rng.uniform(-0.3, 0.3), rng.uniform(-0.1, 0.1)
+        Rcw = _small_rot(rng, 0.05) @ np.array([[np.cos(yaw), 0, -np.sin(yaw)], [0, 1, 0], [np.sin(yaw), 0, np.cos(yaw)]])
+        Rcw = np.array([[1, 0, 0], [0, np.cos(pitch), -np.sin(pitch)], [0, np.sin(pitch), np.cos(pitch)]]) @ Rcw
+        tcw = rng.normal(0, 1.0, 3)
+        truth[f, :3], truth[f, 3:] = tcw, rot_to_quat(Rcw)
+        npf = n_points if points_per_frame is None else int(points_per_frame[f])
+        e0 = len(all_edges)
+        while len(all_edges) - e0 < npf:
+            z = rng.uniform(1.5, 12.0)
+            u, v = rng.uniform(20, width - 20), rng.uniform(20, height - 20)
+            Xc = np.array([(u - cx) * z / fx, (v - cy) * z / fy, z])
+            Xw = Rcw.T @ (Xc - tcw)
+            octv = int(rng.integers(0, nlevels))
+            sc = float(scale[octv])
+            uo, vo = u + rng.normal(0, 1.0) * sc, v + rng.normal(0, 1.0) * sc
+            if rng.random() < outlier_frac:
+                uo += rng.choice([-1, 1]) * rng.uniform(15, 60)
+                vo += rng.choice([-1, 1]) * rng.uniform(15, 60)
+            st = rng.random() < stereo_frac
+            ur = uo - EUROC_BF / z + rng.normal(0, 1.0) * sc if st else -1.0
+            all_edges.append((Xw, (uo, vo, ur if st else 0.0), inv_sigma2[octv], int(st)))
+        Rp = _small_rot(rng, rot_err) @ Rcw
+        frames[f]["pose"][:3] = tcw + rng.normal(0, trans_err, 3)
+        frames[f]["pose"][3:] = rot_to_quat(Rp)
+        frames[f]["cam"] = (fx, fy, cx, cy, EUROC_BF)
+        frames[f]["edge_begin"] = e0
+        frames[f]["n_edges"] = npf
+    edges = np.zeros(len(all_edges), POSE_EDGE_DTYPE)
+    for i, (xw, obs, info, st) in enumerate(all_edges):
+        edges[i]["xw"], edges[i]["obs"], edges[i]["inv_sigma2"], edges[i]["stereo"] = xw, obs, info, st
+    return frames, edges, truth
