@@ -15,6 +15,7 @@ this host's cores on a bounded sample), `stages_ms` (per-stage HIP-event ms per 
 from __future__ import annotations
 
 import argparse
+import ctypes
 import concurrent.futures as cf
 import importlib.util
 import json
@@ -248,6 +249,51 @@ def bench_stereo(pkg, synth, dev, steps, cpu_baseline_on, n_pairs=32):
     return out
 
 
+def bench_pose(pkg, synth, dev, steps, cpu_baseline_on, n_frames=256, n_points=500):
+    """Optimizer::PoseOptimization (tracking's motion-only BA), batched: one step = n_frames frames of
+    ~n_points matched map points (50 % stereo, 8 % gross outliers), device-resident inputs."""
+    import numpy as np
+    import torch
+    frames, edges, _ = synth.pose_opt_batch(n_frames, n_points, stereo_frac=0.5, seed=4242)
+    lib = pkg._lib.load()
+    d_fr = torch.from_numpy(frames.view(np.uint8).reshape(-1)).to(dev)
+    d_ed = torch.from_numpy(edges.view(np.uint8).reshape(-1)).to(dev)
+    d_pose = torch.empty((n_frames, 7), dtype=torch.float64, device=dev)
+    d_out = torch.empty(len(edges), dtype=torch.uint8, device=dev)
+    d_inl = torch.empty(n_frames, dtype=torch.int32, device=dev)
+    st = torch.cuda.current_stream(dev)
+
+    def step():
+        pkg._lib.check(lib.orb_pose_optimization_device(n_frames, d_fr.data_ptr(), len(edges), d_ed.data_ptr(),
+                                                        d_pose.data_ptr(), d_out.data_ptr(), d_inl.data_ptr(),
+                                                        ctypes.c_void_p(st.cuda_stream)), "orb_pose_optimization_device")
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize(dev)
+    reps = max(5, min(steps, 20))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) * 1e3
+    out = {"config": f"PoseOptimization: {n_frames} frames x {n_points} edges (50 % stereo, 8 % outliers) per step, "
+                     "4 rounds x optimize(10), one GPU", "frames_per_ms": round(n_frames * reps / dt, 3),
+           "ms_per_step": round(dt / reps, 4), "dtype": "f64"}
+    if cpu_baseline_on:
+        from oracle import oracle as oracle_mod
+        t0 = time.perf_counter()
+        nfr = 0
+        while time.perf_counter() - t0 < 2.0 or nfr < 8:
+            oracle_mod.pose_optimization(frames[nfr % n_frames:nfr % n_frames + 1], edges)
+            nfr += 1
+        cdt = (time.perf_counter() - t0) * 1e3
+        out["cpu_baseline"] = {"value": round(nfr / cdt, 4), "unit": "frames/ms", "cores": 1, "kind": "port",
+                               "sample": f"{nfr} frames of the same set in {cdt / 1e3:.1f} s, "
+                                         "oracle/orb_pose_oracle.cpp -O2, one thread (as Tracking runs it)"}
+    return out
+
+
 def pmc_traffic():
     p = ROOT / "profiles" / "pmc_latest.json"
     if p.exists():
@@ -268,6 +314,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-ba", action="store_true", help="skip the LocalBA (C5) measurement")
     ap.add_argument("--no-stereo", action="store_true", help="skip the stereo stream (C3) measurement")
+    ap.add_argument("--no-pose", action="store_true", help="skip the PoseOptimization measurement")
     args = ap.parse_args()
 
     import numpy as np
@@ -407,7 +454,15 @@ def main():
             stereo = bench_stereo(pkg, synth, dev, args.steps, not args.no_cpu_baseline)
         except Exception as e:  # noqa: BLE001
             stereo = {"error": repr(e)}
+    pose = None
+    if not args.no_pose and world == 1:
+        try:
+            pose = bench_pose(pkg, synth, dev, args.steps, not args.no_cpu_baseline)
+        except Exception as e:  # noqa: BLE001
+            pose = {"error": repr(e)}
     if rank == 0:
+        if pose is not None:
+            result["pose_optimization"] = pose
         result["localba_iter_ms"] = localba.get("iter_ms") if localba else None
         result["localba"] = localba
         if stereo is not None:
