@@ -246,6 +246,49 @@ int orb_compute_stereo_matches_batch_device(orb_extractor_t left, orb_extractor_
                                             float bf, float b, float* d_u_right, float* d_depth, int32_t* d_kept,
                                             void* stream);
 
+/* ---- DBoW2 TemplatedVocabulary::transform (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1125-1260)
+ * KeyFrame::ComputeBoW / Frame::ComputeBoW (src/KeyFrame.cc:109, src/Frame.cc:1010) call
+ * mpORBvocabulary->transform(descriptors, mBowVec, mFeatVec, 4).  Per descriptor: descend the tree
+ * from the root taking, at every level, the first child of minimal DescriptorDistance (FORB); the
+ * leaf gives the word and its weight; the node passed at level L - levelsup is the FeatureVector
+ * node.  TF_IDF / TF weighting: BowVector += weight per word (words with weight 0 are stop words
+ * and skipped), then the scoring's normalisation (L1 for ORBvoc's L1_NORM).  The vocabulary is
+ * given as flat arrays (ORBvoc.txt itself is not shipped with the reference: .MISSING_LARGE_BLOBS). */
+
+typedef struct orb_vocabulary_view {
+    int32_t k, L;                 /* m_k, m_L (the tree may be unbalanced) */
+    int32_t weighting;            /* DBoW2 WeightingType: 0 TF_IDF, 1 TF, 2 IDF, 3 BINARY */
+    int32_t scoring;              /* DBoW2 ScoringType: 0 L1_NORM, 1 L2_NORM, 2 CHI_SQUARE, 3 KL, 4 BHATTACHARYYA, 5 DOT_PRODUCT */
+    int32_t n_nodes;              /* node 0 = root */
+    const int32_t* child_begin;   /* n_nodes + 1: children of node i = child_idx[child_begin[i] .. child_begin[i+1]) in Node::children order */
+    const int32_t* child_idx;
+    const uint8_t* desc;          /* n_nodes x 32 bytes (the root's is unused) */
+    const int32_t* word_id;       /* per node: WordId of a leaf, -1 for inner nodes */
+    const double* weight;         /* per node: the leaf's WordValue */
+} orb_vocabulary_view_t;
+
+typedef struct orb_vocabulary_s* orb_vocabulary_t;
+
+/* Upload a vocabulary (copied; the view may be freed afterwards). */
+int orb_vocabulary_create(const orb_vocabulary_view_t* view, orb_vocabulary_t* out);
+int orb_vocabulary_destroy(orb_vocabulary_t v);
+
+/* transform() of n descriptors (host, n x 32 bytes).  Outputs, each with capacity n:
+ * bow_word / bow_value (BowVector in ascending WordId order, *n_words entries), fv_node (FeatureVector
+ * nodes ascending, *n_nodes entries), fv_begin (n_nodes + 1 offsets into fv_feat), fv_feat (feature
+ * indices, ascending within a node).  Synchronous.  n <= 8192. */
+int orb_bow_transform(orb_vocabulary_t v, const uint8_t* desc, int n, int levelsup, int32_t* bow_word,
+                      double* bow_value, int32_t* n_words, int32_t* fv_node, int32_t* fv_begin, int32_t* fv_feat,
+                      int32_t* n_nodes);
+/* Device batch: frames f = 0..n_frames-1 hold descriptors d_desc[frame_begin[f] .. frame_begin[f+1])
+ * (d_frame_begin: n_frames + 1 device ints, each frame <= 8192).  Per frame f the outputs start at
+ * frame_begin[f] in every array (capacity = the frame's count; fv_begin: frame_begin[f] + f, with
+ * count + 1 entries); d_counts[2 f] = n_words, d_counts[2 f + 1] = n_nodes.  Async on `stream`. */
+int orb_bow_transform_batch_device(orb_vocabulary_t v, const uint8_t* d_desc, const int32_t* d_frame_begin,
+                                   int n_frames, int n_total, int levelsup, int32_t* d_bow_word,
+                                   double* d_bow_value, int32_t* d_fv_node, int32_t* d_fv_begin, int32_t* d_fv_feat,
+                                   int32_t* d_counts, void* stream);
+
 /* ---- Optimizer::LocalBundleAdjustment (src/Optimizer.cc:1740-2188) ----------------------------- */
 /* The shim keeps the reference's graph gather (B1, src/Optimizer.cc:1744-1855) and the culling /
  * write-back (B10, :2107-2185) on the host and hands the flattened g2o problem across this ABI; the

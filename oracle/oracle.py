@@ -40,6 +40,7 @@ _PROTOS = {
     "oracle_search_by_projection_frame": (_i, [_vp, _vp, _f, _i, _i, _vp]),
     "oracle_search_by_projection_local": (_i, [_vp, _vp, _vp, _f, _i, _f, _f, _vp]),
     "oracle_pose_optimization": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
+    "oracle_bow_transform": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "oracle_compute_stereo_matches": (_i, [_vp, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _f, _f,
                                            _vp, _vp]),
 }
@@ -285,3 +286,31 @@ def pose_optimization(frames, edges):
     load().oracle_pose_optimization(len(fr), fr.ctypes.data, ed.ctypes.data, poses.ctypes.data, outl.ctypes.data,
                                     inl.ctypes.data)
     return poses, outl[:len(ed)].astype(bool), inl[:len(fr)]
+
+
+def bow_transform(voc: dict, desc, levelsup: int = 4):
+    """Oracle TemplatedVocabulary::transform (oracle/orb_bow_oracle.cpp).  Returns (bow: {word: value},
+    feat_vec: {node: [features]}) like the DBoW2 std::maps."""
+    lib = load()
+
+    class View(ctypes.Structure):  # orb_vocabulary_view_t (include/orbgpu.h)
+        _fields_ = [("k", ctypes.c_int32), ("L", ctypes.c_int32), ("weighting", ctypes.c_int32),
+                    ("scoring", ctypes.c_int32), ("n_nodes", ctypes.c_int32), ("child_begin", ctypes.c_void_p),
+                    ("child_idx", ctypes.c_void_p), ("desc", ctypes.c_void_p), ("word_id", ctypes.c_void_p),
+                    ("weight", ctypes.c_void_p)]
+    keep = [np.ascontiguousarray(voc["child_begin"], np.int32), np.ascontiguousarray(voc["child_idx"], np.int32),
+            np.ascontiguousarray(voc["desc"], np.uint8), np.ascontiguousarray(voc["word_id"], np.int32),
+            np.ascontiguousarray(voc["weight"], np.float64)]
+    view = View(int(voc["k"]), int(voc["L"]), int(voc.get("weighting", 0)), int(voc.get("scoring", 0)),
+                len(keep[3]), *[a.ctypes.data for a in keep])
+    d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    n = len(d)
+    m = max(n, 1)
+    bw, bv = np.zeros(m, np.int32), np.zeros(m, np.float64)
+    fn, fb, ff = np.zeros(m, np.int32), np.zeros(m + 1, np.int32), np.zeros(m, np.int32)
+    nw, nn = np.zeros(1, np.int32), np.zeros(1, np.int32)
+    lib.oracle_bow_transform(ctypes.addressof(view), d.ctypes.data, n, int(levelsup), bw.ctypes.data, bv.ctypes.data,
+                             nw.ctypes.data, fn.ctypes.data, fb.ctypes.data, ff.ctypes.data, nn.ctypes.data)
+    bow = {int(bw[i]): float(bv[i]) for i in range(int(nw[0]))}
+    fv = {int(fn[j]): [int(x) for x in ff[fb[j]:fb[j + 1]]] for j in range(int(nn[0]))}
+    return bow, fv

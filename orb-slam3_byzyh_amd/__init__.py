@@ -12,5 +12,6 @@ from .matcher import ORBmatcher
 from .optimizer import LocalBA, local_bundle_adjustment, pose_optimization
 from . import distributed
 from .stereo import compute_stereo_matches, compute_stereo_matches_batch_device
+from .vocabulary import ORBVocabulary
 
-__all__ = ["ORBextractor", "ORBmatcher", "KeyFrame", "Frame", "LocalMapPoints", "LocalBA", "local_bundle_adjustment", "pose_optimization", "compute_stereo_matches", "compute_stereo_matches_batch_device", "KEYPOINT_DTYPE", "OrbGpuError", "keypoints_to_structured", "_lib"]
+__all__ = ["ORBextractor", "ORBmatcher", "KeyFrame", "Frame", "LocalMapPoints", "LocalBA", "local_bundle_adjustment", "pose_optimization", "compute_stereo_matches", "compute_stereo_matches_batch_device", "ORBVocabulary", "KEYPOINT_DTYPE", "OrbGpuError", "keypoints_to_structured", "_lib"]

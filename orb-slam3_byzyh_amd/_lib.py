@@ -37,6 +37,26 @@ POSE_FRAME_DTYPE = np.dtype({"names": ["pose", "cam", "edge_begin", "n_edges"],
 assert POSE_EDGE_DTYPE.itemsize == 56
 
 
+class VocabularyView(ctypes.Structure):  # orb_vocabulary_view_t
+    _fields_ = [("k", ctypes.c_int32), ("L", ctypes.c_int32), ("weighting", ctypes.c_int32),
+                ("scoring", ctypes.c_int32), ("n_nodes", ctypes.c_int32), ("child_begin", ctypes.c_void_p),
+                ("child_idx", ctypes.c_void_p), ("desc", ctypes.c_void_p), ("word_id", ctypes.c_void_p),
+                ("weight", ctypes.c_void_p)]
+
+
+def vocabulary_view(voc: dict) -> tuple:
+    """(VocabularyView, keep-alive arrays) for a vocabulary dict (k, L, weighting, scoring,
+    child_begin, child_idx, desc [n,32], word_id, weight)."""
+    arrs = {"child_begin": np.ascontiguousarray(voc["child_begin"], np.int32),
+            "child_idx": np.ascontiguousarray(voc["child_idx"], np.int32),
+            "desc": np.ascontiguousarray(voc["desc"], np.uint8), "word_id": np.ascontiguousarray(voc["word_id"], np.int32),
+            "weight": np.ascontiguousarray(voc["weight"], np.float64)}
+    v = VocabularyView(int(voc["k"]), int(voc["L"]), int(voc.get("weighting", 0)), int(voc.get("scoring", 0)),
+                       len(arrs["word_id"]), arrs["child_begin"].ctypes.data, arrs["child_idx"].ctypes.data,
+                       arrs["desc"].ctypes.data, arrs["word_id"].ctypes.data, arrs["weight"].ctypes.data)
+    return v, arrs
+
+
 class OrbGpuError(RuntimeError):
     def __init__(self, code: int, where: str, msg: str = ""):
         super().__init__(f"{where} failed with status {code}: {msg}")
@@ -76,6 +96,10 @@ PROTOTYPES = {
                                                      _vp, _vp, _vp]),
     "orb_pose_optimization": (_i, [_i, _vp, _i, _vp, _vp, _vp, _vp]),
     "orb_pose_optimization_device": (_i, [_i, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
+    "orb_vocabulary_create": (_i, [_vp, ctypes.POINTER(_vp)]),
+    "orb_vocabulary_destroy": (_i, [_vp]),
+    "orb_bow_transform": (_i, [_vp, _vp, _i, _i, _vp, _vp, _ip, _vp, _vp, _vp, _ip]),
+    "orb_bow_transform_batch_device": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "orb_ba_create": (_i, [ctypes.POINTER(_vp)]),
     "orb_ba_destroy": (_i, [_vp]),
     "orb_ba_optimize": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
