@@ -294,6 +294,43 @@ def bench_pose(pkg, synth, dev, steps, cpu_baseline_on, n_frames=256, n_points=5
     return out
 
 
+def bench_bow(pkg, synth, dev, steps, cpu_baseline_on, n_frames=64, n_feat=1000):
+    """KeyFrame::ComputeBoW: DBoW2 transform(descriptors, BowVector, FeatureVector, 4) of n_frames
+    frames x n_feat descriptors against an ORBvoc-shaped synthetic vocabulary (k=10, L=6, about a
+    million words), device-resident descriptors."""
+    import numpy as np
+    import torch
+    voc = synth.dbow_vocabulary(10, 6, seed=5, kmin=10, leaf_early=0.0)
+    v = pkg.ORBVocabulary(voc)
+    desc = synth.bow_descriptors(voc, n_frames * n_feat, seed=77)
+    d_desc = torch.from_numpy(desc).to(dev)
+    d_fb = torch.from_numpy(np.arange(n_frames + 1, dtype=np.int32) * n_feat).to(dev)
+    st = torch.cuda.current_stream(dev)
+    for _ in range(3):
+        v.transform_batch_device(d_desc, d_fb, 4, stream=st)
+    torch.cuda.synchronize(dev)
+    reps = max(5, min(steps, 20))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        v.transform_batch_device(d_desc, d_fb, 4, stream=st)
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) * 1e3
+    out = {"config": f"DBoW2 transform (KeyFrame::ComputeBoW, levelsup 4): {n_frames} frames x {n_feat} descriptors "
+                     f"per step, synthetic k=10 L=6 vocabulary ({len(voc['leaves'])} words), one GPU",
+           "frames_per_ms": round(n_frames * reps / dt, 3), "ms_per_step": round(dt / reps, 4)}
+    if cpu_baseline_on:
+        from oracle import oracle as oracle_mod
+        t0 = time.perf_counter()
+        nfr = 0
+        while time.perf_counter() - t0 < 2.0 or nfr < 4:
+            oracle_mod.bow_transform(voc, desc[(nfr % n_frames) * n_feat:(nfr % n_frames + 1) * n_feat], 4)
+            nfr += 1
+        cdt = (time.perf_counter() - t0) * 1e3
+        out["cpu_baseline"] = {"value": round(nfr / cdt, 4), "unit": "frames/ms", "cores": 1, "kind": "port",
+                               "sample": f"{nfr} frames in {cdt / 1e3:.1f} s, oracle/orb_bow_oracle.cpp -O2, one thread"}
+    return out
+
+
 def pmc_traffic():
     p = ROOT / "profiles" / "pmc_latest.json"
     if p.exists():
@@ -315,6 +352,7 @@ def main():
     ap.add_argument("--no-ba", action="store_true", help="skip the LocalBA (C5) measurement")
     ap.add_argument("--no-stereo", action="store_true", help="skip the stereo stream (C3) measurement")
     ap.add_argument("--no-pose", action="store_true", help="skip the PoseOptimization measurement")
+    ap.add_argument("--no-bow", action="store_true", help="skip the DBoW2 transform measurement")
     args = ap.parse_args()
 
     import numpy as np
@@ -460,9 +498,17 @@ def main():
             pose = bench_pose(pkg, synth, dev, args.steps, not args.no_cpu_baseline)
         except Exception as e:  # noqa: BLE001
             pose = {"error": repr(e)}
+    bow = None
+    if not args.no_bow and world == 1:
+        try:
+            bow = bench_bow(pkg, synth, dev, args.steps, not args.no_cpu_baseline)
+        except Exception as e:  # noqa: BLE001
+            bow = {"error": repr(e)}
     if rank == 0:
         if pose is not None:
             result["pose_optimization"] = pose
+        if bow is not None:
+            result["bow"] = bow
         result["localba_iter_ms"] = localba.get("iter_ms") if localba else None
         result["localba"] = localba
         if stereo is not None:

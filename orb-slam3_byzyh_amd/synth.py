@@ -456,51 +456,51 @@ def pose_opt_batch(n_frames: int = 64, n_points: int = 600, stereo_frac: float =
 
 
 def dbow_vocabulary(k: int = 10, L: int = 4, seed: int = 11, flip: float = 0.2, leaf_early: float = 0.05,
-                    stop_frac: float = 0.02, weighting: int = 0, scoring: int = 0):
+                    stop_frac: float = 0.02, weighting: int = 0, scoring: int = 0, kmin=None):
     """A DBoW2-shaped vocabulary tree (stand-in for ORBvoc.txt, absent: .MISSING_LARGE_BLOBS):
-    breadth-first node ids (root 0), up to k children per node, children = the parent's descriptor
-    with `flip` of its bits flipped (a coherent tree), a few nodes ending early as leaves (an
-    unbalanced tree, like real vocabularies) and `stop_frac` stop words (weight 0).  Returns the dict
-    orb_vocabulary_view_t takes, plus `leaves` (node ids of the words)."""
+    breadth-first node ids (root 0), k children at the root and k-3..k below, children = the
+    parent's descriptor with `flip` of its bits flipped (a coherent tree), a few nodes ending early
+    as leaves (an unbalanced tree, like real vocabularies) and `stop_frac` stop words (weight 0).
+    Built level by level (k=10, L=6 -- ORBvoc's shape, ~1.1M nodes -- takes seconds).  Returns the
+    dict orb_vocabulary_view_t takes, plus `leaves` (node ids of the words)."""
     rng = np.random.default_rng(seed)
-    desc = [np.zeros(32, np.uint8)]
-    depth = [0]
-    children = [[]]
-    q = [0]
-    head = 0
-    while head < len(q):
-        node = q[head]
-        head += 1
-        if depth[node] >= L or (node != 0 and rng.random() < leaf_early):
-            continue
-        kk = k if node == 0 else int(rng.integers(max(2, k - 3), k + 1))
-        base = desc[node] if node != 0 else None
-        for _ in range(kk):
-            if base is None:
-                d = rng.integers(0, 256, 32, dtype=np.uint8)
-            else:
-                bits = np.unpackbits(base) ^ (rng.random(256) < flip)
-                d = np.packbits(bits.astype(np.uint8))
-            children[node].append(len(desc))
-            desc.append(d)
-            depth.append(depth[node] + 1)
-            children.append([])
-            q.append(len(desc) - 1)
-    n = len(desc)
-    child_begin = np.zeros(n + 1, np.int32)
-    child_idx = []
-    for i in range(n):
-        child_idx.extend(children[i])
-        child_begin[i + 1] = len(child_idx)
+    desc_levels = [np.zeros((1, 32), np.uint8)]
+    nkids = []            # per level: children count of each node of that level
+    frontier = desc_levels[0]
+    for depth in range(L):
+        m = len(frontier)
+        if depth == 0:
+            kk = np.full(1, k)
+        else:
+            kk = rng.integers(max(2, k - 3) if kmin is None else kmin, k + 1, m)
+            kk[rng.random(m) < leaf_early] = 0
+        nkids.append(kk)
+        parent = np.repeat(np.arange(m), kk)
+        if depth == 0:
+            child = rng.integers(0, 256, (len(parent), 32), dtype=np.uint8)
+        else:
+            bits = np.unpackbits(frontier[parent], axis=1) ^ (rng.random((len(parent), 256)) < flip)
+            child = np.packbits(bits.astype(np.uint8), axis=1)
+        desc_levels.append(child)
+        frontier = child
+    nkids.append(np.zeros(len(frontier), np.int64))
+    counts = np.concatenate(nkids).astype(np.int64)
+    n = len(counts)
+    child_begin = np.zeros(n + 1, np.int64)
+    child_begin[1:] = np.cumsum(counts)
+    child_begin += 0
+    # breadth-first numbering: node i's children are nodes 1 + child_begin[i] ...
+    child_idx = np.arange(1, 1 + child_begin[-1], dtype=np.int32)
+    desc = np.concatenate(desc_levels)
+    assert len(desc) == n
     word_id = np.full(n, -1, np.int32)
     weight = np.zeros(n, np.float64)
-    leaves = [i for i in range(1, n) if not children[i]]
-    for w, node in enumerate(leaves):
-        word_id[node] = w
-        weight[node] = 0.0 if rng.random() < stop_frac else float(rng.uniform(0.2, 6.0))
-    return dict(k=k, L=L, weighting=weighting, scoring=scoring, child_begin=child_begin,
-                child_idx=np.array(child_idx, np.int32), desc=np.stack(desc), word_id=word_id, weight=weight,
-                leaves=np.array(leaves, np.int32))
+    leaves = np.flatnonzero(counts == 0)
+    leaves = leaves[leaves != 0]
+    word_id[leaves] = np.arange(len(leaves), dtype=np.int32)
+    weight[leaves] = np.where(rng.random(len(leaves)) < stop_frac, 0.0, rng.uniform(0.2, 6.0, len(leaves)))
+    return dict(k=k, L=L, weighting=weighting, scoring=scoring, child_begin=child_begin.astype(np.int32),
+                child_idx=child_idx, desc=desc, word_id=word_id, weight=weight, leaves=leaves.astype(np.int32))
 
 
 def bow_descriptors(voc: dict, n: int, seed: int = 12, noise: float = 0.08):
