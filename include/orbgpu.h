@@ -220,6 +220,37 @@ int orb_search_by_projection_local(orb_matcher_t m, const orb_frame_view_t* fram
                                    const orb_local_points_t* pts, float th, int far_points, float th_far_points,
                                    int32_t* match, int32_t* n_matches);
 
+/* ---- Frame::isInFrustum (src/Frame.cc:667-773, pinhole, Nleft == -1) + MapPoint::PredictScale
+ * (src/MapPoint.cc:715-731): the tracking fields of the local map points that
+ * orb_search_by_projection_local reads.  Per point: Pc = Rcw P + tcw, depth > 0, projection inside
+ * [mnMinX, mnMaxX] x [mnMinY, mnMaxY], distance to mOw inside [0.8 mfMinDistance, 1.2 mfMaxDistance],
+ * viewing cosine against the normal >= viewingCosLimit, predicted level ceil(log(mfMaxDistance /
+ * dist) / mfLogScaleFactor) clamped to [0, mnScaleLevels).  Float arithmetic as the reference build
+ * contracts it (see oracle/orb_frustum_oracle.cpp). */
+typedef struct orb_frustum_frame {
+    float Tcw[12];              /* [mRcw | mtcw], row-major 3 x 4 */
+    float Ow[3];                /* mOw (camera centre) */
+    float fx, fy, cx, cy, bf;   /* pinhole parameters, mbf */
+    float min_x, max_x, min_y, max_y;  /* mnMinX, mnMaxX, mnMinY, mnMaxY */
+    float log_scale_factor;     /* mfLogScaleFactor */
+    int32_t n_levels;           /* mnScaleLevels */
+} orb_frustum_frame_t;
+
+/* Host arrays: pos / normal n x 3 (GetWorldPos, GetNormal), min_dist / max_dist (mfMinDistance,
+ * mfMaxDistance).  Writes in_view (mbTrackInView), proj n x 3 (mTrackProjX, mTrackProjY -- also set,
+ * as in the reference, when only the distance / angle tests fail; -1 before the image test --
+ * and mTrackProjXR), depth (mTrackDepth), level (mnTrackScaleLevel), view_cos (mTrackViewCos);
+ * fields the reference leaves untouched for rejected points are written as 0.  Synchronous;
+ * returns the number of points in view. */
+int orb_is_in_frustum(const orb_frustum_frame_t* frame, int n, const float* pos, const float* normal,
+                      const float* min_dist, const float* max_dist, float viewing_cos_limit, uint8_t* in_view,
+                      float* proj, float* depth, int32_t* level, float* view_cos);
+/* The same on device arrays, async on `stream`. */
+int orb_is_in_frustum_device(const orb_frustum_frame_t* frame, int n, const float* d_pos, const float* d_normal,
+                             const float* d_min_dist, const float* d_max_dist, float viewing_cos_limit,
+                             uint8_t* d_in_view, float* d_proj, float* d_depth, int32_t* d_level, float* d_view_cos,
+                             void* stream);
+
 /* ---- Frame::ComputeStereoMatches (src/Frame.cc:1102-1358) ------------------------------------ */
 
 /* Stereo matching of a rectified pair, on the two extractors' device pyramids (mvImagePyramid of

@@ -40,6 +40,7 @@ _PROTOS = {
     "oracle_search_by_projection_frame": (_i, [_vp, _vp, _f, _i, _i, _vp]),
     "oracle_search_by_projection_local": (_i, [_vp, _vp, _vp, _f, _i, _f, _f, _vp]),
     "oracle_pose_optimization": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
+    "oracle_is_in_frustum": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp]),
     "oracle_bow_transform": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "oracle_compute_stereo_matches": (_i, [_vp, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _f, _f,
                                            _vp, _vp]),
@@ -314,3 +315,20 @@ def bow_transform(voc: dict, desc, levelsup: int = 4):
     bow = {int(bw[i]): float(bv[i]) for i in range(int(nw[0]))}
     fv = {int(fn[j]): [int(x) for x in ff[fb[j]:fb[j + 1]]] for j in range(int(nn[0]))}
     return bow, fv
+
+
+def is_in_frustum(frame, pos, normal, min_dist, max_dist, viewing_cos_limit=0.5):
+    """Oracle Frame::isInFrustum (oracle/orb_frustum_oracle.cpp).  frame: an orb_frustum_frame_t
+    ctypes structure.  Returns the same dict of tracking fields as the product's is_in_frustum."""
+    P = np.ascontiguousarray(pos, np.float32).reshape(-1, 3)
+    n = len(P)
+    m = max(n, 1)
+    out = dict(track_in_view=np.zeros(m, np.uint8), track_proj=np.zeros((m, 3), np.float32),
+               track_depth=np.zeros(m, np.float32), track_level=np.zeros(m, np.int32),
+               track_view_cos=np.zeros(m, np.float32))
+    arrs = [np.ascontiguousarray(a, np.float32) for a in (normal, min_dist, max_dist)]
+    load().oracle_is_in_frustum(ctypes.addressof(frame), n, P.ctypes.data, *[a.ctypes.data for a in arrs],
+                                float(viewing_cos_limit), *[out[k].ctypes.data for k in ("track_in_view", "track_proj",
+                                                                                           "track_depth", "track_level",
+                                                                                           "track_view_cos")])
+    return {k: v[:n] for k, v in out.items()}

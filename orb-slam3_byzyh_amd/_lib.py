@@ -96,6 +96,8 @@ PROTOTYPES = {
                                                      _vp, _vp, _vp]),
     "orb_pose_optimization": (_i, [_i, _vp, _i, _vp, _vp, _vp, _vp]),
     "orb_pose_optimization_device": (_i, [_i, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
+    "orb_is_in_frustum": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp]),
+    "orb_is_in_frustum_device": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _vp]),
     "orb_vocabulary_create": (_i, [_vp, ctypes.POINTER(_vp)]),
     "orb_vocabulary_destroy": (_i, [_vp]),
     "orb_bow_transform": (_i, [_vp, _vp, _i, _i, _vp, _vp, _ip, _vp, _vp, _vp, _ip]),

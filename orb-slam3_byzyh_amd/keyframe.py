@@ -150,3 +150,40 @@ class LocalMapPoints:
     def view(self) -> LocalPointsView:
         self._v = LocalPointsView(self.n, *[_ptr(getattr(self, k)) for k, _ in self._fields])
         return self._v
+
+
+class FrustumFrame(ctypes.Structure):  # orb_frustum_frame_t
+    _fields_ = [("Tcw", ctypes.c_float * 12), ("Ow", ctypes.c_float * 3), ("fx", ctypes.c_float), ("fy", ctypes.c_float),
+                ("cx", ctypes.c_float), ("cy", ctypes.c_float), ("bf", ctypes.c_float), ("min_x", ctypes.c_float),
+                ("max_x", ctypes.c_float), ("min_y", ctypes.c_float), ("max_y", ctypes.c_float),
+                ("log_scale_factor", ctypes.c_float), ("n_levels", ctypes.c_int32)]
+
+
+def frustum_frame(Tcw, Ow, camera, bf, bounds, scale_factor: float = 1.2, n_levels: int = 8) -> FrustumFrame:
+    """orb_frustum_frame_t of a Frame: Tcw 3x4 (mRcw | mtcw), Ow = mOw, camera (fx, fy, cx, cy), mbf,
+    bounds (mnMinX, mnMaxX, mnMinY, mnMaxY); mfLogScaleFactor = log(mfScaleFactor) stored as float."""
+    T = np.asarray(Tcw, np.float32).reshape(12)
+    lsf = np.float32(np.log(np.float64(np.float32(scale_factor))))
+    return FrustumFrame((ctypes.c_float * 12)(*T), (ctypes.c_float * 3)(*np.asarray(Ow, np.float32)), *[float(c) for c in camera],
+                        float(bf), *[float(b) for b in bounds], float(lsf), int(n_levels))
+
+
+def is_in_frustum(frame: FrustumFrame, pos, normal, min_dist, max_dist, viewing_cos_limit: float = 0.5) -> dict:
+    """Frame::isInFrustum (src/Frame.cc:667-773) for n map points on the GPU.  Returns the tracking
+    fields LocalMapPoints takes: track_in_view, track_proj (n x 3), track_depth, track_level,
+    track_view_cos (fields of rejected points as documented in include/orbgpu.h)."""
+    from . import _lib
+    from ._lib import check
+    P = np.ascontiguousarray(pos, np.float32).reshape(-1, 3)
+    n = len(P)
+    Nn = np.ascontiguousarray(normal, np.float32).reshape(-1, 3)
+    mn = np.ascontiguousarray(min_dist, np.float32)
+    mx = np.ascontiguousarray(max_dist, np.float32)
+    out = dict(track_in_view=np.zeros(max(n, 1), np.uint8), track_proj=np.zeros((max(n, 1), 3), np.float32),
+               track_depth=np.zeros(max(n, 1), np.float32), track_level=np.zeros(max(n, 1), np.int32),
+               track_view_cos=np.zeros(max(n, 1), np.float32))
+    check(_lib.load().orb_is_in_frustum(ctypes.byref(frame), n, _ptr(P), _ptr(Nn), _ptr(mn), _ptr(mx),
+                                        float(viewing_cos_limit), _ptr(out["track_in_view"]), _ptr(out["track_proj"]),
+                                        _ptr(out["track_depth"]), _ptr(out["track_level"]), _ptr(out["track_view_cos"])),
+          "orb_is_in_frustum")
+    return {k: v[:n] for k, v in out.items()}

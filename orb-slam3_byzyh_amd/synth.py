@@ -511,3 +511,37 @@ def bow_descriptors(voc: dict, n: int, seed: int = 12, noise: float = 0.08):
     pick = voc["desc"][leaves[rng.integers(0, len(leaves), n)]]
     bits = np.unpackbits(pick, axis=1) ^ (rng.random((n, 256)) < noise)
     return np.packbits(bits.astype(np.uint8), axis=1)
+
+
+def frustum_points(n: int = 3000, seed: int = 61, width: int = 752, height: int = 480, nlevels: int = 8):
+    """Local map points around a tracking frame for Frame::isInFrustum: most in front and inside the
+    image, some behind the camera, outside the image, outside their scale-invariance distance range
+    or seen at a grazing angle.  mfMaxDistance / mfMinDistance as MapPoint::UpdateNormalAndDepth sets
+    them (dist * levelScaleFactor, / scaleFactors[nLevels - 1]).  Returns (Tcw 3x4, Ow, pos, normal,
+    min_dist, max_dist), float32."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = EUROC_K
+    scale, _ = scale_tables(nlevels)
+    Rcw = _rot_yaw_pitch(rng.uniform(-0.5, 0.5), rng.uniform(-0.2, 0.2))
+    tcw = rng.normal(0, 1.0, 3)
+    Ow = -Rcw.T @ tcw
+    z = rng.uniform(0.5, 20.0, n)
+    u = rng.uniform(-150, width + 150, n)
+    v = rng.uniform(-100, height + 100, n)
+    Xc = np.stack([(u - cx) * z / fx, (v - cy) * z / fy, z], 1)
+    behind = rng.random(n) < 0.05
+    Xc[behind, 2] *= -1
+    P = (Xc - tcw) @ Rcw  # Rcw^T (Xc - t)
+    view = P - Ow
+    d = np.linalg.norm(view, axis=1)
+    nrm = view / d[:, None]
+    tilt = rng.random(n) < 0.15  # the reference keyframes saw the point from elsewhere
+    nrm[tilt] = nrm[tilt] + rng.normal(0, 0.8, (int(tilt.sum()), 3))
+    nrm /= np.linalg.norm(nrm, axis=1)[:, None]
+    ref = d * rng.uniform(0.6, 1.6, n)  # distance from the reference keyframe
+    lvl = rng.integers(0, nlevels, n)
+    max_dist = ref * scale[lvl]
+    min_dist = max_dist / scale[nlevels - 1]
+    Tcw = np.concatenate([Rcw, tcw[:, None]], 1)
+    f32 = lambda a: np.ascontiguousarray(a, np.float32)
+    return f32(Tcw), f32(Ow), f32(P), f32(nrm), f32(min_dist), f32(max_dist)
