@@ -331,6 +331,65 @@ def bench_bow(pkg, synth, dev, steps, cpu_baseline_on, n_frames=64, n_feat=1000)
     return out
 
 
+def bench_single_frame(pkg, synth, cpu_baseline_on, reps=50):
+    """Tracking's own call pattern: ORBextractor::operator() on ONE host frame (PCIe-inclusive:
+    upload, extraction, download of keypoints and descriptors), 640x480 and EuRoC 752x480; the
+    latency the tracking thread sees, next to the oracle on one core."""
+    import numpy as np
+    out = {}
+    for (w, h, nf) in ((640, 480, 1000), (752, 480, 1200)):
+        img = synth.polygon_frame(w, h, seed=7)
+        ex = pkg.ORBextractor(nf, 1.2, 8, 20, 7, max_width=w, max_height=h)
+        for _ in range(5):
+            ex(img, None, (0, 0))
+        t = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            ex(img, None, (0, 0))
+            t.append((time.perf_counter() - t0) * 1e3)
+        key = f"{w}x{h}"
+        out[key] = {"median_ms": round(float(np.median(t)), 4), "p90_ms": round(float(np.percentile(t, 90)), 4)}
+        if cpu_baseline_on:
+            from oracle import oracle as oracle_mod
+            o = oracle_mod.OracleExtractor(nf, 1.2, 8, 20, 7)
+            tc = []
+            for _ in range(10):
+                t0 = time.perf_counter()
+                o(img, (0, 0))
+                tc.append((time.perf_counter() - t0) * 1e3)
+            out[key]["cpu_port_median_ms"] = round(float(np.median(tc)), 4)
+    out["note"] = "host image in, host keypoints/descriptors out (orb_extract, synchronous); cpu: the oracle, 1 thread"
+    return out
+
+
+def bench_c4(pkg, synth, dev, steps, n_frames=32):
+    """C4's per-GPU shard: 32 frames of 1280x720 (nFeatures 1000) per step, device-resident (the
+    8-GPU run all-gathers the features of every shard; see the main line's N > 1 path)."""
+    import numpy as np
+    import torch
+    frames = np.stack([synth.polygon_frame(1280, 720, seed=1000 + i) for i in range(n_frames)])
+    imgs = torch.from_numpy(frames).to(dev)
+    ex = pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=1280, max_height=720, max_batch=n_frames)
+    cap = 1000 + 16 * 8
+    out = (torch.empty((n_frames, cap, 7), dtype=torch.float32, device=dev),
+           torch.empty((n_frames, cap, 32), dtype=torch.uint8, device=dev),
+           torch.empty((n_frames, 2), dtype=torch.int32, device=dev))
+    st = torch.cuda.current_stream(dev)
+    for _ in range(3):
+        ex.extract_batch_device(imgs, (0, 1000), cap=cap, out=out, stream=st)
+    torch.cuda.synchronize(dev)
+    nfeat = int(out[2][:, 0].sum().item())
+    reps = max(5, min(steps, 20))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ex.extract_batch_device(imgs, (0, 1000), cap=cap, out=out, stream=st)
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) * 1e3
+    return {"config": f"C4 shard: {n_frames} synthetic 1280x720 frames per GPU per step, nFeatures 1000, 8 levels",
+            "features_per_ms": round(nfeat * reps / dt, 3), "frames_per_ms": round(n_frames * reps / dt, 3),
+            "ms_per_step": round(dt / reps, 4)}
+
+
 def pmc_traffic():
     p = ROOT / "profiles" / "pmc_latest.json"
     if p.exists():
@@ -353,6 +412,8 @@ def main():
     ap.add_argument("--no-stereo", action="store_true", help="skip the stereo stream (C3) measurement")
     ap.add_argument("--no-pose", action="store_true", help="skip the PoseOptimization measurement")
     ap.add_argument("--no-bow", action="store_true", help="skip the DBoW2 transform measurement")
+    ap.add_argument("--no-single", action="store_true", help="skip the single-frame latency measurement")
+    ap.add_argument("--no-c4", action="store_true", help="skip the 1280x720 (C4 shard) measurement")
     args = ap.parse_args()
 
     import numpy as np
@@ -504,7 +565,23 @@ def main():
             bow = bench_bow(pkg, synth, dev, args.steps, not args.no_cpu_baseline)
         except Exception as e:  # noqa: BLE001
             bow = {"error": repr(e)}
+    single = None
+    if not args.no_single and world == 1:
+        try:
+            single = bench_single_frame(pkg, synth, not args.no_cpu_baseline)
+        except Exception as e:  # noqa: BLE001
+            single = {"error": repr(e)}
+    c4 = None
+    if not args.no_c4 and world == 1:
+        try:
+            c4 = bench_c4(pkg, synth, dev, args.steps)
+        except Exception as e:  # noqa: BLE001
+            c4 = {"error": repr(e)}
     if rank == 0:
+        if c4 is not None:
+            result["c4_shard"] = c4
+        if single is not None:
+            result["single_frame_latency"] = single
         if pose is not None:
             result["pose_optimization"] = pose
         if bow is not None:
