@@ -33,9 +33,18 @@ using namespace orbgpu;
 
 namespace {
 
-__constant__ int c_pattern[1024] = {
+constexpr int kPatternSrc[1024] = {
 #include "orb_pattern31.inc"
 };
+// test j -> one dword of 4 signed bytes (x0, y0, x1, y1); every coordinate is in [-13, 12]
+struct PackedPattern { uint32_t w[256]; };
+constexpr PackedPattern pack_pattern() {
+    PackedPattern p{};
+    for (int j = 0; j < 256; ++j)
+        for (int c = 0; c < 4; ++c) p.w[j] |= (uint32_t)(uint8_t)(int8_t)kPatternSrc[4 * j + c] << (8 * c);
+    return p;
+}
+__constant__ PackedPattern c_pattern_packed = pack_pattern();
 
 __constant__ uint32_t c_sincos_exc[][3] = {
 #include "orb_sincos_exceptions.inc"
@@ -63,6 +72,16 @@ __device__ __forceinline__ void wave_sync() {
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 __device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
+// Sum over each 32-lane half of the wave, result in every lane of the half: DPP within the rows of 16
+// (quad_perm xor 1 / xor 2, row_ror 4 / 8), then one ds_swizzle (xor 16 inside each 32-lane group),
+// instead of five dependent ds_bpermute round trips.
+__device__ __forceinline__ int half_wave_sum(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false);  // row_ror:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    return v + __builtin_amdgcn_ds_swizzle(v, 0x401F);                // bitmask mode: lane ^ 16
+}
 __device__ __forceinline__ int rank_in(unsigned long long m) {  // set lanes below this one
     return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
 }
@@ -1540,15 +1559,29 @@ __global__ __launch_bounds__(64) void k_quadtree(const KernelGeom* __restrict__ 
 // ================================================================================================
 // 5. IC_Angle + steered rBRIEF, src:91-138, 150-203, 1534-1547, 1656-1676
 // ================================================================================================
-__device__ __forceinline__ void steer_sincos(float ang, float* s, float* c) {
+// The exception keys live in registers (kExcPerLane per lane, loaded at kernel entry), so the lookup
+// is a compare + half-wave ballot; only a hit (rare) reads the table again.
+constexpr int kExcPerLane = (kNumSincosExc + 31) / 32;
+// kLds: the (cos, sin) bits of the exceptions are in LDS (lds_cs), else read from the constant table.
+template <bool kLds = false>
+__device__ __forceinline__ void steer_sincos(float ang, const uint32_t (&exc)[kExcPerLane], int half, int hl,
+                                             float* s, float* c, const uint2* lds_cs = nullptr) {
     orb_det_sincosf(ang, s, c);
     const uint32_t bits = __float_as_uint(ang);
-    int lo = 0, hi = kNumSincosExc - 1;
-    while (lo <= hi) {
-        const int mid = (lo + hi) >> 1;
-        const uint32_t m = c_sincos_exc[mid][0];
-        if (m == bits) { *c = __uint_as_float(c_sincos_exc[mid][1]); *s = __uint_as_float(c_sincos_exc[mid][2]); return; }
-        if (m < bits) lo = mid + 1; else hi = mid - 1;
+    int idx = -1;
+#pragma unroll
+    for (int e = 0; e < kExcPerLane; ++e)
+        if (32 * e + hl < kNumSincosExc && exc[e] == bits) idx = 32 * e + hl;
+    const uint32_t hm = (uint32_t)(ballot(idx >= 0) >> (32 * (half & 1)));
+    if (hm) {
+        const int hit = __shfl(idx, 32 * (half & 1) + __builtin_ctz(hm), 64);
+        if constexpr (kLds) {
+            *c = __uint_as_float(lds_cs[hit].x);
+            *s = __uint_as_float(lds_cs[hit].y);
+        } else {
+            *c = __uint_as_float(c_sincos_exc[hit][1]);
+            *s = __uint_as_float(c_sincos_exc[hit][2]);
+        }
     }
 }
 
@@ -1559,6 +1592,7 @@ constexpr int kDescKpPerBlock = 8;
 constexpr int kPB = 37, kPBW = 10;  // blurred patch rows, dwords per row
 constexpr int kPU = 31, kPUW = 9;   // disc box rows, dwords per row
 constexpr int kDescLds = kPB * kPBW * 4 + kPU * kPUW * 4;  // 2596 bytes per keypoint
+constexpr int kBufDword3 = 0x00020000;  // gfx9 buffer resource word 3 (32-bit data format)
 
 __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__ gp, const uint8_t* __restrict__ pyr,
                                                   const uint8_t* __restrict__ blur, const uint32_t* __restrict__ sel,
@@ -1569,11 +1603,31 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
     const KernelGeom& g = *gp;
     __shared__ __attribute__((aligned(16))) uint32_t patch[kDescKpPerBlock][(kDescLds + 15) / 16 * 4];
     const int half = threadIdx.x >> 5, hl = threadIdx.x & 31;
-    const int slot = blockIdx.x * kDescKpPerBlock + half, level = blockIdx.y, f = blockIdx.z;
+    // blockIdx.x -> (level, chunk): level l owns ceil(sel_cap_l / 8) blocks, so the grid holds no block
+    // beyond a level's capacity (scalar walk over the levels)
+    int level = 0, chunk = blockIdx.x;
+#pragma unroll
+    for (int l = 0; l + 1 < kMaxLevels; ++l) {
+        const int c = (g.lv[l].sel_cap + kDescKpPerBlock - 1) / kDescKpPerBlock;
+        if (l + 1 < g.nlevels && level == l && chunk >= c) { chunk -= c; level = l + 1; }
+    }
+    const int slot = chunk * kDescKpPerBlock + half, f = blockIdx.y;
+    const LevelGeom& L = g.lv[level];
+    // Every load that does not depend on the key is issued here, in one round trip with the key itself:
+    // the key and its rank are read speculatively at a clamped (in-bounds) slot, and the rBRIEF pattern
+    // and sincos exception keys go to registers.
+    const size_t sbase = (size_t)f * g.sel_frame_cap + L.sel_off + (slot < L.sel_cap ? slot : L.sel_cap - 1);
+    const uint32_t key_spec = L.sel_cap > 0 ? sel[sbase] : 0u;
+    const int rk_spec = L.sel_cap > 0 ? rank_in_class[sbase] : 0;
     // per-frame totals over the levels (src:1586-1591) and this level's class bases (src:1613-1676)
     const int li = hl & 15;
     const int cnt_l = li < g.nlevels ? sel_count[(size_t)f * g.nlevels + li] : 0;
     const int lap_l = li < g.nlevels ? lap_count[(size_t)f * g.nlevels + li] : 0;
+    uint32_t pat[8], exc[kExcPerLane];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) pat[m] = c_pattern_packed.w[32 * m + hl];
+#pragma unroll
+    for (int e = 0; e < kExcPerLane; ++e) exc[e] = 32 * e + hl < kNumSincosExc ? c_sincos_exc[32 * e + hl][0] : 0u;
     int total = cnt_l, lap_before = li < level ? lap_l : 0, mono_before = li < level ? cnt_l - lap_l : 0;
 #pragma unroll
     for (int o = 8; o > 0; o >>= 1) {  // within each 16-lane group
@@ -1582,81 +1636,79 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
         mono_before += __shfl_xor(mono_before, o, 64);
     }
     const int n = __shfl(cnt_l, (threadIdx.x & ~15) + level, 64);
-    if (blockIdx.x == 0 && level == 0 && threadIdx.x == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
         int mono = 0;
         for (int l = 0; l < g.nlevels; ++l)
             mono += sel_count[(size_t)f * g.nlevels + l] - lap_count[(size_t)f * g.nlevels + l];
         counts[2 * f] = total;
         counts[2 * f + 1] = total > cap ? ORB_ERR_CAPACITY : mono;
     }
-    if (blockIdx.x * kDescKpPerBlock >= n) return;           // whole block idle
+    if (chunk * kDescKpPerBlock >= n) return;                // whole block idle
     const bool active = slot < n && total <= cap;            // frame within the caller's capacity
-    const LevelGeom& L = g.lv[level];
-    const uint32_t key = active ? sel[(size_t)f * g.sel_frame_cap + L.sel_off + slot] : 0;
+    const uint32_t key = active ? key_spec : 0;
     const int x = key_x(key) + L.minB, y = key_y(key) + L.minB;
-    const size_t cofs = (size_t)f * g.pyr_frame_bytes + L.plane_off + (size_t)(y + kEdge) * L.pitch + (x + kEdge);
-    // ---- stage both patches (over-reads stay inside the padded planes)
-    const uint8_t* b0 = blur + cofs - (size_t)18 * L.pitch - 18;
-    const uint8_t* u0 = pyr + cofs - (size_t)kHalfPatch * L.pitch - kHalfPatch;
-    const int bsh = (int)((uintptr_t)b0 & 3), ush = (int)((uintptr_t)u0 & 3);
-    const uint32_t* bw = reinterpret_cast<const uint32_t*>(b0 - bsh);
-    const uint32_t* uw = reinterpret_cast<const uint32_t*>(u0 - ush);
-    const int pw = L.pitch >> 2;
+    // ---- stage both patches.  Lane (r, w) of a half-wave loads word w of row r of a 3-row group, so
+    // load k reads rows 3k..3k+2 at a per-lane offset computed once plus 3k rows in soffset (raw buffer
+    // loads, plane base in the resource): 10 words x 3 rows of the blurred patch (30 lanes), 9 x 3 of
+    // the disc box (27).  Rows past the patch and idle lanes over-read inside the padded planes and
+    // are not stored.
+    constexpr int kBL = (kPB + 2) / 3, kUL = (kPU + 2) / 3;
+    const int sb = hl / kPBW, cb = hl % kPBW, su = hl / kPUW, cu = hl % kPUW;
+    const size_t plane = (size_t)f * g.pyr_frame_bytes + L.plane_off;
+    const uint8_t* bp = blur + plane;
+    const uint8_t* up = pyr + plane;
+    const int bo = (y + kEdge - 18) * L.pitch + (x + kEdge - 18);
+    const int uo = (y + kEdge - kHalfPatch) * L.pitch + (x + kEdge - kHalfPatch);
+    const int bsh = (int)(((uintptr_t)bp + bo) & 3), ush = (int)(((uintptr_t)up + uo) & 3);
+    const uint32_t vob = (uint32_t)(bo - bsh + sb * L.pitch + 4 * cb);
+    const uint32_t vou = (uint32_t)(uo - ush + su * L.pitch + 4 * cu);
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(bp), (short)0, 0x7fffffff, kBufDword3);
+    const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(up), (short)0, 0x7fffffff, kBufDword3);
     uint32_t* P = patch[half];
-    uint32_t vb[(kPB * kPBW + 31) / 32], vu[(kPU * kPUW + 31) / 32];
+    uint32_t vb[kBL], vu[kUL];
     if (active) {
 #pragma unroll
-        for (int k = 0; k < (kPB * kPBW + 31) / 32; ++k) {
-            const int i = 32 * k + hl;
-            vb[k] = i < kPB * kPBW ? bw[(size_t)(i / kPBW) * pw + i % kPBW] : 0u;
-        }
+        for (int k = 0; k < kBL; ++k) vb[k] = __builtin_amdgcn_raw_buffer_load_b32(rb, vob, 3 * k * L.pitch, 0);
 #pragma unroll
-        for (int k = 0; k < (kPU * kPUW + 31) / 32; ++k) {
-            const int i = 32 * k + hl;
-            vu[k] = i < kPU * kPUW ? uw[(size_t)(i / kPUW) * pw + i % kPUW] : 0u;
-        }
+        for (int k = 0; k < kUL; ++k) vu[k] = __builtin_amdgcn_raw_buffer_load_b32(ru, vou, 3 * k * L.pitch, 0);
 #pragma unroll
-        for (int k = 0; k < (kPB * kPBW + 31) / 32; ++k) {
-            const int i = 32 * k + hl;
-            if (i < kPB * kPBW) P[i] = vb[k];
-        }
+        for (int k = 0; k < kBL; ++k)
+            if (hl < 3 * kPBW && 3 * k + sb < kPB) P[3 * kPBW * k + hl] = vb[k];
 #pragma unroll
-        for (int k = 0; k < (kPU * kPUW + 31) / 32; ++k) {
-            const int i = 32 * k + hl;
-            if (i < kPU * kPUW) P[kPB * kPBW + i] = vu[k];
-        }
+        for (int k = 0; k < kUL; ++k)
+            if (hl < 3 * kPUW && 3 * k + su < kPU) P[kPB * kPBW + 3 * kPUW * k + hl] = vu[k];
     }
     __syncthreads();
     const uint8_t* PB = reinterpret_cast<const uint8_t*>(P) + bsh + 18 * (kPBW * 4) + 18;  // blurred centre
     const uint8_t* PU = reinterpret_cast<const uint8_t*>(P + kPB * kPBW) + ush + kHalfPatch * (kPUW * 4) + kHalfPatch;
-    // ---- IC_Angle on the unblurred level (src:91-138): lane = disc column u
-    const int u = hl - kHalfPatch;
-    int m10 = 0, m01 = 0;
-    if (active && hl < 2 * kHalfPatch + 1) {
+    // ---- IC_Angle on the unblurred level (src:91-138): lane = disc column u, so m10 = u * (column sum).
+    // The reads are unconditional (the whole 31x31 box is staged; lane 31, u = 16, lies outside every
+    // disc row) and the disc mask is a select, so the 31 LDS reads issue back to back.
+    const int u = hl - kHalfPatch, au = u < 0 ? -u : u;
+    int colsum = 0, m01 = 0;
 #pragma unroll
-        for (int v = -kHalfPatch; v <= kHalfPatch; ++v) {
-            const int d = g.umax[v < 0 ? -v : v];
-            const int val = (u >= -d && u <= d) ? PU[v * (kPUW * 4) + u] : 0;
-            m10 += u * val;
-            m01 += v * val;
-        }
+    for (int v = -kHalfPatch; v <= kHalfPatch; ++v) {
+        const int raw = PU[v * (kPUW * 4) + u];
+        const int val = au <= g.umax[v < 0 ? -v : v] ? raw : 0;
+        colsum += val;
+        m01 += v * val;
     }
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) {  // stays inside the 32-lane half
-        m10 += __shfl_xor(m10, o, 64);
-        m01 += __shfl_xor(m01, o, 64);
-    }
+    int m10 = u * colsum;
+    if (!active) m10 = m01 = 0;
+    m10 = half_wave_sum(m10);
+    m01 = half_wave_sum(m01);
     const float angle = orb_fast_atan2((float)m01, (float)m10);
     // ---- steered BRIEF on the blurred level (src:150-203)
     const float ang = angle * (float)(3.14159265358979323846 / 180.f);
     float a, b;
-    steer_sincos(ang, &b, &a);  // a = cos, b = sin
+    steer_sincos(ang, exc, half, hl, &b, &a);  // a = cos, b = sin
     int t0[8], t1[8];
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
-        const int j = 32 * m + hl;  // test j -> byte j/8, bit j%8 (src:173-199)
-        const float px0 = (float)c_pattern[4 * j], py0 = (float)c_pattern[4 * j + 1];
-        const float px1 = (float)c_pattern[4 * j + 2], py1 = (float)c_pattern[4 * j + 3];
+        // test j = 32 m + hl -> byte j/8, bit j%8 (src:173-199)
+        const int pw4 = (int)pat[m];
+        const float px0 = (float)((pw4 << 24) >> 24), py0 = (float)((pw4 << 16) >> 24);
+        const float px1 = (float)((pw4 << 8) >> 24), py1 = (float)(pw4 >> 24);
         const int r0 = (int)__builtin_rintf(__builtin_fmaf(px0, b, py0 * a));
         const int c0 = (int)__builtin_rintf(__builtin_fmaf(px0, a, -(py0 * b)));
         const int r1 = (int)__builtin_rintf(__builtin_fmaf(px1, b, py1 * a));
@@ -1668,7 +1720,7 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
 #pragma unroll
     for (int m = 0; m < 8; ++m) words[m] = (uint32_t)(ballot(t0[m] < t1[m]) >> (32 * (half & 1)));
     if (!active) return;
-    const int rk = rank_in_class[(size_t)f * g.sel_frame_cap + L.sel_off + slot];
+    const int rk = rk_spec;
     const int dst = rk < 0 ? total - 1 - (lap_before + (-rk - 1)) : mono_before + rk;
     if (hl < 8) {
         uint32_t w = words[0];
@@ -2096,8 +2148,12 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     launch_qt(0, k.nlevels, st);
     mark(3);
     mark(4);
-    hipLaunchKernelGGL(k_describe, dim3((G.max_sel + kDescKpPerBlock - 1) / kDescKpPerBlock, k.nlevels, n), dim3(256), 0,
-                       st, e->d_geom, pyr, blr, sel, scount, dst, lapc, cap, kps, desc, counts);
+    {
+        int chunks = 0;  // blocks per frame: ceil(sel_cap_l / 8) per level (see k_describe)
+        for (int l = 0; l < k.nlevels; ++l) chunks += (k.lv[l].sel_cap + kDescKpPerBlock - 1) / kDescKpPerBlock;
+        hipLaunchKernelGGL(k_describe, dim3(chunks, n), dim3(256), 0, st, e->d_geom, pyr, blr, sel, scount, dst, lapc,
+                           cap, kps, desc, counts);
+    }
     mark(5);
     if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "kernel launch failed");
     return ORB_OK;
