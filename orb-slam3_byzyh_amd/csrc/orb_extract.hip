@@ -87,9 +87,41 @@ __device__ __forceinline__ int rank_in(unsigned long long m) {  // set lanes bel
 }
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Wave-wide sum (result uniform): DPP row sums (quad_perm xor 1 / xor 2, row_ror 4 / 8), then the
+// four row totals by readlane -- no ds_bpermute round trips.
 __device__ __forceinline__ int wave_sum(int v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false);  // row_ror:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+           __builtin_amdgcn_readlane(v, 48);
+}
+// Inclusive wave scans (GFX9 DPP): row_shr 1/2/3 on the input, row_shr 4 / 8 under bank masks, then
+// row_bcast 15 / 31 across the rows.
+__device__ __forceinline__ int wave_incl_scan_dpp(int v) {
+    int s = v;
+    s += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    s += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    s += __builtin_amdgcn_update_dpp(0, v, 0x113, 0xF, 0xF, false);  // row_shr:3
+    s += __builtin_amdgcn_update_dpp(0, s, 0x114, 0xF, 0xE, false);  // row_shr:4, banks 1-3
+    s += __builtin_amdgcn_update_dpp(0, s, 0x118, 0xF, 0xC, false);  // row_shr:8, banks 2-3
+    s += __builtin_amdgcn_update_dpp(0, s, 0x142, 0xA, 0xF, false);  // row_bcast:15, rows 1, 3
+    s += __builtin_amdgcn_update_dpp(0, s, 0x143, 0xC, 0xF, false);  // row_bcast:31, rows 2, 3
+    return s;
+}
+// max-scan (INT_MIN is the identity for the lanes a DPP step leaves out)
+__device__ __forceinline__ int wave_incl_max_dpp(int v) {
+    constexpr int kId = -2147483647 - 1;
+    int s = v;
+    s = max(s, __builtin_amdgcn_update_dpp(kId, v, 0x111, 0xF, 0xF, false));
+    s = max(s, __builtin_amdgcn_update_dpp(kId, v, 0x112, 0xF, 0xF, false));
+    s = max(s, __builtin_amdgcn_update_dpp(kId, v, 0x113, 0xF, 0xF, false));
+    s = max(s, __builtin_amdgcn_update_dpp(kId, s, 0x114, 0xF, 0xE, false));
+    s = max(s, __builtin_amdgcn_update_dpp(kId, s, 0x118, 0xF, 0xC, false));
+    s = max(s, __builtin_amdgcn_update_dpp(kId, s, 0x142, 0xA, 0xF, false));
+    s = max(s, __builtin_amdgcn_update_dpp(kId, s, 0x143, 0xC, 0xF, false));
+    return s;
 }
 
 // ================================================================================================
@@ -937,14 +969,7 @@ __device__ __forceinline__ void split_point(const QGen& G, int p, int& sx, int& 
     sy = y0 + ((y1 - y0 + 1) >> 1);
 }
 
-__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
-    return v;
-}
+__device__ __forceinline__ int wave_incl_scan(int v, int) { return wave_incl_scan_dpp(v); }
 
 // child counts of node p of generation G; the whole wave cooperates (result uniform)
 __device__ inline void coop_count(const QTree& t, const QGen& G, int p, int lane, int c[4]) {
@@ -1094,14 +1119,7 @@ __device__ __forceinline__ void qt_copy_node(const QGen& A, QGen& B, int p, int 
     B.ks[to] = A.ks[p]; B.kn[to] = A.kn[p]; B.kb[to] = A.kb[p]; B.leaf[to] = A.leaf[p];
 }
 
-__device__ __forceinline__ int wave_incl_max(int v, int lane) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(v, o, 64);
-        if (lane >= o) v = max(v, t);
-    }
-    return v;
-}
+__device__ __forceinline__ int wave_incl_max(int v, int) { return wave_incl_max_dpp(v); }
 
 // std::sort(vPrevSizeAndPointerToNode, compareNodes) (src:950) on t.prev[0..n), emulated exactly and
 // wave-parallel.  Each libstdc++ partition step (median-of-3 to first, unguarded Hoare partition) is
@@ -1202,7 +1220,7 @@ __device__ void qt_sort(QTree& t, const QGen& A, int n, int lane) {
             }
             t.sel_tmp[r] = el[i];
         }
-        carry = __shfl(v, 63, 64);
+        carry = __builtin_amdgcn_readlane(v, 63);
     }
     wave_sync();
     for (int i = lane; i < n; i += 64) t.prev[i] = (uint16_t)(t.sel_tmp[i] & 0xffff);
@@ -1260,7 +1278,7 @@ __device__ void qt_run(QTree& t, int K, int N, int nroots, float root_w, int spa
                     for (int r = 0; r < kMaxRoots; ++r) rcount[r] += root == r;
                 }
             }
-            carry += __shfl(incl, 63, 64);
+            carry += __builtin_amdgcn_readlane(incl, 63);
         }
 #pragma unroll
         for (int r = 0; r < kMaxRoots; ++r) rcount[r] = uniform(wave_sum(rcount[r]));
@@ -1355,9 +1373,9 @@ __device__ void qt_run(QTree& t, int K, int N, int nroots, float root_w, int spa
                     }
                 }
             }
-            carry_c += __shfl(ic, 63, 64);
-            carry_s += __shfl(is, 63, 64);
-            carry_p += __shfl(ip, 63, 64);
+            carry_c += __builtin_amdgcn_readlane(ic, 63);
+            carry_s += __builtin_amdgcn_readlane(is, 63);
+            carry_p += __builtin_amdgcn_readlane(ip, 63);
         }
         nsplit = carry_p;
         stamp(2);
@@ -1408,7 +1426,7 @@ __device__ void qt_run(QTree& t, int K, int N, int nroots, float root_w, int spa
                     const int inc = wave_incl_scan(d, lane);
                     const unsigned long long hit = ballot(o < np && nlist + carry + inc >= N);
                     if (hit) { ndiv = b + __ffsll((long long)hit); break; }
-                    carry += __shfl(inc, 63, 64);
+                    carry += __builtin_amdgcn_readlane(inc, 63);
                 }
                 ndiv = uniform(ndiv);
                 for (int i = lane; i < nlist; i += 64) t.divided[i] = 0;
@@ -1452,8 +1470,8 @@ __device__ void qt_run(QTree& t, int K, int N, int nroots, float root_w, int spa
                             r++;
                         }
                     }
-                    carry_c += __shfl(ic, 63, 64);
-                    carry_p += __shfl(ip, 63, 64);
+                    carry_c += __builtin_amdgcn_readlane(ic, 63);
+                    carry_p += __builtin_amdgcn_readlane(ip, 63);
                 }
                 nsplit = carry_p;
                 int carry_k = 0;

@@ -7,6 +7,6 @@ timeout -k 10 300 python -u -m pytest tests/test_extract_gpu.py -x -q --timeout 
 tail -1 $O/t.log
 run() {
   env "$@" timeout -k 10 120 python bench.py --no-cpu-baseline --no-ba --no-stereo --no-pose --no-bow --no-single --no-c4 --steps 30 > $O/bench.json 2>$O/bench.err || { echo "bench failed"; tail $O/bench.err; exit 1; }
-  python -c "import json,sys; d=json.load(open('$O/bench.json')); print(sys.argv[1:], d['value'], d['ms_per_step'], d['stages_ms']['describe'])" "$@"
+  python -c "import json,sys; d=json.load(open('$O/bench.json')); print(sys.argv[1:], d['value'], d['ms_per_step'], d['stages_ms'])" "$@"
 }
 for v in "${@:-ORBGPU_DESC_FLAT=1}"; do run $v; done
