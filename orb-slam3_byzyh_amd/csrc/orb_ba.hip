@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
@@ -1846,22 +1847,32 @@ __global__ __launch_bounds__(256) void k_ba_scatter(const uint8_t* __restrict__ 
     if (blockIdx.x == 0 && threadIdx.x < it.bytes % 16) dst[n16 * 16 + threadIdx.x] = sp[n16 * 16 + threadIdx.x];
 }
 
+// Per-solve inputs: add() records (device buffer, host source, bytes); pack() lays them out behind
+// the item table in one pinned buffer (a single copy from each source), which goes up in one
+// H2D copy and is spread by one k_ba_scatter launch.
 struct Stager {
-    std::vector<uint8_t> host;
+    struct Src { const void* p; size_t off, bytes; };
     std::vector<ScatterItem> items;
+    std::vector<Src> srcs;
+    size_t data_bytes = 0;
     template <typename T>
     bool add(DevBuf<T>& d, const T* src, size_t n) {
         if (!d.grow(n)) return false;
         if (n == 0) return true;
-        const size_t off = (host.size() + 15) & ~size_t(15);
-        host.resize(off + n * sizeof(T));
-        memcpy(host.data() + off, src, n * sizeof(T));
+        const size_t off = (data_bytes + 15) & ~size_t(15);
+        data_bytes = off + n * sizeof(T);
         items.push_back({(uint64_t)(uintptr_t)d.p, off, n * sizeof(T)});
+        srcs.push_back({src, off, n * sizeof(T)});
         return true;
     }
     template <typename T>
     bool add(DevBuf<T>& d, const std::vector<T>& v) {
         return add(d, v.data(), v.size());
+    }
+    size_t table_bytes() const { return (items.size() * sizeof(ScatterItem) + 255) & ~size_t(255); }
+    void pack(uint8_t* dst) const {
+        memcpy(dst, items.data(), items.size() * sizeof(ScatterItem));
+        for (const Src& x : srcs) memcpy(dst + table_bytes() + x.off, x.p, x.bytes);
     }
 };
 
@@ -1879,6 +1890,8 @@ struct orb_ba_s {
     DevBuf<unsigned> counters;  // last-block counters of the fused unit kernels
     uint8_t* h_stage = nullptr;  // pinned staging of the per-solve inputs
     size_t h_stage_cap = 0;
+    uint8_t* h_dl = nullptr;     // pinned download of the per-solve results
+    size_t h_dl_cap = 0;
     DevBuf<uint8_t> d_stage;
     LmState* h_lm = nullptr;   // pinned staging of the initial state
     LmProgress* h_prog = nullptr;  // pinned, written by k_lm_trial_done
@@ -1958,6 +1971,7 @@ int orb_ba_destroy(orb_ba_t h) {
     h->counters.release();
     h->d_stage.release();
     if (h->h_stage) hipHostFree(h->h_stage);
+    if (h->h_dl) hipHostFree(h->h_dl);
     if (h->h_lm) hipHostFree(h->h_lm);
     if (h->h_prog) hipHostFree(h->h_prog);
     for (hipEvent_t e : h->unit_ev)
@@ -2077,6 +2091,12 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                     uint8_t* edge_depth_ok, orb_ba_result_t* res) {
     if (!h || !pr || !opt || !res) return orbgpu_fail(ORB_ERR_ARG, "null BA argument");
     memset(res, 0, sizeof(*res));
+    // ORBGPU_BA_TRACE: host-side phase times of each solve on stderr (structure, upload+LM, results)
+    static const bool trace = getenv("ORBGPU_BA_TRACE") != nullptr;
+    using clk = std::chrono::steady_clock;
+    const clk::time_point t_in = clk::now();
+    clk::time_point t_struct = t_in, t_solve = t_in;
+    auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
     const int np = pr->n_poses, nq = pr->n_points, ne_all = pr->n_edges;
     if (np < 0 || nq < 0 || ne_all < 0 || (np && (!pr->pose || !pr->pose_id || !pr->pose_fixed || !pr->pose_camera)) ||
         (nq && (!pr->point || !pr->point_id)) || (ne_all && !pr->edges) || opt->iterations < 0)
@@ -2107,13 +2127,15 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     for (int e = 0; e < ne_all; ++e) { pdeg[pr->edges[e].pose]++; qdeg[pr->edges[e].point]++; }
     std::vector<int> order(np);
     std::iota(order.begin(), order.end(), 0);
-    std::sort(order.begin(), order.end(), [&](int a, int b) { return pr->pose_id[a] < pr->pose_id[b]; });
+    auto by_pose_id = [&](int a, int b) { return pr->pose_id[a] < pr->pose_id[b]; };
+    if (!std::is_sorted(order.begin(), order.end(), by_pose_id)) std::sort(order.begin(), order.end(), by_pose_id);
     std::vector<int32_t> pose_h(np, -1), free_pose;
     for (int i : order)
         if (pdeg[i] && !pr->pose_fixed[i]) { pose_h[i] = (int32_t)free_pose.size(); free_pose.push_back(i); }
     std::vector<int> qorder(nq);
     std::iota(qorder.begin(), qorder.end(), 0);
-    std::sort(qorder.begin(), qorder.end(), [&](int a, int b) { return pr->point_id[a] < pr->point_id[b]; });
+    auto by_point_id = [&](int a, int b) { return pr->point_id[a] < pr->point_id[b]; };
+    if (!std::is_sorted(qorder.begin(), qorder.end(), by_point_id)) std::sort(qorder.begin(), qorder.end(), by_point_id);
     std::vector<int> all_land;
     for (int i : qorder)
         if (qdeg[i]) all_land.push_back(i);
@@ -2190,25 +2212,40 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         blk_j.push_back(i);
         cnt.push_back(0);
     }
-    for (int l = 0; l < nl; ++l)
-        for (int a = landf_off[l]; a < landf_off[l + 1]; ++a)
-            for (int b2 = a; b2 < landf_off[l + 1]; ++b2) {
-                const int i = pose_h[ledges[landf_edge[a]].pose], j = pose_h[ledges[landf_edge[b2]].pose];
-                int32_t& id = blk_id[(size_t)i * nf + j];
-                if (id < 0) { id = (int32_t)blk_i.size(); blk_i.push_back(i); blk_j.push_back(j); cnt.push_back(0); }
-                cnt[id]++;
+    // free-pose row of each landmark -> free-pose edge, then each landmark's pairs (a <= b) in order;
+    // pass 1 assigns the block ids (first-seen order) and keeps them, pass 2 places the pairs
+    std::vector<int32_t> frow(nfe);
+    for (int k = 0; k < nfe; ++k) frow[k] = pose_h[ledges[landf_edge[k]].pose];
+    size_t npairs = 0;
+    for (int l = 0; l < nl; ++l) {
+        const size_t d = (size_t)(landf_off[l + 1] - landf_off[l]);
+        npairs += d * (d + 1) / 2;
+    }
+    std::vector<int32_t> pid(npairs);
+    {
+        size_t q = 0;
+        for (int l = 0; l < nl; ++l)
+            for (int a = landf_off[l]; a < landf_off[l + 1]; ++a) {
+                int32_t* row = blk_id.data() + (size_t)frow[a] * nf;
+                for (int b2 = a; b2 < landf_off[l + 1]; ++b2) {
+                    int32_t& id = row[frow[b2]];
+                    if (id < 0) { id = (int32_t)blk_i.size(); blk_i.push_back(frow[a]); blk_j.push_back(frow[b2]); cnt.push_back(0); }
+                    cnt[id]++;
+                    pid[q++] = id;
+                }
             }
+    }
     const int nblk = (int)blk_i.size();
     std::vector<int32_t> blk_off(nblk + 1, 0);
     for (int k = 0; k < nblk; ++k) blk_off[k + 1] = blk_off[k] + cnt[k];
     std::vector<int32_t> pair_a(blk_off[nblk]), pair_b(blk_off[nblk]);
     {
         std::vector<int32_t> c(blk_off.begin(), blk_off.end() - 1);
+        size_t q = 0;
         for (int l = 0; l < nl; ++l)
             for (int a = landf_off[l]; a < landf_off[l + 1]; ++a)
                 for (int b2 = a; b2 < landf_off[l + 1]; ++b2) {
-                    const int i = pose_h[ledges[landf_edge[a]].pose], j = pose_h[ledges[landf_edge[b2]].pose];
-                    const int id = blk_id[(size_t)i * nf + j];
+                    const int id = pid[q++];
                     pair_a[c[id]] = landf_edge[a];
                     pair_b[c[id]++] = landf_edge[b2];
                 }
@@ -2222,6 +2259,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         if (nn > 0) for (int k = 0; k < 4; ++k) q[k] /= nn;
     }
 
+    t_struct = clk::now();
     const size_t ne1 = std::max(ne, 1);
     Stager st;
     bool ok = st.add(h->pose, pose) && h->pose_bak.grow(7 * (size_t)np) && st.add(h->point, pr->point, 3 * (size_t)nq) &&
@@ -2238,8 +2276,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
               h->depth.grow(ne1);
     if (ok && !st.items.empty()) {
         // [items table | data], one pinned buffer, one copy, one scatter launch
-        const size_t tbl = st.items.size() * sizeof(ScatterItem), data_off = (tbl + 255) & ~size_t(255);
-        const size_t total = data_off + st.host.size();
+        const size_t data_off = st.table_bytes(), total = data_off + st.data_bytes;
         if (total > h->h_stage_cap) {
             if (h->h_stage) hipHostFree(h->h_stage);
             h->h_stage = nullptr;
@@ -2249,8 +2286,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         }
         ok = ok && h->d_stage.grow(total);
         if (ok) {
-            memcpy(h->h_stage, st.items.data(), tbl);
-            memcpy(h->h_stage + data_off, st.host.data(), st.host.size());
+            st.pack(h->h_stage);
             ok = hipMemcpyAsync(h->d_stage.p, h->h_stage, total, hipMemcpyHostToDevice, s) == hipSuccess;
             size_t maxb = 0;
             for (const ScatterItem& it : st.items) maxb = std::max<size_t>(maxb, it.bytes);
@@ -2551,24 +2587,41 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         res->lambda = lambda;
     }
     res->stopped = stop() ? 1 : 0;
+    t_solve = clk::now();
     if (ne)
         hipLaunchKernelGGL(k_ba_final, dim3(grid(ne)), dim3(kT), 0, s, ne, h->edges.p, h->pose.p, h->point.p, h->err.p,
                            h->rho0.p, h->depth.p);
-    hipMemcpyAsync(pr->pose, h->pose.p, sizeof(double) * 7 * (size_t)np, hipMemcpyDeviceToHost, s);
-    std::vector<double> pts(3 * (size_t)nq), lchi(ne1);
-    std::vector<uint8_t> ldep(ne1);
-    hipMemcpyAsync(pts.data(), h->point.p, sizeof(double) * 3 * (size_t)nq, hipMemcpyDeviceToHost, s);
+    // results through one pinned buffer: [poses | points | edge chi2 | depth flags]
+    const size_t dl_bytes = sizeof(double) * (7 * (size_t)np + 3 * (size_t)nq + ne1) + ne1;
+    if (dl_bytes > h->h_dl_cap) {
+        if (h->h_dl) hipHostFree(h->h_dl);
+        h->h_dl = nullptr;
+        h->h_dl_cap = 0;
+        if (hipHostMalloc(&h->h_dl, dl_bytes, hipHostMallocDefault) != hipSuccess)
+            return orbgpu_fail(ORB_ERR_DEVICE, "BA result buffer");
+        h->h_dl_cap = dl_bytes;
+    }
+    double* const dpose = reinterpret_cast<double*>(h->h_dl);
+    double* const pts = dpose + 7 * (size_t)np;
+    double* const lchi = pts + 3 * (size_t)nq;
+    uint8_t* const ldep = reinterpret_cast<uint8_t*>(lchi + ne1);
+    hipMemcpyAsync(dpose, h->pose.p, sizeof(double) * 7 * (size_t)np, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(pts, h->point.p, sizeof(double) * 3 * (size_t)nq, hipMemcpyDeviceToHost, s);
     if (ne) {
-        hipMemcpyAsync(lchi.data(), h->rho0.p, sizeof(double) * ne, hipMemcpyDeviceToHost, s);
-        hipMemcpyAsync(ldep.data(), h->depth.p, ne, hipMemcpyDeviceToHost, s);
+        hipMemcpyAsync(lchi, h->rho0.p, sizeof(double) * ne, hipMemcpyDeviceToHost, s);
+        hipMemcpyAsync(ldep, h->depth.p, ne, hipMemcpyDeviceToHost, s);
     }
     if (hipStreamSynchronize(s) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "BA device error");
+    memcpy(pr->pose, dpose, sizeof(double) * 7 * (size_t)np);
     if (!dist) {
-        memcpy(pr->point, pts.data(), sizeof(double) * 3 * (size_t)nq);
+        memcpy(pr->point, pts, sizeof(double) * 3 * (size_t)nq);
         for (int e = 0; e < ne; ++e) {
             if (edge_chi2) edge_chi2[e] = lchi[e];
             if (edge_depth_ok) edge_depth_ok[e] = ldep[e];
         }
+        if (trace)
+            fprintf(stderr, "[ba] structure %.1f us, upload+LM %.1f us, results %.1f us, it %d trials %d\n",
+                    us(t_in, t_struct), us(t_struct, t_solve), us(t_solve, clk::now()), res->iterations, res->trials);
         return ORB_OK;
     }
     // gather: each rank contributes its landmarks (rank 0 also the points without edges) and its
