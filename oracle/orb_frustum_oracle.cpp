@@ -5,10 +5,11 @@
 // Float arithmetic follows what g++ -O3 -march=native makes of the reference (as in
 // orb_projection_oracle.cpp): Eigen's 3-term row sums and squared norms are contracted as
 // fma(a2, b2, fma(a0, b0, a1 * b1)), `u - bf * invz` as fma(-bf, invz, u); the pose is applied as a
-// 3x4 matrix (the reference's mRcw / mtcw).  PredictScale's unqualified `log(ratio)` resolves to
-// ::log(double) in the reference translation unit (no `using namespace std`), so the level is
-// ceil(log((double)ratio) / (double)mfLogScaleFactor).  Parity with the real reference: unpinned at
-// the ulp level (Eigen's exact evaluation order is not observable without Eigen).
+// 3x4 matrix (the reference's mRcw / mtcw).  PredictScale's unqualified `log(ratio)` and `ceil`
+// resolve to the float overloads: Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:36 has a global
+// `using namespace std` that MapPoint.cc includes (MapPoint.h -> Frame.h -> ORBVocabulary.h), so the
+// level is ceilf(logf(ratio) / mfLogScaleFactor) in float with glibc's logf.  Parity with the real
+// reference: unpinned at the ulp level (Eigen's exact evaluation order is not observable without Eigen).
 #include <cmath>
 #include <cstdint>
 
@@ -51,8 +52,8 @@ extern "C" int oracle_is_in_frustum(const orb_frustum_frame_t* F, int n, const f
         if (dist < minDistance || dist > maxDistance) continue;
         const float viewCos = dot3(PO, normal + 3 * i) / dist;
         if (viewCos < viewingCosLimit) continue;
-        const float ratio = max_dist[i] / dist;  // PredictScale
-        int nScale = (int)std::ceil(std::log((double)ratio) / (double)F->log_scale_factor);
+        const float ratio = max_dist[i] / dist;  // PredictScale, src/MapPoint.cc:715-731
+        int nScale = (int)std::ceil(std::log(ratio) / F->log_scale_factor);  // logf, float division, ceilf
         if (nScale < 0) nScale = 0;
         else if (nScale >= F->n_levels) nScale = F->n_levels - 1;
         in_view[i] = 1;

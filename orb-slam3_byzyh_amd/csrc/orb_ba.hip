@@ -2122,6 +2122,18 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         return h->h_scal[4] != 0.0;
     };
 
+    // A local failure before the solve must be agreed by every rank (MAX over the ranks), so that no
+    // rank returns while the others block in the next collective.  Single process: the local value.
+    auto agree_fail = [&](bool local_fail) -> bool {
+        if (!dist) return local_fail;
+        h->h_scal[6] = local_fail ? 1.0 : 0.0;
+        hipMemcpyAsync(h->scal.p + 6, &h->h_scal[6], sizeof(double), hipMemcpyHostToDevice, s);
+        const bool ok = dev_reduce(h, h->scal.p + 6, 1, ORB_BA_MAX);
+        hipMemcpyAsync(&h->h_scal[6], h->scal.p + 6, sizeof(double), hipMemcpyDeviceToHost, s);
+        if (hipStreamSynchronize(s) != hipSuccess || !ok) return true;
+        return h->h_scal[6] != 0.0;
+    };
+
     // ---- structure (initializeOptimization + BlockSolver::buildStructure), from the whole problem
     std::vector<int> pdeg(np, 0), qdeg(nq, 0);
     for (int e = 0; e < ne_all; ++e) { pdeg[pr->edges[e].pose]++; qdeg[pr->edges[e].point]++; }
@@ -2295,7 +2307,16 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                                h->d_stage.p + data_off, (const ScatterItem*)h->d_stage.p);
         }
     }
-    if (!ok) return orbgpu_fail(ORB_ERR_DEVICE, "BA device allocation / upload");
+    // the pinned result buffer too, before the solve: [poses | points | edge chi2 | depth flags]
+    const size_t dl_bytes = sizeof(double) * (7 * (size_t)np + 3 * (size_t)nq + ne1) + ne1;
+    if (ok && dl_bytes > h->h_dl_cap) {
+        if (h->h_dl) hipHostFree(h->h_dl);
+        h->h_dl = nullptr;
+        h->h_dl_cap = 0;
+        ok = hipHostMalloc(&h->h_dl, dl_bytes, hipHostMallocDefault) == hipSuccess;
+        if (ok) h->h_dl_cap = dl_bytes;
+    }
+    if (agree_fail(!ok)) return orbgpu_fail(ORB_ERR_DEVICE, "BA device allocation / upload");
     hipMemsetAsync(h->x.p, 0, sizeof(double) * (n + m), s);  // g2o's _x starts zeroed
     // S: the block pattern is fixed for the solve, so the blocks outside it are zeroed once here
     if (n) hipMemsetAsync(h->S.p, 0, sizeof(double) * (size_t)n * n, s);
@@ -2591,16 +2612,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     if (ne)
         hipLaunchKernelGGL(k_ba_final, dim3(grid(ne)), dim3(kT), 0, s, ne, h->edges.p, h->pose.p, h->point.p, h->err.p,
                            h->rho0.p, h->depth.p);
-    // results through one pinned buffer: [poses | points | edge chi2 | depth flags]
-    const size_t dl_bytes = sizeof(double) * (7 * (size_t)np + 3 * (size_t)nq + ne1) + ne1;
-    if (dl_bytes > h->h_dl_cap) {
-        if (h->h_dl) hipHostFree(h->h_dl);
-        h->h_dl = nullptr;
-        h->h_dl_cap = 0;
-        if (hipHostMalloc(&h->h_dl, dl_bytes, hipHostMallocDefault) != hipSuccess)
-            return orbgpu_fail(ORB_ERR_DEVICE, "BA result buffer");
-        h->h_dl_cap = dl_bytes;
-    }
+    // results through the pinned buffer sized before the solve
     double* const dpose = reinterpret_cast<double*>(h->h_dl);
     double* const pts = dpose + 7 * (size_t)np;
     double* const lchi = pts + 3 * (size_t)nq;

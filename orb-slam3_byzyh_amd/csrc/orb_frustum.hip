@@ -9,10 +9,15 @@
 #include <cmath>
 #include <cstdint>
 
+#include "orb_predict_scale.h"
 #include "orbgpu.h"
 #include "orbgpu_internal.h"
 
 namespace {
+
+struct ScaleSteps {  // MapPoint::PredictScale level thresholds (orb_predict_scale.h)
+    float t[orbgpu::kPredictMaxLevels];
+};
 
 __device__ __forceinline__ float dot3(const float a[3], const float b[3]) {
     return fmaf(a[2], b[2], fmaf(a[0], b[0], a[1] * b[1]));
@@ -22,7 +27,7 @@ __global__ __launch_bounds__(256) void k_is_in_frustum(orb_frustum_frame_t F, in
                                                        const float* __restrict__ normal,
                                                        const float* __restrict__ min_dist,
                                                        const float* __restrict__ max_dist, float viewingCosLimit,
-                                                       uint8_t* __restrict__ in_view, float* __restrict__ proj,
+                                                       ScaleSteps steps, uint8_t* __restrict__ in_view, float* __restrict__ proj,
                                                        float* __restrict__ depth, int32_t* __restrict__ level,
                                                        float* __restrict__ view_cos) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -53,9 +58,9 @@ __global__ __launch_bounds__(256) void k_is_in_frustum(orb_frustum_frame_t F, in
         const float Pn[3] = {normal[3 * (size_t)i], normal[3 * (size_t)i + 1], normal[3 * (size_t)i + 2]};
         const float viewCos = dot3(PO, Pn) / dist;
         if (viewCos < viewingCosLimit) break;
-        const float ratio = max_dist[i] / dist;  // PredictScale: ::log(double) of the float ratio
-        int nScale = (int)ceil(log((double)ratio) / (double)F.log_scale_factor);
-        nScale = nScale < 0 ? 0 : (nScale >= F.n_levels ? F.n_levels - 1 : nScale);
+        // PredictScale: ceilf(logf(ratio) / mfLogScaleFactor) clamped, through glibc-exact steps
+        const float ratio = max_dist[i] / dist;
+        const int nScale = orbgpu::predict_scale_level(ratio, steps.t, F.n_levels);
         in = 1;
         pxr = fmaf(-F.bf, invz, u);
         dep = Pc_dist;
@@ -82,9 +87,12 @@ int orb_is_in_frustum_device(const orb_frustum_frame_t* frame, int n, const floa
     if (!frame || n < 0 || (n && (!d_pos || !d_normal || !d_min_dist || !d_max_dist || !d_in_view || !d_proj ||
                                   !d_depth || !d_level || !d_view_cos)) || frame->n_levels <= 0)
         return orbgpu_fail(ORB_ERR_ARG, "invalid frustum arguments");
+    ScaleSteps steps{};
+    if (!orbgpu::predict_scale_thresholds(frame->log_scale_factor, frame->n_levels, steps.t))
+        return orbgpu_fail(ORB_ERR_ARG, "log_scale_factor must be > 0 and n_levels <= 32");
     if (n == 0) return ORB_OK;
     hipLaunchKernelGGL(k_is_in_frustum, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, *frame, n, d_pos,
-                       d_normal, d_min_dist, d_max_dist, viewing_cos_limit, d_in_view, d_proj, d_depth, d_level,
+                       d_normal, d_min_dist, d_max_dist, viewing_cos_limit, steps, d_in_view, d_proj, d_depth, d_level,
                        d_view_cos);
     if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "frustum kernel launch failed");
     return ORB_OK;

@@ -12,6 +12,8 @@ and double-buffered, so step i's exchange overlaps step i+1's extraction.
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 import torch.distributed as dist
 
@@ -77,18 +79,23 @@ class ShardedExtractor:
         buf = self._i % 2
         out = self.local.view(buf)
         self.ex.extract_batch_device(images, vLappingArea, cap=self.cap, out=out, stream=stream)
-        prev = self.finish()
-        self._pending = all_gather_features(*out, group=self.group, async_op=True)
+        prev = self.finish(stream)
+        # RCCL orders a collective after torch's CURRENT stream only: issue it with the extraction
+        # stream current, so it cannot read the blocks before the extraction has written them
+        with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
+            self._pending = all_gather_features(*out, group=self.group, async_op=True)
         self._i += 1
         return prev
 
-    def finish(self):
-        """Wait for the in-flight all-gather and return its (kps, desc, counts)."""
+    def finish(self, stream=None):
+        """Make `stream` (default: the current stream) wait for the in-flight all-gather and return
+        its (kps, desc, counts)."""
         if self._pending is None:
             return None
         g_kps, g_desc, g_cnt, works = self._pending
-        for w in works:
-            w.wait()
+        with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
+            for w in works:
+                w.wait()
         self._pending = None
         return g_kps, g_desc, g_cnt
 

@@ -159,11 +159,25 @@ class FrustumFrame(ctypes.Structure):  # orb_frustum_frame_t
                 ("log_scale_factor", ctypes.c_float), ("n_levels", ctypes.c_int32)]
 
 
+_LIBM = None
+
+
+def logf(x: float) -> np.float32:
+    """glibc's logf: the float overload the reference's unqualified log(float) resolves to
+    (`using namespace std` from Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:36)."""
+    global _LIBM
+    if _LIBM is None:
+        _LIBM = ctypes.CDLL("libm.so.6")
+        _LIBM.logf.restype = ctypes.c_float
+        _LIBM.logf.argtypes = [ctypes.c_float]
+    return np.float32(_LIBM.logf(float(np.float32(x))))
+
+
 def frustum_frame(Tcw, Ow, camera, bf, bounds, scale_factor: float = 1.2, n_levels: int = 8) -> FrustumFrame:
     """orb_frustum_frame_t of a Frame: Tcw 3x4 (mRcw | mtcw), Ow = mOw, camera (fx, fy, cx, cy), mbf,
-    bounds (mnMinX, mnMaxX, mnMinY, mnMaxY); mfLogScaleFactor = log(mfScaleFactor) stored as float."""
+    bounds (mnMinX, mnMaxX, mnMinY, mnMaxY); mfLogScaleFactor = logf(mfScaleFactor) (src/Frame.cc:121)."""
     T = np.asarray(Tcw, np.float32).reshape(12)
-    lsf = np.float32(np.log(np.float64(np.float32(scale_factor))))
+    lsf = logf(scale_factor)
     return FrustumFrame((ctypes.c_float * 12)(*T), (ctypes.c_float * 3)(*np.asarray(Ow, np.float32)), *[float(c) for c in camera],
                         float(bf), *[float(b) for b in bounds], float(lsf), int(n_levels))
 

@@ -62,6 +62,21 @@ def make_problem_struct(prob: dict) -> tuple[BaProblem, dict]:
     return s, arrs
 
 
+def stop_flag_address(stop_flag):
+    """Address the library polls for pbStopFlag, or None.  The flag must be memory the caller's
+    other thread writes: a silent converting copy would never see the request, so anything other
+    than a C-contiguous np.int32 array or a ctypes.c_int32 is rejected."""
+    if stop_flag is None:
+        return None
+    if isinstance(stop_flag, ctypes.c_int32):
+        return ctypes.addressof(stop_flag)
+    if isinstance(stop_flag, np.ndarray):
+        if stop_flag.dtype != np.int32 or not stop_flag.flags["C_CONTIGUOUS"] or stop_flag.size < 1:
+            raise TypeError("stop_flag must be a non-empty C-contiguous np.int32 array")
+        return stop_flag.ctypes.data
+    raise TypeError(f"stop_flag must be an np.int32 array or ctypes.c_int32, not {type(stop_flag).__name__}")
+
+
 # orb_ba_host_reduce_fn (include/orbgpu.h): in-place all-reduce of n doubles, op 0 = SUM, 1 = MAX
 HOST_REDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_size_t,
                                   ctypes.c_int)
@@ -144,10 +159,12 @@ class LocalBA:
             self._h = None
 
     def optimize(self, prob: dict, iterations: int = 10, user_lambda_init: float = 0.0, stop_flag=None):
-        """Run optimize(iterations) on a copy of `prob`.  Returns (pose, point, edge_chi2, depth_ok, result)."""
+        """Run optimize(iterations) on a copy of `prob`.  Returns (pose, point, edge_chi2, depth_ok, result).
+
+        stop_flag is the reference's pbStopFlag (sparse_optimizer.h:188): a C-contiguous np.int32
+        array (element 0 is polled) or a ctypes.c_int32, shared with the thread that sets it."""
         s, arrs = make_problem_struct(prob)
-        flag = None if stop_flag is None else np.ascontiguousarray(stop_flag, dtype=np.int32)
-        opt = BaOptions(int(iterations), float(user_lambda_init), None if flag is None else flag.ctypes.data)
+        opt = BaOptions(int(iterations), float(user_lambda_init), stop_flag_address(stop_flag))
         ne = len(arrs["edges"])
         chi2 = np.zeros(ne, np.float64)
         depth = np.zeros(ne, np.uint8)

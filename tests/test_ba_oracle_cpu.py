@@ -141,3 +141,18 @@ def test_oracle_lm_bookkeeping(oracle, synth):
     assert r0["iterations"] == 0 and r0["trials"] == 0
     pose, point, _, _, rs = oracle.local_ba(prob, 10, stop_flag=np.ones(1, np.int32))
     assert rs["stopped"] == 1 and np.array_equal(point, prob["point"])
+
+
+def test_stop_flag_must_be_shared_memory(pkg):
+    """pbStopFlag is polled memory another thread writes; a converting copy would never
+    see the request, so anything but an np.int32 array or a ctypes.c_int32 is refused."""
+    import ctypes
+    from orbslam3_amd.optimizer import stop_flag_address
+    a = np.zeros(1, np.int32)
+    assert stop_flag_address(a) == a.ctypes.data
+    c = ctypes.c_int32(0)
+    assert stop_flag_address(c) == ctypes.addressof(c)
+    assert stop_flag_address(None) is None
+    for bad in (np.zeros(1, bool), np.zeros(1, np.int64), 1, True, np.zeros((2, 2), np.int32)[:, 0], np.zeros(0, np.int32)):
+        with pytest.raises(TypeError):
+            stop_flag_address(bad)

@@ -62,3 +62,16 @@ def test_tracking_chain_frustum_then_local_search(pkg, oracle, synth, seed, th):
     n_ref, exp = oracle.search_by_projection_local(F, pkg.LocalMapPoints(**track_ref, **fixed), th, False, 10.0, 0.8,
                                                    None)
     assert n_gpu == n_ref > 100 and np.array_equal(got, exp)
+
+
+def test_predict_scale_on_scale_steps_gpu(pkg, oracle, synth):
+    """on the GPU the level on exact scale steps (ratio == 1.2f^k, +-1 ulp) follows the
+    reference's float ceilf(logf(ratio) / mfLogScaleFactor), bit-equal to the oracle's glibc logf."""
+    from test_frustum_cpu import predict_scale, scale_step_points
+    T, Ow, P, N, mn, mx, ratios = scale_step_points(synth)
+    fr = pkg.frustum_frame(T, Ow, synth.EUROC_K, synth.EUROC_BF, (0, 752, 0, 480))
+    got = pkg.is_in_frustum(fr, P, N, mn, mx, 0.5)
+    exp = oracle.is_in_frustum(fr, P, N, mn, mx, 0.5)
+    assert np.array_equal(got["track_level"], exp["track_level"])
+    assert list(got["track_level"]) == [predict_scale(q, fr.log_scale_factor, 8) for q in ratios]
+    assert got["track_level"][3] == 1  # ratio 1.2f -> level 1 (double arithmetic would give 2)
