@@ -21,6 +21,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "orb_extract_geom.h"
@@ -127,8 +128,10 @@ __device__ __forceinline__ int wave_incl_max_dpp(int v) {
 // ================================================================================================
 // 1. pyramid level: padded plane + blurred view, src:1687-1740 and src:1629-1637
 // ================================================================================================
-constexpr int kTileW = 128, kTileH = 16, kHalo = 3;  // 128-byte rows: every store fills whole cache lines
-constexpr int kLW = kTileW + 2 * kHalo, kLH = kTileH + 2 * kHalo;  // 134 x 22
+// A tile is 122 x 16 padded-plane pixels; with the 3-px blur halo it is 128 x 22, one lane per column.
+constexpr int kTileW = 122, kTileH = 16, kHalo = 3;
+constexpr int kLW = kTileW + 2 * kHalo, kLH = kTileH + 2 * kHalo;  // 128 x 22
+static_assert(kLW == 128, "one lane per haloed tile column, two waves per row");
 constexpr int kBoxW = 288, kBoxH = 2 * kLH + 4;  // source box (bytes) for scale factors <= 2
 static_assert(kBoxW >= 3 + 2 * kLW + 2, "box too narrow");
 // box for level ratios <= 1.25 (the usual 1.2): 133 * 1.25 + 2 columns + 3 alignment bytes, 21 * 1.25 + 2 rows
@@ -163,175 +166,227 @@ __device__ __forceinline__ int resize_src_index(int d, double scale, int slen) {
     return min(max(s, 0), slen - 1);
 }
 
-// One workgroup = one 64 x 32 tile of a padded level plane (+3-px halo for the blur).
+// XCD-aware tile order.  Blocks are dealt round-robin over the 8 XCDs in dispatch order (block b
+// and b + 8 share an L2); handing each XCD a contiguous run of tiles keeps vertically adjacent tiles,
+// which re-read the same source and halo rows, in one L2.  Performance only: any placement is correct.
+__device__ __forceinline__ int xcd_tile(int b, int share) { return (b & 7) * share + (b >> 3); }
+
+// 7-tap GaussianBlur weights as packed u8 (horizontal pass, v_dot4_u32_u8) and u16 pairs (vertical
+// pass, v_dot2_u32_u16 over row pairs: even output rows start on a pair, odd ones in its high half)
+constexpr uint32_t kBlurK0 = 18u | 34u << 8 | 48u << 16 | 56u << 24, kBlurK1 = 48u | 34u << 8 | 18u << 16;
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 w16(unsigned a, unsigned b) { u16x2 v; v.x = (unsigned short)a; v.y = (unsigned short)b; return v; }
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+
+// One workgroup = one 128 x 16 tile of a padded level plane (+3-px halo for the blur).
 // Level 0 copies the input; level l > 0 resizes the previous level view.  The source pixels the tile
-// needs are staged in LDS (one round of independent loads), the interpolation reads LDS only.
+// needs are staged in LDS (one round of independent loads), then every phase is written for few VALU
+// instructions per pixel (the pyramid is VALU-bound, PMC round 2):
+//   resize  lane per tile column, wave-uniform rows: the column's INTER_LINEAR coefficients stay in
+//           registers, the row coefficients are scalar loads, and each source row's horizontal
+//           interpolation is computed once and streamed (about 1.2 rows per output row)
+//   hblur   4 outputs x 2 rows per item: v_alignbyte + v_dot4_u32_u8, stored as row-pair u16x2
+//   vblur   lane per column, 8 output rows: 4 v_dot2_u32_u16 per output over the row pairs
+// Level geometry by value (kernel arguments): no dependent load of the geometry block before the
+// source loads can be addressed.
+struct PyrArgs {
+    long long frame_bytes;         // one frame's pyramid block (pyramid and blurred pyramid alike)
+    long long plane_off, src_off;  // this level's padded plane; the previous level's view origin
+    int w, h, pw, ph, pitch;       // this level
+    int sw, sh, spitch;            // previous level view (level > 0)
+    int xtab_off, ytab_off, simd_end;
+    int tiles_x, tiles_per_frame, total, share;
+    double scx, scy;               // cv::resize scale: 1 / ((double)w / sw), 1 / ((double)h / sh)
+};
+
 template <bool kLevel0, int kBH = kSmallBoxH, int kBW = kSmallBoxW>
-__global__ __launch_bounds__(256) void k_pyramid_level(const KernelGeom* __restrict__ gp, int level,
-                                                       const uint8_t* __restrict__ in, long long in_frame_stride,
-                                                       int in_stride, uint8_t* __restrict__ pyr,
-                                                       uint8_t* __restrict__ blur, const int2* __restrict__ xtab,
-                                                       const int4* __restrict__ ytab) {
-    const KernelGeom& g = *gp;
+__global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const uint8_t* __restrict__ in,
+                                                          long long in_frame_stride, int in_stride,
+                                                          uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                                          const int2* __restrict__ xtab, const int4* __restrict__ ytab,
+                                                          unsigned long long* __restrict__ stamps) {
+    const int t = xcd_tile(blockIdx.x, A.share);
+    if (t >= A.total) return;
+    // debug (ORBGPU_PYR_STAMPS): per-block phase clocks, thread 0 of each block
+    unsigned long long* stp = stamps ? stamps + (size_t)blockIdx.x * 8 : nullptr;
+    if (stp && threadIdx.x == 0) { stp[6] = wall_clock64(); stp[0] = __builtin_amdgcn_s_memtime(); }
+#define PYR_STAMP(k) do { if (stp && threadIdx.x == 0) stp[k] = __builtin_amdgcn_s_memtime(); } while (0)
     constexpr int kBoxWords = kBW / 4;
+    constexpr int kPairs = kLH / 2;      // 11 row pairs of horizontal sums
+    constexpr int kQuads = (kTileW + 3) / 4;
     __shared__ __attribute__((aligned(16))) uint8_t box[kLevel0 ? 4 : kBH * kBW];
-    __shared__ __attribute__((aligned(16))) uint8_t tile[kLH][kLW + 2 + 8];  // rows 4-aligned, +8 readable slack
-    __shared__ uint16_t hsum[kLH][kTileW];  // <= 255 * 256: exact in 16 bits
-    __shared__ int2 xs[kLW];
-    __shared__ int4 ys[kLH];
-    const int f = blockIdx.z, tid = threadIdx.x;
-    const LevelGeom& L = g.lv[level];
-    const int X0 = blockIdx.x * kTileW, Y0 = blockIdx.y * kTileH;
-    uint8_t* plane = pyr + (size_t)f * g.pyr_frame_bytes + L.plane_off;
-    uint8_t* bplane = blur + (size_t)f * g.pyr_frame_bytes + L.plane_off;
-    // view-coordinate ranges this tile (+halo) reads
-    int vx0, vx1, vy0, vy1;
-    reflect_range(X0 - kHalo - kEdge, X0 + kTileW + kHalo - 1 - kEdge, L.w, vx0, vx1);
-    reflect_range(Y0 - kHalo - kEdge, Y0 + kTileH + kHalo - 1 - kEdge, L.h, vy0, vy1);
+    __shared__ __attribute__((aligned(16))) uint8_t tile[kLH][kLW + 8];      // +8: the last quad's over-read
+    __shared__ __attribute__((aligned(16))) uint32_t hs2[kPairs][kLW];       // (row 2j, row 2j+1) sums, <= 255 * 256
+    __shared__ int4 yrow[kLevel0 ? 1 : kLH];  // per tile row: box row offsets of the two source rows, weights
+    const int f = t / A.tiles_per_frame, rem = t - f * A.tiles_per_frame;
+    const int tyi = rem / A.tiles_x;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = uniform(tid >> 6);
+    const int X0 = (rem - tyi * A.tiles_x) * kTileW, Y0 = tyi * kTileH;
+    uint8_t* plane = pyr + (size_t)f * A.frame_bytes + A.plane_off;
+    uint8_t* bplane = blur + (size_t)f * A.frame_bytes + A.plane_off;
+    // this lane's tile column (waves 0/1: rows [0, 11), waves 2/3: rows [11, 22)) in view coordinates
+    const int tx = (wave & 1) * 64 + lane, r0 = (wave >> 1) * (kLH / 2);
+    const int vx = reflect101(X0 - kHalo + tx - kEdge, A.w);
     if (kLevel0) {
-        // level 0: tile (+halo) straight from the input with reflected indices; 2 rows x 128 columns
-        // per pass, all 22 loads per thread issued before the first LDS store (one round trip)
-        const uint8_t* src = in + (size_t)f * in_frame_stride;
-        const int c0 = tid & 127, rg = tid >> 7;
-        constexpr int kPass = (kLH + 1) / 2;
-        int v[kPass][2];
+        // level 0: the column's 11 rows straight from the input with reflected indices, all loads
+        // issued before the first LDS store (one round trip)
+        const uint8_t* src = in + (size_t)f * in_frame_stride + vx;
+        int v[kLH / 2];
 #pragma unroll
-        for (int q = 0; q < kPass; ++q) {
-            const int ty = 2 * q + rg;
-            const int vy = reflect101(Y0 - kHalo + min(ty, kLH - 1) - kEdge, L.h);
+        for (int k = 0; k < kLH / 2; ++k) v[k] = src[(size_t)reflect101(Y0 - kHalo + r0 + k - kEdge, A.h) * in_stride];
 #pragma unroll
-            for (int hx = 0; hx < 2; ++hx) {
-                const int tx = c0 + 128 * hx;
-                const int vx = reflect101(X0 - kHalo + min(tx, kLW - 1) - kEdge, L.w);
-                v[q][hx] = (ty < kLH && tx < kLW) ? src[(size_t)vy * in_stride + vx] : 0;
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < kPass; ++q)
-#pragma unroll
-            for (int hx = 0; hx < 2; ++hx) {
-                const int ty = 2 * q + rg, tx = c0 + 128 * hx;
-                if (ty < kLH && tx < kLW) tile[ty][tx] = (uint8_t)v[q][hx];
-            }
+        for (int k = 0; k < kLH / 2; ++k) tile[r0 + k][tx] = (uint8_t)v[k];
         __syncthreads();
+        PYR_STAMP(1);
+        PYR_STAMP(2);
     } else {
-        const LevelGeom& P = g.lv[level - 1];
-        const uint8_t* src = pyr + (size_t)f * g.pyr_frame_bytes + P.plane_off + (size_t)kEdge * P.pitch + kEdge;
-        const int sstride = P.pitch;  // multiple of 128: every box row has the same alignment
-        const double scx = 1. / ((double)L.w / P.w), scy = 1. / ((double)L.h / P.h);
-        const int bx0 = resize_src_index(vx0, scx, P.w);
-        const int by0 = resize_src_index(vy0, scy, P.h);
-        const int bw = min(resize_src_index(vx1, scx, P.w) + 1, P.w - 1) - bx0 + 1;
-        const int bh = min(resize_src_index(vy1, scy, P.h) + 1, P.h - 1) - by0 + 1;
-        // coefficient tables of the tile's columns / rows
-        if (tid < kLW) xs[tid] = xtab[L.xtab_off + reflect101(X0 - kHalo + tid - kEdge, L.w)];
-        else if (tid >= 192 && tid < 192 + kLH) ys[tid - 192] = ytab[L.ytab_off + reflect101(Y0 - kHalo + (tid - 192) - kEdge, L.h)];
-        // source box as aligned dwords (over-reads stay inside the previous level's 19-px frame)
-        const uint8_t* row0 = src + (size_t)by0 * sstride + bx0;
+        // view-coordinate ranges this tile (+halo) reads
+        int vx0, vx1, vy0, vy1;
+        reflect_range(X0 - kHalo - kEdge, X0 + kTileW + kHalo - 1 - kEdge, A.w, vx0, vx1);
+        reflect_range(Y0 - kHalo - kEdge, Y0 + kTileH + kHalo - 1 - kEdge, A.h, vy0, vy1);
+        const uint8_t* src = pyr + (size_t)f * A.frame_bytes + A.src_off;
+        const int bx0 = resize_src_index(vx0, A.scx, A.sw);
+        const int by0 = resize_src_index(vy0, A.scy, A.sh);
+        const int bw = min(resize_src_index(vx1, A.scx, A.sw) + 1, A.sw - 1) - bx0 + 1;
+        const int bh = min(resize_src_index(vy1, A.scy, A.sh) + 1, A.sh - 1) - by0 + 1;
+        // source box as aligned dwords (over-reads stay inside the previous level's 19-px frame);
+        // src_off and spitch are multiples of 128, so every box row has the same alignment
+        const uint8_t* row0 = src + (size_t)by0 * A.spitch + bx0;
         const int shift = (int)((uintptr_t)row0 & 3);
         const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(row0 - shift);
         const int nw = (shift + bw + 3) >> 2;
         uint32_t* boxw = reinterpret_cast<uint32_t*>(box);
-        const int wl = tid & 63, rg = tid >> 6;
-        // every load of the box issued before the first LDS store (one round trip per block)
+        const int rg = tid >> 6;
+        // every global load of the block issued before the first LDS store (one round trip): the box,
+        // the row coefficients (22 lanes) and this lane's column coefficients
         constexpr int kRowPass = kBH / 4, kWordPass = (kBoxWords + 63) / 64;
         uint32_t v[kRowPass][kWordPass];
 #pragma unroll
         for (int q = 0; q < kRowPass; ++q)
 #pragma unroll
             for (int hx = 0; hx < kWordPass; ++hx) {
-                const int r = 4 * q + rg, w = wl + 64 * hx;
-                v[q][hx] = (r < bh && w < nw) ? wsrc[(size_t)r * (sstride >> 2) + w] : 0u;
+                const int r = 4 * q + rg, w = lane + 64 * hx;
+                v[q][hx] = (r < bh && w < nw) ? wsrc[(size_t)r * (A.spitch >> 2) + w] : 0u;
             }
+        int4 yv = make_int4(0, 0, 0, 0);
+        if (tid < kLH) yv = ytab[A.ytab_off + reflect101(Y0 - kHalo + tid - kEdge, A.h)];
+        const int2 X = xtab[A.xtab_off + vx];
 #pragma unroll
         for (int q = 0; q < kRowPass; ++q)
 #pragma unroll
             for (int hx = 0; hx < kWordPass; ++hx) {
-                const int r = 4 * q + rg, w = wl + 64 * hx;
+                const int r = 4 * q + rg, w = lane + 64 * hx;
                 if (r < bh && w < nw) boxw[r * kBoxWords + w] = v[q][hx];
             }
+        if (tid < kLH) yrow[tid] = make_int4((yv.x - by0) * kBW, (yv.y - by0) * kBW, yv.z, yv.w);
         __syncthreads();
-        // tile (+halo) values, INTER_LINEAR from the box
-        for (int i = tid; i < kLH * kLW; i += 256) {
-            const int ty = i / kLW, tx = i - ty * kLW;
-            const int2 X = xs[tx];
-            const int4 Y = ys[ty];
-            const int sx = X.x - bx0 + shift, sx1 = min(X.x + 1, bx0 + bw - 1) - bx0 + shift;
-            const int a0 = X.y & 0xffff, a1 = X.y >> 16;
-            const uint8_t* R0 = box + (Y.x - by0) * kBW;
-            const uint8_t* R1 = box + (Y.y - by0) * kBW;
-            const int h0 = R0[sx] * a0 + R0[sx1] * a1, h1 = R1[sx] * a0 + R1[sx1] * a1;
-            const int vx = reflect101(X0 - kHalo + tx - kEdge, L.w);
-            int v;
-            if (vx < L.simd_end) {  // VResizeLinearVec_32s8u: v_mul_hi on (S >> 4), rounding shift by 2
-                const int t0 = min(h0 >> 4, 32767), t1 = min(h1 >> 4, 32767);
-                v = (((t0 * Y.z) >> 16) + ((t1 * Y.w) >> 16) + 2) >> 2;
-            } else {                // FixedPtCast<int, uchar, 22>
-                v = (h0 * Y.z + h1 * Y.w + (1 << 21)) >> 22;
+        PYR_STAMP(1);
+        // INTER_LINEAR down the column: both source rows of every tile row are interpolated
+        // horizontally (no row-to-row dependency, so the unrolled loop keeps many LDS reads in flight).
+        // VResizeLinearVec_32s8u (vx < simd_end): v_mul_hi on S >> 4 (S <= 255 * 2049, so S >> 4 <
+        // 32767 and the reference's int16 saturation never triggers), rounding shift by 2;
+        // else FixedPtCast<int, uchar, 22>.
+        const int sx = X.x - bx0 + shift, sx1 = min(X.x + 1, bx0 + bw - 1) - bx0 + shift;
+        const unsigned a0 = X.y & 0xffff, a1 = (unsigned)X.y >> 16;
+        const bool simd = vx < A.simd_end;
+        auto stream = [&](auto mixed) {
+            constexpr bool kMixed = decltype(mixed)::value;
+            const int hs = simd ? 4 : 0;
+            auto hrow = [&](int off) {
+                const int h = (int)(__umul24(box[off + sx], a0) + __umul24(box[off + sx1], a1));
+                return kMixed ? h >> hs : h >> 4;
+            };
+#pragma unroll
+            for (int k = 0; k < kLH / 2; ++k) {
+                const int4 Y = yrow[r0 + k];  // LDS broadcast
+                const int p0 = (int)__umul24((unsigned)hrow(Y.x), (unsigned)Y.z);  // < 2^20 * 2^11
+                const int p1 = (int)__umul24((unsigned)hrow(Y.y), (unsigned)Y.w);
+                int v = ((p0 >> 16) + (p1 >> 16) + 2) >> 2;
+                if (kMixed && !simd) v = min((p0 + p1 + (1 << 21)) >> 22, 255);
+                tile[r0 + k][tx] = (uint8_t)v;
             }
-            tile[ty][tx] = (uint8_t)min(max(v, 0), 255);
-        }
+        };
+        if (__ballot(!simd) == 0) stream(std::false_type{});
+        else stream(std::true_type{});
         __syncthreads();
+        PYR_STAMP(2);
     }
-    // padded plane: 8 consecutive pixels per thread
-    const int r = tid >> 4, c = (tid & 15) * 8;
+    // padded plane: 8 consecutive pixels per thread (tile columns 3 .. 124)
     {
+        const int r = tid >> 4, c = (tid & 15) * 8;
         const int py = Y0 + r, px = X0 + c;
-        if (py < L.ph) {
-            uint8_t* dst = plane + (size_t)py * L.pitch + px;
-            if (px + 7 < L.pw) {
+        if (py < A.ph && c < kTileW) {
+            uint8_t* dst = plane + (size_t)py * A.pitch + px;
+            if (c + 7 < kTileW && px + 7 < A.pw) {
                 *reinterpret_cast<unsigned long long*>(dst) = lds_bytes8(tile[r + kHalo], c + kHalo);
             } else {
-                for (int k = 0; k < 8 && px + k < L.pw; ++k) dst[k] = tile[r + kHalo][c + kHalo + k];
+                for (int k = 0; k < 8 && c + k < kTileW && px + k < A.pw; ++k) dst[k] = tile[r + kHalo][c + kHalo + k];
             }
         }
     }
+    PYR_STAMP(3);
     // does this tile touch the view at all?
-    if (X0 + kTileW <= kEdge || X0 >= kEdge + L.w || Y0 + kTileH <= kEdge || Y0 >= kEdge + L.h) return;
-    // GaussianBlur 7x7 sigma 2: horizontal pass (exact in 16 bits, kept as int), then vertical
-    for (int i = tid; i < kLH * kTileW / 4; i += 256) {  // 4 outputs per item from 3 aligned dwords
-        const int ty = i / (kTileW / 4), tx = (i - ty * (kTileW / 4)) * 4;
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(tile[ty]) + (tx >> 2);
-        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-        int px[12];
+    if (X0 + kTileW <= kEdge || X0 >= kEdge + A.w || Y0 + kTileH <= kEdge || Y0 >= kEdge + A.h) {
+        if (stp && threadIdx.x == 0) { stp[4] = stp[5] = stp[3]; stp[7] = wall_clock64(); }
+        return;
+    }
+    // GaussianBlur 7x7 sigma 2, horizontal pass: 4 columns x 2 rows per item, exact in 16 bits
+    for (int i = tid; i < kPairs * kQuads; i += 256) {
+        const int j = i / kQuads, q = (i - j * kQuads) * 4;
+        uint32_t o[2][4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            px[k] = (w0 >> (8 * k)) & 0xff;
-            px[4 + k] = (w1 >> (8 * k)) & 0xff;
-            px[8 + k] = (w2 >> (8 * k)) & 0xff;
+        for (int rr = 0; rr < 2; ++rr) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(tile[2 * j + rr]) + (q >> 2);
+            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                o[rr][k] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, k), kBlurK1,
+                                                  __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, k), kBlurK0, 0u, false), false);
         }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            int acc = 0;
-#pragma unroll
-            for (int k = 0; k < 7; ++k) acc += blur_tap(k) * px[q + k];
-            hsum[ty][tx + q] = (uint16_t)acc;
-        }
+        uint4 pk;
+        pk.x = o[0][0] | o[1][0] << 16;
+        pk.y = o[0][1] | o[1][1] << 16;
+        pk.z = o[0][2] | o[1][2] << 16;
+        pk.w = o[0][3] | o[1][3] << 16;
+        *reinterpret_cast<uint4*>(&hs2[j][q]) = pk;
     }
     __syncthreads();
+    PYR_STAMP(4);
+    // vertical pass: lane per column, output rows 8h .. 8h + 7 from row pairs 4h .. 4h + 6
     {
-        const int py = Y0 + r, vy = py - kEdge;
-        if (vy >= 0 && vy < L.h) {
-            unsigned long long w = 0;
-            int outv[8];
+        const int col = tid & (kLW - 1), hh = tid >> 7;
+        const int px = X0 + col;
+        if (col < kTileW && px >= kEdge && px < kEdge + A.w) {
+            uint32_t Pr[7];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                int acc = 0;
+            for (int k = 0; k < 7; ++k) Pr[k] = hs2[4 * hh + k][col];
+            uint8_t* dst = bplane + (size_t)(Y0 + 8 * hh) * A.pitch + px;
 #pragma unroll
-                for (int k = 0; k < 7; ++k) acc += blur_tap(k) * hsum[r + k][c + q];
-                outv[q] = min((acc + (1 << 15)) >> 16, 255);
-                w |= (unsigned long long)outv[q] << (8 * q);
-            }
-            const int px = X0 + c;
-            uint8_t* dst = bplane + (size_t)py * L.pitch + px;
-            if (px >= kEdge && px + 7 < kEdge + L.w) {
-                *reinterpret_cast<unsigned long long*>(dst) = w;
-            } else {
-                for (int q = 0; q < 8; ++q)
-                    if (px + q >= kEdge && px + q < kEdge + L.w) dst[q] = (uint8_t)outv[q];
+            for (int i = 0; i < 8; ++i) {
+                const int m = i >> 1;
+                uint32_t acc = 1u << 15;
+                if ((i & 1) == 0) {
+                    acc = __builtin_amdgcn_udot2(as_u16x2(Pr[m]), w16(18, 34), acc, false);
+                    acc = __builtin_amdgcn_udot2(as_u16x2(Pr[m + 1]), w16(48, 56), acc, false);
+                    acc = __builtin_amdgcn_udot2(as_u16x2(Pr[m + 2]), w16(48, 34), acc, false);
+                    acc = __builtin_amdgcn_udot2(as_u16x2(Pr[m + 3]), w16(18, 0), acc, false);
+                } else {
+                    acc = __builtin_amdgcn_udot2(as_u16x2(Pr[m]), w16(0, 18), acc, false);
+                    acc = __builtin_amdgcn_udot2(as_u16x2(Pr[m + 1]), w16(34, 48), acc, false);
+                    acc = __builtin_amdgcn_udot2(as_u16x2(Pr[m + 2]), w16(56, 48), acc, false);
+                    acc = __builtin_amdgcn_udot2(as_u16x2(Pr[m + 3]), w16(34, 18), acc, false);
+                }
+                const int vy = Y0 + 8 * hh + i - kEdge;
+                if (vy >= 0 && vy < A.h) dst[(size_t)i * A.pitch] = (uint8_t)(acc >> 16);  // <= 255 exactly
             }
         }
     }
+    if (stp) {
+        __syncthreads();
+        if (threadIdx.x == 0) { stp[5] = __builtin_amdgcn_s_memtime(); stp[7] = wall_clock64(); }
+    }
+#undef PYR_STAMP
 }
 
 // ================================================================================================
@@ -2125,18 +2180,59 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
             (void)hipFree(stamps);
         }
     };
+    static const bool pyr_stamps = getenv("ORBGPU_PYR_STAMPS") != nullptr;
     for (int l = 0; l < lfirst; ++l) {
         const orbgpu::LevelGeom& L = k.lv[l];
-        dim3 grid((L.pw + kTileW - 1) / kTileW, (L.ph + kTileH - 1) / kTileH, n);
+        PyrArgs A{};
+        A.frame_bytes = k.pyr_frame_bytes;
+        A.plane_off = L.plane_off;
+        A.w = L.w; A.h = L.h; A.pw = L.pw; A.ph = L.ph; A.pitch = L.pitch;
+        A.xtab_off = L.xtab_off; A.ytab_off = L.ytab_off; A.simd_end = L.simd_end;
+        if (l > 0) {
+            const orbgpu::LevelGeom& P = k.lv[l - 1];
+            A.src_off = P.plane_off + (long long)kEdge * P.pitch + kEdge;
+            A.sw = P.w; A.sh = P.h; A.spitch = P.pitch;
+            A.scx = 1. / ((double)L.w / P.w);
+            A.scy = 1. / ((double)L.h / P.h);
+        }
+        A.tiles_x = (L.pw + kTileW - 1) / kTileW;
+        A.tiles_per_frame = A.tiles_x * ((L.ph + kTileH - 1) / kTileH);
+        A.total = A.tiles_per_frame * n;
+        A.share = (A.total + 7) / 8;  // tiles per XCD (xcd_tile)
+        const dim3 grid(8 * A.share);
+        unsigned long long* stamps = nullptr;
+        if (pyr_stamps && hipMalloc(&stamps, sizeof(unsigned long long) * 8 * grid.x) == hipSuccess)
+            (void)hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * 8 * grid.x, st);
         if (l == 0)
-            hipLaunchKernelGGL(k_pyramid_level<true>, grid, dim3(256), 0, st, e->d_geom, 0, imgs, (long long)frame_stride,
-                               stride, pyr, blr, e->d_xtab, e->d_ytab);
+            hipLaunchKernelGGL(k_pyramid_level<true>, grid, dim3(256), 0, st, A, imgs, (long long)frame_stride, stride,
+                               pyr, blr, e->d_xtab, e->d_ytab, stamps);
         else if (4 * k.lv[l - 1].w <= 5 * L.w && 4 * k.lv[l - 1].h <= 5 * L.h)  // level ratio <= 1.25
-            hipLaunchKernelGGL((k_pyramid_level<false, kSmallBoxH, kSmallBoxW>), grid, dim3(256), 0, st, e->d_geom, l,
-                               nullptr, 0LL, 0, pyr, blr, e->d_xtab, e->d_ytab);
+            hipLaunchKernelGGL((k_pyramid_level<false, kSmallBoxH, kSmallBoxW>), grid, dim3(256), 0, st, A, nullptr,
+                               0LL, 0, pyr, blr, e->d_xtab, e->d_ytab, stamps);
         else
-            hipLaunchKernelGGL((k_pyramid_level<false, kBoxH, kBoxW>), grid, dim3(256), 0, st, e->d_geom, l, nullptr, 0LL,
-                               0, pyr, blr, e->d_xtab, e->d_ytab);
+            hipLaunchKernelGGL((k_pyramid_level<false, kBoxH, kBoxW>), grid, dim3(256), 0, st, A, nullptr, 0LL, 0, pyr,
+                               blr, e->d_xtab, e->d_ytab, stamps);
+        if (stamps) {  // debug: phase clocks of this level's blocks
+            std::vector<unsigned long long> hst((size_t)8 * grid.x);
+            (void)hipStreamSynchronize(st);
+            (void)hipMemcpy(hst.data(), stamps, hst.size() * 8, hipMemcpyDeviceToHost);
+            (void)hipFree(stamps);
+            double ph[6] = {0}, life = 0;
+            unsigned long long t0 = ~0ull, t1 = 0;
+            int cnt = 0;
+            for (unsigned b = 0; b < grid.x; ++b) {
+                const unsigned long long* q = &hst[(size_t)8 * b];
+                if (!q[6]) continue;
+                ++cnt;
+                for (int i = 1; i < 6; ++i) ph[i] += (double)(q[i] - q[i - 1]);
+                life += (double)(q[7] - q[6]);
+                t0 = std::min(t0, q[6]);
+                t1 = std::max(t1, q[7]);
+            }
+            fprintf(stderr, "pyr-stamps L%d blocks %d span %.1f us  mean life %.2f us  concurrency %.0f  phases(cyc) box %.0f resize %.0f store %.0f hblur %.0f vblur %.0f\n",
+                    l, cnt, (t1 - t0) * 0.01, life / cnt * 0.01, life / (double)(t1 - t0), ph[1] / cnt, ph[2] / cnt,
+                    ph[3] / cnt, ph[4] / cnt, ph[5] / cnt);
+        }
         if (split && l == split - 1) {
             hipEventRecord(e->split_ev[0], st);
             hipStreamWaitEvent(e->side, e->split_ev[0], 0);
