@@ -128,6 +128,8 @@ __device__ __forceinline__ int wave_incl_max_dpp(int v) {
 // ================================================================================================
 // 1. pyramid level: padded plane + blurred view, src:1687-1740 and src:1629-1637
 // ================================================================================================
+constexpr int kBufDword3 = 0x00020000;  // gfx9 buffer resource word 3 (32-bit data format)
+
 // A tile is 122 x 16 padded-plane pixels; with the 3-px blur halo it is 128 x 22, one lane per column.
 constexpr int kTileW = 122, kTileH = 16, kHalo = 3;
 constexpr int kLW = kTileW + 2 * kHalo, kLH = kTileH + 2 * kHalo;  // 128 x 22
@@ -195,8 +197,8 @@ struct PyrArgs {
     int w, h, pw, ph, pitch;       // this level
     int sw, sh, spitch;            // previous level view (level > 0)
     int xtab_off, ytab_off, simd_end;
-    int tiles_x, tiles_per_frame, total, share;
-    double scx, scy;               // cv::resize scale: 1 / ((double)w / sw), 1 / ((double)h / sh)
+    int tiles_per_frame, share;    // share: tiles of a frame per XCD (blockIdx.x -> tile, pyr_tile)
+    int tab_off;                   // this level's tile table (tile_tables)
 };
 
 template <bool kLevel0, int kBH = kSmallBoxH, int kBW = kSmallBoxW>
@@ -204,13 +206,18 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
                                                           long long in_frame_stride, int in_stride,
                                                           uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                                           const int2* __restrict__ xtab, const int4* __restrict__ ytab,
+                                                          const int4* __restrict__ tiletab,
                                                           unsigned long long* __restrict__ stamps) {
+    // blockIdx.y = frame; blockIdx.x -> tile of the frame, XCD-chunked (xcd_tile)
     const int t = xcd_tile(blockIdx.x, A.share);
-    if (t >= A.total) return;
+    if (t >= A.tiles_per_frame) return;
+    const int f = blockIdx.y;
     // debug (ORBGPU_PYR_STAMPS): per-block phase clocks, thread 0 of each block
-    unsigned long long* stp = stamps ? stamps + (size_t)blockIdx.x * 8 : nullptr;
+    unsigned long long* stp = stamps ? stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 : nullptr;
     if (stp && threadIdx.x == 0) { stp[6] = wall_clock64(); stp[0] = __builtin_amdgcn_s_memtime(); }
 #define PYR_STAMP(k) do { if (stp && threadIdx.x == 0) stp[k] = __builtin_amdgcn_s_memtime(); } while (0)
+    // tile record (scalar load): origin, and for level > 0 the previous-level view box it reads
+    const int4 T = tiletab[A.tab_off + t];
     constexpr int kBoxWords = kBW / 4;
     constexpr int kPairs = kLH / 2;      // 11 row pairs of horizontal sums
     constexpr int kQuads = (kTileW + 3) / 4;
@@ -218,11 +225,9 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
     __shared__ __attribute__((aligned(16))) uint8_t tile[kLH][kLW + 8];      // +8: the last quad's over-read
     __shared__ __attribute__((aligned(16))) uint32_t hs2[kPairs][kLW];       // (row 2j, row 2j+1) sums, <= 255 * 256
     __shared__ int4 yrow[kLevel0 ? 1 : kLH];  // per tile row: box row offsets of the two source rows, weights
-    const int f = t / A.tiles_per_frame, rem = t - f * A.tiles_per_frame;
-    const int tyi = rem / A.tiles_x;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = uniform(tid >> 6);
-    const int X0 = (rem - tyi * A.tiles_x) * kTileW, Y0 = tyi * kTileH;
+    const int X0 = T.x & 0xffff, Y0 = T.x >> 16;
     uint8_t* plane = pyr + (size_t)f * A.frame_bytes + A.plane_off;
     uint8_t* bplane = blur + (size_t)f * A.frame_bytes + A.plane_off;
     // this lane's tile column (waves 0/1: rows [0, 11), waves 2/3: rows [11, 22)) in view coordinates
@@ -234,28 +239,24 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
         const uint8_t* src = in + (size_t)f * in_frame_stride + vx;
         int v[kLH / 2];
 #pragma unroll
-        for (int k = 0; k < kLH / 2; ++k) v[k] = src[(size_t)reflect101(Y0 - kHalo + r0 + k - kEdge, A.h) * in_stride];
+        for (int k = 0; k < kLH / 2; ++k) v[k] = src[reflect101(Y0 - kHalo + r0 + k - kEdge, A.h) * in_stride];
 #pragma unroll
         for (int k = 0; k < kLH / 2; ++k) tile[r0 + k][tx] = (uint8_t)v[k];
         __syncthreads();
         PYR_STAMP(1);
         PYR_STAMP(2);
     } else {
-        // view-coordinate ranges this tile (+halo) reads
-        int vx0, vx1, vy0, vy1;
-        reflect_range(X0 - kHalo - kEdge, X0 + kTileW + kHalo - 1 - kEdge, A.w, vx0, vx1);
-        reflect_range(Y0 - kHalo - kEdge, Y0 + kTileH + kHalo - 1 - kEdge, A.h, vy0, vy1);
-        const uint8_t* src = pyr + (size_t)f * A.frame_bytes + A.src_off;
-        const int bx0 = resize_src_index(vx0, A.scx, A.sw);
-        const int by0 = resize_src_index(vy0, A.scy, A.sh);
-        const int bw = min(resize_src_index(vx1, A.scx, A.sw) + 1, A.sw - 1) - bx0 + 1;
-        const int bh = min(resize_src_index(vy1, A.scy, A.sh) + 1, A.sh - 1) - by0 + 1;
+        const int bx0 = T.y & 0xffff, bw = T.y >> 16, by0 = T.z & 0xffff, bh = T.z >> 16;
         // source box as aligned dwords (over-reads stay inside the previous level's 19-px frame);
-        // src_off and spitch are multiples of 128, so every box row has the same alignment
-        const uint8_t* row0 = src + (size_t)by0 * A.spitch + bx0;
-        const int shift = (int)((uintptr_t)row0 & 3);
-        const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(row0 - shift);
-        const int nw = (shift + bw + 3) >> 2;
+        // src_off and spitch are multiples of 128, so every box row has the same alignment.  Buffer
+        // loads: one 32-bit lane offset, the row step in the scalar offset.
+        const int shift = (int)((A.src_off + bx0) & 3);  // plane and frame blocks are 256-B aligned
+        // The whole kBH x kBW box is loaded (rows and words past the tile's need are never read); the
+        // descriptor's range ends with the frame's pyramid block, so reads past it return 0.
+        const long long box_off = A.src_off + (long long)by0 * A.spitch + (bx0 - shift);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            pyr + (size_t)f * A.frame_bytes + box_off, (short)0, (int)(A.frame_bytes - box_off), kBufDword3);
+        (void)bh;
         uint32_t* boxw = reinterpret_cast<uint32_t*>(box);
         const int rg = tid >> 6;
         // every global load of the block issued before the first LDS store (one round trip): the box,
@@ -266,8 +267,9 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
         for (int q = 0; q < kRowPass; ++q)
 #pragma unroll
             for (int hx = 0; hx < kWordPass; ++hx) {
-                const int r = 4 * q + rg, w = lane + 64 * hx;
-                v[q][hx] = (r < bh && w < nw) ? wsrc[(size_t)r * (A.spitch >> 2) + w] : 0u;
+                const int w = lane + 64 * hx;
+                v[q][hx] = (w < kBoxWords)
+                               ? __builtin_amdgcn_raw_buffer_load_b32(rs, rg * A.spitch + 4 * w, 4 * q * A.spitch, 0) : 0u;
             }
         int4 yv = make_int4(0, 0, 0, 0);
         if (tid < kLH) yv = ytab[A.ytab_off + reflect101(Y0 - kHalo + tid - kEdge, A.h)];
@@ -277,7 +279,7 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
 #pragma unroll
             for (int hx = 0; hx < kWordPass; ++hx) {
                 const int r = 4 * q + rg, w = lane + 64 * hx;
-                if (r < bh && w < nw) boxw[r * kBoxWords + w] = v[q][hx];
+                if (w < kBoxWords) boxw[r * kBoxWords + w] = v[q][hx];
             }
         if (tid < kLH) yrow[tid] = make_int4((yv.x - by0) * kBW, (yv.y - by0) * kBW, yv.z, yv.w);
         __syncthreads();
@@ -287,6 +289,8 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
         // VResizeLinearVec_32s8u (vx < simd_end): v_mul_hi on S >> 4 (S <= 255 * 2049, so S >> 4 <
         // 32767 and the reference's int16 saturation never triggers), rounding shift by 2;
         // else FixedPtCast<int, uchar, 22>.
+        // (two separate byte reads: an adjacent pair would be merged into an unaligned ds_read_u16,
+        // which gfx950 replays -- measured 5x slower for the whole phase)
         const int sx = X.x - bx0 + shift, sx1 = min(X.x + 1, bx0 + bw - 1) - bx0 + shift;
         const unsigned a0 = X.y & 0xffff, a1 = (unsigned)X.y >> 16;
         const bool simd = vx < A.simd_end;
@@ -302,7 +306,7 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
                 const int4 Y = yrow[r0 + k];  // LDS broadcast
                 const int p0 = (int)__umul24((unsigned)hrow(Y.x), (unsigned)Y.z);  // < 2^20 * 2^11
                 const int p1 = (int)__umul24((unsigned)hrow(Y.y), (unsigned)Y.w);
-                int v = ((p0 >> 16) + (p1 >> 16) + 2) >> 2;
+                int v = ((p0 >> 16) + (p1 >> 16) + 2) >> 2;  // <= (2 * 1020 + 2) >> 2 = 255
                 if (kMixed && !simd) v = min((p0 + p1 + (1 << 21)) >> 22, 255);
                 tile[r0 + k][tx] = (uint8_t)v;
             }
@@ -378,7 +382,7 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
                     acc = __builtin_amdgcn_udot2(as_u16x2(Pr[m + 3]), w16(34, 18), acc, false);
                 }
                 const int vy = Y0 + 8 * hh + i - kEdge;
-                if (vy >= 0 && vy < A.h) dst[(size_t)i * A.pitch] = (uint8_t)(acc >> 16);  // <= 255 exactly
+                if (vy >= 0 && vy < A.h) dst[i * A.pitch] = (uint8_t)(acc >> 16);  // <= 255 exactly
             }
         }
     }
@@ -1665,7 +1669,6 @@ constexpr int kDescKpPerBlock = 8;
 constexpr int kPB = 37, kPBW = 10;  // blurred patch rows, dwords per row
 constexpr int kPU = 31, kPUW = 9;   // disc box rows, dwords per row
 constexpr int kDescLds = kPB * kPBW * 4 + kPU * kPUW * 4;  // 2596 bytes per keypoint
-constexpr int kBufDword3 = 0x00020000;  // gfx9 buffer resource word 3 (32-bit data format)
 
 __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__ gp, const uint8_t* __restrict__ pyr,
                                                   const uint8_t* __restrict__ blur, const uint32_t* __restrict__ sel,
@@ -1831,6 +1834,8 @@ struct Extractor {
     orbgpu::KernelGeom* d_geom = nullptr;  // kernel geometry in device memory (read by every kernel)
     CellDesc* d_cells = nullptr; size_t cells_cap = 0;
     int2* d_xtab = nullptr; size_t xtab_cap = 0;
+    int4* d_tiletab = nullptr; size_t tiletab_cap = 0;  // pyramid tile records (tile_tables)
+    int tile_off[orbgpu::kMaxLevels] = {};
     int4* d_ytab = nullptr; size_t ytab_cap = 0;
     uint8_t* d_pyr = nullptr; size_t pyr_cap = 0;
     uint8_t* d_blur = nullptr; size_t blur_cap = 0;
@@ -1901,6 +1906,47 @@ int grow(T*& p, size_t& cap, size_t need) {
     return ORB_OK;
 }
 
+// Tile records of every pyramid level, one int4 per tile of a frame (row-major):
+//   x: X0 | Y0 << 16 (padded-plane origin)
+//   y: bx0 | bw << 16, z: by0 | bh << 16 (level > 0): the previous-level view box the tile (+3-px halo)
+//      reads -- the view range it covers under REFLECT_101, mapped through cv::resize's source index
+//      (the same double expressions as resize_src_index), plus the second bilinear tap
+void tile_tables(const orbgpu::KernelGeom& k, std::vector<int4>& tab, int* off) {
+    auto refl = [](int a, int b, int len, int& lo, int& hi) {
+        lo = 1 << 30; hi = -1;
+        if (a < 0) { const int e2 = std::min(b, -1); lo = std::min(lo, -e2); hi = std::max(hi, -a); }
+        if (b >= 0 && a < len) { lo = std::min(lo, std::max(a, 0)); hi = std::max(hi, std::min(b, len - 1)); }
+        if (b >= len) { const int s0 = std::max(a, len); lo = std::min(lo, 2 * len - 2 - b); hi = std::max(hi, 2 * len - 2 - s0); }
+    };
+    auto src = [](int d, double scale, int slen) {
+        const float f = (float)((d + 0.5) * scale - 0.5);
+        int s2 = (int)f;
+        s2 -= (s2 > f);
+        return std::min(std::max(s2, 0), slen - 1);
+    };
+    tab.clear();
+    for (int l = 0; l < k.nlevels; ++l) {
+        const orbgpu::LevelGeom& L = k.lv[l];
+        off[l] = (int)tab.size();
+        for (int Y0 = 0; Y0 < L.ph; Y0 += kTileH)
+            for (int X0 = 0; X0 < L.pw; X0 += kTileW) {
+                int4 r = make_int4(X0 | Y0 << 16, 0, 0, 0);
+                if (l > 0) {
+                    const orbgpu::LevelGeom& P = k.lv[l - 1];
+                    const double scx = 1. / ((double)L.w / P.w), scy = 1. / ((double)L.h / P.h);
+                    int a, b;
+                    refl(X0 - kHalo - kEdge, X0 + kTileW + kHalo - 1 - kEdge, L.w, a, b);
+                    const int bx0 = src(a, scx, P.w), bw = std::min(src(b, scx, P.w) + 1, P.w - 1) - bx0 + 1;
+                    refl(Y0 - kHalo - kEdge, Y0 + kTileH + kHalo - 1 - kEdge, L.h, a, b);
+                    const int by0 = src(a, scy, P.h), bh = std::min(src(b, scy, P.h) + 1, P.h - 1) - by0 + 1;
+                    r.y = bx0 | bw << 16;
+                    r.z = by0 | bh << 16;
+                }
+                tab.push_back(r);
+            }
+    }
+}
+
 int prepare(Extractor* e, int w, int h, int n) {
     if (w != e->cur_w || h != e->cur_h) {
         // the tables below are read by in-flight launches of the previous frame size
@@ -1922,6 +1968,11 @@ int prepare(Extractor* e, int w, int h, int n) {
             hipMemcpy(e->d_cells, g.cells.data(), g.cells.size() * sizeof(orbgpu::CellDesc), hipMemcpyHostToDevice) != hipSuccess ||
             (!g.xtab.empty() && hipMemcpy(e->d_xtab, g.xtab.data(), g.xtab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) ||
             (!g.ytab.empty() && hipMemcpy(e->d_ytab, g.ytab.data(), g.ytab.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
+            return orbgpu_fail(ORB_ERR_DEVICE, "table upload failed");
+        std::vector<int4> tt;
+        tile_tables(g.k, tt, e->tile_off);
+        if ((rc = grow(e->d_tiletab, e->tiletab_cap, tt.size())) != ORB_OK) return rc;
+        if (hipMemcpy(e->d_tiletab, tt.data(), tt.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess)
             return orbgpu_fail(ORB_ERR_DEVICE, "table upload failed");
         e->geo_ok = true;
         // quad-tree LDS: node metadata of the largest level + room for ~7k keys (80 KB: two
@@ -2192,35 +2243,33 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
             const orbgpu::LevelGeom& P = k.lv[l - 1];
             A.src_off = P.plane_off + (long long)kEdge * P.pitch + kEdge;
             A.sw = P.w; A.sh = P.h; A.spitch = P.pitch;
-            A.scx = 1. / ((double)L.w / P.w);
-            A.scy = 1. / ((double)L.h / P.h);
         }
-        A.tiles_x = (L.pw + kTileW - 1) / kTileW;
-        A.tiles_per_frame = A.tiles_x * ((L.ph + kTileH - 1) / kTileH);
-        A.total = A.tiles_per_frame * n;
-        A.share = (A.total + 7) / 8;  // tiles per XCD (xcd_tile)
-        const dim3 grid(8 * A.share);
+        A.tab_off = e->tile_off[l];
+        A.tiles_per_frame = ((L.pw + kTileW - 1) / kTileW) * ((L.ph + kTileH - 1) / kTileH);
+        A.share = (A.tiles_per_frame + 7) / 8;  // tiles of a frame per XCD (xcd_tile)
+        const dim3 grid(8 * A.share, n);
         unsigned long long* stamps = nullptr;
-        if (pyr_stamps && hipMalloc(&stamps, sizeof(unsigned long long) * 8 * grid.x) == hipSuccess)
-            (void)hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * 8 * grid.x, st);
+        const size_t nblk = (size_t)grid.x * grid.y;
+        if (pyr_stamps && hipMalloc(&stamps, sizeof(unsigned long long) * 8 * nblk) == hipSuccess)
+            (void)hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * 8 * nblk, st);
         if (l == 0)
             hipLaunchKernelGGL(k_pyramid_level<true>, grid, dim3(256), 0, st, A, imgs, (long long)frame_stride, stride,
-                               pyr, blr, e->d_xtab, e->d_ytab, stamps);
+                               pyr, blr, e->d_xtab, e->d_ytab, e->d_tiletab, stamps);
         else if (4 * k.lv[l - 1].w <= 5 * L.w && 4 * k.lv[l - 1].h <= 5 * L.h)  // level ratio <= 1.25
             hipLaunchKernelGGL((k_pyramid_level<false, kSmallBoxH, kSmallBoxW>), grid, dim3(256), 0, st, A, nullptr,
-                               0LL, 0, pyr, blr, e->d_xtab, e->d_ytab, stamps);
+                               0LL, 0, pyr, blr, e->d_xtab, e->d_ytab, e->d_tiletab, stamps);
         else
             hipLaunchKernelGGL((k_pyramid_level<false, kBoxH, kBoxW>), grid, dim3(256), 0, st, A, nullptr, 0LL, 0, pyr,
-                               blr, e->d_xtab, e->d_ytab, stamps);
+                               blr, e->d_xtab, e->d_ytab, e->d_tiletab, stamps);
         if (stamps) {  // debug: phase clocks of this level's blocks
-            std::vector<unsigned long long> hst((size_t)8 * grid.x);
+            std::vector<unsigned long long> hst((size_t)8 * nblk);
             (void)hipStreamSynchronize(st);
             (void)hipMemcpy(hst.data(), stamps, hst.size() * 8, hipMemcpyDeviceToHost);
             (void)hipFree(stamps);
             double ph[6] = {0}, life = 0;
             unsigned long long t0 = ~0ull, t1 = 0;
             int cnt = 0;
-            for (unsigned b = 0; b < grid.x; ++b) {
+            for (size_t b = 0; b < nblk; ++b) {
                 const unsigned long long* q = &hst[(size_t)8 * b];
                 if (!q[6]) continue;
                 ++cnt;
@@ -2378,7 +2427,7 @@ int orb_extractor_destroy(orb_extractor_t h) {
     Extractor* e = reinterpret_cast<Extractor*>(h);
     if (!e) return ORB_ERR_ARG;
     if (e->stream) hipStreamSynchronize(e->stream);
-    void* bufs[] = {e->d_tasks, e->d_ntasks, e->d_stamps, e->d_geom, e->d_cells, e->d_xtab, e->d_ytab, e->d_pyr, e->d_blur, e->d_cand, e->d_scratch,
+    void* bufs[] = {e->d_tasks, e->d_ntasks, e->d_stamps, e->d_geom, e->d_cells, e->d_xtab, e->d_tiletab, e->d_ytab, e->d_pyr, e->d_blur, e->d_cand, e->d_scratch,
                     e->d_cell_count, e->d_cell_thr, e->d_sel, e->d_dst, e->d_sel_count, e->d_lap_count, e->d_status,
                     e->d_img, e->d_kps, e->d_desc, e->d_counts};
     for (void* b : bufs)
