@@ -778,12 +778,14 @@ __device__ __forceinline__ bool has_run9(unsigned m) {
 
 __device__ __forceinline__ bool fast_corner(const uint8_t* __restrict__ p, const int (&off)[16], int t) {
     const int v = p[0], hi = v + t, lo = v - t;
+    // masks in reverse circle order (a 9-run is a 9-run either way): each bit is the sign of a
+    // difference shifted in with one v_alignbit
     unsigned bm = 0, dm = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const int x = p[off[k]];
-        bm |= (unsigned)(x > hi) << k;
-        dm |= (unsigned)(x < lo) << k;
+        bm = __builtin_amdgcn_alignbit(bm, (unsigned)(hi - x), 31);  // x > hi
+        dm = __builtin_amdgcn_alignbit(dm, (unsigned)(x - lo), 31);  // x < lo
     }
     return has_run9(bm) || has_run9(dm);
 }
@@ -876,9 +878,11 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
                 const uint8_t* q = win + idx;
                 const int v = q[0], hi = v + mint, lo = v - mint;
                 const int p0 = q[off[0]], p4 = q[off[4]], p8 = q[off[8]], p12 = q[off[12]];
-                const bool b0 = p0 > hi, b4 = p4 > hi, b8 = p8 > hi, b12 = p12 > hi;
-                const bool d0 = p0 < lo, d4 = p4 < lo, d8 = p8 < lo, d12 = p12 < lo;
-                pass = (b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0) | (d0 & d4) | (d4 & d8) | (d8 & d12) | (d12 & d0);
+                // a bright (dark) adjacent compass pair <=> the largest pairwise minimum exceeds hi
+                // (the smallest pairwise maximum is below lo): min/max instead of 16 boolean terms
+                const int bmax = max(max(min(p0, p4), min(p4, p8)), max(min(p8, p12), min(p12, p0)));
+                const int dmin = min(min(max(p0, p4), max(p4, p8)), min(max(p8, p12), max(p12, p0)));
+                pass = (bmax > hi) | (dmin < lo);
             }
             const unsigned long long m = ballot(pass);
             if (pass) cl[nlist + rank_in(m)] = (uint16_t)idx;
