@@ -1315,39 +1315,57 @@ __device__ void qt_run(QTree& t, int K, int N, int nroots, float root_w, int spa
         if (debug_flags & 4) { const unsigned long long now = __builtin_amdgcn_s_memtime(); tm[i] += now - t_last; t_last = now; }
     };
     // ---- gather candidates in cell order into keys[1], counting per root (src:756-764).
-    // One lane per cell (cells in chunks of 64); destinations from a wave scan of the cell counts.
+    // Cells in chunks of 64 (lane = cell, a wave scan of the counts gives each cell's start); the
+    // chunk's keys are then spread evenly over the lanes, each lane finding its key's cell by a binary
+    // search over the lanes' starts, with up to 8 x 64 loads in flight per round trip.
     int rcount[kMaxRoots];
 #pragma unroll
     for (int r = 0; r < kMaxRoots; ++r) rcount[r] = 0;
     {
+        constexpr int kGB = 8;
         int carry = 0;
         for (int cb = 0; cb < cell_count; cb += 64) {
             const int c = cb + lane;
             int n = 0, slot = 0;
             if (c < cell_count) { n = ccount[c]; slot = cells[cell_begin + c].slot; }
             const int incl = wave_incl_scan(n, lane);
-            const int start = carry + incl - n;
-            const uint32_t* src = cand_level + slot;
-            for (int i0 = 0; i0 < n; i0 += 8) {
-                uint32_t kk[8];
+            const int start = incl - n;  // chunk-local, non-decreasing over the lanes
+            const int T = uniform(__builtin_amdgcn_readlane(incl, 63));
+            for (int j0 = 0; j0 < T; j0 += 64 * kGB) {
+                uint32_t kk[kGB];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) kk[j] = i0 + j < n ? src[i0 + j] : 0;
+                for (int gi = 0; gi < kGB; ++gi) {
+                    const int i = j0 + 64 * gi + lane;
+                    // the last lane whose start <= i owns key i (empty cells share the next start)
+                    int cl = 0;
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    if (i0 + j >= n) break;
-                    t.keys1[start + i0 + j] = kk[j];
-                    const int root = (int)((float)key_x(kk[j]) / root_w);
+                    for (int s = 32; s > 0; s >>= 1)
+                        if (__shfl(start, cl + s, 64) <= i) cl += s;
+                    const int sl = __shfl(slot, cl, 64), s0 = __shfl(start, cl, 64);
+                    kk[gi] = i < T ? cand_level[sl + (i - s0)] : 0u;
+                }
 #pragma unroll
-                    for (int r = 0; r < kMaxRoots; ++r) rcount[r] += root == r;
+                for (int gi = 0; gi < kGB; ++gi) {
+                    const int i = j0 + 64 * gi + lane;
+                    if (i < T) {
+                        t.keys1[carry + i] = kk[gi];
+                        const int root = (int)((float)key_x(kk[gi]) / root_w);
+#pragma unroll
+                        for (int r = 0; r < kMaxRoots; ++r) rcount[r] += root == r;
+                    }
                 }
             }
-            carry += __builtin_amdgcn_readlane(incl, 63);
+            carry += T;
         }
 #pragma unroll
         for (int r = 0; r < kMaxRoots; ++r) rcount[r] = uniform(wave_sum(rcount[r]));
     }
     wave_sync();
-    {   // stable partition by root into keys[0]
+    if (nroots == 1) {  // one root: the gathered order already is the root's key order
+        uint32_t* k0 = t.keys0;
+        t.keys0 = t.keys1;
+        t.keys1 = k0;
+    } else {   // stable partition by root into keys[0]
         int base[kMaxRoots];
         int acc = 0;
 #pragma unroll
@@ -1357,8 +1375,7 @@ __device__ void qt_run(QTree& t, int K, int N, int nroots, float root_w, int spa
             int root = -1;
             uint32_t k = 0;
             if (i < K) { k = t.keys1[i]; root = (int)((float)key_x(k) / root_w); }
-#pragma unroll
-            for (int r = 0; r < kMaxRoots; ++r) {
+            for (int r = 0; r < nroots; ++r) {
                 const unsigned long long m = ballot(root == r);
                 if (root == r) t.keys0[base[r] + rank_in(m)] = k;
                 base[r] += __popcll(m);
@@ -1864,6 +1881,7 @@ struct Extractor {
     int chunk = 1 << 30, nstreams = 1;  // off by default: measured slower (streams did not overlap)
     int fast_split = 3;                 // FAST on levels [0, fast_split) overlaps the small pyramid levels
     int fast_per_level = 0;             // 1: FAST of each later level right after its pyramid level (side2); measured slower
+    int qt_split = 0;                   // 1: quad-tree of levels [0, fast_split) on the side stream (ORBGPU_QT_SPLIT)
     hipStream_t side = nullptr, side2 = nullptr;
     hipEvent_t split_ev[3] = {};
     hipEvent_t lvl_ev[orbgpu::kMaxLevels] = {};
@@ -2290,6 +2308,7 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
             hipEventRecord(e->split_ev[0], st);
             hipStreamWaitEvent(e->side, e->split_ev[0], 0);
             launch_fast(0, split, e->side);
+            if (e->qt_split) launch_qt(0, split, e->side);
             hipEventRecord(e->split_ev[1], e->side);
         } else if (split && l >= split && e->fast_per_level) {
             // later (small) levels: FAST as soon as the level exists, on a second side stream
@@ -2308,11 +2327,12 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     } else {
         launch_fast(split, k.nlevels, st);
     }
-    if (split && (!band || split <= lfirst)) hipStreamWaitEvent(st, e->split_ev[1], 0);
+    // qt_split: the quad-tree of the early levels runs on the side stream right after their FAST
+    const bool qts = e->qt_split && split && !band && !e->fast_per_level;
+    if (!qts && split && (!band || split <= lfirst)) hipStreamWaitEvent(st, e->split_ev[1], 0);
     mark(2);
-    // (running the quad-tree of the early levels on the side stream was measured slower: its
-    // 80 KB-LDS waves crowd out the FAST work of the late levels)
-    launch_qt(0, k.nlevels, st);
+    launch_qt(qts ? split : 0, k.nlevels, st);
+    if (qts) hipStreamWaitEvent(st, e->split_ev[1], 0);
     mark(3);
     mark(4);
     {
@@ -2391,6 +2411,7 @@ int orb_extractor_create(const orb_params_t* p, int max_width, int max_height, i
         ok = hipEventCreateWithFlags(&e->lvl_ev[k2], hipEventDisableTiming) == hipSuccess;
     if (const char* c = getenv("ORBGPU_FAST_PER_LEVEL")) e->fast_per_level = atoi(c);
     if (const char* c = getenv("ORBGPU_PYR_BAND")) e->band_mode = atoi(c);
+    if (const char* c = getenv("ORBGPU_QT_SPLIT")) e->qt_split = atoi(c);
     if (const char* c = getenv("ORBGPU_PYR_WG_PER_CU")) e->band_wg_per_cu = std::max(1, atoi(c));
     if (const char* c = getenv("ORBGPU_PYR_BAND_FROM")) e->band_from = std::max(0, atoi(c));
     if (const char* c = getenv("ORBGPU_PYR_BAND_R")) e->band_r = std::min(16, std::max(4, atoi(c)));
