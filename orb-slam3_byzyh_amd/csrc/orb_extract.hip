@@ -796,13 +796,18 @@ __device__ __forceinline__ bool fast_corner(const uint8_t* __restrict__ p, const
 __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict__ gp, const CellDesc* __restrict__ cells, int win_cap,
                                                     const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
                                                     int32_t* __restrict__ cell_count, uint8_t* __restrict__ cell_thr,
-                                                    int cell0, int cell_end) {
+                                                    int cell0, int cell_end, unsigned long long* __restrict__ stamps) {
     const KernelGeom& g = *gp;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int cid = cell0 + blockIdx.x * 4 + wave;
     const int f = blockIdx.y;
     if (cid >= cell_end) return;
+    // debug (ORBGPU_FAST_STAMPS): per-cell phase clocks of lane 0 (0 start .. 6 end, 7 wall start, 8 wall end,
+    // 9 survivors, 10 corners)
+    unsigned long long* stp = stamps ? stamps + ((size_t)f * (cell_end - cell0) + (cid - cell0)) * 12 : nullptr;
+    if (stp && lane == 0) { stp[7] = wall_clock64(); stp[0] = __builtin_amdgcn_s_memtime(); }
+#define FAST_STAMP(k) do { if (stp && lane == 0) stp[k] = __builtin_amdgcn_s_memtime(); } while (0)
     const CellDesc C = cells[cid];
     const LevelGeom& L = g.lv[C.level];
     const uint8_t* view = pyr + (size_t)f * g.pyr_frame_bytes + L.plane_off + (size_t)kEdge * L.pitch + kEdge;
@@ -851,6 +856,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
         }
     }
     wave_sync();
+    FAST_STAMP(1);
     win += shift;  // window pixel (r, c) is at win[r * ws + c]; same layout for the score map
     sc += shift;
     const int dw = ww - 6, dh = wh - 6;
@@ -868,31 +874,60 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
     //     pixels are compacted (row-major) into cl[].
     int nlist = 0;
     if (nd > 0) {
-        const int dr = 64 / dw, dc = 64 - dr * dw;
-        int r = lane / dw, c = lane - (lane / dw) * dw;
-        for (int i0 = 0; i0 < nd; i0 += 64) {
-            bool pass = false;
-            int idx = 0;
-            if (i0 + lane < nd) {
-                idx = (r + 3) * ws + (c + 3);
-                const uint8_t* q = win + idx;
-                const int v = q[0], hi = v + mint, lo = v - mint;
-                const int p0 = q[off[0]], p4 = q[off[4]], p8 = q[off[8]], p12 = q[off[12]];
-                // a bright (dark) adjacent compass pair <=> the largest pairwise minimum exceeds hi
-                // (the smallest pairwise maximum is below lo): min/max instead of 16 boolean terms
-                const int bmax = max(max(min(p0, p4), min(p4, p8)), max(min(p8, p12), min(p12, p0)));
-                const int dmin = min(min(max(p0, p4), max(p4, p8)), min(max(p8, p12), max(p12, p0)));
-                pass = (bmax > hi) | (dmin < lo);
+        // Four pixels per lane (a quad of one detectable row), as u16 pairs: the centre, left (x-3),
+        // right (x+3) dwords of the row and the up / down (y-/+3) dwords come from aligned LDS dwords
+        // and v_alignbyte, and a bright (dark) adjacent compass pair <=> the largest pairwise minimum
+        // exceeds v + t (the smallest pairwise maximum plus t is below v), with v_pk_min/max_u16 and
+        // saturating v_pk_sub_u16.  Items are row-major quads, so the compaction stays row-major.
+        const int nq = (dw + 3) >> 2, nitems = dh * nq;
+        const uint32_t* wrow = reinterpret_cast<const uint32_t*>(win - shift);  // aligned window rows
+        const int wsw = ws >> 2;
+        // byte offset o (window coordinates, + shift) -> dword o >> 2, alignbyte o & 3
+        const int oc = shift + 3, orr = shift + 6;
+        const u16x2 tt = w16(mint, mint);
+        auto ext = [&](const uint32_t* row, int q, int o) {  // bytes [4q + o - shift .. +3] of a row
+            const int d = q + (o >> 2);
+            return __builtin_amdgcn_alignbyte(row[d + 1], row[d], o & 3);
+        };
+        auto lo16 = [](uint32_t v) { return as_u16x2(__builtin_amdgcn_perm(v, v, 0x0c010c00u)); };
+        auto hi16 = [](uint32_t v) { return as_u16x2(__builtin_amdgcn_perm(v, v, 0x0c030c02u)); };
+        auto pass2 = [&](u16x2 v, u16x2 p0, u16x2 p4, u16x2 p8, u16x2 p12) {
+            const u16x2 bmax = __builtin_elementwise_max(
+                __builtin_elementwise_max(__builtin_elementwise_min(p0, p4), __builtin_elementwise_min(p4, p8)),
+                __builtin_elementwise_max(__builtin_elementwise_min(p8, p12), __builtin_elementwise_min(p12, p0)));
+            const u16x2 dmin = __builtin_elementwise_min(
+                __builtin_elementwise_min(__builtin_elementwise_max(p0, p4), __builtin_elementwise_max(p4, p8)),
+                __builtin_elementwise_min(__builtin_elementwise_max(p8, p12), __builtin_elementwise_max(p12, p0)));
+            const u16x2 br = __builtin_elementwise_sub_sat(bmax, v + tt);  // > 0 <=> bmax > v + t
+            const u16x2 dk = __builtin_elementwise_sub_sat(v, dmin + tt);  // > 0 <=> dmin < v - t
+            return __builtin_bit_cast(uint32_t, br) | __builtin_bit_cast(uint32_t, dk);
+        };
+        for (int i0 = 0; i0 < nitems; i0 += 64) {
+            const int it = i0 + lane;
+            const int r = it / nq, q = it - r * nq;
+            unsigned bits = 0;
+            if (it < nitems) {
+                const uint32_t* rc = wrow + (r + 3) * wsw;
+                const uint32_t L4 = ext(rc, q, shift), C4 = ext(rc, q, oc), R4 = ext(rc, q, orr);
+                const uint32_t U4 = ext(rc - 3 * wsw, q, oc), D4 = ext(rc + 3 * wsw, q, oc);
+                const uint32_t pl = pass2(lo16(C4), lo16(D4), lo16(R4), lo16(U4), lo16(L4));
+                const uint32_t ph = pass2(hi16(C4), hi16(D4), hi16(R4), hi16(U4), hi16(L4));
+                bits = ((pl & 0xffffu) != 0) | ((pl >> 16) != 0) << 1 | ((ph & 0xffffu) != 0) << 2 | ((ph >> 16) != 0) << 3;
+                const int rem = dw - 4 * q;  // pixels of this quad inside the detectable row
+                if (rem < 4) bits &= (1u << rem) - 1u;
             }
-            const unsigned long long m = ballot(pass);
-            if (pass) cl[nlist + rank_in(m)] = (uint16_t)idx;
-            nlist += __popcll(m);
-            c += dc;
-            r += dr;
-            if (c >= dw) { c -= dw; r++; }
+            const int cnt = __popc(bits);
+            const int incl = wave_incl_scan_dpp(cnt);
+            int pos = nlist + incl - cnt;
+            const int base_idx = (r + 3) * ws + 4 * q + 3;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (bits >> k & 1u) cl[pos++] = (uint16_t)(base_idx + k);
+            nlist += __builtin_amdgcn_readlane(incl, 63);
         }
     }
     wave_sync();
+    FAST_STAMP(2);
     // 1b. full 9-arc test at minTh on the filtered pixels; in-place compaction keeps row-major order
     int ncand = 0;
     for (int j0 = 0; j0 < nlist; j0 += 64) {
@@ -908,12 +943,14 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
         ncand += __popcll(m);
     }
     wave_sync();
+    FAST_STAMP(3);
     // 2. exact score of the candidates
     for (int j = lane; j < ncand; j += 64) {
         const int idx = cl[j];
         sc[idx] = (uint8_t)min(max(fast_score(win + idx, off), 0), 255);
     }
     wave_sync();
+    FAST_STAMP(4);
     // 3. iniTh first; minTh only if the cell has no corner at iniTh (src:1135-1148)
     bool any = false;
     for (int j = lane; j < ncand; j += 64) {
@@ -921,6 +958,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
         any |= (s >= ini) && is_local_max(sc, ws, idx, s);
     }
     const int t = ballot(any) ? ini : mint;
+    FAST_STAMP(5);
     // 4. emission in row-major order (the candidate list is row-major)
     uint32_t* out = cand + (size_t)f * g.cand_frame_cap + L.cand_off + C.slot;
     int count = 0;
@@ -945,6 +983,8 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
         cell_count[(size_t)f * g.ncells + cid] = min(count, (int)C.cap);
         cell_thr[(size_t)f * g.ncells + cid] = (uint8_t)t;
     }
+    if (stp && lane == 0) { stp[6] = __builtin_amdgcn_s_memtime(); stp[8] = wall_clock64(); stp[9] = nlist; stp[10] = ncand; }
+#undef FAST_STAMP
 }
 
 // ================================================================================================
@@ -2196,11 +2236,37 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     // overlapping the latency-bound launches of the small levels (k.lv[split..] ) on `st`.
     const int split = (e->fast_split > 0 && e->fast_split < k.nlevels) ? e->fast_split : 0;
     const int win_cap = (G.max_win + 15) & ~15;
+    static const bool fast_stamps = getenv("ORBGPU_FAST_STAMPS") != nullptr;
     auto launch_fast = [&](int l0, int l1, hipStream_t s2) {
         const int c0 = k.lv[l0].cell_begin, c1 = k.lv[l1 - 1].cell_begin + k.lv[l1 - 1].cell_count;
-        if (c1 > c0)
-            hipLaunchKernelGGL(k_fast_cells, dim3((c1 - c0 + 3) / 4, n), dim3(256), 4 * 4 * win_cap, s2, e->d_geom,
-                               e->d_cells, win_cap, pyr, cand, ccount, cthr, c0, c1);
+        if (c1 <= c0) return;
+        unsigned long long* stamps = nullptr;
+        const size_t ns = (size_t)(c1 - c0) * n * 12;
+        if (fast_stamps && hipMalloc(&stamps, ns * 8) == hipSuccess) (void)hipMemsetAsync(stamps, 0, ns * 8, s2);
+        hipLaunchKernelGGL(k_fast_cells, dim3((c1 - c0 + 3) / 4, n), dim3(256), 4 * 4 * win_cap, s2, e->d_geom,
+                           e->d_cells, win_cap, pyr, cand, ccount, cthr, c0, c1, stamps);
+        if (stamps) {  // debug: mean phase clocks over the launch's cells
+            std::vector<unsigned long long> h(ns);
+            (void)hipStreamSynchronize(s2);
+            (void)hipMemcpy(h.data(), stamps, ns * 8, hipMemcpyDeviceToHost);
+            (void)hipFree(stamps);
+            double ph[6] = {0}, life = 0, sv = 0, cn = 0;
+            unsigned long long t0 = ~0ull, t1 = 0;
+            size_t cnt = 0;
+            for (size_t i = 0; i < ns; i += 12) {
+                if (!h[i + 7]) continue;
+                ++cnt;
+                for (int q = 1; q <= 6; ++q) ph[q - 1] += (double)(h[i + q] - h[i + q - 1]);
+                life += (double)(h[i + 8] - h[i + 7]);
+                sv += (double)h[i + 9];
+                cn += (double)h[i + 10];
+                t0 = std::min(t0, h[i + 7]);
+                t1 = std::max(t1, h[i + 8]);
+            }
+            fprintf(stderr, "fast-stamps L%d-%d cells %zu span %.1f us life %.2f us conc %.0f | stage %.0f compass %.0f full %.0f score %.0f thr %.0f emit %.0f cyc | surv %.1f corners %.1f\n",
+                    l0, l1 - 1, cnt, (t1 - t0) * 0.01, life / cnt * 0.01, life / (double)(t1 - t0), ph[0] / cnt, ph[1] / cnt,
+                    ph[2] / cnt, ph[3] / cnt, ph[4] / cnt, ph[5] / cnt, sv / cnt, cn / cnt);
+        }
     };
     // quad-tree of levels [l0, l1): one wave per (level, frame)
     auto launch_qt = [&](int l0, int l1, hipStream_t s2) {
