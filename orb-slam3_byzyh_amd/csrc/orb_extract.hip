@@ -951,13 +951,19 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
     }
     wave_sync();
     FAST_STAMP(4);
-    // 3. iniTh first; minTh only if the cell has no corner at iniTh (src:1135-1148)
+    // 3. iniTh first; minTh only if the cell has no corner at iniTh (src:1135-1148).  The local-maximum
+    //    test does not depend on the threshold: its result (score + 1, or 0) is kept per candidate in
+    //    the window's pixel buffer, which is free once the scores exist.
+    uint8_t* lmv = win - shift;
     bool any = false;
     for (int j = lane; j < ncand; j += 64) {
         const int idx = cl[j], s = sc[idx];
-        any |= (s >= ini) && is_local_max(sc, ws, idx, s);
+        const bool lm = is_local_max(sc, ws, idx, s);
+        lmv[j] = lm ? (uint8_t)(s + 1) : (uint8_t)0;  // s <= 254 for a corner (9-arc minimum - 1)
+        any |= (s >= ini) && lm;
     }
     const int t = ballot(any) ? ini : mint;
+    wave_sync();
     FAST_STAMP(5);
     // 4. emission in row-major order (the candidate list is row-major)
     uint32_t* out = cand + (size_t)f * g.cand_frame_cap + L.cand_off + C.slot;
@@ -968,8 +974,9 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
         int idx = 0, s = 0;
         if (j < ncand) {
             idx = cl[j];
-            s = sc[idx];
-            keep = (s >= t) && is_local_max(sc, ws, idx, s);
+            const int lv = lmv[j];
+            s = lv - 1;
+            keep = lv > 0 && s >= t;
         }
         const unsigned long long m = ballot(keep);
         if (keep) {
