@@ -790,36 +790,16 @@ __device__ __forceinline__ bool fast_corner(const uint8_t* __restrict__ p, const
     return has_run9(bm) || has_run9(dm);
 }
 
-// One wave per FAST cell.  LDS per wave: window | score map | candidate list (u16 pixel indices).
-// Pixels with score < minTh can neither be emitted nor beat an emitted neighbour, so the exact score
-// is computed only for the pixels that are corners at minTh (compacted list, no divergence).
-__global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict__ gp, const CellDesc* __restrict__ cells, int win_cap,
-                                                    const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
-                                                    int32_t* __restrict__ cell_count, uint8_t* __restrict__ cell_thr,
-                                                    int cell0, int cell_end, unsigned long long* __restrict__ stamps) {
-    const KernelGeom& g = *gp;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int cid = cell0 + blockIdx.x * 4 + wave;
-    const int f = blockIdx.y;
-    if (cid >= cell_end) return;
-    // debug (ORBGPU_FAST_STAMPS): per-cell phase clocks of lane 0 (0 start .. 6 end, 7 wall start, 8 wall end,
-    // 9 survivors, 10 corners)
-    unsigned long long* stp = stamps ? stamps + ((size_t)f * (cell_end - cell0) + (cid - cell0)) * 12 : nullptr;
-    if (stp && lane == 0) { stp[7] = wall_clock64(); stp[0] = __builtin_amdgcn_s_memtime(); }
+// The body of one cell for a window row stride known at compile time (kWS > 0: circle, compass and
+// neighbour offsets become LDS immediates) or at run time (kWS == 0).
 #define FAST_STAMP(k) do { if (stp && lane == 0) stp[k] = __builtin_amdgcn_s_memtime(); } while (0)
-    const CellDesc C = cells[cid];
-    const LevelGeom& L = g.lv[C.level];
-    const uint8_t* view = pyr + (size_t)f * g.pyr_frame_bytes + L.plane_off + (size_t)kEdge * L.pitch + kEdge;
-    uint8_t* win = smem + (size_t)wave * 4 * win_cap;
-    uint8_t* sc = win + win_cap;
-    uint16_t* cl = reinterpret_cast<uint16_t*>(sc + win_cap);
-    const int ww = C.win_w, wh = C.win_h, n = ww * wh;
-    const uint8_t* src = view + (size_t)C.ini_y * L.pitch + C.ini_x;
-    // window rows as aligned dwords into an LDS image whose rows start `shift` bytes in (the level's
-    // 19-px frame keeps the over-read inside the plane); row stride ws = roundup(shift + ww, 4)
-    const int shift = (int)((uintptr_t)src & 3);
-    const int ws = (shift + ww + 3) & ~3, nwr = ws >> 2;
+template <int kWS>
+__device__ __forceinline__ void fast_cell(const KernelGeom& g, const CellDesc& C, const LevelGeom& L, int f, int cid,
+                                          int lane, uint8_t* win, uint8_t* sc, uint16_t* cl, const uint8_t* src,
+                                          int shift, uint32_t* __restrict__ cand, int32_t* __restrict__ cell_count,
+                                          uint8_t* __restrict__ cell_thr, unsigned long long* stp) {
+    const int ww = C.win_w, wh = C.win_h;
+    const int ws = kWS ? kWS : (shift + ww + 3) & ~3, nwr = ws >> 2;
     const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(src - shift);
     uint32_t* win32 = reinterpret_cast<uint32_t*>(win);
     uint32_t* sc32 = reinterpret_cast<uint32_t*>(sc);
@@ -991,8 +971,43 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
         cell_thr[(size_t)f * g.ncells + cid] = (uint8_t)t;
     }
     if (stp && lane == 0) { stp[6] = __builtin_amdgcn_s_memtime(); stp[8] = wall_clock64(); stp[9] = nlist; stp[10] = ncand; }
-#undef FAST_STAMP
 }
+
+
+// One wave per FAST cell.  LDS per wave: window | score map | candidate list (u16 pixel indices).
+// Pixels with score < minTh can neither be emitted nor beat an emitted neighbour, so the exact score
+// is computed only for the pixels that are corners at minTh (compacted list, no divergence).
+__global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict__ gp, const CellDesc* __restrict__ cells, int win_cap,
+                                                    const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
+                                                    int32_t* __restrict__ cell_count, uint8_t* __restrict__ cell_thr,
+                                                    int cell0, int cell_end, unsigned long long* __restrict__ stamps) {
+    const KernelGeom& g = *gp;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int cid = cell0 + blockIdx.x * 4 + wave;
+    const int f = blockIdx.y;
+    if (cid >= cell_end) return;
+    // debug (ORBGPU_FAST_STAMPS): per-cell phase clocks of lane 0 (0 start .. 6 end, 7 wall start, 8 wall end,
+    // 9 survivors, 10 corners)
+    unsigned long long* stp = stamps ? stamps + ((size_t)f * (cell_end - cell0) + (cid - cell0)) * 12 : nullptr;
+    if (stp && lane == 0) { stp[7] = wall_clock64(); stp[0] = __builtin_amdgcn_s_memtime(); }
+    const CellDesc C = cells[cid];
+    const LevelGeom& L = g.lv[C.level];
+    const uint8_t* view = pyr + (size_t)f * g.pyr_frame_bytes + L.plane_off + (size_t)kEdge * L.pitch + kEdge;
+    uint8_t* win = smem + (size_t)wave * 4 * win_cap;
+    uint8_t* sc = win + win_cap;
+    uint16_t* cl = reinterpret_cast<uint16_t*>(sc + win_cap);
+    const uint8_t* src = view + (size_t)C.ini_y * L.pitch + C.ini_x;
+    // window rows as aligned dwords into an LDS image whose rows start `shift` bytes in (the level's
+    // 19-px frame keeps the over-read inside the plane); row stride 48 when the window fits (the usual
+    // 42-px cell window), else ws = roundup(shift + ww, 4)
+    const int shift = (int)((uintptr_t)src & 3);
+    if (shift + C.win_w <= 48 && C.win_h <= 48)
+        fast_cell<48>(g, C, L, f, cid, lane, win, sc, cl, src, shift, cand, cell_count, cell_thr, stp);
+    else
+        fast_cell<0>(g, C, L, f, cid, lane, win, sc, cl, src, shift, cand, cell_count, cell_thr, stp);
+}
+#undef FAST_STAMP
 
 // ================================================================================================
 // 3. DistributeOctTree, src:711-1057, one wave per (frame, level)

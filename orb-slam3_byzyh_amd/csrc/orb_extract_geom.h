@@ -207,7 +207,8 @@ inline bool build_geometry(const Params& P, int width, int height, Geometry& g) 
                 c.cap = ((dw + 1) / 2) * ((dh + 1) / 2);
                 c.slot = level_cap;
                 level_cap += c.cap;
-                g.max_win = std::max(g.max_win, ((int)c.win_w + 6) * c.win_h);  // dword-aligned rows
+                // dword-aligned rows; at least 48 bytes (k_fast_cells uses a fixed 48-byte stride when the window fits)
+                g.max_win = std::max(g.max_win, std::max((int)c.win_w + 6, 48) * c.win_h);
                 g.cells.push_back(c);
             }
         }
