@@ -980,12 +980,16 @@ __device__ __forceinline__ void fast_cell(const KernelGeom& g, const CellDesc& C
 __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict__ gp, const CellDesc* __restrict__ cells, int win_cap,
                                                     const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
                                                     int32_t* __restrict__ cell_count, uint8_t* __restrict__ cell_thr,
-                                                    int cell0, int cell_end, unsigned long long* __restrict__ stamps) {
+                                                    int cell0, int cell_end, unsigned long long* __restrict__ stamps,
+                                                    int groups, int nblocks, int share) {
     const KernelGeom& g = *gp;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int cid = cell0 + blockIdx.x * 4 + wave;
-    const int f = blockIdx.y;
+    // XCD-chunked block order (xcd_tile): neighbouring cells, whose windows overlap, share an L2
+    const int tb = xcd_tile(blockIdx.x, share);
+    if (tb >= nblocks) return;
+    const int f = tb / groups;
+    const int cid = cell0 + (tb - f * groups) * 4 + wave;
     if (cid >= cell_end) return;
     // debug (ORBGPU_FAST_STAMPS): per-cell phase clocks of lane 0 (0 start .. 6 end, 7 wall start, 8 wall end,
     // 9 survivors, 10 corners)
@@ -1758,19 +1762,24 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
                                                   const int32_t* __restrict__ sel_count,
                                                   const int32_t* __restrict__ rank_in_class, const int32_t* __restrict__ lap_count,
                                                   int cap, orb_keypoint_t* __restrict__ kps, uint8_t* __restrict__ desc,
-                                                  int32_t* __restrict__ counts) {
+                                                  int32_t* __restrict__ counts, int chunks, int nblocks, int share) {
     const KernelGeom& g = *gp;
     __shared__ __attribute__((aligned(16))) uint32_t patch[kDescKpPerBlock][(kDescLds + 15) / 16 * 4];
     const int half = threadIdx.x >> 5, hl = threadIdx.x & 31;
     // blockIdx.x -> (level, chunk): level l owns ceil(sel_cap_l / 8) blocks, so the grid holds no block
     // beyond a level's capacity (scalar walk over the levels)
-    int level = 0, chunk = blockIdx.x;
+    // XCD-chunked block order (xcd_tile): each XCD walks a contiguous run of (frame, chunk) blocks,
+    // so the patches of one frame's keypoints are fetched into one L2
+    const int tb = xcd_tile(blockIdx.x, share);
+    if (tb >= nblocks) return;
+    const int f = tb / chunks, chunk0 = tb - f * chunks;
+    int level = 0, chunk = chunk0;
 #pragma unroll
     for (int l = 0; l + 1 < kMaxLevels; ++l) {
         const int c = (g.lv[l].sel_cap + kDescKpPerBlock - 1) / kDescKpPerBlock;
         if (l + 1 < g.nlevels && level == l && chunk >= c) { chunk -= c; level = l + 1; }
     }
-    const int slot = chunk * kDescKpPerBlock + half, f = blockIdx.y;
+    const int slot = chunk * kDescKpPerBlock + half;
     const LevelGeom& L = g.lv[level];
     // Every load that does not depend on the key is issued here, in one round trip with the key itself:
     // the key and its rank are read speculatively at a clamped (in-bounds) slot, and the rBRIEF pattern
@@ -1795,7 +1804,7 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
         mono_before += __shfl_xor(mono_before, o, 64);
     }
     const int n = __shfl(cnt_l, (threadIdx.x & ~15) + level, 64);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (chunk0 == 0 && threadIdx.x == 0) {
         int mono = 0;
         for (int l = 0; l < g.nlevels; ++l)
             mono += sel_count[(size_t)f * g.nlevels + l] - lap_count[(size_t)f * g.nlevels + l];
@@ -2265,8 +2274,9 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
         unsigned long long* stamps = nullptr;
         const size_t ns = (size_t)(c1 - c0) * n * 12;
         if (fast_stamps && hipMalloc(&stamps, ns * 8) == hipSuccess) (void)hipMemsetAsync(stamps, 0, ns * 8, s2);
-        hipLaunchKernelGGL(k_fast_cells, dim3((c1 - c0 + 3) / 4, n), dim3(256), 4 * 4 * win_cap, s2, e->d_geom,
-                           e->d_cells, win_cap, pyr, cand, ccount, cthr, c0, c1, stamps);
+        const int groups = (c1 - c0 + 3) / 4, nblocks = groups * n, share = (nblocks + 7) / 8;
+        hipLaunchKernelGGL(k_fast_cells, dim3(8 * share), dim3(256), 4 * 4 * win_cap, s2, e->d_geom, e->d_cells, win_cap,
+                           pyr, cand, ccount, cthr, c0, c1, stamps, groups, nblocks, share);
         if (stamps) {  // debug: mean phase clocks over the launch's cells
             std::vector<unsigned long long> h(ns);
             (void)hipStreamSynchronize(s2);
@@ -2426,8 +2436,9 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     {
         int chunks = 0;  // blocks per frame: ceil(sel_cap_l / 8) per level (see k_describe)
         for (int l = 0; l < k.nlevels; ++l) chunks += (k.lv[l].sel_cap + kDescKpPerBlock - 1) / kDescKpPerBlock;
-        hipLaunchKernelGGL(k_describe, dim3(chunks, n), dim3(256), 0, st, e->d_geom, pyr, blr, sel, scount, dst, lapc,
-                           cap, kps, desc, counts);
+        const int total = chunks * n, share = (total + 7) / 8;
+        hipLaunchKernelGGL(k_describe, dim3(8 * share), dim3(256), 0, st, e->d_geom, pyr, blr, sel, scount, dst, lapc,
+                           cap, kps, desc, counts, chunks, total, share);
     }
     mark(5);
     if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "kernel launch failed");

@@ -35,8 +35,8 @@ def main(d, out, frames=64):
             wd = cs.get("WRITE_SIZE", {})
             if not fd:
                 continue
-            # per-dispatch averages x launches per step (pyramid: 8 launches per step)
-            nper = 8 if stage == "pyramid" else 1
+            # per-dispatch averages x launches per step
+            nper = {"pyramid": 8, "fast": 2}.get(stage, 1)  # launches per step
             fetch += 2 * 1024 * sum(fd.values()) / len(fd) * nper
             if wd:
                 write += 1024 * sum(wd.values()) / len(wd) * nper
