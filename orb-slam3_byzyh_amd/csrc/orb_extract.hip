@@ -1720,6 +1720,532 @@ __global__ __launch_bounds__(64) void k_quadtree(const KernelGeom* __restrict__ 
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Key-parallel DistributeOctTree (default): one 256-thread workgroup per (level, frame).
+//
+// The keys never move.  They stay in gather order (the reference's vToDistributeKeys order) and
+// each carries the list position of its node in the current generation.  Every node's key vector
+// in the reference is a subsequence of that order (DivideNode pushes in parent order, src:644-662),
+// so "first max-response key of the node" (src:1028-1053) is the max of (score, -gather index),
+// and the stable key partition of the wave-per-tree kernel is not needed.  A step is:
+//   node phase (wave 0): the list logic of one regular pass (src:802-918) or careful round
+//     (src:937-1015) from the child counts, writing the next generation's records, the new
+//     positions of every node's children (cmap) and the split points of the nodes whose children
+//     the next step needs counted (the splittable children, vSizeAndPointerToNode);
+//   key phase (all waves): each key moves to its child's new position and adds itself to the child
+//     counts of its new node (LDS atomics), or, after the last step, to its node's best key.
+// ------------------------------------------------------------------------------------------------
+constexpr int kQtThreads = 256, kQtWaves = kQtThreads / 64;
+constexpr int kQtCtrl = 64;  // ints: [0] fin, [1] overflow, [8..16) root map, [16..24) root counts,
+                             // [24..28) wave totals, [32..36) K partials
+
+struct QT2 {
+    QTree t;                    // list workspace shared with the sort: prev, split, divided, sel_*, pos*, bend
+    int32_t* cnt[2];            // [4][lcap] child counts, per generation
+    uint32_t* sxy[2];           // split point (sx | sy << 16) of the counted nodes, ~0u for the others
+    unsigned long long* cmap;   // [lcap] next-generation positions of a node's children (4 x u16)
+    uint32_t* best;             // [lcap] (score << 24) | (0xffffff - key index)
+    int* ctrl;
+};
+
+__host__ __device__ inline size_t qt2_meta_bytes(int lcap) {
+    // u64: sel_el, sel_tmp, cmap; 32-bit: cnt x2, sxy x2, kn x2, best; u16: 2 x (x0 y0 x1 y1), split,
+    // prev, posA, posB, bend; u8: 2 x leaf, divided
+    return (size_t)lcap * (24 + 32 + 8 + 8 + 4 + 16 + 10 + 3) + kOrbSortStack * 12 + kQtCtrl * 4 + 64;
+}
+
+__device__ inline void qt2_carve(QT2& T, uint8_t* p, int lcap) {
+    QTree& t = T.t;
+    t.lcap = lcap;
+    T.ctrl = (int*)p; p += kQtCtrl * 4;
+    t.sort_ws = (int*)p; p += kOrbSortStack * 12;
+    t.sel_el = (unsigned long long*)p; p += 8 * lcap;
+    t.sel_tmp = (unsigned long long*)p; p += 8 * lcap;
+    T.cmap = (unsigned long long*)p; p += 8 * lcap;
+    QGen* gens[2] = {&t.g0, &t.g1};
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        T.cnt[g] = (int32_t*)p; p += 16 * lcap;
+        T.sxy[g] = (uint32_t*)p; p += 4 * lcap;
+        gens[g]->kn = (int32_t*)p; p += 4 * lcap;
+        gens[g]->ks = nullptr;
+    }
+    T.best = (uint32_t*)p; p += 4 * lcap;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        gens[g]->x0 = (int16_t*)p; p += 2 * lcap;
+        gens[g]->y0 = (int16_t*)p; p += 2 * lcap;
+        gens[g]->x1 = (int16_t*)p; p += 2 * lcap;
+        gens[g]->y1 = (int16_t*)p; p += 2 * lcap;
+    }
+    t.split = (uint16_t*)p; p += 2 * lcap;
+    t.prev = (uint16_t*)p; p += 2 * lcap;
+    t.posA = (uint16_t*)p; p += 2 * lcap;
+    t.posB = (uint16_t*)p; p += 2 * lcap;
+    t.bend = (uint16_t*)p; p += 2 * lcap;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        gens[g]->leaf = p; p += lcap;
+        gens[g]->kb = nullptr;
+    }
+    t.divided = p;
+}
+
+__device__ __forceinline__ uint32_t qt2_split_word(int x0, int y0, int x1, int y1) {
+    return (uint32_t)(x0 + ((x1 - x0 + 1) >> 1)) | ((uint32_t)(y0 + ((y1 - y0 + 1) >> 1)) << 16);  // src:608-609
+}
+__device__ __forceinline__ int qt2_quadrant(uint32_t k, uint32_t s) {  // ~0u: never splits, quadrant 0
+    return (key_x(k) >= (int)(s & 0xffff) ? 1 : 0) + (key_y(k) >= (int)(s >> 16) ? 2 : 0);
+}
+
+// next-generation record at `to` for child q (n keys) of node p; counted next step iff `counted`
+__device__ __forceinline__ void qt2_write_child(const QT2& T, const QGen& A, QGen& B, int32_t* cB, uint32_t* sB,
+                                                int p, int q, int n, int to, bool counted) {
+    int sx, sy;
+    split_point(A, p, sx, sy);
+    const int x0 = (q & 1) ? sx : A.x0[p], x1 = (q & 1) ? A.x1[p] : sx;
+    const int y0 = (q & 2) ? sy : A.y0[p], y1 = (q & 2) ? A.y1[p] : sy;
+    B.x0[to] = (int16_t)x0; B.x1[to] = (int16_t)x1; B.y0[to] = (int16_t)y0; B.y1[to] = (int16_t)y1;
+    B.kn[to] = n;
+    B.leaf[to] = n == 1;
+    sB[to] = counted ? qt2_split_word(x0, y0, x1, y1) : ~0u;
+    const int lcap = T.t.lcap;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) cB[qq * lcap + to] = 0;
+    T.best[to] = 0;
+}
+
+__device__ __forceinline__ void qt2_copy_node(const QT2& T, const QGen& A, QGen& B, int32_t* cB, uint32_t* sB, int p,
+                                              int to) {
+    B.x0[to] = A.x0[p]; B.y0[to] = A.y0[p]; B.x1[to] = A.x1[p]; B.y1[to] = A.y1[p];
+    B.kn[to] = A.kn[p]; B.leaf[to] = A.leaf[p];
+    sB[to] = ~0u;
+    const int lcap = T.t.lcap;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) cB[qq * lcap + to] = 0;
+    T.best[to] = 0;
+}
+
+__device__ __forceinline__ unsigned long long qt2_rep(int to) {
+    const unsigned long long v = (unsigned)to & 0xffffu;
+    return v | (v << 16) | (v << 32) | (v << 48);
+}
+
+// Regular pass (src:823-918) over the list A[0..nlist), wave 0.  Every non-leaf node is divided; its
+// children were counted in cA by the last key phase.
+__device__ void qt2_regular(QT2& T, const QGen& A, QGen& B, const int32_t* cA, int32_t* cB, uint32_t* sB, int nlist,
+                            int N, int lane, int& new_size, int& nsplit, bool& fin, bool& ovf) {
+    QTree& t = T.t;
+    const int lcap = t.lcap;
+    int total_children = 0, total_surv = 0;
+    for (int b = 0; b < nlist; b += 64) {
+        const int i = b + lane;
+        int nc = 0, sv = 0;
+        if (i < nlist) {
+            if (A.leaf[i]) sv = 1;
+            else for (int q = 0; q < 4; ++q) nc += cA[q * lcap + i] > 0;
+        }
+        total_children += wave_sum(nc);
+        total_surv += wave_sum(sv);
+    }
+    total_children = uniform(total_children);
+    total_surv = uniform(total_surv);
+    new_size = total_children + total_surv;
+    if (new_size > lcap) { ovf = true; return; }
+    fin = new_size >= N || new_size == nlist;  // src:912-918
+    int carry_c = 0, carry_s = 0, carry_p = 0;
+    for (int b = 0; b < nlist; b += 64) {
+        const int i = b + lane;
+        int nc = 0, sv = 0, ns = 0, c[4] = {0, 0, 0, 0};
+        if (i < nlist) {
+            if (A.leaf[i]) sv = 1;
+            else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) { c[q] = cA[q * lcap + i]; nc += c[q] > 0; ns += c[q] > 1; }
+            }
+        }
+        const int ic = wave_incl_scan(nc, lane), is = wave_incl_scan(sv, lane), ip = wave_incl_scan(ns, lane);
+        if (i < nlist) {
+            unsigned long long cm = ~0ull;
+            if (sv) {
+                const int to = total_children + carry_s + is - 1;
+                qt2_copy_node(T, A, B, cB, sB, i, to);
+                cm = qt2_rep(to);
+            } else {
+                int r = 0, r2 = 0;
+                const int stackpos = carry_c + ic - nc, splitpos = carry_p + ip - ns;
+                for (int q = 0; q < 4; ++q) {
+                    if (c[q] == 0) continue;
+                    const int to = total_children - 1 - (stackpos + r);  // pushed to the front, src:846-897
+                    qt2_write_child(T, A, B, cB, sB, i, q, c[q], to, !fin && c[q] > 1);
+                    cm = (cm & ~(0xffffull << (16 * q))) | ((unsigned long long)to << (16 * q));
+                    if (c[q] > 1) t.split[splitpos + r2++] = (uint16_t)to;
+                    r++;
+                }
+            }
+            T.cmap[i] = cm;
+        }
+        carry_c += __builtin_amdgcn_readlane(ic, 63);
+        carry_s += __builtin_amdgcn_readlane(is, 63);
+        carry_p += __builtin_amdgcn_readlane(ip, 63);
+    }
+    nsplit = carry_p;
+}
+
+// Careful round (src:937-1015), wave 0: the splittable children of the last step (t.split[0..np),
+// counted in cA) are std::sort-ed with compareNodes and divided from the back until the list holds N.
+__device__ void qt2_careful(QT2& T, const QGen& A, QGen& B, const int32_t* cA, int32_t* cB, uint32_t* sB, int nlist,
+                            int np, int N, int lane, int debug_flags, int& new_size, int& nsplit, bool& fin, bool& ovf,
+                            unsigned long long* tm, unsigned long long& t_last) {
+    QTree& t = T.t;
+    const int lcap = t.lcap;
+    for (int i = lane; i < np; i += 64) t.prev[i] = t.split[i];
+    wave_sync();
+    if (debug_flags & 2) {  // reference single-lane port (A/B check)
+        if (lane == 0) {
+            const int16_t* x0a = A.x0;
+            const int32_t* kc = A.kn;
+            orb_std_sort(t.prev, np, [&](uint16_t a, uint16_t b) {
+                const int ca = kc[a], cb = kc[b];
+                return ca < cb || (ca == cb && x0a[a] < x0a[b]);
+            }, t.sort_ws);
+        }
+        wave_sync();
+    } else {
+        qt_sort(t, A, np, lane);
+    }
+    if (debug_flags & 4) { const unsigned long long now = __builtin_amdgcn_s_memtime(); tm[4] += now - t_last; t_last = now; }
+    // division order o = 0.. is prev[np-1-o]; stop once the list reaches N (src:1006)
+    int ndiv = np, carry = 0;
+    for (int b = 0; b < np; b += 64) {
+        const int o = b + lane;
+        int d = 0;
+        if (o < np) {
+            const int p = t.prev[np - 1 - o];
+            for (int q = 0; q < 4; ++q) d += cA[q * lcap + p] > 0;
+            d -= 1;
+        }
+        const int inc = wave_incl_scan(d, lane);
+        const unsigned long long hit = ballot(o < np && nlist + carry + inc >= N);
+        if (hit) { ndiv = b + __ffsll((long long)hit); break; }
+        carry += __builtin_amdgcn_readlane(inc, 63);
+    }
+    ndiv = uniform(ndiv);
+    for (int i = lane; i < nlist; i += 64) t.divided[i] = 0;
+    wave_sync();
+    for (int o = lane; o < ndiv; o += 64) t.divided[t.prev[np - 1 - o]] = 1;
+    wave_sync();
+    int total_children = 0;
+    for (int b = 0; b < ndiv; b += 64) {
+        const int o = b + lane;
+        int nc = 0;
+        if (o < ndiv) {
+            const int p = t.prev[np - 1 - o];
+            for (int q = 0; q < 4; ++q) nc += cA[q * lcap + p] > 0;
+        }
+        total_children += wave_sum(nc);
+    }
+    total_children = uniform(total_children);
+    int kept = 0;
+    for (int b = 0; b < nlist; b += 64) kept += __popcll(ballot(b + lane < nlist && !t.divided[b + lane]));
+    new_size = total_children + kept;
+    if (new_size > lcap) { ovf = true; return; }
+    fin = new_size >= N || new_size == nlist;  // src:1013-1014
+    int carry_c = 0, carry_p = 0;
+    for (int b = 0; b < ndiv; b += 64) {
+        const int o = b + lane;
+        int nc = 0, ns = 0, c[4] = {0, 0, 0, 0}, p = 0;
+        if (o < ndiv) {
+            p = t.prev[np - 1 - o];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { c[q] = cA[q * lcap + p]; nc += c[q] > 0; ns += c[q] > 1; }
+        }
+        const int ic = wave_incl_scan(nc, lane), ip = wave_incl_scan(ns, lane);
+        if (o < ndiv) {
+            int r = 0, r2 = 0;
+            const int stackpos = carry_c + ic - nc, splitpos = carry_p + ip - ns;
+            unsigned long long cm = ~0ull;
+            for (int q = 0; q < 4; ++q) {
+                if (c[q] == 0) continue;
+                const int to = total_children - 1 - (stackpos + r);
+                qt2_write_child(T, A, B, cB, sB, p, q, c[q], to, !fin && c[q] > 1);
+                cm = (cm & ~(0xffffull << (16 * q))) | ((unsigned long long)to << (16 * q));
+                if (c[q] > 1) t.split[splitpos + r2++] = (uint16_t)to;
+                r++;
+            }
+            T.cmap[p] = cm;
+        }
+        carry_c += __builtin_amdgcn_readlane(ic, 63);
+        carry_p += __builtin_amdgcn_readlane(ip, 63);
+    }
+    nsplit = carry_p;
+    int carry_k = 0;
+    for (int b = 0; b < nlist; b += 64) {
+        const int i = b + lane;
+        const bool keep = i < nlist && !t.divided[i];
+        const unsigned long long m = ballot(keep);
+        if (keep) {
+            const int to = total_children + carry_k + rank_in(m);
+            qt2_copy_node(T, A, B, cB, sB, i, to);
+            T.cmap[i] = qt2_rep(to);
+        }
+        carry_k += __popcll(m);
+    }
+}
+
+template <bool kKeysInLds>
+__device__ void qt2_run(QT2& T, uint32_t* keys, uint16_t* node, int K, int N, int nroots, float root_w, int span_y,
+                        const uint32_t* __restrict__ cand_level, const CellDesc* __restrict__ cells, int cell_begin,
+                        int cell_count, const int32_t* __restrict__ ccount, int n_first, int slot_first,
+                        uint32_t* __restrict__ sel_out, int sel_cap, int* n_sel, int* status, int debug_flags,
+                        unsigned long long* stamps, const QPlace& place) {
+    QTree& t = T.t;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lcap = t.lcap;
+    int* ctrl = T.ctrl;
+    // phase timers of thread 0 (debug_flags & 4): gather, roots, regular node, regular key, sort,
+    // careful node, careful key, final, -, #regular passes, #careful rounds, K
+    unsigned long long tm[kQtStamps] = {};
+    unsigned long long t_last = (debug_flags & 4) ? __builtin_amdgcn_s_memtime() : 0;
+    auto stamp = [&](int i) {
+        if (debug_flags & 4) { const unsigned long long now = __builtin_amdgcn_s_memtime(); tm[i] += now - t_last; t_last = now; }
+    };
+    // ---- gather (src:756-764): cells in chunks of 256, wave w owns 64 of them; a wave scan of the
+    // counts gives each cell's start, the wave's keys are spread over its lanes, each finding its
+    // key's cell by a binary search over the lanes' starts (8 x 64 loads in flight per round trip)
+    int rcount[kMaxRoots];
+#pragma unroll
+    for (int r = 0; r < kMaxRoots; ++r) rcount[r] = 0;
+    {
+        constexpr int kGB = 8;
+        int carry = 0;
+        for (int cb = 0; cb < cell_count; cb += kQtThreads) {
+            const int c = cb + tid;
+            int n = 0, slot = 0;
+            if (cb == 0) { n = n_first; slot = slot_first; }
+            else if (c < cell_count) { n = ccount[c]; slot = cells[cell_begin + c].slot; }
+            const int incl = wave_incl_scan(n, lane);
+            const int start = incl - n;
+            const int Tw = uniform(__builtin_amdgcn_readlane(incl, 63));
+            if (lane == 0) ctrl[24 + wave] = Tw;
+            __syncthreads();
+            int base = carry, tot = 0;
+#pragma unroll
+            for (int w = 0; w < kQtWaves; ++w) {
+                const int v = ctrl[24 + w];
+                base += w < wave ? v : 0;
+                tot += v;
+            }
+            __syncthreads();
+            for (int j0 = 0; j0 < Tw; j0 += 64 * kGB) {
+                uint32_t kk[kGB];
+#pragma unroll
+                for (int gi = 0; gi < kGB; ++gi) {
+                    const int i = j0 + 64 * gi + lane;
+                    int cl = 0;
+#pragma unroll
+                    for (int s = 32; s > 0; s >>= 1)
+                        if (__shfl(start, cl + s, 64) <= i) cl += s;
+                    const int sl = __shfl(slot, cl, 64), s0 = __shfl(start, cl, 64);
+                    kk[gi] = i < Tw ? cand_level[sl + (i - s0)] : 0u;
+                }
+#pragma unroll
+                for (int gi = 0; gi < kGB; ++gi) {
+                    const int i = j0 + 64 * gi + lane;
+                    if (i < Tw) {
+                        int root = 0;
+                        if (nroots > 1) {
+                            root = (int)((float)key_x(kk[gi]) / root_w);  // vpIniNodes[kp.pt.x/hX], src:763
+#pragma unroll
+                            for (int r = 0; r < kMaxRoots; ++r) rcount[r] += root == r;
+                        }
+                        keys[base + i] = kk[gi];
+                        node[base + i] = (uint16_t)root;
+                    }
+                }
+            }
+            carry += tot;
+        }
+    }
+    if (tid < kMaxRoots) ctrl[16 + tid] = 0;
+    __syncthreads();
+    if (nroots > 1) {
+#pragma unroll
+        for (int r = 0; r < kMaxRoots; ++r) {
+            if (r >= nroots) break;
+            const int s = wave_sum(rcount[r]);
+            if (lane == 0 && s) atomicAdd(&ctrl[16 + r], s);
+        }
+    } else if (tid == 0) {
+        ctrl[16] = K;
+    }
+    __syncthreads();
+    stamp(0);
+    // ---- roots (src:733-786): empty roots erased, single-key roots are leaves
+    QGen A = t.g0, B = t.g1;
+    int32_t* cA = T.cnt[0];
+    int32_t* cB = T.cnt[1];
+    uint32_t* sA = T.sxy[0];
+    uint32_t* sB = T.sxy[1];
+    int nlist = 0;
+    if (tid == 0) {
+        int start = 0;
+        for (int r = 0; r < nroots; ++r) {
+            const int n = ctrl[16 + r];
+            if (n > 0) {
+                const int x0 = (int)(root_w * (float)r), x1 = (int)(root_w * (float)(r + 1));
+                A.x0[nlist] = (int16_t)x0; A.x1[nlist] = (int16_t)x1;
+                A.y0[nlist] = 0; A.y1[nlist] = (int16_t)span_y;
+                A.kn[nlist] = n; A.leaf[nlist] = n == 1;
+                sA[nlist] = n > 1 ? qt2_split_word(x0, 0, x1, span_y) : ~0u;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) cA[q * lcap + nlist] = 0;
+                ctrl[8 + r] = nlist;
+                nlist++;
+            }
+            start += n;
+        }
+        ctrl[2] = nlist;
+    }
+    __syncthreads();
+    nlist = ctrl[2];
+    for (int k = tid; k < K; k += kQtThreads) {
+        const int p = nroots > 1 ? ctrl[8 + node[k]] : 0;
+        if (nroots > 1) node[k] = (uint16_t)p;
+        const uint32_t s = sA[p];
+        if (s != ~0u) atomicAdd(&cA[qt2_quadrant(keys[k], s) * lcap + p], 1);
+    }
+    __syncthreads();
+    stamp(1);
+    // ---- steps
+    bool careful = false, fin = false, ovf = false;
+    int nsplit = 0;
+    while (true) {
+        if (wave == 0) {
+            int new_size = 0;
+            if (!careful) {
+                qt2_regular(T, A, B, cA, cB, sB, nlist, N, lane, new_size, nsplit, fin, ovf);
+                // src:932: the next regular pass would overshoot N -> careful rounds
+                if (!fin && !ovf && new_size + nsplit * 3 > N) careful = true;
+                stamp(2);
+                tm[9]++;
+            } else {
+                qt2_careful(T, A, B, cA, cB, sB, nlist, nsplit, N, lane, debug_flags, new_size, nsplit, fin, ovf, tm,
+                            t_last);
+                stamp(5);
+                tm[10]++;
+            }
+            nlist = new_size;
+            if (lane == 0) { ctrl[0] = fin; ctrl[1] = ovf; }
+        }
+        __syncthreads();
+        fin = ctrl[0] != 0;
+        ovf = ctrl[1] != 0;
+        if (ovf) break;
+        // key phase: move to the child's position; count for the next step, or take part in the best key
+        for (int k = tid; k < K; k += kQtThreads) {
+            const int p = node[k];
+            const uint32_t key = keys[k];
+            const int q = qt2_quadrant(key, sA[p]);
+            const int np_ = (int)((T.cmap[p] >> (16 * q)) & 0xffff);
+            node[k] = (uint16_t)np_;
+            if (fin) {
+                atomicMax(&T.best[np_], ((uint32_t)key_score(key) << 24) | (0xffffffu - (uint32_t)k));
+            } else {
+                const uint32_t s2 = sB[np_];
+                if (s2 != ~0u) atomicAdd(&cB[qt2_quadrant(key, s2) * lcap + np_], 1);
+            }
+        }
+        __syncthreads();
+        stamp(careful && !fin ? 6 : 3);
+        { const QGen g = A; A = B; B = g; }
+        { int32_t* c = cA; cA = cB; cB = c; }
+        { uint32_t* s = sA; sA = sB; sB = s; }
+        if (fin) break;
+    }
+    if (wave != 0) return;
+    if (ovf || nlist > sel_cap) {
+        if (lane == 0) { *n_sel = 0; atomicMax(status, 1); }
+        return;
+    }
+    // ---- the first max-response key of every node, in list order (src:1028-1053), ranked within its
+    // vLappingArea class (src:1656-1676) as in qt_run
+    int carry_lap = 0, carry_mono = 0;
+    for (int b = 0; b < nlist; b += 64) {
+        const int i = b + lane;
+        bool lap = false;
+        if (i < nlist) {
+            const uint32_t bw = T.best[i];
+            const uint32_t best = keys[0xffffffu - (bw & 0xffffffu)];
+            sel_out[i] = best;
+            float x = (float)(key_x(best) + place.minB);
+            if (place.level != 0) x = x * place.scale;
+            lap = x >= (float)place.lap0 && x <= (float)place.lap1;
+        }
+        const unsigned long long ml = ballot(i < nlist && lap), mm = ballot(i < nlist && !lap);
+        if (i < nlist) place.rank_out[i] = lap ? -(1 + carry_lap + rank_in(ml)) : carry_mono + rank_in(mm);
+        carry_lap += __popcll(ml);
+        carry_mono += __popcll(mm);
+    }
+    if (lane == 0) { *n_sel = nlist; *place.n_lap = carry_lap; }
+    stamp(7);
+    if ((debug_flags & 4) && stamps && lane == 0) {
+        tm[11] = (unsigned long long)K;
+        for (int i = 0; i < kQtStamps; ++i) stamps[i] = tm[i];
+    }
+}
+
+__global__ __launch_bounds__(kQtThreads) void k_quadtree_kp(
+    const KernelGeom* __restrict__ gp, const CellDesc* __restrict__ cells, const uint32_t* __restrict__ cand,
+    const int32_t* __restrict__ cell_count, uint32_t* __restrict__ key_scratch, uint32_t* __restrict__ sel,
+    int32_t* __restrict__ sel_count, int lds_bytes, int* __restrict__ status, unsigned long long* __restrict__ stamps,
+    int lap0, int lap1, int32_t* __restrict__ rank_out, int32_t* __restrict__ lap_count, int level0) {
+    const KernelGeom& g = *gp;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int level = level0 + blockIdx.x, f = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const LevelGeom& L = g.lv[level];
+    const int32_t* cc = cell_count + (size_t)f * g.ncells + L.cell_begin;
+    int32_t* n_sel = sel_count + (size_t)f * g.nlevels + level;
+    const int lcap = L.sel_cap + 64;
+    const size_t meta = (qt2_meta_bytes(lcap) + 15) & ~(size_t)15;
+    if (meta > (size_t)lds_bytes) {
+        if (tid == 0) { *n_sel = 0; atomicMax(status, 2); }
+        return;
+    }
+    QT2 T;
+    qt2_carve(T, smem, lcap);
+    // K (the first chunk's cell counts and slots stay in registers for the gather)
+    int n_first = 0, slot_first = 0, Kp = 0;
+    for (int c = tid; c < L.cell_count; c += kQtThreads) {
+        const int v = cc[c];
+        if (c == tid) { n_first = v; slot_first = cells[L.cell_begin + c].slot; }
+        Kp += v;
+    }
+    Kp = wave_sum(Kp);
+    if (lane == 0) T.ctrl[32 + wave] = Kp;
+    __syncthreads();
+    int K = 0;
+#pragma unroll
+    for (int w = 0; w < kQtWaves; ++w) K += T.ctrl[32 + w];
+    uint32_t* sel_out = sel + (size_t)f * g.sel_frame_cap + L.sel_off;
+    const uint32_t* cand_level = cand + (size_t)f * g.cand_frame_cap + L.cand_off;
+    QPlace place{level, L.minB, lap0, lap1, L.scale, rank_out + (size_t)f * g.sel_frame_cap + L.sel_off,
+                 lap_count + (size_t)f * g.nlevels + level};
+    unsigned long long* st = stamps ? stamps + ((size_t)f * g.nlevels + level) * kQtStamps : nullptr;
+    if (!(g.debug_flags & 8) && meta + (size_t)K * 6 <= (size_t)lds_bytes) {  // flag 8: force the scratch path (tests)
+        uint32_t* keys = (uint32_t*)(smem + meta);
+        uint16_t* node = (uint16_t*)(keys + K);
+        qt2_run<true>(T, keys, node, K, L.nfeat, L.n_roots, L.root_w, L.maxBY - L.minB, cand_level, cells,
+                      L.cell_begin, L.cell_count, cc, n_first, slot_first, sel_out, L.sel_cap, n_sel, status,
+                      g.debug_flags, st, place);
+    } else {  // keys and node ids in this level's scratch slots (2 x cand_cap words)
+        uint32_t* keys = key_scratch + ((size_t)f * g.cand_frame_cap + L.cand_off) * 2;
+        uint16_t* node = (uint16_t*)(keys + L.cand_cap);
+        qt2_run<false>(T, keys, node, K, L.nfeat, L.n_roots, L.root_w, L.maxBY - L.minB, cand_level, cells,
+                       L.cell_begin, L.cell_count, cc, n_first, slot_first, sel_out, L.sel_cap, n_sel, status,
+                       g.debug_flags, st, place);
+    }
+}
+
 // ================================================================================================
 // 5. IC_Angle + steered rBRIEF, src:91-138, 150-203, 1534-1547, 1656-1676
 // ================================================================================================
@@ -1952,6 +2478,7 @@ struct Extractor {
     int chunk = 1 << 30, nstreams = 1;  // off by default: measured slower (streams did not overlap)
     int fast_split = 3;                 // FAST on levels [0, fast_split) overlaps the small pyramid levels
     int fast_per_level = 0;             // 1: FAST of each later level right after its pyramid level (side2); measured slower
+    int qt_v1 = 0;                      // 1: the wave-per-tree quad-tree (k_quadtree, ORBGPU_QT_V1) instead of k_quadtree_kp
     int qt_split = 0;                   // 1: quad-tree of levels [0, fast_split) on the side stream (ORBGPU_QT_SPLIT)
     hipStream_t side = nullptr, side2 = nullptr;
     hipEvent_t split_ev[3] = {};
@@ -2071,11 +2598,15 @@ int prepare(Extractor* e, int w, int h, int n) {
         // quad-tree LDS: node metadata of the largest level + room for ~7k keys (80 KB: two
         // workgroups per CU); larger feature budgets (e.g. the 5x monocular-init extractor) get more
         size_t meta = 0;
-        for (int l = 0; l < g.k.nlevels; ++l) meta = std::max(meta, (qt_meta_bytes(g.k.lv[l].sel_cap + 64) + 15) & ~(size_t)15);
+        for (int l = 0; l < g.k.nlevels; ++l) {
+            const int lcap = g.k.lv[l].sel_cap + 64;
+            meta = std::max(meta, ((e->qt_v1 ? qt_meta_bytes(lcap) : qt2_meta_bytes(lcap)) + 15) & ~(size_t)15);
+        }
         const size_t want = std::max<size_t>(80 * 1024, meta + 32 * 1024);
         if (meta > 160 * 1024) return orbgpu_fail(ORB_ERR_ARG, "nfeatures too large for the quad-tree LDS budget");
         e->qt_lds = (int)std::min<size_t>(want, 160 * 1024);
-        if (hipFuncSetAttribute((const void*)k_quadtree, hipFuncAttributeMaxDynamicSharedMemorySize, e->qt_lds) != hipSuccess)
+        if (hipFuncSetAttribute(e->qt_v1 ? (const void*)k_quadtree : (const void*)k_quadtree_kp,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, e->qt_lds) != hipSuccess)
             return orbgpu_fail(ORB_ERR_DEVICE, "cannot raise the quad-tree LDS limit");
     }
     const orbgpu::KernelGeom& k = e->geo.k;
@@ -2303,7 +2834,8 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     // quad-tree of levels [l0, l1): one wave per (level, frame)
     auto launch_qt = [&](int l0, int l1, hipStream_t s2) {
         if (l1 > l0)
-            hipLaunchKernelGGL(k_quadtree, dim3(l1 - l0, n), dim3(64), e->qt_lds, s2, e->d_geom, e->d_cells, cand, ccount,
+            hipLaunchKernelGGL(e->qt_v1 ? k_quadtree : k_quadtree_kp, dim3(l1 - l0, n), dim3(e->qt_v1 ? 64 : kQtThreads),
+                               e->qt_lds, s2, e->d_geom, e->d_cells, cand, ccount,
                                scratch, sel, scount, e->qt_lds, e->d_status,
                                e->d_stamps ? e->d_stamps + (size_t)f0 * k.nlevels * kQtStamps : nullptr, lap0, lap1, dst,
                                lapc, l0);
@@ -2499,6 +3031,7 @@ int orb_extractor_create(const orb_params_t* p, int max_width, int max_height, i
         return orbgpu_fail(ORB_ERR_DEVICE, "stream/status allocation failed");
     }
     hipFuncSetAttribute((const void*)k_quadtree, hipFuncAttributeMaxDynamicSharedMemorySize, e->qt_lds);
+    hipFuncSetAttribute((const void*)k_quadtree_kp, hipFuncAttributeMaxDynamicSharedMemorySize, e->qt_lds);
     if (const char* c = getenv("ORBGPU_CHUNK")) e->chunk = std::max(1, atoi(c));
     if (const char* c = getenv("ORBGPU_STREAMS")) e->nstreams = std::min(Extractor::kMaxStreams, std::max(1, atoi(c)));
     if (const char* c = getenv("ORBGPU_FAST_SPLIT")) e->fast_split = atoi(c);
@@ -2511,6 +3044,7 @@ int orb_extractor_create(const orb_params_t* p, int max_width, int max_height, i
     if (const char* c = getenv("ORBGPU_FAST_PER_LEVEL")) e->fast_per_level = atoi(c);
     if (const char* c = getenv("ORBGPU_PYR_BAND")) e->band_mode = atoi(c);
     if (const char* c = getenv("ORBGPU_QT_SPLIT")) e->qt_split = atoi(c);
+    if (const char* c = getenv("ORBGPU_QT_V1")) e->qt_v1 = atoi(c);
     if (const char* c = getenv("ORBGPU_PYR_WG_PER_CU")) e->band_wg_per_cu = std::max(1, atoi(c));
     if (const char* c = getenv("ORBGPU_PYR_BAND_FROM")) e->band_from = std::max(0, atoi(c));
     if (const char* c = getenv("ORBGPU_PYR_BAND_R")) e->band_r = std::min(16, std::max(4, atoi(c)));

@@ -188,3 +188,19 @@ def test_band_pyramid_path_parity(pkg, oracle, frames, synth, monkeypatch, band_
         assert n == len(rk) and int(counts[f, 1]) == rm
         assert np.array_equal(pkg.keypoints_to_structured(kps[f], n).view(np.uint8), rk.view(np.uint8)), f
         assert np.array_equal(desc[f, :n].cpu().numpy(), rd), f
+
+
+@pytest.mark.parametrize("mode", [("ORBGPU_DEBUG_FLAGS", "8"), ("ORBGPU_DEBUG_FLAGS", "2"), ("ORBGPU_QT_V1", "1")],
+                         ids=["kp_scratch_keys", "kp_serial_sort", "wave_per_tree"])
+def test_quadtree_variants_parity(pkg, oracle, frames, monkeypatch, mode):
+    """Quad-tree variants stay bit-exact: the key-parallel kernel with its keys forced into the global
+    scratch (flag 8) or with the single-lane libstdc++ sort port (flag 2), and the wave-per-tree kernel."""
+    monkeypatch.setenv(*mode)
+    for case in ["poly640", "noise1280", "init5000", "odd_size"]:
+        img, nf, lap = frames[case]
+        ex = pkg.ORBextractor(nf, 1.2, 8, 20, 7, max_width=1280, max_height=720)
+        kps, desc, mono = ex(img, None, lap)
+        rkps, rdesc, rmono = oracle.OracleExtractor(nf, 1.2, 8, 20, 7)(img, lap)
+        assert ex._lib.orb_debug_status(ex._h) == 0, case
+        assert mono == rmono and np.array_equal(kps.view(np.uint8), rkps.view(np.uint8)), case
+        assert np.array_equal(desc, rdesc), case
