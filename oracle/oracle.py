@@ -19,6 +19,7 @@ KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle"
 
 _vp, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 _PROTOS = {
+    "oracle_node_sort": (None, [_vp, _vp, _i, _vp]),
     "oracle_orb_create": (_vp, [_i, _f, _i, _i, _i]),
     "oracle_orb_destroy": (None, [_vp]),
     "oracle_orb_params": (None, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -65,6 +66,17 @@ def load() -> ctypes.CDLL:
             fn.argtypes = args
         _LIB = lib
     return _LIB
+
+
+def node_sort(counts, ulx):
+    """libstdc++ std::sort with compareNodes (src/ORBextractor.cc:676-697, 950) of (count, UL.x) records:
+    the record indices in sorted order."""
+    import numpy as np
+    c = np.ascontiguousarray(counts, np.int32)
+    x = np.ascontiguousarray(ulx, np.int32)
+    out = np.zeros(len(c), np.int32)
+    load().oracle_node_sort(c.ctypes.data, x.ctypes.data, len(c), out.ctypes.data)
+    return out
 
 
 class OracleExtractor:

@@ -596,6 +596,15 @@ int oracle_orb_extract(oracle_orb_t* h, const uint8_t* img, int w, int hgt, int 
     return ((Extractor*)h)->run(img, w, hgt, stride, lap0, lap1, (KeyPoint*)kps, desc, cap, n_out);
 }
 
+// std::sort with compareNodes (src:676-697, 950) of n (count, UL.x) records: order[i] = record index
+void oracle_node_sort(const int* counts, const int* ulx, int n, int* order) {
+    std::vector<QNode> nodes(n);
+    std::vector<SizeNode> v(n);
+    for (int i = 0; i < n; ++i) { nodes[i].ulx = ulx[i]; v[i] = SizeNode(counts[i], &nodes[i]); }
+    std::sort(v.begin(), v.end(), by_size_then_x);
+    for (int i = 0; i < n; ++i) order[i] = (int)(v[i].second - nodes.data());
+}
+
 // ---- intermediates of the last oracle_orb_extract call (for stage-by-stage parity tests)
 void oracle_orb_level_dims(oracle_orb_t* h, int level, int* w, int* hh, int* pw, int* ph) {
     const Plane& L = ((Extractor*)h)->pyr[level];

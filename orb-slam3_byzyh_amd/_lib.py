@@ -118,6 +118,7 @@ DEBUG_PROTOTYPES = {
     "orb_debug_status": (_i, [_vp]),
     "orb_extractor_profile": (_i, [_vp, _i]),
     "orb_debug_qt_stamps": (_i, [_vp, _vp, _i]),
+    "orb_debug_node_sort": (_i, [_vp, _vp, _i, _i, _vp]),
     "orb_extractor_stage_ms": (_i, [_vp, _fp, _ip, ctypes.POINTER(ctypes.c_longlong)]),
 }
 

@@ -1356,6 +1356,110 @@ __device__ void qt_sort(QTree& t, const QGen& A, int n, int lane) {
     wave_sync();
 }
 
+// Position of the k-th (0-based) lowest set bit of m (valid for k < popcount(m)): the largest p with
+// popcount(m below p) <= k, by a binary search over p.
+__device__ __forceinline__ int kth_set_bit(unsigned long long m, int k) {
+    int pos = 0;
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1)
+        if (__popcll(m & ((1ull << (pos + s)) - 1)) <= k) pos += s;
+    return pos;
+}
+
+// qt_sort for n <= 64 with one element per lane in registers: the same libstdc++ introsort emulation
+// (median-of-3 to first, unguarded Hoare partition from the two stop lists, stable sort inside the
+// <= 16-element leaf blocks), but the stop lists are ballots, the pair swaps shuffles and the pending
+// ranges a bit mask of block starts (ranges are independent, so their order does not matter; each
+// block start carries its depth budget).  Returns false, leaving t.prev untouched, if a range would hit
+// the depth limit (heap-sort fallback), so the caller runs qt_sort.  Keys: count << 12 | UL.x (callers
+// guarantee counts < 2^20).
+__device__ bool qt_sort_reg(QTree& t, const QGen& A, int n, int lane) {
+    if (n <= 1) return true;
+    int id = 0;
+    uint32_t key = 0xffffffffu;
+    if (lane < n) { id = t.prev[lane]; key = ((uint32_t)A.kn[id] << 12) | (uint32_t)(uint16_t)A.x0[id]; }
+    int lg = 0;
+    for (int m = n; m > 1; m >>= 1) ++lg;
+    uint32_t st_lo = 1u, st_hi = 0u;  // block starts (uniform); a block ends at the next start or n
+    int depth = 2 * lg;               // depth budget, meaningful at block starts
+    const unsigned long long below = (1ull << lane) - 1, above = lane == 63 ? 0ull : ~((2ull << lane) - 1);
+    while (true) {
+        int f = -1, l = 0;
+        for (unsigned long long b = ((unsigned long long)st_hi << 32) | st_lo; b;) {
+            const int s0 = __ffsll((long long)b) - 1;
+            b &= b - 1;
+            const int e = b ? __ffsll((long long)b) - 1 : n;
+            if (e - s0 > 16) { f = s0; l = e; break; }
+        }
+        f = uniform(f);
+        l = uniform(l);
+        if (f < 0) break;
+        int d = uniform(__builtin_amdgcn_readlane(depth, f));
+        if (d == 0) return false;
+        --d;
+        // __move_median_to_first(first, first + 1, mid, last - 1)
+        const int mid = f + (l - f) / 2;
+        const uint32_t ka = __builtin_amdgcn_readlane(key, f + 1), kb = __builtin_amdgcn_readlane(key, mid),
+                       kc = __builtin_amdgcn_readlane(key, l - 1);
+        int sx;
+        if (ka < kb) sx = kb < kc ? mid : (ka < kc ? l - 1 : f + 1);
+        else sx = ka < kc ? f + 1 : (kb < kc ? l - 1 : mid);
+        sx = uniform(sx);
+        const uint32_t kf = __builtin_amdgcn_readlane(key, f), ks = __builtin_amdgcn_readlane(key, sx);
+        const int idf = __builtin_amdgcn_readlane(id, f), ids = __builtin_amdgcn_readlane(id, sx);
+        if (lane == f) { key = ks; id = ids; }
+        else if (lane == sx) { key = kf; id = idf; }
+        const uint32_t p = ks;
+        // __unguarded_partition(first + 1, last, first): stop lists A (ascending, !(a < p)) and
+        // B (descending, !(p < a)), ranked by ballots and listed in LDS; pairs (A_k, B_k) swap while
+        // A_k < B_k.  An element equal to the pivot is in both lists; it moves at most once (swapped
+        // A_k precede every swapped B_k).
+        const bool in = lane > f && lane < l;
+        const bool inA = in && !(key < p), inB = in && !(p < key);
+        const unsigned long long mA = ballot(inA), mB = ballot(inB);
+        const int nA = __popcll(mA), nB = __popcll(mB), lim = min(nA, nB);
+        const int ra = __popcll(mA & below), rb = __popcll(mB & above);
+        if (inA) t.posA[ra] = (uint16_t)lane;
+        if (inB) t.posB[rb] = (uint16_t)lane;
+        wave_sync();
+        const int Ak = lane < nA ? t.posA[lane] : 0, Bk = lane < nB ? t.posB[lane] : 0;
+        const int pa = t.posB[min(ra, 63)], pb = t.posA[min(rb, 63)];
+        const unsigned long long hit = ballot(lane < lim && Ak >= Bk);
+        const int kstop = uniform(hit ? __ffsll((long long)hit) - 1 : lim);
+        const int cut = uniform(min(kstop < nA ? __builtin_amdgcn_readlane(Ak, kstop) : 1 << 30,
+                                    kstop > 0 ? __builtin_amdgcn_readlane(Bk, kstop - 1) : 1 << 30));
+        const int partner = inA && ra < kstop ? pa : (inB && rb < kstop ? pb : lane);
+        key = (uint32_t)__shfl((int)key, partner, 64);
+        id = __shfl(id, partner, 64);
+        wave_sync();  // the lists are rewritten by the next partition
+        if (cut < n) {
+            if (cut < 32) st_lo |= 1u << cut;
+            else st_hi |= 1u << (cut - 32);
+        }
+        if (lane == f || lane == cut) depth = d;
+    }
+    const unsigned long long starts = ((unsigned long long)st_hi << 32) | st_lo;
+    // __final_insertion_sort: a stable sort inside each block (<= 16 elements); the shuffles stay in
+    // uniform control flow
+    {
+        const int s = 63 - __clzll(starts & (below | (1ull << lane)));
+        const unsigned long long up = starts & above;
+        const int e = up ? __ffsll((long long)up) - 1 : n;
+        int r = s;
+#pragma unroll
+        for (int d = 0; d < 16; ++d) {
+            const int j = s + d;
+            const uint32_t kj = (uint32_t)__shfl((int)key, j & 63, 64);
+            r += j < e && ((kj < key) || (kj == key && j < lane));
+        }
+        if (lane < n) t.sel_tmp[r] = (unsigned long long)id;
+    }
+    wave_sync();
+    if (lane < n) t.prev[lane] = (uint16_t)t.sel_tmp[lane];
+    wave_sync();
+    return true;
+}
+
 constexpr int kQtStamps = 12;
 
 struct QPlace {  // vLappingArea classification of the selected keys
@@ -1895,7 +1999,7 @@ __device__ void qt2_regular(QT2& T, const QGen& A, QGen& B, const int32_t* cA, i
 // Careful round (src:937-1015), wave 0: the splittable children of the last step (t.split[0..np),
 // counted in cA) are std::sort-ed with compareNodes and divided from the back until the list holds N.
 __device__ void qt2_careful(QT2& T, const QGen& A, QGen& B, const int32_t* cA, int32_t* cB, uint32_t* sB, int nlist,
-                            int np, int N, int lane, int debug_flags, int& new_size, int& nsplit, bool& fin, bool& ovf,
+                            int np, int N, int lane, int debug_flags, bool reg_sort, int& new_size, int& nsplit, bool& fin, bool& ovf,
                             unsigned long long* tm, unsigned long long& t_last) {
     QTree& t = T.t;
     const int lcap = t.lcap;
@@ -1911,8 +2015,8 @@ __device__ void qt2_careful(QT2& T, const QGen& A, QGen& B, const int32_t* cA, i
             }, t.sort_ws);
         }
         wave_sync();
-    } else {
-        qt_sort(t, A, np, lane);
+    } else if (!(reg_sort && np <= 64 && !(debug_flags & 16) && qt_sort_reg(t, A, np, lane))) {
+        qt_sort(t, A, np, lane);  // > 64 candidates, depth-limit fallback, or forced (flag 16)
     }
     if (debug_flags & 4) { const unsigned long long now = __builtin_amdgcn_s_memtime(); tm[4] += now - t_last; t_last = now; }
     // division order o = 0.. is prev[np-1-o]; stop once the list reaches N (src:1006)
@@ -1991,6 +2095,30 @@ __device__ void qt2_careful(QT2& T, const QGen& A, QGen& B, const int32_t* cA, i
         }
         carry_k += __popcll(m);
     }
+}
+
+// Adds one to cnt[q * lcap + p] for every active lane.  A wave's keys are neighbours in gather (cell)
+// order, so most share a node: up to two leader rounds add a node's four counts from one lane (ballot
+// counts, no same-address atomics); the remaining lanes use per-lane LDS atomics.
+__device__ __forceinline__ void qt2_add_counts(int32_t* cnt, int lcap, int p, int q, bool active, int lane) {
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        const unsigned long long am = ballot(active);
+        if (!am) return;
+        const int first = __ffsll((long long)am) - 1;
+        const int leader = __builtin_amdgcn_readlane(p, first);
+        const bool mine = active && p == leader;
+        const int c0 = __popcll(ballot(mine && q == 0)), c1 = __popcll(ballot(mine && q == 1));
+        const int c2 = __popcll(ballot(mine && q == 2)), c3 = __popcll(ballot(mine && q == 3));
+        if (lane == first) {
+            if (c0) atomicAdd(&cnt[leader], c0);
+            if (c1) atomicAdd(&cnt[lcap + leader], c1);
+            if (c2) atomicAdd(&cnt[2 * lcap + leader], c2);
+            if (c3) atomicAdd(&cnt[3 * lcap + leader], c3);
+        }
+        active = active && !mine;
+    }
+    if (active) atomicAdd(&cnt[q * lcap + p], 1);
 }
 
 template <bool kKeysInLds>
@@ -2088,7 +2216,6 @@ __device__ void qt2_run(QT2& T, uint32_t* keys, uint16_t* node, int K, int N, in
     uint32_t* sB = T.sxy[1];
     int nlist = 0;
     if (tid == 0) {
-        int start = 0;
         for (int r = 0; r < nroots; ++r) {
             const int n = ctrl[16 + r];
             if (n > 0) {
@@ -2102,17 +2229,25 @@ __device__ void qt2_run(QT2& T, uint32_t* keys, uint16_t* node, int K, int N, in
                 ctrl[8 + r] = nlist;
                 nlist++;
             }
-            start += n;
         }
         ctrl[2] = nlist;
     }
     __syncthreads();
     nlist = ctrl[2];
-    for (int k = tid; k < K; k += kQtThreads) {
-        const int p = nroots > 1 ? ctrl[8 + node[k]] : 0;
-        if (nroots > 1) node[k] = (uint16_t)p;
-        const uint32_t s = sA[p];
-        if (s != ~0u) atomicAdd(&cA[qt2_quadrant(keys[k], s) * lcap + p], 1);
+    for (int kb = wave * 64; kb < K; kb += kQtThreads) {
+        const int k = kb + lane;
+        int p = 0, q = 0;
+        bool counted = false;
+        if (k < K) {
+            if (nroots > 1) {
+                p = ctrl[8 + node[k]];
+                node[k] = (uint16_t)p;
+            }
+            const uint32_t s = sA[p];
+            counted = s != ~0u;
+            q = qt2_quadrant(keys[k], s);
+        }
+        if (counted) atomicAdd(&cA[q * lcap + p], 1);
     }
     __syncthreads();
     stamp(1);
@@ -2129,7 +2264,8 @@ __device__ void qt2_run(QT2& T, uint32_t* keys, uint16_t* node, int K, int N, in
                 stamp(2);
                 tm[9]++;
             } else {
-                qt2_careful(T, A, B, cA, cB, sB, nlist, nsplit, N, lane, debug_flags, new_size, nsplit, fin, ovf, tm,
+                tm[8] += (unsigned long long)nsplit << (16 * min((int)tm[10], 3));  // candidates per round (debug)
+                qt2_careful(T, A, B, cA, cB, sB, nlist, nsplit, N, lane, debug_flags, K < (1 << 20), new_size, nsplit, fin, ovf, tm,
                             t_last);
                 stamp(5);
                 tm[10]++;
@@ -2142,17 +2278,25 @@ __device__ void qt2_run(QT2& T, uint32_t* keys, uint16_t* node, int K, int N, in
         ovf = ctrl[1] != 0;
         if (ovf) break;
         // key phase: move to the child's position; count for the next step, or take part in the best key
-        for (int k = tid; k < K; k += kQtThreads) {
-            const int p = node[k];
-            const uint32_t key = keys[k];
-            const int q = qt2_quadrant(key, sA[p]);
-            const int np_ = (int)((T.cmap[p] >> (16 * q)) & 0xffff);
-            node[k] = (uint16_t)np_;
+        // two keys per lane per round: both dependent LDS chains (node -> split/cmap -> next split) in flight
+        for (int kb = wave * 128; kb < K; kb += 2 * kQtThreads) {
+            const int k0 = kb + lane, k1 = kb + 64 + lane;
+            const bool v0 = k0 < K, v1 = k1 < K;
+            const int p0 = v0 ? node[k0] : 0, p1 = v1 ? node[k1] : 0;
+            const uint32_t key0 = v0 ? keys[k0] : 0u, key1 = v1 ? keys[k1] : 0u;
+            const uint32_t s0 = sA[p0], s1 = sA[p1];
+            const unsigned long long m0 = T.cmap[p0], m1 = T.cmap[p1];
+            const int n0 = (int)((m0 >> (16 * qt2_quadrant(key0, s0))) & 0xffff);
+            const int n1 = (int)((m1 >> (16 * qt2_quadrant(key1, s1))) & 0xffff);
+            if (v0) node[k0] = (uint16_t)n0;
+            if (v1) node[k1] = (uint16_t)n1;
             if (fin) {
-                atomicMax(&T.best[np_], ((uint32_t)key_score(key) << 24) | (0xffffffu - (uint32_t)k));
+                if (v0) atomicMax(&T.best[n0], ((uint32_t)key_score(key0) << 24) | (0xffffffu - (uint32_t)k0));
+                if (v1) atomicMax(&T.best[n1], ((uint32_t)key_score(key1) << 24) | (0xffffffu - (uint32_t)k1));
             } else {
-                const uint32_t s2 = sB[np_];
-                if (s2 != ~0u) atomicAdd(&cB[qt2_quadrant(key, s2) * lcap + np_], 1);
+                const uint32_t t0 = v0 ? sB[n0] : ~0u, t1 = v1 ? sB[n1] : ~0u;
+                if (t0 != ~0u) atomicAdd(&cB[qt2_quadrant(key0, t0) * lcap + n0], 1);
+                if (t1 != ~0u) atomicAdd(&cB[qt2_quadrant(key1, t1) * lcap + n1], 1);
             }
         }
         __syncthreads();
@@ -2244,6 +2388,25 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree_kp(
                        L.cell_begin, L.cell_count, cc, n_first, slot_first, sel_out, L.sel_cap, n_sel, status,
                        g.debug_flags, st, place);
     }
+}
+
+// Debug: compareNodes sort of n (count, UL.x) records by the quad-tree's sort emulations, one wave
+// (mode 0: the register version when n <= 64, else qt_sort; mode 1: qt_sort).  *used_reg = 1 if the
+// register version produced the order.
+__global__ __launch_bounds__(64) void k_debug_node_sort(const int* __restrict__ counts, const int* __restrict__ ulx,
+                                                        int n, int mode, int* __restrict__ order, int* __restrict__ used_reg) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    QT2 T;
+    qt2_carve(T, smem, n + 64);
+    QTree& t = T.t;
+    QGen& A = t.g0;
+    const int lane = threadIdx.x;
+    for (int i = lane; i < n; i += 64) { A.kn[i] = counts[i]; A.x0[i] = (int16_t)ulx[i]; t.prev[i] = (uint16_t)i; }
+    wave_sync();
+    const bool reg = mode == 0 && n <= 64 && qt_sort_reg(t, A, n, lane);
+    if (!reg) qt_sort(t, A, n, lane);
+    for (int i = lane; i < n; i += 64) order[i] = t.prev[i];
+    if (lane == 0) *used_reg = reg;
 }
 
 // ================================================================================================
@@ -3206,6 +3369,32 @@ int orb_extractor_level_download(orb_extractor_t h, int frame, int level, uint8_
         hipMemcpy2D(host_padded, L.pw, src, L.pitch, L.pw, L.ph, hipMemcpyDeviceToHost) != hipSuccess)
         return orbgpu_fail(ORB_ERR_DEVICE, "download failed");
     return ORB_OK;
+}
+
+// ---- debug: the quad-tree's compareNodes sort on given records (returns 1 if the register version ran,
+// 0 if qt_sort did, < 0 on error); order[i] = index of the i-th record in sorted order
+int orb_debug_node_sort(const int* counts, const int* ulx, int n, int mode, int* order) {
+    if (n < 0 || n > 1024 || (n && (!counts || !ulx || !order))) return orbgpu_fail(ORB_ERR_ARG, "bad node sort args");
+    for (int i = 0; i < n; ++i)
+        if (counts[i] < 0 || counts[i] >= (1 << 20) || ulx[i] < 0 || ulx[i] >= 4096)
+            return orbgpu_fail(ORB_ERR_ARG, "node record out of range");
+    int* d = nullptr;
+    const size_t words = 3 * (size_t)n + 1;
+    if (hipMalloc(&d, 4 * words) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "hipMalloc failed");
+    int used = -1;
+    const int lds = (int)((qt2_meta_bytes(n + 64) + 15) & ~(size_t)15);
+    bool ok = hipFuncSetAttribute((const void*)k_debug_node_sort, hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess &&
+              (n == 0 || (hipMemcpy(d, counts, 4 * (size_t)n, hipMemcpyHostToDevice) == hipSuccess &&
+                          hipMemcpy(d + n, ulx, 4 * (size_t)n, hipMemcpyHostToDevice) == hipSuccess));
+    if (ok) {
+        hipLaunchKernelGGL(k_debug_node_sort, dim3(1), dim3(64), lds, 0, d, d + n, n, mode, d + 2 * n, d + 3 * n);
+        ok = hipDeviceSynchronize() == hipSuccess &&
+             (n == 0 || hipMemcpy(order, d + 2 * n, 4 * (size_t)n, hipMemcpyDeviceToHost) == hipSuccess) &&
+             hipMemcpy(&used, d + 3 * n, 4, hipMemcpyDeviceToHost) == hipSuccess;
+    }
+    (void)hipFree(d);
+    if (!ok) return orbgpu_fail(ORB_ERR_DEVICE, "node sort failed");
+    return used;
 }
 
 // ---- debug / parity hooks (intermediates of the last call, frame `frame`)

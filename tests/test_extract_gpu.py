@@ -204,3 +204,33 @@ def test_quadtree_variants_parity(pkg, oracle, frames, monkeypatch, mode):
         assert ex._lib.orb_debug_status(ex._h) == 0, case
         assert mono == rmono and np.array_equal(kps.view(np.uint8), rkps.view(np.uint8)), case
         assert np.array_equal(desc, rdesc), case
+
+
+def test_quadtree_node_sort_emulations(pkg, oracle):
+    """The careful rounds' std::sort(compareNodes) emulations (register version for <= 64 nodes, LDS
+    version otherwise) give libstdc++'s exact order, ties included (src/ORBextractor.cc:676-697, 950):
+    random records with many equal (count, UL.x) pairs, sorted / reversed / constant inputs, n 0..300."""
+    lib = pkg._lib.load()
+    rng = np.random.default_rng(77)
+    cases = []
+    for n in list(range(0, 70)) + [100, 129, 200, 300]:
+        for kind in range(4):
+            if kind == 0:
+                c, x = rng.integers(2, 6, n), rng.integers(0, 4, n) * 37
+            elif kind == 1:
+                c, x = rng.integers(2, 200, n), rng.integers(0, 600, n)
+            elif kind == 2:
+                c, x = np.sort(rng.integers(2, 9, n))[::-1].copy(), np.full(n, 5)
+            else:
+                c, x = np.full(n, 3), np.arange(n) % 3
+            cases.append((c.astype(np.int32), x.astype(np.int32)))
+    used_reg = 0
+    for c, x in cases:
+        exp = oracle.node_sort(c, x)
+        for mode in (0, 1):
+            out = np.zeros(len(c), np.int32)
+            rc = lib.orb_debug_node_sort(c.ctypes.data, x.ctypes.data, len(c), mode, out.ctypes.data)
+            assert rc >= 0
+            used_reg += rc
+            assert np.array_equal(out, exp), (len(c), mode, c.tolist(), x.tolist())
+    assert used_reg > 200  # the register version ran for most of the n <= 64 cases

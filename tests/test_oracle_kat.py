@@ -173,3 +173,15 @@ def test_resize_and_blur_sanity(oracle):
     hor = sum(k[i] * pad[:, i:i + 50] for i in range(7))
     ref = sum(k[i] * hor[i:i + 40, :] for i in range(7))
     assert np.abs(b - ref).max() <= 0.5 + 1e-9
+
+
+def test_oracle_node_sort_is_compare_nodes():
+    """oracle.node_sort orders by (count, UL.x) ascending (compareNodes, src/ORBextractor.cc:676-697)."""
+    import numpy as np
+    from oracle import oracle as orc
+    rng = np.random.default_rng(5)
+    c, x = rng.integers(2, 9, 200).astype(np.int32), rng.integers(0, 50, 200).astype(np.int32)
+    o = orc.node_sort(c, x)
+    assert sorted(o.tolist()) == list(range(200))
+    keys = list(zip(c[o].tolist(), x[o].tolist()))
+    assert keys == sorted(keys)
