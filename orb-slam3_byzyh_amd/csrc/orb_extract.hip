@@ -880,26 +880,33 @@ __device__ __forceinline__ void fast_cell(const KernelGeom& g, const CellDesc& C
                 __builtin_elementwise_min(__builtin_elementwise_max(p8, p12), __builtin_elementwise_max(p12, p0)));
             const u16x2 br = __builtin_elementwise_sub_sat(bmax, v + tt);  // > 0 <=> bmax > v + t
             const u16x2 dk = __builtin_elementwise_sub_sat(v, dmin + tt);  // > 0 <=> dmin < v - t
-            return __builtin_bit_cast(uint32_t, br) | __builtin_bit_cast(uint32_t, dk);
+            // 0 / 1 per pixel (pass <=> the saturated difference is non-zero)
+            return __builtin_elementwise_min(br | dk, w16(1, 1));
         };
+        // item -> (row, quad): one division here, then a fixed (row, quad) step of 64 items per round
+        int r = lane / nq, q = lane - (lane / nq) * nq;
+        const int dr = 64 / nq, dq = 64 - dr * nq;
         for (int i0 = 0; i0 < nitems; i0 += 64) {
             const int it = i0 + lane;
-            const int r = it / nq, q = it - r * nq;
             unsigned bits = 0;
             if (it < nitems) {
                 const uint32_t* rc = wrow + (r + 3) * wsw;
                 const uint32_t L4 = ext(rc, q, shift), C4 = ext(rc, q, oc), R4 = ext(rc, q, orr);
                 const uint32_t U4 = ext(rc - 3 * wsw, q, oc), D4 = ext(rc + 3 * wsw, q, oc);
-                const uint32_t pl = pass2(lo16(C4), lo16(D4), lo16(R4), lo16(U4), lo16(L4));
-                const uint32_t ph = pass2(hi16(C4), hi16(D4), hi16(R4), hi16(U4), hi16(L4));
-                bits = ((pl & 0xffffu) != 0) | ((pl >> 16) != 0) << 1 | ((ph & 0xffffu) != 0) << 2 | ((ph >> 16) != 0) << 3;
+                const uint32_t pl = __builtin_bit_cast(uint32_t, pass2(lo16(C4), lo16(D4), lo16(R4), lo16(U4), lo16(L4)));
+                const uint32_t ph = __builtin_bit_cast(uint32_t, pass2(hi16(C4), hi16(D4), hi16(R4), hi16(U4), hi16(L4)));
+                bits = (pl & 1u) | ((pl >> 15) & 2u) | ((ph & 1u) << 2) | ((ph >> 13) & 8u);
                 const int rem = dw - 4 * q;  // pixels of this quad inside the detectable row
                 if (rem < 4) bits &= (1u << rem) - 1u;
             }
+            const int row = r, quad = q;
+            q += dq;
+            r += dr;
+            if (q >= nq) { q -= nq; ++r; }
             const int cnt = __popc(bits);
             const int incl = wave_incl_scan_dpp(cnt);
             int pos = nlist + incl - cnt;
-            const int base_idx = (r + 3) * ws + 4 * q + 3;
+            const int base_idx = (row + 3) * ws + 4 * quad + 3;
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if (bits >> k & 1u) cl[pos++] = (uint16_t)(base_idx + k);
@@ -977,7 +984,7 @@ __device__ __forceinline__ void fast_cell(const KernelGeom& g, const CellDesc& C
 // One wave per FAST cell.  LDS per wave: window | score map | candidate list (u16 pixel indices).
 // Pixels with score < minTh can neither be emitted nor beat an emitted neighbour, so the exact score
 // is computed only for the pixels that are corners at minTh (compacted list, no divergence).
-__global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict__ gp, const CellDesc* __restrict__ cells, int win_cap,
+__global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict__ gp, const CellDesc* __restrict__ cells, int win_cap, int wave_lds,
                                                     const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
                                                     int32_t* __restrict__ cell_count, uint8_t* __restrict__ cell_thr,
                                                     int cell0, int cell_end, unsigned long long* __restrict__ stamps,
@@ -998,7 +1005,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
     const CellDesc C = cells[cid];
     const LevelGeom& L = g.lv[C.level];
     const uint8_t* view = pyr + (size_t)f * g.pyr_frame_bytes + L.plane_off + (size_t)kEdge * L.pitch + kEdge;
-    uint8_t* win = smem + (size_t)wave * 4 * win_cap;
+    uint8_t* win = smem + (size_t)wave * wave_lds;
     uint8_t* sc = win + win_cap;
     uint16_t* cl = reinterpret_cast<uint16_t*>(sc + win_cap);
     const uint8_t* src = view + (size_t)C.ini_y * L.pitch + C.ini_x;
@@ -2960,7 +2967,7 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     // FAST on the first `split` levels runs on a side stream as soon as those pyramid levels exist,
     // overlapping the latency-bound launches of the small levels (k.lv[split..] ) on `st`.
     const int split = (e->fast_split > 0 && e->fast_split < k.nlevels) ? e->fast_split : 0;
-    const int win_cap = (G.max_win + 15) & ~15;
+    static const bool fast_full_lds = getenv("ORBGPU_FAST_FULL_LDS") != nullptr;  // A/B: size every launch for all levels
     static const bool fast_stamps = getenv("ORBGPU_FAST_STAMPS") != nullptr;
     auto launch_fast = [&](int l0, int l1, hipStream_t s2) {
         const int c0 = k.lv[l0].cell_begin, c1 = k.lv[l1 - 1].cell_begin + k.lv[l1 - 1].cell_count;
@@ -2968,8 +2975,15 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
         unsigned long long* stamps = nullptr;
         const size_t ns = (size_t)(c1 - c0) * n * 12;
         if (fast_stamps && hipMalloc(&stamps, ns * 8) == hipSuccess) (void)hipMemsetAsync(stamps, 0, ns * 8, s2);
+        // LDS per wave = 4 x the largest window of the launched levels: the early levels' smaller
+        // windows allow more resident waves than the level-7 window would
+        int mw = 0, md = 0;
+        for (int l = l0; l < l1; ++l) { mw = std::max(mw, G.max_win_lv[l]); md = std::max(md, G.max_det_lv[l]); }
+        const int win_cap = ((fast_full_lds ? G.max_win : mw) + 15) & ~15;
+        // per wave: window | score map | candidate list (u16, at most one entry per detectable pixel)
+        const int wave_lds = fast_full_lds ? 4 * win_cap : 2 * win_cap + ((2 * md + 15) & ~15);
         const int groups = (c1 - c0 + 3) / 4, nblocks = groups * n, share = (nblocks + 7) / 8;
-        hipLaunchKernelGGL(k_fast_cells, dim3(8 * share), dim3(256), 4 * 4 * win_cap, s2, e->d_geom, e->d_cells, win_cap,
+        hipLaunchKernelGGL(k_fast_cells, dim3(8 * share), dim3(256), 4 * wave_lds, s2, e->d_geom, e->d_cells, win_cap, wave_lds,
                            pyr, cand, ccount, cthr, c0, c1, stamps, groups, nblocks, share);
         if (stamps) {  // debug: mean phase clocks over the launch's cells
             std::vector<unsigned long long> h(ns);

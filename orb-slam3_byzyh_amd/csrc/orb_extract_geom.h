@@ -113,6 +113,8 @@ struct Geometry {
     std::vector<int32_t> xtab;  // per level >= 1, per column: sx, (a0 | a1 << 16)
     std::vector<int32_t> ytab;  // per level >= 1, per row: r0, r1, b0, b1
     int max_win = 0;            // largest FAST window (bytes)
+    int max_win_lv[kMaxLevels] = {};  // the same per level (a launch's LDS is sized for its levels)
+    int max_det_lv[kMaxLevels] = {};  // largest detectable region of a window per level (candidate list entries)
     int max_level_cands = 0;    // largest per-level candidate capacity
     int max_sel = 0;            // largest per-level selected capacity
 };
@@ -208,7 +210,10 @@ inline bool build_geometry(const Params& P, int width, int height, Geometry& g) 
                 c.slot = level_cap;
                 level_cap += c.cap;
                 // dword-aligned rows; at least 48 bytes (k_fast_cells uses a fixed 48-byte stride when the window fits)
-                g.max_win = std::max(g.max_win, std::max((int)c.win_w + 6, 48) * c.win_h);
+                const int wbytes = std::max((int)c.win_w + 6, 48) * c.win_h;
+                g.max_win = std::max(g.max_win, wbytes);
+                g.max_win_lv[l] = std::max(g.max_win_lv[l], wbytes);
+                g.max_det_lv[l] = std::max(g.max_det_lv[l], dw * dh);
                 g.cells.push_back(c);
             }
         }
