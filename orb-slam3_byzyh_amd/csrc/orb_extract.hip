@@ -2458,7 +2458,9 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
                                                   const int32_t* __restrict__ sel_count,
                                                   const int32_t* __restrict__ rank_in_class, const int32_t* __restrict__ lap_count,
                                                   int cap, orb_keypoint_t* __restrict__ kps, uint8_t* __restrict__ desc,
-                                                  int32_t* __restrict__ counts, int chunks, int nblocks, int share) {
+                                                  int32_t* __restrict__ counts, int chunks, int nblocks, int share,
+                                                  int stage_levels, int stage_mode, orb_keypoint_t* __restrict__ st_kp,
+                                                  uint8_t* __restrict__ st_desc) {
     const KernelGeom& g = *gp;
     __shared__ __attribute__((aligned(16))) uint32_t patch[kDescKpPerBlock][(kDescLds + 15) / 16 * 4];
     const int half = threadIdx.x >> 5, hl = threadIdx.x & 31;
@@ -2499,8 +2501,12 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
         lap_before += __shfl_xor(lap_before, o, 64);
         mono_before += __shfl_xor(mono_before, o, 64);
     }
+    // Split mode (levels [0, stage_levels) described early, on the side stream, before the later
+    // levels' quad-tree exists): stage_mode 1 computes them into per-slot staging records (the output
+    // slot needs every level's count); the final launch (stage_mode 2) moves them to their slots.
     const int n = __shfl(cnt_l, (threadIdx.x & ~15) + level, 64);
-    if (chunk0 == 0 && threadIdx.x == 0) {
+    const size_t st_idx = sbase;  // staging record of this half-wave's slot (valid when slot < n)
+    if (stage_mode != 1 && chunk0 == 0 && threadIdx.x == 0) {
         int mono = 0;
         for (int l = 0; l < g.nlevels; ++l)
             mono += sel_count[(size_t)f * g.nlevels + l] - lap_count[(size_t)f * g.nlevels + l];
@@ -2508,7 +2514,18 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
         counts[2 * f + 1] = total > cap ? ORB_ERR_CAPACITY : mono;
     }
     if (chunk * kDescKpPerBlock >= n) return;                // whole block idle
-    const bool active = slot < n && total <= cap;            // frame within the caller's capacity
+    const bool active = slot < n && (stage_mode == 1 || total <= cap);  // frame within the caller's capacity
+    if (stage_mode == 2 && level < stage_levels) {  // staged record -> output slot (block-uniform branch)
+        if (!active) return;
+        const int rk = rk_spec;
+        const int dst = rk < 0 ? total - 1 - (lap_before + (-rk - 1)) : mono_before + rk;
+        if (hl < 8)
+            reinterpret_cast<uint32_t*>(desc + ((size_t)f * cap + dst) * 32)[hl] =
+                reinterpret_cast<const uint32_t*>(st_desc + st_idx * 32)[hl];
+        else if (hl == 8)
+            kps[(size_t)f * cap + dst] = st_kp[st_idx];
+        return;
+    }
     const uint32_t key = active ? key_spec : 0;
     const int x = key_x(key) + L.minB, y = key_y(key) + L.minB;
     // ---- stage both patches.  Lane (r, w) of a half-wave loads word w of row r of a 3-row group, so
@@ -2586,11 +2603,13 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
     if (!active) return;
     const int rk = rk_spec;
     const int dst = rk < 0 ? total - 1 - (lap_before + (-rk - 1)) : mono_before + rk;
+    uint8_t* drow = stage_mode == 1 ? st_desc + st_idx * 32 : desc + ((size_t)f * cap + dst) * 32;
+    orb_keypoint_t* kdst = stage_mode == 1 ? st_kp + st_idx : kps + (size_t)f * cap + dst;
     if (hl < 8) {
         uint32_t w = words[0];
 #pragma unroll
         for (int m = 1; m < 8; ++m) if (hl == m) w = words[m];
-        reinterpret_cast<uint32_t*>(desc + ((size_t)f * cap + dst) * 32)[hl] = w;
+        reinterpret_cast<uint32_t*>(drow)[hl] = w;
     } else if (hl == 8) {
         orb_keypoint_t k;
         float fx = (float)x, fy = (float)y;
@@ -2601,7 +2620,7 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
         k.response = (float)key_score(key);
         k.octave = level;
         k.class_id = -1;
-        kps[(size_t)f * cap + dst] = k;
+        *kdst = k;
     }
 }
 
@@ -2648,6 +2667,9 @@ struct Extractor {
     int chunk = 1 << 30, nstreams = 1;  // off by default: measured slower (streams did not overlap)
     int fast_split = 3;                 // FAST on levels [0, fast_split) overlaps the small pyramid levels
     int fast_per_level = 0;             // 1: FAST of each later level right after its pyramid level (side2); measured slower
+    int desc_split = 1;                 // 1: quad-tree + descriptors of levels [0, fast_split) on the side stream (ORBGPU_DESC_SPLIT)
+    orb_keypoint_t* d_st_kp = nullptr; size_t st_kp_cap = 0;   // their staging records (desc_split)
+    uint8_t* d_st_desc = nullptr; size_t st_desc_cap = 0;
     int qt_v1 = 0;                      // 1: the wave-per-tree quad-tree (k_quadtree, ORBGPU_QT_V1) instead of k_quadtree_kp
     int qt_split = 0;                   // 1: quad-tree of levels [0, fast_split) on the side stream (ORBGPU_QT_SPLIT)
     hipStream_t side = nullptr, side2 = nullptr;
@@ -2791,6 +2813,10 @@ int prepare(Extractor* e, int w, int h, int n) {
     if ((rc = grow(e->d_dst, e->dst_cap, (size_t)k.sel_frame_cap * n)) != ORB_OK) return rc;
     if ((rc = grow(e->d_sel_count, e->selcount_cap, (size_t)k.nlevels * n)) != ORB_OK) return rc;
     if ((rc = grow(e->d_lap_count, e->lapcount_cap, (size_t)k.nlevels * n)) != ORB_OK) return rc;
+    if (e->desc_split) {
+        if ((rc = grow(e->d_st_kp, e->st_kp_cap, (size_t)k.sel_frame_cap * n)) != ORB_OK) return rc;
+        if ((rc = grow(e->d_st_desc, e->st_desc_cap, (size_t)k.sel_frame_cap * n * 32)) != ORB_OK) return rc;
+    }
     if ((k.debug_flags & 4) && (rc = grow(e->d_stamps, e->stamps_cap, (size_t)k.nlevels * n * kQtStamps)) != ORB_OK) return rc;
     return ORB_OK;
 }
@@ -3017,6 +3043,18 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
                                e->d_stamps ? e->d_stamps + (size_t)f0 * k.nlevels * kQtStamps : nullptr, lap0, lap1, dst,
                                lapc, l0);
     };
+    // descriptors of levels [0, lim) (stage_mode 1: into the staging records; 2: all levels, the first
+    // `split` from their staging records; 0: all levels computed here)
+    const bool desc_split = e->desc_split && split > 0 && !e->fast_per_level && e->d_st_kp;
+    auto launch_desc = [&](int mode, int lim, hipStream_t s2) {
+        int chunks = 0;  // blocks per frame: ceil(sel_cap_l / 8) per level (see k_describe)
+        for (int l = 0; l < lim; ++l) chunks += (k.lv[l].sel_cap + kDescKpPerBlock - 1) / kDescKpPerBlock;
+        const int total = chunks * n, share = (total + 7) / 8;
+        hipLaunchKernelGGL(k_describe, dim3(8 * share), dim3(256), 0, s2, e->d_geom, pyr, blr, sel, scount, dst, lapc,
+                           cap, kps, desc, counts, chunks, total, share, split, mode,
+                           e->d_st_kp ? e->d_st_kp + (size_t)f0 * k.sel_frame_cap : nullptr,
+                           e->d_st_desc ? e->d_st_desc + (size_t)f0 * k.sel_frame_cap * 32 : nullptr);
+    };
     // levels [0, lfirst): per-level launches; [lfirst, L): one band launch (k_pyramid_band)
     const bool band = ensure_band_plan(e, n);
     const int lfirst = band ? std::min(std::max(e->band_from, 0), k.nlevels - 1) : k.nlevels;
@@ -3115,7 +3153,8 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
             hipEventRecord(e->split_ev[0], st);
             hipStreamWaitEvent(e->side, e->split_ev[0], 0);
             launch_fast(0, split, e->side);
-            if (e->qt_split) launch_qt(0, split, e->side);
+            if (e->qt_split || desc_split) launch_qt(0, split, e->side);
+            if (desc_split) launch_desc(1, split, e->side);
             hipEventRecord(e->split_ev[1], e->side);
         } else if (split && l >= split && e->fast_per_level) {
             // later (small) levels: FAST as soon as the level exists, on a second side stream
@@ -3135,20 +3174,15 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
         launch_fast(split, k.nlevels, st);
     }
     // qt_split: the quad-tree of the early levels runs on the side stream right after their FAST
-    const bool qts = e->qt_split && split && !band && !e->fast_per_level;
+    // (desc_split: and their descriptors, into the staging records)
+    const bool qts = (e->qt_split || desc_split) && split && !band && !e->fast_per_level;
     if (!qts && split && (!band || split <= lfirst)) hipStreamWaitEvent(st, e->split_ev[1], 0);
     mark(2);
     launch_qt(qts ? split : 0, k.nlevels, st);
     if (qts) hipStreamWaitEvent(st, e->split_ev[1], 0);
     mark(3);
     mark(4);
-    {
-        int chunks = 0;  // blocks per frame: ceil(sel_cap_l / 8) per level (see k_describe)
-        for (int l = 0; l < k.nlevels; ++l) chunks += (k.lv[l].sel_cap + kDescKpPerBlock - 1) / kDescKpPerBlock;
-        const int total = chunks * n, share = (total + 7) / 8;
-        hipLaunchKernelGGL(k_describe, dim3(8 * share), dim3(256), 0, st, e->d_geom, pyr, blr, sel, scount, dst, lapc,
-                           cap, kps, desc, counts, chunks, total, share);
-    }
+    launch_desc(desc_split ? 2 : 0, k.nlevels, st);
     mark(5);
     if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "kernel launch failed");
     return ORB_OK;
@@ -3222,6 +3256,7 @@ int orb_extractor_create(const orb_params_t* p, int max_width, int max_height, i
     if (const char* c = getenv("ORBGPU_PYR_BAND")) e->band_mode = atoi(c);
     if (const char* c = getenv("ORBGPU_QT_SPLIT")) e->qt_split = atoi(c);
     if (const char* c = getenv("ORBGPU_QT_V1")) e->qt_v1 = atoi(c);
+    if (const char* c = getenv("ORBGPU_DESC_SPLIT")) e->desc_split = atoi(c);
     if (const char* c = getenv("ORBGPU_PYR_WG_PER_CU")) e->band_wg_per_cu = std::max(1, atoi(c));
     if (const char* c = getenv("ORBGPU_PYR_BAND_FROM")) e->band_from = std::max(0, atoi(c));
     if (const char* c = getenv("ORBGPU_PYR_BAND_R")) e->band_r = std::min(16, std::max(4, atoi(c)));
@@ -3262,7 +3297,7 @@ int orb_extractor_destroy(orb_extractor_t h) {
     Extractor* e = reinterpret_cast<Extractor*>(h);
     if (!e) return ORB_ERR_ARG;
     if (e->stream) hipStreamSynchronize(e->stream);
-    void* bufs[] = {e->d_tasks, e->d_ntasks, e->d_stamps, e->d_geom, e->d_cells, e->d_xtab, e->d_tiletab, e->d_ytab, e->d_pyr, e->d_blur, e->d_cand, e->d_scratch,
+    void* bufs[] = {e->d_st_kp, e->d_st_desc, e->d_tasks, e->d_ntasks, e->d_stamps, e->d_geom, e->d_cells, e->d_xtab, e->d_tiletab, e->d_ytab, e->d_pyr, e->d_blur, e->d_cand, e->d_scratch,
                     e->d_cell_count, e->d_cell_thr, e->d_sel, e->d_dst, e->d_sel_count, e->d_lap_count, e->d_status,
                     e->d_img, e->d_kps, e->d_desc, e->d_counts};
     for (void* b : bufs)

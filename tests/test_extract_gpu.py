@@ -96,8 +96,12 @@ def test_extract_parity(pkg, oracle, frames, case):
     assert np.array_equal(desc, rdesc), f"{case} descriptors: {_first_diff(desc, rdesc)}"
 
 
-def test_batch_equals_single_calls(pkg, oracle, synth):
+@pytest.mark.parametrize("desc_split", ["0", "1"])
+def test_batch_equals_single_calls(pkg, oracle, synth, monkeypatch, desc_split):
+    """Device batch == oracle per frame; also with the early levels' quad-tree and descriptors on the
+    side stream (ORBGPU_DESC_SPLIT=1: staged records placed by the final describe launch)."""
     import torch
+    monkeypatch.setenv("ORBGPU_DESC_SPLIT", desc_split)
     frames = synth.frame_batch(6, 640, 480, seed0=300)
     ex = pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=640, max_height=480, max_batch=8)
     imgs = torch.from_numpy(frames).cuda()
@@ -190,8 +194,9 @@ def test_band_pyramid_path_parity(pkg, oracle, frames, synth, monkeypatch, band_
         assert np.array_equal(desc[f, :n].cpu().numpy(), rd), f
 
 
-@pytest.mark.parametrize("mode", [("ORBGPU_DEBUG_FLAGS", "8"), ("ORBGPU_DEBUG_FLAGS", "2"), ("ORBGPU_QT_V1", "1")],
-                         ids=["kp_scratch_keys", "kp_serial_sort", "wave_per_tree"])
+@pytest.mark.parametrize("mode", [("ORBGPU_DEBUG_FLAGS", "8"), ("ORBGPU_DEBUG_FLAGS", "2"), ("ORBGPU_QT_V1", "1"),
+                                  ("ORBGPU_DESC_SPLIT", "1")],
+                         ids=["kp_scratch_keys", "kp_serial_sort", "wave_per_tree", "desc_split"])
 def test_quadtree_variants_parity(pkg, oracle, frames, monkeypatch, mode):
     """Quad-tree variants stay bit-exact: the key-parallel kernel with its keys forced into the global
     scratch (flag 8) or with the single-lane libstdc++ sort port (flag 2), and the wave-per-tree kernel."""
