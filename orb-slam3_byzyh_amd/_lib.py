@@ -120,6 +120,7 @@ DEBUG_PROTOTYPES = {
     "orb_debug_qt_stamps": (_i, [_vp, _vp, _i]),
     "orb_debug_node_sort": (_i, [_vp, _vp, _i, _i, _vp]),
     "orb_extractor_stage_ms": (_i, [_vp, _fp, _ip, ctypes.POINTER(ctypes.c_longlong)]),
+    "orb_extractor_pyramid_launch_ms": (_i, [_vp, _fp, _ip]),
 }
 
 STAGES = ("pyramid", "fast", "quadtree", "place", "describe")

@@ -2678,7 +2678,11 @@ struct Extractor {
     hipStream_t sub[kMaxStreams] = {};
     hipEvent_t fork_ev = nullptr, join_ev[kMaxStreams] = {};
     long long batches = 0;
-    int profile = 0;  // 0 off, 1 every stage boundary, 2 only the pyramid stage (marks 0 and 1)
+    int profile = 0;  // 0 off, 1 every stage boundary, 2 only the pyramid stage (marks 0 and 1),
+                      // 3 an event pair around every pyramid level launch (k_pyramid_level durations)
+    unsigned long long* d_span = nullptr;  // profile 3: per-block stamps of the recorded pyramid launches
+    size_t span_cap = 0, span_used = 0;    // (u64 words; 8 per block, [6] wall start, [7] wall end)
+    std::vector<std::pair<size_t, size_t>> span_launches;  // (offset, blocks) per recorded launch
     std::vector<hipEvent_t> events;   // kStages + 1 per profiled sub-batch launch
     int ev_used = 0;                  // launches recorded since the last read
     long long frames_profiled = 0;
@@ -3045,7 +3049,7 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     };
     // descriptors of levels [0, lim) (stage_mode 1: into the staging records; 2: all levels, the first
     // `split` from their staging records; 0: all levels computed here)
-    const bool desc_split = e->desc_split && split > 0 && !e->fast_per_level && e->d_st_kp;
+    bool desc_split = false;  // set once the pyramid path is known (below)
     auto launch_desc = [&](int mode, int lim, hipStream_t s2) {
         int chunks = 0;  // blocks per frame: ceil(sel_cap_l / 8) per level (see k_describe)
         for (int l = 0; l < lim; ++l) chunks += (k.lv[l].sel_cap + kDescKpPerBlock - 1) / kDescKpPerBlock;
@@ -3058,6 +3062,10 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     // levels [0, lfirst): per-level launches; [lfirst, L): one band launch (k_pyramid_band)
     const bool band = ensure_band_plan(e, n);
     const int lfirst = band ? std::min(std::max(e->band_from, 0), k.nlevels - 1) : k.nlevels;
+    // the early levels' FAST (and with desc_split their quad-tree + descriptors) go to the side stream
+    // only when those levels come from the per-level launches
+    desc_split = e->desc_split && split > 0 && split <= lfirst && !e->fast_per_level && e->d_st_kp;
+    const bool qts = (e->qt_split || desc_split) && split > 0 && split <= lfirst && !e->fast_per_level;
     auto launch_band = [&]() {
         BandArgs A;
         A.max_tasks = e->plan_max_tasks;
@@ -3119,6 +3127,16 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
         const size_t nblk = (size_t)grid.x * grid.y;
         if (pyr_stamps && hipMalloc(&stamps, sizeof(unsigned long long) * 8 * nblk) == hipSuccess)
             (void)hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * 8 * nblk, st);
+        // profile 3: per-block wall-clock start / end of this launch into the span buffer (the launch's
+        // duration = last block end - first block start; no events between the launches)
+        if (e->profile == 3 && !stamps && e->d_span) {
+            const size_t need = (size_t)8 * nblk;
+            if (e->span_used + need <= e->span_cap) {
+                stamps = e->d_span + e->span_used;
+                e->span_launches.push_back({e->span_used, nblk});
+                e->span_used += need;
+            }
+        }
         if (l == 0)
             hipLaunchKernelGGL(k_pyramid_level<true>, grid, dim3(256), 0, st, A, imgs, (long long)frame_stride, stride,
                                pyr, blr, e->d_xtab, e->d_ytab, e->d_tiletab, stamps);
@@ -3128,7 +3146,7 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
         else
             hipLaunchKernelGGL((k_pyramid_level<false, kBoxH, kBoxW>), grid, dim3(256), 0, st, A, nullptr, 0LL, 0, pyr,
                                blr, e->d_xtab, e->d_ytab, e->d_tiletab, stamps);
-        if (stamps) {  // debug: phase clocks of this level's blocks
+        if (stamps && pyr_stamps) {  // debug: phase clocks of this level's blocks
             std::vector<unsigned long long> hst((size_t)8 * nblk);
             (void)hipStreamSynchronize(st);
             (void)hipMemcpy(hst.data(), stamps, hst.size() * 8, hipMemcpyDeviceToHost);
@@ -3153,7 +3171,7 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
             hipEventRecord(e->split_ev[0], st);
             hipStreamWaitEvent(e->side, e->split_ev[0], 0);
             launch_fast(0, split, e->side);
-            if (e->qt_split || desc_split) launch_qt(0, split, e->side);
+            if (qts) launch_qt(0, split, e->side);
             if (desc_split) launch_desc(1, split, e->side);
             hipEventRecord(e->split_ev[1], e->side);
         } else if (split && l >= split && e->fast_per_level) {
@@ -3175,7 +3193,6 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     }
     // qt_split: the quad-tree of the early levels runs on the side stream right after their FAST
     // (desc_split: and their descriptors, into the staging records)
-    const bool qts = (e->qt_split || desc_split) && split && !band && !e->fast_per_level;
     if (!qts && split && (!band || split <= lfirst)) hipStreamWaitEvent(st, e->split_ev[1], 0);
     mark(2);
     launch_qt(qts ? split : 0, k.nlevels, st);
@@ -3297,7 +3314,7 @@ int orb_extractor_destroy(orb_extractor_t h) {
     Extractor* e = reinterpret_cast<Extractor*>(h);
     if (!e) return ORB_ERR_ARG;
     if (e->stream) hipStreamSynchronize(e->stream);
-    void* bufs[] = {e->d_st_kp, e->d_st_desc, e->d_tasks, e->d_ntasks, e->d_stamps, e->d_geom, e->d_cells, e->d_xtab, e->d_tiletab, e->d_ytab, e->d_pyr, e->d_blur, e->d_cand, e->d_scratch,
+    void* bufs[] = {e->d_span, e->d_st_kp, e->d_st_desc, e->d_tasks, e->d_ntasks, e->d_stamps, e->d_geom, e->d_cells, e->d_xtab, e->d_tiletab, e->d_ytab, e->d_pyr, e->d_blur, e->d_cand, e->d_scratch,
                     e->d_cell_count, e->d_cell_thr, e->d_sel, e->d_dst, e->d_sel_count, e->d_lap_count, e->d_status,
                     e->d_img, e->d_kps, e->d_desc, e->d_counts};
     for (void* b : bufs)
@@ -3508,8 +3525,18 @@ int orb_debug_level_blurred(orb_extractor_t h, int frame, int level, uint8_t* ho
 int orb_extractor_profile(orb_extractor_t h, int enable) {
     Extractor* e = reinterpret_cast<Extractor*>(h);
     if (!e) return ORB_ERR_ARG;
-    e->profile = enable == 2 ? 2 : (enable != 0 ? 1 : 0);
+    e->profile = (enable == 2 || enable == 3) ? enable : (enable != 0 ? 1 : 0);
     e->ev_used = 0;
+    e->span_used = 0;
+    e->span_launches.clear();
+    if (enable == 3) {  // room for 64 steps of 64-frame 640x480 batches (~31k blocks per step)
+        const size_t want = (size_t)8 * 4 * 1024 * 1024;
+        if (!e->d_span) {
+            if (hipMalloc(&e->d_span, want * 8) != hipSuccess) { e->d_span = nullptr; return orbgpu_fail(ORB_ERR_DEVICE, "hipMalloc failed"); }
+            e->span_cap = want;
+        }
+        if (hipMemset(e->d_span, 0, e->span_cap * 8) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "hipMemset failed");
+    }
     e->frames_profiled = 0;
     e->batches = 0;
     return ORB_OK;
@@ -3531,6 +3558,34 @@ int orb_extractor_stage_ms(orb_extractor_t h, float* ms, int* launches, long lon
     }
     if (launches) *launches = (int)e->batches;  // batch calls (each may be several sub-batch launches)
     if (frames) *frames = e->frames_profiled;
+    return ORB_OK;
+}
+
+// Profile mode 3: summed milliseconds of the recorded pyramid level launches (event pair around each
+// k_pyramid_level launch) and their number
+int orb_extractor_pyramid_launch_ms(orb_extractor_t h, float* ms, int* launches) {
+    Extractor* e = reinterpret_cast<Extractor*>(h);
+    if (!e || !ms) return ORB_ERR_ARG;
+    *ms = 0.f;
+    if (launches) *launches = 0;
+    if (!e->d_span || e->span_launches.empty()) return ORB_OK;
+    std::vector<unsigned long long> hst(e->span_used);
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(hst.data(), e->d_span, e->span_used * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "span download failed");
+    double tot = 0;
+    for (const auto& L : e->span_launches) {
+        unsigned long long t0 = ~0ull, t1 = 0;
+        for (size_t b = 0; b < L.second; ++b) {
+            const unsigned long long* q = &hst[L.first + 8 * b];
+            if (!q[6]) continue;  // blocks past the frame's tiles return before stamping
+            t0 = std::min(t0, q[6]);
+            t1 = std::max(t1, q[7]);
+        }
+        if (t1 > t0) tot += (double)(t1 - t0) * 1e-5;  // wall clock: 100 MHz
+    }
+    *ms = (float)tot;
+    if (launches) *launches = (int)e->span_launches.size();
     return ORB_OK;
 }
 

@@ -134,8 +134,9 @@ class ORBextractor:
     # ---- per-stage timing (HIP events on the launch stream)
     def profile(self, enable: bool | str = True) -> None:
         """Record HIP events at stage boundaries: True = every stage, "pyramid" = only around the
-        pyramid stage (2 events per call, for timed regions), False = off."""
-        mode = 2 if enable == "pyramid" else (1 if enable else 0)
+        pyramid stage (2 events per call, for timed regions), "pyramid_launches" = around every
+        pyramid level launch (kernel durations), False = off."""
+        mode = 2 if enable == "pyramid" else 3 if enable == "pyramid_launches" else (1 if enable else 0)
         check(self._lib.orb_extractor_profile(self._h, mode), "orb_extractor_profile")
 
     def stage_ms(self):
@@ -145,6 +146,15 @@ class ORBextractor:
         fr = ctypes.c_longlong()
         check(self._lib.orb_extractor_stage_ms(self._h, ms, ctypes.byref(n), ctypes.byref(fr)), "orb_extractor_stage_ms")
         return dict(zip(_lib.STAGES, (float(v) for v in ms))), n.value, fr.value
+
+    def pyramid_launch_ms(self):
+        """profile("pyramid_launches"): summed ms of the recorded k_pyramid_level launches (an event
+        pair around each launch) and their number."""
+        ms = ctypes.c_float()
+        n = ctypes.c_int()
+        check(self._lib.orb_extractor_pyramid_launch_ms(self._h, ctypes.byref(ms), ctypes.byref(n)),
+              "orb_extractor_pyramid_launch_ms")
+        return float(ms.value), n.value
 
     # ---- public pyramid, include/ORBextractor.h:83
     def level_padded(self, level: int, frame: int = 0) -> np.ndarray:

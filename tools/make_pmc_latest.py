@@ -12,8 +12,11 @@ import json
 import re
 import sys
 
-STAGE_KERNELS = {"pyramid": ["k_pyramid_level"], "fast": ["k_fast_cells"], "quadtree": ["k_quadtree"],
+STAGE_KERNELS = {"pyramid": ["k_pyramid_level"], "fast": ["k_fast_cells"], "quadtree": ["k_quadtree_kp", "k_quadtree"],
                  "describe": ["k_describe"]}
+# launches per step: 8 pyramid levels; FAST, quad-tree and describe each in two launches (levels 0-2 on
+# the side stream, 3-7 on the main stream; the second describe also places the staged levels 0-2)
+LAUNCHES = {"k_pyramid_level": 8, "k_fast_cells": 2, "k_quadtree_kp": 2, "k_quadtree": 1, "k_describe": 2}
 
 
 def main(d, out, frames=64):
@@ -36,7 +39,7 @@ def main(d, out, frames=64):
             if not fd:
                 continue
             # per-dispatch averages x launches per step
-            nper = {"pyramid": 8, "fast": 2}.get(stage, 1)  # launches per step
+            nper = LAUNCHES.get(k, 1)
             fetch += 2 * 1024 * sum(fd.values()) / len(fd) * nper
             if wd:
                 write += 1024 * sum(wd.values()) / len(wd) * nper
@@ -46,7 +49,10 @@ def main(d, out, frames=64):
     dom = max(res["stages"], key=lambda s: res["stages"][s]["hbm_bytes"]) if res["stages"] else None
     res["kernel_stage"] = "pyramid" if "pyramid" in res["stages"] else dom
     if res["kernel_stage"]:
-        res["hbm_bytes_per_launch"] = res["stages"][res["kernel_stage"]]["hbm_bytes"]
+        n = LAUNCHES.get(STAGE_KERNELS[res["kernel_stage"]][0], 1)
+        res["hbm_bytes_per_step"] = res["stages"][res["kernel_stage"]]["hbm_bytes"]
+        res["launches_per_step"] = n
+        res["hbm_bytes_per_launch"] = res["hbm_bytes_per_step"] / n
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
