@@ -5,9 +5,10 @@
 //                    REFLECT_101 frame) + its 7x7 sigma-2 Gaussian (for rBRIEF), one LDS tile pass
 //   k_fast_cells     one wave per (frame, FAST cell): threshold-independent FAST-9 score, 3x3 NMS
 //                    inside the cell window, iniTh/minTh choice, row-major candidate emission
-//   k_quadtree       one wave per (frame, level): DistributeOctTree, exact list/sort semantics, plus the
-//                    keypoint's vLappingArea class rank (level-0 scaling, src:1656-1676)
-//   k_describe       one wave per keypoint: IC_Angle (31-px disc) + steered rBRIEF (256 tests)
+//   k_quadtree_kp    one 256-thread workgroup per (frame, level): DistributeOctTree with exact list and
+//                    std::sort semantics (keys stay put, node ids move), plus each keypoint's
+//                    vLappingArea class rank (level-0 scaling, src:1656-1676)
+//   k_describe       one half-wave per keypoint: IC_Angle (31-px disc) + steered rBRIEF (256 tests)
 //
 // No MFMA anywhere: this is byte / integer / popcount work.  All float arithmetic that reaches an
 // output (resize coefficients are host tables; fastAtan2; pattern steering) is compiled with
@@ -131,13 +132,17 @@ __device__ __forceinline__ int wave_incl_max_dpp(int v) {
 constexpr int kBufDword3 = 0x00020000;  // gfx9 buffer resource word 3 (32-bit data format)
 
 // A tile is 122 x 16 padded-plane pixels; with the 3-px blur halo it is 128 x 22, one lane per column.
-constexpr int kTileW = 122, kTileH = 16, kHalo = 3;
-constexpr int kLW = kTileW + 2 * kHalo, kLH = kTileH + 2 * kHalo;  // 128 x 22
+#ifndef ORBGPU_PYR_TILE_H
+#define ORBGPU_PYR_TILE_H 24
+#endif
+constexpr int kTileW = 122, kTileH = ORBGPU_PYR_TILE_H, kHalo = 3;
+static_assert(kTileH % 4 == 0, "two vertical-blur halves of an even row count");
+constexpr int kLW = kTileW + 2 * kHalo, kLH = kTileH + 2 * kHalo;  // 128 x 38
 static_assert(kLW == 128, "one lane per haloed tile column, two waves per row");
 constexpr int kBoxW = 288, kBoxH = 2 * kLH + 4;  // source box (bytes) for scale factors <= 2
 static_assert(kBoxW >= 3 + 2 * kLW + 2, "box too narrow");
 // box for level ratios <= 1.25 (the usual 1.2): 133 * 1.25 + 2 columns + 3 alignment bytes, 21 * 1.25 + 2 rows
-constexpr int kSmallBoxW = 176, kSmallBoxH = 32;
+constexpr int kSmallBoxW = 176, kSmallBoxH = ((kLH - 1) * 5 / 4 + 3 + 3) & ~3;
 static_assert(kSmallBoxW >= 3 + (kLW - 1) * 5 / 4 + 3 && kSmallBoxH >= (kLH - 1) * 5 / 4 + 3, "small box too small");
 
 // 8 bytes from a 4-byte-aligned LDS row at any byte offset, as aligned dword reads + v_alignbyte.
@@ -316,9 +321,10 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
         __syncthreads();
         PYR_STAMP(2);
     }
-    // padded plane: 8 consecutive pixels per thread (tile columns 3 .. 124)
-    {
-        const int r = tid >> 4, c = (tid & 15) * 8;
+    // padded plane: 8 consecutive pixels per thread (tile columns 3 .. 124), 16 rows per pass
+#pragma unroll
+    for (int r = tid >> 4; r < kTileH; r += 16) {
+        const int c = (tid & 15) * 8;
         const int py = Y0 + r, px = X0 + c;
         if (py < A.ph && c < kTileW) {
             uint8_t* dst = plane + (size_t)py * A.pitch + px;
@@ -357,17 +363,19 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
     }
     __syncthreads();
     PYR_STAMP(4);
-    // vertical pass: lane per column, output rows 8h .. 8h + 7 from row pairs 4h .. 4h + 6
+    // vertical pass: lane per column, output rows kVR*h .. kVR*h + kVR-1 from row pairs
+    // (kVR/2)*h .. (kVR/2)*h + kVR/2 + 2
     {
+        constexpr int kVR = kTileH / 2;
         const int col = tid & (kLW - 1), hh = tid >> 7;
         const int px = X0 + col;
         if (col < kTileW && px >= kEdge && px < kEdge + A.w) {
-            uint32_t Pr[7];
+            uint32_t Pr[kVR / 2 + 3];
 #pragma unroll
-            for (int k = 0; k < 7; ++k) Pr[k] = hs2[4 * hh + k][col];
-            uint8_t* dst = bplane + (size_t)(Y0 + 8 * hh) * A.pitch + px;
+            for (int k = 0; k < kVR / 2 + 3; ++k) Pr[k] = hs2[(kVR / 2) * hh + k][col];
+            uint8_t* dst = bplane + (size_t)(Y0 + kVR * hh) * A.pitch + px;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
+            for (int i = 0; i < kVR; ++i) {
                 const int m = i >> 1;
                 uint32_t acc = 1u << 15;
                 if ((i & 1) == 0) {
@@ -381,7 +389,7 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
                     acc = __builtin_amdgcn_udot2(as_u16x2(Pr[m + 2]), w16(56, 48), acc, false);
                     acc = __builtin_amdgcn_udot2(as_u16x2(Pr[m + 3]), w16(34, 18), acc, false);
                 }
-                const int vy = Y0 + 8 * hh + i - kEdge;
+                const int vy = Y0 + kVR * hh + i - kEdge;
                 if (vy >= 0 && vy < A.h) dst[i * A.pitch] = (uint8_t)(acc >> 16);  // <= 255 exactly
             }
         }
@@ -1021,7 +1029,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
 #undef FAST_STAMP
 
 // ================================================================================================
-// 3. DistributeOctTree, src:711-1057, one wave per (frame, level)
+// 3. DistributeOctTree, src:711-1057, one 256-thread workgroup per (frame, level)
 // ================================================================================================
 // The reference keeps the nodes in a std::list: every non-leaf node is divided and its non-empty
 // children pushed to the FRONT in the order n1..n4, the parent erased.  A pass therefore yields
@@ -1029,25 +1037,16 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
 // In the "careful" phase the splittable children of the last pass are std::sort-ed with
 // compareNodes and divided from the largest until the list reaches N; parents are erased wherever
 // they are, so a round yields list' = reverse(children in push order) ++ (old list minus divided).
-//
-// Here node records live in list order in two generations (current / next).  A pass is computed
-// in parallel: per node child counts (wave-cooperative for big nodes, one lane per node for small
-// ones), wave scans for the positions of children / survivors / splittable children, and a stable
-// 4-way partition of each divided node's keys into the other key buffer.  The careful phase finds
-// its stopping division with a scan over the sorted order.  The sort itself is the exact libstdc++
-// introsort port (orb_hd.h), run by one lane, because compareNodes has ties.
-constexpr int kBigNode = 48;  // nodes with more keys are partitioned by the whole wave
-
+// Node records live in list order in two generations (current / next); the positions of children,
+// survivors and splittable children come from wave scans (k_quadtree_kp below).
 struct QGen {
     int16_t *x0, *y0, *x1, *y1;
-    int32_t *ks, *kn;
-    uint8_t *kb, *leaf;
+    int32_t* kn;  // key count
+    uint8_t* leaf;  // bNoMore
 };
 
-struct QTree {
-    uint32_t *keys0, *keys1;
+struct QTree {          // list workspace: generations, sort arrays and index lists
     QGen g0, g1;
-    int32_t* cnt;        // [4][lcap] child counts of the current generation's nodes
     uint16_t *split, *prev;
     uint8_t* divided;
     int* sort_ws;        // introsort stack (kOrbSortStack * 3 ints)
@@ -1056,49 +1055,6 @@ struct QTree {
     int lcap;
 };
 
-__host__ __device__ inline size_t qt_meta_bytes(int lcap) {
-    return (size_t)lcap * (2 * (4 * 2 + 4 * 2 + 2) + 4 * 4 + 2 * 2 + 1 + 16 + 6) + 64 + kOrbSortStack * 12;
-}
-
-__device__ inline void qt_carve(QTree& t, uint8_t* p, int lcap) {
-    t.lcap = lcap;
-    t.sort_ws = (int*)p;
-    p += kOrbSortStack * 12;  // 480 bytes: keeps the u64 arrays 8-aligned
-    t.sel_el = (unsigned long long*)p; p += 8 * lcap;
-    t.sel_tmp = (unsigned long long*)p; p += 8 * lcap;
-    QGen* gens[2] = {&t.g0, &t.g1};
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-        gens[g]->ks = (int32_t*)p; p += 4 * lcap;
-        gens[g]->kn = (int32_t*)p; p += 4 * lcap;
-    }
-    t.cnt = (int32_t*)p; p += 16 * lcap;
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-        gens[g]->x0 = (int16_t*)p; p += 2 * lcap;
-        gens[g]->y0 = (int16_t*)p; p += 2 * lcap;
-        gens[g]->x1 = (int16_t*)p; p += 2 * lcap;
-        gens[g]->y1 = (int16_t*)p; p += 2 * lcap;
-    }
-    t.split = (uint16_t*)p; p += 2 * lcap;
-    t.prev = (uint16_t*)p; p += 2 * lcap;
-    t.posA = (uint16_t*)p; p += 2 * lcap;
-    t.posB = (uint16_t*)p; p += 2 * lcap;
-    t.bend = (uint16_t*)p; p += 2 * lcap;
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-        gens[g]->kb = p; p += lcap;
-        gens[g]->leaf = p; p += lcap;
-    }
-    t.divided = p;
-}
-
-__device__ __forceinline__ uint32_t* key_buf(const QTree& t, int b) { return b ? t.keys1 : t.keys0; }
-
-__device__ __forceinline__ int quadrant(uint32_t k, int sx, int sy) {  // n1 n2 / n3 n4, src:651-661
-    return (key_x(k) >= sx ? 1 : 0) + (key_y(k) >= sy ? 2 : 0);
-}
-
 __device__ __forceinline__ void split_point(const QGen& G, int p, int& sx, int& sy) {
     const int x0 = G.x0[p], y0 = G.y0[p], x1 = G.x1[p], y1 = G.y1[p];
     sx = x0 + ((x1 - x0 + 1) >> 1);  // UL.x + ceil((float)(UR.x-UL.x)/2), src:608
@@ -1106,154 +1062,6 @@ __device__ __forceinline__ void split_point(const QGen& G, int p, int& sx, int& 
 }
 
 __device__ __forceinline__ int wave_incl_scan(int v, int) { return wave_incl_scan_dpp(v); }
-
-// child counts of node p of generation G; the whole wave cooperates (result uniform)
-__device__ inline void coop_count(const QTree& t, const QGen& G, int p, int lane, int c[4]) {
-    int sx, sy;
-    split_point(G, p, sx, sy);
-    const uint32_t* src = key_buf(t, G.kb[p]) + G.ks[p];
-    const int kn = uniform(G.kn[p]);
-    c[0] = c[1] = c[2] = c[3] = 0;
-    for (int b = 0; b < kn; b += 64) {
-        const int i = b + lane;
-        const int q = i < kn ? quadrant(src[i], sx, sy) : -1;
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) c[qq] += __popcll(ballot(q == qq));
-    }
-}
-
-__device__ inline void coop_scatter(const QTree& t, const QGen& G, int p, int lane, const int c[4]) {
-    int sx, sy;
-    split_point(G, p, sx, sy);
-    const int kb = G.kb[p], ks = G.ks[p];
-    const uint32_t* src = key_buf(t, kb) + ks;
-    uint32_t* dst = key_buf(t, kb ^ 1) + ks;
-    const int kn = uniform(G.kn[p]);
-    int base[4] = {0, c[0], c[0] + c[1], c[0] + c[1] + c[2]};
-    for (int b = 0; b < kn; b += 64) {
-        const int i = b + lane;
-        uint32_t k = 0;
-        int q = -1;
-        if (i < kn) { k = src[i]; q = quadrant(k, sx, sy); }
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-            const unsigned long long m = ballot(q == qq);
-            if (q == qq) dst[base[qq] + rank_in(m)] = k;
-            base[qq] += __popcll(m);
-        }
-    }
-}
-
-__device__ inline void serial_count(const QTree& t, const QGen& G, int p, int c[4]) {
-    int sx, sy;
-    split_point(G, p, sx, sy);
-    const uint32_t* src = key_buf(t, G.kb[p]) + G.ks[p];
-    const int kn = G.kn[p];
-    c[0] = c[1] = c[2] = c[3] = 0;
-    for (int i = 0; i < kn; ++i) {
-        const int q = quadrant(src[i], sx, sy);
-        c[0] += q == 0; c[1] += q == 1; c[2] += q == 2; c[3] += q == 3;
-    }
-}
-
-__device__ inline void serial_scatter(const QTree& t, const QGen& G, int p, const int c[4]) {
-    int sx, sy;
-    split_point(G, p, sx, sy);
-    const int kb = G.kb[p], ks = G.ks[p];
-    const uint32_t* src = key_buf(t, kb) + ks;
-    uint32_t* dst = key_buf(t, kb ^ 1) + ks;
-    const int kn = G.kn[p];
-    int base[4] = {0, c[0], c[0] + c[1], c[0] + c[1] + c[2]};
-    for (int i = 0; i < kn; ++i) {
-        const uint32_t k = src[i];
-        const int q = quadrant(k, sx, sy);
-        const int o = q == 0 ? base[0]++ : q == 1 ? base[1]++ : q == 2 ? base[2]++ : base[3]++;
-        dst[o] = k;
-    }
-}
-
-// Child counts for the nodes at positions pos(i), i < n (pos == nullptr: identity, skipping leaves).
-__device__ inline void qt_count_children(QTree& t, const QGen& G, const uint16_t* pos, int n, int lane) {
-    for (int b = 0; b < n; b += 64) {
-        const int i = b + lane;
-        int p = 0;
-        bool big = false;
-        if (i < n) {
-            p = pos ? pos[i] : i;
-            big = !G.leaf[p] && G.kn[p] > kBigNode;
-        }
-        unsigned long long m = ballot(big);
-        while (m) {
-            const int bit = __ffsll((long long)m) - 1;
-            m &= m - 1;
-            const int pp = uniform(pos ? pos[b + bit] : b + bit);
-            int c[4];
-            coop_count(t, G, pp, lane, c);
-            if (lane == 0) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) t.cnt[q * t.lcap + pp] = c[q];
-            }
-        }
-        if (i < n && !G.leaf[p] && !big) {
-            int c[4];
-            serial_count(t, G, p, c);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) t.cnt[q * t.lcap + p] = c[q];
-        }
-    }
-    wave_sync();
-}
-
-__device__ inline void qt_partition(QTree& t, const QGen& G, const uint16_t* pos, int n, int lane) {
-    for (int b = 0; b < n; b += 64) {
-        const int i = b + lane;
-        int p = 0;
-        bool big = false;
-        if (i < n) {
-            p = pos ? pos[i] : i;
-            big = !G.leaf[p] && G.kn[p] > kBigNode;
-        }
-        unsigned long long m = ballot(big);
-        while (m) {
-            const int bit = __ffsll((long long)m) - 1;
-            m &= m - 1;
-            const int pp = uniform(pos ? pos[b + bit] : b + bit);
-            int c[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) c[q] = uniform(t.cnt[q * t.lcap + pp]);
-            coop_scatter(t, G, pp, lane, c);
-        }
-        if (i < n && !G.leaf[p] && !big) {
-            int c[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) c[q] = t.cnt[q * t.lcap + p];
-            serial_scatter(t, G, p, c);
-        }
-    }
-    wave_sync();
-}
-
-// write child q of node p (generation A) to position `to` of generation B
-__device__ __forceinline__ void qt_write_child(QTree& t, const QGen& A, QGen& B, int p, int q, int n, int to) {
-    int sx, sy;
-    split_point(A, p, sx, sy);
-    const int x0 = A.x0[p], y0 = A.y0[p], x1 = A.x1[p], y1 = A.y1[p];
-    int off = 0;
-    for (int qq = 0; qq < q; ++qq) off += t.cnt[qq * t.lcap + p];
-    B.x0[to] = (int16_t)((q & 1) ? sx : x0);
-    B.x1[to] = (int16_t)((q & 1) ? x1 : sx);
-    B.y0[to] = (int16_t)((q & 2) ? sy : y0);
-    B.y1[to] = (int16_t)((q & 2) ? y1 : sy);
-    B.ks[to] = A.ks[p] + off;
-    B.kn[to] = n;
-    B.kb[to] = (uint8_t)(A.kb[p] ^ 1);
-    B.leaf[to] = n == 1;
-}
-
-__device__ __forceinline__ void qt_copy_node(const QGen& A, QGen& B, int p, int to) {
-    B.x0[to] = A.x0[p]; B.y0[to] = A.y0[p]; B.x1[to] = A.x1[p]; B.y1[to] = A.y1[p];
-    B.ks[to] = A.ks[p]; B.kn[to] = A.kn[p]; B.kb[to] = A.kb[p]; B.leaf[to] = A.leaf[p];
-}
 
 __device__ __forceinline__ int wave_incl_max(int v, int) { return wave_incl_max_dpp(v); }
 
@@ -1476,363 +1284,8 @@ struct QPlace {  // vLappingArea classification of the selected keys
     int32_t* n_lap;
 };
 
-template <bool kKeysInLds>
-__device__ void qt_run(QTree& t, int K, int N, int nroots, float root_w, int span_y,
-                       const uint32_t* __restrict__ cand_level, const CellDesc* __restrict__ cells, int cell_begin,
-                       int cell_count, const int32_t* __restrict__ ccount, uint32_t* __restrict__ sel_out,
-                       int sel_cap, int* n_sel, int* status, int debug_flags, unsigned long long* stamps,
-                       const QPlace& place) {
-    const int lane = lane_id();
-    bool overflow = false;
-    // diagnostic phase timers (debug_flags & 4): gather, reg count, reg scan+write, reg partition, sort,
-    // careful count, careful scan+write, careful partition, final, #regular passes, #careful rounds, K
-    unsigned long long tm[kQtStamps] = {};
-    unsigned long long t_last = (debug_flags & 4) ? __builtin_amdgcn_s_memtime() : 0;
-    auto stamp = [&](int i) {
-        if (debug_flags & 4) { const unsigned long long now = __builtin_amdgcn_s_memtime(); tm[i] += now - t_last; t_last = now; }
-    };
-    // ---- gather candidates in cell order into keys[1], counting per root (src:756-764).
-    // Cells in chunks of 64 (lane = cell, a wave scan of the counts gives each cell's start); the
-    // chunk's keys are then spread evenly over the lanes, each lane finding its key's cell by a binary
-    // search over the lanes' starts, with up to 8 x 64 loads in flight per round trip.
-    int rcount[kMaxRoots];
-#pragma unroll
-    for (int r = 0; r < kMaxRoots; ++r) rcount[r] = 0;
-    {
-        constexpr int kGB = 8;
-        int carry = 0;
-        for (int cb = 0; cb < cell_count; cb += 64) {
-            const int c = cb + lane;
-            int n = 0, slot = 0;
-            if (c < cell_count) { n = ccount[c]; slot = cells[cell_begin + c].slot; }
-            const int incl = wave_incl_scan(n, lane);
-            const int start = incl - n;  // chunk-local, non-decreasing over the lanes
-            const int T = uniform(__builtin_amdgcn_readlane(incl, 63));
-            for (int j0 = 0; j0 < T; j0 += 64 * kGB) {
-                uint32_t kk[kGB];
-#pragma unroll
-                for (int gi = 0; gi < kGB; ++gi) {
-                    const int i = j0 + 64 * gi + lane;
-                    // the last lane whose start <= i owns key i (empty cells share the next start)
-                    int cl = 0;
-#pragma unroll
-                    for (int s = 32; s > 0; s >>= 1)
-                        if (__shfl(start, cl + s, 64) <= i) cl += s;
-                    const int sl = __shfl(slot, cl, 64), s0 = __shfl(start, cl, 64);
-                    kk[gi] = i < T ? cand_level[sl + (i - s0)] : 0u;
-                }
-#pragma unroll
-                for (int gi = 0; gi < kGB; ++gi) {
-                    const int i = j0 + 64 * gi + lane;
-                    if (i < T) {
-                        t.keys1[carry + i] = kk[gi];
-                        const int root = (int)((float)key_x(kk[gi]) / root_w);
-#pragma unroll
-                        for (int r = 0; r < kMaxRoots; ++r) rcount[r] += root == r;
-                    }
-                }
-            }
-            carry += T;
-        }
-#pragma unroll
-        for (int r = 0; r < kMaxRoots; ++r) rcount[r] = uniform(wave_sum(rcount[r]));
-    }
-    wave_sync();
-    if (nroots == 1) {  // one root: the gathered order already is the root's key order
-        uint32_t* k0 = t.keys0;
-        t.keys0 = t.keys1;
-        t.keys1 = k0;
-    } else {   // stable partition by root into keys[0]
-        int base[kMaxRoots];
-        int acc = 0;
-#pragma unroll
-        for (int r = 0; r < kMaxRoots; ++r) { base[r] = acc; acc += rcount[r]; }
-        for (int b = 0; b < K; b += 64) {
-            const int i = b + lane;
-            int root = -1;
-            uint32_t k = 0;
-            if (i < K) { k = t.keys1[i]; root = (int)((float)key_x(k) / root_w); }
-            for (int r = 0; r < nroots; ++r) {
-                const unsigned long long m = ballot(root == r);
-                if (root == r) t.keys0[base[r] + rank_in(m)] = k;
-                base[r] += __popcll(m);
-            }
-        }
-    }
-    stamp(0);
-    // ---- roots (src:733-786): empty roots erased, single-key roots are leaves
-    QGen A = t.g0, B = t.g1;  // current / next generation, swapped after every pass
-    int nlist = 0;
-    {
-        int start = 0;
-        for (int r = 0; r < nroots; ++r) {
-            const int n = rcount[r];
-            if (n > 0) {
-                if (lane == 0) {
-                    A.x0[nlist] = (int16_t)(int)(root_w * (float)r);
-                    A.x1[nlist] = (int16_t)(int)(root_w * (float)(r + 1));
-                    A.y0[nlist] = 0;
-                    A.y1[nlist] = (int16_t)span_y;
-                    A.ks[nlist] = start; A.kn[nlist] = n; A.kb[nlist] = 0; A.leaf[nlist] = n == 1;
-                }
-                nlist++;
-            }
-            start += n;
-        }
-    }
-    wave_sync();
-    int nsplit = 0;
-    bool done = false;
-    while (!done && !overflow) {
-        // ---------------- regular pass (src:802-918)
-        const int prev_size = nlist;
-        qt_count_children(t, A, nullptr, nlist, lane);
-        stamp(1);
-        int total_children = 0, total_surv = 0;
-        for (int b = 0; b < nlist; b += 64) {
-            const int i = b + lane;
-            int nc = 0, sv = 0;
-            if (i < nlist) {
-                if (A.leaf[i]) sv = 1;
-                else for (int q = 0; q < 4; ++q) nc += t.cnt[q * t.lcap + i] > 0;
-            }
-            total_children += wave_sum(nc);
-            total_surv += wave_sum(sv);
-        }
-        total_children = uniform(total_children);
-        total_surv = uniform(total_surv);
-        const int new_size = total_children + total_surv;
-        if (new_size > t.lcap) { overflow = true; break; }
-        int carry_c = 0, carry_s = 0, carry_p = 0;
-        for (int b = 0; b < nlist; b += 64) {
-            const int i = b + lane;
-            int nc = 0, sv = 0, ns = 0, c[4] = {0, 0, 0, 0};
-            if (i < nlist) {
-                if (A.leaf[i]) sv = 1;
-                else {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) { c[q] = t.cnt[q * t.lcap + i]; nc += c[q] > 0; ns += c[q] > 1; }
-                }
-            }
-            const int ic = wave_incl_scan(nc, lane), is = wave_incl_scan(sv, lane), ip = wave_incl_scan(ns, lane);
-            if (i < nlist) {
-                if (sv) {
-                    qt_copy_node(A, B, i, total_children + carry_s + is - 1);
-                } else {
-                    int r = 0, r2 = 0;
-                    const int stackpos = carry_c + ic - nc, splitpos = carry_p + ip - ns;
-                    for (int q = 0; q < 4; ++q) {
-                        if (c[q] == 0) continue;
-                        const int to = total_children - 1 - (stackpos + r);
-                        qt_write_child(t, A, B, i, q, c[q], to);
-                        if (c[q] > 1) t.split[splitpos + r2++] = (uint16_t)to;
-                        r++;
-                    }
-                }
-            }
-            carry_c += __builtin_amdgcn_readlane(ic, 63);
-            carry_s += __builtin_amdgcn_readlane(is, 63);
-            carry_p += __builtin_amdgcn_readlane(ip, 63);
-        }
-        nsplit = carry_p;
-        stamp(2);
-        qt_partition(t, A, nullptr, nlist, lane);
-        { const QGen tmp = A; A = B; B = tmp; }
-        nlist = new_size;
-        const int to_expand = nsplit;
-        stamp(3);
-        tm[9]++;
-        if (nlist >= N || nlist == prev_size) {
-            done = true;
-        } else if (nlist + to_expand * 3 > N) {
-            // ---------------- careful rounds (src:932-1016)
-            while (!done && !overflow) {
-                QGen& A2 = A;
-                QGen& B2 = B;
-                const int round_prev = nlist;
-                const int np = nsplit;
-                for (int i = lane; i < np; i += 64) t.prev[i] = t.split[i];
-                wave_sync();
-                if (debug_flags & 2) {  // reference single-lane port (A/B check)
-                    if (lane == 0) {
-                        const int16_t* x0a = A2.x0;
-                        const int32_t* kc = A2.kn;
-                        orb_std_sort(t.prev, np, [&](uint16_t a, uint16_t b) {
-                            const int ca = kc[a], cb = kc[b];
-                            return ca < cb || (ca == cb && x0a[a] < x0a[b]);
-                        }, t.sort_ws);
-                    }
-                    wave_sync();
-                } else {
-                    qt_sort(t, A2, np, lane);
-                }
-                stamp(4);
-                tm[10]++;
-                qt_count_children(t, A2, t.prev, np, lane);
-                stamp(5);
-                // division order o = 0.. is prev[np-1-o]; stop once the list reaches N (src:1006)
-                int ndiv = np, carry = 0;
-                for (int b = 0; b < np; b += 64) {
-                    const int o = b + lane;
-                    int d = 0;
-                    if (o < np) {
-                        const int p = t.prev[np - 1 - o];
-                        for (int q = 0; q < 4; ++q) d += t.cnt[q * t.lcap + p] > 0;
-                        d -= 1;
-                    }
-                    const int inc = wave_incl_scan(d, lane);
-                    const unsigned long long hit = ballot(o < np && nlist + carry + inc >= N);
-                    if (hit) { ndiv = b + __ffsll((long long)hit); break; }
-                    carry += __builtin_amdgcn_readlane(inc, 63);
-                }
-                ndiv = uniform(ndiv);
-                for (int i = lane; i < nlist; i += 64) t.divided[i] = 0;
-                wave_sync();
-                for (int o = lane; o < ndiv; o += 64) t.divided[t.prev[np - 1 - o]] = 1;
-                wave_sync();
-                // children of the divided nodes, in push order
-                int total_children = 0;
-                for (int b = 0; b < ndiv; b += 64) {
-                    const int o = b + lane;
-                    int nc = 0;
-                    if (o < ndiv) {
-                        const int p = t.prev[np - 1 - o];
-                        for (int q = 0; q < 4; ++q) nc += t.cnt[q * t.lcap + p] > 0;
-                    }
-                    total_children += wave_sum(nc);
-                }
-                total_children = uniform(total_children);
-                int kept = 0;
-                for (int b = 0; b < nlist; b += 64) kept += __popcll(ballot(b + lane < nlist && !t.divided[b + lane]));
-                const int new_size = total_children + kept;
-                if (new_size > t.lcap) { overflow = true; break; }
-                int carry_c = 0, carry_p = 0;
-                for (int b = 0; b < ndiv; b += 64) {
-                    const int o = b + lane;
-                    int nc = 0, ns = 0, c[4] = {0, 0, 0, 0}, p = 0;
-                    if (o < ndiv) {
-                        p = t.prev[np - 1 - o];
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) { c[q] = t.cnt[q * t.lcap + p]; nc += c[q] > 0; ns += c[q] > 1; }
-                    }
-                    const int ic = wave_incl_scan(nc, lane), ip = wave_incl_scan(ns, lane);
-                    if (o < ndiv) {
-                        int r = 0, r2 = 0;
-                        const int stackpos = carry_c + ic - nc, splitpos = carry_p + ip - ns;
-                        for (int q = 0; q < 4; ++q) {
-                            if (c[q] == 0) continue;
-                            const int to = total_children - 1 - (stackpos + r);
-                            qt_write_child(t, A2, B2, p, q, c[q], to);
-                            if (c[q] > 1) t.split[splitpos + r2++] = (uint16_t)to;
-                            r++;
-                        }
-                    }
-                    carry_c += __builtin_amdgcn_readlane(ic, 63);
-                    carry_p += __builtin_amdgcn_readlane(ip, 63);
-                }
-                nsplit = carry_p;
-                int carry_k = 0;
-                for (int b = 0; b < nlist; b += 64) {
-                    const int i = b + lane;
-                    const bool keep = i < nlist && !t.divided[i];
-                    const unsigned long long m = ballot(keep);
-                    if (keep) qt_copy_node(A2, B2, i, total_children + carry_k + rank_in(m));
-                    carry_k += __popcll(m);
-                }
-                stamp(6);
-                // key partition of the divided nodes (prev[np-ndiv .. np-1])
-                qt_partition(t, A2, t.prev + (np - ndiv), ndiv, lane);
-                { const QGen tmp = A; A = B; B = tmp; }
-                nlist = new_size;
-                stamp(7);
-                if (nlist >= N || nlist == round_prev) done = true;
-            }
-        }
-    }
-    if (overflow || nlist > sel_cap) {
-        if (lane == 0) { *n_sel = 0; atomicMax(status, 1); }
-        return;
-    }
-    // ---- keep the first max-response key of every node, in list order (src:1028-1053), and rank it
-    // within its vLappingArea class (src:1656-1676): rank_out = rank among non-lapping keys, or
-    // -(1 + rank among lapping keys); k_describe turns that into the output slot
-    const QGen& F = A;
-    int carry_lap = 0, carry_mono = 0;
-    for (int b = 0; b < nlist; b += 64) {
-        const int i = b + lane;
-        bool lap = false;
-        if (i < nlist) {
-            const uint32_t* kk = key_buf(t, F.kb[i]) + F.ks[i];
-            const int n = F.kn[i];
-            uint32_t best = kk[0];
-            for (int q = 1; q < n; ++q)
-                if (key_score(kk[q]) > key_score(best)) best = kk[q];
-            sel_out[i] = best;
-            float x = (float)(key_x(best) + place.minB);
-            if (place.level != 0) x = x * place.scale;
-            lap = x >= (float)place.lap0 && x <= (float)place.lap1;
-        }
-        const unsigned long long ml = ballot(i < nlist && lap), mm = ballot(i < nlist && !lap);
-        if (i < nlist) place.rank_out[i] = lap ? -(1 + carry_lap + rank_in(ml)) : carry_mono + rank_in(mm);
-        carry_lap += __popcll(ml);
-        carry_mono += __popcll(mm);
-    }
-    if (lane == 0) { *n_sel = nlist; *place.n_lap = carry_lap; }
-    stamp(8);
-    if ((debug_flags & 4) && stamps && lane == 0) {
-        tm[11] = (unsigned long long)K;
-        for (int i = 0; i < kQtStamps; ++i) stamps[i] = tm[i];
-    }
-}
-
-__global__ __launch_bounds__(64) void k_quadtree(const KernelGeom* __restrict__ gp, const CellDesc* __restrict__ cells,
-                                                 const uint32_t* __restrict__ cand, const int32_t* __restrict__ cell_count,
-                                                 uint32_t* __restrict__ key_scratch, uint32_t* __restrict__ sel,
-                                                 int32_t* __restrict__ sel_count, int lds_bytes, int* __restrict__ status,
-                                                 unsigned long long* __restrict__ stamps, int lap0, int lap1,
-                                                 int32_t* __restrict__ rank_out, int32_t* __restrict__ lap_count,
-                                                 int level0) {
-    const KernelGeom& g = *gp;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int level = level0 + blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
-    const LevelGeom& L = g.lv[level];
-    const int32_t* cc = cell_count + (size_t)f * g.ncells + L.cell_begin;
-    int K = 0;
-    for (int c = lane; c < L.cell_count; c += 64) K += cc[c];
-    K = uniform(wave_sum(K));
-    const int N = L.nfeat;
-    const int lcap = L.sel_cap + 64;
-    QTree t;
-    size_t meta = (qt_meta_bytes(lcap) + 15) & ~(size_t)15;
-    qt_carve(t, smem, lcap);
-    uint32_t* sel_out = sel + (size_t)f * g.sel_frame_cap + L.sel_off;
-    int32_t* n_sel = sel_count + (size_t)f * g.nlevels + level;
-    const uint32_t* cand_level = cand + (size_t)f * g.cand_frame_cap + L.cand_off;
-    QPlace place{level, L.minB, lap0, lap1, L.scale, rank_out + (size_t)f * g.sel_frame_cap + L.sel_off,
-                 lap_count + (size_t)f * g.nlevels + level};
-    if (meta > (size_t)lds_bytes) {
-        if (lane == 0) { *n_sel = 0; atomicMax(status, 2); }
-        return;
-    }
-    const size_t key_bytes = (size_t)K * 4 * 2;
-    if (meta + key_bytes <= (size_t)lds_bytes) {
-        t.keys0 = (uint32_t*)(smem + meta);
-        t.keys1 = t.keys0 + K;
-        qt_run<true>(t, K, N, L.n_roots, L.root_w, L.maxBY - L.minB, cand_level, cells, L.cell_begin,
-                     L.cell_count, cc, sel_out, L.sel_cap, n_sel, status, g.debug_flags,
-                     stamps ? stamps + ((size_t)f * g.nlevels + level) * kQtStamps : nullptr, place);
-    } else {
-        uint32_t* scratch = key_scratch + ((size_t)f * g.cand_frame_cap + L.cand_off) * 2;
-        t.keys0 = scratch;
-        t.keys1 = scratch + L.cand_cap;
-        qt_run<false>(t, K, N, L.n_roots, L.root_w, L.maxBY - L.minB, cand_level, cells, L.cell_begin,
-                      L.cell_count, cc, sel_out, L.sel_cap, n_sel, status, g.debug_flags,
-                     stamps ? stamps + ((size_t)f * g.nlevels + level) * kQtStamps : nullptr, place);
-    }
-}
-
 // ------------------------------------------------------------------------------------------------
-// Key-parallel DistributeOctTree (default): one 256-thread workgroup per (level, frame).
+// Key-parallel DistributeOctTree: one 256-thread workgroup per (level, frame).
 //
 // The keys never move.  They stay in gather order (the reference's vToDistributeKeys order) and
 // each carries the list position of its node in the current generation.  Every node's key vector
@@ -1879,7 +1332,6 @@ __device__ inline void qt2_carve(QT2& T, uint8_t* p, int lcap) {
         T.cnt[g] = (int32_t*)p; p += 16 * lcap;
         T.sxy[g] = (uint32_t*)p; p += 4 * lcap;
         gens[g]->kn = (int32_t*)p; p += 4 * lcap;
-        gens[g]->ks = nullptr;
     }
     T.best = (uint32_t*)p; p += 4 * lcap;
 #pragma unroll
@@ -1897,7 +1349,6 @@ __device__ inline void qt2_carve(QT2& T, uint8_t* p, int lcap) {
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
         gens[g]->leaf = p; p += lcap;
-        gens[g]->kb = nullptr;
     }
     t.divided = p;
 }
@@ -2670,7 +2121,6 @@ struct Extractor {
     int desc_split = 1;                 // 1: quad-tree + descriptors of levels [0, fast_split) on the side stream (ORBGPU_DESC_SPLIT)
     orb_keypoint_t* d_st_kp = nullptr; size_t st_kp_cap = 0;   // their staging records (desc_split)
     uint8_t* d_st_desc = nullptr; size_t st_desc_cap = 0;
-    int qt_v1 = 0;                      // 1: the wave-per-tree quad-tree (k_quadtree, ORBGPU_QT_V1) instead of k_quadtree_kp
     int qt_split = 0;                   // 1: quad-tree of levels [0, fast_split) on the side stream (ORBGPU_QT_SPLIT)
     hipStream_t side = nullptr, side2 = nullptr;
     hipEvent_t split_ev[3] = {};
@@ -2796,13 +2246,13 @@ int prepare(Extractor* e, int w, int h, int n) {
         size_t meta = 0;
         for (int l = 0; l < g.k.nlevels; ++l) {
             const int lcap = g.k.lv[l].sel_cap + 64;
-            meta = std::max(meta, ((e->qt_v1 ? qt_meta_bytes(lcap) : qt2_meta_bytes(lcap)) + 15) & ~(size_t)15);
+            meta = std::max(meta, (qt2_meta_bytes(lcap) + 15) & ~(size_t)15);
         }
         const size_t want = std::max<size_t>(80 * 1024, meta + 32 * 1024);
         if (meta > 160 * 1024) return orbgpu_fail(ORB_ERR_ARG, "nfeatures too large for the quad-tree LDS budget");
         e->qt_lds = (int)std::min<size_t>(want, 160 * 1024);
-        if (hipFuncSetAttribute(e->qt_v1 ? (const void*)k_quadtree : (const void*)k_quadtree_kp,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, e->qt_lds) != hipSuccess)
+        if (hipFuncSetAttribute((const void*)k_quadtree_kp, hipFuncAttributeMaxDynamicSharedMemorySize, e->qt_lds) !=
+            hipSuccess)
             return orbgpu_fail(ORB_ERR_DEVICE, "cannot raise the quad-tree LDS limit");
     }
     const orbgpu::KernelGeom& k = e->geo.k;
@@ -3041,8 +2491,7 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     // quad-tree of levels [l0, l1): one wave per (level, frame)
     auto launch_qt = [&](int l0, int l1, hipStream_t s2) {
         if (l1 > l0)
-            hipLaunchKernelGGL(e->qt_v1 ? k_quadtree : k_quadtree_kp, dim3(l1 - l0, n), dim3(e->qt_v1 ? 64 : kQtThreads),
-                               e->qt_lds, s2, e->d_geom, e->d_cells, cand, ccount,
+            hipLaunchKernelGGL(k_quadtree_kp, dim3(l1 - l0, n), dim3(kQtThreads), e->qt_lds, s2, e->d_geom, e->d_cells, cand, ccount,
                                scratch, sel, scount, e->qt_lds, e->d_status,
                                e->d_stamps ? e->d_stamps + (size_t)f0 * k.nlevels * kQtStamps : nullptr, lap0, lap1, dst,
                                lapc, l0);
@@ -3258,7 +2707,6 @@ int orb_extractor_create(const orb_params_t* p, int max_width, int max_height, i
         delete e;
         return orbgpu_fail(ORB_ERR_DEVICE, "stream/status allocation failed");
     }
-    hipFuncSetAttribute((const void*)k_quadtree, hipFuncAttributeMaxDynamicSharedMemorySize, e->qt_lds);
     hipFuncSetAttribute((const void*)k_quadtree_kp, hipFuncAttributeMaxDynamicSharedMemorySize, e->qt_lds);
     if (const char* c = getenv("ORBGPU_CHUNK")) e->chunk = std::max(1, atoi(c));
     if (const char* c = getenv("ORBGPU_STREAMS")) e->nstreams = std::min(Extractor::kMaxStreams, std::max(1, atoi(c)));
@@ -3272,7 +2720,6 @@ int orb_extractor_create(const orb_params_t* p, int max_width, int max_height, i
     if (const char* c = getenv("ORBGPU_FAST_PER_LEVEL")) e->fast_per_level = atoi(c);
     if (const char* c = getenv("ORBGPU_PYR_BAND")) e->band_mode = atoi(c);
     if (const char* c = getenv("ORBGPU_QT_SPLIT")) e->qt_split = atoi(c);
-    if (const char* c = getenv("ORBGPU_QT_V1")) e->qt_v1 = atoi(c);
     if (const char* c = getenv("ORBGPU_DESC_SPLIT")) e->desc_split = atoi(c);
     if (const char* c = getenv("ORBGPU_PYR_WG_PER_CU")) e->band_wg_per_cu = std::max(1, atoi(c));
     if (const char* c = getenv("ORBGPU_PYR_BAND_FROM")) e->band_from = std::max(0, atoi(c));

@@ -194,12 +194,13 @@ def test_band_pyramid_path_parity(pkg, oracle, frames, synth, monkeypatch, band_
         assert np.array_equal(desc[f, :n].cpu().numpy(), rd), f
 
 
-@pytest.mark.parametrize("mode", [("ORBGPU_DEBUG_FLAGS", "8"), ("ORBGPU_DEBUG_FLAGS", "2"), ("ORBGPU_QT_V1", "1"),
-                                  ("ORBGPU_DESC_SPLIT", "1")],
-                         ids=["kp_scratch_keys", "kp_serial_sort", "wave_per_tree", "desc_split"])
+@pytest.mark.parametrize("mode", [("ORBGPU_DEBUG_FLAGS", "8"), ("ORBGPU_DEBUG_FLAGS", "2"), ("ORBGPU_DEBUG_FLAGS", "16"),
+                                  ("ORBGPU_DESC_SPLIT", "0")],
+                         ids=["kp_scratch_keys", "kp_serial_sort", "kp_lds_sort", "no_desc_split"])
 def test_quadtree_variants_parity(pkg, oracle, frames, monkeypatch, mode):
-    """Quad-tree variants stay bit-exact: the key-parallel kernel with its keys forced into the global
-    scratch (flag 8) or with the single-lane libstdc++ sort port (flag 2), and the wave-per-tree kernel."""
+    """Quad-tree variants stay bit-exact: keys forced into the global scratch (flag 8), the single-lane
+    libstdc++ sort port (flag 2), the LDS sort emulation for every candidate set (flag 16), and the
+    pipeline without the side-stream describe of the early levels."""
     monkeypatch.setenv(*mode)
     for case in ["poly640", "noise1280", "init5000", "odd_size"]:
         img, nf, lap = frames[case]

@@ -15,8 +15,7 @@ n=ex._lib.orb_debug_qt_stamps(ex._h, buf.ctypes.data, len(buf))
 st=buf.reshape(64,8,NS).astype(np.float64)
 st[:,:,8]=(buf.reshape(64,8,NS)[:,:,8] & 0xffff).astype(np.float64)
 import os
-names=(["gather","r_count","r_scan","r_part","sort","c_count","c_scan","c_part","final","#reg","#car","K"] if os.environ.get("ORBGPU_QT_V1")=="1" else
-       ["gather","roots","r_node","r_key","sort","c_node","c_key","final","np0","#reg","#car","K"])
+names=["gather","roots","r_node","r_key","sort","c_node","c_key","final","np0","#reg","#car","K"]
 for l in range(8):
     m=st[:,l,:].mean(axis=0); mx=st[:,l,:].max(axis=0)
     print(l, " ".join(f"{nm}={m[i]:.0f}/{mx[i]:.0f}" for i,nm in enumerate(names)))
