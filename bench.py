@@ -406,6 +406,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--frames", type=int, default=FRAMES)
+    ap.add_argument("--in-flight", type=int, default=2,
+                    help="extractor handles with a batch in flight, each on its own stream (consecutive steps "
+                         "overlap: one batch's latency-bound quad-tree/describe tail runs beside the next "
+                         "batch's pyramid/FAST); 1 = one batch at a time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-ba", action="store_true", help="skip the LocalBA (C5) measurement")
@@ -436,45 +440,64 @@ def main():
     nfr = args.frames
     frames = np.stack([synth.polygon_frame(WIDTH, HEIGHT, seed=100 + i) for i in range(nfr)])
     imgs = torch.from_numpy(frames).to(dev)
-    ex = pkg.ORBextractor(NFEAT, 1.2, NLEVELS, 20, 7, max_width=WIDTH, max_height=HEIGHT, max_batch=nfr)
+    H = max(1, args.in_flight)
+    exs = [pkg.ORBextractor(NFEAT, 1.2, NLEVELS, 20, 7, max_width=WIDTH, max_height=HEIGHT, max_batch=nfr)
+           for _ in range(H)]
+    ex = exs[0]
     cap = NFEAT + 16 * NLEVELS
-    out = (torch.empty((nfr, cap, 7), dtype=torch.float32, device=dev),
-           torch.empty((nfr, cap, 32), dtype=torch.uint8, device=dev),
-           torch.empty((nfr, 2), dtype=torch.int32, device=dev))
-    stream = torch.cuda.current_stream(dev)
+    outs = [(torch.empty((nfr, cap, 7), dtype=torch.float32, device=dev),
+             torch.empty((nfr, cap, 32), dtype=torch.uint8, device=dev),
+             torch.empty((nfr, 2), dtype=torch.int32, device=dev)) for _ in range(H)]
+    out = outs[0]
+    # H > 1: every handle on a stream of its own (not the legacy default stream, which would
+    # serialise with the others)
+    streams = [torch.cuda.current_stream(dev)] if H == 1 else [torch.cuda.Stream(dev) for _ in range(H)]
     sharded = None
     if world > 1:
         # C4 data path: every step all-gathers the features of all ranks' frames (RCCL over xGMI),
-        # asynchronously and double-buffered so it overlaps the next step's extraction
+        # asynchronously and multi-buffered so it overlaps the next steps' extraction
         from orbslam3_amd.distributed import ShardedExtractor
-        sharded = ShardedExtractor(ex, nfr, cap)
+        sharded = ShardedExtractor(exs, nfr, cap)
+    it = [0]
 
     def step():
+        h = it[0] % H
+        it[0] += 1
         if sharded is None:
-            ex.extract_batch_device(imgs, (0, 1000), cap=cap, out=out, stream=stream)
+            exs[h].extract_batch_device(imgs, (0, 1000), cap=cap, out=outs[h], stream=streams[h])
         else:
-            sharded.step(imgs, (0, 1000), stream=stream)
+            sharded.step(imgs, (0, 1000), stream=streams[h])
 
     for _ in range(args.warmup):
         step()
     if sharded is not None:
         sharded.finish()
     torch.cuda.synchronize(dev)
-    counts = (out[2] if sharded is None else sharded.local.counts[(args.warmup - 1) % 2]).cpu().numpy()
+    for h in range(min(H, args.warmup)):
+        c = outs[h][2] if sharded is None else sharded.local.counts[h]
+        if not torch.equal(c, outs[0][2] if sharded is None else sharded.local.counts[0]):
+            raise RuntimeError("extractor handles disagree")
+    counts = (out[2] if sharded is None else sharded.local.counts[0]).cpu().numpy()
     feats_per_step = int(counts[:, 0].sum())
     if (counts[:, 1] < 0).any():
         raise RuntimeError("a frame exceeded the keypoint capacity")
 
-    # per-stage breakdown (HIP events at every stage boundary) in an untimed pass
+    # per-stage breakdown (HIP events at every stage boundary) in an untimed pass: one batch at a
+    # time on handle 0, so the stage times are those of a single batch
     ex.profile(True)
     for _ in range(min(10, args.steps)):
-        step()
-    if sharded is not None:
-        sharded.finish()
+        ex.extract_batch_device(imgs, (0, 1000), cap=cap, out=out, stream=streams[0])
     torch.cuda.synchronize(dev)
     stage_ms, launches, _ = ex.stage_ms()
-    # timed region: an event pair around every k_pyramid_level launch (the roofline kernel), on its
-    # launch stream
+    ex.profile(False)
+    # latency of one batch alone (no batch in flight beside it), untimed for `value`
+    t1 = time.perf_counter()
+    for _ in range(min(10, args.steps)):
+        ex.extract_batch_device(imgs, (0, 1000), cap=cap, out=out, stream=streams[0])
+        torch.cuda.synchronize(dev)
+    single_ms = (time.perf_counter() - t1) * 1e3 / min(10, args.steps)
+    # timed region; handle 0 records the wall-clock span of each of its k_pyramid_level launches
+    # (the roofline kernel) from per-block device stamps -- no events between the launches
     ex.profile("pyramid_launches")
     if world > 1:
         dist.barrier()
@@ -490,7 +513,7 @@ def main():
     elapsed_ms = (time.perf_counter() - t0) * 1e3
     pyr_kernel_ms, pyr_kernel_launches = ex.pyramid_launch_ms()
     ex.profile(False)
-    launches_per_step = max(1, pyr_kernel_launches // max(1, args.steps))
+    launches_per_step = NLEVELS  # one k_pyramid_level launch per level per batch
     pyr_launch_avg_ms = pyr_kernel_ms / max(1, pyr_kernel_launches)
 
     total_feats = feats_per_step * args.steps
@@ -533,6 +556,7 @@ def main():
                                    "extraction+description (ORBextractor::operator())",
                        "frames_per_gpu": nfr, "width": WIDTH, "height": HEIGHT, "nfeatures": NFEAT,
                        "nlevels": NLEVELS, "features_per_step_per_gpu": feats_per_step,
+                       "batches_in_flight": H, "single_batch_ms": round(single_ms, 4),
                        "parallelism": f"frame-sharded x{world}" + (
                            f", all-gather of descriptors+keypoints ({backend})" if world > 1 else "")},
             "stages_ms": {k: round(v, 4) for k, v in per_step.items()},

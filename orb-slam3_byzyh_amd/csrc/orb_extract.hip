@@ -2415,7 +2415,7 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     const orbgpu::Geometry& G = e->geo;
     const orbgpu::KernelGeom& k = G.k;
     hipEvent_t* ev = nullptr;
-    if (e->profile) {
+    if (e->profile == 1 || e->profile == 2) {
         const size_t need = (size_t)(e->ev_used + 1) * (orbgpu::kStages + 1);
         while (e->events.size() < need) {
             hipEvent_t x;
@@ -2426,8 +2426,8 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
         e->ev_used++;
         e->frames_profiled += n;
     }
-    auto mark = [&](int i) {
-        if (ev && (e->profile == 1 || i <= 1)) hipEventRecord(ev[i], st);
+    auto mark = [&](int i) {  // profile 3 (per-launch block spans) records no stage events
+        if (ev && (e->profile == 1 || (e->profile == 2 && i <= 1))) hipEventRecord(ev[i], st);
     };
     uint8_t* pyr = e->d_pyr + (size_t)f0 * k.pyr_frame_bytes;
     uint8_t* blr = e->d_blur + (size_t)f0 * k.pyr_frame_bytes;

@@ -62,23 +62,30 @@ class ShardedExtractor:
     """ORB extraction of a global frame batch sharded over the ranks of a process group."""
 
     def __init__(self, extractor, frames_per_rank: int, cap: int | None = None, group=None):
-        self.ex = extractor
+        """`extractor`: one ORBextractor, or a list of them used in turn (batches in flight on their
+        own streams: pass step i's stream as stream i % len)."""
+        self.exs = list(extractor) if isinstance(extractor, (list, tuple)) else [extractor]
+        self.ex = self.exs[0]
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.frames = frames_per_rank
-        self.cap = cap or (extractor.nfeatures + 16 * extractor.nlevels)
+        self.cap = cap or (self.ex.nfeatures + 16 * self.ex.nlevels)
         dev = torch.device("cuda", torch.cuda.current_device())
-        self.local = FeatureBlocks(frames_per_rank, self.cap, dev, count=2)
+        # len(exs) + 1 blocks: step i + len + 1 reuses step i's block on the stream of step i + 1, which
+        # waited for step i's all-gather (finish) before anything it enqueues later
+        self.nbuf = len(self.exs) + 1
+        self.local = FeatureBlocks(frames_per_rank, self.cap, dev, count=self.nbuf)
         self._i = 0
         self._pending = None
 
     def step(self, images, vLappingArea=(0, 0), stream=None):
         """Extract this rank's frames (uint8 [B, H, W] on the GPU) and start the all-gather.
         Returns the previous step's gathered blocks (or None on the first call)."""
-        buf = self._i % 2
+        buf = self._i % self.nbuf
         out = self.local.view(buf)
-        self.ex.extract_batch_device(images, vLappingArea, cap=self.cap, out=out, stream=stream)
+        self.exs[self._i % len(self.exs)].extract_batch_device(images, vLappingArea, cap=self.cap, out=out,
+                                                               stream=stream)
         prev = self.finish(stream)
         # RCCL orders a collective after torch's CURRENT stream only: issue it with the extraction
         # stream current, so it cannot read the blocks before the extraction has written them

@@ -50,5 +50,25 @@ def test_sharded_extractor_single_rank(pkg, synth):
         qa, ta = q.cpu().numpy(), t.cpu().numpy()
         D_ = np.unpackbits(qa[:16, None, :] ^ ta[None, :, :], axis=2).sum(axis=2)
         assert np.array_equal(d1.cpu().numpy()[:16], D_.min(axis=1))
+        # two extractor handles in flight on their own streams (bench.py --in-flight 2): every step's
+        # gathered blocks equal the direct extraction of that step's frames
+        exs = [ex, pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=640, max_height=480, max_batch=4)]
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        sh2 = D.ShardedExtractor(exs, 4)
+        batches = [torch.from_numpy(synth.frame_batch(4, 640, 480, seed0=600 + 10 * i)).cuda() for i in range(5)]
+        got = []
+        for i, b in enumerate(batches):
+            r = sh2.step(b, (0, 1000), stream=streams[i % 2])
+            if r is not None:
+                got.append(r)
+        got.append(sh2.finish(streams[1]))
+        torch.cuda.synchronize()
+        for b, (g_kps, g_desc, g_cnt) in zip(batches, got):
+            kps, desc, cnt = ex.extract_batch_device(b, (0, 1000), cap=sh2.cap)
+            torch.cuda.synchronize()
+            assert torch.equal(g_cnt, cnt)
+            for f in range(4):
+                n = int(cnt[f, 0])
+                assert torch.equal(g_desc[f, :n], desc[f, :n])
     finally:
         dist.destroy_process_group()
