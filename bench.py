@@ -496,9 +496,10 @@ def main():
         ex.extract_batch_device(imgs, (0, 1000), cap=cap, out=out, stream=streams[0])
         torch.cuda.synchronize(dev)
     single_ms = (time.perf_counter() - t1) * 1e3 / min(10, args.steps)
-    # timed region; handle 0 records the wall-clock span of each of its k_pyramid_level launches
+    # timed region; every handle records the wall-clock span of each of its k_pyramid_level launches
     # (the roofline kernel) from per-block device stamps -- no events between the launches
-    ex.profile("pyramid_launches")
+    for e_ in exs:
+        e_.profile("pyramid_launches")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -511,8 +512,12 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed_ms = (time.perf_counter() - t0) * 1e3
-    pyr_kernel_ms, pyr_kernel_launches = ex.pyramid_launch_ms()
-    ex.profile(False)
+    pyr_kernel_ms, pyr_kernel_launches = 0.0, 0
+    for e_ in exs:
+        ms_, n_ = e_.pyramid_launch_ms()
+        pyr_kernel_ms += ms_
+        pyr_kernel_launches += n_
+        e_.profile(False)
     launches_per_step = NLEVELS  # one k_pyramid_level launch per level per batch
     pyr_launch_avg_ms = pyr_kernel_ms / max(1, pyr_kernel_launches)
 
