@@ -862,20 +862,22 @@ __device__ __forceinline__ void fast_cell(const KernelGeom& g, const CellDesc& C
     //     pixels are compacted (row-major) into cl[].
     int nlist = 0;
     if (nd > 0) {
-        // Four pixels per lane (a quad of one detectable row), as u16 pairs: the centre, left (x-3),
-        // right (x+3) dwords of the row and the up / down (y-/+3) dwords come from aligned LDS dwords
-        // and v_alignbyte, and a bright (dark) adjacent compass pair <=> the largest pairwise minimum
-        // exceeds v + t (the smallest pairwise maximum plus t is below v), with v_pk_min/max_u16 and
-        // saturating v_pk_sub_u16.  Items are row-major quads, so the compaction stays row-major.
-        const int nq = (dw + 3) >> 2, nitems = dh * nq;
+        // Eight pixels per lane (an octet of one detectable row), as u16 pairs: the centre, left (x-3),
+        // right (x+3) bytes of the row and the up / down (y-/+3) bytes come from three aligned LDS
+        // dwords and two v_alignbyte each, and a bright (dark) adjacent compass pair <=> the largest
+        // pairwise minimum exceeds v + t (the smallest pairwise maximum plus t is below v), with
+        // v_pk_min/max_u16 and saturating v_pk_sub_u16.  Items are row-major octets, so the compaction
+        // (one wave scan per 8 pixels) stays row-major.
+        const int no = (dw + 7) >> 3, nitems = dh * no;
         const uint32_t* wrow = reinterpret_cast<const uint32_t*>(win - shift);  // aligned window rows
         const int wsw = ws >> 2;
-        // byte offset o (window coordinates, + shift) -> dword o >> 2, alignbyte o & 3
-        const int oc = shift + 3, orr = shift + 6;
         const u16x2 tt = w16(mint, mint);
-        auto ext = [&](const uint32_t* row, int q, int o) {  // bytes [4q + o - shift .. +3] of a row
-            const int d = q + (o >> 2);
-            return __builtin_amdgcn_alignbyte(row[d + 1], row[d], o & 3);
+        // bytes [8o + off .. +7] of an aligned row (off includes the row's shift) as two dwords
+        auto ext8 = [&](const uint32_t* row, int o, int off, uint32_t& a, uint32_t& b) {
+            const int d = 2 * o + (off >> 2);
+            const uint32_t w0 = row[d], w1 = row[d + 1], w2 = row[d + 2];
+            a = __builtin_amdgcn_alignbyte(w1, w0, off & 3);
+            b = __builtin_amdgcn_alignbyte(w2, w1, off & 3);
         };
         auto lo16 = [](uint32_t v) { return as_u16x2(__builtin_amdgcn_perm(v, v, 0x0c010c00u)); };
         auto hi16 = [](uint32_t v) { return as_u16x2(__builtin_amdgcn_perm(v, v, 0x0c030c02u)); };
@@ -889,35 +891,44 @@ __device__ __forceinline__ void fast_cell(const KernelGeom& g, const CellDesc& C
             const u16x2 br = __builtin_elementwise_sub_sat(bmax, v + tt);  // > 0 <=> bmax > v + t
             const u16x2 dk = __builtin_elementwise_sub_sat(v, dmin + tt);  // > 0 <=> dmin < v - t
             // 0 / 1 per pixel (pass <=> the saturated difference is non-zero)
-            return __builtin_elementwise_min(br | dk, w16(1, 1));
+            return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(br | dk, w16(1, 1)));
         };
-        // item -> (row, quad): one division here, then a fixed (row, quad) step of 64 items per round
-        int r = lane / nq, q = lane - (lane / nq) * nq;
-        const int dr = 64 / nq, dq = 64 - dr * nq;
+        auto quad_bits = [&](uint32_t C4, uint32_t D4, uint32_t R4, uint32_t U4, uint32_t L4) {
+            const uint32_t pl = pass2(lo16(C4), lo16(D4), lo16(R4), lo16(U4), lo16(L4));
+            const uint32_t ph = pass2(hi16(C4), hi16(D4), hi16(R4), hi16(U4), hi16(L4));
+            return (pl & 1u) | ((pl >> 15) & 2u) | ((ph & 1u) << 2) | ((ph >> 13) & 8u);
+        };
+        // item -> (row, octet): one division here, then a fixed (row, octet) step of 64 items per round
+        int r = lane / no, o = lane - (lane / no) * no;
+        const int dr = 64 / no, dq = 64 - dr * no;
         for (int i0 = 0; i0 < nitems; i0 += 64) {
             const int it = i0 + lane;
             unsigned bits = 0;
             if (it < nitems) {
                 const uint32_t* rc = wrow + (r + 3) * wsw;
-                const uint32_t L4 = ext(rc, q, shift), C4 = ext(rc, q, oc), R4 = ext(rc, q, orr);
-                const uint32_t U4 = ext(rc - 3 * wsw, q, oc), D4 = ext(rc + 3 * wsw, q, oc);
-                const uint32_t pl = __builtin_bit_cast(uint32_t, pass2(lo16(C4), lo16(D4), lo16(R4), lo16(U4), lo16(L4)));
-                const uint32_t ph = __builtin_bit_cast(uint32_t, pass2(hi16(C4), hi16(D4), hi16(R4), hi16(U4), hi16(L4)));
-                bits = (pl & 1u) | ((pl >> 15) & 2u) | ((ph & 1u) << 2) | ((ph >> 13) & 8u);
-                const int rem = dw - 4 * q;  // pixels of this quad inside the detectable row
-                if (rem < 4) bits &= (1u << rem) - 1u;
+                uint32_t L0, L1, C0, C1, R0, R1, U0, U1, D0, D1;
+                ext8(rc, o, shift, L0, L1);
+                ext8(rc, o, shift + 3, C0, C1);
+                ext8(rc, o, shift + 6, R0, R1);
+                ext8(rc - 3 * wsw, o, shift + 3, U0, U1);
+                ext8(rc + 3 * wsw, o, shift + 3, D0, D1);
+                bits = quad_bits(C0, D0, R0, U0, L0) | (quad_bits(C1, D1, R1, U1, L1) << 4);
+                const int rem = dw - 8 * o;  // pixels of this octet inside the detectable row
+                if (rem < 8) bits &= (1u << rem) - 1u;
             }
-            const int row = r, quad = q;
-            q += dq;
+            const int row = r, oct = o;
+            o += dq;
             r += dr;
-            if (q >= nq) { q -= nq; ++r; }
+            if (o >= no) { o -= no; ++r; }
             const int cnt = __popc(bits);
             const int incl = wave_incl_scan_dpp(cnt);
             int pos = nlist + incl - cnt;
-            const int base_idx = (row + 3) * ws + 4 * quad + 3;
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (bits >> k & 1u) cl[pos++] = (uint16_t)(base_idx + k);
+            const int base_idx = (row + 3) * ws + 8 * oct + 3;
+            while (bits) {
+                const int k = __builtin_ctz(bits);
+                bits &= bits - 1u;
+                cl[pos++] = (uint16_t)(base_idx + k);
+            }
             nlist += __builtin_amdgcn_readlane(incl, 63);
         }
     }
