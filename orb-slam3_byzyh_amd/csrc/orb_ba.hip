@@ -1896,6 +1896,10 @@ struct orb_ba_s {
     LmState* h_lm = nullptr;   // pinned staging of the initial state
     LmProgress* h_prog = nullptr;  // pinned, written by k_lm_trial_done
     hipEvent_t unit_ev[2] = {nullptr, nullptr};
+    // the LM unit (7 launches) captured as a HIP graph, reused while its launch arguments are unchanged
+    hipGraph_t unit_graph = nullptr;
+    hipGraphExec_t unit_exec = nullptr;
+    std::vector<uintptr_t> unit_key;
     float ms_total = 0;
     // multi-GPU: ranks own landmark ranges; partial sums are all-reduced
     int world = 1, rank = 0;
@@ -1976,6 +1980,8 @@ int orb_ba_destroy(orb_ba_t h) {
     if (h->h_prog) hipHostFree(h->h_prog);
     for (hipEvent_t e : h->unit_ev)
         if (e) hipEventDestroy(e);
+    if (h->unit_exec) hipGraphExecDestroy(h->unit_exec);
+    if (h->unit_graph) hipGraphDestroy(h->unit_graph);
     h->trace.release();
     if (h->h_scal) hipHostFree(h->h_scal);
     if (h->h_red) hipHostFree(h->h_red);
@@ -2494,7 +2500,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         // one unit = 7 launches: edges+linearise, reductions (+ chi2, max diag, build controller),
         // Schur edges, Schur blocks + rhs, Cholesky + solves, back-substitution + update, errors at
         // the new estimate (+ chi2, computeScale, trial controller)
-        auto unit = [&](int u) -> bool {
+        auto unit_launches = [&]() {
             hipLaunchKernelGGL(k_u_edges_build, dim3(nparts), dim3(kT), 0, s, ne, h->edges.p, h->cams.p, h->pose.p,
                                h->point.p, h->pose_h.p, hub, h->err.p, h->rho0.p, h->ecl.p, h->hpl.p, h->ecp.p,
                                h->part.p, (const LmState*)L);
@@ -2533,6 +2539,52 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
             hipLaunchKernelGGL(k_u_edges_trial, dim3(nparts), dim3(kT), 0, s, ne, h->edges.p, h->cams.p, h->pose.p,
                                h->point.p, h->pose_h.p, hub, h->err.p, h->rho0.p, h->part.p, h->counters.p + 1, n + m,
                                h->x.p, h->b.p, h->status.p, h->scal.p, L, h->h_prog);
+        };
+        // Every unit launches the same kernels with the same arguments (the device state gates them),
+        // so the unit is captured once as a graph and replayed: one graph launch instead of 7 kernel
+        // launches per trial.  The capture is kept while the arguments (sizes, buffers) are unchanged.
+        static const bool no_graph = getenv("ORBGPU_BA_NO_GRAPH") != nullptr;
+        auto dbits = [](double v) { uintptr_t u; memcpy(&u, &v, sizeof(u)); return u; };
+        bool use_graph = !no_graph && !getenv("ORBGPU_BA_TRACE");
+        if (use_graph) {
+            const std::vector<uintptr_t> key = {
+                (uintptr_t)s, (uintptr_t)n, (uintptr_t)m, (uintptr_t)ne, (uintptr_t)nf, (uintptr_t)nl, (uintptr_t)nfe,
+                (uintptr_t)nblk, (uintptr_t)nparts, (uintptr_t)chol_v1, dbits(hub.delta_mono), dbits(hub.delta_stereo), (uintptr_t)bl,
+                (uintptr_t)h->edges.p, (uintptr_t)h->cams.p, (uintptr_t)h->pose.p, (uintptr_t)h->point.p,
+                (uintptr_t)h->pose_h.p, (uintptr_t)h->err.p, (uintptr_t)h->rho0.p, (uintptr_t)h->ecl.p,
+                (uintptr_t)h->hpl.p, (uintptr_t)h->ecp.p, (uintptr_t)h->part.p, (uintptr_t)h->pose_off.p,
+                (uintptr_t)h->pose_edge.p, (uintptr_t)h->hpp.p, (uintptr_t)h->b.p, (uintptr_t)h->land_off.p,
+                (uintptr_t)h->land_edge.p, (uintptr_t)h->hll.p, (uintptr_t)h->counters.p, (uintptr_t)h->scal.p,
+                (uintptr_t)L, (uintptr_t)lam, (uintptr_t)h->landf_edge.p, (uintptr_t)h->fland.p, (uintptr_t)h->z.p,
+                (uintptr_t)h->cb.p, (uintptr_t)h->blk_i.p, (uintptr_t)h->blk_j.p, (uintptr_t)h->blk_off.p,
+                (uintptr_t)h->pair_a.p, (uintptr_t)h->pair_b.p, (uintptr_t)h->S.p, (uintptr_t)h->bs.p,
+                (uintptr_t)h->x.p, (uintptr_t)h->status.p, (uintptr_t)h->landf_off.p, (uintptr_t)h->free_pose.p,
+                (uintptr_t)h->land_point.p, (uintptr_t)h->pose_bak.p, (uintptr_t)h->point_bak.p, (uintptr_t)h->h_prog};
+            if (!h->unit_exec || key != h->unit_key) {
+                if (h->unit_exec) { hipGraphExecDestroy(h->unit_exec); h->unit_exec = nullptr; }
+                if (h->unit_graph) { hipGraphDestroy(h->unit_graph); h->unit_graph = nullptr; }
+                bool ok = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess;
+                if (ok) {
+                    unit_launches();
+                    ok = hipStreamEndCapture(s, &h->unit_graph) == hipSuccess && h->unit_graph &&
+                         hipGraphInstantiate(&h->unit_exec, h->unit_graph, nullptr, nullptr, 0) == hipSuccess;
+                }
+                if (!ok) {  // fall back to direct launches
+                    (void)hipGetLastError();
+                    if (h->unit_graph) { hipGraphDestroy(h->unit_graph); h->unit_graph = nullptr; }
+                    h->unit_exec = nullptr;
+                    use_graph = false;
+                } else {
+                    h->unit_key = key;
+                }
+            }
+        }
+        auto unit = [&](int u) -> bool {
+            if (use_graph) {
+                if (hipGraphLaunch(h->unit_exec, s) != hipSuccess) return false;
+            } else {
+                unit_launches();
+            }
             return hipEventRecord(h->unit_ev[u & 1], s) == hipSuccess;
         };
         const int max_units = std::max(0, opt->iterations) * 10;
