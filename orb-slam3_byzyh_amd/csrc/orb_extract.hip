@@ -2056,8 +2056,8 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
         const int c0 = (int)__builtin_rintf(__builtin_fmaf(px0, a, -(py0 * b)));
         const int r1 = (int)__builtin_rintf(__builtin_fmaf(px1, b, py1 * a));
         const int c1 = (int)__builtin_rintf(__builtin_fmaf(px1, a, -(py1 * b)));
-        t0[m] = PB[r0 * (kPBW * 4) + c0];
-        t1[m] = PB[r1 * (kPBW * 4) + c1];
+        t0[m] = PB[__mul24(r0, kPBW * 4) + c0];  // |r| <= 18: 24-bit multiply (full rate)
+        t1[m] = PB[__mul24(r1, kPBW * 4) + c1];
     }
     uint32_t words[8];
 #pragma unroll
