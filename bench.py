@@ -371,30 +371,34 @@ def bench_single_frame(pkg, synth, cpu_baseline_on, reps=50):
     return out
 
 
-def bench_c4(pkg, synth, dev, steps, n_frames=32):
+def bench_c4(pkg, synth, dev, steps, n_frames=32, in_flight=2):
     """C4's per-GPU shard: 32 frames of 1280x720 (nFeatures 1000) per step, device-resident (the
-    8-GPU run all-gathers the features of every shard; see the main line's N > 1 path)."""
+    8-GPU run all-gathers the features of every shard; see the main line's N > 1 path), with
+    `in_flight` extractor handles taking the steps in turn on their own streams (as the main line)."""
     import numpy as np
     import torch
     frames = np.stack([synth.polygon_frame(1280, 720, seed=1000 + i) for i in range(n_frames)])
     imgs = torch.from_numpy(frames).to(dev)
-    ex = pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=1280, max_height=720, max_batch=n_frames)
+    H = max(1, in_flight)
+    exs = [pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=1280, max_height=720, max_batch=n_frames)
+           for _ in range(H)]
     cap = 1000 + 16 * 8
-    out = (torch.empty((n_frames, cap, 7), dtype=torch.float32, device=dev),
-           torch.empty((n_frames, cap, 32), dtype=torch.uint8, device=dev),
-           torch.empty((n_frames, 2), dtype=torch.int32, device=dev))
-    st = torch.cuda.current_stream(dev)
-    for _ in range(3):
-        ex.extract_batch_device(imgs, (0, 1000), cap=cap, out=out, stream=st)
+    outs = [(torch.empty((n_frames, cap, 7), dtype=torch.float32, device=dev),
+             torch.empty((n_frames, cap, 32), dtype=torch.uint8, device=dev),
+             torch.empty((n_frames, 2), dtype=torch.int32, device=dev)) for _ in range(H)]
+    sts = [torch.cuda.current_stream(dev)] if H == 1 else [torch.cuda.Stream(dev) for _ in range(H)]
+    for i in range(3 * H):
+        exs[i % H].extract_batch_device(imgs, (0, 1000), cap=cap, out=outs[i % H], stream=sts[i % H])
     torch.cuda.synchronize(dev)
-    nfeat = int(out[2][:, 0].sum().item())
+    nfeat = int(outs[0][2][:, 0].sum().item())
     reps = max(5, min(steps, 20))
     t0 = time.perf_counter()
-    for _ in range(reps):
-        ex.extract_batch_device(imgs, (0, 1000), cap=cap, out=out, stream=st)
+    for i in range(reps):
+        exs[i % H].extract_batch_device(imgs, (0, 1000), cap=cap, out=outs[i % H], stream=sts[i % H])
     torch.cuda.synchronize(dev)
     dt = (time.perf_counter() - t0) * 1e3
-    return {"config": f"C4 shard: {n_frames} synthetic 1280x720 frames per GPU per step, nFeatures 1000, 8 levels",
+    return {"config": f"C4 shard: {n_frames} synthetic 1280x720 frames per GPU per step, nFeatures 1000, 8 levels, "
+                      f"{H} batches in flight",
             "features_per_ms": round(nfeat * reps / dt, 3), "frames_per_ms": round(n_frames * reps / dt, 3),
             "ms_per_step": round(dt / reps, 4)}
 
@@ -619,7 +623,7 @@ def main():
     c4 = None
     if not args.no_c4 and world == 1:
         try:
-            c4 = bench_c4(pkg, synth, dev, args.steps)
+            c4 = bench_c4(pkg, synth, dev, args.steps, in_flight=H)
         except Exception as e:  # noqa: BLE001
             c4 = {"error": repr(e)}
     if rank == 0:
