@@ -212,7 +212,10 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
                                                           uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                                           const int2* __restrict__ xtab, const int4* __restrict__ ytab,
                                                           const int4* __restrict__ tiletab,
-                                                          unsigned long long* __restrict__ stamps) {
+                                                          unsigned long long* __restrict__ stamps,
+                                                          int* __restrict__ status_reset) {
+    // level 0 clears the batch's error status (read after the quad-tree), instead of a memset launch
+    if (kLevel0 && status_reset && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *status_reset = 0;
     // blockIdx.y = frame; blockIdx.x -> tile of the frame, XCD-chunked (xcd_tile)
     const int t = xcd_tile(blockIdx.x, A.share);
     if (t >= A.tiles_per_frame) return;
@@ -2117,6 +2120,7 @@ struct Extractor {
     int32_t* d_sel_count = nullptr; size_t selcount_cap = 0;
     int32_t* d_lap_count = nullptr; size_t lapcount_cap = 0;
     int* d_status = nullptr;
+    bool clear_status_l0 = false;  // this batch's level-0 launch clears d_status (see launch_batch)
     // synchronous path staging
     uint8_t* d_img = nullptr; size_t img_cap = 0;
     orb_keypoint_t* d_kps = nullptr; uint8_t* d_desc = nullptr; int32_t* d_counts = nullptr; size_t out_cap = 0;
@@ -2599,13 +2603,14 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
         }
         if (l == 0)
             hipLaunchKernelGGL(k_pyramid_level<true>, grid, dim3(256), 0, st, A, imgs, (long long)frame_stride, stride,
-                               pyr, blr, e->d_xtab, e->d_ytab, e->d_tiletab, stamps);
+                               pyr, blr, e->d_xtab, e->d_ytab, e->d_tiletab, stamps,
+                               e->clear_status_l0 && f0 == 0 ? e->d_status : nullptr);
         else if (4 * k.lv[l - 1].w <= 5 * L.w && 4 * k.lv[l - 1].h <= 5 * L.h)  // level ratio <= 1.25
             hipLaunchKernelGGL((k_pyramid_level<false, kSmallBoxH, kSmallBoxW>), grid, dim3(256), 0, st, A, nullptr,
-                               0LL, 0, pyr, blr, e->d_xtab, e->d_ytab, e->d_tiletab, stamps);
+                               0LL, 0, pyr, blr, e->d_xtab, e->d_ytab, e->d_tiletab, stamps, nullptr);
         else
             hipLaunchKernelGGL((k_pyramid_level<false, kBoxH, kBoxW>), grid, dim3(256), 0, st, A, nullptr, 0LL, 0, pyr,
-                               blr, e->d_xtab, e->d_ytab, e->d_tiletab, stamps);
+                               blr, e->d_xtab, e->d_ytab, e->d_tiletab, stamps, nullptr);
         if (stamps && pyr_stamps) {  // debug: phase clocks of this level's blocks
             std::vector<unsigned long long> hst((size_t)8 * nblk);
             (void)hipStreamSynchronize(st);
@@ -2672,7 +2677,11 @@ int launch_batch(Extractor* e, const uint8_t* d_images, int n, int w, int h, int
                  int lap0, int lap1, orb_keypoint_t* d_kps, uint8_t* d_desc, int cap, int32_t* d_counts,
                  hipStream_t st) {
     (void)w; (void)h;
-    hipMemsetAsync(e->d_status, 0, sizeof(int), st);
+    // the level-0 pyramid launch of the first (sub-)batch clears the status; the band path has no
+    // level-0 launch when it builds every level, and sub-batches on several streams need it cleared
+    // before the fork
+    e->clear_status_l0 = !(e->band_mode || (e->nstreams > 1 && (n + e->chunk - 1) / e->chunk > 1));
+    if (!e->clear_status_l0) hipMemsetAsync(e->d_status, 0, sizeof(int), st);
     const int nchunks = (n + e->chunk - 1) / e->chunk;
     if (nchunks <= 1 || e->nstreams <= 1) {
         const int rc = launch_chunk(e, 0, d_images, n, stride, frame_stride, lap0, lap1, d_kps, d_desc, cap, d_counts, st);
