@@ -240,3 +240,21 @@ def test_quadtree_node_sort_emulations(pkg, oracle):
             used_reg += rc
             assert np.array_equal(out, exp), (len(c), mode, c.tolist(), x.tolist())
     assert used_reg > 200  # the register version ran for most of the n <= 64 cases
+
+
+def test_sparse_corners_parity(pkg, oracle):
+    """Few corners per level: the quad-tree stops because no node can be split further (src:912-918,
+    nodes == prevSize) rather than at N, single-key roots and levels with one or no candidate."""
+    rng = np.random.default_rng(31)
+    for n_rect in (1, 3, 12):
+        img = np.full((480, 640), 90, np.uint8)
+        for _ in range(n_rect):
+            x0, y0 = int(rng.integers(40, 560)), int(rng.integers(40, 400))
+            img[y0:y0 + int(rng.integers(12, 60)), x0:x0 + int(rng.integers(12, 60))] = int(rng.integers(150, 255))
+        ex = pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=640, max_height=480)
+        kps, desc, mono = ex(img, None, (0, 1000))
+        rkps, rdesc, rmono = oracle.OracleExtractor(1000, 1.2, 8, 20, 7)(img, (0, 1000))
+        assert ex._lib.orb_debug_status(ex._h) == 0
+        assert mono == rmono and len(kps) == len(rkps) > 0, n_rect
+        assert np.array_equal(kps.view(np.uint8), rkps.view(np.uint8)), n_rect
+        assert np.array_equal(desc, rdesc), n_rect
