@@ -2256,17 +2256,23 @@ int prepare(Extractor* e, int w, int h, int n) {
         if (hipMemcpy(e->d_tiletab, tt.data(), tt.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess)
             return orbgpu_fail(ORB_ERR_DEVICE, "table upload failed");
         e->geo_ok = true;
-        // quad-tree LDS: node metadata of the largest level + room for ~7k keys (80 KB: two
-        // workgroups per CU); larger feature budgets (e.g. the 5x monocular-init extractor) get more
+        // quad-tree LDS: node metadata of the largest level (larger feature budgets, e.g. the 5x
+        // monocular-init extractor, need more) + key room
         size_t meta = 0;
         for (int l = 0; l < g.k.nlevels; ++l) {
             const int lcap = g.k.lv[l].sel_cap + 64;
             meta = std::max(meta, (qt2_meta_bytes(lcap) + 15) & ~(size_t)15);
         }
-        const size_t want = std::max<size_t>(80 * 1024, meta + 32 * 1024);
+        // node tables + room for the keys of a typical level (6 B per key); levels with more keys use
+        // the global scratch.  Kept small: the quad-tree blocks are long-lived and latency-bound, and
+        // the LDS they do not hold lets another batch's FAST / pyramid / describe blocks share the CU.
+        static const int qt_key_kb = getenv("ORBGPU_QT_KEY_KB") ? atoi(getenv("ORBGPU_QT_KEY_KB")) : 12;
+        const size_t want = meta + (size_t)std::max(qt_key_kb, 1) * 1024;
         if (meta > 160 * 1024) return orbgpu_fail(ORB_ERR_ARG, "nfeatures too large for the quad-tree LDS budget");
         e->qt_lds = (int)std::min<size_t>(want, 160 * 1024);
-        if (hipFuncSetAttribute((const void*)k_quadtree_kp, hipFuncAttributeMaxDynamicSharedMemorySize, e->qt_lds) !=
+        // the attribute is per function (shared by every handle): allow the whole LDS, each launch
+        // requests its handle's qt_lds
+        if (hipFuncSetAttribute((const void*)k_quadtree_kp, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
             hipSuccess)
             return orbgpu_fail(ORB_ERR_DEVICE, "cannot raise the quad-tree LDS limit");
     }
@@ -2721,13 +2727,13 @@ int orb_extractor_create(const orb_params_t* p, int max_width, int max_height, i
     e->max_w = max_width;
     e->max_h = max_height;
     e->max_batch = max_batch;
-    e->qt_lds = 80 * 1024;
+    e->qt_lds = 64 * 1024;  // set per frame size in prepare()
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&e->d_status, sizeof(int)) != hipSuccess) {
         delete e;
         return orbgpu_fail(ORB_ERR_DEVICE, "stream/status allocation failed");
     }
-    hipFuncSetAttribute((const void*)k_quadtree_kp, hipFuncAttributeMaxDynamicSharedMemorySize, e->qt_lds);
+    hipFuncSetAttribute((const void*)k_quadtree_kp, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (const char* c = getenv("ORBGPU_CHUNK")) e->chunk = std::max(1, atoi(c));
     if (const char* c = getenv("ORBGPU_STREAMS")) e->nstreams = std::min(Extractor::kMaxStreams, std::max(1, atoi(c)));
     if (const char* c = getenv("ORBGPU_FAST_SPLIT")) e->fast_split = atoi(c);
