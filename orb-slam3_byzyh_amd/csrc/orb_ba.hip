@@ -596,7 +596,7 @@ __global__ __launch_bounds__(kCholThreads) void k_ba_chol(int n, const double* _
 // in order of decreasing column, so the active tiles of every step are a prefix of each wave's
 // slots and the load stays balanced as the trailing matrix shrinks.  Every sum has a fixed order.
 typedef double f64x4 __attribute__((ext_vector_type(4)));
-constexpr int kMfTileWaves = 7, kMfMaxNT = 18;
+constexpr int kMfTileWaves = 7, kMf2TileWaves = 11, kMfMaxNT = 18;
 constexpr size_t kMfLds =
     sizeof(double) * (2 * (size_t)kMfMaxNT * 256 + 16 * 17 + 2 * 16 * kMfMaxNT + 16 * kMfMaxNT * (kMfMaxNT - 1) / 2);
 
@@ -640,7 +640,30 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
 // above the diagonal collect garbage that is never read.
 // kColMajor: L^-1 stored column-major with stride 17 (L^-1[i][c] at c * 17 + i: conflict-free for the
 // writes here and for every reader); otherwise in the MFMA operand layout.
-template <bool kColMajor = false>
+// Lane j of each 16-lane row, broadcast to the whole row (DPP row_newbcast): a VALU move, no SGPR
+// round trip (v_readlane + wait states) and no SGPR pressure.  j must fold to a constant.
+__device__ __forceinline__ double row_bcast16(double v, int j) {
+    const uint64_t u = __double_as_longlong(v);
+    const int lo = (int)(uint32_t)u, hi = (int)(uint32_t)(u >> 32);
+    int rl = 0, rh = 0;
+    switch (j) {
+#define MF_RB(J)                                                              \
+    case J:                                                                   \
+        rl = __builtin_amdgcn_update_dpp(0, lo, 0x150 + J, 0xf, 0xf, false); \
+        rh = __builtin_amdgcn_update_dpp(0, hi, 0x150 + J, 0xf, 0xf, false); \
+        break;
+        MF_RB(0) MF_RB(1) MF_RB(2) MF_RB(3) MF_RB(4) MF_RB(5) MF_RB(6) MF_RB(7)
+        MF_RB(8) MF_RB(9) MF_RB(10) MF_RB(11) MF_RB(12) MF_RB(13) MF_RB(14) MF_RB(15)
+#undef MF_RB
+        default: break;
+    }
+    return __longlong_as_double(((uint64_t)(uint32_t)rh << 32) | (uint32_t)rl);
+}
+
+// kDpp: the column values L[j][c] reach the other rows by DPP row broadcasts (every 16-lane row
+// holds the same block, so each row broadcasts within itself); otherwise by v_readlane.  Same
+// arithmetic, same results.
+template <bool kColMajor = false, bool kDpp = false>
 __device__ __forceinline__ void mf_diag(double* __restrict__ dk, double* __restrict__ linv_k,
                                         double* __restrict__ yk, int lane, int* fail, int64_t* tr = nullptr) {
     if (tr && lane == 0) tr[0] = clock64();
@@ -654,18 +677,20 @@ __device__ __forceinline__ void mf_diag(double* __restrict__ dk, double* __restr
     bool bad = false;
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
-        const double piv = readlane_d(row[c], c);
+        const double piv = kDpp ? row_bcast16(row[c], c) : readlane_d(row[c], c);
         bad |= !(piv > 0.0);
         const double inv = rsqrt_nr(piv);  // 1 / L[c][c]
         const double lrc = row[c] * inv;    // L[r][c] for r > c
         xc[c] *= inv;                       // x_c of column r of L^-1
 #pragma unroll
         for (int j = c + 1; j < 16; ++j) {
-            const double ljc = readlane_d(lrc, j);
+            const double ljc = kDpp ? row_bcast16(lrc, j) : readlane_d(lrc, j);
             row[j] = __builtin_fma(-lrc, ljc, row[j]);
             xc[j] = __builtin_fma(-ljc, xc[c], xc[j]);
+            if (kDpp) asm volatile("" : "+v"(row[j]), "+v"(xc[j]));  // computed here: one broadcast live at a time
         }
     }
+    if (kDpp) bad = __ballot(bad) != 0;
     if (lane == 0 && bad) *fail = 1;
     if (tr && lane == 0) tr[1] = clock64();
     if (lane < 16) {
@@ -915,7 +940,7 @@ __device__ __forceinline__ void lds_flag_wait(int* f, int target, int lane, int*
     }
 }
 
-template <int W>
+template <int W, bool kDpp = true>
 __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const double* __restrict__ S,
                                                               const double* __restrict__ b, double* __restrict__ x,
                                                               int32_t* __restrict__ status, int64_t* __restrict__ trace,
@@ -956,7 +981,7 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
             dk[r * 17 + c] = (r < n && c < n) ? S[(size_t)r * n + c] : (r == c ? 1.0 : 0.0);
         }
         mf_wave_sync();
-        mf_diag<true>(dk, linv, yv, lane, &fail);
+        mf_diag<true, kDpp>(dk, linv, yv, lane, &fail);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) __hip_atomic_store(&lk, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         for (int k = 0; k + 1 < NT; ++k) {
@@ -984,35 +1009,85 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
             part += __shfl_xor(part, 32);
             if (lane < 16) yv[16 * (k + 1) + lane] -= part;  // b_{k+1} -= L_{k+1,k} y_k
             mf_wave_sync();
-            mf_diag<true>(dk, linv + (k + 1) * 272, yv + 16 * (k + 1), lane, &fail, trace ? trace + 700 + 4 * k : nullptr);
+            mf_diag<true, kDpp>(dk, linv + (k + 1) * 272, yv + 16 * (k + 1), lane, &fail, trace ? trace + 700 + 4 * k : nullptr);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_store(&lk, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (trace && lane == 0) trace[(k * 8 + W) * 4 + 3] = clock64();
         }
         // backward: x_j = L_jj^-T (y_j - sum_{k >= j+2} c_kj - L_{j+1,j}^T x_{j+1})
-        for (int j = NT - 1; j >= 0; --j) {
-            if (trace && lane == 0) trace[600 + j] = clock64();
-            lds_flag_wait(&cnt[j], NT - 2 - j, lane, &fail, 3);
-            double yj = yv[16 * j + r16];
-            for (int kk = NT - 1; kk >= j + 2; --kk) yj -= contrib[(kk * (kk - 1) / 2 + j) * 16 + r16];
-            if (j + 1 < NT) {
+        if (kDpp) {
+            // The chain x_{j+1} -> x_j stays in registers: x_{j+1} and y_j reach the other lanes of a
+            // row by DPP broadcasts, and both 16x16 operands (L_{j+1,j} row r, L_jj^-1 column r) are
+            // loaded before the wait for the contributions.  Same operations and order as below.
+            double xn = 0.0;  // x_{j+1}[r16]
+            for (int j = NT - 1; j >= 0; --j) {
+                if (trace && lane == 0) trace[600 + j] = clock64();
                 const double* L = sub + j * 256;  // L_{j+1,j}[r][c] at [(c >> 2) * 64 + r + 16 (c & 3)]
-                double t4[4] = {0.0, 0.0, 0.0, 0.0};
+                const double* lj = linv + j * 272;
+                double lr[16], li[16];
 #pragma unroll
-                for (int rr = 0; rr < 16; ++rr)
-                    t4[rr & 3] = __builtin_fma(L[(r16 >> 2) * 64 + rr + 16 * (r16 & 3)], xv[16 * (j + 1) + rr], t4[rr & 3]);
-                yj -= (t4[0] + t4[1]) + (t4[2] + t4[3]);
+                for (int rr = 0; rr < 16; ++rr) {
+                    lr[rr] = j + 1 < NT ? L[(r16 >> 2) * 64 + rr + 16 * (r16 & 3)] : 0.0;
+                    li[rr] = lj[r16 * 17 + rr];
+                }
+                lds_flag_wait(&cnt[j], NT - 2 - j, lane, &fail, 3);
+                if (trace && lane == 0) trace[800 + j] = clock64();
+                double yj = yv[16 * j + r16];
+                {  // every contribution load issued at once, subtracted in the same order (kk descending);
+                   // the missing ones are +0.0, which leaves yj unchanged bit for bit
+                    double cv[kMfMaxNT];
+#pragma unroll
+                    for (int m = 0; m < kMfMaxNT; ++m) {
+                        const int kk = NT - 1 - m;
+                        const bool have = kk >= j + 2;  // (load unconditionally from a valid slot: no branch per load)
+                        const double v = contrib[(have ? kk * (kk - 1) / 2 + j : 0) * 16 + r16];
+                        cv[m] = have ? v : 0.0;
+                    }
+#pragma unroll
+                    for (int m = 0; m < kMfMaxNT; ++m) yj -= cv[m];
+                }
+                if (j + 1 < NT) {
+                    double t4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                    for (int rr = 0; rr < 16; ++rr) t4[rr & 3] = __builtin_fma(lr[rr], row_bcast16(xn, rr), t4[rr & 3]);
+                    yj -= (t4[0] + t4[1]) + (t4[2] + t4[3]);
+                }
+                double v4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int rr = 0; rr < 16; ++rr) v4[rr & 3] = __builtin_fma(li[rr], row_bcast16(yj, rr), v4[rr & 3]);
+                xn = (v4[0] + v4[1]) + (v4[2] + v4[3]);
+                if (lane < 16) xv[16 * j + r16] = xn;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0) __hip_atomic_store(&xready, NT - j, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (trace && lane == 0) trace[830 + j] = clock64();
             }
-            mf_wave_sync();
-            if (lane < 16) yv[16 * j + r16] = yj;
-            mf_wave_sync();
-            const double* lj = linv + j * 272;
-            double v4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int rr = 0; rr < 16; ++rr) v4[rr & 3] = __builtin_fma(lj[r16 * 17 + rr], yv[16 * j + rr], v4[rr & 3]);
-            if (lane < 16) xv[16 * j + r16] = (v4[0] + v4[1]) + (v4[2] + v4[3]);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (lane == 0) __hip_atomic_store(&xready, NT - j, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+            for (int j = NT - 1; j >= 0; --j) {
+                if (trace && lane == 0) trace[600 + j] = clock64();
+                lds_flag_wait(&cnt[j], NT - 2 - j, lane, &fail, 3);
+                if (trace && lane == 0) trace[800 + j] = clock64();
+                double yj = yv[16 * j + r16];
+                for (int kk = NT - 1; kk >= j + 2; --kk) yj -= contrib[(kk * (kk - 1) / 2 + j) * 16 + r16];
+                if (j + 1 < NT) {
+                    const double* L = sub + j * 256;  // L_{j+1,j}[r][c] at [(c >> 2) * 64 + r + 16 (c & 3)]
+                    double t4[4] = {0.0, 0.0, 0.0, 0.0};
+    #pragma unroll
+                    for (int rr = 0; rr < 16; ++rr)
+                        t4[rr & 3] = __builtin_fma(L[(r16 >> 2) * 64 + rr + 16 * (r16 & 3)], xv[16 * (j + 1) + rr], t4[rr & 3]);
+                    yj -= (t4[0] + t4[1]) + (t4[2] + t4[3]);
+                }
+                mf_wave_sync();
+                if (lane < 16) yv[16 * j + r16] = yj;
+                mf_wave_sync();
+                const double* lj = linv + j * 272;
+                double v4[4] = {0.0, 0.0, 0.0, 0.0};
+    #pragma unroll
+                for (int rr = 0; rr < 16; ++rr) v4[rr & 3] = __builtin_fma(lj[r16 * 17 + rr], yv[16 * j + rr], v4[rr & 3]);
+                if (lane < 16) xv[16 * j + r16] = (v4[0] + v4[1]) + (v4[2] + v4[3]);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0) __hip_atomic_store(&xready, NT - j, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (trace && lane == 0) trace[830 + j] = clock64();
+            }
         }
     } else {
         // ---------------- tile waves: slot s holds tile t = s W + w (packed i | j << 8) ----------------
@@ -1147,7 +1222,7 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
         for (int k = NT - 1; k >= 2; --k) {
             bool waited = false;
             double xr = 0.0;
-            for (int j = 0; j + 2 <= k; ++j) {
+            for (int j = k - 2; j >= 0; --j) {  // (k, k-2) first: block k-2 needs it soonest
                 const int t = Tc(j) + (k - j);
                 if (t % W != w) continue;
                 if (!waited) {
@@ -2002,7 +2077,8 @@ void dump_chol_trace(const int64_t* tr, int n, hipStream_t s) {
         for (int w = 0; w <= kMfTileWaves; ++w)
             fprintf(stderr, "MFTRACE k=%d w=%d %lld %lld %lld %lld\n", k, w, rel((k * 8 + w) * 4),
                     rel((k * 8 + w) * 4 + 1), rel((k * 8 + w) * 4 + 2), rel((k * 8 + w) * 4 + 3));
-    for (int k = NT - 1; k >= 0; --k) fprintf(stderr, "MFTRACE back k=%d %lld\n", k, rel(600 + k));
+    for (int k = NT - 1; k >= 0; --k)
+        fprintf(stderr, "MFTRACE back k=%d %lld waited %lld published %lld\n", k, rel(600 + k), rel(800 + k), rel(830 + k));
     fprintf(stderr, "MFTRACE end %lld\n", rel(640));
     for (int k = 0; k + 1 < NT; ++k)
         fprintf(stderr, "MFTRACE diag k=%d factor %lld linv %lld y %lld\n", k, (long long)(ht[701 + 4 * k] - ht[700 + 4 * k]),
@@ -2355,10 +2431,31 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         return orbgpu_fail(ORB_ERR_ARG, "too many free keyframes for the on-chip Cholesky");
     const bool use_mf = !coop_nb && n <= 16 * kMfMaxNT && !getenv("ORBGPU_BA_CHOL_LDS");
     const bool chol_v1 = getenv("ORBGPU_BA_CHOL_V1") != nullptr;
+    // v2 Cholesky shape: 11 tile waves + the diagonal wave (3 waves per SIMD: 2.20 -> 2.14 ms per C5
+    // solve against 7 + 1); ORBGPU_BA_MF_W=7 selects the 8-wave kernel
+    static const int mf_w = getenv("ORBGPU_BA_MF_W") ? atoi(getenv("ORBGPU_BA_MF_W")) : kMf2TileWaves;
+    static const bool diag_readlane = getenv("ORBGPU_BA_DIAG_READLANE") != nullptr;
+    auto launch_mf2 = [&](int64_t* tr, const LmState* g) {
+        if (mf_w == 11 && !diag_readlane)
+            hipLaunchKernelGGL((k_ba_chol_mf2<11, true>), dim3(1), dim3(12 * 64), kMf2Lds, s, n, h->S.p, h->bs.p, h->x.p,
+                               h->status.p, tr, g, (int)kGateTrial);
+        else if (mf_w == 11)
+            hipLaunchKernelGGL((k_ba_chol_mf2<11, false>), dim3(1), dim3(12 * 64), kMf2Lds, s, n, h->S.p, h->bs.p, h->x.p,
+                               h->status.p, tr, g, (int)kGateTrial);
+        else if (!diag_readlane)
+            hipLaunchKernelGGL((k_ba_chol_mf2<kMfTileWaves, true>), dim3(1), dim3((kMfTileWaves + 1) * 64), kMf2Lds, s, n,
+                               h->S.p, h->bs.p, h->x.p, h->status.p, tr, g, (int)kGateTrial);
+        else
+            hipLaunchKernelGGL((k_ba_chol_mf2<kMfTileWaves, false>), dim3(1), dim3((kMfTileWaves + 1) * 64), kMf2Lds, s,
+                               n, h->S.p, h->bs.p, h->x.p, h->status.p, tr, g, (int)kGateTrial);
+    };
     static bool attr_set = false;
     if (!attr_set) {
         hipFuncSetAttribute((const void*)k_ba_chol_mfma<kMfTileWaves>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMfLds);
         hipFuncSetAttribute((const void*)k_ba_chol_mf2<kMfTileWaves>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMf2Lds);
+        hipFuncSetAttribute((const void*)k_ba_chol_mf2<11>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMf2Lds);
+        hipFuncSetAttribute((const void*)k_ba_chol_mf2<11, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMf2Lds);
+        hipFuncSetAttribute((const void*)k_ba_chol_mf2<kMfTileWaves, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMf2Lds);
         hipFuncSetAttribute((const void*)k_ba_chol<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
         hipFuncSetAttribute((const void*)k_ba_chol<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
         (void)hipGetLastError();
@@ -2434,8 +2531,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                     hipLaunchKernelGGL(k_ba_chol_mfma<kMfTileWaves>, dim3(1), dim3((kMfTileWaves + 1) * 64), kMfLds, s,
                                        n, h->S.p, h->bs.p, h->x.p, h->status.p, tr, G, (int)kGateTrial);
                 else
-                    hipLaunchKernelGGL(k_ba_chol_mf2<kMfTileWaves>, dim3(1), dim3((kMfTileWaves + 1) * 64), kMf2Lds, s,
-                                       n, h->S.p, h->bs.p, h->x.p, h->status.p, tr, G, (int)kGateTrial);
+                    launch_mf2(tr, G);
                 if (tr) {
                     trace_left = 0;
                     dump_chol_trace(tr, n, s);
@@ -2525,8 +2621,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                     hipLaunchKernelGGL(k_ba_chol_mfma<kMfTileWaves>, dim3(1), dim3((kMfTileWaves + 1) * 64), kMfLds, s,
                                        n, h->S.p, h->bs.p, h->x.p, h->status.p, tr, (const LmState*)L, (int)kGateTrial);
                 else
-                    hipLaunchKernelGGL(k_ba_chol_mf2<kMfTileWaves>, dim3(1), dim3((kMfTileWaves + 1) * 64), kMf2Lds, s,
-                                       n, h->S.p, h->bs.p, h->x.p, h->status.p, tr, (const LmState*)L, (int)kGateTrial);
+                    launch_mf2(tr, (const LmState*)L);
                 if (tr) {
                     trace_left_u = 0;
                     dump_chol_trace(tr, n, s);
@@ -2549,7 +2644,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         if (use_graph) {
             const std::vector<uintptr_t> key = {
                 (uintptr_t)s, (uintptr_t)n, (uintptr_t)m, (uintptr_t)ne, (uintptr_t)nf, (uintptr_t)nl, (uintptr_t)nfe,
-                (uintptr_t)nblk, (uintptr_t)nparts, (uintptr_t)chol_v1, dbits(hub.delta_mono), dbits(hub.delta_stereo), (uintptr_t)bl,
+                (uintptr_t)nblk, (uintptr_t)nparts, (uintptr_t)chol_v1, (uintptr_t)mf_w, (uintptr_t)diag_readlane, dbits(hub.delta_mono), dbits(hub.delta_stereo), (uintptr_t)bl,
                 (uintptr_t)h->edges.p, (uintptr_t)h->cams.p, (uintptr_t)h->pose.p, (uintptr_t)h->point.p,
                 (uintptr_t)h->pose_h.p, (uintptr_t)h->err.p, (uintptr_t)h->rho0.p, (uintptr_t)h->ecl.p,
                 (uintptr_t)h->hpl.p, (uintptr_t)h->ecp.p, (uintptr_t)h->part.p, (uintptr_t)h->pose_off.p,
