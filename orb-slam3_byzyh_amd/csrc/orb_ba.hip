@@ -244,13 +244,13 @@ __device__ __forceinline__ void ba_reduce_pose(int p, int lane, const int32_t* _
     }
     for (int i = 0; i < 42; ++i) red[i][lane] = s[i];
     __syncthreads();
-    for (int w = 32; w >= 1; w >>= 1) {
-        if (lane < w)
-            for (int i = 0; i < 42; ++i) red[i][lane] += red[i][lane + w];
-        __syncthreads();
-    }
-    if (lane < 36) hpp[36 * (size_t)p + lane] = red[lane][0];
-    else if (lane < 42) bp[6 * (size_t)p + lane - 36] = red[lane][0];
+    // lane i sums component i over the 64 lane partials in lane order (one LDS pass, no tree of
+    // 42-wide barrier-separated levels)
+    if (lane >= 42) return;
+    double t = 0;
+    for (int q = 0; q < 64; ++q) t += red[lane][q];
+    if (lane < 36) hpp[36 * (size_t)p + lane] = t;
+    else bp[6 * (size_t)p + lane - 36] = t;
 }
 
 __global__ __launch_bounds__(64) void k_ba_reduce_pose(const int32_t* __restrict__ off, const int32_t* __restrict__ eidx,
