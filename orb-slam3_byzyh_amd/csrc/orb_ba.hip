@@ -1636,22 +1636,28 @@ __global__ __launch_bounds__(1024) void k_ba_sums(int ne, const double* __restri
     }
 }
 
-__global__ __launch_bounds__(kT) void k_ba_final(int ne, const EdgeDev* __restrict__ edges, const double* __restrict__ pose,
-                                                 const double* __restrict__ point, const double* __restrict__ err,
-                                                 double* __restrict__ chi2, uint8_t* __restrict__ depth_ok) {
-    const int e = blockIdx.x * kT + threadIdx.x;
-    if (e >= ne) return;
-    const EdgeDev E = edges[e];
+// The solve's results straight into the pinned host buffer (no device copies, one launch): poses
+// [np][7], points [nq][3], then per edge chi2 (e^T Omega e) and the depth flag of src/Optimizer.cc:2115-2150.
+__global__ __launch_bounds__(kT) void k_ba_results(int np, int nq, int ne, const EdgeDev* __restrict__ edges,
+                                                   const double* __restrict__ pose, const double* __restrict__ point,
+                                                   const double* __restrict__ err, double* __restrict__ h_pose,
+                                                   double* __restrict__ h_point, double* __restrict__ h_chi2,
+                                                   uint8_t* __restrict__ h_depth) {
+    const int t = blockIdx.x * kT + threadIdx.x;
+    if (t < 7 * np) h_pose[t] = pose[t];
+    if (t < 3 * nq) h_point[t] = point[t];
+    if (t >= ne) return;
+    const EdgeDev E = edges[t];
     const double info = (double)E.inv_sigma2;
-    const double* er = err + 3 * (size_t)e;
+    const double* er = err + 3 * (size_t)t;
     double c = er[0] * info * er[0] + er[1] * info * er[1];
     if (E.stereo) c += er[2] * info * er[2];
-    chi2[e] = c;
+    h_chi2[t] = c;
     const double* T = pose + 7 * (size_t)E.pose;
     const double q[4] = {T[3], T[4], T[5], T[6]};
     double Xc[3];
     qrotate(q, point + 3 * (size_t)E.point, Xc);
-    depth_ok[e] = (Xc[2] + T[2]) > 0.0;
+    h_depth[t] = (Xc[2] + T[2]) > 0.0;
 }
 
 // ---- LM controllers (one thread), g2o OptimizationAlgorithmLevenberg::solve ---------------------
@@ -2699,15 +2705,8 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
             }
         }
         launch_restore();  // undo a rejected last trial (gated on the device state)
-        if (hipStreamSynchronize(s) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "BA device error");
         (void)stopped_mid;
-        const LmProgress pg = *h->h_prog;
-        res->iterations = pg.it;
-        res->trials = pg.trials;
-        res->terminated = pg.terminated;
-        res->initial_chi2 = pg.initial_chi;
-        res->final_chi2 = pg.final_chi;
-        res->lambda = pg.lambda;
+        // (the progress record is read after the results' synchronisation below)
     } else {
         double lambda = 0, ni = 2;
         int nBad = 0, it = 0;
@@ -2756,21 +2755,28 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     }
     res->stopped = stop() ? 1 : 0;
     t_solve = clk::now();
-    if (ne)
-        hipLaunchKernelGGL(k_ba_final, dim3(grid(ne)), dim3(kT), 0, s, ne, h->edges.p, h->pose.p, h->point.p, h->err.p,
-                           h->rho0.p, h->depth.p);
-    // results through the pinned buffer sized before the solve
+    // results through the pinned buffer sized before the solve, written by one kernel (edge chi2 / depth
+    // flags, the poses and points): no device-to-host copies
     double* const dpose = reinterpret_cast<double*>(h->h_dl);
     double* const pts = dpose + 7 * (size_t)np;
     double* const lchi = pts + 3 * (size_t)nq;
     uint8_t* const ldep = reinterpret_cast<uint8_t*>(lchi + ne1);
-    hipMemcpyAsync(dpose, h->pose.p, sizeof(double) * 7 * (size_t)np, hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(pts, h->point.p, sizeof(double) * 3 * (size_t)nq, hipMemcpyDeviceToHost, s);
-    if (ne) {
-        hipMemcpyAsync(lchi, h->rho0.p, sizeof(double) * ne, hipMemcpyDeviceToHost, s);
-        hipMemcpyAsync(ldep, h->depth.p, ne, hipMemcpyDeviceToHost, s);
+    {
+        const int nt = std::max(std::max(7 * np, 3 * nq), ne);
+        if (nt > 0)
+            hipLaunchKernelGGL(k_ba_results, dim3(grid(nt)), dim3(kT), 0, s, np, nq, ne, h->edges.p, h->pose.p,
+                               h->point.p, h->err.p, dpose, pts, lchi, ldep);
     }
     if (hipStreamSynchronize(s) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "BA device error");
+    if (dev_lm) {
+        const LmProgress pg = *h->h_prog;
+        res->iterations = pg.it;
+        res->trials = pg.trials;
+        res->terminated = pg.terminated;
+        res->initial_chi2 = pg.initial_chi;
+        res->final_chi2 = pg.final_chi;
+        res->lambda = pg.lambda;
+    }
     memcpy(pr->pose, dpose, sizeof(double) * 7 * (size_t)np);
     if (!dist) {
         memcpy(pr->point, pts, sizeof(double) * 3 * (size_t)nq);
