@@ -1730,17 +1730,21 @@ __device__ void lm_trial_done(LmState* st, double chi, double scale_part, bool f
 
 // ---- fused kernels of the device-driven unit ------------------------------------------------------
 // fixed-order block sum of one value per thread (blockDim = NT); the result is valid in every thread
+// (DPP row sums, the four row totals by v_readlane, then the wave totals through LDS: two barriers
+// instead of a log2(NT)-level tree)
 template <int NT>
 __device__ __forceinline__ double block_sum(double v) {
-    __shared__ double red[NT];
+    static_assert(NT % 64 == 0, "whole waves");
+    __shared__ double red[NT / 64];
+    v = row16_sum(v);  // row sums in lanes 15, 31, 47, 63
+    const double w = (readlane_d(v, 15) + readlane_d(v, 31)) + (readlane_d(v, 47) + readlane_d(v, 63));
+    __syncthreads();  // red may still be read by the previous call
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = w;
     __syncthreads();
-    red[threadIdx.x] = v;
-    __syncthreads();
-    for (int w = NT / 2; w >= 1; w >>= 1) {
-        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-        __syncthreads();
-    }
-    return red[0];
+    double t = 0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) t += red[i];
+    return t;
 }
 
 // true in the last block to finish (its predecessors' global writes are visible to it)
