@@ -214,9 +214,20 @@ __device__ __forceinline__ void ba_reduce_land(int l, const int32_t* __restrict_
                                                const double* __restrict__ ecl, double* __restrict__ hll,
                                                double* __restrict__ bl) {
     double s[12] = {0};
-    for (int k = off[l]; k < off[l + 1]; ++k) {
-        const double* p = ecl + 12 * (size_t)eidx[k];
-        for (int i = 0; i < 12; ++i) s[i] += p[i];
+    const int k1 = off[l + 1];
+    for (int k0 = off[l]; k0 < k1; k0 += 4) {  // chunks of 4 edges: loads issued together, same sum order
+        double v[4][12];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const double* p = ecl + 12 * (size_t)eidx[min(k0 + u, k1 - 1)];
+#pragma unroll
+            for (int i = 0; i < 12; ++i) v[u][i] = p[i];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (k0 + u < k1)
+#pragma unroll
+                for (int i = 0; i < 12; ++i) s[i] += v[u][i];
     }
     for (int i = 0; i < 9; ++i) hll[9 * (size_t)l + i] = s[i];
     for (int i = 0; i < 3; ++i) bl[3 * (size_t)l + i] = s[9 + i];
@@ -1517,12 +1528,30 @@ __device__ __forceinline__ void ba_backsub(int l, int n, double lambda, const in
                                            const double* __restrict__ bl, const double* __restrict__ hll,
                                            double* __restrict__ x) {
     double cl[3] = {bl[3 * (size_t)l], bl[3 * (size_t)l + 1], bl[3 * (size_t)l + 2]};
-    for (int k = off[l]; k < off[l + 1]; ++k) {
-        const int e = eidx[k];
-        const double* H = hpl + 18 * (size_t)e;
-        const double* xp = x + 6 * (size_t)pose_h[edges[e].pose];
-        for (int c = 0; c < 3; ++c)
-            for (int r = 0; r < 6; ++r) cl[c] += H[3 * r + c] * -xp[r];
+    // edges in chunks of 4: each chunk's three dependent index loads and its operand loads are issued
+    // together (not one chain of four dependent loads per edge); the sums run in the same order
+    const int k1 = off[l + 1];
+    for (int k0 = off[l]; k0 < k1; k0 += 4) {
+        int e[4], ph[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) e[u] = eidx[min(k0 + u, k1 - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ph[u] = pose_h[edges[e[u]].pose];
+        double H[4][18], xp[4][6];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+            for (int q = 0; q < 18; ++q) H[u][q] = hpl[18 * (size_t)e[u] + q];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) xp[u][q] = x[6 * (size_t)ph[u] + q];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (k0 + u < k1)
+#pragma unroll
+                for (int c = 0; c < 3; ++c)
+#pragma unroll
+                    for (int r = 0; r < 6; ++r) cl[c] += H[u][3 * r + c] * -xp[u][r];
     }
     double Di[9];
     land_dinv(hll, l, lambda, Di);
