@@ -1829,9 +1829,27 @@ __global__ __launch_bounds__(64) void k_u_reduce_build(int nf, int nl, const int
     const double chi = block_sum<64>(c);
     double md = 0.0;
     if (st->it == 0) {
-        double m = 0;
-        for (int i = lane; i < 6 * nf; i += 64) m = fmax(m, fabs(hpp[36 * (size_t)(i / 6) + 7 * (i % 6)]));
-        for (int i = lane; i < 3 * nl; i += 64) m = fmax(m, fabs(hll[9 * (size_t)(i / 3) + 4 * (i % 3)]));
+        double m = 0;  // (max is order-independent: loads batched 8 per lane)
+        for (int i0 = lane; i0 < 6 * nf; i0 += 8 * 64) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = min(i0 + 64 * u, 6 * nf - 1);
+                v[u] = fabs(hpp[36 * (size_t)(i / 6) + 7 * (i % 6)]);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) m = fmax(m, v[u]);
+        }
+        for (int i0 = lane; i0 < 3 * nl; i0 += 8 * 64) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = min(i0 + 64 * u, 3 * nl - 1);
+                v[u] = fabs(hll[9 * (size_t)(i / 3) + 4 * (i % 3)]);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) m = fmax(m, v[u]);
+        }
         __shared__ double mx[64];
         mx[lane] = m;
         __syncthreads();
@@ -1911,7 +1929,18 @@ __global__ __launch_bounds__(kT) void k_u_edges_trial(int ne, const EdgeDev* __r
     const double chi = block_sum<kT>(c);
     const double lambda = st->lambda;
     double sc = 0.0;
-    for (int i = threadIdx.x; i < nx; i += kT) sc += x[i] * (lambda * x[i] + b[i]);
+    for (int i0 = threadIdx.x; i0 < nx; i0 += 8 * kT) {  // 8 loads in flight per thread, same sum order
+        double xv[8], bv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = min(i0 + u * kT, nx - 1);
+            xv[u] = x[i];
+            bv[u] = b[i];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (i0 + u * kT < nx) sc += xv[u] * (lambda * xv[u] + bv[u]);
+    }
     const double scale = block_sum<kT>(sc);
     if (threadIdx.x == 0) {
         const bool failed = *status != 0;
