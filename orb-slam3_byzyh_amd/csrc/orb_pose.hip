@@ -108,23 +108,32 @@ __device__ __forceinline__ void block_reduce(double (&v)[N], double* red) {
 // LDL^T of the 6x6 symmetric matrix (LinearSolverDense: Eigen::LDLT; same solution up to rounding)
 __device__ bool ldlt6(const double A[36], const double b[6], double x[6]) {
     double L[36] = {0}, d[6];
+#pragma unroll
     for (int j = 0; j < 6; ++j) {
         double dj = A[7 * j];
+#pragma unroll
         for (int k = 0; k < j; ++k) dj -= L[6 * j + k] * L[6 * j + k] * d[k];
         if (!(dj > 0)) return false;  // LDLT::isPositive (the damped system is SPD unless degenerate)
         d[j] = dj;
+#pragma unroll
         for (int i = j + 1; i < 6; ++i) {
             double v = A[6 * j + i];
+#pragma unroll
             for (int k = 0; k < j; ++k) v -= L[6 * i + k] * L[6 * j + k] * d[k];
             L[6 * i + j] = v / dj;
         }
     }
+#pragma unroll
     for (int i = 0; i < 6; ++i) {
         x[i] = b[i];
+#pragma unroll
         for (int k = 0; k < i; ++k) x[i] -= L[6 * i + k] * x[k];
     }
+#pragma unroll
     for (int i = 0; i < 6; ++i) x[i] /= d[i];
+#pragma unroll
     for (int i = 5; i >= 0; --i)
+#pragma unroll
         for (int k = i + 1; k < 6; ++k) x[i] -= L[6 * k + i] * x[k];
     return true;
 }
@@ -146,7 +155,7 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
     double* ech = echi2 + F.edge_begin;
     for (int e = tid; e < n; e += kPT) lev[e] = 0;  // mvbOutlier[i] = false at edge creation
     if (n < 3) {  // nInitialCorrespondences < 3: return 0, pose untouched
-        if (tid < 7) pose_out[7 * (size_t)f + tid] = F.pose[tid];
+        if (tid < 7) pose_out[7 * (size_t)f + tid] = frames[f].pose[tid];
         if (tid == 0) inliers[f] = 0;
         return;
     }
@@ -154,7 +163,9 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
     bool robust = true;
     int nBad = 0;
     for (int round = 0; round < 4; ++round) {
-        if (tid < 7) T[tid] = F.pose[tid];  // vSE3->setEstimate(pFrame->GetPose())
+        // vSE3->setEstimate(pFrame->GetPose()); read from global: a lane-indexed read of the copy F
+        // would put F in scratch
+        if (tid < 7) T[tid] = frames[f].pose[tid];
         __syncthreads();
         // ---- optimizer.initializeOptimization(0); optimizer.optimize(10)
         int active = 0;
