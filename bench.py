@@ -54,8 +54,17 @@ def level_sizes(w, h, n=NLEVELS, s=1.2):
     return out
 
 
+def survey_bytes_per_frame(w, h, nkp):
+    """SURVEY.md sec. 8(d)'s algorithmic bytes per frame of the whole extraction path: read L0,
+    write + read levels 1..7 (mvImagePyramid must be materialised), keypoints + descriptors out
+    (28 + 32 B each).  640x480 with N = 1000 keypoints: 1,653,864 B."""
+    sizes = level_sizes(w, h)
+    return w * h + 2 * sum(a * b for a, b in sizes[1:]) + nkp * 60
+
+
 def algorithmic_bytes_per_frame(w, h, nkp):
-    """Per-frame algorithmic bytes of each stage (DESIGN.md sec. Measurement)."""
+    """Per-frame bytes each stage of THIS implementation moves (a traffic model, not the roofline's
+    algorithmic figure, which is survey_bytes_per_frame)."""
     sizes = level_sizes(w, h)
     px = [a * b for a, b in sizes]
     pad = [(a + 38) * (b + 38) for a, b in sizes]
@@ -74,13 +83,40 @@ def algorithmic_bytes_per_frame(w, h, nkp):
     }
 
 
-def cpu_baseline(oracle_mod, frames, budget_s=10.0):
-    """Oracle (CPU restatement of ORBextractor) on a thread pool, one frame per thread at a time."""
+def host_cores():
+    """(threads, description): every core this process may run on (sched_getaffinity), limited by
+    a cgroup CPU quota when one is set (a quota of Q CPUs runs at most Q threads at a time)."""
     try:
-        cores = len(os.sched_getaffinity(0))
+        affinity = len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
+        affinity = os.cpu_count() or 1
+    quota = None
+    try:
+        q, period = pathlib.Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except Exception:  # noqa: BLE001 -- no cgroup v2 quota
+        quota = None
+    threads = min(affinity, quota) if quota else affinity
+    model = ""
+    try:
+        for line in pathlib.Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:  # noqa: BLE001
+        pass
+    desc = f"{affinity} cores in the affinity mask" + (f", cgroup quota {quota} CPUs" if quota else ", no cgroup quota")
+    return max(1, threads), desc + (f", {model}" if model else "")
+
+
+ORACLE_FLAGS = "g++ -O3 -march=x86-64-v3 -ffp-contract=off (oracle/Makefile)"
+
+
+def cpu_baseline(oracle_mod, frames, budget_s=10.0):
+    """Oracle (CPU restatement of ORBextractor) on a thread pool over every available host core,
+    one frame per thread at a time (C2 thread pool, one frame per core)."""
+    cores, cores_desc = host_cores()
     ex = [oracle_mod.OracleExtractor(NFEAT, 1.2, NLEVELS, 20, 7) for _ in range(cores)]
     t0 = time.perf_counter()
     done = [0] * cores
@@ -99,8 +135,8 @@ def cpu_baseline(oracle_mod, frames, budget_s=10.0):
     dt = time.perf_counter() - t0
     nf = sum(done)
     return {"value": round(sum(feats) / (dt * 1e3), 3), "unit": "features/ms", "cores": cores, "kind": "port",
-            "sample": f"{nf} frames of the C2 set (640x480, nFeatures 1000) in {dt:.1f} s on {cores} threads, "
-                      "oracle/orb_extractor_oracle.cpp -O2"}
+            "sample": f"{nf} frames of the C2 set (640x480, nFeatures 1000) in {dt:.1f} s on {cores} threads "
+                      f"({cores_desc}), oracle/orb_extractor_oracle.cpp, {ORACLE_FLAGS}"}
 
 
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (= FP64 matrix) peak, AMD spec; not listed in MI355X_MICROARCH.md
@@ -177,7 +213,7 @@ def bench_local_ba(pkg, synth, world, dev, steps, cpu_baseline_on):
             nrep += 1
         cdt = (time.perf_counter() - t0) * 1e3
         out["cpu_baseline"] = {"value": round(cdt / it_cpu, 4), "unit": "ms/iteration", "cores": 1, "kind": "port",
-                               "sample": f"{nrep} solves of the same C5 problem, oracle/orb_ba_oracle.cpp -O2, "
+                               "sample": f"{nrep} solves of the same C5 problem, oracle/orb_ba_oracle.cpp, " + ORACLE_FLAGS + ", "
                                          "one thread (g2o is built without OpenMP)"}
     return out
 
@@ -299,7 +335,7 @@ def bench_pose(pkg, synth, dev, steps, cpu_baseline_on, n_frames=256, n_points=5
         cdt = (time.perf_counter() - t0) * 1e3
         out["cpu_baseline"] = {"value": round(nfr / cdt, 4), "unit": "frames/ms", "cores": 1, "kind": "port",
                                "sample": f"{nfr} frames of the same set in {cdt / 1e3:.1f} s, "
-                                         "oracle/orb_pose_oracle.cpp -O2, one thread (as Tracking runs it)"}
+                                         "oracle/orb_pose_oracle.cpp, " + ORACLE_FLAGS + ", one thread (as Tracking runs it)"}
     return out
 
 
@@ -336,7 +372,7 @@ def bench_bow(pkg, synth, dev, steps, cpu_baseline_on, n_frames=64, n_feat=1000)
             nfr += 1
         cdt = (time.perf_counter() - t0) * 1e3
         out["cpu_baseline"] = {"value": round(nfr / cdt, 4), "unit": "frames/ms", "cores": 1, "kind": "port",
-                               "sample": f"{nfr} frames in {cdt / 1e3:.1f} s, oracle/orb_bow_oracle.cpp -O2, one thread"}
+                               "sample": f"{nfr} frames in {cdt / 1e3:.1f} s, oracle/orb_bow_oracle.cpp, " + ORACLE_FLAGS + ", one thread"}
     return out
 
 
@@ -545,18 +581,22 @@ def main():
 
     if rank == 0:
         per_step = {k: v / max(1, launches) for k, v in stage_ms.items()}
-        # roofline kernel: k_pyramid_level (the stage with the most HBM bytes), launches_per_step
-        # launches per step; achieved = its algorithmic bytes per launch / its mean launch duration
-        # (event pairs around each launch in the timed region, comparable to rocprofv3's average)
+        # roofline kernel: k_pyramid_level, the HBM-facing stage (it reads every input frame and
+        # writes every level), launches_per_step launches per step, each one level of all nfr frames.
+        # achieved = SURVEY.md 8(d)'s algorithmic bytes per frame x nfr / launches_per_step, divided
+        # by the mean launch duration measured in the timed region from per-block wall-clock stamps
+        # (first block start to last block end of each launch; no events between the launches).
+        # The stage with the most time is reported next to it (`dominant_stage`).
         dom = "pyramid"
         nkp_frame = feats_per_step / nfr
-        alg = algorithmic_bytes_per_frame(WIDTH, HEIGHT, nkp_frame)
-        dom_bytes = alg[dom] * nfr / launches_per_step
+        dom_bytes = survey_bytes_per_frame(WIDTH, HEIGHT, nkp_frame) * nfr / launches_per_step
+        model_bytes = algorithmic_bytes_per_frame(WIDTH, HEIGHT, nkp_frame)[dom] * nfr / launches_per_step
         achieved = dom_bytes / (pyr_launch_avg_ms * 1e-3) / 1e9 if pyr_launch_avg_ms > 0 else 0.0
         pmc = pmc_traffic()
         traffic = None
         if pmc and pmc.get("kernel_stage") == dom and pmc.get("frames_per_launch") == nfr:
             traffic = pmc.get("hbm_bytes_per_launch")
+        dominant_stage = max(per_step, key=per_step.get) if per_step else dom
         result = {
             "metric": "ORB features/ms (640x480, 8-level) + LocalBA iter ms @1/2/4/8 GPU",
             "value": round(total_feats / elapsed_ms, 3),
@@ -581,10 +621,17 @@ def main():
             "roofline": {"bound": "hbm", "kernel": "k_pyramid_level", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "algorithmic_bytes_per_launch": int(dom_bytes),
+                         "traffic_over_algorithmic": round(traffic / dom_bytes, 3) if traffic else None,
+                         "traffic_model_bytes_per_launch": int(model_bytes),
                          "launches_per_step": launches_per_step,
                          "launch_avg_us": round(pyr_launch_avg_ms * 1e3, 2),
-                         "note": "per-launch averages over the 8 level launches of a step; traffic = PMC "
-                                 "FETCH_SIZE x2 + WRITE_SIZE (profiles/pmc_latest.json)"},
+                         "dominant_stage": dominant_stage,
+                         "note": "algorithmic bytes = SURVEY.md 8(d) 1,653,864 B per 640x480 frame (L0 read, "
+                                 "levels 1-7 written + read, 60 B per keypoint out) x frames / 8 level launches; "
+                                 "launch_avg_us from per-block wall-clock stamps in the timed region; traffic = "
+                                 "PMC FETCH_SIZE x2 + WRITE_SIZE per launch (profiles/pmc_latest.json); "
+                                 "traffic_model = the bytes this implementation's pyramid moves (padded planes, "
+                                 "blurred levels)"},
         }
         if not args.no_cpu_baseline and world == 1:
             from oracle import oracle as oracle_mod

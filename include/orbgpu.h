@@ -354,6 +354,8 @@ typedef struct orb_ba_options {
     int32_t iterations;                   /* optimizer.optimize(10) (src/Optimizer.cc:2101) */
     double user_lambda_init;              /* 0: tau * max diag(H) (tau = 1e-5); >0: setUserLambdaInit */
     const volatile int32_t* stop_flag;    /* pbStopFlag (polled between iterations and trials), may be NULL */
+    const volatile uint8_t* stop_flag_bool;  /* the same for a C++ `bool* pbStopFlag` (one byte, nonzero = stop),
+                                                as LocalMapping passes &mbAbortBA (src/LocalMapping.cc:208); may be NULL */
 } orb_ba_options_t;
 
 typedef struct orb_ba_result {

@@ -206,7 +206,7 @@ class _BaProblem(ctypes.Structure):
 
 
 class _BaOptions(ctypes.Structure):
-    _fields_ = [("iterations", ctypes.c_int32), ("user_lambda_init", ctypes.c_double), ("stop_flag", _vp)]
+    _fields_ = [("iterations", ctypes.c_int32), ("user_lambda_init", ctypes.c_double), ("stop_flag", _vp), ("stop_flag_bool", _vp)]
 
 
 class _BaResult(ctypes.Structure):

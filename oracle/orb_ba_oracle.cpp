@@ -139,7 +139,7 @@ extern "C" int oracle_local_ba(orb_ba_problem_t* prob, const orb_ba_options_t* o
                                uint8_t* depth_ok_out, orb_ba_result_t* res) {
     Problem P(*prob);
     const int np = prob->n_poses, nq = prob->n_points, ne = prob->n_edges;
-    auto stop = [&]() { return opt->stop_flag && *opt->stop_flag; };
+    auto stop = [&]() { return (opt->stop_flag && *opt->stop_flag) || (opt->stop_flag_bool && *opt->stop_flag_bool); };
     memset(res, 0, sizeof(*res));
     P.pose.resize(np);
     for (int i = 0; i < np; ++i) {

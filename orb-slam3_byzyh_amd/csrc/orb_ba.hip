@@ -1264,6 +1264,191 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
     if (threadIdx.x == 0) *status = fail;
 }
 
+// ---- tile-row Cholesky + solve over many workgroups (any n up to 16 x 256) ----------------------
+// Workgroup i owns tile row i of S (tiles (i, j), j <= i, in the operand layout O of the kernels
+// above) and runs the whole row left to right, eagerly:
+//   step m < i: once row m has published L_mm^-1 and y_m, wave 0 turns its tile (i, m) into
+//     L_im = A_im L_mm^-T (4 MFMAs), publishes it and folds the forward solve in (b_i -= L_im y_m);
+//     then the four waves apply column m to the rest of the row, T_ij -= L_im L_jm^T for
+//     m < j <= i, taking L_jm from row j as soon as row j has published it (tile (i, m+1), the
+//     next step's panel tile, goes first).
+//   diagonal: wave 0 factors T_ii (mf_diag), publishes L_ii^-1 and y_i = L_ii^-1 b_i.
+// The critical chain per step is one hand-off (row m -> row m+1), one panel product, one update
+// and one 16x16 factorisation.  The last row's workgroup, which has by then consumed every
+// published tile, finishes with the backward solve L^T x = y.
+// Hand-offs between workgroups (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the
+// sc1 table): the payload (tiles, y) is stored with agent-scope relaxed 8-byte atomics (sc1
+// write-through stores), each storing wave drains its stores (s_waitcnt vmcnt(0)) before one lane
+// stores the flag (agent scope); the consumer wave polls the flag with agent-scope loads and reads
+// every byte of the payload with agent-scope (sc1) loads; other waves of the consumer read only
+// after a workgroup barrier the polling wave has joined.  Flags hold the launch's epoch (one more
+// than the counter in cflag[0], which the last row advances when it finishes), so they never need
+// clearing between launches; every spin is bounded and a timeout is reported as a failed solve.
+// Rows are kept in LDS up to kRowLdsMaxNT tiles, in a private global scratch beyond.
+constexpr int kRowThreads = 256, kRowLdsMaxNT = 72, kRowMaxNT = 256;
+typedef __attribute__((address_space(1))) unsigned long long ba_gu64;
+typedef __attribute__((address_space(1))) unsigned ba_gu32;
+
+__device__ __forceinline__ double ld_agent(const double* p) {
+    return __longlong_as_double((long long)__hip_atomic_load((ba_gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_agent(double* p, double v) {
+    __hip_atomic_store((ba_gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+// one wave polls one flag word until it holds `epoch` (or later); false after ~4 s
+__device__ __forceinline__ bool flag_wait_agent(const unsigned* f, unsigned epoch) {
+    for (int spin = 0; spin < (1 << 22); ++spin) {
+        if (__hip_atomic_load((ba_gu32*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= epoch) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the payload loads below the poll
+            return true;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return false;
+}
+__device__ __forceinline__ void flag_publish_agent(unsigned* f, unsigned epoch, int lane) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 payload stores have landed
+    if (lane == 0) __hip_atomic_store((ba_gu32*)f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool kLdsRow>
+__global__ __launch_bounds__(kRowThreads) void k_ba_chol_rows(int n, const double* __restrict__ S,
+                                                              const double* __restrict__ b, double* __restrict__ x,
+                                                              int32_t* __restrict__ status, double* __restrict__ lpub,
+                                                              double* __restrict__ ypub, unsigned* __restrict__ cflag,
+                                                              double* __restrict__ racc,
+                                                              const LmState* __restrict__ lm_st, int lm_gk) {
+    if (lm_skip(lm_st, lm_gk)) return;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int NT = (n + 15) >> 4;
+    const int i = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r16 = lane & 15, g4 = lane >> 4;
+    double* R = kLdsRow ? lds : racc + (size_t)i * NT * 256;  // own row: tile j at R + 256 j
+    double* dk = kLdsRow ? lds + (size_t)NT * 256 : lds;      // [16][17] diagonal block
+    double* linv = dk + 272;                                   // [256] O(L_ii^-1)
+    double* rv = linv + 256;                                   // [16] b_i -> y_i
+    double* z = rv + 16;                                       // [16 NT] backward solve (last row)
+    __shared__ int fail;
+    unsigned* flags = cflag + 4;  // [row][col]: tile (row, col) published at this epoch
+    const unsigned E = cflag[0] + 1;
+    if (tid == 0) fail = 0;
+    for (int t = tid; t < (i + 1) * 256; t += kRowThreads) {  // S upper triangle read as S[col blk][row blk]
+        const int j = t >> 8, e = t & 255, q = e >> 6, l = e & 63;
+        const int row = 16 * j + (l >> 4) + 4 * q, col = 16 * i + (l & 15);
+        const double v = S[(size_t)min(row, n - 1) * n + min(col, n - 1)];
+        R[t] = (row < n && col < n) ? v : (row == col ? 1.0 : 0.0);
+    }
+    if (tid < 16) rv[tid] = 16 * i + tid < n ? b[16 * i + tid] : 0.0;
+    __syncthreads();
+    for (int m = 0; m < i; ++m) {
+        if (w == 0) {  // panel tile (i, m) and the forward step
+            if (!flag_wait_agent(flags + m * NT + m, E) && lane == 0) fail = 4;
+            const double* lp = lpub + ((size_t)m * NT + m) * 256;
+            double lq[4], yq[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                lq[q] = ld_agent(lp + q * 64 + lane);
+                yq[q] = ld_agent(ypub + 16 * m + g4 + 4 * q);
+            }
+            double* Tm = R + m * 256;
+            f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(lq[q], Tm[q * 64 + lane], acc, 0, 0, 0);
+            double* dst = lpub + ((size_t)i * NT + m) * 256;
+            double part = 0.0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                Tm[q * 64 + lane] = acc[q];
+                st_agent(dst + q * 64 + lane, acc[q]);
+                part = __builtin_fma(acc[q], yq[q], part);
+            }
+            part += __shfl_xor(part, 16);
+            part += __shfl_xor(part, 32);
+            if (lane < 16) rv[lane] -= part;
+            flag_publish_agent(flags + i * NT + m, E, lane);
+        }
+        __syncthreads();
+        const double* Lim = R + m * 256;
+        for (int j = m + 1 + w; j <= i; j += 4) {  // T_ij -= L_im L_jm^T
+            double a[4];
+            if (j < i) {
+                if (!flag_wait_agent(flags + j * NT + m, E) && lane == 0) fail = 5;
+                const double* lp = lpub + ((size_t)j * NT + m) * 256;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) a[q] = ld_agent(lp + q * 64 + lane);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) a[q] = Lim[q * 64 + lane];
+            }
+            double* T = R + j * 256;
+            f64x4 t = {T[lane], T[64 + lane], T[128 + lane], T[192 + lane]};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) t = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], Lim[q * 64 + lane], t, 0, 0, 1);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) T[q * 64 + lane] = t[q];
+        }
+        __syncthreads();
+    }
+    if (w == 0) {  // diagonal tile: L_ii^-1 and y_i
+        const double* Ti = R + i * 256;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dk[r16 * 17 + g4 + 4 * q] = Ti[q * 64 + lane];
+        mf_wave_sync();
+        mf_diag<false, true>(dk, linv, rv, lane, &fail);
+        mf_wave_sync();
+        double* dst = lpub + ((size_t)i * NT + i) * 256;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) st_agent(dst + q * 64 + lane, linv[q * 64 + lane]);
+        if (lane < 16) st_agent(ypub + 16 * i + lane, rv[lane]);
+        flag_publish_agent(flags + i * NT + i, E, lane);
+    }
+    __syncthreads();
+    if (fail > 3 && tid == 0) __hip_atomic_store((ba_gu32*)(cflag + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (i != NT - 1) return;
+    // ---- backward solve L^T x = y in the last row's workgroup: x_j = L_jj^-T (y_j - sum_{k>j} L_kj^T x_k),
+    // right-looking: after x_j, every z_p (p < j) loses L_jp^T x_j
+    __syncthreads();
+    for (int t = tid; t < 16 * NT; t += kRowThreads) z[t] = t < 16 * (NT - 1) ? ld_agent(ypub + t) : rv[t - 16 * (NT - 1)];
+    __syncthreads();
+    for (int j = NT - 1; j >= 0; --j) {
+        if (w == 0) {  // x_j[c] = sum_r L^-1[r][c] z_j[r]; L^-1[r][c] at (c >> 2) 64 + r + 16 (c & 3)
+            const double* lj = lpub + ((size_t)j * NT + j) * 256;
+            double v4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int rr = 0; rr < 16; ++rr) {
+                const int o = (r16 >> 2) * 64 + rr + 16 * (r16 & 3);
+                const double l = j == NT - 1 ? linv[o] : ld_agent(lj + o);
+                v4[rr & 3] = __builtin_fma(l, z[16 * j + rr], v4[rr & 3]);
+            }
+            const double xj = (v4[0] + v4[1]) + (v4[2] + v4[3]);
+            mf_wave_sync();
+            if (lane < 16) z[16 * j + r16] = xj;
+        }
+        __syncthreads();
+        for (int t = tid; t < 16 * j; t += kRowThreads) {  // z_p[c] -= sum_r L_jp[r][c] x_j[r]
+            const int p = t >> 4, c = t & 15;
+            const double* L = (j == NT - 1 ? R : lpub + (size_t)j * NT * 256) + p * 256 + (c >> 2) * 64 + 16 * (c & 3);
+            double v4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int rr = 0; rr < 16; ++rr) {
+                const double l = j == NT - 1 ? L[rr] : ld_agent(L + rr);
+                v4[rr & 3] = __builtin_fma(l, z[16 * j + rr], v4[rr & 3]);
+            }
+            z[t] -= (v4[0] + v4[1]) + (v4[2] + v4[3]);
+        }
+        __syncthreads();
+    }
+    for (int t = tid; t < n; t += kRowThreads) x[t] = z[t];
+    if (tid == 0) {
+        const unsigned timeouts = __hip_atomic_load((ba_gu32*)(cflag + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *status = fail ? fail : (timeouts ? 6 : 0);
+        cflag[0] = E;  // every row read the epoch before publishing, and this row consumed all of them
+    }
+}
+
 // Cooperative multi-workgroup Cholesky + solve (the fast path for n <= 560 / 1100).
 // Right-looking by block columns of NB: workgroup w < nbc keeps block column w (rows j0..n) in LDS
 // for the whole factorisation; workgroup nbc owns the right-hand side.  Step k: the owner of
@@ -2053,11 +2238,15 @@ struct orb_ba_s {
     size_t h_red_cap = 0;
     DevBuf<double> red_buf;
     DevBuf<int64_t> trace;  // ORBGPU_BA_TRACE stamps (debug)
+    // k_ba_chol_rows: published tiles / y, the epoch + flag words (zeroed when allocated), row scratch
+    DevBuf<double> lpub, ypub, racc;
+    DevBuf<unsigned> cflag;
 
     void release() {
         for (auto* d : {&pose, &pose_bak, &point, &point_bak, &err, &rho0, &ecl, &hpl, &ecp, &hpp, &hll, &b, &z,
-                        &cb, &S, &LT, &Linv, &bs, &x, &scal})
+                        &cb, &S, &LT, &Linv, &bs, &x, &scal, &lpub, &ypub, &racc})
             d->release();
+        cflag.release();
         edges.release();
         cams.release();
         for (auto* d : {&pose_h, &free_pose, &land_point, &land_off, &land_edge, &landf_off, &landf_edge, &fland, &pose_off,
@@ -2237,6 +2426,10 @@ int orb_ba_dist_init_host(orb_ba_t h, orb_ba_host_reduce_fn fn, void* ctx, int w
     return ORB_OK;
 }
 
+static bool stop_requested(const orb_ba_options_t* opt) {
+    return (opt->stop_flag && *opt->stop_flag) || (opt->stop_flag_bool && *opt->stop_flag_bool);
+}
+
 int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* opt, double* edge_chi2,
                     uint8_t* edge_depth_ok, orb_ba_result_t* res) {
     if (!h || !pr || !opt || !res) return orbgpu_fail(ORB_ERR_ARG, "null BA argument");
@@ -2262,7 +2455,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     if (!h->scal.grow(8)) return orbgpu_fail(ORB_ERR_DEVICE, "BA scalar buffer");
     // the stop flag, agreed across the ranks (MAX) so that every rank takes the same path
     auto stop = [&]() -> bool {
-        double f = (opt->stop_flag && *opt->stop_flag) ? 1.0 : 0.0;
+        double f = stop_requested(opt) ? 1.0 : 0.0;
         if (!dist) return f != 0.0;
         h->h_scal[4] = f;
         hipMemcpyAsync(h->scal.p + 4, &h->h_scal[4], sizeof(double), hipMemcpyHostToDevice, s);
@@ -2495,9 +2688,38 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     auto lds_bytes = [&](int b) { return sizeof(double) * ((size_t)b * n + (size_t)n * (b + 1) + n); };
     if (lds_bytes(nb) > 150 * 1024) nb = 8;
     const size_t chol_lds = lds_bytes(nb);
-    if (chol_lds > 150 * 1024 && !coop_nb && n > 16 * kMfMaxNT)
-        return orbgpu_fail(ORB_ERR_ARG, "too many free keyframes for the on-chip Cholesky");
-    const bool use_mf = !coop_nb && n <= 16 * kMfMaxNT && !getenv("ORBGPU_BA_CHOL_LDS");
+    // The tile-row Cholesky (k_ba_chol_rows, one workgroup per 16-row tile row) takes every n it can
+    // hold resident (16 x kRowMaxNT); the register-resident single-workgroup kernel stays for
+    // n <= 288 unless ORBGPU_BA_CHOL=rows.
+    const int NT = (n + 15) / 16;
+    if (NT > kRowMaxNT) {
+        agree_fail(true);
+        return orbgpu_fail(ORB_ERR_ARG, "more than 682 free keyframes in the local window");
+    }
+    static const char* chol_env = getenv("ORBGPU_BA_CHOL");
+    const bool use_rows = n > 0 && (n > 16 * kMfMaxNT || (chol_env && !strcmp(chol_env, "rows")));
+    const bool rows_lds = NT <= kRowLdsMaxNT;
+    const size_t rows_lds_bytes =
+        sizeof(double) * ((rows_lds ? (size_t)NT * 256 : 0) + 272 + 256 + 16 + 16 * (size_t)NT);
+    if (use_rows) {
+        const size_t nflag = 4 + (size_t)NT * NT;
+        bool ok2 = h->lpub.grow((size_t)NT * NT * 256) && h->ypub.grow(16 * (size_t)NT) &&
+                   (rows_lds || h->racc.grow((size_t)NT * NT * 256));
+        if (ok2 && nflag > h->cflag.cap) {  // (re)allocated: epoch and every flag start at 0
+            ok2 = h->cflag.grow(nflag) && hipMemsetAsync(h->cflag.p, 0, nflag * sizeof(unsigned), s) == hipSuccess;
+        }
+        if (agree_fail(!ok2)) return orbgpu_fail(ORB_ERR_DEVICE, "BA Cholesky buffers");
+    }
+    auto launch_rows = [&](const LmState* g) {
+        if (rows_lds)
+            hipLaunchKernelGGL(k_ba_chol_rows<true>, dim3(NT), dim3(kRowThreads), rows_lds_bytes, s, n, h->S.p, h->bs.p,
+                               h->x.p, h->status.p, h->lpub.p, h->ypub.p, h->cflag.p, h->racc.p, g, (int)kGateTrial);
+        else
+            hipLaunchKernelGGL(k_ba_chol_rows<false>, dim3(NT), dim3(kRowThreads), rows_lds_bytes, s, n, h->S.p,
+                               h->bs.p, h->x.p, h->status.p, h->lpub.p, h->ypub.p, h->cflag.p, h->racc.p, g,
+                               (int)kGateTrial);
+    };
+    const bool use_mf = !use_rows && !coop_nb && n <= 16 * kMfMaxNT && !getenv("ORBGPU_BA_CHOL_LDS");
     const bool chol_v1 = getenv("ORBGPU_BA_CHOL_V1") != nullptr;
     // v2 Cholesky shape: 11 tile waves + the diagonal wave (3 waves per SIMD: 2.20 -> 2.14 ms per C5
     // solve against 7 + 1); ORBGPU_BA_MF_W=7 selects the 8-wave kernel
@@ -2526,12 +2748,14 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         hipFuncSetAttribute((const void*)k_ba_chol_mf2<kMfTileWaves, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMf2Lds);
         hipFuncSetAttribute((const void*)k_ba_chol<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
         hipFuncSetAttribute((const void*)k_ba_chol<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+        hipFuncSetAttribute((const void*)k_ba_chol_rows<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_ba_chol_rows<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
         (void)hipGetLastError();
         attr_set = true;
     }
     double* bl = h->b.p + n;
     // The device-driven LM loop (one process, the MFMA Cholesky): no host round trip per trial.
-    const bool dev_lm = !dist && use_mf && !getenv("ORBGPU_BA_HOST_LM");
+    const bool dev_lm = !dist && (use_mf || use_rows) && !getenv("ORBGPU_BA_HOST_LM");
     const LmState* G = dev_lm ? h->lm.p : nullptr;            // gate source for every per-trial kernel
     const double* lam = dev_lm ? &h->lm.p->lambda : h->h_scal + 5;  // the trial's lambda (device / pinned)
     // ---- computeActiveErrors + activeRobustChi2 + buildSystem
@@ -2570,7 +2794,9 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                                primary ? 1 : 0, h->bs.p, G, (int)kGateTrial);
             if (!dev_reduce(h, h->S.p, (size_t)n * n, ORB_BA_SUM) || !dev_reduce(h, h->bs.p, n, ORB_BA_SUM))
                 return false;
-            if (coop_nb) {
+            if (use_rows) {
+                launch_rows(G);
+            } else if (coop_nb) {
                 hipMemsetAsync(h->status.p, 0, sizeof(int32_t), s);
                 int nn = n;
                 double* Sp = h->S.p;
@@ -2685,7 +2911,9 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                     hipMemsetAsync(h->trace.p, 0, 1024 * sizeof(int64_t), s);
                     tr = h->trace.p;
                 }
-                if (chol_v1)
+                if (use_rows)
+                    launch_rows((const LmState*)L);
+                else if (chol_v1)
                     hipLaunchKernelGGL(k_ba_chol_mfma<kMfTileWaves>, dim3(1), dim3((kMfTileWaves + 1) * 64), kMfLds, s,
                                        n, h->S.p, h->bs.p, h->x.p, h->status.p, tr, (const LmState*)L, (int)kGateTrial);
                 else
@@ -2711,7 +2939,10 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         bool use_graph = !no_graph && !getenv("ORBGPU_BA_TRACE");
         // units per graph launch (ORBGPU_BA_UNITS, default 2): each launch boundary costs ~13 us on the
         // device, a gated no-op unit behind the last trial less (C5 solve 1.89 -> 1.87 ms; 3: 1.89)
-        static const int units_per_launch = std::max(1, getenv("ORBGPU_BA_UNITS") ? atoi(getenv("ORBGPU_BA_UNITS")) : 2);
+        // With a stop flag, one unit per launch: the host polls the flag after every launch, so at
+        // most two trials (the running and the queued unit) follow a raised flag, as before.
+        static const int units_env = std::max(1, getenv("ORBGPU_BA_UNITS") ? atoi(getenv("ORBGPU_BA_UNITS")) : 2);
+        const int units_per_launch = (opt->stop_flag || opt->stop_flag_bool) ? 1 : units_env;
         if (use_graph) {
             const std::vector<uintptr_t> key = {
                 (uintptr_t)s, (uintptr_t)n, (uintptr_t)m, (uintptr_t)ne, (uintptr_t)nf, (uintptr_t)nl, (uintptr_t)nfe,
@@ -2725,7 +2956,9 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                 (uintptr_t)h->cb.p, (uintptr_t)h->blk_i.p, (uintptr_t)h->blk_j.p, (uintptr_t)h->blk_off.p,
                 (uintptr_t)h->pair_a.p, (uintptr_t)h->pair_b.p, (uintptr_t)h->S.p, (uintptr_t)h->bs.p,
                 (uintptr_t)h->x.p, (uintptr_t)h->status.p, (uintptr_t)h->landf_off.p, (uintptr_t)h->free_pose.p,
-                (uintptr_t)h->land_point.p, (uintptr_t)h->pose_bak.p, (uintptr_t)h->point_bak.p, (uintptr_t)h->h_prog};
+                (uintptr_t)h->land_point.p, (uintptr_t)h->pose_bak.p, (uintptr_t)h->point_bak.p, (uintptr_t)h->h_prog,
+                (uintptr_t)use_rows, (uintptr_t)h->lpub.p, (uintptr_t)h->ypub.p, (uintptr_t)h->cflag.p,
+                (uintptr_t)h->racc.p};
             if (!h->unit_exec || key != h->unit_key) {
                 if (h->unit_exec) { hipGraphExecDestroy(h->unit_exec); h->unit_exec = nullptr; }
                 if (h->unit_graph) { hipGraphDestroy(h->unit_graph); h->unit_graph = nullptr; }
@@ -2763,7 +2996,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                 if (hipEventSynchronize(h->unit_ev[(u - 1) & 1]) != hipSuccess)
                     return orbgpu_fail(ORB_ERR_DEVICE, "BA device error");
                 if (h->h_prog->done || !more) break;
-                if (opt->stop_flag && *opt->stop_flag) {
+                if (stop_requested(opt)) {
                     stopped_mid = true;
                     break;
                 }

@@ -103,6 +103,13 @@ class ShardedExtractor:
         with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
             for w in works:
                 w.wait()
+            # the gathered blocks were allocated while another step's stream was current; tell the
+            # caching allocator that `stream` uses them too, so their memory is not handed to a later
+            # all-gather (ordered only after its own stream) before this stream has read them
+            consumer = torch.cuda.current_stream()
+            for t in (g_kps, g_desc, g_cnt):
+                if t.is_cuda:
+                    t.record_stream(consumer)
         self._pending = None
         return g_kps, g_desc, g_cnt
 

@@ -30,7 +30,7 @@ class BaProblem(ctypes.Structure):
 
 
 class BaOptions(ctypes.Structure):
-    _fields_ = [("iterations", ctypes.c_int32), ("user_lambda_init", ctypes.c_double), ("stop_flag", _p)]
+    _fields_ = [("iterations", ctypes.c_int32), ("user_lambda_init", ctypes.c_double), ("stop_flag", _p), ("stop_flag_bool", _p)]
 
 
 class BaResult(ctypes.Structure):
