@@ -69,6 +69,15 @@ def test_introsort_port_matches_libstdcxx():
     assert r.returncode == 0 and "\nOK " in "\n" + r.stdout, r.stdout + r.stderr
 
 
+def test_local_ba_shim_on_mock_graph():
+    """include/orbgpu_optimizer.hpp (Optimizer::LocalBundleAdjustment drop-in): window, vertex ids,
+    edge order, stop flag, cull order and write-back on a mock KeyFrame/MapPoint graph."""
+    exe = _compile(ROOT / "tests" / "native" / "local_ba_shim_check.cpp", BUILD / "local_ba_shim_check",
+                   ("-I" + str(ROOT / "include"), "-Wall", "-Werror"))
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "OK local_ba_shim_check" in r.stdout, r.stdout + r.stderr
+
+
 @pytest.mark.slow
 def test_sincos_exception_table_exhaustive():
     """All 1,135,869,952 float angles in [0, 360): deterministic sincos + table == glibc offsets."""
