@@ -78,6 +78,15 @@ def test_local_ba_shim_on_mock_graph():
     assert r.returncode == 0 and "OK local_ba_shim_check" in r.stdout, r.stdout + r.stderr
 
 
+def test_matcher_shim_on_mock_objects():
+    """include/orbgpu_matcher.hpp (ORBmatcher drop-in): the flat views built from KeyFrame / Frame /
+    MapPoint objects and the writes back into vMatchedPairs and mvpMapPoints, against ABI test doubles."""
+    exe = _compile(ROOT / "tests" / "native" / "matcher_shim_check.cpp", BUILD / "matcher_shim_check",
+                   ("-I" + str(ROOT / "include"), "-Wall", "-Werror"))
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "OK matcher_shim_check" in r.stdout, r.stdout + r.stderr
+
+
 @pytest.mark.slow
 def test_sincos_exception_table_exhaustive():
     """All 1,135,869,952 float angles in [0, 360): deterministic sincos + table == glibc offsets."""
