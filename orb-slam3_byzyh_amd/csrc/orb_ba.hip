@@ -50,7 +50,6 @@
 namespace {
 
 constexpr int kT = 256;
-constexpr int kCholThreads = 512;
 
 struct EdgeDev {  // == orb_ba_edge_t
     int32_t point, pose, stereo;
@@ -420,177 +419,7 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     return __longlong_as_double(((uint64_t)hi << 32) | lo);
 }
 
-// Dense Cholesky S = L L^T and the solves L y = b, L^T x = y in one workgroup (512 threads).
-// Left-looking by panels of NB columns: the panel S[k0:n, k0:k0+NB] is staged in LDS and updated
-// with the L rows computed so far (L is kept transposed, LT[j*n + i] = L[i][j], so that column j
-// of L -- what every panel update streams -- is contiguous and the loads coalesce over rows);
-// wave 0 factors the NB x NB diagonal block in registers (lane r = row r, cross-lane reads through
-// v_readlane); all threads then solve the panel rows against it.  LDS: the NB rows of L above
-// the panel (NB x n), the panel (n x (NB+1)) and y (n).
-template <int NB>
-__global__ __launch_bounds__(kCholThreads) void k_ba_chol(int n, const double* __restrict__ S, double* __restrict__ LT,
-                                                          const double* __restrict__ b, double* __restrict__ x,
-                                                          int32_t* __restrict__ status) {
-    extern __shared__ double lds[];
-    double* Lk = lds;                      // [NB][n]: Lk[c*n + j] = L[k0 + c][j], j < k0
-    double* A = Lk + (size_t)NB * n;       // [n][NB + 1]: panel rows
-    double* y = A + (size_t)n * (NB + 1);  // [n]
-    __shared__ double Lkk[NB][NB + 1];
-    __shared__ int fail;
-    const int tid = threadIdx.x;
-    for (int i = tid; i < n; i += kCholThreads) y[i] = b[i];
-    if (tid == 0) fail = 0;
-    for (int k0 = 0; k0 < n; k0 += NB) {
-        const int kb = min(NB, n - k0), m = n - k0;
-        __syncthreads();
-        for (int t = tid; t < NB * k0; t += kCholThreads) {
-            const int c = t % NB, j = t / NB;
-            Lk[(size_t)c * n + j] = c < kb ? LT[(size_t)j * n + k0 + c] : 0.0;
-        }
-        for (int t = tid; t < m * NB; t += kCholThreads) {
-            const int c = t % NB, i = t / NB;
-            A[(size_t)i * (NB + 1) + c] = c < kb ? S[(size_t)(k0 + i) * n + k0 + c] : 0.0;
-        }
-        __syncthreads();
-        // ---- panel update: A[i][c] -= sum_{j < k0} L[k0 + i][j] L[k0 + c][j]; 2 rows x 4 columns per item
-        const int npair = (m + 1) / 2;
-        for (int t = tid; t < npair * (NB / 4); t += kCholThreads) {
-            const int rp = t % npair, cg = t / npair;
-            const int i0 = 2 * rp, c0 = 4 * cg;
-            const bool two = i0 + 1 < m;
-            double acc[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-            const double* col = LT + k0 + i0;
-            const double* l0 = Lk + (size_t)c0 * n;
-#pragma unroll 16
-            for (int j = 0; j < k0; ++j) {
-                const double a0 = col[(size_t)j * n];
-                const double a1 = two ? col[(size_t)j * n + 1] : 0.0;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const double l = l0[(size_t)c * n + j];
-                    acc[0][c] += a0 * l;
-                    acc[1][c] += a1 * l;
-                }
-            }
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                A[(size_t)i0 * (NB + 1) + c0 + c] -= acc[0][c];
-                if (two) A[(size_t)(i0 + 1) * (NB + 1) + c0 + c] -= acc[1][c];
-            }
-        }
-        __syncthreads();
-        // ---- diagonal block (wave 0): lane r holds row r, identity padding beyond kb
-        if (tid < 64) {
-            const int r = tid;
-            double row[NB];
-#pragma unroll
-            for (int c = 0; c < NB; ++c)
-                row[c] = (r < kb && c < kb) ? A[(size_t)r * (NB + 1) + c] : (r == c ? 1.0 : 0.0);
-            bool bad = false;
-#pragma unroll
-            for (int c = 0; c < NB; ++c) {
-                const double piv = readlane_d(row[c], c);
-                bad |= !(piv > 0.0);
-                const double lcc = sqrt(piv);
-                if (r == c) row[c] = lcc;
-                else if (r > c) row[c] = row[c] / lcc;
-#pragma unroll
-                for (int j = c + 1; j < NB; ++j) {
-                    const double ljc = readlane_d(row[c], j);
-                    if (r >= j) row[j] -= row[c] * ljc;
-                }
-            }
-            if (r < NB) {
-#pragma unroll
-                for (int c = 0; c < NB; ++c) {
-                    Lkk[r][c] = c <= r ? row[c] : 0.0;
-                    A[(size_t)r * (NB + 1) + c] = c <= r ? row[c] : 0.0;
-                }
-            }
-            if (r == 0 && bad) fail = 1;
-        }
-        __syncthreads();
-        // ---- panel rows below the diagonal block: solve x L_kk^T = a
-        for (int i = kb + tid; i < m; i += kCholThreads) {
-            asm volatile("" ::: "memory");  // keep the L_kk reads inside the loop (no LICM into 136 registers)
-            double v[NB];
-#pragma unroll
-            for (int c = 0; c < NB; ++c) v[c] = A[(size_t)i * (NB + 1) + c];
-#pragma unroll
-            for (int c = 0; c < NB; ++c) {
-                double s = v[c];
-#pragma unroll
-                for (int k = 0; k < c; ++k) s -= v[k] * Lkk[c][k];
-                v[c] = c < kb ? s / Lkk[c][c] : 0.0;
-            }
-#pragma unroll
-            for (int c = 0; c < NB; ++c) A[(size_t)i * (NB + 1) + c] = v[c];
-        }
-        __syncthreads();
-        // ---- write the panel: LT[(k0 + c) * n + k0 + i] = L[k0 + i][k0 + c]
-        for (int t = tid; t < m * kb; t += kCholThreads) {
-            const int i = t % m, c = t / m;
-            LT[(size_t)(k0 + c) * n + k0 + i] = A[(size_t)i * (NB + 1) + c];
-        }
-    }
-    __syncthreads();
-    // ---- forward: L y = b
-    for (int k0 = 0; k0 < n; k0 += NB) {
-        const int kb = min(NB, n - k0);
-        if (tid < 64) {
-            const int r = tid;
-            double lrow[NB];
-#pragma unroll
-            for (int c = 0; c < NB; ++c)
-                lrow[c] = (r < kb && c < kb && c <= r) ? LT[(size_t)(k0 + c) * n + k0 + r] : (r == c ? 1.0 : 0.0);
-            double yy = r < kb ? y[k0 + r] : 0.0;
-#pragma unroll
-            for (int c = 0; c < NB; ++c) {
-                const double yc = readlane_d(yy, c) / readlane_d(lrow[c], c);
-                if (r == c) yy = yc;
-                else if (r > c) yy -= lrow[c] * yc;
-            }
-            if (r < kb) y[k0 + r] = yy;
-        }
-        __syncthreads();
-        for (int i = k0 + kb + tid; i < n; i += kCholThreads) {
-            double s = 0;
-            for (int c = 0; c < kb; ++c) s += LT[(size_t)(k0 + c) * n + i] * y[k0 + c];
-            y[i] -= s;
-        }
-        __syncthreads();
-    }
-    // ---- backward: L^T x = y
-    for (int k0 = ((n - 1) / NB) * NB; k0 >= 0; k0 -= NB) {
-        const int kb = min(NB, n - k0);
-        if (tid < 64) {
-            const int c = tid;  // lane c holds column c of L_kk
-            double col[NB];
-#pragma unroll
-            for (int r = 0; r < NB; ++r)
-                col[r] = (r < kb && c < kb && r >= c) ? LT[(size_t)(k0 + c) * n + k0 + r] : (r == c ? 1.0 : 0.0);
-            double yy = c < kb ? y[k0 + c] : 0.0;
-#pragma unroll
-            for (int r = NB - 1; r >= 0; --r) {
-                const double xr = readlane_d(yy, r) / readlane_d(col[r], r);
-                if (c == r) yy = xr;
-                else if (c < r) yy -= col[r] * xr;
-            }
-            if (c < kb) y[k0 + c] = yy;
-        }
-        __syncthreads();
-        for (int j = tid; j < k0; j += kCholThreads) {
-            double s = 0;
-            for (int c = 0; c < kb; ++c) s += LT[(size_t)j * n + k0 + c] * y[k0 + c];
-            y[j] -= s;
-        }
-        __syncthreads();
-    }
-    for (int i = tid; i < n; i += kCholThreads) x[i] = y[i];
-    if (tid == 0) *status = fail;
-}
-
-// ---- register-resident MFMA Cholesky + solve (n <= 288, one workgroup of 8 waves) ------------------
+// ---- register-resident MFMA Cholesky + solve (n <= 288, one workgroup of 12 waves) -----------------
 // The lower triangle of S is cut into 16x16 tiles that live in the waves' registers for the whole
 // factorisation.  Each tile holds M in the operand layout O(M) of v_mfma_f64_16x16x4_f64: lane l,
 // register q = M[l & 15][(l >> 4) + 4q].  That is the C/D layout of M^T, so with tiles kept
@@ -598,18 +427,22 @@ __global__ __launch_bounds__(kCholThreads) void k_ba_chol(int n, const double* _
 // lane-linear LDS read:
 //   trailing update  M_ij^T -= L_jk L_ik^T      A = O(L_jk) negated (blgp = neg A), B = O(L_ik)
 //   panel            L_ik^T  = L_kk^-1 A_ik^T   A = O(L_kk^-1), B = the tile itself
-// Right-looking over the 16-column block steps k.  The owner of tile (k, k) factors it in one
-// wave (lane r = row r, cross-lane reads through v_readlane) and inverts L_kk, with a look-ahead:
-// it updates tile (k+1, k+1) first in step k and factors it while the other waves finish their
-// updates.  The forward solve is folded in (y_k = L_kk^-1 b_k, then b_i -= L_ik y_k by the panel
+// Right-looking over the 16-column block steps k.  One wave factors tile (k, k) (lane r = row r,
+// cross-lane reads through DPP row broadcasts) and inverts L_kk, with a look-ahead: tile (k+1, k+1)
+// is updated first in step k and factored while the other waves finish their updates.  The forward solve is folded in (y_k = L_kk^-1 b_k, then b_i -= L_ik y_k by the panel
 // owners); the backward solve walks the tile rows kept in registers, pipelined through LDS
 // flags: the diagonal wave publishes x_k once every L_kj^T x_j contribution has landed.  Tiles are dealt round-robin
 // in order of decreasing column, so the active tiles of every step are a prefix of each wave's
 // slots and the load stays balanced as the trailing matrix shrinks.  Every sum has a fixed order.
 typedef double f64x4 __attribute__((ext_vector_type(4)));
-constexpr int kMfTileWaves = 7, kMf2TileWaves = 11, kMfMaxNT = 18;
-constexpr size_t kMfLds =
-    sizeof(double) * (2 * (size_t)kMfMaxNT * 256 + 16 * 17 + 2 * 16 * kMfMaxNT + 16 * kMfMaxNT * (kMfMaxNT - 1) / 2);
+constexpr int kMf2TileWaves = 11, kMfMaxNT = 18;
+// ORBGPU_BA_TRACE stamps (int64 clock64, kTraceLen entries): step k, wave w, point p at
+// kTrStep + (k * 16 + w) * 4 + p (w = kMf2TileWaves is the diagonal wave); backward step j at
+// kTrBack + j (start), kTrWaited + j (contributions in), kTrPub + j (x_j published); the diagonal
+// factorisation of step k at kTrDiag + 4 k + {0: start, 1: factored, 2: L^-1 stored, 3: y_k}.
+constexpr int kTrStep = 0, kTrEnd = 1199, kTrBack = 1200, kTrWaited = 1300, kTrPub = 1400, kTrDiag = 1500,
+              kTraceLen = 2048;
+static_assert(kTrStep + (kMfMaxNT * 16) * 4 <= kTrEnd && kTrDiag + 4 * kMfMaxNT <= kTraceLen, "trace layout");
 
 template <int N>
 __device__ __forceinline__ double dpp_row_shr(double v) {  // lane l <- lane l - N of its 16-lane row, 0 at the edge
@@ -646,7 +479,7 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
 // One wave: factor the 16x16 block in dk (row-major, stride 17) and write L_kk^-1 in operand layout
 // to linv_k; replace yk[0 .. 16) (= b_k, already reduced by the earlier panels) by y_k = L_kk^-1 b_k.
 // Lane r holds row r of the block and column r of L^-1.  Column step c: one rsqrt, then the values
-// L[j][c] (j > c) are broadcast once (v_readlane) and feed both the rank-1 update of the block and
+// L[j][c] (j > c) are broadcast once and feed both the rank-1 update of the block and
 // the substitution step of L^-1 (x_i -= L[i][c] x_c).  The updates run unconditionally: entries
 // above the diagonal collect garbage that is never read.
 // kColMajor: L^-1 stored column-major with stride 17 (L^-1[i][c] at c * 17 + i: conflict-free for the
@@ -671,10 +504,9 @@ __device__ __forceinline__ double row_bcast16(double v, int j) {
     return __longlong_as_double(((uint64_t)(uint32_t)rh << 32) | (uint32_t)rl);
 }
 
-// kDpp: the column values L[j][c] reach the other rows by DPP row broadcasts (every 16-lane row
-// holds the same block, so each row broadcasts within itself); otherwise by v_readlane.  Same
-// arithmetic, same results.
-template <bool kColMajor = false, bool kDpp = false>
+// The column values L[j][c] reach the other rows by DPP row broadcasts (every 16-lane row holds the
+// same block, so each row broadcasts within itself).
+template <bool kColMajor = false>
 __device__ __forceinline__ void mf_diag(double* __restrict__ dk, double* __restrict__ linv_k,
                                         double* __restrict__ yk, int lane, int* fail, int64_t* tr = nullptr) {
     if (tr && lane == 0) tr[0] = clock64();
@@ -688,20 +520,20 @@ __device__ __forceinline__ void mf_diag(double* __restrict__ dk, double* __restr
     bool bad = false;
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
-        const double piv = kDpp ? row_bcast16(row[c], c) : readlane_d(row[c], c);
+        const double piv = row_bcast16(row[c], c);
         bad |= !(piv > 0.0);
         const double inv = rsqrt_nr(piv);  // 1 / L[c][c]
         const double lrc = row[c] * inv;    // L[r][c] for r > c
         xc[c] *= inv;                       // x_c of column r of L^-1
 #pragma unroll
         for (int j = c + 1; j < 16; ++j) {
-            const double ljc = kDpp ? row_bcast16(lrc, j) : readlane_d(lrc, j);
+            const double ljc = row_bcast16(lrc, j);
             row[j] = __builtin_fma(-lrc, ljc, row[j]);
             xc[j] = __builtin_fma(-ljc, xc[c], xc[j]);
-            if (kDpp) asm volatile("" : "+v"(row[j]), "+v"(xc[j]));  // computed here: one broadcast live at a time
+            asm volatile("" : "+v"(row[j]), "+v"(xc[j]));  // computed here: one broadcast live at a time
         }
     }
-    if (kDpp) bad = __ballot(bad) != 0;
+    bad = __ballot(bad) != 0;
     if (lane == 0 && bad) *fail = 1;
     if (tr && lane == 0) tr[1] = clock64();
     if (lane < 16) {
@@ -723,212 +555,8 @@ __device__ __forceinline__ void mf_diag(double* __restrict__ dk, double* __restr
     if (tr && lane == 0) tr[3] = clock64();
 }
 
-template <int W>  // W tile waves + one wave for the diagonal blocks
-__global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mfma(int n, const double* __restrict__ S,
-                                                               const double* __restrict__ b, double* __restrict__ x,
-                                                               int32_t* __restrict__ status,
-                                                               int64_t* __restrict__ trace,
-        const LmState* __restrict__ lm_st, int lm_gk) {
-    if (lm_skip(lm_st, lm_gk)) return;
-    // trace (debug, ORBGPU_BA_TRACE): clock64 stamps [(k * 8 + wave) * 4 + point], backward at [600 + k]
-#define MF_STAMP(k_, pt_) \
-    if (trace && lane == 0) trace[((k_) * 8 + w) * 4 + (pt_)] = clock64()
-    constexpr int SL = (kMfMaxNT * (kMfMaxNT + 1) / 2 + W - 1) / W;
-    extern __shared__ double lds[];
-    double* pan = lds;                    // [NT][4][64] panel tiles O(L_ik)
-    double* linv = pan + kMfMaxNT * 256;  // [NT][4][64] O(L_kk^-1)
-    double* dk = linv + kMfMaxNT * 256;   // [16][17] diagonal block scratch (+ 1/L_rr)
-    double* yv = dk + 16 * 17;            // [16 NT] b -> y (forward) -> updated y (backward)
-    double* xv = yv + 16 * kMfMaxNT;      // [16 NT] x
-    double* contrib = xv + 16 * kMfMaxNT;  // [k (k - 1) / 2 + j][16]: L_kj^T x_k, one slot per tile (k > j)
-    __shared__ int fail, ready, xready, cnt[kMfMaxNT];
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int NT = (n + 15) >> 4, ntt = NT * (NT + 1) / 2;
-    const int r16 = lane & 15, g4 = lane >> 4;
-    if (w == W) {
-        // ---- the diagonal wave: b -> yv, block (0, 0), then block k + 1 during step k's updates
-        for (int i = lane; i < 16 * NT; i += 64) yv[i] = i < n ? b[i] : 0.0;
-        for (int t = lane; t < 256; t += 64) {
-            const int r = t >> 4, c = t & 15;
-            dk[r * 17 + c] = (r < n && c < n) ? S[(size_t)r * n + c] : (r == c ? 1.0 : 0.0);
-        }
-        if (lane == 0) {
-            fail = 0;
-            ready = 0;
-            xready = NT;
-        }
-        if (lane < kMfMaxNT) cnt[lane] = 0;
-        mf_wave_sync();
-        mf_diag(dk, linv, yv, lane, &fail);
-        __syncthreads();  // S0
-        for (int k = 0; k + 1 < NT; ++k) {
-            __syncthreads();  // S1(k): panel k applied to yv
-            MF_STAMP(k, 1);
-            for (int spin = 0; __hip_atomic_load(&ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < k + 1;
-                 ++spin) {
-                if (spin > (1 << 22)) {  // bounded: a missing hand-off fails the solve instead of hanging
-                    if (lane == 0) fail = 2;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            MF_STAMP(k, 2);
-            mf_diag(dk, linv + (k + 1) * 256, yv + 16 * (k + 1), lane, &fail, trace ? trace + 700 + 4 * k : nullptr);
-            MF_STAMP(k, 3);
-            __syncthreads();  // S2(k)
-        }
-        __syncthreads();  // S1(NT - 1)
-        __syncthreads();  // S2(NT - 1)
-        // ---- backward, producer side: x_j once all L_kj^T x_k (k > j) have landed, summed in fixed order
-        for (int j = NT - 1; j >= 0; --j) {
-            if (trace && lane == 0) trace[600 + j] = clock64();
-            for (int spin = 0; __hip_atomic_load(&cnt[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NT - 1 - j;
-                 ++spin) {
-                if (spin > (1 << 22)) {
-                    if (lane == 0) fail = 3;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            double yj = yv[16 * j + r16];
-            for (int kk = NT - 1; kk > j; --kk) yj -= contrib[(kk * (kk - 1) / 2 + j) * 16 + r16];
-            mf_wave_sync();
-            if (lane < 16) yv[16 * j + r16] = yj;
-            mf_wave_sync();
-            const double* lj = linv + j * 256;
-            double v4[4] = {0.0, 0.0, 0.0, 0.0};  // x_j[c] = sum_r L^-1[r][c] y_j[r], c = lane & 15
-#pragma unroll
-            for (int rr = 0; rr < 16; ++rr)
-                v4[rr & 3] = __builtin_fma(lj[(r16 >> 2) * 64 + rr + 16 * (r16 & 3)], yv[16 * j + rr], v4[rr & 3]);
-            if (lane < 16) xv[16 * j + r16] = (v4[0] + v4[1]) + (v4[2] + v4[3]);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (lane == 0) __hip_atomic_store(&xready, j, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-    } else {
-        // ---- tile waves: slot s holds tile t = s W + w (packed i | j << 8), -1 when empty
-        int tij[SL];
-        f64x4 T[SL];
-#pragma unroll
-        for (int s = 0; s < SL; ++s) {
-            const int t = s * W + w;
-            tij[s] = -1;
-            T[s] = f64x4{0.0, 0.0, 0.0, 0.0};
-            if (t < ntt) {
-                int c = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
-                while ((c + 1) * (c + 2) / 2 <= t) ++c;
-                while (c * (c + 1) / 2 > t) --c;
-                const int j = NT - 1 - c, i = j + (t - c * (c + 1) / 2);
-                tij[s] = i | (j << 8);
-                double e[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {  // S symmetric: read as S[col block][row block], coalesced
-                    const int row = 16 * j + g4 + 4 * q, col = 16 * i + r16;
-                    const double v = S[(size_t)min(row, n - 1) * n + min(col, n - 1)];  // branch-free
-                    e[q] = (row < n && col < n) ? v : (row == col ? 1.0 : 0.0);
-                }
-                T[s] = f64x4{e[0], e[1], e[2], e[3]};
-            }
-        }
-        __syncthreads();  // S0
-        for (int k = 0; k < NT; ++k) {
-            MF_STAMP(k, 0);
-            // ---- panel: L_ik = A_ik L_kk^-T for the tiles (i > k, k); forward b_i -= L_ik y_k
-            const double* lk = linv + k * 256;
-#pragma unroll
-            for (int s = 0; s < SL; ++s) {
-                int v = tij[s];
-                asm volatile("" : "+s"(v));  // no per-slot addresses hoisted out of the k loop
-                const int i = v & 255, j = v >> 8;
-                if (v >= 0 && j == k && i > k) {
-                    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(lk[q * 64 + lane], T[s][q], acc, 0, 0, 0);
-                    T[s] = acc;
-                    double part = 0.0;  // forward: b_i -= L_ik y_k (this tile is the only writer of b_i in step k)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        pan[i * 256 + q * 64 + lane] = acc[q];
-                        part = __builtin_fma(acc[q], yv[16 * k + g4 + 4 * q], part);
-                    }
-                    part += __shfl_xor(part, 16);
-                    part += __shfl_xor(part, 32);
-                    if (lane < 16) yv[16 * i + lane] -= part;
-                }
-            }
-            __syncthreads();  // S1(k)
-            MF_STAMP(k, 1);
-            // (no early exit at k = NT - 1: a break here keeps a second copy of every tile live)
-            // ---- trailing update of the tiles (i, j), j > k; tile (k+1, k+1) first, handed to the diagonal wave
-#pragma unroll
-            for (int s = 0; s < SL; ++s)
-                if (tij[s] == ((k + 1) | ((k + 1) << 8))) {  // (the one slot that matches)
-                    const double* pk = pan + (k + 1) * 256;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        T[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(pk[q * 64 + lane], pk[q * 64 + lane], T[s], 0, 0, 1);
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) dk[r16 * 17 + g4 + 4 * q] = T[s][q];
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    if (lane == 0) __hip_atomic_store(&ready, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-#pragma unroll
-            for (int s = 0; s < SL; ++s) {
-                int v = tij[s];
-                asm volatile("" : "+s"(v));  // no per-slot addresses hoisted out of the k loop
-                const int i = v & 255, j = v >> 8;
-                if (v >= 0 && j > k && !(i == k + 1 && j == k + 1)) {
-                    const double* pi = pan + i * 256;
-                    const double* pj = pan + j * 256;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        T[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(pj[q * 64 + lane], pi[q * 64 + lane], T[s], 0, 0, 1);
-                }
-            }
-            MF_STAMP(k, 3);
-            __syncthreads();  // S2(k)
-        }
-        // ---- backward, consumer side: row k's tiles contribute L_kj^T x_k as soon as x_k is out
-        for (int k = NT - 1; k >= 1; --k) {
-            bool mine = false;
-#pragma unroll
-            for (int s = 0; s < SL; ++s) mine |= tij[s] >= 0 && (tij[s] & 255) == k && (tij[s] >> 8) < k;
-            if (!mine) continue;
-            for (int spin = 0; __hip_atomic_load(&xready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) > k;
-                 ++spin) {
-                if (spin > (1 << 22)) break;
-                __builtin_amdgcn_s_sleep(1);
-            }
-            const double xr = xv[16 * k + r16];
-#pragma unroll
-            for (int s = 0; s < SL; ++s) {
-                int v = tij[s];
-                asm volatile("" : "+s"(v));
-                const int i = v & 255, j = v >> 8;
-                if (v >= 0 && i == k && j < k) {
-                    double* cs = contrib + (k * (k - 1) / 2 + j) * 16;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const double o = row16_sum(T[s][q] * xr);  // sum_r L_kj[r][c] x_k[r], c = g4 + 4q
-                        if (r16 == 15) cs[g4 + 4 * q] = o;
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    if (lane == 0) __hip_atomic_fetch_add(&cnt[j], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-            }
-        }
-    }
-    __syncthreads();  // x complete
-    for (int i = threadIdx.x; i < n; i += (W + 1) * 64) x[i] = xv[i];
-    if (threadIdx.x == 0) *status = fail;
-    if (trace && threadIdx.x == 0) trace[640] = clock64();
-#undef MF_STAMP
-}
-
 // ---- v2: the diagonal wave carries the whole critical chain ----------------------------------------
-// Same tiles, layouts and arithmetic as k_ba_chol_mfma, rescheduled so that the sequential part
-// of every step runs in one wave without workgroup barriers:
+// The sequential part of every step runs in one wave without workgroup barriers:
 //   diagonal wave, step k: wait for the "pre" tiles A_{k+1,k}, P_{k+1,k+1} (updated through panel
 //   k-1, published by their owners in LDS); L_{k+1,k} = A L_kk^-T (4 MFMAs), b_{k+1} -= L y_k,
 //   P -= L L^T (4 MFMAs), factor P (mf_diag), publish L_{k+1,k+1}^-1 and y_{k+1} (flag lk).
@@ -951,7 +579,7 @@ __device__ __forceinline__ void lds_flag_wait(int* f, int target, int lane, int*
     }
 }
 
-template <int W, bool kDpp = true>
+template <int W>
 __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const double* __restrict__ S,
                                                               const double* __restrict__ b, double* __restrict__ x,
                                                               int32_t* __restrict__ status, int64_t* __restrict__ trace,
@@ -992,13 +620,13 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
             dk[r * 17 + c] = (r < n && c < n) ? S[(size_t)r * n + c] : (r == c ? 1.0 : 0.0);
         }
         mf_wave_sync();
-        mf_diag<true, kDpp>(dk, linv, yv, lane, &fail);
+        mf_diag<true>(dk, linv, yv, lane, &fail);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) __hip_atomic_store(&lk, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         for (int k = 0; k + 1 < NT; ++k) {
-            if (trace && lane == 0) trace[(k * 8 + W) * 4 + 1] = clock64();
+            if (trace && lane == 0) trace[kTrStep + (k * 16 + W) * 4 + 1] = clock64();
             lds_flag_wait(&pre_ready[k], 2, lane, &fail, 2);
-            if (trace && lane == 0) trace[(k * 8 + W) * 4 + 2] = clock64();
+            if (trace && lane == 0) trace[kTrStep + (k * 16 + W) * 4 + 2] = clock64();
             const double* A = pre + (k & 1) * 512;
             const double* P = A + 256;
             const double* lkk = linv + k * 272;
@@ -1020,85 +648,56 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
             part += __shfl_xor(part, 32);
             if (lane < 16) yv[16 * (k + 1) + lane] -= part;  // b_{k+1} -= L_{k+1,k} y_k
             mf_wave_sync();
-            mf_diag<true, kDpp>(dk, linv + (k + 1) * 272, yv + 16 * (k + 1), lane, &fail, trace ? trace + 700 + 4 * k : nullptr);
+            mf_diag<true>(dk, linv + (k + 1) * 272, yv + 16 * (k + 1), lane, &fail, trace ? trace + kTrDiag + 4 * k : nullptr);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_store(&lk, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (trace && lane == 0) trace[(k * 8 + W) * 4 + 3] = clock64();
+            if (trace && lane == 0) trace[kTrStep + (k * 16 + W) * 4 + 3] = clock64();
         }
         // backward: x_j = L_jj^-T (y_j - sum_{k >= j+2} c_kj - L_{j+1,j}^T x_{j+1})
-        if (kDpp) {
-            // The chain x_{j+1} -> x_j stays in registers: x_{j+1} and y_j reach the other lanes of a
-            // row by DPP broadcasts, and both 16x16 operands (L_{j+1,j} row r, L_jj^-1 column r) are
-            // loaded before the wait for the contributions.  Same operations and order as below.
-            double xn = 0.0;  // x_{j+1}[r16]
-            for (int j = NT - 1; j >= 0; --j) {
-                if (trace && lane == 0) trace[600 + j] = clock64();
-                const double* L = sub + j * 256;  // L_{j+1,j}[r][c] at [(c >> 2) * 64 + r + 16 (c & 3)]
-                const double* lj = linv + j * 272;
-                double lr[16], li[16];
+        // The chain x_{j+1} -> x_j stays in registers: x_{j+1} and y_j reach the other lanes of a
+        // row by DPP broadcasts, and both 16x16 operands (L_{j+1,j} row r, L_jj^-1 column r) are
+        // loaded before the wait for the contributions.
+        double xn = 0.0;  // x_{j+1}[r16]
+        for (int j = NT - 1; j >= 0; --j) {
+            if (trace && lane == 0) trace[kTrBack + j] = clock64();
+            const double* L = sub + j * 256;  // L_{j+1,j}[r][c] at [(c >> 2) * 64 + r + 16 (c & 3)]
+            const double* lj = linv + j * 272;
+            double lr[16], li[16];
 #pragma unroll
-                for (int rr = 0; rr < 16; ++rr) {
-                    lr[rr] = j + 1 < NT ? L[(r16 >> 2) * 64 + rr + 16 * (r16 & 3)] : 0.0;
-                    li[rr] = lj[r16 * 17 + rr];
-                }
-                lds_flag_wait(&cnt[j], NT - 2 - j, lane, &fail, 3);
-                if (trace && lane == 0) trace[800 + j] = clock64();
-                double yj = yv[16 * j + r16];
-                {  // every contribution load issued at once, subtracted in the same order (kk descending);
-                   // the missing ones are +0.0, which leaves yj unchanged bit for bit
-                    double cv[kMfMaxNT];
-#pragma unroll
-                    for (int m = 0; m < kMfMaxNT; ++m) {
-                        const int kk = NT - 1 - m;
-                        const bool have = kk >= j + 2;  // (load unconditionally from a valid slot: no branch per load)
-                        const double v = contrib[(have ? kk * (kk - 1) / 2 + j : 0) * 16 + r16];
-                        cv[m] = have ? v : 0.0;
-                    }
-#pragma unroll
-                    for (int m = 0; m < kMfMaxNT; ++m) yj -= cv[m];
-                }
-                if (j + 1 < NT) {
-                    double t4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                    for (int rr = 0; rr < 16; ++rr) t4[rr & 3] = __builtin_fma(lr[rr], row_bcast16(xn, rr), t4[rr & 3]);
-                    yj -= (t4[0] + t4[1]) + (t4[2] + t4[3]);
-                }
-                double v4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                for (int rr = 0; rr < 16; ++rr) v4[rr & 3] = __builtin_fma(li[rr], row_bcast16(yj, rr), v4[rr & 3]);
-                xn = (v4[0] + v4[1]) + (v4[2] + v4[3]);
-                if (lane < 16) xv[16 * j + r16] = xn;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                if (lane == 0) __hip_atomic_store(&xready, NT - j, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (trace && lane == 0) trace[830 + j] = clock64();
+            for (int rr = 0; rr < 16; ++rr) {
+                lr[rr] = j + 1 < NT ? L[(r16 >> 2) * 64 + rr + 16 * (r16 & 3)] : 0.0;
+                li[rr] = lj[r16 * 17 + rr];
             }
-        } else {
-            for (int j = NT - 1; j >= 0; --j) {
-                if (trace && lane == 0) trace[600 + j] = clock64();
-                lds_flag_wait(&cnt[j], NT - 2 - j, lane, &fail, 3);
-                if (trace && lane == 0) trace[800 + j] = clock64();
-                double yj = yv[16 * j + r16];
-                for (int kk = NT - 1; kk >= j + 2; --kk) yj -= contrib[(kk * (kk - 1) / 2 + j) * 16 + r16];
-                if (j + 1 < NT) {
-                    const double* L = sub + j * 256;  // L_{j+1,j}[r][c] at [(c >> 2) * 64 + r + 16 (c & 3)]
-                    double t4[4] = {0.0, 0.0, 0.0, 0.0};
-    #pragma unroll
-                    for (int rr = 0; rr < 16; ++rr)
-                        t4[rr & 3] = __builtin_fma(L[(r16 >> 2) * 64 + rr + 16 * (r16 & 3)], xv[16 * (j + 1) + rr], t4[rr & 3]);
-                    yj -= (t4[0] + t4[1]) + (t4[2] + t4[3]);
+            lds_flag_wait(&cnt[j], NT - 2 - j, lane, &fail, 3);
+            if (trace && lane == 0) trace[kTrWaited + j] = clock64();
+            double yj = yv[16 * j + r16];
+            {  // every contribution load issued at once, subtracted in the same order (kk descending);
+               // the missing ones are +0.0, which leaves yj unchanged bit for bit
+                double cv[kMfMaxNT];
+#pragma unroll
+                for (int m = 0; m < kMfMaxNT; ++m) {
+                    const int kk = NT - 1 - m;
+                    const bool have = kk >= j + 2;  // (load unconditionally from a valid slot: no branch per load)
+                    const double v = contrib[(have ? kk * (kk - 1) / 2 + j : 0) * 16 + r16];
+                    cv[m] = have ? v : 0.0;
                 }
-                mf_wave_sync();
-                if (lane < 16) yv[16 * j + r16] = yj;
-                mf_wave_sync();
-                const double* lj = linv + j * 272;
-                double v4[4] = {0.0, 0.0, 0.0, 0.0};
-    #pragma unroll
-                for (int rr = 0; rr < 16; ++rr) v4[rr & 3] = __builtin_fma(lj[r16 * 17 + rr], yv[16 * j + rr], v4[rr & 3]);
-                if (lane < 16) xv[16 * j + r16] = (v4[0] + v4[1]) + (v4[2] + v4[3]);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                if (lane == 0) __hip_atomic_store(&xready, NT - j, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (trace && lane == 0) trace[830 + j] = clock64();
+#pragma unroll
+                for (int m = 0; m < kMfMaxNT; ++m) yj -= cv[m];
             }
+            if (j + 1 < NT) {
+                double t4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int rr = 0; rr < 16; ++rr) t4[rr & 3] = __builtin_fma(lr[rr], row_bcast16(xn, rr), t4[rr & 3]);
+                yj -= (t4[0] + t4[1]) + (t4[2] + t4[3]);
+            }
+            double v4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int rr = 0; rr < 16; ++rr) v4[rr & 3] = __builtin_fma(li[rr], row_bcast16(yj, rr), v4[rr & 3]);
+            xn = (v4[0] + v4[1]) + (v4[2] + v4[3]);
+            if (lane < 16) xv[16 * j + r16] = xn;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) __hip_atomic_store(&xready, NT - j, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (trace && lane == 0) trace[kTrPub + j] = clock64();
         }
     } else {
         // ---------------- tile waves: slot s holds tile t = s W + w (packed i | j << 8) ----------------
@@ -1140,7 +739,7 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
         auto Tc = [&](int k) { return (NT - 1 - k) * (NT - k) / 2; };
         auto slot_lo = [&](int t) { return t <= w ? 0 : (t - w + W - 1) / W; };  // first s with s W + w >= t
         for (int k = 0; k + 1 < NT; ++k) {
-            if (trace && lane == 0) trace[(k * 8 + w) * 4] = clock64();
+            if (trace && lane == 0) trace[kTrStep + (k * 16 + w) * 4] = clock64();
             lds_flag_wait(&lk, k, lane, &fail, 4);
             double* pk = pan + (k & 1) * kMfMaxNT * 256;
             const double* lkk = linv + k * 272;
@@ -1175,7 +774,7 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_fetch_add(&tbar, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             lds_flag_wait(&tbar, W * (k + 1), lane, &fail, 5);
-            if (trace && lane == 0) trace[(k * 8 + w) * 4 + 1] = clock64();
+            if (trace && lane == 0) trace[kTrStep + (k * 16 + w) * 4 + 1] = clock64();
             // ---- trailing update with panel k.  The next step's pre tiles first: A = (k+2, k+1) is
             // t = Tc(k+1) + 1, P = (k+2, k+2) is t = Tc(k+2); the diagonal wave takes (k+1, k+1) = Tc(k+1).
             const int t_diag = Tc(k + 1);
@@ -1212,7 +811,7 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
                         T[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(pj[q * 64 + lane], pi[q * 64 + lane], T[s], 0, 0, 1);
                 }
             }
-            if (trace && lane == 0) trace[(k * 8 + w) * 4 + 3] = clock64();
+            if (trace && lane == 0) trace[kTrStep + (k * 16 + w) * 4 + 3] = clock64();
         }
         // every tile wave is past its last read of the panel buffers before contributions land there
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1262,6 +861,7 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
     __syncthreads();
     for (int i = threadIdx.x; i < n; i += (W + 1) * 64) x[i] = xv[i];
     if (threadIdx.x == 0) *status = fail;
+    if (trace && threadIdx.x == 0) trace[kTrEnd] = clock64();
 }
 
 // ---- tile-row Cholesky + solve over many workgroups (any n up to 16 x 256) ----------------------
@@ -1397,7 +997,7 @@ __global__ __launch_bounds__(kRowThreads) void k_ba_chol_rows(int n, const doubl
 #pragma unroll
         for (int q = 0; q < 4; ++q) dk[r16 * 17 + g4 + 4 * q] = Ti[q * 64 + lane];
         mf_wave_sync();
-        mf_diag<false, true>(dk, linv, rv, lane, &fail);
+        mf_diag<false>(dk, linv, rv, lane, &fail);
         mf_wave_sync();
         double* dst = lpub + ((size_t)i * NT + i) * 256;
 #pragma unroll
@@ -1447,263 +1047,6 @@ __global__ __launch_bounds__(kRowThreads) void k_ba_chol_rows(int n, const doubl
         *status = fail ? fail : (timeouts ? 6 : 0);
         cflag[0] = E;  // every row read the epoch before publishing, and this row consumed all of them
     }
-}
-
-// Cooperative multi-workgroup Cholesky + solve (the fast path for n <= 560 / 1100).
-// Right-looking by block columns of NB: workgroup w < nbc keeps block column w (rows j0..n) in LDS
-// for the whole factorisation; workgroup nbc owns the right-hand side.  Step k: the owner of
-// column k factors its diagonal block (wave 0, registers + v_readlane) and its panel rows and
-// publishes the panel to Lg (row-major L); after a grid barrier every later column applies the
-// panel's update to itself and the rhs owner runs the forward substitution of block k.  The rhs
-// owner finishes with the backward substitution L^T x = y from Lg.  One grid barrier per block
-// column; the matrix never makes a round trip through HBM between steps.
-constexpr int kCoopThreads = 256;
-
-// Cooperative multi-workgroup Cholesky + solve (n <= ~560 with NB = 32).  Workgroup w < nbc keeps
-// block column w (rows j0..n, NB columns) in LDS for the whole factorisation; workgroup nbc owns
-// the right-hand side.  Right-looking with a one-step look-ahead: after panel k is published, the
-// owner of column k+1 "finalizes" (applies panel k, factors its NB x NB diagonal block with a
-// one-wave LDS chain, inverts it, turns its panel rows into L rows with two GEMM passes, publishes
-// L and L_kk^-1), while every later column applies panel k and the rhs owner runs forward block k
-// as matrix-vector products with L_kk^-1.  One grid barrier per block column.
-template <int NB>
-struct CoopShared {
-    double Lkj[NB][NB + 1];   // rows of the current panel that fall in this block column
-    double Linv[NB][NB + 1];  // L_kk^-1 (lower)
-    double yb[NB];
-};
-
-// A[r][c] -= sum_q L[j0 + r][k0 + q] * Lkj[c][q] for r in [r_begin, rows), all NB columns; L rows
-// streamed from Lg (32 loads in flight per item), Lkj from LDS.  Items: (row, half of the columns).
-template <int NB>
-__device__ __forceinline__ void apply_panel(double* __restrict__ A, const double* __restrict__ Lg, int n, int j0,
-                                            int k0, int r_begin, int rows, const CoopShared<NB>& sh) {
-    constexpr int H = NB / 2;
-    const int items = (rows - r_begin) * 2;
-    for (int t = threadIdx.x; t < items; t += kCoopThreads) {
-        asm volatile("" ::: "memory");  // no LICM of the Lkj reads across items
-        const int r = r_begin + t / 2, c0 = H * (t % 2);
-        const double* lrow = Lg + (size_t)(j0 + r) * n + k0;
-        double l[NB];
-#pragma unroll
-        for (int q = 0; q < NB; ++q) l[q] = lrow[q];
-        double acc[H];
-#pragma unroll
-        for (int c = 0; c < H; ++c) acc[c] = 0;
-#pragma unroll
-        for (int q = 0; q < NB; ++q)
-#pragma unroll
-            for (int c = 0; c < H; ++c) acc[c] += l[q] * sh.Lkj[c0 + c][q];
-#pragma unroll
-        for (int c = 0; c < H; ++c) A[(size_t)r * (NB + 1) + c0 + c] -= acc[c];
-    }
-}
-
-template <int NB>
-__device__ __forceinline__ void coop_finalize(double* __restrict__ A, double* __restrict__ Lg, double* __restrict__ Linvg, int n,
-                              int w, int j0, int jb, int rows, CoopShared<NB>& sh, int32_t* __restrict__ status,
-                              int64_t* __restrict__ ft) {
-    const int tid = threadIdx.x;
-#define FT(i) if (ft && tid == 0) ft[i] = wall_clock64();
-    FT(0)
-    if (w > 0) {
-        const int k0 = j0 - NB;  // previous panel (always NB wide)
-        for (int t = tid; t < NB * NB; t += kCoopThreads) {
-            const int c = t / NB, q = t % NB;
-            sh.Lkj[c][q] = c < jb ? Lg[(size_t)(j0 + c) * n + k0 + q] : 0.0;
-        }
-        __syncthreads();
-        for (int t = tid; t < jb * jb; t += kCoopThreads) {  // diagonal block (lower)
-            const int r = t / jb, c = t % jb;
-            if (c > r) continue;
-            double acc = 0;
-#pragma unroll 8
-            for (int q = 0; q < NB; ++q) acc += sh.Lkj[r][q] * sh.Lkj[c][q];
-            A[(size_t)r * (NB + 1) + c] -= acc;
-        }
-        __syncthreads();
-    }
-    FT(1)
-    // ---- left-looking Cholesky of the diagonal block, one wave, lane i = row i
-    if (tid < 64) {
-        const int i = tid;
-        double Lrow[NB];
-        bool bad = false;
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-            Lrow[j] = 0.0;
-            if (j < jb) {
-                double d = A[(size_t)j * (NB + 1) + j], s = (i > j && i < jb) ? A[(size_t)i * (NB + 1) + j] : 0.0;
-#pragma unroll
-                for (int k = 0; k < j; ++k) {
-                    const double ljk = A[(size_t)j * (NB + 1) + k];
-                    d -= ljk * ljk;
-                    s -= Lrow[k] * ljk;
-                }
-                bad |= !(d > 0.0);
-                const double lj = sqrt(d), rl = 1.0 / lj;
-                if (i == j) {
-                    Lrow[j] = lj;
-                    A[(size_t)i * (NB + 1) + j] = lj;
-                } else if (i > j && i < jb) {
-                    Lrow[j] = s * rl;
-                    A[(size_t)i * (NB + 1) + j] = Lrow[j];
-                }
-                __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the row is visible to the next step
-                __builtin_amdgcn_wave_barrier();
-            }
-        }
-        if (i == 0 && bad) atomicOr(status, 1);
-        FT(2)
-        // ---- L_kk^-1: lane c solves L x = e_c (x_r = 0 for r < c)
-        const int c = i;
-        double xcol[NB];
-#pragma unroll
-        for (int r = 0; r < NB; ++r) {
-            double v = 0.0;
-            if (c < jb && r < jb && r >= c) {
-                double acc = (r == c) ? 1.0 : 0.0;
-#pragma unroll
-                for (int k = 0; k < r; ++k)
-                    if (k >= c) acc -= A[(size_t)r * (NB + 1) + k] * xcol[k];
-                v = acc / A[(size_t)r * (NB + 1) + r];
-            }
-            xcol[r] = v;
-        }
-        if (c < NB) {
-#pragma unroll
-            for (int r = 0; r < NB; ++r) sh.Linv[r][c] = xcol[r];
-        }
-    }
-    __syncthreads();
-    FT(3)
-    // ---- panel rows: apply the pending panel, then X = A L_kk^-T (two GEMM passes)
-    if (w > 0) {
-        apply_panel<NB>(A, Lg, n, j0, j0 - NB, jb, rows, sh);
-        __syncthreads();
-    }
-    FT(4)
-    for (int r = jb + tid; r < rows; r += kCoopThreads) {  // one row per thread: X[r] = A[r] L_kk^-T
-        asm volatile("" ::: "memory");
-        double a[NB];
-#pragma unroll
-        for (int q = 0; q < NB; ++q) a[q] = A[(size_t)r * (NB + 1) + q];
-#pragma unroll
-        for (int c = 0; c < NB; ++c) {
-            double acc = 0;
-#pragma unroll
-            for (int q = 0; q <= c; ++q) acc += a[q] * sh.Linv[c][q];
-            A[(size_t)r * (NB + 1) + c] = acc;
-        }
-    }
-    __syncthreads();
-    FT(5)
-    // ---- publish L rows of this block column and L_kk^-1
-    for (int t = tid; t < rows * jb; t += kCoopThreads) {
-        const int r = t / jb, c = t % jb;
-        Lg[(size_t)(j0 + r) * n + j0 + c] = (r < jb && c > r) ? 0.0 : A[(size_t)r * (NB + 1) + c];
-    }
-    for (int t = tid; t < NB * NB; t += kCoopThreads) Linvg[(size_t)w * NB * NB + t] = sh.Linv[t / NB][t % NB];
-    __threadfence();
-    FT(6)
-#undef FT
-}
-
-template <int NB>
-__global__ __launch_bounds__(kCoopThreads) void k_ba_chol_coop(int n, const double* __restrict__ S,
-                                                                double* __restrict__ Lg, double* __restrict__ Linvg,
-                                                                const double* __restrict__ b, double* __restrict__ x,
-                                                                int32_t* __restrict__ status, int64_t* __restrict__ trace) {
-    namespace cg = cooperative_groups;
-    cg::grid_group grid = cg::this_grid();
-    extern __shared__ double lds[];
-    __shared__ CoopShared<NB> sh;
-    const int tid = threadIdx.x, w = blockIdx.x;
-    const int nbc = (n + NB - 1) / NB;
-    const bool rhs = (w == nbc);
-    const int j0 = w * NB, jb = rhs ? 0 : min(NB, n - j0), rows = rhs ? 0 : n - j0;
-    double* A = lds;  // column owner: [rows][NB + 1]; rhs owner: y [n]
-    if (!rhs) {
-        for (int t = tid; t < rows * NB; t += kCoopThreads) {
-            const int r = t / NB, c = t % NB;
-            A[(size_t)r * (NB + 1) + c] = c < jb ? S[(size_t)(j0 + r) * n + j0 + c] : 0.0;
-        }
-    } else {
-        for (int i = tid; i < n; i += kCoopThreads) A[i] = b[i];
-    }
-    __syncthreads();
-    if (trace && tid == 0 && w == 0) { trace[200] = wall_clock64(); trace[201] = clock64(); }
-    if (w == 0) coop_finalize<NB>(A, Lg, Linvg, n, 0, j0, jb, rows, sh, status, trace ? trace + 64 : nullptr);
-    if (trace && tid == 0 && w == 0) { trace[202] = wall_clock64(); trace[203] = clock64(); }
-    if (trace && tid == 0 && w == 0) trace[0] = wall_clock64();
-    for (int k = 0; k < nbc; ++k) {
-        const int k0 = k * NB, kb = min(NB, n - k0);
-        grid.sync();  // panel k and L_kk^-1 are published
-        if (trace && tid == 0 && w == k + 1) trace[1 + 2 * k] = wall_clock64();
-        if (w == k + 1 && !rhs) {
-            coop_finalize<NB>(A, Lg, Linvg, n, w, j0, jb, rows, sh, status, trace ? trace + 64 + 8 * w : nullptr);
-            if (trace && tid == 0) trace[2 + 2 * k] = wall_clock64();
-        } else if (w > k + 1 && !rhs) {
-            for (int t = tid; t < NB * NB; t += kCoopThreads) {
-                const int c = t / NB, q = t % NB;
-                sh.Lkj[c][q] = (c < jb && q < kb) ? Lg[(size_t)(j0 + c) * n + k0 + q] : 0.0;
-            }
-            __syncthreads();
-            apply_panel<NB>(A, Lg, n, j0, k0, 0, rows, sh);
-            __syncthreads();
-        } else if (rhs) {
-            // forward block k: y_k = L_kk^-1 y_k; y_i -= L[i][k0:k1] y_k for i >= k1
-            for (int t = tid; t < NB * NB; t += kCoopThreads) sh.Linv[t / NB][t % NB] = Linvg[(size_t)k * NB * NB + t];
-            __syncthreads();
-            if (tid < NB) {
-                double acc = 0;
-#pragma unroll 8
-                for (int q = 0; q < NB; ++q) acc += sh.Linv[tid][q] * (q < kb ? A[k0 + q] : 0.0);
-                sh.yb[tid] = tid < kb ? acc : 0.0;
-            }
-            __syncthreads();
-            if (tid < kb) A[k0 + tid] = sh.yb[tid];
-            for (int i = k0 + kb + tid; i < n; i += kCoopThreads) {
-                const double* lrow = Lg + (size_t)i * n + k0;
-                double l[NB];
-#pragma unroll
-                for (int q = 0; q < NB; ++q) l[q] = q < kb ? lrow[q] : 0.0;
-                double s2 = 0;
-#pragma unroll
-                for (int q = 0; q < NB; ++q) s2 += l[q] * sh.yb[q];
-                A[i] -= s2;
-            }
-            __syncthreads();
-        }
-    }
-    if (!rhs) return;
-    if (trace && tid == 0) trace[2 * nbc + 1] = wall_clock64();
-    // backward: L^T x = y, block by block from the bottom, with L_kk^-T
-    for (int k = nbc - 1; k >= 0; --k) {
-        const int k0 = k * NB, kb = min(NB, n - k0);
-        for (int t = tid; t < NB * NB; t += kCoopThreads) sh.Linv[t / NB][t % NB] = Linvg[(size_t)k * NB * NB + t];
-        __syncthreads();
-        if (tid < NB) {  // x_c = sum_r Linv[r][c] y_r
-            double acc = 0;
-#pragma unroll 8
-            for (int r = 0; r < NB; ++r) acc += sh.Linv[r][tid] * (r < kb ? A[k0 + r] : 0.0);
-            sh.yb[tid] = tid < kb ? acc : 0.0;
-        }
-        __syncthreads();
-        if (tid < kb) A[k0 + tid] = sh.yb[tid];
-        for (int j = tid; j < k0; j += kCoopThreads) {
-            double l[NB];
-#pragma unroll
-            for (int c = 0; c < NB; ++c) l[c] = c < kb ? Lg[(size_t)(k0 + c) * n + j] : 0.0;
-            double s2 = 0;
-#pragma unroll
-            for (int c = 0; c < NB; ++c) s2 += l[c] * sh.yb[c];
-            A[j] -= s2;
-        }
-        __syncthreads();
-    }
-    for (int i = tid; i < n; i += kCoopThreads) x[i] = A[i];
-    if (trace && tid == 0) trace[2 * nbc + 2] = wall_clock64();
 }
 
 // x_l = Dinv (b_l - sum_e Hpl_e^T x_pose(e))
@@ -2206,7 +1549,7 @@ struct Stager {
 
 struct orb_ba_s {
     hipStream_t stream = nullptr;
-    DevBuf<double> pose, pose_bak, point, point_bak, err, rho0, ecl, hpl, ecp, hpp, hll, b, z, cb, S, LT, Linv, bs, x, scal;
+    DevBuf<double> pose, pose_bak, point, point_bak, err, rho0, ecl, hpl, ecp, hpp, hll, b, z, cb, S, bs, x, scal;
     DevBuf<EdgeDev> edges;
     DevBuf<orb_ba_camera_t> cams;
     DevBuf<int32_t> pose_h, free_pose, land_point, land_off, land_edge, landf_off, landf_edge, fland, pose_off, pose_edge,
@@ -2244,7 +1587,7 @@ struct orb_ba_s {
 
     void release() {
         for (auto* d : {&pose, &pose_bak, &point, &point_bak, &err, &rho0, &ecl, &hpl, &ecp, &hpp, &hll, &b, &z,
-                        &cb, &S, &LT, &Linv, &bs, &x, &scal, &lpub, &ypub, &racc})
+                        &cb, &S, &bs, &x, &scal, &lpub, &ypub, &racc})
             d->release();
         cflag.release();
         edges.release();
@@ -2324,22 +1667,28 @@ int orb_ba_destroy(orb_ba_t h) {
 
 // ORBGPU_BA_TRACE: print the MFMA Cholesky's phase stamps (debug)
 void dump_chol_trace(const int64_t* tr, int n, hipStream_t s) {
-    std::vector<int64_t> ht(1024);
-    hipMemcpyAsync(ht.data(), tr, 1024 * sizeof(int64_t), hipMemcpyDeviceToHost, s);
+    std::vector<int64_t> ht(kTraceLen);
+    hipMemcpyAsync(ht.data(), tr, kTraceLen * sizeof(int64_t), hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
-    const int64_t t0 = ht[0];
+    int64_t t0 = 0;  // the earliest stamp
+    for (int64_t v : ht)
+        if (v && (!t0 || v < t0)) t0 = v;
     const int NT = (n + 15) / 16;
     auto rel = [&](int i) { return (long long)(ht[i] ? ht[i] - t0 : -1); };
     for (int k = 0; k < NT; ++k)
-        for (int w = 0; w <= kMfTileWaves; ++w)
-            fprintf(stderr, "MFTRACE k=%d w=%d %lld %lld %lld %lld\n", k, w, rel((k * 8 + w) * 4),
-                    rel((k * 8 + w) * 4 + 1), rel((k * 8 + w) * 4 + 2), rel((k * 8 + w) * 4 + 3));
+        for (int w = 0; w <= kMf2TileWaves; ++w) {
+            const int b = kTrStep + (k * 16 + w) * 4;
+            fprintf(stderr, "MFTRACE k=%d w=%d %lld %lld %lld %lld\n", k, w, rel(b), rel(b + 1), rel(b + 2), rel(b + 3));
+        }
     for (int k = NT - 1; k >= 0; --k)
-        fprintf(stderr, "MFTRACE back k=%d %lld waited %lld published %lld\n", k, rel(600 + k), rel(800 + k), rel(830 + k));
-    fprintf(stderr, "MFTRACE end %lld\n", rel(640));
-    for (int k = 0; k + 1 < NT; ++k)
-        fprintf(stderr, "MFTRACE diag k=%d factor %lld linv %lld y %lld\n", k, (long long)(ht[701 + 4 * k] - ht[700 + 4 * k]),
-                (long long)(ht[702 + 4 * k] - ht[701 + 4 * k]), (long long)(ht[703 + 4 * k] - ht[702 + 4 * k]));
+        fprintf(stderr, "MFTRACE back k=%d %lld waited %lld published %lld\n", k, rel(kTrBack + k), rel(kTrWaited + k),
+                rel(kTrPub + k));
+    fprintf(stderr, "MFTRACE end %lld\n", rel(kTrEnd));
+    for (int k = 0; k + 1 < NT; ++k) {
+        const int b = kTrDiag + 4 * k;
+        fprintf(stderr, "MFTRACE diag k=%d factor %lld linv %lld y %lld\n", k, (long long)(ht[b + 1] - ht[b]),
+                (long long)(ht[b + 2] - ht[b + 1]), (long long)(ht[b + 3] - ht[b + 2]));
+    }
 }
 
 // ---- collectives of the sharded solve -------------------------------------------------------------
@@ -2626,8 +1975,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
               st.add(h->blk_off, blk_off) && st.add(h->pair_a, pair_a) && st.add(h->pair_b, pair_b) &&
               h->err.grow(3 * ne1) && h->rho0.grow(ne1) && h->ecl.grow(12 * ne1) && h->hpl.grow(18 * ne1) &&
               h->ecp.grow(42 * ne1) && h->hpp.grow(36 * (size_t)nf) && h->hll.grow(9 * (size_t)nl) && h->b.grow(n + m) &&
-              h->z.grow(18 * ne1) && h->cb.grow(6 * ne1) && h->S.grow((size_t)n * n) && h->LT.grow((size_t)n * n) &&
-              h->Linv.grow((size_t)n * 32 + 32 * 32) && h->bs.grow(n) && h->x.grow(n + m) && h->status.grow(1) &&
+              h->z.grow(18 * ne1) && h->cb.grow(6 * ne1) && h->S.grow((size_t)n * n) && h->bs.grow(n) && h->x.grow(n + m) && h->status.grow(1) &&
               h->depth.grow(ne1);
     if (ok && !st.items.empty()) {
         // [items table | data], one pinned buffer, one copy, one scatter launch
@@ -2666,31 +2014,9 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
 
     const float dm = (float)std::sqrt(5.991), ds = (float)std::sqrt(7.815);  // src/Optimizer.cc:1957-1958
     const Huber2 hub{(double)dm, (double)ds, (float)((double)dm * (double)dm), (float)((double)ds * (double)ds)};
-    // cooperative path (optional): block column rows x (NB + 1) doubles per workgroup
-    auto coop_bytes = [&](int b) { return sizeof(double) * (size_t)n * (b + 1); };
-    int coop_nb = 0;
-    if (coop_bytes(32) <= 136 * 1024) coop_nb = 32;
-    else if (coop_bytes(16) <= 136 * 1024) coop_nb = 16;
-    {
-        static int coop_ok = -1;
-        if (coop_ok < 0) {
-            int dev = 0, v = 0;
-            hipGetDevice(&dev);
-            coop_ok = (hipDeviceGetAttribute(&v, hipDeviceAttributeCooperativeLaunch, dev) == hipSuccess && v) ? 1 : 0;
-            hipFuncSetAttribute((const void*)k_ba_chol_coop<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 136 * 1024);
-            hipFuncSetAttribute((const void*)k_ba_chol_coop<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 136 * 1024);
-            (void)hipGetLastError();
-        }
-        if (!coop_ok || !getenv("ORBGPU_BA_COOP")) coop_nb = 0;  // the single-workgroup kernel is the default
-    }
-    const size_t coop_lds = coop_nb ? coop_bytes(coop_nb) : 0;
-    int nb = 16;
-    auto lds_bytes = [&](int b) { return sizeof(double) * ((size_t)b * n + (size_t)n * (b + 1) + n); };
-    if (lds_bytes(nb) > 150 * 1024) nb = 8;
-    const size_t chol_lds = lds_bytes(nb);
-    // The tile-row Cholesky (k_ba_chol_rows, one workgroup per 16-row tile row) takes every n it can
-    // hold resident (16 x kRowMaxNT); the register-resident single-workgroup kernel stays for
-    // n <= 288 unless ORBGPU_BA_CHOL=rows.
+    // Cholesky + solves of the reduced camera system: the register-resident single-workgroup kernel
+    // (k_ba_chol_mf2) for n <= 16 x kMfMaxNT = 288, the tile-row kernel (k_ba_chol_rows, one workgroup
+    // per 16-row tile row) above that and for any n with ORBGPU_BA_CHOL=rows (tests/test_ba_gpu.py).
     const int NT = (n + 15) / 16;
     if (NT > kRowMaxNT) {
         agree_fail(true);
@@ -2710,52 +2036,46 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         }
         if (agree_fail(!ok2)) return orbgpu_fail(ORB_ERR_DEVICE, "BA Cholesky buffers");
     }
-    auto launch_rows = [&](const LmState* g) {
-        if (rows_lds)
-            hipLaunchKernelGGL(k_ba_chol_rows<true>, dim3(NT), dim3(kRowThreads), rows_lds_bytes, s, n, h->S.p, h->bs.p,
-                               h->x.p, h->status.p, h->lpub.p, h->ypub.p, h->cflag.p, h->racc.p, g, (int)kGateTrial);
-        else
-            hipLaunchKernelGGL(k_ba_chol_rows<false>, dim3(NT), dim3(kRowThreads), rows_lds_bytes, s, n, h->S.p,
-                               h->bs.p, h->x.p, h->status.p, h->lpub.p, h->ypub.p, h->cflag.p, h->racc.p, g,
-                               (int)kGateTrial);
-    };
-    const bool use_mf = !use_rows && !coop_nb && n <= 16 * kMfMaxNT && !getenv("ORBGPU_BA_CHOL_LDS");
-    const bool chol_v1 = getenv("ORBGPU_BA_CHOL_V1") != nullptr;
-    // v2 Cholesky shape: 11 tile waves + the diagonal wave (3 waves per SIMD: 2.20 -> 2.14 ms per C5
-    // solve against 7 + 1); ORBGPU_BA_MF_W=7 selects the 8-wave kernel
-    static const int mf_w = getenv("ORBGPU_BA_MF_W") ? atoi(getenv("ORBGPU_BA_MF_W")) : kMf2TileWaves;
-    static const bool diag_readlane = getenv("ORBGPU_BA_DIAG_READLANE") != nullptr;
-    auto launch_mf2 = [&](int64_t* tr, const LmState* g) {
-        if (mf_w == 11 && !diag_readlane)
-            hipLaunchKernelGGL((k_ba_chol_mf2<11, true>), dim3(1), dim3(12 * 64), kMf2Lds, s, n, h->S.p, h->bs.p, h->x.p,
-                               h->status.p, tr, g, (int)kGateTrial);
-        else if (mf_w == 11)
-            hipLaunchKernelGGL((k_ba_chol_mf2<11, false>), dim3(1), dim3(12 * 64), kMf2Lds, s, n, h->S.p, h->bs.p, h->x.p,
-                               h->status.p, tr, g, (int)kGateTrial);
-        else if (!diag_readlane)
-            hipLaunchKernelGGL((k_ba_chol_mf2<kMfTileWaves, true>), dim3(1), dim3((kMfTileWaves + 1) * 64), kMf2Lds, s, n,
-                               h->S.p, h->bs.p, h->x.p, h->status.p, tr, g, (int)kGateTrial);
-        else
-            hipLaunchKernelGGL((k_ba_chol_mf2<kMfTileWaves, false>), dim3(1), dim3((kMfTileWaves + 1) * 64), kMf2Lds, s,
-                               n, h->S.p, h->bs.p, h->x.p, h->status.p, tr, g, (int)kGateTrial);
-    };
     static bool attr_set = false;
     if (!attr_set) {
-        hipFuncSetAttribute((const void*)k_ba_chol_mfma<kMfTileWaves>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMfLds);
-        hipFuncSetAttribute((const void*)k_ba_chol_mf2<kMfTileWaves>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMf2Lds);
-        hipFuncSetAttribute((const void*)k_ba_chol_mf2<11>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMf2Lds);
-        hipFuncSetAttribute((const void*)k_ba_chol_mf2<11, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMf2Lds);
-        hipFuncSetAttribute((const void*)k_ba_chol_mf2<kMfTileWaves, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMf2Lds);
-        hipFuncSetAttribute((const void*)k_ba_chol<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-        hipFuncSetAttribute((const void*)k_ba_chol<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+        hipFuncSetAttribute((const void*)k_ba_chol_mf2<kMf2TileWaves>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMf2Lds);
         hipFuncSetAttribute((const void*)k_ba_chol_rows<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipFuncSetAttribute((const void*)k_ba_chol_rows<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
         (void)hipGetLastError();
         attr_set = true;
     }
+    // ORBGPU_BA_TRACE: the first Cholesky of the process records its phase stamps (dump_chol_trace)
+    static int trace_left = getenv("ORBGPU_BA_TRACE") ? 1 : 0;
+    auto launch_chol = [&](const LmState* g) {
+        if (use_rows) {
+            if (rows_lds)
+                hipLaunchKernelGGL(k_ba_chol_rows<true>, dim3(NT), dim3(kRowThreads), rows_lds_bytes, s, n, h->S.p,
+                                   h->bs.p, h->x.p, h->status.p, h->lpub.p, h->ypub.p, h->cflag.p, h->racc.p, g,
+                                   (int)kGateTrial);
+            else
+                hipLaunchKernelGGL(k_ba_chol_rows<false>, dim3(NT), dim3(kRowThreads), rows_lds_bytes, s, n, h->S.p,
+                                   h->bs.p, h->x.p, h->status.p, h->lpub.p, h->ypub.p, h->cflag.p, h->racc.p, g,
+                                   (int)kGateTrial);
+            return;
+        }
+        int64_t* tr = nullptr;
+        if (trace_left && h->trace.grow(kTraceLen)) {
+            hipMemsetAsync(h->trace.p, 0, kTraceLen * sizeof(int64_t), s);
+            tr = h->trace.p;
+        }
+        hipLaunchKernelGGL((k_ba_chol_mf2<kMf2TileWaves>), dim3(1), dim3((kMf2TileWaves + 1) * 64), kMf2Lds, s, n,
+                           h->S.p, h->bs.p, h->x.p, h->status.p, tr, g, (int)kGateTrial);
+        if (tr) {
+            trace_left = 0;
+            dump_chol_trace(tr, n, s);
+        }
+    };
     double* bl = h->b.p + n;
-    // The device-driven LM loop (one process, the MFMA Cholesky): no host round trip per trial.
-    const bool dev_lm = !dist && (use_mf || use_rows) && !getenv("ORBGPU_BA_HOST_LM");
+    // The device-driven LM loop (one process): no host round trip per trial.  The host-driven loop
+    // serves the sharded solve (its all-reduces are host calls) and ORBGPU_BA_HOST_LM=1 (tested in
+    // tests/test_ba_gpu.py against the oracle).
+    static const bool host_lm_env = getenv("ORBGPU_BA_HOST_LM") != nullptr;
+    const bool dev_lm = !dist && !host_lm_env;
     const LmState* G = dev_lm ? h->lm.p : nullptr;            // gate source for every per-trial kernel
     const double* lam = dev_lm ? &h->lm.p->lambda : h->h_scal + 5;  // the trial's lambda (device / pinned)
     // ---- computeActiveErrors + activeRobustChi2 + buildSystem
@@ -2794,48 +2114,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                                primary ? 1 : 0, h->bs.p, G, (int)kGateTrial);
             if (!dev_reduce(h, h->S.p, (size_t)n * n, ORB_BA_SUM) || !dev_reduce(h, h->bs.p, n, ORB_BA_SUM))
                 return false;
-            if (use_rows) {
-                launch_rows(G);
-            } else if (coop_nb) {
-                hipMemsetAsync(h->status.p, 0, sizeof(int32_t), s);
-                int nn = n;
-                double* Sp = h->S.p;
-                double* Lp = h->LT.p;
-                double* bp = h->bs.p;
-                double* xp = h->x.p;
-                int32_t* stp = h->status.p;
-                int64_t* trp = nullptr;
-                double* Lip = h->Linv.p;
-                void* args[] = {&nn, &Sp, &Lp, &Lip, &bp, &xp, &stp, &trp};
-                const dim3 g((n + coop_nb - 1) / coop_nb + 1);
-                const hipError_t le =
-                    coop_nb == 32 ? hipLaunchCooperativeKernel((const void*)k_ba_chol_coop<32>, g, dim3(kCoopThreads),
-                                                               args, (unsigned)coop_lds, s)
-                                  : hipLaunchCooperativeKernel((const void*)k_ba_chol_coop<16>, g, dim3(kCoopThreads),
-                                                               args, (unsigned)coop_lds, s);
-                if (le != hipSuccess) return false;
-            } else if (use_mf) {
-                int64_t* tr = nullptr;
-                static int trace_left = getenv("ORBGPU_BA_TRACE") ? 1 : 0;
-                if (trace_left && h->trace.grow(1024)) {
-                    hipMemsetAsync(h->trace.p, 0, 1024 * sizeof(int64_t), s);
-                    tr = h->trace.p;
-                }
-                if (chol_v1)
-                    hipLaunchKernelGGL(k_ba_chol_mfma<kMfTileWaves>, dim3(1), dim3((kMfTileWaves + 1) * 64), kMfLds, s,
-                                       n, h->S.p, h->bs.p, h->x.p, h->status.p, tr, G, (int)kGateTrial);
-                else
-                    launch_mf2(tr, G);
-                if (tr) {
-                    trace_left = 0;
-                    dump_chol_trace(tr, n, s);
-                }
-            } else if (nb == 16)
-                hipLaunchKernelGGL(k_ba_chol<16>, dim3(1), dim3(kCholThreads), chol_lds, s, n, h->S.p, h->LT.p, h->bs.p,
-                                   h->x.p, h->status.p);
-            else
-                hipLaunchKernelGGL(k_ba_chol<8>, dim3(1), dim3(kCholThreads), chol_lds, s, n, h->S.p, h->LT.p, h->bs.p,
-                                   h->x.p, h->status.p);
+            launch_chol(G);
         } else if (!dev_lm) {
             hipMemsetAsync(h->status.p, 0, sizeof(int32_t), s);
         }
@@ -2905,23 +2184,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                 hipLaunchKernelGGL(k_u_schur, dim3(nblk + nf), dim3(64), 0, s, n, nblk, lam, h->blk_i.p, h->blk_j.p,
                                    h->blk_off.p, h->pair_a.p, h->pair_b.p, h->z.p, h->hpl.p, h->hpp.p, h->S.p,
                                    h->pose_off.p, h->pose_edge.p, h->cb.p, h->b.p, h->bs.p, (const LmState*)L);
-                int64_t* tr = nullptr;
-                static int trace_left_u = getenv("ORBGPU_BA_TRACE") ? 1 : 0;
-                if (trace_left_u && h->trace.grow(1024)) {
-                    hipMemsetAsync(h->trace.p, 0, 1024 * sizeof(int64_t), s);
-                    tr = h->trace.p;
-                }
-                if (use_rows)
-                    launch_rows((const LmState*)L);
-                else if (chol_v1)
-                    hipLaunchKernelGGL(k_ba_chol_mfma<kMfTileWaves>, dim3(1), dim3((kMfTileWaves + 1) * 64), kMfLds, s,
-                                       n, h->S.p, h->bs.p, h->x.p, h->status.p, tr, (const LmState*)L, (int)kGateTrial);
-                else
-                    launch_mf2(tr, (const LmState*)L);
-                if (tr) {
-                    trace_left_u = 0;
-                    dump_chol_trace(tr, n, s);
-                }
+                launch_chol((const LmState*)L);
             }
             hipLaunchKernelGGL(k_u_backsub_update, dim3(grid(nl + nf)), dim3(kT), 0, s, nl, nf, n, lam, h->landf_off.p,
                                h->landf_edge.p, h->edges.p, h->pose_h.p, h->hpl.p, bl, h->hll.p, h->x.p, h->free_pose.p,
@@ -2934,19 +2197,17 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         // Every unit launches the same kernels with the same arguments (the device state gates them),
         // so the unit is captured once as a graph and replayed: one graph launch instead of 7 kernel
         // launches per trial.  The capture is kept while the arguments (sizes, buffers) are unchanged.
-        static const bool no_graph = getenv("ORBGPU_BA_NO_GRAPH") != nullptr;
         auto dbits = [](double v) { uintptr_t u; memcpy(&u, &v, sizeof(u)); return u; };
-        bool use_graph = !no_graph && !getenv("ORBGPU_BA_TRACE");
-        // units per graph launch (ORBGPU_BA_UNITS, default 2): each launch boundary costs ~13 us on the
-        // device, a gated no-op unit behind the last trial less (C5 solve 1.89 -> 1.87 ms; 3: 1.89)
+        bool use_graph = !trace_left;  // (the trace dump synchronises the stream: not capturable)
+        // two units per graph launch: each launch boundary costs ~13 us on the device, a gated no-op
+        // unit behind the last trial less (C5 solve 1.89 -> 1.87 ms against one unit; three: 1.89)
         // With a stop flag, one unit per launch: the host polls the flag after every launch, so at
         // most two trials (the running and the queued unit) follow a raised flag, as before.
-        static const int units_env = std::max(1, getenv("ORBGPU_BA_UNITS") ? atoi(getenv("ORBGPU_BA_UNITS")) : 2);
-        const int units_per_launch = (opt->stop_flag || opt->stop_flag_bool) ? 1 : units_env;
+        const int units_per_launch = (opt->stop_flag || opt->stop_flag_bool) ? 1 : 2;
         if (use_graph) {
             const std::vector<uintptr_t> key = {
                 (uintptr_t)s, (uintptr_t)n, (uintptr_t)m, (uintptr_t)ne, (uintptr_t)nf, (uintptr_t)nl, (uintptr_t)nfe,
-                (uintptr_t)nblk, (uintptr_t)nparts, (uintptr_t)chol_v1, (uintptr_t)mf_w, (uintptr_t)diag_readlane, (uintptr_t)units_per_launch, dbits(hub.delta_mono), dbits(hub.delta_stereo), (uintptr_t)bl,
+                (uintptr_t)nblk, (uintptr_t)nparts, (uintptr_t)units_per_launch, dbits(hub.delta_mono), dbits(hub.delta_stereo), (uintptr_t)bl,
                 (uintptr_t)h->edges.p, (uintptr_t)h->cams.p, (uintptr_t)h->pose.p, (uintptr_t)h->point.p,
                 (uintptr_t)h->pose_h.p, (uintptr_t)h->err.p, (uintptr_t)h->rho0.p, (uintptr_t)h->ecl.p,
                 (uintptr_t)h->hpl.p, (uintptr_t)h->ecp.p, (uintptr_t)h->part.p, (uintptr_t)h->pose_off.p,

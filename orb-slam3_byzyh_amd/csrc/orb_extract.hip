@@ -2266,8 +2266,7 @@ int prepare(Extractor* e, int w, int h, int n) {
         // node tables + room for the keys of a typical level (6 B per key); levels with more keys use
         // the global scratch.  Kept small: the quad-tree blocks are long-lived and latency-bound, and
         // the LDS they do not hold lets another batch's FAST / pyramid / describe blocks share the CU.
-        static const int qt_key_kb = getenv("ORBGPU_QT_KEY_KB") ? atoi(getenv("ORBGPU_QT_KEY_KB")) : 12;
-        const size_t want = meta + (size_t)std::max(qt_key_kb, 1) * 1024;
+        const size_t want = meta + (size_t)12 * 1024;
         if (meta > 160 * 1024) return orbgpu_fail(ORB_ERR_ARG, "nfeatures too large for the quad-tree LDS budget");
         e->qt_lds = (int)std::min<size_t>(want, 160 * 1024);
         // the attribute is per function (shared by every handle): allow the whole LDS, each launch
@@ -2468,7 +2467,6 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     // FAST on the first `split` levels runs on a side stream as soon as those pyramid levels exist,
     // overlapping the latency-bound launches of the small levels (k.lv[split..] ) on `st`.
     const int split = (e->fast_split > 0 && e->fast_split < k.nlevels) ? e->fast_split : 0;
-    static const bool fast_full_lds = getenv("ORBGPU_FAST_FULL_LDS") != nullptr;  // A/B: size every launch for all levels
     static const bool fast_stamps = getenv("ORBGPU_FAST_STAMPS") != nullptr;
     auto launch_fast = [&](int l0, int l1, hipStream_t s2) {
         const int c0 = k.lv[l0].cell_begin, c1 = k.lv[l1 - 1].cell_begin + k.lv[l1 - 1].cell_count;
@@ -2476,13 +2474,13 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
         unsigned long long* stamps = nullptr;
         const size_t ns = (size_t)(c1 - c0) * n * 12;
         if (fast_stamps && hipMalloc(&stamps, ns * 8) == hipSuccess) (void)hipMemsetAsync(stamps, 0, ns * 8, s2);
-        // LDS per wave = 4 x the largest window of the launched levels: the early levels' smaller
+        // LDS per wave sized by the largest window of the launched levels: the early levels' smaller
         // windows allow more resident waves than the level-7 window would
         int mw = 0, md = 0;
         for (int l = l0; l < l1; ++l) { mw = std::max(mw, G.max_win_lv[l]); md = std::max(md, G.max_det_lv[l]); }
-        const int win_cap = ((fast_full_lds ? G.max_win : mw) + 15) & ~15;
+        const int win_cap = (mw + 15) & ~15;
         // per wave: window | score map | candidate list (u16, at most one entry per detectable pixel)
-        const int wave_lds = fast_full_lds ? 4 * win_cap : 2 * win_cap + ((2 * md + 15) & ~15);
+        const int wave_lds = 2 * win_cap + ((2 * md + 15) & ~15);
         const int groups = (c1 - c0 + 3) / 4, nblocks = groups * n, share = (nblocks + 7) / 8;
         hipLaunchKernelGGL(k_fast_cells, dim3(8 * share), dim3(256), 4 * wave_lds, s2, e->d_geom, e->d_cells, win_cap, wave_lds,
                            pyr, cand, ccount, cthr, c0, c1, stamps, groups, nblocks, share);

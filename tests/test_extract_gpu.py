@@ -166,6 +166,32 @@ def test_hamming_knn2(pkg, oracle):
     assert idx[3] == 5 and d1[3] == 0 and d2[3] == 0
 
 
+@pytest.mark.parametrize("nq,nt", [(1000, 1000), (37, 70000), (5, 0), (130, 3)], ids=["frame", "big_train", "empty", "tiny"])
+def test_hamming_knn2_split_merge(pkg, nq, nt):
+    """The train split (chunks merged in order) equals the sequential scan, ties across chunk
+    boundaries included: every query's exact copy is planted at several train positions."""
+    import torch
+    rng = np.random.default_rng(nq + nt)
+    q = rng.integers(0, 256, (nq, 32), dtype=np.uint8)
+    t = rng.integers(0, 256, (max(nt, 1), 32), dtype=np.uint8)[:nt]
+    for i in range(0, nq, 3):
+        if nt:
+            for j in rng.integers(0, nt, 3):
+                t[j] = q[i]
+    idx, d1, d2 = pkg.ORBmatcher.knn2_device(torch.from_numpy(q).cuda(), torch.from_numpy(t).cuda())
+    idx, d1, d2 = idx.cpu().numpy(), d1.cpu().numpy(), d2.cpu().numpy()
+    if nt == 0:
+        assert (idx == -1).all() and (d1 == 257).all() and (d2 == 257).all()
+        return
+    pc = np.unpackbits(np.arange(256, dtype=np.uint8)[:, None], axis=1).sum(1).astype(np.int32)
+    for i0 in range(0, nq, 8):
+        D = pc[q[i0:i0 + 8, None, :] ^ t[None, :, :]].sum(axis=2)
+        srt = np.sort(D, axis=1)
+        assert np.array_equal(idx[i0:i0 + 8], np.argmin(D, axis=1))
+        assert np.array_equal(d1[i0:i0 + 8], srt[:, 0])
+        assert np.array_equal(d2[i0:i0 + 8], srt[:, 1] if nt > 1 else np.full(len(srt), 257))
+
+
 @pytest.mark.parametrize("band_from", ["0", "3"])
 def test_band_pyramid_path_parity(pkg, oracle, frames, synth, monkeypatch, band_from):
     """The optional whole-pyramid band kernel (ORBGPU_PYR_BAND=1, off by default) stays bit-exact:
@@ -258,3 +284,31 @@ def test_sparse_corners_parity(pkg, oracle):
         assert mono == rmono and len(kps) == len(rkps) > 0, n_rect
         assert np.array_equal(kps.view(np.uint8), rkps.view(np.uint8)), n_rect
         assert np.array_equal(desc, rdesc), n_rect
+
+
+@pytest.mark.parametrize("env", [{"ORBGPU_CHUNK": "2"}, {"ORBGPU_STREAMS": "2", "ORBGPU_CHUNK": "3"},
+                                 {"ORBGPU_FAST_SPLIT": "3"}, {"ORBGPU_FAST_PER_LEVEL": "1"}, {"ORBGPU_QT_SPLIT": "1"},
+                                 {"ORBGPU_PYR_BAND": "1", "ORBGPU_PYR_WG_PER_CU": "2"},
+                                 {"ORBGPU_PYR_BAND": "1", "ORBGPU_PYR_BAND_R": "8"}],
+                         ids=["chunk2", "streams2_chunk3", "fast_split3", "fast_per_level", "qt_split",
+                              "band_2wg_per_cu", "band_r8"])
+def test_schedule_switches_parity(pkg, oracle, synth, monkeypatch, env):
+    """Every per-handle schedule switch (read when the handle is created; orb_extract.hip
+    orb_extractor_create) changes only how the batch is cut into launches and streams: a 7-frame batch
+    (a chunk size that does not divide it) stays bit-exact against the oracle."""
+    import torch
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    frames = synth.frame_batch(7, 640, 480, seed0=1400)
+    ex = pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=640, max_height=480, max_batch=8)
+    kps, desc, counts = ex.extract_batch_device(torch.from_numpy(frames).cuda(), (0, 1000))
+    torch.cuda.synchronize()
+    assert ex._lib.orb_debug_status(ex._h) == 0
+    counts = counts.cpu().numpy()
+    ref = oracle.OracleExtractor(1000, 1.2, 8, 20, 7)
+    for f in range(len(frames)):
+        rk, rd, rm = ref(frames[f], (0, 1000))
+        n = int(counts[f, 0])
+        assert n == len(rk) and int(counts[f, 1]) == rm, f
+        assert np.array_equal(pkg.keypoints_to_structured(kps[f], n).view(np.uint8), rk.view(np.uint8)), f
+        assert np.array_equal(desc[f, :n].cpu().numpy(), rd), f
