@@ -376,6 +376,103 @@ def bench_bow(pkg, synth, dev, steps, cpu_baseline_on, n_frames=64, n_feat=1000)
     return out
 
 
+def _median_ms(fn, reps):
+    import numpy as np
+    t = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        t.append((time.perf_counter() - t0) * 1e3)
+    return float(np.median(t))
+
+
+def bench_matchers(pkg, synth, dev, steps, cpu_baseline_on):
+    """The ORBmatcher calls of C3's workload, each as its caller issues it (host memory in and out,
+    synchronous, PCIe included), next to the oracle on one core (LocalMapping and Tracking are single
+    threads):
+      * SearchForTriangulation: a new keyframe against its 10 best covisible keyframes (stereo,
+        src/LocalMapping.cc:511-515,536,610; ORBmatcher(0.6, false), bOnlyStereo false), batched in
+        one launch;
+      * SearchByProjection(CurrentFrame, LastFrame, th = 7, stereo) (src/Tracking.cc:4149, ORBmatcher(0.9, true));
+      * SearchByProjection(F, local map points, th = 3) (src/Tracking.cc:4825, ORBmatcher(0.8));
+      * knn2 (best / second-best Hamming) of a 1000-descriptor frame against another, device-resident."""
+    import numpy as np
+    import torch
+    from oracle import oracle as oracle_mod
+    reps = max(10, min(steps, 50))
+    out = {}
+    # ---- SearchForTriangulation, 1 + 10 keyframes (752x480, ~1000 keypoints each)
+    kfs = [pkg.KeyFrame(**k) for k in synth.keyframe_scene(n_kf=11, n_points=1500, seed=201)]
+    k1, nbrs = kfs[0], kfs[1:]
+    m = pkg.ORBmatcher(0.6, False)
+    geoms = [m.pair_geometry(k1, k) for k in nbrs]
+    got = m.SearchForTriangulationMany(k1, nbrs, False, False, geoms=geoms)
+    for _ in range(3):
+        m.SearchForTriangulationMany(k1, nbrs, False, False, geoms=geoms)
+    ms = _median_ms(lambda: m.SearchForTriangulationMany(k1, nbrs, False, False, geoms=geoms), reps)
+    sft = {"config": f"C3 keyframe ({k1.N} keypoints) vs its 10 covisible keyframes ({int(np.mean([k.N for k in nbrs]))} "
+                     "keypoints avg), one batched call, host arrays in/out",
+           "ms_per_keyframe": round(ms, 4), "matches": int(sum(n for n, _ in got))}
+    if cpu_baseline_on:
+        t0 = time.perf_counter()
+        nrep = 0
+        while time.perf_counter() - t0 < 2.0 or nrep < 2:
+            for k, g in zip(nbrs, geoms):
+                oracle_mod.search_for_triangulation(k1, k, g, False, False, False)
+            nrep += 1
+        cms = (time.perf_counter() - t0) * 1e3 / nrep
+        sft["cpu_baseline"] = {"value": round(cms, 4), "unit": "ms/keyframe", "cores": 1, "kind": "port",
+                               "sample": f"{nrep} x 10 neighbour calls, oracle/orb_matcher_oracle.cpp, {ORACLE_FLAGS}"}
+    out["search_for_triangulation"] = sft
+    # ---- SearchByProjection(Frame, Frame)
+    cur, last = synth.tracking_pair(seed=31, stereo=True, forward=0.02, dup_frac=0.08)
+    C, L = pkg.Frame(**cur), pkg.Frame(**last)
+    mp = pkg.ORBmatcher(0.9, True)
+    n_ff, _ = mp.SearchByProjectionFrame(C, L, 7, False)
+    ms = _median_ms(lambda: mp.SearchByProjectionFrame(C, L, 7, False), reps)
+    sbf = {"config": f"current frame {C.N} keypoints, last frame {L.N} keypoints with map points, th 7, stereo",
+           "ms_per_call": round(ms, 4), "matches": int(n_ff)}
+    # ---- SearchByProjection(Frame, local map points)
+    P = pkg.LocalMapPoints(**synth.local_map_points(cur, n_points=3000, seed=151))
+    ml = pkg.ORBmatcher(0.8, True)
+    n_lm, _ = ml.SearchByProjection(C, P, 3, False, 50.0)
+    ms = _median_ms(lambda: ml.SearchByProjection(C, P, 3, False, 50.0), reps)
+    sbl = {"config": f"frame {C.N} keypoints, 3000 local map points, th 3", "ms_per_call": round(ms, 4),
+           "matches": int(n_lm)}
+    if cpu_baseline_on:
+        for d, fn, what in ((sbf, lambda: oracle_mod.search_by_projection_frame(C, L, 7, False, True), "frame"),
+                            (sbl, lambda: oracle_mod.search_by_projection_local(C, P, 3, False, 50.0, 0.8), "local")):
+            cms = _median_ms(fn, 20)
+            d["cpu_baseline"] = {"value": round(cms, 4), "unit": "ms/call", "cores": 1, "kind": "port",
+                                 "sample": f"20 calls, oracle/orb_projection_oracle.cpp ({what}), {ORACLE_FLAGS}"}
+    out["search_by_projection_frame"] = sbf
+    out["search_by_projection_local"] = sbl
+    # ---- knn2, 1000 x 1000, device-resident
+    rng = np.random.default_rng(5)
+    q = torch.from_numpy(rng.integers(0, 256, (1000, 32), dtype=np.uint8)).to(dev)
+    t = torch.from_numpy(rng.integers(0, 256, (1000, 32), dtype=np.uint8)).to(dev)
+    st = torch.cuda.current_stream(dev)
+    for _ in range(5):
+        pkg.ORBmatcher.knn2_device(q, t, stream=st)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        pkg.ORBmatcher.knn2_device(q, t, stream=st)
+    e1.record(st)
+    torch.cuda.synchronize(dev)
+    kms = e0.elapsed_time(e1) / reps
+    knn = {"config": "1000 query x 1000 train descriptors, device-resident, async on one stream",
+           "us_per_call": round(kms * 1e3, 2), "pairs_per_us": round(1e6 / (kms * 1e3), 1)}
+    if cpu_baseline_on:
+        qa, ta = q.cpu().numpy(), t.cpu().numpy()
+        cms = _median_ms(lambda: oracle_mod.hamming_knn2(qa, ta), 10)
+        knn["cpu_baseline"] = {"value": round(cms * 1e3, 1), "unit": "us/call", "cores": 1, "kind": "port",
+                               "sample": f"10 scans of the same 1000 x 1000 set, oracle_hamming_knn2 "
+                                         f"(oracle/orb_matcher_oracle.cpp, popcount scan), {ORACLE_FLAGS}"}
+    out["knn2"] = knn
+    return out
+
+
 def bench_single_frame(pkg, synth, cpu_baseline_on, reps=50):
     """Tracking's own call pattern: ORBextractor::operator() on ONE host frame (PCIe-inclusive:
     upload, extraction, download of keypoints and descriptors), 640x480 and EuRoC 752x480; the
@@ -439,6 +536,94 @@ def bench_c4(pkg, synth, dev, steps, n_frames=32, in_flight=2):
             "ms_per_step": round(dt / reps, 4)}
 
 
+def bench_c4_strong(pkg, synth, world, rank, dev, steps, in_flight=2, n_global=256, n_distinct=32):
+    """C4 as strong scaling (BASELINE.json configs[3]): a fixed global batch of 256 1280x720 frames,
+    256/N per rank; every step extracts each rank's shard and all-gathers all ranks' features
+    (keypoints + descriptors + counts, RCCL over xGMI), overlapped with the next step's extraction
+    (distributed.ShardedExtractor).  N = 1 extracts the 256 frames on one GPU with no collective.  At
+    N > 1, rank 0 also times the same 256 frames alone on its GPU (while the others wait), so the line
+    carries the N = 1 reference and the strong-scaling efficiency.  Frames: n_distinct synthetic
+    1280x720 frames (seeds 1000..) repeated over the batch (generating 256 distinct ones takes ~25 s)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from orbslam3_amd.distributed import ShardedExtractor, shard_range
+    b, e = shard_range(n_global, world, rank)
+    per = e - b
+    if world > 1 and n_global % world:
+        raise ValueError("the global batch must divide evenly over the ranks")
+    distinct = {}
+
+    def frame(f):
+        k = f % n_distinct
+        if k not in distinct:
+            distinct[k] = synth.polygon_frame(1280, 720, seed=1000 + k)
+        return distinct[k]
+    H = max(1, in_flight)
+    cap = 1000 + 16 * 8
+
+    def run(first, count, collective):
+        imgs = torch.from_numpy(np.stack([frame(f) for f in range(first, first + count)])).to(dev)
+        exs = [pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=1280, max_height=720, max_batch=count)
+               for _ in range(H)]
+        sts = [torch.cuda.Stream(dev) for _ in range(H)]
+        if collective:
+            sh = ShardedExtractor(exs, count, cap)
+            step = lambda i: sh.step(imgs, (0, 1000), stream=sts[i % H])  # noqa: E731
+            fin = sh.finish
+            counts = lambda: sh.local.counts[0]  # noqa: E731
+        else:
+            outs = [(torch.empty((count, cap, 7), dtype=torch.float32, device=dev),
+                     torch.empty((count, cap, 32), dtype=torch.uint8, device=dev),
+                     torch.empty((count, 2), dtype=torch.int32, device=dev)) for _ in range(H)]
+            step = lambda i: exs[i % H].extract_batch_device(imgs, (0, 1000), cap=cap, out=outs[i % H],  # noqa: E731
+                                                            stream=sts[i % H])
+            fin = lambda: None  # noqa: E731
+            counts = lambda: outs[0][2]  # noqa: E731
+        for i in range(2 * H):
+            step(i)
+        fin()
+        torch.cuda.synchronize(dev)
+        feats = int(counts()[:, 0].sum().item())
+        reps = max(5, min(steps, 20))
+        if collective:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(reps):
+            step(i)
+        fin()
+        torch.cuda.synchronize(dev)
+        if collective:
+            dist.barrier()
+        return (time.perf_counter() - t0) * 1e3 / reps, feats
+
+    ms, feats = run(b, per, world > 1)
+    if world > 1:
+        t = torch.tensor([ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item())
+        f = torch.tensor([feats], dtype=torch.int64, device=dev)
+        dist.all_reduce(f, op=dist.ReduceOp.SUM)
+        feats = int(f.item())
+    out = {"config": f"C4 strong scaling: {n_global} synthetic 1280x720 frames per step in total ({n_distinct} distinct, "
+                     f"repeated), {per} per GPU x {world} GPU(s), nFeatures 1000, 8 levels"
+                     + (", all-gather of keypoints + descriptors + counts per step (RCCL)" if world > 1 else ""),
+           "n_gpus": world, "frames_per_gpu": per, "ms_per_step": round(ms, 4),
+           "frames_per_ms": round(n_global / ms, 3), "features_per_ms": round(feats / ms, 3)}
+    if world > 1:
+        ref = torch.zeros(1, dtype=torch.float64, device=dev)
+        if rank == 0:
+            ms1, _ = run(0, n_global, False)
+            ref[0] = ms1
+        dist.broadcast(ref, 0)
+        ms1 = float(ref.item())
+        out["single_gpu_ms_per_step"] = round(ms1, 4)
+        out["speedup"] = round(ms1 / ms, 3)
+        out["efficiency"] = round(ms1 / (world * ms), 3)
+    return out
+
+
 def pmc_traffic():
     p = ROOT / "profiles" / "pmc_latest.json"
     if p.exists():
@@ -467,6 +652,7 @@ def main():
     ap.add_argument("--no-bow", action="store_true", help="skip the DBoW2 transform measurement")
     ap.add_argument("--no-single", action="store_true", help="skip the single-frame latency measurement")
     ap.add_argument("--no-c4", action="store_true", help="skip the 1280x720 (C4 shard) measurement")
+    ap.add_argument("--no-matchers", action="store_true", help="skip the ORBmatcher measurements")
     args = ap.parse_args()
 
     import numpy as np
@@ -667,6 +853,18 @@ def main():
             single = bench_single_frame(pkg, synth, not args.no_cpu_baseline)
         except Exception as e:  # noqa: BLE001
             single = {"error": repr(e)}
+    c4_strong = None
+    if not args.no_c4:
+        try:
+            c4_strong = bench_c4_strong(pkg, synth, world, rank, dev, args.steps, in_flight=H)
+        except Exception as e:  # noqa: BLE001
+            c4_strong = {"error": repr(e)}
+    matchers = None
+    if not args.no_matchers and world == 1:
+        try:
+            matchers = bench_matchers(pkg, synth, dev, args.steps, not args.no_cpu_baseline)
+        except Exception as e:  # noqa: BLE001
+            matchers = {"error": repr(e)}
     c4 = None
     if not args.no_c4 and world == 1:
         try:
@@ -676,6 +874,10 @@ def main():
     if rank == 0:
         if c4 is not None:
             result["c4_shard"] = c4
+        if c4_strong is not None:
+            result["c4_strong"] = c4_strong
+        if matchers is not None:
+            result["matchers"] = matchers
         if single is not None:
             result["single_frame_latency"] = single
         if pose is not None:

@@ -148,6 +148,20 @@ typedef struct orb_matcher_s* orb_matcher_t;
 int orb_matcher_create(float nnratio, int check_orientation, orb_matcher_t* out);
 int orb_matcher_destroy(orb_matcher_t m);
 
+/* ---- MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:438-529), batched over map points.
+ * Point p's descriptors are rows [offsets[p], offsets[p+1]) of desc (n x 32 bytes): the reference's
+ * vDescriptors, i.e. the observations in std::map order, left then right index, bad keyframes
+ * skipped.  best[p] receives the row (within the point) whose median distance to the point's rows
+ * (index floor(0.5 (N - 1)) of the sorted row, self included) is the smallest, the first one on ties,
+ * or -1 for a point without rows; out[32 p ..] receives that descriptor (mDescriptor), untouched for
+ * an empty point (the reference returns early).  N < 65536 per point. */
+/* Host arrays through the matcher handle's staging buffers, synchronous. */
+int orb_compute_distinctive_descriptors(orb_matcher_t m, const uint8_t* desc, const int32_t* offsets, int n_points,
+                                        int32_t* best, uint8_t* out);
+/* Device arrays (d_offsets: n_points + 1 ints, d_desc / d_out 16-byte aligned), async on `stream`. */
+int orb_compute_distinctive_descriptors_device(const uint8_t* d_desc, const int32_t* d_offsets, int n_points,
+                                               int32_t* d_best, uint8_t* d_out, void* stream);
+
 /* T1w, T2w: 3x4 row-major [R|t] world->camera poses (float); fx..cy: camera of KF2. */
 int orb_kf_pair_geometry(const float T1w[12], const float T2w[12], float fx2, float fy2, float cx2, float cy2,
                          orb_kf_pair_geom_t* out);

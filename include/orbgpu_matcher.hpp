@@ -51,8 +51,10 @@
 #include <cstdint>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <tuple>
 #include <utility>
 #include <vector>
 
@@ -305,6 +307,46 @@ private:
     orb_matcher_t Handle() const { return detail::ThreadHandle(mfNNratio, mbCheckOrientation); }
 };
 
+// MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:438-529) for a batch of map points in one
+// launch, e.g. the loops of LocalMapping::SearchInNeighbors (src/LocalMapping.cc:1045-1060) and
+// ProcessNewKeyFrame (:400-416): each point's result depends only on its own observations, so the
+// batch equals the per-point calls.  Per point, as the reference: skipped when bad or without
+// observations; rows = the observations in std::map order, left then right index, bad keyframes
+// skipped; skipped when no row; otherwise mDescriptor = the row with the least median distance.
+// Accessor members used (besides those above):
+//   static std::map<KeyFrame*, std::tuple<int, int>> ObservationMap(MapPoint*); // GetObservations()
+//   static bool IsBad(KeyFrame*);
+//   static const uint8_t* DescriptorRow(KeyFrame*, int idx);                    // mDescriptors.row(idx)
+//   static void SetDescriptor(MapPoint*, const uint8_t d[32]);                  // mDescriptor = row.clone()
+template <class A>
+void ComputeDistinctiveDescriptors(const std::vector<typename A::MapPoint*>& points) {
+    std::vector<uint8_t> rows;
+    std::vector<int32_t> offsets{0};
+    std::vector<typename A::MapPoint*> todo;
+    for (auto* pMP : points) {
+        if (!pMP || A::IsBad(pMP)) continue;
+        const auto observations = A::ObservationMap(pMP);
+        if (observations.empty()) continue;
+        const size_t before = rows.size();
+        for (const auto& ob : observations) {
+            if (A::IsBad(ob.first)) continue;
+            const int l = std::get<0>(ob.second), r = std::get<1>(ob.second);
+            if (l != -1) rows.insert(rows.end(), A::DescriptorRow(ob.first, l), A::DescriptorRow(ob.first, l) + 32);
+            if (r != -1) rows.insert(rows.end(), A::DescriptorRow(ob.first, r), A::DescriptorRow(ob.first, r) + 32);
+        }
+        if (rows.size() == before) continue;
+        offsets.push_back((int32_t)(rows.size() / 32));
+        todo.push_back(pMP);
+    }
+    if (todo.empty()) return;
+    std::vector<int32_t> best(todo.size());
+    std::vector<uint8_t> out(32 * todo.size());
+    detail::Check(orb_compute_distinctive_descriptors(detail::ThreadHandle(0.6f, false), rows.data(), offsets.data(),
+                                                      (int)todo.size(), best.data(), out.data()),
+                  "orb_compute_distinctive_descriptors");
+    for (size_t p = 0; p < todo.size(); ++p) A::SetDescriptor(todo[p], &out[32 * p]);
+}
+
 }  // namespace orbgpu
 
 // ---- the reference's own types (compile inside the ORB-SLAM3 build: define ORBGPU_WITH_ORBSLAM3 and
@@ -380,6 +422,14 @@ struct ORBSLAM3MatcherAccess {
     static void Descriptor(MapPoint* p, uint8_t d[32]) {
         const cv::Mat m = p->GetDescriptor();
         for (int i = 0; i < 32; ++i) d[i] = m.ptr<uint8_t>()[i];
+    }
+    static std::map<KeyFrame*, std::tuple<int, int>> ObservationMap(MapPoint* p) { return p->GetObservations(); }
+    static bool IsBad(KeyFrame* k) { return k->isBad(); }
+    static const uint8_t* DescriptorRow(KeyFrame* k, int idx) { return k->mDescriptors.ptr<uint8_t>(idx); }
+    // mDescriptor is protected in MapPoint: the integration adds `friend struct orbgpu::ORBSLAM3MatcherAccess;`
+    static void SetDescriptor(MapPoint* p, const uint8_t d[32]) {
+        std::unique_lock<std::mutex> lock(p->mMutexFeatures);
+        p->mDescriptor = cv::Mat(1, 32, CV_8U, const_cast<uint8_t*>(d)).clone();
     }
     static void Track(MapPoint* p, TrackFields* t) {
         t->in_view = p->mbTrackInView;

@@ -36,6 +36,8 @@ _PROTOS = {
     "oracle_fast_atan2": (_f, [_f, _f]),
     "oracle_gaussian_blur": (None, [_vp, _i, _i, _i, _vp]),
     "oracle_descriptor_distance": (_i, [_vp, _vp]),
+    "oracle_compute_distinctive_descriptors": (None, [_vp, _vp, _i, _vp]),
+    "oracle_hamming_knn2": (None, [_vp, _i, _vp, _i, _vp, _vp, _vp]),
     "oracle_search_for_triangulation": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp]),
     "oracle_local_ba": (_i, [_vp, _vp, _vp, _vp, _vp]),
     "oracle_search_by_projection_frame": (_i, [_vp, _vp, _f, _i, _i, _vp]),
@@ -186,6 +188,27 @@ def descriptor_distance(a: np.ndarray, b: np.ndarray) -> int:
     a = np.ascontiguousarray(a, dtype=np.uint8)
     b = np.ascontiguousarray(b, dtype=np.uint8)
     return load().oracle_descriptor_distance(a.ctypes.data, b.ctypes.data)
+
+
+def hamming_knn2(query, train):
+    """Oracle best / second-best Hamming scan (index order, first index on ties); 257 = none."""
+    q = np.ascontiguousarray(query, dtype=np.uint8).reshape(-1, 32)
+    t = np.ascontiguousarray(train, dtype=np.uint8).reshape(-1, 32)
+    n = len(q)
+    out = [np.zeros(max(n, 1), np.int32) for _ in range(3)]
+    load().oracle_hamming_knn2(q.ctypes.data, n, t.ctypes.data, len(t), *(o.ctypes.data for o in out))
+    return tuple(o[:n] for o in out)
+
+
+def compute_distinctive_descriptors(desc, offsets):
+    """Oracle MapPoint::ComputeDistinctiveDescriptors per point (rows offsets[p]..offsets[p+1] of desc):
+    returns best[p] (-1 for an empty point)."""
+    desc = np.ascontiguousarray(desc, dtype=np.uint8).reshape(-1, 32)
+    offsets = np.ascontiguousarray(offsets, dtype=np.int32)
+    n = len(offsets) - 1
+    best = np.zeros(max(n, 1), np.int32)
+    load().oracle_compute_distinctive_descriptors(desc.ctypes.data, offsets.ctypes.data, n, best.ctypes.data)
+    return best[:n]
 
 
 def search_for_triangulation(kf1, kf2, geom, only_stereo: bool, coarse: bool, check_ori: bool):

@@ -9,6 +9,8 @@
 // as Eigen 3.x's closed-form 3x3 inverse and unrolled 3x3 products with those contractions.
 // Parity with the real reference's F12 bits is unpinned (Eigen is absent); everything downstream of
 // F12 is the reference's arithmetic.
+#include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -210,4 +212,65 @@ extern "C" int oracle_search_for_triangulation(const orb_kf_view_t* pKF1, const 
     }
     for (int i = 0; i < pKF1->n; ++i) vMatches12out[i] = vMatches12[i];
     return nmatches;
+}
+
+// MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:438-529) for n_points points: point p's
+// descriptors are rows [offsets[p], offsets[p+1]) of desc.  best[p] = BestIdx, or -1 when the point has
+// no descriptor (the reference returns before choosing).  Written as the reference: a float N x N
+// matrix, each row copied into vector<int>, std::sort, median at index 0.5*(N-1) (size_t truncation),
+// the first strictly smaller median wins.
+extern "C" void oracle_compute_distinctive_descriptors(const uint8_t* desc, const int32_t* offsets, int n_points,
+                                                      int32_t* best) {
+    for (int p = 0; p < n_points; ++p) {
+        const int o = offsets[p];
+        const size_t N = (size_t)(offsets[p + 1] - o);
+        if (N == 0) {
+            best[p] = -1;
+            continue;
+        }
+        std::vector<float> Distances(N * N);
+        for (size_t i = 0; i < N; i++) {
+            Distances[i * N + i] = 0;
+            for (size_t j = i + 1; j < N; j++) {
+                const int distij = descriptor_distance(desc + 32 * (size_t)(o + i), desc + 32 * (size_t)(o + j));
+                Distances[i * N + j] = distij;
+                Distances[j * N + i] = distij;
+            }
+        }
+        int BestMedian = INT_MAX;
+        int BestIdx = 0;
+        for (size_t i = 0; i < N; i++) {
+            std::vector<int> vDists(Distances.begin() + i * N, Distances.begin() + (i + 1) * N);
+            std::sort(vDists.begin(), vDists.end());
+            const int median = vDists[0.5 * (N - 1)];
+            if (median < BestMedian) {
+                BestMedian = median;
+                BestIdx = (int)i;
+            }
+        }
+        best[p] = BestIdx;
+    }
+}
+
+// Best / second-best Hamming scan of every query over the train set in index order, the update rule
+// of the ORBmatcher loops (a strictly smaller distance replaces the best, otherwise a smaller one the
+// second; src/ORBmatcher.cc:1160-1175).  257 = none.
+extern "C" void oracle_hamming_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* best_idx,
+                                   int32_t* best_dist, int32_t* second_dist) {
+    for (int i = 0; i < nq; ++i) {
+        int best = 257, second = 257, bi = -1;
+        for (int j = 0; j < nt; ++j) {
+            const int d = descriptor_distance(q + 32 * (size_t)i, t + 32 * (size_t)j);
+            if (d < best) {
+                second = best;
+                best = d;
+                bi = j;
+            } else if (d < second) {
+                second = d;
+            }
+        }
+        best_idx[i] = bi;
+        best_dist[i] = best;
+        second_dist[i] = second;
+    }
 }

@@ -87,6 +87,8 @@ PROTOTYPES = {
     "orb_hamming_knn2_device": (_i, [_vp, _i, _vp, _i, _vp, _vp, _vp, _vp]),
     "orb_matcher_create": (_i, [_f, _i, ctypes.POINTER(_vp)]),
     "orb_matcher_destroy": (_i, [_vp]),
+    "orb_compute_distinctive_descriptors": (_i, [_vp, _vp, _vp, _i, _vp, _vp]),
+    "orb_compute_distinctive_descriptors_device": (_i, [_vp, _vp, _i, _vp, _vp, _vp]),
     "orb_kf_pair_geometry": (_i, [_vp, _vp, _f, _f, _f, _f, _vp]),
     "orb_search_for_triangulation": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
     "orb_search_by_projection_frame": (_i, [_vp, _vp, _vp, _f, _i, _vp, _vp]),

@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstring>
 
 #include "orbgpu.h"
 #include "orbgpu_internal.h"
@@ -139,5 +140,105 @@ extern "C" int orb_hamming_knn2_device(const uint8_t* d_query, int n_query, cons
         if (hipFreeAsync(part, s) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "knn2 partial buffer free");
     }
     if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "hamming launch failed");
+    return ORB_OK;
+}
+
+// ---- MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:438-529), batched over map points ----
+// Per point, N descriptors (its observations' rows).  The reference builds the N x N distance matrix
+// (DescriptorDistance, diagonal 0), takes for every row i the element at index floor(0.5 (N - 1)) of
+// the sorted row -- the median, self distance included -- and keeps the first row with the smallest
+// median.  One wave per point: lane i computes row i's distances on the fly into a lane-private
+// 257-bin u16 histogram in LDS (hist[bin][lane]), then walks the histogram to the
+// median; the wave reduces (median, i) lexicographically (first index on ties).  Rows beyond 64 are
+// taken 64 at a time.
+namespace {
+constexpr int kDdBins = 257;
+
+__global__ __launch_bounds__(64) void k_distinctive(const uint4* __restrict__ desc, const int32_t* __restrict__ off,
+                                                    int n_points, int32_t* __restrict__ best,
+                                                    uint4* __restrict__ out) {
+    __shared__ uint16_t hist[kDdBins * 64];
+    const int p = blockIdx.x, lane = threadIdx.x;
+    const int o = off[p], N = off[p + 1] - o;
+    if (N <= 0) {
+        if (lane == 0) best[p] = -1;
+        return;
+    }
+    const int k = (int)(0.5 * (double)(N - 1));  // vDists[0.5*(N-1)]: the size_t index truncates
+    unsigned long long bestkey = ~0ull;
+    for (int i0 = 0; i0 < N; i0 += 64) {
+        const int i = i0 + lane;
+        for (int b = 0; b < kDdBins; ++b) hist[b * 64 + lane] = 0;
+        if (i < N) {
+            const uint4 a0 = desc[2 * (size_t)(o + i)], a1 = desc[2 * (size_t)(o + i) + 1];
+            for (int j = 0; j < N; ++j) {  // descriptor j: the same address in every lane (one fetch)
+                const int d = hamming256(a0, a1, desc[2 * (size_t)(o + j)], desc[2 * (size_t)(o + j) + 1]);
+                hist[d * 64 + lane] = (uint16_t)(hist[d * 64 + lane] + 1);
+            }
+            int acc = 0, med = 0;
+            for (int b = 0; b < kDdBins; ++b) {  // the k-th smallest (0-based) of the row
+                acc += (int)hist[b * 64 + lane];
+                if (acc > k) { med = b; break; }
+            }
+            const unsigned long long key = ((unsigned long long)med << 32) | (unsigned)i;
+            bestkey = key < bestkey ? key : bestkey;
+        }
+    }
+    for (int s = 32; s > 0; s >>= 1) {
+        const unsigned long long v = __shfl_xor(bestkey, s, 64);
+        bestkey = v < bestkey ? v : bestkey;
+    }
+    const int bi = (int)(bestkey & 0xffffffffu);
+    if (lane == 0) best[p] = bi;
+    if (lane < 2) out[2 * (size_t)p + lane] = desc[2 * (size_t)(o + bi) + lane];
+}
+}  // namespace
+
+// Defined in orb_triangulation.hip: the matcher handle's staging buffers.
+int orbgpu_matcher_reserve(orb_matcher_t m, size_t bytes, char** d_buf, char** h_buf, hipStream_t* stream,
+                           int* check_ori);
+
+extern "C" int orb_compute_distinctive_descriptors_device(const uint8_t* d_desc, const int32_t* d_offsets, int n_points,
+                                                          int32_t* d_best, uint8_t* d_out, void* stream) {
+    if (n_points < 0 || (n_points > 0 && (!d_desc || !d_offsets || !d_best || !d_out)))
+        return orbgpu_fail(ORB_ERR_ARG, "bad ComputeDistinctiveDescriptors arguments");
+    if (n_points == 0) return ORB_OK;
+    if ((reinterpret_cast<uintptr_t>(d_desc) | reinterpret_cast<uintptr_t>(d_out)) & 15)
+        return orbgpu_fail(ORB_ERR_ARG, "descriptor arrays must be 16-byte aligned");
+    hipLaunchKernelGGL(k_distinctive, dim3(n_points), dim3(64), 0, (hipStream_t)stream, (const uint4*)d_desc, d_offsets,
+                       n_points, d_best, (uint4*)d_out);
+    if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "distinctive descriptors launch failed");
+    return ORB_OK;
+}
+
+extern "C" int orb_compute_distinctive_descriptors(orb_matcher_t m, const uint8_t* desc, const int32_t* offsets,
+                                                   int n_points, int32_t* best, uint8_t* out) {
+    if (!m || n_points < 0 || (n_points > 0 && (!offsets || !best || !out)))
+        return orbgpu_fail(ORB_ERR_ARG, "bad ComputeDistinctiveDescriptors arguments");
+    if (n_points == 0) return ORB_OK;
+    if (offsets[0] != 0) return orbgpu_fail(ORB_ERR_ARG, "offsets[0] must be 0");
+    for (int p = 0; p < n_points; ++p)
+        if (offsets[p + 1] < offsets[p]) return orbgpu_fail(ORB_ERR_ARG, "offsets must be non-decreasing");
+    const size_t nd = (size_t)offsets[n_points];
+    if (nd && !desc) return orbgpu_fail(ORB_ERR_ARG, "null descriptors");
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_d = 0, o_off = al(nd * 32), o_best = o_off + al((size_t)(n_points + 1) * 4),
+                 o_out = o_best + al((size_t)n_points * 4), total = o_out + al((size_t)n_points * 32);
+    char *d = nullptr, *h = nullptr;
+    hipStream_t s = nullptr;
+    int check_ori = 0;
+    if (int rc = orbgpu_matcher_reserve(m, total, &d, &h, &s, &check_ori)) return rc;
+    if (nd) memcpy(h + o_d, desc, nd * 32);
+    memcpy(h + o_off, offsets, (size_t)(n_points + 1) * 4);
+    bool ok = hipMemcpyAsync(d, h, o_best, hipMemcpyHostToDevice, s) == hipSuccess;
+    if (ok) hipLaunchKernelGGL(k_distinctive, dim3(n_points), dim3(64), 0, s, (const uint4*)(d + o_d),
+                               (const int32_t*)(d + o_off), n_points, (int32_t*)(d + o_best), (uint4*)(d + o_out));
+    ok = ok && hipGetLastError() == hipSuccess &&
+         hipMemcpyAsync(h + o_best, d + o_best, total - o_best, hipMemcpyDeviceToHost, s) == hipSuccess &&
+         hipStreamSynchronize(s) == hipSuccess;
+    if (!ok) return orbgpu_fail(ORB_ERR_DEVICE, "ComputeDistinctiveDescriptors failed");
+    memcpy(best, h + o_best, (size_t)n_points * 4);
+    for (int p = 0; p < n_points; ++p)  // an empty point keeps its descriptor (the reference returns early)
+        if (best[p] >= 0) memcpy(out + 32 * (size_t)p, h + o_out + 32 * (size_t)p, 32);
     return ORB_OK;
 }

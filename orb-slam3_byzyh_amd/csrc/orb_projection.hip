@@ -8,12 +8,10 @@
 //   k_proj_candidates  one thread per last-frame point: project, walk the 64 x 48 grid window in the
 //                      reference's cell order and keep (keypoint, distance) of every candidate that
 //                      passes the static tests, plus the first minimum (the unconstrained best).
-//   k_proj_resolve     one wave, points in index order: if the unconstrained best is still free it
-//                      is the answer; otherwise the wave re-scans that point's candidates with the
-//                      claimed ones masked out (first minimum again).  Then the rotation histogram /
+//   k_lmp_candidates   the same for SearchByProjection(Frame, local map points) (src:46-240).
+//   k_resolve_rounds   one workgroup: the in-order assignment of both overloads (ratio test for the
+//                      local map), decided in parallel rounds (below), then the rotation histogram /
 //                      ComputeThreeMaxima filter (src:2158-2181).
-//   k_lmp_candidates / k_lmp_resolve: the same scheme for SearchByProjection(Frame, local map points)
-//                      (src:46-240) with the best / second-best ratio test.
 // Float arithmetic follows the reference build's contractions (see oracle/orb_projection_oracle.cpp);
 // this file is compiled with -ffp-contract=off and every fma is explicit.
 #include <hip/hip_runtime.h>
@@ -129,94 +127,6 @@ __device__ __forceinline__ int rot_bin(float a1, float a2) {
     return bin;
 }
 
-// One wave: the reference's in-order assignment, then the orientation filter.
-// mp[i2] = last-frame index assigned to current keypoint i2 (-1: none).
-__global__ __launch_bounds__(64) void k_proj_resolve(const ProjParams* __restrict__ pp, const Cand* __restrict__ cands,
-                                                     const int32_t* __restrict__ ncand, const int32_t* __restrict__ best_c,
-                                                     const uint8_t* __restrict__ observed,
-                                                     const float* __restrict__ last_angle,
-                                                     const float4* __restrict__ cur_kp, int32_t* __restrict__ mp,
-                                                     int32_t* __restrict__ match_i2, int32_t* __restrict__ match_bin,
-                                                     int32_t* __restrict__ out_n) {
-    const ProjParams& P = *pp;
-    const int lane = threadIdx.x;
-    __shared__ int hist[kHisto];
-    for (int k = lane; k < P.n_cur; k += 64) mp[k] = -1;
-    if (lane < kHisto) hist[lane] = 0;
-    __syncthreads();
-    int nm = 0;
-    for (int i = 0; i < P.n_last; ++i) {
-        const int n = ncand[i];
-        if (n == 0) continue;
-        const Cand* C = cands + (size_t)i * P.cap;
-        int bi2 = -1, bd = 256;
-        {
-            const Cand c = C[best_c[i]];
-            const int owner = mp[c.i2];
-            if (owner < 0 || !observed[owner]) {
-                bi2 = c.i2;
-                bd = c.dist;
-            } else {  // the unconstrained best is claimed: first minimum among the free candidates
-                unsigned long long key = ~0ull;
-                for (int k = lane; k < n; k += 64) {
-                    const Cand q = C[k];
-                    const int o = mp[q.i2];
-                    if (o < 0 || !observed[o]) {
-                        const unsigned long long kk = ((unsigned long long)q.dist << 32) | (unsigned)k;
-                        key = kk < key ? kk : key;
-                    }
-                }
-                for (int off = 32; off > 0; off >>= 1) {
-                    const unsigned long long o = __shfl_xor(key, off, 64);
-                    key = o < key ? o : key;
-                }
-                if (key != ~0ull) {
-                    bd = (int)(key >> 32);
-                    bi2 = C[(int)(key & 0xffffffffu)].i2;
-                }
-            }
-        }
-        __syncthreads();
-        if (bi2 >= 0 && bd <= kThHigh) {
-            if (lane == 0) {
-                mp[bi2] = i;
-                match_i2[nm] = bi2;
-                const int bin = P.check_ori ? rot_bin(last_angle[i], cur_kp[bi2].z) : 0;
-                match_bin[nm] = bin;
-                if (P.check_ori) hist[bin]++;
-            }
-            ++nm;
-        }
-        __syncthreads();
-    }
-    int removed = 0;
-    if (P.check_ori) {
-        __shared__ int keep[3];
-        if (lane == 0) {  // ComputeThreeMaxima (src:2336-2378)
-            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
-            for (int b = 0; b < kHisto; ++b) {
-                const int s = hist[b];
-                if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = b; }
-                else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = b; }
-                else if (s > max3) { max3 = s; ind3 = b; }
-            }
-            if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
-            else if (max3 < 0.1f * (float)max1) ind3 = -1;
-            keep[0] = ind1; keep[1] = ind2; keep[2] = ind3;
-        }
-        __syncthreads();
-        for (int k = lane; k < nm; k += 64) {
-            const int b = match_bin[k];
-            if (b != keep[0] && b != keep[1] && b != keep[2]) {
-                mp[match_i2[k]] = -1;
-                ++removed;
-            }
-        }
-        for (int off = 32; off > 0; off >>= 1) removed += __shfl_xor(removed, off, 64);
-    }
-    if (lane == 0) *out_n = nm - removed;
-}
-
 // ---- SearchByProjection(Frame&, vector<MapPoint*>, th, bFarPoints, thFarPoints), src:46-240 -------
 
 struct LocalParams {
@@ -294,72 +204,176 @@ __global__ __launch_bounds__(256) void k_lmp_candidates(const LocalParams* __res
     if (n > P.cap) atomicMax(overflow, n);
 }
 
-__global__ __launch_bounds__(64) void k_lmp_resolve(const LocalParams* __restrict__ pp, const Cand* __restrict__ cands,
-                                                    const int32_t* __restrict__ ncand, const Best2* __restrict__ best,
-                                                    const uint8_t* __restrict__ observed, const uint8_t* __restrict__ taken0,
-                                                    const float4* __restrict__ cur_kp, int32_t* __restrict__ owner_obs,
-                                                    int32_t* __restrict__ match, int32_t* __restrict__ out_n) {
-    const LocalParams& P = *pp;
-    const int lane = threadIdx.x;
-    for (int k = lane; k < P.n_cur; k += 64) {
-        owner_obs[k] = taken0 ? taken0[k] : 0;
-        match[k] = -1;
+// ---- the in-order assignment, resolved in parallel rounds --------------------------------------
+// Both SearchByProjection loops visit the points in index order, and point i only sees the state the
+// earlier points left: a current keypoint that holds a map point with observations is skipped
+// (src:103-105, src:2040-2042).  That state changes once per keypoint -- the first successful
+// assignment by an observed point -- so point i's answer depends only on which of its candidates
+// earlier observed points claim, and only through the candidates that are (or would become) its
+// first minimum (SearchByProjection(Frame, Frame)) or first two minima (the local-map overload, for
+// the ratio test): candidates elsewhere in its list change neither.
+// One workgroup resolves every point in rounds.  At the start of a round, minNF[j] = the smallest
+// still-undecided observed point that has keypoint j among its candidates.  Point i is decided in the
+// round when no candidate that could still enter its minima is "unknown" (minNF[j] < i: an earlier
+// undecided point might claim it); claimed[j] < i (a decided earlier claim) excludes a candidate.
+// The earliest undecided point is always decidable, so every round makes progress.  A point can only
+// ever claim a candidate at or below the first candidate it already knows to stay free (bound[i],
+// from its previous evaluation), so only those enter minNF: the dependency chains stay short and a
+// frame takes a handful of rounds.  The results are then exactly those of the
+// sequential loop:
+//   mp[j]  = the last point assigned to keypoint j (a later unobserved-free assignment overwrites an
+//            earlier one, src:156 / :2067), or -1;
+//   count  = every successful assignment (the reference's nmatches++ per assignment), minus, for
+//            SearchByProjection(Frame, Frame) with checkOri, every assignment in a rotation bin outside
+//            ComputeThreeMaxima's top three, whose keypoint is then cleared (src:2160-2181).
+// The candidate kernels above store each point's candidates in the reference's scan order (the order
+// key of a candidate is its list position) with their Hamming distances.
+constexpr int kResolveThreads = 1024, kResolveLdsKeypoints = 8192;
+constexpr unsigned long long kNone = ~0ull;
+
+struct ResolveArgs {
+    int n_pts, n_cur, cap;
+    int local;          // 1: best + second best with the ratio test (src:145-167); 0: best only (src:2064-2068)
+    int check_ori;      // rotation histogram (SearchByProjection(Frame, Frame) only)
+    float nnratio;
+    const Cand* cands;
+    const int32_t* ncand;
+    const uint8_t* observed;   // per point: its map point has Observations() > 0
+    const uint8_t* taken0;     // per keypoint: holds a map point with observations before the call (may be null)
+    const float4* cur_kp;      // x, y, angle, octave bits
+    const float* last_angle;   // per point (rotation bins)
+    const int32_t* overflow;   // the candidate pass's overflow (> cap: results not written)
+    int32_t* st;               // per point: -2 undecided, -1 no match, j >= 0 matched to keypoint j
+    unsigned long long* bound; // per point: the key of its first candidate known to stay free (or none)
+    int lds_keypoints;         // 1: minNF / claimed in LDS (dynamic, 8 B per keypoint)
+    int32_t* minNF;            // per keypoint
+    int32_t* claimed;          // per keypoint
+    int32_t* last;             // per keypoint
+    int32_t* removed;          // per keypoint
+    int32_t* mp;               // out: per keypoint
+    int32_t* out_n;            // out
+};
+
+__global__ __launch_bounds__(kResolveThreads) void k_resolve_rounds(ResolveArgs a) {
+    const int tid = threadIdx.x;
+    __shared__ int hist[kHisto], keep[3], cnt[2];
+    extern __shared__ int32_t kp_lds[];
+    int32_t* const minNF = a.lds_keypoints ? kp_lds : a.minNF;
+    int32_t* const claimed = a.lds_keypoints ? kp_lds + a.n_cur : a.claimed;
+    if (*a.overflow > a.cap) {  // the host re-runs with a larger capacity
+        if (tid == 0) *a.out_n = -1;
+        return;
     }
+    for (int i = tid; i < a.n_pts; i += kResolveThreads) {
+        a.st[i] = a.ncand[i] > 0 ? -2 : -1;
+        a.bound[i] = kNone;
+    }
+    for (int j = tid; j < a.n_cur; j += kResolveThreads) {
+        claimed[j] = INT32_MAX;
+        a.last[j] = -1;
+        a.removed[j] = 0;
+    }
+    if (tid < kHisto) hist[tid] = 0;
+    if (tid < 2) cnt[tid] = 0;
     __syncthreads();
-    int nm = 0;
-    for (int i = 0; i < P.n_pts; ++i) {
-        const int n = ncand[i];
-        if (n == 0) continue;
-        const Cand* C = cands + (size_t)i * P.cap;
-        const Best2 B = best[i];
-        int d1 = 256, d2 = 256, j1 = -1, l1 = -1, l2 = -1;
-        const bool t1 = B.c1 >= 0 && owner_obs[C[B.c1].i2];
-        const bool t2 = B.c2 >= 0 && owner_obs[C[B.c2].i2];
-        if (!t1 && !t2) {  // claimed candidates elsewhere in the list change neither minimum
-            if (B.c1 >= 0) { d1 = C[B.c1].dist; j1 = C[B.c1].i2; l1 = __float_as_int(cur_kp[j1].w); }
-            if (B.c2 >= 0) { d2 = C[B.c2].dist; l2 = __float_as_int(cur_kp[C[B.c2].i2].w); }
-        } else {  // first and second minima among the free candidates
-            unsigned long long k1 = ~0ull, k2 = ~0ull;
-            for (int k = lane; k < n; k += 64) {
-                const Cand q = C[k];
-                if (q.dist < 256 && !owner_obs[q.i2]) {
-                    const unsigned long long kk = ((unsigned long long)q.dist << 32) | (unsigned)k;
-                    if (kk < k1) { k2 = k1; k1 = kk; }
-                    else if (kk < k2) k2 = kk;
-                }
-            }
-            for (int off = 32; off > 0; off >>= 1) {  // merge (k1, k2) pairs across lanes
-                const unsigned long long o1 = __shfl_xor(k1, off, 64), o2 = __shfl_xor(k2, off, 64);
-                const unsigned long long m1 = o1 < k1 ? o1 : k1;
-                const unsigned long long hi = o1 < k1 ? k1 : o1;
-                const unsigned long long lo2 = o2 < k2 ? o2 : k2;
-                k2 = hi < lo2 ? hi : lo2;
-                k1 = m1;
-            }
-            if (k1 != ~0ull) {
-                d1 = (int)(k1 >> 32);
-                j1 = C[(int)(k1 & 0xffffffffu)].i2;
-                l1 = __float_as_int(cur_kp[j1].w);
-            }
-            if (k2 != ~0ull) {
-                d2 = (int)(k2 >> 32);
-                l2 = __float_as_int(cur_kp[C[(int)(k2 & 0xffffffffu)].i2].w);
+    for (;;) {
+        for (int j = tid; j < a.n_cur; j += kResolveThreads) minNF[j] = INT32_MAX;
+        __syncthreads();
+        for (int i = tid; i < a.n_pts; i += kResolveThreads) {
+            if (a.st[i] != -2 || !a.observed[i]) continue;
+            const Cand* C = a.cands + (size_t)i * a.cap;
+            const unsigned long long bnd = a.bound[i];
+            for (int k = 0, n = a.ncand[i]; k < n; ++k) {  // the candidates point i might still claim
+                const Cand c = C[k];
+                if (c.dist >= 256 || (a.taken0 && a.taken0[c.i2]) || claimed[c.i2] < i) continue;
+                if ((((unsigned long long)c.dist << 32) | (unsigned)k) <= bnd) atomicMin(&minNF[c.i2], i);
             }
         }
         __syncthreads();
-        if (j1 >= 0 && d1 <= kThHigh) {
-            const bool ratio_fail = (l1 == l2) && ((float)d1 > P.nnratio * (float)d2);  // src:146-148
-            if (!ratio_fail) {
-                if (lane == 0) {
-                    match[j1] = i;
-                    owner_obs[j1] = observed[i];
+        int left = 0;
+        for (int i = tid; i < a.n_pts; i += kResolveThreads) {
+            if (a.st[i] != -2) continue;
+            const Cand* C = a.cands + (size_t)i * a.cap;
+            unsigned long long m1 = kNone, m2 = kNone, u = kNone;
+            for (int k = 0, n = a.ncand[i]; k < n; ++k) {
+                const Cand c = C[k];
+                if (c.dist >= 256) continue;  // never below the initial bestDist / bestDist2 of 256
+                if (a.taken0 && a.taken0[c.i2]) continue;
+                if (__hip_atomic_load(&claimed[c.i2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < i) continue;
+                const unsigned long long key = ((unsigned long long)c.dist << 32) | (unsigned)k;
+                if (minNF[c.i2] < i) {
+                    u = key < u ? key : u;
+                } else if (key < m1) {
+                    m2 = m1;
+                    m1 = key;
+                } else if (key < m2) {
+                    m2 = key;
                 }
-                ++nm;
+            }
+            const unsigned long long need = a.local ? m2 : m1;
+            if (u != kNone && (need == kNone || u < need)) {
+                a.bound[i] = m1;
+                ++left;
+                continue;
+            }
+            int res = -1;
+            if (m1 != kNone) {
+                const int d1 = (int)(m1 >> 32), j1 = C[(int)(m1 & 0xffffffffu)].i2;
+                bool ok = d1 <= kThHigh;
+                if (ok && a.local) {  // src:148-155
+                    const int l1 = __float_as_int(a.cur_kp[j1].w);
+                    const int l2 = m2 != kNone ? __float_as_int(a.cur_kp[C[(int)(m2 & 0xffffffffu)].i2].w) : -1;
+                    const int d2 = m2 != kNone ? (int)(m2 >> 32) : 256;
+                    ok = !(l1 == l2 && (float)d1 > a.nnratio * (float)d2);
+                }
+                if (ok) res = j1;
+            }
+            if (res >= 0 && a.observed[i])
+                __hip_atomic_store(&claimed[res], i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            a.st[i] = res;
+        }
+        if (__syncthreads_count(left) == 0) break;
+    }
+    // results
+    int nsucc = 0;
+    for (int i = tid; i < a.n_pts; i += kResolveThreads) {
+        const int j = a.st[i];
+        if (j < 0) continue;
+        ++nsucc;
+        atomicMax(&a.last[j], i);
+        if (a.check_ori) atomicAdd(&hist[rot_bin(a.last_angle[i], a.cur_kp[j].z)], 1);
+    }
+    atomicAdd(&cnt[0], nsucc);
+    __syncthreads();
+    if (a.check_ori) {
+        if (tid == 0) {  // ComputeThreeMaxima (src:2336-2378)
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+            for (int b = 0; b < kHisto; ++b) {
+                const int s = hist[b];
+                if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = b; }
+                else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = b; }
+                else if (s > max3) { max3 = s; ind3 = b; }
+            }
+            if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+            else if (max3 < 0.1f * (float)max1) ind3 = -1;
+            keep[0] = ind1; keep[1] = ind2; keep[2] = ind3;
+        }
+        __syncthreads();
+        int nrem = 0;
+        for (int i = tid; i < a.n_pts; i += kResolveThreads) {
+            const int j = a.st[i];
+            if (j < 0) continue;
+            const int b = rot_bin(a.last_angle[i], a.cur_kp[j].z);
+            if (b != keep[0] && b != keep[1] && b != keep[2]) {
+                a.removed[j] = 1;
+                ++nrem;
             }
         }
+        atomicAdd(&cnt[1], nrem);
         __syncthreads();
     }
-    if (lane == 0) *out_n = nm;
+    for (int j = tid; j < a.n_cur; j += kResolveThreads) a.mp[j] = a.removed[j] ? -1 : a.last[j];
+    if (tid == 0) *a.out_n = cnt[0] - cnt[1];
 }
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -445,8 +459,9 @@ extern "C" int orb_search_by_projection_frame(orb_matcher_t m, const orb_frame_v
         const size_t o_bc = off; off = align256(off + (size_t)nl * 4);
         const size_t o_ovf = off; off = align256(off + 16);
         const size_t o_mp = off; off = align256(off + (size_t)std::max(n, 1) * 4);
-        const size_t o_mi = off; off = align256(off + (size_t)std::max(nl, 1) * 4);
-        const size_t o_mb = off; off = align256(off + (size_t)std::max(nl, 1) * 4);
+        const size_t o_st = off; off = align256(off + (size_t)std::max(nl, 1) * 4);
+        const size_t o_bd2 = off; off = align256(off + (size_t)std::max(nl, 1) * 8);
+        const size_t o_kw = off; off = align256(off + (size_t)std::max(n, 1) * 16);  // minNF, claimed, last, removed
         if (int rc = orbgpu_matcher_reserve(m, off, &d, &h, &s, &check_ori)) return rc;
         P.check_ori = check_ori;
         memcpy(h + o_p, &P, sizeof(P));
@@ -481,23 +496,32 @@ extern "C" int orb_search_by_projection_frame(orb_matcher_t m, const orb_frame_v
                                (const int32_t*)(d + o_lo), (const float4*)(d + o_kp), (const float*)(d + o_ur),
                                (const uint4*)(d + o_cd), (const int32_t*)(d + o_co), (const int32_t*)(d + o_ci),
                                (Cand*)(d + o_cand), (int32_t*)(d + o_nc), (int32_t*)(d + o_bc), (int32_t*)(d + o_ovf));
-        int32_t ovf = 0;
-        ok = ok && hipMemcpyAsync(&ovf, d + o_ovf, 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
+        ResolveArgs ra{};
+        ra.n_pts = nl; ra.n_cur = n; ra.cap = P.cap; ra.local = 0; ra.check_ori = check_ori; ra.nnratio = 0.f;
+        ra.cands = (const Cand*)(d + o_cand); ra.ncand = (const int32_t*)(d + o_nc); ra.observed = (const uint8_t*)(d + o_ob);
+        ra.taken0 = nullptr; ra.cur_kp = (const float4*)(d + o_kp); ra.last_angle = (const float*)(d + o_la);
+        ra.overflow = (const int32_t*)(d + o_ovf); ra.st = (int32_t*)(d + o_st);
+        int32_t* kw = (int32_t*)(d + o_kw);
+        const size_t nk = (size_t)std::max(n, 1);
+        ra.minNF = kw; ra.claimed = kw + nk; ra.last = kw + 2 * nk; ra.removed = kw + 3 * nk;
+        ra.bound = (unsigned long long*)(d + o_bd2);
+        ra.lds_keypoints = n <= kResolveLdsKeypoints ? 1 : 0;
+        ra.mp = (int32_t*)(d + o_mp); ra.out_n = (int32_t*)(d + o_ovf) + 1;
+        // candidates and the rounds back to back, one synchronisation; an overflowing candidate pass
+        // (a point with more candidates than the capacity) makes the resolve a no-op and is re-run
+        if (ok)
+            hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 8 * (size_t)n : 0, s, ra);
+        ok = ok && hipGetLastError() == hipSuccess &&
+             hipMemcpyAsync(h + o_mp, d + o_mp, (size_t)std::max(n, 1) * 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
+             hipMemcpyAsync(h + o_ovf, d + o_ovf, 16, hipMemcpyDeviceToHost, s) == hipSuccess &&
              hipStreamSynchronize(s) == hipSuccess;
-        if (!ok) return orbgpu_fail(ORB_ERR_DEVICE, "SearchByProjection candidate pass failed");
+        if (!ok) return orbgpu_fail(ORB_ERR_DEVICE, "SearchByProjection failed");
+        int32_t ovf = 0;
+        memcpy(&ovf, h + o_ovf, 4);
         if (ovf > P.cap) {  // a point had more candidates than the capacity: redo with room for all
             P.cap = (ovf + 63) & ~63;
             continue;
         }
-        hipLaunchKernelGGL(k_proj_resolve, dim3(1), dim3(64), 0, s, (const ProjParams*)(d + o_p), (const Cand*)(d + o_cand),
-                           (const int32_t*)(d + o_nc), (const int32_t*)(d + o_bc), (const uint8_t*)(d + o_ob),
-                           (const float*)(d + o_la), (const float4*)(d + o_kp), (int32_t*)(d + o_mp),
-                           (int32_t*)(d + o_mi), (int32_t*)(d + o_mb), (int32_t*)(d + o_ovf + 4));
-        ok = hipGetLastError() == hipSuccess &&
-             hipMemcpyAsync(h + o_mp, d + o_mp, (size_t)std::max(n, 1) * 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
-             hipMemcpyAsync(h + o_ovf, d + o_ovf, 16, hipMemcpyDeviceToHost, s) == hipSuccess &&
-             hipStreamSynchronize(s) == hipSuccess;
-        if (!ok) return orbgpu_fail(ORB_ERR_DEVICE, "SearchByProjection resolve failed");
         if (n) memcpy(match, h + o_mp, (size_t)n * 4);
         memcpy(n_matches, h + o_ovf + 4, 4);
         return ORB_OK;
@@ -564,8 +588,10 @@ extern "C" int orb_search_by_projection_local(orb_matcher_t m, const orb_frame_v
         const size_t o_nc = off; off = align256(off + (size_t)np * 4);
         const size_t o_b2 = off; off = align256(off + (size_t)np * sizeof(Best2));
         const size_t o_ovf = off; off = align256(off + 16);
-        const size_t o_own = off; off = align256(off + (size_t)std::max(n, 1) * 4);
         const size_t o_m = off; off = align256(off + (size_t)std::max(n, 1) * 4);
+        const size_t o_st = off; off = align256(off + (size_t)std::max(np, 1) * 4);
+        const size_t o_bd2 = off; off = align256(off + (size_t)std::max(np, 1) * 8);
+        const size_t o_kw = off; off = align256(off + (size_t)std::max(n, 1) * 16);  // minNF, claimed, last, removed
         if (int rc = orbgpu_matcher_reserve(m, off, &d, &h, &s, &check_ori)) return rc;
         P.nnratio = orbgpu_matcher_nnratio(m);
         memcpy(h + o_p, &P, sizeof(P));
@@ -600,23 +626,30 @@ extern "C" int orb_search_by_projection_local(orb_matcher_t m, const orb_frame_v
                                (const uint4*)(d + o_md), (const float4*)(d + o_kp), (const float*)(d + o_ur),
                                (const uint4*)(d + o_cd), (const int32_t*)(d + o_co), (const int32_t*)(d + o_ci),
                                (Cand*)(d + o_cand), (int32_t*)(d + o_nc), (Best2*)(d + o_b2), (int32_t*)(d + o_ovf));
-        int32_t ovf = 0;
-        ok = ok && hipMemcpyAsync(&ovf, d + o_ovf, 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
+        ResolveArgs ra{};
+        ra.n_pts = np; ra.n_cur = n; ra.cap = P.cap; ra.local = 1; ra.check_ori = 0; ra.nnratio = P.nnratio;
+        ra.cands = (const Cand*)(d + o_cand); ra.ncand = (const int32_t*)(d + o_nc); ra.observed = (const uint8_t*)(d + o_ob);
+        ra.taken0 = frame_taken ? (const uint8_t*)(d + o_tk) : nullptr; ra.cur_kp = (const float4*)(d + o_kp);
+        ra.last_angle = nullptr; ra.overflow = (const int32_t*)(d + o_ovf); ra.st = (int32_t*)(d + o_st);
+        int32_t* kw = (int32_t*)(d + o_kw);
+        const size_t nk = (size_t)std::max(n, 1);
+        ra.minNF = kw; ra.claimed = kw + nk; ra.last = kw + 2 * nk; ra.removed = kw + 3 * nk;
+        ra.bound = (unsigned long long*)(d + o_bd2);
+        ra.lds_keypoints = n <= kResolveLdsKeypoints ? 1 : 0;
+        ra.mp = (int32_t*)(d + o_m); ra.out_n = (int32_t*)(d + o_ovf) + 1;
+        if (ok)
+            hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 8 * (size_t)n : 0, s, ra);
+        ok = ok && hipGetLastError() == hipSuccess &&
+             hipMemcpyAsync(h + o_m, d + o_m, (size_t)std::max(n, 1) * 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
+             hipMemcpyAsync(h + o_ovf, d + o_ovf, 16, hipMemcpyDeviceToHost, s) == hipSuccess &&
              hipStreamSynchronize(s) == hipSuccess;
-        if (!ok) return orbgpu_fail(ORB_ERR_DEVICE, "SearchByProjection(local) candidate pass failed");
+        if (!ok) return orbgpu_fail(ORB_ERR_DEVICE, "SearchByProjection(local) failed");
+        int32_t ovf = 0;
+        memcpy(&ovf, h + o_ovf, 4);
         if (ovf > P.cap) {
             P.cap = (ovf + 63) & ~63;
             continue;
         }
-        hipLaunchKernelGGL(k_lmp_resolve, dim3(1), dim3(64), 0, s, (const LocalParams*)(d + o_p), (const Cand*)(d + o_cand),
-                           (const int32_t*)(d + o_nc), (const Best2*)(d + o_b2), (const uint8_t*)(d + o_ob),
-                           frame_taken ? (const uint8_t*)(d + o_tk) : nullptr, (const float4*)(d + o_kp),
-                           (int32_t*)(d + o_own), (int32_t*)(d + o_m), (int32_t*)(d + o_ovf + 4));
-        ok = hipGetLastError() == hipSuccess &&
-             hipMemcpyAsync(h + o_m, d + o_m, (size_t)std::max(n, 1) * 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
-             hipMemcpyAsync(h + o_ovf, d + o_ovf, 16, hipMemcpyDeviceToHost, s) == hipSuccess &&
-             hipStreamSynchronize(s) == hipSuccess;
-        if (!ok) return orbgpu_fail(ORB_ERR_DEVICE, "SearchByProjection(local) resolve failed");
         if (n) memcpy(match, h + o_m, (size_t)n * 4);
         memcpy(n_matches, h + o_ovf + 4, 4);
         return ORB_OK;

@@ -114,6 +114,45 @@ class ShardedExtractor:
         return g_kps, g_desc, g_cnt
 
 
+def _knn2_device(query, train):
+    from .matcher import ORBmatcher
+    return ORBmatcher.knn2_device(query, train)
+
+
+def distributed_knn2(query, train, group=None, local_fn=None):
+    """Best / second-best Hamming match of every query row against the whole train set, with the
+    query rows split over the ranks (Hamming matching): rank r matches rows
+    [r * P, (r + 1) * P), P = ceil(n_query / world), locally (knn2 kernel, orb_hamming_knn2_device) and one all-gather
+    of the per-query results (best index, best distance, second distance: 12 B per query) gives every
+    rank the full answer.  Every rank passes the same query and train tensors (uint8 [n, 32]; e.g. a
+    frame's descriptors and the all-gathered descriptors of the other frames).  The result equals
+    the single-device knn2 exactly: each query's scan is unchanged, only the rows are distributed.
+    `local_fn(query_rows, train) -> (idx, best, second)` replaces the device kernel (CPU tests)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    n = query.shape[0]
+    fn = local_fn or _knn2_device
+    if world == 1:
+        return fn(query, train)
+    per = (n + world - 1) // world  # equal blocks for all_gather_into_tensor; the last one is padded
+    b0, b1 = min(n, rank * per), min(n, (rank + 1) * per)
+    idx, d1, d2 = fn(query[b0:b1], train)
+    block = torch.full((3, per), -1, dtype=torch.int32, device=query.device)
+    if b1 > b0:
+        block[0, : b1 - b0] = idx
+        block[1, : b1 - b0] = d1
+        block[2, : b1 - b0] = d2
+    gathered = torch.empty((world * 3, per), dtype=torch.int32, device=query.device)
+    if dist.get_backend(group) == "gloo" and block.is_cuda:
+        host = torch.empty((world * 3, per), dtype=torch.int32)
+        dist.all_gather_into_tensor(host, block.cpu(), group=group)
+        gathered.copy_(host)
+    else:
+        dist.all_gather_into_tensor(gathered, block, group=group)
+    flat = gathered.view(world, 3, per).permute(1, 0, 2).reshape(3, world * per)[:, :n]
+    return flat[0].contiguous(), flat[1].contiguous(), flat[2].contiguous()
+
+
 def frame_descriptors(g_desc, g_cnt, frame: int):
     """Descriptors of global frame `frame` from the gathered blocks (a view, count rows)."""
     n = int(g_cnt[frame, 0])

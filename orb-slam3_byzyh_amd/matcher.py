@@ -98,6 +98,38 @@ class ORBmatcher:
               "orb_hamming_knn2_device")
         return idx, d1, d2
 
+    def ComputeDistinctiveDescriptors(self, desc, offsets):
+        """MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:438-529) for a batch of map points:
+        point p's observation descriptors are rows offsets[p]..offsets[p+1] of desc (uint8 [n, 32]).
+        Returns (best int32[P], mDescriptor uint8[P, 32]); best -1 / a zero row for a point without
+        descriptors (the reference leaves its mDescriptor unchanged)."""
+        desc = np.ascontiguousarray(desc, dtype=np.uint8).reshape(-1, 32)
+        offsets = np.ascontiguousarray(offsets, dtype=np.int32)
+        n = len(offsets) - 1
+        best = np.full(max(n, 1), -1, np.int32)
+        out = np.zeros((max(n, 1), 32), np.uint8)
+        check(_lib.load().orb_compute_distinctive_descriptors(self._handle(), desc.ctypes.data, offsets.ctypes.data, n,
+                                                              best.ctypes.data, out.ctypes.data),
+              "orb_compute_distinctive_descriptors")
+        return best[:n], out[:n]
+
+    @staticmethod
+    def compute_distinctive_descriptors_device(desc, offsets, out=None, stream=None):
+        """The same on device tensors (desc uint8 [n, 32], offsets int32 [P + 1]); async on `stream`.
+        Returns (best int32 [P], out uint8 [P, 32])."""
+        import torch
+        d = desc.contiguous()
+        o = offsets.contiguous()
+        n = o.shape[0] - 1
+        best = torch.empty(max(n, 1), dtype=torch.int32, device=d.device)
+        if out is None:
+            out = torch.zeros((max(n, 1), 32), dtype=torch.uint8, device=d.device)
+        st = stream if stream is not None else torch.cuda.current_stream(d.device)
+        check(_lib.load().orb_compute_distinctive_descriptors_device(d.data_ptr(), o.data_ptr(), n, best.data_ptr(),
+                                                                     out.data_ptr(), ctypes.c_void_p(st.cuda_stream)),
+              "orb_compute_distinctive_descriptors_device")
+        return best[:n], out[:n]
+
     def SearchByProjectionFrame(self, CurrentFrame: Frame, LastFrame: Frame, th: float, bMono: bool):
         """SearchByProjection(Frame &CurrentFrame, const Frame &LastFrame, th, bMono)
         (src/ORBmatcher.cc:1951-2185).  Returns (nmatches, match) with match[i2] = the LastFrame index

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <tuple>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -31,12 +32,15 @@ static int g_fail = 0;
     } while (0)
 
 // ---- mock reference objects ------------------------------------------------------------------------
+struct MockKF;
 struct MockMP {
     int obs = 1;
     bool bad = false;
     float X[3] = {0, 0, 0};
     uint8_t desc[32] = {};
     orbgpu::TrackFields track;
+    std::map<MockKF*, std::tuple<int, int>> obsmap;
+    bool desc_set = false;
 };
 
 struct MockKF {
@@ -47,7 +51,7 @@ struct MockKF {
     std::map<unsigned int, std::vector<unsigned int>> fv;
     float K[4] = {458.654f, 457.296f, 367.215f, 248.375f};
     std::vector<float> scale{1.f, 1.2f, 1.44f}, sigma2{1.f, 1.44f, 2.0736f};
-    bool cam2 = false;
+    bool cam2 = false, bad = false;
     int tag = 0;  // identifies the keyframe in PairGeometry
 };
 
@@ -108,6 +112,13 @@ struct Access {
     static void WorldPos(MapPoint* p, float X[3]) { std::memcpy(X, p->X, sizeof p->X); }
     static void Descriptor(MapPoint* p, uint8_t d[32]) { std::memcpy(d, p->desc, 32); }
     static void Track(MapPoint* p, orbgpu::TrackFields* t) { *t = p->track; }
+    static std::map<KeyFrame*, std::tuple<int, int>> ObservationMap(MapPoint* p) { return p->obsmap; }
+    static bool IsBad(KeyFrame* k) { return k->bad; }
+    static const uint8_t* DescriptorRow(KeyFrame* k, int idx) { return k->desc.data() + 32 * idx; }
+    static void SetDescriptor(MapPoint* p, const uint8_t d[32]) {
+        std::memcpy(p->desc, d, 32);
+        p->desc_set = true;
+    }
 };
 using Matcher = orbgpu::ORBmatcher<Access>;
 
@@ -144,6 +155,18 @@ int orb_descriptor_distance(const uint8_t* a, const uint8_t* b) {
     int d = 0;
     for (int i = 0; i < 32; ++i) d += __builtin_popcount((unsigned)(a[i] ^ b[i]));
     return d;
+}
+static std::vector<uint8_t> g_dd_rows;
+static std::vector<int32_t> g_dd_off;
+int orb_compute_distinctive_descriptors(orb_matcher_t, const uint8_t* desc, const int32_t* offsets, int n_points,
+                                        int32_t* best, uint8_t* out) {
+    g_dd_off.assign(offsets, offsets + n_points + 1);
+    g_dd_rows.assign(desc, desc + 32 * (size_t)offsets[n_points]);
+    for (int p = 0; p < n_points; ++p) {  // the double picks each point's last row
+        best[p] = offsets[p + 1] - offsets[p] - 1;
+        std::memcpy(out + 32 * p, desc + 32 * (size_t)(offsets[p + 1] - 1), 32);
+    }
+    return ORB_OK;
 }
 int orb_matcher_create(float nnratio, int check_orientation, orb_matcher_t* out) {
     ++g_creates;
@@ -371,7 +394,34 @@ static void test_errors_and_handles() {
     CHECK(Matcher::DescriptorDistance(k1.desc.data(), k2.desc.data()) == 0);
 }
 
+static void test_distinctive_batch() {
+    // keyframes laid out in one array: std::map<MockKF*> order = index order
+    MockKF K[3];
+    for (int k = 0; k < 3; ++k) {
+        K[k] = make_kf(4, k);
+        for (int r = 0; r < 4; ++r) K[k].desc[32 * r] = (uint8_t)(10 * k + r);  // row tag in byte 0
+    }
+    K[1].bad = true;
+    MockMP a, b, c, d, e;
+    a.obsmap[&K[2]] = std::make_tuple(1, 3);   // left 1 then right 3
+    a.obsmap[&K[0]] = std::make_tuple(2, -1);
+    a.obsmap[&K[1]] = std::make_tuple(0, -1);  // bad keyframe: skipped
+    b.bad = true;                               // bad point: skipped
+    b.obsmap[&K[0]] = std::make_tuple(0, -1);
+    // c: no observations -> skipped
+    d.obsmap[&K[1]] = std::make_tuple(1, -1);   // only a bad keyframe -> no rows -> skipped
+    e.obsmap[&K[0]] = std::make_tuple(-1, 0);   // right index only
+    orbgpu::ComputeDistinctiveDescriptors<Access>(std::vector<MockMP*>{&a, &b, nullptr, &c, &d, &e});
+    CHECK((g_dd_off == std::vector<int32_t>{0, 3, 4}));
+    std::vector<int> tags;
+    for (size_t r = 0; r < g_dd_rows.size() / 32; ++r) tags.push_back(g_dd_rows[32 * r]);
+    CHECK((tags == std::vector<int>{2, 21, 23, 0}));  // a: K0 row 2, K2 rows 1 and 3; e: K0 row 0
+    CHECK(a.desc_set && a.desc[0] == 23 && e.desc_set && e.desc[0] == 0);
+    CHECK(!b.desc_set && !c.desc_set && !d.desc_set);
+}
+
 int main() {
+    test_distinctive_batch();
     test_search_for_triangulation();
     test_search_by_projection_frame();
     test_search_by_projection_local();

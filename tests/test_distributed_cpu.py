@@ -126,3 +126,56 @@ def test_ba_host_reducer_gloo_world2(pkg):
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def _np_knn2(query, train):
+    """Reference scan (src/ORBmatcher.cc:1160-1175 order): best, first index of it, second smallest."""
+    import numpy as np
+    q, t = query.numpy(), train.numpy()
+    n = q.shape[0]
+    if n == 0:
+        z = torch.zeros(0, dtype=torch.int32)
+        return z, z.clone(), z.clone()
+    pc = np.unpackbits(np.arange(256, dtype=np.uint8)[:, None], axis=1).sum(1).astype(np.int32)
+    D = pc[q[:, None, :] ^ t[None, :, :]].sum(axis=2)
+    srt = np.sort(D, axis=1)
+    second = srt[:, 1] if t.shape[0] > 1 else np.full(n, 257)
+    return (torch.from_numpy(np.argmin(D, axis=1).astype(np.int32)), torch.from_numpy(srt[:, 0].astype(np.int32)),
+            torch.from_numpy(second.astype(np.int32)))
+
+
+def _knn_worker(rank, world, port, nq, nt, q_out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from conftest import load_package
+        load_package()
+        from orbslam3_amd import distributed as D
+        g = torch.Generator().manual_seed(77)
+        query = torch.randint(0, 256, (nq, 32), generator=g, dtype=torch.uint8)
+        train = torch.randint(0, 256, (nt, 32), generator=g, dtype=torch.uint8)
+        train[5] = query[min(3, nq - 1)]
+        try:
+            idx, d1, d2 = D.distributed_knn2(query, train, local_fn=_np_knn2)
+            ridx, rd1, rd2 = _np_knn2(query, train)
+            q_out.put((rank, bool(torch.equal(idx, ridx) and torch.equal(d1, rd1) and torch.equal(d2, rd2))))
+        except Exception as e:  # noqa: BLE001 -- reported, not left to the queue timeout
+            q_out.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("nq,nt", [(1000, 300), (7, 50), (1, 20)])
+def test_distributed_knn2_query_split_gloo_world2(pkg, nq, nt):
+    """SURVEY.md 8(e) Hamming matching: the query rows split over 2 ranks (one rank may get none) and
+    the per-query (best index, best, second) all-gathered equal the single-device scan on every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_knn_worker, args=(r, 2, port, nq, nt, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}

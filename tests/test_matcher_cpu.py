@@ -168,3 +168,40 @@ def test_matcher_without_gpu_fails_loudly(pkg):
         pytest.skip("a GPU is visible")
     h = ctypes.c_void_p()
     assert lib.orb_matcher_create(0.6, 0, ctypes.byref(h)) == pkg._lib.ORB_ERR_DEVICE
+
+
+def _distinctive_py(desc, offsets):
+    """Pure-Python reading of MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:438-529)."""
+    out = []
+    for p in range(len(offsets) - 1):
+        rows = desc[offsets[p]:offsets[p + 1]]
+        N = len(rows)
+        if N == 0:
+            out.append(-1)
+            continue
+        D = [[int(np.unpackbits(rows[i] ^ rows[j]).sum()) for j in range(N)] for i in range(N)]
+        best_m, best_i = 2 ** 31 - 1, 0
+        for i in range(N):
+            med = sorted(D[i])[int(0.5 * (N - 1))]
+            if med < best_m:
+                best_m, best_i = med, i
+        out.append(best_i)
+    return np.array(out, np.int32)
+
+
+def test_oracle_distinctive_descriptors(oracle):
+    """The oracle's ComputeDistinctiveDescriptors against a pure-Python reading, including the
+    median index truncation (even N) and first-index ties (copies of one descriptor)."""
+    rng = np.random.default_rng(17)
+    sizes = [0, 1, 2, 3, 4, 5, 8, 13, 30, 0, 64, 2]
+    rows = []
+    for n in sizes:
+        base = rng.integers(0, 256, 32, dtype=np.uint8)
+        blk = np.repeat(base[None], n, 0)
+        for r in range(n):  # noisy copies of one base, a few exact duplicates
+            if r % 4:
+                blk[r] ^= (rng.random(32) < 0.15).astype(np.uint8) * rng.integers(1, 256, 32, dtype=np.uint8)
+        rows.append(blk)
+    desc = np.concatenate(rows) if rows else np.zeros((0, 32), np.uint8)
+    offsets = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
+    assert np.array_equal(oracle.compute_distinctive_descriptors(desc, offsets), _distinctive_py(desc, offsets))

@@ -84,3 +84,34 @@ def test_invalid_views_rejected(pkg, scene):
     bad["octave"][0] = 12  # beyond nlevels
     with pytest.raises(pkg.OrbGpuError):
         matcher.SearchForTriangulationMany(k1, [_variant(pkg, k2, keys_un=bad)], False, False)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_compute_distinctive_descriptors_parity(pkg, oracle, seed):
+    """MapPoint::ComputeDistinctiveDescriptors batched: best row and mDescriptor equal the oracle for
+    point sizes 0..300 (lanes looping over rows beyond 64), duplicates (ties) and random rows."""
+    import torch
+    rng = np.random.default_rng(seed)
+    sizes = [0, 1, 2, 3, 4, 7, 16, 63, 64, 65, 128, 300, 0, 5] + list(rng.integers(1, 40, 200))
+    rows = []
+    for n in sizes:
+        base = rng.integers(0, 256, 32, dtype=np.uint8)
+        blk = np.repeat(base[None], n, 0)
+        flip = rng.random((n, 32)) < rng.uniform(0.02, 0.3)
+        blk ^= (flip * rng.integers(1, 256, (n, 32))).astype(np.uint8)
+        if n > 4:
+            blk[n // 2] = blk[1]  # an exact duplicate
+        rows.append(blk)
+    desc = np.concatenate(rows)
+    offsets = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
+    ref = oracle.compute_distinctive_descriptors(desc, offsets)
+    m = pkg.ORBmatcher(0.6, False)
+    best, out = m.ComputeDistinctiveDescriptors(desc, offsets)
+    assert np.array_equal(best, ref)
+    for p, b in enumerate(ref):
+        exp = desc[offsets[p] + b] if b >= 0 else np.zeros(32, np.uint8)
+        assert np.array_equal(out[p], exp), p
+    dbest, dout = pkg.ORBmatcher.compute_distinctive_descriptors_device(torch.from_numpy(desc).cuda(),
+                                                                       torch.from_numpy(offsets).cuda())
+    assert np.array_equal(dbest.cpu().numpy(), ref)
+    assert np.array_equal(dout.cpu().numpy()[ref >= 0], out[ref >= 0])

@@ -2,7 +2,7 @@
 # A/B of extraction env settings on the GPU box: the default and each variant, twice, interleaved.
 #   tools/ab_multi.sh "VAR=1 VAR2=2" "VAR=3" ...
 set -u
-ARGS="--no-cpu-baseline --no-ba --no-stereo --no-pose --no-bow --no-single --no-c4"
+ARGS="--no-cpu-baseline --no-ba --no-stereo --no-pose --no-bow --no-single --no-c4 --no-matchers"
 for rep in 1 2; do
   timeout -k 10 120 python3 bench.py $ARGS > gpurun_out/abm_base_$rep.json 2>/dev/null || exit 1
   i=0

@@ -3,7 +3,7 @@
 # bench's kernels.  Usage (on the GPU box): tools/pmc_run.sh OUTDIR "bench args"
 set -u
 OUT=${1:-gpurun_out/pmc}
-ARGS=${2:---steps 3 --warmup 1 --no-cpu-baseline --no-ba --no-stereo --no-pose --no-bow --no-single --no-c4}
+ARGS=${2:---steps 3 --warmup 1 --no-cpu-baseline --no-ba --no-stereo --no-pose --no-bow --no-single --no-c4 --no-matchers}
 export TMPDIR=/tmp
 mkdir -p "$OUT"
 i=0

@@ -6,7 +6,7 @@ set -u
 export TMPDIR=/tmp
 O=gpurun_out/round
 mkdir -p $O
-EX="--no-cpu-baseline --no-ba --no-stereo --no-pose --no-bow --no-single --no-c4"
+EX="--no-cpu-baseline --no-ba --no-stereo --no-pose --no-bow --no-single --no-c4 --no-matchers"
 timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o bench -- python3 bench.py $EX > $O/stats_bench.json 2> $O/stats.log || { echo "stats failed"; exit 1; }
 python3 tools/timed_kernel_avg.py $O/stats/bench_kernel_trace.csv 20 > $O/timed_kernel_avg.txt || exit 1
