@@ -48,75 +48,127 @@ __device__ __forceinline__ int hamming(const uint4& a0, const uint4& a1, const u
            __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
 
-__global__ __launch_bounds__(256) void k_proj_candidates(const ProjParams* __restrict__ pp, const uint8_t* __restrict__ valid,
+// One wave scans one point's grid window (Frame::GetFeaturesInArea, src/Frame.cc:859-951) in the
+// reference's order -- cells ix outer, iy inner, keypoints of a cell in index order -- with the lanes
+// spread over the window: 64 cells at a time, a wave prefix sum of the cells' keypoint counts, then
+// 64 keypoints at a time (lane -> cell by binary search of the prefix), `test(j)` -> Hamming distance
+// or -1, and an order-preserving ballot compaction into out[0 .. cap).  Returns the candidate count
+// (wave-uniform; counted beyond cap).
+template <class Test>
+__device__ __forceinline__ int window_candidates(int lane, int* __restrict__ pre, int* __restrict__ beg,
+                                                 const int32_t* __restrict__ cell_off, const int32_t* __restrict__ cell_idx,
+                                                 int x0, int x1, int y0, int y1, Cand* __restrict__ out, int cap,
+                                                 Test test) {
+    const int ny = y1 - y0 + 1, ncells = (x1 - x0 + 1) * ny;
+    int n = 0;
+    for (int c0 = 0; c0 < ncells; c0 += 64) {
+        const int t = c0 + lane;
+        int b = 0, cnt = 0;
+        if (t < ncells) {
+            const int cell = (x0 + t / ny) * kGridRows + (y0 + t % ny);
+            b = cell_off[cell];
+            cnt = cell_off[cell + 1] - b;
+        }
+        int incl = cnt;  // inclusive prefix over the lanes
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        const int total = __shfl(incl, 63, 64);
+        pre[lane] = incl - cnt;
+        beg[lane] = b;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        for (int i0 = 0; i0 < total; i0 += 64) {
+            const int it = i0 + lane;
+            int j = -1, dist = -1;
+            if (it < total) {
+                int lo = 0, hi = 63;  // the last cell lane whose prefix is <= it
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (pre[mid] <= it) lo = mid;
+                    else hi = mid - 1;
+                }
+                j = cell_idx[beg[lo] + it - pre[lo]];
+                dist = test(j);
+            }
+            const unsigned long long m = __ballot(dist >= 0);
+            const int pos = n + (int)__popcll(m & ((1ull << lane) - 1ull));
+            if (dist >= 0 && pos < cap) out[pos] = Cand{j, dist};
+            n += (int)__popcll(m);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    }
+    return n;
+}
+
+constexpr int kCandWaves = 4;
+
+// one wave per last-frame point (src:1978-2062 up to the minimum): project with the current pose,
+// the window by forward / backward motion (src:2019-2024), the stereo u_R test, distances
+__global__ __launch_bounds__(64 * kCandWaves) void k_proj_candidates(const ProjParams* __restrict__ pp, const uint8_t* __restrict__ valid,
                                                          const float* __restrict__ xyz, const uint4* __restrict__ mp_desc,
                                                          const int32_t* __restrict__ last_octave,
                                                          const float4* __restrict__ cur_kp,  // x, y, angle, octave bits
                                                          const float* __restrict__ cur_ur, const uint4* __restrict__ cur_desc,
                                                          const int32_t* __restrict__ cell_off, const int32_t* __restrict__ cell_idx,
                                                          Cand* __restrict__ cands, int32_t* __restrict__ ncand,
-                                                         int32_t* __restrict__ best_c, int32_t* __restrict__ overflow) {
+                                                         int32_t* __restrict__ overflow) {
+    __shared__ int pre_s[kCandWaves][64], beg_s[kCandWaves][64];
     const ProjParams& P = *pp;
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int i = blockIdx.x * kCandWaves + w;
     if (i >= P.n_last) return;
-    ncand[i] = 0;
-    best_c[i] = -1;
-    if (!valid[i]) return;
-    const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
-    float c[3];
+    int n = 0;
+    if (valid[i]) {
+        const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+        float c[3];
 #pragma unroll
-    for (int r = 0; r < 3; ++r)
-        c[r] = __fmaf_rn(P.Tcw[4 * r + 2], z, __fmaf_rn(P.Tcw[4 * r], x, P.Tcw[4 * r + 1] * y)) + P.Tcw[4 * r + 3];
-    const float invzc = (float)(1.0 / (double)c[2]);
-    if (invzc < 0) return;
-    const float u = P.fx * c[0] / c[2] + P.cx;
-    const float v = P.fy * c[1] / c[2] + P.cy;
-    if (u < P.min_x || u > P.max_x || v < P.min_y || v > P.max_y) return;
-    const int oct = last_octave[i];
-    const float radius = P.th * P.scale[oct];
-    int minLevel, maxLevel;
-    if (P.bForward) { minLevel = oct; maxLevel = -1; }
-    else if (P.bBackward) { minLevel = 0; maxLevel = oct; }
-    else { minLevel = oct - 1; maxLevel = oct + 1; }
-    const int nMinCellX = max(0, (int)floorf((u - P.min_x - radius) * P.inv_w));
-    if (nMinCellX >= kGridCols) return;
-    const int nMaxCellX = min(kGridCols - 1, (int)ceilf((u - P.min_x + radius) * P.inv_w));
-    if (nMaxCellX < 0) return;
-    const int nMinCellY = max(0, (int)floorf((v - P.min_y - radius) * P.inv_h));
-    if (nMinCellY >= kGridRows) return;
-    const int nMaxCellY = min(kGridRows - 1, (int)ceilf((v - P.min_y + radius) * P.inv_h));
-    if (nMaxCellY < 0) return;
-    const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
-    const uint4 d0 = mp_desc[2 * (size_t)i], d1 = mp_desc[2 * (size_t)i + 1];
-    const float ur = __fmaf_rn(-P.bf, invzc, u);
-    Cand* out = cands + (size_t)i * P.cap;
-    int n = 0, best = 256, bc = -1;
-    for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
-        for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
-            const int cell = ix * kGridRows + iy;
-            for (int k = cell_off[cell]; k < cell_off[cell + 1]; ++k) {
-                const int j = cell_idx[k];
-                const float4 kp = cur_kp[j];
-                const int koct = __float_as_int(kp.w);
-                if (bCheckLevels) {
-                    if (koct < minLevel) continue;
-                    if (maxLevel >= 0 && koct > maxLevel) continue;
-                }
-                const float distx = kp.x - u, disty = kp.y - v;
-                if (!(fabsf(distx) < radius && fabsf(disty) < radius)) continue;
-                if (P.has_ur && cur_ur[j] > 0) {
-                    const float er = fabsf(ur - cur_ur[j]);
-                    if (er > radius) continue;
-                }
-                const int dist = hamming(d0, d1, cur_desc[2 * (size_t)j], cur_desc[2 * (size_t)j + 1]);
-                if (n < P.cap) out[n] = Cand{j, dist};
-                if (dist < best) { best = dist; bc = n; }
-                ++n;
+        for (int r = 0; r < 3; ++r)
+            c[r] = __fmaf_rn(P.Tcw[4 * r + 2], z, __fmaf_rn(P.Tcw[4 * r], x, P.Tcw[4 * r + 1] * y)) + P.Tcw[4 * r + 3];
+        const float invzc = (float)(1.0 / (double)c[2]);
+        const float u = P.fx * c[0] / c[2] + P.cx;
+        const float v = P.fy * c[1] / c[2] + P.cy;
+        if (!(invzc < 0) && !(u < P.min_x || u > P.max_x || v < P.min_y || v > P.max_y)) {
+            const int oct = last_octave[i];
+            const float radius = P.th * P.scale[oct];
+            int minLevel, maxLevel;
+            if (P.bForward) { minLevel = oct; maxLevel = -1; }
+            else if (P.bBackward) { minLevel = 0; maxLevel = oct; }
+            else { minLevel = oct - 1; maxLevel = oct + 1; }
+            const int x0 = max(0, (int)floorf((u - P.min_x - radius) * P.inv_w));
+            const int x1 = min(kGridCols - 1, (int)ceilf((u - P.min_x + radius) * P.inv_w));
+            const int y0 = max(0, (int)floorf((v - P.min_y - radius) * P.inv_h));
+            const int y1 = min(kGridRows - 1, (int)ceilf((v - P.min_y + radius) * P.inv_h));
+            if (x0 < kGridCols && x1 >= 0 && y0 < kGridRows && y1 >= 0) {
+                const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+                const uint4 d0 = mp_desc[2 * (size_t)i], d1 = mp_desc[2 * (size_t)i + 1];
+                const float ur = __fmaf_rn(-P.bf, invzc, u);
+                n = window_candidates(lane, pre_s[w], beg_s[w], cell_off, cell_idx, x0, x1, y0, y1,
+                                      cands + (size_t)i * P.cap, P.cap, [&](int j) -> int {
+                                          const float4 kp = cur_kp[j];
+                                          const int koct = __float_as_int(kp.w);
+                                          if (bCheckLevels) {
+                                              if (koct < minLevel) return -1;
+                                              if (maxLevel >= 0 && koct > maxLevel) return -1;
+                                          }
+                                          const float distx = kp.x - u, disty = kp.y - v;
+                                          if (!(fabsf(distx) < radius && fabsf(disty) < radius)) return -1;
+                                          if (P.has_ur && cur_ur[j] > 0) {
+                                              const float er = fabsf(ur - cur_ur[j]);
+                                              if (er > radius) return -1;
+                                          }
+                                          return hamming(d0, d1, cur_desc[2 * (size_t)j], cur_desc[2 * (size_t)j + 1]);
+                                      });
             }
         }
-    ncand[i] = n;
-    best_c[i] = bc;
-    if (n > P.cap) atomicMax(overflow, n);
+    }
+    if (lane == 0) {
+        ncand[i] = n;
+        if (n > P.cap) atomicMax(overflow, n);
+    }
 }
 
 __device__ __forceinline__ int rot_bin(float a1, float a2) {
@@ -135,100 +187,81 @@ struct LocalParams {
     int n_cur, n_pts, has_ur, far, nlevels, cap;
 };
 
-// best / second best of the reference's update rule (src:121-138) = the first and second
-// lexicographic minima of (dist, order) among candidates with dist < 256
-struct Best2 {
-    int c1, c2;  // candidate positions, -1 if none
-};
-
-__global__ __launch_bounds__(256) void k_lmp_candidates(const LocalParams* __restrict__ pp, const uint8_t* __restrict__ in_view,
+// one wave per local map point (src:54-143 up to the minima): RadiusByViewingCos, the window at the
+// predicted level (levels level-1 .. level), the stereo u_R test, distances
+__global__ __launch_bounds__(64 * kCandWaves) void k_lmp_candidates(const LocalParams* __restrict__ pp, const uint8_t* __restrict__ in_view,
                                                         const uint8_t* __restrict__ bad, const float* __restrict__ proj,
                                                         const float* __restrict__ view_cos, const float* __restrict__ depth,
                                                         const int32_t* __restrict__ level, const uint4* __restrict__ mp_desc,
                                                         const float4* __restrict__ cur_kp, const float* __restrict__ cur_ur,
                                                         const uint4* __restrict__ cur_desc, const int32_t* __restrict__ cell_off,
                                                         const int32_t* __restrict__ cell_idx, Cand* __restrict__ cands,
-                                                        int32_t* __restrict__ ncand, Best2* __restrict__ best,
-                                                        int32_t* __restrict__ overflow) {
+                                                        int32_t* __restrict__ ncand, int32_t* __restrict__ overflow) {
+    __shared__ int pre_s[kCandWaves][64], beg_s[kCandWaves][64];
     const LocalParams& P = *pp;
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int i = blockIdx.x * kCandWaves + w;
     if (i >= P.n_pts) return;
-    ncand[i] = 0;
-    best[i] = Best2{-1, -1};
-    if (!in_view[i]) return;
-    if (P.far && depth[i] > P.th_far) return;
-    if (bad[i]) return;
-    const int lvl = level[i];
-    float r = ((double)view_cos[i] > 0.998) ? 2.5f : 4.0f;  // RadiusByViewingCos (src:243-250)
-    if (P.th != 1.0f) r *= P.th;
-    const float radius = r * P.scale[lvl];
-    const float x = proj[3 * i], y = proj[3 * i + 1], xr = proj[3 * i + 2];
-    const int minLevel = lvl - 1, maxLevel = lvl;
-    const int nMinCellX = max(0, (int)floorf((x - P.min_x - radius) * P.inv_w));
-    if (nMinCellX >= kGridCols) return;
-    const int nMaxCellX = min(kGridCols - 1, (int)ceilf((x - P.min_x + radius) * P.inv_w));
-    if (nMaxCellX < 0) return;
-    const int nMinCellY = max(0, (int)floorf((y - P.min_y - radius) * P.inv_h));
-    if (nMinCellY >= kGridRows) return;
-    const int nMaxCellY = min(kGridRows - 1, (int)ceilf((y - P.min_y + radius) * P.inv_h));
-    if (nMaxCellY < 0) return;
-    const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
-    const uint4 d0 = mp_desc[2 * (size_t)i], d1 = mp_desc[2 * (size_t)i + 1];
-    Cand* out = cands + (size_t)i * P.cap;
-    int n = 0, b1 = 256, b2 = 256, c1 = -1, c2 = -1;
-    for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
-        for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
-            const int cell = ix * kGridRows + iy;
-            for (int k = cell_off[cell]; k < cell_off[cell + 1]; ++k) {
-                const int j = cell_idx[k];
-                const float4 kp = cur_kp[j];
-                const int koct = __float_as_int(kp.w);
-                if (bCheckLevels) {
-                    if (koct < minLevel) continue;
-                    if (maxLevel >= 0 && koct > maxLevel) continue;
-                }
-                if (!(fabsf(kp.x - x) < radius && fabsf(kp.y - y) < radius)) continue;
-                if (P.has_ur && cur_ur[j] > 0) {
-                    const float er = fabsf(xr - cur_ur[j]);
-                    if (er > r * P.scale[lvl]) continue;
-                }
-                const int dist = hamming(d0, d1, cur_desc[2 * (size_t)j], cur_desc[2 * (size_t)j + 1]);
-                if (n < P.cap) out[n] = Cand{j, dist};
-                if (dist < b1) { b2 = b1; c2 = c1; b1 = dist; c1 = n; }
-                else if (dist < b2) { b2 = dist; c2 = n; }
-                ++n;
-            }
+    int n = 0;
+    if (in_view[i] && !(P.far && depth[i] > P.th_far) && !bad[i]) {
+        const int lvl = level[i];
+        float r = ((double)view_cos[i] > 0.998) ? 2.5f : 4.0f;  // RadiusByViewingCos (src:243-250)
+        if (P.th != 1.0f) r *= P.th;
+        const float radius = r * P.scale[lvl];
+        const float x = proj[3 * i], y = proj[3 * i + 1], xr = proj[3 * i + 2];
+        const int minLevel = lvl - 1, maxLevel = lvl;
+        const int x0 = max(0, (int)floorf((x - P.min_x - radius) * P.inv_w));
+        const int x1 = min(kGridCols - 1, (int)ceilf((x - P.min_x + radius) * P.inv_w));
+        const int y0 = max(0, (int)floorf((y - P.min_y - radius) * P.inv_h));
+        const int y1 = min(kGridRows - 1, (int)ceilf((y - P.min_y + radius) * P.inv_h));
+        if (x0 < kGridCols && x1 >= 0 && y0 < kGridRows && y1 >= 0) {
+            const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+            const uint4 d0 = mp_desc[2 * (size_t)i], d1 = mp_desc[2 * (size_t)i + 1];
+            n = window_candidates(lane, pre_s[w], beg_s[w], cell_off, cell_idx, x0, x1, y0, y1, cands + (size_t)i * P.cap,
+                                  P.cap, [&](int j) -> int {
+                                      const float4 kp = cur_kp[j];
+                                      const int koct = __float_as_int(kp.w);
+                                      if (bCheckLevels) {
+                                          if (koct < minLevel) return -1;
+                                          if (maxLevel >= 0 && koct > maxLevel) return -1;
+                                      }
+                                      if (!(fabsf(kp.x - x) < radius && fabsf(kp.y - y) < radius)) return -1;
+                                      if (P.has_ur && cur_ur[j] > 0) {
+                                          const float er = fabsf(xr - cur_ur[j]);
+                                          if (er > r * P.scale[lvl]) return -1;
+                                      }
+                                      return hamming(d0, d1, cur_desc[2 * (size_t)j], cur_desc[2 * (size_t)j + 1]);
+                                  });
         }
-    ncand[i] = n;
-    best[i] = Best2{c1, c2};
-    if (n > P.cap) atomicMax(overflow, n);
+    }
+    if (lane == 0) {
+        ncand[i] = n;
+        if (n > P.cap) atomicMax(overflow, n);
+    }
 }
 
-// ---- the in-order assignment, resolved in parallel rounds --------------------------------------
+// ---- the in-order assignment, resolved by parallel fixed-point rounds ----------------------------
 // Both SearchByProjection loops visit the points in index order, and point i only sees the state the
 // earlier points left: a current keypoint that holds a map point with observations is skipped
 // (src:103-105, src:2040-2042).  That state changes once per keypoint -- the first successful
-// assignment by an observed point -- so point i's answer depends only on which of its candidates
-// earlier observed points claim, and only through the candidates that are (or would become) its
-// first minimum (SearchByProjection(Frame, Frame)) or first two minima (the local-map overload, for
-// the ratio test): candidates elsewhere in its list change neither.
-// One workgroup resolves every point in rounds.  At the start of a round, minNF[j] = the smallest
-// still-undecided observed point that has keypoint j among its candidates.  Point i is decided in the
-// round when no candidate that could still enter its minima is "unknown" (minNF[j] < i: an earlier
-// undecided point might claim it); claimed[j] < i (a decided earlier claim) excludes a candidate.
-// The earliest undecided point is always decidable, so every round makes progress.  A point can only
-// ever claim a candidate at or below the first candidate it already knows to stay free (bound[i],
-// from its previous evaluation), so only those enter minNF: the dependency chains stay short and a
-// frame takes a handful of rounds.  The results are then exactly those of the
-// sequential loop:
+// assignment by an observed point -- so point i's answer is a function f_i of which of its candidates
+// earlier observed points claimed:
+//   A(i) = f_i({ j : some k < i, observed(k), A(k) = j }).
+// One workgroup iterates this map on all points at once (Jacobi): every round computes claimMin[j] =
+// the smallest observed point whose current answer is j, then every point re-derives its answer with
+// the candidates claimed by an earlier point excluded.  A fixed point is the sequential answer (by
+// induction on i), and after round r the first r points are final, so the iteration ends; in practice
+// after a few rounds more than the longest chain of actual claim conflicts.  The results are then
+// exactly those of the sequential loop:
 //   mp[j]  = the last point assigned to keypoint j (a later unobserved-free assignment overwrites an
 //            earlier one, src:156 / :2067), or -1;
 //   count  = every successful assignment (the reference's nmatches++ per assignment), minus, for
 //            SearchByProjection(Frame, Frame) with checkOri, every assignment in a rotation bin outside
 //            ComputeThreeMaxima's top three, whose keypoint is then cleared (src:2160-2181).
-// The candidate kernels above store each point's candidates in the reference's scan order (the order
-// key of a candidate is its list position) with their Hamming distances.
-constexpr int kResolveThreads = 1024, kResolveLdsKeypoints = 8192;
+// The candidate kernels store each point's candidates in the reference's scan order (the order key of
+// a candidate is its list position) with their Hamming distances; the first / second minimum of the
+// reference's update rules (src:126-142, :2057-2061) are the lexicographic (distance, order) minima.
+constexpr int kResolveThreads = 1024, kResolveLdsKeypoints = 16384;
 constexpr unsigned long long kNone = ~0ull;
 
 struct ResolveArgs {
@@ -243,96 +276,83 @@ struct ResolveArgs {
     const float4* cur_kp;      // x, y, angle, octave bits
     const float* last_angle;   // per point (rotation bins)
     const int32_t* overflow;   // the candidate pass's overflow (> cap: results not written)
-    int32_t* st;               // per point: -2 undecided, -1 no match, j >= 0 matched to keypoint j
-    unsigned long long* bound; // per point: the key of its first candidate known to stay free (or none)
-    int lds_keypoints;         // 1: minNF / claimed in LDS (dynamic, 8 B per keypoint)
-    int32_t* minNF;            // per keypoint
-    int32_t* claimed;          // per keypoint
+    int32_t* st;               // per point: the current answer, -1 no match, j >= 0 keypoint j
+    int lds_keypoints;         // 1: claimMin in LDS (dynamic, 4 B per keypoint)
+    int32_t* claimMin;         // per keypoint (when not in LDS)
     int32_t* last;             // per keypoint
     int32_t* removed;          // per keypoint
     int32_t* mp;               // out: per keypoint
-    int32_t* out_n;            // out
+    int32_t* out_n;            // out: [0] count, [1] rounds
 };
+
+// point i's answer given claimMin (candidates claimed by an earlier point excluded)
+__device__ __forceinline__ int resolve_point(const ResolveArgs& a, const int32_t* claimMin, int i) {
+    const Cand* C = a.cands + (size_t)i * a.cap;
+    unsigned long long m1 = kNone, m2 = kNone;
+    for (int k = 0, n = a.ncand[i]; k < n; ++k) {
+        const Cand c = C[k];
+        if (c.dist >= 256) continue;  // never below the initial bestDist / bestDist2 of 256
+        if (a.taken0 && a.taken0[c.i2]) continue;
+        if (claimMin[c.i2] < i) continue;
+        const unsigned long long key = ((unsigned long long)c.dist << 32) | (unsigned)k;
+        if (key < m1) {
+            m2 = m1;
+            m1 = key;
+        } else if (key < m2) {
+            m2 = key;
+        }
+    }
+    if (m1 == kNone) return -1;
+    const int d1 = (int)(m1 >> 32), j1 = C[(int)(m1 & 0xffffffffu)].i2;
+    if (d1 > kThHigh) return -1;
+    if (a.local) {  // src:148-155
+        const int l1 = __float_as_int(a.cur_kp[j1].w);
+        const int l2 = m2 != kNone ? __float_as_int(a.cur_kp[C[(int)(m2 & 0xffffffffu)].i2].w) : -1;
+        const int d2 = m2 != kNone ? (int)(m2 >> 32) : 256;
+        if (l1 == l2 && (float)d1 > a.nnratio * (float)d2) return -1;
+    }
+    return j1;
+}
 
 __global__ __launch_bounds__(kResolveThreads) void k_resolve_rounds(ResolveArgs a) {
     const int tid = threadIdx.x;
     __shared__ int hist[kHisto], keep[3], cnt[2];
     extern __shared__ int32_t kp_lds[];
-    int32_t* const minNF = a.lds_keypoints ? kp_lds : a.minNF;
-    int32_t* const claimed = a.lds_keypoints ? kp_lds + a.n_cur : a.claimed;
+    int32_t* const claimMin = a.lds_keypoints ? kp_lds : a.claimMin;
     if (*a.overflow > a.cap) {  // the host re-runs with a larger capacity
         if (tid == 0) *a.out_n = -1;
         return;
     }
-    for (int i = tid; i < a.n_pts; i += kResolveThreads) {
-        a.st[i] = a.ncand[i] > 0 ? -2 : -1;
-        a.bound[i] = kNone;
-    }
     for (int j = tid; j < a.n_cur; j += kResolveThreads) {
-        claimed[j] = INT32_MAX;
+        claimMin[j] = INT32_MAX;
         a.last[j] = -1;
         a.removed[j] = 0;
     }
     if (tid < kHisto) hist[tid] = 0;
     if (tid < 2) cnt[tid] = 0;
     __syncthreads();
-    for (;;) {
-        for (int j = tid; j < a.n_cur; j += kResolveThreads) minNF[j] = INT32_MAX;
+    // round 0: no claims (the unconstrained answers)
+    for (int i = tid; i < a.n_pts; i += kResolveThreads) a.st[i] = a.ncand[i] > 0 ? resolve_point(a, claimMin, i) : -1;
+    int rounds = 1;
+    for (;; ++rounds) {
+        __syncthreads();
+        for (int j = tid; j < a.n_cur; j += kResolveThreads) claimMin[j] = INT32_MAX;
         __syncthreads();
         for (int i = tid; i < a.n_pts; i += kResolveThreads) {
-            if (a.st[i] != -2 || !a.observed[i]) continue;
-            const Cand* C = a.cands + (size_t)i * a.cap;
-            const unsigned long long bnd = a.bound[i];
-            for (int k = 0, n = a.ncand[i]; k < n; ++k) {  // the candidates point i might still claim
-                const Cand c = C[k];
-                if (c.dist >= 256 || (a.taken0 && a.taken0[c.i2]) || claimed[c.i2] < i) continue;
-                if ((((unsigned long long)c.dist << 32) | (unsigned)k) <= bnd) atomicMin(&minNF[c.i2], i);
-            }
+            const int j = a.st[i];
+            if (j >= 0 && a.observed[i]) atomicMin(&claimMin[j], i);
         }
         __syncthreads();
-        int left = 0;
+        int changed = 0;
         for (int i = tid; i < a.n_pts; i += kResolveThreads) {
-            if (a.st[i] != -2) continue;
-            const Cand* C = a.cands + (size_t)i * a.cap;
-            unsigned long long m1 = kNone, m2 = kNone, u = kNone;
-            for (int k = 0, n = a.ncand[i]; k < n; ++k) {
-                const Cand c = C[k];
-                if (c.dist >= 256) continue;  // never below the initial bestDist / bestDist2 of 256
-                if (a.taken0 && a.taken0[c.i2]) continue;
-                if (__hip_atomic_load(&claimed[c.i2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < i) continue;
-                const unsigned long long key = ((unsigned long long)c.dist << 32) | (unsigned)k;
-                if (minNF[c.i2] < i) {
-                    u = key < u ? key : u;
-                } else if (key < m1) {
-                    m2 = m1;
-                    m1 = key;
-                } else if (key < m2) {
-                    m2 = key;
-                }
+            if (a.ncand[i] == 0) continue;
+            const int r = resolve_point(a, claimMin, i);
+            if (r != a.st[i]) {
+                a.st[i] = r;
+                ++changed;
             }
-            const unsigned long long need = a.local ? m2 : m1;
-            if (u != kNone && (need == kNone || u < need)) {
-                a.bound[i] = m1;
-                ++left;
-                continue;
-            }
-            int res = -1;
-            if (m1 != kNone) {
-                const int d1 = (int)(m1 >> 32), j1 = C[(int)(m1 & 0xffffffffu)].i2;
-                bool ok = d1 <= kThHigh;
-                if (ok && a.local) {  // src:148-155
-                    const int l1 = __float_as_int(a.cur_kp[j1].w);
-                    const int l2 = m2 != kNone ? __float_as_int(a.cur_kp[C[(int)(m2 & 0xffffffffu)].i2].w) : -1;
-                    const int d2 = m2 != kNone ? (int)(m2 >> 32) : 256;
-                    ok = !(l1 == l2 && (float)d1 > a.nnratio * (float)d2);
-                }
-                if (ok) res = j1;
-            }
-            if (res >= 0 && a.observed[i])
-                __hip_atomic_store(&claimed[res], i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            a.st[i] = res;
         }
-        if (__syncthreads_count(left) == 0) break;
+        if (__syncthreads_count(changed) == 0 || rounds > a.n_pts) break;
     }
     // results
     int nsucc = 0;
@@ -373,7 +393,10 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_rounds(ResolveArgs 
         __syncthreads();
     }
     for (int j = tid; j < a.n_cur; j += kResolveThreads) a.mp[j] = a.removed[j] ? -1 : a.last[j];
-    if (tid == 0) *a.out_n = cnt[0] - cnt[1];
+    if (tid == 0) {
+        a.out_n[0] = cnt[0] - cnt[1];
+        a.out_n[1] = rounds;
+    }
 }
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -456,12 +479,10 @@ extern "C" int orb_search_by_projection_frame(orb_matcher_t m, const orb_frame_v
         const size_t in_bytes = off;
         const size_t o_cand = off; off = align256(off + (size_t)nl * P.cap * sizeof(Cand));
         const size_t o_nc = off; off = align256(off + (size_t)nl * 4);
-        const size_t o_bc = off; off = align256(off + (size_t)nl * 4);
         const size_t o_ovf = off; off = align256(off + 16);
         const size_t o_mp = off; off = align256(off + (size_t)std::max(n, 1) * 4);
         const size_t o_st = off; off = align256(off + (size_t)std::max(nl, 1) * 4);
-        const size_t o_bd2 = off; off = align256(off + (size_t)std::max(nl, 1) * 8);
-        const size_t o_kw = off; off = align256(off + (size_t)std::max(n, 1) * 16);  // minNF, claimed, last, removed
+        const size_t o_kw = off; off = align256(off + (size_t)std::max(n, 1) * 16);  // claimMin, last, removed
         if (int rc = orbgpu_matcher_reserve(m, off, &d, &h, &s, &check_ori)) return rc;
         P.check_ori = check_ori;
         memcpy(h + o_p, &P, sizeof(P));
@@ -491,11 +512,11 @@ extern "C" int orb_search_by_projection_frame(orb_matcher_t m, const orb_frame_v
         bool ok = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s) == hipSuccess;
         ok = ok && hipMemsetAsync(d + o_ovf, 0, 16, s) == hipSuccess;
         if (ok && nl > 0)
-            hipLaunchKernelGGL(k_proj_candidates, dim3((nl + 255) / 256), dim3(256), 0, s, (const ProjParams*)(d + o_p),
+            hipLaunchKernelGGL(k_proj_candidates, dim3((nl + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s, (const ProjParams*)(d + o_p),
                                (const uint8_t*)(d + o_va), (const float*)(d + o_xyz), (const uint4*)(d + o_md),
                                (const int32_t*)(d + o_lo), (const float4*)(d + o_kp), (const float*)(d + o_ur),
                                (const uint4*)(d + o_cd), (const int32_t*)(d + o_co), (const int32_t*)(d + o_ci),
-                               (Cand*)(d + o_cand), (int32_t*)(d + o_nc), (int32_t*)(d + o_bc), (int32_t*)(d + o_ovf));
+                               (Cand*)(d + o_cand), (int32_t*)(d + o_nc), (int32_t*)(d + o_ovf));
         ResolveArgs ra{};
         ra.n_pts = nl; ra.n_cur = n; ra.cap = P.cap; ra.local = 0; ra.check_ori = check_ori; ra.nnratio = 0.f;
         ra.cands = (const Cand*)(d + o_cand); ra.ncand = (const int32_t*)(d + o_nc); ra.observed = (const uint8_t*)(d + o_ob);
@@ -503,14 +524,13 @@ extern "C" int orb_search_by_projection_frame(orb_matcher_t m, const orb_frame_v
         ra.overflow = (const int32_t*)(d + o_ovf); ra.st = (int32_t*)(d + o_st);
         int32_t* kw = (int32_t*)(d + o_kw);
         const size_t nk = (size_t)std::max(n, 1);
-        ra.minNF = kw; ra.claimed = kw + nk; ra.last = kw + 2 * nk; ra.removed = kw + 3 * nk;
-        ra.bound = (unsigned long long*)(d + o_bd2);
+        ra.claimMin = kw; ra.last = kw + nk; ra.removed = kw + 2 * nk;
         ra.lds_keypoints = n <= kResolveLdsKeypoints ? 1 : 0;
         ra.mp = (int32_t*)(d + o_mp); ra.out_n = (int32_t*)(d + o_ovf) + 1;
         // candidates and the rounds back to back, one synchronisation; an overflowing candidate pass
         // (a point with more candidates than the capacity) makes the resolve a no-op and is re-run
         if (ok)
-            hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 8 * (size_t)n : 0, s, ra);
+            hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 4 * (size_t)n : 0, s, ra);
         ok = ok && hipGetLastError() == hipSuccess &&
              hipMemcpyAsync(h + o_mp, d + o_mp, (size_t)std::max(n, 1) * 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
              hipMemcpyAsync(h + o_ovf, d + o_ovf, 16, hipMemcpyDeviceToHost, s) == hipSuccess &&
@@ -586,12 +606,10 @@ extern "C" int orb_search_by_projection_local(orb_matcher_t m, const orb_frame_v
         const size_t in_bytes = off;
         const size_t o_cand = off; off = align256(off + (size_t)np * P.cap * sizeof(Cand));
         const size_t o_nc = off; off = align256(off + (size_t)np * 4);
-        const size_t o_b2 = off; off = align256(off + (size_t)np * sizeof(Best2));
         const size_t o_ovf = off; off = align256(off + 16);
         const size_t o_m = off; off = align256(off + (size_t)std::max(n, 1) * 4);
         const size_t o_st = off; off = align256(off + (size_t)std::max(np, 1) * 4);
-        const size_t o_bd2 = off; off = align256(off + (size_t)std::max(np, 1) * 8);
-        const size_t o_kw = off; off = align256(off + (size_t)std::max(n, 1) * 16);  // minNF, claimed, last, removed
+        const size_t o_kw = off; off = align256(off + (size_t)std::max(n, 1) * 16);  // claimMin, last, removed
         if (int rc = orbgpu_matcher_reserve(m, off, &d, &h, &s, &check_ori)) return rc;
         P.nnratio = orbgpu_matcher_nnratio(m);
         memcpy(h + o_p, &P, sizeof(P));
@@ -620,12 +638,12 @@ extern "C" int orb_search_by_projection_local(orb_matcher_t m, const orb_frame_v
         bool ok = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s) == hipSuccess &&
                   hipMemsetAsync(d + o_ovf, 0, 16, s) == hipSuccess;
         if (ok && np > 0)
-            hipLaunchKernelGGL(k_lmp_candidates, dim3((np + 255) / 256), dim3(256), 0, s, (const LocalParams*)(d + o_p),
+            hipLaunchKernelGGL(k_lmp_candidates, dim3((np + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s, (const LocalParams*)(d + o_p),
                                (const uint8_t*)(d + o_iv), (const uint8_t*)(d + o_bd), (const float*)(d + o_pj),
                                (const float*)(d + o_vc), (const float*)(d + o_dp), (const int32_t*)(d + o_lv),
                                (const uint4*)(d + o_md), (const float4*)(d + o_kp), (const float*)(d + o_ur),
                                (const uint4*)(d + o_cd), (const int32_t*)(d + o_co), (const int32_t*)(d + o_ci),
-                               (Cand*)(d + o_cand), (int32_t*)(d + o_nc), (Best2*)(d + o_b2), (int32_t*)(d + o_ovf));
+                               (Cand*)(d + o_cand), (int32_t*)(d + o_nc), (int32_t*)(d + o_ovf));
         ResolveArgs ra{};
         ra.n_pts = np; ra.n_cur = n; ra.cap = P.cap; ra.local = 1; ra.check_ori = 0; ra.nnratio = P.nnratio;
         ra.cands = (const Cand*)(d + o_cand); ra.ncand = (const int32_t*)(d + o_nc); ra.observed = (const uint8_t*)(d + o_ob);
@@ -633,12 +651,11 @@ extern "C" int orb_search_by_projection_local(orb_matcher_t m, const orb_frame_v
         ra.last_angle = nullptr; ra.overflow = (const int32_t*)(d + o_ovf); ra.st = (int32_t*)(d + o_st);
         int32_t* kw = (int32_t*)(d + o_kw);
         const size_t nk = (size_t)std::max(n, 1);
-        ra.minNF = kw; ra.claimed = kw + nk; ra.last = kw + 2 * nk; ra.removed = kw + 3 * nk;
-        ra.bound = (unsigned long long*)(d + o_bd2);
+        ra.claimMin = kw; ra.last = kw + nk; ra.removed = kw + 2 * nk;
         ra.lds_keypoints = n <= kResolveLdsKeypoints ? 1 : 0;
         ra.mp = (int32_t*)(d + o_m); ra.out_n = (int32_t*)(d + o_ovf) + 1;
         if (ok)
-            hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 8 * (size_t)n : 0, s, ra);
+            hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 4 * (size_t)n : 0, s, ra);
         ok = ok && hipGetLastError() == hipSuccess &&
              hipMemcpyAsync(h + o_m, d + o_m, (size_t)std::max(n, 1) * 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
              hipMemcpyAsync(h + o_ovf, d + o_ovf, 16, hipMemcpyDeviceToHost, s) == hipSuccess &&
