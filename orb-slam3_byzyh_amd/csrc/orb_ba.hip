@@ -484,24 +484,67 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
 // above the diagonal collect garbage that is never read.
 // kColMajor: L^-1 stored column-major with stride 17 (L^-1[i][c] at c * 17 + i: conflict-free for the
 // writes here and for every reader); otherwise in the MFMA operand layout.
-// Lane j of each 16-lane row, broadcast to the whole row (DPP row_newbcast): a VALU move, no SGPR
-// round trip (v_readlane + wait states) and no SGPR pressure.  j must fold to a constant.
-__device__ __forceinline__ double row_bcast16(double v, int j) {
-    const uint64_t u = __double_as_longlong(v);
-    const int lo = (int)(uint32_t)u, hi = (int)(uint32_t)(u >> 32);
-    int rl = 0, rh = 0;
+
+// 64-bit DPP row broadcasts folded into the consuming instruction (gfx950 DPP64: v_mov_b64 and
+// v_fmac_f64 take row_newbcast): one instruction per broadcast / per rank-1 update element instead of
+// two 32-bit DPP moves, their old-value initialisations and a separate FMA.  Each starts with s_nop 1,
+// the VALU-write -> DPP-read wait states, which the compiler cannot see inside inline asm.  j must
+// fold to a constant.
+#define MF_CASES(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15)
+__device__ __forceinline__ double bcast64(double v, int j) {  // lane j of the 16-lane row
+    double r = 0.0;
     switch (j) {
-#define MF_RB(J)                                                              \
-    case J:                                                                   \
-        rl = __builtin_amdgcn_update_dpp(0, lo, 0x150 + J, 0xf, 0xf, false); \
-        rh = __builtin_amdgcn_update_dpp(0, hi, 0x150 + J, 0xf, 0xf, false); \
+#define MF_B64(J)                                                                                        \
+    case J:                                                                                              \
+        asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:" #J " row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(v)); \
         break;
-        MF_RB(0) MF_RB(1) MF_RB(2) MF_RB(3) MF_RB(4) MF_RB(5) MF_RB(6) MF_RB(7)
-        MF_RB(8) MF_RB(9) MF_RB(10) MF_RB(11) MF_RB(12) MF_RB(13) MF_RB(14) MF_RB(15)
-#undef MF_RB
+        MF_CASES(MF_B64)
+#undef MF_B64
         default: break;
     }
-    return __longlong_as_double(((uint64_t)(uint32_t)rh << 32) | (uint32_t)rl);
+    return r;
+}
+// acc = fma(-a_j, b, acc) = acc + a_j * (-b)  with a_j = a of lane j: the same rounding as fma(-a_j, b, acc)
+__device__ __forceinline__ double fmac_bcast_negb(double acc, double a, double b, int j) {
+    switch (j) {
+#define MF_F64(J)                                                                                              \
+    case J:                                                                                                    \
+        asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, -%2 row_newbcast:" #J " row_mask:0xf bank_mask:0xf" : "+v"(acc) \
+            : "v"(a), "v"(b));                                                                                 \
+        break;
+        MF_CASES(MF_F64)
+#undef MF_F64
+        default: break;
+    }
+    return acc;
+}
+// acc = fma(b, a_j, acc)
+__device__ __forceinline__ double fmac_bcast(double acc, double a, double b, int j) {
+    switch (j) {
+#define MF_F64P(J)                                                                                            \
+    case J:                                                                                                   \
+        asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:" #J " row_mask:0xf bank_mask:0xf" : "+v"(acc) \
+            : "v"(a), "v"(b));                                                                                \
+        break;
+        MF_CASES(MF_F64P)
+#undef MF_F64P
+        default: break;
+    }
+    return acc;
+}
+// acc = fma(-a_j, b, acc) with the negation on the broadcast operand
+__device__ __forceinline__ double fmac_negbcast(double acc, double a, double b, int j) {
+    switch (j) {
+#define MF_F64N(J)                                                                                             \
+    case J:                                                                                                    \
+        asm("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:" #J " row_mask:0xf bank_mask:0xf" : "+v"(acc) \
+            : "v"(a), "v"(b));                                                                                 \
+        break;
+        MF_CASES(MF_F64N)
+#undef MF_F64N
+        default: break;
+    }
+    return acc;
 }
 
 // The column values L[j][c] reach the other rows by DPP row broadcasts (every 16-lane row holds the
@@ -517,21 +560,30 @@ __device__ __forceinline__ void mf_diag(double* __restrict__ dk, double* __restr
         row[c] = dk[r * 17 + c];
         xc[c] = c == r ? 1.0 : 0.0;
     }
-    bool bad = false;
+    // Software-pipelined: column c first updates row c+1 and starts column c+1's pivot chain
+    // (broadcast, rsqrt, Newton) before its other updates, which then fill that chain's latency.  The
+    // same operations on the same values as the column-by-column order.
+    const double piv0 = bcast64(row[0], 0);
+    bool bad = !(piv0 > 0.0);
+    double inv = rsqrt_nr(piv0);  // 1 / L[c][c]
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
-        const double piv = row_bcast16(row[c], c);
-        bad |= !(piv > 0.0);
-        const double inv = rsqrt_nr(piv);  // 1 / L[c][c]
-        const double lrc = row[c] * inv;    // L[r][c] for r > c
-        xc[c] *= inv;                       // x_c of column r of L^-1
-#pragma unroll
-        for (int j = c + 1; j < 16; ++j) {
-            const double ljc = row_bcast16(lrc, j);
-            row[j] = __builtin_fma(-lrc, ljc, row[j]);
-            xc[j] = __builtin_fma(-ljc, xc[c], xc[j]);
-            asm volatile("" : "+v"(row[j]), "+v"(xc[j]));  // computed here: one broadcast live at a time
+        const double lrc = row[c] * inv;  // L[r][c] for r > c
+        xc[c] *= inv;                     // x_c of column r of L^-1
+        double inv_next = 0.0;
+        if (c + 1 < 16) {  // row[j] = fma(-L[r][c], L[j][c], row[j]), xc[j] = fma(-L[j][c], xc[c], xc[j])
+            row[c + 1] = fmac_bcast_negb(row[c + 1], lrc, lrc, c + 1);
+            xc[c + 1] = fmac_negbcast(xc[c + 1], lrc, xc[c], c + 1);
+            const double pn = bcast64(row[c + 1], c + 1);
+            bad |= !(pn > 0.0);
+            inv_next = rsqrt_nr(pn);
         }
+#pragma unroll
+        for (int j = c + 2; j < 16; ++j) {
+            row[j] = fmac_bcast_negb(row[j], lrc, lrc, j);
+            xc[j] = fmac_negbcast(xc[j], lrc, xc[c], j);
+        }
+        inv = inv_next;
     }
     bad = __ballot(bad) != 0;
     if (lane == 0 && bad) *fail = 1;
@@ -615,6 +667,10 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
     __syncthreads();  // the only workgroup barrier before the end
     if (w == W) {
         // ---------------- diagonal wave ----------------
+        // It carries the critical chain and is the youngest wave of the workgroup: VALU / MFMA issue
+        // is arbitrated by priority, then age (MI355X_MICROARCH.md, two waves per SIMD), so without a
+        // priority the two tile waves on its SIMD take the issue slots first.
+        __builtin_amdgcn_s_setprio(3);
         for (int t = lane; t < 256; t += 64) {
             const int r = t >> 4, c = t & 15;
             dk[r * 17 + c] = (r < n && c < n) ? S[(size_t)r * n + c] : (r == c ? 1.0 : 0.0);
@@ -687,12 +743,12 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
             if (j + 1 < NT) {
                 double t4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-                for (int rr = 0; rr < 16; ++rr) t4[rr & 3] = __builtin_fma(lr[rr], row_bcast16(xn, rr), t4[rr & 3]);
+                for (int rr = 0; rr < 16; ++rr) t4[rr & 3] = fmac_bcast(t4[rr & 3], xn, lr[rr], rr);
                 yj -= (t4[0] + t4[1]) + (t4[2] + t4[3]);
             }
             double v4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int rr = 0; rr < 16; ++rr) v4[rr & 3] = __builtin_fma(li[rr], row_bcast16(yj, rr), v4[rr & 3]);
+            for (int rr = 0; rr < 16; ++rr) v4[rr & 3] = fmac_bcast(v4[rr & 3], yj, li[rr], rr);
             xn = (v4[0] + v4[1]) + (v4[2] + v4[3]);
             if (lane < 16) xv[16 * j + r16] = xn;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
