@@ -1843,7 +1843,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     static const bool trace = getenv("ORBGPU_BA_TRACE") != nullptr;
     using clk = std::chrono::steady_clock;
     const clk::time_point t_in = clk::now();
-    clk::time_point t_struct = t_in, t_solve = t_in;
+    clk::time_point t_struct = t_in, t_solve = t_in, t_order = t_in, t_csr = t_in, t_pairs = t_in, t_pack = t_in;
     auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
     const int np = pr->n_poses, nq = pr->n_points, ne_all = pr->n_edges;
     if (np < 0 || nq < 0 || ne_all < 0 || (np && (!pr->pose || !pr->pose_id || !pr->pose_fixed || !pr->pose_camera)) ||
@@ -1920,14 +1920,21 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         l_begin = h->rank == 0 ? 0 : cut(h->rank);
         l_end = h->rank == h->world - 1 ? nl_all : cut(h->rank + 1);
     }
+    t_order = clk::now();
     std::vector<int32_t> point_l(nq, -1), land_point(all_land.begin() + l_begin, all_land.begin() + l_end);
     for (int l = 0; l < (int)land_point.size(); ++l) point_l[land_point[l]] = l;
     std::vector<int32_t> lmap;  // local edge -> problem edge (problem order kept)
-    for (int e = 0; e < ne_all; ++e)
-        if (point_l[pr->edges[e].point] >= 0) lmap.push_back(e);
-    std::vector<EdgeDev> ledges(lmap.size());
-    for (size_t k = 0; k < lmap.size(); ++k) memcpy(&ledges[k], &pr->edges[lmap[k]], sizeof(EdgeDev));
-    const int ne = (int)lmap.size(), nl = (int)land_point.size();
+    static_assert(sizeof(EdgeDev) == sizeof(orb_ba_edge_t), "EdgeDev mirrors orb_ba_edge_t");
+    const EdgeDev* ledges = reinterpret_cast<const EdgeDev*>(pr->edges);  // one rank: every edge, in place
+    std::vector<EdgeDev> ledges_copy;
+    if (dist) {
+        for (int e = 0; e < ne_all; ++e)
+            if (point_l[pr->edges[e].point] >= 0) lmap.push_back(e);
+        ledges_copy.resize(lmap.size());
+        for (size_t k = 0; k < lmap.size(); ++k) memcpy(&ledges_copy[k], &pr->edges[lmap[k]], sizeof(EdgeDev));
+        ledges = ledges_copy.data();
+    }
+    const int ne = dist ? (int)lmap.size() : ne_all, nl = (int)land_point.size();
     const int n = 6 * nf, m = 3 * nl;
 
     // landmark -> all edges (edge order), landmark -> free-pose edges (pose row ascending), pose -> edges
@@ -1956,60 +1963,62 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
             }
         }
     }
-    for (int l = 0; l < nl; ++l)
-        std::stable_sort(landf_edge.begin() + landf_off[l], landf_edge.begin() + landf_off[l + 1],
-                         [&](int a, int b) { return pose_h[ledges[a].pose] < pose_h[ledges[b].pose]; });
+    // each landmark's free-pose edges by pose row, stable: an insertion sort (a landmark has a handful
+    // of edges; std::stable_sort allocated a buffer per landmark)
+    for (int l = 0; l < nl; ++l) {
+        int32_t* e0 = landf_edge.data() + landf_off[l];
+        const int d = landf_off[l + 1] - landf_off[l];
+        for (int a = 1; a < d; ++a) {
+            const int32_t v = e0[a];
+            const int32_t key = pose_h[ledges[v].pose];
+            int b = a;
+            for (; b > 0 && pose_h[ledges[e0[b - 1]].pose] > key; --b) e0[b] = e0[b - 1];
+            e0[b] = v;
+        }
+    }
     const int nfe = (int)landf_edge.size();
     std::vector<int32_t> fland(nfe);
     for (int l = 0; l < nl; ++l)
         for (int k = landf_off[l]; k < landf_off[l + 1]; ++k) fland[k] = l;
-    // Schur block pattern: every diagonal block, then the (row_a <= row_b) products per landmark
-    std::vector<int32_t> blk_id((size_t)nf * nf, -1), blk_i, blk_j;
-    std::vector<int32_t> cnt;
-    for (int i = 0; i < nf; ++i) {
-        blk_id[(size_t)i * nf + i] = (int32_t)blk_i.size();
-        blk_i.push_back(i);
-        blk_j.push_back(i);
-        cnt.push_back(0);
-    }
-    // free-pose row of each landmark -> free-pose edge, then each landmark's pairs (a <= b) in order;
-    // pass 1 assigns the block ids (first-seen order) and keeps them, pass 2 places the pairs
+    t_csr = clk::now();
+    // Schur block pattern: every diagonal block, then the (row_a <= row_b) products per landmark.
+    // Blocks are numbered in (row, column) order; each block's products are listed in landmark order
+    // (the fixed summation order of k_u_schur).  Pass 1 counts the products per block cell, pass 2
+    // places them.
     std::vector<int32_t> frow(nfe);
     for (int k = 0; k < nfe; ++k) frow[k] = pose_h[ledges[landf_edge[k]].pose];
-    size_t npairs = 0;
-    for (int l = 0; l < nl; ++l) {
-        const size_t d = (size_t)(landf_off[l + 1] - landf_off[l]);
-        npairs += d * (d + 1) / 2;
-    }
-    std::vector<int32_t> pid(npairs);
-    {
-        size_t q = 0;
-        for (int l = 0; l < nl; ++l)
-            for (int a = landf_off[l]; a < landf_off[l + 1]; ++a) {
-                int32_t* row = blk_id.data() + (size_t)frow[a] * nf;
-                for (int b2 = a; b2 < landf_off[l + 1]; ++b2) {
-                    int32_t& id = row[frow[b2]];
-                    if (id < 0) { id = (int32_t)blk_i.size(); blk_i.push_back(frow[a]); blk_j.push_back(frow[b2]); cnt.push_back(0); }
-                    cnt[id]++;
-                    pid[q++] = id;
-                }
-            }
-    }
+    std::vector<int32_t> cell((size_t)nf * nf, 0);
+    for (int l = 0; l < nl; ++l)
+        for (int a = landf_off[l]; a < landf_off[l + 1]; ++a) {
+            int32_t* row = cell.data() + (size_t)frow[a] * nf;
+            for (int b2 = a; b2 < landf_off[l + 1]; ++b2) row[frow[b2]]++;
+        }
+    std::vector<int32_t> blk_i, blk_j, blk_off{0};
+    std::vector<int32_t> cell_pos((size_t)nf * nf, -1);  // block cell -> next product slot
+    blk_i.reserve(4 * (size_t)nf);
+    blk_j.reserve(4 * (size_t)nf);
+    blk_off.reserve(4 * (size_t)nf + 1);
+    for (int i = 0; i < nf; ++i)
+        for (int j = i; j < nf; ++j) {
+            const int32_t c = cell[(size_t)i * nf + j];
+            if (c == 0 && j != i) continue;
+            cell_pos[(size_t)i * nf + j] = blk_off.back();
+            blk_i.push_back(i);
+            blk_j.push_back(j);
+            blk_off.push_back(blk_off.back() + c);
+        }
     const int nblk = (int)blk_i.size();
-    std::vector<int32_t> blk_off(nblk + 1, 0);
-    for (int k = 0; k < nblk; ++k) blk_off[k + 1] = blk_off[k] + cnt[k];
     std::vector<int32_t> pair_a(blk_off[nblk]), pair_b(blk_off[nblk]);
-    {
-        std::vector<int32_t> c(blk_off.begin(), blk_off.end() - 1);
-        size_t q = 0;
-        for (int l = 0; l < nl; ++l)
-            for (int a = landf_off[l]; a < landf_off[l + 1]; ++a)
-                for (int b2 = a; b2 < landf_off[l + 1]; ++b2) {
-                    const int id = pid[q++];
-                    pair_a[c[id]] = landf_edge[a];
-                    pair_b[c[id]++] = landf_edge[b2];
-                }
-    }
+    for (int l = 0; l < nl; ++l)
+        for (int a = landf_off[l]; a < landf_off[l + 1]; ++a) {
+            int32_t* row = cell_pos.data() + (size_t)frow[a] * nf;
+            for (int b2 = a; b2 < landf_off[l + 1]; ++b2) {
+                const int32_t q = row[frow[b2]]++;
+                pair_a[q] = landf_edge[a];
+                pair_b[q] = landf_edge[b2];
+            }
+        }
+    t_pairs = clk::now();
     // poses normalised as SE3Quat(q, t) does
     std::vector<double> pose(pr->pose, pr->pose + 7 * (size_t)np);
     for (int i = 0; i < np; ++i) {
@@ -2023,7 +2032,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     const size_t ne1 = std::max(ne, 1);
     Stager st;
     bool ok = st.add(h->pose, pose) && h->pose_bak.grow(7 * (size_t)np) && st.add(h->point, pr->point, 3 * (size_t)nq) &&
-              h->point_bak.grow(3 * (size_t)nq) && st.add(h->edges, ledges) && st.add(h->cams, pr->pose_camera, np) &&
+              h->point_bak.grow(3 * (size_t)nq) && st.add(h->edges, ledges, (size_t)ne) && st.add(h->cams, pr->pose_camera, np) &&
               st.add(h->pose_h, pose_h) && st.add(h->free_pose, free_pose) && st.add(h->land_point, land_point) &&
               st.add(h->land_off, land_off) && st.add(h->land_edge, land_edge) && st.add(h->landf_off, landf_off) &&
               st.add(h->landf_edge, landf_edge) && st.add(h->fland, fland) && st.add(h->pose_off, pose_off) &&
@@ -2046,6 +2055,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         ok = ok && h->d_stage.grow(total);
         if (ok) {
             st.pack(h->h_stage);
+            t_pack = clk::now();
             ok = hipMemcpyAsync(h->d_stage.p, h->h_stage, total, hipMemcpyHostToDevice, s) == hipSuccess;
             size_t maxb = 0;
             for (const ScatterItem& it : st.items) maxb = std::max<size_t>(maxb, it.bytes);
@@ -2400,8 +2410,10 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
             if (edge_depth_ok) edge_depth_ok[e] = ldep[e];
         }
         if (trace)
-            fprintf(stderr, "[ba] structure %.1f us, upload+LM %.1f us, results %.1f us, it %d trials %d\n",
-                    us(t_in, t_struct), us(t_struct, t_solve), us(t_solve, clk::now()), res->iterations, res->trials);
+            fprintf(stderr, "[ba] structure %.1f us (order %.1f, csr %.1f, pairs %.1f, rest %.1f), pack %.1f us, upload+LM %.1f us, "
+                            "results %.1f us, it %d trials %d\n",
+                    us(t_in, t_struct), us(t_in, t_order), us(t_order, t_csr), us(t_csr, t_pairs), us(t_pairs, t_struct),
+                    us(t_struct, t_pack), us(t_pack, t_solve), us(t_solve, clk::now()), res->iterations, res->trials);
         return ORB_OK;
     }
     // gather: each rank contributes its landmarks (rank 0 also the points without edges) and its
