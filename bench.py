@@ -67,17 +67,18 @@ def algorithmic_bytes_per_frame(w, h, nkp):
     algorithmic figure, which is survey_bytes_per_frame)."""
     sizes = level_sizes(w, h)
     px = [a * b for a, b in sizes]
-    pad = [(a + 38) * (b + 38) for a, b in sizes]
+    written = [(a + 6) * (b + 6) for a, b in sizes]  # each view + its 3-px REFLECT_101 border
     return {
-        # read L0 + read levels 0..6 to resize; write every padded plane and every blurred level
-        "pyramid": w * h + sum(px[:-1]) + sum(pad) + sum(px),
+        # read L0 + read levels 0..6 to resize; write every level's view + border (no blurred levels:
+        # k_describe blurs its own samples)
+        "pyramid": w * h + sum(px[:-1]) + sum(written),
         # read every level once; candidates are ~1% of pixels (not counted)
         "fast": sum(px),
         # candidates in, selected keys out (small); counted as one level read equivalent of 4 B/cand
         "quadtree": 0,
         "place": 0,
-        # per keypoint: 749-px disc + 512 samples in, 28 + 32 B out
-        "describe": nkp * (749 + 512 + 60),
+        # per keypoint: the 43x43 patch (disc + Gaussian taps of the 512 samples) in, 28 + 32 B out
+        "describe": nkp * (43 * 43 + 60),
         # SURVEY.md sec. 8(d) whole-path figure: L0 read + levels 1..7 written and read + kps/descs out
         "path": w * h + 2 * sum(px[1:]) + nkp * 60,
     }
@@ -731,8 +732,8 @@ def main():
         ex.extract_batch_device(imgs, (0, 1000), cap=cap, out=out, stream=streams[0])
         torch.cuda.synchronize(dev)
     single_ms = (time.perf_counter() - t1) * 1e3 / min(10, args.steps)
-    # timed region; every handle records the wall-clock span of each of its k_pyramid_level launches
-    # (the roofline kernel) from per-block device stamps -- no events between the launches
+    # timed region; every handle records an HIP event pair on its launch stream around each of its
+    # k_pyramid_level launches (the roofline kernel)
     for e_ in exs:
         e_.profile("pyramid_launches")
     if world > 1:
@@ -770,8 +771,8 @@ def main():
         # roofline kernel: k_pyramid_level, the HBM-facing stage (it reads every input frame and
         # writes every level), launches_per_step launches per step, each one level of all nfr frames.
         # achieved = SURVEY.md 8(d)'s algorithmic bytes per frame x nfr / launches_per_step, divided
-        # by the mean launch duration measured in the timed region from per-block wall-clock stamps
-        # (first block start to last block end of each launch; no events between the launches).
+        # by the mean launch duration measured in the timed region with HIP events around each launch
+        # on its stream (the interval rocprofv3's kernel trace reports for the dispatch).
         # The stage with the most time is reported next to it (`dominant_stage`).
         dom = "pyramid"
         nkp_frame = feats_per_step / nfr
@@ -814,10 +815,10 @@ def main():
                          "dominant_stage": dominant_stage,
                          "note": "algorithmic bytes = SURVEY.md 8(d) 1,653,864 B per 640x480 frame (L0 read, "
                                  "levels 1-7 written + read, 60 B per keypoint out) x frames / 8 level launches; "
-                                 "launch_avg_us from per-block wall-clock stamps in the timed region; traffic = "
+                                 "launch_avg_us from HIP event pairs around each launch in the timed region; traffic = "
                                  "PMC FETCH_SIZE x2 + WRITE_SIZE per launch (profiles/pmc_latest.json); "
-                                 "traffic_model = the bytes this implementation's pyramid moves (padded planes, "
-                                 "blurred levels)"},
+                                 "traffic_model = the bytes this implementation's pyramid moves (views + 3-px "
+                                 "borders)"},
         }
         if not args.no_cpu_baseline and world == 1:
             from oracle import oracle as oracle_mod

@@ -1,19 +1,21 @@
 // MI355X (gfx950) ORB extraction: ORBextractor::operator() (reference src/ORBextractor.cc:1557-1682)
 // as five batched HIP kernels over B frames:
 //
-//   k_pyramid_level  per level: padded level plane (INTER_LINEAR from the previous level, 19-px
-//                    REFLECT_101 frame) + its 7x7 sigma-2 Gaussian (for rBRIEF), one LDS tile pass
+//   k_pyramid_level  per level: the level view (INTER_LINEAR from the previous level) + a 3-px
+//                    REFLECT_101 border inside the 19-px padded plane, one LDS tile pass
 //   k_fast_cells     one wave per (frame, FAST cell): threshold-independent FAST-9 score, 3x3 NMS
 //                    inside the cell window, iniTh/minTh choice, row-major candidate emission
 //   k_quadtree_kp    one 256-thread workgroup per (frame, level): DistributeOctTree with exact list and
 //                    std::sort semantics (keys stay put, node ids move), plus each keypoint's
 //                    vLappingArea class rank (level-0 scaling, src:1656-1676)
-//   k_describe       one half-wave per keypoint: IC_Angle (31-px disc) + steered rBRIEF (256 tests)
+//   k_describe       one half-wave per keypoint: IC_Angle (31-px disc) + steered rBRIEF (256 tests) on
+//                    the keypoint's own 7x7 sigma-2 Gaussian, computed from a 43x43 patch in LDS
 //
 // No MFMA anywhere: this is byte / integer / popcount work.  All float arithmetic that reaches an
 // output (resize coefficients are host tables; fastAtan2; pattern steering) is compiled with
 // -ffp-contract=off and uses explicit fmaf() exactly where the reference's g++ -march=native build
 // contracts (see orb_hd.h / orb_sincos.h and DESIGN.md).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -127,23 +129,27 @@ __device__ __forceinline__ int wave_incl_max_dpp(int v) {
 }
 
 // ================================================================================================
-// 1. pyramid level: padded plane + blurred view, src:1687-1740 and src:1629-1637
+// 1. pyramid level: src:1687-1740 (ComputePyramid)
 // ================================================================================================
 constexpr int kBufDword3 = 0x00020000;  // gfx9 buffer resource word 3 (32-bit data format)
 
-// A tile is 122 x 16 padded-plane pixels; with the 3-px blur halo it is 128 x 22, one lane per column.
+// Only the view and a kBorder-px REFLECT_101 border of each padded plane are written: FAST windows
+// (src:1098-1166) and IC_Angle stay inside the view, and the one consumer of border pixels is
+// k_describe's Gaussian, whose 7x7 taps around a sample <= 18 px from a keypoint at >= 19 px from the
+// edge reach 2 px outside (the reference blurs a clone of the view with BORDER_REFLECT_101,
+// src:1629-1637).  The rest of the 19-px frame is never read and never written.
+constexpr int kBorder = 3;
+// A tile is 128 x kTileH plane pixels, one lane per column; tiles start kBorder px before the view.
 #ifndef ORBGPU_PYR_TILE_H
 #define ORBGPU_PYR_TILE_H 24
 #endif
-constexpr int kTileW = 122, kTileH = ORBGPU_PYR_TILE_H, kHalo = 3;
-static_assert(kTileH % 4 == 0, "two vertical-blur halves of an even row count");
-constexpr int kLW = kTileW + 2 * kHalo, kLH = kTileH + 2 * kHalo;  // 128 x 38
-static_assert(kLW == 128, "one lane per haloed tile column, two waves per row");
-constexpr int kBoxW = 288, kBoxH = 2 * kLH + 4;  // source box (bytes) for scale factors <= 2
-static_assert(kBoxW >= 3 + 2 * kLW + 2, "box too narrow");
-// box for level ratios <= 1.25 (the usual 1.2): 133 * 1.25 + 2 columns + 3 alignment bytes, 21 * 1.25 + 2 rows
-constexpr int kSmallBoxW = 176, kSmallBoxH = ((kLH - 1) * 5 / 4 + 3 + 3) & ~3;
-static_assert(kSmallBoxW >= 3 + (kLW - 1) * 5 / 4 + 3 && kSmallBoxH >= (kLH - 1) * 5 / 4 + 3, "small box too small");
+constexpr int kTileW = 128, kTileH = ORBGPU_PYR_TILE_H;
+static_assert(kTileH % 2 == 0, "two row halves per tile");
+constexpr int kBoxW = 288, kBoxH = 2 * kTileH + 4;  // source box (bytes) for scale factors <= 2
+static_assert(kBoxW >= 3 + 2 * kTileW + 2, "box too narrow");
+// box for level ratios <= 1.25 (the usual 1.2): 128 * 1.25 + 2 columns + 3 alignment bytes, 24 * 1.25 + 2 rows
+constexpr int kSmallBoxW = 176, kSmallBoxH = ((kTileH - 1) * 5 / 4 + 3 + 3) & ~3;
+static_assert(kSmallBoxW >= 3 + (kTileW - 1) * 5 / 4 + 3 && kSmallBoxH >= (kTileH - 1) * 5 / 4 + 3, "small box too small");
 
 // 8 bytes from a 4-byte-aligned LDS row at any byte offset, as aligned dword reads + v_alignbyte.
 // (Adjacent byte reads would otherwise be merged by the compiler into unaligned ds_read_u16/b64,
@@ -157,25 +163,9 @@ __device__ __forceinline__ unsigned long long lds_bytes8(const uint8_t* row, int
     return lo | ((unsigned long long)hi << 32);
 }
 
-// range of reflect101(p) over p in [a, b] (view coordinates), len >= 38
-__device__ __forceinline__ void reflect_range(int a, int b, int len, int& lo, int& hi) {
-    lo = 1 << 30; hi = -1;
-    if (a < 0) { const int e = min(b, -1); lo = min(lo, -e); hi = max(hi, -a); }
-    if (b >= 0 && a < len) { lo = min(lo, max(a, 0)); hi = max(hi, min(b, len - 1)); }
-    if (b >= len) { const int s0 = max(a, len); lo = min(lo, 2 * len - 2 - b); hi = max(hi, 2 * len - 2 - s0); }
-}
-
-// cv::resize INTER_LINEAR source index of destination coordinate d (resize.cpp coefficient loop)
-__device__ __forceinline__ int resize_src_index(int d, double scale, int slen) {
-    const float f = (float)((d + 0.5) * scale - 0.5);
-    int s = (int)f;
-    s -= (s > f);
-    return min(max(s, 0), slen - 1);
-}
-
 // XCD-aware tile order.  Blocks are dealt round-robin over the 8 XCDs in dispatch order (block b
 // and b + 8 share an L2); handing each XCD a contiguous run of tiles keeps vertically adjacent tiles,
-// which re-read the same source and halo rows, in one L2.  Performance only: any placement is correct.
+// which re-read the same source rows, in one L2.  Performance only: any placement is correct.
 __device__ __forceinline__ int xcd_tile(int b, int share) { return (b & 7) * share + (b >> 3); }
 
 // 7-tap GaussianBlur weights as packed u8 (horizontal pass, v_dot4_u32_u8) and u16 pairs (vertical
@@ -184,20 +174,18 @@ constexpr uint32_t kBlurK0 = 18u | 34u << 8 | 48u << 16 | 56u << 24, kBlurK1 = 4
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u16x2 w16(unsigned a, unsigned b) { u16x2 v; v.x = (unsigned short)a; v.y = (unsigned short)b; return v; }
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
 
-// One workgroup = one 128 x 16 tile of a padded level plane (+3-px halo for the blur).
+// One workgroup = one 128 x kTileH tile of a level's written region (view + kBorder).
 // Level 0 copies the input; level l > 0 resizes the previous level view.  The source pixels the tile
-// needs are staged in LDS (one round of independent loads), then every phase is written for few VALU
-// instructions per pixel (the pyramid is VALU-bound, PMC round 2):
-//   resize  lane per tile column, wave-uniform rows: the column's INTER_LINEAR coefficients stay in
-//           registers, the row coefficients are scalar loads, and each source row's horizontal
-//           interpolation is computed once and streamed (about 1.2 rows per output row)
-//   hblur   4 outputs x 2 rows per item: v_alignbyte + v_dot4_u32_u8, stored as row-pair u16x2
-//   vblur   lane per column, 8 output rows: 4 v_dot2_u32_u16 per output over the row pairs
+// needs are staged in LDS (one round of independent loads), then the resize is written for few VALU
+// instructions per pixel (the pyramid is VALU-bound, PMC round 2): lane per tile column,
+// wave-uniform rows; the column's INTER_LINEAR coefficients stay in registers, the row coefficients
+// are one broadcast LDS read, and every tile row's two source rows are interpolated horizontally.
 // Level geometry by value (kernel arguments): no dependent load of the geometry block before the
 // source loads can be addressed.
 struct PyrArgs {
-    long long frame_bytes;         // one frame's pyramid block (pyramid and blurred pyramid alike)
+    long long frame_bytes;         // one frame's pyramid block
     long long plane_off, src_off;  // this level's padded plane; the previous level's view origin
     int w, h, pw, ph, pitch;       // this level
     int sw, sh, spitch;            // previous level view (level > 0)
@@ -209,7 +197,7 @@ struct PyrArgs {
 template <bool kLevel0, int kBH = kSmallBoxH, int kBW = kSmallBoxW>
 __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const uint8_t* __restrict__ in,
                                                           long long in_frame_stride, int in_stride,
-                                                          uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                                          uint8_t* __restrict__ pyr,
                                                           const int2* __restrict__ xtab, const int4* __restrict__ ytab,
                                                           const int4* __restrict__ tiletab,
                                                           unsigned long long* __restrict__ stamps,
@@ -227,35 +215,34 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
     // tile record (scalar load): origin, and for level > 0 the previous-level view box it reads
     const int4 T = tiletab[A.tab_off + t];
     constexpr int kBoxWords = kBW / 4;
-    constexpr int kPairs = kLH / 2;      // 11 row pairs of horizontal sums
-    constexpr int kQuads = (kTileW + 3) / 4;
     __shared__ __attribute__((aligned(16))) uint8_t box[kLevel0 ? 4 : kBH * kBW];
-    __shared__ __attribute__((aligned(16))) uint8_t tile[kLH][kLW + 8];      // +8: the last quad's over-read
-    __shared__ __attribute__((aligned(16))) uint32_t hs2[kPairs][kLW];       // (row 2j, row 2j+1) sums, <= 255 * 256
-    __shared__ int4 yrow[kLevel0 ? 1 : kLH];  // per tile row: box row offsets of the two source rows, weights
+    __shared__ __attribute__((aligned(16))) uint8_t tile[kTileH][kTileW + 8];  // +8: lds_bytes8 over-read
+    __shared__ int4 yrow[kLevel0 ? 1 : kTileH];  // per tile row: box row offsets of the two source rows, weights
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = uniform(tid >> 6);
     const int X0 = T.x & 0xffff, Y0 = T.x >> 16;
     uint8_t* plane = pyr + (size_t)f * A.frame_bytes + A.plane_off;
-    uint8_t* bplane = blur + (size_t)f * A.frame_bytes + A.plane_off;
-    // this lane's tile column (waves 0/1: rows [0, 11), waves 2/3: rows [11, 22)) in view coordinates
-    const int tx = (wave & 1) * 64 + lane, r0 = (wave >> 1) * (kLH / 2);
-    const int vx = reflect101(X0 - kHalo + tx - kEdge, A.w);
+    // the written region in plane coordinates, and this lane's tile column (waves 0/1: the upper half
+    // of the rows, waves 2/3: the lower half) in view coordinates; columns and rows past the region
+    // are clamped to its last one (computed, never stored)
+    const int ex = kEdge + A.w + kBorder, ey = kEdge + A.h + kBorder;
+    const int tx = (wave & 1) * 64 + lane, r0 = (wave >> 1) * (kTileH / 2);
+    const int vx = reflect101(min(X0 + tx, ex - 1) - kEdge, A.w);
     if (kLevel0) {
-        // level 0: the column's 11 rows straight from the input with reflected indices, all loads
+        // level 0: the column's rows straight from the input with reflected indices, all loads
         // issued before the first LDS store (one round trip)
         const uint8_t* src = in + (size_t)f * in_frame_stride + vx;
-        int v[kLH / 2];
+        int v[kTileH / 2];
 #pragma unroll
-        for (int k = 0; k < kLH / 2; ++k) v[k] = src[reflect101(Y0 - kHalo + r0 + k - kEdge, A.h) * in_stride];
+        for (int k = 0; k < kTileH / 2; ++k) v[k] = src[reflect101(min(Y0 + r0 + k, ey - 1) - kEdge, A.h) * in_stride];
 #pragma unroll
-        for (int k = 0; k < kLH / 2; ++k) tile[r0 + k][tx] = (uint8_t)v[k];
+        for (int k = 0; k < kTileH / 2; ++k) tile[r0 + k][tx] = (uint8_t)v[k];
         __syncthreads();
         PYR_STAMP(1);
         PYR_STAMP(2);
     } else {
         const int bx0 = T.y & 0xffff, bw = T.y >> 16, by0 = T.z & 0xffff, bh = T.z >> 16;
-        // source box as aligned dwords (over-reads stay inside the previous level's 19-px frame);
+        // source box as aligned dwords (over-reads stay inside the previous level's padded plane);
         // src_off and spitch are multiples of 128, so every box row has the same alignment.  Buffer
         // loads: one 32-bit lane offset, the row step in the scalar offset.
         const int shift = (int)((A.src_off + bx0) & 3);  // plane and frame blocks are 256-B aligned
@@ -268,7 +255,7 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
         uint32_t* boxw = reinterpret_cast<uint32_t*>(box);
         const int rg = tid >> 6;
         // every global load of the block issued before the first LDS store (one round trip): the box,
-        // the row coefficients (22 lanes) and this lane's column coefficients
+        // the row coefficients (kTileH lanes) and this lane's column coefficients
         constexpr int kRowPass = kBH / 4, kWordPass = (kBoxWords + 63) / 64;
         uint32_t v[kRowPass][kWordPass];
 #pragma unroll
@@ -280,7 +267,7 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
                                ? __builtin_amdgcn_raw_buffer_load_b32(rs, rg * A.spitch + 4 * w, 4 * q * A.spitch, 0) : 0u;
             }
         int4 yv = make_int4(0, 0, 0, 0);
-        if (tid < kLH) yv = ytab[A.ytab_off + reflect101(Y0 - kHalo + tid - kEdge, A.h)];
+        if (tid < kTileH) yv = ytab[A.ytab_off + reflect101(min(Y0 + tid, ey - 1) - kEdge, A.h)];
         const int2 X = xtab[A.xtab_off + vx];
 #pragma unroll
         for (int q = 0; q < kRowPass; ++q)
@@ -289,7 +276,7 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
                 const int r = 4 * q + rg, w = lane + 64 * hx;
                 if (w < kBoxWords) boxw[r * kBoxWords + w] = v[q][hx];
             }
-        if (tid < kLH) yrow[tid] = make_int4((yv.x - by0) * kBW, (yv.y - by0) * kBW, yv.z, yv.w);
+        if (tid < kTileH) yrow[tid] = make_int4((yv.x - by0) * kBW, (yv.y - by0) * kBW, yv.z, yv.w);
         __syncthreads();
         PYR_STAMP(1);
         // INTER_LINEAR down the column: both source rows of every tile row are interpolated
@@ -310,7 +297,7 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
                 return kMixed ? h >> hs : h >> 4;
             };
 #pragma unroll
-            for (int k = 0; k < kLH / 2; ++k) {
+            for (int k = 0; k < kTileH / 2; ++k) {
                 const int4 Y = yrow[r0 + k];  // LDS broadcast
                 const int p0 = (int)__umul24((unsigned)hrow(Y.x), (unsigned)Y.z);  // < 2^20 * 2^11
                 const int p1 = (int)__umul24((unsigned)hrow(Y.y), (unsigned)Y.w);
@@ -324,414 +311,42 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
         __syncthreads();
         PYR_STAMP(2);
     }
-    // padded plane: 8 consecutive pixels per thread (tile columns 3 .. 124), 16 rows per pass
+    // store: 8 consecutive pixels per thread, 16 rows per pass, clipped to the written region
 #pragma unroll
     for (int r = tid >> 4; r < kTileH; r += 16) {
         const int c = (tid & 15) * 8;
         const int py = Y0 + r, px = X0 + c;
-        if (py < A.ph && c < kTileW) {
+        if (py < ey && px < ex) {
             uint8_t* dst = plane + (size_t)py * A.pitch + px;
-            if (c + 7 < kTileW && px + 7 < A.pw) {
-                *reinterpret_cast<unsigned long long*>(dst) = lds_bytes8(tile[r + kHalo], c + kHalo);
+            if (px + 7 < ex) {
+                *reinterpret_cast<unsigned long long*>(dst) = lds_bytes8(tile[r], c);
             } else {
-                for (int k = 0; k < 8 && c + k < kTileW && px + k < A.pw; ++k) dst[k] = tile[r + kHalo][c + kHalo + k];
-            }
-        }
-    }
-    PYR_STAMP(3);
-    // does this tile touch the view at all?
-    if (X0 + kTileW <= kEdge || X0 >= kEdge + A.w || Y0 + kTileH <= kEdge || Y0 >= kEdge + A.h) {
-        if (stp && threadIdx.x == 0) { stp[4] = stp[5] = stp[3]; stp[7] = wall_clock64(); }
-        return;
-    }
-    // GaussianBlur 7x7 sigma 2, horizontal pass: 4 columns x 2 rows per item, exact in 16 bits
-    for (int i = tid; i < kPairs * kQuads; i += 256) {
-        const int j = i / kQuads, q = (i - j * kQuads) * 4;
-        uint32_t o[2][4];
-#pragma unroll
-        for (int rr = 0; rr < 2; ++rr) {
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(tile[2 * j + rr]) + (q >> 2);
-            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                o[rr][k] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, k), kBlurK1,
-                                                  __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, k), kBlurK0, 0u, false), false);
-        }
-        uint4 pk;
-        pk.x = o[0][0] | o[1][0] << 16;
-        pk.y = o[0][1] | o[1][1] << 16;
-        pk.z = o[0][2] | o[1][2] << 16;
-        pk.w = o[0][3] | o[1][3] << 16;
-        *reinterpret_cast<uint4*>(&hs2[j][q]) = pk;
-    }
-    __syncthreads();
-    PYR_STAMP(4);
-    // vertical pass: lane per column, output rows kVR*h .. kVR*h + kVR-1 from row pairs
-    // (kVR/2)*h .. (kVR/2)*h + kVR/2 + 2
-    {
-        constexpr int kVR = kTileH / 2;
-        const int col = tid & (kLW - 1), hh = tid >> 7;
-        const int px = X0 + col;
-        if (col < kTileW && px >= kEdge && px < kEdge + A.w) {
-            uint32_t Pr[kVR / 2 + 3];
-#pragma unroll
-            for (int k = 0; k < kVR / 2 + 3; ++k) Pr[k] = hs2[(kVR / 2) * hh + k][col];
-            uint8_t* dst = bplane + (size_t)(Y0 + kVR * hh) * A.pitch + px;
-#pragma unroll
-            for (int i = 0; i < kVR; ++i) {
-                const int m = i >> 1;
-                uint32_t acc = 1u << 15;
-                if ((i & 1) == 0) {
-                    acc = __builtin_amdgcn_udot2(as_u16x2(Pr[m]), w16(18, 34), acc, false);
-                    acc = __builtin_amdgcn_udot2(as_u16x2(Pr[m + 1]), w16(48, 56), acc, false);
-                    acc = __builtin_amdgcn_udot2(as_u16x2(Pr[m + 2]), w16(48, 34), acc, false);
-                    acc = __builtin_amdgcn_udot2(as_u16x2(Pr[m + 3]), w16(18, 0), acc, false);
-                } else {
-                    acc = __builtin_amdgcn_udot2(as_u16x2(Pr[m]), w16(0, 18), acc, false);
-                    acc = __builtin_amdgcn_udot2(as_u16x2(Pr[m + 1]), w16(34, 48), acc, false);
-                    acc = __builtin_amdgcn_udot2(as_u16x2(Pr[m + 2]), w16(56, 48), acc, false);
-                    acc = __builtin_amdgcn_udot2(as_u16x2(Pr[m + 3]), w16(34, 18), acc, false);
-                }
-                const int vy = Y0 + kVR * hh + i - kEdge;
-                if (vy >= 0 && vy < A.h) dst[i * A.pitch] = (uint8_t)(acc >> 16);  // <= 255 exactly
+                for (int k = 0; k < 8 && px + k < ex; ++k) dst[k] = tile[r][c + k];
             }
         }
     }
     if (stp) {
-        __syncthreads();
-        if (threadIdx.x == 0) { stp[5] = __builtin_amdgcn_s_memtime(); stp[7] = wall_clock64(); }
+        PYR_STAMP(3);
+        if (threadIdx.x == 0) { stp[4] = stp[5] = stp[3]; stp[7] = wall_clock64(); }
     }
 #undef PYR_STAMP
 }
 
-// ================================================================================================
-// 1b. whole pyramid in one launch: one workgroup per (frame, horizontal band)
-// ================================================================================================
-// The per-level launches above are latency-bound (a level's tiles cannot start before the previous
-// level exists, and the small levels cannot fill the chip).  Here one 1024-thread workgroup owns a
-// horizontal band of one frame and walks all levels itself: it computes, level by level, every view
-// row its band needs -- its own rows, +-3 rows for the blur, and the source rows of the next
-// level's computed rows -- so it never waits for another workgroup.  Rows computed by two bands
-// (the margins) are written twice with identical bytes.  Per chunk of R rows (a "task"):
-//   P1  resize (level 0: copy) the staged source rows S -> padded rows V (REFLECT_101 columns);
-//       vertical blur of the rows the previous task completed (hsum ring H -> blurred plane)
-//   P2  padded rows V -> pyramid plane (+ the reflected border rows); horizontal blur V -> H;
-//       store the next task's source rows, prefetched into registers during P1, into S
-// Two workgroup barriers per task; the next task's global loads overlap this task's P1.
-struct BandTask {
-    int level, late;  // late: sources written by the previous task, staged after its barrier
-    int a, b;         // view rows [a, b) of `level`
-    int s_lo, s_n;    // staged source rows: previous level view rows (level 0: input rows)
-    int e0, e1;       // blurred view rows completed by this task (emitted during the next P1)
-};
-static_assert(sizeof(BandTask) == 32, "BandTask layout");
-
-constexpr int kBandThreads = 1024;
-constexpr int kBandGranules = 3;  // 16-byte source granules per thread per task
-
-struct BandArgs {  // scalars only: the pointers are __restrict__ kernel parameters (scalar loads)
-    int max_tasks;
-    long long in_frame_stride;
-    int in_stride, in_vec;  // in_vec: 16-byte aligned input rows with width % 16 == 0
-    int xt_total;            // INTER_LINEAR column entries of levels >= 1 (all staged in LDS)
-    int R, ring, s_rows, sp, vp, hp;  // LDS geometry (bytes; hp in uint16)
-};
-
-__device__ __forceinline__ int blur_hsum_end(int w) { return (w + kEdge + 7) & ~7; }  // padded cols [16, end)
-
-// Row entry of cv::resize INTER_LINEAR (source rows r0, r1 and 11-bit weights b0, b1) for
-// destination row dy of dh rows from sh: the same operations as the host table (resize_tables in
-// orb_extract_geom.h), IEEE double / float with no contraction, so the result is bit-identical.
-__device__ __forceinline__ int4 resize_row_coef(int dy, int dh, int sh) {
-    const double scale_y = 1. / ((double)dh / sh);
-    float fy = (float)((dy + 0.5) * scale_y - 0.5);
-    int sy = (int)fy;
-    sy -= (sy > fy);
-    fy -= sy;
-    const int b0 = min(max((int)__builtin_rintf((1.f - fy) * 2048), -32768), 32767);
-    const int b1 = min(max((int)__builtin_rintf(fy * 2048), -32768), 32767);
-    return make_int4(min(max(sy, 0), sh - 1), min(max(sy + 1, 0), sh - 1), b0, b1);
-}
-
-// kOcc = waves per SIMD the register budget must allow: 4 (one workgroup per CU) or 8 (two)
-template <int kOcc>
-__global__ __launch_bounds__(kBandThreads, kOcc) void k_pyramid_band(
-    const KernelGeom* __restrict__ gp, const BandTask* __restrict__ tasks, const int* __restrict__ ntasks,
-    const uint8_t* __restrict__ in, uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
-    const int2* __restrict__ xtab, const int4* __restrict__ ytab, unsigned long long* __restrict__ stamps,
-    BandArgs A) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const KernelGeom& g = *gp;
-    const int tid = threadIdx.x, band = blockIdx.x, f = blockIdx.y;
-    uint8_t* S = lds;
-    uint8_t* V = S + A.s_rows * A.sp;
-    uint16_t* H = reinterpret_cast<uint16_t*>(V + A.R * A.vp);
-    int2* X = reinterpret_cast<int2*>(H + A.ring * A.hp);
-    const int ring_mask = A.ring - 1;                    // ring: power of two
-    const int nt = ntasks[band];
-    const BandTask* T = tasks + (size_t)band * A.max_tasks;
-    uint8_t* const pyr_f = pyr + (size_t)f * g.pyr_frame_bytes;
-    uint8_t* const blur_f = blur + (size_t)f * g.pyr_frame_bytes;
-    const uint8_t* const in_f = in + (size_t)f * A.in_frame_stride;
-    for (int i = tid; i < A.xt_total; i += kBandThreads) X[i] = xtab[i];
-
-    // rows x ncols items: each thread keeps one column and strides over rows (ncols <= 1024; one
-    // integer division per phase instead of one per item)
-#define BAND_FOR(ncols, rows, r, c)                                                   \
-    for (int c = tid % (ncols), r = tid / (ncols), _step = kBandThreads / (ncols);    \
-         r < (rows) && tid < _step * (ncols); r += _step)
-
-    // 16-byte granules of a task's source rows: level 0 from the input, else the previous level's
-    // padded plane from column 16 (view column c lands at S column c + 3)
-    auto granules = [&](const BandTask& t, int& gpr) {
-        gpr = t.level == 0 ? g.lv[0].w >> 4 : (g.lv[t.level - 1].w + 4 + 15) >> 4;
-        return t.s_n * gpr;
-    };
-    auto gsrc = [&](const BandTask& t, int r) -> const uint8_t* {
-        if (t.level == 0) return in_f + (size_t)(t.s_lo + r) * A.in_stride;
-        const LevelGeom& P = g.lv[t.level - 1];
-        return pyr_f + P.plane_off + (size_t)(t.s_lo + r + kEdge) * P.pitch + 16;
-    };
-    static_assert(kBandGranules == 3, "staging registers below");
-    struct Staged { uint4 r0, r1, r2; };  // the next task's source granules
-    auto issue = [&](const BandTask& t, Staged& q) {
-        int gpr;
-        const int n = granules(t, gpr);
-        // unconditional loads (granule index clamped into the task) so that the loads stay in
-        // flight together; commit() stores only the valid ones
-        auto ld = [&](int gi) {
-            gi = min(gi, n - 1);
-            const int r = gi / gpr, j = gi - r * gpr;
-            return *reinterpret_cast<const uint4*>(gsrc(t, r) + 16 * j);
-        };
-        q.r0 = ld(tid);
-        q.r1 = ld(tid + kBandThreads);
-        q.r2 = ld(tid + 2 * kBandThreads);
-    };
-    auto commit = [&](const BandTask& t, const Staged& q, bool keep) {
-        // consume the registers on every path, so that the wait for them sits here and nowhere
-        // else (a wait at the next issue() would also drain every store issued since)
-        if ((q.r0.x ^ q.r1.y ^ q.r2.z) == 0x9e3779b9u && A.in_stride < 0) S[0] = 0;
-        if (!keep) return;
-        int gpr;
-        const int n = granules(t, gpr);
-        auto st = [&](int gi, const uint4& v) {
-            const int r = gi / gpr, j = gi - r * gpr;
-            *reinterpret_cast<uint4*>(S + r * A.sp + 16 * j) = v;
-        };
-        if (tid < n) st(tid, q.r0);
-        if (tid + kBandThreads < n) st(tid + kBandThreads, q.r1);
-        if (tid + 2 * kBandThreads < n) st(tid + 2 * kBandThreads, q.r2);
-    };
-    auto stage_now = [&](const BandTask& t) {
-        if (t.level == 0 && !A.in_vec) {  // unaligned input: byte loads
-            const int w = g.lv[0].w;
-            for (int i = tid; i < t.s_n * w; i += kBandThreads) {
-                const int r = i / w, x = i - r * w;
-                S[r * A.sp + x] = gsrc(t, r)[x];
-            }
-        } else {
-            Staged q;
-            issue(t, q);
-            commit(t, q, true);
-        }
-    };
-    auto is_late = [&](const BandTask& t) { return t.late || (t.level == 0 && !A.in_vec); };
-
-    // P1 (level >= 1): INTER_LINEAR rows [a, b) in padded columns, 4 pixels per item
-    auto resize_rows = [&](const BandTask& t) {
-        const LevelGeom& L = g.lv[t.level];
-        const LevelGeom& P = g.lv[t.level - 1];
-        const int ngr = (L.pw + 3) >> 2;
-        const int2* XL = X + (L.xtab_off - g.lv[1].xtab_off);
-        BAND_FOR(ngr, t.b - t.a, r, gq) {
-            const int px0 = gq * 4;
-            const int4 Y = resize_row_coef(t.a + r, L.h, P.h);
-            const uint8_t* R0 = S + (Y.x - t.s_lo) * A.sp;
-            const uint8_t* R1 = S + (Y.y - t.s_lo) * A.sp;
-            int vx[4];
-            int2 Xk[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                vx[k] = reflect101(min(px0 + k, L.pw - 1) - kEdge, L.w);
-                Xk[k] = XL[vx[k]];
-            }
-            int p0[4], p0n[4], p1[4], p1n[4];
-            if (px0 >= kEdge && px0 + 3 <= L.w + kEdge - 1 && Xk[3].x + 1 - Xk[0].x <= 7) {
-                const unsigned long long q0 = lds_bytes8(R0, Xk[0].x + 3), q1 = lds_bytes8(R1, Xk[0].x + 3);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int d = 8 * (Xk[k].x - Xk[0].x);
-                    p0[k] = (int)((q0 >> d) & 0xff); p0n[k] = (int)((q0 >> (d + 8)) & 0xff);
-                    p1[k] = (int)((q1 >> d) & 0xff); p1n[k] = (int)((q1 >> (d + 8)) & 0xff);
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int s = Xk[k].x + 3;
-                    p0[k] = R0[s]; p0n[k] = R0[s + 1]; p1[k] = R1[s]; p1n[k] = R1[s + 1];
-                }
-            }
-            uint32_t packed = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int a0 = Xk[k].y & 0xffff, a1 = Xk[k].y >> 16;
-                const int h0 = p0[k] * a0 + p0n[k] * a1, h1 = p1[k] * a0 + p1n[k] * a1;
-                int v;
-                if (vx[k] < L.simd_end) {  // VResizeLinearVec_32s8u (see k_pyramid_level)
-                    const int t0 = min(h0 >> 4, 32767), t1 = min(h1 >> 4, 32767);
-                    v = (((t0 * Y.z) >> 16) + ((t1 * Y.w) >> 16) + 2) >> 2;
-                } else {
-                    v = (h0 * Y.z + h1 * Y.w + (1 << 21)) >> 22;
-                }
-                packed |= (uint32_t)min(max(v, 0), 255) << (8 * k);
-            }
-            *reinterpret_cast<uint32_t*>(V + r * A.vp + px0) = packed;
-        }
-    };
-    // P1 (level 0): padded rows straight from the staged input rows
-    auto copy_rows = [&](const BandTask& t) {
-        const LevelGeom& L = g.lv[0];
-        const int ngr = (L.pw + 3) >> 2;
-        BAND_FOR(ngr, t.b - t.a, r, gq) {
-            const int px0 = gq * 4;
-            const uint8_t* row = S + r * A.sp;
-            uint32_t packed;
-            if (px0 >= kEdge && px0 + 3 <= L.w + kEdge - 1) {
-                packed = (uint32_t)lds_bytes8(row, px0 - kEdge);
-            } else {
-                packed = 0;
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    packed |= (uint32_t)row[reflect101(min(px0 + k, L.pw - 1) - kEdge, L.w)] << (8 * k);
-            }
-            *reinterpret_cast<uint32_t*>(V + r * A.vp + px0) = packed;
-        }
-    };
-    // P2: padded rows to the plane (+ REFLECT_101 border rows 19 - y and 2h + 17 - y)
-    auto write_rows = [&](const BandTask& t) {
-        const LevelGeom& L = g.lv[t.level];
-        uint8_t* plane = pyr_f + L.plane_off;
-        const int n8 = (L.pw + 7) >> 3;
-        BAND_FOR(n8, t.b - t.a, r, c8) {
-            const int px = c8 * 8, y = t.a + r;
-            const unsigned long long v = *reinterpret_cast<const unsigned long long*>(V + r * A.vp + px);
-            const int top = (y >= 1 && y <= kEdge) ? kEdge - y : -1;
-            const int bot = (y >= L.h - kEdge - 1 && y <= L.h - 2) ? 2 * L.h + kEdge - 2 - y : -1;
-#pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                const int row = d == 0 ? y + kEdge : d == 1 ? top : bot;
-                if (row < 0) continue;
-                uint8_t* o = plane + (size_t)row * L.pitch + px;
-                if (px + 8 <= L.pw) {
-                    *reinterpret_cast<unsigned long long*>(o) = v;
-                } else {
-                    for (int k = 0; k < 8 && px + k < L.pw; ++k) o[k] = (uint8_t)(v >> (8 * k));
-                }
-            }
-        }
-    };
-    // P2: horizontal 7-tap pass of rows [a, b) into the hsum ring (padded columns [16, end))
-    auto hblur_rows = [&](const BandTask& t) {
-        const LevelGeom& L = g.lv[t.level];
-        const int n4 = (blur_hsum_end(L.w) - 16) >> 2;
-        BAND_FOR(n4, t.b - t.a, r, c4) {
-            const int px = 16 + c4 * 4;
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(V + r * A.vp) + (px >> 2) - 1;
-            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-            int pv[12];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                pv[k] = (w0 >> (8 * k)) & 0xff;
-                pv[4 + k] = (w1 >> (8 * k)) & 0xff;
-                pv[8 + k] = (w2 >> (8 * k)) & 0xff;
-            }
-            unsigned long long out = 0;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                int acc = 0;
-#pragma unroll
-                for (int k = 0; k < 7; ++k) acc += blur_tap(k) * pv[1 + q + k];
-                out |= (unsigned long long)acc << (16 * q);
-            }
-            *reinterpret_cast<unsigned long long*>(H + ((t.a + r) & ring_mask) * A.hp + px) = out;
-        }
-    };
-    // P1 of the next task: vertical 7-tap pass of the completed rows [e0, e1) -> blurred plane
-    auto vblur_rows = [&](const BandTask& t) {
-        if (t.e1 <= t.e0) return;
-        const LevelGeom& L = g.lv[t.level];
-        uint8_t* plane = blur_f + L.plane_off;
-        const int xe = L.w + kEdge, n8 = (blur_hsum_end(L.w) - 16) >> 3;
-        BAND_FOR(n8, t.e1 - t.e0, r, c8) {
-            const int px = 16 + c8 * 8, y = t.e0 + r;
-            int acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-            for (int k = 0; k < 7; ++k) {
-                const int yy = reflect101(y - 3 + k, L.h);
-                const uint4 q = *reinterpret_cast<const uint4*>(H + (yy & ring_mask) * A.hp + px);
-                const uint32_t qq[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    acc[2 * j] += blur_tap(k) * (int)(qq[j] & 0xffff);
-                    acc[2 * j + 1] += blur_tap(k) * (int)(qq[j] >> 16);
-                }
-            }
-            unsigned long long w = 0;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) w |= (unsigned long long)min((acc[q] + (1 << 15)) >> 16, 255) << (8 * q);
-            uint8_t* o = plane + (size_t)(y + kEdge) * L.pitch + px;
-            if (px >= kEdge && px + 8 <= xe) {
-                *reinterpret_cast<unsigned long long*>(o) = w;
-            } else {
-                for (int q = 0; q < 8; ++q)
-                    if (px + q >= kEdge && px + q < xe) o[q] = (uint8_t)(w >> (8 * q));
-            }
-        }
-    };
-#undef BAND_FOR
-
-    BandTask prev;
-    prev.e0 = prev.e1 = 0;
-    prev.level = 0;
-    // debug trace (ORBGPU_BAND_TRACE): wall clock of band 0 / frame 0 at each phase boundary
-    const bool trace = stamps && band == 0 && f == 0 && tid == 0;
-    constexpr int kTr = 10;
-#define BAND_STAMP(k) \
-    if (trace) stamps[kTr * i + (k)] = wall_clock64()
-    for (int i = 0; i < nt; ++i) {
-        const BandTask t = T[i];
-        BAND_STAMP(0);
-        if (i == 0 || is_late(t)) {
-            stage_now(t);
-            __syncthreads();
-        }
-        BAND_STAMP(1);
-        // order: stores of the previous blur rows, then the next task's loads, then the resize;
-        // after the barrier the commit waits for those loads (and the older stores) only
-        const BandTask tn = T[min(i + 1, nt - 1)];
-        const bool pre = i + 1 < nt && !is_late(tn);
-        vblur_rows(prev);
-        BAND_STAMP(2);
-        Staged q;
-        issue(pre ? tn : t, q);  // without a prefetch: a harmless reload, so the wait stays unconditional
-        BAND_STAMP(3);
-        if (t.level == 0) copy_rows(t); else resize_rows(t);
-        BAND_STAMP(4);
-        __syncthreads();
-        BAND_STAMP(5);
-        commit(tn, q, pre);
-        BAND_STAMP(6);
-        write_rows(t);
-        BAND_STAMP(7);
-        hblur_rows(t);
-        BAND_STAMP(8);
-        __syncthreads();
-        BAND_STAMP(9);
-        prev = t;
+// Debug (orb_debug_level_blurred): the reference's GaussianBlur(level.clone(), 7x7, 2, 2,
+// BORDER_REFLECT_101) of a whole level view, one thread per pixel, from the stored view (the
+// descriptor kernel blurs only its own samples; this is the test hook for that arithmetic).
+__global__ __launch_bounds__(256) void k_debug_blur(const uint8_t* __restrict__ view, int pitch, int w, int h,
+                                                    uint8_t* __restrict__ out) {
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x >= w) return;
+    uint32_t acc = 1u << 15;
+    for (int i = 0; i < 7; ++i) {
+        const uint8_t* row = view + (size_t)reflect101(y + i - 3, h) * pitch;
+        uint32_t hs = 0;
+        for (int k = 0; k < 7; ++k) hs += (uint32_t)(blur_tap(k) * row[reflect101(x + k - 3, w)]);
+        acc += (uint32_t)blur_tap(i) * hs;
     }
-#undef BAND_STAMP
-    vblur_rows(prev);
+    out[(size_t)y * w + x] = (uint8_t)(acc >> 16);
 }
 
 // ================================================================================================
@@ -1910,16 +1525,37 @@ __device__ __forceinline__ void steer_sincos(float ang, const uint32_t (&exc)[kE
     }
 }
 
-// One keypoint per 32-lane half-wave, 8 per block.  The keypoint's 37x37 blurred patch (rBRIEF reaches
-// round(13*sqrt(2)) = 18 px) and 31x31 unblurred disc box are staged in LDS with one round of dword
-// loads, so the dependent memory phases are: key -> patches -> stores.
+// One keypoint per 32-lane half-wave, 8 per block.  The keypoint's 43x43 level patch is staged in LDS
+// with one round of dwordx4 loads (rBRIEF samples reach round(13*sqrt(2)) = 18 px, the 7x7 Gaussian
+// 3 more; IC_Angle's 31-px disc lies inside), so the dependent memory phases are: key -> patch ->
+// stores.  The blurred level is never materialised: the reference blurs a clone of every level
+// (src:1629-1637) but reads it only at the 512 samples, so the kernel runs the same separable
+// fixed-point GaussianBlur restricted to them -- the horizontal 7-tap pass over the 43 rows x 37
+// columns the samples can touch (exact u16 sums, stored over the patch as row-pair u16x2 words), then
+// the vertical 7-tap pass per sample (4 v_dot2_u32_u16).  Integer sums throughout, so the value is the
+// reference's bit for bit.
 constexpr int kDescKpPerBlock = 8;
-constexpr int kPB = 37, kPBW = 10;  // blurred patch rows, dwords per row
-constexpr int kPU = 31, kPUW = 9;   // disc box rows, dwords per row
-constexpr int kDescLds = kPB * kPBW * 4 + kPU * kPUW * 4;  // 2596 bytes per keypoint
+constexpr int kPR = 43, kPRW = 12;   // patch rows, dwords per row (43 bytes + up to 3 alignment bytes)
+constexpr int kHP = 22, kHPW = 40;   // horizontal-sum row pairs (rows 2j, 2j+1), words per pair (37 used)
+constexpr int kDescWords = kHP * kHPW;  // 3520 bytes per keypoint: the sums, and before them the patch
+static_assert(kDescWords >= (kPR + 1) * kPRW + 1, "patch + the last pair's odd row and over-read word fit the region");
+
+// Vertical 7-tap pass at one sample (r, c), |r|, |c| <= 18 from the keypoint: blurred row i = r + 18
+// reads sum rows i .. i+6, i.e. the 4 row pairs from i >> 1 (odd i: the first pair's high half).
+__device__ __forceinline__ int blur_sample(const uint32_t* __restrict__ H, int r, int c) {
+    const int i = r + 18;
+    const uint32_t* p = H + (i >> 1) * kHPW + (c + 18);
+    const bool odd = (i & 1) != 0;
+    uint32_t acc = 1u << 15;
+    acc = __builtin_amdgcn_udot2(as_u16x2(p[0]), odd ? w16(0, 18) : w16(18, 34), acc, false);
+    acc = __builtin_amdgcn_udot2(as_u16x2(p[kHPW]), odd ? w16(34, 48) : w16(48, 56), acc, false);
+    acc = __builtin_amdgcn_udot2(as_u16x2(p[2 * kHPW]), odd ? w16(56, 48) : w16(48, 34), acc, false);
+    acc = __builtin_amdgcn_udot2(as_u16x2(p[3 * kHPW]), odd ? w16(34, 18) : w16(18, 0), acc, false);
+    return (int)(acc >> 16);  // <= 255 exactly
+}
 
 __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__ gp, const uint8_t* __restrict__ pyr,
-                                                  const uint8_t* __restrict__ blur, const uint32_t* __restrict__ sel,
+                                                  const uint32_t* __restrict__ sel,
                                                   const int32_t* __restrict__ sel_count,
                                                   const int32_t* __restrict__ rank_in_class, const int32_t* __restrict__ lap_count,
                                                   int cap, orb_keypoint_t* __restrict__ kps, uint8_t* __restrict__ desc,
@@ -1927,7 +1563,7 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
                                                   int stage_levels, int stage_mode, orb_keypoint_t* __restrict__ st_kp,
                                                   uint8_t* __restrict__ st_desc) {
     const KernelGeom& g = *gp;
-    __shared__ __attribute__((aligned(16))) uint32_t patch[kDescKpPerBlock][(kDescLds + 15) / 16 * 4];
+    __shared__ __attribute__((aligned(16))) uint32_t patch[kDescKpPerBlock][kDescWords];
     const int half = threadIdx.x >> 5, hl = threadIdx.x & 31;
     // blockIdx.x -> (level, chunk): level l owns ceil(sel_cap_l / 8) blocks, so the grid holds no block
     // beyond a level's capacity (scalar walk over the levels)
@@ -1993,48 +1629,36 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
     }
     const uint32_t key = active ? key_spec : 0;
     const int x = key_x(key) + L.minB, y = key_y(key) + L.minB;
-    // ---- stage both patches.  Lane (r, w) of a half-wave loads word w of row r of a 3-row group, so
-    // load k reads rows 3k..3k+2 at a per-lane offset computed once plus 3k rows in soffset (raw buffer
-    // loads, plane base in the resource): 10 words x 3 rows of the blurred patch (30 lanes), 9 x 3 of
-    // the disc box (27).  Rows past the patch and idle lanes over-read inside the padded planes and
-    // are not stored.
-    constexpr int kBL = (kPB + 2) / 3, kUL = (kPU + 2) / 3;
-    const int sb = hl / kPBW, cb = hl % kPBW, su = hl / kPUW, cu = hl % kPUW;
-    const size_t plane = (size_t)f * g.pyr_frame_bytes + L.plane_off;
-    const uint8_t* bp = blur + plane;
-    const uint8_t* up = pyr + plane;
-    const int bo = (y + kEdge - 18) * L.pitch + (x + kEdge - 18);
-    const int uo = (y + kEdge - kHalfPatch) * L.pitch + (x + kEdge - kHalfPatch);
-    const int bsh = (int)(((uintptr_t)bp + bo) & 3), ush = (int)(((uintptr_t)up + uo) & 3);
-    const uint32_t vob = (uint32_t)(bo - bsh + sb * L.pitch + 4 * cb);
-    const uint32_t vou = (uint32_t)(uo - ush + su * L.pitch + 4 * cu);
-    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(bp), (short)0, 0x7fffffff, kBufDword3);
+    // ---- stage the patch: rows y-21 .. y+21, columns from x-21 rounded down to a dword.  Lane
+    // (r, q) of a half-wave loads 16 bytes (quarter q of 3) of row r of a 10-row group; load k reads
+    // rows 10k .. 10k+9 (raw buffer loads, plane base in the resource, the row step in soffset).  The
+    // over-read rows (43 .. 49) and columns stay inside the padded plane and are not stored.
+    constexpr int kGroups = (kPR + 9) / 10;
+    const int pr = hl / 3, pq = hl - 3 * pr;
+    const uint8_t* up = pyr + (size_t)f * g.pyr_frame_bytes + L.plane_off;
+    const int po = (y + kEdge - 21) * L.pitch + (x + kEdge - 21);
+    const int sh = po & 3;  // plane base and pitch are 128-B aligned
+    const uint32_t vo = (uint32_t)(po - sh + pr * L.pitch + 16 * pq);
     const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(up), (short)0, 0x7fffffff, kBufDword3);
     uint32_t* P = patch[half];
-    uint32_t vb[kBL], vu[kUL];
-    if (active) {
+    if (active && hl < 30) {
+        v4u32 v[kGroups];
 #pragma unroll
-        for (int k = 0; k < kBL; ++k) vb[k] = __builtin_amdgcn_raw_buffer_load_b32(rb, vob, 3 * k * L.pitch, 0);
+        for (int k = 0; k < kGroups; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b128(ru, vo, 10 * k * L.pitch, 0);
 #pragma unroll
-        for (int k = 0; k < kUL; ++k) vu[k] = __builtin_amdgcn_raw_buffer_load_b32(ru, vou, 3 * k * L.pitch, 0);
-#pragma unroll
-        for (int k = 0; k < kBL; ++k)
-            if (hl < 3 * kPBW && 3 * k + sb < kPB) P[3 * kPBW * k + hl] = vb[k];
-#pragma unroll
-        for (int k = 0; k < kUL; ++k)
-            if (hl < 3 * kPUW && 3 * k + su < kPU) P[kPB * kPBW + 3 * kPUW * k + hl] = vu[k];
+        for (int k = 0; k < kGroups; ++k)
+            if (10 * k + pr < kPR) *reinterpret_cast<v4u32*>(P + (10 * k + pr) * kPRW + 4 * pq) = v[k];
     }
-    __syncthreads();
-    const uint8_t* PB = reinterpret_cast<const uint8_t*>(P) + bsh + 18 * (kPBW * 4) + 18;  // blurred centre
-    const uint8_t* PU = reinterpret_cast<const uint8_t*>(P + kPB * kPBW) + ush + kHalfPatch * (kPUW * 4) + kHalfPatch;
-    // ---- IC_Angle on the unblurred level (src:91-138): lane = disc column u, so m10 = u * (column sum).
-    // The reads are unconditional (the whole 31x31 box is staged; lane 31, u = 16, lies outside every
-    // disc row) and the disc mask is a select, so the 31 LDS reads issue back to back.
+    wave_sync();
+    const uint8_t* PC = reinterpret_cast<const uint8_t*>(P) + sh + 21 * (kPRW * 4) + 21;  // keypoint pixel
+    // ---- IC_Angle on the level (src:91-138): lane = disc column u, so m10 = u * (column sum).
+    // The reads are unconditional (lane 31, u = 16, lies outside every disc row) and the disc mask is
+    // a select, so the 31 LDS reads issue back to back.
     const int u = hl - kHalfPatch, au = u < 0 ? -u : u;
     int colsum = 0, m01 = 0;
 #pragma unroll
     for (int v = -kHalfPatch; v <= kHalfPatch; ++v) {
-        const int raw = PU[v * (kPUW * 4) + u];
+        const int raw = PC[v * (kPRW * 4) + u];
         const int val = au <= g.umax[v < 0 ? -v : v] ? raw : 0;
         colsum += val;
         m01 += v * val;
@@ -2044,7 +1668,34 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
     m10 = half_wave_sum(m10);
     m01 = half_wave_sum(m01);
     const float angle = orb_fast_atan2((float)m01, (float)m10);
-    // ---- steered BRIEF on the blurred level (src:150-203)
+    // ---- horizontal 7-tap pass (GaussianBlur 7x7 sigma 2, exact in 16 bits): item (pair j, quad qq)
+    // = sum columns 4qq .. 4qq+3 of rows 2j, 2j+1 (v_alignbyte + v_dot4_u32_u8 on the patch bytes
+    // shifted by sh), written over the patch in place.  Rounds run from the last pairs down: pair j's
+    // words start at patch row 40j/12, above every row (<= 2j - 1, + 16 over-read bytes) a later,
+    // lower round reads, and within a round the reads precede the writes (one wave, LDS in order).
+    constexpr int kItems = kHP * 10, kIt = (kItems + 31) / 32;
+#pragma unroll
+    for (int it = kIt - 1; it >= 0; --it) {
+        const int i = hl + 32 * it, ic = min(i, kItems - 1), j = ic / 10, qq = ic - 10 * j;
+        uint32_t o[2][4];
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+            const uint32_t* w = P + (2 * j + rr) * kPRW + qq;  // patch bytes 4qq .. 4qq+15 (2 x ds_read2)
+            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
+            const uint32_t a0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
+            const uint32_t a1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+            const uint32_t a2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                o[rr][k] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(a2, a1, k), kBlurK1,
+                                                  __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(a1, a0, k), kBlurK0, 0u, false), false);
+        }
+        if (i < kItems)
+            *reinterpret_cast<uint4*>(P + j * kHPW + 4 * qq) =
+                make_uint4(o[0][0] | o[1][0] << 16, o[0][1] | o[1][1] << 16, o[0][2] | o[1][2] << 16, o[0][3] | o[1][3] << 16);
+    }
+    wave_sync();
+    // ---- steered BRIEF on the blurred samples (src:150-203)
     const float ang = angle * (float)(3.14159265358979323846 / 180.f);
     float a, b;
     steer_sincos(ang, exc, half, hl, &b, &a);  // a = cos, b = sin
@@ -2059,8 +1710,8 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
         const int c0 = (int)__builtin_rintf(__builtin_fmaf(px0, a, -(py0 * b)));
         const int r1 = (int)__builtin_rintf(__builtin_fmaf(px1, b, py1 * a));
         const int c1 = (int)__builtin_rintf(__builtin_fmaf(px1, a, -(py1 * b)));
-        t0[m] = PB[__mul24(r0, kPBW * 4) + c0];  // |r| <= 18: 24-bit multiply (full rate)
-        t1[m] = PB[__mul24(r1, kPBW * 4) + c1];
+        t0[m] = blur_sample(P, r0, c0);  // |r|, |c| <= 18
+        t1[m] = blur_sample(P, r1, c1);
     }
     uint32_t words[8];
 #pragma unroll
@@ -2110,7 +1761,6 @@ struct Extractor {
     int tile_off[orbgpu::kMaxLevels] = {};
     int4* d_ytab = nullptr; size_t ytab_cap = 0;
     uint8_t* d_pyr = nullptr; size_t pyr_cap = 0;
-    uint8_t* d_blur = nullptr; size_t blur_cap = 0;
     uint32_t* d_cand = nullptr; size_t cand_cap = 0;
     uint32_t* d_scratch = nullptr; size_t scratch_cap = 0;
     int32_t* d_cell_count = nullptr; size_t cell_count_cap = 0;
@@ -2145,28 +1795,13 @@ struct Extractor {
     long long batches = 0;
     int profile = 0;  // 0 off, 1 every stage boundary, 2 only the pyramid stage (marks 0 and 1),
                       // 3 an event pair around every pyramid level launch (k_pyramid_level durations)
-    unsigned long long* d_span = nullptr;  // profile 3: per-block stamps of the recorded pyramid launches
-    size_t span_cap = 0, span_used = 0;    // (u64 words; 8 per block, [6] wall start, [7] wall end)
-    std::vector<std::pair<size_t, size_t>> span_launches;  // (offset, blocks) per recorded launch
+    std::vector<hipEvent_t> pyr_events;  // profile 3: an event pair around every recorded pyramid launch
+    size_t pyr_ev_used = 0;              // events recorded since profiling was enabled (2 per launch)
     std::vector<hipEvent_t> events;   // kStages + 1 per profiled sub-batch launch
     int ev_used = 0;                  // launches recorded since the last read
     long long frames_profiled = 0;
     unsigned long long* d_stamps = nullptr;  // quad-tree phase timers (ORBGPU_DEBUG_FLAGS & 4)
     size_t stamps_cap = 0;
-    // whole-pyramid band kernel (k_pyramid_band): plan for the current geometry and band count
-    // off by default: measured slower than the per-level launches (DESIGN.md sec. 4, round 1:
-    // 0.694 ms/step all levels, 0.626 ms from level 3, against 0.610 ms)
-    int band_mode = 0;         // ORBGPU_PYR_BAND=1 enables it
-    int band_wg_per_cu = 1;    // target workgroups per CU (ORBGPU_PYR_WG_PER_CU)
-    int band_from = 0;         // first level built by the band kernel (ORBGPU_PYR_BAND_FROM); earlier: per-level
-    int band_r = 16;           // rows per task (ORBGPU_PYR_BAND_R)
-    int num_cus = 0;
-    int plan_nb = -1;          // band count the device plan was built for (-1: none)
-    bool plan_ok = false;
-    int plan_max_tasks = 0, plan_R = 0, plan_ring = 0, plan_s_rows = 0, plan_sp = 0, plan_vp = 0, plan_hp = 0;
-    size_t plan_lds = 0;
-    BandTask* d_tasks = nullptr; size_t tasks_cap = 0;
-    int* d_ntasks = nullptr; size_t ntasks_cap = 0;
 };
 
 }  // namespace orbgpu
@@ -2189,9 +1824,12 @@ int grow(T*& p, size_t& cap, size_t need) {
 
 // Tile records of every pyramid level, one int4 per tile of a frame (row-major):
 //   x: X0 | Y0 << 16 (padded-plane origin)
-//   y: bx0 | bw << 16, z: by0 | bh << 16 (level > 0): the previous-level view box the tile (+3-px halo)
-//      reads -- the view range it covers under REFLECT_101, mapped through cv::resize's source index
-//      (the same double expressions as resize_src_index), plus the second bilinear tap
+//   y: bx0 | bw << 16, z: by0 | bh << 16 (level > 0): the previous-level view box the tile reads --
+//      the view range its (clamped) columns and rows cover under REFLECT_101, mapped through
+//      cv::resize's source index (the kernel's double expressions), plus the second bilinear tap
+// Tiles cover the written region [kEdge - kBorder, kEdge + len + kBorder) of each axis.
+int pyr_tiles_x(const orbgpu::LevelGeom& L) { return (L.w + 2 * kBorder + kTileW - 1) / kTileW; }
+int pyr_tiles_y(const orbgpu::LevelGeom& L) { return (L.h + 2 * kBorder + kTileH - 1) / kTileH; }
 void tile_tables(const orbgpu::KernelGeom& k, std::vector<int4>& tab, int* off) {
     auto refl = [](int a, int b, int len, int& lo, int& hi) {
         lo = 1 << 30; hi = -1;
@@ -2209,16 +1847,17 @@ void tile_tables(const orbgpu::KernelGeom& k, std::vector<int4>& tab, int* off) 
     for (int l = 0; l < k.nlevels; ++l) {
         const orbgpu::LevelGeom& L = k.lv[l];
         off[l] = (int)tab.size();
-        for (int Y0 = 0; Y0 < L.ph; Y0 += kTileH)
-            for (int X0 = 0; X0 < L.pw; X0 += kTileW) {
+        for (int ty = 0; ty < pyr_tiles_y(L); ++ty)
+            for (int tx = 0; tx < pyr_tiles_x(L); ++tx) {
+                const int X0 = kEdge - kBorder + tx * kTileW, Y0 = kEdge - kBorder + ty * kTileH;
                 int4 r = make_int4(X0 | Y0 << 16, 0, 0, 0);
                 if (l > 0) {
                     const orbgpu::LevelGeom& P = k.lv[l - 1];
                     const double scx = 1. / ((double)L.w / P.w), scy = 1. / ((double)L.h / P.h);
                     int a, b;
-                    refl(X0 - kHalo - kEdge, X0 + kTileW + kHalo - 1 - kEdge, L.w, a, b);
+                    refl(X0 - kEdge, std::min(X0 + kTileW - 1 - kEdge, L.w + kBorder - 1), L.w, a, b);
                     const int bx0 = src(a, scx, P.w), bw = std::min(src(b, scx, P.w) + 1, P.w - 1) - bx0 + 1;
-                    refl(Y0 - kHalo - kEdge, Y0 + kTileH + kHalo - 1 - kEdge, L.h, a, b);
+                    refl(Y0 - kEdge, std::min(Y0 + kTileH - 1 - kEdge, L.h + kBorder - 1), L.h, a, b);
                     const int by0 = src(a, scy, P.h), bh = std::min(src(b, scy, P.h) + 1, P.h - 1) - by0 + 1;
                     r.y = bx0 | bw << 16;
                     r.z = by0 | bh << 16;
@@ -2237,8 +1876,6 @@ int prepare(Extractor* e, int w, int h, int n) {
         e->geo = g;
         e->cur_w = w;
         e->cur_h = h;
-        e->plan_nb = -1;
-        e->plan_ok = false;
         int rc;
         if ((rc = grow(e->d_cells, e->cells_cap, g.cells.size())) != ORB_OK) return rc;
         if ((rc = grow(e->d_xtab, e->xtab_cap, std::max<size_t>(1, g.xtab.size() / 2))) != ORB_OK) return rc;
@@ -2278,7 +1915,6 @@ int prepare(Extractor* e, int w, int h, int n) {
     const orbgpu::KernelGeom& k = e->geo.k;
     int rc;
     if ((rc = grow(e->d_pyr, e->pyr_cap, (size_t)k.pyr_frame_bytes * n)) != ORB_OK) return rc;
-    if ((rc = grow(e->d_blur, e->blur_cap, (size_t)k.pyr_frame_bytes * n)) != ORB_OK) return rc;
     if ((rc = grow(e->d_cand, e->cand_cap, (size_t)k.cand_frame_cap * n)) != ORB_OK) return rc;
     if ((rc = grow(e->d_scratch, e->scratch_cap, (size_t)k.cand_frame_cap * n * 2)) != ORB_OK) return rc;
     if ((rc = grow(e->d_cell_count, e->cell_count_cap, (size_t)k.ncells * n)) != ORB_OK) return rc;
@@ -2293,140 +1929,6 @@ int prepare(Extractor* e, int w, int h, int n) {
     }
     if ((k.debug_flags & 4) && (rc = grow(e->d_stamps, e->stamps_cap, (size_t)k.nlevels * n * kQtStamps)) != ORB_OK) return rc;
     return ORB_OK;
-}
-
-// Band plan of k_pyramid_band for nb bands (host, once per geometry and band count).  Own rows
-// of band b at level l: [b*h/nb, (b+1)*h/nb).  Computed rows C_l, from the top level down: own rows
-// +-3 (blur), and the source rows of C_{l+1}.  Tasks are chunks of R rows of C_l, level by level.
-// Returns false when the plan does not fit (LDS, staging registers, hsum ring): per-level path.
-bool build_band_plan(const orbgpu::Geometry& G, int nb, int R, int ring, int lfirst, std::vector<BandTask>& tasks,
-                     std::vector<int>& counts, int& max_tasks, int& s_rows) {
-    const orbgpu::KernelGeom& k = G.k;
-    const int L = k.nlevels;
-    std::vector<std::vector<BandTask>> per(nb);
-    s_rows = R;
-    auto yt = [&](int l, int y) { return &G.ytab[4 * ((size_t)k.lv[l].ytab_off + y)]; };
-    for (int b = 0; b < nb; ++b) {
-        std::vector<int> c0(L), c1(L), o0(L), o1(L);
-        for (int l = L - 1; l >= lfirst; --l) {
-            const int h = k.lv[l].h;
-            o0[l] = (int)((long long)b * h / nb);
-            o1[l] = (int)((long long)(b + 1) * h / nb);
-            int lo = std::max(o0[l] - 3, 0), hi = std::min(o1[l] + 3, h);
-            if (l + 1 < L && c1[l + 1] > c0[l + 1]) {
-                lo = std::min(lo, yt(l + 1, c0[l + 1])[0]);
-                hi = std::max(hi, yt(l + 1, c1[l + 1] - 1)[1] + 1);
-            }
-            c0[l] = lo;
-            c1[l] = hi;
-        }
-        std::vector<BandTask>& T = per[b];
-        std::vector<int> first(L, 0);
-        for (int l = lfirst; l < L; ++l) {
-            const int h = k.lv[l].h;
-            first[l] = (int)T.size();
-            int e_next = o0[l];
-            for (int a = c0[l]; a < c1[l]; a += R) {
-                BandTask t{};
-                t.level = l;
-                t.a = a;
-                t.b = std::min(a + R, c1[l]);
-                if (l == 0) {
-                    t.s_lo = t.a;
-                    t.s_n = t.b - t.a;
-                } else {
-                    t.s_lo = yt(l, t.a)[0];
-                    t.s_n = yt(l, t.b - 1)[1] - t.s_lo + 1;
-                    // producer of the last source row (level l-1 chunks are consecutive from first[l-1]);
-                    // level lfirst reads a level written by an earlier launch
-                    if (l > lfirst) {
-                        const int p = first[l - 1] + (yt(l, t.b - 1)[1] - c0[l - 1]) / R;
-                        t.late = p >= (int)T.size() - 1;
-                        if (yt(l, t.a)[0] < c0[l - 1] || yt(l, t.b - 1)[1] >= c1[l - 1]) return false;
-                    }
-                }
-                s_rows = std::max(s_rows, t.s_n);
-                t.e0 = e_next;
-                t.e1 = std::max(e_next, std::min(o1[l], t.b == h ? h : t.b - 3));
-                // every hsum row the emitted rows read must still be in the ring
-                for (int y = t.e0; y < t.e1; ++y)
-                    for (int d = -3; d <= 3; ++d) {
-                        int yy = y + d;
-                        yy = yy < 0 ? -yy : yy >= h ? 2 * h - 2 - yy : yy;
-                        if (yy >= t.b || yy < t.b - ring || yy < c0[l]) return false;
-                    }
-                e_next = t.e1;
-                T.push_back(t);
-            }
-            if (e_next != o1[l]) return false;
-        }
-    }
-    max_tasks = 0;
-    for (auto& T : per) max_tasks = std::max(max_tasks, (int)T.size());
-    tasks.assign((size_t)nb * max_tasks, BandTask{});
-    counts.assign(nb, 0);
-    for (int b = 0; b < nb; ++b) {
-        counts[b] = (int)per[b].size();
-        std::copy(per[b].begin(), per[b].end(), tasks.begin() + (size_t)b * max_tasks);
-    }
-    return true;
-}
-
-// Prepare (or reuse) the band plan for a batch of n frames; false: use the per-level launches.
-bool ensure_band_plan(Extractor* e, int n) {
-    if (!e->band_mode) return false;
-    const orbgpu::Geometry& G = e->geo;
-    const orbgpu::KernelGeom& k = G.k;
-    if (e->num_cus <= 0) {
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 256;
-        e->num_cus = std::max(1, cus);
-    }
-    const int lfirst = std::min(std::max(e->band_from, 0), k.nlevels - 1);
-    const int max_nb = std::max(1, k.lv[k.nlevels - 1].h / 8);
-    const int nb = std::min(max_nb, std::max(1, (e->num_cus * e->band_wg_per_cu + n - 1) / n));
-    if (nb == e->plan_nb) return e->plan_ok;
-    if (e->plan_nb >= 0 && hipDeviceSynchronize() != hipSuccess) return false;  // old plan may be in flight
-    e->plan_nb = nb;
-    e->plan_ok = false;
-    // widest level the kernel touches: the source of level lfirst (or lfirst itself for level 0)
-    const int w0 = k.lv[lfirst > 0 ? lfirst - 1 : 0].w, pw0 = k.lv[lfirst].pw;
-    const int sp = (w0 + 16 + 15) & ~15, vp = (pw0 + 8 + 15) & ~15, hp = (k.lv[lfirst].w + 34 + 7) & ~7;
-    const size_t xt = G.xtab.size() / 2;
-    if ((pw0 + 3) / 4 > kBandThreads) return false;
-    for (int R = e->band_r; R >= 4; R /= 2) {
-        int ring = 1;
-        while (ring < R + 8) ring *= 2;
-        std::vector<BandTask> tasks;
-        std::vector<int> counts;
-        int max_tasks = 0, s_rows = 0;
-        if (!build_band_plan(G, nb, R, ring, lfirst, tasks, counts, max_tasks, s_rows)) continue;
-        const size_t lds = (size_t)s_rows * sp + (size_t)R * vp + (size_t)ring * hp * 2 + xt * 8;
-        if (lds > 160 * 1024) continue;
-        // staged source granules per task must fit kBandGranules per thread
-        const int gmax = std::max(s_rows * ((w0 + 4 + 15) >> 4), R * (k.lv[0].w >> 4));
-        if (gmax > kBandGranules * kBandThreads) continue;
-        if (grow(e->d_tasks, e->tasks_cap, tasks.size()) != ORB_OK || grow(e->d_ntasks, e->ntasks_cap, counts.size()) != ORB_OK)
-            return false;
-        if (hipMemcpy(e->d_tasks, tasks.data(), tasks.size() * sizeof(BandTask), hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemcpy(e->d_ntasks, counts.data(), counts.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
-            return false;
-        if (hipFuncSetAttribute((const void*)k_pyramid_band<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess ||
-            hipFuncSetAttribute((const void*)k_pyramid_band<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-            return false;
-        e->plan_max_tasks = max_tasks;
-        e->plan_R = R;
-        e->plan_ring = ring;
-        e->plan_s_rows = s_rows;
-        e->plan_sp = sp;
-        e->plan_vp = vp;
-        e->plan_hp = hp;
-        e->plan_lds = lds;
-        e->plan_ok = true;
-        return true;
-    }
-    return false;
 }
 
 // Enqueue the five stages for frames [f0, f0 + n) of the handle's buffers on stream st.
@@ -2446,11 +1948,10 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
         e->ev_used++;
         e->frames_profiled += n;
     }
-    auto mark = [&](int i) {  // profile 3 (per-launch block spans) records no stage events
+    auto mark = [&](int i) {  // profile 3 (per-launch event pairs) records no stage events
         if (ev && (e->profile == 1 || (e->profile == 2 && i <= 1))) hipEventRecord(ev[i], st);
     };
     uint8_t* pyr = e->d_pyr + (size_t)f0 * k.pyr_frame_bytes;
-    uint8_t* blr = e->d_blur + (size_t)f0 * k.pyr_frame_bytes;
     uint32_t* cand = e->d_cand + (size_t)f0 * k.cand_frame_cap;
     uint32_t* scratch = e->d_scratch + (size_t)f0 * k.cand_frame_cap * 2;
     int32_t* ccount = e->d_cell_count + (size_t)f0 * k.ncells;
@@ -2522,60 +2023,16 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
         int chunks = 0;  // blocks per frame: ceil(sel_cap_l / 8) per level (see k_describe)
         for (int l = 0; l < lim; ++l) chunks += (k.lv[l].sel_cap + kDescKpPerBlock - 1) / kDescKpPerBlock;
         const int total = chunks * n, share = (total + 7) / 8;
-        hipLaunchKernelGGL(k_describe, dim3(8 * share), dim3(256), 0, s2, e->d_geom, pyr, blr, sel, scount, dst, lapc,
+        hipLaunchKernelGGL(k_describe, dim3(8 * share), dim3(256), 0, s2, e->d_geom, pyr, sel, scount, dst, lapc,
                            cap, kps, desc, counts, chunks, total, share, split, mode,
                            e->d_st_kp ? e->d_st_kp + (size_t)f0 * k.sel_frame_cap : nullptr,
                            e->d_st_desc ? e->d_st_desc + (size_t)f0 * k.sel_frame_cap * 32 : nullptr);
     };
-    // levels [0, lfirst): per-level launches; [lfirst, L): one band launch (k_pyramid_band)
-    const bool band = ensure_band_plan(e, n);
-    const int lfirst = band ? std::min(std::max(e->band_from, 0), k.nlevels - 1) : k.nlevels;
     // the early levels' FAST (and with desc_split their quad-tree + descriptors) go to the side stream
-    // only when those levels come from the per-level launches
-    desc_split = e->desc_split && split > 0 && split <= lfirst && !e->fast_per_level && e->d_st_kp;
-    const bool qts = (e->qt_split || desc_split) && split > 0 && split <= lfirst && !e->fast_per_level;
-    auto launch_band = [&]() {
-        BandArgs A;
-        A.max_tasks = e->plan_max_tasks;
-        A.in_frame_stride = (long long)frame_stride;
-        A.in_stride = stride;
-        A.in_vec = ((uintptr_t)imgs % 16 == 0 && stride % 16 == 0 && frame_stride % 16 == 0 && k.lv[0].w % 16 == 0) ? 1 : 0;
-        A.xt_total = (int)(G.xtab.size() / 2);
-        A.R = e->plan_R;
-        A.ring = e->plan_ring;
-        A.s_rows = e->plan_s_rows;
-        A.sp = e->plan_sp;
-        A.vp = e->plan_vp;
-        A.hp = e->plan_hp;
-        static const bool trace = getenv("ORBGPU_BAND_TRACE") != nullptr;
-        unsigned long long* stamps = nullptr;
-        if (trace) (void)hipMalloc(&stamps, sizeof(unsigned long long) * 10 * e->plan_max_tasks);
-        if (e->band_wg_per_cu >= 2 && 2 * e->plan_lds <= 160 * 1024)
-            hipLaunchKernelGGL(k_pyramid_band<8>, dim3(e->plan_nb, n), dim3(kBandThreads), e->plan_lds, st, e->d_geom,
-                               e->d_tasks, e->d_ntasks, imgs, pyr, blr, e->d_xtab, e->d_ytab, stamps, A);
-        else
-            hipLaunchKernelGGL(k_pyramid_band<4>, dim3(e->plan_nb, n), dim3(kBandThreads), e->plan_lds, st, e->d_geom,
-                               e->d_tasks, e->d_ntasks, imgs, pyr, blr, e->d_xtab, e->d_ytab, stamps, A);
-        if (stamps) {  // debug: per-task phase times of band 0, frame 0 (wave 0's view)
-            std::vector<unsigned long long> h(10 * e->plan_max_tasks);
-            std::vector<BandTask> tk(e->plan_max_tasks);
-            int nt0 = 0;
-            (void)hipStreamSynchronize(st);
-            (void)hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost);
-            (void)hipMemcpy(tk.data(), e->d_tasks, tk.size() * sizeof(BandTask), hipMemcpyDeviceToHost);
-            (void)hipMemcpy(&nt0, e->d_ntasks, sizeof(int), hipMemcpyDeviceToHost);
-            for (int i = 0; i < nt0; ++i) {
-                fprintf(stderr, "band-trace task %2d L%d rows [%3d,%3d) late %d |", i, tk[i].level, tk[i].a, tk[i].b, tk[i].late);
-                for (int k = 1; k < 10; ++k) fprintf(stderr, " %5.2f", (h[10 * i + k] - h[10 * i + k - 1]) * 0.01);
-                fprintf(stderr, "\n");
-            }
-            fprintf(stderr, "band-trace (stage vblur issue resize bar1 commit write hblur bar2) total %.2f us, %d tasks, nb %d, R %d\n",
-                    (h[10 * (nt0 - 1) + 9] - h[0]) * 0.01, nt0, e->plan_nb, e->plan_R);
-            (void)hipFree(stamps);
-        }
-    };
+    desc_split = e->desc_split && split > 0 && !e->fast_per_level && e->d_st_kp;
+    const bool qts = (e->qt_split || desc_split) && split > 0 && !e->fast_per_level;
     static const bool pyr_stamps = getenv("ORBGPU_PYR_STAMPS") != nullptr;
-    for (int l = 0; l < lfirst; ++l) {
+    for (int l = 0; l < k.nlevels; ++l) {
         const orbgpu::LevelGeom& L = k.lv[l];
         PyrArgs A{};
         A.frame_bytes = k.pyr_frame_bytes;
@@ -2588,53 +2045,56 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
             A.sw = P.w; A.sh = P.h; A.spitch = P.pitch;
         }
         A.tab_off = e->tile_off[l];
-        A.tiles_per_frame = ((L.pw + kTileW - 1) / kTileW) * ((L.ph + kTileH - 1) / kTileH);
+        A.tiles_per_frame = pyr_tiles_x(L) * pyr_tiles_y(L);
         A.share = (A.tiles_per_frame + 7) / 8;  // tiles of a frame per XCD (xcd_tile)
         const dim3 grid(8 * A.share, n);
         unsigned long long* stamps = nullptr;
         const size_t nblk = (size_t)grid.x * grid.y;
         if (pyr_stamps && hipMalloc(&stamps, sizeof(unsigned long long) * 8 * nblk) == hipSuccess)
             (void)hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * 8 * nblk, st);
-        // profile 3: per-block wall-clock start / end of this launch into the span buffer (the launch's
-        // duration = last block end - first block start; no events between the launches)
-        if (e->profile == 3 && !stamps && e->d_span) {
-            const size_t need = (size_t)8 * nblk;
-            if (e->span_used + need <= e->span_cap) {
-                stamps = e->d_span + e->span_used;
-                e->span_launches.push_back({e->span_used, nblk});
-                e->span_used += need;
-            }
+        // profile 3: the launch carries an event pair (hipExtLaunchKernel) that takes the dispatch's own
+        // begin / end timestamps -- the interval rocprofv3's kernel trace reports for it
+        hipEvent_t* pe = nullptr;
+        if (e->profile == 3 && e->pyr_ev_used + 2 <= e->pyr_events.size()) {
+            pe = &e->pyr_events[e->pyr_ev_used];
+            e->pyr_ev_used += 2;
         }
+        auto go = [&](auto kern, auto... args) {
+            if (pe) hipExtLaunchKernelGGL(kern, grid, dim3(256), 0, st, pe[0], pe[1], 0, args...);
+            else hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, args...);
+        };
+        const int2* xt = e->d_xtab;
+        const int4* yt = e->d_ytab;
+        const int4* tt = e->d_tiletab;
         if (l == 0)
-            hipLaunchKernelGGL(k_pyramid_level<true>, grid, dim3(256), 0, st, A, imgs, (long long)frame_stride, stride,
-                               pyr, blr, e->d_xtab, e->d_ytab, e->d_tiletab, stamps,
-                               e->clear_status_l0 && f0 == 0 ? e->d_status : nullptr);
+            go(k_pyramid_level<true>, A, imgs, (long long)frame_stride, stride, pyr, xt, yt, tt, stamps,
+               e->clear_status_l0 && f0 == 0 ? e->d_status : (int*)nullptr);
         else if (4 * k.lv[l - 1].w <= 5 * L.w && 4 * k.lv[l - 1].h <= 5 * L.h)  // level ratio <= 1.25
-            hipLaunchKernelGGL((k_pyramid_level<false, kSmallBoxH, kSmallBoxW>), grid, dim3(256), 0, st, A, nullptr,
-                               0LL, 0, pyr, blr, e->d_xtab, e->d_ytab, e->d_tiletab, stamps, nullptr);
+            go(k_pyramid_level<false, kSmallBoxH, kSmallBoxW>, A, (const uint8_t*)nullptr, 0LL, 0, pyr, xt, yt, tt, stamps,
+               (int*)nullptr);
         else
-            hipLaunchKernelGGL((k_pyramid_level<false, kBoxH, kBoxW>), grid, dim3(256), 0, st, A, nullptr, 0LL, 0, pyr,
-                               blr, e->d_xtab, e->d_ytab, e->d_tiletab, stamps, nullptr);
+            go(k_pyramid_level<false, kBoxH, kBoxW>, A, (const uint8_t*)nullptr, 0LL, 0, pyr, xt, yt, tt, stamps,
+               (int*)nullptr);
         if (stamps && pyr_stamps) {  // debug: phase clocks of this level's blocks
             std::vector<unsigned long long> hst((size_t)8 * nblk);
             (void)hipStreamSynchronize(st);
             (void)hipMemcpy(hst.data(), stamps, hst.size() * 8, hipMemcpyDeviceToHost);
             (void)hipFree(stamps);
-            double ph[6] = {0}, life = 0;
+            double ph[4] = {0}, life = 0;
             unsigned long long t0 = ~0ull, t1 = 0;
             int cnt = 0;
             for (size_t b = 0; b < nblk; ++b) {
                 const unsigned long long* q = &hst[(size_t)8 * b];
                 if (!q[6]) continue;
                 ++cnt;
-                for (int i = 1; i < 6; ++i) ph[i] += (double)(q[i] - q[i - 1]);
+                for (int i = 1; i < 4; ++i) ph[i] += (double)(q[i] - q[i - 1]);
                 life += (double)(q[7] - q[6]);
                 t0 = std::min(t0, q[6]);
                 t1 = std::max(t1, q[7]);
             }
-            fprintf(stderr, "pyr-stamps L%d blocks %d span %.1f us  mean life %.2f us  concurrency %.0f  phases(cyc) box %.0f resize %.0f store %.0f hblur %.0f vblur %.0f\n",
+            fprintf(stderr, "pyr-stamps L%d blocks %d span %.1f us  mean life %.2f us  concurrency %.0f  phases(cyc) box %.0f resize %.0f store %.0f\n",
                     l, cnt, (t1 - t0) * 0.01, life / cnt * 0.01, life / (double)(t1 - t0), ph[1] / cnt, ph[2] / cnt,
-                    ph[3] / cnt, ph[4] / cnt, ph[5] / cnt);
+                    ph[3] / cnt);
         }
         if (split && l == split - 1) {
             hipEventRecord(e->split_ev[0], st);
@@ -2650,11 +2110,8 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
             launch_fast(l, l + 1, e->side2);
         }
     }
-    if (band) launch_band();
     mark(1);
-    if (band && (split == 0 || split > lfirst)) {
-        launch_fast(0, k.nlevels, st);
-    } else if (split && e->fast_per_level && !band) {
+    if (split && e->fast_per_level) {
         hipEventRecord(e->split_ev[2], e->side2);
         hipStreamWaitEvent(st, e->split_ev[2], 0);
     } else {
@@ -2662,7 +2119,7 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     }
     // qt_split: the quad-tree of the early levels runs on the side stream right after their FAST
     // (desc_split: and their descriptors, into the staging records)
-    if (!qts && split && (!band || split <= lfirst)) hipStreamWaitEvent(st, e->split_ev[1], 0);
+    if (!qts && split) hipStreamWaitEvent(st, e->split_ev[1], 0);
     mark(2);
     launch_qt(qts ? split : 0, k.nlevels, st);
     if (qts) hipStreamWaitEvent(st, e->split_ev[1], 0);
@@ -2681,10 +2138,9 @@ int launch_batch(Extractor* e, const uint8_t* d_images, int n, int w, int h, int
                  int lap0, int lap1, orb_keypoint_t* d_kps, uint8_t* d_desc, int cap, int32_t* d_counts,
                  hipStream_t st) {
     (void)w; (void)h;
-    // the level-0 pyramid launch of the first (sub-)batch clears the status; the band path has no
-    // level-0 launch when it builds every level, and sub-batches on several streams need it cleared
-    // before the fork
-    e->clear_status_l0 = !(e->band_mode || (e->nstreams > 1 && (n + e->chunk - 1) / e->chunk > 1));
+    // the level-0 pyramid launch of the first (sub-)batch clears the status; sub-batches on several
+    // streams need it cleared before the fork
+    e->clear_status_l0 = !(e->nstreams > 1 && (n + e->chunk - 1) / e->chunk > 1);
     if (!e->clear_status_l0) hipMemsetAsync(e->d_status, 0, sizeof(int), st);
     const int nchunks = (n + e->chunk - 1) / e->chunk;
     if (nchunks <= 1 || e->nstreams <= 1) {
@@ -2742,12 +2198,8 @@ int orb_extractor_create(const orb_params_t* p, int max_width, int max_height, i
     for (int k2 = 0; k2 < orbgpu::kMaxLevels && ok; ++k2)
         ok = hipEventCreateWithFlags(&e->lvl_ev[k2], hipEventDisableTiming) == hipSuccess;
     if (const char* c = getenv("ORBGPU_FAST_PER_LEVEL")) e->fast_per_level = atoi(c);
-    if (const char* c = getenv("ORBGPU_PYR_BAND")) e->band_mode = atoi(c);
     if (const char* c = getenv("ORBGPU_QT_SPLIT")) e->qt_split = atoi(c);
     if (const char* c = getenv("ORBGPU_DESC_SPLIT")) e->desc_split = atoi(c);
-    if (const char* c = getenv("ORBGPU_PYR_WG_PER_CU")) e->band_wg_per_cu = std::max(1, atoi(c));
-    if (const char* c = getenv("ORBGPU_PYR_BAND_FROM")) e->band_from = std::max(0, atoi(c));
-    if (const char* c = getenv("ORBGPU_PYR_BAND_R")) e->band_r = std::min(16, std::max(4, atoi(c)));
     for (int s = 0; s < Extractor::kMaxStreams && ok; ++s)
         ok = hipStreamCreateWithFlags(&e->sub[s], hipStreamNonBlocking) == hipSuccess &&
              hipEventCreateWithFlags(&e->join_ev[s], hipEventDisableTiming) == hipSuccess;
@@ -2785,12 +2237,13 @@ int orb_extractor_destroy(orb_extractor_t h) {
     Extractor* e = reinterpret_cast<Extractor*>(h);
     if (!e) return ORB_ERR_ARG;
     if (e->stream) hipStreamSynchronize(e->stream);
-    void* bufs[] = {e->d_span, e->d_st_kp, e->d_st_desc, e->d_tasks, e->d_ntasks, e->d_stamps, e->d_geom, e->d_cells, e->d_xtab, e->d_tiletab, e->d_ytab, e->d_pyr, e->d_blur, e->d_cand, e->d_scratch,
+    void* bufs[] = {e->d_st_kp, e->d_st_desc, e->d_stamps, e->d_geom, e->d_cells, e->d_xtab, e->d_tiletab, e->d_ytab, e->d_pyr, e->d_cand, e->d_scratch,
                     e->d_cell_count, e->d_cell_thr, e->d_sel, e->d_dst, e->d_sel_count, e->d_lap_count, e->d_status,
                     e->d_img, e->d_kps, e->d_desc, e->d_counts};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t x : e->events) (void)hipEventDestroy(x);
+    for (hipEvent_t x : e->pyr_events) (void)hipEventDestroy(x);
     if (e->side) { hipStreamSynchronize(e->side); hipStreamDestroy(e->side); }
     if (e->side2) { hipStreamSynchronize(e->side2); hipStreamDestroy(e->side2); }
     for (int k2 = 0; k2 < 3; ++k2)
@@ -2982,12 +2435,15 @@ int orb_debug_level_blurred(orb_extractor_t h, int frame, int level, uint8_t* ho
     if (!e || !host_view || !e->geo_ok || frame < 0 || frame >= e->last_n || level < 0 || level >= e->P.nlevels)
         return orbgpu_fail(ORB_ERR_ARG, "no such level");
     const orbgpu::LevelGeom& L = e->geo.k.lv[level];
-    const uint8_t* src = e->d_blur + (size_t)frame * e->geo.k.pyr_frame_bytes + L.plane_off +
-                         (size_t)orbgpu::kEdge * L.pitch + orbgpu::kEdge;
-    hipDeviceSynchronize();
-    if (hipMemcpy2D(host_view, L.w, src, L.pitch, L.w, L.h, hipMemcpyDeviceToHost) != hipSuccess)
-        return orbgpu_fail(ORB_ERR_DEVICE, "download failed");
-    return ORB_OK;
+    const uint8_t* view = e->d_pyr + (size_t)frame * e->geo.k.pyr_frame_bytes + L.plane_off +
+                          (size_t)orbgpu::kEdge * L.pitch + orbgpu::kEdge;
+    uint8_t* d = nullptr;
+    if (hipDeviceSynchronize() != hipSuccess || hipMalloc(&d, (size_t)L.w * L.h) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "debug blur allocation failed");
+    hipLaunchKernelGGL(k_debug_blur, dim3((L.w + 255) / 256, L.h), dim3(256), 0, 0, view, L.pitch, L.w, L.h, d);
+    const bool ok = hipMemcpy(host_view, d, (size_t)L.w * L.h, hipMemcpyDeviceToHost) == hipSuccess;
+    (void)hipFree(d);
+    return ok ? ORB_OK : orbgpu_fail(ORB_ERR_DEVICE, "download failed");
 }
 
 // Per-stage timing (HIP events on the launch stream).  enable != 0 starts recording (and clears
@@ -2998,15 +2454,14 @@ int orb_extractor_profile(orb_extractor_t h, int enable) {
     if (!e) return ORB_ERR_ARG;
     e->profile = (enable == 2 || enable == 3) ? enable : (enable != 0 ? 1 : 0);
     e->ev_used = 0;
-    e->span_used = 0;
-    e->span_launches.clear();
-    if (enable == 3) {  // room for 64 steps of 64-frame 640x480 batches (~31k blocks per step)
-        const size_t want = (size_t)8 * 4 * 1024 * 1024;
-        if (!e->d_span) {
-            if (hipMalloc(&e->d_span, want * 8) != hipSuccess) { e->d_span = nullptr; return orbgpu_fail(ORB_ERR_DEVICE, "hipMalloc failed"); }
-            e->span_cap = want;
+    e->pyr_ev_used = 0;
+    if (enable == 3) {  // event pairs for 256 batches of every level, created before the timed region
+        const size_t want = (size_t)2 * orbgpu::kMaxLevels * 256;
+        while (e->pyr_events.size() < want) {
+            hipEvent_t x;
+            if (hipEventCreate(&x) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "hipEventCreate failed");
+            e->pyr_events.push_back(x);
         }
-        if (hipMemset(e->d_span, 0, e->span_cap * 8) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "hipMemset failed");
     }
     e->frames_profiled = 0;
     e->batches = 0;
@@ -3039,24 +2494,16 @@ int orb_extractor_pyramid_launch_ms(orb_extractor_t h, float* ms, int* launches)
     if (!e || !ms) return ORB_ERR_ARG;
     *ms = 0.f;
     if (launches) *launches = 0;
-    if (!e->d_span || e->span_launches.empty()) return ORB_OK;
-    std::vector<unsigned long long> hst(e->span_used);
-    if (hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpy(hst.data(), e->d_span, e->span_used * 8, hipMemcpyDeviceToHost) != hipSuccess)
-        return orbgpu_fail(ORB_ERR_DEVICE, "span download failed");
     double tot = 0;
-    for (const auto& L : e->span_launches) {
-        unsigned long long t0 = ~0ull, t1 = 0;
-        for (size_t b = 0; b < L.second; ++b) {
-            const unsigned long long* q = &hst[L.first + 8 * b];
-            if (!q[6]) continue;  // blocks past the frame's tiles return before stamping
-            t0 = std::min(t0, q[6]);
-            t1 = std::max(t1, q[7]);
-        }
-        if (t1 > t0) tot += (double)(t1 - t0) * 1e-5;  // wall clock: 100 MHz
+    for (size_t i = 0; i + 1 < e->pyr_ev_used; i += 2) {
+        float t = 0.f;
+        if (hipEventSynchronize(e->pyr_events[i + 1]) != hipSuccess ||
+            hipEventElapsedTime(&t, e->pyr_events[i], e->pyr_events[i + 1]) != hipSuccess)
+            return orbgpu_fail(ORB_ERR_DEVICE, "pyramid launch events failed");
+        tot += t;
     }
     *ms = (float)tot;
-    if (launches) *launches = (int)e->span_launches.size();
+    if (launches) *launches = (int)(e->pyr_ev_used / 2);
     return ORB_OK;
 }
 

@@ -158,7 +158,8 @@ class ORBextractor:
 
     # ---- public pyramid, include/ORBextractor.h:83
     def level_padded(self, level: int, frame: int = 0) -> np.ndarray:
-        """Padded plane ((h+38) x (w+38)) of level `level` of frame `frame` of the last call."""
+        """Padded plane ((h+38) x (w+38)) of level `level` of frame `frame` of the last call.  Only the
+        view and its 3-px REFLECT_101 border ([16:-16, 16:-16]) are written by the extractor."""
         w, h, pitch = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         check(self._lib.orb_extractor_level(self._h, frame, level, None, ctypes.byref(w), ctypes.byref(h),
                                             ctypes.byref(pitch)), "orb_extractor_level")

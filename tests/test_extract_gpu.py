@@ -1,6 +1,6 @@
 """GPU parity of the HIP ORB extractor against the CPU oracle, stage by stage and end to end.
 
-Bar: bit-exact (pyramid bytes, blurred bytes, FAST candidates + per-cell thresholds, quad-tree
+Bar: bit-exact (pyramid bytes, the blurred levels, FAST candidates + per-cell thresholds, quad-tree
 selection order, keypoint structs, descriptors, monoIndex).  Runs on the MI355X box (-m gpu).
 """
 from __future__ import annotations
@@ -58,9 +58,11 @@ def test_extract_parity(pkg, oracle, frames, case):
     rkps, rdesc, rmono = ref(img, lap)
     lib = ex._lib
     for l in range(8):
-        # 1. pyramid (padded planes incl. the REFLECT_101 frame)
+        # 1. pyramid: the view and the 3-px REFLECT_101 border the extractor keeps (the rest of the
+        #    19-px frame is never read, so it is not written)
         gp, rp = ex.level_padded(l), ref.level_padded(l)
-        assert np.array_equal(gp, rp), f"{case} level {l} pyramid: {_first_diff(gp, rp)}"
+        assert np.array_equal(gp[16:-16, 16:-16], rp[16:-16, 16:-16]), \
+            f"{case} level {l} pyramid: {_first_diff(gp[16:-16, 16:-16], rp[16:-16, 16:-16])}"
         # 2. blurred level == GaussianBlur(level.clone(), 7x7, 2) of the oracle's level
         lw, lh = rp.shape[1] - 38, rp.shape[0] - 38
         gb = np.zeros((lh, lw), np.uint8)
@@ -192,34 +194,6 @@ def test_hamming_knn2_split_merge(pkg, nq, nt):
         assert np.array_equal(d2[i0:i0 + 8], srt[:, 1] if nt > 1 else np.full(len(srt), 257))
 
 
-@pytest.mark.parametrize("band_from", ["0", "3"])
-def test_band_pyramid_path_parity(pkg, oracle, frames, synth, monkeypatch, band_from):
-    """The optional whole-pyramid band kernel (ORBGPU_PYR_BAND=1, off by default) stays bit-exact:
-    single frames (aligned 752, unaligned 643 -> byte staging path) and a device batch."""
-    import torch
-    monkeypatch.setenv("ORBGPU_PYR_BAND", "1")
-    monkeypatch.setenv("ORBGPU_PYR_BAND_FROM", band_from)
-    for case in ["stereoL752", "odd_size"]:
-        img, nf, lap = frames[case]
-        ex = pkg.ORBextractor(nf, 1.2, 8, 20, 7, max_width=1280, max_height=720)
-        kps, desc, mono = ex(img, None, lap)
-        rkps, rdesc, rmono = oracle.OracleExtractor(nf, 1.2, 8, 20, 7)(img, lap)
-        assert mono == rmono and np.array_equal(kps.view(np.uint8), rkps.view(np.uint8)), case
-        assert np.array_equal(desc, rdesc), case
-    batch = synth.frame_batch(5, 640, 480, seed0=900)
-    ex = pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=640, max_height=480, max_batch=8)
-    kps, desc, counts = ex.extract_batch_device(torch.from_numpy(batch).cuda(), (0, 1000))
-    torch.cuda.synchronize()
-    counts = counts.cpu().numpy()
-    ref = oracle.OracleExtractor(1000, 1.2, 8, 20, 7)
-    for f in range(len(batch)):
-        rk, rd, rm = ref(batch[f], (0, 1000))
-        n = int(counts[f, 0])
-        assert n == len(rk) and int(counts[f, 1]) == rm
-        assert np.array_equal(pkg.keypoints_to_structured(kps[f], n).view(np.uint8), rk.view(np.uint8)), f
-        assert np.array_equal(desc[f, :n].cpu().numpy(), rd), f
-
-
 @pytest.mark.parametrize("mode", [("ORBGPU_DEBUG_FLAGS", "8"), ("ORBGPU_DEBUG_FLAGS", "2"), ("ORBGPU_DEBUG_FLAGS", "16"),
                                   ("ORBGPU_DESC_SPLIT", "0")],
                          ids=["kp_scratch_keys", "kp_serial_sort", "kp_lds_sort", "no_desc_split"])
@@ -287,11 +261,8 @@ def test_sparse_corners_parity(pkg, oracle):
 
 
 @pytest.mark.parametrize("env", [{"ORBGPU_CHUNK": "2"}, {"ORBGPU_STREAMS": "2", "ORBGPU_CHUNK": "3"},
-                                 {"ORBGPU_FAST_SPLIT": "3"}, {"ORBGPU_FAST_PER_LEVEL": "1"}, {"ORBGPU_QT_SPLIT": "1"},
-                                 {"ORBGPU_PYR_BAND": "1", "ORBGPU_PYR_WG_PER_CU": "2"},
-                                 {"ORBGPU_PYR_BAND": "1", "ORBGPU_PYR_BAND_R": "8"}],
-                         ids=["chunk2", "streams2_chunk3", "fast_split3", "fast_per_level", "qt_split",
-                              "band_2wg_per_cu", "band_r8"])
+                                 {"ORBGPU_FAST_SPLIT": "3"}, {"ORBGPU_FAST_PER_LEVEL": "1"}, {"ORBGPU_QT_SPLIT": "1"}],
+                         ids=["chunk2", "streams2_chunk3", "fast_split3", "fast_per_level", "qt_split"])
 def test_schedule_switches_parity(pkg, oracle, synth, monkeypatch, env):
     """Every per-handle schedule switch (read when the handle is created; orb_extract.hip
     orb_extractor_create) changes only how the batch is cut into launches and streams: a 7-frame batch
