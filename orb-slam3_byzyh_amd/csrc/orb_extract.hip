@@ -647,11 +647,13 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
     uint16_t* cl = reinterpret_cast<uint16_t*>(sc + win_cap);
     const uint8_t* src = view + (size_t)C.ini_y * L.pitch + C.ini_x;
     // window rows as aligned dwords into an LDS image whose rows start `shift` bytes in (the level's
-    // 19-px frame keeps the over-read inside the plane); row stride 48 when the window fits (the usual
-    // 42-px cell window), else ws = roundup(shift + ww, 4)
+    // padded plane keeps the over-read inside it); row stride 52 when the window fits (the usual 42-px
+    // cell window), else ws = roundup(shift + ww, 4).  52 B = 13 dwords: the compass phase's 32-lane
+    // groups (5 octets x ~6.4 rows, 3 dwords each) spread over the 32 banks 2-way instead of the 3-way
+    // a 48-B stride gives (rows 12 dwords apart repeat the bank pattern every 8 rows)
     const int shift = (int)((uintptr_t)src & 3);
-    if (shift + C.win_w <= 48 && C.win_h <= 48)
-        fast_cell<48>(g, C, L, f, cid, lane, win, sc, cl, src, shift, cand, cell_count, cell_thr, stp);
+    if (shift + C.win_w <= 52 && C.win_h <= 48)
+        fast_cell<52>(g, C, L, f, cid, lane, win, sc, cl, src, shift, cand, cell_count, cell_thr, stp);
     else
         fast_cell<0>(g, C, L, f, cid, lane, win, sc, cl, src, shift, cand, cell_count, cell_thr, stp);
 }

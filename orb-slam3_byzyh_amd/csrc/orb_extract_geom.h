@@ -209,8 +209,8 @@ inline bool build_geometry(const Params& P, int width, int height, Geometry& g) 
                 c.cap = ((dw + 1) / 2) * ((dh + 1) / 2);
                 c.slot = level_cap;
                 level_cap += c.cap;
-                // dword-aligned rows; at least 48 bytes (k_fast_cells uses a fixed 48-byte stride when the window fits)
-                const int wbytes = std::max((int)c.win_w + 6, 48) * c.win_h;
+                // dword-aligned rows; at least 52 bytes (k_fast_cells uses a fixed 52-byte stride when the window fits)
+                const int wbytes = std::max((int)c.win_w + 6, 52) * c.win_h;  // k_fast_cells row stride
                 g.max_win = std::max(g.max_win, wbytes);
                 g.max_win_lv[l] = std::max(g.max_win_lv[l], wbytes);
                 g.max_det_lv[l] = std::max(g.max_det_lv[l], dw * dh);
