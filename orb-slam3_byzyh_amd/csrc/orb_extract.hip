@@ -499,13 +499,12 @@ __device__ __forceinline__ void fast_cell(const KernelGeom& g, const CellDesc& C
         };
         auto lo16 = [](uint32_t v) { return as_u16x2(__builtin_amdgcn_perm(v, v, 0x0c010c00u)); };
         auto hi16 = [](uint32_t v) { return as_u16x2(__builtin_amdgcn_perm(v, v, 0x0c030c02u)); };
+        // The adjacent compass pairs are exactly the pairs of one vertical point {p0, p8} and one
+        // horizontal point {p4, p12}, so the largest pairwise minimum is min(max(p0, p8), max(p4, p12))
+        // and the smallest pairwise maximum is max(min(p0, p8), min(p4, p12)): 3 packed ops each.
         auto pass2 = [&](u16x2 v, u16x2 p0, u16x2 p4, u16x2 p8, u16x2 p12) {
-            const u16x2 bmax = __builtin_elementwise_max(
-                __builtin_elementwise_max(__builtin_elementwise_min(p0, p4), __builtin_elementwise_min(p4, p8)),
-                __builtin_elementwise_max(__builtin_elementwise_min(p8, p12), __builtin_elementwise_min(p12, p0)));
-            const u16x2 dmin = __builtin_elementwise_min(
-                __builtin_elementwise_min(__builtin_elementwise_max(p0, p4), __builtin_elementwise_max(p4, p8)),
-                __builtin_elementwise_min(__builtin_elementwise_max(p8, p12), __builtin_elementwise_max(p12, p0)));
+            const u16x2 bmax = __builtin_elementwise_min(__builtin_elementwise_max(p0, p8), __builtin_elementwise_max(p4, p12));
+            const u16x2 dmin = __builtin_elementwise_max(__builtin_elementwise_min(p0, p8), __builtin_elementwise_min(p4, p12));
             const u16x2 br = __builtin_elementwise_sub_sat(bmax, v + tt);  // > 0 <=> bmax > v + t
             const u16x2 dk = __builtin_elementwise_sub_sat(v, dmin + tt);  // > 0 <=> dmin < v - t
             // 0 / 1 per pixel (pass <=> the saturated difference is non-zero)
