@@ -55,6 +55,27 @@ __constant__ uint32_t c_sincos_exc[][3] = {
 };
 constexpr int kNumSincosExc = sizeof(c_sincos_exc) / sizeof(c_sincos_exc[0]);
 
+// IC_Angle disc (src:91-138, umax of ORBextractor's constructor, src:484-505) for HALF_PATCH_SIZE 15,
+// pinned by tests/test_oracle_kat.py; build_geometry checks the host table against it.
+constexpr int kDiscUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+// Per lane r (disc row v = r - 15; lane 31 outside), 8 mask dwords then 8 weight dwords over the 32
+// columns u = -15 .. 16 as bytes: mask = [|u| <= umax[|v|]], weight = (u + 16) * mask.
+struct DiscTable { uint32_t w[32][16]; };
+constexpr DiscTable make_disc_table() {
+    DiscTable t{};
+    for (int r = 0; r < 31; ++r) {
+        const int v = r - 15, U = kDiscUmax[v < 0 ? -v : v];
+        for (int j = 0; j < 32; ++j) {
+            const int u = j - 15;
+            const uint32_t m = (u >= -U && u <= U) ? 1u : 0u;
+            t.w[r][j >> 2] |= m << (8 * (j & 3));
+            t.w[r][8 + (j >> 2)] |= (m * (uint32_t)(u + 16)) << (8 * (j & 3));
+        }
+    }
+    return t;
+}
+__constant__ DiscTable c_disc = make_disc_table();
+
 // 8-fraction-bit GaussianBlur(7x7, sigma=2) kernel of OpenCV's bit-exact 8U path
 // (getGaussianKernelBitExact + error-diffusion fixed point): sums to 256.
 __device__ __forceinline__ int blur_tap(int k) {
@@ -422,7 +443,7 @@ __device__ __forceinline__ bool fast_corner(const uint8_t* __restrict__ p, const
 template <int kWS>
 __device__ __forceinline__ void fast_cell(const KernelGeom& g, const CellDesc& C, const LevelGeom& L, int f, int cid,
                                           int lane, uint8_t* win, uint8_t* sc, uint16_t* cl, const uint8_t* src,
-                                          int shift, uint32_t* __restrict__ cand, int32_t* __restrict__ cell_count,
+                                          int shift, int room, uint32_t* __restrict__ cand, int32_t* __restrict__ cell_count,
                                           uint8_t* __restrict__ cell_thr, unsigned long long* stp) {
     const int ww = C.win_w, wh = C.win_h;
     const int ws = kWS ? kWS : (shift + ww + 3) & ~3, nwr = ws >> 2;
@@ -432,13 +453,19 @@ __device__ __forceinline__ void fast_cell(const KernelGeom& g, const CellDesc& C
     // lanes = 4 rows x 16 dwords (a second column pass only for windows wider than 16 dwords)
     const int lr = lane >> 4, lw = lane & 15;
     if (nwr <= 16 && wh <= 48) {
-        // the usual cell window (<= 64 bytes x 48 rows): every load issued before any LDS store
+        // the usual cell window (<= 64 bytes x 48 rows): every load issued before any LDS store, as
+        // raw buffer loads (one lane offset, the row step in the scalar offset; `room` bytes to the
+        // end of the frame's pyramid block bound the unconditional over-read, which returns 0 past it)
+        // (the window is per wave: make the resource operands wave-uniform, or the compiler wraps
+        // every load in a readfirstlane loop)
+        const uintptr_t wb = reinterpret_cast<uintptr_t>(wsrc);
+        const uint64_t wbu = (uint64_t)(uint32_t)uniform((int)(uint32_t)wb) | (uint64_t)(uint32_t)uniform((int)(uint32_t)(wb >> 32)) << 32;
+        const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(wbu), (short)0, uniform(room), kBufDword3);
+        const int pitch = uniform(L.pitch);
+        const uint32_t vo = (uint32_t)(lr * pitch + 4 * lw);
         uint32_t v[12];
 #pragma unroll
-        for (int k = 0; k < 12; ++k) {
-            const int r = 4 * k + lr;
-            v[k] = (r < wh && lw < nwr) ? wsrc[(size_t)r * (L.pitch >> 2) + lw] : 0u;
-        }
+        for (int k = 0; k < 12; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b32(rw, vo, 4 * k * pitch, 0);
 #pragma unroll
         for (int k = 0; k < 12; ++k) {
             const int r = 4 * k + lr;
@@ -505,15 +532,25 @@ __device__ __forceinline__ void fast_cell(const KernelGeom& g, const CellDesc& C
         auto pass2 = [&](u16x2 v, u16x2 p0, u16x2 p4, u16x2 p8, u16x2 p12) {
             const u16x2 bmax = __builtin_elementwise_min(__builtin_elementwise_max(p0, p8), __builtin_elementwise_max(p4, p12));
             const u16x2 dmin = __builtin_elementwise_max(__builtin_elementwise_min(p0, p8), __builtin_elementwise_min(p4, p12));
-            const u16x2 br = __builtin_elementwise_sub_sat(bmax, v + tt);  // > 0 <=> bmax > v + t
-            const u16x2 dk = __builtin_elementwise_sub_sat(v, dmin + tt);  // > 0 <=> dmin < v - t
-            // 0 / 1 per pixel (pass <=> the saturated difference is non-zero)
-            return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(br | dk, w16(1, 1)));
+            // bright <=> bmax - v > t, dark <=> v - dmin > t (saturating differences of u16 values <= 255)
+            const u16x2 m = __builtin_elementwise_max(__builtin_elementwise_sub_sat(bmax, v), __builtin_elementwise_sub_sat(v, dmin));
+            // 0 / 1 per pixel (pass <=> m - t, saturated, is non-zero): one v_pk_min_u16 (as written
+            // in C the compiler turns the min into two compares, two selects and a v_perm)
+            uint32_t r;
+            asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(__builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(m, tt))), "v"(0x00010001u));
+            return r;
         };
-        auto quad_bits = [&](uint32_t C4, uint32_t D4, uint32_t R4, uint32_t U4, uint32_t L4) {
-            const uint32_t pl = pass2(lo16(C4), lo16(D4), lo16(R4), lo16(U4), lo16(L4));
-            const uint32_t ph = pass2(hi16(C4), hi16(D4), hi16(R4), hi16(U4), hi16(L4));
-            return (pl & 1u) | ((pl >> 15) & 2u) | ((ph & 1u) << 2) | ((ph >> 13) & 8u);
+        // pass2 results of pixels (0,1), (2,3), (4,5), (6,7) as 0/1 halves, shifted into one word whose
+        // low half holds the even pixels' bits and high half the odd ones': bit k = pixel k after
+        // folding the high half down by 15
+        auto octet_bits = [&](uint32_t C0, uint32_t D0, uint32_t R0, uint32_t U0, uint32_t L0, uint32_t C1,
+                              uint32_t D1, uint32_t R1, uint32_t U1, uint32_t L1) {
+            const uint32_t p01 = pass2(lo16(C0), lo16(D0), lo16(R0), lo16(U0), lo16(L0));
+            const uint32_t p23 = pass2(hi16(C0), hi16(D0), hi16(R0), hi16(U0), hi16(L0));
+            const uint32_t p45 = pass2(lo16(C1), lo16(D1), lo16(R1), lo16(U1), lo16(L1));
+            const uint32_t p67 = pass2(hi16(C1), hi16(D1), hi16(R1), hi16(U1), hi16(L1));
+            const uint32_t t = p01 | (p23 << 2) | (p45 << 4) | (p67 << 6);
+            return (t & 0xffu) | (t >> 15);
         };
         // item -> (row, octet): one division here, then a fixed (row, octet) step of 64 items per round
         int r = lane / no, o = lane - (lane / no) * no;
@@ -529,7 +566,7 @@ __device__ __forceinline__ void fast_cell(const KernelGeom& g, const CellDesc& C
                 ext8(rc, o, shift + 6, R0, R1);
                 ext8(rc - 3 * wsw, o, shift + 3, U0, U1);
                 ext8(rc + 3 * wsw, o, shift + 3, D0, D1);
-                bits = quad_bits(C0, D0, R0, U0, L0) | (quad_bits(C1, D1, R1, U1, L1) << 4);
+                bits = octet_bits(C0, D0, R0, U0, L0, C1, D1, R1, U1, L1);
                 const int rem = dw - 8 * o;  // pixels of this octet inside the detectable row
                 if (rem < 8) bits &= (1u << rem) - 1u;
             }
@@ -651,10 +688,11 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
     // groups (5 octets x ~6.4 rows, 3 dwords each) spread over the 32 banks 2-way instead of the 3-way
     // a 48-B stride gives (rows 12 dwords apart repeat the bank pattern every 8 rows)
     const int shift = (int)((uintptr_t)src & 3);
+    const int room = (int)(g.pyr_frame_bytes - (L.plane_off + (long long)(kEdge + C.ini_y) * L.pitch + kEdge + C.ini_x - shift));
     if (shift + C.win_w <= 52 && C.win_h <= 48)
-        fast_cell<52>(g, C, L, f, cid, lane, win, sc, cl, src, shift, cand, cell_count, cell_thr, stp);
+        fast_cell<52>(g, C, L, f, cid, lane, win, sc, cl, src, shift, room, cand, cell_count, cell_thr, stp);
     else
-        fast_cell<0>(g, C, L, f, cid, lane, win, sc, cl, src, shift, cand, cell_count, cell_thr, stp);
+        fast_cell<0>(g, C, L, f, cid, lane, win, sc, cl, src, shift, room, cand, cell_count, cell_thr, stp);
 }
 #undef FAST_STAMP
 
@@ -1591,9 +1629,11 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
     const int li = hl & 15;
     const int cnt_l = li < g.nlevels ? sel_count[(size_t)f * g.nlevels + li] : 0;
     const int lap_l = li < g.nlevels ? lap_count[(size_t)f * g.nlevels + li] : 0;
-    uint32_t pat[8], exc[kExcPerLane];
+    uint32_t pat[8], exc[kExcPerLane], disc[16];
 #pragma unroll
     for (int m = 0; m < 8; ++m) pat[m] = c_pattern_packed.w[32 * m + hl];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) disc[m] = c_disc.w[hl][m];
 #pragma unroll
     for (int e = 0; e < kExcPerLane; ++e) exc[e] = 32 * e + hl < kNumSincosExc ? c_sincos_exc[32 * e + hl][0] : 0u;
     int total = cnt_l, lap_before = li < level ? lap_l : 0, mono_before = li < level ? cnt_l - lap_l : 0;
@@ -1651,21 +1691,29 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
             if (10 * k + pr < kPR) *reinterpret_cast<v4u32*>(P + (10 * k + pr) * kPRW + 4 * pq) = v[k];
     }
     wave_sync();
-    const uint8_t* PC = reinterpret_cast<const uint8_t*>(P) + sh + 21 * (kPRW * 4) + 21;  // keypoint pixel
-    // ---- IC_Angle on the level (src:91-138): lane = disc column u, so m10 = u * (column sum).
-    // The reads are unconditional (lane 31, u = 16, lies outside every disc row) and the disc mask is
-    // a select, so the 31 LDS reads issue back to back.
-    const int u = hl - kHalfPatch, au = u < 0 ? -u : u;
-    int colsum = 0, m01 = 0;
+    // ---- IC_Angle on the level (src:91-138): lane = disc row v (lanes 0..30), its 32 bytes u = -15 ..
+    // 16 as 8 dwords (aligned reads + v_alignbyte).  Row sum S = sum mask*I and W = sum (u+16)*mask*I
+    // by v_dot4_u32_u8 against the lane's table row (loaded at entry), so m01 += v*S, m10 += W - 16 S.
+    int m10 = 0, m01 = 0;
+    {
+        const int rb = sh + (hl + 6) * (kPRW * 4) + 6;  // byte of (v = hl - 15, u = -15)
+        const uint32_t* rw = P + (rb >> 2);
+        const int ra = rb & 3;
+        uint32_t d[9];
 #pragma unroll
-    for (int v = -kHalfPatch; v <= kHalfPatch; ++v) {
-        const int raw = PC[v * (kPRW * 4) + u];
-        const int val = au <= g.umax[v < 0 ? -v : v] ? raw : 0;
-        colsum += val;
-        m01 += v * val;
+        for (int k = 0; k < 9; ++k) d[k] = rw[k];  // rows 6..37 of the patch region (lane 31: unused)
+        uint32_t S = 0, W = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t x = __builtin_amdgcn_alignbyte(d[k + 1], d[k], ra);
+            S = __builtin_amdgcn_udot4(x, disc[k], S, false);
+            W = __builtin_amdgcn_udot4(x, disc[8 + k], W, false);
+        }
+        if (active && hl < 31) {
+            m01 = (hl - 15) * (int)S;
+            m10 = (int)W - 16 * (int)S;
+        }
     }
-    int m10 = u * colsum;
-    if (!active) m10 = m01 = 0;
     m10 = half_wave_sum(m10);
     m01 = half_wave_sum(m01);
     const float angle = orb_fast_atan2((float)m01, (float)m10);
@@ -1874,6 +1922,8 @@ int prepare(Extractor* e, int w, int h, int n) {
         if (e->cur_w >= 0 && hipDeviceSynchronize() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "sync failed");
         orbgpu::Geometry g;
         if (!orbgpu::build_geometry(e->P, w, h, g)) return orbgpu_fail(ORB_ERR_ARG, "image too small for the pyramid/cell grid");
+        for (int v = 0; v < 16; ++v)  // k_describe's compile-time disc table (c_disc) assumes these
+            if (g.k.umax[v] != kDiscUmax[v]) return orbgpu_fail(ORB_ERR_INTERNAL, "umax differs from the IC_Angle disc table");
         e->geo = g;
         e->cur_w = w;
         e->cur_h = h;
