@@ -505,7 +505,7 @@ def bench_single_frame(pkg, synth, cpu_baseline_on, reps=50):
     return out
 
 
-def bench_c4(pkg, synth, dev, steps, n_frames=32, in_flight=2):
+def bench_c4(pkg, synth, dev, steps, n_frames=32, in_flight=3):
     """C4's per-GPU shard: 32 frames of 1280x720 (nFeatures 1000) per step, device-resident (the
     8-GPU run all-gathers the features of every shard; see the main line's N > 1 path), with
     `in_flight` extractor handles taking the steps in turn on their own streams (as the main line)."""
@@ -537,7 +537,7 @@ def bench_c4(pkg, synth, dev, steps, n_frames=32, in_flight=2):
             "ms_per_step": round(dt / reps, 4)}
 
 
-def bench_c4_strong(pkg, synth, world, rank, dev, steps, in_flight=2, n_global=256, n_distinct=32):
+def bench_c4_strong(pkg, synth, world, rank, dev, steps, in_flight=3, n_global=256, n_distinct=32):
     """C4 as strong scaling (BASELINE.json configs[3]): a fixed global batch of 256 1280x720 frames,
     256/N per rank; every step extracts each rank's shard and all-gathers all ranks' features
     (keypoints + descriptors + counts, RCCL over xGMI), overlapped with the next step's extraction
@@ -641,7 +641,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--frames", type=int, default=FRAMES)
-    ap.add_argument("--in-flight", type=int, default=2,
+    ap.add_argument("--in-flight", type=int, default=3,
                     help="extractor handles with a batch in flight, each on its own stream (consecutive steps "
                          "overlap: one batch's latency-bound quad-tree/describe tail runs beside the next "
                          "batch's pyramid/FAST); 1 = one batch at a time")

@@ -1,6 +1,6 @@
 """The benched workloads themselves, checked frame by frame against the oracle.
 
-bench.py times C2 as 64 frames (seeds 100..163) with two extractor handles taking the steps in
+bench.py times C2 as 64 frames (seeds 100..163) with three extractor handles taking the steps in
 turn on their own streams, so one batch's quad-tree/describe tail runs beside the next batch's
 pyramid/FAST, with the pyramid launch stamps on (profile "pyramid_launches").  The C4 line runs
 32 frames of 1280x720 per GPU the same way.  Both are reproduced here at full size and every frame
@@ -17,7 +17,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _run_in_flight(pkg, imgs, nf, w, h, lap, steps=4, handles=2, stamps=True):
+def _run_in_flight(pkg, imgs, nf, w, h, lap, steps=6, handles=3, stamps=True):
     """bench.py's timed loop: `handles` extractors on their own streams, step i on handle i % handles."""
     import torch
     b = imgs.shape[0]
@@ -59,7 +59,7 @@ def _check_against_oracle(pkg, oracle, frames, outs, nf, lap):
 
 
 def test_c2_as_benched(pkg, oracle, synth):
-    """C2 exactly as bench.py runs it: 64 frames (seeds 100..163), 2 handles in flight, 4 steps."""
+    """C2 exactly as bench.py runs it: 64 frames (seeds 100..163), 3 handles in flight, 6 steps."""
     import torch
     frames = np.stack([synth.polygon_frame(640, 480, seed=100 + i) for i in range(64)])
     outs = _run_in_flight(pkg, torch.from_numpy(frames).cuda(), 1000, 640, 480, (0, 1000))
@@ -68,7 +68,7 @@ def test_c2_as_benched(pkg, oracle, synth):
 
 
 def test_c4_shard_as_benched(pkg, oracle, synth):
-    """C4's per-GPU shard: 32 frames of 1280x720 (seeds 1000..1031), 2 handles in flight."""
+    """C4's per-GPU shard: 32 frames of 1280x720 (seeds 1000..1031), 3 handles in flight."""
     import torch
     frames = np.stack([synth.polygon_frame(1280, 720, seed=1000 + i) for i in range(32)])
     outs = _run_in_flight(pkg, torch.from_numpy(frames).cuda(), 1000, 1280, 720, (0, 1000), stamps=False)
