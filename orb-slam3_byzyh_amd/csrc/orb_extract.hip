@@ -378,24 +378,39 @@ __global__ __launch_bounds__(256) void k_debug_blur(const uint8_t* __restrict__ 
 // (a candidate survives iff its score beats the 8 neighbours' *thresholded* scores inside the
 // window) is then equivalent to: score >= t && score > score(n) for every neighbour n inside the
 // window's detectable region (neighbours below t can never beat a corner).
+// Packed: the 16 differences d = v - x go into 8 u16 pairs (circle points k, k+8), offset by 256
+// (values 1..511, so unsigned v_pk_min/max_u16 order them), and every sliding min / max step works on
+// both halves at once; wrapping past point 15 is the pair with its halves swapped.
+__device__ __forceinline__ u16x2 swap16(u16x2 a) { return __builtin_shufflevector(a, a, 1, 0); }
 __device__ __forceinline__ int fast_score(const uint8_t* __restrict__ p, const int (&off)[16]) {
     const int v = p[0];
-    int d[16];
+    const u16x2 vv = w16(v + 256, v + 256);
+    u16x2 D[8];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) d[k] = v - (int)p[off[k]];
-    int mn2[16], mx2[16];
+    for (int k = 0; k < 8; ++k)
+        D[k] = vv - __builtin_bit_cast(u16x2, (uint32_t)p[off[k]] | ((uint32_t)p[off[k + 8]] << 16));
+    auto at = [&](const u16x2 (&a)[8], int k) { return k < 8 ? a[k] : swap16(a[k - 8]); };
+    u16x2 mn2[8], mx2[8], mn4[8], mx4[8];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) { mn2[k] = min(d[k], d[(k + 1) & 15]); mx2[k] = max(d[k], d[(k + 1) & 15]); }
-    int mn4[16], mx4[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) { mn4[k] = min(mn2[k], mn2[(k + 2) & 15]); mx4[k] = max(mx2[k], mx2[(k + 2) & 15]); }
-    int best_dark = -1000, best_bright = 1000;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int mn8 = min(mn4[k], mn4[(k + 4) & 15]), mx8 = max(mx4[k], mx4[(k + 4) & 15]);
-        best_dark = max(best_dark, min(mn8, d[(k + 8) & 15]));
-        best_bright = min(best_bright, max(mx8, d[(k + 8) & 15]));
+    for (int k = 0; k < 8; ++k) {
+        mn2[k] = __builtin_elementwise_min(D[k], at(D, k + 1));
+        mx2[k] = __builtin_elementwise_max(D[k], at(D, k + 1));
     }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        mn4[k] = __builtin_elementwise_min(mn2[k], at(mn2, k + 2));
+        mx4[k] = __builtin_elementwise_max(mx2[k], at(mx2, k + 2));
+    }
+    // arc k (points k .. k+8) in the low half, arc k+8 in the high half
+    u16x2 dark = w16(0, 0), bright = w16(0xffff, 0xffff);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const u16x2 mn8 = __builtin_elementwise_min(mn4[k], at(mn4, k + 4));
+        const u16x2 mx8 = __builtin_elementwise_max(mx4[k], at(mx4, k + 4));
+        dark = __builtin_elementwise_max(dark, __builtin_elementwise_min(mn8, swap16(D[k])));
+        bright = __builtin_elementwise_min(bright, __builtin_elementwise_max(mx8, swap16(D[k])));
+    }
+    const int best_dark = (int)max(dark.x, dark.y) - 256, best_bright = (int)min(bright.x, bright.y) - 256;
     return max(best_dark, -best_bright) - 1;
 }
 
@@ -411,31 +426,6 @@ __device__ __forceinline__ uint32_t pack_key(int x, int y, int score) {
 __device__ __forceinline__ int key_x(uint32_t k) { return (int)((k >> 8) & 0xfff); }
 __device__ __forceinline__ int key_y(uint32_t k) { return (int)(k >> 20); }
 __device__ __forceinline__ int key_score(uint32_t k) { return (int)(k & 0xff); }
-
-// corner(t) for the pixel at p: a run of >= 9 contiguous circle pixels all brighter than v+t or all
-// darker than v-t (FAST_t<16>, OpenCV fast.cpp).  Bit k of the 16-bit masks = circle pixel k.
-__device__ __forceinline__ bool has_run9(unsigned m) {
-    const unsigned m2 = m | (m << 16);  // circular
-    unsigned r = m2 & (m2 >> 1);        // runs of 2
-    r &= r >> 2;                        // 4
-    r &= r >> 4;                        // 8
-    r &= m2 >> 8;                       // 9
-    return (r & 0xFFFFu) != 0;
-}
-
-__device__ __forceinline__ bool fast_corner(const uint8_t* __restrict__ p, const int (&off)[16], int t) {
-    const int v = p[0], hi = v + t, lo = v - t;
-    // masks in reverse circle order (a 9-run is a 9-run either way): each bit is the sign of a
-    // difference shifted in with one v_alignbit
-    unsigned bm = 0, dm = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int x = p[off[k]];
-        bm = __builtin_amdgcn_alignbit(bm, (unsigned)(hi - x), 31);  // x > hi
-        dm = __builtin_amdgcn_alignbit(dm, (unsigned)(x - lo), 31);  // x < lo
-    }
-    return has_run9(bm) || has_run9(dm);
-}
 
 // The body of one cell for a window row stride known at compile time (kWS > 0: circle, compass and
 // neighbour offsets become LDS immediates) or at run time (kWS == 0).
@@ -588,28 +578,28 @@ __device__ __forceinline__ void fast_cell(const KernelGeom& g, const CellDesc& C
     }
     wave_sync();
     FAST_STAMP(2);
-    // 1b. full 9-arc test at minTh on the filtered pixels; in-place compaction keeps row-major order
+    // 1b. exact score of the filtered pixels: score >= minTh <=> a 9-arc corner at minTh (see
+    //     fast_score), so one pass both tests and scores; corners are compacted in place (row-major
+    //     order kept: every lane reads its entry before any lane writes, and writes land below j0 + 64)
+    //     and their scores go to the map
     int ncand = 0;
     for (int j0 = 0; j0 < nlist; j0 += 64) {
         const int j = j0 + lane;
-        int idx = 0;
-        bool is_c = false;
+        int idx = 0, s = -1;
         if (j < nlist) {
             idx = cl[j];
-            is_c = fast_corner(win + idx, off, mint);
+            s = fast_score(win + idx, off);
         }
+        const bool is_c = s >= mint;
         const unsigned long long m = ballot(is_c);
-        if (is_c) cl[ncand + rank_in(m)] = (uint16_t)idx;
+        if (is_c) {
+            cl[ncand + rank_in(m)] = (uint16_t)idx;
+            sc[idx] = (uint8_t)min(s, 255);
+        }
         ncand += __popcll(m);
     }
     wave_sync();
     FAST_STAMP(3);
-    // 2. exact score of the candidates
-    for (int j = lane; j < ncand; j += 64) {
-        const int idx = cl[j];
-        sc[idx] = (uint8_t)min(max(fast_score(win + idx, off), 0), 255);
-    }
-    wave_sync();
     FAST_STAMP(4);
     // 3. iniTh first; minTh only if the cell has no corner at iniTh (src:1135-1148).  The local-maximum
     //    test does not depend on the threshold: its result (score + 1, or 0) is kept per candidate in
