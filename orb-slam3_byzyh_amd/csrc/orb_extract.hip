@@ -1569,11 +1569,17 @@ constexpr int kHP = 22, kHPW = 40;   // horizontal-sum row pairs (rows 2j, 2j+1)
 constexpr int kDescWords = kHP * kHPW;  // 3520 bytes per keypoint: the sums, and before them the patch
 static_assert(kDescWords >= (kPR + 1) * kPRW + 1, "patch + the last pair's odd row and over-read word fit the region");
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+constexpr f32x2 kRound2 = {12582912.0f, 12582912.0f};  // 1.5 * 2^23: v + it has ulp 1 (|v| < 2^22)
+constexpr int kRoundBits = 0x4B400000;                 // its bit pattern
+
 // Vertical 7-tap pass at one sample (r, c), |r|, |c| <= 18 from the keypoint: blurred row i = r + 18
 // reads sum rows i .. i+6, i.e. the 4 row pairs from i >> 1 (odd i: the first pair's high half).
 __device__ __forceinline__ int blur_sample(const uint32_t* __restrict__ H, int r, int c) {
-    const int i = r + 18;
-    const uint32_t* p = H + (i >> 1) * kHPW + (c + 18);
+    // (the masks are no-ops for |r|, |c| <= 18; they bound the range so the offsets stay 24-bit
+    // multiplies and the four reads fold into two ds_read2_b32)
+    const unsigned i = (unsigned)(r + 18) & 63u, cc = (unsigned)(c + 18) & 63u;
+    const uint32_t* p = H + __umul24(i >> 1, (unsigned)kHPW) + cc;
     const bool odd = (i & 1) != 0;
     uint32_t acc = 1u << 15;
     acc = __builtin_amdgcn_udot2(as_u16x2(p[0]), odd ? w16(0, 18) : w16(18, 34), acc, false);
@@ -1745,12 +1751,13 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
         const int pw4 = (int)pat[m];
         const float px0 = (float)((pw4 << 24) >> 24), py0 = (float)((pw4 << 16) >> 24);
         const float px1 = (float)((pw4 << 8) >> 24), py1 = (float)(pw4 >> 24);
-        const int r0 = (int)__builtin_rintf(__builtin_fmaf(px0, b, py0 * a));
-        const int c0 = (int)__builtin_rintf(__builtin_fmaf(px0, a, -(py0 * b)));
-        const int r1 = (int)__builtin_rintf(__builtin_fmaf(px1, b, py1 * a));
-        const int c1 = (int)__builtin_rintf(__builtin_fmaf(px1, a, -(py1 * b)));
-        t0[m] = blur_sample(P, r0, c0);  // |r|, |c| <= 18
-        t1[m] = blur_sample(P, r1, c1);
+        // (r, c) = (fma(x, b, y*a), fma(x, a, -(y*b))) as one packed multiply and one packed FMA
+        // (y*(-b) == -(y*b) exactly), rounded to nearest-even by adding 1.5 * 2^23 and reading the
+        // integer out of the mantissa (|r|, |c| <= 18)
+        const f32x2 rc0 = __builtin_elementwise_fma(f32x2{px0, px0}, f32x2{b, a}, f32x2{py0, py0} * f32x2{a, -b}) + kRound2;
+        const f32x2 rc1 = __builtin_elementwise_fma(f32x2{px1, px1}, f32x2{b, a}, f32x2{py1, py1} * f32x2{a, -b}) + kRound2;
+        t0[m] = blur_sample(P, __float_as_int(rc0.x) - kRoundBits, __float_as_int(rc0.y) - kRoundBits);
+        t1[m] = blur_sample(P, __float_as_int(rc1.x) - kRoundBits, __float_as_int(rc1.y) - kRoundBits);
     }
     uint32_t words[8];
 #pragma unroll
