@@ -43,6 +43,19 @@ struct Cand {
     int32_t dist;
 };
 
+// After a point's candidates are written: the wave (lanes over its list) records, for every usable
+// candidate keypoint (distance < 256, not already taken), the earliest observed point listing it
+// (`lister`, initialised to 0x7f7f7f7f).  k_resolve_init uses it to find the points whose answer no
+// earlier point can change.
+__device__ __forceinline__ void record_listers(int lane, int i, int n, int cap, const Cand* __restrict__ c_i,
+                                               const uint8_t* __restrict__ taken0, int32_t* __restrict__ lister) {
+    if (n > cap) return;  // overflow: the call is redone with a larger capacity
+    for (int k = lane; k < n; k += 64) {
+        const Cand c = c_i[k];
+        if (c.dist < 256 && !(taken0 && taken0[c.i2])) atomicMin(&lister[c.i2], i);
+    }
+}
+
 __device__ __forceinline__ int hamming(const uint4& a0, const uint4& a1, const uint4& b0, const uint4& b1) {
     return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
            __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
@@ -115,7 +128,8 @@ __global__ __launch_bounds__(64 * kCandWaves) void k_proj_candidates(const ProjP
                                                          const float* __restrict__ cur_ur, const uint4* __restrict__ cur_desc,
                                                          const int32_t* __restrict__ cell_off, const int32_t* __restrict__ cell_idx,
                                                          Cand* __restrict__ cands, int32_t* __restrict__ ncand,
-                                                         int32_t* __restrict__ overflow) {
+                                                         int32_t* __restrict__ overflow, const uint8_t* __restrict__ observed,
+                                                         int32_t* __restrict__ lister) {
     __shared__ int pre_s[kCandWaves][64], beg_s[kCandWaves][64];
     const ProjParams& P = *pp;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -169,6 +183,8 @@ __global__ __launch_bounds__(64 * kCandWaves) void k_proj_candidates(const ProjP
         ncand[i] = n;
         if (n > P.cap) atomicMax(overflow, n);
     }
+    __threadfence_block();  // the wave's own candidate stores, read back across lanes
+    if (observed[i]) record_listers(lane, i, n, P.cap, cands + (size_t)i * P.cap, nullptr, lister);
 }
 
 __device__ __forceinline__ int rot_bin(float a1, float a2) {
@@ -196,7 +212,9 @@ __global__ __launch_bounds__(64 * kCandWaves) void k_lmp_candidates(const LocalP
                                                         const float4* __restrict__ cur_kp, const float* __restrict__ cur_ur,
                                                         const uint4* __restrict__ cur_desc, const int32_t* __restrict__ cell_off,
                                                         const int32_t* __restrict__ cell_idx, Cand* __restrict__ cands,
-                                                        int32_t* __restrict__ ncand, int32_t* __restrict__ overflow) {
+                                                        int32_t* __restrict__ ncand, int32_t* __restrict__ overflow,
+                                                        const uint8_t* __restrict__ observed, const uint8_t* __restrict__ taken0,
+                                                        int32_t* __restrict__ lister) {
     __shared__ int pre_s[kCandWaves][64], beg_s[kCandWaves][64];
     const LocalParams& P = *pp;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -238,6 +256,8 @@ __global__ __launch_bounds__(64 * kCandWaves) void k_lmp_candidates(const LocalP
         ncand[i] = n;
         if (n > P.cap) atomicMax(overflow, n);
     }
+    __threadfence_block();  // the wave's own candidate stores, read back across lanes
+    if (observed[i]) record_listers(lane, i, n, P.cap, cands + (size_t)i * P.cap, taken0, lister);
 }
 
 // ---- the in-order assignment, resolved by parallel fixed-point rounds ----------------------------
@@ -263,6 +283,7 @@ __global__ __launch_bounds__(64 * kCandWaves) void k_lmp_candidates(const LocalP
 // reference's update rules (src:126-142, :2057-2061) are the lexicographic (distance, order) minima.
 constexpr int kResolveThreads = 1024, kResolveLdsKeypoints = 16384;
 constexpr unsigned long long kNone = ~0ull;
+constexpr int kTop = 8;  // best usable candidates kept per point for the rounds
 
 struct ResolveArgs {
     int n_pts, n_cur, cap;
@@ -279,38 +300,184 @@ struct ResolveArgs {
     int32_t* st;               // per point: the current answer, -1 no match, j >= 0 keypoint j
     int lds_keypoints;         // 1: claimMin in LDS (dynamic, 4 B per keypoint)
     int32_t* claimMin;         // per keypoint (when not in LDS)
+    const int32_t* lister;     // per keypoint: the first observed point listing it (candidate kernels)
+    int32_t* fixed;            // per keypoint: the smallest final (unaffected) observed claimant (0x7f.. none)
+    int32_t* work;             // the points whose answer can change (the rounds' list), count in out_n[2]
+    int4* top;                 // per point: its kTop best usable candidates as (dist, i2) pairs, by (dist, order)
+    int32_t* nusable;          // per point: its usable candidate count
     int32_t* last;             // per keypoint
     int32_t* removed;          // per keypoint
     int32_t* mp;               // out: per keypoint
     int32_t* out_n;            // out: [0] count, [1] rounds
 };
 
-// point i's answer given claimMin (candidates claimed by an earlier point excluded)
-__device__ __forceinline__ int resolve_point(const ResolveArgs& a, const int32_t* claimMin, int i) {
+// a candidate resolve_point can take (the lister pass counts exactly these)
+__device__ __forceinline__ bool usable(const ResolveArgs& a, const Cand& c) {
+    return c.dist < 256 && !(a.taken0 && a.taken0[c.i2]);
+}
+
+// Visit point i's usable candidates in list order, fn(candidate, position).  The list is read 8
+// entries at a time (and their taken0 bytes 8 at a time), so a thread keeps 8 loads in flight instead
+// of one dependent round trip per candidate.
+template <class Fn>
+__device__ __forceinline__ void for_each_usable(const ResolveArgs& a, int i, Fn fn) {
     const Cand* C = a.cands + (size_t)i * a.cap;
-    unsigned long long m1 = kNone, m2 = kNone;
-    for (int k = 0, n = a.ncand[i]; k < n; ++k) {
-        const Cand c = C[k];
-        if (c.dist >= 256) continue;  // never below the initial bestDist / bestDist2 of 256
-        if (a.taken0 && a.taken0[c.i2]) continue;
-        if (claimMin[c.i2] < i) continue;
-        const unsigned long long key = ((unsigned long long)c.dist << 32) | (unsigned)k;
-        if (key < m1) {
-            m2 = m1;
-            m1 = key;
-        } else if (key < m2) {
-            m2 = key;
-        }
+    const int n = a.ncand[i];
+    for (int k0 = 0; k0 < n; k0 += 8) {
+        Cand cs[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) cs[u] = k0 + u < n ? C[k0 + u] : Cand{0, 256};
+        bool tk[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) tk[u] = a.taken0 && cs[u].dist < 256 && a.taken0[cs[u].i2];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (cs[u].dist < 256 && !tk[u]) fn(cs[u], k0 + u);  // dist >= 256: never below the initial 256
     }
+}
+
+// point i's answer given claimMin (candidates claimed by an earlier point excluded): the first and
+// second minimum of (distance, list position), the reference's update order
+__device__ __forceinline__ int resolve_point(const ResolveArgs& a, const int32_t* claimMin, int i) {
+    unsigned long long m1 = kNone, m2 = kNone;
+    int j1 = -1, j2 = -1;
+    for_each_usable(a, i, [&](const Cand& c, int k) {  // (selects, no branches: the state stays in registers)
+        const bool ok = claimMin[c.i2] >= i;
+        const unsigned long long key = ((unsigned long long)c.dist << 32) | (unsigned)k;
+        const bool lt1 = ok && key < m1, lt2 = ok && key < m2;
+        m2 = lt1 ? m1 : (lt2 ? key : m2);
+        j2 = lt1 ? j1 : (lt2 ? c.i2 : j2);
+        m1 = lt1 ? key : m1;
+        j1 = lt1 ? c.i2 : j1;
+    });
     if (m1 == kNone) return -1;
-    const int d1 = (int)(m1 >> 32), j1 = C[(int)(m1 & 0xffffffffu)].i2;
+    const int d1 = (int)(m1 >> 32);
     if (d1 > kThHigh) return -1;
     if (a.local) {  // src:148-155
         const int l1 = __float_as_int(a.cur_kp[j1].w);
-        const int l2 = m2 != kNone ? __float_as_int(a.cur_kp[C[(int)(m2 & 0xffffffffu)].i2].w) : -1;
+        const int l2 = m2 != kNone ? __float_as_int(a.cur_kp[j2].w) : -1;
         const int d2 = m2 != kNone ? (int)(m2 >> 32) : 256;
         if (l1 == l2 && (float)d1 > a.nnratio * (float)d2) return -1;
     }
+    return j1;
+}
+
+// The answer rules (src:145-167 / :2064-2068) given the first and second unclaimed candidates.
+__device__ __forceinline__ int decide(const ResolveArgs& a, int d1, int j1, int d2, int j2) {
+    if (j1 < 0 || d1 > kThHigh) return -1;
+    if (a.local) {  // src:148-155
+        const int l1 = __float_as_int(a.cur_kp[j1].w);
+        const int l2 = j2 >= 0 ? __float_as_int(a.cur_kp[j2].w) : -1;
+        if (l1 == l2 && (float)d1 > a.nnratio * (float)(j2 >= 0 ? d2 : 256)) return -1;
+    }
+    return j1;
+}
+
+// Points that cannot be affected are taken out of the rounds: point i can only lose a candidate j to
+// an observed point k < i that has j among its usable candidates, so if every usable candidate of i
+// has no such earlier lister, i's unconstrained answer is final, and its claim is fixed.
+// k_resolve_init (one thread per point, over the whole chip): the unconstrained answer, the point's
+// kTop best usable candidates in (distance, order), the classification, the work list and the fixed
+// claims.  k_resolve_rounds (one workgroup) then iterates only the work list, each point re-deciding
+// from its kTop best (a full scan only when too many of them are claimed).
+__global__ __launch_bounds__(256) void k_resolve_init(ResolveArgs a) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n_pts || *a.overflow > a.cap) return;
+    unsigned long long t[kTop];
+    int ti[kTop];
+#pragma unroll
+    for (int q = 0; q < kTop; ++q) { t[q] = kNone; ti[q] = -1; }
+    int nu = 0;
+    bool affected = false;
+    for_each_usable(a, i, [&](const Cand& c, int k) {
+        ++nu;
+        affected |= a.lister[c.i2] < i;
+        unsigned long long key = ((unsigned long long)c.dist << 32) | (unsigned)k;
+        int j = c.i2;
+#pragma unroll
+        for (int q = 0; q < kTop; ++q) {  // insertion into the sorted kTop (selects only)
+            const bool lt = key < t[q];
+            const unsigned long long tk = t[q];
+            const int tj = ti[q];
+            t[q] = lt ? key : tk;
+            ti[q] = lt ? j : tj;
+            key = lt ? tk : key;
+            j = lt ? tj : j;
+        }
+    });
+    const int st = decide(a, (int)(t[0] >> 32), ti[0], (int)(t[1] >> 32), ti[1]);
+    a.st[i] = st;
+#pragma unroll
+    for (int q = 0; q < kTop; q += 2)
+        a.top[(size_t)i * (kTop / 2) + q / 2] = make_int4((int)(t[q] >> 32), ti[q], (int)(t[q + 1] >> 32), ti[q + 1]);
+    a.nusable[i] = nu;
+    if (affected) a.work[atomicAdd(&a.out_n[2], 1)] = i;
+    else if (st >= 0 && a.observed[i]) atomicMin(&a.fixed[st], i);
+}
+
+// point i's answer in a round, from its kTop best (claims by earlier points excluded)
+__device__ __forceinline__ int resolve_top(const ResolveArgs& a, const int32_t* claimMin, int i) {
+    int d1 = 0, j1 = -1, d2 = 0, j2 = -1, found = 0;
+#pragma unroll
+    for (int q = 0; q < kTop; q += 2) {
+        const int4 e = a.top[(size_t)i * (kTop / 2) + q / 2];
+        const int d[2] = {e.x, e.z}, j[2] = {e.y, e.w};
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            if (j[u] < 0 || claimMin[j[u]] < i) continue;
+            if (found == 0) { d1 = d[u]; j1 = j[u]; }
+            else if (found == 1) { d2 = d[u]; j2 = j[u]; }
+            ++found;
+        }
+    }
+    const int need = a.local ? 2 : 1;
+    if (found < need && a.nusable[i] > kTop) return resolve_point(a, claimMin, i);
+    return decide(a, d1, j1, d2, j2);
+}
+
+// A work point's round state in registers: its kTop best (keypoint, distance, level), usable count,
+// index, observed flag and current answer; the rounds then touch only LDS.
+struct WorkPoint {
+    int i, st, nu, obs;
+    uint32_t e[kTop];  // keypoint (16 bits) | distance << 16 (8 bits) | (level + 1) << 24; 0xffffffff: none
+};
+constexpr int kWorkPerThread = 2;
+
+__device__ __forceinline__ void load_work(const ResolveArgs& a, int i, WorkPoint& p) {
+    p.i = i;
+    p.st = a.st[i];
+    p.nu = a.nusable[i];
+    p.obs = a.observed[i];
+    int d[kTop], j[kTop];
+#pragma unroll
+    for (int q = 0; q < kTop; q += 2) {
+        const int4 t = a.top[(size_t)i * (kTop / 2) + q / 2];
+        d[q] = t.x; j[q] = t.y; d[q + 1] = t.z; j[q + 1] = t.w;
+    }
+#pragma unroll
+    for (int q = 0; q < kTop; ++q) {  // octaves are 0 .. 11, distances < 256, keypoints < 65536
+        const int l1 = (a.local && j[q] >= 0) ? __float_as_int(a.cur_kp[j[q]].w) + 1 : 0;
+        p.e[q] = j[q] < 0 ? 0xffffffffu : (uint32_t)j[q] | (uint32_t)d[q] << 16 | (uint32_t)l1 << 24;
+    }
+}
+
+// resolve_top on a register-resident work point (same rules; the full scan when its kTop best run out)
+__device__ __forceinline__ int resolve_reg(const ResolveArgs& a, const int32_t* claimMin, const WorkPoint& p) {
+    uint32_t e1 = 0xffffffffu, e2 = 256u << 16;  // (e2 default: distance 256, level -1)
+    int found = 0;
+#pragma unroll
+    for (int q = 0; q < kTop; ++q) {
+        const bool ok = p.e[q] != 0xffffffffu && claimMin[p.e[q] & 0xffffu] >= p.i;
+        if (ok && found == 0) e1 = p.e[q];
+        else if (ok && found == 1) e2 = p.e[q];
+        found += ok ? 1 : 0;
+    }
+    if (found < (a.local ? 2 : 1) && p.nu > kTop) return resolve_point(a, claimMin, p.i);
+    if (found == 0) return -1;
+    const int j1 = (int)(e1 & 0xffffu), d1 = (int)((e1 >> 16) & 0xffu), l1 = (int)(e1 >> 24) - 1;
+    const int d2 = found > 1 ? (int)((e2 >> 16) & 0xffu) : 256, l2 = found > 1 ? (int)(e2 >> 24) - 1 : -1;
+    if (d1 > kThHigh) return -1;
+    if (a.local && l1 == l2 && (float)d1 > a.nnratio * (float)d2) return -1;  // src:148-155
     return j1;
 }
 
@@ -324,35 +491,68 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_rounds(ResolveArgs 
         return;
     }
     for (int j = tid; j < a.n_cur; j += kResolveThreads) {
-        claimMin[j] = INT32_MAX;
         a.last[j] = -1;
         a.removed[j] = 0;
     }
     if (tid < kHisto) hist[tid] = 0;
     if (tid < 2) cnt[tid] = 0;
-    __syncthreads();
-    // round 0: no claims (the unconstrained answers)
-    for (int i = tid; i < a.n_pts; i += kResolveThreads) a.st[i] = a.ncand[i] > 0 ? resolve_point(a, claimMin, i) : -1;
+    const int nw = a.out_n[2];
     int rounds = 1;
-    for (;; ++rounds) {
-        __syncthreads();
-        for (int j = tid; j < a.n_cur; j += kResolveThreads) claimMin[j] = INT32_MAX;
-        __syncthreads();
-        for (int i = tid; i < a.n_pts; i += kResolveThreads) {
-            const int j = a.st[i];
-            if (j >= 0 && a.observed[i]) atomicMin(&claimMin[j], i);
+    if (nw <= kWorkPerThread * kResolveThreads && a.n_cur <= 65536) {
+        // the usual case: every work point in registers, the fixed claims in LDS next to claimMin
+        int32_t* const fixedL = a.lds_keypoints ? kp_lds + a.n_cur : a.fixed;
+        WorkPoint wp[kWorkPerThread];
+#pragma unroll
+        for (int q = 0; q < kWorkPerThread; ++q) {
+            const int w = tid + q * kResolveThreads;
+            wp[q].i = -1;
+            if (w < nw) load_work(a, a.work[w], wp[q]);
         }
-        __syncthreads();
-        int changed = 0;
-        for (int i = tid; i < a.n_pts; i += kResolveThreads) {
-            if (a.ncand[i] == 0) continue;
-            const int r = resolve_point(a, claimMin, i);
-            if (r != a.st[i]) {
-                a.st[i] = r;
-                ++changed;
+        if (a.lds_keypoints)
+            for (int j = tid; j < a.n_cur; j += kResolveThreads) fixedL[j] = a.fixed[j];
+        for (;; ++rounds) {
+            __syncthreads();
+            for (int j = tid; j < a.n_cur; j += kResolveThreads) claimMin[j] = fixedL[j];
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < kWorkPerThread; ++q)
+                if (wp[q].i >= 0 && wp[q].st >= 0 && wp[q].obs) atomicMin(&claimMin[wp[q].st], wp[q].i);
+            __syncthreads();
+            int changed = 0;
+#pragma unroll
+            for (int q = 0; q < kWorkPerThread; ++q) {
+                if (wp[q].i < 0) continue;
+                const int r = resolve_reg(a, claimMin, wp[q]);
+                changed += r != wp[q].st;
+                wp[q].st = r;
             }
+            if (__syncthreads_count(changed) == 0 || rounds > a.n_pts) break;
         }
-        if (__syncthreads_count(changed) == 0 || rounds > a.n_pts) break;
+#pragma unroll
+        for (int q = 0; q < kWorkPerThread; ++q)
+            if (wp[q].i >= 0) a.st[wp[q].i] = wp[q].st;
+        __syncthreads();  // (global st: visible to the workgroup's results pass below)
+    } else {
+        for (;; ++rounds) {
+            __syncthreads();
+            for (int j = tid; j < a.n_cur; j += kResolveThreads) claimMin[j] = a.fixed[j];
+            __syncthreads();
+            for (int w = tid; w < nw; w += kResolveThreads) {
+                const int i = a.work[w], j = a.st[i];
+                if (j >= 0 && a.observed[i]) atomicMin(&claimMin[j], i);
+            }
+            __syncthreads();
+            int changed = 0;
+            for (int w = tid; w < nw; w += kResolveThreads) {
+                const int i = a.work[w];
+                const int r = resolve_top(a, claimMin, i);
+                if (r != a.st[i]) {
+                    a.st[i] = r;
+                    ++changed;
+                }
+            }
+            if (__syncthreads_count(changed) == 0 || rounds > a.n_pts) break;
+        }
     }
     // results
     int nsucc = 0;
@@ -396,10 +596,18 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_rounds(ResolveArgs 
     if (tid == 0) {
         a.out_n[0] = cnt[0] - cnt[1];
         a.out_n[1] = rounds;
+        a.out_n[2] = nw;
     }
 }
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// k_resolve_rounds keeps claimMin and the fixed claims in dynamic LDS (8 B per keypoint, up to 128 KB)
+bool resolve_lds_ready() {
+    static const bool ok = hipFuncSetAttribute((const void*)k_resolve_rounds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               8 * kResolveLdsKeypoints) == hipSuccess;
+    return ok;
+}
 
 }  // namespace
 
@@ -482,7 +690,9 @@ extern "C" int orb_search_by_projection_frame(orb_matcher_t m, const orb_frame_v
         const size_t o_ovf = off; off = align256(off + 16);
         const size_t o_mp = off; off = align256(off + (size_t)std::max(n, 1) * 4);
         const size_t o_st = off; off = align256(off + (size_t)std::max(nl, 1) * 4);
-        const size_t o_kw = off; off = align256(off + (size_t)std::max(n, 1) * 16);  // claimMin, last, removed
+        const size_t o_kw = off; off = align256(off + (size_t)std::max(n, 1) * 20);  // claimMin, last, removed | lister, fixed
+        const size_t o_wl = off; off = align256(off + (size_t)std::max(nl, 1) * 4);  // resolve work list
+        const size_t o_top = off; off = align256(off + (size_t)std::max(nl, 1) * 68);  // 8 best (64 B) + usable count
         if (int rc = orbgpu_matcher_reserve(m, off, &d, &h, &s, &check_ori)) return rc;
         P.check_ori = check_ori;
         memcpy(h + o_p, &P, sizeof(P));
@@ -510,13 +720,15 @@ extern "C" int orb_search_by_projection_frame(orb_matcher_t m, const orb_frame_v
             la[i] = last->kps_un[i].angle;
         }
         bool ok = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s) == hipSuccess;
-        ok = ok && hipMemsetAsync(d + o_ovf, 0, 16, s) == hipSuccess;
+        ok = ok && hipMemsetAsync(d + o_ovf, 0, 16, s) == hipSuccess &&
+             hipMemsetAsync(d + o_kw + (size_t)std::max(n, 1) * 12, 0x7f, (size_t)std::max(n, 1) * 8, s) == hipSuccess;  // lister, fixed
         if (ok && nl > 0)
             hipLaunchKernelGGL(k_proj_candidates, dim3((nl + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s, (const ProjParams*)(d + o_p),
                                (const uint8_t*)(d + o_va), (const float*)(d + o_xyz), (const uint4*)(d + o_md),
                                (const int32_t*)(d + o_lo), (const float4*)(d + o_kp), (const float*)(d + o_ur),
                                (const uint4*)(d + o_cd), (const int32_t*)(d + o_co), (const int32_t*)(d + o_ci),
-                               (Cand*)(d + o_cand), (int32_t*)(d + o_nc), (int32_t*)(d + o_ovf));
+                               (Cand*)(d + o_cand), (int32_t*)(d + o_nc), (int32_t*)(d + o_ovf), (const uint8_t*)(d + o_ob),
+                               (int32_t*)(d + o_kw + (size_t)std::max(n, 1) * 12));
         ResolveArgs ra{};
         ra.n_pts = nl; ra.n_cur = n; ra.cap = P.cap; ra.local = 0; ra.check_ori = check_ori; ra.nnratio = 0.f;
         ra.cands = (const Cand*)(d + o_cand); ra.ncand = (const int32_t*)(d + o_nc); ra.observed = (const uint8_t*)(d + o_ob);
@@ -524,13 +736,17 @@ extern "C" int orb_search_by_projection_frame(orb_matcher_t m, const orb_frame_v
         ra.overflow = (const int32_t*)(d + o_ovf); ra.st = (int32_t*)(d + o_st);
         int32_t* kw = (int32_t*)(d + o_kw);
         const size_t nk = (size_t)std::max(n, 1);
-        ra.claimMin = kw; ra.last = kw + nk; ra.removed = kw + 2 * nk;
-        ra.lds_keypoints = n <= kResolveLdsKeypoints ? 1 : 0;
+        ra.claimMin = kw; ra.last = kw + nk; ra.removed = kw + 2 * nk; ra.lister = kw + 3 * nk; ra.fixed = kw + 4 * nk;
+        ra.work = (int32_t*)(d + o_wl);
+        ra.top = (int4*)(d + o_top); ra.nusable = (int32_t*)(d + o_top + (size_t)std::max(nl, 1) * 64);
+        ra.lds_keypoints = n <= kResolveLdsKeypoints && resolve_lds_ready() ? 1 : 0;
         ra.mp = (int32_t*)(d + o_mp); ra.out_n = (int32_t*)(d + o_ovf) + 1;
         // candidates and the rounds back to back, one synchronisation; an overflowing candidate pass
         // (a point with more candidates than the capacity) makes the resolve a no-op and is re-run
-        if (ok)
-            hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 4 * (size_t)n : 0, s, ra);
+        if (ok) {
+            if (ra.n_pts > 0) hipLaunchKernelGGL(k_resolve_init, dim3((ra.n_pts + 255) / 256), dim3(256), 0, s, ra);
+            hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 8 * (size_t)n : 0, s, ra);
+        }
         ok = ok && hipGetLastError() == hipSuccess &&
              hipMemcpyAsync(h + o_mp, d + o_mp, (size_t)std::max(n, 1) * 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
              hipMemcpyAsync(h + o_ovf, d + o_ovf, 16, hipMemcpyDeviceToHost, s) == hipSuccess &&
@@ -609,7 +825,9 @@ extern "C" int orb_search_by_projection_local(orb_matcher_t m, const orb_frame_v
         const size_t o_ovf = off; off = align256(off + 16);
         const size_t o_m = off; off = align256(off + (size_t)std::max(n, 1) * 4);
         const size_t o_st = off; off = align256(off + (size_t)std::max(np, 1) * 4);
-        const size_t o_kw = off; off = align256(off + (size_t)std::max(n, 1) * 16);  // claimMin, last, removed
+        const size_t o_kw = off; off = align256(off + (size_t)std::max(n, 1) * 20);  // claimMin, last, removed | lister, fixed
+        const size_t o_wl = off; off = align256(off + (size_t)std::max(np, 1) * 4);  // resolve work list
+        const size_t o_top = off; off = align256(off + (size_t)std::max(np, 1) * 68);  // 8 best (64 B) + usable count
         if (int rc = orbgpu_matcher_reserve(m, off, &d, &h, &s, &check_ori)) return rc;
         P.nnratio = orbgpu_matcher_nnratio(m);
         memcpy(h + o_p, &P, sizeof(P));
@@ -636,14 +854,16 @@ extern "C" int orb_search_by_projection_local(orb_matcher_t m, const orb_frame_v
             memcpy(h + o_md, pts->desc, (size_t)np * 32);
         }
         bool ok = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s) == hipSuccess &&
-                  hipMemsetAsync(d + o_ovf, 0, 16, s) == hipSuccess;
+                  hipMemsetAsync(d + o_ovf, 0, 16, s) == hipSuccess &&
+                  hipMemsetAsync(d + o_kw + (size_t)std::max(n, 1) * 12, 0x7f, (size_t)std::max(n, 1) * 8, s) == hipSuccess;  // lister, fixed
         if (ok && np > 0)
             hipLaunchKernelGGL(k_lmp_candidates, dim3((np + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s, (const LocalParams*)(d + o_p),
                                (const uint8_t*)(d + o_iv), (const uint8_t*)(d + o_bd), (const float*)(d + o_pj),
                                (const float*)(d + o_vc), (const float*)(d + o_dp), (const int32_t*)(d + o_lv),
                                (const uint4*)(d + o_md), (const float4*)(d + o_kp), (const float*)(d + o_ur),
                                (const uint4*)(d + o_cd), (const int32_t*)(d + o_co), (const int32_t*)(d + o_ci),
-                               (Cand*)(d + o_cand), (int32_t*)(d + o_nc), (int32_t*)(d + o_ovf));
+                               (Cand*)(d + o_cand), (int32_t*)(d + o_nc), (int32_t*)(d + o_ovf), (const uint8_t*)(d + o_ob),
+                               frame_taken ? (const uint8_t*)(d + o_tk) : nullptr, (int32_t*)(d + o_kw + (size_t)std::max(n, 1) * 12));
         ResolveArgs ra{};
         ra.n_pts = np; ra.n_cur = n; ra.cap = P.cap; ra.local = 1; ra.check_ori = 0; ra.nnratio = P.nnratio;
         ra.cands = (const Cand*)(d + o_cand); ra.ncand = (const int32_t*)(d + o_nc); ra.observed = (const uint8_t*)(d + o_ob);
@@ -651,11 +871,15 @@ extern "C" int orb_search_by_projection_local(orb_matcher_t m, const orb_frame_v
         ra.last_angle = nullptr; ra.overflow = (const int32_t*)(d + o_ovf); ra.st = (int32_t*)(d + o_st);
         int32_t* kw = (int32_t*)(d + o_kw);
         const size_t nk = (size_t)std::max(n, 1);
-        ra.claimMin = kw; ra.last = kw + nk; ra.removed = kw + 2 * nk;
-        ra.lds_keypoints = n <= kResolveLdsKeypoints ? 1 : 0;
+        ra.claimMin = kw; ra.last = kw + nk; ra.removed = kw + 2 * nk; ra.lister = kw + 3 * nk; ra.fixed = kw + 4 * nk;
+        ra.work = (int32_t*)(d + o_wl);
+        ra.top = (int4*)(d + o_top); ra.nusable = (int32_t*)(d + o_top + (size_t)std::max(np, 1) * 64);
+        ra.lds_keypoints = n <= kResolveLdsKeypoints && resolve_lds_ready() ? 1 : 0;
         ra.mp = (int32_t*)(d + o_m); ra.out_n = (int32_t*)(d + o_ovf) + 1;
-        if (ok)
-            hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 4 * (size_t)n : 0, s, ra);
+        if (ok) {
+            if (ra.n_pts > 0) hipLaunchKernelGGL(k_resolve_init, dim3((ra.n_pts + 255) / 256), dim3(256), 0, s, ra);
+            hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 8 * (size_t)n : 0, s, ra);
+        }
         ok = ok && hipGetLastError() == hipSuccess &&
              hipMemcpyAsync(h + o_m, d + o_m, (size_t)std::max(n, 1) * 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
              hipMemcpyAsync(h + o_ovf, d + o_ovf, 16, hipMemcpyDeviceToHost, s) == hipSuccess &&

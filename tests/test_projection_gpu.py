@@ -52,3 +52,24 @@ def test_search_by_projection_local_parity(pkg, oracle, synth, seed, th, far, ra
     assert n == rn, f"{n} vs oracle {rn}"
     assert np.array_equal(got, exp), f"{int((got != exp).sum())} differing assignments"
     assert n > 50
+
+
+def test_search_by_projection_large_paths(pkg, oracle, synth):
+    """The resolve's memory-resident paths: more than 2,048 local map points whose answer an earlier
+    point can change (the rounds read their state from memory instead of registers), and a current
+    frame of more than 16,384 keypoints (claims in global memory instead of LDS)."""
+    cur, _ = synth.tracking_pair(seed=61)
+    F = pkg.Frame(**cur)
+    P = pkg.LocalMapPoints(**synth.local_map_points(cur, n_points=9000, seed=161))
+    taken = np.zeros(F.N, np.uint8)
+    m = pkg.ORBmatcher(0.8, True)
+    n, got = m.SearchByProjection(F, P, 10, False, 10.0, taken)
+    rn, exp = oracle.search_by_projection_local(F, P, 10, False, 10.0, 0.8, taken)
+    assert n == rn and np.array_equal(got, exp), f"{n} vs {rn}, {int((got != exp).sum())} differing"
+    cur, last = synth.tracking_pair(n_points=1500, clutter=17000, seed=62)
+    C, L = pkg.Frame(**cur), pkg.Frame(**last)
+    assert C.N > 16384
+    mf = pkg.ORBmatcher(0.9, True)
+    n, got = mf.SearchByProjectionFrame(C, L, 7, False)
+    rn, exp = oracle.search_by_projection_frame(C, L, 7, False, True)
+    assert n == rn and np.array_equal(got, exp), f"{n} vs {rn}, {int((got != exp).sum())} differing"
