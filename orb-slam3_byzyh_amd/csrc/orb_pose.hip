@@ -35,7 +35,7 @@ namespace {
 
 constexpr int kPT = 256;               // threads per frame
 constexpr int kPW = kPT / 64;          // waves
-constexpr int kNV = 28;                // reduced values: H upper (21), b (6), chi2
+constexpr int kEdgeSlots = 2;          // edges per thread kept in registers (512 per frame)
 
 static_assert(sizeof(orb_pose_edge_t) == 56, "pose edge layout");
 
@@ -80,34 +80,80 @@ __device__ __forceinline__ double robust_rho(const EdgeEval& ev, bool robust, Hu
     return rho0;
 }
 
-// fixed-order workgroup sum of N doubles per thread; result in red[0..N) for every thread
-template <int N>
-__device__ __forceinline__ void block_reduce(double (&v)[N], double* red) {
+// Partner exchanges of a double for the transposed butterfly below.  Pairs differ in lane bit M:
+// M = 32 ds_bpermute, 16 ds_swizzle (xor 16 in each half), 8 DPP row_mirror (i <-> 15 - i), 4 DPP
+// row_half_mirror (i <-> 7 - i), 2 / 1 DPP quad_perm; only the last four stay in the VALU.
+template <int M>
+__device__ __forceinline__ double xchg(double v) {
+    if constexpr (M == 32) {
+        return __shfl_xor(v, 32, 64);
+    } else {
+        const int2 h = __builtin_bit_cast(int2, v);
+        int2 r;
+        if constexpr (M == 16) {
+            r.x = __builtin_amdgcn_ds_swizzle(h.x, 0x401F);
+            r.y = __builtin_amdgcn_ds_swizzle(h.y, 0x401F);
+        } else {
+            constexpr int ctl = M == 8 ? 0x140 : M == 4 ? 0x141 : M == 2 ? 0x4E : 0xB1;
+            r.x = __builtin_amdgcn_update_dpp(0, h.x, ctl, 0xF, 0xF, false);
+            r.y = __builtin_amdgcn_update_dpp(0, h.y, ctl, 0xF, 0xF, false);
+        }
+        return __builtin_bit_cast(double, r);
+    }
+}
+// One transposed butterfly step: lanes with bit M set keep values [C, 2C) and send [0, C), their
+// partners the reverse, so the partner's half arrives with one exchange per kept value.  Partners
+// hold the same value set before each step (they agree in every lane bit above M).
+template <int C, int M>
+__device__ __forceinline__ void tb_step(double (&v)[32], int lane) {
+    const bool up = (lane & M) != 0;
+#pragma unroll
+    for (int i = 0; i < C; ++i) {
+        const double send = up ? v[i] : v[i + C];
+        const double keep = up ? v[i + C] : v[i];
+        v[i] = keep + xchg<M>(send);
+    }
+}
+// Wave sums of 32 per-lane doubles in 32 exchanges (16 + 8 + 4 + 2 + 1, then the pair) instead of
+// 32 x 6 shuffles: afterwards v[0] of lanes 2k and 2k + 1 is the wave's sum of value k, also stored
+// to part[wave * 32 + k].  The workgroup total of value k is ((p0 + p1) + p2) + p3 over the waves.
+__device__ __forceinline__ void wave_partials32(double (&v)[32], double* part) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    tb_step<16, 32>(v, lane);
+    tb_step<8, 16>(v, lane);
+    tb_step<4, 8>(v, lane);
+    tb_step<2, 4>(v, lane);
+    tb_step<1, 2>(v, lane);
+    v[0] += xchg<1>(v[0]);
+    if (!(lane & 1)) part[wv * 32 + (lane >> 1)] = v[0];
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const int2 h = __builtin_bit_cast(int2, v);
+    int2 r;
+    r.x = __builtin_amdgcn_readlane(h.x, l);
+    r.y = __builtin_amdgcn_readlane(h.y, l);
+    return __builtin_bit_cast(double, r);
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
-    for (int k = 0; k < N; ++k)
-        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
-    __syncthreads();  // red may still be read from the previous reduction
-    if (lane < N) {
-        double mine = 0;
-#pragma unroll
-        for (int k = 0; k < N; ++k) mine = lane == k ? v[k] : mine;
-        red[wv * N + lane] = mine;
-    }
-    __syncthreads();
-    if (threadIdx.x < N) {
-        double s = 0;
-        for (int w = 0; w < kPW; ++w) s += red[w * N + threadIdx.x];
-        red[kPW * N + threadIdx.x] = s;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < N; ++k) v[k] = red[kPW * N + k];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
 }
 
-// LDL^T of the 6x6 symmetric matrix (LinearSolverDense: Eigen::LDLT; same solution up to rounding)
-__device__ bool ldlt6(const double A[36], const double b[6], double x[6]) {
-    double L[36] = {0}, d[6];
+// LDL^T of the 6x6 symmetric matrix given as its upper triangle row by row (LinearSolverDense:
+// Eigen::LDLT; the same solution up to rounding); one reciprocal per pivot
+__device__ __forceinline__ bool ldlt6(const double (&U)[21], double lambda, const double (&b)[6], double (&x)[6]) {
+    double A[36];
+    {
+        int k = 0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int j = i; j < 6; ++j) { A[6 * i + j] = A[6 * j + i] = U[k]; ++k; }
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) A[7 * i] += lambda;
+    double L[36] = {0}, d[6], id[6];
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
         double dj = A[7 * j];
@@ -115,12 +161,13 @@ __device__ bool ldlt6(const double A[36], const double b[6], double x[6]) {
         for (int k = 0; k < j; ++k) dj -= L[6 * j + k] * L[6 * j + k] * d[k];
         if (!(dj > 0)) return false;  // LDLT::isPositive (the damped system is SPD unless degenerate)
         d[j] = dj;
+        id[j] = 1.0 / dj;
 #pragma unroll
         for (int i = j + 1; i < 6; ++i) {
             double v = A[6 * j + i];
 #pragma unroll
             for (int k = 0; k < j; ++k) v -= L[6 * i + k] * L[6 * j + k] * d[k];
-            L[6 * i + j] = v / dj;
+            L[6 * i + j] = v * id[j];
         }
     }
 #pragma unroll
@@ -130,7 +177,7 @@ __device__ bool ldlt6(const double A[36], const double b[6], double x[6]) {
         for (int k = 0; k < i; ++k) x[i] -= L[6 * i + k] * x[k];
     }
 #pragma unroll
-    for (int i = 0; i < 6; ++i) x[i] /= d[i];
+    for (int i = 0; i < 6; ++i) x[i] *= id[i];
 #pragma unroll
     for (int i = 5; i >= 0; --i)
 #pragma unroll
@@ -138,30 +185,218 @@ __device__ bool ldlt6(const double A[36], const double b[6], double x[6]) {
     return true;
 }
 
+__device__ __forceinline__ void qnormalize_r(double q[4]) {  // SE3Quat::normalizeRotation, one reciprocal
+    if (q[3] < 0) for (int i = 0; i < 4; ++i) q[i] = -q[i];
+    const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    if (n > 0) {
+        const double in = 1.0 / n;
+        for (int i = 0; i < 4; ++i) q[i] *= in;
+    }
+}
+
+// pose <- exp(u) * pose (VertexSE3Expmap::oplusImpl, SE3Quat::exp then operator*), as orb_se3.h's
+// se3_oplus with sincos and reciprocals instead of divisions (the pose bar is 1e-6 RMSE)
+__device__ __forceinline__ void se3_oplus_r(double (&T)[7], const double (&u)[6]) {
+    const double w0 = u[0], w1 = u[1], w2 = u[2];
+    const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+    const double O[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
+    double O2[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) O2[3 * i + j] = O[3 * i] * O[j] + O[3 * i + 1] * O[3 + j] + O[3 * i + 2] * O[6 + j];
+    double R[9], V[9];
+    if (theta < 0.00001) {
+        for (int k = 0; k < 9; ++k) R[k] = V[k] = (k % 4 == 0 ? 1.0 : 0.0) + O[k] + O2[k];
+    } else {
+        double sn, cs;
+        sincos(theta, &sn, &cs);
+        const double it = 1.0 / theta, it2 = it * it;
+        const double a = sn * it, b = (1 - cs) * it2, d = (theta - sn) * (it2 * it);
+        for (int k = 0; k < 9; ++k) {
+            const double I = (k % 4 == 0 ? 1.0 : 0.0);
+            R[k] = I + a * O[k] + b * O2[k];
+            V[k] = I + b * O[k] + d * O2[k];
+        }
+    }
+    double eq[4], et[3];
+    qfrom_matrix(R, eq);
+    for (int i = 0; i < 3; ++i) et[i] = V[3 * i] * u[3] + V[3 * i + 1] * u[4] + V[3 * i + 2] * u[5];
+    qnormalize_r(eq);
+    const double q[4] = {T[3], T[4], T[5], T[6]};
+    double rt[3];
+    qrotate(eq, T, rt);
+    double nq[4] = {eq[3] * q[0] + eq[0] * q[3] + eq[1] * q[2] - eq[2] * q[1],
+                    eq[3] * q[1] + eq[1] * q[3] + eq[2] * q[0] - eq[0] * q[2],
+                    eq[3] * q[2] + eq[2] * q[3] + eq[0] * q[1] - eq[1] * q[0],
+                    eq[3] * q[3] - eq[0] * q[0] - eq[1] * q[1] - eq[2] * q[2]};
+    qnormalize_r(nq);
+    T[0] = et[0] + rt[0];
+    T[1] = et[1] + rt[1];
+    T[2] = et[2] + rt[2];
+    for (int i = 0; i < 4; ++i) T[3 + i] = nq[i];
+}
+
+// Error, robust chi2 and the J^T W J / -J^T W e contributions of one edge at pose T, added to acc:
+// acc[0..21) the upper triangle of H row by row, acc[21..27) b, acc[27] the robust chi2.  Returns the
+// edge's chi2.  One reciprocal of the depth replaces the divisions of computeError / linearizeOplus.
+// An edge with `on` false contributes exactly zero (zero information, and a zero depth reciprocal so
+// that no product is infinite).
+__device__ __forceinline__ double linearize_edge(const orb_pose_edge_t& Ed, const double* T, const orb_ba_camera_t& cam,
+                                                 bool robust, Huber2 hub, double (&acc)[32], bool on = true) {
+    const double q[4] = {T[3], T[4], T[5], T[6]};
+    double Xc[3];
+    qrotate(q, Ed.xw, Xc);
+    Xc[0] += T[0]; Xc[1] += T[1]; Xc[2] += T[2];
+    const double x = Xc[0], y = Xc[1], z = Xc[2], fx = cam.fx, fy = cam.fy;
+    const double iz = on ? 1.0 / z : 0.0, iz2 = iz * iz;
+    EdgeEval ev;
+    double B[18];
+    if (!Ed.stereo) {
+        ev.er[0] = Ed.obs[0] - (fx * x * iz + (double)cam.cx);
+        ev.er[1] = Ed.obs[1] - (fy * y * iz + (double)cam.cy);
+        ev.er[2] = 0.0;
+        const double j00 = -(fx * iz), j02 = fx * x * iz2, j11 = -(fy * iz), j12 = fy * y * iz2;
+        B[0] = j02 * y;  B[1] = j00 * z - j02 * x; B[2] = -j00 * y; B[3] = j00; B[4] = 0;   B[5] = j02;
+        B[6] = -j11 * z + j12 * y; B[7] = -j12 * x; B[8] = j11 * x;  B[9] = 0;  B[10] = j11; B[11] = j12;
+        for (int k = 12; k < 18; ++k) B[k] = 0;
+    } else {  // cam_project: float invz, double fx, fy, cx, cy, bf members
+        const float finvz = (float)(1.0f / z);
+        const double u = x * finvz * fx + (double)cam.cx;
+        const double v = y * finvz * fy + (double)cam.cy;
+        ev.er[0] = Ed.obs[0] - u;
+        ev.er[1] = Ed.obs[1] - v;
+        ev.er[2] = Ed.obs[2] - (u - (double)cam.bf * finvz);
+        const double bf = cam.bf;
+        B[0] = x * y * iz2 * fx;    B[1] = -(1 + (x * x * iz2)) * fx; B[2] = y * iz * fx;
+        B[3] = -iz * fx;            B[4] = 0;                         B[5] = x * iz2 * fx;
+        B[6] = (1 + y * y * iz2) * fy; B[7] = -x * y * iz2 * fy;      B[8] = -x * iz * fy;
+        B[9] = 0;                   B[10] = -iz * fy;                 B[11] = y * iz2 * fy;
+        B[12] = B[0] - bf * y * iz2; B[13] = B[1] + bf * x * iz2;     B[14] = B[2];
+        B[15] = B[3];               B[16] = 0;                        B[17] = B[5] - bf * iz2;
+    }
+    const double info = on ? (double)Ed.inv_sigma2 : 0.0;
+    ev.chi2 = ev.er[0] * info * ev.er[0] + ev.er[1] * info * ev.er[1];
+    if (Ed.stereo) ev.chi2 += ev.er[2] * info * ev.er[2];
+    ev.stereo = Ed.stereo;
+    double rho1;
+    acc[27] += robust_rho(ev, robust, hub, rho1);
+    const double w = rho1 * info;
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+#pragma unroll
+        for (int j = i; j < 6; ++j) {
+            double s = B[i] * w * B[j] + B[6 + i] * w * B[6 + j];
+            if (Ed.stereo) s += B[12 + i] * w * B[12 + j];
+            acc[k++] += s;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        double bs = B[i] * info * ev.er[0] + B[6 + i] * info * ev.er[1];
+        if (Ed.stereo) bs += B[12 + i] * info * ev.er[2];
+        acc[21 + i] -= rho1 * bs;
+    }
+    return ev.chi2;
+}
+
+// LM state of a frame's optimize(10), kept in registers of the workgroup's thread 0
+struct LmState {
+    double H[21], b[6], x[6], Tb[7];
+    double lambda, ni, current, ini;
+    int nbad, qmax, it, ok;
+};
+
+// One 256-thread workgroup per frame.  The first kS * kPT edges of the frame (and their outlier flag
+// and last chi2) stay in registers for the whole optimisation; edges beyond are read from memory on
+// every pass.  Every trial evaluates the new pose and linearises there in the same pass: g2o rebuilds
+// the system at the accepted state before the next iteration, and a rejected trial keeps the old
+// linearisation, so the next iteration's build is this pass's sums.  Thread 0 holds the LM state; per
+// trial it takes the totals, decides, and solves the next trial, between two barriers.
+template <int kS>
 __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __restrict__ frames,
                                                   const orb_pose_edge_t* __restrict__ edges,
                                                   double* __restrict__ pose_out, uint8_t* __restrict__ level,
                                                   int32_t* __restrict__ inliers, double* __restrict__ echi2, Huber2 hub) {
-    __shared__ double red[(kPW + 1) * kNV];
-    __shared__ double T[7], Tb[7];
-    __shared__ double H[36], bvec[6];
-    __shared__ double s_lambda, s_ni, s_current, s_ini, s_temp;
-    __shared__ int s_go, s_qmax, s_nbad, s_trial_go;
+    __shared__ double part[kPW * 32];
+    __shared__ double T[7];
+    __shared__ int s_state;  // 1: evaluate the trial pose in T, 2: the round's optimize() is done
     const int tid = threadIdx.x, f = blockIdx.x;
     const orb_pose_frame_t F = frames[f];
     const int n = F.n_edges;
     const orb_pose_edge_t* E = edges + F.edge_begin;
     uint8_t* lev = level + F.edge_begin;
     double* ech = echi2 + F.edge_begin;
-    for (int e = tid; e < n; e += kPT) lev[e] = 0;  // mvbOutlier[i] = false at edge creation
     if (n < 3) {  // nInitialCorrespondences < 3: return 0, pose untouched
+        for (int e = tid; e < n; e += kPT) lev[e] = 0;
         if (tid < 7) pose_out[7 * (size_t)f + tid] = frames[f].pose[tid];
         if (tid == 0) inliers[f] = 0;
         return;
     }
-    const orb_ba_camera_t cam = F.cam;
+    orb_pose_edge_t ed[kS];
+    int lv[kS];
+    double ch[kS];
+#pragma unroll
+    for (int s = 0; s < kS; ++s) {
+        const int e = tid + s * kPT;
+        if (e < n) ed[s] = E[e];
+        lv[s] = 0;  // mvbOutlier[i] = false at edge creation
+        ch[s] = 0;
+    }
+    for (int e = tid + kS * kPT; e < n; e += kPT) lev[e] = 0;
+    // fn(edge, outlier flag, last chi2) over this thread's edges
+    auto visit = [&](auto&& fn) {
+#pragma unroll
+        for (int s = 0; s < kS; ++s)
+            if (tid + s * kPT < n) fn(ed[s], lv[s], ch[s]);
+        for (int e = tid + kS * kPT; e < n; e += kPT) {
+            int l = lev[e];
+            double c = ech[e];
+            fn(E[e], l, c);
+            lev[e] = (uint8_t)l;
+            ech[e] = c;
+        }
+    };
+    // a linearisation pass at T over the active edges (chi2 kept when `keep`), reduced: wave 0's lane
+    // 2k ends with the workgroup total of value k.  The register slots are linearised without branches
+    // (an inactive slot computes a zero-information dummy edge), so their latency chains interleave.
+    orb_pose_edge_t dummy{};
+    dummy.xw[2] = 1.0;
+    auto pass = [&](bool robust, bool keep, double (&acc)[32]) {
+#pragma unroll
+        for (int k = 0; k < 32; ++k) acc[k] = 0;
+        double Tl[7];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) Tl[i] = T[i];
+#pragma unroll
+        for (int s = 0; s < kS; ++s) {
+            const bool on = tid + s * kPT < n && !lv[s];
+            const double c2 = linearize_edge(on ? ed[s] : dummy, Tl, F.cam, robust, hub, acc, on);
+            if (keep && on) ch[s] = c2;
+        }
+        for (int e = tid + kS * kPT; e < n; e += kPT) {
+            if (lev[e]) continue;
+            const double c2 = linearize_edge(E[e], Tl, F.cam, robust, hub, acc);
+            if (keep) ech[e] = c2;
+        }
+        wave_partials32(acc, part);
+        __syncthreads();
+        if (tid < 64) {
+            const int k = (tid >> 1) & 31;
+            acc[0] = ((acc[0] + part[32 + k]) + part[64 + k]) + part[96 + k];
+        }
+    };
+    auto solve = [&](LmState& S) {  // thread 0: the damped system, the trial pose into T
+        for (int i = 0; i < 7; ++i) S.Tb[i] = T[i];
+        S.ok = ldlt6(S.H, S.lambda, S.b, S.x);
+        if (!S.ok) for (int i = 0; i < 6; ++i) S.x[i] = 0;
+        double Tn[7];
+        for (int i = 0; i < 7; ++i) Tn[i] = S.Tb[i];
+        se3_oplus_r(Tn, S.x);
+        for (int i = 0; i < 7; ++i) T[i] = Tn[i];
+    };
     bool robust = true;
     int nBad = 0;
+    LmState S;
     for (int round = 0; round < 4; ++round) {
         // vSE3->setEstimate(pFrame->GetPose()); read from global: a lane-indexed read of the copy F
         // would put F in scratch
@@ -169,166 +404,120 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
         __syncthreads();
         // ---- optimizer.initializeOptimization(0); optimizer.optimize(10)
         int active = 0;
-        for (int e = tid; e < n; e += kPT) active += lev[e] == 0;
+        visit([&](const orb_pose_edge_t&, int& l, double&) { active += l == 0; });
         active = __syncthreads_or(active);
-        for (int it = 0; it < 10 && active; ++it) {
-            // computeActiveErrors + buildSystem at T
-            double acc[kNV];
+        if (active) {
+            double acc[32];
+            pass(robust, false, acc);  // computeActiveErrors + buildSystem at the round's start pose
+            double t[28];
+            if (tid < 64) {
 #pragma unroll
-            for (int k = 0; k < kNV; ++k) acc[k] = 0;
-            for (int e = tid; e < n; e += kPT) {
-                if (lev[e]) continue;
-                const orb_pose_edge_t Ed = E[e];
-                double Xc[3];
-                EdgeEval ev;
-                pose_edge_error(Ed, T, cam, Xc, ev);
-                double rho1;
-                acc[27] += robust_rho(ev, robust, hub, rho1);
-                const double x = Xc[0], y = Xc[1], z = Xc[2], fx = cam.fx, fy = cam.fy;
-                double B[18];
-                if (!Ed.stereo) {
-                    const double j00 = -(fx / z), j02 = -(-fx * x / (z * z)), j11 = -(fy / z), j12 = -(-fy * y / (z * z));
-                    B[0] = j02 * y;  B[1] = j00 * z - j02 * x; B[2] = -j00 * y; B[3] = j00; B[4] = 0;   B[5] = j02;
-                    B[6] = -j11 * z + j12 * y; B[7] = -j12 * x; B[8] = j11 * x;  B[9] = 0;  B[10] = j11; B[11] = j12;
-                    for (int k = 12; k < 18; ++k) B[k] = 0;
-                } else {
-                    const double bf = cam.bf, invz = 1.0 / z, invz_2 = invz * invz;
-                    B[0] = x * y * invz_2 * fx;    B[1] = -(1 + (x * x * invz_2)) * fx; B[2] = y * invz * fx;
-                    B[3] = -invz * fx;             B[4] = 0;                            B[5] = x * invz_2 * fx;
-                    B[6] = (1 + y * y * invz_2) * fy; B[7] = -x * y * invz_2 * fy;      B[8] = -x * invz * fy;
-                    B[9] = 0;                      B[10] = -invz * fy;                  B[11] = y * invz_2 * fy;
-                    B[12] = B[0] - bf * y * invz_2; B[13] = B[1] + bf * x * invz_2;     B[14] = B[2];
-                    B[15] = B[3];                  B[16] = 0;                           B[17] = B[5] - bf * invz_2;
-                }
-                const double info = (double)Ed.inv_sigma2, w = rho1 * info;
-                int k = 0;
-#pragma unroll
-                for (int i = 0; i < 6; ++i) {
-#pragma unroll
-                    for (int j = i; j < 6; ++j) {
-                        double s = B[i] * w * B[j] + B[6 + i] * w * B[6 + j];
-                        if (Ed.stereo) s += B[12 + i] * w * B[12 + j];
-                        acc[k++] += s;
-                    }
-                }
-#pragma unroll
-                for (int i = 0; i < 6; ++i) {
-                    double bs = B[i] * info * ev.er[0] + B[6 + i] * info * ev.er[1];
-                    if (Ed.stereo) bs += B[12 + i] * info * ev.er[2];
-                    acc[21 + i] -= rho1 * bs;
-                }
+                for (int k = 0; k < 28; ++k) t[k] = readlane_d(acc[0], 2 * k);
             }
-            block_reduce<kNV>(acc, red);
             if (tid == 0) {
-                int k = 0;
-                for (int i = 0; i < 6; ++i)
-                    for (int j = i; j < 6; ++j) H[6 * i + j] = H[6 * j + i] = acc[k++];
-                for (int i = 0; i < 6; ++i) bvec[i] = acc[21 + i];
-                s_current = s_ini = acc[27];
-                if (it == 0) {  // computeLambdaInit: tau * max |diag H|
-                    double m = 0;
-                    for (int i = 0; i < 6; ++i) m = fmax(fabs(H[7 * i]), m);
-                    s_lambda = 1e-5 * m;
-                    s_ni = 2;
-                    s_nbad = 0;
-                }
-                s_qmax = 0;
-                s_trial_go = 1;
+#pragma unroll
+                for (int k = 0; k < 21; ++k) S.H[k] = t[k];
+#pragma unroll
+                for (int i = 0; i < 6; ++i) S.b[i] = t[21 + i];
+                S.current = S.ini = t[27];
+                double m = 0;  // computeLambdaInit: tau * max |diag H|
+                constexpr int kDiag[6] = {0, 6, 11, 15, 18, 20};
+#pragma unroll
+                for (int i = 0; i < 6; ++i) m = fmax(fabs(S.H[kDiag[i]]), m);
+                S.lambda = 1e-5 * m;
+                S.ni = 2;
+                S.nbad = 0;
+                S.qmax = 0;
+                S.it = 0;
+                solve(S);
             }
             __syncthreads();
-            double rho = 0;
-            while (s_trial_go) {
-                __shared__ int s_ok2;
-                __shared__ double s_x[6];
-                if (tid == 0) {
-                    for (int i = 0; i < 7; ++i) Tb[i] = T[i];
-                    double A[36];
-                    for (int i = 0; i < 36; ++i) A[i] = H[i];
-                    for (int i = 0; i < 6; ++i) A[7 * i] += s_lambda;
-                    double x[6];
-                    s_ok2 = ldlt6(A, bvec, x);
-                    if (!s_ok2) for (int i = 0; i < 6; ++i) x[i] = 0;
-                    for (int i = 0; i < 6; ++i) s_x[i] = x[i];
-                    double Tn[7];
-                    for (int i = 0; i < 7; ++i) Tn[i] = T[i];
-                    se3_oplus(Tn, x);
-                    for (int i = 0; i < 7; ++i) T[i] = Tn[i];
+            for (;;) {
+                // evaluate (and linearise) at the trial pose; every active edge's chi2 is kept, since
+                // g2o classifies on the last evaluated state even when it was rejected
+                pass(robust, true, acc);
+                if (tid < 64) {
+#pragma unroll
+                    for (int k = 0; k < 28; ++k) t[k] = readlane_d(acc[0], 2 * k);
                 }
-                __syncthreads();
-                double tc[1] = {0};
-                for (int e = tid; e < n; e += kPT) {
-                    if (lev[e]) continue;
-                    double Xc[3];
-                    EdgeEval ev;
-                    pose_edge_error(E[e], T, cam, Xc, ev);
-                    ech[e] = ev.chi2;  // the last evaluated state's chi2 (read by the classification)
-                    double rho1;
-                    tc[0] += robust_rho(ev, robust, hub, rho1);
-                }
-                block_reduce<1>(tc, red);
                 if (tid == 0) {
-                    double tempChi = tc[0];
-                    if (!s_ok2) tempChi = DBL_MAX;
-                    double r = s_current - tempChi;
+                    double tempChi = t[27];
+                    if (!S.ok) tempChi = DBL_MAX;
+                    double r = S.current - tempChi;
                     double scale = 0;
-                    for (int i = 0; i < 6; ++i) scale += s_x[i] * (s_lambda * s_x[i] + bvec[i]);
+                    for (int i = 0; i < 6; ++i) scale += S.x[i] * (S.lambda * S.x[i] + S.b[i]);
                     scale += 1e-3;
                     r /= scale;
-                    if (r > 0 && isfinite(tempChi)) {
-                        double alpha = 1. - pow((2 * r - 1), 3);
+                    const bool accept = r > 0 && isfinite(tempChi);
+                    if (accept) {
+                        const double c = 2 * r - 1;
+                        double alpha = 1. - c * c * c;  // 1 - pow(2 rho - 1, 3)
                         alpha = fmin(alpha, 2. / 3.);
-                        s_lambda *= fmax(1. / 3., alpha);
-                        s_ni = 2;
-                        s_current = tempChi;
+                        S.lambda *= fmax(1. / 3., alpha);
+                        S.ni = 2;
+                        S.current = tempChi;
                     } else {
-                        s_lambda *= s_ni;
-                        s_ni *= 2;
-                        for (int i = 0; i < 7; ++i) T[i] = Tb[i];
+                        S.lambda *= S.ni;
+                        S.ni *= 2;
+                        for (int i = 0; i < 7; ++i) T[i] = S.Tb[i];
                     }
-                    s_qmax++;
-                    s_temp = r;
-                    s_trial_go = (r < 0 && s_qmax < 10);
+                    S.qmax++;
+                    int st = 1;
+                    if (!(r < 0 && S.qmax < 10)) {
+                        // the iteration ends; optimize()'s loop stops on qmax == 10 or rho == 0, after
+                        // 10 iterations, or on the third consecutive small chi2 decrease
+                        if (S.qmax == 10 || r == 0) {
+                            st = 2;
+                        } else {
+                            if ((S.ini - S.current) * 1e3 < S.ini) S.nbad++;
+                            else S.nbad = 0;
+                            if (S.nbad >= 3 || ++S.it == 10) st = 2;
+                        }
+                        if (st == 1) {  // accepted: the next iteration's system is this pass's linearisation
+#pragma unroll
+                            for (int k = 0; k < 21; ++k) S.H[k] = t[k];
+#pragma unroll
+                            for (int i = 0; i < 6; ++i) S.b[i] = t[21 + i];
+                            S.ini = S.current;
+                            S.qmax = 0;
+                        }
+                    }
+                    if (st == 1) solve(S);
+                    s_state = st;
                 }
                 __syncthreads();
-                rho = s_temp;
+                if (s_state == 2) break;
             }
-            // termination (uniform: every thread read the same shared values)
-            if (s_qmax == 10 || rho == 0) break;
-            if (tid == 0) {
-                if ((s_ini - s_current) * 1e3 < s_ini) s_nbad++;
-                else s_nbad = 0;
-                s_go = s_nbad < 3;
-            }
-            __syncthreads();
-            if (!s_go) break;
         }
-        __syncthreads();
         // ---- re-classification (src/Optimizer.cc:285-386)
         int bad = 0;
-        for (int e = tid; e < n; e += kPT) {
-            double c2;
-            if (lev[e]) {
+        visit([&](const orb_pose_edge_t& Ed, int& l, double& c) {
+            double c2 = c;
+            if (l) {
                 double Xc[3];
                 EdgeEval ev;
-                pose_edge_error(E[e], T, cam, Xc, ev);
+                pose_edge_error(Ed, T, F.cam, Xc, ev);
                 c2 = ev.chi2;
-            } else {
-                c2 = ech[e];
             }
             const float chi2 = (float)c2;
-            const bool out = chi2 > (E[e].stereo ? 7.815f : 5.991f);
-            lev[e] = out;
-            bad += out;
-        }
+            l = chi2 > (Ed.stereo ? 7.815f : 5.991f);
+            bad += l;
+        });
         {
-            double nb[1] = {(double)bad};
-            block_reduce<1>(nb, red);
-            nBad = (int)nb[0];
+            const double wb = wave_sum_d((double)bad);
+            if ((tid & 63) == 0) part[tid >> 6] = wb;
+            __syncthreads();
+            nBad = (int)(((part[0] + part[1]) + part[2]) + part[3]);
+            __syncthreads();  // part is rewritten by the next round
         }
         if (round == 2) robust = false;
         if (n < 10) break;  // optimizer.edges().size() < 10
     }
-    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < kS; ++s) {
+        const int e = tid + s * kPT;
+        if (e < n) lev[e] = (uint8_t)lv[s];
+    }
     if (tid < 7) pose_out[7 * (size_t)f + tid] = T[tid];
     if (tid == 0) inliers[f] = n - nBad;
 }
@@ -367,8 +556,8 @@ int orb_pose_optimization_device(int n_frames, const orb_pose_frame_t* d_frames,
         if (hipMalloc(&g_chi, need * sizeof(double)) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "hipMalloc failed");
         g_chi_cap = need;
     }
-    hipLaunchKernelGGL(k_pose_opt, dim3(n_frames), dim3(kPT), 0, (hipStream_t)stream, d_frames, d_edges, d_pose_out,
-                       d_outlier, d_inliers, g_chi, make_huber());
+    hipLaunchKernelGGL(k_pose_opt<kEdgeSlots>, dim3(n_frames), dim3(kPT), 0, (hipStream_t)stream, d_frames, d_edges,
+                       d_pose_out, d_outlier, d_inliers, g_chi, make_huber());
     if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "pose kernel launch failed");
     return ORB_OK;
 }
