@@ -140,6 +140,16 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     return v;
 }
 
+// 1 / d from v_rcp_f64 and two Newton steps (within an ulp; d finite and nonzero): five dependent
+// operations instead of the IEEE division sequence, on thread 0's serial chain
+__device__ __forceinline__ double rcp_nr(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-d, r, 1.0);
+    return fma(r, e, r);
+}
+
 // LDL^T of the 6x6 symmetric matrix given as its upper triangle row by row (LinearSolverDense:
 // Eigen::LDLT; the same solution up to rounding); one reciprocal per pivot
 __device__ __forceinline__ bool ldlt6(const double (&U)[21], double lambda, const double (&b)[6], double (&x)[6]) {
@@ -161,7 +171,7 @@ __device__ __forceinline__ bool ldlt6(const double (&U)[21], double lambda, cons
         for (int k = 0; k < j; ++k) dj -= L[6 * j + k] * L[6 * j + k] * d[k];
         if (!(dj > 0)) return false;  // LDLT::isPositive (the damped system is SPD unless degenerate)
         d[j] = dj;
-        id[j] = 1.0 / dj;
+        id[j] = rcp_nr(dj);
 #pragma unroll
         for (int i = j + 1; i < 6; ++i) {
             double v = A[6 * j + i];
@@ -189,7 +199,7 @@ __device__ __forceinline__ void qnormalize_r(double q[4]) {  // SE3Quat::normali
     if (q[3] < 0) for (int i = 0; i < 4; ++i) q[i] = -q[i];
     const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
     if (n > 0) {
-        const double in = 1.0 / n;
+        const double in = rcp_nr(n);
         for (int i = 0; i < 4; ++i) q[i] *= in;
     }
 }
@@ -209,7 +219,7 @@ __device__ __forceinline__ void se3_oplus_r(double (&T)[7], const double (&u)[6]
     } else {
         double sn, cs;
         sincos(theta, &sn, &cs);
-        const double it = 1.0 / theta, it2 = it * it;
+        const double it = rcp_nr(theta), it2 = it * it;
         const double a = sn * it, b = (1 - cs) * it2, d = (theta - sn) * (it2 * it);
         for (int k = 0; k < 9; ++k) {
             const double I = (k % 4 == 0 ? 1.0 : 0.0);
@@ -447,7 +457,7 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
                     double scale = 0;
                     for (int i = 0; i < 6; ++i) scale += S.x[i] * (S.lambda * S.x[i] + S.b[i]);
                     scale += 1e-3;
-                    r /= scale;
+                    r *= rcp_nr(scale);
                     const bool accept = r > 0 && isfinite(tempChi);
                     if (accept) {
                         const double c = 2 * r - 1;
