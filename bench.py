@@ -520,6 +520,50 @@ def bench_single_frame(pkg, synth, cpu_baseline_on, reps=50):
     return out
 
 
+def bench_c2_pcie(pkg, synth, dev, steps, n_frames=64, in_flight=3):
+    """SURVEY.md 8(d)'s wording of the metric, H2D -> extract -> D2H: the C2 batch starts in pinned
+    host memory and the keypoints, descriptors and counts end there, every step, with the same
+    handles in flight as the main line (each handle's copies and kernels on its own stream).  Never
+    `value` (the task's value is device-resident); reported beside it."""
+    import numpy as np
+    import torch
+    frames = np.stack([synth.polygon_frame(640, 480, seed=100 + i) for i in range(n_frames)])
+    host = torch.from_numpy(frames).pin_memory()
+    H = max(1, in_flight)
+    exs = [pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=640, max_height=480, max_batch=n_frames) for _ in range(H)]
+    cap = 1000 + 16 * 8
+    dimg = [torch.empty_like(host, device=dev) for _ in range(H)]
+    outs = [(torch.empty((n_frames, cap, 7), dtype=torch.float32, device=dev),
+             torch.empty((n_frames, cap, 32), dtype=torch.uint8, device=dev),
+             torch.empty((n_frames, 2), dtype=torch.int32, device=dev)) for _ in range(H)]
+    houts = [tuple(torch.empty(o.shape, dtype=o.dtype).pin_memory() for o in outs[h]) for h in range(H)]
+    sts = [torch.cuda.Stream(dev) for _ in range(H)]
+
+    def step(i):
+        h = i % H
+        with torch.cuda.stream(sts[h]):
+            dimg[h].copy_(host, non_blocking=True)
+            exs[h].extract_batch_device(dimg[h], (0, 1000), cap=cap, out=outs[h], stream=sts[h])
+            for d, o in zip(houts[h], outs[h]):
+                d.copy_(o, non_blocking=True)
+    for i in range(3 * H):
+        step(i)
+    torch.cuda.synchronize(dev)
+    nfeat = int(houts[0][2][:, 0].sum().item())
+    reps = max(6, min(steps, 21))
+    t0 = time.perf_counter()
+    for i in range(reps):
+        step(i)
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) * 1e3
+    h2d = host.numel()
+    d2h = sum(o.numel() * o.element_size() for o in outs[0])
+    return {"config": f"C2 ({n_frames} x 640x480) from pinned host memory to pinned host outputs, {H} batches in flight",
+            "features_per_ms": round(nfeat * reps / dt, 3), "ms_per_step": round(dt / reps, 4),
+            "h2d_bytes_per_step": h2d, "d2h_bytes_per_step": d2h,
+            "pcie_gb_per_s": round((h2d + d2h) * reps / dt / 1e6, 2)}
+
+
 def bench_c4(pkg, synth, dev, steps, n_frames=32, in_flight=3):
     """C4's per-GPU shard: 32 frames of 1280x720 (nFeatures 1000) per step, device-resident (the
     8-GPU run all-gathers the features of every shard; see the main line's N > 1 path), with
@@ -881,6 +925,12 @@ def main():
             matchers = bench_matchers(pkg, synth, dev, args.steps, not args.no_cpu_baseline)
         except Exception as e:  # noqa: BLE001
             matchers = {"error": repr(e)}
+    pcie = None
+    if not args.no_single and world == 1:
+        try:
+            pcie = bench_c2_pcie(pkg, synth, dev, args.steps, in_flight=H)
+        except Exception as e:  # noqa: BLE001
+            pcie = {"error": repr(e)}
     c4 = None
     if not args.no_c4 and world == 1:
         try:
@@ -888,6 +938,8 @@ def main():
         except Exception as e:  # noqa: BLE001
             c4 = {"error": repr(e)}
     if rank == 0:
+        if pcie is not None:
+            result["pcie_inclusive"] = pcie
         if c4 is not None:
             result["c4_shard"] = c4
         if c4_strong is not None:
