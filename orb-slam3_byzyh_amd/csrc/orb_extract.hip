@@ -1845,9 +1845,15 @@ struct Extractor {
     int32_t* d_lap_count = nullptr; size_t lapcount_cap = 0;
     int* d_status = nullptr;
     bool clear_status_l0 = false;  // this batch's level-0 launch clears d_status (see launch_batch)
-    // synchronous path staging
+    // synchronous path (orb_extract): the image, and one output block (keypoints | descriptors |
+    // counts | status) downloaded in one copy into pinned staging
     uint8_t* d_img = nullptr; size_t img_cap = 0;
+    uint8_t* d_out = nullptr; uint8_t* h_out = nullptr;
     orb_keypoint_t* d_kps = nullptr; uint8_t* d_desc = nullptr; int32_t* d_counts = nullptr; size_t out_cap = 0;
+    // its launch sequence and download captured as one graph, replayed while g1_key (sizes, buffers) holds
+    hipGraph_t g1_graph = nullptr;
+    hipGraphExec_t g1_exec = nullptr;
+    std::vector<uintptr_t> g1_key;
     hipStream_t stream = nullptr;
     int last_n = 0;
     int qt_lds = 0;
@@ -2043,7 +2049,8 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     mark(0);
     // FAST on the first `split` levels runs on a side stream as soon as those pyramid levels exist,
     // overlapping the latency-bound launches of the small levels (k.lv[split..] ) on `st`.
-    const int split = (e->fast_split > 0 && e->fast_split < k.nlevels) ? e->fast_split : 0;
+    // (a single frame runs as one chain: too few blocks per level for the overlap to pay)
+    const int split = (n > 1 && e->fast_split > 0 && e->fast_split < k.nlevels) ? e->fast_split : 0;
     static const bool fast_stamps = getenv("ORBGPU_FAST_STAMPS") != nullptr;
     auto launch_fast = [&](int l0, int l1, hipStream_t s2) {
         const int c0 = k.lv[l0].cell_begin, c1 = k.lv[l1 - 1].cell_begin + k.lv[l1 - 1].cell_count;
@@ -2315,9 +2322,12 @@ int orb_extractor_destroy(orb_extractor_t h) {
     if (e->stream) hipStreamSynchronize(e->stream);
     void* bufs[] = {e->d_st_kp, e->d_st_desc, e->d_stamps, e->d_geom, e->d_cells, e->d_xtab, e->d_tiletab, e->d_ytab, e->d_pyr, e->d_cand, e->d_scratch,
                     e->d_cell_count, e->d_cell_thr, e->d_sel, e->d_dst, e->d_sel_count, e->d_lap_count, e->d_status,
-                    e->d_img, e->d_kps, e->d_desc, e->d_counts};
+                    e->d_img, e->d_out};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
+    if (e->h_out) (void)hipHostFree(e->h_out);
+    if (e->g1_exec) (void)hipGraphExecDestroy(e->g1_exec);
+    if (e->g1_graph) (void)hipGraphDestroy(e->g1_graph);
     for (hipEvent_t x : e->events) (void)hipEventDestroy(x);
     for (hipEvent_t x : e->pyr_events) (void)hipEventDestroy(x);
     if (e->side) { hipStreamSynchronize(e->side); hipStreamDestroy(e->side); }
@@ -2378,34 +2388,84 @@ int orb_extract(orb_extractor_t h, const uint8_t* image, int width, int height, 
     if (rc != ORB_OK) return rc;
     const int dcap = std::max(cap, 1);
     if ((rc = grow(e->d_img, e->img_cap, (size_t)width * height)) != ORB_OK) return rc;
-    if (e->out_cap < (size_t)dcap || !e->d_kps) {
-        if (e->d_kps) hipFree(e->d_kps);
-        if (e->d_desc) hipFree(e->d_desc);
-        if (e->d_counts) hipFree(e->d_counts);
-        e->d_kps = nullptr; e->d_desc = nullptr; e->d_counts = nullptr; e->out_cap = 0;
-        if (hipMalloc(&e->d_kps, sizeof(orb_keypoint_t) * dcap) != hipSuccess ||
-            hipMalloc(&e->d_desc, 32 * (size_t)dcap) != hipSuccess || hipMalloc(&e->d_counts, 8) != hipSuccess)
-            return orbgpu_fail(ORB_ERR_DEVICE, "hipMalloc failed");
+    const size_t desc_off = (sizeof(orb_keypoint_t) * dcap + 255) & ~(size_t)255;
+    const size_t cnt_off = desc_off + ((32 * (size_t)dcap + 255) & ~(size_t)255), st_off = cnt_off + 8, blk = st_off + 8;
+    if (e->out_cap < (size_t)dcap || !e->d_out) {
+        (void)hipStreamSynchronize(e->stream);
+        if (e->d_out) (void)hipFree(e->d_out);
+        if (e->h_out) (void)hipHostFree(e->h_out);
+        e->d_out = e->h_out = nullptr;
+        e->out_cap = 0;
+        if (hipMalloc(&e->d_out, blk) != hipSuccess || hipHostMalloc(&e->h_out, blk, 0) != hipSuccess)
+            return orbgpu_fail(ORB_ERR_DEVICE, "output allocation failed");
         e->out_cap = dcap;
     }
+    e->d_kps = reinterpret_cast<orb_keypoint_t*>(e->d_out);
+    e->d_desc = e->d_out + desc_off;
+    e->d_counts = reinterpret_cast<int32_t*>(e->d_out + cnt_off);
     if (hipMemcpy2DAsync(e->d_img, width, image, stride, width, height, hipMemcpyHostToDevice, e->stream) != hipSuccess)
         return orbgpu_fail(ORB_ERR_DEVICE, "upload failed");
-    rc = launch_batch(e, e->d_img, 1, width, height, width, (size_t)width * height, lap_x0, lap_x1, e->d_kps,
-                      e->d_desc, cap, e->d_counts, e->stream);
-    if (rc != ORB_OK) return rc;
-    int32_t cnt[2] = {0, 0};
-    int status = 0;
-    if (hipMemcpyAsync(cnt, e->d_counts, 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
-        hipMemcpyAsync(&status, e->d_status, 4, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
-        hipStreamSynchronize(e->stream) != hipSuccess)
-        return orbgpu_fail(ORB_ERR_DEVICE, "download failed");
+    // the launches and one download of the whole output block (keypoints, descriptors, counts) plus
+    // the status word
+    auto enqueue = [&]() -> int {
+        const int r = launch_batch(e, e->d_img, 1, width, height, width, (size_t)width * height, lap_x0, lap_x1, e->d_kps,
+                                   e->d_desc, cap, e->d_counts, e->stream);
+        if (r != ORB_OK) return r;
+        if (hipMemcpyAsync(e->h_out, e->d_out, cnt_off + 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+            hipMemcpyAsync(e->h_out + st_off, e->d_status, 4, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
+            return orbgpu_fail(ORB_ERR_DEVICE, "download failed");
+        return ORB_OK;
+    };
+    // Tracking calls this once per frame with the same sizes: the ~20 launches and their event
+    // hand-offs are replayed as one graph (host enqueue gaps between the device's launches otherwise
+    // dominate a single frame).  Timing / debug modes launch directly.
+    static const bool graph_off = getenv("ORBGPU_FAST_STAMPS") || getenv("ORBGPU_PYR_STAMPS");
+    bool use_graph = !graph_off && e->profile == 0 && !(e->geo.k.debug_flags & 4);
+    if (use_graph) {
+        const std::vector<uintptr_t> key = {
+            (uintptr_t)width, (uintptr_t)height, (uintptr_t)lap_x0, (uintptr_t)lap_x1, (uintptr_t)cap,
+            (uintptr_t)e->d_img, (uintptr_t)e->d_out, (uintptr_t)e->h_out, (uintptr_t)e->d_pyr, (uintptr_t)e->d_cand,
+            (uintptr_t)e->d_scratch, (uintptr_t)e->d_cell_count, (uintptr_t)e->d_cell_thr, (uintptr_t)e->d_sel,
+            (uintptr_t)e->d_dst, (uintptr_t)e->d_sel_count, (uintptr_t)e->d_lap_count, (uintptr_t)e->d_st_kp,
+            (uintptr_t)e->d_st_desc, (uintptr_t)e->d_geom, (uintptr_t)e->d_cells, (uintptr_t)e->d_xtab,
+            (uintptr_t)e->d_ytab, (uintptr_t)e->d_tiletab, (uintptr_t)e->qt_lds, (uintptr_t)e->d_stamps};
+        if (!e->g1_exec || key != e->g1_key) {
+            if (e->g1_exec) { (void)hipGraphExecDestroy(e->g1_exec); e->g1_exec = nullptr; }
+            if (e->g1_graph) { (void)hipGraphDestroy(e->g1_graph); e->g1_graph = nullptr; }
+            bool ok = hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
+            if (ok) {
+                const int r = enqueue();
+                ok = hipStreamEndCapture(e->stream, &e->g1_graph) == hipSuccess && r == ORB_OK && e->g1_graph &&
+                     hipGraphInstantiate(&e->g1_exec, e->g1_graph, nullptr, nullptr, 0) == hipSuccess;
+            }
+            if (!ok) {  // launch directly
+                (void)hipGetLastError();
+                if (e->g1_graph) { (void)hipGraphDestroy(e->g1_graph); e->g1_graph = nullptr; }
+                e->g1_exec = nullptr;
+                use_graph = false;
+            } else {
+                e->g1_key = key;
+            }
+        }
+    }
+    if (use_graph) {
+        if (hipGraphLaunch(e->g1_exec, e->stream) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "graph launch failed");
+        e->batches++;
+        e->last_n = 1;
+    } else if ((rc = enqueue()) != ORB_OK) {
+        return rc;
+    }
+    if (hipStreamSynchronize(e->stream) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "download failed");
+    int32_t cnt[2];
+    int status;
+    memcpy(cnt, e->h_out + cnt_off, 8);
+    memcpy(&status, e->h_out + st_off, 4);
     if (status != 0) return orbgpu_fail(ORB_ERR_INTERNAL, "quad-tree capacity guard tripped");
     if (n_kps) *n_kps = cnt[0];
     if (cnt[1] < 0) return orbgpu_fail(ORB_ERR_CAPACITY, "output capacity too small");
     if (cnt[0] > 0) {
-        if (hipMemcpy(kps, e->d_kps, sizeof(orb_keypoint_t) * cnt[0], hipMemcpyDeviceToHost) != hipSuccess ||
-            hipMemcpy(desc, e->d_desc, 32 * (size_t)cnt[0], hipMemcpyDeviceToHost) != hipSuccess)
-            return orbgpu_fail(ORB_ERR_DEVICE, "download failed");
+        memcpy(kps, e->h_out, sizeof(orb_keypoint_t) * cnt[0]);
+        memcpy(desc, e->h_out + desc_off, 32 * (size_t)cnt[0]);
     }
     return cnt[1];
 }
