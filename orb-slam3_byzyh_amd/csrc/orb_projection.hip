@@ -684,13 +684,16 @@ extern "C" int orb_search_by_projection_frame(orb_matcher_t m, const orb_frame_v
         const size_t o_md = off; off = align256(off + (size_t)nl * 32);
         const size_t o_lo = off; off = align256(off + (size_t)nl * 4);
         const size_t o_la = off; off = align256(off + (size_t)nl * 4);
+        // initialised with the inputs (one upload, no fills): the lister / fixed claims (0x7f..) and
+        // the overflow word + counters (0), which the one download then reads back with the matches
+        const size_t o_lf = off; off = align256(off + (size_t)std::max(n, 1) * 8);
+        const size_t o_ovf = off; off = align256(off + 16);
         const size_t in_bytes = off;
+        const size_t o_mp = off; off = align256(off + (size_t)std::max(n, 1) * 4);
         const size_t o_cand = off; off = align256(off + (size_t)nl * P.cap * sizeof(Cand));
         const size_t o_nc = off; off = align256(off + (size_t)nl * 4);
-        const size_t o_ovf = off; off = align256(off + 16);
-        const size_t o_mp = off; off = align256(off + (size_t)std::max(n, 1) * 4);
         const size_t o_st = off; off = align256(off + (size_t)std::max(nl, 1) * 4);
-        const size_t o_kw = off; off = align256(off + (size_t)std::max(n, 1) * 20);  // claimMin, last, removed | lister, fixed
+        const size_t o_kw = off; off = align256(off + (size_t)std::max(n, 1) * 12);  // claimMin, last, removed
         const size_t o_wl = off; off = align256(off + (size_t)std::max(nl, 1) * 4);  // resolve work list
         const size_t o_top = off; off = align256(off + (size_t)std::max(nl, 1) * 68);  // 8 best (64 B) + usable count
         if (int rc = orbgpu_matcher_reserve(m, off, &d, &h, &s, &check_ori)) return rc;
@@ -719,16 +722,16 @@ extern "C" int orb_search_by_projection_frame(orb_matcher_t m, const orb_frame_v
             lo[i] = last->kps_un[i].octave;
             la[i] = last->kps_un[i].angle;
         }
+        memset(h + o_lf, 0x7f, (size_t)std::max(n, 1) * 8);
+        memset(h + o_ovf, 0, 16);
         bool ok = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s) == hipSuccess;
-        ok = ok && hipMemsetAsync(d + o_ovf, 0, 16, s) == hipSuccess &&
-             hipMemsetAsync(d + o_kw + (size_t)std::max(n, 1) * 12, 0x7f, (size_t)std::max(n, 1) * 8, s) == hipSuccess;  // lister, fixed
         if (ok && nl > 0)
             hipLaunchKernelGGL(k_proj_candidates, dim3((nl + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s, (const ProjParams*)(d + o_p),
                                (const uint8_t*)(d + o_va), (const float*)(d + o_xyz), (const uint4*)(d + o_md),
                                (const int32_t*)(d + o_lo), (const float4*)(d + o_kp), (const float*)(d + o_ur),
                                (const uint4*)(d + o_cd), (const int32_t*)(d + o_co), (const int32_t*)(d + o_ci),
                                (Cand*)(d + o_cand), (int32_t*)(d + o_nc), (int32_t*)(d + o_ovf), (const uint8_t*)(d + o_ob),
-                               (int32_t*)(d + o_kw + (size_t)std::max(n, 1) * 12));
+                               (int32_t*)(d + o_lf));
         ResolveArgs ra{};
         ra.n_pts = nl; ra.n_cur = n; ra.cap = P.cap; ra.local = 0; ra.check_ori = check_ori; ra.nnratio = 0.f;
         ra.cands = (const Cand*)(d + o_cand); ra.ncand = (const int32_t*)(d + o_nc); ra.observed = (const uint8_t*)(d + o_ob);
@@ -736,7 +739,8 @@ extern "C" int orb_search_by_projection_frame(orb_matcher_t m, const orb_frame_v
         ra.overflow = (const int32_t*)(d + o_ovf); ra.st = (int32_t*)(d + o_st);
         int32_t* kw = (int32_t*)(d + o_kw);
         const size_t nk = (size_t)std::max(n, 1);
-        ra.claimMin = kw; ra.last = kw + nk; ra.removed = kw + 2 * nk; ra.lister = kw + 3 * nk; ra.fixed = kw + 4 * nk;
+        ra.claimMin = kw; ra.last = kw + nk; ra.removed = kw + 2 * nk;
+        ra.lister = (int32_t*)(d + o_lf); ra.fixed = (int32_t*)(d + o_lf) + nk;
         ra.work = (int32_t*)(d + o_wl);
         ra.top = (int4*)(d + o_top); ra.nusable = (int32_t*)(d + o_top + (size_t)std::max(nl, 1) * 64);
         ra.lds_keypoints = n <= kResolveLdsKeypoints && resolve_lds_ready() ? 1 : 0;
@@ -748,8 +752,8 @@ extern "C" int orb_search_by_projection_frame(orb_matcher_t m, const orb_frame_v
             hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 8 * (size_t)n : 0, s, ra);
         }
         ok = ok && hipGetLastError() == hipSuccess &&
-             hipMemcpyAsync(h + o_mp, d + o_mp, (size_t)std::max(n, 1) * 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
-             hipMemcpyAsync(h + o_ovf, d + o_ovf, 16, hipMemcpyDeviceToHost, s) == hipSuccess &&
+             hipMemcpyAsync(h + o_ovf, d + o_ovf, o_mp - o_ovf + (size_t)std::max(n, 1) * 4, hipMemcpyDeviceToHost, s) ==
+                 hipSuccess &&
              hipStreamSynchronize(s) == hipSuccess;
         if (!ok) return orbgpu_fail(ORB_ERR_DEVICE, "SearchByProjection failed");
         int32_t ovf = 0;
@@ -819,13 +823,14 @@ extern "C" int orb_search_by_projection_local(orb_matcher_t m, const orb_frame_v
         const size_t o_dp = off; off = align256(off + (size_t)np * 4);
         const size_t o_lv = off; off = align256(off + (size_t)np * 4);
         const size_t o_md = off; off = align256(off + (size_t)np * 32);
+        const size_t o_lf = off; off = align256(off + (size_t)std::max(n, 1) * 8);  // lister, fixed (0x7f..)
+        const size_t o_ovf = off; off = align256(off + 16);                          // overflow + counters (0)
         const size_t in_bytes = off;
+        const size_t o_m = off; off = align256(off + (size_t)std::max(n, 1) * 4);
         const size_t o_cand = off; off = align256(off + (size_t)np * P.cap * sizeof(Cand));
         const size_t o_nc = off; off = align256(off + (size_t)np * 4);
-        const size_t o_ovf = off; off = align256(off + 16);
-        const size_t o_m = off; off = align256(off + (size_t)std::max(n, 1) * 4);
         const size_t o_st = off; off = align256(off + (size_t)std::max(np, 1) * 4);
-        const size_t o_kw = off; off = align256(off + (size_t)std::max(n, 1) * 20);  // claimMin, last, removed | lister, fixed
+        const size_t o_kw = off; off = align256(off + (size_t)std::max(n, 1) * 12);  // claimMin, last, removed
         const size_t o_wl = off; off = align256(off + (size_t)std::max(np, 1) * 4);  // resolve work list
         const size_t o_top = off; off = align256(off + (size_t)std::max(np, 1) * 68);  // 8 best (64 B) + usable count
         if (int rc = orbgpu_matcher_reserve(m, off, &d, &h, &s, &check_ori)) return rc;
@@ -853,9 +858,9 @@ extern "C" int orb_search_by_projection_local(orb_matcher_t m, const orb_frame_v
             memcpy(h + o_lv, pts->track_level, (size_t)np * 4);
             memcpy(h + o_md, pts->desc, (size_t)np * 32);
         }
-        bool ok = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s) == hipSuccess &&
-                  hipMemsetAsync(d + o_ovf, 0, 16, s) == hipSuccess &&
-                  hipMemsetAsync(d + o_kw + (size_t)std::max(n, 1) * 12, 0x7f, (size_t)std::max(n, 1) * 8, s) == hipSuccess;  // lister, fixed
+        memset(h + o_lf, 0x7f, (size_t)std::max(n, 1) * 8);
+        memset(h + o_ovf, 0, 16);
+        bool ok = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s) == hipSuccess;
         if (ok && np > 0)
             hipLaunchKernelGGL(k_lmp_candidates, dim3((np + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s, (const LocalParams*)(d + o_p),
                                (const uint8_t*)(d + o_iv), (const uint8_t*)(d + o_bd), (const float*)(d + o_pj),
@@ -863,7 +868,7 @@ extern "C" int orb_search_by_projection_local(orb_matcher_t m, const orb_frame_v
                                (const uint4*)(d + o_md), (const float4*)(d + o_kp), (const float*)(d + o_ur),
                                (const uint4*)(d + o_cd), (const int32_t*)(d + o_co), (const int32_t*)(d + o_ci),
                                (Cand*)(d + o_cand), (int32_t*)(d + o_nc), (int32_t*)(d + o_ovf), (const uint8_t*)(d + o_ob),
-                               frame_taken ? (const uint8_t*)(d + o_tk) : nullptr, (int32_t*)(d + o_kw + (size_t)std::max(n, 1) * 12));
+                               frame_taken ? (const uint8_t*)(d + o_tk) : nullptr, (int32_t*)(d + o_lf));
         ResolveArgs ra{};
         ra.n_pts = np; ra.n_cur = n; ra.cap = P.cap; ra.local = 1; ra.check_ori = 0; ra.nnratio = P.nnratio;
         ra.cands = (const Cand*)(d + o_cand); ra.ncand = (const int32_t*)(d + o_nc); ra.observed = (const uint8_t*)(d + o_ob);
@@ -871,7 +876,8 @@ extern "C" int orb_search_by_projection_local(orb_matcher_t m, const orb_frame_v
         ra.last_angle = nullptr; ra.overflow = (const int32_t*)(d + o_ovf); ra.st = (int32_t*)(d + o_st);
         int32_t* kw = (int32_t*)(d + o_kw);
         const size_t nk = (size_t)std::max(n, 1);
-        ra.claimMin = kw; ra.last = kw + nk; ra.removed = kw + 2 * nk; ra.lister = kw + 3 * nk; ra.fixed = kw + 4 * nk;
+        ra.claimMin = kw; ra.last = kw + nk; ra.removed = kw + 2 * nk;
+        ra.lister = (int32_t*)(d + o_lf); ra.fixed = (int32_t*)(d + o_lf) + nk;
         ra.work = (int32_t*)(d + o_wl);
         ra.top = (int4*)(d + o_top); ra.nusable = (int32_t*)(d + o_top + (size_t)std::max(np, 1) * 64);
         ra.lds_keypoints = n <= kResolveLdsKeypoints && resolve_lds_ready() ? 1 : 0;
@@ -881,8 +887,8 @@ extern "C" int orb_search_by_projection_local(orb_matcher_t m, const orb_frame_v
             hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 8 * (size_t)n : 0, s, ra);
         }
         ok = ok && hipGetLastError() == hipSuccess &&
-             hipMemcpyAsync(h + o_m, d + o_m, (size_t)std::max(n, 1) * 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
-             hipMemcpyAsync(h + o_ovf, d + o_ovf, 16, hipMemcpyDeviceToHost, s) == hipSuccess &&
+             hipMemcpyAsync(h + o_ovf, d + o_ovf, o_m - o_ovf + (size_t)std::max(n, 1) * 4, hipMemcpyDeviceToHost, s) ==
+                 hipSuccess &&
              hipStreamSynchronize(s) == hipSuccess;
         if (!ok) return orbgpu_fail(ORB_ERR_DEVICE, "SearchByProjection(local) failed");
         int32_t ovf = 0;
