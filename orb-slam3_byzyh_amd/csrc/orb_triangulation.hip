@@ -393,8 +393,8 @@ int orb_search_for_triangulation(orb_matcher_t m, const orb_kf_view_t* kf1, cons
     const size_t o_node = off; off = align256(off + nnode * 4);
     const size_t o_csr = off; off = align256(off + ncsr * 4);
     const size_t o_idx = off; off = align256(off + nidx * 4);
+    const size_t o_match = off; off = align256(off + (size_t)n_pairs * kf1->n * 4);  // -1 from the host, uploaded
     const size_t in_bytes = off;
-    const size_t o_match = off; off = align256(off + (size_t)n_pairs * kf1->n * 4);
     const size_t o_cnt = off; off = align256(off + (size_t)n_pairs * 4);
     if (int rc = m->reserve(off)) return rc;
 
@@ -440,8 +440,8 @@ int orb_search_for_triangulation(orb_matcher_t m, const orb_kf_view_t* kf1, cons
 
     char* d = m->d_buf;
     hipStream_t s = m->stream;
+    memset(h + o_match, 0xFF, (size_t)n_pairs * kf1->n * 4);
     bool ok = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s) == hipSuccess;
-    ok = ok && hipMemsetAsync(d + o_match, 0xFF, (size_t)n_pairs * kf1->n * 4, s) == hipSuccess;
     if (ok && kf1->n_nodes > 0) {
         hipLaunchKernelGGL(k_tri_match, dim3((kf1->n_nodes + kWaves - 1) / kWaves, n_pairs), dim3(64 * kWaves), 0, s,
                            (const KfDev*)(d + o_kf), (const PairDev*)(d + o_pair), (const KpRec*)(d + o_kp),
