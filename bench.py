@@ -219,57 +219,63 @@ def bench_local_ba(pkg, synth, world, dev, steps, cpu_baseline_on):
     return out
 
 
-def bench_stereo(pkg, synth, dev, steps, cpu_baseline_on, n_pairs=32):
+def bench_stereo(pkg, synth, dev, steps, cpu_baseline_on, n_pairs=32, n_sets=2):
     """C3 stereo stream (752x480, nFeatures 1200, EuRoC bf/b): one step = extract the left and the
     right batch of n_pairs frames + Frame::ComputeStereoMatches on the device pyramids.  Reports
-    stereo frames per ms, the matching kernels' share, and the CPU oracle on a bounded sample."""
+    stereo frames per ms, the matching kernels' share, and the CPU oracle on a bounded sample.
+    `n_sets` (left, right) extractor pairs take the steps in turn, each with its own left, right and
+    matching streams, so one step's matching and quad-tree tail overlap the next step's pyramids (as
+    the main line's batches in flight)."""
     import numpy as np
     import torch
     bf, b = 47.90639384423901, 0.110074
     pairs = [synth.stereo_pair(752, 480, seed=2000 + i) for i in range(n_pairs)]
     L = torch.from_numpy(np.stack([p[0] for p in pairs])).to(dev)
     R = torch.from_numpy(np.stack([p[1] for p in pairs])).to(dev)
-    exl = pkg.ORBextractor(1200, 1.2, 8, 20, 7, max_width=752, max_height=480, max_batch=n_pairs)
-    exr = pkg.ORBextractor(1200, 1.2, 8, 20, 7, max_width=752, max_height=480, max_batch=n_pairs)
     cap = 1200 + 16 * 8
-    st = torch.cuda.current_stream(dev)
-    # left and right extractions run concurrently on their own streams, as Frame.cc:136-141 runs the
-    # two extractors on two threads; the matching waits for both
-    s_l, s_r = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-    mk = lambda: (torch.empty((n_pairs, cap, 7), dtype=torch.float32, device=dev),
+    mk = lambda: (torch.empty((n_pairs, cap, 7), dtype=torch.float32, device=dev),  # noqa: E731
                   torch.empty((n_pairs, cap, 32), dtype=torch.uint8, device=dev),
                   torch.empty((n_pairs, 2), dtype=torch.int32, device=dev))
-    out_l, out_r = mk(), mk()
+    sets = []
+    for _ in range(max(1, n_sets)):
+        sets.append({"exl": pkg.ORBextractor(1200, 1.2, 8, 20, 7, max_width=752, max_height=480, max_batch=n_pairs),
+                     "exr": pkg.ORBextractor(1200, 1.2, 8, 20, 7, max_width=752, max_height=480, max_batch=n_pairs),
+                     "out_l": mk(), "out_r": mk(), "s_l": torch.cuda.Stream(dev), "s_r": torch.cuda.Stream(dev),
+                     "s_m": torch.cuda.Stream(dev)})
 
-    def extract_pair():
-        s_l.wait_stream(st)  # the previous matching has read the pyramids
-        s_r.wait_stream(st)
-        exl.extract_batch_device(L, (0, 0), cap=cap, out=out_l, stream=s_l)
-        exr.extract_batch_device(R, (0, 0), cap=cap, out=out_r, stream=s_r)
-        st.wait_stream(s_l)
-        st.wait_stream(s_r)
+    # left and right extractions run concurrently on their own streams, as Frame.cc:136-141 runs the
+    # two extractors on two threads; the matching waits for both
+    def step(i, ev=None):
+        S = sets[i % len(sets)]
+        S["s_l"].wait_stream(S["s_m"])  # this set's previous matching has read the pyramids
+        S["s_r"].wait_stream(S["s_m"])
+        S["exl"].extract_batch_device(L, (0, 0), cap=cap, out=S["out_l"], stream=S["s_l"])
+        S["exr"].extract_batch_device(R, (0, 0), cap=cap, out=S["out_r"], stream=S["s_r"])
+        S["s_m"].wait_stream(S["s_l"])
+        S["s_m"].wait_stream(S["s_r"])
+        if ev is not None:
+            ev[0].record(S["s_m"])
+        with torch.cuda.stream(S["s_m"]):
+            r = pkg.compute_stereo_matches_batch_device(S["exl"], S["exr"], S["out_l"], S["out_r"], bf, b, stream=S["s_m"])
+        if ev is not None:
+            ev[1].record(S["s_m"])
+        return r
 
-    def step():
-        extract_pair()
-        return pkg.compute_stereo_matches_batch_device(exl, exr, out_l, out_r, bf, b, stream=st)
-
-    for _ in range(3):
-        step()
+    for i in range(3 * len(sets)):
+        step(i)
     torch.cuda.synchronize(dev)
-    reps = max(5, min(steps, 20))
+    reps = max(6, min(steps, 20))
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     t0 = time.perf_counter()
     for i in range(reps):
-        extract_pair()
-        ev[i][0].record(st)
-        _, _, kept = pkg.compute_stereo_matches_batch_device(exl, exr, out_l, out_r, bf, b, stream=st)
-        ev[i][1].record(st)
+        _, _, kept = step(i, ev[i])
     torch.cuda.synchronize(dev)
     dt = (time.perf_counter() - t0) * 1e3
     match_ms = sum(a.elapsed_time(z) for a, z in ev)
     kept = kept.cpu().numpy()
     out = {"config": f"C3: {n_pairs} stereo pairs 752x480 per step (synthetic EuRoC-shaped, disparity 4-48 px), "
-                     "nFeatures 1200, extract left || right (two streams) + Frame::ComputeStereoMatches, one GPU",
+                     "nFeatures 1200, extract left || right (two streams) + Frame::ComputeStereoMatches, one GPU, "
+                     f"{len(sets)} steps in flight",
            "stereo_frames_per_ms": round(n_pairs * reps / dt, 4), "ms_per_step": round(dt / reps, 4),
            "match_ms_per_step": round(match_ms / reps, 4),
            "matches_per_frame": round(float(kept.mean()), 1)}

@@ -232,9 +232,6 @@ int launch(orb_vocabulary_t v, const uint8_t* d_desc, const int32_t* d_frame_beg
     return ORB_OK;
 }
 
-std::mutex g_tmp_mu;
-uint8_t* g_tmp = nullptr;  // per-descriptor word / weight / node of the batch path (grow-only)
-size_t g_tmp_cap = 0;
 
 }  // namespace
 
@@ -290,19 +287,17 @@ int orb_bow_transform_batch_device(orb_vocabulary_t v, const uint8_t* d_desc, co
         return orbgpu_fail(ORB_ERR_ARG, "invalid BoW arguments");
     if (n_frames == 0) return ORB_OK;
     if (v->n_nodes <= 1) return orbgpu_fail(ORB_ERR_ARG, "empty vocabulary");
-    std::lock_guard<std::mutex> lk(g_tmp_mu);
-    const size_t need = (size_t)std::max(n_total, 1) * 16;
-    if (need > g_tmp_cap) {
-        if (g_tmp) (void)hipFree(g_tmp);
-        g_tmp = nullptr;
-        g_tmp_cap = 0;
-        if (hipMalloc(&g_tmp, need) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "hipMalloc failed");
-        g_tmp_cap = need;
-    }
+    // per-descriptor word / weight / node scratch, stream-ordered (allocated and freed on the call's
+    // stream), so calls on different streams may run concurrently
     const size_t m = std::max(n_total, 1);
-    return launch(v, d_desc, d_frame_begin, n_frames, n_total, levelsup, reinterpret_cast<int32_t*>(g_tmp + 8 * m),
-                  reinterpret_cast<double*>(g_tmp), reinterpret_cast<int32_t*>(g_tmp + 12 * m), d_bow_word, d_bow_value,
-                  d_fv_node, d_fv_begin, d_fv_feat, d_counts, (hipStream_t)stream);
+    uint8_t* tmp = nullptr;
+    if (hipMallocAsync(reinterpret_cast<void**>(&tmp), m * 16, (hipStream_t)stream) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "hipMallocAsync failed");
+    int rc = launch(v, d_desc, d_frame_begin, n_frames, n_total, levelsup, reinterpret_cast<int32_t*>(tmp + 8 * m),
+                    reinterpret_cast<double*>(tmp), reinterpret_cast<int32_t*>(tmp + 12 * m), d_bow_word, d_bow_value,
+                    d_fv_node, d_fv_begin, d_fv_feat, d_counts, (hipStream_t)stream);
+    if (hipFreeAsync(tmp, (hipStream_t)stream) != hipSuccess && rc == ORB_OK) rc = orbgpu_fail(ORB_ERR_DEVICE, "hipFreeAsync failed");
+    return rc;
 }
 
 int orb_bow_transform(orb_vocabulary_t v, const uint8_t* desc, int n, int levelsup, int32_t* bow_word,

@@ -532,9 +532,6 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
     if (tid == 0) inliers[f] = n - nBad;
 }
 
-std::mutex g_mu;
-double* g_chi = nullptr;
-size_t g_chi_cap = 0;
 
 Huber2 make_huber() {
     Huber2 h;
@@ -557,18 +554,17 @@ int orb_pose_optimization_device(int n_frames, const orb_pose_frame_t* d_frames,
         (n_edges && (!d_edges || !d_outlier)))
         return orbgpu_fail(ORB_ERR_ARG, "invalid pose optimisation arguments");
     if (n_frames == 0) return ORB_OK;
-    std::lock_guard<std::mutex> lk(g_mu);
-    const size_t need = std::max<size_t>(1, (size_t)n_edges);
-    if (need > g_chi_cap) {
-        if (g_chi) (void)hipFree(g_chi);
-        g_chi = nullptr;
-        g_chi_cap = 0;
-        if (hipMalloc(&g_chi, need * sizeof(double)) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "hipMalloc failed");
-        g_chi_cap = need;
-    }
+    // the chi2 of edges beyond the register slots: stream-ordered scratch (allocated and freed on the
+    // call's stream), so calls on different streams may run concurrently
+    double* chi = nullptr;
+    if (hipMallocAsync(reinterpret_cast<void**>(&chi), std::max<size_t>(1, (size_t)n_edges) * sizeof(double),
+                       (hipStream_t)stream) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "hipMallocAsync failed");
     hipLaunchKernelGGL(k_pose_opt<kEdgeSlots>, dim3(n_frames), dim3(kPT), 0, (hipStream_t)stream, d_frames, d_edges,
-                       d_pose_out, d_outlier, d_inliers, g_chi, make_huber());
-    if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "pose kernel launch failed");
+                       d_pose_out, d_outlier, d_inliers, chi, make_huber());
+    const bool launched = hipGetLastError() == hipSuccess;
+    if (hipFreeAsync(chi, (hipStream_t)stream) != hipSuccess || !launched)
+        return orbgpu_fail(ORB_ERR_DEVICE, "pose kernel launch failed");
     return ORB_OK;
 }
 

@@ -293,10 +293,6 @@ int launch(const StereoGeom& G, const OrbPyramidView& vl, const OrbPyramidView& 
     return ORB_OK;
 }
 
-std::mutex g_sad_mu;
-int32_t* g_sad = nullptr;  // per-keypoint SAD scratch of the batch path (grow-only)
-size_t g_sad_cap = 0;
-
 }  // namespace
 
 extern "C" {
@@ -314,17 +310,17 @@ int orb_compute_stereo_matches_batch_device(orb_extractor_t left, orb_extractor_
     OrbPyramidView vl, vr;
     int rc = make_geom(left, right, n, G, vl, vr);
     if (rc != ORB_OK) return rc;
-    std::lock_guard<std::mutex> lk(g_sad_mu);
+    // the per-keypoint SAD scratch is stream-ordered (allocated and freed on the call's stream), so
+    // calls on different handles and streams may run concurrently
     const size_t need = (size_t)n * std::max(cap_l, 1);
-    if (need > g_sad_cap) {
-        if (g_sad) (void)hipFree(g_sad);
-        g_sad = nullptr;
-        g_sad_cap = 0;
-        if (hipMalloc(&g_sad, need * sizeof(int32_t)) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "hipMalloc failed");
-        g_sad_cap = need;
-    }
-    return launch(G, vl, vr, n, d_kps_l, d_counts_l, d_desc_l, cap_l, d_kps_r, d_counts_r, d_desc_r, cap_r, bf, b,
-                  d_u_right, d_depth, g_sad, d_kept, (hipStream_t)stream);
+    int32_t* sad = nullptr;
+    if (hipMallocAsync(reinterpret_cast<void**>(&sad), need * sizeof(int32_t), (hipStream_t)stream) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "hipMallocAsync failed");
+    rc = launch(G, vl, vr, n, d_kps_l, d_counts_l, d_desc_l, cap_l, d_kps_r, d_counts_r, d_desc_r, cap_r, bf, b,
+                d_u_right, d_depth, sad, d_kept, (hipStream_t)stream);
+    if (hipFreeAsync(sad, (hipStream_t)stream) != hipSuccess && rc == ORB_OK)
+        rc = orbgpu_fail(ORB_ERR_DEVICE, "hipFreeAsync failed");
+    return rc;
 }
 
 int orb_compute_stereo_matches(orb_extractor_t left, orb_extractor_t right, const orb_keypoint_t* kps_l, int n_l,
