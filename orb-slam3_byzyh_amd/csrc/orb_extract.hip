@@ -1971,6 +1971,20 @@ int prepare(Extractor* e, int w, int h, int n) {
             return orbgpu_fail(ORB_ERR_DEVICE, "table upload failed");
         std::vector<int4> tt;
         tile_tables(g.k, tt, e->tile_off);
+        // every tile's source box must fit the LDS box of the k_pyramid_level instance its level
+        // launches (launch_chunk: the small box for level ratios <= 1.25, else the wide one, sized for
+        // ratios up to 2; the alignment shift takes up to 3 more bytes)
+        for (int l = 1; l < g.k.nlevels; ++l) {
+            const bool small = 4 * g.k.lv[l - 1].w <= 5 * g.k.lv[l].w && 4 * g.k.lv[l - 1].h <= 5 * g.k.lv[l].h;
+            const int bwmax = (small ? kSmallBoxW : kBoxW) - 3, bhmax = small ? kSmallBoxH : kBoxH;
+            const int t1 = l + 1 < g.k.nlevels ? e->tile_off[l + 1] : (int)tt.size();
+            for (int t = e->tile_off[l]; t < t1; ++t)
+                if ((tt[t].y >> 16) > bwmax || (tt[t].z >> 16) > bhmax) {
+                    e->cur_w = e->cur_h = -1;  // the next call rebuilds (and rejects) the geometry
+                    e->geo_ok = false;
+                    return orbgpu_fail(ORB_ERR_ARG, "pyramid level ratio above 2 (scale factor too large)");
+                }
+        }
         if ((rc = grow(e->d_tiletab, e->tiletab_cap, tt.size())) != ORB_OK) return rc;
         if (hipMemcpy(e->d_tiletab, tt.data(), tt.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess)
             return orbgpu_fail(ORB_ERR_DEVICE, "table upload failed");

@@ -283,3 +283,37 @@ def test_schedule_switches_parity(pkg, oracle, synth, monkeypatch, env):
         assert n == len(rk) and int(counts[f, 1]) == rm, f
         assert np.array_equal(pkg.keypoints_to_structured(kps[f], n).view(np.uint8), rk.view(np.uint8)), f
         assert np.array_equal(desc[f, :n].cpu().numpy(), rd), f
+
+
+@pytest.mark.parametrize("w,h,kind,nf,scale,nlevels,ini,mn", [
+    (1280, 720, "poly", 1500, 1.5, 6, 25, 10),   # level ratio > 1.25: the wide-box resize path
+    (1280, 720, "noise", 800, 2.0, 4, 20, 7),    # ratio 2, few levels
+    (752, 480, "poly", 1000, 1.1, 12, 15, 5),    # 12 levels (kMaxLevels), low thresholds
+])
+def test_extract_parity_other_parameters(pkg, oracle, synth, w, h, kind, nf, scale, nlevels, ini, mn):
+    """ORBextractor parameters other than the 1.2 / 8 / 20 / 7 of the bench configs (the reference
+    reads them from the settings file, src/Tracking.cc:1346-1362): pyramid levels, keypoints (bitwise)
+    and descriptors against the oracle."""
+    img = synth.polygon_frame(w, h, seed=21) if kind == "poly" else synth.blurred_noise_frame(w, h, seed=22)
+    ex = pkg.ORBextractor(nf, scale, nlevels, ini, mn, max_width=w, max_height=h)
+    ref = oracle.OracleExtractor(nf, scale, nlevels, ini, mn)
+    kps, desc, mono = ex(img, None, (0, 1000))
+    rkps, rdesc, rmono = ref(img, (0, 1000))
+    for l in range(nlevels):
+        gp, rp = ex.level_padded(l), ref.level_padded(l)
+        assert np.array_equal(gp[16:-16, 16:-16], rp[16:-16, 16:-16]), f"level {l}: {_first_diff(gp[16:-16, 16:-16], rp[16:-16, 16:-16])}"
+    assert mono == rmono and len(kps) == len(rkps) > 0
+    assert np.array_equal(kps.view(np.uint8), rkps.view(np.uint8)), \
+        _first_diff(kps.view(np.uint32).reshape(-1, 7), rkps.view(np.uint32).reshape(-1, 7))
+    assert np.array_equal(desc, rdesc), _first_diff(desc, rdesc)
+
+
+def test_scale_factor_above_two_is_rejected(pkg, synth):
+    """The pyramid tiles' LDS source boxes cover level ratios up to 2: a larger scale factor fails
+    loudly instead of reading past the box."""
+    img = synth.polygon_frame(1280, 720, seed=23)
+    ex = pkg.ORBextractor(500, 3.0, 3, 20, 7, max_width=1280, max_height=720)
+    with pytest.raises(pkg.OrbGpuError):
+        ex(img, None, (0, 0))
+    with pytest.raises(pkg.OrbGpuError):  # and again: the rejected geometry is not reused
+        ex(img, None, (0, 0))
