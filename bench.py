@@ -674,7 +674,7 @@ def bench_c4_strong(pkg, synth, world, rank, dev, steps, in_flight=3, n_global=2
         feats = int(f.item())
     out = {"config": f"C4 strong scaling: {n_global} synthetic 1280x720 frames per step in total ({n_distinct} distinct, "
                      f"repeated), {per} per GPU x {world} GPU(s), nFeatures 1000, 8 levels"
-                     + (", all-gather of keypoints + descriptors + counts per step (RCCL)" if world > 1 else ""),
+                     + (", all-gather of keypoints + descriptors + counts per step (" + {"nccl": "RCCL"}.get(dist.get_backend(), dist.get_backend()) + ")" if world > 1 else ""),
            "n_gpus": world, "frames_per_gpu": per, "ms_per_step": round(ms, 4),
            "frames_per_ms": round(n_global / ms, 3), "features_per_ms": round(feats / ms, 3)}
     if world > 1:
