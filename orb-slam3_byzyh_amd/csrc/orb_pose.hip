@@ -205,7 +205,8 @@ __device__ __forceinline__ void qnormalize_r(double q[4]) {  // SE3Quat::normali
 }
 
 // pose <- exp(u) * pose (VertexSE3Expmap::oplusImpl, SE3Quat::exp then operator*), as orb_se3.h's
-// se3_oplus with sincos and reciprocals instead of divisions (the pose bar is 1e-6 RMSE)
+// se3_oplus with reciprocals instead of divisions and, above g2o's small-angle threshold, the rotation's
+// quaternion in closed form instead of Quaterniond(R) (the pose bar is 1e-6 RMSE)
 __device__ __forceinline__ void se3_oplus_r(double (&T)[7], const double (&u)[6]) {
     const double w0 = u[0], w1 = u[1], w2 = u[2];
     const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
@@ -213,24 +214,25 @@ __device__ __forceinline__ void se3_oplus_r(double (&T)[7], const double (&u)[6]
     double O2[9];
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) O2[3 * i + j] = O[3 * i] * O[j] + O[3 * i + 1] * O[3 + j] + O[3 * i + 2] * O[6 + j];
-    double R[9], V[9];
-    if (theta < 0.00001) {
+    double V[9], eq[4], et[3];
+    if (theta < 0.00001) {  // g2o's small-angle branch: R = V = I + Omega + Omega^2, then Quaterniond(R)
+        double R[9];
         for (int k = 0; k < 9; ++k) R[k] = V[k] = (k % 4 == 0 ? 1.0 : 0.0) + O[k] + O2[k];
+        qfrom_matrix(R, eq);
+        qnormalize_r(eq);
     } else {
-        double sn, cs;
-        sincos(theta, &sn, &cs);
+        // Quaterniond(R) of the Rodrigues R is (sin(theta/2) w / theta, cos(theta/2)), already unit:
+        // one sincos of the half angle gives it, and sin(theta) = 2 s c, 1 - cos(theta) = 2 s^2 for V
+        double sh, chh;
+        sincos(0.5 * theta, &sh, &chh);
         const double it = rcp_nr(theta), it2 = it * it;
-        const double a = sn * it, b = (1 - cs) * it2, d = (theta - sn) * (it2 * it);
-        for (int k = 0; k < 9; ++k) {
-            const double I = (k % 4 == 0 ? 1.0 : 0.0);
-            R[k] = I + a * O[k] + b * O2[k];
-            V[k] = I + b * O[k] + d * O2[k];
-        }
+        const double sn = 2 * sh * chh, omc = 2 * sh * sh;
+        const double b = omc * it2, d = (theta - sn) * (it2 * it);
+        for (int k = 0; k < 9; ++k) V[k] = (k % 4 == 0 ? 1.0 : 0.0) + b * O[k] + d * O2[k];
+        const double f = sh * it;
+        eq[0] = f * w0; eq[1] = f * w1; eq[2] = f * w2; eq[3] = chh;
     }
-    double eq[4], et[3];
-    qfrom_matrix(R, eq);
     for (int i = 0; i < 3; ++i) et[i] = V[3 * i] * u[3] + V[3 * i + 1] * u[4] + V[3 * i + 2] * u[5];
-    qnormalize_r(eq);
     const double q[4] = {T[3], T[4], T[5], T[6]};
     double rt[3];
     qrotate(eq, T, rt);
