@@ -4,15 +4,17 @@
 // One 256-thread workgroup per frame runs the whole optimisation: 4 rounds of g2o's optimize(10)
 // (OptimizationAlgorithmLevenberg::solve, core/optimization_algorithm_levenberg.cpp:61-194, with
 // LinearSolverDense on the single 6x6 pose block), each round restarting from the frame's pose and
-// followed by the chi2 re-classification of every edge.  Per LM step:
-//   build  threads stride over the active (level-0) edges: error, Huber weight, Jacobian
-//          (EdgeSE3ProjectXYZOnlyPose: -projectJac * SE3deriv; EdgeStereoSE3ProjectXYZOnlyPose:
-//          types_six_dof_expmap.cpp:375-404), the 21 + 6 entries of J^T W J / -J^T W e and the
-//          robust chi2, reduced over the workgroup in a fixed order (wave shuffles, then LDS)
-//   trial  lane 0 of wave 0 factors H + lambda I (LDL^T), exponentiates and applies the step; the
-//          workgroup evaluates the new robust chi2 (storing every edge's chi2: g2o classifies the
-//          active edges on the error of the LAST evaluated state, even a rejected one); lane 0 runs
-//          g2o's accept / reject rule and restores the pose on a rejection
+// followed by the chi2 re-classification of every edge.  Per LM trial:
+//   solve  thread 0 factors H + lambda I (LDL^T), exponentiates and applies the step
+//   pass   threads evaluate their active (level-0) edges at the trial pose -- error, Huber weight,
+//          Jacobian (EdgeSE3ProjectXYZOnlyPose: -projectJac * SE3deriv;
+//          EdgeStereoSE3ProjectXYZOnlyPose: types_six_dof_expmap.cpp:375-404) -- and keep every
+//          edge's chi2 (g2o classifies the active edges on the error of the LAST evaluated state,
+//          even a rejected one); the 21 + 6 entries of J^T W J / -J^T W e and the robust chi2 are
+//          reduced in a fixed order (a transposed butterfly in each wave, then the waves in order)
+//   decide thread 0 runs g2o's accept / reject rule, restores the pose on a rejection, and on an
+//          acceptance takes the pass's sums as the next iteration's system (g2o rebuilds it at the
+//          accepted state), then solves the next trial
 // No MFMA: a 6x6 system per frame; the work is the per-edge linearisation and reductions.
 #include <hip/hip_runtime.h>
 
