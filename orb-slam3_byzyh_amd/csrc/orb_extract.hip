@@ -1843,7 +1843,8 @@ struct Extractor {
     int32_t* d_dst = nullptr; size_t dst_cap = 0;
     int32_t* d_sel_count = nullptr; size_t selcount_cap = 0;
     int32_t* d_lap_count = nullptr; size_t lapcount_cap = 0;
-    int* d_status = nullptr;
+    int* d_status = nullptr;      // the handle's status word: d_status_own, or inside d_out once orb_extract
+    int* d_status_own = nullptr;  // has allocated it (so the one download carries it)
     bool clear_status_l0 = false;  // this batch's level-0 launch clears d_status (see launch_batch)
     // synchronous path (orb_extract): the image, and one output block (keypoints | descriptors |
     // counts | status) downloaded in one copy into pinned staging
@@ -2280,10 +2281,11 @@ int orb_extractor_create(const orb_params_t* p, int max_width, int max_height, i
     e->max_batch = max_batch;
     e->qt_lds = 64 * 1024;  // set per frame size in prepare()
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&e->d_status, sizeof(int)) != hipSuccess) {
+        hipMalloc(&e->d_status_own, sizeof(int)) != hipSuccess) {
         delete e;
         return orbgpu_fail(ORB_ERR_DEVICE, "stream/status allocation failed");
     }
+    e->d_status = e->d_status_own;
     hipFuncSetAttribute((const void*)k_quadtree_kp, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (const char* c = getenv("ORBGPU_CHUNK")) e->chunk = std::max(1, atoi(c));
     if (const char* c = getenv("ORBGPU_STREAMS")) e->nstreams = std::min(Extractor::kMaxStreams, std::max(1, atoi(c)));
@@ -2335,7 +2337,7 @@ int orb_extractor_destroy(orb_extractor_t h) {
     if (!e) return ORB_ERR_ARG;
     if (e->stream) hipStreamSynchronize(e->stream);
     void* bufs[] = {e->d_st_kp, e->d_st_desc, e->d_stamps, e->d_geom, e->d_cells, e->d_xtab, e->d_tiletab, e->d_ytab, e->d_pyr, e->d_cand, e->d_scratch,
-                    e->d_cell_count, e->d_cell_thr, e->d_sel, e->d_dst, e->d_sel_count, e->d_lap_count, e->d_status,
+                    e->d_cell_count, e->d_cell_thr, e->d_sel, e->d_dst, e->d_sel_count, e->d_lap_count, e->d_status_own,
                     e->d_img, e->d_out};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -2410,9 +2412,11 @@ int orb_extract(orb_extractor_t h, const uint8_t* image, int width, int height, 
         if (e->h_out) (void)hipHostFree(e->h_out);
         e->d_out = e->h_out = nullptr;
         e->out_cap = 0;
+        e->d_status = e->d_status_own;
         if (hipMalloc(&e->d_out, blk) != hipSuccess || hipHostMalloc(&e->h_out, blk, 0) != hipSuccess)
             return orbgpu_fail(ORB_ERR_DEVICE, "output allocation failed");
         e->out_cap = dcap;
+        e->d_status = reinterpret_cast<int*>(e->d_out + st_off);  // downloaded with the outputs
     }
     e->d_kps = reinterpret_cast<orb_keypoint_t*>(e->d_out);
     e->d_desc = e->d_out + desc_off;
@@ -2425,8 +2429,7 @@ int orb_extract(orb_extractor_t h, const uint8_t* image, int width, int height, 
         const int r = launch_batch(e, e->d_img, 1, width, height, width, (size_t)width * height, lap_x0, lap_x1, e->d_kps,
                                    e->d_desc, cap, e->d_counts, e->stream);
         if (r != ORB_OK) return r;
-        if (hipMemcpyAsync(e->h_out, e->d_out, cnt_off + 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
-            hipMemcpyAsync(e->h_out + st_off, e->d_status, 4, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
+        if (hipMemcpyAsync(e->h_out, e->d_out, st_off + 4, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
             return orbgpu_fail(ORB_ERR_DEVICE, "download failed");
         return ORB_OK;
     };
