@@ -250,17 +250,62 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
     const int tx = (wave & 1) * 64 + lane, r0 = (wave >> 1) * (kTileH / 2);
     const int vx = reflect101(min(X0 + tx, ex - 1) - kEdge, A.w);
     if (kLevel0) {
-        // level 0: the column's rows straight from the input with reflected indices, all loads
-        // issued before the first LDS store (one round trip)
-        const uint8_t* src = in + (size_t)f * in_frame_stride + vx;
-        int v[kTileH / 2];
+        // level 0: the written region is the input with REFLECT_101 borders.  Each thread makes 8
+        // consecutive plane bytes of a tile row (16 threads per 128-px row, 16 rows per pass) and
+        // stores them at once (plane columns of a chunk start 8-aligned).  Interior chunks are two
+        // v_alignbyte of three aligned dwords of the input row (buffer loads over the frame rounded up
+        // to whole dwords -- an aligned dword never crosses a page -- and 0 past it); chunks that touch
+        // the view's left or right edge go byte by byte through reflect101.
+        (void)vx; (void)r0;
+        const uint8_t* fbase = in + (size_t)f * in_frame_stride;
+        const uintptr_t fb = reinterpret_cast<uintptr_t>(fbase);
+        const int fmis = uniform((int)(fb & 3));
+        const uint64_t fal = (uint64_t)(uint32_t)uniform((int)(uint32_t)(fb - fmis)) |
+                             (uint64_t)(uint32_t)uniform((int)(uint32_t)((fb - fmis) >> 32)) << 32;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<void*>(fal), (short)0, uniform((fmis + (A.h - 1) * in_stride + A.w + 3) & ~3), kBufDword3);
+        const int c = (tid & 15) * 8, px = X0 + c, x0 = px - kEdge;
+        const bool interior = x0 >= 0 && x0 + 8 <= A.w;
+        constexpr int kPasses = (kTileH + 15) / 16;
+        unsigned long long val[kPasses];
 #pragma unroll
-        for (int k = 0; k < kTileH / 2; ++k) v[k] = src[reflect101(min(Y0 + r0 + k, ey - 1) - kEdge, A.h) * in_stride];
+        for (int ps = 0; ps < kPasses; ++ps) {
+            const int r = (tid >> 4) + 16 * ps;
+            const int vy = reflect101(min(Y0 + r, ey - 1) - kEdge, A.h);
+            if (interior) {
+                const int off = fmis + vy * in_stride + x0, oa = off & ~3, sh = off & 3;
+                const uint32_t w0 = __builtin_amdgcn_raw_buffer_load_b32(rs, oa, 0, 0);
+                const uint32_t w1 = __builtin_amdgcn_raw_buffer_load_b32(rs, oa, 4, 0);
+                const uint32_t w2 = __builtin_amdgcn_raw_buffer_load_b32(rs, oa, 8, 0);
+                val[ps] = __builtin_amdgcn_alignbyte(w1, w0, sh) |
+                          (unsigned long long)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32;
+            } else {
+                const uint8_t* srow = fbase + (size_t)vy * in_stride;
+                unsigned long long v8 = 0;
 #pragma unroll
-        for (int k = 0; k < kTileH / 2; ++k) tile[r0 + k][tx] = (uint8_t)v[k];
-        __syncthreads();
+                for (int i = 0; i < 8; ++i)
+                    v8 |= (unsigned long long)srow[reflect101(min(px + i, ex - 1) - kEdge, A.w)] << (8 * i);
+                val[ps] = v8;
+            }
+        }
         PYR_STAMP(1);
         PYR_STAMP(2);
+#pragma unroll
+        for (int ps = 0; ps < kPasses; ++ps) {
+            const int r = (tid >> 4) + 16 * ps, py = Y0 + r;
+            if (r >= kTileH || py >= ey || px >= ex) continue;
+            uint8_t* dst = plane + (size_t)py * A.pitch + px;
+            if (px + 7 < ex) {
+                *reinterpret_cast<unsigned long long*>(dst) = val[ps];
+            } else {
+                for (int i = 0; i < 8 && px + i < ex; ++i) dst[i] = (uint8_t)(val[ps] >> (8 * i));
+            }
+        }
+        if (stp) {
+            PYR_STAMP(3);
+            if (threadIdx.x == 0) { stp[4] = stp[5] = stp[3]; stp[7] = wall_clock64(); }
+        }
+        return;
     } else {
         const int bx0 = T.y & 0xffff, bw = T.y >> 16, by0 = T.z & 0xffff, bh = T.z >> 16;
         // source box as aligned dwords (over-reads stay inside the previous level's padded plane);
