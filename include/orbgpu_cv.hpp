@@ -8,10 +8,11 @@
  *     #include "orbgpu_cv.hpp"
  *     namespace ORB_SLAM3 { using ORBextractor = orbgpu::ORBextractor; }
  *
- * Needs OpenCV (core) and liborbgpu.so at link time.  mvImagePyramid is filled on demand
- * (SyncPyramid()) because only Frame::ComputeStereoMatches reads it (src/Frame.cc:1126,1249);
- * the levels are views into padded planes, like the reference's (src/ORBextractor.cc:1695-1697),
- * so the 19-pixel border stays readable.
+ * Needs OpenCV (core) and liborbgpu.so at link time.  mvImagePyramid is downloaded on first
+ * access after each extraction: only Frame::ComputeStereoMatches reads it (src/Frame.cc:1126,
+ * 1249,1268,1275, always through operator[]), so tracking without stereo never pays the copy and
+ * the caller compiles unchanged.  The levels are views into padded planes, like the reference's
+ * (src/ORBextractor.cc:1695-1697), so the 19-pixel border stays readable.
  */
 #ifndef ORBGPU_CV_HPP
 #define ORBGPU_CV_HPP
@@ -25,6 +26,27 @@
 #include "orbgpu.h"
 
 namespace orbgpu {
+
+class ORBextractor;
+
+// std::vector<cv::Mat>-like view of the last frame's pyramid that downloads it from the device on
+// the first operator[] after an extraction (the reference member is a plain vector, include/
+// ORBextractor.h:83; its readers use only operator[], size() and iteration).
+class LazyPyramid {
+public:
+    explicit LazyPyramid(ORBextractor* owner) : owner_(owner) {}
+    cv::Mat& operator[](size_t l);
+    const cv::Mat& operator[](size_t l) const { return const_cast<LazyPyramid*>(this)->operator[](l); }
+    size_t size() const { return levels_.size(); }
+    void resize(size_t n) { levels_.resize(n); }
+    std::vector<cv::Mat>::iterator begin();
+    std::vector<cv::Mat>::iterator end() { return levels_.end(); }
+
+private:
+    friend class ORBextractor;
+    ORBextractor* owner_;
+    std::vector<cv::Mat> levels_;
+};
 
 class ORBextractor {
 public:
@@ -45,6 +67,8 @@ public:
                              mvInvLevelSigma2_.data(), per.data());
         mvImagePyramid.resize(nlevels);
     }
+    // mvImagePyramid refers back to this object
+    ORBextractor(ORBextractor&&) = delete;
     ~ORBextractor() { orb_extractor_destroy(h_); }
     ORBextractor(const ORBextractor&) = delete;
     ORBextractor& operator=(const ORBextractor&) = delete;
@@ -85,7 +109,8 @@ public:
     std::vector<float> inline GetScaleSigmaSquares() { return mvLevelSigma2_; }
     std::vector<float> inline GetInverseScaleSigmaSquares() { return mvInvLevelSigma2_; }
 
-    // Download the pyramid of the last frame into mvImagePyramid (call before reading it).
+    // Download the pyramid of the last frame into mvImagePyramid.  mvImagePyramid[l] calls this
+    // itself; an explicit call only moves the copy to a chosen point.
     void SyncPyramid() {
         if (!pyramidStale_) return;
         for (int l = 0; l < nlevels_; ++l) {
@@ -94,12 +119,12 @@ public:
                 throw std::runtime_error(std::string("orb_extractor_level: ") + orb_last_error());
             padded_[l].create(h + 38, w + 38, CV_8U);
             orb_extractor_level_download(h_, 0, l, padded_[l].data);
-            mvImagePyramid[l] = padded_[l](cv::Rect(19, 19, w, h));
+            mvImagePyramid.levels_[l] = padded_[l](cv::Rect(19, 19, w, h));
         }
         pyramidStale_ = false;
     }
 
-    std::vector<cv::Mat> mvImagePyramid;
+    LazyPyramid mvImagePyramid{this};
 
     // the underlying handle, for the device-side consumers of the pyramid (orb_compute_stereo_matches)
     orb_extractor_t handle() const { return h_; }
@@ -115,6 +140,15 @@ private:
     cv::Mat padded_[12];
     std::vector<float> mvScaleFactor_, mvInvScaleFactor_, mvLevelSigma2_, mvInvLevelSigma2_;
 };
+
+inline cv::Mat& LazyPyramid::operator[](size_t l) {
+    owner_->SyncPyramid();
+    return levels_[l];
+}
+inline std::vector<cv::Mat>::iterator LazyPyramid::begin() {
+    owner_->SyncPyramid();
+    return levels_.begin();
+}
 
 }  // namespace orbgpu
 

@@ -87,6 +87,17 @@ def test_matcher_shim_on_mock_objects():
     assert r.returncode == 0 and "OK matcher_shim_check" in r.stdout, r.stdout + r.stderr
 
 
+def test_extractor_shim_on_mock_opencv():
+    """include/orbgpu_cv.hpp (ORBextractor drop-in) compiled against a minimal OpenCV stand-in
+    (tests/native/mock_cv) and ABI test doubles: parameters, getters, keypoint / descriptor conversion,
+    the capacity retry, errors, and mvImagePyramid downloaded lazily on the first operator[]."""
+    exe = _compile(ROOT / "tests" / "native" / "cv_shim_check.cpp", BUILD / "cv_shim_check",
+                   ("-I" + str(ROOT / "include"), "-I" + str(ROOT / "tests" / "native" / "mock_cv"),
+                    "-Wall", "-Werror"))
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "OK cv_shim_check" in r.stdout, r.stdout + r.stderr
+
+
 @pytest.mark.slow
 def test_sincos_exception_table_exhaustive():
     """All 1,135,869,952 float angles in [0, 360): deterministic sincos + table == glibc offsets."""
