@@ -1907,6 +1907,7 @@ struct Extractor {
     // sub-batching over internal streams
     static constexpr int kMaxStreams = 4;
     int chunk = 1 << 30, nstreams = 1;  // off by default: measured slower (streams did not overlap)
+    bool fast_stamps = false, pyr_stamps = false;  // debug phase clocks (ORBGPU_FAST_STAMPS / _PYR_STAMPS)
     int fast_split = 3;                 // FAST on levels [0, fast_split) overlaps the small pyramid levels
     int fast_per_level = 0;             // 1: FAST of each later level right after its pyramid level (side2); measured slower
     int desc_split = 1;                 // 1: quad-tree + descriptors of levels [0, fast_split) on the side stream (ORBGPU_DESC_SPLIT)
@@ -2111,7 +2112,7 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     // overlapping the latency-bound launches of the small levels (k.lv[split..] ) on `st`.
     // (a single frame runs as one chain: too few blocks per level for the overlap to pay)
     const int split = (n > 1 && e->fast_split > 0 && e->fast_split < k.nlevels) ? e->fast_split : 0;
-    static const bool fast_stamps = getenv("ORBGPU_FAST_STAMPS") != nullptr;
+    const bool fast_stamps = e->fast_stamps;
     auto launch_fast = [&](int l0, int l1, hipStream_t s2) {
         const int c0 = k.lv[l0].cell_begin, c1 = k.lv[l1 - 1].cell_begin + k.lv[l1 - 1].cell_count;
         if (c1 <= c0) return;
@@ -2174,7 +2175,7 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     // the early levels' FAST (and with desc_split their quad-tree + descriptors) go to the side stream
     desc_split = e->desc_split && split > 0 && !e->fast_per_level && e->d_st_kp;
     const bool qts = (e->qt_split || desc_split) && split > 0 && !e->fast_per_level;
-    static const bool pyr_stamps = getenv("ORBGPU_PYR_STAMPS") != nullptr;
+    const bool pyr_stamps = e->pyr_stamps;
     for (int l = 0; l < k.nlevels; ++l) {
         const orbgpu::LevelGeom& L = k.lv[l];
         PyrArgs A{};
@@ -2344,6 +2345,8 @@ int orb_extractor_create(const orb_params_t* p, int max_width, int max_height, i
     if (const char* c = getenv("ORBGPU_FAST_PER_LEVEL")) e->fast_per_level = atoi(c);
     if (const char* c = getenv("ORBGPU_QT_SPLIT")) e->qt_split = atoi(c);
     if (const char* c = getenv("ORBGPU_DESC_SPLIT")) e->desc_split = atoi(c);
+    e->fast_stamps = getenv("ORBGPU_FAST_STAMPS") != nullptr;
+    e->pyr_stamps = getenv("ORBGPU_PYR_STAMPS") != nullptr;
     for (int s = 0; s < Extractor::kMaxStreams && ok; ++s)
         ok = hipStreamCreateWithFlags(&e->sub[s], hipStreamNonBlocking) == hipSuccess &&
              hipEventCreateWithFlags(&e->join_ev[s], hipEventDisableTiming) == hipSuccess;

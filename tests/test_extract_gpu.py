@@ -261,8 +261,9 @@ def test_sparse_corners_parity(pkg, oracle):
 
 
 @pytest.mark.parametrize("env", [{"ORBGPU_CHUNK": "2"}, {"ORBGPU_STREAMS": "2", "ORBGPU_CHUNK": "3"},
-                                 {"ORBGPU_FAST_SPLIT": "3"}, {"ORBGPU_FAST_PER_LEVEL": "1"}, {"ORBGPU_QT_SPLIT": "1"}],
-                         ids=["chunk2", "streams2_chunk3", "fast_split3", "fast_per_level", "qt_split"])
+                                 {"ORBGPU_FAST_SPLIT": "3"}, {"ORBGPU_FAST_PER_LEVEL": "1"}, {"ORBGPU_QT_SPLIT": "1"},
+                                 {"ORBGPU_FAST_STAMPS": "1", "ORBGPU_PYR_STAMPS": "1"}],
+                         ids=["chunk2", "streams2_chunk3", "fast_split3", "fast_per_level", "qt_split", "phase_stamps"])
 def test_schedule_switches_parity(pkg, oracle, synth, monkeypatch, env):
     """Every per-handle schedule switch (read when the handle is created; orb_extract.hip
     orb_extractor_create) changes only how the batch is cut into launches and streams: a 7-frame batch

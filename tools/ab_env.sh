@@ -12,5 +12,5 @@ import json
 for tag in ("base", "var"):
     for i in (1, 2):
         d = json.load(open(f"gpurun_out/ab_{tag}{i}.json"))
-        print(tag, i, d["value"], d["ms_per_step"], d["stages_ms"])
+        print(tag, i, d["value"], d["ms_per_step"], d["stages_ms"], d["roofline"]["launch_avg_us"])
 PY
