@@ -9,9 +9,12 @@
 //   best = min, idx = the first index attaining it, second = the second smallest of the multiset
 // so partial results over consecutive train ranges merge exactly:
 //   best = min(b1, b2), idx = b1 <= b2 ? i1 : i2 (range 1 first), second = min(max(b1, b2), s1, s2).
-// The launch is cut two ways so that one frame (~1000 queries) fills the chip: 64-query tiles (one
-// query per lane) x train chunks; the four waves of a block scan quarters of the block's chunk (staged
-// in LDS, read as broadcasts) and merge in wave order; chunks merge in chunk order in a second kernel.
+// 64-query tiles (one query per lane); the waves of a block scan consecutive parts of the block's train
+// range (staged in LDS, read as broadcasts) and merge in wave order.  A train set that fits one block's
+// LDS (<= 1024 descriptors, a frame) is one launch of 16-wave blocks writing the results directly: a
+// frame-sized call is launch-latency bound, so a second (merge) launch and its partial buffer cost more
+// than the parallelism they buy.  Larger train sets are cut into chunks as well (4-wave blocks, enough
+// to fill the chip) whose partials merge in chunk order in a second kernel.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -23,7 +26,8 @@
 
 namespace {
 
-constexpr int kKnnWaves = 4, kKnnThreads = 64 * kKnnWaves;
+constexpr int kKnnWaves = 4, kKnnThreads = 64 * kKnnWaves;  // chunked launch
+constexpr int kKnnWaves1 = 16;                               // single-launch (one chunk) blocks
 constexpr int kKnnMaxChunk = 1024;  // train descriptors per block (32 KiB of LDS)
 constexpr int kKnnMinChunk = 64;
 constexpr int kKnnTargetBlocks = 1024;
@@ -55,24 +59,25 @@ __device__ __forceinline__ Knn knn_merge(const Knn& a, const Knn& b) {
 
 // grid (query tiles, chunks).  nchunk == 1: the block writes the final result; otherwise its partial
 // goes to part[(chunk * nq + query)].
-__global__ __launch_bounds__(kKnnThreads) void k_hamming_knn2(const uint8_t* __restrict__ q, int nq,
+template <int kW>
+__global__ __launch_bounds__(64 * kW) void k_hamming_knn2(const uint8_t* __restrict__ q, int nq,
                                                               const uint8_t* __restrict__ t, int nt, int chunk,
                                                               Knn* __restrict__ part, int32_t* __restrict__ best_idx,
                                                               int32_t* __restrict__ best_dist,
                                                               int32_t* __restrict__ second_dist) {
     __shared__ uint4 tile[kKnnMaxChunk * 2];
-    __shared__ Knn wpart[kKnnWaves - 1][64];
+    __shared__ Knn wpart[kW - 1][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int qi = blockIdx.x * 64 + lane;
     const int c0 = blockIdx.y * chunk, n = min(chunk, nt - c0);
-    for (int i = threadIdx.x; i < 2 * n; i += kKnnThreads) tile[i] = reinterpret_cast<const uint4*>(t)[2 * (size_t)c0 + i];
+    for (int i = threadIdx.x; i < 2 * n; i += 64 * kW) tile[i] = reinterpret_cast<const uint4*>(t)[2 * (size_t)c0 + i];
     uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
     if (qi < nq) {
         a0 = reinterpret_cast<const uint4*>(q)[2 * (size_t)qi];
         a1 = reinterpret_cast<const uint4*>(q)[2 * (size_t)qi + 1];
     }
     __syncthreads();
-    const int sub = (n + kKnnWaves - 1) / kKnnWaves, j0 = w * sub, j1 = min(n, j0 + sub);
+    const int sub = (n + kW - 1) / kW, j0 = w * sub, j1 = min(n, j0 + sub);
     Knn r{257, 257, -1};
     for (int j = j0; j < j1; ++j) {
         const int d = hamming256(a0, a1, tile[2 * j], tile[2 * j + 1]);
@@ -83,7 +88,7 @@ __global__ __launch_bounds__(kKnnThreads) void k_hamming_knn2(const uint8_t* __r
     __syncthreads();
     if (w != 0 || qi >= nq) return;
 #pragma unroll
-    for (int k = 0; k < kKnnWaves - 1; ++k) r = knn_merge(r, wpart[k][lane]);
+    for (int k = 0; k < kW - 1; ++k) r = knn_merge(r, wpart[k][lane]);
     if (part) {
         part[(size_t)blockIdx.y * nq + qi] = r;
     } else {
@@ -118,6 +123,12 @@ extern "C" int orb_hamming_knn2_device(const uint8_t* d_query, int n_query, cons
         return orbgpu_fail(ORB_ERR_ARG, "descriptor arrays must be 16-byte aligned");
     hipStream_t s = (hipStream_t)stream;
     const int qtiles = (n_query + 63) / 64;
+    if (n_train <= kKnnMaxChunk) {  // one chunk: a single launch, results written by the blocks
+        hipLaunchKernelGGL(k_hamming_knn2<kKnnWaves1>, dim3(qtiles, 1), dim3(64 * kKnnWaves1), 0, s, d_query, n_query,
+                           d_train, n_train, std::max(n_train, 1), (Knn*)nullptr, d_best_idx, d_best_dist, d_second_dist);
+        if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "hamming launch failed");
+        return ORB_OK;
+    }
     // chunks: enough blocks to fill the chip, at least kKnnMinChunk descriptors per block, at most
     // what one block stages in LDS
     int nchunk = std::max(1, std::min((kKnnTargetBlocks + qtiles - 1) / qtiles, (n_train + kKnnMinChunk - 1) / kKnnMinChunk));
@@ -132,7 +143,7 @@ extern "C" int orb_hamming_knn2_device(const uint8_t* d_query, int n_query, cons
     if (nchunk > 1 &&
         hipMallocAsync(reinterpret_cast<void**>(&part), sizeof(Knn) * (size_t)nchunk * n_query, s) != hipSuccess)
         return orbgpu_fail(ORB_ERR_DEVICE, "knn2 partial buffer");
-    hipLaunchKernelGGL(k_hamming_knn2, dim3(qtiles, nchunk), dim3(kKnnThreads), 0, s, d_query, n_query, d_train, n_train,
+    hipLaunchKernelGGL(k_hamming_knn2<kKnnWaves>, dim3(qtiles, nchunk), dim3(kKnnThreads), 0, s, d_query, n_query, d_train, n_train,
                        chunk, part, d_best_idx, d_best_dist, d_second_dist);
     if (part) {
         hipLaunchKernelGGL(k_hamming_knn2_merge, dim3((n_query + 255) / 256), dim3(256), 0, s, n_query, nchunk, part,

@@ -168,7 +168,8 @@ def test_hamming_knn2(pkg, oracle):
     assert idx[3] == 5 and d1[3] == 0 and d2[3] == 0
 
 
-@pytest.mark.parametrize("nq,nt", [(1000, 1000), (37, 70000), (5, 0), (130, 3)], ids=["frame", "big_train", "empty", "tiny"])
+@pytest.mark.parametrize("nq,nt", [(1000, 1000), (37, 70000), (5, 0), (130, 3), (100, 1024), (100, 1025)],
+                         ids=["frame", "big_train", "empty", "tiny", "one_block_max", "two_chunks"])
 def test_hamming_knn2_split_merge(pkg, nq, nt):
     """The train split (chunks merged in order) equals the sequential scan, ties across chunk
     boundaries included: every query's exact copy is planted at several train positions."""
