@@ -492,6 +492,35 @@ def bench_matchers(pkg, synth, dev, steps, cpu_baseline_on):
                                "sample": f"10 scans of the same 1000 x 1000 set, oracle_hamming_knn2 "
                                          f"(oracle/orb_matcher_oracle.cpp, popcount scan), {ORACLE_FLAGS}"}
     out["knn2"] = knn
+    # ---- MapPoint::ComputeDistinctiveDescriptors batched over the map points LocalMapping updates after
+    # a keyframe (new and fused points, src/LocalMapping.cc:416,901,1054): 2000 points of 2-12 observations
+    rng = np.random.default_rng(7)
+    nobs = rng.integers(2, 13, 2000).astype(np.int32)
+    offs = np.concatenate([[0], np.cumsum(nobs)]).astype(np.int32)
+    dd = rng.integers(0, 256, (int(offs[-1]), 32), dtype=np.uint8)
+    best_h, _ = ml.ComputeDistinctiveDescriptors(dd, offs)
+    ms = _median_ms(lambda: ml.ComputeDistinctiveDescriptors(dd, offs), reps)
+    d_dd, d_offs = torch.from_numpy(dd).to(dev), torch.from_numpy(offs).to(dev)
+    d_out = torch.zeros((2000, 32), dtype=torch.uint8, device=dev)
+    with torch.cuda.stream(st):
+        for _ in range(3):
+            pkg.ORBmatcher.compute_distinctive_descriptors_device(d_dd, d_offs, out=d_out, stream=st)
+        e0.record(st)
+        for _ in range(reps):
+            pkg.ORBmatcher.compute_distinctive_descriptors_device(d_dd, d_offs, out=d_out, stream=st)
+        e1.record(st)
+    torch.cuda.synchronize(dev)
+    dist = {"config": f"2000 map points, 2-12 observations each ({int(offs[-1])} descriptors), host arrays in/out "
+                      f"(synchronous, as LocalMapping calls it); device_us_per_batch: the same batch device-resident, async",
+            "ms_per_batch": round(ms, 4), "device_us_per_batch": round(e0.elapsed_time(e1) / reps * 1e3, 1)}
+    if cpu_baseline_on:
+        ob = oracle_mod.compute_distinctive_descriptors(dd, offs)
+        assert np.array_equal(ob, best_h), "ComputeDistinctiveDescriptors differs from the oracle"
+        cms = _median_ms(lambda: oracle_mod.compute_distinctive_descriptors(dd, offs), 10)
+        dist["cpu_baseline"] = {"value": round(cms, 4), "unit": "ms/batch", "cores": 1, "kind": "port",
+                                "sample": f"10 batches of the same 2000 points, oracle_compute_distinctive_descriptors "
+                                          f"(oracle/orb_matcher_oracle.cpp), {ORACLE_FLAGS}"}
+    out["compute_distinctive_descriptors"] = dist
     return out
 
 

@@ -161,9 +161,63 @@ extern "C" int orb_hamming_knn2_device(const uint8_t* d_query, int n_query, cons
 // median.  One wave per point: lane i computes row i's distances on the fly into a lane-private
 // 257-bin u16 histogram in LDS (hist[bin][lane]), then walks the histogram to the
 // median; the wave reduces (median, i) lexicographically (first index on ties).  Rows beyond 64 are
-// taken 64 at a time.
+// taken 64 at a time.  That kernel serves only points of more than 64 observations: the usual point
+// (a few to a few dozen observations) goes to k_distinctive_wave, which needs no LDS at all.
 namespace {
 constexpr int kDdBins = 257;
+constexpr int kDdWaveMax = 64;  // k_distinctive_wave: observations per point
+
+// Points of at most 64 observations.  Lane j holds descriptor j.  For each row i, in order, row i's
+// descriptor is broadcast (v_readlane), every lane computes d_ij, and the row's k-th smallest distance
+// is found by a 9-step radix select over wave ballots (d <= 256): at each bit, the candidates with a 0
+// there number nz; k < nz keeps them, otherwise k -= nz and the prefix takes a 1.  The first row with
+// the smallest median wins (strict <, rows in order), as src/MapPoint.cc:509-517 does.
+__global__ __launch_bounds__(64) void k_distinctive_wave(const uint4* __restrict__ desc, const int32_t* __restrict__ off,
+                                                         int n_points, int32_t* __restrict__ best,
+                                                         uint4* __restrict__ out) {
+    const int p = blockIdx.x, lane = threadIdx.x;
+    const int o = off[p], N = off[p + 1] - o;
+    if (N <= 0) {
+        if (lane == 0) best[p] = -1;
+        return;
+    }
+    if (N > kDdWaveMax) return;  // k_distinctive
+    const int k = (int)(0.5 * (double)(N - 1));  // vDists[0.5*(N-1)]: the size_t index truncates
+    const bool act = lane < N;
+    uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
+    if (act) {
+        a0 = desc[2 * (size_t)(o + lane)];
+        a1 = desc[2 * (size_t)(o + lane) + 1];
+    }
+    const unsigned long long live = __ballot(act);
+    int bmed = 1 << 30, bi = 0;
+    for (int i = 0; i < N; ++i) {
+        const auto rl = [i](unsigned v) { return (unsigned)__builtin_amdgcn_readlane((int)v, i); };
+        const uint4 r0 = make_uint4(rl(a0.x), rl(a0.y), rl(a0.z), rl(a0.w));
+        const uint4 r1 = make_uint4(rl(a1.x), rl(a1.y), rl(a1.z), rl(a1.w));
+        const int d = hamming256(a0, a1, r0, r1);
+        int kk = k, med = 0;
+        unsigned long long cand = live;
+#pragma unroll
+        for (int bit = 8; bit >= 0; --bit) {
+            const unsigned long long zeros = cand & __ballot(((d >> bit) & 1) == 0);
+            const int nz = __popcll(zeros);
+            if (kk < nz) {
+                cand = zeros;
+            } else {
+                kk -= nz;
+                cand &= ~zeros;
+                med |= 1 << bit;
+            }
+        }
+        if (med < bmed) {
+            bmed = med;
+            bi = i;
+        }
+    }
+    if (lane == 0) best[p] = bi;
+    if (lane < 2) out[2 * (size_t)p + lane] = desc[2 * (size_t)(o + bi) + lane];
+}
 
 __global__ __launch_bounds__(64) void k_distinctive(const uint4* __restrict__ desc, const int32_t* __restrict__ off,
                                                     int n_points, int32_t* __restrict__ best,
@@ -171,10 +225,7 @@ __global__ __launch_bounds__(64) void k_distinctive(const uint4* __restrict__ de
     __shared__ uint16_t hist[kDdBins * 64];
     const int p = blockIdx.x, lane = threadIdx.x;
     const int o = off[p], N = off[p + 1] - o;
-    if (N <= 0) {
-        if (lane == 0) best[p] = -1;
-        return;
-    }
+    if (N <= kDdWaveMax) return;  // k_distinctive_wave (empty points included)
     const int k = (int)(0.5 * (double)(N - 1));  // vDists[0.5*(N-1)]: the size_t index truncates
     unsigned long long bestkey = ~0ull;
     for (int i0 = 0; i0 < N; i0 += 64) {
@@ -216,6 +267,8 @@ extern "C" int orb_compute_distinctive_descriptors_device(const uint8_t* d_desc,
     if (n_points == 0) return ORB_OK;
     if ((reinterpret_cast<uintptr_t>(d_desc) | reinterpret_cast<uintptr_t>(d_out)) & 15)
         return orbgpu_fail(ORB_ERR_ARG, "descriptor arrays must be 16-byte aligned");
+    hipLaunchKernelGGL(k_distinctive_wave, dim3(n_points), dim3(64), 0, (hipStream_t)stream, (const uint4*)d_desc,
+                       d_offsets, n_points, d_best, (uint4*)d_out);
     hipLaunchKernelGGL(k_distinctive, dim3(n_points), dim3(64), 0, (hipStream_t)stream, (const uint4*)d_desc, d_offsets,
                        n_points, d_best, (uint4*)d_out);
     if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "distinctive descriptors launch failed");
@@ -242,8 +295,13 @@ extern "C" int orb_compute_distinctive_descriptors(orb_matcher_t m, const uint8_
     if (nd) memcpy(h + o_d, desc, nd * 32);
     memcpy(h + o_off, offsets, (size_t)(n_points + 1) * 4);
     bool ok = hipMemcpyAsync(d, h, o_best, hipMemcpyHostToDevice, s) == hipSuccess;
-    if (ok) hipLaunchKernelGGL(k_distinctive, dim3(n_points), dim3(64), 0, s, (const uint4*)(d + o_d),
+    int max_n = 0;
+    for (int p = 0; p < n_points; ++p) max_n = std::max(max_n, offsets[p + 1] - offsets[p]);
+    if (ok) hipLaunchKernelGGL(k_distinctive_wave, dim3(n_points), dim3(64), 0, s, (const uint4*)(d + o_d),
                                (const int32_t*)(d + o_off), n_points, (int32_t*)(d + o_best), (uint4*)(d + o_out));
+    if (ok && max_n > kDdWaveMax)  // points of more than 64 observations
+        hipLaunchKernelGGL(k_distinctive, dim3(n_points), dim3(64), 0, s, (const uint4*)(d + o_d),
+                           (const int32_t*)(d + o_off), n_points, (int32_t*)(d + o_best), (uint4*)(d + o_out));
     ok = ok && hipGetLastError() == hipSuccess &&
          hipMemcpyAsync(h + o_best, d + o_best, total - o_best, hipMemcpyDeviceToHost, s) == hipSuccess &&
          hipStreamSynchronize(s) == hipSuccess;
