@@ -1,4 +1,4 @@
-"""The C3 matcher calls of bench.py's `matchers` section, 50 times each, for rocprofv3 kernel traces:
+"""The matcher calls of bench.py's `matchers` section (C3 calls, knn2, ComputeDistinctiveDescriptors), 50 times each, for rocprofv3 kernel traces:
     rocprofv3 --kernel-trace --stats -d OUT -o m -- python3 tools/matcher_time.py
 Prints the host-side median per call."""
 import pathlib
@@ -36,3 +36,12 @@ print("SBP frame ms", med(lambda: mp.SearchByProjectionFrame(C, L, 7, False)), f
 P = pkg.LocalMapPoints(**synth.local_map_points(cur, n_points=3000, seed=151))
 ml = pkg.ORBmatcher(0.8, True)
 print("SBP local ms", med(lambda: ml.SearchByProjection(C, P, 3, False, 50.0)), flush=True)
+rng = np.random.default_rng(5)
+import torch  # noqa: E402
+q = torch.from_numpy(rng.integers(0, 256, (1000, 32), dtype=np.uint8)).cuda()
+t = torch.from_numpy(rng.integers(0, 256, (1000, 32), dtype=np.uint8)).cuda()
+print("knn2 ms", med(lambda: (pkg.ORBmatcher.knn2_device(q, t), torch.cuda.synchronize())), flush=True)
+nobs = rng.integers(2, 13, 2000).astype(np.int32)
+offs = np.concatenate([[0], np.cumsum(nobs)]).astype(np.int32)
+dd = rng.integers(0, 256, (int(offs[-1]), 32), dtype=np.uint8)
+print("distinctive ms", med(lambda: ml.ComputeDistinctiveDescriptors(dd, offs)), flush=True)
