@@ -9,12 +9,13 @@
 //   best = min, idx = the first index attaining it, second = the second smallest of the multiset
 // so partial results over consecutive train ranges merge exactly:
 //   best = min(b1, b2), idx = b1 <= b2 ? i1 : i2 (range 1 first), second = min(max(b1, b2), s1, s2).
-// 64-query tiles (one query per lane); the waves of a block scan consecutive parts of the block's train
-// range (staged in LDS, read as broadcasts) and merge in wave order.  A train set that fits one block's
-// LDS (<= 1024 descriptors, a frame) is one launch of 16-wave blocks writing the results directly: a
-// frame-sized call is launch-latency bound, so a second (merge) launch and its partial buffer cost more
-// than the parallelism they buy.  Larger train sets are cut into chunks as well (4-wave blocks, enough
-// to fill the chip) whose partials merge in chunk order in a second kernel.
+// A train set that fits one block's LDS (<= 1024 descriptors, a frame) is one launch that writes the
+// results directly (k_hamming_knn2_frame: 16 queries per block, the train set cut into 64 parts merged
+// in order in LDS): a frame-sized call is latency bound, so a second (merge) launch and its partial
+// buffer cost more than they buy.  Larger train sets: 64-query tiles (one query per lane) x train
+// chunks (enough blocks to fill the chip); the waves of a block scan consecutive parts of the chunk
+// (staged in LDS, read as broadcasts) and merge in wave order, and the chunks' partials merge in chunk
+// order in a second kernel.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -27,7 +28,6 @@
 namespace {
 
 constexpr int kKnnWaves = 4, kKnnThreads = 64 * kKnnWaves;  // chunked launch
-constexpr int kKnnWaves1 = 16;                               // single-launch (one chunk) blocks
 constexpr int kKnnMaxChunk = 1024;  // train descriptors per block (32 KiB of LDS)
 constexpr int kKnnMinChunk = 64;
 constexpr int kKnnTargetBlocks = 1024;
@@ -98,6 +98,56 @@ __global__ __launch_bounds__(64 * kW) void k_hamming_knn2(const uint8_t* __restr
     }
 }
 
+// Frame-sized train sets (<= kKnnMaxChunk): 16 queries per 1024-thread block and the train set cut
+// into 64 consecutive parts, so each lane scans ~16 rows instead of a whole chunk.  Lane l of wave w
+// takes query 16 blockIdx.x + (l & 15) and part 4 w + (l >> 4).  The 64 partials of a query merge in
+// part order by an adjacent-pair tree in LDS (knn_merge is associative over consecutive ranges).
+constexpr int kKnnQ = 16, kKnnParts = 64;
+__global__ __launch_bounds__(1024) void k_hamming_knn2_frame(const uint8_t* __restrict__ q, int nq,
+                                                             const uint8_t* __restrict__ t, int nt,
+                                                             int32_t* __restrict__ best_idx,
+                                                             int32_t* __restrict__ best_dist,
+                                                             int32_t* __restrict__ second_dist) {
+    __shared__ uint4 tile[kKnnMaxChunk * 2];
+    __shared__ Knn red[kKnnParts][kKnnQ];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int ql = lane & (kKnnQ - 1), part = 4 * w + (lane >> 4);
+    const int qi = blockIdx.x * kKnnQ + ql;
+    for (int i = threadIdx.x; i < 2 * nt; i += 1024) tile[i] = reinterpret_cast<const uint4*>(t)[i];
+    uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
+    if (qi < nq) {
+        a0 = reinterpret_cast<const uint4*>(q)[2 * (size_t)qi];
+        a1 = reinterpret_cast<const uint4*>(q)[2 * (size_t)qi + 1];
+    }
+    __syncthreads();
+    const int sub = (nt + kKnnParts - 1) / kKnnParts, j0 = part * sub, j1 = min(nt, j0 + sub);
+    Knn r{257, 257, -1};
+    for (int j = j0; j < j1; ++j) {
+        const int d = hamming256(a0, a1, tile[2 * j], tile[2 * j + 1]);
+        if (d < r.best) { r.second = r.best; r.best = d; r.idx = j; }
+        else if (d < r.second) r.second = d;
+    }
+    red[part][ql] = r;
+    __syncthreads();
+#pragma unroll
+    for (int s = 1; s < kKnnParts; s <<= 1) {
+        if ((int)threadIdx.x < (kKnnParts / (2 * s)) * kKnnQ) {
+            const int p = (threadIdx.x / kKnnQ) * 2 * s, qq = threadIdx.x & (kKnnQ - 1);
+            red[p][qq] = knn_merge(red[p][qq], red[p + s][qq]);
+        }
+        __syncthreads();
+    }
+    if ((int)threadIdx.x < kKnnQ) {
+        const int qo = blockIdx.x * kKnnQ + threadIdx.x;
+        if (qo < nq) {
+            const Knn f = red[0][threadIdx.x];
+            best_idx[qo] = f.idx;
+            best_dist[qo] = f.best;
+            second_dist[qo] = f.second;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_hamming_knn2_merge(int nq, int nchunk, const Knn* __restrict__ part,
                                                             int32_t* __restrict__ best_idx, int32_t* __restrict__ best_dist,
                                                             int32_t* __restrict__ second_dist) {
@@ -124,8 +174,8 @@ extern "C" int orb_hamming_knn2_device(const uint8_t* d_query, int n_query, cons
     hipStream_t s = (hipStream_t)stream;
     const int qtiles = (n_query + 63) / 64;
     if (n_train <= kKnnMaxChunk) {  // one chunk: a single launch, results written by the blocks
-        hipLaunchKernelGGL(k_hamming_knn2<kKnnWaves1>, dim3(qtiles, 1), dim3(64 * kKnnWaves1), 0, s, d_query, n_query,
-                           d_train, n_train, std::max(n_train, 1), (Knn*)nullptr, d_best_idx, d_best_dist, d_second_dist);
+        hipLaunchKernelGGL(k_hamming_knn2_frame, dim3((n_query + kKnnQ - 1) / kKnnQ), dim3(1024), 0, s, d_query, n_query,
+                           d_train, n_train, d_best_idx, d_best_dist, d_second_dist);
         if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "hamming launch failed");
         return ORB_OK;
     }
