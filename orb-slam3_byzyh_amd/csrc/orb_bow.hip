@@ -62,21 +62,39 @@ __global__ __launch_bounds__(256) void k_bow_descend(const int32_t* __restrict__
     const int nid_level = L - levelsup;
     int node_at = nid_level <= 0 ? 0 : -1;
     int final_id = 0, level = 0;
-    do {
+    // Children are visited in groups of kGroup: the group's child ids are loaded together, then their
+    // descriptors together, so a level costs two dependent round trips per group instead of two per
+    // child.  Within a group the comparisons still run in child order (first minimum kept).
+    constexpr int kGroup = 8;
+    int cb = child_begin[0], ce = child_begin[1];
+    while (ce > cb && level < 64) {
         ++level;
-        const int cb = child_begin[final_id], ce = child_begin[final_id + 1];
-        final_id = child_idx[cb];
-        int best_d = hamming256(a0, a1, D[2 * (size_t)final_id], D[2 * (size_t)final_id + 1]);
-        for (int c = cb + 1; c < ce; ++c) {
-            const int id = child_idx[c];
-            const int d = hamming256(a0, a1, D[2 * (size_t)id], D[2 * (size_t)id + 1]);
-            if (d < best_d) {  // first minimum (the reference compares doubles of these ints)
-                best_d = d;
-                final_id = id;
+        int best_d = 1 << 30, best_id = -1;
+        for (int g = cb; g < ce; g += kGroup) {
+            int ids[kGroup];
+#pragma unroll
+            for (int u = 0; u < kGroup; ++u) ids[u] = g + u < ce ? child_idx[g + u] : -1;
+            uint4 b0[kGroup], b1[kGroup];
+#pragma unroll
+            for (int u = 0; u < kGroup; ++u) {
+                const size_t o = 2 * (size_t)(ids[u] < 0 ? 0 : ids[u]);
+                b0[u] = D[o];
+                b1[u] = D[o + 1];
+            }
+#pragma unroll
+            for (int u = 0; u < kGroup; ++u) {
+                const int d = hamming256(a0, a1, b0[u], b1[u]);
+                if (ids[u] >= 0 && d < best_d) {  // first minimum (the reference compares doubles of these ints)
+                    best_d = d;
+                    best_id = ids[u];
+                }
             }
         }
+        final_id = best_id;
         if (level == nid_level) node_at = final_id;
-    } while (child_begin[final_id + 1] > child_begin[final_id] && level < 64);
+        cb = child_begin[final_id];
+        ce = child_begin[final_id + 1];
+    }
     word[i] = word_id[final_id];
     w[i] = weight[final_id];
     nid[i] = node_at < 0 ? final_id : node_at;  // leaf above level L - levelsup: the leaf (see oracle)
