@@ -101,6 +101,46 @@ __global__ __launch_bounds__(256) void k_bow_descend(const int32_t* __restrict__
 }
 
 __device__ void bitonic_sort(unsigned long long* keys, int P) {
+    if (P <= kAggThreads) {
+        // One key per thread (position tid).  The stages with partner distance j < 64 stay inside a
+        // wave: the pair is exchanged by a lane shuffle and each side keeps its element of the
+        // compare-swap (the lower position the minimum when ascending), with no LDS round trip or
+        // barrier; only the stages with j >= 64 go through LDS.  Same network, same result.
+        const int i = threadIdx.x;
+        unsigned long long key = i < P ? keys[i] : 0ull;
+        for (int k = 2; k <= P; k <<= 1) {
+            int j = k >> 1;
+            if (j >= 64) {
+                if (i < P) keys[i] = key;
+                __syncthreads();
+                for (; j >= 64; j >>= 1) {
+                    if (i < P) {
+                        const int ixj = i ^ j;
+                        if (ixj > i) {
+                            const unsigned long long a = keys[i], b = keys[ixj];
+                            if ((a > b) == ((i & k) == 0)) {
+                                keys[i] = b;
+                                keys[ixj] = a;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                }
+                if (i < P) key = keys[i];
+            }
+            const bool up = (i & k) == 0;
+            for (; j > 0; j >>= 1) {
+                const unsigned long long other = __shfl_xor(key, j, 64);
+                const bool lower = (i & j) == 0;
+                const unsigned long long lo = key < other ? key : other, hi = key < other ? other : key;
+                key = (lower == up) ? lo : hi;
+            }
+        }
+        __syncthreads();  // every read of the LDS stage is done before the write-back
+        if (i < P) keys[i] = key;
+        __syncthreads();
+        return;
+    }
     for (int k = 2; k <= P; k <<= 1)
         for (int j = k >> 1; j > 0; j >>= 1) {
             for (int i = threadIdx.x; i < P; i += kAggThreads) {
