@@ -91,11 +91,14 @@ int orb_extract_batch_device(orb_extractor_t h, const uint8_t* d_images, int n, 
 
 /* mvImagePyramid[level] of frame `frame` of the last call (include/ORBextractor.h:83; read by
  * Frame::ComputeStereoMatches src/Frame.cc:1126,1249).  Gives the device address of the view
- * (first pixel of the level image inside its 19-pixel REFLECT_101 border), its size and row pitch.
- * The border is readable at negative offsets down to -19 rows/columns. */
+ * (first pixel of the level image inside its padded plane), its size and row pitch.  On the device
+ * only a 3-pixel REFLECT_101 border around the view is written (all that the stereo matcher's SAD
+ * windows and the descriptor's blur reach); the plane extends 19 pixels each way. */
 int orb_extractor_level(orb_extractor_t h, int frame, int level, const uint8_t** d_view, int* width,
                         int* height, int* pitch);
-/* Copy the padded level plane ((w+38) x (h+38), row-major, tight) to host memory. */
+/* Copy the padded level plane ((w+38) x (h+38), row-major, tight) to host memory, with its whole
+ * 19-pixel border REFLECT_101 as the reference's copyMakeBorder makes it (src/ORBextractor.cc:1712-1716,
+ * 1734-1736): the part beyond the device's 3-pixel border is filled on the host. */
 int orb_extractor_level_download(orb_extractor_t h, int frame, int level, uint8_t* host_padded);
 
 /* ---- ORBmatcher (src/ORBmatcher.cc) ---------------------------------------------------------- */

@@ -12,7 +12,10 @@
  * access after each extraction: only Frame::ComputeStereoMatches reads it (src/Frame.cc:1126,
  * 1249,1268,1275, always through operator[]), so tracking without stereo never pays the copy and
  * the caller compiles unchanged.  The levels are views into padded planes, like the reference's
- * (src/ORBextractor.cc:1695-1697), so the 19-pixel border stays readable.
+ * (src/ORBextractor.cc:1695-1697).  The device writes each level plus a 3-pixel border; the download
+ * (orb_extractor_level_download) fills the rest of the 19-pixel ring on the host by the REFLECT_101
+ * rule of the reference's copyMakeBorder (:1712-1716, 1734-1736), so every byte reachable through the
+ * view's ROI equals the reference's padded plane.
  */
 #ifndef ORBGPU_CV_HPP
 #define ORBGPU_CV_HPP

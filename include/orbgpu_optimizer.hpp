@@ -38,7 +38,12 @@
  *   };
  *
  * The two-camera fisheye rig (KeyFrame::mpCamera2, EdgeSE3ProjectXYZToBody) is outside this path:
- * Gather reports kCamera2 and the caller keeps the reference's own optimiser for such maps.
+ * Gather reports kCamera2, and LocalBundleAdjustment returns kFallback (1) so that the caller runs the
+ * reference's own body.  So does a window the device cannot take or a device failure.  Before such a
+ * return every mnBALocalForKF / mnBAFixedForKF mark Gather wrote is restored to its previous value:
+ * the reference body sets and tests the same marks (src/Optimizer.cc:1748-1803) and would otherwise
+ * find every neighbour already marked, collect no local map point and no fixed keyframe, and stop at
+ * "LBA aborted" (:1851-1855).
  */
 #ifndef ORBGPU_OPTIMIZER_HPP
 #define ORBGPU_OPTIMIZER_HPP
@@ -86,6 +91,18 @@ struct LocalBAWindow {
     std::vector<orb_ba_edge_t> edges;
     std::vector<KF*> edge_kf;                 // vpEdgeKFMono / vpEdgeKFStereo, per edge
     std::vector<MP*> edge_mp;                 // vpMapPointEdgeMono / vpMapPointEdgeStereo, per edge
+    // every mark Gather wrote, with its value before (restored in reverse order by RestoreMarks)
+    std::vector<std::pair<unsigned long*, unsigned long>> mark_log;
+
+    void Mark(unsigned long& m, unsigned long v) {
+        mark_log.emplace_back(&m, m);
+        m = v;
+    }
+    // Undo Gather's marks, so that the reference body can build the same window itself.
+    void RestoreMarks() {
+        for (auto it = mark_log.rbegin(); it != mark_log.rend(); ++it) *it->first = it->second;
+        mark_log.clear();
+    }
 
     orb_ba_problem_t Problem() {
         orb_ba_problem_t p{};
@@ -109,10 +126,10 @@ struct LocalBAWindow {
         // local keyframes: pKF and its covisible keyframes (:1744-1760); the mark is set before the
         // bad / other-map test, so such a neighbour is neither local nor fixed
         local_kfs.push_back(pKF);
-        A::BALocalForKF(pKF) = kfid;
+        Mark(A::BALocalForKF(pKF), kfid);
         auto* cur_map = A::GetMap(pKF);
         for (KF* pKFi : A::Covisible(pKF)) {
-            A::BALocalForKF(pKFi) = kfid;
+            Mark(A::BALocalForKF(pKFi), kfid);
             if (!A::IsBad(pKFi) && A::GetMap(pKFi) == cur_map) local_kfs.push_back(pKFi);
         }
         // local map points (:1762-1789)
@@ -123,7 +140,7 @@ struct LocalBAWindow {
                 if (!pMP || A::IsBad(pMP) || A::GetMap(pMP) != cur_map) continue;
                 if (A::BALocalForKF(pMP) != kfid) {
                     local_mps.push_back(pMP);
-                    A::BALocalForKF(pMP) = kfid;
+                    Mark(A::BALocalForKF(pMP), kfid);
                 }
             }
         }
@@ -132,7 +149,7 @@ struct LocalBAWindow {
             for (const auto& ob : A::Observations(pMP)) {
                 KF* pKFi = ob.first;
                 if (A::BALocalForKF(pKFi) != kfid && A::BAFixedForKF(pKFi) != kfid) {
-                    A::BAFixedForKF(pKFi) = kfid;
+                    Mark(A::BAFixedForKF(pKFi), kfid);
                     if (!A::IsBad(pKFi) && A::GetMap(pKFi) == cur_map) fixed_kfs.push_back(pKFi);
                 }
             }
@@ -225,18 +242,27 @@ inline bool DepthPositive(const double* T, const double* X) {
     return r20 * X[0] + r21 * X[1] + r22 * X[2] + T[2] > 0.0;
 }
 
+// LocalBundleAdjustment's return value when the caller must run the reference's own body.
+constexpr int kFallback = 1;
+
 // Optimizer::LocalBundleAdjustment(pKF, pbStopFlag, pMap, num_fixedKF, num_OptKF, num_MPs, num_edges)
-// on a GPU BA handle.  Returns ORB_OK (also for the reference's silent early returns), 1 when the
-// window holds a two-camera keyframe (the caller runs the reference optimiser), or a negative
-// orbgpu status.  num_MPs is left untouched, as in the reference.
+// on a GPU BA handle.  Returns ORB_OK (also for the reference's silent early returns) or kFallback:
+// the window holds a two-camera keyframe, or the library could not solve it (a window beyond the
+// device's limits, a device error; orb_last_error() says which).  On kFallback nothing in the map has
+// been changed and Gather's marks are restored, so the caller runs the reference body (:1742-2187)
+// on the same arguments, as INTEGRATION.md shows; the reference is slower there, never wrong.
+// num_MPs is left untouched, as in the reference.
 template <class A>
 int LocalBundleAdjustment(orb_ba_t h, typename A::KeyFrame* pKF, bool* pbStopFlag, typename A::Map* pMap,
                           int& num_fixedKF, int& num_OptKF, int& /*num_MPs*/, int& num_edges) {
     LocalBAWindow<A> w;
     const auto st = w.Gather(pKF, pMap);
+    if (st == LocalBAWindow<A>::kCamera2) {
+        w.RestoreMarks();
+        return kFallback;
+    }
     num_fixedKF = w.num_fixed_kf;
-    if (st == LocalBAWindow<A>::kNoFixed) return ORB_OK;
-    if (st == LocalBAWindow<A>::kCamera2) return 1;
+    if (st == LocalBAWindow<A>::kNoFixed) return ORB_OK;  // the reference keeps its marks here too
     {  // DEBUG LBA sets of the current map (:1879-1880, 1896, 1914)
         std::set<unsigned long> opt, fixed;
         for (auto* k : w.local_kfs) opt.insert(A::Id(k));
@@ -256,9 +282,12 @@ int LocalBundleAdjustment(orb_ba_t h, typename A::KeyFrame* pKF, bool* pbStopFla
     std::vector<uint8_t> depth(w.edges.size());
     orb_ba_result_t res{};
     const int rc = orb_ba_optimize(h, &prob, &opt, chi2.data(), depth.data(), &res);
+    if (rc != ORB_OK && rc != ORB_ERR_ABORTED) {  // nothing written back: the reference body takes over
+        w.RestoreMarks();
+        return kFallback;
+    }
     // a flag raised before the first iteration: g2o's optimize() returns without an update and the
     // reference still culls and writes back the unchanged estimates
-    if (rc != ORB_OK && rc != ORB_ERR_ABORTED) return rc;
     if (rc == ORB_ERR_ABORTED) {
         // no iteration ran: the estimates are the initial ones and no edge error was ever computed
         // (g2o leaves _error as constructed), so only isDepthPositive can cull: Xc = R X + t, z > 0

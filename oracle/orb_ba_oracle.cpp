@@ -135,12 +135,21 @@ void linearize(const Problem& P, int e, double A[9], double B[18]) {
 
 }  // namespace
 
+namespace {
+// Test hook (oracle_local_ba_stop_after): the solve behaves as if the caller's stop flag went up right
+// after trial `stop_after_trials` (0: before the first iteration).
+int g_stop_after = -1;
+}  // namespace
+
 extern "C" int oracle_local_ba(orb_ba_problem_t* prob, const orb_ba_options_t* opt, double* edge_chi2_out,
                                uint8_t* depth_ok_out, orb_ba_result_t* res) {
     Problem P(*prob);
     const int np = prob->n_poses, nq = prob->n_points, ne = prob->n_edges;
-    auto stop = [&]() { return (opt->stop_flag && *opt->stop_flag) || (opt->stop_flag_bool && *opt->stop_flag_bool); };
     memset(res, 0, sizeof(*res));
+    auto stop = [&]() {
+        return (opt->stop_flag && *opt->stop_flag) || (opt->stop_flag_bool && *opt->stop_flag_bool) ||
+               (g_stop_after >= 0 && res->trials >= g_stop_after);
+    };
     P.pose.resize(np);
     for (int i = 0; i < np; ++i) {
         const double* v = prob->pose + 7 * i;
@@ -377,4 +386,15 @@ extern "C" int oracle_local_ba(orb_ba_problem_t* prob, const orb_ba_options_t* o
         }
     }
     return 0;
+}
+
+// oracle_local_ba with the stop flag raised right after `stop_after_trials` LM trials (g2o polls the
+// flag after each trial and before each iteration: optimization_algorithm_levenberg.cpp:149,
+// sparse_optimizer.cpp:376).  Used to check a GPU solve interrupted by a real flag.
+extern "C" int oracle_local_ba_stop_after(orb_ba_problem_t* prob, const orb_ba_options_t* opt, int stop_after_trials,
+                                          double* edge_chi2_out, uint8_t* depth_ok_out, orb_ba_result_t* res) {
+    g_stop_after = stop_after_trials;
+    const int rc = oracle_local_ba(prob, opt, edge_chi2_out, depth_ok_out, res);
+    g_stop_after = -1;
+    return rc;
 }

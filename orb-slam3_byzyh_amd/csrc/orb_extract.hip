@@ -2559,6 +2559,21 @@ int orb_extractor_level_download(orb_extractor_t h, int frame, int level, uint8_
     if (hipStreamSynchronize(e->stream) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
         hipMemcpy2D(host_padded, L.pw, src, L.pitch, L.pw, L.ph, hipMemcpyDeviceToHost) != hipSuccess)
         return orbgpu_fail(ORB_ERR_DEVICE, "download failed");
+    // the ring beyond the device's 3-pixel border: cv::borderInterpolate(p, len, BORDER_REFLECT_101)
+    auto reflect101 = [](int p, int len) {
+        if (len == 1) return 0;
+        while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - 2 - p;
+        return p;
+    };
+    const int E = orbgpu::kEdge, w = L.w, hh = L.h;
+    for (int y = 0; y < hh; ++y) {
+        uint8_t* row = host_padded + (size_t)(y + E) * L.pw + E;
+        for (int x = -E; x < 0; ++x) row[x] = row[reflect101(x, w)];
+        for (int x = w; x < w + E; ++x) row[x] = row[reflect101(x, w)];
+    }
+    for (int y = -E; y < hh + E; ++y)
+        if (y < 0 || y >= hh)
+            memcpy(host_padded + (size_t)(y + E) * L.pw, host_padded + (size_t)(reflect101(y, hh) + E) * L.pw, (size_t)L.pw);
     return ORB_OK;
 }
 

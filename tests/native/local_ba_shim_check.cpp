@@ -288,13 +288,37 @@ static void test_init_kf_local_and_abort() {
         CHECK(rc == ORB_OK && nf == 0 && no == -1 && ne == -1 && nmp == 77);
         CHECK(g_solve.calls == 0 && g.M.change == 0 && g.M.opt.empty());
     }
-    {   // a two-camera keyframe in the window: left to the reference optimiser
+    {   // a two-camera keyframe in the window: left to the reference optimiser, with every mark restored
         Graph g;
         g.K[3].cam2 = true;
+        g.K[1].fixed = 3;  // marks left by an earlier window (pKF = K3) must come back as they were
+        g.P[0].local = 3;
         g_solve = SolveRecord();
+        int nf = -7, no = -7, nmp = -7, ne = -7;
+        CHECK(orbgpu::LocalBundleAdjustment<Access>(nullptr, &g.K[5], nullptr, &g.M, nf, no, nmp, ne) ==
+              orbgpu::kFallback);
+        CHECK(g_solve.calls == 0 && nf == -7 && no == -7 && ne == -7 && g.M.opt.empty());
+        for (int i = 0; i < 10; ++i) CHECK(g.K[i].local == 0 && g.K[i].fixed == (i == 1 ? 3u : 0u));
+        for (int i = 0; i < 8; ++i) CHECK(g.P[i].local == (i == 0 ? 3u : 0u));
+        // the reference body, run next on the same graph, builds the full window from the marks
+        // (src/Optimizer.cc:1748-1803; Gather restates exactly that part)
+        orbgpu::LocalBAWindow<Access> ref;
+        ref.Gather(&g.K[5], &g.M);
+        CHECK((ref.local_kfs == std::vector<MockKF*>{&g.K[5], &g.K[4], &g.K[3], &g.K[2]}));
+        CHECK((ref.local_mps == std::vector<MockMP*>{&g.P[2], &g.P[0], &g.P[1], &g.P[3], &g.P[4]}));
+        CHECK((ref.fixed_kfs == std::vector<MockKF*>{&g.K[1], &g.K[0], &g.K[6]}) && ref.num_fixed_kf == 3);
+    }
+    {   // the library cannot take the window (or the device fails): the same fallback, nothing written
+        Graph g;
+        g_solve = SolveRecord();
+        g_solve.rc = ORB_ERR_DEVICE;
+        bool stop = false;
         int nf, no, nmp, ne;
-        CHECK(orbgpu::LocalBundleAdjustment<Access>(nullptr, &g.K[5], nullptr, &g.M, nf, no, nmp, ne) == 1);
-        CHECK(g_solve.calls == 0);
+        CHECK(orbgpu::LocalBundleAdjustment<Access>(nullptr, &g.K[5], &stop, &g.M, nf, no, nmp, ne) ==
+              orbgpu::kFallback);
+        CHECK(g_solve.calls == 1 && g.M.change == 0 && g.M.erased.empty() && !g.K[5].pose_written);
+        for (int i = 0; i < 10; ++i) CHECK(g.K[i].local == 0 && g.K[i].fixed == 0);
+        for (int i = 0; i < 8; ++i) CHECK(g.P[i].local == 0 && !g.P[i].pos_written);
     }
 }
 
