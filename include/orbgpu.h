@@ -178,6 +178,39 @@ int orb_search_for_triangulation(orb_matcher_t m, const orb_kf_view_t* kf1, cons
                                  const orb_kf_pair_geom_t* geoms, int n_pairs, int only_stereo, int coarse,
                                  int32_t* matches12, int32_t* n_matches);
 
+/* The same search on device-resident keyframes: the features orb_extract_batch_device wrote (d_kps /
+ * d_desc at frame f * cap, the count at d_counts[2 f]), the u_right orb_compute_stereo_matches_batch_device
+ * wrote and the FeatureVector orb_bow_transform_frames_device wrote, with no host hop for any of them
+ * (the chain KeyFrame::ComputeBoW -> LocalMapping::CreateNewMapPoints, src/KeyFrame.cc:109,
+ * src/LocalMapping.cc:536-610, after the stereo Frame of src/Frame.cc:136-146).  Counts are read on
+ * the device; `cap` bounds them. */
+typedef struct orb_kf_device {
+    const orb_keypoint_t* kps;     /* device: mvKeysUn, cap entries */
+    const uint8_t* desc;           /* device: cap x 32 bytes */
+    const int32_t* n;              /* device: KeyFrame::N (e.g. &d_counts[2 f] of orb_extract_batch_device) */
+    const float* u_right;          /* device: mvuRight (cap), NULL = monocular */
+    const uint8_t* has_mappoint;   /* device: cap flags (GetMapPoint(i) != NULL), NULL = none */
+    const int32_t* fv_node;        /* device: FeatureVector node ids, ascending */
+    const int32_t* fv_begin;       /* device: n_nodes + 1 offsets into fv_feat */
+    const int32_t* fv_feat;        /* device: feature indices, each node's in ascending order */
+    const int32_t* n_nodes;        /* device: FeatureVector size (e.g. &d_bow_counts[2 f + 1]) */
+    int32_t cap;                   /* upper bound of *n and *n_nodes */
+    float fx, fy, cx, cy;          /* host: pinhole parameters */
+    int32_t nlevels;               /* <= 12 */
+    const float* scale_factors;    /* host: mvScaleFactors */
+    const float* level_sigma2;     /* host: mvLevelSigma2 */
+} orb_kf_device_t;
+
+/* SearchForTriangulation(kf1s[pair_kf1[p]], kf2s[p]) for p < n_pairs in one launch, device-resident,
+ * asynchronous on `stream`: the neighbours of one new keyframe (pair_kf1 = NULL: every pair uses
+ * kf1s[0]), or of several queued keyframes.  With C = max over kf1s of cap:
+ * d_matches12[p * C + i] = index in kf2s[p] or -1 (i < C); d_n_matches[p] = the count.  The pair
+ * geometry and F12 are uploaded from the host (a few hundred bytes per pair). */
+int orb_search_for_triangulation_device(orb_matcher_t m, const orb_kf_device_t* kf1s, int n_kf1,
+                                        const orb_kf_device_t* kf2s, const int32_t* pair_kf1,
+                                        const orb_kf_pair_geom_t* geoms, int n_pairs, int only_stereo, int coarse,
+                                        int32_t* d_matches12, int32_t* d_n_matches, void* stream);
+
 /* ---- ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono) (src/ORBmatcher.cc:1951-2185)
  * Pinhole frames without a second camera (Nleft == -1). */
 
@@ -336,6 +369,13 @@ int orb_bow_transform_batch_device(orb_vocabulary_t v, const uint8_t* d_desc, co
                                    int n_frames, int n_total, int levelsup, int32_t* d_bow_word,
                                    double* d_bow_value, int32_t* d_fv_node, int32_t* d_fv_begin, int32_t* d_fv_feat,
                                    int32_t* d_counts, void* stream);
+/* The same on the frames as orb_extract_batch_device leaves them: frame f's descriptors at
+ * d_desc[f * cap * 32 ..], its count at d_kp_counts[2 f] (<= cap, <= 8192).  Per frame f the outputs
+ * start at f * cap in every array (fv_begin at f * (cap + 1)); d_counts[2 f] = n_words,
+ * d_counts[2 f + 1] = n_nodes.  Async on `stream`. */
+int orb_bow_transform_frames_device(orb_vocabulary_t v, const uint8_t* d_desc, const int32_t* d_kp_counts, int n_frames,
+                                    int cap, int levelsup, int32_t* d_bow_word, double* d_bow_value, int32_t* d_fv_node,
+                                    int32_t* d_fv_begin, int32_t* d_fv_feat, int32_t* d_counts, void* stream);
 
 /* ---- Optimizer::LocalBundleAdjustment (src/Optimizer.cc:1740-2188) ----------------------------- */
 /* The shim keeps the reference's graph gather (B1, src/Optimizer.cc:1744-1855) and the culling /

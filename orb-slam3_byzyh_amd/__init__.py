@@ -7,7 +7,7 @@ __graft_entry__.py), which register it under the import name ``orbslam3_amd``.
 from . import _lib
 from ._lib import KEYPOINT_DTYPE, POSE_EDGE_DTYPE, POSE_FRAME_DTYPE, OrbGpuError
 from .extractor import ORBextractor, keypoints_to_structured
-from .keyframe import Frame, KeyFrame, LocalMapPoints, frustum_frame, is_in_frustum
+from .keyframe import DeviceKeyFrame, Frame, KeyFrame, LocalMapPoints, frustum_frame, is_in_frustum
 from .matcher import ORBmatcher
 from .optimizer import LocalBA, local_bundle_adjustment, pose_optimization
 from . import distributed

@@ -1062,7 +1062,9 @@ __global__ __launch_bounds__(kRowThreads) void k_ba_chol_rows(int n, const doubl
         flag_publish_agent(flags + i * NT + i, E, lane);
     }
     __syncthreads();
-    if (fail > 3 && tid == 0) __hip_atomic_store((ba_gu32*)(cflag + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // a timed-out wait is reported to the last row tagged with this launch's epoch, so that it fails
+    // this solve only (a later launch compares against its own epoch: no clearing needed)
+    if (fail > 3 && tid == 0) __hip_atomic_store((ba_gu32*)(cflag + 1), E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (i != NT - 1) return;
     // ---- backward solve L^T x = y in the last row's workgroup: x_j = L_jj^-T (y_j - sum_{k>j} L_kj^T x_k),
     // right-looking: after x_j, every z_p (p < j) loses L_jp^T x_j
@@ -1100,7 +1102,7 @@ __global__ __launch_bounds__(kRowThreads) void k_ba_chol_rows(int n, const doubl
     for (int t = tid; t < n; t += kRowThreads) x[t] = z[t];
     if (tid == 0) {
         const unsigned timeouts = __hip_atomic_load((ba_gu32*)(cflag + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *status = fail ? fail : (timeouts ? 6 : 0);
+        *status = fail ? fail : (timeouts == E ? 6 : 0);
         cflag[0] = E;  // every row read the epoch before publishing, and this row consumed all of them
     }
 }

@@ -53,9 +53,11 @@ __global__ __launch_bounds__(256) void k_bow_descend(const int32_t* __restrict__
                                                      const double* __restrict__ weight, int L,
                                                      const uint8_t* __restrict__ feat, int n, int levelsup,
                                                      int32_t* __restrict__ word, double* __restrict__ w,
-                                                     int32_t* __restrict__ nid) {
+                                                     int32_t* __restrict__ nid, const int32_t* __restrict__ kp_counts,
+                                                     int cap) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    if (kp_counts && i % cap >= kp_counts[2 * (i / cap)]) return;  // frames at stride cap: past the count
     const uint4* fp = reinterpret_cast<const uint4*>(feat + 32 * (size_t)i);
     const uint4 a0 = fp[0], a1 = fp[1];
     const uint4* D = reinterpret_cast<const uint4*>(vdesc);
@@ -178,12 +180,14 @@ __global__ __launch_bounds__(kAggThreads) void k_bow_aggregate(
     const int32_t* __restrict__ frame_begin, const int32_t* __restrict__ word, const double* __restrict__ w,
     const int32_t* __restrict__ nid, int weighting, int scoring, int32_t* __restrict__ bow_word,
     double* __restrict__ bow_value, int32_t* __restrict__ fv_node, int32_t* __restrict__ fv_begin,
-    int32_t* __restrict__ fv_feat, int32_t* __restrict__ counts) {
+    int32_t* __restrict__ fv_feat, int32_t* __restrict__ counts, const int32_t* __restrict__ kp_counts, int cap) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long keys[];
     __shared__ int scan[kAggThreads];
     __shared__ double s_norm;
     const int f = blockIdx.x, tid = threadIdx.x;
-    const int base = frame_begin[f], n = frame_begin[f + 1] - base;
+    // contiguous frames (frame_begin) or the extractor's layout (frame f at f * cap, kp_counts[2 f] features)
+    const int base = kp_counts ? f * cap : frame_begin[f];
+    const int n = kp_counts ? kp_counts[2 * f] : frame_begin[f + 1] - base;
     double* vals = reinterpret_cast<double*>(keys + kMaxFrameFeatures);
     if (n > kMaxFrameFeatures) {
         if (tid == 0) counts[2 * f] = counts[2 * f + 1] = ORB_ERR_CAPACITY;
@@ -274,18 +278,18 @@ __global__ __launch_bounds__(kAggThreads) void k_bow_aggregate(
 int launch(orb_vocabulary_t v, const uint8_t* d_desc, const int32_t* d_frame_begin, int n_frames, int n_total,
            int levelsup, int32_t* d_word_tmp, double* d_w_tmp, int32_t* d_nid_tmp, int32_t* d_bow_word,
            double* d_bow_value, int32_t* d_fv_node, int32_t* d_fv_begin, int32_t* d_fv_feat, int32_t* d_counts,
-           hipStream_t st) {
+           hipStream_t st, const int32_t* d_kp_counts = nullptr, int cap = 0) {
     if (n_total > 0)
         hipLaunchKernelGGL(k_bow_descend, dim3((n_total + 255) / 256), dim3(256), 0, st, v->d_child_begin, v->d_child_idx,
                            v->d_desc, v->d_word, v->d_weight, v->L, d_desc, n_total, levelsup, d_word_tmp, d_w_tmp,
-                           d_nid_tmp);
+                           d_nid_tmp, d_kp_counts, cap);
     const size_t lds = (size_t)kMaxFrameFeatures * 16;
     static bool attr = hipFuncSetAttribute((const void*)k_bow_aggregate, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)lds) == hipSuccess;
     if (!attr) return orbgpu_fail(ORB_ERR_DEVICE, "cannot raise the BoW aggregation LDS limit");
     hipLaunchKernelGGL(k_bow_aggregate, dim3(n_frames), dim3(kAggThreads), lds, st, d_frame_begin, d_word_tmp, d_w_tmp,
                        d_nid_tmp, v->weighting, v->scoring, d_bow_word, d_bow_value, d_fv_node, d_fv_begin, d_fv_feat,
-                       d_counts);
+                       d_counts, d_kp_counts, cap);
     if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "BoW kernel launch failed");
     return ORB_OK;
 }
@@ -354,6 +358,26 @@ int orb_bow_transform_batch_device(orb_vocabulary_t v, const uint8_t* d_desc, co
     int rc = launch(v, d_desc, d_frame_begin, n_frames, n_total, levelsup, reinterpret_cast<int32_t*>(tmp + 8 * m),
                     reinterpret_cast<double*>(tmp), reinterpret_cast<int32_t*>(tmp + 12 * m), d_bow_word, d_bow_value,
                     d_fv_node, d_fv_begin, d_fv_feat, d_counts, (hipStream_t)stream);
+    if (hipFreeAsync(tmp, (hipStream_t)stream) != hipSuccess && rc == ORB_OK) rc = orbgpu_fail(ORB_ERR_DEVICE, "hipFreeAsync failed");
+    return rc;
+}
+
+int orb_bow_transform_frames_device(orb_vocabulary_t v, const uint8_t* d_desc, const int32_t* d_kp_counts, int n_frames,
+                                    int cap, int levelsup, int32_t* d_bow_word, double* d_bow_value, int32_t* d_fv_node,
+                                    int32_t* d_fv_begin, int32_t* d_fv_feat, int32_t* d_counts, void* stream) {
+    if (!v || n_frames < 0 || cap <= 0 || (n_frames && (!d_desc || !d_kp_counts)) || !d_bow_word || !d_bow_value ||
+        !d_fv_node || !d_fv_begin || !d_fv_feat || !d_counts)
+        return orbgpu_fail(ORB_ERR_ARG, "invalid BoW arguments");
+    if (n_frames == 0) return ORB_OK;
+    if (v->n_nodes <= 1) return orbgpu_fail(ORB_ERR_ARG, "empty vocabulary");
+    const size_t total = (size_t)n_frames * (size_t)cap;
+    if (total >= (size_t)INT32_MAX / 32) return orbgpu_fail(ORB_ERR_ARG, "BoW batch too large");
+    uint8_t* tmp = nullptr;
+    if (hipMallocAsync(reinterpret_cast<void**>(&tmp), total * 16, (hipStream_t)stream) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "hipMallocAsync failed");
+    int rc = launch(v, d_desc, nullptr, n_frames, (int)total, levelsup, reinterpret_cast<int32_t*>(tmp + 8 * total),
+                    reinterpret_cast<double*>(tmp), reinterpret_cast<int32_t*>(tmp + 12 * total), d_bow_word,
+                    d_bow_value, d_fv_node, d_fv_begin, d_fv_feat, d_counts, (hipStream_t)stream, d_kp_counts, cap);
     if (hipFreeAsync(tmp, (hipStream_t)stream) != hipSuccess && rc == ORB_OK) rc = orbgpu_fail(ORB_ERR_DEVICE, "hipFreeAsync failed");
     return rc;
 }

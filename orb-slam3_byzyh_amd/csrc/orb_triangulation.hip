@@ -61,52 +61,112 @@ __device__ __forceinline__ int hamming(const uint4& a0, const uint4& a1, const u
            __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
 
-__global__ __launch_bounds__(64 * kWaves) void k_tri_match(const KfDev* __restrict__ kfs, const PairDev* __restrict__ pairs,
-                                                         const KpRec* __restrict__ kps, const uint4* __restrict__ desc,
-                                                         const uint32_t* __restrict__ nodes,
-                                                         const int32_t* __restrict__ csr,
-                                                         const int32_t* __restrict__ fidx, int only_stereo, int coarse,
-                                                         int32_t* __restrict__ matches) {
+// Keyframes packed host-side into one upload (orb_search_for_triangulation).
+struct PackedSrc {
+    const KfDev* kfs;
+    const KpRec* kps;
+    const uint4* desc;
+    const uint32_t* nodes;
+    const int32_t* csr;
+    const int32_t* fidx;
+    __device__ int n(int k) const { return kfs[k].n; }
+    __device__ int n_nodes(int k) const { return kfs[k].n_nodes; }
+    __device__ uint32_t node(int k, int i) const { return nodes[kfs[k].node_off + i]; }
+    __device__ int node_begin(int k, int i) const { return csr[kfs[k].csr_off + i]; }
+    __device__ int feat(int k, int j) const { return fidx[j]; }
+    __device__ KpRec kp(int k, int idx) const { return kps[kfs[k].kp_off + idx]; }
+    __device__ float angle(int k, int idx) const { return kps[kfs[k].kp_off + idx].angle; }
+    __device__ void descriptor(int k, int idx, uint4& a, uint4& b) const {
+        const size_t o = 2 * (size_t)(kfs[k].kp_off + idx);
+        a = desc[o];
+        b = desc[o + 1];
+    }
+};
+
+// Keyframes left on the device by the extraction / stereo / BoW kernels (orb_search_for_triangulation_device).
+struct KfPtrs {
+    const orb_keypoint_t* kps;
+    const uint4* desc;
+    const int32_t* n;
+    const float* u_right;
+    const uint8_t* has_mp;
+    const int32_t* fv_node;
+    const int32_t* fv_begin;
+    const int32_t* fv_feat;
+    const int32_t* n_nodes;
+    int32_t cap, pad;
+};
+struct DirectSrc {
+    const KfPtrs* kfs;
+    __device__ int n(int k) const { return *kfs[k].n; }
+    __device__ int n_nodes(int k) const { return *kfs[k].n_nodes; }
+    __device__ uint32_t node(int k, int i) const { return (uint32_t)kfs[k].fv_node[i]; }
+    __device__ int node_begin(int k, int i) const { return kfs[k].fv_begin[i]; }
+    __device__ int feat(int k, int j) const { return kfs[k].fv_feat[j]; }
+    __device__ KpRec kp(int k, int idx) const {
+        const KfPtrs& K = kfs[k];
+        const float* f = reinterpret_cast<const float*>(K.kps + idx);  // x, y, size, angle, response, octave
+        const float2 xy = *reinterpret_cast<const float2*>(f);
+        const int oct = reinterpret_cast<const int32_t*>(f)[5];
+        const bool mp = K.has_mp && K.has_mp[idx];
+        const bool st = K.u_right && K.u_right[idx] >= 0;  // bStereo = mvuRight[i] >= 0 (src:1135)
+        return KpRec{xy.x, xy.y, f[3], oct | (mp ? 0x100 : 0) | (st ? 0x200 : 0)};
+    }
+    __device__ float angle(int k, int idx) const { return kfs[k].kps[idx].angle; }
+    __device__ void descriptor(int k, int idx, uint4& a, uint4& b) const {
+        a = kfs[k].desc[2 * (size_t)idx];
+        b = kfs[k].desc[2 * (size_t)idx + 1];
+    }
+};
+
+// matches12 row p starts at p * mstride (KF1's N for the packed form, its capacity for the device form)
+// Keyframe indices of pair p: KF1 = k1of[p] (0 without the table), KF2 = k2base + p.
+template <class Src>
+__global__ __launch_bounds__(64 * kWaves) void k_tri_match(Src src, const PairDev* __restrict__ pairs,
+                                                         const int32_t* __restrict__ k1of, int k2base, int only_stereo,
+                                                         int coarse, int mstride, int32_t* __restrict__ matches) {
     const int lane = threadIdx.x & 63;
     const int node1 = blockIdx.x * kWaves + (threadIdx.x >> 6);
     const int p = blockIdx.y;
-    const KfDev k1 = kfs[0];
-    if (node1 >= k1.n_nodes) return;
-    const KfDev k2 = kfs[1 + p];
+    const int K1 = k1of ? k1of[p] : 0, K2 = k2base + p;
+    if (node1 >= src.n_nodes(K1)) return;
+    const int nn2 = src.n_nodes(K2);
     // the shared-node walk of src:1112-1287 visits exactly the node ids present in both maps
-    const uint32_t id = nodes[k1.node_off + node1];
-    int lo = 0, hi = k2.n_nodes;
+    const uint32_t id = src.node(K1, node1);
+    int lo = 0, hi = nn2;
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if (nodes[k2.node_off + mid] < id) lo = mid + 1;
+        if (src.node(K2, mid) < id) lo = mid + 1;
         else hi = mid;
     }
-    if (lo >= k2.n_nodes || nodes[k2.node_off + lo] != id) return;
-    const int b1 = csr[k1.csr_off + node1], e1 = csr[k1.csr_off + node1 + 1];
-    const int b2 = csr[k2.csr_off + lo], e2 = csr[k2.csr_off + lo + 1];
+    if (lo >= nn2 || src.node(K2, lo) != id) return;
+    const int b1 = src.node_begin(K1, node1), e1 = src.node_begin(K1, node1 + 1);
+    const int b2 = src.node_begin(K2, lo), e2 = src.node_begin(K2, lo + 1);
     const PairDev& pd = pairs[p];
     const float F00 = pd.F[0], F01 = pd.F[1], F02 = pd.F[2], F10 = pd.F[3], F11 = pd.F[4], F12 = pd.F[5],
                 F20 = pd.F[6], F21 = pd.F[7], F22 = pd.F[8];
     for (int i1 = b1 + lane; i1 < e1; i1 += 64) {
-        const int idx1 = fidx[i1];
-        const KpRec r1 = kps[k1.kp_off + idx1];
+        const int idx1 = src.feat(K1, i1);
+        const KpRec r1 = src.kp(K1, idx1);
         if (r1.meta & 0x100) continue;  // pMP1 != NULL (src:1127-1132)
         const bool stereo1 = (r1.meta & 0x200) != 0;
         if (only_stereo && !stereo1) continue;
-        const uint4 d10 = desc[2 * (size_t)(k1.kp_off + idx1)], d11 = desc[2 * (size_t)(k1.kp_off + idx1) + 1];
+        uint4 d10, d11;
+        src.descriptor(K1, idx1, d10, d11);
         // epipolar line of kp1 (Pinhole.cpp:200-202), fma(x, F0j, y*F1j) + F2j as compiled upstream
         const float la = __fmaf_rn(r1.x, F00, r1.y * F10) + F20;
         const float lb = __fmaf_rn(r1.x, F01, r1.y * F11) + F21;
         const float lc = __fmaf_rn(r1.x, F02, r1.y * F12) + F22;
         int best = kThLow, bi = -1;
         for (int i2 = b2; i2 < e2; ++i2) {
-            const int idx2 = fidx[i2];
-            const KpRec r2 = kps[k2.kp_off + idx2];
+            const int idx2 = src.feat(K2, i2);
+            const KpRec r2 = src.kp(K2, idx2);
             if (r2.meta & 0x100) continue;  // vbMatched2[idx2] is never set (src:1158); pMP2 != NULL
             const bool stereo2 = (r2.meta & 0x200) != 0;
             if (only_stereo && !stereo2) continue;
-            const int dist = hamming(d10, d11, desc[2 * (size_t)(k2.kp_off + idx2)],
-                                     desc[2 * (size_t)(k2.kp_off + idx2) + 1]);
+            uint4 d20, d21;
+            src.descriptor(K2, idx2, d20, d21);
+            const int dist = hamming(d10, d11, d20, d21);
             if (dist > kThLow || dist > best) continue;  // src:1178
             const int oct2 = r2.meta & 0xFF;
             if (!stereo1 && !stereo2) {  // too close to the epipole (src:1190-1202)
@@ -127,7 +187,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_tri_match(const KfDev* __restri
                 best = dist;
             }
         }
-        matches[(size_t)p * k1.n + idx1] = bi;
+        matches[(size_t)p * mstride + idx1] = bi;
     }
 }
 
@@ -140,25 +200,27 @@ __device__ __forceinline__ int rot_bin(float a1, float a2) {
     return bin;
 }
 
-__global__ __launch_bounds__(256) void k_tri_finish(const KfDev* __restrict__ kfs, const KpRec* __restrict__ kps,
-                                                    int check_ori, int32_t* __restrict__ matches,
+template <class Src>
+__global__ __launch_bounds__(256) void k_tri_finish(Src src, const int32_t* __restrict__ k1of, int k2base, int check_ori,
+                                                    int mstride, int32_t* __restrict__ matches,
                                                     int32_t* __restrict__ counts) {
     __shared__ int hist[kHistoLength];
     __shared__ int keep[3];
     __shared__ int total;
     const int p = blockIdx.x;
-    const KfDev k1 = kfs[0], k2 = kfs[1 + p];
-    int32_t* m = matches + (size_t)p * k1.n;
+    const int K1 = k1of ? k1of[p] : 0, K2 = k2base + p;
+    const int n1 = src.n(K1);
+    int32_t* m = matches + (size_t)p * mstride;
     if (threadIdx.x < kHistoLength) hist[threadIdx.x] = 0;
     if (threadIdx.x == 0) total = 0;
     __syncthreads();
     int cnt = 0;
-    for (int i = threadIdx.x; i < k1.n; i += blockDim.x) {
+    for (int i = threadIdx.x; i < n1; i += blockDim.x) {
         const int j = m[i];
         if (j < 0) continue;
         ++cnt;
         if (check_ori) {
-            const int bin = rot_bin(kps[k1.kp_off + i].angle, kps[k2.kp_off + j].angle);
+            const int bin = rot_bin(src.angle(K1, i), src.angle(K2, j));
             if (bin >= 0 && bin < kHistoLength) atomicAdd(&hist[bin], 1);
         }
     }
@@ -183,10 +245,10 @@ __global__ __launch_bounds__(256) void k_tri_finish(const KfDev* __restrict__ kf
             keep[0] = ind1; keep[1] = ind2; keep[2] = ind3;
         }
         __syncthreads();
-        for (int i = threadIdx.x; i < k1.n; i += blockDim.x) {
+        for (int i = threadIdx.x; i < n1; i += blockDim.x) {
             const int j = m[i];
             if (j < 0) continue;
-            const int bin = rot_bin(kps[k1.kp_off + i].angle, kps[k2.kp_off + j].angle);
+            const int bin = rot_bin(src.angle(K1, i), src.angle(K2, j));
             if (bin != keep[0] && bin != keep[1] && bin != keep[2]) {
                 m[i] = -1;
                 --cnt;
@@ -224,10 +286,10 @@ void matmul3(const float a[9], const float b[9], float out[9]) {
     memcpy(out, t, sizeof(t));
 }
 
-// F12 = K1^-T * [t12]x * R12 * K2^-1 (Pinhole.cpp:191-194).
-void fundamental(const orb_kf_view_t& k1, const orb_kf_view_t& k2, const orb_kf_pair_geom_t& g, float F[9]) {
-    const float K1t[9] = {k1.fx, 0.f, 0.f, 0.f, k1.fy, 0.f, k1.cx, k1.cy, 1.f};
-    const float K2[9] = {k2.fx, 0.f, k2.cx, 0.f, k2.fy, k2.cy, 0.f, 0.f, 1.f};
+// F12 = K1^-T * [t12]x * R12 * K2^-1 (Pinhole.cpp:191-194); k = fx, fy, cx, cy.
+void fundamental(const float k1[4], const float k2[4], const orb_kf_pair_geom_t& g, float F[9]) {
+    const float K1t[9] = {k1[0], 0.f, 0.f, 0.f, k1[1], 0.f, k1[2], k1[3], 1.f};
+    const float K2[9] = {k2[0], 0.f, k2[2], 0.f, k2[1], k2[3], 0.f, 0.f, 1.f};
     const float* t = g.t12;
     const float tx[9] = {0.f, -t[2], t[1], t[2], 0.f, -t[0], -t[1], t[0], 0.f};  // Sophus::SO3f::hat
     float K1ti[9], K2i[9];
@@ -265,12 +327,30 @@ bool check_view(const orb_kf_view_t* v, bool first) {
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
+// The per-pair constants of k_tri_match: F12, the epipole, 100 * scale (src:1193), 3.84 sigma2 (Pinhole.cpp:215).
+PairDev make_pair(const float k1[4], const float k2[4], int nlevels2, const float* scale2, const float* sigma2_2,
+                  const orb_kf_pair_geom_t& g) {
+    PairDev d{};
+    fundamental(k1, k2, g, d.F);
+    d.ep[0] = g.ep[0];
+    d.ep[1] = g.ep[1];
+    for (int l = 0; l < kMaxLevels; ++l) {
+        d.scale100[l] = l < nlevels2 ? 100 * scale2[l] : 0.f;
+        d.thr[l] = l < nlevels2 ? 3.84 * (double)sigma2_2[l] : 0.0;
+    }
+    return d;
+}
+
 }  // namespace
 
 struct orb_matcher_s {
     float nnratio = 0.6f;
     int check_ori = 1;
     hipStream_t stream = nullptr;
+    // pinned upload slot of the device-resident entry points; `dev_ev` marks the end of its last copy
+    char* h_dev = nullptr;
+    size_t h_dev_cap = 0;
+    hipEvent_t dev_ev = nullptr;
     char* d_buf = nullptr;
     size_t d_cap = 0;
     char* h_buf = nullptr;
@@ -333,6 +413,11 @@ int orb_matcher_create(float nnratio, int check_orientation, orb_matcher_t* out)
 int orb_matcher_destroy(orb_matcher_t m) {
     if (!m) return ORB_OK;
     if (m->stream) hipStreamSynchronize(m->stream);
+    if (m->dev_ev) {
+        hipEventSynchronize(m->dev_ev);
+        hipEventDestroy(m->dev_ev);
+    }
+    if (m->h_dev) hipHostFree(m->h_dev);
     if (m->d_buf) hipFree(m->d_buf);
     if (m->h_buf) hipHostFree(m->h_buf);
     if (m->stream) hipStreamDestroy(m->stream);
@@ -401,17 +486,11 @@ int orb_search_for_triangulation(orb_matcher_t m, const orb_kf_view_t* kf1, cons
     char* h = m->h_buf;
     memcpy(h + o_kf, kd.data(), nkf * sizeof(KfDev));
     auto* pd = reinterpret_cast<PairDev*>(h + o_pair);
+    const float K1[4] = {kf1->fx, kf1->fy, kf1->cx, kf1->cy};
     for (int p = 0; p < n_pairs; ++p) {
         const orb_kf_view_t& v2 = kf2s[p];
-        PairDev d{};
-        fundamental(*kf1, v2, geoms[p], d.F);
-        d.ep[0] = geoms[p].ep[0];
-        d.ep[1] = geoms[p].ep[1];
-        for (int l = 0; l < kMaxLevels; ++l) {
-            d.scale100[l] = l < v2.nlevels ? 100 * v2.scale_factors[l] : 0.f;
-            d.thr[l] = l < v2.nlevels ? 3.84 * (double)v2.level_sigma2[l] : 0.0;
-        }
-        pd[p] = d;
+        const float K2[4] = {v2.fx, v2.fy, v2.cx, v2.cy};
+        pd[p] = make_pair(K1, K2, v2.nlevels, v2.scale_factors, v2.level_sigma2, geoms[p]);
     }
     auto* kp = reinterpret_cast<KpRec*>(h + o_kp);
     auto* nodes = reinterpret_cast<uint32_t*>(h + o_node);
@@ -442,17 +521,17 @@ int orb_search_for_triangulation(orb_matcher_t m, const orb_kf_view_t* kf1, cons
     hipStream_t s = m->stream;
     memset(h + o_match, 0xFF, (size_t)n_pairs * kf1->n * 4);
     bool ok = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s) == hipSuccess;
+    const PackedSrc src{(const KfDev*)(d + o_kf), (const KpRec*)(d + o_kp), (const uint4*)(d + o_desc),
+                        (const uint32_t*)(d + o_node), (const int32_t*)(d + o_csr), (const int32_t*)(d + o_idx)};
     if (ok && kf1->n_nodes > 0) {
-        hipLaunchKernelGGL(k_tri_match, dim3((kf1->n_nodes + kWaves - 1) / kWaves, n_pairs), dim3(64 * kWaves), 0, s,
-                           (const KfDev*)(d + o_kf), (const PairDev*)(d + o_pair), (const KpRec*)(d + o_kp),
-                           (const uint4*)(d + o_desc), (const uint32_t*)(d + o_node), (const int32_t*)(d + o_csr),
-                           (const int32_t*)(d + o_idx), only_stereo ? 1 : 0, coarse ? 1 : 0,
-                           (int32_t*)(d + o_match));
+        hipLaunchKernelGGL(k_tri_match<PackedSrc>, dim3((kf1->n_nodes + kWaves - 1) / kWaves, n_pairs), dim3(64 * kWaves),
+                           0, s, src, (const PairDev*)(d + o_pair), (const int32_t*)nullptr, 1, only_stereo ? 1 : 0,
+                           coarse ? 1 : 0, kf1->n, (int32_t*)(d + o_match));
         ok = hipGetLastError() == hipSuccess;
     }
     if (ok) {
-        hipLaunchKernelGGL(k_tri_finish, dim3(n_pairs), dim3(256), 0, s, (const KfDev*)(d + o_kf),
-                           (const KpRec*)(d + o_kp), m->check_ori, (int32_t*)(d + o_match), (int32_t*)(d + o_cnt));
+        hipLaunchKernelGGL(k_tri_finish<PackedSrc>, dim3(n_pairs), dim3(256), 0, s, src, (const int32_t*)nullptr, 1,
+                           m->check_ori, kf1->n, (int32_t*)(d + o_match), (int32_t*)(d + o_cnt));
         ok = hipGetLastError() == hipSuccess;
     }
     ok = ok && hipMemcpyAsync(h + o_match, d + o_match, o_cnt + (size_t)n_pairs * 4 - o_match, hipMemcpyDeviceToHost,
@@ -462,6 +541,80 @@ int orb_search_for_triangulation(orb_matcher_t m, const orb_kf_view_t* kf1, cons
     if (kf1->n) memcpy(matches12, h + o_match, (size_t)n_pairs * kf1->n * 4);
     memcpy(n_matches, h + o_cnt, (size_t)n_pairs * 4);
     return ORB_OK;
+}
+
+int orb_search_for_triangulation_device(orb_matcher_t m, const orb_kf_device_t* kf1s, int n_kf1,
+                                        const orb_kf_device_t* kf2s, const int32_t* pair_kf1,
+                                        const orb_kf_pair_geom_t* geoms, int n_pairs, int only_stereo, int coarse,
+                                        int32_t* d_matches12, int32_t* d_n_matches, void* stream) {
+    if (!m || !kf1s || n_kf1 <= 0 || n_pairs < 0 || (n_pairs > 0 && (!kf2s || !geoms || !d_matches12 || !d_n_matches)))
+        return orbgpu_fail(ORB_ERR_ARG, "bad SearchForTriangulation arguments");
+    if (n_pairs == 0) return ORB_OK;
+    auto bad = [](const orb_kf_device_t& k) {
+        return k.cap <= 0 || !k.kps || !k.desc || !k.n || !k.fv_node || !k.fv_begin || !k.fv_feat || !k.n_nodes ||
+               k.nlevels <= 0 || k.nlevels > kMaxLevels || !k.scale_factors || !k.level_sigma2 ||
+               (reinterpret_cast<uintptr_t>(k.desc) & 15) != 0;
+    };
+    int C = 0;
+    for (int k = 0; k < n_kf1; ++k) {
+        if (bad(kf1s[k])) return orbgpu_fail(ORB_ERR_ARG, "invalid keyframe 1 device view");
+        C = std::max(C, kf1s[k].cap);
+    }
+    for (int p = 0; p < n_pairs; ++p) {
+        if (bad(kf2s[p])) return orbgpu_fail(ORB_ERR_ARG, "invalid keyframe 2 device view");
+        if (pair_kf1 && (pair_kf1[p] < 0 || pair_kf1[p] >= n_kf1)) return orbgpu_fail(ORB_ERR_ARG, "bad pair_kf1");
+    }
+    hipStream_t s = (hipStream_t)stream;
+    const int nkf = n_kf1 + n_pairs;
+    // upload: KfPtrs [n_kf1 first keyframes | n_pairs neighbours] | PairDev [n_pairs] | kf1 index per pair
+    const size_t o_pair = align256(nkf * sizeof(KfPtrs)), o_k1 = o_pair + align256(n_pairs * sizeof(PairDev));
+    const size_t bytes = o_k1 + align256(4 * (size_t)n_pairs);
+    // the pinned slot: wait until the previous call's upload has left it
+    if (!m->dev_ev && hipEventCreateWithFlags(&m->dev_ev, hipEventDisableTiming) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "event create");
+    if (hipEventSynchronize(m->dev_ev) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "device error");
+    if (bytes > m->h_dev_cap) {
+        if (m->h_dev) hipHostFree(m->h_dev);
+        m->h_dev = nullptr;
+        m->h_dev_cap = 0;
+        if (hipHostMalloc(&m->h_dev, bytes, hipHostMallocDefault) != hipSuccess)
+            return orbgpu_fail(ORB_ERR_DEVICE, "matcher pinned alloc");
+        m->h_dev_cap = bytes;
+    }
+    auto* kp = reinterpret_cast<KfPtrs*>(m->h_dev);
+    auto* pd = reinterpret_cast<PairDev*>(m->h_dev + o_pair);
+    auto* k1 = reinterpret_cast<int32_t*>(m->h_dev + o_k1);
+    for (int k = 0; k < nkf; ++k) {
+        const orb_kf_device_t& v = k < n_kf1 ? kf1s[k] : kf2s[k - n_kf1];
+        kp[k] = KfPtrs{v.kps, reinterpret_cast<const uint4*>(v.desc), v.n, v.u_right, v.has_mappoint, v.fv_node,
+                       v.fv_begin, v.fv_feat, v.n_nodes, v.cap, 0};
+    }
+    for (int p = 0; p < n_pairs; ++p) {
+        const orb_kf_device_t& v1 = kf1s[pair_kf1 ? pair_kf1[p] : 0];
+        const orb_kf_device_t& v2 = kf2s[p];
+        const float K1[4] = {v1.fx, v1.fy, v1.cx, v1.cy}, K2[4] = {v2.fx, v2.fy, v2.cx, v2.cy};
+        pd[p] = make_pair(K1, K2, v2.nlevels, v2.scale_factors, v2.level_sigma2, geoms[p]);
+        k1[p] = pair_kf1 ? pair_kf1[p] : 0;
+    }
+    // device copy, stream-ordered (calls on different streams do not share it)
+    char* d = nullptr;
+    if (hipMallocAsync(reinterpret_cast<void**>(&d), bytes, s) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "hipMallocAsync failed");
+    bool ok = hipMemcpyAsync(d, m->h_dev, bytes, hipMemcpyHostToDevice, s) == hipSuccess &&
+              hipEventRecord(m->dev_ev, s) == hipSuccess &&
+              hipMemsetAsync(d_matches12, 0xFF, (size_t)n_pairs * C * 4, s) == hipSuccess;
+    const DirectSrc src{reinterpret_cast<const KfPtrs*>(d)};
+    const int32_t* k1of = reinterpret_cast<const int32_t*>(d + o_k1);
+    if (ok) {  // node1 < *n_nodes <= cap: the grid covers the capacity, waves past the count return
+        hipLaunchKernelGGL(k_tri_match<DirectSrc>, dim3((C + kWaves - 1) / kWaves, n_pairs), dim3(64 * kWaves), 0, s, src,
+                           reinterpret_cast<const PairDev*>(d + o_pair), k1of, n_kf1, only_stereo ? 1 : 0,
+                           coarse ? 1 : 0, C, d_matches12);
+        hipLaunchKernelGGL(k_tri_finish<DirectSrc>, dim3(n_pairs), dim3(256), 0, s, src, k1of, n_kf1, m->check_ori, C,
+                           d_matches12, d_n_matches);
+        ok = hipGetLastError() == hipSuccess;
+    }
+    if (hipFreeAsync(d, s) != hipSuccess) ok = false;
+    return ok ? ORB_OK : orbgpu_fail(ORB_ERR_DEVICE, "SearchForTriangulation device error");
 }
 
 }  // extern "C"

@@ -69,6 +69,44 @@ class KeyFrame:
         return self._view
 
 
+class KfDeviceView(ctypes.Structure):  # orb_kf_device_t
+    _fields_ = [("kps", ctypes.c_void_p), ("desc", ctypes.c_void_p), ("n", ctypes.c_void_p), ("u_right", ctypes.c_void_p),
+                ("has_mappoint", ctypes.c_void_p), ("fv_node", ctypes.c_void_p), ("fv_begin", ctypes.c_void_p),
+                ("fv_feat", ctypes.c_void_p), ("n_nodes", ctypes.c_void_p), ("cap", ctypes.c_int32),
+                ("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),
+                ("nlevels", ctypes.c_int32), ("scale_factors", ctypes.c_void_p), ("level_sigma2", ctypes.c_void_p)]
+
+
+class DeviceKeyFrame:
+    """A keyframe whose features never left the GPU: frame `f` of the outputs of
+    ORBextractor.extract_batch_device (kps, desc, counts), compute_stereo_matches_batch_device (u_right,
+    optional) and ORBVocabulary.transform_frames_device (bow), plus the pose and intrinsics the pair
+    geometry needs.  has_mappoint: optional [B, cap] uint8 CUDA tensor."""
+
+    def __init__(self, extracted, bow, f: int, Tcw, camera, scale_factors, level_sigma2, u_right=None,
+                 has_mappoint=None):
+        kps, desc, counts = extracted
+        self._keep = (kps, desc, counts, bow, u_right, has_mappoint)
+        self.cap = int(kps.shape[1])
+        self.f = int(f)
+        self.Tcw = np.ascontiguousarray(Tcw, dtype=np.float32).reshape(3, 4)
+        self.fx, self.fy, self.cx, self.cy = (float(np.float32(v)) for v in camera)
+        self.mvScaleFactors = np.ascontiguousarray(scale_factors, dtype=np.float32)
+        self.mvLevelSigma2 = np.ascontiguousarray(level_sigma2, dtype=np.float32)
+        cap, f = self.cap, self.f
+        fv_node, fv_begin, fv_feat, bcounts = bow[2], bow[3], bow[4], bow[5]
+        self._view = KfDeviceView(kps.data_ptr() + 28 * cap * f, desc.data_ptr() + 32 * cap * f,
+                                  counts.data_ptr() + 8 * f, None if u_right is None else u_right.data_ptr() + 4 * cap * f,
+                                  None if has_mappoint is None else has_mappoint.data_ptr() + cap * f,
+                                  fv_node.data_ptr() + 4 * cap * f, fv_begin.data_ptr() + 4 * (cap + 1) * f,
+                                  fv_feat.data_ptr() + 4 * cap * f, bcounts.data_ptr() + 8 * f + 4, cap, self.fx,
+                                  self.fy, self.cx, self.cy, len(self.mvScaleFactors), self.mvScaleFactors.ctypes.data,
+                                  self.mvLevelSigma2.ctypes.data)
+
+    def view(self) -> KfDeviceView:
+        return self._view
+
+
 class FrameView(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int32), ("kps_un", ctypes.c_void_p), ("desc", ctypes.c_void_p),
                 ("u_right", ctypes.c_void_p), ("min_x", ctypes.c_float), ("max_x", ctypes.c_float),

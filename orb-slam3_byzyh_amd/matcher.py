@@ -7,7 +7,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import check
-from .keyframe import Frame, KeyFrame, KfView, LocalMapPoints, PairGeom
+from .keyframe import DeviceKeyFrame, Frame, KeyFrame, KfDeviceView, KfView, LocalMapPoints, PairGeom
 
 TH_HIGH = 100  # src/ORBmatcher.cc:36
 TH_LOW = 50    # src/ORBmatcher.cc:37
@@ -74,6 +74,47 @@ class ORBmatcher:
                                                        int(bOnlyStereo), int(bCoarse), m12.ctypes.data,
                                                        cnt.ctypes.data), "orb_search_for_triangulation")
         return [(int(cnt[i]), m12[i, :pKF1.N]) for i in range(p)]
+
+    def SearchForTriangulationDevice(self, pKF1: DeviceKeyFrame, neighbours, bOnlyStereo: bool, bCoarse: bool = False,
+                                     stream=None, out=None):
+        """SearchForTriangulation of a device-resident keyframe against device-resident neighbours
+        (orb_search_for_triangulation_device): no host hop for features, stereo depths or FeatureVectors.
+        Returns (matches12 [P, cap1] int32, counts [P] int32) CUDA tensors, asynchronous on `stream`."""
+        return self.SearchForTriangulationDeviceBatch([(pKF1, list(neighbours))], bOnlyStereo, bCoarse, stream, out)
+
+    def SearchForTriangulationDeviceBatch(self, groups, bOnlyStereo: bool, bCoarse: bool = False, stream=None, out=None,
+                                          prepared=None):
+        """Several new keyframes, each with its neighbours, in one launch: groups = [(kf1, [kf2, ...]), ...].
+        Returns (matches12 [P, C] int32, counts [P] int32), pairs in group order, C = max cap of the kf1s.
+        `prepared` (from prepare_device_batch) reuses the ctypes arrays of an identical earlier call."""
+        import torch
+        if prepared is None:
+            prepared = self.prepare_device_batch(groups)
+        kf1v, n1, kf2v, k1, geoms, n_pairs, C, dev = prepared
+        if out is None:
+            out = (torch.empty((max(n_pairs, 1), C), dtype=torch.int32, device=dev),
+                   torch.empty(max(n_pairs, 1), dtype=torch.int32, device=dev))
+        if n_pairs == 0:
+            return out
+        st = stream if stream is not None else torch.cuda.current_stream(dev)
+        check(_lib.load().orb_search_for_triangulation_device(self._handle(), kf1v, n1, kf2v, k1, geoms, n_pairs,
+                                                              int(bOnlyStereo), int(bCoarse), out[0].data_ptr(),
+                                                              out[1].data_ptr(), ctypes.c_void_p(st.cuda_stream)),
+              "orb_search_for_triangulation_device")
+        return out
+
+    def prepare_device_batch(self, groups):
+        """The ctypes arguments of SearchForTriangulationDeviceBatch for `groups` (views, pair table, geometry)."""
+        groups = [(k1, list(nb)) for k1, nb in groups]
+        n1 = len(groups)
+        kf1v = (KfDeviceView * max(n1, 1))(*[g[0].view() for g in groups])
+        pairs = [(i, k2) for i, (_, nb) in enumerate(groups) for k2 in nb]
+        n_pairs = len(pairs)
+        kf2v = (KfDeviceView * max(n_pairs, 1))(*[k2.view() for _, k2 in pairs])
+        k1 = (ctypes.c_int32 * max(n_pairs, 1))(*[i for i, _ in pairs])
+        geoms = (PairGeom * max(n_pairs, 1))(*[self.pair_geometry(groups[i][0], k2) for i, k2 in pairs])
+        C = max(g[0].cap for g in groups)
+        return kf1v, n1, kf2v, k1, geoms, n_pairs, C, groups[0][0]._keep[0].device
 
     @staticmethod
     def DescriptorDistance(a, b) -> int:

@@ -68,6 +68,29 @@ def stereo_pair(width: int = 752, height: int = 480, seed: int = 200, dmin: int 
     return left, right, disp
 
 
+def stereo_sequence(n: int, width: int = 752, height: int = 480, seed: int = 210, step_px: int = 6, disparity: int = 13,
+                    noise: float = 2.0):
+    """C3 as a keyframe stream: n rectified stereo pairs of one fronto-parallel textured plane seen by a
+    camera translating along x.  With the plane at depth Z = bf / disparity, frame k is the crop of a
+    wide polygon canvas at x = step_px * k (left) and step_px * k + disparity (right, u_R = u_L - d), so
+    every frame pair shares most of its corners and the epipolar geometry of the poses is exact:
+    Tcw_k = [I | -(k * step_px * Z / fx, 0, 0)].  Returns (left [n, H, W], right [n, H, W], Tcw [n, 3, 4],
+    Z)."""
+    fx = EUROC_K[0]
+    Z = EUROC_BF / disparity
+    canvas = polygon_frame(width + step_px * (n - 1) + disparity + 8, height, seed=seed,
+                           n_shapes=int(400 * (width + step_px * n) / width))
+    rng = np.random.default_rng(seed + 1)
+    left = np.stack([canvas[:, step_px * k: step_px * k + width] for k in range(n)])
+    right = np.stack([canvas[:, step_px * k + disparity: step_px * k + disparity + width] for k in range(n)])
+    right = np.clip(np.rint(right.astype(np.float32) + rng.normal(0.0, noise, right.shape)), 0, 255).astype(np.uint8)
+    Tcw = np.zeros((n, 3, 4), np.float32)
+    for k in range(n):
+        Tcw[k, :, :3] = np.eye(3)
+        Tcw[k, 0, 3] = -k * step_px * Z / fx
+    return np.ascontiguousarray(left), np.ascontiguousarray(right), Tcw, Z
+
+
 def frame_batch(n: int, width: int = 640, height: int = 480, seed0: int = 100) -> np.ndarray:
     return np.stack([polygon_frame(width, height, seed=seed0 + i) for i in range(n)])
 
