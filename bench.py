@@ -301,6 +301,160 @@ def bench_stereo(pkg, synth, dev, steps, cpu_baseline_on, n_pairs=32, n_sets=2):
     return out
 
 
+def bench_c3_chain(pkg, synth, dev, steps, cpu_baseline_on, n_kf=32, n_nb=10):
+    """C3 as LocalMapping consumes it, device-resident end to end: one step = n_kf new stereo keyframes
+    (752x480, nFeatures 1200) extracted left || right, Frame::ComputeStereoMatches, KeyFrame::ComputeBoW
+    (levelsup 4, k=10 L=6 vocabulary) and SearchForTriangulation of every new keyframe against its n_nb
+    predecessors in the stream (LocalMapping::CreateNewMapPoints, src/LocalMapping.cc:506-610), the
+    predecessors of the first keyframes coming from the previous step's buffers.  No host hop between the
+    stages.  Also one keyframe alone through the same chain (the latency LocalMapping sees)."""
+    import numpy as np
+    import torch
+    bf, b = 47.90639384423901, 0.110074
+    n_img = n_kf + n_nb
+    L_all, R_all, Tcw, _ = synth.stereo_sequence(n_img, seed=2100)
+    # step images: frames n_nb .. n_nb + n_kf - 1 of the stream; the previous step's buffers hold the
+    # same images, standing for frames 0 .. n_kf - 1 (their poses give the true relative geometry)
+    L = torch.from_numpy(L_all[n_nb:]).to(dev)
+    R = torch.from_numpy(R_all[n_nb:]).to(dev)
+    voc = synth.dbow_vocabulary(10, 6, seed=5, kmin=10, leaf_early=0.0)
+    vocab = pkg.ORBVocabulary(voc)
+    scale, sigma2 = synth.scale_tables()
+    cap = 1200 + 16 * 8
+    sets = []
+    for _ in range(2):
+        S = {"exl": pkg.ORBextractor(1200, 1.2, 8, 20, 7, max_width=752, max_height=480, max_batch=n_kf),
+             "exr": pkg.ORBextractor(1200, 1.2, 8, 20, 7, max_width=752, max_height=480, max_batch=n_kf),
+             "s_l": torch.cuda.Stream(dev), "s_r": torch.cuda.Stream(dev), "s_m": torch.cuda.Stream(dev)}
+        mk = lambda: (torch.empty((n_kf, cap, 7), dtype=torch.float32, device=dev),  # noqa: E731
+                      torch.empty((n_kf, cap, 32), dtype=torch.uint8, device=dev),
+                      torch.empty((n_kf, 2), dtype=torch.int32, device=dev))
+        S["out_l"], S["out_r"] = mk(), mk()
+        S["u"] = torch.empty((n_kf, cap), dtype=torch.float32, device=dev)
+        S["st_out"] = (S["u"], torch.empty((n_kf, cap), dtype=torch.float32, device=dev),
+                       torch.empty(n_kf, dtype=torch.int32, device=dev))
+        S["bow"] = (torch.empty((n_kf, cap), dtype=torch.int32, device=dev),
+                    torch.empty((n_kf, cap), dtype=torch.float64, device=dev),
+                    torch.empty((n_kf, cap), dtype=torch.int32, device=dev),
+                    torch.empty((n_kf, cap + 1), dtype=torch.int32, device=dev),
+                    torch.empty((n_kf, cap), dtype=torch.int32, device=dev),
+                    torch.empty((n_kf, 2), dtype=torch.int32, device=dev))
+        sets.append(S)
+    kfs = []  # kfs[set][f]: frame f of that set's buffers, at stream index n_nb + f (set 0) or f (set 1)
+    for si, S in enumerate(sets):
+        base = n_nb if si == 0 else 0
+        kfs.append([pkg.DeviceKeyFrame(S["out_l"], S["bow"], f, Tcw[base + f], synth.EUROC_K, scale, sigma2,
+                                       u_right=S["u"]) for f in range(n_kf)])
+    matcher = pkg.ORBmatcher(0.6, False)  # LocalMapping's ORBmatcher(0.6, false) (src/LocalMapping.cc:536)
+    # the new keyframes of set 0 against their predecessors: in set 0 before them, then the end of set 1
+    groups = []
+    for f in range(n_kf):
+        nb = [kfs[0][f - j] if f - j >= 0 else kfs[1][n_kf + f - j] for j in range(1, n_nb + 1)]
+        groups.append((kfs[0][f], nb))
+    prepared = matcher.prepare_device_batch(groups)
+    m_out = (torch.empty((n_kf * n_nb, cap), dtype=torch.int32, device=dev),
+             torch.empty(n_kf * n_nb, dtype=torch.int32, device=dev))
+
+    def extract(S, stream_done=None):
+        S["s_l"].wait_stream(S["s_m"])
+        S["s_r"].wait_stream(S["s_m"])
+        S["exl"].extract_batch_device(L, (0, 0), cap=cap, out=S["out_l"], stream=S["s_l"])
+        S["exr"].extract_batch_device(R, (0, 0), cap=cap, out=S["out_r"], stream=S["s_r"])
+        S["s_m"].wait_stream(S["s_l"])
+        S["s_m"].wait_stream(S["s_r"])
+        pkg.compute_stereo_matches_batch_device(S["exl"], S["exr"], S["out_l"], S["out_r"], bf, b, stream=S["s_m"],
+                                                out=S["st_out"])
+        vocab.transform_frames_device(S["out_l"][1], S["out_l"][2], 4, stream=S["s_m"], out=S["bow"])
+
+    # set 1 holds the previous step once; every timed step rebuilds set 0 and matches it
+    extract(sets[1])
+    S0 = sets[0]
+
+    def step(ev=None):
+        extract(S0)
+        if ev is not None:
+            ev[0].record(S0["s_m"])
+        matcher.SearchForTriangulationDeviceBatch(groups, False, False, stream=S0["s_m"], out=m_out, prepared=prepared)
+        if ev is not None:
+            ev[1].record(S0["s_m"])
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize(dev)
+    reps = max(6, min(steps, 20))
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    t0 = time.perf_counter()
+    for i in range(reps):
+        step(ev[i])
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) * 1e3
+    sft_ms = sum(a.elapsed_time(z) for a, z in ev) / reps
+    cnt = m_out[1].cpu().numpy()
+    # one keyframe alone (LocalMapping's latency): batch of 1 through the same chain, host sync at the end
+    one = {"exl": pkg.ORBextractor(1200, 1.2, 8, 20, 7, max_width=752, max_height=480, max_batch=1),
+           "exr": pkg.ORBextractor(1200, 1.2, 8, 20, 7, max_width=752, max_height=480, max_batch=1)}
+    st = torch.cuda.Stream(dev)
+    L1, R1 = L[n_kf - 1:n_kf].contiguous(), R[n_kf - 1:n_kf].contiguous()
+    o_l = (torch.empty((1, cap, 7), dtype=torch.float32, device=dev), torch.empty((1, cap, 32), dtype=torch.uint8, device=dev),
+           torch.empty((1, 2), dtype=torch.int32, device=dev))
+    o_r = tuple(torch.empty_like(t) for t in o_l)
+    nb1 = [kfs[0][n_kf - 1 - j] for j in range(1, n_nb + 1)]
+    o_st = (torch.empty((1, cap), dtype=torch.float32, device=dev), torch.empty((1, cap), dtype=torch.float32, device=dev),
+            torch.empty(1, dtype=torch.int32, device=dev))
+    o_bow = tuple(t[:1].clone() for t in sets[0]["bow"])
+    k1 = pkg.DeviceKeyFrame(o_l, o_bow, 0, Tcw[n_nb + n_kf - 1], synth.EUROC_K, scale, sigma2, u_right=o_st[0])
+    prep1 = matcher.prepare_device_batch([(k1, nb1)])
+    o_m = (torch.empty((n_nb, cap), dtype=torch.int32, device=dev), torch.empty(n_nb, dtype=torch.int32, device=dev))
+
+    def single():
+        one["exl"].extract_batch_device(L1, (0, 0), cap=cap, out=o_l, stream=st)
+        one["exr"].extract_batch_device(R1, (0, 0), cap=cap, out=o_r, stream=st)
+        pkg.compute_stereo_matches_batch_device(one["exl"], one["exr"], o_l, o_r, bf, b, stream=st, out=o_st)
+        vocab.transform_frames_device(o_l[1], o_l[2], 4, stream=st, out=o_bow)
+        r = matcher.SearchForTriangulationDeviceBatch(None, False, False, stream=st, out=o_m, prepared=prep1)
+        st.synchronize()
+        return r
+
+    for _ in range(3):
+        single()
+    lat = _median_ms(single, 30)
+    out = {"config": f"C3 keyframe stream: {n_kf} new stereo keyframes 752x480 per step (synthetic plane, camera "
+                     "translating along x), nFeatures 1200, extract left || right + ComputeStereoMatches + ComputeBoW "
+                     f"(k=10 L=6) + SearchForTriangulation of each against its {n_nb} predecessors, device-resident, "
+                     "one GPU",
+           "keyframes_per_ms": round(n_kf * reps / dt, 4), "ms_per_step": round(dt / reps, 4),
+           "sft_ms_per_step": round(sft_ms, 4), "sft_pairs_per_step": n_kf * n_nb,
+           "matches_per_pair": round(float(cnt.mean()), 1), "single_keyframe_ms": round(lat, 4)}
+    if cpu_baseline_on:
+        from oracle import oracle as oracle_mod
+        import concurrent.futures as cf
+        exo = [oracle_mod.OracleExtractor(1200, 1.2, 8, 20, 7) for _ in range(2)]
+        sc = exo[0].params()
+        hist = []
+        t0 = time.perf_counter()
+        nfr = 0
+        with cf.ThreadPoolExecutor(2) as pool:  # left || right, as Frame.cc:136-141; the rest on one thread
+            while time.perf_counter() - t0 < 4.0 or nfr < n_nb + 2:
+                g = nfr % n_img
+                (kl, dl, _), (kr, dr, _) = pool.map(lambda a: a[0](a[1], (0, 0)), [(exo[0], L_all[g]), (exo[1], R_all[g])])
+                ur, _, _ = oracle_mod.compute_stereo_matches(kl, dl, kr, dr, [exo[0].level_padded(l) for l in range(8)],
+                                                             [exo[1].level_padded(l) for l in range(8)], sc["scale"],
+                                                             sc["inv_scale"], bf, b)
+                _, fv = oracle_mod.bow_transform(voc, dl, 4)
+                k = pkg.KeyFrame(keys_un=kl, descriptors=dl, Tcw=Tcw[g], camera=synth.EUROC_K, scale_factors=scale,
+                                 level_sigma2=sigma2, u_right=ur, feat_vec=fv)
+                for k2 in hist[-n_nb:]:
+                    oracle_mod.search_for_triangulation(k, k2, matcher.pair_geometry(k, k2), False, False, False)
+                hist.append(k)
+                nfr += 1
+        cdt = (time.perf_counter() - t0) * 1e3
+        out["cpu_baseline"] = {"value": round(nfr / cdt, 5), "unit": "keyframes/ms", "cores": 2, "kind": "port",
+                               "sample": f"{nfr} keyframes of the stream in {cdt / 1e3:.1f} s: left and right extraction "
+                                         "on 2 threads, then stereo, BoW and SearchForTriangulation against up to "
+                                         f"{n_nb} predecessors on one (oracle)"}
+    return out
+
+
 def bench_pose(pkg, synth, dev, steps, cpu_baseline_on, n_frames=256, n_points=500):
     """Optimizer::PoseOptimization (tracking's motion-only BA), batched: one step = n_frames frames of
     ~n_points matched map points (50 % stereo, 8 % gross outliers), device-resident inputs."""
@@ -936,6 +1090,12 @@ def main():
             pose = bench_pose(pkg, synth, dev, args.steps, not args.no_cpu_baseline)
         except Exception as e:  # noqa: BLE001
             pose = {"error": repr(e)}
+    c3_chain = None
+    if not args.no_stereo and world == 1:
+        try:
+            c3_chain = bench_c3_chain(pkg, synth, dev, args.steps, not args.no_cpu_baseline)
+        except Exception as e:  # noqa: BLE001
+            c3_chain = {"error": repr(e)}
     bow = None
     if not args.no_bow and world == 1:
         try:
@@ -991,6 +1151,8 @@ def main():
         result["localba"] = localba
         if stereo is not None:
             result["stereo"] = stereo
+        if c3_chain is not None:
+            result["c3_chain"] = c3_chain
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -91,7 +91,7 @@ PROTOTYPES = {
     "orb_compute_distinctive_descriptors_device": (_i, [_vp, _vp, _i, _vp, _vp, _vp]),
     "orb_kf_pair_geometry": (_i, [_vp, _vp, _f, _f, _f, _f, _vp]),
     "orb_search_for_triangulation": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp]),
-    "orb_search_for_triangulation_device": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp]),
+    "orb_search_for_triangulation_device": (_i, [_vp, _vp, _i, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp]),
     "orb_search_by_projection_frame": (_i, [_vp, _vp, _vp, _f, _i, _vp, _vp]),
     "orb_search_by_projection_local": (_i, [_vp, _vp, _vp, _vp, _f, _i, _f, _vp, _vp]),
     "orb_compute_stereo_matches": (_i, [_vp, _vp, _vp, _i, _vp, _vp, _i, _vp, _f, _f, _vp, _vp]),

@@ -30,7 +30,7 @@ def compute_stereo_matches(left, right, keys_left, desc_left, keys_right, desc_r
     return ur, dp, kept
 
 
-def compute_stereo_matches_batch_device(left, right, out_left, out_right, mbf: float, mb: float, stream=None):
+def compute_stereo_matches_batch_device(left, right, out_left, out_right, mbf: float, mb: float, stream=None, out=None):
     """Batch form on the outputs of ``extract_batch_device`` of both extractors (frames 0..B-1).
 
     Returns (u_right [B, cap_l] float32, depth [B, cap_l] float32, kept [B] int32) CUDA tensors;
@@ -40,9 +40,11 @@ def compute_stereo_matches_batch_device(left, right, out_left, out_right, mbf: f
     kps_r, desc_r, counts_r = out_right
     b, cap_l = kps_l.shape[0], kps_l.shape[1]
     cap_r = kps_r.shape[1]
-    u = torch.empty((b, cap_l), dtype=torch.float32, device=kps_l.device)
-    d = torch.empty((b, cap_l), dtype=torch.float32, device=kps_l.device)
-    kept = torch.empty((b,), dtype=torch.int32, device=kps_l.device)
+    if out is None:
+        out = (torch.empty((b, cap_l), dtype=torch.float32, device=kps_l.device),
+               torch.empty((b, cap_l), dtype=torch.float32, device=kps_l.device),
+               torch.empty((b,), dtype=torch.int32, device=kps_l.device))
+    u, d, kept = out
     st = stream if stream is not None else torch.cuda.current_stream(kps_l.device)
     check(_lib.load().orb_compute_stereo_matches_batch_device(
         left._h, right._h, b, kps_l.data_ptr(), counts_l.data_ptr(), desc_l.data_ptr(), cap_l, kps_r.data_ptr(),

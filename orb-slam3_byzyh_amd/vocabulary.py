@@ -70,7 +70,7 @@ class ORBVocabulary:
                                                        ctypes.c_void_p(st.cuda_stream)), "orb_bow_transform_batch_device")
         return out
 
-    def transform_frames_device(self, desc, counts, levelsup: int = 4, stream=None):
+    def transform_frames_device(self, desc, counts, levelsup: int = 4, stream=None, out=None):
         """Device batch on the extractor's layout: desc [B, cap, 32] uint8 and counts [B, 2] int32 CUDA
         tensors as ORBextractor.extract_batch_device returns them (no compaction, no host hop).
         Returns (bow_word [B, cap], bow_value [B, cap], fv_node [B, cap], fv_begin [B, cap + 1],
@@ -78,9 +78,12 @@ class ORBVocabulary:
         import torch
         b, cap = desc.shape[0], desc.shape[1]
         dev = desc.device
-        out = (torch.empty((b, cap), dtype=torch.int32, device=dev), torch.empty((b, cap), dtype=torch.float64, device=dev),
-               torch.empty((b, cap), dtype=torch.int32, device=dev), torch.empty((b, cap + 1), dtype=torch.int32, device=dev),
-               torch.empty((b, cap), dtype=torch.int32, device=dev), torch.empty((b, 2), dtype=torch.int32, device=dev))
+        if out is None:
+            out = (torch.empty((b, cap), dtype=torch.int32, device=dev),
+                   torch.empty((b, cap), dtype=torch.float64, device=dev),
+                   torch.empty((b, cap), dtype=torch.int32, device=dev),
+                   torch.empty((b, cap + 1), dtype=torch.int32, device=dev),
+                   torch.empty((b, cap), dtype=torch.int32, device=dev), torch.empty((b, 2), dtype=torch.int32, device=dev))
         st = stream if stream is not None else torch.cuda.current_stream(dev)
         check(self._lib.orb_bow_transform_frames_device(self._h, desc.data_ptr(), counts.data_ptr(), b, cap, int(levelsup),
                                                         *[t.data_ptr() for t in out], ctypes.c_void_p(st.cuda_stream)),

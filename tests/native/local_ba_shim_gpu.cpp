@@ -253,34 +253,37 @@ static Expected expect(const Input& in, int stop_after, bool inertial, bool dept
     return x;
 }
 
+// The window's local point order (Gather on an untouched copy of the graph: the write-back's erasures
+// change MapPointMatches, so it cannot be re-derived from the graph after the call), as point indices.
+static std::vector<int> local_point_order(const Input& in) {
+    Graph g(in);
+    Window w;
+    w.Gather(g.pKF(), &g.M);
+    std::vector<int> idx;
+    for (MockMP* p : w.local_mps) idx.push_back((int)(p - g.P.data()));
+    return idx;
+}
+
 // RMSE of the written-back local keyframe poses (t, q) and points against the expectation's arrays
-static void written_rmse(Graph& g, const Expected& x, double* pose_rmse, double* point_rmse) {
-    Window w;  // the same window order (marks of a new kfid are not needed: a fresh graph is not used here)
+static void written_rmse(Graph& g, const Input& in, const Expected& x, double* pose_rmse, double* point_rmse) {
     double sp = 0, sq = 0;
     size_t np = 0, nq = 0;
-    // local KFs are pKF then its covisible list, in the vertex order of the expectation
+    // local KFs: pKF then its covisible list, the vertex order of the expectation
     std::vector<MockKF*> locals{g.pKF()};
     for (MockKF* k : g.pKF()->cov) locals.push_back(k);
     for (size_t i = 0; i < locals.size(); ++i) {
         const double* e = &x.pose[7 * i];
         for (int k = 0; k < 3; ++k) sp += (locals[i]->t[k] - e[k]) * (locals[i]->t[k] - e[k]);
-        // g2o normalises the sign of q (w >= 0) in the same way on both sides
         for (int k = 0; k < 4; ++k) sp += (locals[i]->q[k] - e[3 + k]) * (locals[i]->q[k] - e[3 + k]);
         np += 7;
     }
-    // local points: the window's order is pKF's slots, then each covisible KF's, first occurrence
-    std::vector<MockMP*> pts;
-    std::set<MockMP*> seen;
-    for (MockKF* k : locals)
-        for (MockMP* p : k->mps)
-            if (p && seen.insert(p).second) pts.push_back(p);
-    for (size_t i = 0; i < pts.size() && 3 * i + 2 < x.point.size(); ++i)
+    const std::vector<int> order = local_point_order(in);
+    for (size_t i = 0; i < order.size() && 3 * i + 2 < x.point.size(); ++i)
         for (int k = 0; k < 3; ++k) {
-            const double d = pts[i]->X[k] - x.point[3 * i + k];
+            const double d = g.P[order[i]].X[k] - x.point[3 * i + k];
             sq += d * d;
             ++nq;
         }
-    (void)w;
     *pose_rmse = std::sqrt(sp / std::max<size_t>(np, 1));
     *point_rmse = std::sqrt(sq / std::max<size_t>(nq, 1));
 }
@@ -296,7 +299,7 @@ static void test_full(orb_ba_t h, const Input& in, bool inertial) {
     CHECK(rc == ORB_OK);
     if (rc != ORB_OK) std::printf("  rc %d: %s\n", rc, orb_last_error());
     double pr, qr;
-    written_rmse(g, x, &pr, &qr);
+    written_rmse(g, in, x, &pr, &qr);
     std::printf("full(inertial=%d): %d it %d trials, pose rmse %.3g, point rmse %.3g, %zu erased (oracle %zu)\n",
                 (int)inertial, x.res.iterations, x.res.trials, pr, qr, g.M.erased.size(), x.erased.size());
     CHECK(pr < 1e-6 && qr < 1e-6);
@@ -327,7 +330,7 @@ static void test_aborted(orb_ba_t h, Input in) {
     int nf, no, nmp, ne;
     CHECK(orbgpu::LocalBundleAdjustment<Access>(h, g.pKF(), &stop, &g.M, nf, no, nmp, ne) == ORB_OK);
     double pr, qr;
-    written_rmse(g, x, &pr, &qr);
+    written_rmse(g, in, x, &pr, &qr);
     std::printf("aborted: %zu erased (expected %zu), pose diff %.3g, point diff %.3g\n", g.M.erased.size(),
                 x.erased.size(), pr, qr);
     CHECK(!x.erased.empty() && g.M.erased == x.erased);
@@ -360,7 +363,7 @@ static void test_stop_during(orb_ba_t h, const Input& in) {
         double best_p = 1e30, best_q = 1e30;
         for (int t = 0; t <= tfull; ++t) {
             double pr, qr;
-            written_rmse(g, at[t], &pr, &qr);
+            written_rmse(g, in, at[t], &pr, &qr);
             if (pr + qr < best_p + best_q) { best = t; best_p = pr; best_q = qr; }
         }
         std::printf("during (flag after %d us): matches the oracle stopped after %d of %d trials (pose %.3g, point "

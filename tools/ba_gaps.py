@@ -23,7 +23,8 @@ dur = defaultdict(list)
 gap = defaultdict(list)
 prev_end = None
 for name, st, en in rows_of(sys.argv[1]):
-    short = name.split("(")[0].replace("_ZN12_GLOBAL__N_1", "")[:40]
+    short = name.replace("(anonymous namespace)::", "").replace("_ZN12_GLOBAL__N_1", "")
+    short = (short[5:] if short.startswith("void ") else short).split("(")[0][:40]
     dur[short].append((en - st) / 1e3)
     if prev_end is not None and 0 <= st - prev_end < 200e3:
         gap[short].append((st - prev_end) / 1e3)
