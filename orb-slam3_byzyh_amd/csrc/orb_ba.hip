@@ -547,6 +547,20 @@ __device__ __forceinline__ double fmac_negbcast(double acc, double a, double b, 
     return acc;
 }
 
+// acc[c & 3] += w[c] * src(lane c of the 16-lane row), c = 0..15 in order: the 16 DPP FMAs in one block
+// with a single s_nop for the broadcast source (written before the block; no instruction inside
+// writes it), instead of one per FMA.  The accumulators' own dependencies are interlocked.
+#define MF_FMAC(C, A, W) "v_fmac_f64_dpp %" #A ", %4, %" #W " row_newbcast:" #C " row_mask:0xf bank_mask:0xf\n\t"
+__device__ __forceinline__ void fmac16_bcast(double acc[4], double src, const double w[16]) {
+    asm("s_nop 1\n\t" MF_FMAC(0, 0, 5) MF_FMAC(1, 1, 6) MF_FMAC(2, 2, 7) MF_FMAC(3, 3, 8) MF_FMAC(4, 0, 9)
+        MF_FMAC(5, 1, 10) MF_FMAC(6, 2, 11) MF_FMAC(7, 3, 12) MF_FMAC(8, 0, 13) MF_FMAC(9, 1, 14) MF_FMAC(10, 2, 15)
+        MF_FMAC(11, 3, 16) MF_FMAC(12, 0, 17) MF_FMAC(13, 1, 18) MF_FMAC(14, 2, 19) MF_FMAC(15, 3, 20)
+        : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])
+        : "v"(src), "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]), "v"(w[6]), "v"(w[7]),
+          "v"(w[8]), "v"(w[9]), "v"(w[10]), "v"(w[11]), "v"(w[12]), "v"(w[13]), "v"(w[14]), "v"(w[15]));
+}
+#undef MF_FMAC
+
 // The column values L[j][c] reach the other rows by DPP row broadcasts (every 16-lane row holds the
 // same block, so each row broadcasts within itself).
 template <bool kColMajor = false>
@@ -648,7 +662,7 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
     double* dk = pre + 4 * 256;               // [16][17]
     double* yv = dk + 16 * 17;                // [16 NT]
     double* xv = yv + 16 * kMfMaxNT;          // [16 NT]
-    __shared__ int fail, lk, tbar, xready, pre_ready[kMfMaxNT], cnt[kMfMaxNT];
+    __shared__ int fail, lk, tbar, xready, wdone, pre_ready[kMfMaxNT], cnt[kMfMaxNT];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int NT = (n + 15) >> 4, ntt = NT * (NT + 1) / 2;
@@ -657,6 +671,7 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
         fail = 0;
         lk = -1;
         tbar = 0;
+        wdone = 0;   // tile waves done with the backward operators W1 / W2
         xready = 0;  // number of x blocks published (x_{NT-1} first)
     }
     if (threadIdx.x < kMfMaxNT) {
@@ -709,51 +724,64 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
             if (lane == 0) __hip_atomic_store(&lk, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (trace && lane == 0) trace[kTrStep + (k * 16 + W) * 4 + 3] = clock64();
         }
-        // backward: x_j = L_jj^-T (y_j - sum_{k >= j+2} c_kj - L_{j+1,j}^T x_{j+1})
-        // The chain x_{j+1} -> x_j stays in registers: x_{j+1} and y_j reach the other lanes of a
-        // row by DPP broadcasts, and both 16x16 operands (L_{j+1,j} row r, L_jj^-1 column r) are
-        // loaded before the wait for the contributions.
-        double xn = 0.0;  // x_{j+1}[r16]
+        // backward: x_j = d_j - W1_j x_{j+1} - W2_j x_{j+2}, with W1_j = L_jj^-T L_{j+1,j}^T and
+        // W2_j = L_jj^-T L_{j+2,j}^T (16x16, formed by the tile waves from their registers after the
+        // forward) and d_j = L_jj^-T (y_j - sum_{k >= j+3} L_kj^T x_k).  The rows k >= j+3 were
+        // published three steps earlier, so their contributions are in by the time block j needs them:
+        // nothing on the x chain waits for another wave, and the chain itself is one 16-term product.
+        double* w2 = pan + kMfMaxNT * (kMfMaxNT - 1) / 2 * 16;  // W2_j (after the contribution slots)
+        // The operand rows are loaded without branches: W1 / W2 of a block without that neighbour come
+        // from a clamped slot and meet x = 0 there.  Slots no tile wave writes (NT < 3) are zeroed, so
+        // those products are exactly 0.
+        if (NT < 3) {
+            for (int t = lane; t < 256; t += 64) {
+                w2[t] = 0.0;
+                if (NT < 2) sub[t] = 0.0;
+            }
+            mf_wave_sync();
+        }
+        lds_flag_wait(&wdone, W, lane, &fail, 8);
+        double x1 = 0.0, x2 = 0.0;  // x_{j+1}[r16], x_{j+2}[r16]
         for (int j = NT - 1; j >= 0; --j) {
             if (trace && lane == 0) trace[kTrBack + j] = clock64();
-            const double* L = sub + j * 256;  // L_{j+1,j}[r][c] at [(c >> 2) * 64 + r + 16 (c & 3)]
             const double* lj = linv + j * 272;
-            double lr[16], li[16];
+            const double* w1j = sub + max(min(j, NT - 2), 0) * 256;
+            const double* w2j = w2 + max(min(j, NT - 3), 0) * 256;
+            double li[16], a1[16], a2[16];
 #pragma unroll
-            for (int rr = 0; rr < 16; ++rr) {
-                lr[rr] = j + 1 < NT ? L[(r16 >> 2) * 64 + rr + 16 * (r16 & 3)] : 0.0;
-                li[rr] = lj[r16 * 17 + rr];
+            for (int c = 0; c < 16; ++c) {  // L_jj^-1[c][r16]; W1_j, W2_j row r16 from O(W)
+                li[c] = lj[r16 * 17 + c];
+                const int o = (c >> 2) * 64 + r16 + 16 * (c & 3);
+                a1[c] = w1j[o];
+                a2[c] = w2j[o];
             }
-            lds_flag_wait(&cnt[j], NT - 2 - j, lane, &fail, 3);
+            lds_flag_wait(&cnt[j], NT - 3 - j, lane, &fail, 3);
             if (trace && lane == 0) trace[kTrWaited + j] = clock64();
-            double yj = yv[16 * j + r16];
+            double v = yv[16 * j + r16];
             {  // every contribution load issued at once, subtracted in the same order (kk descending);
-               // the missing ones are +0.0, which leaves yj unchanged bit for bit
+               // the missing ones are +0.0, which leaves v unchanged bit for bit
                 double cv[kMfMaxNT];
 #pragma unroll
                 for (int m = 0; m < kMfMaxNT; ++m) {
                     const int kk = NT - 1 - m;
-                    const bool have = kk >= j + 2;  // (load unconditionally from a valid slot: no branch per load)
-                    const double v = contrib[(have ? kk * (kk - 1) / 2 + j : 0) * 16 + r16];
-                    cv[m] = have ? v : 0.0;
+                    const bool have = kk >= j + 3;  // (load unconditionally from a valid slot: no branch per load)
+                    const double cval = contrib[(have ? kk * (kk - 1) / 2 + j : 0) * 16 + r16];
+                    cv[m] = have ? cval : 0.0;
                 }
 #pragma unroll
-                for (int m = 0; m < kMfMaxNT; ++m) yj -= cv[m];
+                for (int m = 0; m < kMfMaxNT; ++m) v -= cv[m];
             }
-            if (j + 1 < NT) {
-                double t4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                for (int rr = 0; rr < 16; ++rr) t4[rr & 3] = fmac_bcast(t4[rr & 3], xn, lr[rr], rr);
-                yj -= (t4[0] + t4[1]) + (t4[2] + t4[3]);
-            }
-            double v4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int rr = 0; rr < 16; ++rr) v4[rr & 3] = fmac_bcast(v4[rr & 3], yj, li[rr], rr);
-            xn = (v4[0] + v4[1]) + (v4[2] + v4[3]);
-            if (lane < 16) xv[16 * j + r16] = xn;
+            double d4[4] = {0.0, 0.0, 0.0, 0.0}, s4[4] = {0.0, 0.0, 0.0, 0.0};
+            fmac16_bcast(d4, v, li);
+            fmac16_bcast(s4, x2, a2);
+            fmac16_bcast(s4, x1, a1);
+            const double xj = ((d4[0] + d4[1]) + (d4[2] + d4[3])) - ((s4[0] + s4[1]) + (s4[2] + s4[3]));
+            if (lane < 16) xv[16 * j + r16] = xj;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_store(&xready, NT - j, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (trace && lane == 0) trace[kTrPub + j] = clock64();
+            x2 = x1;
+            x1 = xj;
         }
     } else {
         // ---------------- tile waves: slot s holds tile t = s W + w (packed i | j << 8) ----------------
@@ -873,8 +901,34 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) __hip_atomic_fetch_add(&tbar, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         lds_flag_wait(&tbar, W * NT, lane, &fail, 6);
-        // ---- backward: row k's tiles (k, j <= k - 2) contribute L_kj^T x_k; tile (k, j) is
-        // t = Tc(j) + (k - j), so the wave finds its own by arithmetic and dispatches to the slot
+        // ---- the backward operators of the diagonal wave: for the tiles (j+1, j) and (j+2, j) this
+        // wave holds, W = L_jj^-T L_ij^T = O^-1 form O(M X^T) with X = L_ij (A operand = the tile's own
+        // registers) and M = L_jj^-T (B operand from L_jj^-1, column-major); W1 -> sub[j], W2 -> w2[j]
+        {
+            double* w2 = pan + kMfMaxNT * (kMfMaxNT - 1) / 2 * 16;
+            auto make_w = [&](const f64x4& Tv, int i, int j) {
+                const double* lj = linv + j * 272;
+                f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Tv[q], lj[r16 * 17 + g4 + 4 * q], acc, 0, 0, 0);
+                double* dst = (i == j + 1 ? sub : w2) + j * 256;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) dst[q * 64 + lane] = acc[q];
+            };
+            // (a static walk over the wave's own slots: the slot index stays a compile-time
+            // constant, so T[] stays in registers, and no per-tile dispatch runs)
+#pragma unroll
+            for (int sl = 0; sl < SL; ++sl) {
+                if (tij[sl] < 0) continue;
+                const int i = tij[sl] & 255, j = tij[sl] >> 8;
+                if (i == j + 1 || i == j + 2) make_w(T[sl], i, j);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) __hip_atomic_fetch_add(&wdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        // ---- backward: row k's tiles (k, j <= k - 3) contribute L_kj^T x_k (the diagonal wave applies
+        // the two nearest sub-diagonal tiles itself, through W1 / W2), walking the wave's own slots
         auto contribute = [&](const f64x4& Tv, int k, int j, double xr) {
             double* cs = contrib + (k * (k - 1) / 2 + j) * 16;
 #pragma unroll
@@ -885,33 +939,20 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_fetch_add(&cnt[j], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         };
-        for (int k = NT - 1; k >= 2; --k) {
-            bool waited = false;
-            double xr = 0.0;
-            for (int j = k - 2; j >= 0; --j) {  // (k, k-2) first: block k-2 needs it soonest
-                const int t = Tc(j) + (k - j);
-                if (t % W != w) continue;
-                if (!waited) {
-                    lds_flag_wait(&xready, NT - k, lane, &fail, 7);  // x_k published
-                    xr = xv[16 * k + r16];
-                    waited = true;
-                }
-                switch (t / W) {
-#define MF_SLOT(S)                                                                            \
-    case S:                                                                                   \
-        if constexpr (S < SL) {                                                               \
-            asm volatile("; slot " #S); /* distinct cases: keeps T in registers (no merging) */ \
-            contribute(T[S], k, j, xr);                                                       \
-        }                                                                                     \
-        break;
-                    MF_SLOT(0) MF_SLOT(1) MF_SLOT(2) MF_SLOT(3) MF_SLOT(4) MF_SLOT(5) MF_SLOT(6) MF_SLOT(7)
-                    MF_SLOT(8) MF_SLOT(9) MF_SLOT(10) MF_SLOT(11) MF_SLOT(12) MF_SLOT(13) MF_SLOT(14) MF_SLOT(15)
-                    MF_SLOT(16) MF_SLOT(17) MF_SLOT(18) MF_SLOT(19) MF_SLOT(20) MF_SLOT(21) MF_SLOT(22) MF_SLOT(23)
-                    MF_SLOT(24) MF_SLOT(25) MF_SLOT(26) MF_SLOT(27) MF_SLOT(28) MF_SLOT(29) MF_SLOT(30) MF_SLOT(31)
-#undef MF_SLOT
-                    default: break;
-                }
-            }
+        auto mine = [&](int sl, int k) {  // slot sl holds a tile (k, j <= k - 3)
+            return tij[sl] >= 0 && (tij[sl] & 255) == k && (tij[sl] >> 8) <= k - 3;
+        };
+        for (int k = NT - 1; k >= 3; --k) {
+            bool any = false;
+#pragma unroll
+            for (int sl = 0; sl < SL; ++sl) any |= mine(sl, k);
+            if (!any) continue;
+            lds_flag_wait(&xready, NT - k, lane, &fail, 7);  // x_k published
+            const double xr = xv[16 * k + r16];
+            // the wave's tiles of row k, (k, k-3) first: slots ascend as the column descends
+#pragma unroll
+            for (int sl = 0; sl < SL; ++sl)
+                if (mine(sl, k)) contribute(T[sl], k, tij[sl] >> 8, xr);
         }
     }
     __syncthreads();
