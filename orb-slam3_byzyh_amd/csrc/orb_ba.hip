@@ -9,8 +9,8 @@
 //   chi2, Hpl = B^T W A, the point and pose parts of the quadratic form), Hpp (6x6 per free pose),
 //   Hll (3x3 per landmark), b, Dinv, Z = Hpl Dinv, S (dense n x n, n = 6 * free poses), x.
 // Host-built structure (once per call, g2o's buildStructure): Hessian indices (free poses by id,
-// then landmarks by id), landmark -> edges CSR (pose rows ascending), pose -> edges CSR, and the
-// list of (edge, edge) products feeding each upper block of S, in landmark order.
+// then landmarks by id), landmark -> edges CSR (pose rows ascending) and pose -> (landmark, edge)
+// lists in landmark order; the landmarks two poses share are found on the device (k_ba_schur_blocks).
 //
 // One LM iteration = k_ba_build (per edge: error, Huber weight, Jacobians, quadratic form parts)
 // -> k_ba_reduce_land / k_ba_reduce_pose (fixed-order reductions) -> per trial:
@@ -51,6 +51,17 @@ namespace {
 
 constexpr int kT = 256;
 
+// A free pose's observations: its free edges in landmark order, each with its landmark (the host's
+// pose_fl list; a landmark twice in one list = two edges between one keyframe and one map point).
+struct LandEdge {
+    int32_t l, e;
+};
+// one product of a Schur block: Z of edge a times Hpl of edge b
+struct EdgePair {
+    int32_t a, b;
+};
+
+
 struct EdgeDev {  // == orb_ba_edge_t
     int32_t point, pose, stereo;
     float inv_sigma2;
@@ -64,7 +75,8 @@ static_assert(sizeof(EdgeDev) == sizeof(orb_ba_edge_t), "edge layout");
 // exactly as g2o's OptimizationAlgorithmLevenberg::solve does on the host.
 struct LmState {
     double lambda, ni, current_chi, ini_chi, final_chi, initial_chi, user_lambda, tau;
-    int32_t it, qmax, nbad, phase, done, reject, terminated, trials, iterations, pad;
+    int32_t it, qmax, nbad, phase, done, reject, terminated, trials, iterations;
+    int32_t lin;  // which half of the double-buffered Hpl holds the current linearisation
 };
 // what the host reads after each unit (pinned)
 struct LmProgress {
@@ -72,6 +84,11 @@ struct LmProgress {
     int32_t done, it, trials, terminated;
 };
 enum { kGateBuild = 0, kGateBuild0 = 1, kGateTrial = 2, kGateRestore = 3 };
+
+// Hpl is double-buffered on the device-driven path: every trial linearises at its new estimate into
+// the other half, which becomes current when the trial is accepted (the next iteration's build
+// then has nothing left to compute).  Host-driven path (no state): the first half.
+__device__ __forceinline__ size_t hpl_cur(const LmState* st, size_t alt) { return st && st->lin ? alt : 0; }
 
 __device__ __forceinline__ bool lm_skip(const LmState* st, int kind) {
     if (!st) return false;
@@ -243,13 +260,13 @@ __global__ __launch_bounds__(kT) void k_ba_reduce_land(int nl, const int32_t* __
 
 // Hpp and b_p per free pose: one wave, lanes stride the pose's edges, fixed-order tree in LDS
 __device__ __forceinline__ void ba_reduce_pose(int p, int lane, const int32_t* __restrict__ off,
-                                               const int32_t* __restrict__ eidx, const double* __restrict__ ecp,
+                                               const LandEdge* __restrict__ eidx, const double* __restrict__ ecp,
                                                double* __restrict__ hpp, double* __restrict__ bp) {
     __shared__ double red[42][65];
     double s[42];
     for (int i = 0; i < 42; ++i) s[i] = 0;
     for (int k = off[p] + lane; k < off[p + 1]; k += 64) {
-        const double* q = ecp + 42 * (size_t)eidx[k];
+        const double* q = ecp + 42 * (size_t)eidx[k].e;
         for (int i = 0; i < 42; ++i) s[i] += q[i];
     }
     for (int i = 0; i < 42; ++i) red[i][lane] = s[i];
@@ -263,7 +280,7 @@ __device__ __forceinline__ void ba_reduce_pose(int p, int lane, const int32_t* _
     else bp[6 * (size_t)p + lane - 36] = t;
 }
 
-__global__ __launch_bounds__(64) void k_ba_reduce_pose(const int32_t* __restrict__ off, const int32_t* __restrict__ eidx,
+__global__ __launch_bounds__(64) void k_ba_reduce_pose(const int32_t* __restrict__ off, const LandEdge* __restrict__ eidx,
                                                        const double* __restrict__ ecp, double* __restrict__ hpp,
                                                        double* __restrict__ bp, const LmState* __restrict__ lm_st,
                                                        int lm_gk) {
@@ -311,9 +328,10 @@ __device__ __forceinline__ void land_dinv(const double* __restrict__ hll, int l,
 __global__ __launch_bounds__(kT) void k_ba_schur_edges(int nfe, const double* __restrict__ lam, const int32_t* __restrict__ fedge,
                                                        const int32_t* __restrict__ fland, const double* __restrict__ hll,
                                                        const double* __restrict__ bl, const double* __restrict__ hpl,
-                                                       double* __restrict__ z, double* __restrict__ cb,
+                                                       size_t hpl_alt, double* __restrict__ z, double* __restrict__ cb,
         const LmState* __restrict__ lm_st, int lm_gk) {
     if (lm_skip(lm_st, lm_gk)) return;
+    hpl += hpl_cur(lm_st, hpl_alt);
     const double lambda = *lam;
     const int t = blockIdx.x * kT + threadIdx.x;
     if (t >= nfe) return;
@@ -333,22 +351,91 @@ __global__ __launch_bounds__(kT) void k_ba_schur_edges(int nfe, const double* __
     }
 }
 
-// S block (bi, bj), bi <= bj, one wave: lanes split the block's (Z_a, Hpl_b) products, each
-// accumulating the full 6x6 partial sum; lane e < 36 then adds the 64 partials in lane order.
-// S = [Hpp + lambda I] - sum Z_a Hpl_b^T; written to both triangles.
-__device__ __forceinline__ void ba_schur_block(int blk, int lane, int n, double lambda, int add_diag,
-                                               const int32_t* __restrict__ bi, const int32_t* __restrict__ bj,
-                                               const int32_t* __restrict__ off, const int32_t* __restrict__ pa,
-                                               const int32_t* __restrict__ pb, const double* __restrict__ z,
+// upper-triangle block number -> (i, j), i <= j, row-major: row i starts at i nf - i (i - 1) / 2
+__device__ __forceinline__ void schur_block_ij(int blk, int nf, int& i, int& j) {
+    auto cum = [nf](int r) { return r * nf - r * (r - 1) / 2; };
+    const double T = 2.0 * nf + 1.0;
+    int r = (int)floor((T - sqrt(T * T - 8.0 * blk)) * 0.5);
+    r = max(0, min(r, nf - 1));
+    while (r > 0 && cum(r) > blk) --r;
+    while (r < nf - 1 && cum(r + 1) <= blk) ++r;
+    i = r;
+    j = r + (blk - cum(r));
+}
+
+constexpr int kSchurChunk = 512;  // landmarks of pose j's list staged in LDS per pass
+
+// The product list of S block (i, j), i <= j, built on the device once per solve (one wave per block):
+// the landmarks both poses see are found by searching each of pose i's observations in pose j's
+// (sorted by landmark, staged in LDS); the (Z edge, Hpl edge) pairs go out compacted in pose i's
+// list order (= landmark order) to pairs[blk_off[blk] ...], at most min(|i|, |j|) of them (a pose
+// sees a landmark once: the host rejects repeated (pose, point) edges), and the count to cnt[blk].
+__global__ __launch_bounds__(64) void k_ba_schur_pairs(int nf, const int32_t* __restrict__ pose_off,
+                                                       const LandEdge* __restrict__ pose_fl,
+                                                       const int32_t* __restrict__ blk_off, EdgePair* __restrict__ pairs,
+                                                       int32_t* __restrict__ cnt) {
+    __shared__ int32_t sl[kSchurChunk], se[kSchurChunk];
+    const int blk = blockIdx.x, lane = threadIdx.x;
+    int i, j;
+    schur_block_ij(blk, nf, i, j);
+    const int ib = pose_off[i], ie = pose_off[i + 1], jb = pose_off[j], je = pose_off[j + 1];
+    EdgePair* out = pairs + blk_off[blk];
+    int q = 0;  // pairs written (wave-uniform)
+    for (int jc = jb; jc < je; jc += kSchurChunk) {
+        const int jn = min(kSchurChunk, je - jc);
+        __syncthreads();  // the previous chunk's searches are done
+        for (int k = lane; k < jn; k += 64) {
+            const LandEdge v = pose_fl[jc + k];
+            sl[k] = v.l;
+            se[k] = v.e;
+        }
+        __syncthreads();
+        const int lmin = sl[0], lmax = sl[jn - 1];
+        for (int k0 = ib; k0 < ie; k0 += 64) {
+            const int k = k0 + lane;
+            LandEdge v{-1, -1};
+            if (k < ie) v = pose_fl[k];
+            int lo = 0;
+            bool has = false;
+            if (k < ie && v.l >= lmin && v.l <= lmax) {
+                int hi = jn;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (sl[mid] < v.l) lo = mid + 1;
+                    else hi = mid;
+                }
+                has = lo < jn && sl[lo] == v.l;
+            }
+            const uint64_t mask = __ballot(has);
+            const int pos = q + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+            if (has) out[pos] = EdgePair{v.e, se[lo]};
+            q += __popcll(mask);
+        }
+    }
+    if (lane == 0) cnt[blk] = q;
+}
+
+// S block (i, j), i <= j, one wave: lanes split the block's (Z_a, Hpl_b) products (k_ba_schur_pairs),
+// each accumulating the full 6x6 partial sum; lane e < 36 then adds the 64 partials in lane order.
+// S = [Hpp + lambda I] - sum Z_a Hpl_b^T, written to both triangles (every block of S, empty ones as 0).
+__device__ __forceinline__ void ba_schur_block(int blk, int lane, int n, int nf, double lambda, int add_diag,
+                                               const int32_t* __restrict__ blk_off, const EdgePair* __restrict__ pairs,
+                                               const int32_t* __restrict__ cnt, const double* __restrict__ z,
                                                const double* __restrict__ hpl, const double* __restrict__ hpp,
                                                double* __restrict__ S) {
     __shared__ double red[36][65];
+    int i, j;
+    schur_block_ij(blk, nf, i, j);
     double acc[36];
 #pragma unroll
     for (int k = 0; k < 36; ++k) acc[k] = 0;
-    for (int k = off[blk] + lane; k < off[blk + 1]; k += 64) {
-        const double* Z = z + 18 * (size_t)pa[k];
-        const double* H = hpl + 18 * (size_t)pb[k];
+    const EdgePair* pl = pairs + blk_off[blk];
+    const int np = cnt[blk];
+    for (int k = lane; k < np; k += 64) {
+        const EdgePair pr = pl[k];
+        const double* Z = z + 18 * (size_t)pr.a;
+        const double* H = hpl + 18 * (size_t)pr.b;
         double zr[18], hr[18];
 #pragma unroll
         for (int q = 0; q < 18; ++q) { zr[q] = Z[q]; hr[q] = H[q]; }
@@ -365,33 +452,31 @@ __device__ __forceinline__ void ba_schur_block(int blk, int lane, int n, double 
     double sum = 0;
     for (int q = 0; q < 64; ++q) sum += red[lane][q];
     const int r = lane / 6, c = lane % 6;
-    const int i = bi[blk], j = bj[blk];
-    double v = -sum;
+    double v = 0.0 - sum;
     if (i == j && add_diag) v = (hpp[36 * (size_t)i + 6 * r + c] + (r == c ? lambda : 0.0)) - sum;
     S[(size_t)(6 * i + r) * n + 6 * j + c] = v;
     S[(size_t)(6 * j + c) * n + 6 * i + r] = v;
 }
 
 
-__global__ __launch_bounds__(64) void k_ba_schur_blocks(int n, const double* __restrict__ lam, int add_diag,
-                                                        const int32_t* __restrict__ bi, const int32_t* __restrict__ bj,
-                                                        const int32_t* __restrict__ off, const int32_t* __restrict__ pa,
-                                                        const int32_t* __restrict__ pb, const double* __restrict__ z,
-                                                        const double* __restrict__ hpl, const double* __restrict__ hpp,
-                                                        double* __restrict__ S, const LmState* __restrict__ lm_st,
-                                                        int lm_gk) {
+__global__ __launch_bounds__(64) void k_ba_schur_blocks(int n, int nf, const double* __restrict__ lam, int add_diag,
+                                                        const int32_t* __restrict__ blk_off,
+                                                        const EdgePair* __restrict__ pairs, const int32_t* __restrict__ cnt,
+                                                        const double* __restrict__ z, const double* __restrict__ hpl,
+                                                        const double* __restrict__ hpp, double* __restrict__ S,
+                                                        const LmState* __restrict__ lm_st, int lm_gk) {
     if (lm_skip(lm_st, lm_gk)) return;
-    ba_schur_block(blockIdx.x, threadIdx.x, n, *lam, add_diag, bi, bj, off, pa, pb, z, hpl, hpp, S);
+    ba_schur_block(blockIdx.x, threadIdx.x, n, nf, *lam, add_diag, blk_off, pairs, cnt, z, hpl, hpp, S);
 }
 
 // b_S = b_p - sum over the pose's edges of Hpl_e db (one wave per free pose)
 __device__ __forceinline__ void ba_schur_rhs(int p, int lane, const int32_t* __restrict__ off,
-                                             const int32_t* __restrict__ eidx, const double* __restrict__ cb,
+                                             const LandEdge* __restrict__ eidx, const double* __restrict__ cb,
                                              const double* __restrict__ bp, int use_bp, double* __restrict__ bs) {
     __shared__ double red[6][65];
     double s[6] = {0, 0, 0, 0, 0, 0};
     for (int k = off[p] + lane; k < off[p + 1]; k += 64) {
-        const double* q = cb + 6 * (size_t)eidx[k];
+        const double* q = cb + 6 * (size_t)eidx[k].e;
         for (int i = 0; i < 6; ++i) s[i] += q[i];
     }
     for (int i = 0; i < 6; ++i) red[i][lane] = s[i];
@@ -404,7 +489,7 @@ __device__ __forceinline__ void ba_schur_rhs(int p, int lane, const int32_t* __r
     if (lane < 6) bs[6 * (size_t)p + lane] = (use_bp ? bp[6 * (size_t)p + lane] : 0.0) - red[lane][0];
 }
 
-__global__ __launch_bounds__(64) void k_ba_schur_rhs(const int32_t* __restrict__ off, const int32_t* __restrict__ eidx,
+__global__ __launch_bounds__(64) void k_ba_schur_rhs(const int32_t* __restrict__ off, const LandEdge* __restrict__ eidx,
                                                      const double* __restrict__ cb, const double* __restrict__ bp,
                                                      int use_bp, double* __restrict__ bs, const LmState* __restrict__ lm_st,
                                                      int lm_gk) {
@@ -1335,7 +1420,8 @@ __device__ void lm_build_done(LmState* st, double chi, double maxdiag) {
 // after a trial: accept (lambda shrinks) or reject (lambda grows; the next update starts from the
 // backup, and a final restore launch undoes a rejected last trial); at the end of the trial loop
 // the termination tests
-__device__ void lm_trial_done(LmState* st, double chi, double scale_part, bool failed, LmProgress* prog) {
+__device__ void lm_trial_done(LmState* st, double chi, double scale_part, bool failed, LmProgress* prog,
+                              bool flip_lin = false) {
     double tempChi = chi;
     if (failed) tempChi = DBL_MAX;
     double rho = st->current_chi - tempChi;
@@ -1348,6 +1434,7 @@ __device__ void lm_trial_done(LmState* st, double chi, double scale_part, bool f
         st->ni = 2;
         st->current_chi = tempChi;
         st->reject = 0;
+        if (flip_lin) st->lin ^= 1;  // the trial's linearisation (k_u_edges_trial<true>) is the next build's
     } else {
         st->lambda *= st->ni;
         st->ni *= 2;
@@ -1434,7 +1521,7 @@ __global__ __launch_bounds__(kT) void k_u_edges_build(int ne, const EdgeDev* __r
 // unit step 2 (build): Hpp/b_p (blocks [0, nf)), Hll/b_l (64 landmarks per block); the last block
 // sums chi2, takes max diag at iteration 0 and runs the build controller
 __global__ __launch_bounds__(64) void k_u_reduce_build(int nf, int nl, const int32_t* __restrict__ pose_off,
-                                                       const int32_t* __restrict__ pose_edge, const double* __restrict__ ecp,
+                                                       const LandEdge* __restrict__ pose_edge, const double* __restrict__ ecp,
                                                        double* __restrict__ hpp, double* __restrict__ bp,
                                                        const int32_t* __restrict__ land_off,
                                                        const int32_t* __restrict__ land_edge,
@@ -1494,21 +1581,20 @@ __global__ __launch_bounds__(64) void k_u_reduce_build(int nf, int nl, const int
     }
 }
 
-// unit step 4 (trial): S blocks (blocks [0, nblk)) and b_S (one block per free pose)
-__global__ __launch_bounds__(64) void k_u_schur(int n, int nblk, const double* __restrict__ lam,
-                                                const int32_t* __restrict__ bi, const int32_t* __restrict__ bj,
-                                                const int32_t* __restrict__ off, const int32_t* __restrict__ pa,
-                                                const int32_t* __restrict__ pb, const double* __restrict__ z,
-                                                const double* __restrict__ hpl, const double* __restrict__ hpp,
-                                                double* __restrict__ S, const int32_t* __restrict__ pose_off,
-                                                const int32_t* __restrict__ pose_edge, const double* __restrict__ cb,
-                                                const double* __restrict__ bp, double* __restrict__ bs,
-                                                const LmState* __restrict__ st) {
+// unit step 4 (trial): S blocks (blocks [0, nblk), the upper triangle) and b_S (one block per free pose)
+__global__ __launch_bounds__(64) void k_u_schur(int n, int nf, int nblk, const double* __restrict__ lam,
+                                                const int32_t* __restrict__ blk_off, const EdgePair* __restrict__ pairs,
+                                                const int32_t* __restrict__ cnt, const int32_t* __restrict__ pose_off,
+                                                const LandEdge* __restrict__ pose_fl, const double* __restrict__ z, const double* __restrict__ hpl,
+                                                size_t hpl_alt, const double* __restrict__ hpp, double* __restrict__ S,
+                                                const double* __restrict__ cb, const double* __restrict__ bp,
+                                                double* __restrict__ bs, const LmState* __restrict__ st) {
     if (lm_skip(st, kGateTrial)) return;
+    hpl += hpl_cur(st, hpl_alt);
     if ((int)blockIdx.x < nblk)
-        ba_schur_block(blockIdx.x, threadIdx.x, n, *lam, 1, bi, bj, off, pa, pb, z, hpl, hpp, S);
+        ba_schur_block(blockIdx.x, threadIdx.x, n, nf, *lam, 1, blk_off, pairs, cnt, z, hpl, hpp, S);
     else
-        ba_schur_rhs(blockIdx.x - nblk, threadIdx.x, pose_off, pose_edge, cb, bp, 1, bs);
+        ba_schur_rhs(blockIdx.x - nblk, threadIdx.x, pose_off, pose_fl, cb, bp, 1, bs);
 }
 
 // unit step 6 (trial): x_l per landmark and its update, then the pose updates; a rejected previous
@@ -1517,12 +1603,14 @@ __global__ __launch_bounds__(kT) void k_u_backsub_update(int nl, int nf, int n, 
                                                          const int32_t* __restrict__ off, const int32_t* __restrict__ eidx,
                                                          const EdgeDev* __restrict__ edges,
                                                          const int32_t* __restrict__ pose_h, const double* __restrict__ hpl,
-                                                         const double* __restrict__ bl, const double* __restrict__ hll,
+                                                         size_t hpl_alt, const double* __restrict__ bl,
+                                                         const double* __restrict__ hll,
                                                          double* __restrict__ x, const int32_t* __restrict__ free_pose,
                                                          const int32_t* __restrict__ land_point, double* __restrict__ pose,
                                                          double* __restrict__ pose_bak, double* __restrict__ point,
                                                          double* __restrict__ point_bak, const LmState* __restrict__ st) {
     if (lm_skip(st, kGateTrial)) return;
+    hpl += hpl_cur(st, hpl_alt);
     const bool rej = st->reject != 0;
     const int t = blockIdx.x * kT + threadIdx.x;
     if (t < nl) {
@@ -1533,13 +1621,18 @@ __global__ __launch_bounds__(kT) void k_u_backsub_update(int nl, int nf, int n, 
     }
 }
 
-// unit step 7 (trial): errors at the new estimate; the last block sums chi2 and computeScale and
-// runs the trial controller
+// unit step 7 (trial): errors at the new estimate and its linearisation (Hll/b_l and Hpp/b_p parts
+// in place: nothing reads them before the next build; Hpl into the other half); the last block sums
+// chi2 and computeScale and runs the trial controller, which makes the new linearisation current on
+// accept -- the next iteration's build at the same estimate would compute exactly these values
+template <bool kLin>
 __global__ __launch_bounds__(kT) void k_u_edges_trial(int ne, const EdgeDev* __restrict__ edges,
                                                       const orb_ba_camera_t* __restrict__ cams,
                                                       const double* __restrict__ pose, const double* __restrict__ point,
                                                       const int32_t* __restrict__ pose_h, Huber2 hub,
                                                       double* __restrict__ err, double* __restrict__ rho0_out,
+                                                      double* __restrict__ ecl, double* __restrict__ hpl, size_t hpl_alt,
+                                                      double* __restrict__ ecp,
                                                       double* __restrict__ part, unsigned* counter, int nx,
                                                       const double* __restrict__ x, const double* __restrict__ b,
                                                       const int32_t* __restrict__ status, double* __restrict__ scal,
@@ -1547,7 +1640,9 @@ __global__ __launch_bounds__(kT) void k_u_edges_trial(int ne, const EdgeDev* __r
     if (lm_skip(st, kGateTrial)) return;
     const int e = blockIdx.x * kT + threadIdx.x;
     double r = 0.0;
-    if (e < ne) r = ba_edge<false>(e, edges, cams, pose, point, pose_h, hub, err, rho0_out, nullptr, nullptr, nullptr, 0);
+    if (e < ne)
+        r = ba_edge<kLin>(e, edges, cams, pose, point, pose_h, hub, err, rho0_out, ecl, hpl + (st->lin ? 0 : hpl_alt),
+                          ecp, 0);
     const double bsum = block_sum<kT>(r);
     if (threadIdx.x == 0) part[blockIdx.x] = bsum;
     if (!last_block(counter)) return;
@@ -1574,7 +1669,7 @@ __global__ __launch_bounds__(kT) void k_u_edges_trial(int ne, const EdgeDev* __r
         scal[0] = chi;
         scal[1] = scale;
         scal[2] = failed ? 1.0 : 0.0;
-        lm_trial_done(st, chi, scale, failed, prog);
+        lm_trial_done(st, chi, scale, failed, prog, kLin);
         *counter = 0;
     }
 }
@@ -1607,19 +1702,28 @@ struct ScatterItem {
     uint64_t dst, off, bytes;
 };
 
+constexpr uint64_t kScatterZero = ~0ull;  // ScatterItem::off of an item that zero-fills its buffer
+
 __global__ __launch_bounds__(256) void k_ba_scatter(const uint8_t* __restrict__ src, const ScatterItem* __restrict__ items) {
     const ScatterItem it = items[blockIdx.y];
     uint8_t* dst = reinterpret_cast<uint8_t*>(it.dst);
-    const uint8_t* sp = src + it.off;
     const size_t n16 = it.bytes / 16;
+    if (it.off == kScatterZero) {
+        for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256)
+            reinterpret_cast<uint4*>(dst)[i] = make_uint4(0, 0, 0, 0);
+        if (blockIdx.x == 0 && threadIdx.x < it.bytes % 16) dst[n16 * 16 + threadIdx.x] = 0;
+        return;
+    }
+    const uint8_t* sp = src + it.off;
     for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256)
         reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(sp)[i];
     if (blockIdx.x == 0 && threadIdx.x < it.bytes % 16) dst[n16 * 16 + threadIdx.x] = sp[n16 * 16 + threadIdx.x];
 }
 
-// Per-solve inputs: add() records (device buffer, host source, bytes); pack() lays them out behind
-// the item table in one pinned buffer (a single copy from each source), which goes up in one
-// H2D copy and is spread by one k_ba_scatter launch.
+// Per-solve inputs: add() records (device buffer, host source, bytes), zero() a buffer to clear;
+// pack() lays the sources out behind the item table in one pinned buffer (a single copy from each
+// source), which goes up in one H2D copy and is spread by one k_ba_scatter launch (the clears too:
+// no memset launches).
 struct Stager {
     struct Src { const void* p; size_t off, bytes; };
     std::vector<ScatterItem> items;
@@ -1639,6 +1743,12 @@ struct Stager {
     bool add(DevBuf<T>& d, const std::vector<T>& v) {
         return add(d, v.data(), v.size());
     }
+    template <typename T>
+    bool zero(DevBuf<T>& d, size_t n) {
+        if (!d.grow(n)) return false;
+        if (n) items.push_back({(uint64_t)(uintptr_t)d.p, kScatterZero, n * sizeof(T)});
+        return true;
+    }
     size_t table_bytes() const { return (items.size() * sizeof(ScatterItem) + 255) & ~size_t(255); }
     void pack(uint8_t* dst) const {
         memcpy(dst, items.data(), items.size() * sizeof(ScatterItem));
@@ -1648,11 +1758,14 @@ struct Stager {
 
 struct orb_ba_s {
     hipStream_t stream = nullptr;
+    hipStream_t tail = nullptr;  // the end of a device-driven solve, beside the queued no-op unit
     DevBuf<double> pose, pose_bak, point, point_bak, err, rho0, ecl, hpl, ecp, hpp, hll, b, z, cb, S, bs, x, scal;
     DevBuf<EdgeDev> edges;
     DevBuf<orb_ba_camera_t> cams;
-    DevBuf<int32_t> pose_h, free_pose, land_point, land_off, land_edge, landf_off, landf_edge, fland, pose_off, pose_edge,
-        blk_i, blk_j, blk_off, pair_a, pair_b, status;
+    DevBuf<int32_t> pose_h, free_pose, land_point, land_off, land_edge, landf_off, landf_edge, fland, pose_off, status;
+    DevBuf<LandEdge> pose_fl;
+    DevBuf<int32_t> blk_off, blk_cnt;  // Schur block product lists (k_ba_schur_pairs)
+    DevBuf<EdgePair> pairs;
     DevBuf<uint8_t> depth;
     double* h_scal = nullptr;  // pinned: [0] chi2, [1] scale, [2] status, [3] maxdiag, [4] stop, [5] lambda
     DevBuf<LmState> lm;        // device-driven LM state
@@ -1663,7 +1776,6 @@ struct orb_ba_s {
     uint8_t* h_dl = nullptr;     // pinned download of the per-solve results
     size_t h_dl_cap = 0;
     DevBuf<uint8_t> d_stage;
-    LmState* h_lm = nullptr;   // pinned staging of the initial state
     LmProgress* h_prog = nullptr;  // pinned, written by k_lm_trial_done
     hipEvent_t unit_ev[2] = {nullptr, nullptr};
     // the LM unit (7 launches) captured as a HIP graph, reused while its launch arguments are unchanged
@@ -1692,8 +1804,12 @@ struct orb_ba_s {
         edges.release();
         cams.release();
         for (auto* d : {&pose_h, &free_pose, &land_point, &land_off, &land_edge, &landf_off, &landf_edge, &fland, &pose_off,
-                        &pose_edge, &blk_i, &blk_j, &blk_off, &pair_a, &pair_b, &status})
+                        &status})
             d->release();
+        pose_fl.release();
+        blk_off.release();
+        blk_cnt.release();
+        pairs.release();
         depth.release();
     }
 };
@@ -1727,8 +1843,8 @@ int orb_ba_create(orb_ba_t* out) {
     }
     auto* h = new orb_ba_s();
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&h->tail, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc(&h->h_scal, 8 * sizeof(double), hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc(&h->h_lm, sizeof(LmState), hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&h->h_prog, sizeof(LmProgress), hipHostMallocDefault) != hipSuccess || !h->lm.grow(1) ||
         hipEventCreateWithFlags(&h->unit_ev[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->unit_ev[1], hipEventDisableTiming) != hipSuccess) {
@@ -1742,6 +1858,7 @@ int orb_ba_create(orb_ba_t* out) {
 int orb_ba_destroy(orb_ba_t h) {
     if (!h) return ORB_OK;
     hipStreamSynchronize(h->stream);
+    hipStreamSynchronize(h->tail);
     h->release();
     h->red_buf.release();
     h->lm.release();
@@ -1750,7 +1867,6 @@ int orb_ba_destroy(orb_ba_t h) {
     h->d_stage.release();
     if (h->h_stage) hipHostFree(h->h_stage);
     if (h->h_dl) hipHostFree(h->h_dl);
-    if (h->h_lm) hipHostFree(h->h_lm);
     if (h->h_prog) hipHostFree(h->h_prog);
     for (hipEvent_t e : h->unit_ev)
         if (e) hipEventDestroy(e);
@@ -1759,7 +1875,8 @@ int orb_ba_destroy(orb_ba_t h) {
     h->trace.release();
     if (h->h_scal) hipHostFree(h->h_scal);
     if (h->h_red) hipHostFree(h->h_red);
-    hipStreamDestroy(h->stream);
+    if (h->stream) hipStreamDestroy(h->stream);
+    if (h->tail) hipStreamDestroy(h->tail);
     delete h;
     return ORB_OK;
 }
@@ -1887,6 +2004,8 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     using clk = std::chrono::steady_clock;
     const clk::time_point t_in = clk::now();
     clk::time_point t_struct = t_in, t_solve = t_in, t_order = t_in, t_csr = t_in, t_pairs = t_in, t_pack = t_in;
+    double unit_t[32];  // (trace) when each unit launch was seen complete, from t_pack
+    int n_unit_t = 0;
     auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
     const int np = pr->n_poses, nq = pr->n_points, ne_all = pr->n_edges;
     if (np < 0 || nq < 0 || ne_all < 0 || (np && (!pr->pose || !pr->pose_id || !pr->pose_fixed || !pr->pose_camera)) ||
@@ -1980,9 +2099,11 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     const int ne = dist ? (int)lmap.size() : ne_all, nl = (int)land_point.size();
     const int n = 6 * nf, m = 3 * nl;
 
-    // landmark -> all edges (edge order), landmark -> free-pose edges (pose row ascending), pose -> edges
-    std::vector<int32_t> land_off(nl + 1, 0), land_edge(ne), landf_off(nl + 1, 0), landf_edge, pose_off(nf + 1, 0),
-        pose_edge;
+    // landmark -> all edges (edge order), landmark -> free-pose edges (pose row ascending), pose -> its
+    // free edges in landmark order with the landmark (pose_fl: the Schur blocks find the landmarks two
+    // poses share by searching one pose's list in the other's, no product list)
+    std::vector<int32_t> land_off(nl + 1, 0), land_edge(ne), landf_off(nl + 1, 0), landf_edge, pose_off(nf + 1, 0);
+    std::vector<LandEdge> pose_fl;
     for (int e = 0; e < ne; ++e) {
         land_off[point_l[ledges[e].point] + 1]++;
         if (pose_h[ledges[e].pose] >= 0) {
@@ -1993,75 +2114,59 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     for (int l = 0; l < nl; ++l) { land_off[l + 1] += land_off[l]; landf_off[l + 1] += landf_off[l]; }
     for (int p = 0; p < nf; ++p) pose_off[p + 1] += pose_off[p];
     landf_edge.resize(landf_off[nl]);
-    pose_edge.resize(pose_off[nf]);
+    pose_fl.resize(pose_off[nf]);
     {
-        std::vector<int32_t> c1(land_off.begin(), land_off.end() - 1), c2(landf_off.begin(), landf_off.end() - 1),
-            c3(pose_off.begin(), pose_off.end() - 1);
+        std::vector<int32_t> c1(land_off.begin(), land_off.end() - 1), c2(landf_off.begin(), landf_off.end() - 1);
         for (int e = 0; e < ne; ++e) {
-            const int l = point_l[ledges[e].point], p = pose_h[ledges[e].pose];
+            const int l = point_l[ledges[e].point];
             land_edge[c1[l]++] = e;
-            if (p >= 0) {
-                landf_edge[c2[l]++] = e;
-                pose_edge[c3[p]++] = e;
-            }
+            if (pose_h[ledges[e].pose] >= 0) landf_edge[c2[l]++] = e;
         }
     }
     // each landmark's free-pose edges by pose row, stable: an insertion sort (a landmark has a handful
-    // of edges; std::stable_sort allocated a buffer per landmark)
-    for (int l = 0; l < nl; ++l) {
-        int32_t* e0 = landf_edge.data() + landf_off[l];
-        const int d = landf_off[l + 1] - landf_off[l];
-        for (int a = 1; a < d; ++a) {
-            const int32_t v = e0[a];
-            const int32_t key = pose_h[ledges[v].pose];
-            int b = a;
-            for (; b > 0 && pose_h[ledges[e0[b - 1]].pose] > key; --b) e0[b] = e0[b - 1];
-            e0[b] = v;
-        }
-    }
+    // of edges; std::stable_sort allocated a buffer per landmark); then the pose lists in landmark order
     const int nfe = (int)landf_edge.size();
     std::vector<int32_t> fland(nfe);
-    for (int l = 0; l < nl; ++l)
-        for (int k = landf_off[l]; k < landf_off[l + 1]; ++k) fland[k] = l;
-    t_csr = clk::now();
-    // Schur block pattern: every diagonal block, then the (row_a <= row_b) products per landmark.
-    // Blocks are numbered in (row, column) order; each block's products are listed in landmark order
-    // (the fixed summation order of k_u_schur).  Pass 1 counts the products per block cell, pass 2
-    // places them.
-    std::vector<int32_t> frow(nfe);
-    for (int k = 0; k < nfe; ++k) frow[k] = pose_h[ledges[landf_edge[k]].pose];
-    std::vector<int32_t> cell((size_t)nf * nf, 0);
-    for (int l = 0; l < nl; ++l)
-        for (int a = landf_off[l]; a < landf_off[l + 1]; ++a) {
-            int32_t* row = cell.data() + (size_t)frow[a] * nf;
-            for (int b2 = a; b2 < landf_off[l + 1]; ++b2) row[frow[b2]]++;
-        }
-    std::vector<int32_t> blk_i, blk_j, blk_off{0};
-    std::vector<int32_t> cell_pos((size_t)nf * nf, -1);  // block cell -> next product slot
-    blk_i.reserve(4 * (size_t)nf);
-    blk_j.reserve(4 * (size_t)nf);
-    blk_off.reserve(4 * (size_t)nf + 1);
-    for (int i = 0; i < nf; ++i)
-        for (int j = i; j < nf; ++j) {
-            const int32_t c = cell[(size_t)i * nf + j];
-            if (c == 0 && j != i) continue;
-            cell_pos[(size_t)i * nf + j] = blk_off.back();
-            blk_i.push_back(i);
-            blk_j.push_back(j);
-            blk_off.push_back(blk_off.back() + c);
-        }
-    const int nblk = (int)blk_i.size();
-    std::vector<int32_t> pair_a(blk_off[nblk]), pair_b(blk_off[nblk]);
-    for (int l = 0; l < nl; ++l)
-        for (int a = landf_off[l]; a < landf_off[l + 1]; ++a) {
-            int32_t* row = cell_pos.data() + (size_t)frow[a] * nf;
-            for (int b2 = a; b2 < landf_off[l + 1]; ++b2) {
-                const int32_t q = row[frow[b2]]++;
-                pair_a[q] = landf_edge[a];
-                pair_b[q] = landf_edge[b2];
+    bool dup_edge = false;
+    {
+        std::vector<int32_t> c3(pose_off.begin(), pose_off.end() - 1);
+        for (int l = 0; l < nl; ++l) {
+            int32_t* e0 = landf_edge.data() + landf_off[l];
+            const int d = landf_off[l + 1] - landf_off[l];
+            for (int a = 1; a < d; ++a) {
+                const int32_t v = e0[a];
+                const int32_t key = pose_h[ledges[v].pose];
+                int b = a;
+                for (; b > 0 && pose_h[ledges[e0[b - 1]].pose] > key; --b) e0[b] = e0[b - 1];
+                e0[b] = v;
+            }
+            for (int k = 0; k < d; ++k) {
+                fland[landf_off[l] + k] = l;
+                pose_fl[c3[pose_h[ledges[e0[k]].pose]]++] = LandEdge{l, e0[k]};
+                if (k && pose_h[ledges[e0[k]].pose] == pose_h[ledges[e0[k - 1]].pose]) dup_edge = true;
             }
         }
-    t_pairs = clk::now();
+    }
+    if (agree_fail(dup_edge)) return orbgpu_fail(ORB_ERR_ARG, "two edges between one keyframe and one map point");
+    // every upper-triangle block of S (empty ones written as 0); block (i, j) lists at most
+    // min(|i|, |j|) products
+    const int nblk = nf * (nf + 1) / 2;
+    std::vector<int32_t> blk_off(nblk + 1);
+    {
+        int b = 0;
+        long long acc = 0;
+        for (int i = 0; i < nf; ++i) {
+            const int li = pose_off[i + 1] - pose_off[i];
+            for (int j = i; j < nf; ++j, ++b) {
+                blk_off[b] = (int32_t)acc;
+                acc += std::min(li, pose_off[j + 1] - pose_off[j]);
+            }
+        }
+        if (agree_fail(acc > INT32_MAX)) return orbgpu_fail(ORB_ERR_ARG, "BA window too large");
+        blk_off[nblk] = (int32_t)std::min<long long>(acc, INT32_MAX);
+    }
+    t_csr = clk::now();
+    t_pairs = t_csr;
     // poses normalised as SE3Quat(q, t) does
     std::vector<double> pose(pr->pose, pr->pose + 7 * (size_t)np);
     for (int i = 0; i < np; ++i) {
@@ -2071,6 +2176,14 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         if (nn > 0) for (int k = 0; k < 4; ++k) q[k] /= nn;
     }
 
+    const double tau = 1e-5;
+    LmState lm_init{};  // the device-driven loop's start (g2o's Levenberg state before iteration 0)
+    lm_init.ni = 2;
+    lm_init.user_lambda = opt->user_lambda_init;
+    lm_init.tau = tau;
+    lm_init.iterations = opt->iterations;
+    lm_init.done = opt->iterations <= 0;
+
     t_struct = clk::now();
     const size_t ne1 = std::max(ne, 1);
     Stager st;
@@ -2079,12 +2192,16 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
               st.add(h->pose_h, pose_h) && st.add(h->free_pose, free_pose) && st.add(h->land_point, land_point) &&
               st.add(h->land_off, land_off) && st.add(h->land_edge, land_edge) && st.add(h->landf_off, landf_off) &&
               st.add(h->landf_edge, landf_edge) && st.add(h->fland, fland) && st.add(h->pose_off, pose_off) &&
-              st.add(h->pose_edge, pose_edge) && st.add(h->blk_i, blk_i) && st.add(h->blk_j, blk_j) &&
-              st.add(h->blk_off, blk_off) && st.add(h->pair_a, pair_a) && st.add(h->pair_b, pair_b) &&
-              h->err.grow(3 * ne1) && h->rho0.grow(ne1) && h->ecl.grow(12 * ne1) && h->hpl.grow(18 * ne1) &&
+              st.add(h->pose_fl, pose_fl) && st.add(h->blk_off, blk_off) && h->blk_cnt.grow(std::max(nblk, 1)) &&
+              h->pairs.grow(std::max<size_t>(1, (size_t)blk_off[nblk])) &&
+              h->err.grow(3 * ne1) && h->rho0.grow(ne1) && h->ecl.grow(12 * ne1) && h->hpl.grow(36 * ne1) &&
               h->ecp.grow(42 * ne1) && h->hpp.grow(36 * (size_t)nf) && h->hll.grow(9 * (size_t)nl) && h->b.grow(n + m) &&
-              h->z.grow(18 * ne1) && h->cb.grow(6 * ne1) && h->S.grow((size_t)n * n) && h->bs.grow(n) && h->x.grow(n + m) && h->status.grow(1) &&
-              h->depth.grow(ne1);
+              h->z.grow(18 * ne1) && h->cb.grow(6 * ne1) && h->S.grow((size_t)n * n) && h->bs.grow(n) &&
+              h->depth.grow(ne1) && h->part.grow(grid(ne)) &&
+              // cleared by the scatter launch: g2o's _x starts zeroed, the scalars, the factorisation
+              // status, the last-block counters of the unit kernels; and the device LM state's start
+              st.zero(h->x, n + m) && st.zero(h->scal, 8) && st.zero(h->status, 1) && st.zero(h->counters, 2) &&
+              st.add(h->lm, &lm_init, 1);
     if (ok && !st.items.empty()) {
         // [items table | data], one pinned buffer, one copy, one scatter launch
         const size_t data_off = st.table_bytes(), total = data_off + st.data_bytes;
@@ -2105,6 +2222,9 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
             const unsigned gx = (unsigned)std::min<size_t>(64, std::max<size_t>(1, (maxb / 16 + 255) / 256));
             hipLaunchKernelGGL(k_ba_scatter, dim3(gx, (unsigned)st.items.size()), dim3(256), 0, s,
                                h->d_stage.p + data_off, (const ScatterItem*)h->d_stage.p);
+            if (nblk)  // the Schur blocks' product lists, for every trial of the solve
+                hipLaunchKernelGGL(k_ba_schur_pairs, dim3(nblk), dim3(64), 0, s, nf, h->pose_off.p, h->pose_fl.p,
+                                   h->blk_off.p, h->pairs.p, h->blk_cnt.p);
         }
     }
     // the pinned result buffer too, before the solve: [poses | points | edge chi2 | depth flags]
@@ -2117,9 +2237,6 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         if (ok) h->h_dl_cap = dl_bytes;
     }
     if (agree_fail(!ok)) return orbgpu_fail(ORB_ERR_DEVICE, "BA device allocation / upload");
-    hipMemsetAsync(h->x.p, 0, sizeof(double) * (n + m), s);  // g2o's _x starts zeroed
-    // S: the block pattern is fixed for the solve, so the blocks outside it are zeroed once here
-    if (n) hipMemsetAsync(h->S.p, 0, sizeof(double) * (size_t)n * n, s);
 
     const float dm = (float)std::sqrt(5.991), ds = (float)std::sqrt(7.815);  // src/Optimizer.cc:1957-1958
     const Huber2 hub{(double)dm, (double)ds, (float)((double)dm * (double)dm), (float)((double)ds * (double)ds)};
@@ -2180,6 +2297,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         }
     };
     double* bl = h->b.p + n;
+    const size_t hpl_alt = 18 * ne1;  // the second half of the double-buffered Hpl
     // The device-driven LM loop (one process): no host round trip per trial.  The host-driven loop
     // serves the sharded solve (its all-reduces are host calls) and ORBGPU_BA_HOST_LM=1 (tested in
     // tests/test_ba_gpu.py against the oracle).
@@ -2197,7 +2315,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
             hipLaunchKernelGGL(k_ba_reduce_land, dim3(grid(nl)), dim3(kT), 0, s, nl, h->land_off.p, h->land_edge.p,
                                h->ecl.p, h->hll.p, bl, G, (int)kGateBuild);
         if (nf) {
-            hipLaunchKernelGGL(k_ba_reduce_pose, dim3(nf), dim3(64), 0, s, h->pose_off.p, h->pose_edge.p, h->ecp.p,
+            hipLaunchKernelGGL(k_ba_reduce_pose, dim3(nf), dim3(64), 0, s, h->pose_off.p, h->pose_fl.p, h->ecp.p,
                                h->hpp.p, h->b.p, G, (int)kGateBuild);
             if (!dev_reduce(h, h->hpp.p, 36 * (size_t)nf, ORB_BA_SUM) || !dev_reduce(h, h->b.p, n, ORB_BA_SUM))
                 return false;
@@ -2214,12 +2332,11 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     auto launch_trial = [&]() -> bool {
         if (nfe)
             hipLaunchKernelGGL(k_ba_schur_edges, dim3(grid(nfe)), dim3(kT), 0, s, nfe, lam, h->landf_edge.p, h->fland.p,
-                               h->hll.p, bl, h->hpl.p, h->z.p, h->cb.p, G, (int)kGateTrial);
+                               h->hll.p, bl, h->hpl.p, hpl_alt, h->z.p, h->cb.p, G, (int)kGateTrial);
         if (nf) {
-            hipLaunchKernelGGL(k_ba_schur_blocks, dim3(nblk), dim3(64), 0, s, n, lam, primary ? 1 : 0, h->blk_i.p,
-                               h->blk_j.p, h->blk_off.p, h->pair_a.p, h->pair_b.p, h->z.p, h->hpl.p, h->hpp.p, h->S.p, G,
-                               (int)kGateTrial);
-            hipLaunchKernelGGL(k_ba_schur_rhs, dim3(nf), dim3(64), 0, s, h->pose_off.p, h->pose_edge.p, h->cb.p, h->b.p,
+            hipLaunchKernelGGL(k_ba_schur_blocks, dim3(nblk), dim3(64), 0, s, n, nf, lam, primary ? 1 : 0, h->blk_off.p,
+                               h->pairs.p, h->blk_cnt.p, h->z.p, h->hpl.p, h->hpp.p, h->S.p, G, (int)kGateTrial);
+            hipLaunchKernelGGL(k_ba_schur_rhs, dim3(nf), dim3(64), 0, s, h->pose_off.p, h->pose_fl.p, h->cb.p, h->b.p,
                                primary ? 1 : 0, h->bs.p, G, (int)kGateTrial);
             if (!dev_reduce(h, h->S.p, (size_t)n * n, ORB_BA_SUM) || !dev_reduce(h, h->bs.p, n, ORB_BA_SUM))
                 return false;
@@ -2241,8 +2358,9 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                            dev_lm || dist ? nullptr : h->h_scal, G, (int)kGateTrial);
         return true;
     };
+    hipStream_t rs = s;  // the stream of the restore and the results (see the device-driven loop)
     auto launch_restore = [&]() {
-        hipLaunchKernelGGL(k_ba_restore, dim3(grid(nf + nl)), dim3(kT), 0, s, nf, nl, h->free_pose.p, h->land_point.p,
+        hipLaunchKernelGGL(k_ba_restore, dim3(grid(nf + nl)), dim3(kT), 0, rs, nf, nl, h->free_pose.p, h->land_point.p,
                            h->pose.p, h->pose_bak.p, h->point.p, h->point_bak.p, G, (int)kGateRestore);
     };
     // the host loop reads [0] chi2, [1] computeScale, [2] status, [3] max diag (reduced over the ranks)
@@ -2254,54 +2372,54 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         return hipStreamSynchronize(s) == hipSuccess;
     };
 
-    const double tau = 1e-5;
-    hipMemsetAsync(h->scal.p, 0, 8 * sizeof(double), s);
     if (dev_lm) {
-        // One unit per trial: build (gated to the start of an iteration), the build controller, the
-        // trial, the trial controller, restore on reject.  The host keeps one unit queued behind the
-        // running one and reads the pinned progress after each unit's event; once the solve is done
-        // the queued unit is a run of no-op launches.
-        LmState init{};
-        init.ni = 2;
-        init.user_lambda = opt->user_lambda_init;
-        init.tau = tau;
-        init.iterations = opt->iterations;
-        init.done = opt->iterations <= 0;
-        *h->h_lm = init;
-        hipMemcpyAsync(h->lm.p, h->h_lm, sizeof(LmState), hipMemcpyHostToDevice, s);
+        // One unit per trial: the build's reductions and controller (gated to the start of an
+        // iteration; the linearisation itself comes from the accepted trial, or from the one build
+        // launch before the first unit), the trial, the trial controller, restore on reject.  The host
+        // keeps one unit queued behind the running one and reads the pinned progress after each
+        // unit's event; once the solve is done the queued unit is a run of no-op launches.
+        // (the state's start, the counters and the status went up with the inputs)
         memset(h->h_prog, 0, sizeof(LmProgress));
         const int nparts = (int)grid(ne);
-        if (!h->part.grow(nparts) || !h->counters.grow(2)) return orbgpu_fail(ORB_ERR_DEVICE, "BA unit buffers");
-        hipMemsetAsync(h->counters.p, 0, 2 * sizeof(unsigned), s);
-        hipMemsetAsync(h->status.p, 0, sizeof(int32_t), s);
         LmState* L = h->lm.p;
-        // one unit = 7 launches: edges+linearise, reductions (+ chi2, max diag, build controller),
-        // Schur edges, Schur blocks + rhs, Cholesky + solves, back-substitution + update, errors at
-        // the new estimate (+ chi2, computeScale, trial controller)
-        auto unit_launches = [&]() {
+        // one unit = 6 launches: reductions (+ chi2, max diag, build controller), Schur edges, Schur
+        // blocks + rhs, Cholesky + solves, back-substitution + update, errors and linearisation at the
+        // new estimate (+ chi2, computeScale, trial controller)
+        // ORBGPU_BA_TRIAL_LIN=1: every trial also linearises at its new estimate, so an accepted
+        // trial leaves nothing for the next build (default off: on MI355X the trial then costs what
+        // the build launch saves, C5 1.590 vs 1.582 ms per solve)
+        static const char* tl_env = getenv("ORBGPU_BA_TRIAL_LIN");
+        const bool trial_lin = tl_env && !strcmp(tl_env, "1");
+        auto launch_edges_build = [&]() {
             hipLaunchKernelGGL(k_u_edges_build, dim3(nparts), dim3(kT), 0, s, ne, h->edges.p, h->cams.p, h->pose.p,
                                h->point.p, h->pose_h.p, hub, h->err.p, h->rho0.p, h->ecl.p, h->hpl.p, h->ecp.p,
                                h->part.p, (const LmState*)L);
+        };
+        if (trial_lin) launch_edges_build();
+        auto unit_launches = [&]() {
+            if (!trial_lin) launch_edges_build();
             hipLaunchKernelGGL(k_u_reduce_build, dim3(nf + (nl + 63) / 64), dim3(64), 0, s, nf, nl, h->pose_off.p,
-                               h->pose_edge.p, h->ecp.p, h->hpp.p, h->b.p, h->land_off.p, h->land_edge.p, h->ecl.p,
+                               h->pose_fl.p, h->ecp.p, h->hpp.p, h->b.p, h->land_off.p, h->land_edge.p, h->ecl.p,
                                h->hll.p, bl, h->part.p, nparts, h->counters.p, h->scal.p, L);
             if (nfe)
                 hipLaunchKernelGGL(k_ba_schur_edges, dim3(grid(nfe)), dim3(kT), 0, s, nfe, lam, h->landf_edge.p,
-                                   h->fland.p, h->hll.p, bl, h->hpl.p, h->z.p, h->cb.p, (const LmState*)L,
+                                   h->fland.p, h->hll.p, bl, h->hpl.p, hpl_alt, h->z.p, h->cb.p, (const LmState*)L,
                                    (int)kGateTrial);
             if (nf) {
-                hipLaunchKernelGGL(k_u_schur, dim3(nblk + nf), dim3(64), 0, s, n, nblk, lam, h->blk_i.p, h->blk_j.p,
-                                   h->blk_off.p, h->pair_a.p, h->pair_b.p, h->z.p, h->hpl.p, h->hpp.p, h->S.p,
-                                   h->pose_off.p, h->pose_edge.p, h->cb.p, h->b.p, h->bs.p, (const LmState*)L);
+                hipLaunchKernelGGL(k_u_schur, dim3(nblk + nf), dim3(64), 0, s, n, nf, nblk, lam, h->blk_off.p,
+                                   h->pairs.p, h->blk_cnt.p, h->pose_off.p, h->pose_fl.p, h->z.p, h->hpl.p, hpl_alt, h->hpp.p, h->S.p, h->cb.p, h->b.p, h->bs.p,
+                                   (const LmState*)L);
                 launch_chol((const LmState*)L);
             }
             hipLaunchKernelGGL(k_u_backsub_update, dim3(grid(nl + nf)), dim3(kT), 0, s, nl, nf, n, lam, h->landf_off.p,
-                               h->landf_edge.p, h->edges.p, h->pose_h.p, h->hpl.p, bl, h->hll.p, h->x.p, h->free_pose.p,
+                               h->landf_edge.p, h->edges.p, h->pose_h.p, h->hpl.p, hpl_alt, bl, h->hll.p, h->x.p,
+                               h->free_pose.p,
                                h->land_point.p, h->pose.p, h->pose_bak.p, h->point.p, h->point_bak.p,
                                (const LmState*)L);
-            hipLaunchKernelGGL(k_u_edges_trial, dim3(nparts), dim3(kT), 0, s, ne, h->edges.p, h->cams.p, h->pose.p,
-                               h->point.p, h->pose_h.p, hub, h->err.p, h->rho0.p, h->part.p, h->counters.p + 1, n + m,
-                               h->x.p, h->b.p, h->status.p, h->scal.p, L, h->h_prog);
+            hipLaunchKernelGGL(trial_lin ? k_u_edges_trial<true> : k_u_edges_trial<false>, dim3(nparts), dim3(kT), 0, s, ne, h->edges.p, h->cams.p, h->pose.p,
+                               h->point.p, h->pose_h.p, hub, h->err.p, h->rho0.p, h->ecl.p, h->hpl.p, hpl_alt, h->ecp.p,
+                               h->part.p, h->counters.p + 1, n + m, h->x.p, h->b.p, h->status.p, h->scal.p, L,
+                               h->h_prog);
         };
         // Every unit launches the same kernels with the same arguments (the device state gates them),
         // so the unit is captured once as a graph and replayed: one graph launch instead of 7 kernel
@@ -2320,14 +2438,14 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                 (uintptr_t)h->edges.p, (uintptr_t)h->cams.p, (uintptr_t)h->pose.p, (uintptr_t)h->point.p,
                 (uintptr_t)h->pose_h.p, (uintptr_t)h->err.p, (uintptr_t)h->rho0.p, (uintptr_t)h->ecl.p,
                 (uintptr_t)h->hpl.p, (uintptr_t)h->ecp.p, (uintptr_t)h->part.p, (uintptr_t)h->pose_off.p,
-                (uintptr_t)h->pose_edge.p, (uintptr_t)h->hpp.p, (uintptr_t)h->b.p, (uintptr_t)h->land_off.p,
+                (uintptr_t)h->pose_fl.p, (uintptr_t)h->hpp.p, (uintptr_t)h->b.p, (uintptr_t)h->land_off.p,
                 (uintptr_t)h->land_edge.p, (uintptr_t)h->hll.p, (uintptr_t)h->counters.p, (uintptr_t)h->scal.p,
                 (uintptr_t)L, (uintptr_t)lam, (uintptr_t)h->landf_edge.p, (uintptr_t)h->fland.p, (uintptr_t)h->z.p,
-                (uintptr_t)h->cb.p, (uintptr_t)h->blk_i.p, (uintptr_t)h->blk_j.p, (uintptr_t)h->blk_off.p,
-                (uintptr_t)h->pair_a.p, (uintptr_t)h->pair_b.p, (uintptr_t)h->S.p, (uintptr_t)h->bs.p,
+                (uintptr_t)h->cb.p, (uintptr_t)h->S.p, (uintptr_t)h->blk_off.p, (uintptr_t)h->pairs.p,
+                (uintptr_t)h->blk_cnt.p, (uintptr_t)h->bs.p,
                 (uintptr_t)h->x.p, (uintptr_t)h->status.p, (uintptr_t)h->landf_off.p, (uintptr_t)h->free_pose.p,
                 (uintptr_t)h->land_point.p, (uintptr_t)h->pose_bak.p, (uintptr_t)h->point_bak.p, (uintptr_t)h->h_prog,
-                (uintptr_t)use_rows, (uintptr_t)h->lpub.p, (uintptr_t)h->ypub.p, (uintptr_t)h->cflag.p,
+                (uintptr_t)use_rows, (uintptr_t)trial_lin, (uintptr_t)h->lpub.p, (uintptr_t)h->ypub.p, (uintptr_t)h->cflag.p,
                 (uintptr_t)h->racc.p};
             if (!h->unit_exec || key != h->unit_key) {
                 if (h->unit_exec) { hipGraphExecDestroy(h->unit_exec); h->unit_exec = nullptr; }
@@ -2357,7 +2475,6 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
             return hipEventRecord(h->unit_ev[u & 1], s) == hipSuccess;
         };
         const int max_units = (std::max(0, opt->iterations) * 10 + units_per_launch - 1) / units_per_launch;
-        bool stopped_mid = false;
         if (max_units > 0) {
             if (!unit(0)) return orbgpu_fail(ORB_ERR_DEVICE, "BA launch failed");
             for (int u = 1;; ++u) {
@@ -2365,15 +2482,19 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                 if (more && !unit(u)) return orbgpu_fail(ORB_ERR_DEVICE, "BA launch failed");
                 if (hipEventSynchronize(h->unit_ev[(u - 1) & 1]) != hipSuccess)
                     return orbgpu_fail(ORB_ERR_DEVICE, "BA device error");
-                if (h->h_prog->done || !more) break;
-                if (stop_requested(opt)) {
-                    stopped_mid = true;
-                    break;
+                if (trace && n_unit_t < 32) unit_t[n_unit_t++] = us(t_pack, clk::now());
+                if (h->h_prog->done && more) {
+                    // the solve ended inside unit u-1 and unit u, queued behind it, is a run of gated
+                    // no-op launches: the restore and the results go on the tail stream beside it
+                    if (hipStreamWaitEvent(h->tail, h->unit_ev[(u - 1) & 1], 0) != hipSuccess)
+                        return orbgpu_fail(ORB_ERR_DEVICE, "BA device error");
+                    rs = h->tail;
                 }
+                if (h->h_prog->done || !more) break;
+                if (stop_requested(opt)) break;  // (the queued unit is live: the tail stays on s)
             }
         }
         launch_restore();  // undo a rejected last trial (gated on the device state)
-        (void)stopped_mid;
         // (the progress record is read after the results' synchronisation below)
     } else {
         double lambda = 0, ni = 2;
@@ -2432,10 +2553,10 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     {
         const int nt = std::max(std::max(7 * np, 3 * nq), ne);
         if (nt > 0)
-            hipLaunchKernelGGL(k_ba_results, dim3(grid(nt)), dim3(kT), 0, s, np, nq, ne, h->edges.p, h->pose.p,
+            hipLaunchKernelGGL(k_ba_results, dim3(grid(nt)), dim3(kT), 0, rs, np, nq, ne, h->edges.p, h->pose.p,
                                h->point.p, h->err.p, dpose, pts, lchi, ldep);
     }
-    if (hipStreamSynchronize(s) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "BA device error");
+    if (hipStreamSynchronize(rs) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "BA device error");
     if (dev_lm) {
         const LmProgress pg = *h->h_prog;
         res->iterations = pg.it;
@@ -2457,6 +2578,11 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                             "results %.1f us, it %d trials %d\n",
                     us(t_in, t_struct), us(t_in, t_order), us(t_order, t_csr), us(t_csr, t_pairs), us(t_pairs, t_struct),
                     us(t_struct, t_pack), us(t_pack, t_solve), us(t_solve, clk::now()), res->iterations, res->trials);
+        if (trace && n_unit_t) {
+            fprintf(stderr, "[ba] launches seen done at");
+            for (int i = 0; i < n_unit_t; ++i) fprintf(stderr, " %.1f", unit_t[i]);
+            fprintf(stderr, " us\n");
+        }
         return ORB_OK;
     }
     // gather: each rank contributes its landmarks (rank 0 also the points without edges) and its

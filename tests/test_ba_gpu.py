@@ -82,3 +82,16 @@ def test_local_bundle_adjustment_culling(pkg, oracle, synth):
     rerase = np.where(st, rchi2 > 7.815, rchi2 > 5.991) | ~rdepth
     assert np.array_equal(erase, rerase)
     assert 0 < erase.sum() < len(erase)
+
+
+def test_local_ba_repeated_edge_rejected(pkg, synth, solver):
+    """Two edges between one free keyframe and one map point (only the two-camera rig makes them,
+    src/Optimizer.cc:1879-1912, and the LocalBA shim hands that window to the reference body) are
+    refused with ORB_ERR_ARG before anything runs on the device; the handle stays usable."""
+    prob = synth.local_ba_problem(n_kf=6, n_points=150, obs_per_point=4, n_fixed=1, seed=3)
+    free = np.flatnonzero(prob["pose_fixed"][prob["edges"]["pose"]] == 0)
+    dup = dict(prob, edges=np.concatenate([prob["edges"], prob["edges"][free[:1]]]))
+    with pytest.raises(RuntimeError, match="one keyframe and one map point"):
+        solver.optimize(dup, 5)
+    _, _, _, _, res = solver.optimize(prob, 5)
+    assert res["iterations"] > 0

@@ -13,6 +13,7 @@ tail -3 $O/ba_${T}_tests.log
 ORBGPU_BA_TRACE=1 timeout -k 10 120 python3 tools/ba_trace.py > $O/ba_${T}_trace.log 2>&1 || exit 1
 python3 tools/chol_trace_summary.py $O/ba_${T}_trace.log > $O/ba_${T}_trace_summary.txt || exit 1
 head -3 $O/ba_${T}_trace_summary.txt
+grep "^\[ba\]" $O/ba_${T}_trace.log | tail -3
 timeout -k 10 120 python3 tools/ba_time.py --gpu-only > $O/ba_${T}_time.txt 2>&1 || exit 1
 cat $O/ba_${T}_time.txt
 timeout -k 10 150 rocprofv3 --kernel-trace --output-format csv -d $PWD/$O/ba_${T}_kt -o k -- python3 tools/ba_time.py --gpu-only > /dev/null 2>&1 || exit 1

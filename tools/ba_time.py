@@ -23,7 +23,16 @@ for st in (0.0, 0.5):
         _, _, _, _, res = ba.optimize(prob, 10)
     dt = (time.perf_counter() - t) / reps * 1e3
     if "--gpu-only" in sys.argv:
-        print(f"stereo {st}: gpu {dt:.3f} ms/solve ({res['iterations']} it, {res['trials']} trials)", flush=True)
+        # the marginal cost of an iteration: solves capped at 2 and at the full count
+        t = time.perf_counter()
+        for _ in range(reps):
+            _, _, _, _, r2 = ba.optimize(prob, 2)
+        dt2 = (time.perf_counter() - t) / reps * 1e3
+        di = res["iterations"] - r2["iterations"]
+        marg = (dt - dt2) / di if di > 0 else float("nan")
+        print(f"stereo {st}: gpu {dt:.3f} ms/solve ({res['iterations']} it, {res['trials']} trials); "
+              f"{dt2:.3f} ms at {r2['iterations']} it: {marg:.4f} ms per added iteration, "
+              f"fixed part {dt - marg * res['iterations']:.3f} ms", flush=True)
         continue
     t = time.perf_counter()
     _, _, _, _, rres = oracle.local_ba(prob, 10)

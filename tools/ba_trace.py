@@ -16,3 +16,6 @@ from orbslam3_amd import synth  # noqa: E402
 prob = synth.local_ba_problem()
 ba = pkg.LocalBA()
 ba.optimize(prob, 1)
+# steady state: the host phases of a few optimize(10) solves ([ba] lines on stderr)
+for _ in range(6):
+    ba.optimize(prob, 10)
