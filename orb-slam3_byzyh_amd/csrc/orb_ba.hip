@@ -39,6 +39,7 @@
 #include <numeric>
 #include <vector>
 
+#include "ba_structure.h"
 #include "orbgpu.h"
 #include "orbgpu_internal.h"
 
@@ -51,15 +52,10 @@ namespace {
 
 constexpr int kT = 256;
 
-// A free pose's observations: its free edges in landmark order, each with its landmark (the host's
-// pose_fl list; a landmark twice in one list = two edges between one keyframe and one map point).
-struct LandEdge {
-    int32_t l, e;
-};
-// one product of a Schur block: Z of edge a times Hpl of edge b
-struct EdgePair {
-    int32_t a, b;
-};
+// The host structure's list entries (csrc/ba_structure.h): a free pose's (landmark, edge) observations
+// and the Schur blocks' (Z edge, Hpl edge) products.
+using orbgpu_ba::EdgePair;
+using orbgpu_ba::LandEdge;
 
 
 struct EdgeDev {  // == orb_ba_edge_t
@@ -230,20 +226,25 @@ __device__ __forceinline__ void ba_reduce_land(int l, const int32_t* __restrict_
                                                const double* __restrict__ ecl, double* __restrict__ hll,
                                                double* __restrict__ bl) {
     double s[12] = {0};
-    const int k1 = off[l + 1];
-    for (int k0 = off[l]; k0 < k1; k0 += 4) {  // chunks of 4 edges: loads issued together, same sum order
-        double v[4][12];
+    const int k0 = off[l], k1 = off[l + 1];
+    for (int kb = k0; kb < k1; kb += 8) {  // the indices of 8 edges first, operands 4 at a time, same sum order
+        int e[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const double* p = ecl + 12 * (size_t)eidx[min(k0 + u, k1 - 1)];
+        for (int u = 0; u < 8; ++u) e[u] = eidx[min(kb + u, k1 - 1)];
 #pragma unroll
-            for (int i = 0; i < 12; ++i) v[u][i] = p[i];
+        for (int h = 0; h < 8; h += 4) {
+            if (kb + h >= k1) break;
+            double v[4][12];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int i = 0; i < 12; ++i) v[u][i] = ecl[12 * (size_t)e[h + u] + i];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (kb + h + u < k1)
+#pragma unroll
+                    for (int i = 0; i < 12; ++i) s[i] += v[u][i];
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (k0 + u < k1)
-#pragma unroll
-                for (int i = 0; i < 12; ++i) s[i] += v[u][i];
     }
     for (int i = 0; i < 9; ++i) hll[9 * (size_t)l + i] = s[i];
     for (int i = 0; i < 3; ++i) bl[3 * (size_t)l + i] = s[9 + i];
@@ -258,26 +259,57 @@ __global__ __launch_bounds__(kT) void k_ba_reduce_land(int nl, const int32_t* __
     if (l < nl) ba_reduce_land(l, off, eidx, ecl, hll, bl);
 }
 
-// Hpp and b_p per free pose: one wave, lanes stride the pose's edges, fixed-order tree in LDS
+// Sum of 64 lanes' partials of NC values, lane c < NC adding value c's partials in lane order
+// (LDS transpose; one pass, no barrier-separated tree).  Returns value `lane`'s sum in lanes < NC.
+template <int NC>
+__device__ __forceinline__ double wave_sum_cols(const double (&v)[NC], int lane) {
+    __shared__ double red[NC][65];
+#pragma unroll
+    for (int i = 0; i < NC; ++i) red[i][lane] = v[i];
+    __syncthreads();
+    double t = 0;
+    if (lane < NC)
+        for (int q = 0; q < 64; ++q) t += red[lane][q];
+    return t;
+}
+
+// Hpp and b_p per free pose: one wave; lane l sums the pose's edges l, l + 64, ... in order.  The
+// indices of up to 8 edges per lane are loaded first, then two edges' 42 values at a time, so the
+// usual pose (a few hundred edges) takes three rounds of loads instead of two per edge.
 __device__ __forceinline__ void ba_reduce_pose(int p, int lane, const int32_t* __restrict__ off,
                                                const LandEdge* __restrict__ eidx, const double* __restrict__ ecp,
                                                double* __restrict__ hpp, double* __restrict__ bp) {
-    __shared__ double red[42][65];
     double s[42];
+#pragma unroll
     for (int i = 0; i < 42; ++i) s[i] = 0;
-    for (int k = off[p] + lane; k < off[p + 1]; k += 64) {
+    const int k0 = off[p] + lane, k1 = off[p + 1];
+    int e[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) e[u] = k0 + 64 * u < k1 ? eidx[k0 + 64 * u].e : 0;
+#pragma unroll
+    for (int u = 0; u < 8; u += 2) {
+        if (k0 + 64 * u >= k1) break;
+        const bool two = k0 + 64 * (u + 1) < k1;
+        double a[42], b[42];
+#pragma unroll
+        for (int i = 0; i < 42; ++i) {
+            a[i] = ecp[42 * (size_t)e[u] + i];
+            b[i] = ecp[42 * (size_t)e[u + 1] + i];
+        }
+#pragma unroll
+        for (int i = 0; i < 42; ++i) s[i] += a[i];
+        if (two)
+#pragma unroll
+            for (int i = 0; i < 42; ++i) s[i] += b[i];
+    }
+    for (int k = k0 + 64 * 8; k < k1; k += 64) {  // poses of more than 512 edges
         const double* q = ecp + 42 * (size_t)eidx[k].e;
+#pragma unroll
         for (int i = 0; i < 42; ++i) s[i] += q[i];
     }
-    for (int i = 0; i < 42; ++i) red[i][lane] = s[i];
-    __syncthreads();
-    // lane i sums component i over the 64 lane partials in lane order (one LDS pass, no tree of
-    // 42-wide barrier-separated levels)
-    if (lane >= 42) return;
-    double t = 0;
-    for (int q = 0; q < 64; ++q) t += red[lane][q];
+    const double t = wave_sum_cols<42>(s, lane);
     if (lane < 36) hpp[36 * (size_t)p + lane] = t;
-    else bp[6 * (size_t)p + lane - 36] = t;
+    else if (lane < 42) bp[6 * (size_t)p + lane - 36] = t;
 }
 
 __global__ __launch_bounds__(64) void k_ba_reduce_pose(const int32_t* __restrict__ off, const LandEdge* __restrict__ eidx,
@@ -417,14 +449,23 @@ __global__ __launch_bounds__(64) void k_ba_schur_pairs(int nf, const int32_t* __
 }
 
 // S block (i, j), i <= j, one wave: lanes split the block's (Z_a, Hpl_b) products (k_ba_schur_pairs),
-// each accumulating the full 6x6 partial sum; lane e < 36 then adds the 64 partials in lane order.
-// S = [Hpp + lambda I] - sum Z_a Hpl_b^T, written to both triangles (every block of S, empty ones as 0).
+// lane l taking products l, l + 64, ... in order and accumulating the full 6x6 partial sum; the pair
+// indices of up to 4 rounds are loaded first, then two products' operands at a time.  Lane e < 36
+// then adds the 64 partials in lane order.  S = [Hpp + lambda I] - sum Z_a Hpl_b^T, written to both
+// triangles (every block of S, empty ones as 0).
+__device__ __forceinline__ void schur_acc(double (&acc)[36], const double* __restrict__ Z, const double* __restrict__ H) {
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = 0; c < 6; ++c)
+            acc[6 * r + c] += Z[3 * r] * H[3 * c] + Z[3 * r + 1] * H[3 * c + 1] + Z[3 * r + 2] * H[3 * c + 2];
+}
+
 __device__ __forceinline__ void ba_schur_block(int blk, int lane, int n, int nf, double lambda, int add_diag,
                                                const int32_t* __restrict__ blk_off, const EdgePair* __restrict__ pairs,
                                                const int32_t* __restrict__ cnt, const double* __restrict__ z,
                                                const double* __restrict__ hpl, const double* __restrict__ hpp,
                                                double* __restrict__ S) {
-    __shared__ double red[36][65];
     int i, j;
     schur_block_ij(blk, nf, i, j);
     double acc[36];
@@ -432,25 +473,32 @@ __device__ __forceinline__ void ba_schur_block(int blk, int lane, int n, int nf,
     for (int k = 0; k < 36; ++k) acc[k] = 0;
     const EdgePair* pl = pairs + blk_off[blk];
     const int np = cnt[blk];
-    for (int k = lane; k < np; k += 64) {
-        const EdgePair pr = pl[k];
-        const double* Z = z + 18 * (size_t)pr.a;
-        const double* H = hpl + 18 * (size_t)pr.b;
+    EdgePair pr[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) pr[u] = lane + 64 * u < np ? pl[lane + 64 * u] : EdgePair{0, 0};
+#pragma unroll
+    for (int u = 0; u < 4; u += 2) {
+        if (lane + 64 * u >= np) break;
+        double z0[18], h0[18], z1[18], h1[18];
+#pragma unroll
+        for (int q = 0; q < 18; ++q) {
+            z0[q] = z[18 * (size_t)pr[u].a + q];
+            h0[q] = hpl[18 * (size_t)pr[u].b + q];
+            z1[q] = z[18 * (size_t)pr[u + 1].a + q];
+            h1[q] = hpl[18 * (size_t)pr[u + 1].b + q];
+        }
+        schur_acc(acc, z0, h0);
+        if (lane + 64 * (u + 1) < np) schur_acc(acc, z1, h1);
+    }
+    for (int k = lane + 256; k < np; k += 64) {  // blocks of more than 256 products
+        const EdgePair p2 = pl[k];
         double zr[18], hr[18];
 #pragma unroll
-        for (int q = 0; q < 18; ++q) { zr[q] = Z[q]; hr[q] = H[q]; }
-#pragma unroll
-        for (int r = 0; r < 6; ++r)
-#pragma unroll
-            for (int c = 0; c < 6; ++c)
-                acc[6 * r + c] += zr[3 * r] * hr[3 * c] + zr[3 * r + 1] * hr[3 * c + 1] + zr[3 * r + 2] * hr[3 * c + 2];
+        for (int q = 0; q < 18; ++q) { zr[q] = z[18 * (size_t)p2.a + q]; hr[q] = hpl[18 * (size_t)p2.b + q]; }
+        schur_acc(acc, zr, hr);
     }
-#pragma unroll
-    for (int k = 0; k < 36; ++k) red[k][lane] = acc[k];
-    __syncthreads();
+    const double sum = wave_sum_cols<36>(acc, lane);
     if (lane >= 36) return;
-    double sum = 0;
-    for (int q = 0; q < 64; ++q) sum += red[lane][q];
     const int r = lane / 6, c = lane % 6;
     double v = 0.0 - sum;
     if (i == j && add_diag) v = (hpp[36 * (size_t)i + 6 * r + c] + (r == c ? lambda : 0.0)) - sum;
@@ -469,24 +517,33 @@ __global__ __launch_bounds__(64) void k_ba_schur_blocks(int n, int nf, const dou
     ba_schur_block(blockIdx.x, threadIdx.x, n, nf, *lam, add_diag, blk_off, pairs, cnt, z, hpl, hpp, S);
 }
 
-// b_S = b_p - sum over the pose's edges of Hpl_e db (one wave per free pose)
+// b_S = b_p - sum over the pose's edges of Hpl_e db (one wave per free pose; the indices of up to 8
+// edges per lane first, then their 6 values each, all in flight)
 __device__ __forceinline__ void ba_schur_rhs(int p, int lane, const int32_t* __restrict__ off,
                                              const LandEdge* __restrict__ eidx, const double* __restrict__ cb,
                                              const double* __restrict__ bp, int use_bp, double* __restrict__ bs) {
-    __shared__ double red[6][65];
     double s[6] = {0, 0, 0, 0, 0, 0};
-    for (int k = off[p] + lane; k < off[p + 1]; k += 64) {
+    const int k0 = off[p] + lane, k1 = off[p + 1];
+    int e[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) e[u] = k0 + 64 * u < k1 ? eidx[k0 + 64 * u].e : 0;
+    double v[8][6];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int i = 0; i < 6; ++i) v[u][i] = cb[6 * (size_t)e[u] + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+        if (k0 + 64 * u < k1)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) s[i] += v[u][i];
+    for (int k = k0 + 64 * 8; k < k1; k += 64) {
         const double* q = cb + 6 * (size_t)eidx[k].e;
+#pragma unroll
         for (int i = 0; i < 6; ++i) s[i] += q[i];
     }
-    for (int i = 0; i < 6; ++i) red[i][lane] = s[i];
-    __syncthreads();
-    for (int w = 32; w >= 1; w >>= 1) {
-        if (lane < w)
-            for (int i = 0; i < 6; ++i) red[i][lane] += red[i][lane + w];
-        __syncthreads();
-    }
-    if (lane < 6) bs[6 * (size_t)p + lane] = (use_bp ? bp[6 * (size_t)p + lane] : 0.0) - red[lane][0];
+    const double t = wave_sum_cols<6>(s, lane);
+    if (lane < 6) bs[6 * (size_t)p + lane] = (use_bp ? bp[6 * (size_t)p + lane] : 0.0) - t;
 }
 
 __global__ __launch_bounds__(64) void k_ba_schur_rhs(const int32_t* __restrict__ off, const LandEdge* __restrict__ eidx,
@@ -1233,52 +1290,60 @@ __global__ __launch_bounds__(kRowThreads) void k_ba_chol_rows(int n, const doubl
     }
 }
 
-// x_l = Dinv (b_l - sum_e Hpl_e^T x_pose(e))
+// x_l = Dinv (b_l - sum_e Hpl_e^T x_pose(e)).  The free edges' indices and pose rows (host-built
+// erow) of up to 8 edges are loaded first, then the operands 4 edges at a time: two rounds of
+// dependent loads for the usual landmark, not four per edge.  xl: x_l (also stored to x).
 __device__ __forceinline__ void ba_backsub(int l, int n, double lambda, const int32_t* __restrict__ off,
-                                           const int32_t* __restrict__ eidx, const EdgeDev* __restrict__ edges,
-                                           const int32_t* __restrict__ pose_h, const double* __restrict__ hpl,
-                                           const double* __restrict__ bl, const double* __restrict__ hll,
-                                           double* __restrict__ x) {
+                                           const int32_t* __restrict__ eidx, const int32_t* __restrict__ erow,
+                                           const double* __restrict__ hpl, const double* __restrict__ bl,
+                                           const double* __restrict__ hll, double* __restrict__ x, double xl[3]) {
     double cl[3] = {bl[3 * (size_t)l], bl[3 * (size_t)l + 1], bl[3 * (size_t)l + 2]};
-    // edges in chunks of 4: each chunk's three dependent index loads and its operand loads are issued
-    // together (not one chain of four dependent loads per edge); the sums run in the same order
-    const int k1 = off[l + 1];
-    for (int k0 = off[l]; k0 < k1; k0 += 4) {
-        int e[4], ph[4];
+    const int k0 = off[l], k1 = off[l + 1];
+    for (int kb = k0; kb < k1; kb += 8) {
+        int e[8], ph[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) e[u] = eidx[min(k0 + u, k1 - 1)];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) ph[u] = pose_h[edges[e[u]].pose];
-        double H[4][18], xp[4][6];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-#pragma unroll
-            for (int q = 0; q < 18; ++q) H[u][q] = hpl[18 * (size_t)e[u] + q];
-#pragma unroll
-            for (int q = 0; q < 6; ++q) xp[u][q] = x[6 * (size_t)ph[u] + q];
+        for (int u = 0; u < 8; ++u) {
+            const int k = min(kb + u, k1 - 1);
+            e[u] = eidx[k];
+            ph[u] = erow[k];
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (k0 + u < k1)
+        for (int h = 0; h < 8; h += 4) {
+            if (kb + h >= k1) break;
+            double H[4][18], xp[4][6];
 #pragma unroll
-                for (int c = 0; c < 3; ++c)
+            for (int u = 0; u < 4; ++u) {
 #pragma unroll
-                    for (int r = 0; r < 6; ++r) cl[c] += H[u][3 * r + c] * -xp[u][r];
+                for (int q = 0; q < 18; ++q) H[u][q] = hpl[18 * (size_t)e[h + u] + q];
+#pragma unroll
+                for (int q = 0; q < 6; ++q) xp[u][q] = x[6 * (size_t)ph[h + u] + q];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (kb + h + u < k1)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c)
+#pragma unroll
+                        for (int r = 0; r < 6; ++r) cl[c] += H[u][3 * r + c] * -xp[u][r];
+        }
     }
     double Di[9];
     land_dinv(hll, l, lambda, Di);
-    for (int r = 0; r < 3; ++r) x[n + 3 * (size_t)l + r] = Di[3 * r] * cl[0] + Di[3 * r + 1] * cl[1] + Di[3 * r + 2] * cl[2];
+    for (int r = 0; r < 3; ++r) {
+        xl[r] = Di[3 * r] * cl[0] + Di[3 * r + 1] * cl[1] + Di[3 * r + 2] * cl[2];
+        x[n + 3 * (size_t)l + r] = xl[r];
+    }
 }
 
 __global__ __launch_bounds__(kT) void k_ba_backsub(int nl, int n, const double* __restrict__ lam,
                                                    const int32_t* __restrict__ off, const int32_t* __restrict__ eidx,
-                                                   const EdgeDev* __restrict__ edges, const int32_t* __restrict__ pose_h,
-                                                   const double* __restrict__ hpl, const double* __restrict__ bl,
-                                                   const double* __restrict__ hll, double* __restrict__ x,
-                                                   const LmState* __restrict__ lm_st, int lm_gk) {
+                                                   const int32_t* __restrict__ erow, const double* __restrict__ hpl,
+                                                   const double* __restrict__ bl, const double* __restrict__ hll,
+                                                   double* __restrict__ x, const LmState* __restrict__ lm_st, int lm_gk) {
     if (lm_skip(lm_st, lm_gk)) return;
     const int l = blockIdx.x * kT + threadIdx.x;
-    if (l < nl) ba_backsub(l, n, *lam, off, eidx, edges, pose_h, hpl, bl, hll, x);
+    double xl[3];
+    if (l < nl) ba_backsub(l, n, *lam, off, eidx, erow, hpl, bl, hll, x, xl);
 }
 
 // push + oplus for every free vertex: threads [0, nf) poses, [nf, nf + nl) landmarks
@@ -1585,8 +1650,9 @@ __global__ __launch_bounds__(64) void k_u_reduce_build(int nf, int nl, const int
 __global__ __launch_bounds__(64) void k_u_schur(int n, int nf, int nblk, const double* __restrict__ lam,
                                                 const int32_t* __restrict__ blk_off, const EdgePair* __restrict__ pairs,
                                                 const int32_t* __restrict__ cnt, const int32_t* __restrict__ pose_off,
-                                                const LandEdge* __restrict__ pose_fl, const double* __restrict__ z, const double* __restrict__ hpl,
-                                                size_t hpl_alt, const double* __restrict__ hpp, double* __restrict__ S,
+                                                const LandEdge* __restrict__ pose_fl, const double* __restrict__ z,
+                                                const double* __restrict__ hpl, size_t hpl_alt,
+                                                const double* __restrict__ hpp, double* __restrict__ S,
                                                 const double* __restrict__ cb, const double* __restrict__ bp,
                                                 double* __restrict__ bs, const LmState* __restrict__ st) {
     if (lm_skip(st, kGateTrial)) return;
@@ -1598,33 +1664,59 @@ __global__ __launch_bounds__(64) void k_u_schur(int n, int nf, int nblk, const d
 }
 
 // unit step 6 (trial): x_l per landmark and its update, then the pose updates; a rejected previous
-// trial is undone here (from the backup) instead of by a restore launch
+// trial is undone here (from the backup) instead of by a restore launch.  Each block also leaves its
+// part of computeScale, sum x (lambda x + b) over its vertices' rows, in part2[block] (summed in
+// block order by k_u_edges_trial: one load round there instead of a pass over x and b).
 __global__ __launch_bounds__(kT) void k_u_backsub_update(int nl, int nf, int n, const double* __restrict__ lam,
                                                          const int32_t* __restrict__ off, const int32_t* __restrict__ eidx,
-                                                         const EdgeDev* __restrict__ edges,
-                                                         const int32_t* __restrict__ pose_h, const double* __restrict__ hpl,
+                                                         const int32_t* __restrict__ erow, const double* __restrict__ hpl,
                                                          size_t hpl_alt, const double* __restrict__ bl,
-                                                         const double* __restrict__ hll,
-                                                         double* __restrict__ x, const int32_t* __restrict__ free_pose,
+                                                         const double* __restrict__ hll, double* __restrict__ x,
+                                                         const double* __restrict__ bp, const int32_t* __restrict__ free_pose,
                                                          const int32_t* __restrict__ land_point, double* __restrict__ pose,
                                                          double* __restrict__ pose_bak, double* __restrict__ point,
-                                                         double* __restrict__ point_bak, const LmState* __restrict__ st) {
+                                                         double* __restrict__ point_bak, double* __restrict__ part2,
+                                                         const LmState* __restrict__ st) {
     if (lm_skip(st, kGateTrial)) return;
     hpl += hpl_cur(st, hpl_alt);
     const bool rej = st->reject != 0;
+    const double lambda = *lam;
     const int t = blockIdx.x * kT + threadIdx.x;
+    double c = 0.0;
     if (t < nl) {
-        ba_backsub(t, n, *lam, off, eidx, edges, pose_h, hpl, bl, hll, x);
-        ba_update(nf + t, nf, nl, n, rej, free_pose, land_point, x, pose, pose_bak, point, point_bak);
+        double xl[3];
+        ba_backsub(t, n, lambda, off, eidx, erow, hpl, bl, hll, x, xl);
+        for (int r = 0; r < 3; ++r) c += xl[r] * (lambda * xl[r] + bl[3 * (size_t)t + r]);
+        double* X = point + 3 * (size_t)land_point[t];
+        double* Xb = point_bak + 3 * (size_t)land_point[t];
+        for (int i = 0; i < 3; ++i) {
+            const double v = rej ? Xb[i] : X[i];
+            Xb[i] = v;
+            X[i] = v + xl[i];
+        }
     } else if (t < nl + nf) {
-        ba_update(t - nl, nf, nl, n, rej, free_pose, land_point, x, pose, pose_bak, point, point_bak);
+        const int p = t - nl;
+        double* T = pose + 7 * (size_t)free_pose[p];
+        double* Tb = pose_bak + 7 * (size_t)free_pose[p];
+        double v[7], u[6];
+        for (int i = 0; i < 6; ++i) u[i] = x[6 * (size_t)p + i];
+        for (int i = 0; i < 6; ++i) c += u[i] * (lambda * u[i] + bp[6 * (size_t)p + i]);
+        for (int i = 0; i < 7; ++i) {
+            v[i] = rej ? Tb[i] : T[i];
+            Tb[i] = v[i];
+        }
+        se3_oplus(v, u);
+        for (int i = 0; i < 7; ++i) T[i] = v[i];
     }
+    const double bsum = block_sum<kT>(c);
+    if (threadIdx.x == 0) part2[blockIdx.x] = bsum;
 }
 
-// unit step 7 (trial): errors at the new estimate and its linearisation (Hll/b_l and Hpp/b_p parts
-// in place: nothing reads them before the next build; Hpl into the other half); the last block sums
-// chi2 and computeScale and runs the trial controller, which makes the new linearisation current on
-// accept -- the next iteration's build at the same estimate would compute exactly these values
+// unit step 7 (trial): errors at the new estimate (with kLin also its linearisation: Hll/b_l and
+// Hpp/b_p parts in place -- nothing reads them before the next build -- and Hpl into the other half);
+// the last block sums chi2 and computeScale (part2, from k_u_backsub_update) and runs the trial
+// controller, which on accept makes the kLin linearisation current: the next iteration's build at
+// the same estimate would compute exactly these values
 template <bool kLin>
 __global__ __launch_bounds__(kT) void k_u_edges_trial(int ne, const EdgeDev* __restrict__ edges,
                                                       const orb_ba_camera_t* __restrict__ cams,
@@ -1632,9 +1724,8 @@ __global__ __launch_bounds__(kT) void k_u_edges_trial(int ne, const EdgeDev* __r
                                                       const int32_t* __restrict__ pose_h, Huber2 hub,
                                                       double* __restrict__ err, double* __restrict__ rho0_out,
                                                       double* __restrict__ ecl, double* __restrict__ hpl, size_t hpl_alt,
-                                                      double* __restrict__ ecp,
-                                                      double* __restrict__ part, unsigned* counter, int nx,
-                                                      const double* __restrict__ x, const double* __restrict__ b,
+                                                      double* __restrict__ ecp, double* __restrict__ part,
+                                                      unsigned* counter, const double* __restrict__ part2, int nparts2,
                                                       const int32_t* __restrict__ status, double* __restrict__ scal,
                                                       LmState* st, LmProgress* prog) {
     if (lm_skip(st, kGateTrial)) return;
@@ -1646,24 +1737,11 @@ __global__ __launch_bounds__(kT) void k_u_edges_trial(int ne, const EdgeDev* __r
     const double bsum = block_sum<kT>(r);
     if (threadIdx.x == 0) part[blockIdx.x] = bsum;
     if (!last_block(counter)) return;
-    double c = 0.0;
+    double c = 0.0, d = 0.0;
     for (int i = threadIdx.x; i < (int)gridDim.x; i += kT) c += part[i];
+    for (int i = threadIdx.x; i < nparts2; i += kT) d += part2[i];
     const double chi = block_sum<kT>(c);
-    const double lambda = st->lambda;
-    double sc = 0.0;
-    for (int i0 = threadIdx.x; i0 < nx; i0 += 8 * kT) {  // 8 loads in flight per thread, same sum order
-        double xv[8], bv[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = min(i0 + u * kT, nx - 1);
-            xv[u] = x[i];
-            bv[u] = b[i];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (i0 + u * kT < nx) sc += xv[u] * (lambda * xv[u] + bv[u]);
-    }
-    const double scale = block_sum<kT>(sc);
+    const double scale = block_sum<kT>(d);
     if (threadIdx.x == 0) {
         const bool failed = *status != 0;
         scal[0] = chi;
@@ -1757,12 +1835,14 @@ struct Stager {
 };
 
 struct orb_ba_s {
+    orbgpu_ba::BaStructure st;  // the host structure of the last solve (vectors reused)
     hipStream_t stream = nullptr;
     hipStream_t tail = nullptr;  // the end of a device-driven solve, beside the queued no-op unit
     DevBuf<double> pose, pose_bak, point, point_bak, err, rho0, ecl, hpl, ecp, hpp, hll, b, z, cb, S, bs, x, scal;
     DevBuf<EdgeDev> edges;
     DevBuf<orb_ba_camera_t> cams;
-    DevBuf<int32_t> pose_h, free_pose, land_point, land_off, land_edge, landf_off, landf_edge, fland, pose_off, status;
+    DevBuf<int32_t> pose_h, free_pose, land_point, land_off, land_edge, landf_off, landf_edge, landf_row, fland, pose_off,
+        status;
     DevBuf<LandEdge> pose_fl;
     DevBuf<int32_t> blk_off, blk_cnt;  // Schur block product lists (k_ba_schur_pairs)
     DevBuf<EdgePair> pairs;
@@ -1803,7 +1883,8 @@ struct orb_ba_s {
         cflag.release();
         edges.release();
         cams.release();
-        for (auto* d : {&pose_h, &free_pose, &land_point, &land_off, &land_edge, &landf_off, &landf_edge, &fland, &pose_off,
+        for (auto* d : {&pose_h, &free_pose, &land_point, &land_off, &land_edge, &landf_off, &landf_edge, &landf_row, &fland,
+                        &pose_off,
                         &status})
             d->release();
         pose_fl.release();
@@ -2044,129 +2125,27 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         return h->h_scal[6] != 0.0;
     };
 
-    // ---- structure (initializeOptimization + BlockSolver::buildStructure), from the whole problem
-    std::vector<int> pdeg(np, 0), qdeg(nq, 0);
-    for (int e = 0; e < ne_all; ++e) { pdeg[pr->edges[e].pose]++; qdeg[pr->edges[e].point]++; }
-    std::vector<int> order(np);
-    std::iota(order.begin(), order.end(), 0);
-    auto by_pose_id = [&](int a, int b) { return pr->pose_id[a] < pr->pose_id[b]; };
-    if (!std::is_sorted(order.begin(), order.end(), by_pose_id)) std::sort(order.begin(), order.end(), by_pose_id);
-    std::vector<int32_t> pose_h(np, -1), free_pose;
-    for (int i : order)
-        if (pdeg[i] && !pr->pose_fixed[i]) { pose_h[i] = (int32_t)free_pose.size(); free_pose.push_back(i); }
-    std::vector<int> qorder(nq);
-    std::iota(qorder.begin(), qorder.end(), 0);
-    auto by_point_id = [&](int a, int b) { return pr->point_id[a] < pr->point_id[b]; };
-    if (!std::is_sorted(qorder.begin(), qorder.end(), by_point_id)) std::sort(qorder.begin(), qorder.end(), by_point_id);
-    std::vector<int> all_land;
-    for (int i : qorder)
-        if (qdeg[i]) all_land.push_back(i);
-    const int nf = (int)free_pose.size(), nl_all = (int)all_land.size();
-    if (ne_all == 0 || nf + nl_all == 0) {  // SparseOptimizer::optimize returns -1: nothing to do
+    // ---- structure (initializeOptimization + BlockSolver::buildStructure), csrc/ba_structure.h
+    orbgpu_ba::BaStructure& T = h->st;
+    if (!orbgpu_ba::ba_build_structure(pr, h->world, h->rank, T)) {  // SparseOptimizer::optimize returns -1: nothing to do
         for (int e = 0; e < ne_all; ++e) {
             if (edge_chi2) edge_chi2[e] = 0;
             if (edge_depth_ok) edge_depth_ok[e] = 0;
         }
         return ORB_OK;
     }
+    t_order = t_csr = clk::now();
     if (stop()) { res->stopped = 1; return ORB_ERR_ABORTED; }
-    // this rank's landmarks: a contiguous range of the landmark order with about 1/world of the edges
-    int l_begin = 0, l_end = nl_all;
-    if (dist) {
-        std::vector<long long> cum(nl_all + 1, 0);
-        for (int l = 0; l < nl_all; ++l) cum[l + 1] = cum[l] + qdeg[all_land[l]];
-        auto cut = [&](int r) {
-            const long long target = cum[nl_all] * r / h->world;
-            return (int)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
-        };
-        l_begin = h->rank == 0 ? 0 : cut(h->rank);
-        l_end = h->rank == h->world - 1 ? nl_all : cut(h->rank + 1);
-    }
-    t_order = clk::now();
-    std::vector<int32_t> point_l(nq, -1), land_point(all_land.begin() + l_begin, all_land.begin() + l_end);
-    for (int l = 0; l < (int)land_point.size(); ++l) point_l[land_point[l]] = l;
-    std::vector<int32_t> lmap;  // local edge -> problem edge (problem order kept)
+    if (agree_fail(T.dup_edge)) return orbgpu_fail(ORB_ERR_ARG, "two edges between one keyframe and one map point");
+    if (agree_fail(T.n_products > INT32_MAX)) return orbgpu_fail(ORB_ERR_ARG, "BA window too large");
     static_assert(sizeof(EdgeDev) == sizeof(orb_ba_edge_t), "EdgeDev mirrors orb_ba_edge_t");
-    const EdgeDev* ledges = reinterpret_cast<const EdgeDev*>(pr->edges);  // one rank: every edge, in place
-    std::vector<EdgeDev> ledges_copy;
-    if (dist) {
-        for (int e = 0; e < ne_all; ++e)
-            if (point_l[pr->edges[e].point] >= 0) lmap.push_back(e);
-        ledges_copy.resize(lmap.size());
-        for (size_t k = 0; k < lmap.size(); ++k) memcpy(&ledges_copy[k], &pr->edges[lmap[k]], sizeof(EdgeDev));
-        ledges = ledges_copy.data();
-    }
-    const int ne = dist ? (int)lmap.size() : ne_all, nl = (int)land_point.size();
+    const EdgeDev* ledges = reinterpret_cast<const EdgeDev*>(T.ledges);
+    const int nf = T.nf, ne = T.ne, nl = T.nl, nfe = T.nfe, nblk = T.nblk;
     const int n = 6 * nf, m = 3 * nl;
-
-    // landmark -> all edges (edge order), landmark -> free-pose edges (pose row ascending), pose -> its
-    // free edges in landmark order with the landmark (pose_fl: the Schur blocks find the landmarks two
-    // poses share by searching one pose's list in the other's, no product list)
-    std::vector<int32_t> land_off(nl + 1, 0), land_edge(ne), landf_off(nl + 1, 0), landf_edge, pose_off(nf + 1, 0);
-    std::vector<LandEdge> pose_fl;
-    for (int e = 0; e < ne; ++e) {
-        land_off[point_l[ledges[e].point] + 1]++;
-        if (pose_h[ledges[e].pose] >= 0) {
-            landf_off[point_l[ledges[e].point] + 1]++;
-            pose_off[pose_h[ledges[e].pose] + 1]++;
-        }
-    }
-    for (int l = 0; l < nl; ++l) { land_off[l + 1] += land_off[l]; landf_off[l + 1] += landf_off[l]; }
-    for (int p = 0; p < nf; ++p) pose_off[p + 1] += pose_off[p];
-    landf_edge.resize(landf_off[nl]);
-    pose_fl.resize(pose_off[nf]);
-    {
-        std::vector<int32_t> c1(land_off.begin(), land_off.end() - 1), c2(landf_off.begin(), landf_off.end() - 1);
-        for (int e = 0; e < ne; ++e) {
-            const int l = point_l[ledges[e].point];
-            land_edge[c1[l]++] = e;
-            if (pose_h[ledges[e].pose] >= 0) landf_edge[c2[l]++] = e;
-        }
-    }
-    // each landmark's free-pose edges by pose row, stable: an insertion sort (a landmark has a handful
-    // of edges; std::stable_sort allocated a buffer per landmark); then the pose lists in landmark order
-    const int nfe = (int)landf_edge.size();
-    std::vector<int32_t> fland(nfe);
-    bool dup_edge = false;
-    {
-        std::vector<int32_t> c3(pose_off.begin(), pose_off.end() - 1);
-        for (int l = 0; l < nl; ++l) {
-            int32_t* e0 = landf_edge.data() + landf_off[l];
-            const int d = landf_off[l + 1] - landf_off[l];
-            for (int a = 1; a < d; ++a) {
-                const int32_t v = e0[a];
-                const int32_t key = pose_h[ledges[v].pose];
-                int b = a;
-                for (; b > 0 && pose_h[ledges[e0[b - 1]].pose] > key; --b) e0[b] = e0[b - 1];
-                e0[b] = v;
-            }
-            for (int k = 0; k < d; ++k) {
-                fland[landf_off[l] + k] = l;
-                pose_fl[c3[pose_h[ledges[e0[k]].pose]]++] = LandEdge{l, e0[k]};
-                if (k && pose_h[ledges[e0[k]].pose] == pose_h[ledges[e0[k - 1]].pose]) dup_edge = true;
-            }
-        }
-    }
-    if (agree_fail(dup_edge)) return orbgpu_fail(ORB_ERR_ARG, "two edges between one keyframe and one map point");
-    // every upper-triangle block of S (empty ones written as 0); block (i, j) lists at most
-    // min(|i|, |j|) products
-    const int nblk = nf * (nf + 1) / 2;
-    std::vector<int32_t> blk_off(nblk + 1);
-    {
-        int b = 0;
-        long long acc = 0;
-        for (int i = 0; i < nf; ++i) {
-            const int li = pose_off[i + 1] - pose_off[i];
-            for (int j = i; j < nf; ++j, ++b) {
-                blk_off[b] = (int32_t)acc;
-                acc += std::min(li, pose_off[j + 1] - pose_off[j]);
-            }
-        }
-        if (agree_fail(acc > INT32_MAX)) return orbgpu_fail(ORB_ERR_ARG, "BA window too large");
-        blk_off[nblk] = (int32_t)std::min<long long>(acc, INT32_MAX);
-    }
-    t_csr = clk::now();
-    t_pairs = t_csr;
+    const std::vector<int32_t>& point_l = T.point_l;
+    const std::vector<int32_t>& qdeg = T.qdeg;
+    const std::vector<int32_t>& lmap = T.lmap;
+    t_pairs = clk::now();
     // poses normalised as SE3Quat(q, t) does
     std::vector<double> pose(pr->pose, pr->pose + 7 * (size_t)np);
     for (int i = 0; i < np; ++i) {
@@ -2189,15 +2168,16 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     Stager st;
     bool ok = st.add(h->pose, pose) && h->pose_bak.grow(7 * (size_t)np) && st.add(h->point, pr->point, 3 * (size_t)nq) &&
               h->point_bak.grow(3 * (size_t)nq) && st.add(h->edges, ledges, (size_t)ne) && st.add(h->cams, pr->pose_camera, np) &&
-              st.add(h->pose_h, pose_h) && st.add(h->free_pose, free_pose) && st.add(h->land_point, land_point) &&
-              st.add(h->land_off, land_off) && st.add(h->land_edge, land_edge) && st.add(h->landf_off, landf_off) &&
-              st.add(h->landf_edge, landf_edge) && st.add(h->fland, fland) && st.add(h->pose_off, pose_off) &&
-              st.add(h->pose_fl, pose_fl) && st.add(h->blk_off, blk_off) && h->blk_cnt.grow(std::max(nblk, 1)) &&
-              h->pairs.grow(std::max<size_t>(1, (size_t)blk_off[nblk])) &&
+              st.add(h->pose_h, T.pose_h) && st.add(h->free_pose, T.free_pose) && st.add(h->land_point, T.land_point) &&
+              st.add(h->land_off, T.land_off) && st.add(h->land_edge, T.land_edge) &&
+              st.add(h->landf_off, T.landf_off) && st.add(h->landf_edge, T.landf_edge) && st.add(h->fland, T.fland) &&
+              st.add(h->landf_row, T.landf_row) && st.add(h->pose_off, T.pose_off) && st.add(h->pose_fl, T.pose_fl) &&
+              st.add(h->blk_off, T.blk_off) && h->blk_cnt.grow(std::max(nblk, 1)) &&
+              h->pairs.grow(std::max<size_t>(1, (size_t)T.blk_off[nblk])) &&
               h->err.grow(3 * ne1) && h->rho0.grow(ne1) && h->ecl.grow(12 * ne1) && h->hpl.grow(36 * ne1) &&
               h->ecp.grow(42 * ne1) && h->hpp.grow(36 * (size_t)nf) && h->hll.grow(9 * (size_t)nl) && h->b.grow(n + m) &&
               h->z.grow(18 * ne1) && h->cb.grow(6 * ne1) && h->S.grow((size_t)n * n) && h->bs.grow(n) &&
-              h->depth.grow(ne1) && h->part.grow(grid(ne)) &&
+              h->depth.grow(ne1) && h->part.grow(grid(ne) + grid(nl + nf)) &&
               // cleared by the scatter launch: g2o's _x starts zeroed, the scalars, the factorisation
               // status, the last-block counters of the unit kernels; and the device LM state's start
               st.zero(h->x, n + m) && st.zero(h->scal, 8) && st.zero(h->status, 1) && st.zero(h->counters, 2) &&
@@ -2346,7 +2326,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         }
         if (nl)
             hipLaunchKernelGGL(k_ba_backsub, dim3(grid(nl)), dim3(kT), 0, s, nl, n, lam, h->landf_off.p, h->landf_edge.p,
-                               h->edges.p, h->pose_h.p, h->hpl.p, bl, h->hll.p, h->x.p, G, (int)kGateTrial);
+                               h->landf_row.p, h->hpl.p, bl, h->hll.p, h->x.p, G, (int)kGateTrial);
         hipLaunchKernelGGL(k_ba_update, dim3(grid(nf + nl)), dim3(kT), 0, s, nf, nl, n, h->free_pose.p, h->land_point.p,
                            h->x.p, h->pose.p, h->pose_bak.p, h->point.p, h->point_bak.p, G, (int)kGateTrial);
         if (ne)
@@ -2380,7 +2360,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         // unit's event; once the solve is done the queued unit is a run of no-op launches.
         // (the state's start, the counters and the status went up with the inputs)
         memset(h->h_prog, 0, sizeof(LmProgress));
-        const int nparts = (int)grid(ne);
+        const int nparts = (int)grid(ne), nparts2 = (int)grid(nl + nf);  // partials: edge blocks, vertex blocks
         LmState* L = h->lm.p;
         // one unit = 6 launches: reductions (+ chi2, max diag, build controller), Schur edges, Schur
         // blocks + rhs, Cholesky + solves, back-substitution + update, errors and linearisation at the
@@ -2398,7 +2378,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         if (trial_lin) launch_edges_build();
         auto unit_launches = [&]() {
             if (!trial_lin) launch_edges_build();
-            hipLaunchKernelGGL(k_u_reduce_build, dim3(nf + (nl + 63) / 64), dim3(64), 0, s, nf, nl, h->pose_off.p,
+            hipLaunchKernelGGL(k_u_reduce_build, dim3(nf + grid(nl, 64)), dim3(64), 0, s, nf, nl, h->pose_off.p,
                                h->pose_fl.p, h->ecp.p, h->hpp.p, h->b.p, h->land_off.p, h->land_edge.p, h->ecl.p,
                                h->hll.p, bl, h->part.p, nparts, h->counters.p, h->scal.p, L);
             if (nfe)
@@ -2411,14 +2391,13 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                                    (const LmState*)L);
                 launch_chol((const LmState*)L);
             }
-            hipLaunchKernelGGL(k_u_backsub_update, dim3(grid(nl + nf)), dim3(kT), 0, s, nl, nf, n, lam, h->landf_off.p,
-                               h->landf_edge.p, h->edges.p, h->pose_h.p, h->hpl.p, hpl_alt, bl, h->hll.p, h->x.p,
-                               h->free_pose.p,
-                               h->land_point.p, h->pose.p, h->pose_bak.p, h->point.p, h->point_bak.p,
-                               (const LmState*)L);
+            hipLaunchKernelGGL(k_u_backsub_update, dim3(nparts2), dim3(kT), 0, s, nl, nf, n, lam, h->landf_off.p,
+                               h->landf_edge.p, h->landf_row.p, h->hpl.p, hpl_alt, bl, h->hll.p, h->x.p, h->b.p,
+                               h->free_pose.p, h->land_point.p, h->pose.p, h->pose_bak.p, h->point.p, h->point_bak.p,
+                               h->part.p + nparts, (const LmState*)L);
             hipLaunchKernelGGL(trial_lin ? k_u_edges_trial<true> : k_u_edges_trial<false>, dim3(nparts), dim3(kT), 0, s, ne, h->edges.p, h->cams.p, h->pose.p,
                                h->point.p, h->pose_h.p, hub, h->err.p, h->rho0.p, h->ecl.p, h->hpl.p, hpl_alt, h->ecp.p,
-                               h->part.p, h->counters.p + 1, n + m, h->x.p, h->b.p, h->status.p, h->scal.p, L,
+                               h->part.p, h->counters.p + 1, h->part.p + nparts, nparts2, h->status.p, h->scal.p, L,
                                h->h_prog);
         };
         // Every unit launches the same kernels with the same arguments (the device state gates them),
@@ -2443,7 +2422,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                 (uintptr_t)L, (uintptr_t)lam, (uintptr_t)h->landf_edge.p, (uintptr_t)h->fland.p, (uintptr_t)h->z.p,
                 (uintptr_t)h->cb.p, (uintptr_t)h->S.p, (uintptr_t)h->blk_off.p, (uintptr_t)h->pairs.p,
                 (uintptr_t)h->blk_cnt.p, (uintptr_t)h->bs.p,
-                (uintptr_t)h->x.p, (uintptr_t)h->status.p, (uintptr_t)h->landf_off.p, (uintptr_t)h->free_pose.p,
+                (uintptr_t)h->x.p, (uintptr_t)h->status.p, (uintptr_t)h->landf_off.p, (uintptr_t)h->landf_row.p, (uintptr_t)h->free_pose.p,
                 (uintptr_t)h->land_point.p, (uintptr_t)h->pose_bak.p, (uintptr_t)h->point_bak.p, (uintptr_t)h->h_prog,
                 (uintptr_t)use_rows, (uintptr_t)trial_lin, (uintptr_t)h->lpub.p, (uintptr_t)h->ypub.p, (uintptr_t)h->cflag.p,
                 (uintptr_t)h->racc.p};
