@@ -791,12 +791,15 @@ def bench_c4_strong(pkg, synth, world, rank, dev, steps, in_flight=3, n_global=2
     (keypoints + descriptors + counts, RCCL over xGMI), overlapped with the next step's extraction
     (distributed.ShardedExtractor).  N = 1 extracts the 256 frames on one GPU with no collective.  At
     N > 1, rank 0 also times the same 256 frames alone on its GPU (while the others wait), so the line
-    carries the N = 1 reference and the strong-scaling efficiency.  Frames: n_distinct synthetic
-    1280x720 frames (seeds 1000..) repeated over the batch (generating 256 distinct ones takes ~25 s)."""
+    carries the N = 1 reference and the strong-scaling efficiency.  Every step also matches each frame
+    against its predecessor in the global batch (knn2 over the gathered blocks, one
+    orb_hamming_knn2_frames_device launch per rank for its frames; at N = 1 over the local blocks).
+    Frames: n_distinct synthetic 1280x720 frames (seeds 1000..) repeated over the batch (generating 256
+    distinct ones takes ~25 s)."""
     import numpy as np
     import torch
     import torch.distributed as dist
-    from orbslam3_amd.distributed import ShardedExtractor, shard_range
+    from orbslam3_amd.distributed import ShardedExtractor, frame_pairs, match_gathered, shard_range
     b, e = shard_range(n_global, world, rank)
     per = e - b
     if world > 1 and n_global % world:
@@ -817,18 +820,28 @@ def bench_c4_strong(pkg, synth, world, rank, dev, steps, in_flight=3, n_global=2
                for _ in range(H)]
         sts = [torch.cuda.Stream(dev) for _ in range(H)]
         if collective:
-            sh = ShardedExtractor(exs, count, cap)
+            sh = ShardedExtractor(exs, count, cap, match=True)
             step = lambda i: sh.step(imgs, (0, 1000), stream=sts[i % H])  # noqa: E731
-            fin = sh.finish
+
+            def fin():
+                g = sh.finish()  # the last step's gather, matched like the others
+                match_gathered(g[1], g[2], sh.pairs)
             counts = lambda: sh.local.counts[0]  # noqa: E731
+            match_once = lambda: match_gathered(sh.local.desc[0], sh.local.counts[0],  # noqa: E731
+                                                frame_pairs(0, count, count).to(dev))
         else:
             outs = [(torch.empty((count, cap, 7), dtype=torch.float32, device=dev),
                      torch.empty((count, cap, 32), dtype=torch.uint8, device=dev),
                      torch.empty((count, 2), dtype=torch.int32, device=dev)) for _ in range(H)]
-            step = lambda i: exs[i % H].extract_batch_device(imgs, (0, 1000), cap=cap, out=outs[i % H],  # noqa: E731
-                                                            stream=sts[i % H])
+            pairs = frame_pairs(0, count, count).to(dev)
+            mouts = [tuple(torch.empty((count, cap), dtype=torch.int32, device=dev) for _ in range(3)) for _ in range(H)]
+
+            def step(i):
+                o = exs[i % H].extract_batch_device(imgs, (0, 1000), cap=cap, out=outs[i % H], stream=sts[i % H])
+                match_gathered(o[1], o[2], pairs, stream=sts[i % H], out=mouts[i % H])
             fin = lambda: None  # noqa: E731
             counts = lambda: outs[0][2]  # noqa: E731
+            match_once = lambda: match_gathered(outs[0][1], outs[0][2], pairs, out=mouts[0])  # noqa: E731
         for i in range(2 * H):
             step(i)
         fin()
@@ -845,9 +858,20 @@ def bench_c4_strong(pkg, synth, world, rank, dev, steps, in_flight=3, n_global=2
         torch.cuda.synchronize(dev)
         if collective:
             dist.barrier()
-        return (time.perf_counter() - t0) * 1e3 / reps, feats
+        ms_step = (time.perf_counter() - t0) * 1e3 / reps
+        # the matching launch alone (its share of the step), timed on the current stream
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        match_once()
+        e0.record()
+        for _ in range(10):
+            match_once()
+        e1.record()
+        torch.cuda.synchronize(dev)
+        run.match_ms = e0.elapsed_time(e1) / 10
+        return ms_step, feats
 
     ms, feats = run(b, per, world > 1)
+    match_ms = run.match_ms
     if world > 1:
         t = torch.tensor([ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -859,7 +883,11 @@ def bench_c4_strong(pkg, synth, world, rank, dev, steps, in_flight=3, n_global=2
                      f"repeated), {per} per GPU x {world} GPU(s), nFeatures 1000, 8 levels"
                      + (", all-gather of keypoints + descriptors + counts per step (" + {"nccl": "RCCL"}.get(dist.get_backend(), dist.get_backend()) + ")" if world > 1 else ""),
            "n_gpus": world, "frames_per_gpu": per, "ms_per_step": round(ms, 4),
-           "frames_per_ms": round(n_global / ms, 3), "features_per_ms": round(feats / ms, 3)}
+           "frames_per_ms": round(n_global / ms, 3), "features_per_ms": round(feats / ms, 3),
+           "cross_frame_match": {"pairs_per_gpu": per, "ms_per_launch": round(match_ms, 4),
+                                 "what": "each frame's descriptors vs its predecessor's (knn2, best / second "
+                                         "best, DescriptorDistance), one orb_hamming_knn2_frames_device launch "
+                                         "per rank after the all-gather, inside the timed step"}}
     if world > 1:
         ref = torch.zeros(1, dtype=torch.float64, device=dev)
         if rank == 0:

@@ -113,6 +113,16 @@ int orb_hamming_knn2_device(const uint8_t* d_query, int n_query, const uint8_t* 
                             int32_t* d_best_idx, int32_t* d_best_dist, int32_t* d_second_dist,
                             void* stream);
 
+/* Cross-frame matching on a batch of device feature blocks (the extractor's [F][cap] layout, e.g. the
+ * C4 all-gather's): for each pair p = (query frame pairs[2p], train frame pairs[2p+1]) every query
+ * descriptor's best / second-best train descriptor, as orb_hamming_knn2_device (DescriptorDistance,
+ * src/ORBmatcher.cc:2384-2404; first index on ties).  Frame f holds counts[f * count_stride] descriptors
+ * (read on the device); outputs are [n_pairs][cap], rows beyond the query frame's count get
+ * (-1, 257, 257).  cap <= 2048.  One launch, async on `stream`. */
+int orb_hamming_knn2_frames_device(const uint8_t* d_desc, const int32_t* d_counts, int count_stride, int cap,
+                                   const int32_t* d_pairs, int n_pairs, int32_t* d_best_idx, int32_t* d_best_dist,
+                                   int32_t* d_second_dist, void* stream);
+
 /* ---- ORBmatcher::SearchForTriangulation (src/ORBmatcher.cc:1046-1324) ------------------------- */
 
 /* Flat view of the KeyFrame fields SearchForTriangulation reads (host memory).  Pinhole camera,

@@ -85,6 +85,7 @@ PROTOTYPES = {
     "orb_extractor_level_download": (_i, [_vp, _i, _i, _vp]),
     "orb_descriptor_distance": (_i, [_vp, _vp]),
     "orb_hamming_knn2_device": (_i, [_vp, _i, _vp, _i, _vp, _vp, _vp, _vp]),
+    "orb_hamming_knn2_frames_device": (_i, [_vp, _vp, _i, _i, _vp, _i, _vp, _vp, _vp, _vp]),
     "orb_matcher_create": (_i, [_f, _i, ctypes.POINTER(_vp)]),
     "orb_matcher_destroy": (_i, [_vp]),
     "orb_compute_distinctive_descriptors": (_i, [_vp, _vp, _vp, _i, _vp, _vp]),

@@ -160,6 +160,75 @@ __global__ __launch_bounds__(256) void k_hamming_knn2_merge(int nq, int nchunk, 
     second_dist[qi] = r.second;
 }
 
+// Many (query frame, train frame) pairs of one batch of feature blocks in one launch (cross-frame
+// matching after the C4 all-gather): block (x, p) takes queries 16x .. 16x + 15 of pair p's query
+// frame against the whole train frame staged in LDS (up to `cap` descriptors, dynamic shared
+// memory), the same 64-part scan and in-order merge as k_hamming_knn2_frame.  Frame sizes come from
+// the device counts (no host round trip); rows at or beyond the query frame's count get (-1, 257, 257).
+__global__ __launch_bounds__(1024) void k_hamming_knn2_frames(const uint8_t* __restrict__ desc,
+                                                              const int32_t* __restrict__ counts, int cstride, int cap,
+                                                              const int32_t* __restrict__ pairs,
+                                                              int32_t* __restrict__ best_idx,
+                                                              int32_t* __restrict__ best_dist,
+                                                              int32_t* __restrict__ second_dist) {
+    extern __shared__ uint4 ftile[];
+    __shared__ Knn red[kKnnParts][kKnnQ];
+    const int p = blockIdx.y;
+    const int qf = pairs[2 * p], tf = pairs[2 * p + 1];
+    const int nq = min(max(counts[(size_t)qf * cstride], 0), cap), nt = min(max(counts[(size_t)tf * cstride], 0), cap);
+    const size_t o = (size_t)p * cap;
+    const int q0 = blockIdx.x * kKnnQ;
+    if (q0 >= nq) {  // (block-uniform) nothing to match here: the rows get "no match"
+        const int qo = q0 + (int)threadIdx.x;
+        if ((int)threadIdx.x < kKnnQ && qo < cap) {
+            best_idx[o + qo] = -1;
+            best_dist[o + qo] = 257;
+            second_dist[o + qo] = 257;
+        }
+        return;
+    }
+    const uint4* t = reinterpret_cast<const uint4*>(desc + (size_t)tf * cap * 32);
+    const uint4* q = reinterpret_cast<const uint4*>(desc + (size_t)qf * cap * 32);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int ql = lane & (kKnnQ - 1), part = 4 * w + (lane >> 4);
+    const int qi = q0 + ql;
+    for (int i = threadIdx.x; i < 2 * nt; i += 1024) ftile[i] = t[i];
+    uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
+    if (qi < nq) {
+        a0 = q[2 * (size_t)qi];
+        a1 = q[2 * (size_t)qi + 1];
+    }
+    __syncthreads();
+    const int sub = (nt + kKnnParts - 1) / kKnnParts, j0 = part * sub, j1 = min(nt, j0 + sub);
+    Knn r{257, 257, -1};
+    for (int j = j0; j < j1; ++j) {
+        const int d = hamming256(a0, a1, ftile[2 * j], ftile[2 * j + 1]);
+        if (d < r.best) { r.second = r.best; r.best = d; r.idx = j; }
+        else if (d < r.second) r.second = d;
+    }
+    red[part][ql] = r;
+    __syncthreads();
+#pragma unroll
+    for (int s = 1; s < kKnnParts; s <<= 1) {
+        if ((int)threadIdx.x < (kKnnParts / (2 * s)) * kKnnQ) {
+            const int pp = (threadIdx.x / kKnnQ) * 2 * s, qq = threadIdx.x & (kKnnQ - 1);
+            red[pp][qq] = knn_merge(red[pp][qq], red[pp + s][qq]);
+        }
+        __syncthreads();
+    }
+    if ((int)threadIdx.x < kKnnQ) {
+        const int qo = q0 + threadIdx.x;
+        if (qo < cap) {
+            const Knn f = qo < nq ? red[0][threadIdx.x] : Knn{257, 257, -1};
+            best_idx[o + qo] = f.idx;
+            best_dist[o + qo] = f.best;
+            second_dist[o + qo] = f.second;
+        }
+    }
+}
+
+constexpr int kKnnFramesMaxCap = 2048;  // 64 KiB of train descriptors in LDS
+
 }  // namespace
 
 extern "C" int orb_hamming_knn2_device(const uint8_t* d_query, int n_query, const uint8_t* d_train, int n_train,
@@ -201,6 +270,29 @@ extern "C" int orb_hamming_knn2_device(const uint8_t* d_query, int n_query, cons
         if (hipFreeAsync(part, s) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "knn2 partial buffer free");
     }
     if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "hamming launch failed");
+    return ORB_OK;
+}
+
+extern "C" int orb_hamming_knn2_frames_device(const uint8_t* d_desc, const int32_t* d_counts, int count_stride,
+                                              int cap, const int32_t* d_pairs, int n_pairs, int32_t* d_best_idx,
+                                              int32_t* d_best_dist, int32_t* d_second_dist, void* stream) {
+    if (n_pairs < 0 || cap < 1 || cap > kKnnFramesMaxCap || count_stride < 1 ||
+        (n_pairs > 0 && (!d_desc || !d_counts || !d_pairs || !d_best_idx || !d_best_dist || !d_second_dist)))
+        return orbgpu_fail(ORB_ERR_ARG, "bad frame-pair matcher arguments");
+    if (n_pairs == 0) return ORB_OK;
+    if (n_pairs > 65535) return orbgpu_fail(ORB_ERR_ARG, "more than 65535 frame pairs in one call");
+    if (reinterpret_cast<uintptr_t>(d_desc) & 15) return orbgpu_fail(ORB_ERR_ARG, "descriptor blocks must be 16-byte aligned");
+    static bool attr = false;
+    if (!attr) {
+        hipFuncSetAttribute((const void*)k_hamming_knn2_frames, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kKnnFramesMaxCap * 32);
+        (void)hipGetLastError();
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_hamming_knn2_frames, dim3((cap + kKnnQ - 1) / kKnnQ, n_pairs), dim3(1024), (size_t)cap * 32,
+                       (hipStream_t)stream, d_desc, d_counts, count_stride, cap, d_pairs, d_best_idx, d_best_dist,
+                       d_second_dist);
+    if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "frame-pair hamming launch failed");
     return ORB_OK;
 }
 

@@ -4,8 +4,9 @@ One process per GPU (torch.distributed, backend "nccl" = RCCL on ROCm; "gloo" on
 Frames are independent units.  Rank r extracts frames [r*B, (r+1)*B) of the global batch into
 fixed-capacity blocks, then a single all-gather over xGMI gives every rank the features of all
 frames: descriptors [W*B, cap, 32] u8, keypoints [W*B, cap, 7] (cv::KeyPoint layout) and counts
-[W*B, 2].  Cross-frame matching then runs locally against the gathered set (knn2 of a frame's
-descriptors vs. the other frames', src/ORBmatcher.cc DescriptorDistance).
+[W*B, 2].  Cross-frame matching then runs locally against the gathered set: each rank matches its
+own frames against their predecessors in the global batch (knn2, src/ORBmatcher.cc
+DescriptorDistance; one orb_hamming_knn2_frames_device launch for all of the rank's frames).
 
 The all-gather is the only data-path collective.  It is issued asynchronously on RCCL's stream
 and double-buffered, so step i's exchange overlaps step i+1's extraction.
@@ -61,9 +62,10 @@ def all_gather_features(kps, desc, counts, group=None, async_op: bool = False):
 class ShardedExtractor:
     """ORB extraction of a global frame batch sharded over the ranks of a process group."""
 
-    def __init__(self, extractor, frames_per_rank: int, cap: int | None = None, group=None):
+    def __init__(self, extractor, frames_per_rank: int, cap: int | None = None, group=None, match: bool = False):
         """`extractor`: one ORBextractor, or a list of them used in turn (batches in flight on their
-        own streams: pass step i's stream as stream i % len)."""
+        own streams: pass step i's stream as stream i % len).  match: after each all-gather, knn2 of
+        this rank's frames against their predecessors in the gathered blocks (self.matches)."""
         self.exs = list(extractor) if isinstance(extractor, (list, tuple)) else [extractor]
         self.ex = self.exs[0]
         self.group = group
@@ -78,6 +80,13 @@ class ShardedExtractor:
         self.local = FeatureBlocks(frames_per_rank, self.cap, dev, count=self.nbuf)
         self._i = 0
         self._pending = None
+        self.match = match
+        self.matches = None  # (idx, best, second) [frames_per_rank, cap] of the last gathered step
+        if match:
+            first = self.rank * frames_per_rank  # equal shards: global frame f sits at row f of the gather
+            self.pairs = frame_pairs(first, frames_per_rank, self.world * frames_per_rank).to(dev)
+            self._mbuf = [tuple(torch.empty((frames_per_rank, self.cap), dtype=torch.int32, device=dev)
+                                for _ in range(3)) for _ in range(self.nbuf)]
 
     def step(self, images, vLappingArea=(0, 0), stream=None):
         """Extract this rank's frames (uint8 [B, H, W] on the GPU) and start the all-gather.
@@ -87,6 +96,9 @@ class ShardedExtractor:
         self.exs[self._i % len(self.exs)].extract_batch_device(images, vLappingArea, cap=self.cap, out=out,
                                                                stream=stream)
         prev = self.finish(stream)
+        if self.match and prev is not None:
+            self.matches = match_gathered(prev[1], prev[2], self.pairs, stream=stream,
+                                          out=self._mbuf[(self._i - 1) % self.nbuf])
         # RCCL orders a collective after torch's CURRENT stream only: issue it with the extraction
         # stream current, so it cannot read the blocks before the extraction has written them
         with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
@@ -151,6 +163,32 @@ def distributed_knn2(query, train, group=None, local_fn=None):
         dist.all_gather_into_tensor(gathered, block, group=group)
     flat = gathered.view(world, 3, per).permute(1, 0, 2).reshape(3, world * per)[:, :n]
     return flat[0].contiguous(), flat[1].contiguous(), flat[2].contiguous()
+
+
+def frame_pairs(first: int, count: int, n_total: int) -> torch.Tensor:
+    """(query frame, train frame) = (f, f - 1 mod n_total) for frames f in [first, first + count): each
+    frame against its predecessor in the global batch (frame 0 against the last), as tracking matches a
+    frame against the previous one.  int32 [count, 2] (CPU)."""
+    f = torch.arange(first, first + count, dtype=torch.int32)
+    return torch.stack([f, (f - 1) % n_total], 1).to(torch.int32)
+
+
+def match_gathered(g_desc, g_cnt, pairs, local_fn=None, stream=None, out=None):
+    """knn2 of each pair's query frame against its train frame in gathered feature blocks (desc
+    [F, cap, 32], counts [F, 2], pairs int32 [P, 2]): one device launch (orb_hamming_knn2_frames_device).
+    `local_fn(query_rows, train_rows) -> (idx, best, second)` replaces it pair by pair (CPU tests).
+    Returns (idx, best, second), int32 [P, cap]; rows beyond a query frame's count hold (-1, 257, 257)."""
+    if local_fn is None:
+        from .matcher import ORBmatcher
+        return ORBmatcher.knn2_frames_device(g_desc, g_cnt, pairs, stream=stream, out=out)
+    n_pairs, cap = pairs.shape[0], g_desc.shape[1]
+    res = tuple(torch.full((n_pairs, cap), v, dtype=torch.int32) for v in (-1, 257, 257))
+    for p, (qf, tf) in enumerate(pairs.tolist()):
+        nq, nt = int(g_cnt[qf, 0]), int(g_cnt[tf, 0])
+        got = local_fn(g_desc[qf, :nq].cpu(), g_desc[tf, :nt].cpu())
+        for k in range(3):
+            res[k][p, :nq] = got[k]
+    return res
 
 
 def frame_descriptors(g_desc, g_cnt, frame: int):

@@ -139,6 +139,25 @@ class ORBmatcher:
               "orb_hamming_knn2_device")
         return idx, d1, d2
 
+    @staticmethod
+    def knn2_frames_device(desc, counts, pairs, stream=None, out=None):
+        """Cross-frame knn2 over a batch of device feature blocks (orb_hamming_knn2_frames_device):
+        desc uint8 [F, cap, 32], counts int32 [F, >= 1] (column 0 = descriptors per frame), pairs int32
+        [P, 2] (query frame, train frame) on the device.  Returns (idx, best, second), int32 [P, cap]."""
+        import torch
+        d = desc.contiguous()
+        c = counts.contiguous()
+        pr = pairs.to(device=d.device, dtype=torch.int32).contiguous()
+        n_pairs, cap = pr.shape[0], d.shape[1]
+        if out is None:
+            out = tuple(torch.empty((n_pairs, cap), dtype=torch.int32, device=d.device) for _ in range(3))
+        st = stream if stream is not None else torch.cuda.current_stream(d.device)
+        check(_lib.load().orb_hamming_knn2_frames_device(d.data_ptr(), c.data_ptr(), c.shape[1], cap, pr.data_ptr(),
+                                                         n_pairs, out[0].data_ptr(), out[1].data_ptr(),
+                                                         out[2].data_ptr(), ctypes.c_void_p(st.cuda_stream)),
+              "orb_hamming_knn2_frames_device")
+        return out
+
     def ComputeDistinctiveDescriptors(self, desc, offsets):
         """MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:438-529) for a batch of map points:
         point p's observation descriptors are rows offsets[p]..offsets[p+1] of desc (uint8 [n, 32]).

@@ -179,3 +179,62 @@ def test_distributed_knn2_query_split_gloo_world2(pkg, nq, nt):
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def _np_knn2_any(query, train):
+    """_np_knn2 with an empty train set allowed (no match: -1, 257, 257)."""
+    if train.shape[0] == 0:
+        n = query.shape[0]
+        return (torch.full((n,), -1, dtype=torch.int32), torch.full((n,), 257, dtype=torch.int32),
+                torch.full((n,), 257, dtype=torch.int32))
+    return _np_knn2(query, train)
+
+
+def _match_worker(rank, world, port, total, cap, q_out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from conftest import load_package
+        load_package()
+        from orbslam3_amd import distributed as D
+        per = total // world
+        b = rank * per
+        kps = torch.zeros((per, cap, 7))
+        desc = torch.zeros((per, cap, 32), dtype=torch.uint8)
+        cnt = torch.zeros((per, 2), dtype=torch.int32)
+        for i in range(per):
+            kps[i], desc[i], cnt[i] = _fill(b + i, cap)
+        g_kps, g_desc, g_cnt = D.all_gather_features(kps, desc, cnt)
+        pairs = D.frame_pairs(b, per, total)
+        idx, d1, d2 = D.match_gathered(g_desc, g_cnt, pairs, local_fn=_np_knn2_any)
+        ok = True
+        for i in range(per):  # the single-process scan of frame f against its predecessor
+            f = b + i
+            _, qd, qc = _fill(f, cap)
+            _, td, tc = _fill((f - 1) % total, cap)
+            n = int(qc[0])
+            ri, r1, r2 = _np_knn2_any(qd[:n], td[: int(tc[0])])
+            ok &= bool(torch.equal(idx[i, :n], ri) and torch.equal(d1[i, :n], r1) and torch.equal(d2[i, :n], r2))
+            ok &= bool((idx[i, n:] == -1).all() and (d1[i, n:] == 257).all())
+        ok &= pairs.tolist() == [[b + i, (b + i - 1) % total] for i in range(per)]
+        q_out.put((rank, ok))
+    except Exception as e:  # noqa: BLE001 -- reported, not left to the queue timeout
+        q_out.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_then_cross_frame_match_gloo_world2(pkg):
+    """C4 with matching: each rank extracts (here: fills) its frames, all-gathers every rank's blocks,
+    then matches its own frames against their predecessors in the gathered set; the result equals the
+    single-process scan of the same pairs (frame 0's predecessor, the last frame, lives on the other rank)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_match_worker, args=(r, 2, port, 8, 24, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}
