@@ -709,11 +709,15 @@ def bench_single_frame(pkg, synth, cpu_baseline_on, reps=50):
     return out
 
 
-def bench_c2_pcie(pkg, synth, dev, steps, n_frames=64, in_flight=3):
+def bench_c2_pcie(pkg, synth, dev, steps, n_frames=64, in_flight=2):
     """SURVEY.md 8(d)'s wording of the metric, H2D -> extract -> D2H: the C2 batch starts in pinned
-    host memory and the keypoints, descriptors and counts end there, every step, with the same
-    handles in flight as the main line (each handle's copies and kernels on its own stream).  Never
-    `value` (the task's value is device-resident); reported beside it."""
+    host memory and the keypoints, descriptors and counts end there, every step.  The copies run on
+    their own streams (one H2D, one D2H: the link's two directions and their DMA queues) beside
+    `in_flight` extraction streams, ordered by events, so batch i+1's upload and batch i-1's download
+    overlap batch i's extraction (2 + 2 streams = the 4 hardware queues a process gets).  The link's
+    own rates are measured here too (each direction alone, both at once) and the step is compared with
+    its bound, max(upload, download, extraction).  Never `value` (the task's value is
+    device-resident); reported beside it."""
     import numpy as np
     import torch
     frames = np.stack([synth.polygon_frame(640, 480, seed=100 + i) for i in range(n_frames)])
@@ -727,14 +731,33 @@ def bench_c2_pcie(pkg, synth, dev, steps, n_frames=64, in_flight=3):
              torch.empty((n_frames, 2), dtype=torch.int32, device=dev)) for _ in range(H)]
     houts = [tuple(torch.empty(o.shape, dtype=o.dtype).pin_memory() for o in outs[h]) for h in range(H)]
     sts = [torch.cuda.Stream(dev) for _ in range(H)]
+    up, down = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    ev = lambda: torch.cuda.Event()  # noqa: E731
+    up_done = [ev() for _ in range(H)]    # dimg[h] holds the batch
+    ext_done = [ev() for _ in range(H)]   # outs[h] written, dimg[h] free
+    down_done = [ev() for _ in range(H)]  # outs[h] downloaded (free)
+    started = [False] * H
 
     def step(i):
         h = i % H
-        with torch.cuda.stream(sts[h]):
+        with torch.cuda.stream(up):
+            if started[h]:
+                up.wait_event(ext_done[h])  # the previous extraction of this handle has read dimg[h]
             dimg[h].copy_(host, non_blocking=True)
+            up_done[h].record(up)
+        with torch.cuda.stream(sts[h]):
+            sts[h].wait_event(up_done[h])
+            if started[h]:
+                sts[h].wait_event(down_done[h])  # outs[h] is downloaded
             exs[h].extract_batch_device(dimg[h], (0, 1000), cap=cap, out=outs[h], stream=sts[h])
+            ext_done[h].record(sts[h])
+        with torch.cuda.stream(down):
+            down.wait_event(ext_done[h])
             for d, o in zip(houts[h], outs[h]):
                 d.copy_(o, non_blocking=True)
+            down_done[h].record(down)
+        started[h] = True
+
     for i in range(3 * H):
         step(i)
     torch.cuda.synchronize(dev)
@@ -747,10 +770,43 @@ def bench_c2_pcie(pkg, synth, dev, steps, n_frames=64, in_flight=3):
     dt = (time.perf_counter() - t0) * 1e3
     h2d = host.numel()
     d2h = sum(o.numel() * o.element_size() for o in outs[0])
-    return {"config": f"C2 ({n_frames} x 640x480) from pinned host memory to pinned host outputs, {H} batches in flight",
+
+    # the link alone: each direction, then both at once (the same buffers and sizes as the step)
+    def timed(fn, n=10):
+        fn()
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t) * 1e3 / n
+
+    def upload():
+        with torch.cuda.stream(up):
+            dimg[0].copy_(host, non_blocking=True)
+
+    def download():
+        with torch.cuda.stream(down):
+            for d, o in zip(houts[0], outs[0]):
+                d.copy_(o, non_blocking=True)
+
+    def both():
+        upload()
+        download()
+
+    def extract():
+        exs[0].extract_batch_device(dimg[0], (0, 1000), cap=cap, out=outs[0], stream=sts[0])
+    up_ms, down_ms, both_ms, ext_ms = timed(upload), timed(download), timed(both), timed(extract)
+    bound = max(up_ms, down_ms, ext_ms)
+    return {"config": f"C2 ({n_frames} x 640x480) from pinned host memory to pinned host outputs: upload and download "
+                      f"on their own streams, {H} extraction streams, event-ordered",
             "features_per_ms": round(nfeat * reps / dt, 3), "ms_per_step": round(dt / reps, 4),
             "h2d_bytes_per_step": h2d, "d2h_bytes_per_step": d2h,
-            "pcie_gb_per_s": round((h2d + d2h) * reps / dt / 1e6, 2)}
+            "pcie_gb_per_s": round((h2d + d2h) * reps / dt / 1e6, 2),
+            "link": {"h2d_gb_per_s": round(h2d / up_ms / 1e6, 2), "d2h_gb_per_s": round(d2h / down_ms / 1e6, 2),
+                     "both_directions_gb_per_s": round((h2d + d2h) / both_ms / 1e6, 2),
+                     "upload_ms": round(up_ms, 4), "download_ms": round(down_ms, 4), "extract_ms": round(ext_ms, 4)},
+            "bound_ms_per_step": round(bound, 4), "frac_of_bound": round(bound / (dt / reps), 3)}
 
 
 def bench_c4(pkg, synth, dev, steps, n_frames=32, in_flight=3):
@@ -1151,7 +1207,7 @@ def main():
     pcie = None
     if not args.no_single and world == 1:
         try:
-            pcie = bench_c2_pcie(pkg, synth, dev, args.steps, in_flight=H)
+            pcie = bench_c2_pcie(pkg, synth, dev, args.steps)
         except Exception as e:  # noqa: BLE001
             pcie = {"error": repr(e)}
     c4 = None

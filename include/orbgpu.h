@@ -101,6 +101,19 @@ int orb_extractor_level(orb_extractor_t h, int frame, int level, const uint8_t**
  * 1734-1736): the part beyond the device's 3-pixel border is filled on the host. */
 int orb_extractor_level_download(orb_extractor_t h, int frame, int level, uint8_t* host_padded);
 
+/* ---- REGISTER_TIMES (include/Settings.h:24, src/Tracking.cc:318-420) ------------------------- */
+/* Wall-clock stage timers with the reference's names: "ORB Extraction" (orb_extract; mTimeORB_Ext,
+ * src/Frame.cc:132-146), "Stereo Matching" (orb_compute_stereo_matches; src/Frame.cc:158-170), "LBA"
+ * (orb_ba_optimize; vdLBA_ms, src/LocalMapping.cc:213-230).  Off by default; on with
+ * orb_timers_enable(1) or ORBGPU_REGISTER_TIMES=1.  orb_timer_stats gives mean and population std
+ * (calcAverage / calcDeviation, src/Tracking.cc:189-208); orb_timers_write writes them as ExecMean.txt
+ * lines ("ORB Extraction: mean$\pm$std").  orb_timer_add records a caller's own bracket. */
+int orb_timers_enable(int on);
+int orb_timers_reset(void);
+int orb_timer_add(const char* name, double ms);
+int orb_timer_stats(const char* name, double* mean_ms, double* std_ms, long long* count);
+int orb_timers_write(const char* path);
+
 /* ---- ORBmatcher (src/ORBmatcher.cc) ---------------------------------------------------------- */
 
 /* ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:2384-2404) on host data, for ABI completeness. */

@@ -10,7 +10,7 @@ from .extractor import ORBextractor, keypoints_to_structured
 from .keyframe import DeviceKeyFrame, Frame, KeyFrame, LocalMapPoints, frustum_frame, is_in_frustum
 from .matcher import ORBmatcher
 from .optimizer import LocalBA, local_bundle_adjustment, pose_optimization
-from . import distributed
+from . import distributed, timers
 from .stereo import compute_stereo_matches, compute_stereo_matches_batch_device
 from .vocabulary import ORBVocabulary
 

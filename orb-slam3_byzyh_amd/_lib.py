@@ -83,6 +83,12 @@ PROTOTYPES = {
     "orb_extract_batch_device": (_i, [_vp, _vp, _i, _i, _i, _i, _sz, _i, _i, _vp, _vp, _i, _vp, _vp]),
     "orb_extractor_level": (_i, [_vp, _i, _i, ctypes.POINTER(_vp), _ip, _ip, _ip]),
     "orb_extractor_level_download": (_i, [_vp, _i, _i, _vp]),
+    "orb_timers_enable": (_i, [_i]),
+    "orb_timers_reset": (_i, []),
+    "orb_timer_add": (_i, [ctypes.c_char_p, ctypes.c_double]),
+    "orb_timer_stats": (_i, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                             ctypes.POINTER(ctypes.c_longlong)]),
+    "orb_timers_write": (_i, [ctypes.c_char_p]),
     "orb_descriptor_distance": (_i, [_vp, _vp]),
     "orb_hamming_knn2_device": (_i, [_vp, _i, _vp, _i, _vp, _vp, _vp, _vp]),
     "orb_hamming_knn2_frames_device": (_i, [_vp, _vp, _i, _i, _vp, _i, _vp, _vp, _vp, _vp]),

@@ -2441,6 +2441,7 @@ int orb_extract_batch_device(orb_extractor_t h, const uint8_t* d_images, int n, 
 
 int orb_extract(orb_extractor_t h, const uint8_t* image, int width, int height, int stride, int lap_x0, int lap_x1,
                 orb_keypoint_t* kps, uint8_t* desc, int cap, int* n_kps) {
+    orbgpu::StageTimer timer("ORB Extraction");  // mTimeORB_Ext (src/Frame.cc:132-146)
     Extractor* e = reinterpret_cast<Extractor*>(h);
     if (n_kps) *n_kps = 0;
     if (!e) return orbgpu_fail(ORB_ERR_ARG, "null handle");

@@ -326,6 +326,7 @@ int orb_compute_stereo_matches_batch_device(orb_extractor_t left, orb_extractor_
 int orb_compute_stereo_matches(orb_extractor_t left, orb_extractor_t right, const orb_keypoint_t* kps_l, int n_l,
                                const uint8_t* desc_l, const orb_keypoint_t* kps_r, int n_r, const uint8_t* desc_r,
                                float bf, float b, float* u_right, float* depth) {
+    orbgpu::StageTimer timer("Stereo Matching");  // src/Frame.cc:158-170
     if (!left || !right || n_l < 0 || n_r < 0 || n_r > 65536 || (n_l && (!kps_l || !desc_l || !u_right || !depth)) ||
         (n_r && (!kps_r || !desc_r)) || !(b > 0.0f))
         return orbgpu_fail(ORB_ERR_ARG, "invalid stereo matching arguments");

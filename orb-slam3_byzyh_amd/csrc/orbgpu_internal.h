@@ -1,5 +1,6 @@
 // Internal helpers shared by the liborbgpu.so translation units (not part of the C ABI).
 #pragma once
+#include <chrono>
 #include <cstdint>
 
 #include "orbgpu.h"
@@ -20,3 +21,21 @@ struct OrbPyramidView {
     void* stream;           // the handle's stream (orb_extract's synchronous path runs on it)
 };
 extern "C" int orbgpu_extractor_pyramid(orb_extractor_t h, OrbPyramidView* out);
+
+// REGISTER_TIMES brackets (csrc/orb_timers.hip): StageTimer t("LBA") records the scope's wall time
+// under that name when the timers are on.
+namespace orbgpu {
+bool timers_on();
+void timer_add(const char* name, double ms);
+struct StageTimer {
+    const char* name;
+    bool on;
+    std::chrono::steady_clock::time_point t0;
+    explicit StageTimer(const char* n) : name(n), on(timers_on()) {
+        if (on) t0 = std::chrono::steady_clock::now();
+    }
+    ~StageTimer() {
+        if (on) timer_add(name, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+};
+}  // namespace orbgpu

@@ -1,0 +1,51 @@
+"""REGISTER_TIMES-compatible timers (include/orbgpu.h, csrc/orb_timers.hip): statistics as the
+reference's calcAverage / calcDeviation (src/Tracking.cc:189-208, population std), ExecMean.txt lines
+(src/Tracking.cc:356-357 format), and the brackets inside the synchronous entry points on the GPU."""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import pytest
+
+
+def test_timer_stats_and_execmean_format(pkg, tmp_path):
+    from orbslam3_amd import timers
+    timers.reset()
+    for v in (1.0, 2.0, 4.0):
+        timers.add("LBA", v)
+    timers.add("ORB Extraction", 3.5)
+    m, s, n = timers.stats("LBA")
+    mean = 7.0 / 3.0
+    assert n == 3 and math.isclose(m, mean) and math.isclose(s, math.sqrt(sum((v - mean) ** 2 for v in (1, 2, 4)) / 3))
+    assert timers.stats("Stereo Matching") == (0.0, 0.0, 0)
+    p = tmp_path / "ExecMean.txt"
+    timers.write(p)
+    lines = p.read_text().splitlines()
+    assert lines[0] == " TIME STATS in ms (mean$\\pm$std)"
+    assert lines[1] == "ORB Extraction: 3.50000$\\pm$0.00000"  # the reference's stage order, empty ones skipped
+    assert lines[2] == f"LBA: {mean:.5f}$\\pm${s:.5f}"
+    timers.reset()
+    assert timers.stats("LBA")[2] == 0
+
+
+@pytest.mark.gpu
+def test_timers_bracket_entry_points(pkg, synth):
+    from orbslam3_amd import timers
+    timers.reset()
+    img = synth.polygon_frame(640, 480, seed=5)
+    ex = pkg.ORBextractor(1000, 1.2, 8, 20, 7)
+    ex(img)  # off: nothing recorded
+    assert timers.stats("ORB Extraction")[2] == 0
+    timers.enable(True)
+    try:
+        for _ in range(3):
+            ex(img)
+        prob = synth.local_ba_problem(n_kf=6, n_points=150, obs_per_point=4, n_fixed=1, seed=3)
+        pkg.LocalBA().optimize(prob, 5)
+        m, s, n = timers.stats("ORB Extraction")
+        assert n == 3 and m > 0
+        assert timers.stats("LBA")[2] == 1
+    finally:
+        timers.enable(False)
+        timers.reset()
