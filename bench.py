@@ -709,21 +709,31 @@ def bench_single_frame(pkg, synth, cpu_baseline_on, reps=50):
     return out
 
 
-def bench_c2_pcie(pkg, synth, dev, steps, n_frames=64, in_flight=2):
+def bench_c2_pcie(pkg, synth, dev, steps, n_frames=64, in_flight=3):
     """SURVEY.md 8(d)'s wording of the metric, H2D -> extract -> D2H: the C2 batch starts in pinned
-    host memory and the keypoints, descriptors and counts end there, every step.  The copies run on
-    their own streams (one H2D, one D2H: the link's two directions and their DMA queues) beside
-    `in_flight` extraction streams, ordered by events, so batch i+1's upload and batch i-1's download
-    overlap batch i's extraction (2 + 2 streams = the 4 hardware queues a process gets).  The link's
-    own rates are measured here too (each direction alone, both at once) and the step is compared with
-    its bound, max(upload, download, extraction).  Never `value` (the task's value is
-    device-resident); reported beside it."""
+    host memory and the keypoints, descriptors and counts end there, every step.  `in_flight` handles
+    take the steps in turn, each on its own stream with its upload, extraction and download in order,
+    so one batch's copies overlap the others' kernels.  These handles run without their side streams
+    (ORBGPU_FAST_SPLIT=0 at creation): a process gets 4 hardware queues, and with 3 handles x 3 streams
+    the copies queued behind other handles' kernels (tools/pcie_probe.py: 0.83 -> 0.41 ms per step;
+    separate upload / download streams: 0.67).  The link's own rates are measured here too (each
+    direction alone, both at once) and the step is compared with its bound, max(upload, download,
+    extraction).  Never `value` (the task's value is device-resident); reported beside it."""
     import numpy as np
     import torch
     frames = np.stack([synth.polygon_frame(640, 480, seed=100 + i) for i in range(n_frames)])
     host = torch.from_numpy(frames).pin_memory()
     H = max(1, in_flight)
-    exs = [pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=640, max_height=480, max_batch=n_frames) for _ in range(H)]
+    prev = os.environ.get("ORBGPU_FAST_SPLIT")
+    os.environ["ORBGPU_FAST_SPLIT"] = "0"  # read when a handle is created
+    try:
+        exs = [pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=640, max_height=480, max_batch=n_frames)
+               for _ in range(H)]
+    finally:
+        if prev is None:
+            os.environ.pop("ORBGPU_FAST_SPLIT", None)
+        else:
+            os.environ["ORBGPU_FAST_SPLIT"] = prev
     cap = 1000 + 16 * 8
     dimg = [torch.empty_like(host, device=dev) for _ in range(H)]
     outs = [(torch.empty((n_frames, cap, 7), dtype=torch.float32, device=dev),
@@ -731,32 +741,15 @@ def bench_c2_pcie(pkg, synth, dev, steps, n_frames=64, in_flight=2):
              torch.empty((n_frames, 2), dtype=torch.int32, device=dev)) for _ in range(H)]
     houts = [tuple(torch.empty(o.shape, dtype=o.dtype).pin_memory() for o in outs[h]) for h in range(H)]
     sts = [torch.cuda.Stream(dev) for _ in range(H)]
-    up, down = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-    ev = lambda: torch.cuda.Event()  # noqa: E731
-    up_done = [ev() for _ in range(H)]    # dimg[h] holds the batch
-    ext_done = [ev() for _ in range(H)]   # outs[h] written, dimg[h] free
-    down_done = [ev() for _ in range(H)]  # outs[h] downloaded (free)
-    started = [False] * H
+    up, down = sts[0], sts[0]  # (the link measurements below)
 
     def step(i):
         h = i % H
-        with torch.cuda.stream(up):
-            if started[h]:
-                up.wait_event(ext_done[h])  # the previous extraction of this handle has read dimg[h]
-            dimg[h].copy_(host, non_blocking=True)
-            up_done[h].record(up)
         with torch.cuda.stream(sts[h]):
-            sts[h].wait_event(up_done[h])
-            if started[h]:
-                sts[h].wait_event(down_done[h])  # outs[h] is downloaded
+            dimg[h].copy_(host, non_blocking=True)
             exs[h].extract_batch_device(dimg[h], (0, 1000), cap=cap, out=outs[h], stream=sts[h])
-            ext_done[h].record(sts[h])
-        with torch.cuda.stream(down):
-            down.wait_event(ext_done[h])
             for d, o in zip(houts[h], outs[h]):
                 d.copy_(o, non_blocking=True)
-            down_done[h].record(down)
-        started[h] = True
 
     for i in range(3 * H):
         step(i)
@@ -791,15 +784,18 @@ def bench_c2_pcie(pkg, synth, dev, steps, n_frames=64, in_flight=2):
                 d.copy_(o, non_blocking=True)
 
     def both():
-        upload()
-        download()
+        with torch.cuda.stream(sts[0]):
+            dimg[0].copy_(host, non_blocking=True)
+        with torch.cuda.stream(sts[1 % H]):
+            for d, o in zip(houts[1 % H], outs[1 % H]):
+                d.copy_(o, non_blocking=True)
 
     def extract():
         exs[0].extract_batch_device(dimg[0], (0, 1000), cap=cap, out=outs[0], stream=sts[0])
     up_ms, down_ms, both_ms, ext_ms = timed(upload), timed(download), timed(both), timed(extract)
     bound = max(up_ms, down_ms, ext_ms)
-    return {"config": f"C2 ({n_frames} x 640x480) from pinned host memory to pinned host outputs: upload and download "
-                      f"on their own streams, {H} extraction streams, event-ordered",
+    return {"config": f"C2 ({n_frames} x 640x480) from pinned host memory to pinned host outputs, {H} batches in flight "
+                      f"(each handle: upload, extraction, download on its own stream; no side streams)",
             "features_per_ms": round(nfeat * reps / dt, 3), "ms_per_step": round(dt / reps, 4),
             "h2d_bytes_per_step": h2d, "d2h_bytes_per_step": d2h,
             "pcie_gb_per_s": round((h2d + d2h) * reps / dt / 1e6, 2),
@@ -986,6 +982,8 @@ def main():
     ap.add_argument("--no-single", action="store_true", help="skip the single-frame latency measurement")
     ap.add_argument("--no-c4", action="store_true", help="skip the 1280x720 (C4 shard) measurement")
     ap.add_argument("--no-matchers", action="store_true", help="skip the ORBmatcher measurements")
+    ap.add_argument("--launch-dump", default=None,
+                    help="write the timed region's per-launch kernel durations (JSON) to this path")
     args = ap.parse_args()
 
     import numpy as np
@@ -1064,10 +1062,7 @@ def main():
         ex.extract_batch_device(imgs, (0, 1000), cap=cap, out=out, stream=streams[0])
         torch.cuda.synchronize(dev)
     single_ms = (time.perf_counter() - t1) * 1e3 / min(10, args.steps)
-    # timed region; every handle records an HIP event pair on its launch stream around each of its
-    # k_pyramid_level launches (the roofline kernel)
-    for e_ in exs:
-        e_.profile("pyramid_launches")
+    # timed region (value), uninstrumented
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -1080,14 +1075,28 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed_ms = (time.perf_counter() - t0) * 1e3
-    pyr_kernel_ms, pyr_kernel_launches = 0.0, 0
+    # the same steps again, every handle recording an HIP event pair on each stage kernel's dispatch
+    # (hipExtLaunchKernel: the dispatch's own begin / end, on its stream): the roofline's launch
+    # durations.  (A separate pass: the event pairs on every launch cost the timed region ~5 %.)
     for e_ in exs:
-        ms_, n_ = e_.pyramid_launch_ms()
-        pyr_kernel_ms += ms_
-        pyr_kernel_launches += n_
+        e_.profile("pyramid_launches")
+    for _ in range(args.steps):
+        step()
+    if sharded is not None:
+        sharded.finish()
+    torch.cuda.synchronize(dev)
+    launch_ms = {k: [] for k in pkg.ORBextractor.LAUNCH_KERNELS}
+    for e_ in exs:
+        for k in launch_ms:
+            launch_ms[k] += e_.launch_durations(k)
         e_.profile(False)
+    if args.launch_dump and rank == 0:
+        pathlib.Path(args.launch_dump).write_text(json.dumps(
+            {"steps": args.steps, "frames_per_step": nfr, "features_per_step": feats_per_step,
+             "note": "per-launch durations (ms) of the timed region, HIP event pair on each dispatch "
+                     "(hipExtLaunchKernel), all in-flight handles", "launch_ms": launch_ms}))
     launches_per_step = NLEVELS  # one k_pyramid_level launch per level per batch
-    pyr_launch_avg_ms = pyr_kernel_ms / max(1, pyr_kernel_launches)
+    pyr_launch_avg_ms = sum(launch_ms["k_pyramid_level"]) / max(1, len(launch_ms["k_pyramid_level"]))
 
     total_feats = feats_per_step * args.steps
     if world > 1:
@@ -1116,6 +1125,34 @@ def main():
         if pmc and pmc.get("kernel_stage") == dom and pmc.get("frames_per_launch") == nfr:
             traffic = pmc.get("hbm_bytes_per_launch")
         dominant_stage = max(per_step, key=per_step.get) if per_step else dom
+        # every stage kernel against HBM (its algorithmic bytes per step / its launch time per step)
+        # and against the integer-VALU bound (PMC counters, profiles/pmc_latest.json); the dominant
+        # kernel is the one with the most launch time in the timed region
+        alg = algorithmic_bytes_per_frame(WIDTH, HEIGHT, nkp_frame)
+        stage_of = {"k_pyramid_level": "pyramid", "k_fast_cells": "fast", "k_quadtree_kp": "quadtree",
+                    "k_describe": "describe"}
+        kern = {}
+        for k, v in launch_ms.items():
+            if not v:
+                continue
+            per_step_ms = sum(v) / args.steps
+            st = stage_of[k]
+            bytes_step = (survey_bytes_per_frame(WIDTH, HEIGHT, nkp_frame) if st == "pyramid" else alg[st]) * nfr
+            ent = {"launches_per_step": round(len(v) / args.steps, 2), "launch_avg_us": round(1e3 * sum(v) / len(v), 2),
+                   "ms_per_step": round(per_step_ms, 4), "algorithmic_bytes_per_step": int(bytes_step),
+                   "hbm_frac": round(bytes_step / (per_step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if bytes_step else 0.0}
+            ps = (pmc or {}).get("stages", {}).get(st, {})
+            if ps.get("valu_frac") is not None:
+                ent["valu_frac"] = round(ps["valu_frac"], 4)
+                ent["valu_insts_per_launch"] = int(ps["valu_insts_per_launch"])
+            if ps.get("hbm_bytes"):
+                ent["traffic_bytes_per_step"] = int(ps["hbm_bytes"])
+            if ps.get("lds_conflict_cycles_per_lds_inst") is not None:
+                ent["lds_conflict_cycles_per_lds_inst"] = round(ps["lds_conflict_cycles_per_lds_inst"], 3)
+            kern[k] = ent
+        dom_k = max(kern, key=lambda k: kern[k]["ms_per_step"]) if kern else "k_pyramid_level"
+        dk = kern.get(dom_k, {})
+        dom_ach = dk.get("algorithmic_bytes_per_step", 0) / (dk.get("ms_per_step", 1) * 1e-3) / 1e9 if dk else 0.0
         result = {
             "metric": "ORB features/ms (640x480, 8-level) + LocalBA iter ms @1/2/4/8 GPU",
             "value": round(total_feats / elapsed_ms, 3),
@@ -1137,20 +1174,31 @@ def main():
                        "parallelism": f"frame-sharded x{world}" + (
                            f", all-gather of descriptors+keypoints ({backend})" if world > 1 else "")},
             "stages_ms": {k: round(v, 4) for k, v in per_step.items()},
-            "roofline": {"bound": "hbm", "kernel": "k_pyramid_level", "achieved": round(achieved, 2),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": traffic, "algorithmic_bytes_per_launch": int(dom_bytes),
-                         "traffic_over_algorithmic": round(traffic / dom_bytes, 3) if traffic else None,
-                         "traffic_model_bytes_per_launch": int(model_bytes),
-                         "launches_per_step": launches_per_step,
-                         "launch_avg_us": round(pyr_launch_avg_ms * 1e3, 2),
-                         "dominant_stage": dominant_stage,
-                         "note": "algorithmic bytes = SURVEY.md 8(d) 1,653,864 B per 640x480 frame (L0 read, "
-                                 "levels 1-7 written + read, 60 B per keypoint out) x frames / 8 level launches; "
-                                 "launch_avg_us from HIP event pairs around each launch in the timed region; traffic = "
-                                 "PMC FETCH_SIZE x2 + WRITE_SIZE per launch (profiles/pmc_latest.json); "
-                                 "traffic_model = the bytes this implementation's pyramid moves (views + 3-px "
-                                 "borders)"},
+            "roofline": {"bound": "hbm", "kernel": dom_k, "achieved": round(dom_ach, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(dom_ach / HBM_PEAK_GBS, 5),
+                         "traffic": (round(dk["traffic_bytes_per_step"] / dk["launches_per_step"])
+                                     if dk.get("traffic_bytes_per_step") and dk.get("launches_per_step") else None),
+                         "algorithmic_bytes_per_launch": (int(dk["algorithmic_bytes_per_step"] / dk["launches_per_step"])
+                                                          if dk.get("launches_per_step") else None),
+                         "launches_per_step": dk.get("launches_per_step"), "launch_avg_us": dk.get("launch_avg_us"),
+                         "valu": {"bound": "integer VALU", "frac": dk.get("valu_frac"),
+                                  "formula": "SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8), "
+                                             "profiles/pmc_latest.json (rocprofv3 --pmc pass of this bench)"},
+                         "kernels": kern, "dominant_stage": dominant_stage,
+                         "pyramid": {"kernel": "k_pyramid_level", "achieved": round(achieved, 2),
+                                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                                     "algorithmic_bytes_per_launch": int(dom_bytes),
+                                     "traffic_over_algorithmic": round(traffic / dom_bytes, 3) if traffic else None,
+                                     "traffic_model_bytes_per_launch": int(model_bytes),
+                                     "launches_per_step": launches_per_step,
+                                     "launch_avg_us": round(pyr_launch_avg_ms * 1e3, 2)},
+                         "note": "kernel = the stage kernel with the most launch time in the timed region; achieved = its "
+                                 "algorithmic bytes per step (bench.algorithmic_bytes_per_frame: FAST reads every level "
+                                 "once; describe 43x43 patch + 60 B per keypoint; pyramid: SURVEY.md 8(d) 1,653,864 B "
+                                 "per 640x480 frame) / its summed launch time per step; launch times from an HIP event "
+                                 "pair on every dispatch in a second pass of the timed region's steps (bench.py --launch-dump writes them; "
+                                 "profiles/r04/launch_durations_*.json); traffic = PMC FETCH_SIZE x2 + WRITE_SIZE per "
+                                 "launch (profiles/pmc_latest.json)"},
         }
         if not args.no_cpu_baseline and world == 1:
             from oracle import oracle as oracle_mod
@@ -1207,7 +1255,7 @@ def main():
     pcie = None
     if not args.no_single and world == 1:
         try:
-            pcie = bench_c2_pcie(pkg, synth, dev, args.steps)
+            pcie = bench_c2_pcie(pkg, synth, dev, args.steps, in_flight=3)
         except Exception as e:  # noqa: BLE001
             pcie = {"error": repr(e)}
     c4 = None

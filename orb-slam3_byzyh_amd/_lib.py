@@ -132,6 +132,7 @@ DEBUG_PROTOTYPES = {
     "orb_debug_node_sort": (_i, [_vp, _vp, _i, _i, _vp]),
     "orb_extractor_stage_ms": (_i, [_vp, _fp, _ip, ctypes.POINTER(ctypes.c_longlong)]),
     "orb_extractor_pyramid_launch_ms": (_i, [_vp, _fp, _ip]),
+    "orb_extractor_launch_durations": (_i, [_vp, _i, _fp, _i, _ip]),
 }
 
 STAGES = ("pyramid", "fast", "quadtree", "place", "describe")

@@ -853,7 +853,6 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
             double part = 0.0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                sub[k * 256 + q * 64 + lane] = L[q];
                 part = __builtin_fma(L[q], yv[16 * k + g4 + 4 * q], part);
                 dk[r16 * 17 + g4 + 4 * q] = Pm[q];
             }

@@ -1866,6 +1866,8 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
 // ================================================================================================
 namespace orbgpu {
 
+enum { kLaunchPyramid = 0, kLaunchFast = 1, kLaunchQuadtree = 2, kLaunchDescribe = 3 };  // profile 3 tags
+
 struct Extractor {
     Params P;
     int max_w = 0, max_h = 0, max_batch = 0;
@@ -1924,6 +1926,7 @@ struct Extractor {
                       // 3 an event pair around every pyramid level launch (k_pyramid_level durations)
     std::vector<hipEvent_t> pyr_events;  // profile 3: an event pair around every recorded pyramid launch
     size_t pyr_ev_used = 0;              // events recorded since profiling was enabled (2 per launch)
+    std::vector<int> pyr_ev_kernel;      // profile 3: the kernel of each recorded pair (kLaunch*)
     std::vector<hipEvent_t> events;   // kStages + 1 per profiled sub-batch launch
     int ev_used = 0;                  // launches recorded since the last read
     long long frames_profiled = 0;
@@ -2113,6 +2116,14 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     // (a single frame runs as one chain: too few blocks per level for the overlap to pay)
     const int split = (n > 1 && e->fast_split > 0 && e->fast_split < k.nlevels) ? e->fast_split : 0;
     const bool fast_stamps = e->fast_stamps;
+    // profile 3: the next free event pair, tagged with its kernel (nullptr when not profiling)
+    auto launch_events = [&](int kernel) -> hipEvent_t* {
+        if (e->profile != 3 || e->pyr_ev_used + 2 > e->pyr_events.size()) return nullptr;
+        hipEvent_t* pe = &e->pyr_events[e->pyr_ev_used];
+        e->pyr_ev_kernel[e->pyr_ev_used / 2] = kernel;
+        e->pyr_ev_used += 2;
+        return pe;
+    };
     auto launch_fast = [&](int l0, int l1, hipStream_t s2) {
         const int c0 = k.lv[l0].cell_begin, c1 = k.lv[l1 - 1].cell_begin + k.lv[l1 - 1].cell_count;
         if (c1 <= c0) return;
@@ -2127,8 +2138,13 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
         // per wave: window | score map | candidate list (u16, at most one entry per detectable pixel)
         const int wave_lds = 2 * win_cap + ((2 * md + 15) & ~15);
         const int groups = (c1 - c0 + 3) / 4, nblocks = groups * n, share = (nblocks + 7) / 8;
-        hipLaunchKernelGGL(k_fast_cells, dim3(8 * share), dim3(256), 4 * wave_lds, s2, e->d_geom, e->d_cells, win_cap, wave_lds,
-                           pyr, cand, ccount, cthr, c0, c1, stamps, groups, nblocks, share);
+        if (hipEvent_t* pe = launch_events(kLaunchFast))
+            hipExtLaunchKernelGGL(k_fast_cells, dim3(8 * share), dim3(256), 4 * wave_lds, s2, pe[0], pe[1], 0, e->d_geom,
+                                  e->d_cells, win_cap, wave_lds, pyr, cand, ccount, cthr, c0, c1, stamps, groups, nblocks,
+                                  share);
+        else
+            hipLaunchKernelGGL(k_fast_cells, dim3(8 * share), dim3(256), 4 * wave_lds, s2, e->d_geom, e->d_cells, win_cap,
+                               wave_lds, pyr, cand, ccount, cthr, c0, c1, stamps, groups, nblocks, share);
         if (stamps) {  // debug: mean phase clocks over the launch's cells
             std::vector<unsigned long long> h(ns);
             (void)hipStreamSynchronize(s2);
@@ -2154,11 +2170,15 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     };
     // quad-tree of levels [l0, l1): one wave per (level, frame)
     auto launch_qt = [&](int l0, int l1, hipStream_t s2) {
-        if (l1 > l0)
-            hipLaunchKernelGGL(k_quadtree_kp, dim3(l1 - l0, n), dim3(kQtThreads), e->qt_lds, s2, e->d_geom, e->d_cells, cand, ccount,
-                               scratch, sel, scount, e->qt_lds, e->d_status,
-                               e->d_stamps ? e->d_stamps + (size_t)f0 * k.nlevels * kQtStamps : nullptr, lap0, lap1, dst,
-                               lapc, l0);
+        if (l1 <= l0) return;
+        unsigned long long* qst = e->d_stamps ? e->d_stamps + (size_t)f0 * k.nlevels * kQtStamps : nullptr;
+        if (hipEvent_t* pe = launch_events(kLaunchQuadtree))
+            hipExtLaunchKernelGGL(k_quadtree_kp, dim3(l1 - l0, n), dim3(kQtThreads), e->qt_lds, s2, pe[0], pe[1], 0,
+                                  e->d_geom, e->d_cells, cand, ccount, scratch, sel, scount, e->qt_lds, e->d_status, qst,
+                                  lap0, lap1, dst, lapc, l0);
+        else
+            hipLaunchKernelGGL(k_quadtree_kp, dim3(l1 - l0, n), dim3(kQtThreads), e->qt_lds, s2, e->d_geom, e->d_cells, cand,
+                               ccount, scratch, sel, scount, e->qt_lds, e->d_status, qst, lap0, lap1, dst, lapc, l0);
     };
     // descriptors of levels [0, lim) (stage_mode 1: into the staging records; 2: all levels, the first
     // `split` from their staging records; 0: all levels computed here)
@@ -2167,10 +2187,14 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
         int chunks = 0;  // blocks per frame: ceil(sel_cap_l / 8) per level (see k_describe)
         for (int l = 0; l < lim; ++l) chunks += (k.lv[l].sel_cap + kDescKpPerBlock - 1) / kDescKpPerBlock;
         const int total = chunks * n, share = (total + 7) / 8;
-        hipLaunchKernelGGL(k_describe, dim3(8 * share), dim3(256), 0, s2, e->d_geom, pyr, sel, scount, dst, lapc,
-                           cap, kps, desc, counts, chunks, total, share, split, mode,
-                           e->d_st_kp ? e->d_st_kp + (size_t)f0 * k.sel_frame_cap : nullptr,
-                           e->d_st_desc ? e->d_st_desc + (size_t)f0 * k.sel_frame_cap * 32 : nullptr);
+        orb_keypoint_t* skp = e->d_st_kp ? e->d_st_kp + (size_t)f0 * k.sel_frame_cap : nullptr;
+        uint8_t* sdesc = e->d_st_desc ? e->d_st_desc + (size_t)f0 * k.sel_frame_cap * 32 : nullptr;
+        if (hipEvent_t* pe = launch_events(kLaunchDescribe))
+            hipExtLaunchKernelGGL(k_describe, dim3(8 * share), dim3(256), 0, s2, pe[0], pe[1], 0, e->d_geom, pyr, sel, scount,
+                                  dst, lapc, cap, kps, desc, counts, chunks, total, share, split, mode, skp, sdesc);
+        else
+            hipLaunchKernelGGL(k_describe, dim3(8 * share), dim3(256), 0, s2, e->d_geom, pyr, sel, scount, dst, lapc, cap,
+                               kps, desc, counts, chunks, total, share, split, mode, skp, sdesc);
     };
     // the early levels' FAST (and with desc_split their quad-tree + descriptors) go to the side stream
     desc_split = e->desc_split && split > 0 && !e->fast_per_level && e->d_st_kp;
@@ -2198,11 +2222,7 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
             (void)hipMemsetAsync(stamps, 0, sizeof(unsigned long long) * 8 * nblk, st);
         // profile 3: the launch carries an event pair (hipExtLaunchKernel) that takes the dispatch's own
         // begin / end timestamps -- the interval rocprofv3's kernel trace reports for it
-        hipEvent_t* pe = nullptr;
-        if (e->profile == 3 && e->pyr_ev_used + 2 <= e->pyr_events.size()) {
-            pe = &e->pyr_events[e->pyr_ev_used];
-            e->pyr_ev_used += 2;
-        }
+        hipEvent_t* pe = launch_events(kLaunchPyramid);
         auto go = [&](auto kern, auto... args) {
             if (pe) hipExtLaunchKernelGGL(kern, grid, dim3(256), 0, st, pe[0], pe[1], 0, args...);
             else hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, args...);
@@ -2672,13 +2692,14 @@ int orb_extractor_profile(orb_extractor_t h, int enable) {
     e->profile = (enable == 2 || enable == 3) ? enable : (enable != 0 ? 1 : 0);
     e->ev_used = 0;
     e->pyr_ev_used = 0;
-    if (enable == 3) {  // event pairs for 256 batches of every level, created before the timed region
-        const size_t want = (size_t)2 * orbgpu::kMaxLevels * 256;
+    if (enable == 3) {  // event pairs for 256 batches of every launch, created before the timed region
+        const size_t want = (size_t)2 * (orbgpu::kMaxLevels + 8) * 256;
         while (e->pyr_events.size() < want) {
             hipEvent_t x;
             if (hipEventCreate(&x) != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "hipEventCreate failed");
             e->pyr_events.push_back(x);
         }
+        e->pyr_ev_kernel.assign(want / 2, -1);
     }
     e->frames_profiled = 0;
     e->batches = 0;
@@ -2712,15 +2733,38 @@ int orb_extractor_pyramid_launch_ms(orb_extractor_t h, float* ms, int* launches)
     *ms = 0.f;
     if (launches) *launches = 0;
     double tot = 0;
+    int cnt = 0;
     for (size_t i = 0; i + 1 < e->pyr_ev_used; i += 2) {
+        if (e->pyr_ev_kernel[i / 2] != kLaunchPyramid) continue;
         float t = 0.f;
         if (hipEventSynchronize(e->pyr_events[i + 1]) != hipSuccess ||
             hipEventElapsedTime(&t, e->pyr_events[i], e->pyr_events[i + 1]) != hipSuccess)
             return orbgpu_fail(ORB_ERR_DEVICE, "pyramid launch events failed");
         tot += t;
+        ++cnt;
     }
     *ms = (float)tot;
-    if (launches) *launches = (int)(e->pyr_ev_used / 2);
+    if (launches) *launches = cnt;
+    return ORB_OK;
+}
+
+// Profile mode 3: each recorded launch of one stage kernel (0 k_pyramid_level, 1 k_fast_cells,
+// 2 k_quadtree_kp, 3 k_describe), in launch order: its duration from the dispatch's own event pair
+// (hipExtLaunchKernel: the dispatch's begin / end timestamps, as rocprofv3's kernel trace).
+int orb_extractor_launch_durations(orb_extractor_t h, int kernel, float* ms, int cap, int* n) {
+    Extractor* e = reinterpret_cast<Extractor*>(h);
+    if (!e || !n || (cap > 0 && !ms)) return ORB_ERR_ARG;
+    int cnt = 0;
+    for (size_t i = 0; i + 1 < e->pyr_ev_used; i += 2) {
+        if (e->pyr_ev_kernel[i / 2] != kernel) continue;
+        float t = 0.f;
+        if (hipEventSynchronize(e->pyr_events[i + 1]) != hipSuccess ||
+            hipEventElapsedTime(&t, e->pyr_events[i], e->pyr_events[i + 1]) != hipSuccess)
+            return orbgpu_fail(ORB_ERR_DEVICE, "launch events failed");
+        if (cnt < cap) ms[cnt] = t;
+        ++cnt;
+    }
+    *n = cnt;
     return ORB_OK;
 }
 

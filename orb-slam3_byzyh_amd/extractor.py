@@ -156,6 +156,20 @@ class ORBextractor:
               "orb_extractor_pyramid_launch_ms")
         return float(ms.value), n.value
 
+    LAUNCH_KERNELS = ("k_pyramid_level", "k_fast_cells", "k_quadtree_kp", "k_describe")
+
+    def launch_durations(self, kernel: str):
+        """profile("pyramid_launches"): every recorded launch of one stage kernel, in launch order, in
+        ms (each from the dispatch's own event pair)."""
+        k = self.LAUNCH_KERNELS.index(kernel)
+        n = ctypes.c_int()
+        check(self._lib.orb_extractor_launch_durations(self._h, k, None, 0, ctypes.byref(n)),
+              "orb_extractor_launch_durations")
+        buf = (ctypes.c_float * max(1, n.value))()
+        check(self._lib.orb_extractor_launch_durations(self._h, k, buf, n.value, ctypes.byref(n)),
+              "orb_extractor_launch_durations")
+        return [float(buf[i]) for i in range(n.value)]
+
     # ---- public pyramid, include/ORBextractor.h:83
     def level_padded(self, level: int, frame: int = 0) -> np.ndarray:
         """Padded plane ((h+38) x (w+38)) of level `level` of frame `frame` of the last call.  Only the

@@ -16,5 +16,6 @@ done <<'PASSES'
 
 FETCH_SIZE
 WRITE_SIZE
+SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE
 PASSES
 echo "pmc done: $i passes"
