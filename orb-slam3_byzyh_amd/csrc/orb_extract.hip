@@ -192,6 +192,11 @@ __device__ __forceinline__ int xcd_tile(int b, int share) { return (b & 7) * sha
 // 7-tap GaussianBlur weights as packed u8 (horizontal pass, v_dot4_u32_u8) and u16 pairs (vertical
 // pass, v_dot2_u32_u16 over row pairs: even output rows start on a pair, odd ones in its high half)
 constexpr uint32_t kBlurK0 = 18u | 34u << 8 | 48u << 16 | 56u << 24, kBlurK1 = 48u | 34u << 8 | 18u << 16;
+// the 7 taps shifted by k bytes against three consecutive words (word 0, 1, 2 of output column k)
+constexpr uint32_t kBlurS0[4] = {kBlurK0, 18u << 8 | 34u << 16 | 48u << 24, 18u << 16 | 34u << 24, 18u << 24};
+constexpr uint32_t kBlurS1[4] = {kBlurK1, 56u | 48u << 8 | 34u << 16 | 18u << 24, 48u | 56u << 8 | 48u << 16 | 34u << 24,
+                                 34u | 48u << 8 | 56u << 16 | 48u << 24};
+constexpr uint32_t kBlurS2[4] = {0u, 0u, 18u, 34u | 18u << 8};
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u16x2 w16(unsigned a, unsigned b) { u16x2 v; v.x = (unsigned short)a; v.y = (unsigned short)b; return v; }
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
@@ -503,16 +508,19 @@ __device__ __forceinline__ int key_score(uint32_t k) { return (int)(k & 0xff); }
 // The body of one cell for a window row stride known at compile time (kWS > 0: circle, compass and
 // neighbour offsets become LDS immediates) or at run time (kWS == 0).
 #define FAST_STAMP(k) do { if (stp && lane == 0) stp[k] = __builtin_amdgcn_s_memtime(); } while (0)
-template <int kWS>
+template <int kWS, int kSS>
 __device__ __forceinline__ void fast_cell(const KernelGeom& g, const CellDesc& C, const LevelGeom& L, int f, int cid,
                                           int lane, uint8_t* win, uint8_t* sc, uint16_t* cl, const uint8_t* src,
                                           int shift, int room, uint32_t* __restrict__ cand, int32_t* __restrict__ cell_count,
                                           uint8_t* __restrict__ cell_thr, unsigned long long* stp) {
     const int ww = C.win_w, wh = C.win_h;
     const int ws = kWS ? kWS : (shift + ww + 3) & ~3, nwr = ws >> 2;
+    // score map row stride: the map holds window rows 2 .. wh-3, columns 2 .. ww-3 (candidate list
+    // entries are (row << 7 | column) in window coordinates; windows are < 128 pixels wide)
+    const int ss = kSS ? kSS : (ww - 4 + 3) & ~3;
+    auto sc_at = [&](int e) { return ((e >> 7) - 2) * ss + (e & 127) - 2; };
     const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(src - shift);
     uint32_t* win32 = reinterpret_cast<uint32_t*>(win);
-    uint32_t* sc32 = reinterpret_cast<uint32_t*>(sc);
     // lanes = 4 rows x 16 dwords (a second column pass only for windows wider than 16 dwords)
     const int lr = lane >> 4, lw = lane & 15;
     if (nwr <= 16 && wh <= 48) {
@@ -532,7 +540,7 @@ __device__ __forceinline__ void fast_cell(const KernelGeom& g, const CellDesc& C
 #pragma unroll
         for (int k = 0; k < 12; ++k) {
             const int r = 4 * k + lr;
-            if (r < wh && lw < nwr) { win32[r * nwr + lw] = v[k]; sc32[r * nwr + lw] = 0u; }
+            if (r < wh && lw < nwr) win32[r * nwr + lw] = v[k];
         }
     } else
     for (int w0 = 0; w0 < nwr; w0 += 16) {
@@ -547,14 +555,13 @@ __device__ __forceinline__ void fast_cell(const KernelGeom& g, const CellDesc& C
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int r = r0 + 4 * k + lr;
-                if (r < wh && w < nwr) { win32[r * nwr + w] = v[k]; sc32[r * nwr + w] = 0u; }
+                if (r < wh && w < nwr) win32[r * nwr + w] = v[k];
             }
         }
     }
     wave_sync();
     FAST_STAMP(1);
-    win += shift;  // window pixel (r, c) is at win[r * ws + c]; same layout for the score map
-    sc += shift;
+    win += shift;  // window pixel (r, c) is at win[r * ws + c]; its score at sc[sc_at(r << 7 | c)]
     const int dw = ww - 6, dh = wh - 6;
     const int nd = (dw > 0 && dh > 0) ? dw * dh : 0;
     int off[16];
@@ -640,7 +647,7 @@ __device__ __forceinline__ void fast_cell(const KernelGeom& g, const CellDesc& C
             const int cnt = __popc(bits);
             const int incl = wave_incl_scan_dpp(cnt);
             int pos = nlist + incl - cnt;
-            const int base_idx = (row + 3) * ws + 8 * oct + 3;
+            const int base_idx = ((row + 3) << 7) + 8 * oct + 3;  // (row << 7 | column), window coordinates
             while (bits) {
                 const int k = __builtin_ctz(bits);
                 bits &= bits - 1u;
@@ -661,13 +668,13 @@ __device__ __forceinline__ void fast_cell(const KernelGeom& g, const CellDesc& C
         int idx = 0, s = -1;
         if (j < nlist) {
             idx = cl[j];
-            s = fast_score(win + idx, off);
+            s = fast_score(win + (idx >> 7) * ws + (idx & 127), off);
         }
         const bool is_c = s >= mint;
         const unsigned long long m = ballot(is_c);
         if (is_c) {
             cl[ncand + rank_in(m)] = (uint16_t)idx;
-            sc[idx] = (uint8_t)min(s, 255);
+            sc[sc_at(idx)] = (uint8_t)min(s, 255);
         }
         ncand += __popcll(m);
     }
@@ -680,8 +687,8 @@ __device__ __forceinline__ void fast_cell(const KernelGeom& g, const CellDesc& C
     uint8_t* lmv = win - shift;
     bool any = false;
     for (int j = lane; j < ncand; j += 64) {
-        const int idx = cl[j], s = sc[idx];
-        const bool lm = is_local_max(sc, ws, idx, s);
+        const int si = sc_at(cl[j]), s = sc[si];
+        const bool lm = is_local_max(sc, ss, si, s);
         lmv[j] = lm ? (uint8_t)(s + 1) : (uint8_t)0;  // s <= 254 for a corner (9-arc minimum - 1)
         any |= (s >= ini) && lm;
     }
@@ -704,7 +711,7 @@ __device__ __forceinline__ void fast_cell(const KernelGeom& g, const CellDesc& C
         const unsigned long long m = ballot(keep);
         if (keep) {
             const int pos = count + rank_in(m);
-            const int r = idx / ws, c = idx - (idx / ws) * ws;
+            const int r = idx >> 7, c = idx & 127;
             if (pos < C.cap) out[pos] = pack_key(C.off_x + c, C.off_y + r, s);
         }
         count += __popcll(m);
@@ -720,7 +727,7 @@ __device__ __forceinline__ void fast_cell(const KernelGeom& g, const CellDesc& C
 // One wave per FAST cell.  LDS per wave: window | score map | candidate list (u16 pixel indices).
 // Pixels with score < minTh can neither be emitted nor beat an emitted neighbour, so the exact score
 // is computed only for the pixels that are corners at minTh (compacted list, no divergence).
-__global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict__ gp, const CellDesc* __restrict__ cells, int win_cap, int wave_lds,
+__global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict__ gp, const CellDesc* __restrict__ cells, int win_cap, int sc_cap, int wave_lds,
                                                     const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
                                                     int32_t* __restrict__ cell_count, uint8_t* __restrict__ cell_thr,
                                                     int cell0, int cell_end, unsigned long long* __restrict__ stamps,
@@ -743,7 +750,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
     const uint8_t* view = pyr + (size_t)f * g.pyr_frame_bytes + L.plane_off + (size_t)kEdge * L.pitch + kEdge;
     uint8_t* win = smem + (size_t)wave * wave_lds;
     uint8_t* sc = win + win_cap;
-    uint16_t* cl = reinterpret_cast<uint16_t*>(sc + win_cap);
+    uint16_t* cl = reinterpret_cast<uint16_t*>(sc + sc_cap);
     const uint8_t* src = view + (size_t)C.ini_y * L.pitch + C.ini_x;
     // window rows as aligned dwords into an LDS image whose rows start `shift` bytes in (the level's
     // padded plane keeps the over-read inside it); row stride 52 when the window fits (the usual 42-px
@@ -752,10 +759,17 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
     // a 48-B stride gives (rows 12 dwords apart repeat the bank pattern every 8 rows)
     const int shift = (int)((uintptr_t)src & 3);
     const int room = (int)(g.pyr_frame_bytes - (L.plane_off + (long long)(kEdge + C.ini_y) * L.pitch + kEdge + C.ini_x - shift));
-    if (shift + C.win_w <= 52 && C.win_h <= 48)
-        fast_cell<52>(g, C, L, f, cid, lane, win, sc, cl, src, shift, room, cand, cell_count, cell_thr, stp);
-    else
-        fast_cell<0>(g, C, L, f, cid, lane, win, sc, cl, src, shift, room, cand, cell_count, cell_thr, stp);
+    // score map zeroed here (rows 2 .. win_h-3 and columns 2 .. win_w-3 of the window: every
+    // detectable pixel and its 3x3 neighbours)
+    for (int i = lane; i < (sc_cap >> 4); i += 64) reinterpret_cast<uint4*>(sc)[i] = make_uint4(0u, 0u, 0u, 0u);
+    if (shift + C.win_w <= 52 && C.win_h <= 48) {
+        if (C.win_w <= 44)
+            fast_cell<52, 40>(g, C, L, f, cid, lane, win, sc, cl, src, shift, room, cand, cell_count, cell_thr, stp);
+        else
+            fast_cell<52, 48>(g, C, L, f, cid, lane, win, sc, cl, src, shift, room, cand, cell_count, cell_thr, stp);
+    } else {
+        fast_cell<0, 0>(g, C, L, f, cid, lane, win, sc, cl, src, shift, room, cand, cell_count, cell_thr, stp);
+    }
 }
 #undef FAST_STAMP
 
@@ -1030,9 +1044,13 @@ struct QPlace {  // vLappingArea classification of the selected keys
 //   key phase (all waves): each key moves to its child's new position and adds itself to the child
 //     counts of its new node (LDS atomics), or, after the last step, to its node's best key.
 // ------------------------------------------------------------------------------------------------
-constexpr int kQtThreads = 256, kQtWaves = kQtThreads / 64;
+#ifndef ORB_QT_THREADS
+#define ORB_QT_THREADS 256
+#endif
+constexpr int kQtThreads = ORB_QT_THREADS, kQtWaves = kQtThreads / 64;
 constexpr int kQtCtrl = 64;  // ints: [0] fin, [1] overflow, [8..16) root map, [16..24) root counts,
-                             // [24..28) wave totals, [32..36) K partials
+                             // [24..24+W) wave totals, [24+W..24+2W) K partials (W = kQtWaves)
+static_assert(kQtThreads % 64 == 0 && 24 + 2 * kQtWaves <= kQtCtrl, "quad-tree control words");
 
 struct QT2 {
     QTree t;                    // list workspace shared with the sort: prev, split, divided, sel_*, pos*, bend
@@ -1554,11 +1572,11 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree_kp(
         Kp += v;
     }
     Kp = wave_sum(Kp);
-    if (lane == 0) T.ctrl[32 + wave] = Kp;
+    if (lane == 0) T.ctrl[24 + kQtWaves + wave] = Kp;
     __syncthreads();
     int K = 0;
 #pragma unroll
-    for (int w = 0; w < kQtWaves; ++w) K += T.ctrl[32 + w];
+    for (int w = 0; w < kQtWaves; ++w) K += T.ctrl[24 + kQtWaves + w];
     uint32_t* sel_out = sel + (size_t)f * g.sel_frame_cap + L.sel_off;
     const uint32_t* cand_level = cand + (size_t)f * g.cand_frame_cap + L.cand_off;
     QPlace place{level, L.minB, lap0, lap1, L.scale, rank_out + (size_t)f * g.sel_frame_cap + L.sel_off,
@@ -1803,10 +1821,14 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
             const uint32_t a0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
             const uint32_t a1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
             const uint32_t a2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                o[rr][k] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(a2, a1, k), kBlurK1,
-                                                  __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(a1, a0, k), kBlurK0, 0u, false), false);
+            // column k = bytes k .. k+6 of (a0, a1, a2): the kernel shifted by k bytes against the
+            // aligned words (10 v_dot4 instead of 8 v_dot4 + 8 v_alignbyte)
+            o[rr][0] = __builtin_amdgcn_udot4(a1, kBlurK1, __builtin_amdgcn_udot4(a0, kBlurK0, 0u, false), false);
+            o[rr][1] = __builtin_amdgcn_udot4(a1, kBlurS1[1], __builtin_amdgcn_udot4(a0, kBlurS0[1], 0u, false), false);
+            o[rr][2] = __builtin_amdgcn_udot4(a2, kBlurS2[2], __builtin_amdgcn_udot4(a1, kBlurS1[2],
+                                              __builtin_amdgcn_udot4(a0, kBlurS0[2], 0u, false), false), false);
+            o[rr][3] = __builtin_amdgcn_udot4(a2, kBlurS2[3], __builtin_amdgcn_udot4(a1, kBlurS1[3],
+                                              __builtin_amdgcn_udot4(a0, kBlurS0[3], 0u, false), false), false);
         }
         if (i < kItems)
             *reinterpret_cast<uint4*>(P + j * kHPW + 4 * qq) =
@@ -2132,19 +2154,23 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
         if (fast_stamps && hipMalloc(&stamps, ns * 8) == hipSuccess) (void)hipMemsetAsync(stamps, 0, ns * 8, s2);
         // LDS per wave sized by the largest window of the launched levels: the early levels' smaller
         // windows allow more resident waves than the level-7 window would
-        int mw = 0, md = 0;
-        for (int l = l0; l < l1; ++l) { mw = std::max(mw, G.max_win_lv[l]); md = std::max(md, G.max_det_lv[l]); }
-        const int win_cap = (mw + 15) & ~15;
+        int mw = 0, md = 0, ms = 0;
+        for (int l = l0; l < l1; ++l) {
+            mw = std::max(mw, G.max_win_lv[l]);
+            md = std::max(md, G.max_det_lv[l]);
+            ms = std::max(ms, G.max_sc_lv[l]);
+        }
+        const int win_cap = (mw + 15) & ~15, sc_cap = (ms + 15) & ~15;
         // per wave: window | score map | candidate list (u16, at most one entry per detectable pixel)
-        const int wave_lds = 2 * win_cap + ((2 * md + 15) & ~15);
+        const int wave_lds = win_cap + sc_cap + ((2 * md + 15) & ~15);
         const int groups = (c1 - c0 + 3) / 4, nblocks = groups * n, share = (nblocks + 7) / 8;
         if (hipEvent_t* pe = launch_events(kLaunchFast))
             hipExtLaunchKernelGGL(k_fast_cells, dim3(8 * share), dim3(256), 4 * wave_lds, s2, pe[0], pe[1], 0, e->d_geom,
-                                  e->d_cells, win_cap, wave_lds, pyr, cand, ccount, cthr, c0, c1, stamps, groups, nblocks,
+                                  e->d_cells, win_cap, sc_cap, wave_lds, pyr, cand, ccount, cthr, c0, c1, stamps, groups, nblocks,
                                   share);
         else
             hipLaunchKernelGGL(k_fast_cells, dim3(8 * share), dim3(256), 4 * wave_lds, s2, e->d_geom, e->d_cells, win_cap,
-                               wave_lds, pyr, cand, ccount, cthr, c0, c1, stamps, groups, nblocks, share);
+                               sc_cap, wave_lds, pyr, cand, ccount, cthr, c0, c1, stamps, groups, nblocks, share);
         if (stamps) {  // debug: mean phase clocks over the launch's cells
             std::vector<unsigned long long> h(ns);
             (void)hipStreamSynchronize(s2);

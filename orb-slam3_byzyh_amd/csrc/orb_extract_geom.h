@@ -115,6 +115,7 @@ struct Geometry {
     int max_win = 0;            // largest FAST window (bytes)
     int max_win_lv[kMaxLevels] = {};  // the same per level (a launch's LDS is sized for its levels)
     int max_det_lv[kMaxLevels] = {};  // largest detectable region of a window per level (candidate list entries)
+    int max_sc_lv[kMaxLevels] = {};   // largest FAST score map per level (bytes, k_fast_cells' layout)
     int max_level_cands = 0;    // largest per-level candidate capacity
     int max_sel = 0;            // largest per-level selected capacity
 };
@@ -214,6 +215,11 @@ inline bool build_geometry(const Params& P, int width, int height, Geometry& g) 
                 g.max_win = std::max(g.max_win, wbytes);
                 g.max_win_lv[l] = std::max(g.max_win_lv[l], wbytes);
                 g.max_det_lv[l] = std::max(g.max_det_lv[l], dw * dh);
+                if (c.win_w >= 128 || c.win_h >= 512) return false;  // k_fast_cells' (row << 7 | column) entries
+                // score map: rows 2 .. win_h-3, columns 2 .. win_w-3, row stride 40 (win_w <= 44) or
+                // 48 (the fixed-stride kernel path), else win_w - 4 rounded up to a dword
+                const int ss = c.win_w <= 44 ? 40 : std::max(48, (c.win_w - 4 + 3) & ~3);
+                g.max_sc_lv[l] = std::max(g.max_sc_lv[l], std::max(0, c.win_h - 4) * ss);
                 g.cells.push_back(c);
             }
         }

@@ -291,6 +291,7 @@ def test_schedule_switches_parity(pkg, oracle, synth, monkeypatch, env):
     (1280, 720, "poly", 1500, 1.5, 6, 25, 10),   # level ratio > 1.25: the wide-box resize path
     (1280, 720, "noise", 800, 2.0, 4, 20, 7),    # ratio 2, few levels
     (752, 480, "poly", 1000, 1.1, 12, 15, 5),    # 12 levels (kMaxLevels), low thresholds
+    (104, 110, "noise", 200, 1.2, 2, 20, 7),     # one cell column per level: 72- and 55-px FAST windows
 ])
 def test_extract_parity_other_parameters(pkg, oracle, synth, w, h, kind, nf, scale, nlevels, ini, mn):
     """ORBextractor parameters other than the 1.2 / 8 / 20 / 7 of the bench configs (the reference

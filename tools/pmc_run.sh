@@ -10,7 +10,7 @@ i=0
 while read -r line; do
   [ -z "$line" ] && continue
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $line --kernel-trace --output-format csv -d "$OUT" -o "pass$i" -- python3 bench.py $ARGS > "$OUT/pass$i.log" 2>&1 || { echo "pass $i failed"; exit 1; }
+  ORB_BENCH_SETTLE_MS=0 timeout -k 10 300 rocprofv3 --pmc $line --kernel-trace --output-format csv -d "$OUT" -o "pass$i" -- python3 bench.py $ARGS > "$OUT/pass$i.log" 2>&1 || { echo "pass $i failed"; exit 1; }
 done <<'PASSES'
 
 
