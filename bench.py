@@ -242,6 +242,7 @@ def bench_stereo(pkg, synth, dev, steps, cpu_baseline_on, n_pairs=32, n_sets=2):
                      "exr": pkg.ORBextractor(1200, 1.2, 8, 20, 7, max_width=752, max_height=480, max_batch=n_pairs),
                      "out_l": mk(), "out_r": mk(), "s_l": torch.cuda.Stream(dev), "s_r": torch.cuda.Stream(dev),
                      "s_m": torch.cuda.Stream(dev)})
+        throughput_mode([sets[-1]["exl"], sets[-1]["exr"]])
 
     # left and right extractions run concurrently on their own streams, as Frame.cc:136-141 runs the
     # two extractors on two threads; the matching waits for both
@@ -330,6 +331,7 @@ def bench_c3_chain(pkg, synth, dev, steps, cpu_baseline_on, n_kf=32, n_nb=10):
                       torch.empty((n_kf, cap, 32), dtype=torch.uint8, device=dev),
                       torch.empty((n_kf, 2), dtype=torch.int32, device=dev))
         S["out_l"], S["out_r"] = mk(), mk()
+        throughput_mode([S["exl"], S["exr"]])
         S["u"] = torch.empty((n_kf, cap), dtype=torch.float32, device=dev)
         S["st_out"] = (S["u"], torch.empty((n_kf, cap), dtype=torch.float32, device=dev),
                        torch.empty(n_kf, dtype=torch.int32, device=dev))
@@ -714,9 +716,7 @@ def bench_c2_pcie(pkg, synth, dev, steps, n_frames=64, in_flight=3):
     host memory and the keypoints, descriptors and counts end there, every step.  `in_flight` handles
     take the steps in turn, each on its own stream with its upload, extraction and download in order,
     so one batch's copies overlap the others' kernels.  These handles run without their side streams
-    (ORBGPU_FAST_SPLIT=0 at creation): a process gets 4 hardware queues, and with 3 handles x 3 streams
-    the copies queued behind other handles' kernels (tools/pcie_probe.py: 0.83 -> 0.41 ms per step;
-    separate upload / download streams: 0.67).  The link's own rates are measured here too (each
+    (set_overlap(False)): a process gets 4 hardware queues.  The link's own rates are measured here too (each
     direction alone, both at once) and the step is compared with its bound, max(upload, download,
     extraction).  Never `value` (the task's value is device-resident); reported beside it."""
     import numpy as np
@@ -724,16 +724,10 @@ def bench_c2_pcie(pkg, synth, dev, steps, n_frames=64, in_flight=3):
     frames = np.stack([synth.polygon_frame(640, 480, seed=100 + i) for i in range(n_frames)])
     host = torch.from_numpy(frames).pin_memory()
     H = int(os.environ.get("ORB_PCIE_H", max(1, in_flight)))
-    prev = os.environ.get("ORBGPU_FAST_SPLIT")
-    os.environ["ORBGPU_FAST_SPLIT"] = "0"  # read when a handle is created
-    try:
-        exs = [pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=640, max_height=480, max_batch=n_frames)
-               for _ in range(H)]
-    finally:
-        if prev is None:
-            os.environ.pop("ORBGPU_FAST_SPLIT", None)
-        else:
-            os.environ["ORBGPU_FAST_SPLIT"] = prev
+    exs = [pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=640, max_height=480, max_batch=n_frames)
+           for _ in range(H)]
+    for e in exs:
+        e.set_overlap(False)  # one chain per batch on its handle's stream (no side streams)
     cap = 1000 + 16 * 8
     dimg = [torch.empty_like(host, device=dev) for _ in range(H)]
     outs = [(torch.empty((n_frames, cap, 7), dtype=torch.float32, device=dev),
@@ -822,6 +816,16 @@ def bench_c2_pcie(pkg, synth, dev, steps, n_frames=64, in_flight=3):
             "bound_ms_per_step": round(bound, 4), "frac_of_bound": round(bound / (dt / reps), 3)}
 
 
+def throughput_mode(exs):
+    """Handles that keep several batches in flight run each batch as one chain on its own stream
+    (ORBextractor.set_overlap(False)); ORB_BENCH_OVERLAP=1 keeps the side streams (A/B)."""
+    if len(exs) > 1:
+        on = os.environ.get("ORB_BENCH_OVERLAP", "0") == "1"
+        for e in exs:
+            e.set_overlap(on)
+    return exs
+
+
 def run_pcie_child(steps):
     """bench_c2_pcie in a process of its own.  HIP maps a process's streams onto 4 hardware queues
     by use count; after the other measurements have created their handles' streams, the three
@@ -847,8 +851,8 @@ def bench_c4(pkg, synth, dev, steps, n_frames=32, in_flight=3):
     frames = np.stack([synth.polygon_frame(1280, 720, seed=1000 + i) for i in range(n_frames)])
     imgs = torch.from_numpy(frames).to(dev)
     H = max(1, in_flight)
-    exs = [pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=1280, max_height=720, max_batch=n_frames)
-           for _ in range(H)]
+    exs = throughput_mode([pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=1280, max_height=720, max_batch=n_frames)
+                           for _ in range(H)])
     cap = 1000 + 16 * 8
     outs = [(torch.empty((n_frames, cap, 7), dtype=torch.float32, device=dev),
              torch.empty((n_frames, cap, 32), dtype=torch.uint8, device=dev),
@@ -901,6 +905,8 @@ def bench_c4_strong(pkg, synth, world, rank, dev, steps, in_flight=3, n_global=2
 
     def run(first, count, collective):
         imgs = torch.from_numpy(np.stack([frame(f) for f in range(first, first + count)])).to(dev)
+        # (batches of 256 frames fill the chip alone: the side-stream overlap stays on, 131k vs 123k
+        # features/ms without it)
         exs = [pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=1280, max_height=720, max_batch=count)
                for _ in range(H)]
         sts = [torch.cuda.Stream(dev) for _ in range(H)]
@@ -1048,6 +1054,10 @@ def main():
     H = max(1, args.in_flight)
     exs = [pkg.ORBextractor(NFEAT, 1.2, NLEVELS, 20, 7, max_width=WIDTH, max_height=HEIGHT, max_batch=nfr)
            for _ in range(H)]
+    # several batches in flight: each batch as one chain on its handle's stream.  The side streams
+    # (intra-batch overlap, the default) shorten one batch alone but share the process's 4 hardware
+    # queues with the other handles' streams: 297k -> 320k features/ms without them at H = 3.
+    throughput_mode(exs)
     ex = exs[0]
     cap = NFEAT + 16 * NLEVELS
     outs = [(torch.empty((nfr, cap, 7), dtype=torch.float32, device=dev),

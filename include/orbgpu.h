@@ -89,6 +89,14 @@ int orb_extract_batch_device(orb_extractor_t h, const uint8_t* d_images, int n, 
                              orb_keypoint_t* d_kps, uint8_t* d_desc, int cap, int32_t* d_counts,
                              void* stream);
 
+/* Scheduling of a batch on the device path (no reference counterpart).  mode 1 (the default): the
+ * early levels' FAST, quad-tree and descriptors run on the handle's side streams beside the small
+ * pyramid levels -- the shortest time for one batch alone.  mode 0: a batch runs as one chain on the
+ * caller's stream -- the higher throughput when several handles keep batches in flight on their own
+ * streams (their side streams would share the process's hardware queues).  Results are identical;
+ * takes effect at the next call. */
+int orb_extractor_set_overlap(orb_extractor_t h, int mode);
+
 /* mvImagePyramid[level] of frame `frame` of the last call (include/ORBextractor.h:83; read by
  * Frame::ComputeStereoMatches src/Frame.cc:1126,1249).  Gives the device address of the view
  * (first pixel of the level image inside its padded plane), its size and row pitch.  On the device

@@ -81,6 +81,7 @@ PROTOTYPES = {
     "orb_extractor_scales": (_i, [_vp, _fp, _fp, _fp, _fp, _ip]),
     "orb_extract": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _ip]),
     "orb_extract_batch_device": (_i, [_vp, _vp, _i, _i, _i, _i, _sz, _i, _i, _vp, _vp, _i, _vp, _vp]),
+    "orb_extractor_set_overlap": (_i, [_vp, _i]),
     "orb_extractor_level": (_i, [_vp, _i, _i, ctypes.POINTER(_vp), _ip, _ip, _ip]),
     "orb_extractor_level_download": (_i, [_vp, _i, _i, _vp]),
     "orb_timers_enable": (_i, [_i]),

@@ -1933,6 +1933,7 @@ struct Extractor {
     int chunk = 1 << 30, nstreams = 1;  // off by default: measured slower (streams did not overlap)
     bool fast_stamps = false, pyr_stamps = false;  // debug phase clocks (ORBGPU_FAST_STAMPS / _PYR_STAMPS)
     int fast_split = 3;                 // FAST on levels [0, fast_split) overlaps the small pyramid levels
+    int fast_split_cfg = 3;             // the configured split (orb_extractor_set_overlap(h, 0) sets fast_split 0)
     int fast_per_level = 0;             // 1: FAST of each later level right after its pyramid level (side2); measured slower
     int desc_split = 1;                 // 1: quad-tree + descriptors of levels [0, fast_split) on the side stream (ORBGPU_DESC_SPLIT)
     orb_keypoint_t* d_st_kp = nullptr; size_t st_kp_cap = 0;   // their staging records (desc_split)
@@ -2382,6 +2383,7 @@ int orb_extractor_create(const orb_params_t* p, int max_width, int max_height, i
     if (const char* c = getenv("ORBGPU_CHUNK")) e->chunk = std::max(1, atoi(c));
     if (const char* c = getenv("ORBGPU_STREAMS")) e->nstreams = std::min(Extractor::kMaxStreams, std::max(1, atoi(c)));
     if (const char* c = getenv("ORBGPU_FAST_SPLIT")) e->fast_split = atoi(c);
+    e->fast_split_cfg = e->fast_split;
     bool ok = hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) == hipSuccess &&
               hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&e->side2, hipStreamNonBlocking) == hipSuccess;
@@ -2483,6 +2485,13 @@ int orb_extract_batch_device(orb_extractor_t h, const uint8_t* d_images, int n, 
     if (rc != ORB_OK) return rc;
     return launch_batch(e, d_images, n, width, height, stride, frame_stride, lap_x0, lap_x1, d_kps, d_desc, cap,
                         d_counts, (hipStream_t)stream);
+}
+
+int orb_extractor_set_overlap(orb_extractor_t h, int mode) {
+    Extractor* e = reinterpret_cast<Extractor*>(h);
+    if (!e || (mode != 0 && mode != 1)) return orbgpu_fail(ORB_ERR_ARG, "bad handle or overlap mode");
+    e->fast_split = mode ? e->fast_split_cfg : 0;
+    return ORB_OK;
 }
 
 int orb_extract(orb_extractor_t h, const uint8_t* image, int width, int height, int stride, int lap_x0, int lap_x1,

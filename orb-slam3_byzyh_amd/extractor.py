@@ -131,6 +131,12 @@ class ORBextractor:
         self._last_frames = b
         return kps, desc, counts
 
+    def set_overlap(self, on: bool) -> None:
+        """Batch scheduling on the device path (orb_extractor_set_overlap): True (default) runs the
+        early levels on the handle's side streams (one batch alone finishes sooner); False runs each
+        batch as one chain on the caller's stream (more throughput with several handles in flight)."""
+        check(self._lib.orb_extractor_set_overlap(self._h, 1 if on else 0), "orb_extractor_set_overlap")
+
     # ---- per-stage timing (HIP events on the launch stream)
     def profile(self, enable: bool | str = True) -> None:
         """Record HIP events at stage boundaries: True = every stage, "pyramid" = only around the

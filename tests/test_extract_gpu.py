@@ -287,6 +287,29 @@ def test_schedule_switches_parity(pkg, oracle, synth, monkeypatch, env):
         assert np.array_equal(desc[f, :n].cpu().numpy(), rd), f
 
 
+def test_set_overlap_parity(pkg, oracle, synth):
+    """orb_extractor_set_overlap: a batch as one chain on the caller's stream (0) and with the early
+    levels on the side streams (1, the default) give the oracle's keypoints and descriptors; bad modes
+    are rejected."""
+    import torch
+    frames = synth.frame_batch(5, 640, 480, seed0=1500)
+    ex = pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=640, max_height=480, max_batch=8)
+    ref = oracle.OracleExtractor(1000, 1.2, 8, 20, 7)
+    imgs = torch.from_numpy(frames).cuda()
+    for on in (False, True, False):
+        ex.set_overlap(on)
+        kps, desc, counts = ex.extract_batch_device(imgs, (0, 1000))
+        torch.cuda.synchronize()
+        counts = counts.cpu().numpy()
+        for f in range(len(frames)):
+            rk, rd, rm = ref(frames[f], (0, 1000))
+            n = int(counts[f, 0])
+            assert n == len(rk) and int(counts[f, 1]) == rm, (on, f)
+            assert np.array_equal(pkg.keypoints_to_structured(kps[f], n).view(np.uint8), rk.view(np.uint8)), (on, f)
+            assert np.array_equal(desc[f, :n].cpu().numpy(), rd), (on, f)
+    assert ex._lib.orb_extractor_set_overlap(ex._h, 2) < 0
+
+
 @pytest.mark.parametrize("w,h,kind,nf,scale,nlevels,ini,mn", [
     (1280, 720, "poly", 1500, 1.5, 6, 25, 10),   # level ratio > 1.25: the wide-box resize path
     (1280, 720, "noise", 800, 2.0, 4, 20, 7),    # ratio 2, few levels
