@@ -714,11 +714,13 @@ def bench_single_frame(pkg, synth, cpu_baseline_on, reps=50):
 def bench_c2_pcie(pkg, synth, dev, steps, n_frames=64, in_flight=3):
     """SURVEY.md 8(d)'s wording of the metric, H2D -> extract -> D2H: the C2 batch starts in pinned
     host memory and the keypoints, descriptors and counts end there, every step.  `in_flight` handles
-    take the steps in turn, each on its own stream with its upload, extraction and download in order,
-    so one batch's copies overlap the others' kernels.  These handles run without their side streams
-    (set_overlap(False)): a process gets 4 hardware queues.  The link's own rates are measured here too (each
-    direction alone, both at once) and the step is compared with its bound, max(upload, download,
-    extraction).  Never `value` (the task's value is device-resident); reported beside it."""
+    take the steps in turn.  The uploads run by DMA on one upload stream; each handle's extraction
+    waits for its batch's upload on the handle's stream and its kernels write the outputs straight into
+    the pinned host buffers (the D2H leg is the describe kernel's own stores over the link), so the next
+    batch's upload overlaps this batch's kernels.  The handles run without their side streams
+    (set_overlap(False)).  The link's own rates are measured here too (each direction alone, both at
+    once) and the step is compared with its bound, max(upload, extraction).  Never `value` (the task's
+    value is device-resident); reported beside it."""
     import numpy as np
     import torch
     frames = np.stack([synth.polygon_frame(640, 480, seed=100 + i) for i in range(n_frames)])
@@ -737,10 +739,15 @@ def bench_c2_pcie(pkg, synth, dev, steps, n_frames=64, in_flight=3):
     sts = [torch.cuda.Stream(dev) for _ in range(H)]
     up, down = sts[0], sts[0]  # (the link measurements below)
 
-    # ORB_PCIE_MODE (A/B): "copy" = DMA copies on each handle's stream; "zc_in" = the level-0 pyramid
-    # kernel reads the pinned frames itself; "zc_all" = that, and the kernels write the outputs into the
-    # pinned host buffers (no copies)
-    mode = os.environ.get("ORB_PCIE_MODE", "copy")
+    # ORB_PCIE_MODE (A/B, tools: one box, two passes each, ms per step at H = 2 / 3):
+    #   "up_zc_out" (default): uploads by DMA on one upload stream, event-ordered with each handle's
+    #       extraction, which writes keypoints, descriptors and counts straight into the pinned host
+    #       buffers (no download copy): 0.456-0.519 / 0.508-0.524;
+    #   "copy": upload, extraction and download copy on each handle's stream: 0.494-0.497 / 0.733-0.742;
+    #   "zc_out": upload on the handle's stream, outputs written to host: 0.596-0.748 / 0.783-0.793;
+    #   "zc_in": the level-0 pyramid kernel reads the pinned frames itself: 1.01-1.06;
+    #   "zc_all": zc_in + outputs written to host: 0.707-0.733.
+    mode = os.environ.get("ORB_PCIE_MODE", "up_zc_out")
 
     def abi_extract(h, img_ptr, o):
         e = exs[h]
@@ -750,15 +757,36 @@ def bench_c2_pcie(pkg, synth, dev, steps, n_frames=64, in_flight=3):
         if rc < 0:
             raise RuntimeError(f"orb_extract_batch_device failed ({rc})")
 
+    # "zc_out": upload by DMA on the handle's stream, outputs written by the kernels into the pinned host
+    # buffers; "up_zc_out": the same with the uploads on one upload stream, event-ordered
+    upl = torch.cuda.Stream(dev) if mode == "up_zc_out" else None
+    up_done = [torch.cuda.Event() for _ in range(H)]
+    ext_done = [torch.cuda.Event() for _ in range(H)]
+    started = [False] * H
+
     def step(i):
         h = i % H
-        with torch.cuda.stream(sts[h]):
-            if mode == "copy":
+        if mode == "up_zc_out":
+            with torch.cuda.stream(upl):
+                if started[h]:
+                    upl.wait_event(ext_done[h])  # the handle's previous extraction has read dimg[h]
                 dimg[h].copy_(host, non_blocking=True)
-                exs[h].extract_batch_device(dimg[h], (0, 1000), cap=cap, out=outs[h], stream=sts[h])
+                up_done[h].record(upl)
+            sts[h].wait_event(up_done[h])
+            abi_extract(h, dimg[h].data_ptr(), houts[h])
+            ext_done[h].record(sts[h])
+            started[h] = True
+            return
+        with torch.cuda.stream(sts[h]):
+            if mode in ("copy", "zc_out"):
+                dimg[h].copy_(host, non_blocking=True)
+                if mode == "copy":
+                    exs[h].extract_batch_device(dimg[h], (0, 1000), cap=cap, out=outs[h], stream=sts[h])
+                else:
+                    abi_extract(h, dimg[h].data_ptr(), houts[h])
             else:  # the level-0 pyramid kernel reads the pinned host frames itself
                 abi_extract(h, host.data_ptr(), outs[h] if mode == "zc_in" else houts[h])
-            if mode != "zc_all":
+            if mode in ("copy", "zc_in"):
                 for d, o in zip(houts[h], outs[h]):
                     d.copy_(o, non_blocking=True)
 
@@ -804,9 +832,10 @@ def bench_c2_pcie(pkg, synth, dev, steps, n_frames=64, in_flight=3):
     def extract():
         exs[0].extract_batch_device(dimg[0], (0, 1000), cap=cap, out=outs[0], stream=sts[0])
     up_ms, down_ms, both_ms, ext_ms = timed(upload), timed(download), timed(both), timed(extract)
-    bound = max(up_ms, down_ms, ext_ms)
+    bound = max(up_ms, ext_ms) if mode in ("up_zc_out", "zc_out", "zc_all") else max(up_ms, down_ms, ext_ms)
     return {"config": f"C2 ({n_frames} x 640x480) from pinned host memory to pinned host outputs, {H} batches in flight "
-                      f"(each handle: upload, extraction, download on its own stream; no side streams; mode {mode})",
+                      f"(mode {mode}: uploads on one upload stream, each extraction on its handle's stream writing "
+                      f"its outputs into pinned host memory)",
             "features_per_ms": round(nfeat * reps / dt, 3), "ms_per_step": round(dt / reps, 4),
             "h2d_bytes_per_step": h2d, "d2h_bytes_per_step": d2h,
             "pcie_gb_per_s": round((h2d + d2h) * reps / dt / 1e6, 2),

@@ -83,7 +83,9 @@ int orb_extract(orb_extractor_t h, const uint8_t* image, int width, int height, 
  * rows `stride` bytes apart.  Frame f writes d_kps[f*cap ...], d_desc[(f*cap ...)*32] and
  * d_counts[2f] = number of keypoints, d_counts[2f+1] = monoIndex (or ORB_ERR_CAPACITY if the frame
  * had more than cap keypoints; then d_counts[2f] still holds the count).  stream: hipStream_t
- * (NULL = default stream).  Returns after enqueueing. */
+ * (NULL = default stream).  Returns after enqueueing.  The outputs (and d_images) may also be pinned,
+ * device-mapped host memory (hipHostMalloc): the kernels then read / write it over the link, which is
+ * how a host-input pipeline skips the download copy. */
 int orb_extract_batch_device(orb_extractor_t h, const uint8_t* d_images, int n, int width, int height,
                              int stride, size_t frame_stride, int lap_x0, int lap_x1,
                              orb_keypoint_t* d_kps, uint8_t* d_desc, int cap, int32_t* d_counts,

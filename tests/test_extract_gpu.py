@@ -287,6 +287,32 @@ def test_schedule_switches_parity(pkg, oracle, synth, monkeypatch, env):
         assert np.array_equal(desc[f, :n].cpu().numpy(), rd), f
 
 
+def test_batch_outputs_to_pinned_host(pkg, synth):
+    """orb_extract_batch_device writing keypoints, descriptors and counts straight into pinned host
+    memory (the PCIe bench's download-free form) gives the bytes of the device-output call."""
+    import ctypes
+    import torch
+    frames = synth.frame_batch(4, 640, 480, seed0=1600)
+    ex = pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=640, max_height=480, max_batch=4)
+    imgs = torch.from_numpy(frames).cuda()
+    kps, desc, counts = ex.extract_batch_device(imgs, (0, 1000))
+    cap = kps.shape[1]
+    hk = torch.empty(kps.shape, dtype=kps.dtype).pin_memory()
+    hd = torch.empty(desc.shape, dtype=desc.dtype).pin_memory()
+    hc = torch.empty(counts.shape, dtype=counts.dtype).pin_memory()
+    st = torch.cuda.current_stream()
+    rc = ex._lib.orb_extract_batch_device(ex._h, imgs.data_ptr(), 4, 640, 480, 640, 640 * 480, 0, 1000,
+                                          hk.data_ptr(), hd.data_ptr(), cap, hc.data_ptr(), ctypes.c_void_p(st.cuda_stream))
+    assert rc >= 0
+    torch.cuda.synchronize()
+    c = counts.cpu()
+    assert torch.equal(hc, c)
+    for f in range(4):
+        n = int(c[f, 0])
+        assert torch.equal(hk[f, :n].view(torch.int32), kps[f, :n].cpu().view(torch.int32)), f
+        assert torch.equal(hd[f, :n], desc[f, :n].cpu()), f
+
+
 def test_set_overlap_parity(pkg, oracle, synth):
     """orb_extractor_set_overlap: a batch as one chain on the caller's stream (0) and with the early
     levels on the side streams (1, the default) give the oracle's keypoints and descriptors; bad modes
