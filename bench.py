@@ -1145,7 +1145,7 @@ def main():
     settle_s = float(os.environ.get("ORB_BENCH_SETTLE_MS", "300")) * 1e-3
     t_settle = time.perf_counter()
     while time.perf_counter() - t_settle < settle_s:
-        for _ in range(H):
+        for _ in range(8 * H):  # batches stay in flight; a sync every 8 rounds bounds the queue
             step()
         torch.cuda.synchronize(dev)
     if sharded is not None:
