@@ -1934,6 +1934,7 @@ struct Extractor {
     bool fast_stamps = false, pyr_stamps = false;  // debug phase clocks (ORBGPU_FAST_STAMPS / _PYR_STAMPS)
     int fast_split = 3;                 // FAST on levels [0, fast_split) overlaps the small pyramid levels
     int fast_split_cfg = 3;             // the configured split (orb_extractor_set_overlap(h, 0) sets fast_split 0)
+    int chain_fast_split = 1;           // one-chain FAST launches (see launch_chunk; ORBGPU_CHAIN_FAST)
     int fast_per_level = 0;             // 1: FAST of each later level right after its pyramid level (side2); measured slower
     int desc_split = 1;                 // 1: quad-tree + descriptors of levels [0, fast_split) on the side stream (ORBGPU_DESC_SPLIT)
     orb_keypoint_t* d_st_kp = nullptr; size_t st_kp_cap = 0;   // their staging records (desc_split)
@@ -2223,6 +2224,11 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
             hipLaunchKernelGGL(k_describe, dim3(8 * share), dim3(256), 0, s2, e->d_geom, pyr, sel, scount, dst, lapc, cap,
                                kps, desc, counts, chunks, total, share, split, mode, skp, sdesc);
     };
+    // One chain (no side-stream split): FAST of levels [0, chain_s) and [chain_s, n) as two launches, each
+    // sizing its LDS for its own windows (the tall level-6/7 windows would otherwise set the level-0
+    // occupancy); chain_lds_split 1: both after the pyramid, 2: the first right after level chain_s - 1
+    const int chain_s = std::min(std::max(e->fast_split_cfg, 1), k.nlevels);
+    const int chain_lds_split = (n > 1 && chain_s < k.nlevels) ? e->chain_fast_split : 0;
     // the early levels' FAST (and with desc_split their quad-tree + descriptors) go to the side stream
     desc_split = e->desc_split && split > 0 && !e->fast_per_level && e->d_st_kp;
     const bool qts = (e->qt_split || desc_split) && split > 0 && !e->fast_per_level;
@@ -2287,7 +2293,9 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
                     l, cnt, (t1 - t0) * 0.01, life / cnt * 0.01, life / (double)(t1 - t0), ph[1] / cnt, ph[2] / cnt,
                     ph[3] / cnt);
         }
-        if (split && l == split - 1) {
+        if (!split && chain_lds_split == 2 && l == chain_s - 1) {
+            launch_fast(0, chain_s, st);  // one chain: the early levels' FAST right after their pyramid levels
+        } else if (split && l == split - 1) {
             hipEventRecord(e->split_ev[0], st);
             hipStreamWaitEvent(e->side, e->split_ev[0], 0);
             launch_fast(0, split, e->side);
@@ -2305,6 +2313,11 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     if (split && e->fast_per_level) {
         hipEventRecord(e->split_ev[2], e->side2);
         hipStreamWaitEvent(st, e->split_ev[2], 0);
+    } else if (!split && chain_lds_split == 1) {
+        launch_fast(0, chain_s, st);
+        launch_fast(chain_s, k.nlevels, st);
+    } else if (!split && chain_lds_split == 2) {
+        launch_fast(chain_s, k.nlevels, st);
     } else {
         launch_fast(split, k.nlevels, st);
     }
@@ -2384,6 +2397,7 @@ int orb_extractor_create(const orb_params_t* p, int max_width, int max_height, i
     if (const char* c = getenv("ORBGPU_STREAMS")) e->nstreams = std::min(Extractor::kMaxStreams, std::max(1, atoi(c)));
     if (const char* c = getenv("ORBGPU_FAST_SPLIT")) e->fast_split = atoi(c);
     e->fast_split_cfg = e->fast_split;
+    if (const char* c = getenv("ORBGPU_CHAIN_FAST")) e->chain_fast_split = atoi(c);
     bool ok = hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) == hipSuccess &&
               hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&e->side2, hipStreamNonBlocking) == hipSuccess;
