@@ -14,9 +14,9 @@ import sys
 
 STAGE_KERNELS = {"pyramid": ["k_pyramid_level"], "fast": ["k_fast_cells"], "quadtree": ["k_quadtree_kp"],
                  "describe": ["k_describe"]}
-# launches per step: 8 pyramid levels; FAST, quad-tree and describe one launch each (the bench's handles
+# launches per step: 8 pyramid levels; FAST two (levels 0-2, 3-7), quad-tree and describe one each (the bench's handles
 # run one chain per batch, orb_extractor_set_overlap(h, 0); with the side-stream overlap they are two)
-LAUNCHES = {"k_pyramid_level": 8, "k_fast_cells": 1, "k_quadtree_kp": 1, "k_describe": 1}
+LAUNCHES = {"k_pyramid_level": 8, "k_fast_cells": 2, "k_quadtree_kp": 1, "k_describe": 1}
 
 
 def main(d, out, frames=64):

@@ -11,7 +11,7 @@ timeout -k 10 400 python3 bench.py --launch-dump $O/launch_durations.json > $O/b
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o bench -- python3 bench.py $EX --launch-dump $O/stats_launch_durations.json > $O/stats_bench.json 2> $O/stats.log || { echo "stats failed"; exit 1; }
 # the last 20 steps' dispatches = bench.py's instrumented pass (the roofline's per-launch durations)
 : > $O/timed_kernel_avg.txt
-for kp in "k_pyramid_level 8" "k_fast_cells 1" "k_quadtree_kp 1" "k_describe 1"; do
+for kp in "k_pyramid_level 8" "k_fast_cells 2" "k_quadtree_kp 1" "k_describe 1"; do
   python3 tools/timed_kernel_avg.py $O/stats/bench_kernel_trace.csv 20 $kp >> $O/timed_kernel_avg.txt || exit 1
 done
 tools/pmc_run.sh $O/pmc "--steps 3 --warmup 1 $EX" || { echo "pmc failed"; exit 1; }
