@@ -190,7 +190,8 @@ int orb_matcher_destroy(orb_matcher_t m);
  * skipped.  best[p] receives the row (within the point) whose median distance to the point's rows
  * (index floor(0.5 (N - 1)) of the sorted row, self included) is the smallest, the first one on ties,
  * or -1 for a point without rows; out[32 p ..] receives that descriptor (mDescriptor), untouched for
- * an empty point (the reference returns early).  N < 65536 per point. */
+ * an empty point (the reference returns early).  N < 65536 per point: the host entry rejects a larger
+ * point with ORB_ERR_ARG; the device entry cannot see the offsets, so its caller keeps that limit. */
 /* Host arrays through the matcher handle's staging buffers, synchronous. */
 int orb_compute_distinctive_descriptors(orb_matcher_t m, const uint8_t* desc, const int32_t* offsets, int n_points,
                                         int32_t* best, uint8_t* out);

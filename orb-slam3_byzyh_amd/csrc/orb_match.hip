@@ -365,9 +365,11 @@ __global__ __launch_bounds__(64) void k_distinctive(const uint4* __restrict__ de
                                                     int n_points, int32_t* __restrict__ best,
                                                     uint4* __restrict__ out) {
     __shared__ uint16_t hist[kDdBins * 64];
-    const int p = blockIdx.x, lane = threadIdx.x;
+    const int lane = threadIdx.x;
+    // grid-stride over the points (a bounded grid: most points have <= 64 rows and are skipped here)
+    for (int p = blockIdx.x; p < n_points; p += gridDim.x) {
     const int o = off[p], N = off[p + 1] - o;
-    if (N <= kDdWaveMax) return;  // k_distinctive_wave (empty points included)
+    if (N <= kDdWaveMax) continue;  // k_distinctive_wave (empty points included)
     const int k = (int)(0.5 * (double)(N - 1));  // vDists[0.5*(N-1)]: the size_t index truncates
     unsigned long long bestkey = ~0ull;
     for (int i0 = 0; i0 < N; i0 += 64) {
@@ -395,7 +397,10 @@ __global__ __launch_bounds__(64) void k_distinctive(const uint4* __restrict__ de
     const int bi = (int)(bestkey & 0xffffffffu);
     if (lane == 0) best[p] = bi;
     if (lane < 2) out[2 * (size_t)p + lane] = desc[2 * (size_t)(o + bi) + lane];
+    __syncthreads();  // hist is reused by the next point
+    }
 }
+constexpr int kDdBigGrid = 512;  // k_distinctive blocks (grid-stride over the points)
 }  // namespace
 
 // Defined in orb_triangulation.hip: the matcher handle's staging buffers.
@@ -411,8 +416,9 @@ extern "C" int orb_compute_distinctive_descriptors_device(const uint8_t* d_desc,
         return orbgpu_fail(ORB_ERR_ARG, "descriptor arrays must be 16-byte aligned");
     hipLaunchKernelGGL(k_distinctive_wave, dim3(n_points), dim3(64), 0, (hipStream_t)stream, (const uint4*)d_desc,
                        d_offsets, n_points, d_best, (uint4*)d_out);
-    hipLaunchKernelGGL(k_distinctive, dim3(n_points), dim3(64), 0, (hipStream_t)stream, (const uint4*)d_desc, d_offsets,
-                       n_points, d_best, (uint4*)d_out);
+    // (points of more than 64 rows; the caller keeps every point below 65536 rows, the u16 histogram's range)
+    hipLaunchKernelGGL(k_distinctive, dim3(std::min(n_points, kDdBigGrid)), dim3(64), 0, (hipStream_t)stream,
+                       (const uint4*)d_desc, d_offsets, n_points, d_best, (uint4*)d_out);
     if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "distinctive descriptors launch failed");
     return ORB_OK;
 }
@@ -423,8 +429,10 @@ extern "C" int orb_compute_distinctive_descriptors(orb_matcher_t m, const uint8_
         return orbgpu_fail(ORB_ERR_ARG, "bad ComputeDistinctiveDescriptors arguments");
     if (n_points == 0) return ORB_OK;
     if (offsets[0] != 0) return orbgpu_fail(ORB_ERR_ARG, "offsets[0] must be 0");
-    for (int p = 0; p < n_points; ++p)
+    for (int p = 0; p < n_points; ++p) {
         if (offsets[p + 1] < offsets[p]) return orbgpu_fail(ORB_ERR_ARG, "offsets must be non-decreasing");
+        if (offsets[p + 1] - offsets[p] >= 65536) return orbgpu_fail(ORB_ERR_ARG, "a point has 65536 or more descriptors");
+    }
     const size_t nd = (size_t)offsets[n_points];
     if (nd && !desc) return orbgpu_fail(ORB_ERR_ARG, "null descriptors");
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -442,7 +450,7 @@ extern "C" int orb_compute_distinctive_descriptors(orb_matcher_t m, const uint8_
     if (ok) hipLaunchKernelGGL(k_distinctive_wave, dim3(n_points), dim3(64), 0, s, (const uint4*)(d + o_d),
                                (const int32_t*)(d + o_off), n_points, (int32_t*)(d + o_best), (uint4*)(d + o_out));
     if (ok && max_n > kDdWaveMax)  // points of more than 64 observations
-        hipLaunchKernelGGL(k_distinctive, dim3(n_points), dim3(64), 0, s, (const uint4*)(d + o_d),
+        hipLaunchKernelGGL(k_distinctive, dim3(std::min(n_points, kDdBigGrid)), dim3(64), 0, s, (const uint4*)(d + o_d),
                            (const int32_t*)(d + o_off), n_points, (int32_t*)(d + o_best), (uint4*)(d + o_out));
     ok = ok && hipGetLastError() == hipSuccess &&
          hipMemcpyAsync(h + o_best, d + o_best, total - o_best, hipMemcpyDeviceToHost, s) == hipSuccess &&

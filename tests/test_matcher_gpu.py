@@ -86,6 +86,33 @@ def test_invalid_views_rejected(pkg, scene):
         matcher.SearchForTriangulationMany(k1, [_variant(pkg, k2, keys_un=bad)], False, False)
 
 
+def test_distinctive_large_points_grid_stride(pkg, oracle):
+    """The large-point kernel walks the points with a bounded grid (512 blocks): points of more than 64
+    rows past index 512 and 1024 are still found, on both entries; a point of 65536 rows is rejected
+    by the host entry (its u16 histogram's range)."""
+    import torch
+    rng = np.random.default_rng(77)
+    sizes = list(rng.integers(0, 30, 1200))
+    for p, n in ((3, 90), (600, 150), (1030, 70), (1199, 65)):
+        sizes[p] = n
+    desc = rng.integers(0, 256, (int(sum(sizes)), 32), dtype=np.uint8)
+    offsets = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
+    ref = oracle.compute_distinctive_descriptors(desc, offsets)
+    m = pkg.ORBmatcher(0.6, False)
+    best, out = m.ComputeDistinctiveDescriptors(desc, offsets)
+    assert np.array_equal(best, ref)
+    dbest, dout = pkg.ORBmatcher.compute_distinctive_descriptors_device(torch.from_numpy(desc).cuda(),
+                                                                       torch.from_numpy(offsets).cuda())
+    assert np.array_equal(dbest.cpu().numpy(), ref)
+    big = np.array([0, 65536], np.int32)
+    bd = np.zeros((65536, 32), np.uint8)
+    b = np.zeros(1, np.int32)
+    o = np.zeros((1, 32), np.uint8)
+    rc = pkg._lib.load().orb_compute_distinctive_descriptors(m._handle(), bd.ctypes.data, big.ctypes.data, 1,
+                                                             b.ctypes.data, o.ctypes.data)
+    assert rc == pkg._lib.ORB_ERR_ARG
+
+
 @pytest.mark.parametrize("seed", [1, 2])
 def test_compute_distinctive_descriptors_parity(pkg, oracle, seed):
     """MapPoint::ComputeDistinctiveDescriptors batched: best row and mDescriptor equal the oracle for
