@@ -1935,6 +1935,7 @@ struct Extractor {
     int fast_split = 3;                 // FAST on levels [0, fast_split) overlaps the small pyramid levels
     int fast_split_cfg = 3;             // the configured split (orb_extractor_set_overlap(h, 0) sets fast_split 0)
     int chain_fast_split = 1;           // one-chain FAST launches (see launch_chunk; ORBGPU_CHAIN_FAST)
+    int qt_key_room = 4;                // KB of quad-tree LDS for keys beyond the node tables (ORBGPU_QT_KEYROOM)
     int fast_per_level = 0;             // 1: FAST of each later level right after its pyramid level (side2); measured slower
     int desc_split = 1;                 // 1: quad-tree + descriptors of levels [0, fast_split) on the side stream (ORBGPU_DESC_SPLIT)
     orb_keypoint_t* d_st_kp = nullptr; size_t st_kp_cap = 0;   // their staging records (desc_split)
@@ -2070,10 +2071,11 @@ int prepare(Extractor* e, int w, int h, int n) {
             const int lcap = g.k.lv[l].sel_cap + 64;
             meta = std::max(meta, (qt2_meta_bytes(lcap) + 15) & ~(size_t)15);
         }
-        // node tables + room for the keys of a typical level (6 B per key); levels with more keys use
+        // node tables + room for the keys of a small level (6 B per key); levels with more keys use
         // the global scratch.  Kept small: the quad-tree blocks are long-lived and latency-bound, and
-        // the LDS they do not hold lets another batch's FAST / pyramid / describe blocks share the CU.
-        const size_t want = meta + (size_t)12 * 1024;
+        // the LDS they do not hold lets another batch's FAST / pyramid / describe blocks share the CU
+        // (round 4, 3 batches in flight: 32 KB 313-315k, 12 KB 318-320k, 4 KB 322-326k features/ms).
+        const size_t want = meta + (size_t)e->qt_key_room * 1024;
         if (meta > 160 * 1024) return orbgpu_fail(ORB_ERR_ARG, "nfeatures too large for the quad-tree LDS budget");
         e->qt_lds = (int)std::min<size_t>(want, 160 * 1024);
         // the attribute is per function (shared by every handle): allow the whole LDS, each launch
@@ -2398,6 +2400,7 @@ int orb_extractor_create(const orb_params_t* p, int max_width, int max_height, i
     if (const char* c = getenv("ORBGPU_FAST_SPLIT")) e->fast_split = atoi(c);
     e->fast_split_cfg = e->fast_split;
     if (const char* c = getenv("ORBGPU_CHAIN_FAST")) e->chain_fast_split = atoi(c);
+    if (const char* c = getenv("ORBGPU_QT_KEYROOM")) e->qt_key_room = std::max(0, atoi(c));
     bool ok = hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) == hipSuccess &&
               hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&e->side2, hipStreamNonBlocking) == hipSuccess;
