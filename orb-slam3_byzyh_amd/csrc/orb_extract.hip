@@ -1225,7 +1225,7 @@ __device__ void qt2_careful(QT2& T, const QGen& A, QGen& B, const int32_t* cA, i
     } else if (!(reg_sort && np <= 64 && !(debug_flags & 16) && qt_sort_reg(t, A, np, lane))) {
         qt_sort(t, A, np, lane);  // > 64 candidates, depth-limit fallback, or forced (flag 16)
     }
-    if (debug_flags & 4) { const unsigned long long now = __builtin_amdgcn_s_memtime(); tm[4] += now - t_last; t_last = now; }
+    if (tm) { const unsigned long long now = __builtin_amdgcn_s_memtime(); tm[4] += now - t_last; t_last = now; }
     // division order o = 0.. is prev[np-1-o]; stop once the list reaches N (src:1006)
     int ndiv = np, carry = 0;
     for (int b = 0; b < np; b += 64) {
@@ -1339,10 +1339,13 @@ __device__ void qt2_run(QT2& T, uint32_t* keys, uint16_t* node, int K, int N, in
     int* ctrl = T.ctrl;
     // phase timers of thread 0 (debug_flags & 4): gather, roots, regular node, regular key, sort,
     // careful node, careful key, final, -, #regular passes, #careful rounds, K
-    unsigned long long tm[kQtStamps] = {};
-    unsigned long long t_last = (debug_flags & 4) ? __builtin_amdgcn_s_memtime() : 0;
+    // (accumulated in the stamps record itself, by thread 0 only: no register state in normal runs)
+    unsigned long long* tm = ((debug_flags & 4) && stamps && tid == 0) ? stamps : nullptr;
+    if (tm)
+        for (int i = 0; i < kQtStamps; ++i) tm[i] = 0;
+    unsigned long long t_last = tm ? __builtin_amdgcn_s_memtime() : 0;
     auto stamp = [&](int i) {
-        if (debug_flags & 4) { const unsigned long long now = __builtin_amdgcn_s_memtime(); tm[i] += now - t_last; t_last = now; }
+        if (tm) { const unsigned long long now = __builtin_amdgcn_s_memtime(); tm[i] += now - t_last; t_last = now; }
     };
     // ---- gather (src:756-764): cells in chunks of 256, wave w owns 64 of them; a wave scan of the
     // counts gives each cell's start, the wave's keys are spread over its lanes, each finding its
@@ -1469,13 +1472,13 @@ __device__ void qt2_run(QT2& T, uint32_t* keys, uint16_t* node, int K, int N, in
                 // src:932: the next regular pass would overshoot N -> careful rounds
                 if (!fin && !ovf && new_size + nsplit * 3 > N) careful = true;
                 stamp(2);
-                tm[9]++;
+                if (tm) tm[9]++;
             } else {
-                tm[8] += (unsigned long long)nsplit << (16 * min((int)tm[10], 3));  // candidates per round (debug)
+                if (tm) tm[8] += (unsigned long long)nsplit << (16 * min((int)tm[10], 3));  // candidates per round (debug)
                 qt2_careful(T, A, B, cA, cB, sB, nlist, nsplit, N, lane, debug_flags, K < (1 << 20), new_size, nsplit, fin, ovf, tm,
                             t_last);
                 stamp(5);
-                tm[10]++;
+                if (tm) tm[10]++;
             }
             nlist = new_size;
             if (lane == 0) { ctrl[0] = fin; ctrl[1] = ovf; }
@@ -1539,10 +1542,7 @@ __device__ void qt2_run(QT2& T, uint32_t* keys, uint16_t* node, int K, int N, in
     }
     if (lane == 0) { *n_sel = nlist; *place.n_lap = carry_lap; }
     stamp(7);
-    if ((debug_flags & 4) && stamps && lane == 0) {
-        tm[11] = (unsigned long long)K;
-        for (int i = 0; i < kQtStamps; ++i) stamps[i] = tm[i];
-    }
+    if (tm) tm[11] = (unsigned long long)K;
 }
 
 __global__ __launch_bounds__(kQtThreads) void k_quadtree_kp(
