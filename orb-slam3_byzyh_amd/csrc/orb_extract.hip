@@ -1062,9 +1062,21 @@ struct QT2 {
 };
 
 __host__ __device__ inline size_t qt2_meta_bytes(int lcap) {
-    // u64: sel_el, sel_tmp, cmap; 32-bit: cnt x2, sxy x2, kn x2, best; u16: 2 x (x0 y0 x1 y1), split,
-    // prev, posA, posB, bend; u8: 2 x leaf, divided
-    return (size_t)lcap * (24 + 32 + 8 + 8 + 4 + 16 + 10 + 3) + kOrbSortStack * 12 + kQtCtrl * 4 + 64;
+    // u64: cmap; 32-bit: cnt x2, sxy x2, kn x2, best; u16: 2 x (x0 y0 x1 y1), split, prev; u8: 2 x leaf,
+    // divided.  The sort's arrays (sel_el, sel_tmp: u64; posA, posB, bend: u16) live in the next
+    // generation's counts and in cmap, which no careful round uses until its sort is done (qt2_careful)
+    return (size_t)lcap * (8 + 32 + 8 + 8 + 4 + 16 + 4 + 3) + kOrbSortStack * 12 + kQtCtrl * 4 + 64;
+}
+
+// The sort's workspace over a counts array that is free while a careful round sorts (16 B per entry:
+// sel_el, sel_tmp) and over cmap (8 B per entry: posA, posB, bend)
+__device__ __forceinline__ void qt2_sort_space(QT2& T, int32_t* free_cnt) {
+    QTree& t = T.t;
+    t.sel_el = reinterpret_cast<unsigned long long*>(free_cnt);
+    t.sel_tmp = t.sel_el + t.lcap;
+    t.posA = reinterpret_cast<uint16_t*>(T.cmap);
+    t.posB = t.posA + t.lcap;
+    t.bend = t.posB + t.lcap;
 }
 
 __device__ inline void qt2_carve(QT2& T, uint8_t* p, int lcap) {
@@ -1072,8 +1084,6 @@ __device__ inline void qt2_carve(QT2& T, uint8_t* p, int lcap) {
     t.lcap = lcap;
     T.ctrl = (int*)p; p += kQtCtrl * 4;
     t.sort_ws = (int*)p; p += kOrbSortStack * 12;
-    t.sel_el = (unsigned long long*)p; p += 8 * lcap;
-    t.sel_tmp = (unsigned long long*)p; p += 8 * lcap;
     T.cmap = (unsigned long long*)p; p += 8 * lcap;
     QGen* gens[2] = {&t.g0, &t.g1};
 #pragma unroll
@@ -1092,14 +1102,12 @@ __device__ inline void qt2_carve(QT2& T, uint8_t* p, int lcap) {
     }
     t.split = (uint16_t*)p; p += 2 * lcap;
     t.prev = (uint16_t*)p; p += 2 * lcap;
-    t.posA = (uint16_t*)p; p += 2 * lcap;
-    t.posB = (uint16_t*)p; p += 2 * lcap;
-    t.bend = (uint16_t*)p; p += 2 * lcap;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
         gens[g]->leaf = p; p += lcap;
     }
     t.divided = p;
+    qt2_sort_space(T, T.cnt[1]);
 }
 
 __device__ __forceinline__ uint32_t qt2_split_word(int x0, int y0, int x1, int y1) {
@@ -1210,6 +1218,7 @@ __device__ void qt2_careful(QT2& T, const QGen& A, QGen& B, const int32_t* cA, i
                             unsigned long long* tm, unsigned long long& t_last) {
     QTree& t = T.t;
     const int lcap = t.lcap;
+    qt2_sort_space(T, cB);  // cB and cmap are rewritten only after the sort (qt2_write_child / qt2_copy_node)
     for (int i = lane; i < np; i += 64) t.prev[i] = t.split[i];
     wave_sync();
     if (debug_flags & 2) {  // reference single-lane port (A/B check)
