@@ -108,12 +108,33 @@ __device__ __forceinline__ double xchg(double v) {
 // hold the same value set before each step (they agree in every lane bit above M).
 template <int C, int M>
 __device__ __forceinline__ void tb_step(double (&v)[32], int lane) {
-    const bool up = (lane & M) != 0;
+    if constexpr (M == 32 || M == 16) {
+        // v_permlane32_swap / v_permlane16_swap (gfx950): the upper half-wave (odd 16-lane row) of
+        // v[i] trades places with the lower half (even row) of v[i + C], so each lane then holds its
+        // kept value in one register and its partner's sent value in the other: one add, no LDS
+        // (the sum is keep + recv in either order, the same double)
 #pragma unroll
-    for (int i = 0; i < C; ++i) {
-        const double send = up ? v[i] : v[i + C];
-        const double keep = up ? v[i + C] : v[i];
-        v[i] = keep + xchg<M>(send);
+        for (int i = 0; i < C; ++i) {
+            int2 a = __builtin_bit_cast(int2, v[i]), b = __builtin_bit_cast(int2, v[i + C]);
+            if constexpr (M == 32) {
+                const auto rx = __builtin_amdgcn_permlane32_swap(a.x, b.x, false, false);
+                const auto ry = __builtin_amdgcn_permlane32_swap(a.y, b.y, false, false);
+                a.x = rx[0]; b.x = rx[1]; a.y = ry[0]; b.y = ry[1];
+            } else {
+                const auto rx = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+                const auto ry = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+                a.x = rx[0]; b.x = rx[1]; a.y = ry[0]; b.y = ry[1];
+            }
+            v[i] = __builtin_bit_cast(double, a) + __builtin_bit_cast(double, b);
+        }
+    } else {
+        const bool up = (lane & M) != 0;
+#pragma unroll
+        for (int i = 0; i < C; ++i) {
+            const double send = up ? v[i] : v[i + C];
+            const double keep = up ? v[i + C] : v[i];
+            v[i] = keep + xchg<M>(send);
+        }
     }
 }
 // Wave sums of 32 per-lane doubles in 32 exchanges (16 + 8 + 4 + 2 + 1, then the pair) instead of
