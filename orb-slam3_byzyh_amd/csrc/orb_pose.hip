@@ -35,9 +35,13 @@
 
 namespace {
 
-constexpr int kPT = 256;               // threads per frame
+#ifndef ORB_POSE_THREADS
+#define ORB_POSE_THREADS 256
+#endif
+constexpr int kPT = ORB_POSE_THREADS;  // threads per frame
 constexpr int kPW = kPT / 64;          // waves
-constexpr int kEdgeSlots = 2;          // edges per thread kept in registers (512 per frame)
+constexpr int kEdgeSlots = 512 / kPT;  // edges per thread kept in registers (512 per frame)
+static_assert(kPT % 64 == 0 && kEdgeSlots >= 1 && kPW <= 32, "pose workgroup shape");
 
 static_assert(sizeof(orb_pose_edge_t) == 56, "pose edge layout");
 
@@ -417,7 +421,8 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
         __syncthreads();
         if (tid < 64) {
             const int k = (tid >> 1) & 31;
-            acc[0] = ((acc[0] + part[32 + k]) + part[64 + k]) + part[96 + k];
+#pragma unroll
+            for (int w = 1; w < kPW; ++w) acc[0] += part[32 * w + k];  // the waves in order
         }
     };
     auto solve = [&](LmState& S) {  // thread 0: the damped system, the trial pose into T
@@ -542,7 +547,10 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
             const double wb = wave_sum_d((double)bad);
             if ((tid & 63) == 0) part[tid >> 6] = wb;
             __syncthreads();
-            nBad = (int)(((part[0] + part[1]) + part[2]) + part[3]);
+            double nb = part[0];
+#pragma unroll
+            for (int w = 1; w < kPW; ++w) nb += part[w];
+            nBad = (int)nb;
             __syncthreads();  // part is rewritten by the next round
         }
         if (round == 2) robust = false;
