@@ -154,13 +154,6 @@ __device__ __forceinline__ void wave_partials32(double (&v)[32], double* part) {
     v[0] += xchg<1>(v[0]);
     if (!(lane & 1)) part[wv * 32 + (lane >> 1)] = v[0];
 }
-__device__ __forceinline__ double readlane_d(double v, int l) {
-    const int2 h = __builtin_bit_cast(int2, v);
-    int2 r;
-    r.x = __builtin_amdgcn_readlane(h.x, l);
-    r.y = __builtin_amdgcn_readlane(h.y, l);
-    return __builtin_bit_cast(double, r);
-}
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -357,6 +350,7 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
                                                   double* __restrict__ pose_out, uint8_t* __restrict__ level,
                                                   int32_t* __restrict__ inliers, double* __restrict__ echi2, Huber2 hub) {
     __shared__ double part[kPW * 32];
+    __shared__ double tot[28];
     __shared__ double T[7];
     __shared__ int s_state;  // 1: evaluate the trial pose in T, 2: the round's optimize() is done
     const int tid = threadIdx.x, f = blockIdx.x;
@@ -425,6 +419,18 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
             for (int w = 1; w < kPW; ++w) acc[0] += part[32 * w + k];  // the waves in order
         }
     };
+    // the 28 workgroup totals to thread 0: wave 0's lane 2k holds total k; they go through LDS (one
+    // store, thread 0's loads issued together) instead of 56 v_readlane in every lane of wave 0
+    auto totals = [&](const double (&acc)[32], double (&t)[28]) {
+        if (tid < 56 && !(tid & 1)) tot[tid >> 1] = acc[0];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (tid == 0) {
+#pragma unroll
+            for (int k = 0; k < 28; ++k) t[k] = tot[k];
+        }
+    };
     auto solve = [&](LmState& S) {  // thread 0: the damped system, the trial pose into T
         for (int i = 0; i < 7; ++i) S.Tb[i] = T[i];
         S.ok = ldlt6(S.H, S.lambda, S.b, S.x);
@@ -450,10 +456,7 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
             double acc[32];
             pass(robust, false, acc);  // computeActiveErrors + buildSystem at the round's start pose
             double t[28];
-            if (tid < 64) {
-#pragma unroll
-                for (int k = 0; k < 28; ++k) t[k] = readlane_d(acc[0], 2 * k);
-            }
+            totals(acc, t);
             if (tid == 0) {
 #pragma unroll
                 for (int k = 0; k < 21; ++k) S.H[k] = t[k];
@@ -476,10 +479,7 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
                 // evaluate (and linearise) at the trial pose; every active edge's chi2 is kept, since
                 // g2o classifies on the last evaluated state even when it was rejected
                 pass(robust, true, acc);
-                if (tid < 64) {
-#pragma unroll
-                    for (int k = 0; k < 28; ++k) t[k] = readlane_d(acc[0], 2 * k);
-                }
+                totals(acc, t);
                 if (tid == 0) {
                     double tempChi = t[27];
                     if (!S.ok) tempChi = DBL_MAX;
