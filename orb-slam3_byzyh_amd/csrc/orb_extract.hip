@@ -122,6 +122,14 @@ __device__ __forceinline__ int wave_sum(int v) {
     return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
            __builtin_amdgcn_readlane(v, 48);
 }
+// Sum over each 16-lane row, in every lane of the row (DPP only)
+__device__ __forceinline__ int row16_isum(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false);  // row_ror:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    return v;
+}
 // Inclusive wave scans (GFX9 DPP): row_shr 1/2/3 on the input, row_shr 4 / 8 under bank masks, then
 // row_bcast 15 / 31 across the rows.
 __device__ __forceinline__ int wave_incl_scan_dpp(int v) {
@@ -1733,12 +1741,11 @@ __global__ __launch_bounds__(256) void k_describe(const KernelGeom* __restrict__
 #pragma unroll
     for (int e = 0; e < kExcPerLane; ++e) exc[e] = 32 * e + hl < kNumSincosExc ? c_sincos_exc[32 * e + hl][0] : 0u;
     int total = cnt_l, lap_before = li < level ? lap_l : 0, mono_before = li < level ? cnt_l - lap_l : 0;
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) {  // within each 16-lane group
-        total += __shfl_xor(total, o, 64);
-        lap_before += __shfl_xor(lap_before, o, 64);
-        mono_before += __shfl_xor(mono_before, o, 64);
-    }
+    // sums within each 16-lane row, in every lane of it: DPP (xor 1, xor 2, row_ror 4, 8) instead of
+    // four dependent ds_bpermute round trips per value
+    total = row16_isum(total);
+    lap_before = row16_isum(lap_before);
+    mono_before = row16_isum(mono_before);
     // Split mode (levels [0, stage_levels) described early, on the side stream, before the later
     // levels' quad-tree exists): stage_mode 1 computes them into per-slot staging records (the output
     // slot needs every level's count); the final launch (stage_mode 2) moves them to their slots.
