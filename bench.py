@@ -944,8 +944,7 @@ def bench_c4_strong(pkg, synth, world, rank, dev, steps, in_flight=3, n_global=2
             step = lambda i: sh.step(imgs, (0, 1000), stream=sts[i % H])  # noqa: E731
 
             def fin():
-                g = sh.finish()  # the last step's gather, matched like the others
-                match_gathered(g[1], g[2], sh.pairs)
+                sh.finish()  # the last step's gather, matched like the others (inside finish)
             counts = lambda: sh.local.counts[0]  # noqa: E731
             match_once = lambda: match_gathered(sh.local.desc[0], sh.local.counts[0],  # noqa: E731
                                                 frame_pairs(0, count, count).to(dev))

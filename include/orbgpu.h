@@ -239,7 +239,10 @@ typedef struct orb_kf_device {
  * asynchronous on `stream`: the neighbours of one new keyframe (pair_kf1 = NULL: every pair uses
  * kf1s[0]), or of several queued keyframes.  With C = max over kf1s of cap:
  * d_matches12[p * C + i] = index in kf2s[p] or -1 (i < C); d_n_matches[p] = the count.  The pair
- * geometry and F12 are uploaded from the host (a few hundred bytes per pair). */
+ * geometry and F12 are uploaded from the host (a few hundred bytes per pair).  Counts are clamped to
+ * cap; a keyframe whose *n is negative or above cap, or whose *n_nodes is negative (a frame the
+ * extractor flagged ORB_ERR_CAPACITY, which the BoW transform passes on), gets no matches and its
+ * pairs report d_n_matches[p] = ORB_ERR_CAPACITY. */
 int orb_search_for_triangulation_device(orb_matcher_t m, const orb_kf_device_t* kf1s, int n_kf1,
                                         const orb_kf_device_t* kf2s, const int32_t* pair_kf1,
                                         const orb_kf_pair_geom_t* geoms, int n_pairs, int only_stereo, int coarse,
@@ -406,7 +409,9 @@ int orb_bow_transform_batch_device(orb_vocabulary_t v, const uint8_t* d_desc, co
 /* The same on the frames as orb_extract_batch_device leaves them: frame f's descriptors at
  * d_desc[f * cap * 32 ..], its count at d_kp_counts[2 f] (<= cap, <= 8192).  Per frame f the outputs
  * start at f * cap in every array (fv_begin at f * (cap + 1)); d_counts[2 f] = n_words,
- * d_counts[2 f + 1] = n_nodes.  Async on `stream`. */
+ * d_counts[2 f + 1] = n_nodes.  A frame the extractor flagged (d_kp_counts[2 f + 1] ==
+ * ORB_ERR_CAPACITY, or a count outside [0, cap]) is not read: both its counts are ORB_ERR_CAPACITY.
+ * Async on `stream`. */
 int orb_bow_transform_frames_device(orb_vocabulary_t v, const uint8_t* d_desc, const int32_t* d_kp_counts, int n_frames,
                                     int cap, int levelsup, int32_t* d_bow_word, double* d_bow_value, int32_t* d_fv_node,
                                     int32_t* d_fv_begin, int32_t* d_fv_feat, int32_t* d_counts, void* stream);

@@ -134,6 +134,8 @@ DEBUG_PROTOTYPES = {
     "orb_extractor_stage_ms": (_i, [_vp, _fp, _ip, ctypes.POINTER(ctypes.c_longlong)]),
     "orb_extractor_pyramid_launch_ms": (_i, [_vp, _fp, _ip]),
     "orb_extractor_launch_durations": (_i, [_vp, _i, _fp, _i, _ip]),
+    "orb_debug_ba_chol_timeout": (_i, [_i, _i]),
+    "orb_debug_ba_chol_timeout_status": (_i, [_ip]),
 }
 
 STAGES = ("pyramid", "fast", "quadtree", "place", "describe")

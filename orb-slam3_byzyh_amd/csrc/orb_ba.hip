@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cfloat>
 #include <cmath>
@@ -1135,8 +1136,8 @@ __device__ __forceinline__ void st_agent(double* p, double v) {
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 // one wave polls one flag word until it holds `epoch` (or later); false after ~4 s
-__device__ __forceinline__ bool flag_wait_agent(const unsigned* f, unsigned epoch) {
-    for (int spin = 0; spin < (1 << 22); ++spin) {
+__device__ __forceinline__ bool flag_wait_agent(const unsigned* f, unsigned epoch, int limit = 1 << 22) {
+    for (int spin = 0; spin < limit; ++spin) {
         if (__hip_atomic_load((ba_gu32*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= epoch) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the payload loads below the poll
             return true;
@@ -1149,6 +1150,13 @@ __device__ __forceinline__ void flag_publish_agent(unsigned* f, unsigned epoch, 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 payload stores have landed
     if (lane == 0) __hip_atomic_store((ba_gu32*)f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+// Forced-timeout hook (orb_debug_ba_chol_timeout, tests/test_ba_gpu.py): one row's first flag wait
+// asks for a later epoch, so it times out and the launch must fail with status 6 (another row's
+// timeout) while the next launch, at its own epoch, is clean.  One-shot: the armed row clears it.
+__device__ int g_dbg_chol_row = -1;
+__device__ unsigned g_dbg_chol_epoch = 0;
+__device__ int g_dbg_chol_status = -1;
 
 template <bool kLdsRow>
 __global__ __launch_bounds__(kRowThreads) void k_ba_chol_rows(int n, const double* __restrict__ S,
@@ -1172,7 +1180,16 @@ __global__ __launch_bounds__(kRowThreads) void k_ba_chol_rows(int n, const doubl
     __shared__ int fail;
     unsigned* flags = cflag + 4;  // [row][col]: tile (row, col) published at this epoch
     const unsigned E = cflag[0] + 1;
-    if (tid == 0) fail = 0;
+    __shared__ unsigned dbg_bump;
+    if (tid == 0) {
+        fail = 0;
+        dbg_bump = 0;
+        if (__hip_atomic_load((ba_gu32*)&g_dbg_chol_row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == i &&
+            atomicCAS(&g_dbg_chol_row, i, -1) == i) {
+            dbg_bump = 1000;
+            __hip_atomic_store((ba_gu32*)&g_dbg_chol_epoch, E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
     for (int t = tid; t < (i + 1) * 256; t += kRowThreads) {  // S upper triangle read as S[col blk][row blk]
         const int j = t >> 8, e = t & 255, q = e >> 6, l = e & 63;
         const int row = 16 * j + (l >> 4) + 4 * q, col = 16 * i + (l & 15);
@@ -1183,7 +1200,10 @@ __global__ __launch_bounds__(kRowThreads) void k_ba_chol_rows(int n, const doubl
     __syncthreads();
     for (int m = 0; m < i; ++m) {
         if (w == 0) {  // panel tile (i, m) and the forward step
-            if (!flag_wait_agent(flags + m * NT + m, E) && lane == 0) fail = 4;
+            // (the armed debug wait gives up after ~4k polls, long before any other row's bound)
+            if (!flag_wait_agent(flags + m * NT + m, E + (m == 0 ? dbg_bump : 0u),
+                                 m == 0 && dbg_bump ? 1 << 12 : 1 << 22) && lane == 0)
+                fail = 4;
             const double* lp = lpub + ((size_t)m * NT + m) * 256;
             double lq[4], yq[4];
 #pragma unroll
@@ -1285,6 +1305,8 @@ __global__ __launch_bounds__(kRowThreads) void k_ba_chol_rows(int n, const doubl
     if (tid == 0) {
         const unsigned timeouts = __hip_atomic_load((ba_gu32*)(cflag + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *status = fail ? fail : (timeouts == E ? 6 : 0);
+        if (__hip_atomic_load((ba_gu32*)&g_dbg_chol_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == E)
+            __hip_atomic_store(&g_dbg_chol_status, *status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         cflag[0] = E;  // every row read the epoch before publishing, and this row consumed all of them
     }
 }
@@ -1911,6 +1933,10 @@ unsigned grid(size_t n, int t = kT) { return (unsigned)std::max<size_t>(1, (n + 
 
 }  // namespace
 
+namespace {
+std::atomic<bool> g_force_rows{false};  // orb_debug_ba_chol_timeout(force_rows, ...)
+}
+
 extern "C" {
 
 int orb_ba_create(orb_ba_t* out) {
@@ -2075,6 +2101,28 @@ static bool stop_requested(const orb_ba_options_t* opt) {
     return (opt->stop_flag && *opt->stop_flag) || (opt->stop_flag_bool && *opt->stop_flag_bool);
 }
 
+// Debug hook (not in the public header): force_rows selects k_ba_chol_rows for every n; row >= 0 arms
+// the forced timeout of that tile row's first wait in the next k_ba_chol_rows launch.  Synchronous.
+int orb_debug_ba_chol_timeout(int force_rows, int row) {
+    g_force_rows.store(force_rows != 0, std::memory_order_relaxed);
+    const int none = -1;
+    const unsigned zero = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_chol_row), &row, sizeof(int)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_chol_epoch), &zero, sizeof(unsigned)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_chol_status), &none, sizeof(int)) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "debug symbol copy");
+    return ORB_OK;
+}
+
+// The status the armed launch ended with (-1: no armed launch has finished).  Synchronous.
+int orb_debug_ba_chol_timeout_status(int32_t* status) {
+    if (!status) return orbgpu_fail(ORB_ERR_ARG, "null status");
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpyFromSymbol(status, HIP_SYMBOL(g_dbg_chol_status), sizeof(int32_t)) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "debug symbol read");
+    return ORB_OK;
+}
+
 int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* opt, double* edge_chi2,
                     uint8_t* edge_depth_ok, orb_ba_result_t* res) {
     orbgpu::StageTimer timer("LBA");  // vdLBA_ms (src/LocalMapping.cc:213-230)
@@ -2229,7 +2277,8 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         return orbgpu_fail(ORB_ERR_ARG, "more than 682 free keyframes in the local window");
     }
     static const char* chol_env = getenv("ORBGPU_BA_CHOL");
-    const bool use_rows = n > 0 && (n > 16 * kMfMaxNT || (chol_env && !strcmp(chol_env, "rows")));
+    const bool use_rows = n > 0 && (n > 16 * kMfMaxNT || (chol_env && !strcmp(chol_env, "rows")) ||
+                                    g_force_rows.load(std::memory_order_relaxed));
     const bool rows_lds = NT <= kRowLdsMaxNT;
     const size_t rows_lds_bytes =
         sizeof(double) * ((rows_lds ? (size_t)NT * 256 : 0) + 272 + 256 + 16 + 16 * (size_t)NT);

@@ -57,7 +57,10 @@ __global__ __launch_bounds__(256) void k_bow_descend(const int32_t* __restrict__
                                                      int cap) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    if (kp_counts && i % cap >= kp_counts[2 * (i / cap)]) return;  // frames at stride cap: past the count
+    if (kp_counts) {  // frames at stride cap: past the count, or a frame the extractor could not place
+        const int fr = i / cap, c = kp_counts[2 * fr];
+        if (kp_counts[2 * fr + 1] == ORB_ERR_CAPACITY || c < 0 || c > cap || i % cap >= c) return;
+    }
     const uint4* fp = reinterpret_cast<const uint4*>(feat + 32 * (size_t)i);
     const uint4 a0 = fp[0], a1 = fp[1];
     const uint4* D = reinterpret_cast<const uint4*>(vdesc);
@@ -189,7 +192,11 @@ __global__ __launch_bounds__(kAggThreads) void k_bow_aggregate(
     const int base = kp_counts ? f * cap : frame_begin[f];
     const int n = kp_counts ? kp_counts[2 * f] : frame_begin[f + 1] - base;
     double* vals = reinterpret_cast<double*>(keys + kMaxFrameFeatures);
-    if (n > kMaxFrameFeatures) {
+    // A frame over the extractor's capacity has no features in its slice (orb_extract_batch_device flags
+    // it with ORB_ERR_CAPACITY and still reports the needed count): it fails here too, and the
+    // triangulation skips it by its negative n_nodes.
+    const bool failed = kp_counts && (kp_counts[2 * f + 1] == ORB_ERR_CAPACITY || n < 0 || n > cap);
+    if (failed || n > kMaxFrameFeatures) {
         if (tid == 0) counts[2 * f] = counts[2 * f + 1] = ORB_ERR_CAPACITY;
         return;
     }

@@ -71,6 +71,7 @@ struct PackedSrc {
     const int32_t* fidx;
     __device__ int n(int k) const { return kfs[k].n; }
     __device__ int n_nodes(int k) const { return kfs[k].n_nodes; }
+    __device__ bool failed(int) const { return false; }  // validated on the host
     __device__ uint32_t node(int k, int i) const { return nodes[kfs[k].node_off + i]; }
     __device__ int node_begin(int k, int i) const { return csr[kfs[k].csr_off + i]; }
     __device__ int feat(int k, int j) const { return fidx[j]; }
@@ -98,8 +99,14 @@ struct KfPtrs {
 };
 struct DirectSrc {
     const KfPtrs* kfs;
-    __device__ int n(int k) const { return *kfs[k].n; }
-    __device__ int n_nodes(int k) const { return *kfs[k].n_nodes; }
+    // The counts are the producers' device outputs: clamped to the keyframe's capacity, and a keyframe
+    // the extractor or the BoW transform flagged (count above cap, negative FeatureVector size) fails.
+    __device__ bool failed(int k) const {
+        const int c = *kfs[k].n, nn = *kfs[k].n_nodes;
+        return c < 0 || c > kfs[k].cap || nn < 0 || nn > kfs[k].cap;
+    }
+    __device__ int n(int k) const { return min(max(*kfs[k].n, 0), kfs[k].cap); }
+    __device__ int n_nodes(int k) const { return min(max(*kfs[k].n_nodes, 0), kfs[k].cap); }
     __device__ uint32_t node(int k, int i) const { return (uint32_t)kfs[k].fv_node[i]; }
     __device__ int node_begin(int k, int i) const { return kfs[k].fv_begin[i]; }
     __device__ int feat(int k, int j) const { return kfs[k].fv_feat[j]; }
@@ -129,7 +136,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_tri_match(Src src, const PairDe
     const int node1 = blockIdx.x * kWaves + (threadIdx.x >> 6);
     const int p = blockIdx.y;
     const int K1 = k1of ? k1of[p] : 0, K2 = k2base + p;
-    if (node1 >= src.n_nodes(K1)) return;
+    if (node1 >= src.n_nodes(K1) || src.failed(K1) || src.failed(K2)) return;
     const int nn2 = src.n_nodes(K2);
     // the shared-node walk of src:1112-1287 visits exactly the node ids present in both maps
     const uint32_t id = src.node(K1, node1);
@@ -209,6 +216,10 @@ __global__ __launch_bounds__(256) void k_tri_finish(Src src, const int32_t* __re
     __shared__ int total;
     const int p = blockIdx.x;
     const int K1 = k1of ? k1of[p] : 0, K2 = k2base + p;
+    if (src.failed(K1) || src.failed(K2)) {  // no matches (the rows stay -1), the pair reports the failure
+        if (threadIdx.x == 0) counts[p] = ORB_ERR_CAPACITY;
+        return;
+    }
     const int n1 = src.n(K1);
     int32_t* m = matches + (size_t)p * mstride;
     if (threadIdx.x < kHistoLength) hist[threadIdx.x] = 0;

@@ -81,7 +81,10 @@ class ShardedExtractor:
         self._i = 0
         self._pending = None
         self.match = match
-        self.matches = None  # (idx, best, second) [frames_per_rank, cap] of the last gathered step
+        # (idx, best, second) [frames_per_rank, cap] of the latest gathered step: inside step() that is
+        # the previous step's gather, after finish() the last one.  The tensors cycle through nbuf
+        # buffers, so a result is overwritten nbuf steps later: copy it to keep it.
+        self.matches = None
         if match:
             first = self.rank * frames_per_rank  # equal shards: global frame f sits at row f of the gather
             self.pairs = frame_pairs(first, frames_per_rank, self.world * frames_per_rank).to(dev)
@@ -95,10 +98,8 @@ class ShardedExtractor:
         out = self.local.view(buf)
         self.exs[self._i % len(self.exs)].extract_batch_device(images, vLappingArea, cap=self.cap, out=out,
                                                                stream=stream)
-        prev = self.finish(stream)
-        if self.match and prev is not None:
-            self.matches = match_gathered(prev[1], prev[2], self.pairs, stream=stream,
-                                          out=self._mbuf[(self._i - 1) % self.nbuf])
+        prev = self._wait(stream)
+        self._match(prev, stream)
         # RCCL orders a collective after torch's CURRENT stream only: issue it with the extraction
         # stream current, so it cannot read the blocks before the extraction has written them
         with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
@@ -106,9 +107,19 @@ class ShardedExtractor:
         self._i += 1
         return prev
 
+    def _match(self, gathered, stream):
+        if self.match and gathered is not None:  # the gather of step self._i - 1
+            self.matches = match_gathered(gathered[1], gathered[2], self.pairs, stream=stream,
+                                          out=self._mbuf[(self._i - 1) % self.nbuf])
+
     def finish(self, stream=None):
         """Make `stream` (default: the current stream) wait for the in-flight all-gather and return
-        its (kps, desc, counts)."""
+        its (kps, desc, counts); with match=True the last step's gather is matched too (self.matches)."""
+        gathered = self._wait(stream)
+        self._match(gathered, stream)
+        return gathered
+
+    def _wait(self, stream=None):
         if self._pending is None:
             return None
         g_kps, g_desc, g_cnt, works = self._pending

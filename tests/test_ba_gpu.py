@@ -95,3 +95,27 @@ def test_local_ba_repeated_edge_rejected(pkg, synth, solver):
         solver.optimize(dup, 5)
     _, _, _, _, res = solver.optimize(prob, 5)
     assert res["iterations"] > 0
+
+
+def test_chol_rows_forced_timeout_fails_one_solve_only(pkg, oracle, synth):
+    """a flag wait of the tile-row Cholesky (k_ba_chol_rows) that times out fails
+    that launch with status 6 (the last row reads the timeout tagged with its own epoch), and the next
+    solve, at a fresh epoch, is clean: the same LM path and poses as the oracle."""
+    import ctypes
+    lib = pkg._lib.load()
+    prob = synth.local_ba_problem(n_kf=8, n_points=200, obs_per_point=4, n_fixed=1, seed=5)  # n = 42: 3 tile rows
+    solver = pkg.LocalBA()
+    st = ctypes.c_int32(0)
+    try:
+        assert lib.orb_debug_ba_chol_timeout(1, 1) == 0  # rows kernel; row 1's first wait times out
+        solver.optimize(prob, 1)
+        assert lib.orb_debug_ba_chol_timeout_status(ctypes.byref(st)) == 0
+        assert st.value == 6, st.value
+        assert lib.orb_debug_ba_chol_timeout(1, -1) == 0  # still the rows kernel, nothing armed
+        pose, point, _, _, res = solver.optimize(prob, 10)
+        rpose, rpoint, _, _, rres = oracle.local_ba(prob, 10)
+        assert res["iterations"] == rres["iterations"] and res["trials"] == rres["trials"]
+        assert _rmse(pose[:, :3], rpose[:, :3]) < 1e-6 and _rmse(point, rpoint) < 1e-6
+        assert lib.orb_debug_ba_chol_timeout_status(ctypes.byref(st)) == 0 and st.value == -1
+    finally:
+        lib.orb_debug_ba_chol_timeout(0, -1)

@@ -113,3 +113,52 @@ def test_chain_batched_keyframes(pkg, chain):
         torch.cuda.synchronize()
         assert torch.equal(cnt[p:p + len(nb)], c) and torch.equal(m12[p:p + len(nb), :k1.cap], a)
         p += len(nb)
+
+
+def test_chain_capacity_overflow(pkg, synth, oracle):
+    """A caller-chosen cap below a frame's keypoint count: the extractor flags the frame
+    ORB_ERR_CAPACITY, the BoW transform does not read its slice and reports ORB_ERR_CAPACITY, and every
+    SearchForTriangulation pair with it reports ORB_ERR_CAPACITY with no matches; the frames that fit
+    are unaffected and still equal the oracle chain."""
+    import torch
+    L, _, Tcw, _ = synth.stereo_sequence(3, seed=214)
+    imgs = L.copy()
+    for f in (1, 2):  # small textured windows: few keypoints, under the cap
+        flat = np.full_like(imgs[f], 128)
+        flat[140:300, 200:420] = imgs[f][140:300, 200:420]
+        imgs[f] = flat
+    voc = synth.dbow_vocabulary(10, 4, seed=61)
+    scale, sigma2 = synth.scale_tables()
+    ex = pkg.ORBextractor(1200, 1.2, 8, 20, 7, max_width=752, max_height=480, max_batch=4)
+    vocab = pkg.ORBVocabulary(voc)
+    ref = [oracle.OracleExtractor(1200, 1.2, 8, 20, 7)(imgs[f], (0, 0)) for f in range(3)]
+    cap = max(len(ref[1][0]), len(ref[2][0])) + 8
+    assert len(ref[0][0]) > cap
+    out = ex.extract_batch_device(torch.from_numpy(imgs).cuda(), (0, 0), cap=cap)
+    bow = vocab.transform_frames_device(out[1], out[2], 4)
+    torch.cuda.synchronize()
+    counts, bcounts = out[2].cpu().numpy(), bow[5].cpu().numpy()
+    assert counts[0, 0] == len(ref[0][0]) and counts[0, 1] == pkg._lib.ORB_ERR_CAPACITY
+    assert (bcounts[0] == pkg._lib.ORB_ERR_CAPACITY).all()
+    kfs, dev = [], []
+    for f in (1, 2):
+        assert counts[f, 0] == len(ref[f][0]) and counts[f, 1] >= 0
+        rbow, fv = oracle.bow_transform(voc, ref[f][1], 4)
+        nn = int(bcounts[f, 1])
+        fvn, fvb, fvf = bow[2][f].cpu().numpy(), bow[3][f].cpu().numpy(), bow[4][f].cpu().numpy()
+        assert {int(fvn[j]): [int(x) for x in fvf[fvb[j]:fvb[j + 1]]] for j in range(nn)} == fv
+        kfs.append(pkg.KeyFrame(keys_un=ref[f][0], descriptors=ref[f][1], Tcw=Tcw[f], camera=synth.EUROC_K,
+                                scale_factors=scale, level_sigma2=sigma2, feat_vec=fv))
+    dev = [pkg.DeviceKeyFrame(out, bow, f, Tcw[f], synth.EUROC_K, scale, sigma2) for f in range(3)]
+    m = pkg.ORBmatcher(0.6, True)
+    for k1, nbrs in ((1, (0, 2)), (0, (1, 2))):
+        m12, cnt = m.SearchForTriangulationDevice(dev[k1], [dev[f] for f in nbrs], False, True)
+        torch.cuda.synchronize()
+        m12, cnt = m12.cpu().numpy(), cnt.cpu().numpy()
+        for p, f in enumerate(nbrs):
+            if 0 in (k1, f):
+                assert cnt[p] == pkg._lib.ORB_ERR_CAPACITY and (m12[p] == -1).all(), (k1, f)
+                continue
+            r1, r2 = kfs[k1 - 1], kfs[f - 1]
+            rn, rm = oracle.search_for_triangulation(r1, r2, m.pair_geometry(r1, r2), False, True, True)
+            assert cnt[p] == rn and np.array_equal(m12[p, :r1.N], rm), (k1, f, cnt[p], rn)

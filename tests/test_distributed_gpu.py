@@ -64,7 +64,10 @@ def test_sharded_extractor_single_rank(pkg, synth, oracle):
             ri, r1, r2 = oracle.hamming_knn2(desc[f, :n].cpu().numpy(), desc[pf, :nt].cpu().numpy())
             assert np.array_equal(idx[f, :n], ri) and np.array_equal(d1[f, :n], r1) and np.array_equal(d2[f, :n], r2)
             assert (idx[f, n:] == -1).all() and (d1[f, n:] == 257).all()
-        shm.finish()
+        first = shm.matches[0]
+        shm.finish()  # the last step's gather is matched too, into the next buffer
+        torch.cuda.synchronize()
+        assert shm.matches[0] is not first and torch.equal(shm.matches[0], first)
         # two extractor handles in flight on their own streams (bench.py --in-flight 2): every step's
         # gathered blocks equal the direct extraction of that step's frames
         exs = [ex, pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=640, max_height=480, max_batch=4)]
