@@ -690,6 +690,40 @@ __device__ __forceinline__ double fmac_negbcast(double acc, double a, double b, 
     return acc;
 }
 
+// The same three forms without the leading s_nop, for the factor's pivot steps: every DPP read there
+// has its source (the column value lrc, or row[c+1]) written at least two VALU instructions earlier,
+// which mf_diag guarantees by one s_nop per pivot (dpp_fence) and by the order of its volatile
+// statements (volatile asm keeps its order; other instructions the compiler places between them only
+// add wait states).
+#define MF_DPP_NN(NAME, ASM)                                                                  \
+    __device__ __forceinline__ double NAME(double acc, double a, double b, int j) {          \
+        switch (j) { MF_CASES(ASM) default: break; }                                          \
+        return acc;                                                                           \
+    }
+#define MF_NN_NEGB(J) \
+    case J: asm volatile("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:" #J " row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(a), "v"(b)); break;
+#define MF_NN_NEGBC(J) \
+    case J: asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:" #J " row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(a), "v"(b)); break;
+MF_DPP_NN(fmac_bcast_negb_nn, MF_NN_NEGB)
+MF_DPP_NN(fmac_negbcast_nn, MF_NN_NEGBC)
+#undef MF_NN_NEGB
+#undef MF_NN_NEGBC
+#undef MF_DPP_NN
+// v_mov_b64_dpp without the s_nop (the caller spaces it from the source's write)
+__device__ __forceinline__ double bcast64_nn(double v, int j) {
+    double r = 0.0;
+    switch (j) {
+#define MF_B64NN(J) \
+    case J: asm volatile("v_mov_b64_dpp %0, %1 row_newbcast:" #J " row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(v)); break;
+        MF_CASES(MF_B64NN)
+#undef MF_B64NN
+        default: break;
+    }
+    return r;
+}
+// two wait states after the VALU write of v, before the DPP reads of it that follow (in program order)
+__device__ __forceinline__ void dpp_fence(double v) { asm volatile("s_nop 1" ::"v"(v)); }
+
 // acc[c & 3] += w[c] * src(lane c of the 16-lane row), c = 0..15 in order: the 16 DPP FMAs in one block
 // with a single s_nop for the broadcast source (written before the block; no instruction inside
 // writes it), instead of one per FMA.  The accumulators' own dependencies are interlocked.
@@ -703,6 +737,37 @@ __device__ __forceinline__ void fmac16_bcast(double acc[4], double src, const do
           "v"(w[8]), "v"(w[9]), "v"(w[10]), "v"(w[11]), "v"(w[12]), "v"(w[13]), "v"(w[14]), "v"(w[15]));
 }
 #undef MF_FMAC
+
+// the rest of pivot C's rank-1 update, j = J .. 15
+template <int C, int J>
+__device__ __forceinline__ void mf_update(double (&row)[16], double (&xc)[16], double lrc) {
+    if constexpr (J < 16) {
+        row[J] = fmac_bcast_negb_nn(row[J], lrc, lrc, J);
+        xc[J] = fmac_negbcast_nn(xc[J], lrc, xc[C], J);
+        mf_update<C, J + 1>(row, xc, lrc);
+    }
+}
+
+// Pivot C of mf_diag (and, recursively, the ones after it).  row[j] = fma(-L[r][C], L[j][C], row[j]),
+// xc[j] = fma(-L[j][C], xc[C], xc[j]) for j > C, in the order and rounding of the column loop.
+template <int C>
+__device__ __forceinline__ void mf_pivot(double (&row)[16], double (&xc)[16], double inv, bool& bad) {
+    const double lrc = row[C] * inv;  // L[r][C] for r > C
+    xc[C] *= inv;                     // x_C of column r of L^-1
+    if constexpr (C + 1 < 16) {
+        dpp_fence(lrc);
+        row[C + 1] = fmac_bcast_negb_nn(row[C + 1], lrc, lrc, C + 1);
+        xc[C + 1] = fmac_negbcast_nn(xc[C + 1], lrc, xc[C], C + 1);
+        if constexpr (C + 2 < 16) row[C + 2] = fmac_bcast_negb_nn(row[C + 2], lrc, lrc, C + 2);
+        else asm volatile("s_nop 0");
+        const double pn = bcast64_nn(row[C + 1], C + 1);  // two VALU writes after row[C+1]'s
+        bad |= !(pn > 0.0);
+        const double inv_next = rsqrt_nr(pn);
+        if constexpr (C + 2 < 16) xc[C + 2] = fmac_negbcast_nn(xc[C + 2], lrc, xc[C], C + 2);
+        mf_update<C, C + 3>(row, xc, lrc);
+        mf_pivot<C + 1 < 16 ? C + 1 : 15>(row, xc, inv_next, bad);
+    }
+}
 
 // The column values L[j][c] reach the other rows by DPP row broadcasts (every 16-lane row holds the
 // same block, so each row broadcasts within itself).
@@ -723,25 +788,14 @@ __device__ __forceinline__ void mf_diag(double* __restrict__ dk, double* __restr
     const double piv0 = bcast64(row[0], 0);
     bool bad = !(piv0 > 0.0);
     double inv = rsqrt_nr(piv0);  // 1 / L[c][c]
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-        const double lrc = row[c] * inv;  // L[r][c] for r > c
-        xc[c] *= inv;                     // x_c of column r of L^-1
-        double inv_next = 0.0;
-        if (c + 1 < 16) {  // row[j] = fma(-L[r][c], L[j][c], row[j]), xc[j] = fma(-L[j][c], xc[c], xc[j])
-            row[c + 1] = fmac_bcast_negb(row[c + 1], lrc, lrc, c + 1);
-            xc[c + 1] = fmac_negbcast(xc[c + 1], lrc, xc[c], c + 1);
-            const double pn = bcast64(row[c + 1], c + 1);
-            bad |= !(pn > 0.0);
-            inv_next = rsqrt_nr(pn);
-        }
-#pragma unroll
-        for (int j = c + 2; j < 16; ++j) {
-            row[j] = fmac_bcast_negb(row[j], lrc, lrc, j);
-            xc[j] = fmac_negbcast(xc[j], lrc, xc[c], j);
-        }
-        inv = inv_next;
-    }
+    // One s_nop per pivot (round 5): every DPP FMA of a pivot reads the same source lrc, so only the
+    // first needs the two wait states after lrc's write; the next pivot's broadcast of row[c+1] is
+    // spaced from its write by the two FMAs issued between them.  FP64 VALU on gfx950 is issue-bound
+    // (a dependent v_fma_f64 costs its 4-5 issue cycles, tools/probe/f64_lat_probe.hip), so the
+    // pivot's cost is its instruction count; the per-FMA s_nop had nearly doubled it.  The pivots are
+    // instantiated one by one (mf_pivot<C>): with volatile asm inside, `#pragma unroll` left the loop
+    // rolled and indexed the registers at run time.
+    mf_pivot<0>(row, xc, inv, bad);
     bad = __ballot(bad) != 0;
     if (lane == 0 && bad) *fail = 1;
     if (tr && lane == 0) tr[1] = clock64();
