@@ -248,6 +248,17 @@ int orb_search_for_triangulation_device(orb_matcher_t m, const orb_kf_device_t* 
                                         const orb_kf_pair_geom_t* geoms, int n_pairs, int only_stereo, int coarse,
                                         int32_t* d_matches12, int32_t* d_n_matches, void* stream);
 
+/* ---- Frame::UndistortKeyPoints (src/Frame.cc:1003-1051): mvKeysUn from mvKeys by cv::undistortPoints
+ * (OpenCV 4.x: five fixed-point iterations of the inverse k1 k2 p1 p2 k3 model in double, P = K, the
+ * result rounded to float; parity with a real OpenCV build unpinned), on the extractor's device layout:
+ * frame f's keypoints at d_kps[f * cap], its count at d_counts[2 f] (orb_extract_batch_device).
+ * d_kps_un receives the same records with pt undistorted (i < count; the rest is not written); a frame
+ * flagged ORB_ERR_CAPACITY is skipped.  K = (fx, fy, cx, cy); dist = mDistCoef (n_dist 4 or 5 floats);
+ * dist[0] == 0 copies mvKeys, as the reference does.  d_kps_un may equal d_kps.  Async on `stream`. */
+int orb_undistort_keypoints_device(const orb_keypoint_t* d_kps, const int32_t* d_counts, int n_frames, int cap,
+                                   const float K[4], const float* dist, int n_dist, orb_keypoint_t* d_kps_un,
+                                   void* stream);
+
 /* ---- ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono) (src/ORBmatcher.cc:1951-2185)
  * Pinhole frames without a second camera (Nleft == -1). */
 

@@ -45,6 +45,7 @@ _PROTOS = {
     "oracle_pose_optimization": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
     "oracle_is_in_frustum": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp]),
     "oracle_bow_transform": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "oracle_undistort_keypoints": (None, [_vp, _i, _vp, _vp, _i, _vp]),
     "oracle_compute_stereo_matches": (_i, [_vp, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _f, _f,
                                            _vp, _vp]),
 }
@@ -367,3 +368,14 @@ def is_in_frustum(frame, pos, normal, min_dist, max_dist, viewing_cos_limit=0.5)
                                                                                            "track_depth", "track_level",
                                                                                            "track_view_cos")])
     return {k: v[:n] for k, v in out.items()}
+
+
+def undistort_keypoints(kps, K, dist):
+    """Frame::UndistortKeyPoints (src/Frame.cc:1003-1051): mvKeysUn from mvKeys with cv::undistortPoints
+    (OpenCV 4.x, restated; parity unpinned).  K = (fx, fy, cx, cy), dist = mDistCoef (4 or 5 floats)."""
+    k = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+    out = np.empty_like(k)
+    Kf = np.ascontiguousarray(K, np.float32)
+    d = np.ascontiguousarray(dist, np.float32)
+    load().oracle_undistort_keypoints(k.ctypes.data, len(k), Kf.ctypes.data, d.ctypes.data, len(d), out.ctypes.data)
+    return out

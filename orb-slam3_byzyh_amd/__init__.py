@@ -6,7 +6,7 @@ __graft_entry__.py), which register it under the import name ``orbslam3_amd``.
 """
 from . import _lib
 from ._lib import KEYPOINT_DTYPE, POSE_EDGE_DTYPE, POSE_FRAME_DTYPE, OrbGpuError
-from .extractor import ORBextractor, keypoints_to_structured
+from .extractor import ORBextractor, keypoints_to_structured, undistort_keypoints_device
 from .keyframe import DeviceKeyFrame, Frame, KeyFrame, LocalMapPoints, frustum_frame, is_in_frustum
 from .matcher import ORBmatcher
 from .optimizer import LocalBA, local_bundle_adjustment, pose_optimization
@@ -14,4 +14,4 @@ from . import distributed, timers
 from .stereo import compute_stereo_matches, compute_stereo_matches_batch_device
 from .vocabulary import ORBVocabulary
 
-__all__ = ["ORBextractor", "ORBmatcher", "KeyFrame", "Frame", "LocalMapPoints", "LocalBA", "local_bundle_adjustment", "pose_optimization", "compute_stereo_matches", "compute_stereo_matches_batch_device", "ORBVocabulary", "frustum_frame", "is_in_frustum", "KEYPOINT_DTYPE", "OrbGpuError", "keypoints_to_structured", "_lib"]
+__all__ = ["ORBextractor", "ORBmatcher", "KeyFrame", "Frame", "LocalMapPoints", "LocalBA", "local_bundle_adjustment", "pose_optimization", "compute_stereo_matches", "compute_stereo_matches_batch_device", "ORBVocabulary", "frustum_frame", "is_in_frustum", "KEYPOINT_DTYPE", "OrbGpuError", "keypoints_to_structured", "undistort_keypoints_device", "_lib"]

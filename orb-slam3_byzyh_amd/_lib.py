@@ -114,6 +114,7 @@ PROTOTYPES = {
     "orb_bow_transform": (_i, [_vp, _vp, _i, _i, _vp, _vp, _ip, _vp, _vp, _vp, _ip]),
     "orb_bow_transform_batch_device": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "orb_bow_transform_frames_device": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "orb_undistort_keypoints_device": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _vp, _vp]),
     "orb_ba_create": (_i, [ctypes.POINTER(_vp)]),
     "orb_ba_destroy": (_i, [_vp]),
     "orb_ba_optimize": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),

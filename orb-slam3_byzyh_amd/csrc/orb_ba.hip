@@ -584,7 +584,8 @@ constexpr int kMf2TileWaves = 11, kMfMaxNT = 18;
 // kTrBack + j (start), kTrWaited + j (contributions in), kTrPub + j (x_j published); the diagonal
 // factorisation of step k at kTrDiag + 4 k + {0: start, 1: factored, 2: L^-1 stored, 3: y_k}.
 constexpr int kTrStep = 0, kTrEnd = 1199, kTrBack = 1200, kTrWaited = 1300, kTrPub = 1400, kTrDiag = 1500,
-              kTraceLen = 2048;
+              kTrE = 1600, kTrC = 1640, kTrD = 2240, kTraceLen = 2304;  // kTrE + 2 j: e_j's contributions in, e_j formed;
+                                                           // kTrC + 32 k + 2 w: wave w's row k contributions start / end
 static_assert(kTrStep + (kMfMaxNT * 16) * 4 <= kTrEnd && kTrDiag + 4 * kMfMaxNT <= kTraceLen, "trace layout");
 
 template <int N>
@@ -602,6 +603,21 @@ __device__ __forceinline__ double row16_sum(double v) {
     v += dpp_row_shr<4>(v);
     v += dpp_row_shr<8>(v);
     return v;
+}
+
+// Sum over the four 16-lane rows of a wave, ((p_0 + p_1) + (p_2 + p_3)), the same double in every lane:
+// v_permlane16_swap then v_permlane32_swap (gfx950), a swap and an add each, no LDS round trip.  The
+// operand order matches `p += shfl_xor(p, 16); p += shfl_xor(p, 32)` bit for bit.
+__device__ __forceinline__ double group4_sum(double p) {
+    const int2 a = __builtin_bit_cast(int2, p);
+    const auto x = __builtin_amdgcn_permlane16_swap(a.x, a.x, false, false);
+    const auto y = __builtin_amdgcn_permlane16_swap(a.y, a.y, false, false);
+    const double s = __builtin_bit_cast(double, int2{(int)x[0], (int)y[0]}) +
+                     __builtin_bit_cast(double, int2{(int)x[1], (int)y[1]});
+    const int2 b = __builtin_bit_cast(int2, s);
+    const auto u = __builtin_amdgcn_permlane32_swap(b.x, b.x, false, false);
+    const auto v = __builtin_amdgcn_permlane32_swap(b.y, b.y, false, false);
+    return __builtin_bit_cast(double, int2{(int)u[0], (int)v[0]}) + __builtin_bit_cast(double, int2{(int)u[1], (int)v[1]});
 }
 
 __device__ __forceinline__ void mf_wave_sync() {
@@ -738,6 +754,33 @@ __device__ __forceinline__ void fmac16_bcast(double acc[4], double src, const do
 }
 #undef MF_FMAC
 
+// The same sum four terms at a time (c = C0 .. C0 + 3 into acc[0..3]), for callers short of registers;
+// kNop: the first block after src's write carries the two wait states.
+#define MF_FMAC4(C, A, W) "v_fmac_f64_dpp %" #A ", %4, %" #W " row_newbcast:" #C " row_mask:0xf bank_mask:0xf\n\t"
+template <int C0, bool kNop>
+__device__ __forceinline__ void fmac4_bcast(double acc[4], double src, double w0, double w1, double w2, double w3);
+#define MF_FMAC4_DEF(C0, C1, C2, C3)                                                                          \
+    template <>                                                                                               \
+    __device__ __forceinline__ void fmac4_bcast<C0, true>(double acc[4], double src, double w0, double w1,    \
+                                                          double w2, double w3) {                             \
+        asm volatile("s_nop 1\n\t" MF_FMAC4(C0, 0, 5) MF_FMAC4(C1, 1, 6) MF_FMAC4(C2, 2, 7) MF_FMAC4(C3, 3, 8)  \
+                     : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])                                  \
+                     : "v"(src), "v"(w0), "v"(w1), "v"(w2), "v"(w3));                                         \
+    }                                                                                                         \
+    template <>                                                                                               \
+    __device__ __forceinline__ void fmac4_bcast<C0, false>(double acc[4], double src, double w0, double w1,   \
+                                                           double w2, double w3) {                            \
+        asm volatile(MF_FMAC4(C0, 0, 5) MF_FMAC4(C1, 1, 6) MF_FMAC4(C2, 2, 7) MF_FMAC4(C3, 3, 8)               \
+                     : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])                                  \
+                     : "v"(src), "v"(w0), "v"(w1), "v"(w2), "v"(w3));                                         \
+    }
+MF_FMAC4_DEF(0, 1, 2, 3)
+MF_FMAC4_DEF(4, 5, 6, 7)
+MF_FMAC4_DEF(8, 9, 10, 11)
+MF_FMAC4_DEF(12, 13, 14, 15)
+#undef MF_FMAC4_DEF
+#undef MF_FMAC4
+
 // the rest of pivot C's rank-1 update, j = J .. 15
 template <int C, int J>
 __device__ __forceinline__ void mf_update(double (&row)[16], double (&xc)[16], double lrc) {
@@ -859,7 +902,7 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
     double* dk = pre + 4 * 256;               // [16][17]
     double* yv = dk + 16 * 17;                // [16 NT]
     double* xv = yv + 16 * kMfMaxNT;          // [16 NT]
-    __shared__ int fail, lk, tbar, xready, wdone, pre_ready[kMfMaxNT], cnt[kMfMaxNT];
+    __shared__ int fail, lk, tbar, xready, pre_ready[kMfMaxNT], cnt[kMfMaxNT], wrdy[kMfMaxNT];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int NT = (n + 15) >> 4, ntt = NT * (NT + 1) / 2;
@@ -868,12 +911,12 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
         fail = 0;
         lk = -1;
         tbar = 0;
-        wdone = 0;   // tile waves done with the backward operators W1 / W2
         xready = 0;  // number of x blocks published (x_{NT-1} first)
     }
     if (threadIdx.x < kMfMaxNT) {
         pre_ready[threadIdx.x] = 0;
         cnt[threadIdx.x] = 0;
+        wrdy[threadIdx.x] = 0;  // W1_j / W2_j made (0, 1 or 2 of them)
     }
     for (int i = threadIdx.x; i < 16 * NT; i += (W + 1) * 64) yv[i] = i < n ? b[i] : 0.0;
     __syncthreads();  // the only workgroup barrier before the end
@@ -920,63 +963,40 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
             if (lane == 0) __hip_atomic_store(&lk, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (trace && lane == 0) trace[kTrStep + (k * 16 + W) * 4 + 3] = clock64();
         }
-        // backward: x_j = d_j - W1_j x_{j+1} - W2_j x_{j+2}, with W1_j = L_jj^-T L_{j+1,j}^T and
-        // W2_j = L_jj^-T L_{j+2,j}^T (16x16, formed by the tile waves from their registers after the
-        // forward) and d_j = L_jj^-T (y_j - sum_{k >= j+3} L_kj^T x_k).  The rows k >= j+3 were
-        // published three steps earlier, so their contributions are in by the time block j needs them:
-        // nothing on the x chain waits for another wave, and the chain itself is one 16-term product.
-        double* w2 = pan + kMfMaxNT * (kMfMaxNT - 1) / 2 * 16;  // W2_j (after the contribution slots)
-        // The operand rows are loaded without branches: W1 / W2 of a block without that neighbour come
-        // from a clamped slot and meet x = 0 there.  Slots no tile wave writes (NT < 3) are zeroed, so
-        // those products are exactly 0.
-        if (NT < 3) {
-            for (int t = lane; t < 256; t += 64) {
-                w2[t] = 0.0;
-                if (NT < 2) sub[t] = 0.0;
-            }
-            mf_wave_sync();
-        }
-        lds_flag_wait(&wdone, W, lane, &fail, 8);
-        double x1 = 0.0, x2 = 0.0;  // x_{j+1}[r16], x_{j+2}[r16]
+        // backward (round 5): x_j = e_j - W1_j x_{j+1}, with W1_j = L_jj^-T L_{j+1,j}^T (16x16, formed by
+        // the owner of tile (j+1, j) at its panel step) and e_j = L_jj^-T (y_j - sum_{k >= j+2} L_kj^T x_k):
+        // the tile waves subtract the rows k >= j+2 from y_j in place as the x_k are published (row
+        // j+2 one block before x_j is due), so this wave runs e_j's 16-term product, W1_j x_{j+1} and
+        // the publication per block.  Round 4 summed every contribution here and applied two operators:
+        // ~2.6k cycles per block, 48k for the backward of n = 288.
+        double x1 = 0.0;  // x_{j+1}[r16]
         for (int j = NT - 1; j >= 0; --j) {
             if (trace && lane == 0) trace[kTrBack + j] = clock64();
-            const double* lj = linv + j * 272;
-            const double* w1j = sub + max(min(j, NT - 2), 0) * 256;
-            const double* w2j = w2 + max(min(j, NT - 3), 0) * 256;
-            double li[16], a1[16], a2[16];
+            const double* lj = linv + j * 272 + r16 * 17;  // L_jj^-1[c][r16], c = 0..15
+            double a1[16];
+            if (j + 1 < NT) {  // W1_j row r16 (operand layout O(W))
+                lds_flag_wait(&wrdy[j], 1, lane, &fail, 8);
 #pragma unroll
-            for (int c = 0; c < 16; ++c) {  // L_jj^-1[c][r16]; W1_j, W2_j row r16 from O(W)
-                li[c] = lj[r16 * 17 + c];
-                const int o = (c >> 2) * 64 + r16 + 16 * (c & 3);
-                a1[c] = w1j[o];
-                a2[c] = w2j[o];
+                for (int c = 0; c < 16; ++c) a1[c] = sub[j * 256 + (c >> 2) * 64 + r16 + 16 * (c & 3)];
             }
-            lds_flag_wait(&cnt[j], NT - 3 - j, lane, &fail, 3);
+            if (j + 2 < NT) lds_flag_wait(&cnt[j + 2], j + 1, lane, &fail, 3);  // row j+2 (and above) applied
+            if (trace && lane == 0) trace[kTrE + 2 * j] = clock64();
+            const double v = yv[16 * j + r16];
+            double d4[4] = {0.0, 0.0, 0.0, 0.0};  // e_j = sum_c L_jj^-1[c][r16] v_c, four terms at a time
+            fmac4_bcast<0, true>(d4, v, lj[0], lj[1], lj[2], lj[3]);
+            fmac4_bcast<4, false>(d4, v, lj[4], lj[5], lj[6], lj[7]);
+            fmac4_bcast<8, false>(d4, v, lj[8], lj[9], lj[10], lj[11]);
+            fmac4_bcast<12, false>(d4, v, lj[12], lj[13], lj[14], lj[15]);
+            const double e = (d4[0] + d4[1]) + (d4[2] + d4[3]);
+            if (trace && lane == 0) trace[kTrE + 2 * j + 1] = clock64();
+            double s4[4] = {0.0, 0.0, 0.0, 0.0};
+            if (j + 1 < NT) fmac16_bcast(s4, x1, a1);
             if (trace && lane == 0) trace[kTrWaited + j] = clock64();
-            double v = yv[16 * j + r16];
-            {  // every contribution load issued at once, subtracted in the same order (kk descending);
-               // the missing ones are +0.0, which leaves v unchanged bit for bit
-                double cv[kMfMaxNT];
-#pragma unroll
-                for (int m = 0; m < kMfMaxNT; ++m) {
-                    const int kk = NT - 1 - m;
-                    const bool have = kk >= j + 3;  // (load unconditionally from a valid slot: no branch per load)
-                    const double cval = contrib[(have ? kk * (kk - 1) / 2 + j : 0) * 16 + r16];
-                    cv[m] = have ? cval : 0.0;
-                }
-#pragma unroll
-                for (int m = 0; m < kMfMaxNT; ++m) v -= cv[m];
-            }
-            double d4[4] = {0.0, 0.0, 0.0, 0.0}, s4[4] = {0.0, 0.0, 0.0, 0.0};
-            fmac16_bcast(d4, v, li);
-            fmac16_bcast(s4, x2, a2);
-            fmac16_bcast(s4, x1, a1);
-            const double xj = ((d4[0] + d4[1]) + (d4[2] + d4[3])) - ((s4[0] + s4[1]) + (s4[2] + s4[3]));
+            const double xj = e - ((s4[0] + s4[1]) + (s4[2] + s4[3]));
             if (lane < 16) xv[16 * j + r16] = xj;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_store(&xready, NT - j, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (trace && lane == 0) trace[kTrPub + j] = clock64();
-            x2 = x1;
             x1 = xj;
         }
     } else {
@@ -1036,7 +1056,6 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
 #pragma unroll
                     for (int q = 0; q < 4; ++q)
                         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(lkk[(g4 + 4 * q) * 17 + r16], T[s][q], acc, 0, 0, 0);
-                    T[s] = acc;
                     double part = 0.0;
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
@@ -1044,10 +1063,32 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
                         part = __builtin_fma(acc[q], yv[16 * k + g4 + 4 * q], part);
                     }
                     if (i > k + 1) {
-                        part += __shfl_xor(part, 16);
-                        part += __shfl_xor(part, 32);
-                        if (lane < 16) yv[16 * i + lane] -= part;
+                        part = group4_sum(part);
+                        // (the lane index laundered per step: the compiler otherwise hoists one address
+                        // register per slot out of the step loop, which the tile waves cannot afford)
+                        int lo = lane;
+                        asm volatile("" : "+v"(lo));
+                        if (lane < 16) yv[16 * i + lo] -= part;
+                    } else {  // i = k + 1: the backward operator W1_k = L_kk^-T L_{k+1,k}^T = O^-1 form
+                              // O(M X^T), X = L_{k+1,k} (A operand = acc), M = L_kk^-T (B from L_kk^-1)
+                        f64x4 wv = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            wv = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[q], lkk[r16 * 17 + g4 + 4 * q], wv, 0, 0, 0);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) sub[k * 256 + q * 64 + lane] = wv[q];
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                        if (lane == 0) __hip_atomic_store(&wrdy[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
+                    // The tile is final (L_ik); the forward does not touch it again.  Keep it transposed,
+                    // O(L_ik^T) = the D layout of L_ik = A (O(L_ik)) times the identity, so that the
+                    // backward's L_ik^T x_i is four FMAs and a four-row sum per lane instead of four
+                    // 16-lane reductions.
+                    f64x4 tr = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        tr = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[q], (4 * q + g4 == r16) ? 1.0 : 0.0, tr, 0, 0, 0);
+                    T[s] = tr;
                 }
             }
             // ---- tile-wave barrier (the diagonal wave does not take part)
@@ -1093,62 +1134,44 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
             }
             if (trace && lane == 0) trace[kTrStep + (k * 16 + w) * 4 + 3] = clock64();
         }
-        // every tile wave is past its last read of the panel buffers before contributions land there
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) __hip_atomic_fetch_add(&tbar, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        lds_flag_wait(&tbar, W * NT, lane, &fail, 6);
-        // ---- the backward operators of the diagonal wave: for the tiles (j+1, j) and (j+2, j) this
-        // wave holds, W = L_jj^-T L_ij^T = O^-1 form O(M X^T) with X = L_ij (A operand = the tile's own
-        // registers) and M = L_jj^-T (B operand from L_jj^-1, column-major); W1 -> sub[j], W2 -> w2[j]
-        {
-            double* w2 = pan + kMfMaxNT * (kMfMaxNT - 1) / 2 * 16;
-            auto make_w = [&](const f64x4& Tv, int i, int j) {
-                const double* lj = linv + j * 272;
-                f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Tv[q], lj[r16 * 17 + g4 + 4 * q], acc, 0, 0, 0);
-                double* dst = (i == j + 1 ? sub : w2) + j * 256;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) dst[q * 64 + lane] = acc[q];
-            };
-            // (a static walk over the wave's own slots: the slot index stays a compile-time
-            // constant, so T[] stays in registers, and no per-tile dispatch runs)
-#pragma unroll
-            for (int sl = 0; sl < SL; ++sl) {
-                if (tij[sl] < 0) continue;
-                const int i = tij[sl] & 255, j = tij[sl] >> 8;
-                if (i == j + 1 || i == j + 2) make_w(T[sl], i, j);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (lane == 0) __hip_atomic_fetch_add(&wdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        // ---- backward: row k's tiles (k, j <= k - 3) contribute L_kj^T x_k (the diagonal wave applies
-        // the two nearest sub-diagonal tiles itself, through W1 / W2), walking the wave's own slots
-        auto contribute = [&](const f64x4& Tv, int k, int j, double xr) {
-            double* cs = contrib + (k * (k - 1) / 2 + j) * 16;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const double o = row16_sum(Tv[q] * xr);  // sum_r L_kj[r][c] x_k[r], c = g4 + 4q
-                if (r16 == 15) cs[g4 + 4 * q] = o;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (lane == 0) __hip_atomic_fetch_add(&cnt[j], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // ---- backward: row k's tiles (k, m <= k - 2), kept transposed since their panel step, subtract
+        // L_km^T x_k from y_m in place (the diagonal wave applies (k, k - 1) itself, through W1).  A tile
+        // gives y_m[c] -= sum_r L_km[r][c] x_k[r]: lane (c, g) holds L_km[g + 4q][c] in register q, so
+        // four FMAs with x_k[g + 4q] and a four-row sum.  cnt[k] counts row k's applied tiles, and row
+        // k starts once row k + 1 is complete, so every y_m loses its rows in the order k = NT - 1,
+        // NT - 2, ... (one read-modify-write each).
+        auto mine = [&](int sl, int k) {  // slot sl holds a tile (k, m <= k - 2)
+            return tij[sl] >= 0 && (tij[sl] & 255) == k && (tij[sl] >> 8) <= k - 2;
         };
-        auto mine = [&](int sl, int k) {  // slot sl holds a tile (k, j <= k - 3)
-            return tij[sl] >= 0 && (tij[sl] & 255) == k && (tij[sl] >> 8) <= k - 3;
-        };
-        for (int k = NT - 1; k >= 3; --k) {
-            bool any = false;
+        for (int k = NT - 1; k >= 2; --k) {
+            int nown = 0;
 #pragma unroll
-            for (int sl = 0; sl < SL; ++sl) any |= mine(sl, k);
-            if (!any) continue;
+            for (int sl = 0; sl < SL; ++sl) nown += mine(sl, k);
+            if (!nown) continue;
             lds_flag_wait(&xready, NT - k, lane, &fail, 7);  // x_k published
-            const double xr = xv[16 * k + r16];
-            // the wave's tiles of row k, (k, k-3) first: slots ascend as the column descends
+            if (k + 1 < NT) lds_flag_wait(&cnt[k + 1], k, lane, &fail, 3);  // row k + 1's k tiles applied
+            if (trace && lane == 0) trace[kTrC + 32 * k + 2 * w] = clock64();
+            double xq[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) xq[q] = xv[16 * k + g4 + 4 * q];
+            if (trace && lane == 0 && k >= NT - 2) trace[kTrD + 32 * (NT - 1 - k) + 2 * w] = clock64();
 #pragma unroll
             for (int sl = 0; sl < SL; ++sl)
-                if (mine(sl, k)) contribute(T[sl], k, tij[sl] >> 8, xr);
+                if (mine(sl, k)) {
+                    const int m = tij[sl] >> 8;
+                    double p = 0.0;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) p = __builtin_fma(T[sl][q], xq[q], p);
+                    p = group4_sum(p);
+                    int lo = lane;  // (laundered, as in the panel)
+                    asm volatile("" : "+v"(lo));
+                    if (lane < 16) yv[16 * m + lo] -= p;
+                }
+            // one release for the row's tiles (a fence and an LDS atomic cost ~250 cycles)
+            if (trace && lane == 0 && k >= NT - 2) trace[kTrD + 32 * (NT - 1 - k) + 2 * w + 1] = clock64();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) __hip_atomic_fetch_add(&cnt[k], nown, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (trace && lane == 0) trace[kTrC + 32 * k + 2 * w + 1] = clock64();
         }
     }
     __syncthreads();
@@ -2056,9 +2079,24 @@ void dump_chol_trace(const int64_t* tr, int n, hipStream_t s) {
             const int b = kTrStep + (k * 16 + w) * 4;
             fprintf(stderr, "MFTRACE k=%d w=%d %lld %lld %lld %lld\n", k, w, rel(b), rel(b + 1), rel(b + 2), rel(b + 3));
         }
-    for (int k = NT - 1; k >= 0; --k)
+    for (int k = NT - 1; k >= 0; --k) {
+        long long c0 = -1, c1 = -1;  // row k's contributions: first wave in, last wave done
+        for (int w = 0; w < kMf2TileWaves; ++w) {
+            const long long a = rel(kTrC + 32 * k + 2 * w), b = rel(kTrC + 32 * k + 2 * w + 1);
+            if (a >= 0 && (c0 < 0 || a < c0)) c0 = a;
+            if (b > c1) c1 = b;
+        }
+        fprintf(stderr, "MFTRACE e k=%d in %lld formed %lld row_contrib %lld-%lld\n", k, rel(kTrE + 2 * k),
+                rel(kTrE + 2 * k + 1), c0, c1);
+        for (int w = 0; w < kMf2TileWaves; ++w)
+            if (rel(kTrC + 32 * k + 2 * w) >= 0)
+                fprintf(stderr, "MFTRACE rowc k=%d w=%d %lld %lld  (x loaded %lld, tiles done %lld)\n", k, w,
+                        rel(kTrC + 32 * k + 2 * w), rel(kTrC + 32 * k + 2 * w + 1),
+                        k >= NT - 2 ? rel(kTrD + 32 * (NT - 1 - k) + 2 * w) : -1,
+                        k >= NT - 2 ? rel(kTrD + 32 * (NT - 1 - k) + 2 * w + 1) : -1);
         fprintf(stderr, "MFTRACE back k=%d %lld waited %lld published %lld\n", k, rel(kTrBack + k), rel(kTrWaited + k),
                 rel(kTrPub + k));
+    }
     fprintf(stderr, "MFTRACE end %lld\n", rel(kTrEnd));
     for (int k = 0; k + 1 < NT; ++k) {
         const int b = kTrDiag + 4 * k;

@@ -202,3 +202,21 @@ def keypoints_to_structured(kps_tensor, count: int) -> np.ndarray:
     """Convert one frame's [cap, 7] float32 keypoint rows from extract_batch_device to KEYPOINT_DTYPE."""
     arr = kps_tensor[:count].contiguous().cpu().numpy()
     return arr.view(KEYPOINT_DTYPE).reshape(-1)
+
+
+def undistort_keypoints_device(extracted, K, dist, out=None, stream=None):
+    """Frame::UndistortKeyPoints (src/Frame.cc:1003-1051) on ORBextractor.extract_batch_device's outputs:
+    returns mvKeysUn as a [B, cap, 7] tensor (keypoints past each frame's count are not written).
+    K = (fx, fy, cx, cy); dist = mDistCoef, 4 or 5 floats (k1, k2, p1, p2[, k3])."""
+    import torch
+    kps, _, counts = extracted
+    b, cap = kps.shape[0], kps.shape[1]
+    out = torch.empty_like(kps) if out is None else out
+    Kf = np.ascontiguousarray(K, np.float32)
+    d = np.ascontiguousarray(dist, np.float32)
+    st = stream if stream is not None else torch.cuda.current_stream(kps.device)
+    check(_lib.load().orb_undistort_keypoints_device(kps.data_ptr(), counts.data_ptr(), b, cap, Kf.ctypes.data,
+                                                     d.ctypes.data, len(d), out.data_ptr(),
+                                                     ctypes.c_void_p(st.cuda_stream)),
+          "orb_undistort_keypoints_device")
+    return out

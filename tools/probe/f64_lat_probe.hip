@@ -111,7 +111,45 @@ __global__ void k_lat(long long* cyc, double* sink, double seed) {
         for (int u = 0; u < 8; ++u) iv = __builtin_amdgcn_ds_bpermute((iv & 63) << 2, iv);
     }
     t1 = clock64(); rec(t1 - t0);
-    sink[lane] = a + a1 + a2 + a3 + a4 + a5 + a6 + a7 + r + r1 + r2 + r3 + acc[0] + acc2[1] + acc3[2] + acc4[3] + fa + iv;
+    // 14: dependent v_permlane16_swap (pairs, 64-bit value as in group4_sum) + add
+    double pv = a;
+    t0 = clock64();
+    for (int i = 0; i < kIt; ++i) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int2 q = __builtin_bit_cast(int2, pv);
+            const auto x = __builtin_amdgcn_permlane16_swap(q.x, q.x, false, false);
+            const auto y = __builtin_amdgcn_permlane16_swap(q.y, q.y, false, false);
+            pv = __builtin_bit_cast(double, int2{(int)x[0], (int)y[0]}) + __builtin_bit_cast(double, int2{(int)x[1], (int)y[1]});
+        }
+    }
+    t1 = clock64(); rec(t1 - t0);
+    // 15: the same with v_permlane32_swap
+    t0 = clock64();
+    for (int i = 0; i < kIt; ++i) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int2 q = __builtin_bit_cast(int2, pv);
+            const auto x = __builtin_amdgcn_permlane32_swap(q.x, q.x, false, false);
+            const auto y = __builtin_amdgcn_permlane32_swap(q.y, q.y, false, false);
+            pv = __builtin_bit_cast(double, int2{(int)x[0], (int)y[0]}) + __builtin_bit_cast(double, int2{(int)x[1], (int)y[1]});
+        }
+    }
+    t1 = clock64(); rec(t1 - t0);
+    // 16: LDS read-modify-write of one double + release fence + LDS atomic add (the contribution tail)
+    __shared__ double sh[64];
+    __shared__ int cnt;
+    sh[lane] = 0.0;
+    if (lane == 0) cnt = 0;
+    __syncthreads();
+    t0 = clock64();
+    for (int i = 0; i < kIt * 8; ++i) {
+        sh[lane] -= pv;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_fetch_add(&cnt, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    t1 = clock64(); rec(t1 - t0);
+    sink[lane] = sh[lane] + pv + cnt + a + a1 + a2 + a3 + a4 + a5 + a6 + a7 + r + r1 + r2 + r3 + acc[0] + acc2[1] + acc3[2] + acc4[3] + fa + iv;
 }
 
 int main() {
@@ -124,7 +162,8 @@ int main() {
                            "v_mov_b64_dpp bcast dep (+s_nop 1)", "v_fmac_f64_dpp dep (+s_nop 1)",
                            "v_fmac_f64_dpp independent (8, one s_nop)", "mfma_f64_16x16x4 dependent",
                            "mfma_f64_16x16x4 independent (4 acc)", "v_add_f64 dependent", "v_fma_f32 dependent",
-                           "ds_bpermute dependent"};
+                           "ds_bpermute dependent", "permlane16_swap pair + add_f64 (dep)",
+                           "permlane32_swap pair + add_f64 (dep)", "LDS RMW f64 + release fence + LDS atomic"};
     const int n = sizeof(names) / sizeof(names[0]);
     long long h[64];
     for (int rep = 0; rep < 3; ++rep) {
