@@ -680,6 +680,100 @@ def bench_matchers(pkg, synth, dev, steps, cpu_baseline_on):
     return out
 
 
+def _chain_inputs(pkg, synth, dev, seed):
+    """One tracking-chain frame (synth.tracking_chain_scene) as device tables: the current frame, the
+    last frame's map points and the local map; plus the host Frames for the oracle."""
+    import numpy as np
+    import torch
+    sc = synth.tracking_chain_scene(seed=seed)
+    C, L = pkg.Frame(**sc["cur"]), pkg.Frame(**sc["last"])
+
+    def up(a, dt):
+        return torch.from_numpy(np.ascontiguousarray(a, dt)).to(dev)
+
+    def dframe(F):
+        ur = None if F.mvuRight is None else up(F.mvuRight.reshape(1, F.N), np.float32)
+        return pkg.DeviceFrame(up(F.mvKeysUn.view(np.float32).reshape(1, F.N, 7), np.float32),
+                               up(F.mDescriptors.reshape(1, F.N, 32), np.uint8), up(np.array([[F.N, 0]]), np.int32), 0,
+                               F.Tcw, sc["cur"]["camera"], F.mvScaleFactors, sc["level_sigma2"], int(F.mnMaxX),
+                               int(F.mnMaxY), F.mbf, ur)
+    cur, lastf = dframe(C), dframe(L)
+    mp = L.map_points
+    last = pkg.DeviceLastPoints(lastf, up(mp["valid"], np.uint8), up(mp["observed"], np.uint8),
+                                up(mp["xyz"], np.float32), up(mp["desc"], np.uint8))
+    local = pkg.DeviceLocalMap.from_host(dev, **sc["local"])
+    return sc, C, L, cur, last, local
+
+
+def bench_tracking_chain(pkg, synth, dev, steps, cpu_baseline_on, n_scenes=8, batch=32, n_streams=4):
+    """One frame of Tracking::TrackWithMotionModel -> TrackLocalMap, device-resident (tracking.TrackingChain:
+    SearchByProjection(LastFrame) -> PoseOptimization -> discard -> isInFrustum -> SearchByProjection(local
+    map) -> PoseOptimization, no host hop): single-frame latency (host launch to result, one stream) and
+    batched throughput (`batch` frames' chains over `n_streams` streams), next to the oracle chain on one
+    core.  Scenes: synth.tracking_chain_scene, EuRoC stereo geometry, ~1850 keypoints, 1800 local points."""
+    import numpy as np
+    import torch
+    scenes = [_chain_inputs(pkg, synth, dev, 4400 + s) for s in range(n_scenes)]
+    cap = max(s[3].cap for s in scenes)
+    chains = [pkg.TrackingChain(cap, device=dev, th_motion=7, th_local=1) for _ in range(batch)]
+    streams = [torch.cuda.Stream(dev) for _ in range(n_streams)]
+    reps = max(10, min(steps, 50))
+    # single frame: launch on one stream, wait for it
+    sc, C, L, cur, last, local = scenes[0]
+    st = streams[0]
+    ch = chains[0]
+    for _ in range(3):
+        ch.track(cur, last, local, sc["pose7_pred"], stream=st)
+        st.synchronize()
+    lat, gpu = [], []
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        e0.record(st)
+        ch.track(cur, last, local, sc["pose7_pred"], stream=st)
+        e1.record(st)
+        st.synchronize()
+        lat.append((time.perf_counter() - t0) * 1e3)
+        gpu.append(e0.elapsed_time(e1))
+    n1 = int(ch.n_match[0])
+    n2 = int(ch.n_match[1])
+
+    def batched():
+        for b, chn in enumerate(chains):
+            s = scenes[b % n_scenes]
+            chn.track(s[3], s[4], s[5], s[0]["pose7_pred"], stream=streams[b % n_streams])
+
+    for _ in range(2):
+        batched()
+    torch.cuda.synchronize(dev)
+    brep = max(3, min(steps, 10))
+    t0 = time.perf_counter()
+    for _ in range(brep):
+        batched()
+    torch.cuda.synchronize(dev)
+    bdt = (time.perf_counter() - t0) * 1e3
+    out = {"config": f"TrackWithMotionModel -> TrackLocalMap on one frame: {C.N} keypoints (stereo), last frame "
+                     f"{L.N} keypoints / {int(L.map_points['valid'].sum())} map points, {len(sc['local']['pos'])} local "
+                     f"map points; th 7 / 1, ORBmatcher(0.9, true) / (0.8); device-resident, one GPU",
+           "single_frame_ms": round(float(np.median(lat)), 4), "single_frame_gpu_ms": round(float(np.median(gpu)), 4),
+           "batched_frames_per_ms": round(batch * brep / bdt, 4), "batch": batch, "streams": n_streams,
+           "matches_last_frame": n1, "matches_local_map": n2, "dtype": "u8 / f32 / f64"}
+    if cpu_baseline_on:
+        from oracle import tracking_chain as oracle_chain
+        t0 = time.perf_counter()
+        nfr = 0
+        while time.perf_counter() - t0 < 3.0 or nfr < 4:
+            s = scenes[nfr % n_scenes]
+            oracle_chain.track(pkg, s[1], s[2], s[0]["local"], s[0]["pose7_pred"], s[0]["level_sigma2"], 7, 1)
+            nfr += 1
+        cdt = (time.perf_counter() - t0) * 1e3
+        out["cpu_baseline"] = {"value": round(cdt / nfr, 4), "unit": "ms/frame", "cores": 1, "kind": "port",
+                               "sample": f"{nfr} frames of the {n_scenes} scenes in {cdt / 1e3:.1f} s, the oracle chain "
+                                         "(oracle/tracking_chain.py over oracle/orb_projection_oracle.cpp, "
+                                         "orb_pose_oracle.cpp, orb_frustum_oracle.cpp), " + ORACLE_FLAGS + ", one thread"}
+    return out
+
+
 def bench_single_frame(pkg, synth, cpu_baseline_on, reps=50):
     """Tracking's own call pattern: ORBextractor::operator() on ONE host frame (PCIe-inclusive:
     upload, extraction, download of keypoints and descriptors), 640x480 and EuRoC 752x480; the
@@ -1049,6 +1143,7 @@ def main():
     ap.add_argument("--no-single", action="store_true", help="skip the single-frame latency measurement")
     ap.add_argument("--no-c4", action="store_true", help="skip the 1280x720 (C4 shard) measurement")
     ap.add_argument("--no-matchers", action="store_true", help="skip the ORBmatcher measurements")
+    ap.add_argument("--no-chain", action="store_true", help="skip the device tracking-chain measurement")
     ap.add_argument("--pcie-only", action="store_true",
                     help="internal: run only the PCIe-inclusive C2 measurement and print its JSON (bench.py runs "
                          "it in a child process of its own)")
@@ -1339,6 +1434,12 @@ def main():
             matchers = bench_matchers(pkg, synth, dev, args.steps, not args.no_cpu_baseline)
         except Exception as e:  # noqa: BLE001
             matchers = {"error": repr(e)}
+    chain = None
+    if not args.no_chain and world == 1:
+        try:
+            chain = bench_tracking_chain(pkg, synth, dev, args.steps, not args.no_cpu_baseline)
+        except Exception as e:  # noqa: BLE001
+            chain = {"error": repr(e)}
     pcie = None
     if not args.no_single and world == 1:
         try:
@@ -1360,6 +1461,8 @@ def main():
             result["c4_strong"] = c4_strong
         if matchers is not None:
             result["matchers"] = matchers
+        if chain is not None:
+            result["tracking_chain"] = chain
         if single is not None:
             result["single_frame_latency"] = single
         if pose is not None:

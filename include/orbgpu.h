@@ -318,6 +318,63 @@ int orb_search_by_projection_local(orb_matcher_t m, const orb_frame_view_t* fram
                                    const orb_local_points_t* pts, float th, int far_points, float th_far_points,
                                    int32_t* match, int32_t* n_matches);
 
+/* ---- The same two searches on device-resident frames (the tracking chain of Tracking::TrackWithMotionModel
+ * -> TrackLocalMap, src/Tracking.cc:4112-4217, 4742-4825, without a host hop between the stages).  The
+ * current frame's keypoints are the extractor's (or orb_undistort_keypoints_device's) device outputs;
+ * counts are read on the device and clamped to `cap`.  Host scalars (pose, bounds, camera) travel in the
+ * struct.  Results land in device memory, asynchronously on `stream`: d_match[i] for i < cap (-1 past
+ * the frame's count), *d_n_matches.  Every candidate list is sized for the whole frame, so no call is
+ * redone; scratch is allocated and freed on `stream`.  The matcher handle contributes only its ratio
+ * and orientation flag (calls on different streams may share it). */
+typedef struct orb_frame_device {
+    const orb_keypoint_t* kps_un;   /* device: mvKeysUn, cap entries */
+    const uint8_t* desc;            /* device: cap x 32 */
+    const int32_t* n;               /* device: N (e.g. &d_counts[2 f] of orb_extract_batch_device) */
+    const float* u_right;           /* device: mvuRight (cap), NULL = monocular */
+    int32_t cap;                    /* upper bound of *n, <= 16384 */
+    float min_x, max_x, min_y, max_y;       /* mnMinX, mnMaxX, mnMinY, mnMaxY */
+    float grid_inv_w, grid_inv_h;           /* mfGridElementWidthInv, mfGridElementHeightInv */
+    float fx, fy, cx, cy;                   /* mpCamera parameters */
+    float bf, b;                            /* mbf, mb */
+    int32_t nlevels;
+    const float* scale_factors;             /* host: mvScaleFactors (nlevels) */
+    float Tcw[12];                          /* host: GetPose(), 3x4 row-major [R|t] */
+} orb_frame_device_t;
+
+/* The last frame's tracked map points, device arrays indexed like its keypoints (cap entries). */
+typedef struct orb_last_points_device {
+    const int32_t* n;               /* device: LastFrame.N */
+    int32_t cap;
+    const uint8_t* valid;           /* mvpMapPoints[i] != NULL && !mvbOutlier[i] */
+    const uint8_t* observed;        /* mvpMapPoints[i]->Observations() > 0 */
+    const float* xyz;               /* mvpMapPoints[i]->GetWorldPos(), cap x 3 */
+    const uint8_t* desc;            /* mvpMapPoints[i]->GetDescriptor(), cap x 32 */
+    const orb_keypoint_t* kps_un;   /* LastFrame.mvKeysUn (octave and angle) */
+    float Tcw[12];                  /* host: LastFrame.GetPose() */
+} orb_last_points_device_t;
+
+/* Local map points, device arrays (n on the host: the size of mvpLocalMapPoints), e.g. the outputs of
+ * orb_is_in_frustum_device for the tracking fields. */
+typedef struct orb_local_points_device {
+    int32_t n;
+    const uint8_t* track_in_view;
+    const uint8_t* is_bad;
+    const uint8_t* observed;
+    const float* track_proj;        /* n x 3 */
+    const float* track_view_cos;
+    const float* track_depth;
+    const int32_t* track_level;
+    const uint8_t* desc;            /* n x 32 */
+} orb_local_points_device_t;
+
+int orb_search_by_projection_frame_device(orb_matcher_t m, const orb_frame_device_t* cur,
+                                          const orb_last_points_device_t* last, float th, int mono, int32_t* d_match,
+                                          int32_t* d_n_matches, void* stream);
+/* d_frame_taken: device, cap flags (NULL: none). */
+int orb_search_by_projection_local_device(orb_matcher_t m, const orb_frame_device_t* frame, const uint8_t* d_frame_taken,
+                                          const orb_local_points_device_t* pts, float th, int far_points,
+                                          float th_far_points, int32_t* d_match, int32_t* d_n_matches, void* stream);
+
 /* ---- Frame::isInFrustum (src/Frame.cc:667-773, pinhole, Nleft == -1) + MapPoint::PredictScale
  * (src/MapPoint.cc:715-731): the tracking fields of the local map points that
  * orb_search_by_projection_local reads.  Per point: Pc = Rcw P + tcw, depth > 0, projection inside
@@ -348,6 +405,16 @@ int orb_is_in_frustum_device(const orb_frustum_frame_t* frame, int n, const floa
                              const float* d_min_dist, const float* d_max_dist, float viewing_cos_limit,
                              uint8_t* d_in_view, float* d_proj, float* d_depth, int32_t* d_level, float* d_view_cos,
                              void* stream);
+
+/* The same with the frame's pose read on the device: d_pose7 is PoseOptimization's output (the
+ * g2o SE3Quat vector tx ty tz qx qy qz qw); the frame's Tcw / Ow follow Frame::SetPose on its float cast
+ * (src/Optimizer.cc:390-395, src/Frame.cc:533-599: the quaternion normalised, Eigen's rotation matrix, Ow =
+ * q^-1 (-t)); frame->Tcw and frame->Ow are ignored.  The link between PoseOptimization and
+ * SearchLocalPoints in the device tracking chain. */
+int orb_is_in_frustum_pose_device(const orb_frustum_frame_t* frame, const double* d_pose7, int n, const float* d_pos,
+                                  const float* d_normal, const float* d_min_dist, const float* d_max_dist,
+                                  float viewing_cos_limit, uint8_t* d_in_view, float* d_proj, float* d_depth,
+                                  int32_t* d_level, float* d_view_cos, void* stream);
 
 /* ---- Frame::ComputeStereoMatches (src/Frame.cc:1102-1358) ------------------------------------ */
 
@@ -520,6 +587,35 @@ int orb_pose_optimization(int n_frames, const orb_pose_frame_t* frames, int n_ed
 int orb_pose_optimization_device(int n_frames, const orb_pose_frame_t* d_frames, int n_edges,
                                  const orb_pose_edge_t* d_edges, double* d_pose_out, uint8_t* d_outlier,
                                  int32_t* d_inliers, void* stream);
+
+/* ---- the device tracking chain's glue (Tracking::TrackWithMotionModel / TrackLocalMap,
+ * src/Tracking.cc:4112-4217, 4234-4300) between the matchers and PoseOptimization, on device arrays.
+ * PoseOptimization's graph for one device frame (src/Optimizer.cc:93-180): an edge per keypoint i < N
+ * whose map point is d_match_b[i] (>= 0, a row of d_xyz_b) or else d_match_a[i] (a row of d_xyz_a), in
+ * keypoint order; stereo when u_right[i] >= 0; information inv_level_sigma2[octave] (host, nlevels);
+ * the camera from the frame view.  The start pose is d_pose (device, 7 doubles: the previous
+ * optimisation's result) or else pose (host).  Writes *d_frame (edge_begin 0, n_edges = the count),
+ * d_edges (up to cap) and d_edge_kp[e] = the keypoint of edge e.  d_match_b may be NULL. */
+int orb_tracking_pose_edges_device(const orb_frame_device_t* frame, const int32_t* d_match_a, const float* d_xyz_a,
+                                   const int32_t* d_match_b, const float* d_xyz_b, const float* inv_level_sigma2,
+                                   const double* d_pose, const double pose[7], orb_pose_frame_t* d_frame,
+                                   orb_pose_edge_t* d_edges, int32_t* d_edge_kp, void* stream);
+/* TrackWithMotionModel's outlier discard (src/Tracking.cc:4180-4203): each edge PoseOptimization marked
+ * an outlier clears its keypoint's map point in both match arrays; d_n_out[0] = the edges kept,
+ * d_n_out[1] = those whose map point has observations (nmatchesMap; d_observed_a / _b per table row,
+ * NULL = all observed).  d_match_b may be NULL.  d_taken (optional, cap entries): afterwards, whether
+ * keypoint i holds a map point with observations -- SearchByProjection(F, local points)'s skip set. */
+int orb_tracking_discard_outliers_device(const orb_pose_frame_t* d_frame, const int32_t* d_edge_kp,
+                                         const uint8_t* d_outlier, int32_t* d_match_a, const uint8_t* d_observed_a,
+                                         int32_t* d_match_b, const uint8_t* d_observed_b, int32_t* d_n_out, int cap,
+                                         uint8_t* d_taken, void* stream);
+/* SearchLocalPoints' skip of the map points the frame has seen (src/Tracking.cc:4745-4766, 4778, the
+ * mnLastFrameSeen test): local map point j is the last frame's row d_last_row[j] (-1: not tracked by the
+ * last frame); when a keypoint's d_match_a (cap entries: SearchByProjection(LastFrame)'s assignments
+ * BEFORE the discard, since the discarded outliers are marked seen too, :4195) names that row,
+ * d_in_view[j] (orb_is_in_frustum*_device's output) is cleared.  last_cap <= 16384. */
+int orb_tracking_local_seen_device(const int32_t* d_match_a, int cap, int last_cap, const int32_t* d_last_row,
+                                   int n_local, uint8_t* d_in_view, void* stream);
 
 /* ---- multi-GPU local BA: one process per GPU, every rank passes the same
  * problem; rank r owns a contiguous, edge-balanced range of the landmarks and their edges, and

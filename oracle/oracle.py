@@ -46,6 +46,8 @@ _PROTOS = {
     "oracle_is_in_frustum": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp]),
     "oracle_bow_transform": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "oracle_undistort_keypoints": (None, [_vp, _i, _vp, _vp, _i, _vp]),
+    "oracle_pose7_to_frame": (None, [_vp, _vp, _vp]),
+    "oracle_pose7_float_roundtrip": (None, [_vp, _vp]),
     "oracle_compute_stereo_matches": (_i, [_vp, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _f, _f,
                                            _vp, _vp]),
 }
@@ -378,4 +380,23 @@ def undistort_keypoints(kps, K, dist):
     Kf = np.ascontiguousarray(K, np.float32)
     d = np.ascontiguousarray(dist, np.float32)
     load().oracle_undistort_keypoints(k.ctypes.data, len(k), Kf.ctypes.data, d.ctypes.data, len(d), out.ctypes.data)
+    return out
+
+
+def pose7_to_frame(pose7):
+    """Frame::SetPose(SE3f(q.cast<float>(), t.cast<float>())) after PoseOptimization: (Tcw 3x4 float32,
+    Ow float32[3]) from the g2o SE3Quat vector (tx ty tz qx qy qz qw)."""
+    p = np.ascontiguousarray(pose7, np.float64).reshape(7)
+    T = np.zeros(12, np.float32)
+    O = np.zeros(3, np.float32)
+    load().oracle_pose7_to_frame(p.ctypes.data, T.ctypes.data, O.ctypes.data)
+    return T.reshape(3, 4), O
+
+
+def pose7_float_roundtrip(pose7):
+    """The pose the next PoseOptimization starts from after Frame::SetPose (float cast, Sophus's
+    quaternion normalisation, back to double)."""
+    p = np.ascontiguousarray(pose7, np.float64).reshape(7)
+    out = np.zeros(7, np.float64)
+    load().oracle_pose7_float_roundtrip(p.ctypes.data, out.ctypes.data)
     return out

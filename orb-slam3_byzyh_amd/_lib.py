@@ -115,6 +115,12 @@ PROTOTYPES = {
     "orb_bow_transform_batch_device": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "orb_bow_transform_frames_device": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "orb_undistort_keypoints_device": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _vp, _vp]),
+    "orb_search_by_projection_frame_device": (_i, [_vp, _vp, _vp, _f, _i, _vp, _vp, _vp]),
+    "orb_search_by_projection_local_device": (_i, [_vp, _vp, _vp, _vp, _f, _i, _f, _vp, _vp, _vp]),
+    "orb_is_in_frustum_pose_device": (_i, [_vp, _vp, _i, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "orb_tracking_pose_edges_device": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "orb_tracking_discard_outliers_device": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp]),
+    "orb_tracking_local_seen_device": (_i, [_vp, _i, _i, _vp, _i, _vp, _vp]),
     "orb_ba_create": (_i, [ctypes.POINTER(_vp)]),
     "orb_ba_destroy": (_i, [_vp]),
     "orb_ba_optimize": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
@@ -136,6 +142,7 @@ DEBUG_PROTOTYPES = {
     "orb_extractor_pyramid_launch_ms": (_i, [_vp, _fp, _ip]),
     "orb_extractor_launch_durations": (_i, [_vp, _i, _fp, _i, _ip]),
     "orb_debug_ba_chol_timeout": (_i, [_i, _i]),
+    "orb_debug_pose_trace": (_i, [_vp, _i]),
     "orb_debug_ba_chol_timeout_status": (_i, [_ip]),
 }
 

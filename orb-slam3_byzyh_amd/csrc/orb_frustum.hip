@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdint>
 
+#include "orb_pose_frame.h"
 #include "orb_predict_scale.h"
 #include "orbgpu.h"
 #include "orbgpu_internal.h"
@@ -23,7 +24,8 @@ __device__ __forceinline__ float dot3(const float a[3], const float b[3]) {
     return fmaf(a[2], b[2], fmaf(a[0], b[0], a[1] * b[1]));
 }
 
-__global__ __launch_bounds__(256) void k_is_in_frustum(orb_frustum_frame_t F, int n, const float* __restrict__ pos,
+__global__ __launch_bounds__(256) void k_is_in_frustum(orb_frustum_frame_t F, const double* __restrict__ pose7, int n,
+                                                       const float* __restrict__ pos,
                                                        const float* __restrict__ normal,
                                                        const float* __restrict__ min_dist,
                                                        const float* __restrict__ max_dist, float viewingCosLimit,
@@ -32,6 +34,11 @@ __global__ __launch_bounds__(256) void k_is_in_frustum(orb_frustum_frame_t F, in
                                                        float* __restrict__ view_cos) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    if (pose7) {  // the frame's pose is the device result of PoseOptimization (Frame::SetPose)
+        double p[7];
+        for (int k = 0; k < 7; ++k) p[k] = pose7[k];
+        orb_pose7_to_frame(p, F.Tcw, F.Ow);
+    }
     uint8_t in = 0;
     float px = -1, py = -1, pxr = 0, dep = 0, vc = 0;
     int lev = 0;
@@ -80,10 +87,10 @@ __global__ __launch_bounds__(256) void k_is_in_frustum(orb_frustum_frame_t F, in
 
 extern "C" {
 
-int orb_is_in_frustum_device(const orb_frustum_frame_t* frame, int n, const float* d_pos, const float* d_normal,
-                             const float* d_min_dist, const float* d_max_dist, float viewing_cos_limit,
-                             uint8_t* d_in_view, float* d_proj, float* d_depth, int32_t* d_level, float* d_view_cos,
-                             void* stream) {
+int orb_is_in_frustum_pose_device(const orb_frustum_frame_t* frame, const double* d_pose7, int n, const float* d_pos,
+                                  const float* d_normal, const float* d_min_dist, const float* d_max_dist,
+                                  float viewing_cos_limit, uint8_t* d_in_view, float* d_proj, float* d_depth,
+                                  int32_t* d_level, float* d_view_cos, void* stream) {
     if (!frame || n < 0 || (n && (!d_pos || !d_normal || !d_min_dist || !d_max_dist || !d_in_view || !d_proj ||
                                   !d_depth || !d_level || !d_view_cos)) || frame->n_levels <= 0)
         return orbgpu_fail(ORB_ERR_ARG, "invalid frustum arguments");
@@ -91,11 +98,19 @@ int orb_is_in_frustum_device(const orb_frustum_frame_t* frame, int n, const floa
     if (!orbgpu::predict_scale_thresholds(frame->log_scale_factor, frame->n_levels, steps.t))
         return orbgpu_fail(ORB_ERR_ARG, "log_scale_factor must be > 0 and n_levels <= 32");
     if (n == 0) return ORB_OK;
-    hipLaunchKernelGGL(k_is_in_frustum, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, *frame, n, d_pos,
+    hipLaunchKernelGGL(k_is_in_frustum, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, *frame, d_pose7, n, d_pos,
                        d_normal, d_min_dist, d_max_dist, viewing_cos_limit, steps, d_in_view, d_proj, d_depth, d_level,
                        d_view_cos);
     if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "frustum kernel launch failed");
     return ORB_OK;
+}
+
+int orb_is_in_frustum_device(const orb_frustum_frame_t* frame, int n, const float* d_pos, const float* d_normal,
+                             const float* d_min_dist, const float* d_max_dist, float viewing_cos_limit,
+                             uint8_t* d_in_view, float* d_proj, float* d_depth, int32_t* d_level, float* d_view_cos,
+                             void* stream) {
+    return orb_is_in_frustum_pose_device(frame, nullptr, n, d_pos, d_normal, d_min_dist, d_max_dist, viewing_cos_limit,
+                                         d_in_view, d_proj, d_depth, d_level, d_view_cos, stream);
 }
 
 int orb_is_in_frustum(const orb_frustum_frame_t* frame, int n, const float* pos, const float* normal,

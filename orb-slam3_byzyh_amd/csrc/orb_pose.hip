@@ -331,6 +331,13 @@ __device__ __forceinline__ double linearize_edge(const orb_pose_edge_t& Ed, cons
     return ev.chi2;
 }
 
+// Phase stamps of frame 0 (orb_debug_pose_trace, tools/pose_trace.py): per LM trial, s_memtime at the
+// pass start, after the pass's reduction, after the totals reached thread 0, after its decision and
+// solve, after the barrier that ends the trial, and inside the solve: its start, after the LDL^T,
+// after the exponential.
+__device__ long long* g_pose_trace = nullptr;
+__device__ int g_pose_trace_cap = 0;
+
 // LM state of a frame's optimize(10), kept in registers of the workgroup's thread 0
 struct LmState {
     double H[21], b[6], x[6], Tb[7];
@@ -354,6 +361,12 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
     __shared__ double T[7];
     __shared__ int s_state;  // 1: evaluate the trial pose in T, 2: the round's optimize() is done
     const int tid = threadIdx.x, f = blockIdx.x;
+    long long* const tr = f == 0 ? g_pose_trace : nullptr;
+    const int tr_cap = g_pose_trace_cap;
+    int tr_n = 0;  // trials stamped
+    auto stamp = [&](int k) {
+        if (tr && tid == 0 && tr_n < tr_cap) tr[8 * tr_n + k] = clock64();
+    };
     const orb_pose_frame_t F = frames[f];
     const int n = F.n_edges;
     const orb_pose_edge_t* E = edges + F.edge_begin;
@@ -432,12 +445,15 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
         }
     };
     auto solve = [&](LmState& S) {  // thread 0: the damped system, the trial pose into T
+        stamp(5);
         for (int i = 0; i < 7; ++i) S.Tb[i] = T[i];
         S.ok = ldlt6(S.H, S.lambda, S.b, S.x);
         if (!S.ok) for (int i = 0; i < 6; ++i) S.x[i] = 0;
+        stamp(6);
         double Tn[7];
         for (int i = 0; i < 7; ++i) Tn[i] = S.Tb[i];
         se3_oplus_r(Tn, S.x);
+        stamp(7);
         for (int i = 0; i < 7; ++i) T[i] = Tn[i];
     };
     bool robust = true;
@@ -478,8 +494,11 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
             for (;;) {
                 // evaluate (and linearise) at the trial pose; every active edge's chi2 is kept, since
                 // g2o classifies on the last evaluated state even when it was rejected
+                stamp(0);
                 pass(robust, true, acc);
+                stamp(1);
                 totals(acc, t);
+                stamp(2);
                 if (tid == 0) {
                     double tempChi = t[27];
                     if (!S.ok) tempChi = DBL_MAX;
@@ -525,7 +544,10 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
                     if (st == 1) solve(S);
                     s_state = st;
                 }
+                stamp(3);
                 __syncthreads();
+                stamp(4);
+                ++tr_n;
                 if (s_state == 2) break;
             }
         }
@@ -598,6 +620,15 @@ int orb_pose_optimization_device(int n_frames, const orb_pose_frame_t* d_frames,
     const bool launched = hipGetLastError() == hipSuccess;
     if (hipFreeAsync(chi, (hipStream_t)stream) != hipSuccess || !launched)
         return orbgpu_fail(ORB_ERR_DEVICE, "pose kernel launch failed");
+    return ORB_OK;
+}
+
+// Debug hook (not in the public header): stamp frame 0's LM trials into d_buf (8 int64 per trial, up
+// to `cap` trials; NULL turns it off).  Synchronous.
+int orb_debug_pose_trace(long long* d_buf, int cap) {
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_pose_trace), &d_buf, sizeof(d_buf)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(g_pose_trace_cap), &cap, sizeof(cap)) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "debug symbol copy");
     return ORB_OK;
 }
 

@@ -309,6 +309,7 @@ struct ResolveArgs {
     int32_t* removed;          // per keypoint
     int32_t* mp;               // out: per keypoint
     int32_t* out_n;            // out: [0] count, [1] rounds
+    const int32_t* dims;       // device forms: [0] n_pts, [1] n_cur read on the device (NULL: the fields above)
 };
 
 // a candidate resolve_point can take (the lister pass counts exactly these)
@@ -381,6 +382,10 @@ __device__ __forceinline__ int decide(const ResolveArgs& a, int d1, int j1, int 
 // claims.  k_resolve_rounds (one workgroup) then iterates only the work list, each point re-deciding
 // from its kTop best (a full scan only when too many of them are claimed).
 __global__ __launch_bounds__(256) void k_resolve_init(ResolveArgs a) {
+    if (a.dims) {
+        a.n_pts = a.dims[0];
+        a.n_cur = a.dims[1];
+    }
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= a.n_pts || *a.overflow > a.cap) return;
     unsigned long long t[kTop];
@@ -482,6 +487,10 @@ __device__ __forceinline__ int resolve_reg(const ResolveArgs& a, const int32_t* 
 }
 
 __global__ __launch_bounds__(kResolveThreads) void k_resolve_rounds(ResolveArgs a) {
+    if (a.dims) {
+        a.n_pts = a.dims[0];
+        a.n_cur = a.dims[1];
+    }
     const int tid = threadIdx.x;
     __shared__ int hist[kHisto], keep[3], cnt[2];
     extern __shared__ int32_t kp_lds[];
@@ -600,6 +609,111 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_rounds(ResolveArgs 
     }
 }
 
+// ---- device-resident forms: the frame's grid and packed keypoints built on the device ------------
+
+// Frame::AssignFeaturesToGrid (src/Frame.cc:1418-1440) on a device frame, one workgroup: cell
+// (round((x - mnMinX) inv_w), round((y - mnMinY) inv_h)), keypoints in index order inside each cell
+// (counting sort, then each cell's few entries put back in index order); the (x, y, angle, octave) float4
+// rows the candidate kernels read; the clamped count into n_out[0] and n_out[1].
+constexpr int kPrepThreads = 1024, kCells = kGridCols * kGridRows;
+__global__ __launch_bounds__(kPrepThreads) void k_frame_prep(const orb_keypoint_t* __restrict__ kps,
+                                                             const int32_t* __restrict__ n_ptr, int cap, float min_x,
+                                                             float min_y, float inv_w, float inv_h,
+                                                             float4* __restrict__ kp4, int32_t* __restrict__ cell_off,
+                                                             int32_t* __restrict__ cell_idx, int32_t* __restrict__ cell_of,
+                                                             int32_t* n_out0, int32_t* n_out1) {
+    __shared__ int cnt[kCells];
+    __shared__ int part[kPrepThreads];
+    const int tid = threadIdx.x;
+    const int n = min(max(*n_ptr, 0), cap);
+    for (int c = tid; c < kCells; c += kPrepThreads) cnt[c] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += kPrepThreads) {
+        const orb_keypoint_t kp = kps[i];
+        kp4[i] = make_float4(kp.x, kp.y, kp.angle, __int_as_float(kp.octave));
+        const int px = (int)roundf((kp.x - min_x) * inv_w);
+        const int py = (int)roundf((kp.y - min_y) * inv_h);
+        int cell = -1;
+        if (px >= 0 && px < kGridCols && py >= 0 && py < kGridRows) {
+            cell = px * kGridRows + py;
+            atomicAdd(&cnt[cell], 1);
+        }
+        cell_of[i] = cell;
+    }
+    __syncthreads();
+    // exclusive scan of the 3072 counts: three cells per thread
+    constexpr int kPer = kCells / kPrepThreads;
+    static_assert(kCells % kPrepThreads == 0, "cells per thread");
+    int loc[kPer], sum = 0;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        loc[q] = sum;
+        sum += cnt[tid * kPer + q];
+    }
+    part[tid] = sum;
+    __syncthreads();
+    for (int o = 1; o < kPrepThreads; o <<= 1) {
+        const int v = tid >= o ? part[tid - o] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    const int base = part[tid] - sum;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        cell_off[tid * kPer + q] = base + loc[q];
+        cnt[tid * kPer + q] = base + loc[q];  // becomes the fill cursor
+    }
+    if (tid == kPrepThreads - 1) cell_off[kCells] = base + sum;
+    if (tid == 0) {
+        *n_out0 = n;
+        if (n_out1) *n_out1 = n;
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += kPrepThreads) {
+        const int c = cell_of[i];
+        if (c >= 0) cell_idx[atomicAdd(&cnt[c], 1)] = i;
+    }
+    __threadfence_block();
+    __syncthreads();
+    for (int c = tid; c < kCells; c += kPrepThreads) {  // index order inside each cell (insertion sort)
+        const int b = c == 0 ? 0 : cell_off[c], e = cell_off[c + 1];
+        for (int a = b + 1; a < e; ++a) {
+            const int v = cell_idx[a];
+            int k = a;
+            for (; k > b && cell_idx[k - 1] > v; --k) cell_idx[k] = cell_idx[k - 1];
+            cell_idx[k] = v;
+        }
+    }
+}
+
+// the last frame's per-point inputs of k_proj_candidates / the rotation bins: a point whose octave is
+// outside the pyramid is not valid (the host form rejects the call instead)
+__global__ __launch_bounds__(256) void k_last_prep(const orb_keypoint_t* __restrict__ kps, const uint8_t* __restrict__ valid,
+                                                   const int32_t* __restrict__ n_ptr, int cap, int nlevels,
+                                                   uint8_t* __restrict__ valid2, int32_t* __restrict__ octave,
+                                                   float* __restrict__ angle, int32_t* n_out0, int32_t* n_out1) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int n = min(max(*n_ptr, 0), cap);
+    if (i == 0) {
+        *n_out0 = n;
+        *n_out1 = n;
+    }
+    if (i >= n) return;
+    const orb_keypoint_t kp = kps[i];
+    octave[i] = kp.octave;
+    angle[i] = kp.angle;
+    valid2[i] = valid[i] && kp.octave >= 0 && kp.octave < nlevels;
+}
+
+// local map points: a predicted level outside the pyramid leaves the point out
+__global__ __launch_bounds__(256) void k_local_prep(const uint8_t* __restrict__ in_view, const int32_t* __restrict__ level,
+                                                    int n, int nlevels, uint8_t* __restrict__ in_view2) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) in_view2[i] = in_view[i] && level[i] >= 0 && level[i] < nlevels;
+}
+
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 // k_resolve_rounds keeps claimMin and the fixed claims in dynamic LDS (8 B per keypoint, up to 128 KB)
@@ -615,6 +729,7 @@ bool resolve_lds_ready() {
 int orbgpu_matcher_reserve(orb_matcher_t m, size_t bytes, char** d_buf, char** h_buf, hipStream_t* stream,
                            int* check_ori);
 float orbgpu_matcher_nnratio(orb_matcher_t m);
+int orbgpu_matcher_check_ori(orb_matcher_t m);
 
 extern "C" int orb_search_by_projection_frame(orb_matcher_t m, const orb_frame_view_t* cur, const orb_last_points_t* last,
                                               float th, int mono, int32_t* match, int32_t* n_matches) {
@@ -902,4 +1017,199 @@ extern "C" int orb_search_by_projection_local(orb_matcher_t m, const orb_frame_v
         return ORB_OK;
     }
     return orbgpu_fail(ORB_ERR_INTERNAL, "SearchByProjection(local) candidate capacity");
+}
+
+namespace {
+
+// the stream-ordered scratch of one device call
+struct DevScratch {
+    char* base = nullptr;
+    size_t off = 0;
+    template <class T>
+    T* take(size_t count) {
+        T* p = reinterpret_cast<T*>(base + off);
+        off = align256(off + std::max<size_t>(count, 1) * sizeof(T));
+        return p;
+    }
+};
+
+bool frame_device_ok(const orb_frame_device_t* F) {
+    return F && F->kps_un && F->desc && F->n && F->cap > 0 && F->cap <= kResolveLdsKeypoints && F->nlevels > 0 &&
+           F->nlevels <= kMaxLevels && F->scale_factors && F->grid_inv_w > 0 && F->grid_inv_h > 0 &&
+           (reinterpret_cast<uintptr_t>(F->desc) & 15) == 0;
+}
+
+}  // namespace
+
+extern "C" int orb_search_by_projection_frame_device(orb_matcher_t m, const orb_frame_device_t* cur,
+                                                     const orb_last_points_device_t* last, float th, int mono,
+                                                     int32_t* d_match, int32_t* d_n_matches, void* stream) {
+    if (!m || !frame_device_ok(cur) || !last || !d_match || !d_n_matches || !last->n || last->cap < 0 ||
+        (last->cap > 0 && (!last->valid || !last->observed || !last->xyz || !last->desc || !last->kps_un)) ||
+        (reinterpret_cast<uintptr_t>(last->desc) & 15) != 0)
+        return orbgpu_fail(ORB_ERR_ARG, "bad SearchByProjection device arguments");
+    hipStream_t s = (hipStream_t)stream;
+    const int C = cur->cap, NL = last->cap;
+    ProjParams P{};
+    memcpy(P.Tcw, cur->Tcw, sizeof(P.Tcw));
+    P.min_x = cur->min_x; P.max_x = cur->max_x; P.min_y = cur->min_y; P.max_y = cur->max_y;
+    P.inv_w = cur->grid_inv_w; P.inv_h = cur->grid_inv_h;
+    P.fx = cur->fx; P.fy = cur->fy; P.cx = cur->cx; P.cy = cur->cy; P.bf = cur->bf; P.th = th;
+    for (int l = 0; l < cur->nlevels; ++l) P.scale[l] = cur->scale_factors[l];
+    P.n_cur = 0; P.n_last = 0; P.has_ur = cur->u_right != nullptr;
+    {   // twc = -R^T t, tlc = Tlw * twc (src:1960-1968), as the host form computes them
+        const float* T = cur->Tcw;
+        float twc[3], tlc[3];
+        for (int i = 0; i < 3; ++i) twc[i] = -std::fma(T[8 + i], T[11], std::fma(T[i], T[3], T[4 + i] * T[7]));
+        for (int i = 0; i < 3; ++i)
+            tlc[i] = std::fma(last->Tcw[4 * i + 2], twc[2], std::fma(last->Tcw[4 * i], twc[0], last->Tcw[4 * i + 1] * twc[1])) +
+                     last->Tcw[4 * i + 3];
+        P.bForward = tlc[2] > cur->b && !mono;
+        P.bBackward = -tlc[2] > cur->b && !mono;
+    }
+    P.cap = C;  // a point's candidates are distinct current keypoints: never more than the frame holds
+    P.check_ori = orbgpu_matcher_check_ori(m);
+    // scratch: params | dims | kp4 | cells | cell_of | last prep | lister + fixed | overflow block |
+    // candidates | ncand | st | claimMin, last, removed | work list | top
+    size_t bytes = 0;
+    {
+        DevScratch z;
+        z.take<ProjParams>(1); z.take<int32_t>(2); z.take<float4>(C); z.take<int32_t>(kCells + 1); z.take<int32_t>(C);
+        z.take<int32_t>(C); z.take<uint8_t>(NL); z.take<int32_t>(NL); z.take<float>(NL); z.take<int32_t>(2 * (size_t)C);
+        z.take<int32_t>(4); z.take<Cand>((size_t)NL * C); z.take<int32_t>(NL); z.take<int32_t>(NL);
+        z.take<int32_t>(3 * (size_t)C); z.take<int32_t>(NL); z.take<int4>((kTop / 2) * (size_t)NL); z.take<int32_t>(NL);
+        bytes = z.off;
+    }
+    DevScratch z;
+    if (hipMallocAsync(reinterpret_cast<void**>(&z.base), bytes, s) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "hipMallocAsync failed");
+    ProjParams* dP = z.take<ProjParams>(1);
+    int32_t* dims = z.take<int32_t>(2);
+    float4* kp4 = z.take<float4>(C);
+    int32_t* cell_off = z.take<int32_t>(kCells + 1);
+    int32_t* cell_idx = z.take<int32_t>(C);
+    int32_t* cell_of = z.take<int32_t>(C);
+    uint8_t* valid2 = z.take<uint8_t>(NL);
+    int32_t* loct = z.take<int32_t>(NL);
+    float* lang = z.take<float>(NL);
+    int32_t* lf = z.take<int32_t>(2 * (size_t)C);
+    int32_t* ovf = z.take<int32_t>(4);
+    Cand* cands = z.take<Cand>((size_t)NL * C);
+    int32_t* nc = z.take<int32_t>(NL);
+    int32_t* st = z.take<int32_t>(NL);
+    int32_t* kw = z.take<int32_t>(3 * (size_t)C);
+    int32_t* wl = z.take<int32_t>(NL);
+    int4* top = z.take<int4>((kTop / 2) * (size_t)NL);
+    int32_t* nus = z.take<int32_t>(NL);
+    bool ok = hipMemcpyAsync(dP, &P, sizeof(P), hipMemcpyHostToDevice, s) == hipSuccess &&
+              hipMemsetAsync(lf, 0x7f, 2 * (size_t)C * 4, s) == hipSuccess && hipMemsetAsync(ovf, 0, 16, s) == hipSuccess &&
+              hipMemsetAsync(d_match, 0xFF, (size_t)C * 4, s) == hipSuccess;
+    if (ok) {
+        hipLaunchKernelGGL(k_frame_prep, dim3(1), dim3(kPrepThreads), 0, s, cur->kps_un, cur->n, C, cur->min_x, cur->min_y,
+                           cur->grid_inv_w, cur->grid_inv_h, kp4, cell_off, cell_idx, cell_of, &dP->n_cur, dims + 1);
+        if (NL > 0) {
+            hipLaunchKernelGGL(k_last_prep, dim3((NL + 255) / 256), dim3(256), 0, s, last->kps_un, last->valid, last->n, NL,
+                               cur->nlevels, valid2, loct, lang, &dP->n_last, dims);
+            hipLaunchKernelGGL(k_proj_candidates, dim3((NL + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s,
+                               (const ProjParams*)dP, (const uint8_t*)valid2, last->xyz, (const uint4*)last->desc,
+                               (const int32_t*)loct, (const float4*)kp4, cur->u_right, (const uint4*)cur->desc,
+                               (const int32_t*)cell_off, (const int32_t*)cell_idx, cands, nc, ovf, last->observed, lf);
+        } else {
+            ok = hipMemsetAsync(dims, 0, 4, s) == hipSuccess;
+        }
+        ResolveArgs ra{};
+        ra.n_pts = NL; ra.n_cur = C; ra.cap = C; ra.local = 0; ra.check_ori = P.check_ori; ra.nnratio = 0.f;
+        ra.cands = cands; ra.ncand = nc; ra.observed = last->observed; ra.taken0 = nullptr; ra.cur_kp = kp4;
+        ra.last_angle = lang; ra.overflow = ovf; ra.st = st;
+        ra.claimMin = kw; ra.last = kw + C; ra.removed = kw + 2 * (size_t)C;
+        ra.lister = lf; ra.fixed = lf + C; ra.work = wl; ra.top = top; ra.nusable = nus;
+        ra.lds_keypoints = resolve_lds_ready() ? 1 : 0;
+        ra.mp = d_match; ra.out_n = ovf + 1; ra.dims = dims;
+        if (NL > 0) hipLaunchKernelGGL(k_resolve_init, dim3((NL + 255) / 256), dim3(256), 0, s, ra);
+        hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 8 * (size_t)C : 0, s, ra);
+        ok = ok && hipGetLastError() == hipSuccess &&
+             hipMemcpyAsync(d_n_matches, ovf + 1, 4, hipMemcpyDeviceToDevice, s) == hipSuccess;
+    }
+    if (hipFreeAsync(z.base, s) != hipSuccess) ok = false;
+    return ok ? ORB_OK : orbgpu_fail(ORB_ERR_DEVICE, "SearchByProjection device failed");
+}
+
+extern "C" int orb_search_by_projection_local_device(orb_matcher_t m, const orb_frame_device_t* F,
+                                                     const uint8_t* d_frame_taken, const orb_local_points_device_t* pts,
+                                                     float th, int far_points, float th_far_points, int32_t* d_match,
+                                                     int32_t* d_n_matches, void* stream) {
+    if (!m || !frame_device_ok(F) || !pts || pts->n < 0 || !d_match || !d_n_matches ||
+        (pts->n && (!pts->track_in_view || !pts->is_bad || !pts->observed || !pts->track_proj || !pts->track_view_cos ||
+                    !pts->track_depth || !pts->track_level || !pts->desc)) ||
+        (reinterpret_cast<uintptr_t>(pts->desc) & 15) != 0)
+        return orbgpu_fail(ORB_ERR_ARG, "bad SearchByProjection(local map) device arguments");
+    hipStream_t s = (hipStream_t)stream;
+    const int C = F->cap, np = pts->n;
+    LocalParams P{};
+    P.min_x = F->min_x; P.min_y = F->min_y; P.inv_w = F->grid_inv_w; P.inv_h = F->grid_inv_h;
+    P.th = th; P.th_far = th_far_points;
+    for (int l = 0; l < F->nlevels; ++l) P.scale[l] = F->scale_factors[l];
+    P.n_cur = 0; P.n_pts = np; P.has_ur = F->u_right != nullptr; P.far = far_points ? 1 : 0; P.nlevels = F->nlevels;
+    P.cap = C;
+    P.nnratio = orbgpu_matcher_nnratio(m);
+    size_t bytes = 0;
+    {
+        DevScratch z;
+        z.take<LocalParams>(1); z.take<int32_t>(2); z.take<float4>(C); z.take<int32_t>(kCells + 1); z.take<int32_t>(C);
+        z.take<int32_t>(C); z.take<uint8_t>(np); z.take<int32_t>(2 * (size_t)C); z.take<int32_t>(4);
+        z.take<Cand>((size_t)np * C); z.take<int32_t>(np); z.take<int32_t>(np); z.take<int32_t>(3 * (size_t)C);
+        z.take<int32_t>(np); z.take<int4>((kTop / 2) * (size_t)np); z.take<int32_t>(np);
+        bytes = z.off;
+    }
+    DevScratch z;
+    if (hipMallocAsync(reinterpret_cast<void**>(&z.base), bytes, s) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "hipMallocAsync failed");
+    LocalParams* dP = z.take<LocalParams>(1);
+    int32_t* dims = z.take<int32_t>(2);
+    float4* kp4 = z.take<float4>(C);
+    int32_t* cell_off = z.take<int32_t>(kCells + 1);
+    int32_t* cell_idx = z.take<int32_t>(C);
+    int32_t* cell_of = z.take<int32_t>(C);
+    uint8_t* iv2 = z.take<uint8_t>(np);
+    int32_t* lf = z.take<int32_t>(2 * (size_t)C);
+    int32_t* ovf = z.take<int32_t>(4);
+    Cand* cands = z.take<Cand>((size_t)np * C);
+    int32_t* nc = z.take<int32_t>(np);
+    int32_t* st = z.take<int32_t>(np);
+    int32_t* kw = z.take<int32_t>(3 * (size_t)C);
+    int32_t* wl = z.take<int32_t>(np);
+    int4* top = z.take<int4>((kTop / 2) * (size_t)np);
+    int32_t* nus = z.take<int32_t>(np);
+    const int32_t dims_h[2] = {np, 0};
+    bool ok = hipMemcpyAsync(dP, &P, sizeof(P), hipMemcpyHostToDevice, s) == hipSuccess &&
+              hipMemcpyAsync(dims, dims_h, sizeof(dims_h), hipMemcpyHostToDevice, s) == hipSuccess &&
+              hipMemsetAsync(lf, 0x7f, 2 * (size_t)C * 4, s) == hipSuccess && hipMemsetAsync(ovf, 0, 16, s) == hipSuccess &&
+              hipMemsetAsync(d_match, 0xFF, (size_t)C * 4, s) == hipSuccess;
+    if (ok) {
+        hipLaunchKernelGGL(k_frame_prep, dim3(1), dim3(kPrepThreads), 0, s, F->kps_un, F->n, C, F->min_x, F->min_y,
+                           F->grid_inv_w, F->grid_inv_h, kp4, cell_off, cell_idx, cell_of, &dP->n_cur, dims + 1);
+        if (np > 0) {
+            hipLaunchKernelGGL(k_local_prep, dim3((np + 255) / 256), dim3(256), 0, s, pts->track_in_view, pts->track_level,
+                               np, F->nlevels, iv2);
+            hipLaunchKernelGGL(k_lmp_candidates, dim3((np + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s,
+                               (const LocalParams*)dP, (const uint8_t*)iv2, pts->is_bad, pts->track_proj, pts->track_view_cos,
+                               pts->track_depth, pts->track_level, (const uint4*)pts->desc, (const float4*)kp4, F->u_right,
+                               (const uint4*)F->desc, (const int32_t*)cell_off, (const int32_t*)cell_idx, cands, nc, ovf,
+                               pts->observed, d_frame_taken, lf);
+        }
+        ResolveArgs ra{};
+        ra.n_pts = np; ra.n_cur = C; ra.cap = C; ra.local = 1; ra.check_ori = 0; ra.nnratio = P.nnratio;
+        ra.cands = cands; ra.ncand = nc; ra.observed = pts->observed; ra.taken0 = d_frame_taken; ra.cur_kp = kp4;
+        ra.last_angle = nullptr; ra.overflow = ovf; ra.st = st;
+        ra.claimMin = kw; ra.last = kw + C; ra.removed = kw + 2 * (size_t)C;
+        ra.lister = lf; ra.fixed = lf + C; ra.work = wl; ra.top = top; ra.nusable = nus;
+        ra.lds_keypoints = resolve_lds_ready() ? 1 : 0;
+        ra.mp = d_match; ra.out_n = ovf + 1; ra.dims = dims;
+        if (np > 0) hipLaunchKernelGGL(k_resolve_init, dim3((np + 255) / 256), dim3(256), 0, s, ra);
+        hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 8 * (size_t)C : 0, s, ra);
+        ok = hipGetLastError() == hipSuccess &&
+             hipMemcpyAsync(d_n_matches, ovf + 1, 4, hipMemcpyDeviceToDevice, s) == hipSuccess;
+    }
+    if (hipFreeAsync(z.base, s) != hipSuccess) ok = false;
+    return ok ? ORB_OK : orbgpu_fail(ORB_ERR_DEVICE, "SearchByProjection(local) device failed");
 }

@@ -399,6 +399,7 @@ int orbgpu_matcher_reserve(orb_matcher_t m, size_t bytes, char** d_buf, char** h
 }
 
 float orbgpu_matcher_nnratio(orb_matcher_t m) { return m->nnratio; }
+int orbgpu_matcher_check_ori(orb_matcher_t m) { return m->check_ori; }
 
 extern "C" {
 

@@ -478,6 +478,100 @@ def pose_opt_batch(n_frames: int = 64, n_points: int = 600, stereo_frac: float =
     return frames, edges, truth
 
 
+def tracking_chain_scene(n_points: int = 1800, seed: int = 81, width: int = 752, height: int = 480,
+                         stereo: bool = True, clutter: int = 300, tracked_frac: float = 0.7, outlier_frac: float = 0.06,
+                         unobserved_frac: float = 0.1, bad_frac: float = 0.02, nlevels: int = 8,
+                         pred_rot: float = 0.004, pred_trans: float = 0.02, step: float = 0.05):
+    """One frame of Tracking::TrackWithMotionModel -> TrackLocalMap: a map of points (position,
+    descriptor, normal, mfMinDistance / mfMaxDistance from the octave of their reference observation,
+    observed / bad flags), the last frame (pose 0) holding `tracked_frac` of the points it sees (a few of
+    them at positions off by ~0.1 m: PoseOptimization's outliers), the current frame at the true pose 1
+    (noisy keypoints at octave +-1, perturbed descriptors, stereo u_right for 60 %, clutter) and the
+    motion model's prediction of its pose, off the truth by ~pred_rot rad / pred_trans m.  The local
+    map is every point; last_row[j] names the last frame's keypoint that holds point j (-1: none).
+    Returns dict(cur=Frame kwargs, last=Frame kwargs with map_points, local=dict of local map arrays,
+    pose7_pred, pose7_true, level_sigma2)."""
+    from ._lib import KEYPOINT_DTYPE
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = EUROC_K
+    scale, sigma2 = scale_tables(nlevels)
+    P = np.stack([rng.uniform(-4, 4, n_points), rng.uniform(-2.5, 2.5, n_points), rng.uniform(2, 12, n_points)], 1)
+    base = rng.integers(0, 256, (n_points, 32), dtype=np.uint8)
+    ang = rng.uniform(0, 360, n_points)
+    octv = rng.integers(0, nlevels, n_points)
+    R0, t0 = np.eye(3), np.zeros(3)
+    R1 = _rot_yaw_pitch(np.deg2rad(0.6), np.deg2rad(0.2))
+    C1 = np.array([0.02, -0.005, step])
+    t1 = -R1 @ C1
+
+    def frame(R, t, noise, flips, oct_jitter):
+        Xc = P @ R.T + t
+        z = Xc[:, 2]
+        u = fx * Xc[:, 0] / z + cx
+        v = fy * Xc[:, 1] / z + cy
+        vis = np.flatnonzero((z > 0.3) & (u >= 0) & (u < width) & (v >= 0) & (v < height))
+        nv = len(vis)
+        kps = np.zeros(nv + clutter, KEYPOINT_DTYPE)
+        o = np.clip(octv[vis] + (rng.integers(-1, 2, nv) if oct_jitter else 0), 0, nlevels - 1)
+        kps["octave"][:nv] = o
+        kps["x"][:nv] = np.clip(u[vis] + rng.normal(0, noise, nv) * scale[o], 0, width - 1)
+        kps["y"][:nv] = np.clip(v[vis] + rng.normal(0, noise, nv) * scale[o], 0, height - 1)
+        kps["angle"][:nv] = np.mod(ang[vis] + rng.normal(0, 3, nv), 360)
+        kps["x"][nv:] = rng.uniform(0, width - 1, clutter)
+        kps["y"][nv:] = rng.uniform(0, height - 1, clutter)
+        kps["octave"][nv:] = rng.integers(0, nlevels, clutter)
+        kps["angle"][nv:] = rng.uniform(0, 360, clutter)
+        kps["size"] = 31 * scale[kps["octave"]]
+        kps["response"] = rng.uniform(5, 100, nv + clutter)
+        kps["class_id"] = -1
+        bits = np.unpackbits(base[vis], axis=1)
+        for i in range(nv):
+            bits[i, rng.choice(256, int(rng.integers(0, flips)), replace=False)] ^= 1
+        desc = np.concatenate([np.packbits(bits, axis=1), rng.integers(0, 256, (clutter, 32), dtype=np.uint8)])
+        ur = np.full(nv + clutter, -1.0, np.float32)
+        if stereo:
+            st = rng.random(nv) < 0.6
+            ur[:nv][st] = (kps["x"][:nv][st] - EUROC_BF / z[vis][st] + rng.normal(0, 0.5, st.sum())).astype(np.float32)
+        perm = rng.permutation(nv + clutter)
+        ids = np.concatenate([vis, np.full(clutter, -1)])[perm]
+        return kps[perm], desc[perm], ur[perm], ids
+
+    lk, ld, lur, lids = frame(R0, t0, 0.3, 12, False)
+    ck, cd, cur_ur, _ = frame(R1, t1, 0.5, 30, True)
+    # map point positions (the map's estimate): small noise, a few gross errors
+    Pm = (P + rng.normal(0, 0.01, P.shape)).astype(np.float32)
+    gross = rng.random(n_points) < outlier_frac
+    Pm[gross] += rng.normal(0, 0.1, (int(gross.sum()), 3)).astype(np.float32)
+    observed = (rng.random(n_points) > unobserved_frac).astype(np.uint8)
+    has = lids >= 0
+    valid = has & (rng.random(len(lids)) < tracked_frac)
+    xyz = np.zeros((len(lids), 3), np.float32)
+    mdesc = np.zeros((len(lids), 32), np.uint8)
+    obs_rows = np.zeros(len(lids), np.uint8)
+    xyz[has], mdesc[has], obs_rows[has] = Pm[lids[has]], base[lids[has]], observed[lids[has]]
+    last_row = np.full(n_points, -1, np.int32)
+    last_row[lids[valid]] = np.flatnonzero(valid)
+    # MapPoint::UpdateNormalAndDepth from the pose-0 observation (src/MapPoint.cc:619-668)
+    d0 = np.linalg.norm(Pm, axis=1)
+    normal = (Pm / d0[:, None]).astype(np.float32)
+    max_dist = (d0 * scale[octv]).astype(np.float32)
+    min_dist = (max_dist / scale[nlevels - 1]).astype(np.float32)
+    # the motion model's prediction, as the float SE3 a Frame holds (Sophus SE3f)
+    Rp = _small_rot(rng, pred_rot) @ R1
+    tp = t1 + rng.normal(0, pred_trans, 3)
+    pose7_pred = np.concatenate([tp.astype(np.float32), rot_to_quat(Rp).astype(np.float32)]).astype(np.float64)
+    Tp = np.concatenate([quat_to_rot(pose7_pred[3:]), pose7_pred[:3, None]], 1).astype(np.float32)
+    common = dict(camera=EUROC_K, scale_factors=scale, width=width, height=height, bf=EUROC_BF if stereo else 0.0)
+    last = dict(keys_un=lk, descriptors=ld, Tcw=np.concatenate([R0, t0[:, None]], 1).astype(np.float32),
+                u_right=lur if stereo else None,
+                map_points=dict(valid=valid.astype(np.uint8), observed=obs_rows, xyz=xyz, desc=mdesc), **common)
+    cur = dict(keys_un=ck, descriptors=cd, Tcw=Tp, u_right=cur_ur if stereo else None, **common)
+    local = dict(pos=Pm, normal=normal, min_dist=min_dist, max_dist=max_dist, desc=base.copy(), observed=observed,
+                 is_bad=((rng.random(n_points) < bad_frac) & (last_row < 0)).astype(np.uint8), last_row=last_row)
+    truth = np.concatenate([t1, rot_to_quat(R1)])
+    return dict(cur=cur, last=last, local=local, pose7_pred=pose7_pred, pose7_true=truth, level_sigma2=sigma2)
+
+
 def dbow_vocabulary(k: int = 10, L: int = 4, seed: int = 11, flip: float = 0.2, leaf_early: float = 0.05,
                     stop_frac: float = 0.02, weighting: int = 0, scoring: int = 0, kmin=None):
     """A DBoW2-shaped vocabulary tree (stand-in for ORBvoc.txt, absent: .MISSING_LARGE_BLOBS):

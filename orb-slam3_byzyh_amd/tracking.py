@@ -1,0 +1,286 @@
+"""The device-resident tracking chain: one frame of Tracking::TrackWithMotionModel -> TrackLocalMap
+(reference src/Tracking.cc:4112-4217, 4234-4300, 4742-4825) with every stage on the GPU and no host
+round trip between them:
+
+    SearchByProjection(CurrentFrame, LastFrame, th)         orb_search_by_projection_frame_device
+    Optimizer::PoseOptimization                             orb_tracking_pose_edges_device +
+                                                            orb_pose_optimization_device
+    Frame::isInFrustum of the local map at the new pose     orb_is_in_frustum_pose_device +
+        (points the first search assigned are skipped)      orb_tracking_local_seen_device
+    discard the outliers (nmatchesMap, SearchLocalPoints'   orb_tracking_discard_outliers_device
+        skip set)
+    SearchByProjection(Frame, local map points, th)         orb_search_by_projection_local_device
+    Optimizer::PoseOptimization                             (edges from both searches) + pose kernel
+
+isInFrustum and the seen marks run before the discard here: they read the first pose and the first
+search's assignments, which the discard does not change (the reference marks its discarded outliers
+seen too, src/Tracking.cc:4195), so the order gives the reference's result.
+
+The current frame is frame `f` of device arrays (ORBextractor.extract_batch_device, optionally
+undistort_keypoints_device, compute_stereo_matches_batch_device).  The last frame's tracked map points
+are a table indexed by its keypoints (Frame::mvpMapPoints with MapPoint::GetWorldPos / GetDescriptor /
+Observations); the local map (Tracking::mvpLocalMapPoints, as UpdateLocalMap leaves it) is a second
+table with the fields isInFrustum reads.  What the chain does not cover (the caller's): the motion
+model's pose prediction (mVelocity * mLastFrame.GetPose()), UpdateLocalMap's keyframe / point
+selection, the MapPoint counters (IncreaseVisible / IncreaseFound) and the IMU / relocalisation paths.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import POSE_EDGE_DTYPE, POSE_FRAME_DTYPE, check
+from .keyframe import FRAME_GRID_COLS, FRAME_GRID_ROWS, FrustumFrame, logf
+from .matcher import ORBmatcher
+
+
+class FrameDeviceView(ctypes.Structure):  # orb_frame_device_t
+    _fields_ = [("kps_un", ctypes.c_void_p), ("desc", ctypes.c_void_p), ("n", ctypes.c_void_p),
+                ("u_right", ctypes.c_void_p), ("cap", ctypes.c_int32), ("min_x", ctypes.c_float),
+                ("max_x", ctypes.c_float), ("min_y", ctypes.c_float), ("max_y", ctypes.c_float),
+                ("grid_inv_w", ctypes.c_float), ("grid_inv_h", ctypes.c_float), ("fx", ctypes.c_float),
+                ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float), ("bf", ctypes.c_float),
+                ("b", ctypes.c_float), ("nlevels", ctypes.c_int32), ("scale_factors", ctypes.c_void_p),
+                ("Tcw", ctypes.c_float * 12)]
+
+
+class LastPointsDeviceView(ctypes.Structure):  # orb_last_points_device_t
+    _fields_ = [("n", ctypes.c_void_p), ("cap", ctypes.c_int32), ("valid", ctypes.c_void_p),
+                ("observed", ctypes.c_void_p), ("xyz", ctypes.c_void_p), ("desc", ctypes.c_void_p),
+                ("kps_un", ctypes.c_void_p), ("Tcw", ctypes.c_float * 12)]
+
+
+class LocalPointsDeviceView(ctypes.Structure):  # orb_local_points_device_t
+    _fields_ = [("n", ctypes.c_int32), ("track_in_view", ctypes.c_void_p), ("is_bad", ctypes.c_void_p),
+                ("observed", ctypes.c_void_p), ("track_proj", ctypes.c_void_p), ("track_view_cos", ctypes.c_void_p),
+                ("track_depth", ctypes.c_void_p), ("track_level", ctypes.c_void_p), ("desc", ctypes.c_void_p)]
+
+
+def _stream_handle(stream, device):
+    import torch
+    st = stream if stream is not None else torch.cuda.current_stream(device)
+    return ctypes.c_void_p(st.cuda_stream)
+
+
+class DeviceFrame:
+    """A Frame whose features live on the GPU: frame `f` of kps_un [B, cap, 7] (cv::KeyPoint rows,
+    mvKeysUn), desc [B, cap, 32], counts [B, 2] (N at counts[f, 0]) and optionally u_right [B, cap]
+    (mvuRight).  Host fields: the pose Tcw (3 x 4), camera (fx, fy, cx, cy), mvScaleFactors,
+    mvLevelSigma2, mbf and the undistorted image bounds (mnMinX, mnMaxX, mnMinY, mnMaxY; default the
+    image rectangle, Frame::ComputeImageBounds without distortion, src/Frame.cc:1053-1100)."""
+
+    def __init__(self, kps_un, desc, counts, f: int, Tcw, camera, scale_factors, level_sigma2, width: int,
+                 height: int, bf: float = 0.0, u_right=None, bounds=None):
+        self._keep = (kps_un, desc, counts, u_right)
+        self.device = kps_un.device
+        self.cap = int(kps_un.shape[1])
+        self.f = int(f)
+        self.fx, self.fy, self.cx, self.cy = (float(np.float32(v)) for v in camera)
+        self.mvScaleFactors = np.ascontiguousarray(scale_factors, np.float32)
+        self.mvLevelSigma2 = np.ascontiguousarray(level_sigma2, np.float32)
+        self.mvInvLevelSigma2 = (np.float32(1.0) / self.mvLevelSigma2).astype(np.float32)  # src/Frame.cc:124
+        self.mbf = float(np.float32(bf))
+        self.mb = float(np.float32(np.float32(bf) / np.float32(self.fx))) if bf else 0.0
+        b = (0.0, float(width), 0.0, float(height)) if bounds is None else tuple(float(v) for v in bounds)
+        self.mnMinX, self.mnMaxX, self.mnMinY, self.mnMaxY = b
+        gw = float(np.float32(FRAME_GRID_COLS) / np.float32(self.mnMaxX - self.mnMinX))
+        gh = float(np.float32(FRAME_GRID_ROWS) / np.float32(self.mnMaxY - self.mnMinY))
+        cap, f = self.cap, self.f
+        self._view = FrameDeviceView(kps_un.data_ptr() + 28 * cap * f, desc.data_ptr() + 32 * cap * f,
+                                     counts.data_ptr() + 8 * f,
+                                     None if u_right is None else u_right.data_ptr() + 4 * cap * f, cap, self.mnMinX,
+                                     self.mnMaxX, self.mnMinY, self.mnMaxY, gw, gh, self.fx, self.fy, self.cx, self.cy,
+                                     self.mbf, self.mb, len(self.mvScaleFactors), self.mvScaleFactors.ctypes.data)
+        self.set_pose(Tcw)
+
+    def set_pose(self, Tcw) -> None:
+        self.Tcw = np.ascontiguousarray(Tcw, np.float32).reshape(3, 4)
+        self._view.Tcw[:] = [float(x) for x in self.Tcw.reshape(-1)]
+
+    def view(self) -> FrameDeviceView:
+        return self._view
+
+    def frustum_frame(self, scale_factor: float = 1.2) -> FrustumFrame:
+        """orb_frustum_frame_t of this frame (pose fields unused by orb_is_in_frustum_pose_device)."""
+        T = self.Tcw.reshape(12)
+        return FrustumFrame((ctypes.c_float * 12)(*T), (ctypes.c_float * 3)(0, 0, 0), self.fx, self.fy, self.cx,
+                            self.cy, self.mbf, self.mnMinX, self.mnMaxX, self.mnMinY, self.mnMaxY,
+                            float(logf(scale_factor)), len(self.mvScaleFactors))
+
+
+class DeviceLastPoints:
+    """The last frame's tracked map points, device arrays indexed like its keypoints: valid
+    (mvpMapPoints[i] && !mvbOutlier[i]), observed (Observations() > 0), xyz (GetWorldPos, cap x 3
+    float32), desc (GetDescriptor, cap x 32).  `frame` is the last frame (its keypoints, N and pose)."""
+
+    def __init__(self, frame: DeviceFrame, valid, observed, xyz, desc):
+        self.frame = frame
+        self._keep = (valid, observed, xyz, desc)
+        self.xyz = xyz
+        self.observed = observed
+        self.cap = frame.cap
+        fv = frame.view()
+        self._view = LastPointsDeviceView(fv.n, frame.cap, valid.data_ptr(), observed.data_ptr(), xyz.data_ptr(),
+                                          desc.data_ptr(), fv.kps_un)
+        self._view.Tcw[:] = list(fv.Tcw)
+
+    def view(self) -> LastPointsDeviceView:
+        self._view.Tcw[:] = list(self.frame.view().Tcw)
+        return self._view
+
+
+class DeviceLocalMap:
+    """Tracking::mvpLocalMapPoints as device arrays: pos / normal (n x 3, GetWorldPos / GetNormal),
+    min_dist / max_dist (mfMinDistance, mfMaxDistance), desc (n x 32), observed, is_bad and last_row
+    (the last frame's keypoint holding the point, -1: none; the mnLastFrameSeen skip).  Owns the
+    tracking fields isInFrustum writes (track_in_view, track_proj, track_depth, track_level,
+    track_view_cos)."""
+
+    def __init__(self, pos, normal, min_dist, max_dist, desc, observed, is_bad, last_row=None):
+        import torch
+        self.n = int(pos.shape[0])
+        self.device = pos.device
+        self.pos, self.normal, self.min_dist, self.max_dist = pos, normal, min_dist, max_dist
+        self.desc, self.observed, self.is_bad, self.last_row = desc, observed, is_bad, last_row
+        m = max(self.n, 1)
+        dev = self.device
+        self.track_in_view = torch.zeros(m, dtype=torch.uint8, device=dev)
+        self.track_proj = torch.zeros((m, 3), dtype=torch.float32, device=dev)
+        self.track_depth = torch.zeros(m, dtype=torch.float32, device=dev)
+        self.track_level = torch.zeros(m, dtype=torch.int32, device=dev)
+        self.track_view_cos = torch.zeros(m, dtype=torch.float32, device=dev)
+        self._view = LocalPointsDeviceView(self.n, self.track_in_view.data_ptr(), is_bad.data_ptr(),
+                                           observed.data_ptr(), self.track_proj.data_ptr(),
+                                           self.track_view_cos.data_ptr(), self.track_depth.data_ptr(),
+                                           self.track_level.data_ptr(), desc.data_ptr())
+
+    @classmethod
+    def from_host(cls, device, **arrays):
+        import torch
+        dt = dict(pos=np.float32, normal=np.float32, min_dist=np.float32, max_dist=np.float32, desc=np.uint8,
+                  observed=np.uint8, is_bad=np.uint8, last_row=np.int32)
+        t = {k: torch.from_numpy(np.ascontiguousarray(arrays[k], dt[k])).to(device) for k in dt if k in arrays}
+        return cls(**t)
+
+    def view(self) -> LocalPointsDeviceView:
+        return self._view
+
+
+class TrackResult:
+    """Device outputs of one TrackingChain.track call (valid once the stream reaches them)."""
+
+    def __init__(self, chain, stream):
+        self.chain, self.stream = chain, stream
+
+    def sync(self) -> dict:
+        """Wait for the stream and return host copies: n1 (SearchByProjection(LastFrame) matches), m1 /
+        m2 (per keypoint: the last-frame row / local map point assigned, m1 after the discard), pose1 /
+        pose2 (SE3Quat vectors), edges1 / edges2 (the PoseOptimization graphs), edge_kp1 / edge_kp2,
+        outlier1 / outlier2 (per edge), inliers (the PoseOptimization returns), n_kept (nmatches after
+        the discard), n_map (nmatchesMap), n2 (SearchByProjection(local) matches)."""
+        c = self.chain
+        self.stream.synchronize()
+        fr = c.frames.cpu().numpy().view(POSE_FRAME_DTYPE).reshape(2)
+        ne = [int(fr[0]["n_edges"]), int(fr[1]["n_edges"])]
+        out = dict(frames=fr, n1=int(c.n_match[0]), n2=int(c.n_match[1]), m1=c.m1.cpu().numpy(),
+                   m2=c.m2.cpu().numpy(), pose1=c.poses[0].cpu().numpy(), pose2=c.poses[1].cpu().numpy(),
+                   inliers=c.inliers.cpu().numpy(), n_kept=int(c.n_out[0]), n_map=int(c.n_out[1]))
+        for k in (0, 1):
+            out[f"edges{k + 1}"] = c.edges[k][:ne[k]].cpu().numpy().view(POSE_EDGE_DTYPE).reshape(-1)
+            out[f"edge_kp{k + 1}"] = c.edge_kp[k][:ne[k]].cpu().numpy()
+            out[f"outlier{k + 1}"] = c.outlier[k][:ne[k]].cpu().numpy().astype(bool)
+        return out
+
+
+class TrackingChain:
+    """Buffers and launch sequence for TrackWithMotionModel -> TrackLocalMap on frames of up to `cap`
+    keypoints (one chain object per concurrently tracked frame).  th_motion: 7 for stereo, 15
+    otherwise (src/Tracking.cc:4141-4146); th_local: SearchLocalPoints' th (1 for stereo / mono
+    without IMU, 3 for RGB-D, src/Tracking.cc:4801-4823); mono: bMono of the last-frame search."""
+
+    def __init__(self, cap: int, device=None, th_motion: float = 7, th_local: float = 1, mono: bool = False,
+                 far_points: bool = False, th_far_points: float = 20.0, viewing_cos_limit: float = 0.5,
+                 scale_factor: float = 1.2):
+        import torch
+        self.device = torch.device(device if device is not None else "cuda")
+        self.cap = int(cap)
+        self.th_motion, self.th_local, self.mono = float(th_motion), float(th_local), bool(mono)
+        self.far_points, self.th_far_points = bool(far_points), float(th_far_points)
+        self.viewing_cos_limit, self.scale_factor = float(viewing_cos_limit), float(scale_factor)
+        self.m_motion = ORBmatcher(0.9, True)   # TrackWithMotionModel's ORBmatcher(0.9, true)
+        self.m_local = ORBmatcher(0.8, True)    # SearchLocalPoints' ORBmatcher(0.8)
+        d, c = self.device, self.cap
+        self.m1 = torch.empty(c, dtype=torch.int32, device=d)
+        self.m2 = torch.empty(c, dtype=torch.int32, device=d)
+        self.n_match = torch.zeros(2, dtype=torch.int32, device=d)
+        self.frames = torch.zeros(2 * POSE_FRAME_DTYPE.itemsize, dtype=torch.uint8, device=d)
+        self.edges = [torch.empty((c, POSE_EDGE_DTYPE.itemsize), dtype=torch.uint8, device=d) for _ in range(2)]
+        self.edge_kp = [torch.empty(c, dtype=torch.int32, device=d) for _ in range(2)]
+        self.outlier = [torch.empty(c, dtype=torch.uint8, device=d) for _ in range(2)]
+        self.poses = torch.zeros((2, 7), dtype=torch.float64, device=d)
+        self.inliers = torch.zeros(2, dtype=torch.int32, device=d)
+        self.n_out = torch.zeros(2, dtype=torch.int32, device=d)
+        self.taken = torch.empty(c, dtype=torch.uint8, device=d)
+
+    def track(self, cur: DeviceFrame, last: DeviceLastPoints, local: DeviceLocalMap, pose7, stream=None,
+              wide: bool = False) -> TrackResult:
+        """Enqueue the chain for `cur` on `stream` (default: torch's current stream).  pose7: the motion
+        model's prediction as the SE3Quat vector PoseOptimization starts from (tx ty tz qx qy qz qw of
+        the frame's float pose); cur's Tcw must be the same pose.  wide: the 2 th retry of
+        TrackWithMotionModel (src/Tracking.cc:4153-4160); TrackResult's caller decides it from n1."""
+        import torch
+        if cur.cap > self.cap:
+            raise ValueError(f"frame capacity {cur.cap} exceeds the chain's {self.cap}")
+        lib = _lib.load()
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        s = ctypes.c_void_p(st.cuda_stream)
+        fv = cur.view()
+        fsz = POSE_FRAME_DTYPE.itemsize
+        fr0, fr1 = self.frames.data_ptr(), self.frames.data_ptr() + fsz
+        p0 = np.ascontiguousarray(pose7, np.float64).reshape(7)
+        isg = cur.mvInvLevelSigma2
+        nm = self.n_match.data_ptr()
+        th = self.th_motion * (2 if wide else 1)
+        check(lib.orb_search_by_projection_frame_device(self.m_motion._handle(), ctypes.byref(fv),
+                                                        ctypes.byref(last.view()), th, int(self.mono),
+                                                        self.m1.data_ptr(), nm, s),
+              "orb_search_by_projection_frame_device")
+        check(lib.orb_tracking_pose_edges_device(ctypes.byref(fv), self.m1.data_ptr(), last.xyz.data_ptr(), None, None,
+                                                 isg.ctypes.data, None, p0.ctypes.data, fr0, self.edges[0].data_ptr(),
+                                                 self.edge_kp[0].data_ptr(), s), "orb_tracking_pose_edges_device")
+        check(lib.orb_pose_optimization_device(1, fr0, cur.cap, self.edges[0].data_ptr(), self.poses[0].data_ptr(),
+                                               self.outlier[0].data_ptr(), self.inliers.data_ptr(), s),
+              "orb_pose_optimization_device")
+        ff = cur.frustum_frame(self.scale_factor)
+        check(lib.orb_is_in_frustum_pose_device(ctypes.byref(ff), self.poses[0].data_ptr(), local.n,
+                                                local.pos.data_ptr(), local.normal.data_ptr(),
+                                                local.min_dist.data_ptr(), local.max_dist.data_ptr(),
+                                                self.viewing_cos_limit, local.track_in_view.data_ptr(),
+                                                local.track_proj.data_ptr(), local.track_depth.data_ptr(),
+                                                local.track_level.data_ptr(), local.track_view_cos.data_ptr(), s),
+              "orb_is_in_frustum_pose_device")
+        if local.last_row is not None and local.n > 0:
+            check(lib.orb_tracking_local_seen_device(self.m1.data_ptr(), cur.cap, last.cap, local.last_row.data_ptr(),
+                                                     local.n, local.track_in_view.data_ptr(), s),
+                  "orb_tracking_local_seen_device")
+        check(lib.orb_tracking_discard_outliers_device(fr0, self.edge_kp[0].data_ptr(), self.outlier[0].data_ptr(),
+                                                       self.m1.data_ptr(), last.observed.data_ptr(), None, None,
+                                                       self.n_out.data_ptr(), cur.cap, self.taken.data_ptr(), s),
+              "orb_tracking_discard_outliers_device")
+        check(lib.orb_search_by_projection_local_device(self.m_local._handle(), ctypes.byref(fv),
+                                                        self.taken.data_ptr(), ctypes.byref(local.view()),
+                                                        self.th_local, int(self.far_points), self.th_far_points,
+                                                        self.m2.data_ptr(), nm + 4, s),
+              "orb_search_by_projection_local_device")
+        has_local = local.n > 0  # an empty local map: the second search assigned nothing
+        check(lib.orb_tracking_pose_edges_device(ctypes.byref(fv), self.m1.data_ptr(), last.xyz.data_ptr(),
+                                                 self.m2.data_ptr() if has_local else None,
+                                                 local.pos.data_ptr() if has_local else None, isg.ctypes.data,
+                                                 self.poses[0].data_ptr(), None, fr1, self.edges[1].data_ptr(),
+                                                 self.edge_kp[1].data_ptr(), s), "orb_tracking_pose_edges_device")
+        check(lib.orb_pose_optimization_device(1, fr1, cur.cap, self.edges[1].data_ptr(), self.poses[1].data_ptr(),
+                                               self.outlier[1].data_ptr(), self.inliers.data_ptr() + 4, s),
+              "orb_pose_optimization_device")
+        return TrackResult(self, st)

@@ -1,0 +1,126 @@
+"""The device-resident tracking chain (tracking.TrackingChain: Tracking::TrackWithMotionModel ->
+TrackLocalMap, src/Tracking.cc:4112-4217, 4234-4300, 4742-4825) against the same chain on the oracle:
+SearchByProjection(LastFrame) -> PoseOptimization -> outlier discard -> isInFrustum at the optimised
+pose (skipping the points the frame holds) -> SearchByProjection(local map) -> PoseOptimization.
+
+Two checks per scene.  Stage by stage: each oracle stage is fed the device's previous outputs, and its
+outputs must equal the device's bit for bit (matches, graphs, outlier flags, the discard's counts) --
+the poses within PoseOptimization's 1e-6 bar.  End to end: the oracle chain run on its own poses gives
+the same matches and outlier flags."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _device(pkg, sc, C, L):
+    import torch
+    dev = torch.device("cuda")
+
+    def up(a, dt):
+        return torch.from_numpy(np.ascontiguousarray(a, dt)).to(dev)
+
+    def dframe(F, pad=37):
+        # capacity past the count, filled with junk keypoints the chain must not read
+        rng = np.random.default_rng(F.N)
+        cap = F.N + pad
+        k = np.concatenate([F.mvKeysUn, F.mvKeysUn[rng.integers(0, F.N, pad)]])
+        d = np.concatenate([F.mDescriptors, rng.integers(0, 256, (pad, 32), dtype=np.uint8)])
+        kps = up(k.view(np.float32).reshape(1, cap, 7), np.float32)
+        desc = up(d.reshape(1, cap, 32), np.uint8)
+        counts = up(np.array([[F.N, 0]]), np.int32)
+        ur = None if F.mvuRight is None else up(np.concatenate([F.mvuRight, np.full(pad, 100, np.float32)]).reshape(1, cap),
+                                                np.float32)
+        return pkg.DeviceFrame(kps, desc, counts, 0, F.Tcw, sc["cur"]["camera"], F.mvScaleFactors, sc["level_sigma2"],
+                               int(F.mnMaxX), int(F.mnMaxY), F.mbf, ur)
+
+    cur, last = dframe(C), dframe(L)
+    mp = L.map_points
+    pad = last.cap - L.N
+
+    def padded(a, v):
+        return np.concatenate([a, np.full((pad,) + a.shape[1:], v, a.dtype)])
+    lastp = pkg.DeviceLastPoints(last, up(padded(mp["valid"], 1), np.uint8), up(padded(mp["observed"], 1), np.uint8),
+                                 up(padded(mp["xyz"], 1.0), np.float32), up(padded(mp["desc"], 0), np.uint8))
+    local = pkg.DeviceLocalMap.from_host(dev, **sc["local"])
+    return cur, lastp, local
+
+
+def _frames(pkg, sc):
+    return pkg.Frame(**sc["cur"]), pkg.Frame(**sc["last"])
+
+
+def _oracle_stages(pkg, sc, C, L, th_motion, th_local, pose1=None):
+    from oracle import tracking_chain
+    return tracking_chain.track(pkg, C, L, sc["local"], sc["pose7_pred"], sc["level_sigma2"], th_motion, th_local,
+                                pose1=pose1)
+
+
+@pytest.mark.parametrize("seed,stereo", [(81, True), (82, True), (83, False)])
+def test_tracking_chain_vs_oracle(pkg, oracle, synth, seed, stereo):
+    import torch
+    sc = synth.tracking_chain_scene(seed=seed, stereo=stereo)
+    C, L = _frames(pkg, sc)
+    th_motion = 7 if stereo else 15
+    cur, last, local = _device(pkg, sc, C, L)
+    chain = pkg.TrackingChain(cur.cap, th_motion=th_motion, th_local=1)
+    r = chain.track(cur, last, local, sc["pose7_pred"]).sync()
+    # stage by stage, the oracle fed the device's pose
+    o = _oracle_stages(pkg, sc, C, L, th_motion, 1, pose1=r["pose1"])
+    assert r["n1"] == o["n1"] > 100
+    assert np.array_equal(r["edges1"].view(np.uint8), o["e1"].view(np.uint8))
+    assert np.array_equal(r["edge_kp1"], o["kp1"])
+    assert np.array_equal(r["outlier1"], o["O1"]) and o["O1"].sum() > 0
+    assert np.abs(r["pose1"] - o["pose1"]).max() < 1e-6
+    assert r["inliers"][0] == o["I1"]
+    assert np.array_equal(r["m1"][:C.N], o["m1"])
+    assert (r["n_kept"], r["n_map"]) == (o["n_kept"], o["n_map"])
+    assert np.array_equal(chain.taken[:C.N].cpu().numpy(), o["taken"])
+    tiv = local.track_in_view[:local.n].cpu().numpy()
+    assert np.array_equal(tiv, o["in_view"])
+    assert (o["in_view"] == 0).sum() > (o["tf"]["track_in_view"] == 0).sum()  # the held points were skipped
+    for k in ("track_proj", "track_depth", "track_level", "track_view_cos"):
+        got = getattr(local, k)[:local.n].cpu().numpy()
+        assert np.array_equal(got[tiv == 1], o["tf"][k][tiv == 1]), k
+    assert r["n2"] == o["n2"] > 50
+    assert np.array_equal(r["m2"][:C.N], o["m2"])
+    assert np.array_equal(r["edges2"].view(np.uint8), o["e2"].view(np.uint8))
+    assert np.array_equal(r["edge_kp2"], o["kp2"])
+    assert np.array_equal(r["outlier2"], o["O2"])
+    assert np.abs(r["pose2"] - o["pose2"]).max() < 1e-6
+    assert r["inliers"][1] == o["I2"]
+    # end to end: the oracle on its own poses
+    e = _oracle_stages(pkg, sc, C, L, th_motion, 1)
+    for k in ("m1", "m2", "O1", "O2"):
+        assert np.array_equal(e[k], o[k]), k
+    assert np.abs(e["pose2"] - r["pose2"]).max() < 1e-6
+    # and the chain tracked: the final pose is closer to the truth than the prediction
+    t = sc["pose7_true"]
+    assert np.linalg.norm(r["pose2"][:3] - t[:3]) < 0.5 * np.linalg.norm(sc["pose7_pred"][:3] - t[:3])
+    torch.cuda.synchronize()
+
+
+def test_tracking_chain_reuse_and_no_local_map(pkg, oracle, synth):
+    """A chain object tracks several frames in turn (buffers reused, state from the previous frame not
+    leaking), and an empty local map leaves the second search without matches."""
+    import torch
+    chain = None
+    for seed in (84, 85):
+        sc = synth.tracking_chain_scene(seed=seed, n_points=1200)
+        C, L = _frames(pkg, sc)
+        cur, last, local = _device(pkg, sc, C, L)
+        chain = chain or pkg.TrackingChain(max(cur.cap, 4096))
+        r = chain.track(cur, last, local, sc["pose7_pred"]).sync()
+        o = _oracle_stages(pkg, sc, C, L, 7, 1, pose1=r["pose1"])
+        assert np.array_equal(r["m1"][:C.N], o["m1"]) and np.array_equal(r["m2"][:C.N], o["m2"])
+        assert (r["m1"][C.N:cur.cap] == -1).all() and (r["m2"][C.N:cur.cap] == -1).all()
+        assert np.abs(r["pose2"] - o["pose2"]).max() < 1e-6
+    sc = synth.tracking_chain_scene(seed=86, n_points=1200)
+    C, L = _frames(pkg, sc)
+    cur, last, _ = _device(pkg, sc, C, L)
+    empty = pkg.DeviceLocalMap.from_host(torch.device("cuda"), **{k: v[:0] for k, v in sc["local"].items()})
+    r = chain.track(cur, last, empty, sc["pose7_pred"]).sync()
+    assert r["n2"] == 0 and (r["m2"][:cur.cap] == -1).all()
+    assert r["n1"] > 100 and len(r["edges2"]) == r["n_kept"]
