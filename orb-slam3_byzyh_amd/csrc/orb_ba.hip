@@ -1682,7 +1682,10 @@ __global__ __launch_bounds__(kT) void k_u_edges_build(int ne, const EdgeDev* __r
 }
 
 // unit step 2 (build): Hpp/b_p (blocks [0, nf)), Hll/b_l (64 landmarks per block); the last block
-// sums chi2, takes max diag at iteration 0 and runs the build controller
+// sums chi2, takes max diag at iteration 0 and runs the build controller.  Sharded (dist): hpp / bp are
+// this rank's partial buffers, and the last block leaves its chi2 in sc_part[0] and its landmarks' max
+// diag in the rank's slot sc_part[4 + rank] (zero elsewhere: the SUM all-reduce gathers the slots) for
+// k_lm_build_ctl after the all-reduce
 __global__ __launch_bounds__(64) void k_u_reduce_build(int nf, int nl, const int32_t* __restrict__ pose_off,
                                                        const LandEdge* __restrict__ pose_edge, const double* __restrict__ ecp,
                                                        double* __restrict__ hpp, double* __restrict__ bp,
@@ -1691,7 +1694,7 @@ __global__ __launch_bounds__(64) void k_u_reduce_build(int nf, int nl, const int
                                                        const double* __restrict__ ecl, double* __restrict__ hll,
                                                        double* __restrict__ bl, const double* __restrict__ part,
                                                        int nparts, unsigned* counter, double* __restrict__ scal,
-                                                       LmState* st) {
+                                                       LmState* st, int dist, double* __restrict__ sc_part, int rank) {
     if (lm_skip(st, kGateBuild)) return;
     const int b = blockIdx.x, lane = threadIdx.x;
     if (b < nf) {
@@ -1707,7 +1710,7 @@ __global__ __launch_bounds__(64) void k_u_reduce_build(int nf, int nl, const int
     double md = 0.0;
     if (st->it == 0) {
         double m = 0;  // (max is order-independent: loads batched 8 per lane)
-        for (int i0 = lane; i0 < 6 * nf; i0 += 8 * 64) {
+        for (int i0 = lane; !dist && i0 < 6 * nf; i0 += 8 * 64) {  // (sharded: from the reduced Hpp later)
             double v[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
@@ -1737,14 +1740,48 @@ __global__ __launch_bounds__(64) void k_u_reduce_build(int nf, int nl, const int
         md = mx[0];
     }
     if (lane == 0) {
-        scal[0] = chi;
-        scal[3] = md;
-        lm_build_done(st, chi, md);
+        if (dist) {
+            sc_part[0] = chi;
+            sc_part[4 + rank] = md;
+        } else {
+            scal[0] = chi;
+            scal[3] = md;
+            lm_build_done(st, chi, md);
+        }
         *counter = 0;
     }
 }
 
-// unit step 4 (trial): S blocks (blocks [0, nblk), the upper triangle) and b_S (one block per free pose)
+// sharded build controller, after the all-reduce of the build partials: chi2 = sc_red[0]; at iteration
+// 0 max diag over the reduced Hpp and the ranks' landmark slots sc_red[4 .. 4 + world)
+__global__ __launch_bounds__(64) void k_lm_build_ctl(int nf, const double* __restrict__ hpp,
+                                                     const double* __restrict__ sc_red, int world,
+                                                     double* __restrict__ scal, LmState* st) {
+    if (lm_skip(st, kGateBuild)) return;
+    const int lane = threadIdx.x;
+    double md = 0.0;
+    if (st->it == 0) {
+        double m = 0;
+        for (int i = lane; i < 6 * nf; i += 64) m = fmax(m, fabs(hpp[36 * (size_t)(i / 6) + 7 * (i % 6)]));
+        for (int r = lane; r < world; r += 64) m = fmax(m, sc_red[4 + r]);
+        __shared__ double mx[64];
+        mx[lane] = m;
+        __syncthreads();
+        for (int w = 32; w >= 1; w >>= 1) {
+            if (lane < w) mx[lane] = fmax(mx[lane], mx[lane + w]);
+            __syncthreads();
+        }
+        md = mx[0];
+    }
+    if (lane == 0) {
+        scal[0] = sc_red[0];
+        scal[3] = md;
+        lm_build_done(st, sc_red[0], md);
+    }
+}
+
+// unit step 4 (trial): S blocks (blocks [0, nblk), the upper triangle) and b_S (one block per free pose).
+// Sharded: S / bs are this rank's partials and only rank 0 (primary) adds Hpp + lambda I and b_p.
 __global__ __launch_bounds__(64) void k_u_schur(int n, int nf, int nblk, const double* __restrict__ lam,
                                                 const int32_t* __restrict__ blk_off, const EdgePair* __restrict__ pairs,
                                                 const int32_t* __restrict__ cnt, const int32_t* __restrict__ pose_off,
@@ -1752,13 +1789,13 @@ __global__ __launch_bounds__(64) void k_u_schur(int n, int nf, int nblk, const d
                                                 const double* __restrict__ hpl, size_t hpl_alt,
                                                 const double* __restrict__ hpp, double* __restrict__ S,
                                                 const double* __restrict__ cb, const double* __restrict__ bp,
-                                                double* __restrict__ bs, const LmState* __restrict__ st) {
+                                                double* __restrict__ bs, const LmState* __restrict__ st, int primary) {
     if (lm_skip(st, kGateTrial)) return;
     hpl += hpl_cur(st, hpl_alt);
     if ((int)blockIdx.x < nblk)
-        ba_schur_block(blockIdx.x, threadIdx.x, n, nf, *lam, 1, blk_off, pairs, cnt, z, hpl, hpp, S);
+        ba_schur_block(blockIdx.x, threadIdx.x, n, nf, *lam, primary, blk_off, pairs, cnt, z, hpl, hpp, S);
     else
-        ba_schur_rhs(blockIdx.x - nblk, threadIdx.x, pose_off, pose_fl, cb, bp, 1, bs);
+        ba_schur_rhs(blockIdx.x - nblk, threadIdx.x, pose_off, pose_fl, cb, bp, primary, bs);
 }
 
 // unit step 6 (trial): x_l per landmark and its update, then the pose updates; a rejected previous
@@ -1774,7 +1811,7 @@ __global__ __launch_bounds__(kT) void k_u_backsub_update(int nl, int nf, int n, 
                                                          const int32_t* __restrict__ land_point, double* __restrict__ pose,
                                                          double* __restrict__ pose_bak, double* __restrict__ point,
                                                          double* __restrict__ point_bak, double* __restrict__ part2,
-                                                         const LmState* __restrict__ st) {
+                                                         const LmState* __restrict__ st, int pose_scale) {
     if (lm_skip(st, kGateTrial)) return;
     hpl += hpl_cur(st, hpl_alt);
     const bool rej = st->reject != 0;
@@ -1798,7 +1835,8 @@ __global__ __launch_bounds__(kT) void k_u_backsub_update(int nl, int nf, int n, 
         double* Tb = pose_bak + 7 * (size_t)free_pose[p];
         double v[7], u[6];
         for (int i = 0; i < 6; ++i) u[i] = x[6 * (size_t)p + i];
-        for (int i = 0; i < 6; ++i) c += u[i] * (lambda * u[i] + bp[6 * (size_t)p + i]);
+        if (pose_scale)  // (sharded: the pose rows' computeScale part on rank 0 only)
+            for (int i = 0; i < 6; ++i) c += u[i] * (lambda * u[i] + bp[6 * (size_t)p + i]);
         for (int i = 0; i < 7; ++i) {
             v[i] = rej ? Tb[i] : T[i];
             Tb[i] = v[i];
@@ -1825,7 +1863,8 @@ __global__ __launch_bounds__(kT) void k_u_edges_trial(int ne, const EdgeDev* __r
                                                       double* __restrict__ ecp, double* __restrict__ part,
                                                       unsigned* counter, const double* __restrict__ part2, int nparts2,
                                                       const int32_t* __restrict__ status, double* __restrict__ scal,
-                                                      LmState* st, LmProgress* prog) {
+                                                      LmState* st, LmProgress* prog, int dist, double* __restrict__ sc_part,
+                                                      const volatile int32_t* h_stop) {
     if (lm_skip(st, kGateTrial)) return;
     const int e = blockIdx.x * kT + threadIdx.x;
     double r = 0.0;
@@ -1841,12 +1880,38 @@ __global__ __launch_bounds__(kT) void k_u_edges_trial(int ne, const EdgeDev* __r
     const double chi = block_sum<kT>(c);
     const double scale = block_sum<kT>(d);
     if (threadIdx.x == 0) {
-        const bool failed = *status != 0;
-        scal[0] = chi;
-        scal[1] = scale;
-        scal[2] = failed ? 1.0 : 0.0;
-        lm_trial_done(st, chi, scale, failed, prog, kLin);
+        if (dist) {  // this rank's parts and its stop flag, for k_lm_trial_ctl after the all-reduce
+            sc_part[0] = chi;
+            sc_part[1] = scale;
+            sc_part[2] = (h_stop && *h_stop) ? 1.0 : 0.0;
+        } else {
+            const bool failed = *status != 0;
+            scal[0] = chi;
+            scal[1] = scale;
+            scal[2] = failed ? 1.0 : 0.0;
+            lm_trial_done(st, chi, scale, failed, prog, kLin);
+        }
         *counter = 0;
+    }
+}
+
+// sharded trial controller, after the all-reduce of the trial partials (sc_red: chi2, computeScale,
+// the number of ranks whose stop flag is raised): every rank takes the same decision; a raised flag
+// on any rank ends the solve after this trial (g2o's force-stop flag, tested between iterations)
+template <bool kLin>
+__global__ __launch_bounds__(64) void k_lm_trial_ctl(const double* __restrict__ sc_red, const int32_t* __restrict__ status,
+                                                     double* __restrict__ scal, LmState* st, LmProgress* prog) {
+    if (lm_skip(st, kGateTrial)) return;
+    if (threadIdx.x != 0) return;
+    const bool failed = *status != 0;
+    scal[0] = sc_red[0];
+    scal[1] = sc_red[1];
+    scal[2] = failed ? 1.0 : 0.0;
+    lm_trial_done(st, sc_red[0], sc_red[1], failed, prog, kLin);
+    if (sc_red[2] > 0 && !st->done) {
+        st->done = 1;
+        prog->done = 1;
+        __threadfence_system();
     }
 }
 
@@ -1969,6 +2034,12 @@ struct orb_ba_s {
     double* h_red = nullptr;  // pinned staging of the host reducer
     size_t h_red_cap = 0;
     DevBuf<double> red_buf;
+    // sharded device-driven loop: this rank's partials (all-reduced out of place into the solve's
+    // buffers: a gated no-op unit re-reduces unchanged partials into unchanged sums) and the stop flag
+    // the host raises for the trial controller (pinned)
+    DevBuf<double> dpart;
+    int32_t* h_stop = nullptr;
+    bool force_dist = false;  // ORBGPU_BA_DIST_FORCE=1 with a one-rank RCCL communicator (tests)
     DevBuf<int64_t> trace;  // ORBGPU_BA_TRACE stamps (debug)
     // k_ba_chol_rows: published tiles / y, the epoch + flag words (zeroed when allocated), row scratch
     DevBuf<double> lpub, ypub, racc;
@@ -2029,6 +2100,7 @@ int orb_ba_create(orb_ba_t* out) {
         hipStreamCreateWithFlags(&h->tail, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc(&h->h_scal, 8 * sizeof(double), hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&h->h_prog, sizeof(LmProgress), hipHostMallocDefault) != hipSuccess || !h->lm.grow(1) ||
+        hipHostMalloc(&h->h_stop, sizeof(int32_t), hipHostMallocDefault) != hipSuccess ||
         hipEventCreateWithFlags(&h->unit_ev[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->unit_ev[1], hipEventDisableTiming) != hipSuccess) {
         delete h;
@@ -2051,6 +2123,8 @@ int orb_ba_destroy(orb_ba_t h) {
     if (h->h_stage) hipHostFree(h->h_stage);
     if (h->h_dl) hipHostFree(h->h_dl);
     if (h->h_prog) hipHostFree(h->h_prog);
+    if (h->h_stop) hipHostFree(h->h_stop);
+    h->dpart.release();
     for (hipEvent_t e : h->unit_ev)
         if (e) hipEventDestroy(e);
     if (h->unit_exec) hipGraphExecDestroy(h->unit_exec);
@@ -2110,9 +2184,12 @@ namespace {
 
 // RCCL entry points, resolved from the librccl.so.1 already loaded in the process (torch's) or from
 // /opt/rocm/lib: no link-time dependency, one RCCL instance per process.
+struct NcclUniqueId {  // ncclUniqueId: 128 opaque bytes, passed BY VALUE to ncclCommInitRank
+    char internal[128];
+};
 struct Rccl {
     typedef int (*GetUniqueId)(void*);
-    typedef int (*CommInitRank)(void**, int, const void*, int);
+    typedef int (*CommInitRank)(void**, int, NcclUniqueId, int);
     typedef int (*AllReduce)(const void*, void*, size_t, int, int, void*, hipStream_t);
     typedef int (*CommDestroy)(void*);
     GetUniqueId get_id = nullptr;
@@ -2137,7 +2214,7 @@ constexpr int kNcclDouble = 8, kNcclSum = 0, kNcclMax = 2;  // ncclDataType_t / 
 
 // In-place all-reduce of n doubles at device address d (stream-ordered); no-op on one rank.
 bool dev_reduce(orb_ba_s* h, double* d, size_t n, int op) {
-    if (h->world <= 1 || n == 0) return true;
+    if ((h->world <= 1 && !h->force_dist) || n == 0) return true;
     if (h->nccl_comm)
         return g_rccl.all_reduce(d, d, n, kNcclDouble, op == ORB_BA_MAX ? kNcclMax : kNcclSum, h->nccl_comm,
                                  h->stream) == 0;
@@ -2155,6 +2232,17 @@ bool dev_reduce(orb_ba_s* h, double* d, size_t n, int op) {
     return hipMemcpyAsync(d, h->h_red, n * sizeof(double), hipMemcpyHostToDevice, h->stream) == hipSuccess;
 }
 
+// Out-of-place all-reduce of n doubles, send -> recv (stream-ordered with RCCL; the host reducer
+// synchronises the stream).
+bool dev_reduce2(orb_ba_s* h, const double* send, double* recv, size_t n, int op) {
+    if (n == 0) return true;
+    if (h->nccl_comm)
+        return g_rccl.all_reduce(send, recv, n, kNcclDouble, op == ORB_BA_MAX ? kNcclMax : kNcclSum, h->nccl_comm,
+                                 h->stream) == 0;
+    if (hipMemcpyAsync(recv, send, n * sizeof(double), hipMemcpyDeviceToDevice, h->stream) != hipSuccess) return false;
+    return h->world <= 1 || dev_reduce(h, recv, n, op);
+}
+
 }  // namespace
 
 int orb_ba_dist_unique_id(uint8_t id[128]) {
@@ -2169,11 +2257,19 @@ int orb_ba_dist_init_rccl(orb_ba_t h, const uint8_t id[128], int world, int rank
     if (!g_rccl.load()) return orbgpu_fail(ORB_ERR_DEVICE, "librccl.so.1 not found");
     if (h->nccl_comm) g_rccl.destroy(h->nccl_comm);
     h->nccl_comm = nullptr;
-    if (world > 1 && g_rccl.init(&h->nccl_comm, world, id, rank) != 0)
+    NcclUniqueId uid;
+    memcpy(uid.internal, id, sizeof(uid.internal));
+    if (g_rccl.init(&h->nccl_comm, world, uid, rank) != 0) {
+        h->nccl_comm = nullptr;
         return orbgpu_fail(ORB_ERR_DEVICE, "ncclCommInitRank failed");
+    }
     h->world = world;
     h->rank = rank;
     h->host_fn = nullptr;
+    // ORBGPU_BA_DIST_FORCE=1: a one-rank communicator still takes the sharded path (its collectives are
+    // RCCL calls on one rank), so the sharded device loop and RCCL run on a one-GPU box
+    const char* fd = getenv("ORBGPU_BA_DIST_FORCE");
+    h->force_dist = world == 1 && fd && !strcmp(fd, "1");
     return ORB_OK;
 }
 
@@ -2182,6 +2278,7 @@ int orb_ba_dist_init_host(orb_ba_t h, orb_ba_host_reduce_fn fn, void* ctx, int w
         return orbgpu_fail(ORB_ERR_ARG, "bad host reducer arguments");
     if (h->nccl_comm) g_rccl.destroy(h->nccl_comm);
     h->nccl_comm = nullptr;
+    h->force_dist = false;
     h->host_fn = fn;
     h->host_ctx = ctx;
     h->world = world;
@@ -2237,7 +2334,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         if (E.point < 0 || E.point >= nq || E.pose < 0 || E.pose >= np || (E.stereo != 0 && E.stereo != 1))
             return orbgpu_fail(ORB_ERR_ARG, "BA edge references a missing vertex");
     }
-    const bool dist = h->world > 1;
+    const bool dist = h->world > 1 || h->force_dist;
     const bool primary = h->rank == 0;
     hipStream_t s = h->stream;
     if (!h->scal.grow(8)) return orbgpu_fail(ORB_ERR_DEVICE, "BA scalar buffer");
@@ -2315,8 +2412,8 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
               st.add(h->blk_off, T.blk_off) && h->blk_cnt.grow(std::max(nblk, 1)) &&
               h->pairs.grow(std::max<size_t>(1, (size_t)T.blk_off[nblk])) &&
               h->err.grow(3 * ne1) && h->rho0.grow(ne1) && h->ecl.grow(12 * ne1) && h->hpl.grow(36 * ne1) &&
-              h->ecp.grow(42 * ne1) && h->hpp.grow(36 * (size_t)nf) && h->hll.grow(9 * (size_t)nl) && h->b.grow(n + m) &&
-              h->z.grow(18 * ne1) && h->cb.grow(6 * ne1) && h->S.grow((size_t)n * n) && h->bs.grow(n) &&
+              h->ecp.grow(42 * ne1) && h->hpp.grow(36 * (size_t)nf + n + m) && h->hll.grow(9 * (size_t)nl) &&
+              h->z.grow(18 * ne1) && h->cb.grow(6 * ne1) && h->S.grow((size_t)n * n + n) &&
               h->depth.grow(ne1) && h->part.grow(grid(ne) + grid(nl + nf)) &&
               // cleared by the scatter launch: g2o's _x starts zeroed, the scalars, the factorisation
               // status, the last-block counters of the unit kernels; and the device LM state's start
@@ -2357,6 +2454,12 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         if (ok) h->h_dl_cap = dl_bytes;
     }
     if (agree_fail(!ok)) return orbgpu_fail(ORB_ERR_DEVICE, "BA device allocation / upload");
+    // [Hpp | b_p | b_l] and [S | b_S] are contiguous: a sharded solve all-reduces [Hpp | b_p] and
+    // [S | b_S] in one collective each
+    double* const HPP = h->hpp.p;
+    double* const BV = HPP + 36 * (size_t)nf;
+    double* const SS = h->S.p;
+    double* const BSV = SS + (size_t)n * n;
 
     const float dm = (float)std::sqrt(5.991), ds = (float)std::sqrt(7.815);  // src/Optimizer.cc:1957-1958
     const Huber2 hub{(double)dm, (double)ds, (float)((double)dm * (double)dm), (float)((double)ds * (double)ds)};
@@ -2396,12 +2499,12 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     auto launch_chol = [&](const LmState* g) {
         if (use_rows) {
             if (rows_lds)
-                hipLaunchKernelGGL(k_ba_chol_rows<true>, dim3(NT), dim3(kRowThreads), rows_lds_bytes, s, n, h->S.p,
-                                   h->bs.p, h->x.p, h->status.p, h->lpub.p, h->ypub.p, h->cflag.p, h->racc.p, g,
+                hipLaunchKernelGGL(k_ba_chol_rows<true>, dim3(NT), dim3(kRowThreads), rows_lds_bytes, s, n, SS,
+                                   BSV, h->x.p, h->status.p, h->lpub.p, h->ypub.p, h->cflag.p, h->racc.p, g,
                                    (int)kGateTrial);
             else
-                hipLaunchKernelGGL(k_ba_chol_rows<false>, dim3(NT), dim3(kRowThreads), rows_lds_bytes, s, n, h->S.p,
-                                   h->bs.p, h->x.p, h->status.p, h->lpub.p, h->ypub.p, h->cflag.p, h->racc.p, g,
+                hipLaunchKernelGGL(k_ba_chol_rows<false>, dim3(NT), dim3(kRowThreads), rows_lds_bytes, s, n, SS,
+                                   BSV, h->x.p, h->status.p, h->lpub.p, h->ypub.p, h->cflag.p, h->racc.p, g,
                                    (int)kGateTrial);
             return;
         }
@@ -2411,19 +2514,20 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
             tr = h->trace.p;
         }
         hipLaunchKernelGGL((k_ba_chol_mf2<kMf2TileWaves>), dim3(1), dim3((kMf2TileWaves + 1) * 64), kMf2Lds, s, n,
-                           h->S.p, h->bs.p, h->x.p, h->status.p, tr, g, (int)kGateTrial);
+                           SS, BSV, h->x.p, h->status.p, tr, g, (int)kGateTrial);
         if (tr) {
             trace_left = 0;
             dump_chol_trace(tr, n, s);
         }
     };
-    double* bl = h->b.p + n;
+    double* bl = BV + n;
     const size_t hpl_alt = 18 * ne1;  // the second half of the double-buffered Hpl
-    // The device-driven LM loop (one process): no host round trip per trial.  The host-driven loop
-    // serves the sharded solve (its all-reduces are host calls) and ORBGPU_BA_HOST_LM=1 (tested in
+    // The device-driven LM loop: no host round trip per trial.  Sharded, its all-reduces are
+    // stream-ordered RCCL calls between the unit's launches (every rank reduces to the same values and
+    // takes the same LM decisions).  The host-driven loop serves ORBGPU_BA_HOST_LM=1 (tested in
     // tests/test_ba_gpu.py against the oracle).
     static const bool host_lm_env = getenv("ORBGPU_BA_HOST_LM") != nullptr;
-    const bool dev_lm = !dist && !host_lm_env;
+    const bool dev_lm = !host_lm_env;
     const LmState* G = dev_lm ? h->lm.p : nullptr;            // gate source for every per-trial kernel
     const double* lam = dev_lm ? &h->lm.p->lambda : h->h_scal + 5;  // the trial's lambda (device / pinned)
     // ---- computeActiveErrors + activeRobustChi2 + buildSystem
@@ -2437,15 +2541,15 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                                h->ecl.p, h->hll.p, bl, G, (int)kGateBuild);
         if (nf) {
             hipLaunchKernelGGL(k_ba_reduce_pose, dim3(nf), dim3(64), 0, s, h->pose_off.p, h->pose_fl.p, h->ecp.p,
-                               h->hpp.p, h->b.p, G, (int)kGateBuild);
-            if (!dev_reduce(h, h->hpp.p, 36 * (size_t)nf, ORB_BA_SUM) || !dev_reduce(h, h->b.p, n, ORB_BA_SUM))
+                               HPP, BV, G, (int)kGateBuild);
+            if (!dev_reduce(h, HPP, 36 * (size_t)nf, ORB_BA_SUM) || !dev_reduce(h, BV, n, ORB_BA_SUM))
                 return false;
         }
         if (first)  // (on the device path the gate limits it to iteration 0)
-            hipLaunchKernelGGL(k_ba_maxdiag, dim3(1), dim3(kT), 0, s, nf, nl, h->hpp.p, h->hll.p, h->scal.p + 3, G,
+            hipLaunchKernelGGL(k_ba_maxdiag, dim3(1), dim3(kT), 0, s, nf, nl, HPP, h->hll.p, h->scal.p + 3, G,
                                (int)kGateBuild0);
         hipLaunchKernelGGL(k_ba_sums, dim3(1), dim3(1024), 0, s, ne, h->rho0.p, primary ? 0 : n, n + m, lam,
-                           (const double*)nullptr, h->b.p, h->status.p, h->scal.p, dev_lm || dist ? nullptr : h->h_scal,
+                           (const double*)nullptr, BV, h->status.p, h->scal.p, dev_lm || dist ? nullptr : h->h_scal,
                            G, (int)kGateBuild);
         return true;
     };
@@ -2456,10 +2560,10 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                                h->hll.p, bl, h->hpl.p, hpl_alt, h->z.p, h->cb.p, G, (int)kGateTrial);
         if (nf) {
             hipLaunchKernelGGL(k_ba_schur_blocks, dim3(nblk), dim3(64), 0, s, n, nf, lam, primary ? 1 : 0, h->blk_off.p,
-                               h->pairs.p, h->blk_cnt.p, h->z.p, h->hpl.p, h->hpp.p, h->S.p, G, (int)kGateTrial);
-            hipLaunchKernelGGL(k_ba_schur_rhs, dim3(nf), dim3(64), 0, s, h->pose_off.p, h->pose_fl.p, h->cb.p, h->b.p,
-                               primary ? 1 : 0, h->bs.p, G, (int)kGateTrial);
-            if (!dev_reduce(h, h->S.p, (size_t)n * n, ORB_BA_SUM) || !dev_reduce(h, h->bs.p, n, ORB_BA_SUM))
+                               h->pairs.p, h->blk_cnt.p, h->z.p, h->hpl.p, HPP, SS, G, (int)kGateTrial);
+            hipLaunchKernelGGL(k_ba_schur_rhs, dim3(nf), dim3(64), 0, s, h->pose_off.p, h->pose_fl.p, h->cb.p, BV,
+                               primary ? 1 : 0, BSV, G, (int)kGateTrial);
+            if (!dev_reduce(h, SS, (size_t)n * n, ORB_BA_SUM) || !dev_reduce(h, BSV, n, ORB_BA_SUM))
                 return false;
             launch_chol(G);
         } else if (!dev_lm) {
@@ -2475,7 +2579,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                                h->point.p, h->pose_h.p, hub, h->err.p, h->rho0.p, h->ecl.p, h->hpl.p, h->ecp.p, G,
                                (int)kGateTrial);
         hipLaunchKernelGGL(k_ba_sums, dim3(1), dim3(1024), 0, s, ne, h->rho0.p, primary ? 0 : n, n + m, lam,
-                           (const double*)h->x.p, h->b.p, h->status.p, h->scal.p,
+                           (const double*)h->x.p, BV, h->status.p, h->scal.p,
                            dev_lm || dist ? nullptr : h->h_scal, G, (int)kGateTrial);
         return true;
     };
@@ -2501,6 +2605,12 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         // unit's event; once the solve is done the queued unit is a run of no-op launches.
         // (the state's start, the counters and the status went up with the inputs)
         memset(h->h_prog, 0, sizeof(LmProgress));
+        *h->h_stop = 0;
+        if (dist) {  // the partial buffers; the scalar slots must start at zero (the ranks' max diag slots)
+            const size_t nd = 36 * (size_t)nf + n + (size_t)n * n + n + 2 * (size_t)(4 + h->world + 4);
+            const bool okp = h->dpart.grow(nd) && hipMemsetAsync(h->dpart.p, 0, nd * sizeof(double), s) == hipSuccess;
+            if (agree_fail(!okp)) return orbgpu_fail(ORB_ERR_DEVICE, "BA sharded buffers");
+        }
         const int nparts = (int)grid(ne), nparts2 = (int)grid(nl + nf);  // partials: edge blocks, vertex blocks
         LmState* L = h->lm.p;
         // one unit = 6 launches: reductions (+ chi2, max diag, build controller), Schur edges, Schur
@@ -2517,35 +2627,61 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                                h->part.p, (const LmState*)L);
         };
         if (trial_lin) launch_edges_build();
+        // sharded: the partials [Hpp | b_p], [S | b_S], the build scalars (chi2, slots of the ranks'
+        // max diag at 4 + r) and the trial scalars (chi2, computeScale, stop), then their sums
+        const int nsb = 4 + h->world;
+        double* const p_hb = dist ? h->dpart.p : nullptr;
+        double* const p_sb = dist ? p_hb + 36 * (size_t)nf + n : nullptr;
+        double* const p_scb = dist ? p_sb + (size_t)n * n + n : nullptr;
+        double* const p_sct = dist ? p_scb + nsb : nullptr;
+        double* const r_scb = dist ? p_sct + 4 : nullptr;
+        double* const r_sct = dist ? r_scb + nsb : nullptr;
+        bool coll_ok = true;
         auto unit_launches = [&]() {
             if (!trial_lin) launch_edges_build();
             hipLaunchKernelGGL(k_u_reduce_build, dim3(nf + grid(nl, 64)), dim3(64), 0, s, nf, nl, h->pose_off.p,
-                               h->pose_fl.p, h->ecp.p, h->hpp.p, h->b.p, h->land_off.p, h->land_edge.p, h->ecl.p,
-                               h->hll.p, bl, h->part.p, nparts, h->counters.p, h->scal.p, L);
+                               h->pose_fl.p, h->ecp.p, dist ? p_hb : HPP, dist ? p_hb + 36 * (size_t)nf : BV,
+                               h->land_off.p, h->land_edge.p, h->ecl.p, h->hll.p, bl, h->part.p, nparts, h->counters.p,
+                               h->scal.p, L, dist ? 1 : 0, p_scb, h->rank);
+            if (dist) {
+                coll_ok = coll_ok && dev_reduce2(h, p_hb, HPP, 36 * (size_t)nf + n, ORB_BA_SUM) &&
+                          dev_reduce2(h, p_scb, r_scb, nsb, ORB_BA_SUM);
+                hipLaunchKernelGGL(k_lm_build_ctl, dim3(1), dim3(64), 0, s, nf, (const double*)HPP, (const double*)r_scb,
+                                   h->world, h->scal.p, L);
+            }
             if (nfe)
                 hipLaunchKernelGGL(k_ba_schur_edges, dim3(grid(nfe)), dim3(kT), 0, s, nfe, lam, h->landf_edge.p,
                                    h->fland.p, h->hll.p, bl, h->hpl.p, hpl_alt, h->z.p, h->cb.p, (const LmState*)L,
                                    (int)kGateTrial);
             if (nf) {
                 hipLaunchKernelGGL(k_u_schur, dim3(nblk + nf), dim3(64), 0, s, n, nf, nblk, lam, h->blk_off.p,
-                                   h->pairs.p, h->blk_cnt.p, h->pose_off.p, h->pose_fl.p, h->z.p, h->hpl.p, hpl_alt, h->hpp.p, h->S.p, h->cb.p, h->b.p, h->bs.p,
-                                   (const LmState*)L);
+                                   h->pairs.p, h->blk_cnt.p, h->pose_off.p, h->pose_fl.p, h->z.p, h->hpl.p, hpl_alt, HPP,
+                                   dist ? p_sb : SS, h->cb.p, BV, dist ? p_sb + (size_t)n * n : BSV, (const LmState*)L,
+                                   primary ? 1 : 0);
+                if (dist) coll_ok = coll_ok && dev_reduce2(h, p_sb, SS, (size_t)n * n + n, ORB_BA_SUM);
                 launch_chol((const LmState*)L);
             }
             hipLaunchKernelGGL(k_u_backsub_update, dim3(nparts2), dim3(kT), 0, s, nl, nf, n, lam, h->landf_off.p,
-                               h->landf_edge.p, h->landf_row.p, h->hpl.p, hpl_alt, bl, h->hll.p, h->x.p, h->b.p,
+                               h->landf_edge.p, h->landf_row.p, h->hpl.p, hpl_alt, bl, h->hll.p, h->x.p, BV,
                                h->free_pose.p, h->land_point.p, h->pose.p, h->pose_bak.p, h->point.p, h->point_bak.p,
-                               h->part.p + nparts, (const LmState*)L);
-            hipLaunchKernelGGL(trial_lin ? k_u_edges_trial<true> : k_u_edges_trial<false>, dim3(nparts), dim3(kT), 0, s, ne, h->edges.p, h->cams.p, h->pose.p,
-                               h->point.p, h->pose_h.p, hub, h->err.p, h->rho0.p, h->ecl.p, h->hpl.p, hpl_alt, h->ecp.p,
-                               h->part.p, h->counters.p + 1, h->part.p + nparts, nparts2, h->status.p, h->scal.p, L,
-                               h->h_prog);
+                               h->part.p + nparts, (const LmState*)L, primary ? 1 : 0);
+            hipLaunchKernelGGL(trial_lin ? k_u_edges_trial<true> : k_u_edges_trial<false>, dim3(nparts), dim3(kT), 0, s,
+                               ne, h->edges.p, h->cams.p, h->pose.p, h->point.p, h->pose_h.p, hub, h->err.p, h->rho0.p,
+                               h->ecl.p, h->hpl.p, hpl_alt, h->ecp.p, h->part.p, h->counters.p + 1, h->part.p + nparts,
+                               nparts2, h->status.p, h->scal.p, L, h->h_prog, dist ? 1 : 0, p_sct,
+                               (const volatile int32_t*)h->h_stop);
+            if (dist) {
+                coll_ok = coll_ok && dev_reduce2(h, p_sct, r_sct, 4, ORB_BA_SUM);
+                hipLaunchKernelGGL(trial_lin ? k_lm_trial_ctl<true> : k_lm_trial_ctl<false>, dim3(1), dim3(64), 0, s,
+                                   (const double*)r_sct, (const int32_t*)h->status.p, h->scal.p, L, h->h_prog);
+            }
         };
         // Every unit launches the same kernels with the same arguments (the device state gates them),
         // so the unit is captured once as a graph and replayed: one graph launch instead of 7 kernel
         // launches per trial.  The capture is kept while the arguments (sizes, buffers) are unchanged.
         auto dbits = [](double v) { uintptr_t u; memcpy(&u, &v, sizeof(u)); return u; };
-        bool use_graph = !trace_left;  // (the trace dump synchronises the stream: not capturable)
+        bool use_graph = !trace_left && !dist;  // (the trace dump synchronises the stream: not capturable;
+                                                // sharded, the collectives stay direct calls)
         // two units per graph launch: each launch boundary costs ~13 us on the device, a gated no-op
         // unit behind the last trial less (C5 solve 1.89 -> 1.87 ms against one unit; three: 1.89)
         // With a stop flag, one unit per launch: the host polls the flag after every launch, so at
@@ -2558,11 +2694,11 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                 (uintptr_t)h->edges.p, (uintptr_t)h->cams.p, (uintptr_t)h->pose.p, (uintptr_t)h->point.p,
                 (uintptr_t)h->pose_h.p, (uintptr_t)h->err.p, (uintptr_t)h->rho0.p, (uintptr_t)h->ecl.p,
                 (uintptr_t)h->hpl.p, (uintptr_t)h->ecp.p, (uintptr_t)h->part.p, (uintptr_t)h->pose_off.p,
-                (uintptr_t)h->pose_fl.p, (uintptr_t)h->hpp.p, (uintptr_t)h->b.p, (uintptr_t)h->land_off.p,
+                (uintptr_t)h->pose_fl.p, (uintptr_t)HPP, (uintptr_t)BV, (uintptr_t)h->land_off.p,
                 (uintptr_t)h->land_edge.p, (uintptr_t)h->hll.p, (uintptr_t)h->counters.p, (uintptr_t)h->scal.p,
                 (uintptr_t)L, (uintptr_t)lam, (uintptr_t)h->landf_edge.p, (uintptr_t)h->fland.p, (uintptr_t)h->z.p,
-                (uintptr_t)h->cb.p, (uintptr_t)h->S.p, (uintptr_t)h->blk_off.p, (uintptr_t)h->pairs.p,
-                (uintptr_t)h->blk_cnt.p, (uintptr_t)h->bs.p,
+                (uintptr_t)h->cb.p, (uintptr_t)SS, (uintptr_t)h->blk_off.p, (uintptr_t)h->pairs.p,
+                (uintptr_t)h->blk_cnt.p, (uintptr_t)BSV,
                 (uintptr_t)h->x.p, (uintptr_t)h->status.p, (uintptr_t)h->landf_off.p, (uintptr_t)h->landf_row.p, (uintptr_t)h->free_pose.p,
                 (uintptr_t)h->land_point.p, (uintptr_t)h->pose_bak.p, (uintptr_t)h->point_bak.p, (uintptr_t)h->h_prog,
                 (uintptr_t)use_rows, (uintptr_t)trial_lin, (uintptr_t)h->lpub.p, (uintptr_t)h->ypub.p, (uintptr_t)h->cflag.p,
@@ -2587,6 +2723,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
             }
         }
         auto unit = [&](int u) -> bool {
+            if (dist) *h->h_stop = stop_requested(opt) ? 1 : 0;  // read by the trial's last block
             if (use_graph) {
                 if (hipGraphLaunch(h->unit_exec, s) != hipSuccess) return false;
             } else {
@@ -2610,8 +2747,11 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                         return orbgpu_fail(ORB_ERR_DEVICE, "BA device error");
                     rs = h->tail;
                 }
+                if (!coll_ok) return orbgpu_fail(ORB_ERR_DEVICE, "BA collective failed");
                 if (h->h_prog->done || !more) break;
-                if (stop_requested(opt)) break;  // (the queued unit is live: the tail stays on s)
+                // (the queued unit is live: the tail stays on s; sharded, the ranks agree on the stop on
+                // the device instead, so that every rank launches the same collectives)
+                if (!dist && stop_requested(opt)) break;
             }
         }
         launch_restore();  // undo a rejected last trial (gated on the device state)
@@ -2713,8 +2853,9 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         if (point_l[q] >= 0 || (primary && qdeg[q] == 0))
             for (int k = 0; k < 3; ++k) contrib[3 * (size_t)q + k] = pts[3 * (size_t)q + k];
     for (int e = 0; e < ne; ++e) {
-        contrib[3 * (size_t)nq + lmap[e]] = lchi[e];
-        contrib[3 * (size_t)nq + ne_all + lmap[e]] = ldep[e] ? 1.0 : 0.0;
+        const int ge = lmap.empty() ? e : lmap[e];  // (one rank: the structure keeps the edge order)
+        contrib[3 * (size_t)nq + ge] = lchi[e];
+        contrib[3 * (size_t)nq + ne_all + ge] = ldep[e] ? 1.0 : 0.0;
     }
     if (!h->red_buf.grow(nred) ||
         hipMemcpyAsync(h->red_buf.p, contrib.data(), nred * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess ||

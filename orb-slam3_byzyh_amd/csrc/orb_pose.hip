@@ -40,7 +40,8 @@ namespace {
 #endif
 constexpr int kPT = ORB_POSE_THREADS;  // threads per frame
 constexpr int kPW = kPT / 64;          // waves
-constexpr int kEdgeSlots = 512 / kPT;  // edges per thread kept in registers (512 per frame)
+constexpr int kEdgeSlots = 512 / kPT;   // edges per thread kept in registers (512 per frame)
+constexpr int kLdsSlots = 1536 / kPT;   // and in LDS (the next 1536)
 static_assert(kPT % 64 == 0 && kEdgeSlots >= 1 && kPW <= 32, "pose workgroup shape");
 
 static_assert(sizeof(orb_pose_edge_t) == 56, "pose edge layout");
@@ -170,87 +171,137 @@ __device__ __forceinline__ double rcp_nr(double d) {
     return fma(r, e, r);
 }
 
-// LDL^T of the 6x6 symmetric matrix given as its upper triangle row by row (LinearSolverDense:
-// Eigen::LDLT; the same solution up to rounding); one reciprocal per pivot
-__device__ __forceinline__ bool ldlt6(const double (&U)[21], double lambda, const double (&b)[6], double (&x)[6]) {
-    double A[36];
-    {
-        int k = 0;
-#pragma unroll
-        for (int i = 0; i < 6; ++i)
-#pragma unroll
-            for (int j = i; j < 6; ++j) { A[6 * i + j] = A[6 * j + i] = U[k]; ++k; }
-    }
-#pragma unroll
-    for (int i = 0; i < 6; ++i) A[7 * i] += lambda;
-    double L[36] = {0}, d[6], id[6];
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-        double dj = A[7 * j];
-#pragma unroll
-        for (int k = 0; k < j; ++k) dj -= L[6 * j + k] * L[6 * j + k] * d[k];
-        if (!(dj > 0)) return false;  // LDLT::isPositive (the damped system is SPD unless degenerate)
-        d[j] = dj;
-        id[j] = rcp_nr(dj);
-#pragma unroll
-        for (int i = j + 1; i < 6; ++i) {
-            double v = A[6 * j + i];
-#pragma unroll
-            for (int k = 0; k < j; ++k) v -= L[6 * i + k] * L[6 * j + k] * d[k];
-            L[6 * i + j] = v * id[j];
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        x[i] = b[i];
-#pragma unroll
-        for (int k = 0; k < i; ++k) x[i] -= L[6 * i + k] * x[k];
-    }
-#pragma unroll
-    for (int i = 0; i < 6; ++i) x[i] *= id[i];
-#pragma unroll
-    for (int i = 5; i >= 0; --i)
-#pragma unroll
-        for (int k = i + 1; k < 6; ++k) x[i] -= L[6 * k + i] * x[k];
-    return true;
+// 1 / sqrt(x) from v_rsq_f64 and two Newton steps (x > 0 finite)
+__device__ __forceinline__ double rsq_nr(double x) {
+    double r = __builtin_amdgcn_rsq(x);
+    double h = 0.5 * x;
+    r = r * fma(-h * r, r, 1.5);
+    return r * fma(-h * r, r, 1.5);
 }
 
-__device__ __forceinline__ void qnormalize_r(double q[4]) {  // SE3Quat::normalizeRotation, one reciprocal
+// (H + lambda I) x = b for the 6x6 symmetric H given as its upper triangle row by row
+// (LinearSolverDense: Eigen::LDLT; the same solution up to rounding).  As 3x3 blocks [A B; B^T C]:
+// A^-1 and the Schur complement's inverse by cofactors (no pivot chain: the cofactors are independent
+// products, one reciprocal per block), so the serial depth is about half of a 6-pivot LDL^T.  Returns
+// LDLT::isPositive's answer by Sylvester's criterion: the leading minors of A, and those of the Schur
+// complement (det of H's leading k x k for k > 3 is det A times them), are all positive.
+__device__ __forceinline__ bool inv3sym(const double (&a)[6], double (&ai)[6], double& m2, double& det) {
+    // a = (a00, a01, a02, a11, a12, a22)
+    const double c00 = a[3] * a[5] - a[4] * a[4], c01 = a[2] * a[4] - a[1] * a[5], c02 = a[1] * a[4] - a[2] * a[3];
+    const double c11 = a[0] * a[5] - a[2] * a[2], c12 = a[1] * a[2] - a[0] * a[4], c22 = a[0] * a[3] - a[1] * a[1];
+    det = a[0] * c00 + a[1] * c01 + a[2] * c02;
+    m2 = c22;
+    const double id = rcp_nr(det);
+    ai[0] = c00 * id; ai[1] = c01 * id; ai[2] = c02 * id; ai[3] = c11 * id; ai[4] = c12 * id; ai[5] = c22 * id;
+    return a[0] > 0 && c22 > 0 && det > 0;
+}
+__device__ __forceinline__ void sym3_mul(const double (&s)[6], const double (&v)[3], double (&o)[3]) {
+    o[0] = s[0] * v[0] + s[1] * v[1] + s[2] * v[2];
+    o[1] = s[1] * v[0] + s[3] * v[1] + s[4] * v[2];
+    o[2] = s[2] * v[0] + s[4] * v[1] + s[5] * v[2];
+}
+__device__ __forceinline__ bool solve6(const double (&U)[21], double lambda, const double (&b)[6], double (&x)[6]) {
+    // U rows: (0,0..5) = 0..5, (1,1..5) = 6..10, (2,2..5) = 11..14, (3,3..5) = 15..17, (4,4..5) = 18, 19, (5,5) = 20
+    const double A[6] = {U[0] + lambda, U[1], U[2], U[6] + lambda, U[7], U[11] + lambda};
+    const double B[3][3] = {{U[3], U[4], U[5]}, {U[8], U[9], U[10]}, {U[12], U[13], U[14]}};  // B[i][j] = H[i][3 + j]
+    double Ai[6], mA2, dA;
+    const bool okA = inv3sym(A, Ai, mA2, dA);
+    double X[3][3];  // A^-1 B
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const double col[3] = {B[0][j], B[1][j], B[2][j]};
+        double o[3];
+        sym3_mul(Ai, col, o);
+        X[0][j] = o[0]; X[1][j] = o[1]; X[2][j] = o[2];
+    }
+    // Schur complement C - B^T A^-1 B (symmetric)
+    auto btx = [&](int i, int j) { return B[0][i] * X[0][j] + B[1][i] * X[1][j] + B[2][i] * X[2][j]; };
+    const double Sc[6] = {U[15] + lambda - btx(0, 0), U[16] - btx(0, 1), U[17] - btx(0, 2),
+                          U[18] + lambda - btx(1, 1), U[19] - btx(1, 2), U[20] + lambda - btx(2, 2)};
+    double Si[6], mS2, dS;
+    const bool okS = inv3sym(Sc, Si, mS2, dS);
+    const double b1[3] = {b[0], b[1], b[2]};
+    double y1[3];
+    sym3_mul(Ai, b1, y1);
+    const double r2[3] = {b[3] - (B[0][0] * y1[0] + B[1][0] * y1[1] + B[2][0] * y1[2]),
+                          b[4] - (B[0][1] * y1[0] + B[1][1] * y1[1] + B[2][1] * y1[2]),
+                          b[5] - (B[0][2] * y1[0] + B[1][2] * y1[1] + B[2][2] * y1[2])};
+    double x2[3];
+    sym3_mul(Si, r2, x2);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        x[3 + i] = x2[i];
+        x[i] = y1[i] - (X[i][0] * x2[0] + X[i][1] * x2[1] + X[i][2] * x2[2]);
+    }
+    return okA && okS;
+}
+
+__device__ __forceinline__ void qnormalize_r(double q[4]) {  // SE3Quat::normalizeRotation, one reciprocal root
     if (q[3] < 0) for (int i = 0; i < 4; ++i) q[i] = -q[i];
-    const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-    if (n > 0) {
-        const double in = rcp_nr(n);
+    const double n2 = q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3];
+    if (n2 > 0) {
+        const double in = rsq_nr(n2);
         for (int i = 0; i < 4; ++i) q[i] *= in;
     }
 }
 
 // pose <- exp(u) * pose (VertexSE3Expmap::oplusImpl, SE3Quat::exp then operator*), as orb_se3.h's
-// se3_oplus with reciprocals instead of divisions and, above g2o's small-angle threshold, the rotation's
-// quaternion in closed form instead of Quaterniond(R) (the pose bar is 1e-6 RMSE)
+// se3_oplus with reciprocal roots instead of divisions (the pose bar is 1e-6 RMSE).  Below g2o's
+// small-angle threshold its branch (R = V = I + Omega + Omega^2, Quaterniond(R)); up to theta = 0.5 the
+// functions of theta as their Taylor series in theta^2 (no sqrt, no sincos): the quaternion of the
+// Rodrigues R is (sin(theta/2) / theta w, cos(theta/2)), V = I + (1 - cos) / theta^2 Omega +
+// (theta - sin) / theta^3 Omega^2; beyond, sincos of the half angle.
 __device__ __forceinline__ void se3_oplus_r(double (&T)[7], const double (&u)[6]) {
     const double w0 = u[0], w1 = u[1], w2 = u[2];
-    const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+    const double t2 = w0 * w0 + w1 * w1 + w2 * w2;
     const double O[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
     double O2[9];
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) O2[3 * i + j] = O[3 * i] * O[j] + O[3 * i + 1] * O[3 + j] + O[3 * i + 2] * O[6 + j];
     double V[9], eq[4], et[3];
-    if (theta < 0.00001) {  // g2o's small-angle branch: R = V = I + Omega + Omega^2, then Quaterniond(R)
+    if (t2 < 1e-10) {  // theta < 0.00001
         double R[9];
         for (int k = 0; k < 9; ++k) R[k] = V[k] = (k % 4 == 0 ? 1.0 : 0.0) + O[k] + O2[k];
-        qfrom_matrix(R, eq);
+        const double tr = R[0] + R[4] + R[8];
+        if (tr > 0) {  // Quaterniond(R), trace branch, with one reciprocal root
+            const double rs = rsq_nr(tr + 1.0);
+            eq[3] = 0.5 * ((tr + 1.0) * rs);
+            const double h = 0.5 * rs;
+            eq[0] = (R[7] - R[5]) * h;
+            eq[1] = (R[2] - R[6]) * h;
+            eq[2] = (R[3] - R[1]) * h;
+        } else {
+            qfrom_matrix(R, eq);
+        }
         qnormalize_r(eq);
     } else {
-        // Quaterniond(R) of the Rodrigues R is (sin(theta/2) w / theta, cos(theta/2)), already unit:
-        // one sincos of the half angle gives it, and sin(theta) = 2 s c, 1 - cos(theta) = 2 s^2 for V
-        double sh, chh;
-        sincos(0.5 * theta, &sh, &chh);
-        const double it = rcp_nr(theta), it2 = it * it;
-        const double sn = 2 * sh * chh, omc = 2 * sh * sh;
-        const double b = omc * it2, d = (theta - sn) * (it2 * it);
+        double f, c, b, d;
+        if (t2 < 0.25) {
+            const double s = t2;  // theta^2; half angle h^2 = s / 4
+            // sin(h) / theta = (1/2) sum (-1)^k h^2k / (2k+1)!,  cos(h) = sum (-1)^k h^2k / (2k)!
+            const double hh = 0.25 * s;
+            f = 0.5 * (1 + hh * (-1. / 6 + hh * (1. / 120 + hh * (-1. / 5040 + hh * (1. / 362880 +
+                  hh * (-1. / 39916800 + hh * (1. / 6227020800. + hh * (-1. / 1307674368000.))))))));
+            c = 1 + hh * (-1. / 2 + hh * (1. / 24 + hh * (-1. / 720 + hh * (1. / 40320 + hh * (-1. / 3628800 +
+                  hh * (1. / 479001600. + hh * (-1. / 87178291200.)))))));
+            // (1 - cos theta) / theta^2 = sum (-1)^k s^k / (2k+2)!,  (theta - sin theta) / theta^3 = sum (-1)^k s^k / (2k+3)!
+            b = 1. / 2 + s * (-1. / 24 + s * (1. / 720 + s * (-1. / 40320 + s * (1. / 3628800 + s * (-1. / 479001600. +
+                  s * (1. / 87178291200. + s * (-1. / 20922789888000.)))))));
+            d = 1. / 6 + s * (-1. / 120 + s * (1. / 5040 + s * (-1. / 362880 + s * (1. / 39916800 + s * (-1. / 6227020800. +
+                  s * (1. / 1307674368000. + s * (-1. / 355687428096000.)))))));
+        } else {
+            const double theta = sqrt(t2);
+            double sh, chh;
+            sincos(0.5 * theta, &sh, &chh);
+            const double it = rcp_nr(theta), it2 = it * it;
+            const double sn = 2 * sh * chh, omc = 2 * sh * sh;
+            b = omc * it2;
+            d = (theta - sn) * (it2 * it);
+            f = sh * it;
+            c = chh;
+        }
         for (int k = 0; k < 9; ++k) V[k] = (k % 4 == 0 ? 1.0 : 0.0) + b * O[k] + d * O2[k];
-        const double f = sh * it;
-        eq[0] = f * w0; eq[1] = f * w1; eq[2] = f * w2; eq[3] = chh;
+        eq[0] = f * w0; eq[1] = f * w1; eq[2] = f * w2; eq[3] = c;
     }
     for (int i = 0; i < 3; ++i) et[i] = V[3 * i] * u[3] + V[3 * i + 1] * u[4] + V[3 * i + 2] * u[5];
     const double q[4] = {T[3], T[4], T[5], T[6]};
@@ -267,68 +318,110 @@ __device__ __forceinline__ void se3_oplus_r(double (&T)[7], const double (&u)[6]
     for (int i = 0; i < 4; ++i) T[3 + i] = nq[i];
 }
 
-// Error, robust chi2 and the J^T W J / -J^T W e contributions of one edge at pose T, added to acc:
-// acc[0..21) the upper triangle of H row by row, acc[21..27) b, acc[27] the robust chi2.  Returns the
-// edge's chi2.  One reciprocal of the depth replaces the divisions of computeError / linearizeOplus.
-// An edge with `on` false contributes exactly zero (zero information, and a zero depth reciprocal so
-// that no product is infinite).
-__device__ __forceinline__ double linearize_edge(const orb_pose_edge_t& Ed, const double* T, const orb_ba_camera_t& cam,
-                                                 bool robust, Huber2 hub, double (&acc)[32], bool on = true) {
+// The pose as a rotation matrix and translation, once per pass (SE3Quat::map = R x + t)
+struct PoseRT {
+    double r[9], t[3];
+};
+__device__ __forceinline__ PoseRT pose_rt(const double (&T)[7]) {
+    PoseRT P;
     const double q[4] = {T[3], T[4], T[5], T[6]};
-    double Xc[3];
-    qrotate(q, Ed.xw, Xc);
-    Xc[0] += T[0]; Xc[1] += T[1]; Xc[2] += T[2];
-    const double x = Xc[0], y = Xc[1], z = Xc[2], fx = cam.fx, fy = cam.fy;
-    const double iz = on ? 1.0 / z : 0.0, iz2 = iz * iz;
-    EdgeEval ev;
-    double B[18];
-    if (!Ed.stereo) {
-        ev.er[0] = Ed.obs[0] - (fx * x * iz + (double)cam.cx);
-        ev.er[1] = Ed.obs[1] - (fy * y * iz + (double)cam.cy);
-        ev.er[2] = 0.0;
+    qmatrix(q, P.r);
+    P.t[0] = T[0]; P.t[1] = T[1]; P.t[2] = T[2];
+    return P;
+}
+
+// Error, robust chi2 and the J^T W J / -J^T W e contributions of one edge at pose P, added to acc:
+// acc[0..21) the upper triangle of H row by row, acc[21..27) b, acc[27] the robust chi2.  Returns the
+// edge's chi2.  The Jacobian rows of EdgeSE3ProjectXYZOnlyPose (two) and EdgeStereoSE3ProjectXYZOnlyPose
+// (three; types_six_dof_expmap.cpp:375-404) share their zero pattern: row 0 (and the stereo row 2) has
+// column 4 zero, row 1 column 3; the products with those zeros are skipped.  The stereo row is a
+// separate block, so a wave of one edge type runs only its own path (edges are sorted by type).  One
+// reciprocal of the depth replaces the divisions.  An edge with `on` false contributes exactly zero
+// (zero information and a zero depth reciprocal; its values must be finite).
+__device__ __forceinline__ double linearize_edge(const orb_pose_edge_t& Ed, const PoseRT& P, const orb_ba_camera_t& cam,
+                                                 bool robust, Huber2 hub, double (&acc)[32], bool on) {
+    const double X = Ed.xw[0], Y = Ed.xw[1], Z = Ed.xw[2];
+    const double x = P.r[0] * X + P.r[1] * Y + P.r[2] * Z + P.t[0];
+    const double y = P.r[3] * X + P.r[4] * Y + P.r[5] * Z + P.t[1];
+    const double z = P.r[6] * X + P.r[7] * Y + P.r[8] * Z + P.t[2];
+    const double fx = cam.fx, fy = cam.fy;
+    const double iz = on ? rcp_nr(z) : 0.0, iz2 = iz * iz;
+    const bool st = Ed.stereo != 0;
+    double r0[6], r1[6], r2[6], e0, e1, e2 = 0.0;
+    if (!st) {
+        e0 = Ed.obs[0] - (fx * x * iz + (double)cam.cx);
+        e1 = Ed.obs[1] - (fy * y * iz + (double)cam.cy);
         const double j00 = -(fx * iz), j02 = fx * x * iz2, j11 = -(fy * iz), j12 = fy * y * iz2;
-        B[0] = j02 * y;  B[1] = j00 * z - j02 * x; B[2] = -j00 * y; B[3] = j00; B[4] = 0;   B[5] = j02;
-        B[6] = -j11 * z + j12 * y; B[7] = -j12 * x; B[8] = j11 * x;  B[9] = 0;  B[10] = j11; B[11] = j12;
-        for (int k = 12; k < 18; ++k) B[k] = 0;
+        r0[0] = j02 * y; r0[1] = j00 * z - j02 * x; r0[2] = -j00 * y; r0[3] = j00; r0[4] = 0; r0[5] = j02;
+        r1[0] = -j11 * z + j12 * y; r1[1] = -j12 * x; r1[2] = j11 * x; r1[3] = 0; r1[4] = j11; r1[5] = j12;
     } else {  // cam_project: float invz, double fx, fy, cx, cy, bf members
-        const float finvz = (float)(1.0f / z);
+        const float finvz = (float)iz;
         const double u = x * finvz * fx + (double)cam.cx;
         const double v = y * finvz * fy + (double)cam.cy;
-        ev.er[0] = Ed.obs[0] - u;
-        ev.er[1] = Ed.obs[1] - v;
-        ev.er[2] = Ed.obs[2] - (u - (double)cam.bf * finvz);
+        e0 = Ed.obs[0] - u;
+        e1 = Ed.obs[1] - v;
+        e2 = Ed.obs[2] - (u - (double)cam.bf * finvz);
         const double bf = cam.bf;
-        B[0] = x * y * iz2 * fx;    B[1] = -(1 + (x * x * iz2)) * fx; B[2] = y * iz * fx;
-        B[3] = -iz * fx;            B[4] = 0;                         B[5] = x * iz2 * fx;
-        B[6] = (1 + y * y * iz2) * fy; B[7] = -x * y * iz2 * fy;      B[8] = -x * iz * fy;
-        B[9] = 0;                   B[10] = -iz * fy;                 B[11] = y * iz2 * fy;
-        B[12] = B[0] - bf * y * iz2; B[13] = B[1] + bf * x * iz2;     B[14] = B[2];
-        B[15] = B[3];               B[16] = 0;                        B[17] = B[5] - bf * iz2;
+        r0[0] = x * y * iz2 * fx; r0[1] = -(1 + (x * x * iz2)) * fx; r0[2] = y * iz * fx;
+        r0[3] = -iz * fx; r0[4] = 0; r0[5] = x * iz2 * fx;
+        r1[0] = (1 + y * y * iz2) * fy; r1[1] = -x * y * iz2 * fy; r1[2] = -x * iz * fy;
+        r1[3] = 0; r1[4] = -iz * fy; r1[5] = y * iz2 * fy;
+        r2[0] = r0[0] - bf * y * iz2; r2[1] = r0[1] + bf * x * iz2; r2[2] = r0[2];
+        r2[3] = r0[3]; r2[4] = 0; r2[5] = r0[5] - bf * iz2;
     }
     const double info = on ? (double)Ed.inv_sigma2 : 0.0;
-    ev.chi2 = ev.er[0] * info * ev.er[0] + ev.er[1] * info * ev.er[1];
-    if (Ed.stereo) ev.chi2 += ev.er[2] * info * ev.er[2];
-    ev.stereo = Ed.stereo;
-    double rho1;
-    acc[27] += robust_rho(ev, robust, hub, rho1);
-    const double w = rho1 * info;
-    int k = 0;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-#pragma unroll
-        for (int j = i; j < 6; ++j) {
-            double s = B[i] * w * B[j] + B[6 + i] * w * B[6 + j];
-            if (Ed.stereo) s += B[12 + i] * w * B[12 + j];
-            acc[k++] += s;
+    double chi2 = e0 * info * e0 + e1 * info * e1;
+    if (st) chi2 += e2 * info * e2;
+    double rho0 = chi2, rho1 = 1.0;
+    if (robust) {  // RobustKernelHuber with its float dsqr (robust_kernel_impl.cpp:78-91)
+        const double dsq = (double)(st ? hub.dsqr_stereo : hub.dsqr_mono);
+        if (!(chi2 <= dsq)) {
+            const double delta = st ? hub.delta_stereo : hub.delta_mono;
+            const double rs = rsq_nr(chi2);
+            rho0 = 2 * (chi2 * rs) * delta - dsq;
+            rho1 = delta * rs;
         }
     }
+    acc[27] += rho0;
+    const double w = rho1 * info;
+    constexpr bool nz0[6] = {true, true, true, true, false, true};   // rows 0 and 2
+    constexpr bool nz1[6] = {true, true, true, false, true, true};   // row 1
+    double w0[6], w1[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
-        double bs = B[i] * info * ev.er[0] + B[6 + i] * info * ev.er[1];
-        if (Ed.stereo) bs += B[12 + i] * info * ev.er[2];
-        acc[21 + i] -= rho1 * bs;
+        w0[i] = w * r0[i];
+        w1[i] = w * r1[i];
     }
-    return ev.chi2;
+    {
+        int k = 0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int j = i; j < 6; ++j, ++k) {
+                if (nz0[i] && nz0[j]) acc[k] += w0[i] * r0[j];
+                if (nz1[i] && nz1[j]) acc[k] += w1[i] * r1[j];
+            }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            if (nz0[i]) acc[21 + i] -= w0[i] * e0;
+            if (nz1[i]) acc[21 + i] -= w1[i] * e1;
+        }
+    }
+    if (st) {
+        double w2[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) w2[i] = w * r2[i];
+        int k = 0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int j = i; j < 6; ++j, ++k)
+                if (nz0[i] && nz0[j]) acc[k] += w2[i] * r2[j];
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+            if (nz0[i]) acc[21 + i] -= w2[i] * e2;
+    }
+    return chi2;
 }
 
 // Phase stamps of frame 0 (orb_debug_pose_trace, tools/pose_trace.py): per LM trial, s_memtime at the
@@ -340,32 +433,36 @@ __device__ int g_pose_trace_cap = 0;
 
 // LM state of a frame's optimize(10), kept in registers of the workgroup's thread 0
 struct LmState {
-    double H[21], b[6], x[6], Tb[7];
+    double x[6];
     double lambda, ni, current, ini;
-    int nbad, qmax, it, ok;
+    int nbad, qmax, it, ok, cur;  // cur: the buffer of sys holding the system
 };
 
-// One 256-thread workgroup per frame.  The first kS * kPT edges of the frame (and their outlier flag
-// and last chi2) stay in registers for the whole optimisation; edges beyond are read from memory on
-// every pass.  Every trial evaluates the new pose and linearises there in the same pass: g2o rebuilds
-// the system at the accepted state before the next iteration, and a rejected trial keeps the old
-// linearisation, so the next iteration's build is this pass's sums.  Thread 0 holds the LM state; per
-// trial it takes the totals, decides, and solves the next trial, between two barriers.
+// One workgroup per frame.  The first kS * kPT edges of the frame (and their outlier flag and last
+// chi2) stay in registers for the whole optimisation, sorted by type -- the monocular edges first, then
+// the stereo ones, each in index order -- so that a wave runs one edge type's path; edges beyond are read
+// from memory on every pass.  Every trial evaluates the new pose and linearises there in the same pass:
+// g2o rebuilds the system at the accepted state before the next iteration, and a rejected trial keeps
+// the old linearisation, so the next iteration's build is this pass's sums.  Thread 0 holds the LM
+// state; per trial it takes the totals, decides, and solves the next trial, between two barriers.
 template <int kS>
 __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __restrict__ frames,
                                                   const orb_pose_edge_t* __restrict__ edges,
                                                   double* __restrict__ pose_out, uint8_t* __restrict__ level,
                                                   int32_t* __restrict__ inliers, double* __restrict__ echi2, Huber2 hub) {
     __shared__ double part[kPW * 32];
-    __shared__ double tot[28];
     __shared__ double T[7];
     __shared__ int s_state;  // 1: evaluate the trial pose in T, 2: the round's optimize() is done
+    constexpr int kA = kS + kLdsSlots;  // slots per thread: registers, then LDS
+    __shared__ int perm[kA * kPT];      // slot position -> edge index
+    __shared__ int scan[kPT];
+    __shared__ orb_pose_edge_t led[kLdsSlots * kPT];
     const int tid = threadIdx.x, f = blockIdx.x;
     long long* const tr = f == 0 ? g_pose_trace : nullptr;
     const int tr_cap = g_pose_trace_cap;
     int tr_n = 0;  // trials stamped
     auto stamp = [&](int k) {
-        if (tr && tid == 0 && tr_n < tr_cap) tr[8 * tr_n + k] = clock64();
+        if (tr && tid == 0 && tr_n < tr_cap) tr[16 * tr_n + k] = clock64();
     };
     const orb_pose_frame_t F = frames[f];
     const int n = F.n_edges;
@@ -378,23 +475,71 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
         if (tid == 0) inliers[f] = 0;
         return;
     }
+    // ---- the slot edges sorted by type: thread t ranks edges [kA t, kA t + kA)
+    const int nr = min(n, kA * kPT);
+    {
+        int mono = 0;
+        bool st[kA];
+#pragma unroll
+        for (int s = 0; s < kA; ++s) {
+            const int e = kA * tid + s;
+            st[s] = e < nr ? E[e].stereo != 0 : true;
+            mono += e < nr && !st[s];
+        }
+        scan[tid] = mono;
+        __syncthreads();
+        for (int o = 1; o < kPT; o <<= 1) {
+            const int v = tid >= o ? scan[tid - o] : 0;
+            __syncthreads();
+            scan[tid] += v;
+            __syncthreads();
+        }
+        const int nmono = scan[kPT - 1];
+        int rm = scan[tid] - mono;       // monocular edges before this thread's
+        int rs = kA * tid - rm;          // stereo edges before this thread's (of the e < nr ones)
+#pragma unroll
+        for (int s = 0; s < kA; ++s) {
+            const int e = kA * tid + s;
+            if (e < nr) perm[st[s] ? nmono + rs++ : rm++] = e;
+        }
+        __syncthreads();
+    }
+    // register slots: edge, outlier flag, last chi2; LDS slots: the same in led / llv / lch
+    __shared__ uint8_t llv[kLdsSlots * kPT];
+    __shared__ double lch[kLdsSlots * kPT];
     orb_pose_edge_t ed[kS];
     int lv[kS];
     double ch[kS];
+    orb_pose_edge_t dummy{};  // a finite edge: the pass computes it with zero information
+    dummy.xw[2] = 1.0;
 #pragma unroll
     for (int s = 0; s < kS; ++s) {
-        const int e = tid + s * kPT;
-        if (e < n) ed[s] = E[e];
+        const int p = tid + s * kPT;
+        ed[s] = p < nr ? E[perm[p]] : dummy;
         lv[s] = 0;  // mvbOutlier[i] = false at edge creation
         ch[s] = 0;
     }
-    for (int e = tid + kS * kPT; e < n; e += kPT) lev[e] = 0;
+    for (int q = tid; q < kLdsSlots * kPT; q += kPT) {
+        const int p = q + kS * kPT;
+        led[q] = p < nr ? E[perm[p]] : dummy;
+        llv[q] = 0;
+        lch[q] = 0;
+    }
+    for (int e = tid + kA * kPT; e < n; e += kPT) lev[e] = 0;
+    __syncthreads();
     // fn(edge, outlier flag, last chi2) over this thread's edges
     auto visit = [&](auto&& fn) {
 #pragma unroll
         for (int s = 0; s < kS; ++s)
-            if (tid + s * kPT < n) fn(ed[s], lv[s], ch[s]);
-        for (int e = tid + kS * kPT; e < n; e += kPT) {
+            if (tid + s * kPT < nr) fn(ed[s], lv[s], ch[s]);
+        for (int q = tid; q + kS * kPT < nr; q += kPT) {
+            int l = llv[q];
+            double c = lch[q];
+            fn(led[q], l, c);
+            llv[q] = (uint8_t)l;
+            lch[q] = c;
+        }
+        for (int e = tid + kA * kPT; e < n; e += kPT) {
             int l = lev[e];
             double c = ech[e];
             fn(E[e], l, c);
@@ -403,57 +548,81 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
         }
     };
     // a linearisation pass at T over the active edges (chi2 kept when `keep`), reduced: wave 0's lane
-    // 2k ends with the workgroup total of value k.  The register slots are linearised without branches
-    // (an inactive slot computes a zero-information dummy edge), so their latency chains interleave.
-    orb_pose_edge_t dummy{};
-    dummy.xw[2] = 1.0;
+    // 2k ends with the workgroup total of value k.  A slot is skipped by a wave none of whose lanes holds
+    // an edge there; inside a wave, an outlier slot computes with zero information.  The LDS slots run
+    // as a loop.
     auto pass = [&](bool robust, bool keep, double (&acc)[32]) {
 #pragma unroll
         for (int k = 0; k < 32; ++k) acc[k] = 0;
         double Tl[7];
 #pragma unroll
         for (int i = 0; i < 7; ++i) Tl[i] = T[i];
+        const PoseRT P = pose_rt(Tl);
+        const int wbase = tid & ~63;
+        stamp(8);
 #pragma unroll
         for (int s = 0; s < kS; ++s) {
-            const bool on = tid + s * kPT < n && !lv[s];
-            const double c2 = linearize_edge(on ? ed[s] : dummy, Tl, F.cam, robust, hub, acc, on);
-            if (keep && on) ch[s] = c2;
+            if (wbase + s * kPT < nr) {  // wave-uniform
+                const bool on = tid + s * kPT < nr && !lv[s];
+                const double c2 = linearize_edge(ed[s], P, F.cam, robust, hub, acc, on);
+                if (keep && on) ch[s] = c2;
+            }
+            stamp(9 + s);
         }
-        for (int e = tid + kS * kPT; e < n; e += kPT) {
+        {
+            const int nq = nr - kS * kPT;  // LDS slot positions in use
+            int q = tid;
+            for (int qb = wbase; qb < nq; qb += kPT, q += kPT) {  // wave-uniform trip count
+                const bool on = q < nq && !llv[q];
+                const double c2 = linearize_edge(led[q], P, F.cam, robust, hub, acc, on);
+                if (keep && on) lch[q] = c2;
+            }
+        }
+        for (int e = tid + kA * kPT; e < n; e += kPT) {
             if (lev[e]) continue;
-            const double c2 = linearize_edge(E[e], Tl, F.cam, robust, hub, acc);
+            const double c2 = linearize_edge(E[e], P, F.cam, robust, hub, acc, true);
             if (keep) ech[e] = c2;
         }
+        stamp(11);
         wave_partials32(acc, part);
+        stamp(12);
         __syncthreads();
+        stamp(13);
         if (tid < 64) {
             const int k = (tid >> 1) & 31;
 #pragma unroll
             for (int w = 1; w < kPW; ++w) acc[0] += part[32 * w + k];  // the waves in order
         }
     };
-    // the 28 workgroup totals to thread 0: wave 0's lane 2k holds total k; they go through LDS (one
-    // store, thread 0's loads issued together) instead of 56 v_readlane in every lane of wave 0
-    auto totals = [&](const double (&acc)[32], double (&t)[28]) {
-        if (tid < 56 && !(tid & 1)) tot[tid >> 1] = acc[0];
+    // the 28 workgroup totals (wave 0's lane 2k holds total k) into sys[buf]: the linear system and
+    // chi2 live in LDS, double-buffered -- an accepted trial's pass becomes the system by a buffer swap
+    __shared__ double sys[2][28];
+    __shared__ double Tb[7];  // the pose before the trial step (restored on a rejection)
+    auto totals = [&](const double (&acc)[32], int buf) {
+        if (tid < 56 && !(tid & 1)) sys[buf][tid >> 1] = acc[0];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (tid == 0) {
-#pragma unroll
-            for (int k = 0; k < 28; ++k) t[k] = tot[k];
-        }
     };
-    auto solve = [&](LmState& S) {  // thread 0: the damped system, the trial pose into T
+    auto solve = [&](LmState& S) {  // thread 0: the damped system sys[cur], the trial pose into T
         stamp(5);
-        for (int i = 0; i < 7; ++i) S.Tb[i] = T[i];
-        S.ok = ldlt6(S.H, S.lambda, S.b, S.x);
-        if (!S.ok) for (int i = 0; i < 6; ++i) S.x[i] = 0;
+        double U[21], b[6], Tn[7];
+#pragma unroll
+        for (int k = 0; k < 21; ++k) U[k] = sys[S.cur][k];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) b[i] = sys[S.cur][21 + i];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) Tn[i] = T[i];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) Tb[i] = Tn[i];
+        S.ok = solve6(U, S.lambda, b, S.x);
+        if (!S.ok)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) S.x[i] = 0;
         stamp(6);
-        double Tn[7];
-        for (int i = 0; i < 7; ++i) Tn[i] = S.Tb[i];
         se3_oplus_r(Tn, S.x);
         stamp(7);
+#pragma unroll
         for (int i = 0; i < 7; ++i) T[i] = Tn[i];
     };
     bool robust = true;
@@ -469,20 +638,17 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
         visit([&](const orb_pose_edge_t&, int& l, double&) { active += l == 0; });
         active = __syncthreads_or(active);
         if (active) {
+            int cur = 0;  // every thread tracks the system buffer
             double acc[32];
             pass(robust, false, acc);  // computeActiveErrors + buildSystem at the round's start pose
-            double t[28];
-            totals(acc, t);
+            totals(acc, cur);
             if (tid == 0) {
-#pragma unroll
-                for (int k = 0; k < 21; ++k) S.H[k] = t[k];
-#pragma unroll
-                for (int i = 0; i < 6; ++i) S.b[i] = t[21 + i];
-                S.current = S.ini = t[27];
+                S.cur = cur;
+                S.current = S.ini = sys[cur][27];
                 double m = 0;  // computeLambdaInit: tau * max |diag H|
                 constexpr int kDiag[6] = {0, 6, 11, 15, 18, 20};
 #pragma unroll
-                for (int i = 0; i < 6; ++i) m = fmax(fabs(S.H[kDiag[i]]), m);
+                for (int i = 0; i < 6; ++i) m = fmax(fabs(sys[cur][kDiag[i]]), m);
                 S.lambda = 1e-5 * m;
                 S.ni = 2;
                 S.nbad = 0;
@@ -494,17 +660,19 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
             for (;;) {
                 // evaluate (and linearise) at the trial pose; every active edge's chi2 is kept, since
                 // g2o classifies on the last evaluated state even when it was rejected
+                const int wb = cur ^ 1;
                 stamp(0);
                 pass(robust, true, acc);
                 stamp(1);
-                totals(acc, t);
+                totals(acc, wb);
                 stamp(2);
                 if (tid == 0) {
-                    double tempChi = t[27];
+                    double tempChi = sys[wb][27];
                     if (!S.ok) tempChi = DBL_MAX;
                     double r = S.current - tempChi;
                     double scale = 0;
-                    for (int i = 0; i < 6; ++i) scale += S.x[i] * (S.lambda * S.x[i] + S.b[i]);
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) scale += S.x[i] * (S.lambda * S.x[i] + sys[cur][21 + i]);
                     scale += 1e-3;
                     r *= rcp_nr(scale);
                     const bool accept = r > 0 && isfinite(tempChi);
@@ -518,10 +686,11 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
                     } else {
                         S.lambda *= S.ni;
                         S.ni *= 2;
-                        for (int i = 0; i < 7; ++i) T[i] = S.Tb[i];
+#pragma unroll
+                        for (int i = 0; i < 7; ++i) T[i] = Tb[i];
                     }
                     S.qmax++;
-                    int st = 1;
+                    int st = 1, swap = 0;
                     if (!(r < 0 && S.qmax < 10)) {
                         // the iteration ends; optimize()'s loop stops on qmax == 10 or rho == 0, after
                         // 10 iterations, or on the third consecutive small chi2 decrease
@@ -533,22 +702,22 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
                             if (S.nbad >= 3 || ++S.it == 10) st = 2;
                         }
                         if (st == 1) {  // accepted: the next iteration's system is this pass's linearisation
-#pragma unroll
-                            for (int k = 0; k < 21; ++k) S.H[k] = t[k];
-#pragma unroll
-                            for (int i = 0; i < 6; ++i) S.b[i] = t[21 + i];
+                            swap = 1;
+                            S.cur = wb;
                             S.ini = S.current;
                             S.qmax = 0;
                         }
                     }
                     if (st == 1) solve(S);
-                    s_state = st;
+                    s_state = st | (swap << 2);
                 }
                 stamp(3);
                 __syncthreads();
                 stamp(4);
                 ++tr_n;
-                if (s_state == 2) break;
+                const int ss = s_state;
+                if (ss & 4) cur = wb;
+                if ((ss & 3) == 2) break;
             }
         }
         // ---- re-classification (src/Optimizer.cc:285-386)
@@ -580,9 +749,10 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
     }
 #pragma unroll
     for (int s = 0; s < kS; ++s) {
-        const int e = tid + s * kPT;
-        if (e < n) lev[e] = (uint8_t)lv[s];
+        const int p = tid + s * kPT;
+        if (p < nr) lev[perm[p]] = (uint8_t)lv[s];
     }
+    for (int q = tid; q + kS * kPT < nr; q += kPT) lev[perm[q + kS * kPT]] = llv[q];
     if (tid < 7) pose_out[7 * (size_t)f + tid] = T[tid];
     if (tid == 0) inliers[f] = n - nBad;
 }
@@ -623,7 +793,7 @@ int orb_pose_optimization_device(int n_frames, const orb_pose_frame_t* d_frames,
     return ORB_OK;
 }
 
-// Debug hook (not in the public header): stamp frame 0's LM trials into d_buf (8 int64 per trial, up
+// Debug hook (not in the public header): stamp frame 0's LM trials into d_buf (16 int64 per trial, up
 // to `cap` trials; NULL turns it off).  Synchronous.
 int orb_debug_pose_trace(long long* d_buf, int cap) {
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_pose_trace), &d_buf, sizeof(d_buf)) != hipSuccess ||

@@ -82,3 +82,59 @@ def test_sharded_local_ba_matches_oracle(oracle, synth, world, stereo_frac, seed
         # every rank holds the same result
         assert np.array_equal(pose, out[0][0]) and np.array_equal(point, out[0][1])
         assert np.array_equal(chi2, out[0][2])
+
+
+def _rccl_one_rank_worker(port, kw, q):
+    """One rank with an RCCL communicator forced onto the sharded path (ORBGPU_BA_DIST_FORCE=1): the
+    device LM loop with its all-reduces as real RCCL calls, next to a plain single-GPU handle."""
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ORBGPU_BA_DIST_FORCE="1")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        from conftest import load_package
+        pkg = load_package()
+        from orbslam3_amd import synth
+        prob = synth.local_ba_problem(**kw)
+        sharded = pkg.LocalBA().attach(transport="rccl")
+        a = sharded.optimize(prob, 10)
+        b = pkg.LocalBA().optimize(prob, 10)
+        q.put((0, (a, b)))
+    except Exception as e:  # noqa: BLE001
+        q.put((0, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_one_rank_sharded_device_loop(oracle, synth):
+    """The sharded device-driven LM loop with RCCL (stream-ordered all-reduces between the unit's
+    launches, the build / trial controllers after them) on one rank: the same state as the
+    single-GPU solve bit for bit, and the oracle's LM path."""
+    import torch.multiprocessing as mp
+    kw = dict(n_kf=20, n_points=800, obs_per_point=5, stereo_frac=0.3, seed=12)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_one_rank_worker, args=(_port(), kw, q))
+    p.start()
+    import queue
+    import time
+    t0 = time.time()
+    v = None
+    while v is None:  # a crashed worker fails the test instead of blocking on the queue
+        try:
+            _, v = q.get(timeout=5)
+        except queue.Empty:
+            assert p.is_alive(), f"worker exited with {p.exitcode}"
+            assert time.time() - t0 < 150, "worker timed out"
+    p.join(timeout=60)
+    assert not isinstance(v, str), v
+    (pose, point, chi2, depth, res), (pose1, point1, chi21, depth1, res1) = v
+    for k in ("iterations", "trials", "terminated", "stopped"):
+        assert res[k] == res1[k], k
+    assert np.array_equal(pose, pose1) and np.array_equal(point, point1)
+    assert np.array_equal(chi2, chi21) and np.array_equal(depth, depth1)
+    prob = synth.local_ba_problem(**kw)
+    rpose, rpoint, _, _, rres = oracle.local_ba(prob, 10)
+    assert res["iterations"] == rres["iterations"] and res["trials"] == rres["trials"]
+    assert _rmse(pose[:, :3], rpose[:, :3]) < 1e-6 and _rmse(point, rpoint) < 1e-6

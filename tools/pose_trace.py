@@ -17,7 +17,8 @@ pkg = load_package()
 import torch  # noqa: E402
 from orbslam3_amd import synth  # noqa: E402
 
-frames, edges, _ = synth.pose_opt_batch(4, 500, stereo_frac=0.5, seed=4242)
+NPTS = int(sys.argv[1]) if len(sys.argv) > 1 else 500
+frames, edges, _ = synth.pose_opt_batch(4, NPTS, stereo_frac=0.5, seed=4242)
 lib = pkg._lib.load()
 dev = torch.device("cuda", 0)
 d_fr = torch.from_numpy(frames.view(np.uint8).reshape(-1)).to(dev)
@@ -45,12 +46,12 @@ for _ in range(reps):
 torch.cuda.synchronize()
 print(f"single frame ({n1} edges): {(time.perf_counter() - t0) / reps * 1e3:.4f} ms per call")
 cap = 128
-buf = torch.zeros(8 * cap, dtype=torch.int64, device=dev)
+buf = torch.zeros(16 * cap, dtype=torch.int64, device=dev)
 pkg._lib.check(lib.orb_debug_pose_trace(buf.data_ptr(), cap), "trace on")
 call()
 torch.cuda.synchronize()
 pkg._lib.check(lib.orb_debug_pose_trace(None, 0), "trace off")
-t = buf.cpu().numpy().reshape(cap, 8)
+t = buf.cpu().numpy().reshape(cap, 16)
 t = t[t[:, 0] != 0]
 d = np.diff(t[:, :5], axis=1)
 sv = t[t[:, 5] != 0]
@@ -60,3 +61,8 @@ nxt = t[1:, 0] - t[:-1, 4]
 print(f"{len(t)} trials; median cycles: pass {np.median(d[:, 0]):.0f}, totals {np.median(d[:, 1]):.0f}, "
       f"decide+solve {np.median(d[:, 2]):.0f}, barrier {np.median(d[:, 3]):.0f}, between trials {np.median(nxt):.0f}; "
       f"trial span median {np.median(t[:, 4] - t[:, 0]):.0f}, first-to-last {t[-1, 4] - t[0, 0]}")
+pz = t[t[:, 8] != 0]
+print(f"pass detail (wave 0): T+rt {np.median(pz[:, 8] - pz[:, 0]):.0f}, slot0 {np.median(pz[:, 9] - pz[:, 8]):.0f}, "
+      f"slot1 {np.median(pz[:, 10] - pz[:, 9]):.0f}, lds/mem slots {np.median(pz[:, 11] - pz[:, 10]):.0f}, "
+      f"butterfly {np.median(pz[:, 12] - pz[:, 11]):.0f}, barrier {np.median(pz[:, 13] - pz[:, 12]):.0f}, "
+      f"wave sums {np.median(pz[:, 1] - pz[:, 13]):.0f}")
