@@ -36,13 +36,16 @@
 namespace {
 
 #ifndef ORB_POSE_THREADS
-#define ORB_POSE_THREADS 256
+#define ORB_POSE_THREADS 512
+#endif
+#ifndef ORB_POSE_REG_EDGES
+#define ORB_POSE_REG_EDGES 0
 #endif
 constexpr int kPT = ORB_POSE_THREADS;  // threads per frame
 constexpr int kPW = kPT / 64;          // waves
-constexpr int kEdgeSlots = 512 / kPT;   // edges per thread kept in registers (512 per frame)
-constexpr int kLdsSlots = 1536 / kPT;   // and in LDS (the next 1536)
-static_assert(kPT % 64 == 0 && kEdgeSlots >= 1 && kPW <= 32, "pose workgroup shape");
+constexpr int kEdgeSlots = ORB_POSE_REG_EDGES / kPT;  // edges per thread kept in registers
+constexpr int kLdsSlots = (2048 - ORB_POSE_REG_EDGES) / kPT;  // and in LDS (2048 per frame in all)
+static_assert(kPT % 64 == 0 && kEdgeSlots >= 0 && kLdsSlots >= 1 && kPW <= 32, "pose workgroup shape");
 
 static_assert(sizeof(orb_pose_edge_t) == 56, "pose edge layout");
 
@@ -245,35 +248,48 @@ __device__ __forceinline__ void qnormalize_r(double q[4]) {  // SE3Quat::normali
     }
 }
 
+// sin / cos of h >= 0.25 (a step of more than half a radian: rare): h / 2^k below 0.25 by its
+// exponent, the Taylor series there, then k double-angle steps -- a few ulps per step, far inside the
+// pose bar, and without the library's large register footprint (Payne-Hanek reduction) in this kernel
+__device__ __forceinline__ void sincos_halving(double h, double& sn, double& cs) {
+    int e;
+    (void)frexp(h, &e);  // h = m 2^e, 0.5 <= m < 1
+    const int k = min(max(e + 2, 0), 64);
+    const double a = ldexp(h, -k), a2 = a * a;
+    double s = a * (1 + a2 * (-1. / 6 + a2 * (1. / 120 + a2 * (-1. / 5040 + a2 * (1. / 362880 + a2 * (-1. / 39916800 +
+               a2 * (1. / 6227020800. + a2 * (-1. / 1307674368000.))))))));
+    double c = 1 + a2 * (-1. / 2 + a2 * (1. / 24 + a2 * (-1. / 720 + a2 * (1. / 40320 + a2 * (-1. / 3628800 +
+               a2 * (1. / 479001600. + a2 * (-1. / 87178291200. + a2 * (1. / 20922789888000.))))))));
+    for (int i = 0; i < k; ++i) {
+        const double s2 = 2 * s * c;
+        c = (c - s) * (c + s);
+        s = s2;
+    }
+    sn = s;
+    cs = c;
+}
+
 // pose <- exp(u) * pose (VertexSE3Expmap::oplusImpl, SE3Quat::exp then operator*), as orb_se3.h's
-// se3_oplus with reciprocal roots instead of divisions (the pose bar is 1e-6 RMSE).  Below g2o's
-// small-angle threshold its branch (R = V = I + Omega + Omega^2, Quaterniond(R)); up to theta = 0.5 the
-// functions of theta as their Taylor series in theta^2 (no sqrt, no sincos): the quaternion of the
-// Rodrigues R is (sin(theta/2) / theta w, cos(theta/2)), V = I + (1 - cos) / theta^2 Omega +
-// (theta - sin) / theta^3 Omega^2; beyond, sincos of the half angle.
+// se3_oplus with reciprocal roots instead of divisions (the pose bar is 1e-6 RMSE), written with
+// Omega^2 = w w^T - theta^2 I so that no product with a zero entry is issued: V = a I + b Omega + c w w^T
+// and V u = a u + b (w x u) + c w (w . u).
+//   theta < 0.00001 (g2o's small-angle branch): R = V = I + Omega + Omega^2 (a = 1 - theta^2, b = c = 1)
+//     and Quaterniond(R) by its trace branch, normalised: R - R^T = 2 Omega gives the vector part
+//     w / s with s = sqrt(tr R + 1) = sqrt(4 - 2 theta^2), the scalar part s / 2;
+//   theta < 0.5: the Rodrigues quaternion (sin(theta/2) / theta w, cos(theta/2)) and the coefficients
+//     (1 - cos) / theta^2, (theta - sin) / theta^3 as Taylor series in theta^2 (no sqrt, no sincos);
+//   beyond: sincos of the half angle.
 __device__ __forceinline__ void se3_oplus_r(double (&T)[7], const double (&u)[6]) {
     const double w0 = u[0], w1 = u[1], w2 = u[2];
     const double t2 = w0 * w0 + w1 * w1 + w2 * w2;
-    const double O[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
-    double O2[9];
-    for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) O2[3 * i + j] = O[3 * i] * O[j] + O[3 * i + 1] * O[3 + j] + O[3 * i + 2] * O[6 + j];
-    double V[9], eq[4], et[3];
-    if (t2 < 1e-10) {  // theta < 0.00001
-        double R[9];
-        for (int k = 0; k < 9; ++k) R[k] = V[k] = (k % 4 == 0 ? 1.0 : 0.0) + O[k] + O2[k];
-        const double tr = R[0] + R[4] + R[8];
-        if (tr > 0) {  // Quaterniond(R), trace branch, with one reciprocal root
-            const double rs = rsq_nr(tr + 1.0);
-            eq[3] = 0.5 * ((tr + 1.0) * rs);
-            const double h = 0.5 * rs;
-            eq[0] = (R[7] - R[5]) * h;
-            eq[1] = (R[2] - R[6]) * h;
-            eq[2] = (R[3] - R[1]) * h;
-        } else {
-            qfrom_matrix(R, eq);
-        }
+    double eq[4], va, vb, vc;
+    if (t2 < 1e-10) {
+        const double tr1 = 4.0 - 2.0 * t2;  // tr R + 1
+        const double rs = rsq_nr(tr1);
+        const double f = rs;                // (R[7] - R[5]) * (0.5 / s) = 2 w0 * 0.5 / s
+        eq[0] = f * w0; eq[1] = f * w1; eq[2] = f * w2; eq[3] = 0.5 * (tr1 * rs);
         qnormalize_r(eq);
+        va = 1.0 - t2; vb = 1.0; vc = 1.0;
     } else {
         double f, c, b, d;
         if (t2 < 0.25) {
@@ -292,7 +308,7 @@ __device__ __forceinline__ void se3_oplus_r(double (&T)[7], const double (&u)[6]
         } else {
             const double theta = sqrt(t2);
             double sh, chh;
-            sincos(0.5 * theta, &sh, &chh);
+            sincos_halving(0.5 * theta, sh, chh);
             const double it = rcp_nr(theta), it2 = it * it;
             const double sn = 2 * sh * chh, omc = 2 * sh * sh;
             b = omc * it2;
@@ -300,10 +316,14 @@ __device__ __forceinline__ void se3_oplus_r(double (&T)[7], const double (&u)[6]
             f = sh * it;
             c = chh;
         }
-        for (int k = 0; k < 9; ++k) V[k] = (k % 4 == 0 ? 1.0 : 0.0) + b * O[k] + d * O2[k];
         eq[0] = f * w0; eq[1] = f * w1; eq[2] = f * w2; eq[3] = c;
+        va = 1.0 - d * t2; vb = b; vc = d;
     }
-    for (int i = 0; i < 3; ++i) et[i] = V[3 * i] * u[3] + V[3 * i + 1] * u[4] + V[3 * i + 2] * u[5];
+    // V upsilon
+    const double wu = w0 * u[3] + w1 * u[4] + w2 * u[5];
+    const double x0 = w1 * u[5] - w2 * u[4], x1 = w2 * u[3] - w0 * u[5], x2 = w0 * u[4] - w1 * u[3];
+    const double cw = vc * wu;
+    const double et[3] = {va * u[3] + vb * x0 + cw * w0, va * u[4] + vb * x1 + cw * w1, va * u[5] + vb * x2 + cw * w2};
     const double q[4] = {T[3], T[4], T[5], T[6]};
     double rt[3];
     qrotate(eq, T, rt);
@@ -507,9 +527,10 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
     // register slots: edge, outlier flag, last chi2; LDS slots: the same in led / llv / lch
     __shared__ uint8_t llv[kLdsSlots * kPT];
     __shared__ double lch[kLdsSlots * kPT];
-    orb_pose_edge_t ed[kS];
-    int lv[kS];
-    double ch[kS];
+    constexpr int kS1 = kS > 0 ? kS : 1;  // (array extent when no register slot is configured)
+    orb_pose_edge_t ed[kS1];
+    int lv[kS1];
+    double ch[kS1];
     orb_pose_edge_t dummy{};  // a finite edge: the pass computes it with zero information
     dummy.xw[2] = 1.0;
 #pragma unroll
@@ -627,7 +648,9 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
     };
     bool robust = true;
     int nBad = 0;
-    LmState S;
+    // thread 0's LM state lives in LDS between trials (loaded into registers for the decision and the
+    // solve only), so that it holds no registers during the pass
+    __shared__ LmState sS;
     for (int round = 0; round < 4; ++round) {
         // vSE3->setEstimate(pFrame->GetPose()); read from global: a lane-indexed read of the copy F
         // would put F in scratch
@@ -643,6 +666,7 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
             pass(robust, false, acc);  // computeActiveErrors + buildSystem at the round's start pose
             totals(acc, cur);
             if (tid == 0) {
+                LmState S;
                 S.cur = cur;
                 S.current = S.ini = sys[cur][27];
                 double m = 0;  // computeLambdaInit: tau * max |diag H|
@@ -655,6 +679,7 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
                 S.qmax = 0;
                 S.it = 0;
                 solve(S);
+                sS = S;
             }
             __syncthreads();
             for (;;) {
@@ -667,6 +692,7 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
                 totals(acc, wb);
                 stamp(2);
                 if (tid == 0) {
+                    LmState S = sS;
                     double tempChi = sys[wb][27];
                     if (!S.ok) tempChi = DBL_MAX;
                     double r = S.current - tempChi;
@@ -709,6 +735,7 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
                         }
                     }
                     if (st == 1) solve(S);
+                    sS = S;
                     s_state = st | (swap << 2);
                 }
                 stamp(3);

@@ -121,7 +121,8 @@ constexpr int kCandWaves = 4;
 
 // one wave per last-frame point (src:1978-2062 up to the minimum): project with the current pose,
 // the window by forward / backward motion (src:2019-2024), the stereo u_R test, distances
-__global__ __launch_bounds__(64 * kCandWaves) void k_proj_candidates(const ProjParams* __restrict__ pp, const uint8_t* __restrict__ valid,
+__global__ __launch_bounds__(64 * kCandWaves) void k_proj_candidates(const ProjParams P, const int32_t* __restrict__ n_dev,
+                                                         const uint8_t* __restrict__ valid,
                                                          const float* __restrict__ xyz, const uint4* __restrict__ mp_desc,
                                                          const int32_t* __restrict__ last_octave,
                                                          const float4* __restrict__ cur_kp,  // x, y, angle, octave bits
@@ -131,10 +132,9 @@ __global__ __launch_bounds__(64 * kCandWaves) void k_proj_candidates(const ProjP
                                                          int32_t* __restrict__ overflow, const uint8_t* __restrict__ observed,
                                                          int32_t* __restrict__ lister) {
     __shared__ int pre_s[kCandWaves][64], beg_s[kCandWaves][64];
-    const ProjParams& P = *pp;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int i = blockIdx.x * kCandWaves + w;
-    if (i >= P.n_last) return;
+    if (i >= (n_dev ? *n_dev : P.n_last)) return;  // (device forms: the count the prep kernel clamped)
     int n = 0;
     if (valid[i]) {
         const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
@@ -205,7 +205,7 @@ struct LocalParams {
 
 // one wave per local map point (src:54-143 up to the minima): RadiusByViewingCos, the window at the
 // predicted level (levels level-1 .. level), the stereo u_R test, distances
-__global__ __launch_bounds__(64 * kCandWaves) void k_lmp_candidates(const LocalParams* __restrict__ pp, const uint8_t* __restrict__ in_view,
+__global__ __launch_bounds__(64 * kCandWaves) void k_lmp_candidates(const LocalParams P, const uint8_t* __restrict__ in_view,
                                                         const uint8_t* __restrict__ bad, const float* __restrict__ proj,
                                                         const float* __restrict__ view_cos, const float* __restrict__ depth,
                                                         const int32_t* __restrict__ level, const uint4* __restrict__ mp_desc,
@@ -216,7 +216,6 @@ __global__ __launch_bounds__(64 * kCandWaves) void k_lmp_candidates(const LocalP
                                                         const uint8_t* __restrict__ observed, const uint8_t* __restrict__ taken0,
                                                         int32_t* __restrict__ lister) {
     __shared__ int pre_s[kCandWaves][64], beg_s[kCandWaves][64];
-    const LocalParams& P = *pp;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int i = blockIdx.x * kCandWaves + w;
     if (i >= P.n_pts) return;
@@ -309,6 +308,7 @@ struct ResolveArgs {
     int32_t* removed;          // per keypoint
     int32_t* mp;               // out: per keypoint
     int32_t* out_n;            // out: [0] count, [1] rounds
+    int32_t* out_user;         // out (device forms, may be null): the count, for the caller
     const int32_t* dims;       // device forms: [0] n_pts, [1] n_cur read on the device (NULL: the fields above)
 };
 
@@ -606,10 +606,24 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_rounds(ResolveArgs 
         a.out_n[0] = cnt[0] - cnt[1];
         a.out_n[1] = rounds;
         a.out_n[2] = nw;
+        if (a.out_user) a.out_user[0] = cnt[0] - cnt[1];
     }
 }
 
 // ---- device-resident forms: the frame's grid and packed keypoints built on the device ------------
+
+// scratch initialisation done by k_frame_prep (the device forms launch no fills): fill_7f (lister /
+// fixed claims) with 0x7f7f7f7f, fill_m1 (the match array) with -1, the 4 overflow / counter words
+// zero, and dims[0] = dims0 when dims0 >= 0 (the local-map form's point count)
+struct ScratchInit {
+    int32_t* fill_7f;
+    int n_7f;
+    int32_t* fill_m1;
+    int n_m1;
+    int32_t* zero4;
+    int32_t* dims;
+    int dims0;
+};
 
 // Frame::AssignFeaturesToGrid (src/Frame.cc:1418-1440) on a device frame, one workgroup: cell
 // (round((x - mnMinX) inv_w), round((y - mnMinY) inv_h)), keypoints in index order inside each cell
@@ -621,11 +635,16 @@ __global__ __launch_bounds__(kPrepThreads) void k_frame_prep(const orb_keypoint_
                                                              float min_y, float inv_w, float inv_h,
                                                              float4* __restrict__ kp4, int32_t* __restrict__ cell_off,
                                                              int32_t* __restrict__ cell_idx, int32_t* __restrict__ cell_of,
-                                                             int32_t* n_out0, int32_t* n_out1) {
+                                                             int32_t* n_out0, int32_t* n_out1, ScratchInit z) {
     __shared__ int cnt[kCells];
     __shared__ int part[kPrepThreads];
     const int tid = threadIdx.x;
     const int n = min(max(*n_ptr, 0), cap);
+    // the call's scratch words, in place of fill launches (the later kernels of the call read them)
+    for (int i = tid; i < z.n_7f; i += kPrepThreads) z.fill_7f[i] = 0x7f7f7f7f;
+    for (int i = tid; i < z.n_m1; i += kPrepThreads) z.fill_m1[i] = -1;
+    if (tid < 4) z.zero4[tid] = 0;
+    if (tid == 0 && z.dims0 >= 0) z.dims[0] = z.dims0;
     for (int c = tid; c < kCells; c += kPrepThreads) cnt[c] = 0;
     __syncthreads();
     for (int i = tid; i < n; i += kPrepThreads) {
@@ -841,7 +860,8 @@ extern "C" int orb_search_by_projection_frame(orb_matcher_t m, const orb_frame_v
         memset(h + o_ovf, 0, 16);
         bool ok = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s) == hipSuccess;
         if (ok && nl > 0)
-            hipLaunchKernelGGL(k_proj_candidates, dim3((nl + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s, (const ProjParams*)(d + o_p),
+            hipLaunchKernelGGL(k_proj_candidates, dim3((nl + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s, P,
+                               (const int32_t*)nullptr,
                                (const uint8_t*)(d + o_va), (const float*)(d + o_xyz), (const uint4*)(d + o_md),
                                (const int32_t*)(d + o_lo), (const float4*)(d + o_kp), (const float*)(d + o_ur),
                                (const uint4*)(d + o_cd), (const int32_t*)(d + o_co), (const int32_t*)(d + o_ci),
@@ -977,7 +997,7 @@ extern "C" int orb_search_by_projection_local(orb_matcher_t m, const orb_frame_v
         memset(h + o_ovf, 0, 16);
         bool ok = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s) == hipSuccess;
         if (ok && np > 0)
-            hipLaunchKernelGGL(k_lmp_candidates, dim3((np + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s, (const LocalParams*)(d + o_p),
+            hipLaunchKernelGGL(k_lmp_candidates, dim3((np + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s, P,
                                (const uint8_t*)(d + o_iv), (const uint8_t*)(d + o_bd), (const float*)(d + o_pj),
                                (const float*)(d + o_vc), (const float*)(d + o_dp), (const int32_t*)(d + o_lv),
                                (const uint4*)(d + o_md), (const float4*)(d + o_kp), (const float*)(d + o_ur),
@@ -1074,7 +1094,7 @@ extern "C" int orb_search_by_projection_frame_device(orb_matcher_t m, const orb_
     size_t bytes = 0;
     {
         DevScratch z;
-        z.take<ProjParams>(1); z.take<int32_t>(2); z.take<float4>(C); z.take<int32_t>(kCells + 1); z.take<int32_t>(C);
+        z.take<int32_t>(2); z.take<float4>(C); z.take<int32_t>(kCells + 1); z.take<int32_t>(C);
         z.take<int32_t>(C); z.take<uint8_t>(NL); z.take<int32_t>(NL); z.take<float>(NL); z.take<int32_t>(2 * (size_t)C);
         z.take<int32_t>(4); z.take<Cand>((size_t)NL * C); z.take<int32_t>(NL); z.take<int32_t>(NL);
         z.take<int32_t>(3 * (size_t)C); z.take<int32_t>(NL); z.take<int4>((kTop / 2) * (size_t)NL); z.take<int32_t>(NL);
@@ -1083,7 +1103,6 @@ extern "C" int orb_search_by_projection_frame_device(orb_matcher_t m, const orb_
     DevScratch z;
     if (hipMallocAsync(reinterpret_cast<void**>(&z.base), bytes, s) != hipSuccess)
         return orbgpu_fail(ORB_ERR_DEVICE, "hipMallocAsync failed");
-    ProjParams* dP = z.take<ProjParams>(1);
     int32_t* dims = z.take<int32_t>(2);
     float4* kp4 = z.take<float4>(C);
     int32_t* cell_off = z.take<int32_t>(kCells + 1);
@@ -1101,21 +1120,19 @@ extern "C" int orb_search_by_projection_frame_device(orb_matcher_t m, const orb_
     int32_t* wl = z.take<int32_t>(NL);
     int4* top = z.take<int4>((kTop / 2) * (size_t)NL);
     int32_t* nus = z.take<int32_t>(NL);
-    bool ok = hipMemcpyAsync(dP, &P, sizeof(P), hipMemcpyHostToDevice, s) == hipSuccess &&
-              hipMemsetAsync(lf, 0x7f, 2 * (size_t)C * 4, s) == hipSuccess && hipMemsetAsync(ovf, 0, 16, s) == hipSuccess &&
-              hipMemsetAsync(d_match, 0xFF, (size_t)C * 4, s) == hipSuccess;
-    if (ok) {
+    bool ok = true;
+    {
+        const ScratchInit zi{lf, 2 * C, d_match, C, ovf, dims, NL > 0 ? -1 : 0};
         hipLaunchKernelGGL(k_frame_prep, dim3(1), dim3(kPrepThreads), 0, s, cur->kps_un, cur->n, C, cur->min_x, cur->min_y,
-                           cur->grid_inv_w, cur->grid_inv_h, kp4, cell_off, cell_idx, cell_of, &dP->n_cur, dims + 1);
+                           cur->grid_inv_w, cur->grid_inv_h, kp4, cell_off, cell_idx, cell_of, dims + 1, (int32_t*)nullptr,
+                           zi);
         if (NL > 0) {
             hipLaunchKernelGGL(k_last_prep, dim3((NL + 255) / 256), dim3(256), 0, s, last->kps_un, last->valid, last->n, NL,
-                               cur->nlevels, valid2, loct, lang, &dP->n_last, dims);
+                               cur->nlevels, valid2, loct, lang, dims, (int32_t*)nullptr);
             hipLaunchKernelGGL(k_proj_candidates, dim3((NL + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s,
-                               (const ProjParams*)dP, (const uint8_t*)valid2, last->xyz, (const uint4*)last->desc,
+                               P, (const int32_t*)dims, (const uint8_t*)valid2, last->xyz, (const uint4*)last->desc,
                                (const int32_t*)loct, (const float4*)kp4, cur->u_right, (const uint4*)cur->desc,
                                (const int32_t*)cell_off, (const int32_t*)cell_idx, cands, nc, ovf, last->observed, lf);
-        } else {
-            ok = hipMemsetAsync(dims, 0, 4, s) == hipSuccess;
         }
         ResolveArgs ra{};
         ra.n_pts = NL; ra.n_cur = C; ra.cap = C; ra.local = 0; ra.check_ori = P.check_ori; ra.nnratio = 0.f;
@@ -1124,11 +1141,10 @@ extern "C" int orb_search_by_projection_frame_device(orb_matcher_t m, const orb_
         ra.claimMin = kw; ra.last = kw + C; ra.removed = kw + 2 * (size_t)C;
         ra.lister = lf; ra.fixed = lf + C; ra.work = wl; ra.top = top; ra.nusable = nus;
         ra.lds_keypoints = resolve_lds_ready() ? 1 : 0;
-        ra.mp = d_match; ra.out_n = ovf + 1; ra.dims = dims;
+        ra.mp = d_match; ra.out_n = ovf + 1; ra.dims = dims; ra.out_user = d_n_matches;
         if (NL > 0) hipLaunchKernelGGL(k_resolve_init, dim3((NL + 255) / 256), dim3(256), 0, s, ra);
         hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 8 * (size_t)C : 0, s, ra);
-        ok = ok && hipGetLastError() == hipSuccess &&
-             hipMemcpyAsync(d_n_matches, ovf + 1, 4, hipMemcpyDeviceToDevice, s) == hipSuccess;
+        ok = hipGetLastError() == hipSuccess;
     }
     if (hipFreeAsync(z.base, s) != hipSuccess) ok = false;
     return ok ? ORB_OK : orbgpu_fail(ORB_ERR_DEVICE, "SearchByProjection device failed");
@@ -1155,7 +1171,7 @@ extern "C" int orb_search_by_projection_local_device(orb_matcher_t m, const orb_
     size_t bytes = 0;
     {
         DevScratch z;
-        z.take<LocalParams>(1); z.take<int32_t>(2); z.take<float4>(C); z.take<int32_t>(kCells + 1); z.take<int32_t>(C);
+        z.take<int32_t>(2); z.take<float4>(C); z.take<int32_t>(kCells + 1); z.take<int32_t>(C);
         z.take<int32_t>(C); z.take<uint8_t>(np); z.take<int32_t>(2 * (size_t)C); z.take<int32_t>(4);
         z.take<Cand>((size_t)np * C); z.take<int32_t>(np); z.take<int32_t>(np); z.take<int32_t>(3 * (size_t)C);
         z.take<int32_t>(np); z.take<int4>((kTop / 2) * (size_t)np); z.take<int32_t>(np);
@@ -1164,7 +1180,6 @@ extern "C" int orb_search_by_projection_local_device(orb_matcher_t m, const orb_
     DevScratch z;
     if (hipMallocAsync(reinterpret_cast<void**>(&z.base), bytes, s) != hipSuccess)
         return orbgpu_fail(ORB_ERR_DEVICE, "hipMallocAsync failed");
-    LocalParams* dP = z.take<LocalParams>(1);
     int32_t* dims = z.take<int32_t>(2);
     float4* kp4 = z.take<float4>(C);
     int32_t* cell_off = z.take<int32_t>(kCells + 1);
@@ -1180,19 +1195,17 @@ extern "C" int orb_search_by_projection_local_device(orb_matcher_t m, const orb_
     int32_t* wl = z.take<int32_t>(np);
     int4* top = z.take<int4>((kTop / 2) * (size_t)np);
     int32_t* nus = z.take<int32_t>(np);
-    const int32_t dims_h[2] = {np, 0};
-    bool ok = hipMemcpyAsync(dP, &P, sizeof(P), hipMemcpyHostToDevice, s) == hipSuccess &&
-              hipMemcpyAsync(dims, dims_h, sizeof(dims_h), hipMemcpyHostToDevice, s) == hipSuccess &&
-              hipMemsetAsync(lf, 0x7f, 2 * (size_t)C * 4, s) == hipSuccess && hipMemsetAsync(ovf, 0, 16, s) == hipSuccess &&
-              hipMemsetAsync(d_match, 0xFF, (size_t)C * 4, s) == hipSuccess;
-    if (ok) {
+    bool ok = true;
+    {
+        const ScratchInit zi{lf, 2 * C, d_match, C, ovf, dims, np};
         hipLaunchKernelGGL(k_frame_prep, dim3(1), dim3(kPrepThreads), 0, s, F->kps_un, F->n, C, F->min_x, F->min_y,
-                           F->grid_inv_w, F->grid_inv_h, kp4, cell_off, cell_idx, cell_of, &dP->n_cur, dims + 1);
+                           F->grid_inv_w, F->grid_inv_h, kp4, cell_off, cell_idx, cell_of, dims + 1, (int32_t*)nullptr,
+                           zi);
         if (np > 0) {
             hipLaunchKernelGGL(k_local_prep, dim3((np + 255) / 256), dim3(256), 0, s, pts->track_in_view, pts->track_level,
                                np, F->nlevels, iv2);
             hipLaunchKernelGGL(k_lmp_candidates, dim3((np + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s,
-                               (const LocalParams*)dP, (const uint8_t*)iv2, pts->is_bad, pts->track_proj, pts->track_view_cos,
+                               P, (const uint8_t*)iv2, pts->is_bad, pts->track_proj, pts->track_view_cos,
                                pts->track_depth, pts->track_level, (const uint4*)pts->desc, (const float4*)kp4, F->u_right,
                                (const uint4*)F->desc, (const int32_t*)cell_off, (const int32_t*)cell_idx, cands, nc, ovf,
                                pts->observed, d_frame_taken, lf);
@@ -1204,11 +1217,10 @@ extern "C" int orb_search_by_projection_local_device(orb_matcher_t m, const orb_
         ra.claimMin = kw; ra.last = kw + C; ra.removed = kw + 2 * (size_t)C;
         ra.lister = lf; ra.fixed = lf + C; ra.work = wl; ra.top = top; ra.nusable = nus;
         ra.lds_keypoints = resolve_lds_ready() ? 1 : 0;
-        ra.mp = d_match; ra.out_n = ovf + 1; ra.dims = dims;
+        ra.mp = d_match; ra.out_n = ovf + 1; ra.dims = dims; ra.out_user = d_n_matches;
         if (np > 0) hipLaunchKernelGGL(k_resolve_init, dim3((np + 255) / 256), dim3(256), 0, s, ra);
         hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 8 * (size_t)C : 0, s, ra);
-        ok = hipGetLastError() == hipSuccess &&
-             hipMemcpyAsync(d_n_matches, ovf + 1, 4, hipMemcpyDeviceToDevice, s) == hipSuccess;
+        ok = hipGetLastError() == hipSuccess;
     }
     if (hipFreeAsync(z.base, s) != hipSuccess) ok = false;
     return ok ? ORB_OK : orbgpu_fail(ORB_ERR_DEVICE, "SearchByProjection(local) device failed");

@@ -13,3 +13,5 @@ from orbslam3_amd import synth  # noqa: E402
 cpu = "--cpu" in sys.argv
 out = bench.bench_tracking_chain(pkg, synth, torch.device("cuda:0"), 20, cpu)
 print(json.dumps(out, indent=1))
+if "--pose" in sys.argv:
+    print(json.dumps(bench.bench_pose(pkg, synth, torch.device("cuda:0"), 20, cpu), indent=1))
