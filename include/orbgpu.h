@@ -114,11 +114,19 @@ int orb_extractor_level_download(orb_extractor_t h, int frame, int level, uint8_
 /* ---- REGISTER_TIMES (include/Settings.h:24, src/Tracking.cc:318-420) ------------------------- */
 /* Wall-clock stage timers with the reference's names: "ORB Extraction" (orb_extract; mTimeORB_Ext,
  * src/Frame.cc:132-146), "Stereo Matching" (orb_compute_stereo_matches; src/Frame.cc:158-170), "LBA"
- * (orb_ba_optimize; vdLBA_ms, src/LocalMapping.cc:213-230).  Off by default; on with
- * orb_timers_enable(1) or ORBGPU_REGISTER_TIMES=1.  orb_timer_stats gives mean and population std
- * (calcAverage / calcDeviation, src/Tracking.cc:189-208); orb_timers_write writes them as ExecMean.txt
- * lines ("ORB Extraction: mean$\pm$std").  orb_timer_add records a caller's own bracket. */
+ * (the host side of Optimizer::LocalBundleAdjustment in include/orbgpu_optimizer.hpp, gather to
+ * write-back, as vdLBA_ms brackets the whole call, src/LocalMapping.cc:208-219; no sample when the
+ * shim returns kFallback).  Off by default.  orb_timers_enable(1) (or ORBGPU_REGISTER_TIMES=1): every
+ * orb_extract / orb_compute_stereo_matches call records a sample -- one per image, where the reference
+ * records one per Frame (a stereo pair's two extractions, run in parallel, are one sample).
+ * orb_timers_enable(2) (or ORBGPU_REGISTER_TIMES=2): no per-call samples; the caller brackets its
+ * Frame and records it with orb_timer_add, as Frame.cc does.  orb_timer_stats gives mean and
+ * population std (calcAverage / calcDeviation, src/Tracking.cc:189-208); orb_timers_write writes them
+ * as ExecMean.txt lines ("ORB Extraction: mean$\pm$std", fixed with 5 decimals: `f << fixed`,
+ * src/Tracking.cc:327, then setprecision(5), :335). */
 int orb_timers_enable(int on);
+/* The timer mode (0 off, 1 per-call brackets, 2 caller brackets only). */
+int orb_timers_enabled(void);
 int orb_timers_reset(void);
 int orb_timer_add(const char* name, double ms);
 int orb_timer_stats(const char* name, double* mean_ms, double* std_ms, long long* count);

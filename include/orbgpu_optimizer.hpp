@@ -54,6 +54,7 @@
 #include <list>
 #include <map>
 #include <mutex>
+#include <chrono>
 #include <set>
 #include <stdexcept>
 #include <string>
@@ -253,8 +254,8 @@ constexpr int kFallback = 1;
 // on the same arguments, as INTEGRATION.md shows; the reference is slower there, never wrong.
 // num_MPs is left untouched, as in the reference.
 template <class A>
-int LocalBundleAdjustment(orb_ba_t h, typename A::KeyFrame* pKF, bool* pbStopFlag, typename A::Map* pMap,
-                          int& num_fixedKF, int& num_OptKF, int& /*num_MPs*/, int& num_edges) {
+int LocalBundleAdjustmentBody(orb_ba_t h, typename A::KeyFrame* pKF, bool* pbStopFlag, typename A::Map* pMap,
+                              int& num_fixedKF, int& num_OptKF, int& num_edges) {
     LocalBAWindow<A> w;
     const auto st = w.Gather(pKF, pMap);
     if (st == LocalBAWindow<A>::kCamera2) {
@@ -300,6 +301,27 @@ int LocalBundleAdjustment(orb_ba_t h, typename A::KeyFrame* pKF, bool* pbStopFla
     }
     w.CullAndWriteBack(pMap, chi2.data(), depth.data());
     return ORB_OK;
+}
+
+// REGISTER_TIMES: the "LBA" sample covers the whole call as vdLBA_ms does (src/LocalMapping.cc:208-219),
+// recorded when the library's timers are on (orb_timers_enabled) and the call did not fall back.
+struct LbaTimer {
+    const bool on = orb_timers_enabled() != 0;
+    const std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    bool record = true;
+    ~LbaTimer() {
+        if (on && record)
+            orb_timer_add("LBA", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+};
+
+template <class A>
+int LocalBundleAdjustment(orb_ba_t h, typename A::KeyFrame* pKF, bool* pbStopFlag, typename A::Map* pMap,
+                          int& num_fixedKF, int& num_OptKF, int& /*num_MPs*/, int& num_edges) {
+    LbaTimer timer;
+    const int rc = LocalBundleAdjustmentBody<A>(h, pKF, pbStopFlag, pMap, num_fixedKF, num_OptKF, num_edges);
+    timer.record = rc != kFallback;  // the reference body's own run is the caller's to time
+    return rc;
 }
 
 }  // namespace orbgpu

@@ -85,6 +85,7 @@ PROTOTYPES = {
     "orb_extractor_level": (_i, [_vp, _i, _i, ctypes.POINTER(_vp), _ip, _ip, _ip]),
     "orb_extractor_level_download": (_i, [_vp, _i, _i, _vp]),
     "orb_timers_enable": (_i, [_i]),
+    "orb_timers_enabled": (_i, []),
     "orb_timers_reset": (_i, []),
     "orb_timer_add": (_i, [ctypes.c_char_p, ctypes.c_double]),
     "orb_timer_stats": (_i, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),

@@ -2314,7 +2314,6 @@ int orb_debug_ba_chol_timeout_status(int32_t* status) {
 
 int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* opt, double* edge_chi2,
                     uint8_t* edge_depth_ok, orb_ba_result_t* res) {
-    orbgpu::StageTimer timer("LBA");  // vdLBA_ms (src/LocalMapping.cc:213-230)
     if (!h || !pr || !opt || !res) return orbgpu_fail(ORB_ERR_ARG, "null BA argument");
     memset(res, 0, sizeof(*res));
     // ORBGPU_BA_TRACE: host-side phase times of each solve on stderr (structure, upload+LM, results)

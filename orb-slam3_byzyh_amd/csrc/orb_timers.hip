@@ -4,8 +4,14 @@
 // (src/LocalMapping.cc:213-230, vdLBA_ms), and prints mean $\pm$ population std per stage to ExecMean.txt
 // (src/Tracking.cc:189-208, 318-420).  Here the same wall-clock brackets sit inside the synchronous
 // entry points (orb_extract -> "ORB Extraction", orb_compute_stereo_matches -> "Stereo Matching",
-// orb_ba_optimize -> "LBA"), switched on at run time (orb_timers_enable, or ORBGPU_REGISTER_TIMES in
-// the environment) instead of at compile time; off, a bracket costs one relaxed atomic load.
+// and the host side of Optimizer::LocalBundleAdjustment -> "LBA": the shim include/orbgpu_optimizer.hpp and
+// the Python mirror, gather to write-back, no sample when the reference body has to take over),
+// switched on at run time (orb_timers_enable, or ORBGPU_REGISTER_TIMES in the environment) instead of at
+// compile time; off, a bracket costs one relaxed atomic load.  Mode 2 leaves the per-call brackets off
+// for a caller that times a whole Frame itself: the reference's "ORB Extraction" sample is one per
+// Frame, covering a stereo pair's two extractions run in parallel (src/Frame.cc:132-146), which such a
+// caller records with orb_timer_add.  ExecMean.txt's numbers are fixed with 5 decimals: the reference
+// sets `f << fixed` (src/Tracking.cc:327) and then `setprecision(5)` (:335).
 #include <algorithm>
 #include <atomic>
 #include <cmath>
@@ -35,12 +41,12 @@ bool timers_on() {
     int v = g_on.load(std::memory_order_relaxed);
     if (v < 0) {
         const char* e = getenv("ORBGPU_REGISTER_TIMES");
-        v = (e && *e && *e != '0') ? 1 : 0;
+        v = (e && *e && *e != '0') ? (*e == '2' ? 2 : 1) : 0;
         int expect = -1;
         g_on.compare_exchange_strong(expect, v);
         v = g_on.load(std::memory_order_relaxed);
     }
-    return v != 0;
+    return v == 1;  // mode 2: the caller brackets its own stages (orb_timer_add); no per-call brackets
 }
 void timer_add(const char* name, double ms) {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -51,8 +57,14 @@ void timer_add(const char* name, double ms) {
 extern "C" {
 
 int orb_timers_enable(int on) {
-    g_on.store(on ? 1 : 0, std::memory_order_relaxed);
+    if (on < 0 || on > 2) return orbgpu_fail(ORB_ERR_ARG, "timer mode must be 0, 1 or 2");
+    g_on.store(on, std::memory_order_relaxed);
     return ORB_OK;
+}
+
+int orb_timers_enabled(void) {
+    (void)orbgpu::timers_on();  // (reads ORBGPU_REGISTER_TIMES on first use)
+    return g_on.load(std::memory_order_relaxed);
 }
 
 int orb_timers_reset(void) {

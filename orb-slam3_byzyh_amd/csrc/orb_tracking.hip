@@ -107,7 +107,7 @@ __global__ __launch_bounds__(kThreads) void k_track_pose_edges(EdgeParams P, con
 
 // outliers lose their map point; n_out[0] = the edges kept, n_out[1] = those whose map point has
 // observations (nmatchesMap, src/Tracking.cc:4198-4200)
-__global__ __launch_bounds__(256) void k_track_discard(const orb_pose_frame_t* __restrict__ frame,
+__global__ __launch_bounds__(kThreads) void k_track_discard(const orb_pose_frame_t* __restrict__ frame,
                                                        const int32_t* __restrict__ edge_kp,
                                                        const uint8_t* __restrict__ outlier, int32_t* __restrict__ match_a,
                                                        const uint8_t* __restrict__ observed_a, int32_t* __restrict__ match_b,
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256) void k_track_discard(const orb_pose_frame_t* _
     __syncthreads();
     const int ne = frame->n_edges;
     int k = 0, o = 0;
-    for (int e = threadIdx.x; e < ne; e += 256) {
+    for (int e = threadIdx.x; e < ne; e += kThreads) {
         const int i = edge_kp[e];
         const int mb = match_b ? match_b[i] : -1;
         if (outlier[e]) {
@@ -129,8 +129,14 @@ __global__ __launch_bounds__(256) void k_track_discard(const orb_pose_frame_t* _
         ++k;
         o += mb >= 0 ? (observed_b ? observed_b[mb] != 0 : 1) : (observed_a ? observed_a[match_a[i]] != 0 : 1);
     }
-    atomicAdd(&keep, k);
-    atomicAdd(&obs, o);
+    for (int off = 32; off > 0; off >>= 1) {  // wave sums, then one LDS atomic per wave
+        k += __shfl_xor(k, off, 64);
+        o += __shfl_xor(o, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&keep, k);
+        atomicAdd(&obs, o);
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         n_out[0] = keep;
@@ -141,7 +147,7 @@ __global__ __launch_bounds__(256) void k_track_discard(const orb_pose_frame_t* _
     // that now hold a map point with observations
     __threadfence_block();
     __syncthreads();
-    for (int i = threadIdx.x; i < cap; i += 256) {
+    for (int i = threadIdx.x; i < cap; i += kThreads) {
         const int mb = match_b ? match_b[i] : -1, ma = match_a[i];
         uint8_t t = 0;
         if (mb >= 0) t = observed_b ? observed_b[mb] != 0 : 1;
@@ -216,7 +222,7 @@ int orb_tracking_discard_outliers_device(const orb_pose_frame_t* d_frame, const 
                                          uint8_t* d_taken, void* stream) {
     if (!d_frame || !d_edge_kp || !d_outlier || !d_match_a || !d_n_out || (d_taken && cap <= 0))
         return orbgpu_fail(ORB_ERR_ARG, "bad tracking discard arguments");
-    hipLaunchKernelGGL(k_track_discard, dim3(1), dim3(256), 0, (hipStream_t)stream, d_frame, d_edge_kp, d_outlier, d_match_a,
+    hipLaunchKernelGGL(k_track_discard, dim3(1), dim3(kThreads), 0, (hipStream_t)stream, d_frame, d_edge_kp, d_outlier, d_match_a,
                        d_observed_a, d_match_b, d_observed_b, d_n_out, cap, d_taken);
     if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "tracking discard launch failed");
     return ORB_OK;

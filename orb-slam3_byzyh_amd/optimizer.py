@@ -179,10 +179,16 @@ class LocalBA:
 def local_bundle_adjustment(prob: dict, iterations: int = 10, solver: LocalBA | None = None):
     """optimize(10) and the reference's culling pass (src/Optimizer.cc:2107-2160): returns
     (pose, point, erase_mask over edges, result)."""
+    import time
+    lib = _lib.load()
+    timed = lib.orb_timers_enabled() != 0  # REGISTER_TIMES "LBA": the whole call (src/LocalMapping.cc:208-219)
+    t0 = time.perf_counter()
     solver = solver or LocalBA()
     pose, point, chi2, depth, res = solver.optimize(prob, iterations)
     stereo = np.asarray(prob["edges"]["stereo"]) != 0
     erase = np.where(stereo, chi2 > CHI2_STEREO, chi2 > CHI2_MONO) | ~depth
+    if timed:
+        check(lib.orb_timer_add(b"LBA", (time.perf_counter() - t0) * 1e3), "orb_timer_add")
     return pose, point, erase, res
 
 

@@ -1,6 +1,8 @@
-"""REGISTER_TIMES-compatible stage timers of the library (csrc/orb_timers.hip): "ORB Extraction",
-"Stereo Matching" and "LBA" brackets inside the synchronous entry points, with ExecMean.txt output
-(src/Tracking.cc:318-420)."""
+"""REGISTER_TIMES-compatible stage timers of the library (csrc/orb_timers.hip): "ORB Extraction" and
+"Stereo Matching" brackets inside the synchronous entry points, "LBA" around the host side of
+LocalBundleAdjustment (the C++ shim, optimizer.local_bundle_adjustment), with ExecMean.txt output
+(src/Tracking.cc:318-420).  Mode 2 leaves the per-call brackets off for callers that time a whole
+Frame themselves (one "ORB Extraction" sample per stereo Frame, as src/Frame.cc:132-146 records it)."""
 from __future__ import annotations
 
 import ctypes
@@ -11,8 +13,14 @@ from ._lib import check
 STAGES = ("ORB Extraction", "Stereo Matching", "LBA")
 
 
-def enable(on: bool = True) -> None:
-    check(_lib.load().orb_timers_enable(1 if on else 0), "orb_timers_enable")
+def enable(on: bool | int = True) -> None:
+    """True / 1: per-call brackets; 2: caller brackets only (add()); False / 0: off."""
+    mode = int(on) if not isinstance(on, bool) else (1 if on else 0)
+    check(_lib.load().orb_timers_enable(mode), "orb_timers_enable")
+
+
+def enabled() -> int:
+    return int(_lib.load().orb_timers_enabled())
 
 
 def reset() -> None:

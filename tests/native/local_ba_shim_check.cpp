@@ -147,6 +147,9 @@ struct SolveRecord {
     double pose_shift = 0.5;        // added to every non-fixed pose's tx, every point's x
 } g_solve;
 
+// REGISTER_TIMES doubles: the shim's "LBA" bracket (timers off here; the GPU shim test links the library)
+extern "C" int orb_timers_enabled(void) { return 0; }
+extern "C" int orb_timer_add(const char*, double) { return 0; }
 extern "C" int orb_ba_optimize(orb_ba_t, orb_ba_problem_t* p, const orb_ba_options_t* o, double* chi2,
                                uint8_t* depth, orb_ba_result_t* res) {
     ++g_solve.calls;

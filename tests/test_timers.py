@@ -23,10 +23,24 @@ def test_timer_stats_and_execmean_format(pkg, tmp_path):
     timers.write(p)
     lines = p.read_text().splitlines()
     assert lines[0] == " TIME STATS in ms (mean$\\pm$std)"
-    assert lines[1] == "ORB Extraction: 3.50000$\\pm$0.00000"  # the reference's stage order, empty ones skipped
+    # the reference's stage order, empty ones skipped; 5 decimals: `f << fixed` (src/Tracking.cc:327)
+    # then setprecision(5) (:335)
+    assert lines[1] == "ORB Extraction: 3.50000$\\pm$0.00000"
     assert lines[2] == f"LBA: {mean:.5f}$\\pm${s:.5f}"
     timers.reset()
     assert timers.stats("LBA")[2] == 0
+
+
+def test_timer_modes(pkg):
+    from orbslam3_amd import timers
+    try:
+        for mode in (2, 1, 0):
+            timers.enable(mode)
+            assert timers.enabled() == mode
+        with pytest.raises(Exception):
+            timers.enable(3)
+    finally:
+        timers.enable(False)
 
 
 @pytest.mark.gpu
@@ -42,10 +56,20 @@ def test_timers_bracket_entry_points(pkg, synth):
         for _ in range(3):
             ex(img)
         prob = synth.local_ba_problem(n_kf=6, n_points=150, obs_per_point=4, n_fixed=1, seed=3)
-        pkg.LocalBA().optimize(prob, 5)
+        pkg.LocalBA().optimize(prob, 5)  # the bare solve records nothing: "LBA" is the whole call
+        assert timers.stats("LBA")[2] == 0
+        pkg.local_bundle_adjustment(prob, 5)
         m, s, n = timers.stats("ORB Extraction")
         assert n == 3 and m > 0
         assert timers.stats("LBA")[2] == 1
+        # mode 2: no per-call samples; the caller's own bracket (one per stereo Frame) goes in by add()
+        timers.enable(2)
+        ex(img)
+        ex(img)
+        timers.add("ORB Extraction", 1.25)
+        assert timers.stats("ORB Extraction")[2] == 4
+        pkg.local_bundle_adjustment(prob, 5)
+        assert timers.stats("LBA")[2] == 2
     finally:
         timers.enable(False)
         timers.reset()
