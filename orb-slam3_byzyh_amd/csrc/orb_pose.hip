@@ -36,10 +36,10 @@
 namespace {
 
 #ifndef ORB_POSE_THREADS
-#define ORB_POSE_THREADS 512
+#define ORB_POSE_THREADS 256
 #endif
 #ifndef ORB_POSE_REG_EDGES
-#define ORB_POSE_REG_EDGES 0
+#define ORB_POSE_REG_EDGES 512
 #endif
 constexpr int kPT = ORB_POSE_THREADS;  // threads per frame
 constexpr int kPW = kPT / 64;          // waves

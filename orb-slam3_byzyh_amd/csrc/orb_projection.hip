@@ -628,18 +628,25 @@ struct ScratchInit {
 // Frame::AssignFeaturesToGrid (src/Frame.cc:1418-1440) on a device frame, one workgroup: cell
 // (round((x - mnMinX) inv_w), round((y - mnMinY) inv_h)), keypoints in index order inside each cell
 // (counting sort, then each cell's few entries put back in index order); the (x, y, angle, octave) float4
-// rows the candidate kernels read; the clamped count into n_out[0] and n_out[1].
-constexpr int kPrepThreads = 1024, kCells = kGridCols * kGridRows;
+// rows the candidate kernels read; the clamped count into n_out[0] and n_out[1].  The counts, offsets
+// and (up to kPrepLds keypoints) the cell lists are built in LDS and written out once; a thread keeps its
+// keypoints' cells in registers.
+constexpr int kPrepThreads = 1024, kCells = kGridCols * kGridRows, kPrepLds = 8192;
+constexpr int kPrepPer = 16;  // keypoints per thread: cap <= 16384
 __global__ __launch_bounds__(kPrepThreads) void k_frame_prep(const orb_keypoint_t* __restrict__ kps,
                                                              const int32_t* __restrict__ n_ptr, int cap, float min_x,
                                                              float min_y, float inv_w, float inv_h,
                                                              float4* __restrict__ kp4, int32_t* __restrict__ cell_off,
                                                              int32_t* __restrict__ cell_idx, int32_t* __restrict__ cell_of,
                                                              int32_t* n_out0, int32_t* n_out1, ScratchInit z) {
-    __shared__ int cnt[kCells];
-    __shared__ int part[kPrepThreads];
-    const int tid = threadIdx.x;
+    __shared__ int cnt[kCells];       // counts, then fill cursors
+    __shared__ int off[kCells + 1];   // cell offsets
+    __shared__ int wtot[kPrepThreads / 64];
+    __shared__ int sidx[kPrepLds];    // the cell lists (n <= kPrepLds)
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n = min(max(*n_ptr, 0), cap);
+    const bool lds = n <= kPrepLds;
+    int* const idx = lds ? sidx : cell_idx;
     // the call's scratch words, in place of fill launches (the later kernels of the call read them)
     for (int i = tid; i < z.n_7f; i += kPrepThreads) z.fill_7f[i] = 0x7f7f7f7f;
     for (int i = tid; i < z.n_m1; i += kPrepThreads) z.fill_m1[i] = -1;
@@ -647,20 +654,26 @@ __global__ __launch_bounds__(kPrepThreads) void k_frame_prep(const orb_keypoint_
     if (tid == 0 && z.dims0 >= 0) z.dims[0] = z.dims0;
     for (int c = tid; c < kCells; c += kPrepThreads) cnt[c] = 0;
     __syncthreads();
-    for (int i = tid; i < n; i += kPrepThreads) {
-        const orb_keypoint_t kp = kps[i];
-        kp4[i] = make_float4(kp.x, kp.y, kp.angle, __int_as_float(kp.octave));
-        const int px = (int)roundf((kp.x - min_x) * inv_w);
-        const int py = (int)roundf((kp.y - min_y) * inv_h);
+    int mine[kPrepPer];
+#pragma unroll
+    for (int k = 0; k < kPrepPer; ++k) {
+        const int i = tid + k * kPrepThreads;
         int cell = -1;
-        if (px >= 0 && px < kGridCols && py >= 0 && py < kGridRows) {
-            cell = px * kGridRows + py;
-            atomicAdd(&cnt[cell], 1);
+        if (i < n) {
+            const orb_keypoint_t kp = kps[i];
+            kp4[i] = make_float4(kp.x, kp.y, kp.angle, __int_as_float(kp.octave));
+            const int px = (int)roundf((kp.x - min_x) * inv_w);
+            const int py = (int)roundf((kp.y - min_y) * inv_h);
+            if (px >= 0 && px < kGridCols && py >= 0 && py < kGridRows) {
+                cell = px * kGridRows + py;
+                atomicAdd(&cnt[cell], 1);
+            }
+            cell_of[i] = cell;
         }
-        cell_of[i] = cell;
+        mine[k] = cell;
     }
     __syncthreads();
-    // exclusive scan of the 3072 counts: three cells per thread
+    // exclusive scan of the 3072 counts: three cells per thread, a wave scan, the wave totals
     constexpr int kPer = kCells / kPrepThreads;
     static_assert(kCells % kPrepThreads == 0, "cells per thread");
     int loc[kPer], sum = 0;
@@ -669,41 +682,45 @@ __global__ __launch_bounds__(kPrepThreads) void k_frame_prep(const orb_keypoint_
         loc[q] = sum;
         sum += cnt[tid * kPer + q];
     }
-    part[tid] = sum;
-    __syncthreads();
-    for (int o = 1; o < kPrepThreads; o <<= 1) {
-        const int v = tid >= o ? part[tid - o] : 0;
-        __syncthreads();
-        part[tid] += v;
-        __syncthreads();
+    int incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
     }
-    const int base = part[tid] - sum;
+    if (lane == 63) wtot[wv] = incl;
     __syncthreads();
+    int base = incl - sum;
+    for (int w = 0; w < wv; ++w) base += wtot[w];
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
-        cell_off[tid * kPer + q] = base + loc[q];
+        off[tid * kPer + q] = base + loc[q];
         cnt[tid * kPer + q] = base + loc[q];  // becomes the fill cursor
     }
-    if (tid == kPrepThreads - 1) cell_off[kCells] = base + sum;
+    if (tid == kPrepThreads - 1) off[kCells] = base + sum;
     if (tid == 0) {
         *n_out0 = n;
         if (n_out1) *n_out1 = n;
     }
     __syncthreads();
-    for (int i = tid; i < n; i += kPrepThreads) {
-        const int c = cell_of[i];
-        if (c >= 0) cell_idx[atomicAdd(&cnt[c], 1)] = i;
-    }
+#pragma unroll
+    for (int k = 0; k < kPrepPer; ++k)
+        if (mine[k] >= 0) idx[atomicAdd(&cnt[mine[k]], 1)] = tid + k * kPrepThreads;
     __threadfence_block();
     __syncthreads();
     for (int c = tid; c < kCells; c += kPrepThreads) {  // index order inside each cell (insertion sort)
-        const int b = c == 0 ? 0 : cell_off[c], e = cell_off[c + 1];
+        const int b = off[c], e = off[c + 1];
         for (int a = b + 1; a < e; ++a) {
-            const int v = cell_idx[a];
+            const int v = idx[a];
             int k = a;
-            for (; k > b && cell_idx[k - 1] > v; --k) cell_idx[k] = cell_idx[k - 1];
-            cell_idx[k] = v;
+            for (; k > b && idx[k - 1] > v; --k) idx[k] = idx[k - 1];
+            idx[k] = v;
         }
+    }
+    for (int c = tid; c <= kCells; c += kPrepThreads) cell_off[c] = off[c];
+    if (lds) {
+        __syncthreads();
+        for (int i = tid; i < n; i += kPrepThreads) cell_idx[i] = sidx[i];
     }
 }
 
@@ -717,7 +734,7 @@ __global__ __launch_bounds__(256) void k_last_prep(const orb_keypoint_t* __restr
     const int n = min(max(*n_ptr, 0), cap);
     if (i == 0) {
         *n_out0 = n;
-        *n_out1 = n;
+        if (n_out1) *n_out1 = n;
     }
     if (i >= n) return;
     const orb_keypoint_t kp = kps[i];
