@@ -625,6 +625,52 @@ int orb_tracking_discard_outliers_device(const orb_pose_frame_t* d_frame, const 
 int orb_tracking_local_seen_device(const int32_t* d_match_a, int cap, int last_cap, const int32_t* d_last_row,
                                    int n_local, uint8_t* d_in_view, void* stream);
 
+/* The whole chain in one call (the sequence above): SearchByProjection(F, LastFrame)
+ * -> PoseOptimization -> isInFrustum at the new pose + the seen skip -> discard -> SearchByProjection(F,
+ * local points) -> PoseOptimization, every stage async on `stream`.  The caller owns the per-frame
+ * device buffers (sized for frame->cap; m1 / m2 and the pose outputs are the results) and the local
+ * map's tracking-field arrays (local->track_* are written by the frustum stage). */
+typedef struct orb_tracking_chain_params {
+    float th_motion;            /* TrackWithMotionModel's th: 7 stereo, 15 otherwise (src/Tracking.cc:4141-4146);
+                                   the caller's nmatches < 20 retry passes 2 th */
+    int32_t mono;               /* bMono of SearchByProjection(F, LastFrame) */
+    float th_local;             /* SearchLocalPoints' th (src/Tracking.cc:4801-4823) */
+    int32_t far_points;         /* mpLocalMapper->mbFarPoints */
+    float th_far_points;        /* mpLocalMapper->mThFarPoints */
+    float viewing_cos_limit;    /* isInFrustum's 0.5 */
+} orb_tracking_chain_params_t;
+
+typedef struct orb_tracking_chain_buffers {
+    int32_t* m1;                /* cap: SearchByProjection(LastFrame)'s last-frame row per keypoint, after the discard */
+    int32_t* m2;                /* cap: SearchByProjection(local)'s local point per keypoint */
+    int32_t* n_match;           /* 2: the two searches' counts */
+    orb_pose_frame_t* frames;   /* 2: the two PoseOptimization graphs' frame records */
+    orb_pose_edge_t* edges1;    /* cap */
+    orb_pose_edge_t* edges2;    /* cap */
+    int32_t* edge_kp1;          /* cap: keypoint of each edge */
+    int32_t* edge_kp2;
+    uint8_t* outlier1;          /* cap: mvbOutlier per edge */
+    uint8_t* outlier2;
+    double* poses;              /* 14: the two optimised poses (SE3Quat vectors) */
+    int32_t* inliers;           /* 2: the two PoseOptimization returns */
+    int32_t* n_out;             /* 2: nmatches after the discard, nmatchesMap */
+    uint8_t* taken;             /* cap: SearchLocalPoints' skip set */
+} orb_tracking_chain_buffers_t;
+
+/* m_motion: ORBmatcher(0.9, true); m_local: ORBmatcher(0.8) (the handles' ratio / orientation).
+ * local: the local map's view (track_* arrays written here); pos / normal / min_dist / max_dist:
+ * GetWorldPos / GetNormal / mfMinDistance / mfMaxDistance per local point; last_row: -1 or the last
+ * frame's row holding the point (NULL: none holds one).  frustum: the frame's bounds, camera, log scale
+ * and levels (its pose fields are ignored).  pose7: the motion model's pose as PoseOptimization reads
+ * it (tx ty tz qx qy qz qw of the frame's float pose; frame->Tcw must be the same pose). */
+int orb_tracking_chain_device(orb_matcher_t m_motion, orb_matcher_t m_local, const orb_frame_device_t* frame,
+                              const orb_last_points_device_t* last, const orb_local_points_device_t* local,
+                              const float* d_pos, const float* d_normal, const float* d_min_dist,
+                              const float* d_max_dist, const int32_t* d_last_row, const orb_frustum_frame_t* frustum,
+                              const float* inv_level_sigma2, const double pose7[7],
+                              const orb_tracking_chain_params_t* params, const orb_tracking_chain_buffers_t* bufs,
+                              void* stream);
+
 /* ---- multi-GPU local BA: one process per GPU, every rank passes the same
  * problem; rank r owns a contiguous, edge-balanced range of the landmarks and their edges, and
  * the ranks all-reduce the partial Hpp/b_p, the partial reduced camera system (S, b_S) of each LM

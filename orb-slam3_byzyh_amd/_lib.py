@@ -122,6 +122,8 @@ PROTOTYPES = {
     "orb_tracking_pose_edges_device": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "orb_tracking_discard_outliers_device": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp]),
     "orb_tracking_local_seen_device": (_i, [_vp, _i, _i, _vp, _i, _vp, _vp]),
+    "orb_tracking_chain_device": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                        _vp]),
     "orb_ba_create": (_i, [ctypes.POINTER(_vp)]),
     "orb_ba_destroy": (_i, [_vp]),
     "orb_ba_optimize": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),

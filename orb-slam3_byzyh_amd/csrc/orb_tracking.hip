@@ -228,4 +228,53 @@ int orb_tracking_discard_outliers_device(const orb_pose_frame_t* d_frame, const 
     return ORB_OK;
 }
 
+int orb_tracking_chain_device(orb_matcher_t m_motion, orb_matcher_t m_local, const orb_frame_device_t* F,
+                              const orb_last_points_device_t* last, const orb_local_points_device_t* local,
+                              const float* d_pos, const float* d_normal, const float* d_min_dist,
+                              const float* d_max_dist, const int32_t* d_last_row, const orb_frustum_frame_t* frustum,
+                              const float* inv_level_sigma2, const double pose7[7],
+                              const orb_tracking_chain_params_t* P, const orb_tracking_chain_buffers_t* B,
+                              void* stream) {
+    if (!m_motion || !m_local || !F || !last || !local || !frustum || !inv_level_sigma2 || !pose7 || !P || !B ||
+        !B->m1 || !B->m2 || !B->n_match || !B->frames || !B->edges1 || !B->edges2 || !B->edge_kp1 || !B->edge_kp2 ||
+        !B->outlier1 || !B->outlier2 || !B->poses || !B->inliers || !B->n_out || !B->taken ||
+        (local->n > 0 && (!d_pos || !d_normal || !d_min_dist || !d_max_dist)))
+        return orbgpu_fail(ORB_ERR_ARG, "bad tracking chain arguments");
+    int rc;
+    if ((rc = orb_search_by_projection_frame_device(m_motion, F, last, P->th_motion, P->mono, B->m1, B->n_match, stream)))
+        return rc;
+    if ((rc = orb_tracking_pose_edges_device(F, B->m1, last->xyz, nullptr, nullptr, inv_level_sigma2, nullptr, pose7,
+                                             B->frames, B->edges1, B->edge_kp1, stream)))
+        return rc;
+    if ((rc = orb_pose_optimization_device(1, B->frames, F->cap, B->edges1, B->poses, B->outlier1, B->inliers, stream)))
+        return rc;
+    // isInFrustum at the first pose and the seen skip read the first search's assignments, which the
+    // discard does not change (the reference marks its discarded outliers seen too, Tracking.cc:4195)
+    if (local->n > 0) {
+        if ((rc = orb_is_in_frustum_pose_device(frustum, B->poses, local->n, d_pos, d_normal, d_min_dist, d_max_dist,
+                                                P->viewing_cos_limit, const_cast<uint8_t*>(local->track_in_view),
+                                                const_cast<float*>(local->track_proj), const_cast<float*>(local->track_depth),
+                                                const_cast<int32_t*>(local->track_level),
+                                                const_cast<float*>(local->track_view_cos), stream)))
+            return rc;
+        if (d_last_row &&
+            (rc = orb_tracking_local_seen_device(B->m1, F->cap, last->cap, d_last_row, local->n,
+                                                 const_cast<uint8_t*>(local->track_in_view), stream)))
+            return rc;
+    }
+    if ((rc = orb_tracking_discard_outliers_device(B->frames, B->edge_kp1, B->outlier1, B->m1, last->observed, nullptr,
+                                                   nullptr, B->n_out, F->cap, B->taken, stream)))
+        return rc;
+    if ((rc = orb_search_by_projection_local_device(m_local, F, B->taken, local, P->th_local, P->far_points,
+                                                    P->th_far_points, B->m2, B->n_match + 1, stream)))
+        return rc;
+    const bool has_local = local->n > 0;  // an empty local map: the second search assigned nothing
+    if ((rc = orb_tracking_pose_edges_device(F, B->m1, last->xyz, has_local ? B->m2 : nullptr, has_local ? d_pos : nullptr,
+                                             inv_level_sigma2, B->poses, nullptr, B->frames + 1, B->edges2, B->edge_kp2,
+                                             stream)))
+        return rc;
+    return orb_pose_optimization_device(1, B->frames + 1, F->cap, B->edges2, B->poses + 7, B->outlier2, B->inliers + 1,
+                                        stream);
+}
+
 }  // extern "C"

@@ -58,6 +58,18 @@ class LocalPointsDeviceView(ctypes.Structure):  # orb_local_points_device_t
                 ("track_depth", ctypes.c_void_p), ("track_level", ctypes.c_void_p), ("desc", ctypes.c_void_p)]
 
 
+class TrackingChainParams(ctypes.Structure):  # orb_tracking_chain_params_t
+    _fields_ = [("th_motion", ctypes.c_float), ("mono", ctypes.c_int32), ("th_local", ctypes.c_float),
+                ("far_points", ctypes.c_int32), ("th_far_points", ctypes.c_float),
+                ("viewing_cos_limit", ctypes.c_float)]
+
+
+class TrackingChainBuffers(ctypes.Structure):  # orb_tracking_chain_buffers_t
+    _fields_ = [(k, ctypes.c_void_p) for k in ("m1", "m2", "n_match", "frames", "edges1", "edges2", "edge_kp1",
+                                               "edge_kp2", "outlier1", "outlier2", "poses", "inliers", "n_out",
+                                               "taken")]
+
+
 def _stream_handle(stream, device):
     import torch
     st = stream if stream is not None else torch.cuda.current_stream(device)
@@ -98,16 +110,22 @@ class DeviceFrame:
     def set_pose(self, Tcw) -> None:
         self.Tcw = np.ascontiguousarray(Tcw, np.float32).reshape(3, 4)
         self._view.Tcw[:] = [float(x) for x in self.Tcw.reshape(-1)]
+        self._ff = None
 
     def view(self) -> FrameDeviceView:
         return self._view
 
     def frustum_frame(self, scale_factor: float = 1.2) -> FrustumFrame:
         """orb_frustum_frame_t of this frame (pose fields unused by orb_is_in_frustum_pose_device)."""
+        key = float(scale_factor)
+        if getattr(self, "_ff", None) is not None and self._ff[0] == key:
+            return self._ff[1]
         T = self.Tcw.reshape(12)
-        return FrustumFrame((ctypes.c_float * 12)(*T), (ctypes.c_float * 3)(0, 0, 0), self.fx, self.fy, self.cx,
-                            self.cy, self.mbf, self.mnMinX, self.mnMaxX, self.mnMinY, self.mnMaxY,
-                            float(logf(scale_factor)), len(self.mvScaleFactors))
+        ff = FrustumFrame((ctypes.c_float * 12)(*T), (ctypes.c_float * 3)(0, 0, 0), self.fx, self.fy, self.cx,
+                          self.cy, self.mbf, self.mnMinX, self.mnMaxX, self.mnMinY, self.mnMaxY,
+                          float(logf(scale_factor)), len(self.mvScaleFactors))
+        self._ff = (key, ff)
+        return ff
 
 
 class DeviceLastPoints:
@@ -223,6 +241,16 @@ class TrackingChain:
         self.inliers = torch.zeros(2, dtype=torch.int32, device=d)
         self.n_out = torch.zeros(2, dtype=torch.int32, device=d)
         self.taken = torch.empty(c, dtype=torch.uint8, device=d)
+        self._h_motion, self._h_local = self.m_motion._handle(), self.m_local._handle()
+        self._params = TrackingChainParams(self.th_motion, int(self.mono), self.th_local, int(self.far_points),
+                                           self.th_far_points, self.viewing_cos_limit)
+        fsz = POSE_FRAME_DTYPE.itemsize
+        self._bufs = TrackingChainBuffers(
+            self.m1.data_ptr(), self.m2.data_ptr(), self.n_match.data_ptr(), self.frames.data_ptr(),
+            self.edges[0].data_ptr(), self.edges[1].data_ptr(), self.edge_kp[0].data_ptr(),
+            self.edge_kp[1].data_ptr(), self.outlier[0].data_ptr(), self.outlier[1].data_ptr(),
+            self.poses.data_ptr(), self.inliers.data_ptr(), self.n_out.data_ptr(), self.taken.data_ptr())
+        assert self.frames.numel() == 2 * fsz
 
     def track(self, cur: DeviceFrame, last: DeviceLastPoints, local: DeviceLocalMap, pose7, stream=None,
               wide: bool = False) -> TrackResult:
@@ -235,52 +263,16 @@ class TrackingChain:
             raise ValueError(f"frame capacity {cur.cap} exceeds the chain's {self.cap}")
         lib = _lib.load()
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
-        s = ctypes.c_void_p(st.cuda_stream)
-        fv = cur.view()
-        fsz = POSE_FRAME_DTYPE.itemsize
-        fr0, fr1 = self.frames.data_ptr(), self.frames.data_ptr() + fsz
         p0 = np.ascontiguousarray(pose7, np.float64).reshape(7)
-        isg = cur.mvInvLevelSigma2
-        nm = self.n_match.data_ptr()
-        th = self.th_motion * (2 if wide else 1)
-        check(lib.orb_search_by_projection_frame_device(self.m_motion._handle(), ctypes.byref(fv),
-                                                        ctypes.byref(last.view()), th, int(self.mono),
-                                                        self.m1.data_ptr(), nm, s),
-              "orb_search_by_projection_frame_device")
-        check(lib.orb_tracking_pose_edges_device(ctypes.byref(fv), self.m1.data_ptr(), last.xyz.data_ptr(), None, None,
-                                                 isg.ctypes.data, None, p0.ctypes.data, fr0, self.edges[0].data_ptr(),
-                                                 self.edge_kp[0].data_ptr(), s), "orb_tracking_pose_edges_device")
-        check(lib.orb_pose_optimization_device(1, fr0, cur.cap, self.edges[0].data_ptr(), self.poses[0].data_ptr(),
-                                               self.outlier[0].data_ptr(), self.inliers.data_ptr(), s),
-              "orb_pose_optimization_device")
-        ff = cur.frustum_frame(self.scale_factor)
-        check(lib.orb_is_in_frustum_pose_device(ctypes.byref(ff), self.poses[0].data_ptr(), local.n,
-                                                local.pos.data_ptr(), local.normal.data_ptr(),
-                                                local.min_dist.data_ptr(), local.max_dist.data_ptr(),
-                                                self.viewing_cos_limit, local.track_in_view.data_ptr(),
-                                                local.track_proj.data_ptr(), local.track_depth.data_ptr(),
-                                                local.track_level.data_ptr(), local.track_view_cos.data_ptr(), s),
-              "orb_is_in_frustum_pose_device")
-        if local.last_row is not None and local.n > 0:
-            check(lib.orb_tracking_local_seen_device(self.m1.data_ptr(), cur.cap, last.cap, local.last_row.data_ptr(),
-                                                     local.n, local.track_in_view.data_ptr(), s),
-                  "orb_tracking_local_seen_device")
-        check(lib.orb_tracking_discard_outliers_device(fr0, self.edge_kp[0].data_ptr(), self.outlier[0].data_ptr(),
-                                                       self.m1.data_ptr(), last.observed.data_ptr(), None, None,
-                                                       self.n_out.data_ptr(), cur.cap, self.taken.data_ptr(), s),
-              "orb_tracking_discard_outliers_device")
-        check(lib.orb_search_by_projection_local_device(self.m_local._handle(), ctypes.byref(fv),
-                                                        self.taken.data_ptr(), ctypes.byref(local.view()),
-                                                        self.th_local, int(self.far_points), self.th_far_points,
-                                                        self.m2.data_ptr(), nm + 4, s),
-              "orb_search_by_projection_local_device")
-        has_local = local.n > 0  # an empty local map: the second search assigned nothing
-        check(lib.orb_tracking_pose_edges_device(ctypes.byref(fv), self.m1.data_ptr(), last.xyz.data_ptr(),
-                                                 self.m2.data_ptr() if has_local else None,
-                                                 local.pos.data_ptr() if has_local else None, isg.ctypes.data,
-                                                 self.poses[0].data_ptr(), None, fr1, self.edges[1].data_ptr(),
-                                                 self.edge_kp[1].data_ptr(), s), "orb_tracking_pose_edges_device")
-        check(lib.orb_pose_optimization_device(1, fr1, cur.cap, self.edges[1].data_ptr(), self.poses[1].data_ptr(),
-                                               self.outlier[1].data_ptr(), self.inliers.data_ptr() + 4, s),
-              "orb_pose_optimization_device")
+        self._params.th_motion = self.th_motion * (2 if wide else 1)
+        lr = local.last_row
+        check(lib.orb_tracking_chain_device(self._h_motion, self._h_local, ctypes.byref(cur.view()),
+                                            ctypes.byref(last.view()), ctypes.byref(local.view()),
+                                            local.pos.data_ptr(), local.normal.data_ptr(), local.min_dist.data_ptr(),
+                                            local.max_dist.data_ptr(), None if lr is None else lr.data_ptr(),
+                                            ctypes.byref(cur.frustum_frame(self.scale_factor)),
+                                            cur.mvInvLevelSigma2.ctypes.data, p0.ctypes.data,
+                                            ctypes.byref(self._params), ctypes.byref(self._bufs),
+                                            ctypes.c_void_p(st.cuda_stream)),
+              "orb_tracking_chain_device")
         return TrackResult(self, st)

@@ -5,7 +5,9 @@ k_describe on one handle's stream), then per batch its span (first start to last
 inside it, and the gaps between its kernels (the batch waiting for the device: other batches' kernels
 hold the CUs, or the host had not enqueued the next launch).  With H batches in flight the step time
 is about span / H when the batches overlap fully; the report says where each batch's span goes.
-    tools/c2_critical_path.py TRACE.csv [N_LAST_BATCHES]
+    tools/c2_critical_path.py TRACE.csv [N_BATCHES] [FIRST_BATCH]
+(default: the N_BATCHES (20) consecutive batches with the shortest start-to-start period, i.e. the
+bench's steady timed steps, not the warm-up or the instrumented second pass)
 """
 import collections
 import csv
@@ -38,8 +40,13 @@ for key, rs in by_stream.items():
     if cur and short(cur[-1]["Kernel_Name"]) == "k_describe":
         batches.append((key, cur))
 batches.sort(key=lambda b: int(b[1][0]["Start_Timestamp"]))
-nlast = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-sel = batches[-nlast:]
+nsel = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+bstart = [int(rs[0]["Start_Timestamp"]) for _, rs in batches]
+if len(sys.argv) > 3:
+    first = int(sys.argv[3])
+else:
+    first = min(range(max(1, len(batches) - nsel)), key=lambda i: bstart[min(i + nsel, len(bstart) - 1)] - bstart[i])
+sel = batches[first:first + nsel]
 spans, busy, gaps = [], [], []
 stage_t = collections.defaultdict(list)
 gap_before = collections.defaultdict(list)
@@ -63,7 +70,7 @@ for _, rs in sel:
         stage_t[nm].append(v / 1e3)
 starts = [int(rs[0]["Start_Timestamp"]) for _, rs in sel]
 period = (starts[-1] - starts[0]) / 1e3 / max(1, len(starts) - 1)
-print(f"{len(batches)} batches in the trace on {len(by_stream)} streams; the last {len(sel)}:")
+print(f"{len(batches)} batches in the trace on {len(by_stream)} streams; batches {first}..{first + len(sel) - 1}:")
 print(f"  batch span median {st.median(spans):.1f} us = kernels {st.median(busy):.1f} + gaps {st.median(gaps):.1f}")
 print(f"  a batch starts every {period:.1f} us (step time per batch); span / period = {st.median(spans) / period:.2f} "
       "batches in flight")
