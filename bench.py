@@ -725,12 +725,13 @@ def bench_tracking_chain(pkg, synth, dev, steps, cpu_baseline_on, n_scenes=8, ba
     for _ in range(3):
         ch.track(cur, last, local, sc["pose7_pred"], stream=st)
         st.synchronize()
-    lat, gpu = [], []
+    lat, gpu, enq = [], [], []
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(reps):
         t0 = time.perf_counter()
         e0.record(st)
         ch.track(cur, last, local, sc["pose7_pred"], stream=st)
+        enq.append((time.perf_counter() - t0) * 1e3)
         e1.record(st)
         st.synchronize()
         lat.append((time.perf_counter() - t0) * 1e3)
@@ -756,6 +757,7 @@ def bench_tracking_chain(pkg, synth, dev, steps, cpu_baseline_on, n_scenes=8, ba
                      f"{L.N} keypoints / {int(L.map_points['valid'].sum())} map points, {len(sc['local']['pos'])} local "
                      f"map points; th 7 / 1, ORBmatcher(0.9, true) / (0.8); device-resident, one GPU",
            "single_frame_ms": round(float(np.median(lat)), 4), "single_frame_gpu_ms": round(float(np.median(gpu)), 4),
+           "single_frame_enqueue_ms": round(float(np.median(enq)), 4),
            "batched_frames_per_ms": round(batch * brep / bdt, 4), "batch": batch, "streams": n_streams,
            "matches_last_frame": n1, "matches_local_map": n2, "dtype": "u8 / f32 / f64"}
     if cpu_baseline_on:

@@ -38,14 +38,11 @@ namespace {
 #ifndef ORB_POSE_THREADS
 #define ORB_POSE_THREADS 256
 #endif
-#ifndef ORB_POSE_REG_EDGES
-#define ORB_POSE_REG_EDGES 512
-#endif
 constexpr int kPT = ORB_POSE_THREADS;  // threads per frame
 constexpr int kPW = kPT / 64;          // waves
-constexpr int kEdgeSlots = ORB_POSE_REG_EDGES / kPT;  // edges per thread kept in registers
-constexpr int kLdsSlots = (2048 - ORB_POSE_REG_EDGES) / kPT;  // and in LDS (2048 per frame in all)
-static_assert(kPT % 64 == 0 && kEdgeSlots >= 0 && kLdsSlots >= 1 && kPW <= 32, "pose workgroup shape");
+constexpr int kCap = 2048;             // edges per frame held in LDS (beyond: read from memory every pass)
+constexpr int kPair = 2 * kPT;         // edge positions per pair step of the pass
+static_assert(kPT % 64 == 0 && kCap % kPair == 0 && kPW <= 32, "pose workgroup shape");
 
 static_assert(sizeof(orb_pose_edge_t) == 56, "pose edge layout");
 
@@ -444,6 +441,111 @@ __device__ __forceinline__ double linearize_edge(const orb_pose_edge_t& Ed, cons
     return chi2;
 }
 
+// linearize_edge for one edge type known at compile time, without branches (the Huber weight by
+// selects; a non-robust pass passes an infinite dsq), split in two: lin_front computes the error, the
+// Jacobian rows and the weight, lin_accum adds the products to the sums.  A pair step runs both fronts
+// before both accumulations, so that the scheduler can overlap the two edges' dependent chains (one
+// wave per SIMD cannot hide a single edge's).  Same arithmetic as linearize_edge.
+struct EdgeLin {
+    double r0[6], r1[6], r2[6], e0, e1, e2, w, rho0, chi2;
+};
+template <bool St>
+__device__ __forceinline__ EdgeLin lin_front(double X, double Y, double Z, double o0, double o1, double o2, float isg,
+                                             const PoseRT& P, const orb_ba_camera_t& cam, double delta, double dsq,
+                                             bool on) {
+    EdgeLin L;
+    const double x = P.r[0] * X + P.r[1] * Y + P.r[2] * Z + P.t[0];
+    const double y = P.r[3] * X + P.r[4] * Y + P.r[5] * Z + P.t[1];
+    const double z = P.r[6] * X + P.r[7] * Y + P.r[8] * Z + P.t[2];
+    const double fx = cam.fx, fy = cam.fy;
+    const double iz = on ? rcp_nr(z) : 0.0, iz2 = iz * iz;
+    L.e2 = 0.0;
+    if constexpr (!St) {
+        L.e0 = o0 - (fx * x * iz + (double)cam.cx);
+        L.e1 = o1 - (fy * y * iz + (double)cam.cy);
+        const double j00 = -(fx * iz), j02 = fx * x * iz2, j11 = -(fy * iz), j12 = fy * y * iz2;
+        L.r0[0] = j02 * y; L.r0[1] = j00 * z - j02 * x; L.r0[2] = -j00 * y; L.r0[3] = j00; L.r0[4] = 0; L.r0[5] = j02;
+        L.r1[0] = -j11 * z + j12 * y; L.r1[1] = -j12 * x; L.r1[2] = j11 * x; L.r1[3] = 0; L.r1[4] = j11; L.r1[5] = j12;
+    } else {
+        const float finvz = (float)iz;
+        const double u = x * finvz * fx + (double)cam.cx;
+        const double v = y * finvz * fy + (double)cam.cy;
+        L.e0 = o0 - u;
+        L.e1 = o1 - v;
+        L.e2 = o2 - (u - (double)cam.bf * finvz);
+        const double bf = cam.bf;
+        L.r0[0] = x * y * iz2 * fx; L.r0[1] = -(1 + (x * x * iz2)) * fx; L.r0[2] = y * iz * fx;
+        L.r0[3] = -iz * fx; L.r0[4] = 0; L.r0[5] = x * iz2 * fx;
+        L.r1[0] = (1 + y * y * iz2) * fy; L.r1[1] = -x * y * iz2 * fy; L.r1[2] = -x * iz * fy;
+        L.r1[3] = 0; L.r1[4] = -iz * fy; L.r1[5] = y * iz2 * fy;
+        L.r2[0] = L.r0[0] - bf * y * iz2; L.r2[1] = L.r0[1] + bf * x * iz2; L.r2[2] = L.r0[2];
+        L.r2[3] = L.r0[3]; L.r2[4] = 0; L.r2[5] = L.r0[5] - bf * iz2;
+    }
+    const double info = on ? (double)isg : 0.0;
+    double chi2 = L.e0 * info * L.e0 + L.e1 * info * L.e1;
+    if constexpr (St) chi2 += L.e2 * info * L.e2;
+    const double rs = rsq_nr(chi2);  // unused (possibly not finite) unless the edge is beyond dsq
+    const bool big = !(chi2 <= dsq);
+    L.rho0 = big ? 2 * (chi2 * rs) * delta - dsq : chi2;
+    const double rho1 = big ? delta * rs : 1.0;
+    L.w = rho1 * info;
+    L.chi2 = chi2;
+    return L;
+}
+template <bool St>
+__device__ __forceinline__ void lin_accum(const EdgeLin& L, double (&acc)[32]) {
+    acc[27] += L.rho0;
+    constexpr bool nz0[6] = {true, true, true, true, false, true};   // rows 0 and 2
+    constexpr bool nz1[6] = {true, true, true, false, true, true};   // row 1
+    double w0[6], w1[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        w0[i] = L.w * L.r0[i];
+        w1[i] = L.w * L.r1[i];
+    }
+    {
+        int k = 0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int j = i; j < 6; ++j, ++k) {
+                if (nz0[i] && nz0[j]) acc[k] += w0[i] * L.r0[j];
+                if (nz1[i] && nz1[j]) acc[k] += w1[i] * L.r1[j];
+            }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            if (nz0[i]) acc[21 + i] -= w0[i] * L.e0;
+            if (nz1[i]) acc[21 + i] -= w1[i] * L.e1;
+        }
+    }
+    if constexpr (St) {
+        double w2[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) w2[i] = L.w * L.r2[i];
+        int k = 0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int j = i; j < 6; ++j, ++k)
+                if (nz0[i] && nz0[j]) acc[k] += w2[i] * L.r2[j];
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+            if (nz0[i]) acc[21 + i] -= w2[i] * L.e2;
+    }
+}
+// both edges of a pair step of one type: both fronts, then both accumulations
+template <bool St>
+__device__ __forceinline__ void lin_pair(const double2 (&xw)[3], const double2 (&ob)[3], float2 is, const PoseRT& P,
+                                         const orb_ba_camera_t& cam, double delta, double dsq, double (&acc)[32],
+                                         bool on0, bool on1, double& c0, double& c1) {
+    const EdgeLin a = lin_front<St>(xw[0].x, xw[1].x, xw[2].x, ob[0].x, ob[1].x, ob[2].x, is.x, P, cam, delta, dsq, on0);
+    const EdgeLin b = lin_front<St>(xw[0].y, xw[1].y, xw[2].y, ob[0].y, ob[1].y, ob[2].y, is.y, P, cam, delta, dsq, on1);
+    lin_accum<St>(a, acc);
+    lin_accum<St>(b, acc);
+    c0 = a.chi2;
+    c1 = b.chi2;
+}
+
 // Phase stamps of frame 0 (orb_debug_pose_trace, tools/pose_trace.py): per LM trial, s_memtime at the
 // pass start, after the pass's reduction, after the totals reached thread 0, after its decision and
 // solve, after the barrier that ends the trial, and inside the solve: its start, after the LDL^T,
@@ -458,14 +560,17 @@ struct LmState {
     int nbad, qmax, it, ok, cur;  // cur: the buffer of sys holding the system
 };
 
-// One workgroup per frame.  The first kS * kPT edges of the frame (and their outlier flag and last
-// chi2) stay in registers for the whole optimisation, sorted by type -- the monocular edges first, then
-// the stereo ones, each in index order -- so that a wave runs one edge type's path; edges beyond are read
-// from memory on every pass.  Every trial evaluates the new pose and linearises there in the same pass:
-// g2o rebuilds the system at the accepted state before the next iteration, and a rejected trial keeps
-// the old linearisation, so the next iteration's build is this pass's sums.  Thread 0 holds the LM
-// state; per trial it takes the totals, decides, and solves the next trial, between two barriers.
-template <int kS>
+// One workgroup per frame.  The frame's first kCap edges live in LDS for the whole optimisation,
+// field by field (structure of arrays), sorted by type -- the monocular edges first, then the stereo
+// ones, each in index order -- with their outlier flag and last chi2; edges beyond are read from memory
+// on every pass.  A pass steps over the positions in pairs: thread t takes positions 2t and 2t + 1 of
+// each 2 kPT block, both of one type in every wave but the one at the type boundary, so that the two
+// linearisations are straight-line code of one type that the scheduler interleaves (one wave per SIMD
+// cannot hide a single edge's dependent FP64 chain).  Every trial evaluates the new pose and linearises
+// there in the same pass: g2o rebuilds the system at the accepted state before the next iteration, and
+// a rejected trial keeps the old linearisation, so the next iteration's build is this pass's sums.
+// Thread 0 holds the LM state; per trial it takes the totals, decides, and solves the next trial,
+// between two barriers.
 __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __restrict__ frames,
                                                   const orb_pose_edge_t* __restrict__ edges,
                                                   double* __restrict__ pose_out, uint8_t* __restrict__ level,
@@ -473,10 +578,13 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
     __shared__ double part[kPW * 32];
     __shared__ double T[7];
     __shared__ int s_state;  // 1: evaluate the trial pose in T, 2: the round's optimize() is done
-    constexpr int kA = kS + kLdsSlots;  // slots per thread: registers, then LDS
-    __shared__ int perm[kA * kPT];      // slot position -> edge index
+    constexpr int kA = kCap / kPT;  // edges ranked per thread by the type sort
+    __shared__ int perm[kCap];      // position -> edge index
     __shared__ int scan[kPT];
-    __shared__ orb_pose_edge_t led[kLdsSlots * kPT];
+    __shared__ double lxw[3][kCap], lob[3][kCap];  // xw, obs by position
+    __shared__ float lis[kCap];                    // inv_sigma2
+    __shared__ double lch[kCap];                   // last chi2
+    __shared__ uint8_t llv[kCap];                  // level (1: outlier)
     const int tid = threadIdx.x, f = blockIdx.x;
     long long* const tr = f == 0 ? g_pose_trace : nullptr;
     const int tr_cap = g_pose_trace_cap;
@@ -495,8 +603,11 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
         if (tid == 0) inliers[f] = 0;
         return;
     }
-    // ---- the slot edges sorted by type: thread t ranks edges [kA t, kA t + kA)
-    const int nr = min(n, kA * kPT);
+    // ---- the LDS edges sorted by type: thread t ranks edges [kA t, kA t + kA).  The monocular edges
+    // take positions [0, nmono), the stereo ones start at s0 (nmono rounded up to a wave's 128 positions
+    // of a pair step, the gap filled with dummies), so every wave of a pair step runs one edge type.
+    const int nr = min(n, kCap - 128);
+    int nmono, s0, npos;
     {
         int mono = 0;
         bool st[kA];
@@ -514,64 +625,61 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
             scan[tid] += v;
             __syncthreads();
         }
-        const int nmono = scan[kPT - 1];
+        nmono = scan[kPT - 1];
+        s0 = (nmono + 127) & ~127;
+        npos = s0 + nr - nmono;
         int rm = scan[tid] - mono;       // monocular edges before this thread's
         int rs = kA * tid - rm;          // stereo edges before this thread's (of the e < nr ones)
 #pragma unroll
         for (int s = 0; s < kA; ++s) {
             const int e = kA * tid + s;
-            if (e < nr) perm[st[s] ? nmono + rs++ : rm++] = e;
+            if (e < nr) perm[st[s] ? s0 + rs++ : rm++] = e;
         }
         __syncthreads();
     }
-    // register slots: edge, outlier flag, last chi2; LDS slots: the same in led / llv / lch
-    __shared__ uint8_t llv[kLdsSlots * kPT];
-    __shared__ double lch[kLdsSlots * kPT];
-    constexpr int kS1 = kS > 0 ? kS : 1;  // (array extent when no register slot is configured)
-    orb_pose_edge_t ed[kS1];
-    int lv[kS1];
-    double ch[kS1];
-    orb_pose_edge_t dummy{};  // a finite edge: the pass computes it with zero information
-    dummy.xw[2] = 1.0;
+    // the gap and the positions up to the pair step's round-up hold finite dummies (level 2: never
+    // active, computed with zero information)
+    const int nfill = (npos + kPair - 1) / kPair * kPair;
+    for (int q = tid; q < nfill; q += kPT) {
+        const bool real = q < nmono || (q >= s0 && q < npos);
+        if (real) {
+            const orb_pose_edge_t Ed = E[perm[q]];
 #pragma unroll
-    for (int s = 0; s < kS; ++s) {
-        const int p = tid + s * kPT;
-        ed[s] = p < nr ? E[perm[p]] : dummy;
-        lv[s] = 0;  // mvbOutlier[i] = false at edge creation
-        ch[s] = 0;
-    }
-    for (int q = tid; q < kLdsSlots * kPT; q += kPT) {
-        const int p = q + kS * kPT;
-        led[q] = p < nr ? E[perm[p]] : dummy;
-        llv[q] = 0;
+            for (int i = 0; i < 3; ++i) {
+                lxw[i][q] = Ed.xw[i];
+                lob[i][q] = Ed.obs[i];
+            }
+            lis[q] = Ed.inv_sigma2;
+        } else {
+            lxw[0][q] = 0; lxw[1][q] = 0; lxw[2][q] = 1.0;
+            lob[0][q] = 0; lob[1][q] = 0; lob[2][q] = 0;
+            lis[q] = 0;
+        }
+        llv[q] = real ? 0 : 2;  // mvbOutlier[i] = false at edge creation
         lch[q] = 0;
     }
-    for (int e = tid + kA * kPT; e < n; e += kPT) lev[e] = 0;
+    for (int e = tid + nr; e < n; e += kPT) lev[e] = 0;
     __syncthreads();
-    // fn(edge, outlier flag, last chi2) over this thread's edges
+    // fn(edge index, LDS position or -1, outlier flag, last chi2) over this thread's edges
     auto visit = [&](auto&& fn) {
-#pragma unroll
-        for (int s = 0; s < kS; ++s)
-            if (tid + s * kPT < nr) fn(ed[s], lv[s], ch[s]);
-        for (int q = tid; q + kS * kPT < nr; q += kPT) {
+        for (int q = tid; q < npos; q += kPT) {
             int l = llv[q];
+            if (l == 2) continue;
             double c = lch[q];
-            fn(led[q], l, c);
+            fn(perm[q], q, l, c);
             llv[q] = (uint8_t)l;
             lch[q] = c;
         }
-        for (int e = tid + kA * kPT; e < n; e += kPT) {
+        for (int e = tid + nr; e < n; e += kPT) {
             int l = lev[e];
             double c = ech[e];
-            fn(E[e], l, c);
+            fn(e, -1, l, c);
             lev[e] = (uint8_t)l;
             ech[e] = c;
         }
     };
     // a linearisation pass at T over the active edges (chi2 kept when `keep`), reduced: wave 0's lane
-    // 2k ends with the workgroup total of value k.  A slot is skipped by a wave none of whose lanes holds
-    // an edge there; inside a wave, an outlier slot computes with zero information.  The LDS slots run
-    // as a loop.
+    // 2k ends with the workgroup total of value k.  A wave skips the pair steps past the frame's edges.
     auto pass = [&](bool robust, bool keep, double (&acc)[32]) {
 #pragma unroll
         for (int k = 0; k < 32; ++k) acc[k] = 0;
@@ -579,27 +687,31 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
 #pragma unroll
         for (int i = 0; i < 7; ++i) Tl[i] = T[i];
         const PoseRT P = pose_rt(Tl);
-        const int wbase = tid & ~63;
+        const int wv = tid >> 6;
+        const double dsqm = robust ? (double)hub.dsqr_mono : INFINITY;
+        const double dsqs = robust ? (double)hub.dsqr_stereo : INFINITY;
         stamp(8);
+        for (int jb = 0; jb < npos; jb += kPair) {
+            const int wlo = jb + 128 * wv;  // the wave's first position (wave-uniform)
+            if (wlo >= npos) continue;
+            const int p = jb + 2 * tid;
+            double2 xw[3], ob[3];
 #pragma unroll
-        for (int s = 0; s < kS; ++s) {
-            if (wbase + s * kPT < nr) {  // wave-uniform
-                const bool on = tid + s * kPT < nr && !lv[s];
-                const double c2 = linearize_edge(ed[s], P, F.cam, robust, hub, acc, on);
-                if (keep && on) ch[s] = c2;
+            for (int i = 0; i < 3; ++i) {
+                xw[i] = *reinterpret_cast<const double2*>(&lxw[i][p]);
+                ob[i] = *reinterpret_cast<const double2*>(&lob[i][p]);
             }
-            stamp(9 + s);
-        }
-        {
-            const int nq = nr - kS * kPT;  // LDS slot positions in use
-            int q = tid;
-            for (int qb = wbase; qb < nq; qb += kPT, q += kPT) {  // wave-uniform trip count
-                const bool on = q < nq && !llv[q];
-                const double c2 = linearize_edge(led[q], P, F.cam, robust, hub, acc, on);
-                if (keep && on) lch[q] = c2;
+            const float2 is = *reinterpret_cast<const float2*>(&lis[p]);
+            const bool on0 = !llv[p], on1 = !llv[p + 1];
+            double c0, c1;
+            if (wlo < s0) lin_pair<false>(xw, ob, is, P, F.cam, hub.delta_mono, dsqm, acc, on0, on1, c0, c1);
+            else lin_pair<true>(xw, ob, is, P, F.cam, hub.delta_stereo, dsqs, acc, on0, on1, c0, c1);
+            if (keep) {
+                if (on0) lch[p] = c0;
+                if (on1) lch[p + 1] = c1;
             }
         }
-        for (int e = tid + kA * kPT; e < n; e += kPT) {
+        for (int e = tid + nr; e < n; e += kPT) {
             if (lev[e]) continue;
             const double c2 = linearize_edge(E[e], P, F.cam, robust, hub, acc, true);
             if (keep) ech[e] = c2;
@@ -658,7 +770,7 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
         __syncthreads();
         // ---- optimizer.initializeOptimization(0); optimizer.optimize(10)
         int active = 0;
-        visit([&](const orb_pose_edge_t&, int& l, double&) { active += l == 0; });
+        visit([&](int, int, int& l, double&) { active += l == 0; });
         active = __syncthreads_or(active);
         if (active) {
             int cur = 0;  // every thread tracks the system buffer
@@ -749,16 +861,29 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
         }
         // ---- re-classification (src/Optimizer.cc:285-386)
         int bad = 0;
-        visit([&](const orb_pose_edge_t& Ed, int& l, double& c) {
+        visit([&](int e, int q, int& l, double& c) {
+            const bool stereo = q >= 0 ? q >= s0 : E[e].stereo != 0;
             double c2 = c;
-            if (l) {
+            if (l) {  // an outlier's error at the round's final pose
+                orb_pose_edge_t Ed;
+                if (q >= 0) {
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) {
+                        Ed.xw[i] = lxw[i][q];
+                        Ed.obs[i] = lob[i][q];
+                    }
+                    Ed.inv_sigma2 = lis[q];
+                    Ed.stereo = stereo;
+                } else {
+                    Ed = E[e];
+                }
                 double Xc[3];
                 EdgeEval ev;
                 pose_edge_error(Ed, T, F.cam, Xc, ev);
                 c2 = ev.chi2;
             }
             const float chi2 = (float)c2;
-            l = chi2 > (Ed.stereo ? 7.815f : 5.991f);
+            l = chi2 > (stereo ? 7.815f : 5.991f);
             bad += l;
         });
         {
@@ -774,12 +899,8 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
         if (round == 2) robust = false;
         if (n < 10) break;  // optimizer.edges().size() < 10
     }
-#pragma unroll
-    for (int s = 0; s < kS; ++s) {
-        const int p = tid + s * kPT;
-        if (p < nr) lev[perm[p]] = (uint8_t)lv[s];
-    }
-    for (int q = tid; q + kS * kPT < nr; q += kPT) lev[perm[q + kS * kPT]] = llv[q];
+    for (int q = tid; q < npos; q += kPT)
+        if (llv[q] != 2) lev[perm[q]] = llv[q];
     if (tid < 7) pose_out[7 * (size_t)f + tid] = T[tid];
     if (tid == 0) inliers[f] = n - nBad;
 }
@@ -812,7 +933,7 @@ int orb_pose_optimization_device(int n_frames, const orb_pose_frame_t* d_frames,
     if (hipMallocAsync(reinterpret_cast<void**>(&chi), std::max<size_t>(1, (size_t)n_edges) * sizeof(double),
                        (hipStream_t)stream) != hipSuccess)
         return orbgpu_fail(ORB_ERR_DEVICE, "hipMallocAsync failed");
-    hipLaunchKernelGGL(k_pose_opt<kEdgeSlots>, dim3(n_frames), dim3(kPT), 0, (hipStream_t)stream, d_frames, d_edges,
+    hipLaunchKernelGGL(k_pose_opt, dim3(n_frames), dim3(kPT), 0, (hipStream_t)stream, d_frames, d_edges,
                        d_pose_out, d_outlier, d_inliers, chi, make_huber());
     const bool launched = hipGetLastError() == hipSuccess;
     if (hipFreeAsync(chi, (hipStream_t)stream) != hipSuccess || !launched)
