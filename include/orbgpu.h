@@ -655,7 +655,13 @@ typedef struct orb_tracking_chain_buffers {
     int32_t* inliers;           /* 2: the two PoseOptimization returns */
     int32_t* n_out;             /* 2: nmatches after the discard, nmatchesMap */
     uint8_t* taken;             /* cap: SearchLocalPoints' skip set */
+    void* scratch;              /* orb_tracking_chain_scratch_bytes(cap, last cap, local points), reused stage
+                                   after stage on the stream; NULL: each stage allocates its own (stream-ordered) */
 } orb_tracking_chain_buffers_t;
+
+/* Scratch bytes of one chain call for frames of `cap` keypoints, a last frame of `last_cap` and `n_local`
+ * local map points (the largest of its stages'). */
+size_t orb_tracking_chain_scratch_bytes(int cap, int last_cap, int n_local);
 
 /* m_motion: ORBmatcher(0.9, true); m_local: ORBmatcher(0.8) (the handles' ratio / orientation).
  * local: the local map's view (track_* arrays written here); pos / normal / min_dist / max_dist:

@@ -923,23 +923,35 @@ extern "C" {
 int orb_pose_optimization_device(int n_frames, const orb_pose_frame_t* d_frames, int n_edges,
                                  const orb_pose_edge_t* d_edges, double* d_pose_out, uint8_t* d_outlier,
                                  int32_t* d_inliers, void* stream) {
+    return orbgpu_pose_optimization_device_scratch(n_frames, d_frames, n_edges, d_edges, d_pose_out, d_outlier, d_inliers,
+                                                   stream, nullptr);
+}
+
+}  // extern "C"
+
+// d_chi: max(n_edges, 1) doubles of the caller's, or NULL: the chi2 of edges beyond the LDS (only frames
+// of more than kCap - 128 edges use it) in stream-ordered scratch (allocated and freed on the call's
+// stream), so calls on different streams may run concurrently
+int orbgpu_pose_optimization_device_scratch(int n_frames, const orb_pose_frame_t* d_frames, int n_edges,
+                                            const orb_pose_edge_t* d_edges, double* d_pose_out, uint8_t* d_outlier,
+                                            int32_t* d_inliers, void* stream, double* d_chi) {
     if (n_frames < 0 || n_edges < 0 || (n_frames && (!d_frames || !d_pose_out || !d_inliers)) ||
         (n_edges && (!d_edges || !d_outlier)))
         return orbgpu_fail(ORB_ERR_ARG, "invalid pose optimisation arguments");
     if (n_frames == 0) return ORB_OK;
-    // the chi2 of edges beyond the register slots: stream-ordered scratch (allocated and freed on the
-    // call's stream), so calls on different streams may run concurrently
-    double* chi = nullptr;
-    if (hipMallocAsync(reinterpret_cast<void**>(&chi), std::max<size_t>(1, (size_t)n_edges) * sizeof(double),
-                       (hipStream_t)stream) != hipSuccess)
+    double* chi = d_chi;
+    if (!chi && hipMallocAsync(reinterpret_cast<void**>(&chi), std::max<size_t>(1, (size_t)n_edges) * sizeof(double),
+                               (hipStream_t)stream) != hipSuccess)
         return orbgpu_fail(ORB_ERR_DEVICE, "hipMallocAsync failed");
     hipLaunchKernelGGL(k_pose_opt, dim3(n_frames), dim3(kPT), 0, (hipStream_t)stream, d_frames, d_edges,
                        d_pose_out, d_outlier, d_inliers, chi, make_huber());
     const bool launched = hipGetLastError() == hipSuccess;
-    if (hipFreeAsync(chi, (hipStream_t)stream) != hipSuccess || !launched)
+    if ((!d_chi && hipFreeAsync(chi, (hipStream_t)stream) != hipSuccess) || !launched)
         return orbgpu_fail(ORB_ERR_DEVICE, "pose kernel launch failed");
     return ORB_OK;
 }
+
+extern "C" {
 
 // Debug hook (not in the public header): stamp frame 0's LM trials into d_buf (16 int64 per trial, up
 // to `cap` trials; NULL turns it off).  Synchronous.

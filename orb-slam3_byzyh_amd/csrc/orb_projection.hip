@@ -1078,9 +1078,24 @@ bool frame_device_ok(const orb_frame_device_t* F) {
 
 }  // namespace
 
+size_t orbgpu_sbp_frame_scratch_bytes(int C, int NL) {
+    DevScratch z;
+    z.take<int32_t>(2); z.take<float4>(C); z.take<int32_t>(kCells + 1); z.take<int32_t>(C);
+    z.take<int32_t>(C); z.take<uint8_t>(NL); z.take<int32_t>(NL); z.take<float>(NL); z.take<int32_t>(2 * (size_t)C);
+    z.take<int32_t>(4); z.take<Cand>((size_t)NL * C); z.take<int32_t>(NL); z.take<int32_t>(NL);
+    z.take<int32_t>(3 * (size_t)C); z.take<int32_t>(NL); z.take<int4>((kTop / 2) * (size_t)NL); z.take<int32_t>(NL);
+    return z.off;
+}
+
 extern "C" int orb_search_by_projection_frame_device(orb_matcher_t m, const orb_frame_device_t* cur,
                                                      const orb_last_points_device_t* last, float th, int mono,
                                                      int32_t* d_match, int32_t* d_n_matches, void* stream) {
+    return orbgpu_sbp_frame_device_scratch(m, cur, last, th, mono, d_match, d_n_matches, stream, nullptr);
+}
+
+int orbgpu_sbp_frame_device_scratch(orb_matcher_t m, const orb_frame_device_t* cur, const orb_last_points_device_t* last,
+                                    float th, int mono, int32_t* d_match, int32_t* d_n_matches, void* stream,
+                                    void* scratch) {
     if (!m || !frame_device_ok(cur) || !last || !d_match || !d_n_matches || !last->n || last->cap < 0 ||
         (last->cap > 0 && (!last->valid || !last->observed || !last->xyz || !last->desc || !last->kps_un)) ||
         (reinterpret_cast<uintptr_t>(last->desc) & 15) != 0)
@@ -1108,17 +1123,9 @@ extern "C" int orb_search_by_projection_frame_device(orb_matcher_t m, const orb_
     P.check_ori = orbgpu_matcher_check_ori(m);
     // scratch: params | dims | kp4 | cells | cell_of | last prep | lister + fixed | overflow block |
     // candidates | ncand | st | claimMin, last, removed | work list | top
-    size_t bytes = 0;
-    {
-        DevScratch z;
-        z.take<int32_t>(2); z.take<float4>(C); z.take<int32_t>(kCells + 1); z.take<int32_t>(C);
-        z.take<int32_t>(C); z.take<uint8_t>(NL); z.take<int32_t>(NL); z.take<float>(NL); z.take<int32_t>(2 * (size_t)C);
-        z.take<int32_t>(4); z.take<Cand>((size_t)NL * C); z.take<int32_t>(NL); z.take<int32_t>(NL);
-        z.take<int32_t>(3 * (size_t)C); z.take<int32_t>(NL); z.take<int4>((kTop / 2) * (size_t)NL); z.take<int32_t>(NL);
-        bytes = z.off;
-    }
     DevScratch z;
-    if (hipMallocAsync(reinterpret_cast<void**>(&z.base), bytes, s) != hipSuccess)
+    z.base = static_cast<char*>(scratch);  // the caller's (orbgpu_sbp_frame_scratch_bytes), else stream-ordered
+    if (!z.base && hipMallocAsync(reinterpret_cast<void**>(&z.base), orbgpu_sbp_frame_scratch_bytes(C, NL), s) != hipSuccess)
         return orbgpu_fail(ORB_ERR_DEVICE, "hipMallocAsync failed");
     int32_t* dims = z.take<int32_t>(2);
     float4* kp4 = z.take<float4>(C);
@@ -1163,14 +1170,30 @@ extern "C" int orb_search_by_projection_frame_device(orb_matcher_t m, const orb_
         hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 8 * (size_t)C : 0, s, ra);
         ok = hipGetLastError() == hipSuccess;
     }
-    if (hipFreeAsync(z.base, s) != hipSuccess) ok = false;
+    if (!scratch && hipFreeAsync(z.base, s) != hipSuccess) ok = false;
     return ok ? ORB_OK : orbgpu_fail(ORB_ERR_DEVICE, "SearchByProjection device failed");
+}
+
+size_t orbgpu_sbp_local_scratch_bytes(int C, int np) {
+    DevScratch z;
+    z.take<int32_t>(2); z.take<float4>(C); z.take<int32_t>(kCells + 1); z.take<int32_t>(C);
+    z.take<int32_t>(C); z.take<uint8_t>(np); z.take<int32_t>(2 * (size_t)C); z.take<int32_t>(4);
+    z.take<Cand>((size_t)np * C); z.take<int32_t>(np); z.take<int32_t>(np); z.take<int32_t>(3 * (size_t)C);
+    z.take<int32_t>(np); z.take<int4>((kTop / 2) * (size_t)np); z.take<int32_t>(np);
+    return z.off;
 }
 
 extern "C" int orb_search_by_projection_local_device(orb_matcher_t m, const orb_frame_device_t* F,
                                                      const uint8_t* d_frame_taken, const orb_local_points_device_t* pts,
                                                      float th, int far_points, float th_far_points, int32_t* d_match,
                                                      int32_t* d_n_matches, void* stream) {
+    return orbgpu_sbp_local_device_scratch(m, F, d_frame_taken, pts, th, far_points, th_far_points, d_match, d_n_matches,
+                                           stream, nullptr);
+}
+
+int orbgpu_sbp_local_device_scratch(orb_matcher_t m, const orb_frame_device_t* F, const uint8_t* d_frame_taken,
+                                    const orb_local_points_device_t* pts, float th, int far_points, float th_far_points,
+                                    int32_t* d_match, int32_t* d_n_matches, void* stream, void* scratch) {
     if (!m || !frame_device_ok(F) || !pts || pts->n < 0 || !d_match || !d_n_matches ||
         (pts->n && (!pts->track_in_view || !pts->is_bad || !pts->observed || !pts->track_proj || !pts->track_view_cos ||
                     !pts->track_depth || !pts->track_level || !pts->desc)) ||
@@ -1185,17 +1208,9 @@ extern "C" int orb_search_by_projection_local_device(orb_matcher_t m, const orb_
     P.n_cur = 0; P.n_pts = np; P.has_ur = F->u_right != nullptr; P.far = far_points ? 1 : 0; P.nlevels = F->nlevels;
     P.cap = C;
     P.nnratio = orbgpu_matcher_nnratio(m);
-    size_t bytes = 0;
-    {
-        DevScratch z;
-        z.take<int32_t>(2); z.take<float4>(C); z.take<int32_t>(kCells + 1); z.take<int32_t>(C);
-        z.take<int32_t>(C); z.take<uint8_t>(np); z.take<int32_t>(2 * (size_t)C); z.take<int32_t>(4);
-        z.take<Cand>((size_t)np * C); z.take<int32_t>(np); z.take<int32_t>(np); z.take<int32_t>(3 * (size_t)C);
-        z.take<int32_t>(np); z.take<int4>((kTop / 2) * (size_t)np); z.take<int32_t>(np);
-        bytes = z.off;
-    }
     DevScratch z;
-    if (hipMallocAsync(reinterpret_cast<void**>(&z.base), bytes, s) != hipSuccess)
+    z.base = static_cast<char*>(scratch);  // the caller's (orbgpu_sbp_local_scratch_bytes), else stream-ordered
+    if (!z.base && hipMallocAsync(reinterpret_cast<void**>(&z.base), orbgpu_sbp_local_scratch_bytes(C, np), s) != hipSuccess)
         return orbgpu_fail(ORB_ERR_DEVICE, "hipMallocAsync failed");
     int32_t* dims = z.take<int32_t>(2);
     float4* kp4 = z.take<float4>(C);
@@ -1239,6 +1254,6 @@ extern "C" int orb_search_by_projection_local_device(orb_matcher_t m, const orb_
         hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 8 * (size_t)C : 0, s, ra);
         ok = hipGetLastError() == hipSuccess;
     }
-    if (hipFreeAsync(z.base, s) != hipSuccess) ok = false;
+    if (!scratch && hipFreeAsync(z.base, s) != hipSuccess) ok = false;
     return ok ? ORB_OK : orbgpu_fail(ORB_ERR_DEVICE, "SearchByProjection(local) device failed");
 }

@@ -15,6 +15,8 @@
 // has one there (SearchByProjection(F, local points) overwrites, src/ORBmatcher.cc:156), else the first.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <cstdint>
 #include <cstring>
 
@@ -228,6 +230,12 @@ int orb_tracking_discard_outliers_device(const orb_pose_frame_t* d_frame, const 
     return ORB_OK;
 }
 
+size_t orb_tracking_chain_scratch_bytes(int cap, int last_cap, int n_local) {
+    if (cap <= 0 || last_cap < 0 || n_local < 0) return 0;
+    return std::max({orbgpu_sbp_frame_scratch_bytes(cap, last_cap), orbgpu_sbp_local_scratch_bytes(cap, n_local),
+                     (size_t)cap * sizeof(double)});
+}
+
 int orb_tracking_chain_device(orb_matcher_t m_motion, orb_matcher_t m_local, const orb_frame_device_t* F,
                               const orb_last_points_device_t* last, const orb_local_points_device_t* local,
                               const float* d_pos, const float* d_normal, const float* d_min_dist,
@@ -241,12 +249,14 @@ int orb_tracking_chain_device(orb_matcher_t m_motion, orb_matcher_t m_local, con
         (local->n > 0 && (!d_pos || !d_normal || !d_min_dist || !d_max_dist)))
         return orbgpu_fail(ORB_ERR_ARG, "bad tracking chain arguments");
     int rc;
-    if ((rc = orb_search_by_projection_frame_device(m_motion, F, last, P->th_motion, P->mono, B->m1, B->n_match, stream)))
+    void* const z = B->scratch;  // stream order: each stage's scratch is free again when the next one runs
+    if ((rc = orbgpu_sbp_frame_device_scratch(m_motion, F, last, P->th_motion, P->mono, B->m1, B->n_match, stream, z)))
         return rc;
     if ((rc = orb_tracking_pose_edges_device(F, B->m1, last->xyz, nullptr, nullptr, inv_level_sigma2, nullptr, pose7,
                                              B->frames, B->edges1, B->edge_kp1, stream)))
         return rc;
-    if ((rc = orb_pose_optimization_device(1, B->frames, F->cap, B->edges1, B->poses, B->outlier1, B->inliers, stream)))
+    if ((rc = orbgpu_pose_optimization_device_scratch(1, B->frames, F->cap, B->edges1, B->poses, B->outlier1, B->inliers,
+                                                      stream, static_cast<double*>(z))))
         return rc;
     // isInFrustum at the first pose and the seen skip read the first search's assignments, which the
     // discard does not change (the reference marks its discarded outliers seen too, Tracking.cc:4195)
@@ -265,16 +275,16 @@ int orb_tracking_chain_device(orb_matcher_t m_motion, orb_matcher_t m_local, con
     if ((rc = orb_tracking_discard_outliers_device(B->frames, B->edge_kp1, B->outlier1, B->m1, last->observed, nullptr,
                                                    nullptr, B->n_out, F->cap, B->taken, stream)))
         return rc;
-    if ((rc = orb_search_by_projection_local_device(m_local, F, B->taken, local, P->th_local, P->far_points,
-                                                    P->th_far_points, B->m2, B->n_match + 1, stream)))
+    if ((rc = orbgpu_sbp_local_device_scratch(m_local, F, B->taken, local, P->th_local, P->far_points, P->th_far_points,
+                                              B->m2, B->n_match + 1, stream, z)))
         return rc;
     const bool has_local = local->n > 0;  // an empty local map: the second search assigned nothing
     if ((rc = orb_tracking_pose_edges_device(F, B->m1, last->xyz, has_local ? B->m2 : nullptr, has_local ? d_pos : nullptr,
                                              inv_level_sigma2, B->poses, nullptr, B->frames + 1, B->edges2, B->edge_kp2,
                                              stream)))
         return rc;
-    return orb_pose_optimization_device(1, B->frames + 1, F->cap, B->edges2, B->poses + 7, B->outlier2, B->inliers + 1,
-                                        stream);
+    return orbgpu_pose_optimization_device_scratch(1, B->frames + 1, F->cap, B->edges2, B->poses + 7, B->outlier2,
+                                                   B->inliers + 1, stream, static_cast<double*>(z));
 }
 
 }  // extern "C"

@@ -22,6 +22,21 @@ struct OrbPyramidView {
 };
 extern "C" int orbgpu_extractor_pyramid(orb_extractor_t h, OrbPyramidView* out);
 
+// The device SearchByProjection forms and PoseOptimization with the caller's scratch (the tracking
+// chain's, reused stage after stage on its stream): `scratch` of at least the _bytes size, or NULL
+// for the public functions' stream-ordered allocation.
+size_t orbgpu_sbp_frame_scratch_bytes(int cap, int last_cap);
+size_t orbgpu_sbp_local_scratch_bytes(int cap, int n_points);
+int orbgpu_sbp_frame_device_scratch(orb_matcher_t m, const orb_frame_device_t* cur, const orb_last_points_device_t* last,
+                                    float th, int mono, int32_t* d_match, int32_t* d_n_matches, void* stream,
+                                    void* scratch);
+int orbgpu_sbp_local_device_scratch(orb_matcher_t m, const orb_frame_device_t* F, const uint8_t* d_frame_taken,
+                                    const orb_local_points_device_t* pts, float th, int far_points, float th_far_points,
+                                    int32_t* d_match, int32_t* d_n_matches, void* stream, void* scratch);
+int orbgpu_pose_optimization_device_scratch(int n_frames, const orb_pose_frame_t* d_frames, int n_edges,
+                                            const orb_pose_edge_t* d_edges, double* d_pose_out, uint8_t* d_outlier,
+                                            int32_t* d_inliers, void* stream, double* d_chi);
+
 // REGISTER_TIMES brackets (csrc/orb_timers.hip): StageTimer t("LBA") records the scope's wall time
 // under that name when the timers are on.
 namespace orbgpu {

@@ -67,7 +67,7 @@ class TrackingChainParams(ctypes.Structure):  # orb_tracking_chain_params_t
 class TrackingChainBuffers(ctypes.Structure):  # orb_tracking_chain_buffers_t
     _fields_ = [(k, ctypes.c_void_p) for k in ("m1", "m2", "n_match", "frames", "edges1", "edges2", "edge_kp1",
                                                "edge_kp2", "outlier1", "outlier2", "poses", "inliers", "n_out",
-                                               "taken")]
+                                               "taken", "scratch")]
 
 
 def _stream_handle(stream, device):
@@ -251,6 +251,9 @@ class TrackingChain:
             self.edge_kp[1].data_ptr(), self.outlier[0].data_ptr(), self.outlier[1].data_ptr(),
             self.poses.data_ptr(), self.inliers.data_ptr(), self.n_out.data_ptr(), self.taken.data_ptr())
         assert self.frames.numel() == 2 * fsz
+        self._scratch = torch.empty(0, dtype=torch.uint8, device=d)
+        self._scratch_key = None
+        self._retired = []
 
     def track(self, cur: DeviceFrame, last: DeviceLastPoints, local: DeviceLocalMap, pose7, stream=None,
               wide: bool = False) -> TrackResult:
@@ -266,6 +269,14 @@ class TrackingChain:
         p0 = np.ascontiguousarray(pose7, np.float64).reshape(7)
         self._params.th_motion = self.th_motion * (2 if wide else 1)
         lr = local.last_row
+        key = (cur.cap, last.cap, local.n)
+        if key != self._scratch_key:  # one scratch for every stage of the call, grown as the sizes need
+            need = int(lib.orb_tracking_chain_scratch_bytes(*key))
+            if need > self._scratch.numel():
+                self._retired.append(self._scratch)  # earlier calls' stages may still be reading it
+                self._scratch = torch.empty(need, dtype=torch.uint8, device=self.device)
+                self._bufs.scratch = self._scratch.data_ptr()
+            self._scratch_key = key
         check(lib.orb_tracking_chain_device(self._h_motion, self._h_local, ctypes.byref(cur.view()),
                                             ctypes.byref(last.view()), ctypes.byref(local.view()),
                                             local.pos.data_ptr(), local.normal.data_ptr(), local.min_dist.data_ptr(),
