@@ -555,7 +555,7 @@ __device__ int g_pose_trace_cap = 0;
 
 // LM state of a frame's optimize(10), kept in registers of the workgroup's thread 0
 struct LmState {
-    double x[6];
+    double iscale;  // 1 / computeScale of the trial's step (x . (lambda x + b) + 1e-3), known at its solve
     double lambda, ni, current, ini;
     int nbad, qmax, it, ok, cur;  // cur: the buffer of sys holding the system
 };
@@ -748,12 +748,20 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
         for (int i = 0; i < 7; ++i) Tn[i] = T[i];
 #pragma unroll
         for (int i = 0; i < 7; ++i) Tb[i] = Tn[i];
-        S.ok = solve6(U, S.lambda, b, S.x);
+        double x[6];
+        S.ok = solve6(U, S.lambda, b, x);
         if (!S.ok)
 #pragma unroll
-            for (int i = 0; i < 6; ++i) S.x[i] = 0;
+            for (int i = 0; i < 6; ++i) x[i] = 0;
+        // the decision's computeScale needs only this step: computed here (beside the exponential's
+        // chain) instead of on the path from the pass to the decision
+        double scale = 0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) scale += x[i] * (S.lambda * x[i] + b[i]);
+        scale += 1e-3;
+        S.iscale = rcp_nr(scale);
         stamp(6);
-        se3_oplus_r(Tn, S.x);
+        se3_oplus_r(Tn, x);
         stamp(7);
 #pragma unroll
         for (int i = 0; i < 7; ++i) T[i] = Tn[i];
@@ -808,11 +816,7 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
                     double tempChi = sys[wb][27];
                     if (!S.ok) tempChi = DBL_MAX;
                     double r = S.current - tempChi;
-                    double scale = 0;
-#pragma unroll
-                    for (int i = 0; i < 6; ++i) scale += S.x[i] * (S.lambda * S.x[i] + sys[cur][21 + i]);
-                    scale += 1e-3;
-                    r *= rcp_nr(scale);
+                    r *= S.iscale;
                     const bool accept = r > 0 && isfinite(tempChi);
                     if (accept) {
                         const double c = 2 * r - 1;
