@@ -768,9 +768,8 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
     };
     bool robust = true;
     int nBad = 0;
-    // thread 0's LM state lives in LDS between trials (loaded into registers for the decision and the
-    // solve only), so that it holds no registers during the pass
-    __shared__ LmState sS;
+    // thread 0's LM state, in its registers for the whole optimisation
+    LmState S;
     for (int round = 0; round < 4; ++round) {
         // vSE3->setEstimate(pFrame->GetPose()); read from global: a lane-indexed read of the copy F
         // would put F in scratch
@@ -786,7 +785,6 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
             pass(robust, false, acc);  // computeActiveErrors + buildSystem at the round's start pose
             totals(acc, cur);
             if (tid == 0) {
-                LmState S;
                 S.cur = cur;
                 S.current = S.ini = sys[cur][27];
                 double m = 0;  // computeLambdaInit: tau * max |diag H|
@@ -799,7 +797,6 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
                 S.qmax = 0;
                 S.it = 0;
                 solve(S);
-                sS = S;
             }
             __syncthreads();
             for (;;) {
@@ -812,7 +809,6 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
                 totals(acc, wb);
                 stamp(2);
                 if (tid == 0) {
-                    LmState S = sS;
                     double tempChi = sys[wb][27];
                     if (!S.ok) tempChi = DBL_MAX;
                     double r = S.current - tempChi;
@@ -851,7 +847,6 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
                         }
                     }
                     if (st == 1) solve(S);
-                    sS = S;
                     s_state = st | (swap << 2);
                 }
                 stamp(3);
