@@ -147,6 +147,7 @@ DEBUG_PROTOTYPES = {
     "orb_extractor_launch_durations": (_i, [_vp, _i, _fp, _i, _ip]),
     "orb_debug_ba_chol_timeout": (_i, [_i, _i]),
     "orb_debug_pose_trace": (_i, [_vp, _i]),
+    "orb_debug_pose_extra": (_i, [_i]),
     "orb_debug_ba_chol_timeout_status": (_i, [_ip]),
 }
 

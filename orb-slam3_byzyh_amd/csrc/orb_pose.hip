@@ -552,6 +552,12 @@ __device__ __forceinline__ void lin_pair(const double2 (&xw)[3], const double2 (
 // after the exponential.
 __device__ long long* g_pose_trace = nullptr;
 __device__ int g_pose_trace_cap = 0;
+// Cost probe (built with -DORB_POSE_PROBE; orb_debug_pose_extra, tools/pose_trace.py): bit 0 runs the
+// block solve once more and bit 1 the exponential once more, each on the dependent path of the real
+// one, so the kernel-time difference is that step's latency.  Off by default: its branches cost ~3 %.
+#ifdef ORB_POSE_PROBE
+__device__ int g_pose_extra = 0;
+#endif
 
 // LM state of a frame's optimize(10), kept in registers of the workgroup's thread 0
 struct LmState {
@@ -749,7 +755,20 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
 #pragma unroll
         for (int i = 0; i < 7; ++i) Tb[i] = Tn[i];
         double x[6];
-        S.ok = solve6(U, S.lambda, b, x);
+#ifdef ORB_POSE_PROBE
+        const int extra = g_pose_extra;
+#else
+        constexpr int extra = 0;
+#endif
+        double lam = S.lambda;
+        if (extra & 1) {
+            double xd[6];
+            (void)solve6(U, lam, b, xd);
+            double z = xd[5];
+            asm volatile("" : "+v"(z));
+            lam += z * 0.0;
+        }
+        S.ok = solve6(U, lam, b, x);
         if (!S.ok)
 #pragma unroll
             for (int i = 0; i < 6; ++i) x[i] = 0;
@@ -761,6 +780,15 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
         scale += 1e-3;
         S.iscale = rcp_nr(scale);
         stamp(6);
+        if (extra & 2) {
+            double Td[7];
+#pragma unroll
+            for (int i = 0; i < 7; ++i) Td[i] = Tn[i];
+            se3_oplus_r(Td, x);
+            double z = Td[6];
+            asm volatile("" : "+v"(z));
+            x[0] += z * 0.0;
+        }
         se3_oplus_r(Tn, x);
         stamp(7);
 #pragma unroll
@@ -959,6 +987,18 @@ int orb_debug_pose_trace(long long* d_buf, int cap) {
         hipMemcpyToSymbol(HIP_SYMBOL(g_pose_trace_cap), &cap, sizeof(cap)) != hipSuccess)
         return orbgpu_fail(ORB_ERR_DEVICE, "debug symbol copy");
     return ORB_OK;
+}
+
+// Debug hook (not in the public header): the cost probe's mode (g_pose_extra).  Synchronous.
+int orb_debug_pose_extra(int mode) {
+#ifdef ORB_POSE_PROBE
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_pose_extra), &mode, sizeof(mode)) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "debug symbol copy");
+    return ORB_OK;
+#else
+    (void)mode;
+    return orbgpu_fail(ORB_ERR_ARG, "built without ORB_POSE_PROBE");
+#endif
 }
 
 int orb_pose_optimization(int n_frames, const orb_pose_frame_t* frames, int n_edges, const orb_pose_edge_t* edges,

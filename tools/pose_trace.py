@@ -66,3 +66,26 @@ print(f"pass detail (wave 0): T+rt {np.median(pz[:, 8] - pz[:, 0]):.0f}, slot0 {
       f"slot1 {np.median(pz[:, 10] - pz[:, 9]):.0f}, lds/mem slots {np.median(pz[:, 11] - pz[:, 10]):.0f}, "
       f"butterfly {np.median(pz[:, 12] - pz[:, 11]):.0f}, barrier {np.median(pz[:, 13] - pz[:, 12]):.0f}, "
       f"wave sums {np.median(pz[:, 1] - pz[:, 13]):.0f}")
+
+# cost probe (a library built with -DORB_POSE_PROBE): the kernel time with the block solve / the
+# exponential run twice on the dependent path
+if lib.orb_debug_pose_extra(0) == 0:
+    ntr = len(t)
+
+    def timed():
+        for _ in range(5):
+            call()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            call()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps * 1e3
+
+    base = timed()
+    for mode, name in ((1, "block solve"), (2, "exponential"), (3, "solve + exponential")):
+        lib.orb_debug_pose_extra(mode)
+        ms = timed()
+        lib.orb_debug_pose_extra(0)
+        print(f"probe: {name} once more per trial adds {(ms - base) * 1e3:.1f} us = "
+              f"{(ms - base) * 1e-3 * 2.4e9 / max(ntr, 1):.0f} cycles per trial (at 2.4 GHz, {ntr} trials)")
