@@ -677,6 +677,48 @@ int orb_tracking_chain_device(orb_matcher_t m_motion, orb_matcher_t m_local, con
                               const orb_tracking_chain_params_t* params, const orb_tracking_chain_buffers_t* bufs,
                               void* stream);
 
+/* The chain over a batch of frames in one call: every stage is one launch for the whole batch (one
+ * grid row per frame), so B frames cost one host crossing and ~20 launches instead of B of each, and
+ * the frames' single-workgroup stages (the resolve, PoseOptimization) run side by side over the CUs.
+ * Frame b's results are the single call's on the same inputs, bit for bit.  All frames share `cap`
+ * (their frame views' cap); a last frame and a local map per frame. */
+typedef struct orb_tracking_chain_frame {
+    const orb_frame_device_t* frame;
+    const orb_last_points_device_t* last;
+    const orb_local_points_device_t* local;   /* its track_* arrays are written */
+    const float* pos;                         /* the local map's fields, as orb_tracking_chain_device */
+    const float* normal;
+    const float* min_dist;
+    const float* max_dist;
+    const int32_t* last_row;                  /* NULL: no local point is held by the last frame */
+    const orb_frustum_frame_t* frustum;
+    const float* inv_level_sigma2;            /* host, nlevels floats */
+    double pose7[7];                          /* the motion model's pose (tx ty tz qx qy qz qw) */
+} orb_tracking_chain_frame_t;
+
+typedef struct orb_tracking_chain_batch_buffers {
+    int32_t* m1;                /* B x cap */
+    int32_t* m2;                /* B x cap */
+    int32_t* n_match;           /* B x 2 */
+    orb_pose_frame_t* frames;   /* 2 x B (B = the call's n_frames): the first graphs, then the second ones */
+    orb_pose_edge_t* edges1;    /* B x cap (frame b's edges from b cap on) */
+    orb_pose_edge_t* edges2;    /* B x cap */
+    int32_t* edge_kp1;          /* B x cap */
+    int32_t* edge_kp2;          /* B x cap */
+    uint8_t* outlier1;          /* B x cap */
+    uint8_t* outlier2;          /* B x cap */
+    double* poses;              /* 2 x B x 7 (B = the call's n_frames) */
+    int32_t* inliers;           /* 2 x B */
+    int32_t* n_out;             /* B x 2 */
+    uint8_t* taken;             /* B x cap */
+    void* scratch;              /* orb_tracking_chain_batch_scratch_bytes(B, cap, max last cap, max local points) */
+} orb_tracking_chain_batch_buffers_t;
+
+size_t orb_tracking_chain_batch_scratch_bytes(int n_frames, int cap, int last_cap, int n_local);
+int orb_tracking_chain_batch_device(orb_matcher_t m_motion, orb_matcher_t m_local, int n_frames,
+                                    const orb_tracking_chain_frame_t* frames, const orb_tracking_chain_params_t* params,
+                                    const orb_tracking_chain_batch_buffers_t* bufs, void* stream);
+
 /* ---- multi-GPU local BA: one process per GPU, every rank passes the same
  * problem; rank r owns a contiguous, edge-balanced range of the landmarks and their edges, and
  * the ranks all-reduce the partial Hpp/b_p, the partial reduced camera system (S, b_S) of each LM

@@ -12,7 +12,7 @@ from .matcher import ORBmatcher
 from .optimizer import LocalBA, local_bundle_adjustment, pose_optimization
 from . import distributed, timers
 from .stereo import compute_stereo_matches, compute_stereo_matches_batch_device
-from .tracking import DeviceFrame, DeviceLastPoints, DeviceLocalMap, TrackingChain
+from .tracking import DeviceFrame, DeviceLastPoints, DeviceLocalMap, TrackingChain, TrackingChainBatch
 from .vocabulary import ORBVocabulary
 
-__all__ = ["ORBextractor", "ORBmatcher", "KeyFrame", "Frame", "LocalMapPoints", "LocalBA", "local_bundle_adjustment", "pose_optimization", "compute_stereo_matches", "compute_stereo_matches_batch_device", "ORBVocabulary", "frustum_frame", "is_in_frustum", "KEYPOINT_DTYPE", "OrbGpuError", "keypoints_to_structured", "undistort_keypoints_device", "DeviceFrame", "DeviceLastPoints", "DeviceLocalMap", "TrackingChain", "_lib"]
+__all__ = ["ORBextractor", "ORBmatcher", "KeyFrame", "Frame", "LocalMapPoints", "LocalBA", "local_bundle_adjustment", "pose_optimization", "compute_stereo_matches", "compute_stereo_matches_batch_device", "ORBVocabulary", "frustum_frame", "is_in_frustum", "KEYPOINT_DTYPE", "OrbGpuError", "keypoints_to_structured", "undistort_keypoints_device", "DeviceFrame", "DeviceLastPoints", "DeviceLocalMap", "TrackingChain", "TrackingChainBatch", "_lib"]

@@ -123,6 +123,8 @@ PROTOTYPES = {
     "orb_tracking_discard_outliers_device": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp]),
     "orb_tracking_local_seen_device": (_i, [_vp, _i, _i, _vp, _i, _vp, _vp]),
     "orb_tracking_chain_scratch_bytes": (_sz, [_i, _i, _i]),
+    "orb_tracking_chain_batch_scratch_bytes": (_sz, [_i, _i, _i, _i]),
+    "orb_tracking_chain_batch_device": (_i, [_vp, _vp, _i, _vp, _vp, _vp, _vp]),
     "orb_tracking_chain_device": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                         _vp]),
     "orb_ba_create": (_i, [ctypes.POINTER(_vp)]),

@@ -6,8 +6,12 @@
 // library is built with -ffp-contract=off, so nothing else is fused.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <vector>
+
 #include <cmath>
 #include <cstdint>
+#include <cstring>
 
 #include "orb_pose_frame.h"
 #include "orb_predict_scale.h"
@@ -24,7 +28,7 @@ __device__ __forceinline__ float dot3(const float a[3], const float b[3]) {
     return fmaf(a[2], b[2], fmaf(a[0], b[0], a[1] * b[1]));
 }
 
-__global__ __launch_bounds__(256) void k_is_in_frustum(orb_frustum_frame_t F, const double* __restrict__ pose7, int n,
+__device__ __forceinline__ void k_is_in_frustum_body(orb_frustum_frame_t F, const double* __restrict__ pose7, int n,
                                                        const float* __restrict__ pos,
                                                        const float* __restrict__ normal,
                                                        const float* __restrict__ min_dist,
@@ -82,6 +86,37 @@ __global__ __launch_bounds__(256) void k_is_in_frustum(orb_frustum_frame_t F, co
     level[i] = lev;
     view_cos[i] = vc;
 }
+__global__ __launch_bounds__(256) void k_is_in_frustum(orb_frustum_frame_t F, const double* __restrict__ pose7, int n,
+                                                       const float* __restrict__ pos,
+                                                       const float* __restrict__ normal,
+                                                       const float* __restrict__ min_dist,
+                                                       const float* __restrict__ max_dist, float viewingCosLimit,
+                                                       ScaleSteps steps, uint8_t* __restrict__ in_view, float* __restrict__ proj,
+                                                       float* __restrict__ depth, int32_t* __restrict__ level,
+                                                       float* __restrict__ view_cos) {
+    k_is_in_frustum_body(F, pose7, n, pos, normal, min_dist, max_dist, viewingCosLimit, steps, in_view, proj, depth, level, view_cos);
+}
+struct k_is_in_frustum_args {
+    orb_frustum_frame_t F;
+    const double* pose7;
+    int n;
+    const float* pos;
+    const float* normal;
+    const float* min_dist;
+    const float* max_dist;
+    float viewingCosLimit;
+    ScaleSteps steps;
+    uint8_t* in_view;
+    float* proj;
+    float* depth;
+    int32_t* level;
+    float* view_cos;
+};
+// the same on frame blockIdx.y of a batch (one argument block per frame)
+__global__ __launch_bounds__(256) void k_is_in_frustum_b(const k_is_in_frustum_args* __restrict__ a) {
+    const k_is_in_frustum_args& A = a[blockIdx.y];
+    k_is_in_frustum_body(A.F, A.pose7, A.n, A.pos, A.normal, A.min_dist, A.max_dist, A.viewingCosLimit, A.steps, A.in_view, A.proj, A.depth, A.level, A.view_cos);
+}
 
 }  // namespace
 
@@ -104,6 +139,44 @@ int orb_is_in_frustum_pose_device(const orb_frustum_frame_t* frame, const double
     if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "frustum kernel launch failed");
     return ORB_OK;
 }
+
+}  // extern "C"
+
+// The tracking chain's batch: frame b's local map tested at its optimised pose d_poses[7 b], one grid row
+// per frame (argument blocks copied into d_args).
+int orbgpu_frustum_chain_batch(int B, const orb_tracking_chain_frame_t* fr, const double* d_poses, float viewing_cos_limit,
+                               void* d_args, void* h_args, size_t args_cap, void* stream) {
+    if (B <= 0 || !fr || !d_poses || !d_args || !h_args) return orbgpu_fail(ORB_ERR_ARG, "invalid frustum batch arguments");
+    std::vector<k_is_in_frustum_args> a(B);
+    int maxn = 0;
+    for (int b = 0; b < B; ++b) {
+        const orb_frustum_frame_t* F = fr[b].frustum;
+        const orb_local_points_device_t* L = fr[b].local;
+        if (!F || !L || L->n < 0 || F->n_levels <= 0 ||
+            (L->n && (!fr[b].pos || !fr[b].normal || !fr[b].min_dist || !fr[b].max_dist || !L->track_in_view ||
+                      !L->track_proj || !L->track_depth || !L->track_level || !L->track_view_cos)))
+            return orbgpu_fail(ORB_ERR_ARG, "invalid frustum batch frame");
+        ScaleSteps steps{};
+        if (!orbgpu::predict_scale_thresholds(F->log_scale_factor, F->n_levels, steps.t))
+            return orbgpu_fail(ORB_ERR_ARG, "log_scale_factor must be > 0 and n_levels <= 32");
+        a[b] = k_is_in_frustum_args{*F, d_poses + 7 * (size_t)b, L->n, fr[b].pos, fr[b].normal, fr[b].min_dist,
+                                    fr[b].max_dist, viewing_cos_limit, steps, const_cast<uint8_t*>(L->track_in_view),
+                                    const_cast<float*>(L->track_proj), const_cast<float*>(L->track_depth),
+                                    const_cast<int32_t*>(L->track_level), const_cast<float*>(L->track_view_cos)};
+        maxn = std::max(maxn, L->n);
+    }
+    if (maxn == 0) return ORB_OK;
+    if (a.size() * sizeof(k_is_in_frustum_args) > args_cap) return orbgpu_fail(ORB_ERR_ARG, "frustum batch: argument area too small");
+    hipStream_t s = (hipStream_t)stream;
+    memcpy(h_args, a.data(), a.size() * sizeof(k_is_in_frustum_args));  // pinned staging
+    if (hipMemcpyAsync(d_args, h_args, a.size() * sizeof(k_is_in_frustum_args), hipMemcpyHostToDevice, s) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "batch argument upload failed");
+    hipLaunchKernelGGL(k_is_in_frustum_b, dim3((maxn + 255) / 256, B), dim3(256), 0, s,
+                       (const k_is_in_frustum_args*)d_args);
+    return hipGetLastError() == hipSuccess ? ORB_OK : orbgpu_fail(ORB_ERR_DEVICE, "frustum batch launch failed");
+}
+
+extern "C" {
 
 int orb_is_in_frustum_device(const orb_frustum_frame_t* frame, int n, const float* d_pos, const float* d_normal,
                              const float* d_min_dist, const float* d_max_dist, float viewing_cos_limit,

@@ -121,7 +121,7 @@ constexpr int kCandWaves = 4;
 
 // one wave per last-frame point (src:1978-2062 up to the minimum): project with the current pose,
 // the window by forward / backward motion (src:2019-2024), the stereo u_R test, distances
-__global__ __launch_bounds__(64 * kCandWaves) void k_proj_candidates(const ProjParams P, const int32_t* __restrict__ n_dev,
+__device__ __forceinline__ void k_proj_candidates_body(const ProjParams P, const int32_t* __restrict__ n_dev,
                                                          const uint8_t* __restrict__ valid,
                                                          const float* __restrict__ xyz, const uint4* __restrict__ mp_desc,
                                                          const int32_t* __restrict__ last_octave,
@@ -186,6 +186,41 @@ __global__ __launch_bounds__(64 * kCandWaves) void k_proj_candidates(const ProjP
     __threadfence_block();  // the wave's own candidate stores, read back across lanes
     if (observed[i]) record_listers(lane, i, n, P.cap, cands + (size_t)i * P.cap, nullptr, lister);
 }
+__global__ __launch_bounds__(64 * kCandWaves) void k_proj_candidates(const ProjParams P, const int32_t* __restrict__ n_dev,
+                                                         const uint8_t* __restrict__ valid,
+                                                         const float* __restrict__ xyz, const uint4* __restrict__ mp_desc,
+                                                         const int32_t* __restrict__ last_octave,
+                                                         const float4* __restrict__ cur_kp,  // x, y, angle, octave bits
+                                                         const float* __restrict__ cur_ur, const uint4* __restrict__ cur_desc,
+                                                         const int32_t* __restrict__ cell_off, const int32_t* __restrict__ cell_idx,
+                                                         Cand* __restrict__ cands, int32_t* __restrict__ ncand,
+                                                         int32_t* __restrict__ overflow, const uint8_t* __restrict__ observed,
+                                                         int32_t* __restrict__ lister) {
+    k_proj_candidates_body(P, n_dev, valid, xyz, mp_desc, last_octave, cur_kp, cur_ur, cur_desc, cell_off, cell_idx, cands, ncand, overflow, observed, lister);
+}
+struct k_proj_candidates_args {
+    ProjParams P;
+    const int32_t* n_dev;
+    const uint8_t* valid;
+    const float* xyz;
+    const uint4* mp_desc;
+    const int32_t* last_octave;
+    const float4* cur_kp;
+    const float* cur_ur;
+    const uint4* cur_desc;
+    const int32_t* cell_off;
+    const int32_t* cell_idx;
+    Cand* cands;
+    int32_t* ncand;
+    int32_t* overflow;
+    const uint8_t* observed;
+    int32_t* lister;
+};
+// the same on frame blockIdx.y of a batch (one argument block per frame)
+__global__ __launch_bounds__(64 * kCandWaves) void k_proj_candidates_b(const k_proj_candidates_args* __restrict__ a) {
+    const k_proj_candidates_args& A = a[blockIdx.y];
+    k_proj_candidates_body(A.P, A.n_dev, A.valid, A.xyz, A.mp_desc, A.last_octave, A.cur_kp, A.cur_ur, A.cur_desc, A.cell_off, A.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.lister);
+}
 
 __device__ __forceinline__ int rot_bin(float a1, float a2) {
     float rot = a1 - a2;
@@ -205,7 +240,7 @@ struct LocalParams {
 
 // one wave per local map point (src:54-143 up to the minima): RadiusByViewingCos, the window at the
 // predicted level (levels level-1 .. level), the stereo u_R test, distances
-__global__ __launch_bounds__(64 * kCandWaves) void k_lmp_candidates(const LocalParams P, const uint8_t* __restrict__ in_view,
+__device__ __forceinline__ void k_lmp_candidates_body(const LocalParams P, const uint8_t* __restrict__ in_view,
                                                         const uint8_t* __restrict__ bad, const float* __restrict__ proj,
                                                         const float* __restrict__ view_cos, const float* __restrict__ depth,
                                                         const int32_t* __restrict__ level, const uint4* __restrict__ mp_desc,
@@ -257,6 +292,44 @@ __global__ __launch_bounds__(64 * kCandWaves) void k_lmp_candidates(const LocalP
     }
     __threadfence_block();  // the wave's own candidate stores, read back across lanes
     if (observed[i]) record_listers(lane, i, n, P.cap, cands + (size_t)i * P.cap, taken0, lister);
+}
+__global__ __launch_bounds__(64 * kCandWaves) void k_lmp_candidates(const LocalParams P, const uint8_t* __restrict__ in_view,
+                                                        const uint8_t* __restrict__ bad, const float* __restrict__ proj,
+                                                        const float* __restrict__ view_cos, const float* __restrict__ depth,
+                                                        const int32_t* __restrict__ level, const uint4* __restrict__ mp_desc,
+                                                        const float4* __restrict__ cur_kp, const float* __restrict__ cur_ur,
+                                                        const uint4* __restrict__ cur_desc, const int32_t* __restrict__ cell_off,
+                                                        const int32_t* __restrict__ cell_idx, Cand* __restrict__ cands,
+                                                        int32_t* __restrict__ ncand, int32_t* __restrict__ overflow,
+                                                        const uint8_t* __restrict__ observed, const uint8_t* __restrict__ taken0,
+                                                        int32_t* __restrict__ lister) {
+    k_lmp_candidates_body(P, in_view, bad, proj, view_cos, depth, level, mp_desc, cur_kp, cur_ur, cur_desc, cell_off, cell_idx, cands, ncand, overflow, observed, taken0, lister);
+}
+struct k_lmp_candidates_args {
+    LocalParams P;
+    const uint8_t* in_view;
+    const uint8_t* bad;
+    const float* proj;
+    const float* view_cos;
+    const float* depth;
+    const int32_t* level;
+    const uint4* mp_desc;
+    const float4* cur_kp;
+    const float* cur_ur;
+    const uint4* cur_desc;
+    const int32_t* cell_off;
+    const int32_t* cell_idx;
+    Cand* cands;
+    int32_t* ncand;
+    int32_t* overflow;
+    const uint8_t* observed;
+    const uint8_t* taken0;
+    int32_t* lister;
+};
+// the same on frame blockIdx.y of a batch (one argument block per frame)
+__global__ __launch_bounds__(64 * kCandWaves) void k_lmp_candidates_b(const k_lmp_candidates_args* __restrict__ a) {
+    const k_lmp_candidates_args& A = a[blockIdx.y];
+    k_lmp_candidates_body(A.P, A.in_view, A.bad, A.proj, A.view_cos, A.depth, A.level, A.mp_desc, A.cur_kp, A.cur_ur, A.cur_desc, A.cell_off, A.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.taken0, A.lister);
 }
 
 // ---- the in-order assignment, resolved by parallel fixed-point rounds ----------------------------
@@ -381,7 +454,7 @@ __device__ __forceinline__ int decide(const ResolveArgs& a, int d1, int j1, int 
 // kTop best usable candidates in (distance, order), the classification, the work list and the fixed
 // claims.  k_resolve_rounds (one workgroup) then iterates only the work list, each point re-deciding
 // from its kTop best (a full scan only when too many of them are claimed).
-__global__ __launch_bounds__(256) void k_resolve_init(ResolveArgs a) {
+__device__ __forceinline__ void k_resolve_init_body(ResolveArgs a) {
     if (a.dims) {
         a.n_pts = a.dims[0];
         a.n_cur = a.dims[1];
@@ -418,6 +491,17 @@ __global__ __launch_bounds__(256) void k_resolve_init(ResolveArgs a) {
     a.nusable[i] = nu;
     if (affected) a.work[atomicAdd(&a.out_n[2], 1)] = i;
     else if (st >= 0 && a.observed[i]) atomicMin(&a.fixed[st], i);
+}
+__global__ __launch_bounds__(256) void k_resolve_init(ResolveArgs a) {
+    k_resolve_init_body(a);
+}
+struct k_resolve_init_args {
+    ResolveArgs a;
+};
+// the same on frame blockIdx.y of a batch (one argument block per frame)
+__global__ __launch_bounds__(256) void k_resolve_init_b(const k_resolve_init_args* __restrict__ a) {
+    const k_resolve_init_args& A = a[blockIdx.y];
+    k_resolve_init_body(A.a);
 }
 
 // point i's answer in a round, from its kTop best (claims by earlier points excluded)
@@ -486,7 +570,7 @@ __device__ __forceinline__ int resolve_reg(const ResolveArgs& a, const int32_t* 
     return j1;
 }
 
-__global__ __launch_bounds__(kResolveThreads) void k_resolve_rounds(ResolveArgs a) {
+__device__ __forceinline__ void k_resolve_rounds_body(ResolveArgs a) {
     if (a.dims) {
         a.n_pts = a.dims[0];
         a.n_cur = a.dims[1];
@@ -609,6 +693,17 @@ __global__ __launch_bounds__(kResolveThreads) void k_resolve_rounds(ResolveArgs 
         if (a.out_user) a.out_user[0] = cnt[0] - cnt[1];
     }
 }
+__global__ __launch_bounds__(kResolveThreads) void k_resolve_rounds(ResolveArgs a) {
+    k_resolve_rounds_body(a);
+}
+struct k_resolve_rounds_args {
+    ResolveArgs a;
+};
+// the same on frame blockIdx.y of a batch (one argument block per frame)
+__global__ __launch_bounds__(kResolveThreads) void k_resolve_rounds_b(const k_resolve_rounds_args* __restrict__ a) {
+    const k_resolve_rounds_args& A = a[blockIdx.y];
+    k_resolve_rounds_body(A.a);
+}
 
 // ---- device-resident forms: the frame's grid and packed keypoints built on the device ------------
 
@@ -633,7 +728,7 @@ struct ScratchInit {
 // keypoints' cells in registers.
 constexpr int kPrepThreads = 1024, kCells = kGridCols * kGridRows, kPrepLds = 8192;
 constexpr int kPrepPer = 16;  // keypoints per thread: cap <= 16384
-__global__ __launch_bounds__(kPrepThreads) void k_frame_prep(const orb_keypoint_t* __restrict__ kps,
+__device__ __forceinline__ void k_frame_prep_body(const orb_keypoint_t* __restrict__ kps,
                                                              const int32_t* __restrict__ n_ptr, int cap, float min_x,
                                                              float min_y, float inv_w, float inv_h,
                                                              float4* __restrict__ kp4, int32_t* __restrict__ cell_off,
@@ -723,10 +818,39 @@ __global__ __launch_bounds__(kPrepThreads) void k_frame_prep(const orb_keypoint_
         for (int i = tid; i < n; i += kPrepThreads) cell_idx[i] = sidx[i];
     }
 }
+__global__ __launch_bounds__(kPrepThreads) void k_frame_prep(const orb_keypoint_t* __restrict__ kps,
+                                                             const int32_t* __restrict__ n_ptr, int cap, float min_x,
+                                                             float min_y, float inv_w, float inv_h,
+                                                             float4* __restrict__ kp4, int32_t* __restrict__ cell_off,
+                                                             int32_t* __restrict__ cell_idx, int32_t* __restrict__ cell_of,
+                                                             int32_t* n_out0, int32_t* n_out1, ScratchInit z) {
+    k_frame_prep_body(kps, n_ptr, cap, min_x, min_y, inv_w, inv_h, kp4, cell_off, cell_idx, cell_of, n_out0, n_out1, z);
+}
+struct k_frame_prep_args {
+    const orb_keypoint_t* kps;
+    const int32_t* n_ptr;
+    int cap;
+    float min_x;
+    float min_y;
+    float inv_w;
+    float inv_h;
+    float4* kp4;
+    int32_t* cell_off;
+    int32_t* cell_idx;
+    int32_t* cell_of;
+    int32_t* n_out0;
+    int32_t* n_out1;
+    ScratchInit z;
+};
+// the same on frame blockIdx.y of a batch (one argument block per frame)
+__global__ __launch_bounds__(kPrepThreads) void k_frame_prep_b(const k_frame_prep_args* __restrict__ a) {
+    const k_frame_prep_args& A = a[blockIdx.y];
+    k_frame_prep_body(A.kps, A.n_ptr, A.cap, A.min_x, A.min_y, A.inv_w, A.inv_h, A.kp4, A.cell_off, A.cell_idx, A.cell_of, A.n_out0, A.n_out1, A.z);
+}
 
 // the last frame's per-point inputs of k_proj_candidates / the rotation bins: a point whose octave is
 // outside the pyramid is not valid (the host form rejects the call instead)
-__global__ __launch_bounds__(256) void k_last_prep(const orb_keypoint_t* __restrict__ kps, const uint8_t* __restrict__ valid,
+__device__ __forceinline__ void k_last_prep_body(const orb_keypoint_t* __restrict__ kps, const uint8_t* __restrict__ valid,
                                                    const int32_t* __restrict__ n_ptr, int cap, int nlevels,
                                                    uint8_t* __restrict__ valid2, int32_t* __restrict__ octave,
                                                    float* __restrict__ angle, int32_t* n_out0, int32_t* n_out1) {
@@ -742,12 +866,51 @@ __global__ __launch_bounds__(256) void k_last_prep(const orb_keypoint_t* __restr
     angle[i] = kp.angle;
     valid2[i] = valid[i] && kp.octave >= 0 && kp.octave < nlevels;
 }
+__global__ __launch_bounds__(256) void k_last_prep(const orb_keypoint_t* __restrict__ kps, const uint8_t* __restrict__ valid,
+                                                   const int32_t* __restrict__ n_ptr, int cap, int nlevels,
+                                                   uint8_t* __restrict__ valid2, int32_t* __restrict__ octave,
+                                                   float* __restrict__ angle, int32_t* n_out0, int32_t* n_out1) {
+    k_last_prep_body(kps, valid, n_ptr, cap, nlevels, valid2, octave, angle, n_out0, n_out1);
+}
+struct k_last_prep_args {
+    const orb_keypoint_t* kps;
+    const uint8_t* valid;
+    const int32_t* n_ptr;
+    int cap;
+    int nlevels;
+    uint8_t* valid2;
+    int32_t* octave;
+    float* angle;
+    int32_t* n_out0;
+    int32_t* n_out1;
+};
+// the same on frame blockIdx.y of a batch (one argument block per frame)
+__global__ __launch_bounds__(256) void k_last_prep_b(const k_last_prep_args* __restrict__ a) {
+    const k_last_prep_args& A = a[blockIdx.y];
+    k_last_prep_body(A.kps, A.valid, A.n_ptr, A.cap, A.nlevels, A.valid2, A.octave, A.angle, A.n_out0, A.n_out1);
+}
 
 // local map points: a predicted level outside the pyramid leaves the point out
-__global__ __launch_bounds__(256) void k_local_prep(const uint8_t* __restrict__ in_view, const int32_t* __restrict__ level,
+__device__ __forceinline__ void k_local_prep_body(const uint8_t* __restrict__ in_view, const int32_t* __restrict__ level,
                                                     int n, int nlevels, uint8_t* __restrict__ in_view2) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i < n) in_view2[i] = in_view[i] && level[i] >= 0 && level[i] < nlevels;
+}
+__global__ __launch_bounds__(256) void k_local_prep(const uint8_t* __restrict__ in_view, const int32_t* __restrict__ level,
+                                                    int n, int nlevels, uint8_t* __restrict__ in_view2) {
+    k_local_prep_body(in_view, level, n, nlevels, in_view2);
+}
+struct k_local_prep_args {
+    const uint8_t* in_view;
+    const int32_t* level;
+    int n;
+    int nlevels;
+    uint8_t* in_view2;
+};
+// the same on frame blockIdx.y of a batch (one argument block per frame)
+__global__ __launch_bounds__(256) void k_local_prep_b(const k_local_prep_args* __restrict__ a) {
+    const k_local_prep_args& A = a[blockIdx.y];
+    k_local_prep_body(A.in_view, A.level, A.n, A.nlevels, A.in_view2);
 }
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -1093,15 +1256,31 @@ extern "C" int orb_search_by_projection_frame_device(orb_matcher_t m, const orb_
     return orbgpu_sbp_frame_device_scratch(m, cur, last, th, mono, d_match, d_n_matches, stream, nullptr);
 }
 
-int orbgpu_sbp_frame_device_scratch(orb_matcher_t m, const orb_frame_device_t* cur, const orb_last_points_device_t* last,
-                                    float th, int mono, int32_t* d_match, int32_t* d_n_matches, void* stream,
-                                    void* scratch) {
-    if (!m || !frame_device_ok(cur) || !last || !d_match || !d_n_matches || !last->n || last->cap < 0 ||
-        (last->cap > 0 && (!last->valid || !last->observed || !last->xyz || !last->desc || !last->kps_un)) ||
-        (reinterpret_cast<uintptr_t>(last->desc) & 15) != 0)
-        return orbgpu_fail(ORB_ERR_ARG, "bad SearchByProjection device arguments");
-    hipStream_t s = (hipStream_t)stream;
+namespace {
+
+// One frame's launches of a device SearchByProjection form, as argument blocks (the single-frame call
+// launches them by value, the batch copies them to the device and launches one grid row per frame).
+struct SbpFramePlan {
+    k_frame_prep_args prep;
+    k_last_prep_args lprep;
+    k_proj_candidates_args cand;
+    k_resolve_init_args init;
+    k_resolve_rounds_args rounds;
+    int C, NL;
+};
+
+bool sbp_frame_args_ok(orb_matcher_t m, const orb_frame_device_t* cur, const orb_last_points_device_t* last,
+                       const int32_t* d_match, const int32_t* d_n_matches) {
+    return m && frame_device_ok(cur) && last && d_match && d_n_matches && last->n && last->cap >= 0 &&
+           (last->cap == 0 || (last->valid && last->observed && last->xyz && last->desc && last->kps_un)) &&
+           (reinterpret_cast<uintptr_t>(last->desc) & 15) == 0;
+}
+
+void sbp_frame_plan(orb_matcher_t m, const orb_frame_device_t* cur, const orb_last_points_device_t* last, float th,
+                    int mono, int32_t* d_match, int32_t* d_n_matches, char* base, SbpFramePlan& pl) {
     const int C = cur->cap, NL = last->cap;
+    pl.C = C;
+    pl.NL = NL;
     ProjParams P{};
     memcpy(P.Tcw, cur->Tcw, sizeof(P.Tcw));
     P.min_x = cur->min_x; P.max_x = cur->max_x; P.min_y = cur->min_y; P.max_y = cur->max_y;
@@ -1121,12 +1300,10 @@ int orbgpu_sbp_frame_device_scratch(orb_matcher_t m, const orb_frame_device_t* c
     }
     P.cap = C;  // a point's candidates are distinct current keypoints: never more than the frame holds
     P.check_ori = orbgpu_matcher_check_ori(m);
-    // scratch: params | dims | kp4 | cells | cell_of | last prep | lister + fixed | overflow block |
-    // candidates | ncand | st | claimMin, last, removed | work list | top
+    // scratch: dims | kp4 | cells | cell_of | last prep | lister + fixed | overflow block | candidates |
+    // ncand | st | claimMin, last, removed | work list | top
     DevScratch z;
-    z.base = static_cast<char*>(scratch);  // the caller's (orbgpu_sbp_frame_scratch_bytes), else stream-ordered
-    if (!z.base && hipMallocAsync(reinterpret_cast<void**>(&z.base), orbgpu_sbp_frame_scratch_bytes(C, NL), s) != hipSuccess)
-        return orbgpu_fail(ORB_ERR_DEVICE, "hipMallocAsync failed");
+    z.base = base;
     int32_t* dims = z.take<int32_t>(2);
     float4* kp4 = z.take<float4>(C);
     int32_t* cell_off = z.take<int32_t>(kCells + 1);
@@ -1144,34 +1321,110 @@ int orbgpu_sbp_frame_device_scratch(orb_matcher_t m, const orb_frame_device_t* c
     int32_t* wl = z.take<int32_t>(NL);
     int4* top = z.take<int4>((kTop / 2) * (size_t)NL);
     int32_t* nus = z.take<int32_t>(NL);
-    bool ok = true;
-    {
-        const ScratchInit zi{lf, 2 * C, d_match, C, ovf, dims, NL > 0 ? -1 : 0};
-        hipLaunchKernelGGL(k_frame_prep, dim3(1), dim3(kPrepThreads), 0, s, cur->kps_un, cur->n, C, cur->min_x, cur->min_y,
-                           cur->grid_inv_w, cur->grid_inv_h, kp4, cell_off, cell_idx, cell_of, dims + 1, (int32_t*)nullptr,
-                           zi);
-        if (NL > 0) {
-            hipLaunchKernelGGL(k_last_prep, dim3((NL + 255) / 256), dim3(256), 0, s, last->kps_un, last->valid, last->n, NL,
-                               cur->nlevels, valid2, loct, lang, dims, (int32_t*)nullptr);
-            hipLaunchKernelGGL(k_proj_candidates, dim3((NL + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s,
-                               P, (const int32_t*)dims, (const uint8_t*)valid2, last->xyz, (const uint4*)last->desc,
-                               (const int32_t*)loct, (const float4*)kp4, cur->u_right, (const uint4*)cur->desc,
-                               (const int32_t*)cell_off, (const int32_t*)cell_idx, cands, nc, ovf, last->observed, lf);
-        }
-        ResolveArgs ra{};
-        ra.n_pts = NL; ra.n_cur = C; ra.cap = C; ra.local = 0; ra.check_ori = P.check_ori; ra.nnratio = 0.f;
-        ra.cands = cands; ra.ncand = nc; ra.observed = last->observed; ra.taken0 = nullptr; ra.cur_kp = kp4;
-        ra.last_angle = lang; ra.overflow = ovf; ra.st = st;
-        ra.claimMin = kw; ra.last = kw + C; ra.removed = kw + 2 * (size_t)C;
-        ra.lister = lf; ra.fixed = lf + C; ra.work = wl; ra.top = top; ra.nusable = nus;
-        ra.lds_keypoints = resolve_lds_ready() ? 1 : 0;
-        ra.mp = d_match; ra.out_n = ovf + 1; ra.dims = dims; ra.out_user = d_n_matches;
-        if (NL > 0) hipLaunchKernelGGL(k_resolve_init, dim3((NL + 255) / 256), dim3(256), 0, s, ra);
-        hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 8 * (size_t)C : 0, s, ra);
-        ok = hipGetLastError() == hipSuccess;
+    const ScratchInit zi{lf, 2 * C, d_match, C, ovf, dims, NL > 0 ? -1 : 0};
+    pl.prep = k_frame_prep_args{cur->kps_un, cur->n, C, cur->min_x, cur->min_y, cur->grid_inv_w, cur->grid_inv_h, kp4,
+                                cell_off, cell_idx, cell_of, dims + 1, nullptr, zi};
+    pl.lprep = k_last_prep_args{last->kps_un, last->valid, last->n, NL, cur->nlevels, valid2, loct, lang, dims, nullptr};
+    pl.cand = k_proj_candidates_args{P, dims, valid2, last->xyz, (const uint4*)last->desc, loct, kp4, cur->u_right,
+                                     (const uint4*)cur->desc, cell_off, cell_idx, cands, nc, ovf, last->observed, lf};
+    ResolveArgs ra{};
+    ra.n_pts = NL; ra.n_cur = C; ra.cap = C; ra.local = 0; ra.check_ori = P.check_ori; ra.nnratio = 0.f;
+    ra.cands = cands; ra.ncand = nc; ra.observed = last->observed; ra.taken0 = nullptr; ra.cur_kp = kp4;
+    ra.last_angle = lang; ra.overflow = ovf; ra.st = st;
+    ra.claimMin = kw; ra.last = kw + C; ra.removed = kw + 2 * (size_t)C;
+    ra.lister = lf; ra.fixed = lf + C; ra.work = wl; ra.top = top; ra.nusable = nus;
+    ra.lds_keypoints = resolve_lds_ready() ? 1 : 0;
+    ra.mp = d_match; ra.out_n = ovf + 1; ra.dims = dims; ra.out_user = d_n_matches;
+    pl.init.a = ra;
+    pl.rounds.a = ra;
+}
+
+// Argument blocks of B frames into one host block (each kernel's B blocks contiguous, 256-B aligned),
+// copied once; pointers of each kernel's array on the device.
+struct ArgPacker {
+    std::vector<char> host;
+    template <class T>
+    size_t add(const std::vector<T>& v) {
+        const size_t off = align256(host.size());
+        host.resize(off + v.size() * sizeof(T));
+        memcpy(host.data() + off, v.data(), v.size() * sizeof(T));
+        return off;
     }
-    if (!scratch && hipFreeAsync(z.base, s) != hipSuccess) ok = false;
+};
+
+}  // namespace
+
+int orbgpu_sbp_frame_device_scratch(orb_matcher_t m, const orb_frame_device_t* cur, const orb_last_points_device_t* last,
+                                    float th, int mono, int32_t* d_match, int32_t* d_n_matches, void* stream,
+                                    void* scratch) {
+    if (!sbp_frame_args_ok(m, cur, last, d_match, d_n_matches))
+        return orbgpu_fail(ORB_ERR_ARG, "bad SearchByProjection device arguments");
+    hipStream_t s = (hipStream_t)stream;
+    const int C = cur->cap, NL = last->cap;
+    char* base = static_cast<char*>(scratch);  // the caller's (orbgpu_sbp_frame_scratch_bytes), else stream-ordered
+    if (!base && hipMallocAsync(reinterpret_cast<void**>(&base), orbgpu_sbp_frame_scratch_bytes(C, NL), s) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "hipMallocAsync failed");
+    SbpFramePlan pl;
+    sbp_frame_plan(m, cur, last, th, mono, d_match, d_n_matches, base, pl);
+    const k_frame_prep_args& fp = pl.prep;
+    hipLaunchKernelGGL(k_frame_prep, dim3(1), dim3(kPrepThreads), 0, s, fp.kps, fp.n_ptr, fp.cap, fp.min_x, fp.min_y,
+                       fp.inv_w, fp.inv_h, fp.kp4, fp.cell_off, fp.cell_idx, fp.cell_of, fp.n_out0, fp.n_out1, fp.z);
+    if (NL > 0) {
+        const k_last_prep_args& lp = pl.lprep;
+        hipLaunchKernelGGL(k_last_prep, dim3((NL + 255) / 256), dim3(256), 0, s, lp.kps, lp.valid, lp.n_ptr, lp.cap,
+                           lp.nlevels, lp.valid2, lp.octave, lp.angle, lp.n_out0, lp.n_out1);
+        const k_proj_candidates_args& c = pl.cand;
+        hipLaunchKernelGGL(k_proj_candidates, dim3((NL + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s,
+                           c.P, c.n_dev, c.valid, c.xyz, c.mp_desc, c.last_octave, c.cur_kp, c.cur_ur, c.cur_desc,
+                           c.cell_off, c.cell_idx, c.cands, c.ncand, c.overflow, c.observed, c.lister);
+        hipLaunchKernelGGL(k_resolve_init, dim3((NL + 255) / 256), dim3(256), 0, s, pl.init.a);
+    }
+    hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), pl.rounds.a.lds_keypoints ? 8 * (size_t)C : 0, s,
+                       pl.rounds.a);
+    bool ok = hipGetLastError() == hipSuccess;
+    if (!scratch && hipFreeAsync(base, s) != hipSuccess) ok = false;
     return ok ? ORB_OK : orbgpu_fail(ORB_ERR_DEVICE, "SearchByProjection device failed");
+}
+
+int orbgpu_sbp_frame_batch(orb_matcher_t m, int B, const orb_frame_device_t* const* cur,
+                           const orb_last_points_device_t* const* last, float th, int mono, int32_t* const* d_match,
+                           int32_t* const* d_n_matches, char* scratch, size_t stride, void* d_args, void* h_args,
+                           size_t args_cap, void* stream) {
+    if (B <= 0 || !scratch || !d_args || !h_args) return orbgpu_fail(ORB_ERR_ARG, "bad SearchByProjection batch arguments");
+    hipStream_t s = (hipStream_t)stream;
+    std::vector<k_frame_prep_args> fp(B);
+    std::vector<k_last_prep_args> lp(B);
+    std::vector<k_proj_candidates_args> ca(B);
+    std::vector<k_resolve_init_args> ri(B);
+    std::vector<k_resolve_rounds_args> rr(B);
+    int C = -1, maxNL = 0;
+    for (int b = 0; b < B; ++b) {
+        if (!sbp_frame_args_ok(m, cur[b], last[b], d_match[b], d_n_matches[b]) || (C >= 0 && cur[b]->cap != C) ||
+            orbgpu_sbp_frame_scratch_bytes(cur[b]->cap, last[b]->cap) > stride)
+            return orbgpu_fail(ORB_ERR_ARG, "bad SearchByProjection batch frame (caps must agree, scratch stride)");
+        C = cur[b]->cap;
+        SbpFramePlan pl;
+        sbp_frame_plan(m, cur[b], last[b], th, mono, d_match[b], d_n_matches[b], scratch + (size_t)b * stride, pl);
+        fp[b] = pl.prep; lp[b] = pl.lprep; ca[b] = pl.cand; ri[b] = pl.init; rr[b] = pl.rounds;
+        maxNL = std::max(maxNL, pl.NL);
+    }
+    ArgPacker pk;
+    const size_t o_fp = pk.add(fp), o_lp = pk.add(lp), o_ca = pk.add(ca), o_ri = pk.add(ri), o_rr = pk.add(rr);
+    if (pk.host.size() > args_cap) return orbgpu_fail(ORB_ERR_ARG, "SearchByProjection batch: argument area too small");
+    char* d = static_cast<char*>(d_args);
+    memcpy(h_args, pk.host.data(), pk.host.size());  // pinned staging: the copy reads it when the stream runs it
+    if (hipMemcpyAsync(d, h_args, pk.host.size(), hipMemcpyHostToDevice, s) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "batch argument upload failed");
+    hipLaunchKernelGGL(k_frame_prep_b, dim3(1, B), dim3(kPrepThreads), 0, s, (const k_frame_prep_args*)(d + o_fp));
+    if (maxNL > 0) {  // grids sized for the largest frame; the kernels bound themselves by their own counts
+        hipLaunchKernelGGL(k_last_prep_b, dim3((maxNL + 255) / 256, B), dim3(256), 0, s, (const k_last_prep_args*)(d + o_lp));
+        hipLaunchKernelGGL(k_proj_candidates_b, dim3((maxNL + kCandWaves - 1) / kCandWaves, B), dim3(64 * kCandWaves), 0, s,
+                           (const k_proj_candidates_args*)(d + o_ca));
+        hipLaunchKernelGGL(k_resolve_init_b, dim3((maxNL + 255) / 256, B), dim3(256), 0, s, (const k_resolve_init_args*)(d + o_ri));
+    }
+    hipLaunchKernelGGL(k_resolve_rounds_b, dim3(1, B), dim3(kResolveThreads), rr[0].a.lds_keypoints ? 8 * (size_t)C : 0, s,
+                       (const k_resolve_rounds_args*)(d + o_rr));
+    return hipGetLastError() == hipSuccess ? ORB_OK : orbgpu_fail(ORB_ERR_DEVICE, "SearchByProjection batch launch failed");
 }
 
 size_t orbgpu_sbp_local_scratch_bytes(int C, int np) {
@@ -1191,16 +1444,31 @@ extern "C" int orb_search_by_projection_local_device(orb_matcher_t m, const orb_
                                            stream, nullptr);
 }
 
-int orbgpu_sbp_local_device_scratch(orb_matcher_t m, const orb_frame_device_t* F, const uint8_t* d_frame_taken,
-                                    const orb_local_points_device_t* pts, float th, int far_points, float th_far_points,
-                                    int32_t* d_match, int32_t* d_n_matches, void* stream, void* scratch) {
-    if (!m || !frame_device_ok(F) || !pts || pts->n < 0 || !d_match || !d_n_matches ||
-        (pts->n && (!pts->track_in_view || !pts->is_bad || !pts->observed || !pts->track_proj || !pts->track_view_cos ||
-                    !pts->track_depth || !pts->track_level || !pts->desc)) ||
-        (reinterpret_cast<uintptr_t>(pts->desc) & 15) != 0)
-        return orbgpu_fail(ORB_ERR_ARG, "bad SearchByProjection(local map) device arguments");
-    hipStream_t s = (hipStream_t)stream;
+namespace {
+
+struct SbpLocalPlan {
+    k_frame_prep_args prep;
+    k_local_prep_args lprep;
+    k_lmp_candidates_args cand;
+    k_resolve_init_args init;
+    k_resolve_rounds_args rounds;
+    int C, np;
+};
+
+bool sbp_local_args_ok(orb_matcher_t m, const orb_frame_device_t* F, const orb_local_points_device_t* pts,
+                       const int32_t* d_match, const int32_t* d_n_matches) {
+    return m && frame_device_ok(F) && pts && pts->n >= 0 && d_match && d_n_matches &&
+           (pts->n == 0 || (pts->track_in_view && pts->is_bad && pts->observed && pts->track_proj && pts->track_view_cos &&
+                            pts->track_depth && pts->track_level && pts->desc)) &&
+           (reinterpret_cast<uintptr_t>(pts->desc) & 15) == 0;
+}
+
+void sbp_local_plan(orb_matcher_t m, const orb_frame_device_t* F, const uint8_t* d_frame_taken,
+                    const orb_local_points_device_t* pts, float th, int far_points, float th_far_points, int32_t* d_match,
+                    int32_t* d_n_matches, char* base, SbpLocalPlan& pl) {
     const int C = F->cap, np = pts->n;
+    pl.C = C;
+    pl.np = np;
     LocalParams P{};
     P.min_x = F->min_x; P.min_y = F->min_y; P.inv_w = F->grid_inv_w; P.inv_h = F->grid_inv_h;
     P.th = th; P.th_far = th_far_points;
@@ -1209,9 +1477,7 @@ int orbgpu_sbp_local_device_scratch(orb_matcher_t m, const orb_frame_device_t* F
     P.cap = C;
     P.nnratio = orbgpu_matcher_nnratio(m);
     DevScratch z;
-    z.base = static_cast<char*>(scratch);  // the caller's (orbgpu_sbp_local_scratch_bytes), else stream-ordered
-    if (!z.base && hipMallocAsync(reinterpret_cast<void**>(&z.base), orbgpu_sbp_local_scratch_bytes(C, np), s) != hipSuccess)
-        return orbgpu_fail(ORB_ERR_DEVICE, "hipMallocAsync failed");
+    z.base = base;
     int32_t* dims = z.take<int32_t>(2);
     float4* kp4 = z.take<float4>(C);
     int32_t* cell_off = z.take<int32_t>(kCells + 1);
@@ -1227,33 +1493,98 @@ int orbgpu_sbp_local_device_scratch(orb_matcher_t m, const orb_frame_device_t* F
     int32_t* wl = z.take<int32_t>(np);
     int4* top = z.take<int4>((kTop / 2) * (size_t)np);
     int32_t* nus = z.take<int32_t>(np);
-    bool ok = true;
-    {
-        const ScratchInit zi{lf, 2 * C, d_match, C, ovf, dims, np};
-        hipLaunchKernelGGL(k_frame_prep, dim3(1), dim3(kPrepThreads), 0, s, F->kps_un, F->n, C, F->min_x, F->min_y,
-                           F->grid_inv_w, F->grid_inv_h, kp4, cell_off, cell_idx, cell_of, dims + 1, (int32_t*)nullptr,
-                           zi);
-        if (np > 0) {
-            hipLaunchKernelGGL(k_local_prep, dim3((np + 255) / 256), dim3(256), 0, s, pts->track_in_view, pts->track_level,
-                               np, F->nlevels, iv2);
-            hipLaunchKernelGGL(k_lmp_candidates, dim3((np + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s,
-                               P, (const uint8_t*)iv2, pts->is_bad, pts->track_proj, pts->track_view_cos,
-                               pts->track_depth, pts->track_level, (const uint4*)pts->desc, (const float4*)kp4, F->u_right,
-                               (const uint4*)F->desc, (const int32_t*)cell_off, (const int32_t*)cell_idx, cands, nc, ovf,
-                               pts->observed, d_frame_taken, lf);
-        }
-        ResolveArgs ra{};
-        ra.n_pts = np; ra.n_cur = C; ra.cap = C; ra.local = 1; ra.check_ori = 0; ra.nnratio = P.nnratio;
-        ra.cands = cands; ra.ncand = nc; ra.observed = pts->observed; ra.taken0 = d_frame_taken; ra.cur_kp = kp4;
-        ra.last_angle = nullptr; ra.overflow = ovf; ra.st = st;
-        ra.claimMin = kw; ra.last = kw + C; ra.removed = kw + 2 * (size_t)C;
-        ra.lister = lf; ra.fixed = lf + C; ra.work = wl; ra.top = top; ra.nusable = nus;
-        ra.lds_keypoints = resolve_lds_ready() ? 1 : 0;
-        ra.mp = d_match; ra.out_n = ovf + 1; ra.dims = dims; ra.out_user = d_n_matches;
-        if (np > 0) hipLaunchKernelGGL(k_resolve_init, dim3((np + 255) / 256), dim3(256), 0, s, ra);
-        hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 8 * (size_t)C : 0, s, ra);
-        ok = hipGetLastError() == hipSuccess;
+    const ScratchInit zi{lf, 2 * C, d_match, C, ovf, dims, np};
+    pl.prep = k_frame_prep_args{F->kps_un, F->n, C, F->min_x, F->min_y, F->grid_inv_w, F->grid_inv_h, kp4, cell_off,
+                                cell_idx, cell_of, dims + 1, nullptr, zi};
+    pl.lprep = k_local_prep_args{pts->track_in_view, pts->track_level, np, F->nlevels, iv2};
+    pl.cand = k_lmp_candidates_args{P, iv2, pts->is_bad, pts->track_proj, pts->track_view_cos, pts->track_depth,
+                                    pts->track_level, (const uint4*)pts->desc, kp4, F->u_right, (const uint4*)F->desc,
+                                    cell_off, cell_idx, cands, nc, ovf, pts->observed, d_frame_taken, lf};
+    ResolveArgs ra{};
+    ra.n_pts = np; ra.n_cur = C; ra.cap = C; ra.local = 1; ra.check_ori = 0; ra.nnratio = P.nnratio;
+    ra.cands = cands; ra.ncand = nc; ra.observed = pts->observed; ra.taken0 = d_frame_taken; ra.cur_kp = kp4;
+    ra.last_angle = nullptr; ra.overflow = ovf; ra.st = st;
+    ra.claimMin = kw; ra.last = kw + C; ra.removed = kw + 2 * (size_t)C;
+    ra.lister = lf; ra.fixed = lf + C; ra.work = wl; ra.top = top; ra.nusable = nus;
+    ra.lds_keypoints = resolve_lds_ready() ? 1 : 0;
+    ra.mp = d_match; ra.out_n = ovf + 1; ra.dims = dims; ra.out_user = d_n_matches;
+    pl.init.a = ra;
+    pl.rounds.a = ra;
+}
+
+}  // namespace
+
+int orbgpu_sbp_local_device_scratch(orb_matcher_t m, const orb_frame_device_t* F, const uint8_t* d_frame_taken,
+                                    const orb_local_points_device_t* pts, float th, int far_points, float th_far_points,
+                                    int32_t* d_match, int32_t* d_n_matches, void* stream, void* scratch) {
+    if (!sbp_local_args_ok(m, F, pts, d_match, d_n_matches))
+        return orbgpu_fail(ORB_ERR_ARG, "bad SearchByProjection(local map) device arguments");
+    hipStream_t s = (hipStream_t)stream;
+    const int C = F->cap, np = pts->n;
+    char* base = static_cast<char*>(scratch);  // the caller's (orbgpu_sbp_local_scratch_bytes), else stream-ordered
+    if (!base && hipMallocAsync(reinterpret_cast<void**>(&base), orbgpu_sbp_local_scratch_bytes(C, np), s) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "hipMallocAsync failed");
+    SbpLocalPlan pl;
+    sbp_local_plan(m, F, d_frame_taken, pts, th, far_points, th_far_points, d_match, d_n_matches, base, pl);
+    const k_frame_prep_args& fp = pl.prep;
+    hipLaunchKernelGGL(k_frame_prep, dim3(1), dim3(kPrepThreads), 0, s, fp.kps, fp.n_ptr, fp.cap, fp.min_x, fp.min_y,
+                       fp.inv_w, fp.inv_h, fp.kp4, fp.cell_off, fp.cell_idx, fp.cell_of, fp.n_out0, fp.n_out1, fp.z);
+    if (np > 0) {
+        const k_local_prep_args& lp = pl.lprep;
+        hipLaunchKernelGGL(k_local_prep, dim3((np + 255) / 256), dim3(256), 0, s, lp.in_view, lp.level, lp.n, lp.nlevels,
+                           lp.in_view2);
+        const k_lmp_candidates_args& c = pl.cand;
+        hipLaunchKernelGGL(k_lmp_candidates, dim3((np + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s,
+                           c.P, c.in_view, c.bad, c.proj, c.view_cos, c.depth, c.level, c.mp_desc, c.cur_kp, c.cur_ur,
+                           c.cur_desc, c.cell_off, c.cell_idx, c.cands, c.ncand, c.overflow, c.observed, c.taken0, c.lister);
+        hipLaunchKernelGGL(k_resolve_init, dim3((np + 255) / 256), dim3(256), 0, s, pl.init.a);
     }
-    if (!scratch && hipFreeAsync(z.base, s) != hipSuccess) ok = false;
+    hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), pl.rounds.a.lds_keypoints ? 8 * (size_t)C : 0, s,
+                       pl.rounds.a);
+    bool ok = hipGetLastError() == hipSuccess;
+    if (!scratch && hipFreeAsync(base, s) != hipSuccess) ok = false;
     return ok ? ORB_OK : orbgpu_fail(ORB_ERR_DEVICE, "SearchByProjection(local) device failed");
+}
+
+int orbgpu_sbp_local_batch(orb_matcher_t m, int B, const orb_frame_device_t* const* F, const uint8_t* const* d_frame_taken,
+                           const orb_local_points_device_t* const* pts, float th, int far_points, float th_far_points,
+                           int32_t* const* d_match, int32_t* const* d_n_matches, char* scratch, size_t stride,
+                           void* d_args, void* h_args, size_t args_cap, void* stream) {
+    if (B <= 0 || !scratch || !d_args || !h_args)
+        return orbgpu_fail(ORB_ERR_ARG, "bad SearchByProjection(local) batch arguments");
+    hipStream_t s = (hipStream_t)stream;
+    std::vector<k_frame_prep_args> fp(B);
+    std::vector<k_local_prep_args> lp(B);
+    std::vector<k_lmp_candidates_args> ca(B);
+    std::vector<k_resolve_init_args> ri(B);
+    std::vector<k_resolve_rounds_args> rr(B);
+    int C = -1, maxNp = 0;
+    for (int b = 0; b < B; ++b) {
+        if (!sbp_local_args_ok(m, F[b], pts[b], d_match[b], d_n_matches[b]) || (C >= 0 && F[b]->cap != C) ||
+            orbgpu_sbp_local_scratch_bytes(F[b]->cap, pts[b]->n) > stride)
+            return orbgpu_fail(ORB_ERR_ARG, "bad SearchByProjection(local) batch frame (caps must agree, scratch stride)");
+        C = F[b]->cap;
+        SbpLocalPlan pl;
+        sbp_local_plan(m, F[b], d_frame_taken[b], pts[b], th, far_points, th_far_points, d_match[b], d_n_matches[b],
+                       scratch + (size_t)b * stride, pl);
+        fp[b] = pl.prep; lp[b] = pl.lprep; ca[b] = pl.cand; ri[b] = pl.init; rr[b] = pl.rounds;
+        maxNp = std::max(maxNp, pl.np);
+    }
+    ArgPacker pk;
+    const size_t o_fp = pk.add(fp), o_lp = pk.add(lp), o_ca = pk.add(ca), o_ri = pk.add(ri), o_rr = pk.add(rr);
+    if (pk.host.size() > args_cap) return orbgpu_fail(ORB_ERR_ARG, "SearchByProjection(local) batch: argument area too small");
+    char* d = static_cast<char*>(d_args);
+    memcpy(h_args, pk.host.data(), pk.host.size());  // pinned staging: the copy reads it when the stream runs it
+    if (hipMemcpyAsync(d, h_args, pk.host.size(), hipMemcpyHostToDevice, s) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "batch argument upload failed");
+    hipLaunchKernelGGL(k_frame_prep_b, dim3(1, B), dim3(kPrepThreads), 0, s, (const k_frame_prep_args*)(d + o_fp));
+    if (maxNp > 0) {
+        hipLaunchKernelGGL(k_local_prep_b, dim3((maxNp + 255) / 256, B), dim3(256), 0, s, (const k_local_prep_args*)(d + o_lp));
+        hipLaunchKernelGGL(k_lmp_candidates_b, dim3((maxNp + kCandWaves - 1) / kCandWaves, B), dim3(64 * kCandWaves), 0, s,
+                           (const k_lmp_candidates_args*)(d + o_ca));
+        hipLaunchKernelGGL(k_resolve_init_b, dim3((maxNp + 255) / 256, B), dim3(256), 0, s, (const k_resolve_init_args*)(d + o_ri));
+    }
+    hipLaunchKernelGGL(k_resolve_rounds_b, dim3(1, B), dim3(kResolveThreads), rr[0].a.lds_keypoints ? 8 * (size_t)C : 0, s,
+                       (const k_resolve_rounds_args*)(d + o_rr));
+    return hipGetLastError() == hipSuccess ? ORB_OK : orbgpu_fail(ORB_ERR_DEVICE, "SearchByProjection(local) batch launch failed");
 }

@@ -16,6 +16,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <vector>
+#include <unordered_map>
+#include <mutex>
 
 #include <cstdint>
 #include <cstring>
@@ -31,11 +34,12 @@ constexpr int kThreads = 1024, kMaxLevels = 12;
 struct EdgeParams {
     float inv_sigma2[kMaxLevels];
     int nlevels, cap, has_pose_dev, has_b;
+    int edge_begin;  // the frame record's edge_begin (a batch's frame b: b cap into the batch's edge array)
     double pose[7];
     orb_ba_camera_t cam;
 };
 
-__global__ __launch_bounds__(kThreads) void k_track_pose_edges(EdgeParams P, const orb_keypoint_t* __restrict__ kps,
+__device__ __forceinline__ void k_track_pose_edges_body(EdgeParams P, const orb_keypoint_t* __restrict__ kps,
                                                                 const float* __restrict__ u_right,
                                                                 const int32_t* __restrict__ n_ptr,
                                                                 const int32_t* __restrict__ match_a,
@@ -101,15 +105,47 @@ __global__ __launch_bounds__(kThreads) void k_track_pose_edges(EdgeParams P, con
             for (int k = 0; k < 7; ++k) F.pose[k] = P.pose[k];
         }
         F.cam = P.cam;
-        F.edge_begin = 0;
+        F.edge_begin = P.edge_begin;
         F.n_edges = part[kThreads - 1];
         *frame = F;
     }
 }
+__global__ __launch_bounds__(kThreads) void k_track_pose_edges(EdgeParams P, const orb_keypoint_t* __restrict__ kps,
+                                                                const float* __restrict__ u_right,
+                                                                const int32_t* __restrict__ n_ptr,
+                                                                const int32_t* __restrict__ match_a,
+                                                                const float* __restrict__ xyz_a,
+                                                                const int32_t* __restrict__ match_b,
+                                                                const float* __restrict__ xyz_b,
+                                                                const double* __restrict__ pose_dev,
+                                                                orb_pose_frame_t* __restrict__ frame,
+                                                                orb_pose_edge_t* __restrict__ edges,
+                                                                int32_t* __restrict__ edge_kp) {
+    k_track_pose_edges_body(P, kps, u_right, n_ptr, match_a, xyz_a, match_b, xyz_b, pose_dev, frame, edges, edge_kp);
+}
+struct k_track_pose_edges_args {
+    EdgeParams P;
+    const orb_keypoint_t* kps;
+    const float* u_right;
+    const int32_t* n_ptr;
+    const int32_t* match_a;
+    const float* xyz_a;
+    const int32_t* match_b;
+    const float* xyz_b;
+    const double* pose_dev;
+    orb_pose_frame_t* frame;
+    orb_pose_edge_t* edges;
+    int32_t* edge_kp;
+};
+// the same on frame blockIdx.y of a batch (one argument block per frame)
+__global__ __launch_bounds__(kThreads) void k_track_pose_edges_b(const k_track_pose_edges_args* __restrict__ a) {
+    const k_track_pose_edges_args& A = a[blockIdx.y];
+    k_track_pose_edges_body(A.P, A.kps, A.u_right, A.n_ptr, A.match_a, A.xyz_a, A.match_b, A.xyz_b, A.pose_dev, A.frame, A.edges, A.edge_kp);
+}
 
 // outliers lose their map point; n_out[0] = the edges kept, n_out[1] = those whose map point has
 // observations (nmatchesMap, src/Tracking.cc:4198-4200)
-__global__ __launch_bounds__(kThreads) void k_track_discard(const orb_pose_frame_t* __restrict__ frame,
+__device__ __forceinline__ void k_track_discard_body(const orb_pose_frame_t* __restrict__ frame,
                                                        const int32_t* __restrict__ edge_kp,
                                                        const uint8_t* __restrict__ outlier, int32_t* __restrict__ match_a,
                                                        const uint8_t* __restrict__ observed_a, int32_t* __restrict__ match_b,
@@ -157,6 +193,31 @@ __global__ __launch_bounds__(kThreads) void k_track_discard(const orb_pose_frame
         taken[i] = t;
     }
 }
+__global__ __launch_bounds__(kThreads) void k_track_discard(const orb_pose_frame_t* __restrict__ frame,
+                                                       const int32_t* __restrict__ edge_kp,
+                                                       const uint8_t* __restrict__ outlier, int32_t* __restrict__ match_a,
+                                                       const uint8_t* __restrict__ observed_a, int32_t* __restrict__ match_b,
+                                                       const uint8_t* __restrict__ observed_b, int32_t* __restrict__ n_out,
+                                                       int cap, uint8_t* __restrict__ taken) {
+    k_track_discard_body(frame, edge_kp, outlier, match_a, observed_a, match_b, observed_b, n_out, cap, taken);
+}
+struct k_track_discard_args {
+    const orb_pose_frame_t* frame;
+    const int32_t* edge_kp;
+    const uint8_t* outlier;
+    int32_t* match_a;
+    const uint8_t* observed_a;
+    int32_t* match_b;
+    const uint8_t* observed_b;
+    int32_t* n_out;
+    int cap;
+    uint8_t* taken;
+};
+// the same on frame blockIdx.y of a batch (one argument block per frame)
+__global__ __launch_bounds__(kThreads) void k_track_discard_b(const k_track_discard_args* __restrict__ a) {
+    const k_track_discard_args& A = a[blockIdx.y];
+    k_track_discard_body(A.frame, A.edge_kp, A.outlier, A.match_a, A.observed_a, A.match_b, A.observed_b, A.n_out, A.cap, A.taken);
+}
 
 // SearchLocalPoints' first loop (src/Tracking.cc:4250-4266): a local map point the frame already holds
 // (mnLastFrameSeen == mCurrentFrame.mnId) is not tested against the frustum.  With the local map as its own
@@ -164,7 +225,7 @@ __global__ __launch_bounds__(kThreads) void k_track_discard(const orb_pose_frame
 // the rows the frame still holds after the discard go into an LDS bitmap.
 constexpr int kSeenBits = 16384;
 
-__global__ __launch_bounds__(kThreads) void k_track_local_seen(const int32_t* __restrict__ match_a, int cap, int last_cap,
+__device__ __forceinline__ void k_track_local_seen_body(const int32_t* __restrict__ match_a, int cap, int last_cap,
                                                                 const int32_t* __restrict__ last_row, int n_local,
                                                                 uint8_t* __restrict__ in_view) {
     __shared__ uint32_t bits[kSeenBits / 32];
@@ -180,6 +241,40 @@ __global__ __launch_bounds__(kThreads) void k_track_local_seen(const int32_t* __
         if (r >= 0 && r < last_cap && ((bits[r >> 5] >> (r & 31)) & 1u)) in_view[j] = 0;
     }
 }
+__global__ __launch_bounds__(kThreads) void k_track_local_seen(const int32_t* __restrict__ match_a, int cap, int last_cap,
+                                                                const int32_t* __restrict__ last_row, int n_local,
+                                                                uint8_t* __restrict__ in_view) {
+    k_track_local_seen_body(match_a, cap, last_cap, last_row, n_local, in_view);
+}
+struct k_track_local_seen_args {
+    const int32_t* match_a;
+    int cap;
+    int last_cap;
+    const int32_t* last_row;
+    int n_local;
+    uint8_t* in_view;
+};
+// the same on frame blockIdx.y of a batch (one argument block per frame)
+__global__ __launch_bounds__(kThreads) void k_track_local_seen_b(const k_track_local_seen_args* __restrict__ a) {
+    const k_track_local_seen_args& A = a[blockIdx.y];
+    k_track_local_seen_body(A.match_a, A.cap, A.last_cap, A.last_row, A.n_local, A.in_view);
+}
+
+// the batch's argument areas: one per stage, each room for B frames' largest argument blocks (the
+// SearchByProjection stages pack five kernels' blocks, 256-B aligned)
+constexpr int kBatchArgStages = 7;
+size_t batch_args_bytes(int B) { return ((size_t)B * 4096 + 8 * 256 + 255) & ~(size_t)255; }
+
+// The pinned host side of a batch's argument areas, one per batch scratch (the caller's batch object),
+// and an event after the call's last copy: the next call on that scratch writes the staging only once
+// the previous call's copies have read it (stream-ordered copies read pinned memory when they run).
+struct BatchStaging {
+    void* host = nullptr;
+    size_t bytes = 0;
+    hipEvent_t copied = nullptr;
+};
+std::mutex g_staging_mu;
+std::unordered_map<const void*, BatchStaging> g_staging;
 
 }  // namespace
 
@@ -285,6 +380,143 @@ int orb_tracking_chain_device(orb_matcher_t m_motion, orb_matcher_t m_local, con
         return rc;
     return orbgpu_pose_optimization_device_scratch(1, B->frames + 1, F->cap, B->edges2, B->poses + 7, B->outlier2,
                                                    B->inliers + 1, stream, static_cast<double*>(z));
+}
+
+size_t orb_tracking_chain_batch_scratch_bytes(int n_frames, int cap, int last_cap, int n_local) {
+    if (n_frames <= 0 || cap <= 0 || last_cap < 0 || n_local < 0) return 0;
+    const size_t stride = (std::max(orbgpu_sbp_frame_scratch_bytes(cap, last_cap),
+                                    orbgpu_sbp_local_scratch_bytes(cap, n_local)) + 255) & ~(size_t)255;
+    const size_t args = (size_t)kBatchArgStages * batch_args_bytes(n_frames);
+    return args + (size_t)n_frames * stride + (size_t)n_frames * cap * sizeof(double) + 256;
+}
+
+int orb_tracking_chain_batch_device(orb_matcher_t m_motion, orb_matcher_t m_local, int B,
+                                    const orb_tracking_chain_frame_t* fr, const orb_tracking_chain_params_t* P,
+                                    const orb_tracking_chain_batch_buffers_t* Bf, void* stream) {
+    if (!m_motion || !m_local || B <= 0 || !fr || !P || !Bf || !Bf->m1 || !Bf->m2 || !Bf->n_match || !Bf->frames ||
+        !Bf->edges1 || !Bf->edges2 || !Bf->edge_kp1 || !Bf->edge_kp2 || !Bf->outlier1 || !Bf->outlier2 || !Bf->poses ||
+        !Bf->inliers || !Bf->n_out || !Bf->taken || !Bf->scratch)
+        return orbgpu_fail(ORB_ERR_ARG, "bad tracking chain batch arguments");
+    int C = 0, NL = 0, NP = 0;
+    for (int b = 0; b < B; ++b) {
+        const orb_tracking_chain_frame_t& f = fr[b];
+        if (!f.frame || !f.last || !f.local || !f.frustum || !f.inv_level_sigma2 || f.frame->cap <= 0 ||
+            (b && f.frame->cap != C) || f.frame->nlevels <= 0 || f.frame->nlevels > kMaxLevels || f.last->cap > kSeenBits ||
+            (f.local->n > 0 && (!f.pos || !f.normal || !f.min_dist || !f.max_dist)))
+            return orbgpu_fail(ORB_ERR_ARG, "bad tracking chain batch frame (every frame the same cap)");
+        C = f.frame->cap;
+        NL = std::max(NL, f.last->cap);
+        NP = std::max(NP, f.local->n);
+    }
+    hipStream_t s = (hipStream_t)stream;
+    // scratch: argument areas (one per stage) | the frames' SearchByProjection scratch | PoseOptimization chi2
+    const size_t abytes = batch_args_bytes(B);
+    char* base = static_cast<char*>(Bf->scratch);
+    auto args = [&](int stage) { return static_cast<void*>(base + (size_t)stage * abytes); };
+    std::lock_guard<std::mutex> lock(g_staging_mu);
+    BatchStaging& stg = g_staging[Bf->scratch];
+    if (stg.copied && hipEventSynchronize(stg.copied) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "batch staging wait failed");
+    if (stg.bytes < (size_t)kBatchArgStages * abytes) {
+        if (stg.host) (void)hipHostFree(stg.host);
+        stg.host = nullptr;
+        stg.bytes = 0;
+        if (hipHostMalloc(&stg.host, (size_t)kBatchArgStages * abytes, hipHostMallocDefault) != hipSuccess)
+            return orbgpu_fail(ORB_ERR_DEVICE, "hipHostMalloc failed");
+        stg.bytes = (size_t)kBatchArgStages * abytes;
+    }
+    if (!stg.copied && hipEventCreateWithFlags(&stg.copied, hipEventDisableTiming) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "hipEventCreate failed");
+    auto hargs = [&](int stage) { return static_cast<void*>(static_cast<char*>(stg.host) + (size_t)stage * abytes); };
+    const size_t stride = (std::max(orbgpu_sbp_frame_scratch_bytes(C, NL), orbgpu_sbp_local_scratch_bytes(C, NP)) + 255) &
+                          ~(size_t)255;
+    char* sbp = base + (size_t)kBatchArgStages * abytes;
+    double* chi = reinterpret_cast<double*>(sbp + (size_t)B * stride);
+    std::vector<const orb_frame_device_t*> cur(B);
+    std::vector<const orb_last_points_device_t*> last(B);
+    std::vector<const orb_local_points_device_t*> loc(B);
+    std::vector<int32_t*> m1(B), m2(B), n1(B), n2(B);
+    std::vector<const uint8_t*> taken(B);
+    for (int b = 0; b < B; ++b) {
+        cur[b] = fr[b].frame;
+        last[b] = fr[b].last;
+        loc[b] = fr[b].local;
+        m1[b] = Bf->m1 + (size_t)b * C;
+        m2[b] = Bf->m2 + (size_t)b * C;
+        n1[b] = Bf->n_match + 2 * (size_t)b;
+        n2[b] = n1[b] + 1;
+        taken[b] = Bf->taken + (size_t)b * C;
+    }
+    orb_pose_frame_t* fr1 = Bf->frames;
+    orb_pose_frame_t* fr2 = Bf->frames + B;
+    double* pose1 = Bf->poses;
+    double* pose2 = Bf->poses + 7 * (size_t)B;
+    int rc;
+    if ((rc = orbgpu_sbp_frame_batch(m_motion, B, cur.data(), last.data(), P->th_motion, P->mono, m1.data(), n1.data(),
+                                     sbp, stride, args(0), hargs(0), abytes, s)))
+        return rc;
+    // the first graphs: the last frame's points, the motion model's pose
+    auto edges_args = [&](int b, bool second) {
+        const orb_tracking_chain_frame_t& f = fr[b];
+        const orb_frame_device_t* F = f.frame;
+        EdgeParams E{};
+        for (int l = 0; l < F->nlevels; ++l) E.inv_sigma2[l] = f.inv_level_sigma2[l];
+        E.nlevels = F->nlevels;
+        E.cap = C;
+        E.has_pose_dev = second;
+        E.has_b = second && f.local->n > 0;
+        E.edge_begin = b * C;
+        if (!second) memcpy(E.pose, f.pose7, sizeof(E.pose));
+        E.cam = orb_ba_camera_t{F->fx, F->fy, F->cx, F->cy, F->bf};
+        const size_t o = (size_t)b * C;
+        return k_track_pose_edges_args{E, F->kps_un, F->u_right, F->n, m1[b], f.last->xyz, E.has_b ? m2[b] : nullptr,
+                                       E.has_b ? f.pos : nullptr, second ? pose1 + 7 * (size_t)b : nullptr,
+                                       second ? fr2 + b : fr1 + b, (second ? Bf->edges2 : Bf->edges1) + o,
+                                       (second ? Bf->edge_kp2 : Bf->edge_kp1) + o};
+    };
+    auto upload = [&](int stage, const void* h, size_t n) {
+        if (n > abytes) return false;
+        memcpy(hargs(stage), h, n);
+        return hipMemcpyAsync(args(stage), hargs(stage), n, hipMemcpyHostToDevice, s) == hipSuccess;
+    };
+    std::vector<k_track_pose_edges_args> ea(B);
+    for (int b = 0; b < B; ++b) ea[b] = edges_args(b, false);
+    if (!upload(1, ea.data(), B * sizeof(ea[0]))) return orbgpu_fail(ORB_ERR_DEVICE, "batch argument upload failed");
+    hipLaunchKernelGGL(k_track_pose_edges_b, dim3(1, B), dim3(kThreads), 0, s, (const k_track_pose_edges_args*)args(1));
+    if ((rc = orbgpu_pose_optimization_device_scratch(B, fr1, B * C, Bf->edges1, pose1, Bf->outlier1, Bf->inliers, stream, chi)))
+        return rc;
+    // isInFrustum at the first poses, the seen skip, the discard
+    if ((rc = orbgpu_frustum_chain_batch(B, fr, pose1, P->viewing_cos_limit, args(2), hargs(2), abytes, stream))) return rc;
+    std::vector<k_track_local_seen_args> sa(B);
+    bool any_seen = false;
+    for (int b = 0; b < B; ++b) {
+        const bool on = fr[b].last_row && fr[b].local->n > 0;
+        any_seen |= on;
+        sa[b] = k_track_local_seen_args{m1[b], C, fr[b].last->cap, fr[b].last_row, on ? fr[b].local->n : 0,
+                                        const_cast<uint8_t*>(fr[b].local->track_in_view)};
+    }
+    if (any_seen) {
+        if (!upload(3, sa.data(), B * sizeof(sa[0]))) return orbgpu_fail(ORB_ERR_DEVICE, "batch argument upload failed");
+        hipLaunchKernelGGL(k_track_local_seen_b, dim3(1, B), dim3(kThreads), 0, s, (const k_track_local_seen_args*)args(3));
+    }
+    std::vector<k_track_discard_args> da(B);
+    for (int b = 0; b < B; ++b)
+        da[b] = k_track_discard_args{fr1 + b, Bf->edge_kp1 + (size_t)b * C, Bf->outlier1 + (size_t)b * C, m1[b],
+                                     fr[b].last->observed, nullptr, nullptr, Bf->n_out + 2 * (size_t)b, C,
+                                     Bf->taken + (size_t)b * C};
+    if (!upload(4, da.data(), B * sizeof(da[0]))) return orbgpu_fail(ORB_ERR_DEVICE, "batch argument upload failed");
+    hipLaunchKernelGGL(k_track_discard_b, dim3(1, B), dim3(kThreads), 0, s, (const k_track_discard_args*)args(4));
+    if ((rc = orbgpu_sbp_local_batch(m_local, B, cur.data(), taken.data(), loc.data(), P->th_local, P->far_points,
+                                     P->th_far_points, m2.data(), n2.data(), sbp, stride, args(5), hargs(5), abytes, s)))
+        return rc;
+    // the second graphs: both searches, the first poses
+    for (int b = 0; b < B; ++b) ea[b] = edges_args(b, true);
+    if (!upload(6, ea.data(), B * sizeof(ea[0]))) return orbgpu_fail(ORB_ERR_DEVICE, "batch argument upload failed");
+    hipLaunchKernelGGL(k_track_pose_edges_b, dim3(1, B), dim3(kThreads), 0, s, (const k_track_pose_edges_args*)args(6));
+    if (hipGetLastError() != hipSuccess || hipEventRecord(stg.copied, s) != hipSuccess)
+        return orbgpu_fail(ORB_ERR_DEVICE, "tracking chain batch launch failed");
+    return orbgpu_pose_optimization_device_scratch(B, fr2, B * C, Bf->edges2, pose2, Bf->outlier2, Bf->inliers + B, stream,
+                                                   chi);
 }
 
 }  // extern "C"

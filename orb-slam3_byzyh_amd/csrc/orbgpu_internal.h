@@ -37,6 +37,20 @@ int orbgpu_pose_optimization_device_scratch(int n_frames, const orb_pose_frame_t
                                             const orb_pose_edge_t* d_edges, double* d_pose_out, uint8_t* d_outlier,
                                             int32_t* d_inliers, void* stream, double* d_chi);
 
+// The tracking chain's batch (orb_tracking_chain_batch_device): frame b's SearchByProjection scratch at
+// scratch + b stride; each call writes its frames' argument blocks into the pinned h_args and copies
+// them into d_args (args_cap bytes each) on the stream.
+int orbgpu_sbp_frame_batch(orb_matcher_t m, int B, const orb_frame_device_t* const* cur,
+                           const orb_last_points_device_t* const* last, float th, int mono, int32_t* const* d_match,
+                           int32_t* const* d_n_matches, char* scratch, size_t stride, void* d_args, void* h_args,
+                           size_t args_cap, void* stream);
+int orbgpu_sbp_local_batch(orb_matcher_t m, int B, const orb_frame_device_t* const* F, const uint8_t* const* d_frame_taken,
+                           const orb_local_points_device_t* const* pts, float th, int far_points, float th_far_points,
+                           int32_t* const* d_match, int32_t* const* d_n_matches, char* scratch, size_t stride,
+                           void* d_args, void* h_args, size_t args_cap, void* stream);
+int orbgpu_frustum_chain_batch(int B, const orb_tracking_chain_frame_t* fr, const double* d_poses, float viewing_cos_limit,
+                               void* d_args, void* h_args, size_t args_cap, void* stream);
+
 // REGISTER_TIMES brackets (csrc/orb_timers.hip): StageTimer t("LBA") records the scope's wall time
 // under that name when the timers are on.
 namespace orbgpu {

@@ -287,3 +287,120 @@ class TrackingChain:
                                             ctypes.c_void_p(st.cuda_stream)),
               "orb_tracking_chain_device")
         return TrackResult(self, st)
+
+
+class TrackingChainFrame(ctypes.Structure):  # orb_tracking_chain_frame_t
+    _fields_ = [("frame", ctypes.c_void_p), ("last", ctypes.c_void_p), ("local", ctypes.c_void_p),
+                ("pos", ctypes.c_void_p), ("normal", ctypes.c_void_p), ("min_dist", ctypes.c_void_p),
+                ("max_dist", ctypes.c_void_p), ("last_row", ctypes.c_void_p), ("frustum", ctypes.c_void_p),
+                ("inv_level_sigma2", ctypes.c_void_p), ("pose7", ctypes.c_double * 7)]
+
+
+class TrackingChainBatchBuffers(ctypes.Structure):  # orb_tracking_chain_batch_buffers_t
+    _fields_ = TrackingChainBuffers._fields_
+
+
+class BatchTrackResult:
+    """Device outputs of one TrackingChainBatch.track call: sync() returns one TrackResult-style dict
+    per frame."""
+
+    def __init__(self, chain, stream, nb):
+        self.chain, self.stream, self.nb = chain, stream, nb
+
+    def sync(self) -> list:
+        c, B = self.chain, self.nb
+        self.stream.synchronize()
+        # the per-graph arrays are laid out 2 x (frames of the call)
+        fr = c.frames.cpu().numpy().view(POSE_FRAME_DTYPE)[:2 * B].reshape(2, B)
+        m1, m2 = c.m1.cpu().numpy(), c.m2.cpu().numpy()
+        nm, no = c.n_match.cpu().numpy(), c.n_out.cpu().numpy()
+        poses = c.poses.cpu().numpy().reshape(-1)[:14 * B].reshape(2, B, 7)
+        inl = c.inliers.cpu().numpy().reshape(-1)[:2 * B].reshape(2, B)
+        edges = [c.edges[k].cpu().numpy() for k in (0, 1)]
+        ekp = [c.edge_kp[k].cpu().numpy() for k in (0, 1)]
+        outl = [c.outlier[k].cpu().numpy() for k in (0, 1)]
+        out = []
+        for b in range(B):
+            d = dict(frames=fr[:, b].copy(), n1=int(nm[b, 0]), n2=int(nm[b, 1]), m1=m1[b], m2=m2[b], pose1=poses[0, b],
+                     pose2=poses[1, b], inliers=inl[:, b].copy(), n_kept=int(no[b, 0]), n_map=int(no[b, 1]))
+            for k in (0, 1):
+                ne = int(fr[k, b]["n_edges"])
+                d[f"edges{k + 1}"] = edges[k][b, :ne].view(POSE_EDGE_DTYPE).reshape(-1)
+                d[f"edge_kp{k + 1}"] = ekp[k][b, :ne]
+                d[f"outlier{k + 1}"] = outl[k][b, :ne].astype(bool)
+            out.append(d)
+        return out
+
+
+class TrackingChainBatch:
+    """TrackWithMotionModel -> TrackLocalMap for up to B frames in one call
+    (orb_tracking_chain_batch_device): every stage is one launch over the batch, frame b's results are
+    the single chain's.  All frames of a call share `cap`; per frame its own last frame, local map and
+    motion-model pose.  Parameters as TrackingChain."""
+
+    def __init__(self, cap: int, B: int, device=None, th_motion: float = 7, th_local: float = 1, mono: bool = False,
+                 far_points: bool = False, th_far_points: float = 20.0, viewing_cos_limit: float = 0.5,
+                 scale_factor: float = 1.2):
+        import torch
+        self.device = torch.device(device if device is not None else "cuda")
+        self.cap, self.B = int(cap), int(B)
+        self.th_motion, self.th_local, self.mono = float(th_motion), float(th_local), bool(mono)
+        self.scale_factor = float(scale_factor)
+        self.m_motion = ORBmatcher(0.9, True)
+        self.m_local = ORBmatcher(0.8, True)
+        d, c, B = self.device, self.cap, self.B
+        self.m1 = torch.empty((B, c), dtype=torch.int32, device=d)
+        self.m2 = torch.empty((B, c), dtype=torch.int32, device=d)
+        self.n_match = torch.zeros((B, 2), dtype=torch.int32, device=d)
+        self.frames = torch.zeros(2 * B * POSE_FRAME_DTYPE.itemsize, dtype=torch.uint8, device=d)
+        self.edges = [torch.empty((B, c, POSE_EDGE_DTYPE.itemsize), dtype=torch.uint8, device=d) for _ in range(2)]
+        self.edge_kp = [torch.empty((B, c), dtype=torch.int32, device=d) for _ in range(2)]
+        self.outlier = [torch.empty((B, c), dtype=torch.uint8, device=d) for _ in range(2)]
+        self.poses = torch.zeros((2, B, 7), dtype=torch.float64, device=d)
+        self.inliers = torch.zeros((2, B), dtype=torch.int32, device=d)
+        self.n_out = torch.zeros((B, 2), dtype=torch.int32, device=d)
+        self.taken = torch.empty((B, c), dtype=torch.uint8, device=d)
+        self._scratch = torch.empty(0, dtype=torch.uint8, device=d)
+        self._retired = []
+        self._h_motion, self._h_local = self.m_motion._handle(), self.m_local._handle()
+        self._params = TrackingChainParams(self.th_motion, int(self.mono), self.th_local, int(far_points),
+                                           float(th_far_points), float(viewing_cos_limit))
+        self._bufs = TrackingChainBatchBuffers(
+            self.m1.data_ptr(), self.m2.data_ptr(), self.n_match.data_ptr(), self.frames.data_ptr(),
+            self.edges[0].data_ptr(), self.edges[1].data_ptr(), self.edge_kp[0].data_ptr(),
+            self.edge_kp[1].data_ptr(), self.outlier[0].data_ptr(), self.outlier[1].data_ptr(),
+            self.poses.data_ptr(), self.inliers.data_ptr(), self.n_out.data_ptr(), self.taken.data_ptr(), None)
+
+    def track(self, items, stream=None, wide: bool = False) -> BatchTrackResult:
+        """items: up to B tuples (cur DeviceFrame, DeviceLastPoints, DeviceLocalMap, pose7)."""
+        import torch
+        nb = len(items)
+        if not 0 < nb <= self.B:
+            raise ValueError(f"{nb} frames for a batch of {self.B}")
+        lib = _lib.load()
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        arr = (TrackingChainFrame * nb)()
+        keep = []
+        last_cap = n_local = 0
+        for b, (cur, last, local, pose7) in enumerate(items):
+            if cur.cap != self.cap:
+                raise ValueError(f"frame capacity {cur.cap} differs from the batch's {self.cap}")
+            fv, lv, mv, ff = cur.view(), last.view(), local.view(), cur.frustum_frame(self.scale_factor)
+            keep += [fv, lv, mv, ff]
+            lr = local.last_row
+            arr[b] = TrackingChainFrame(ctypes.addressof(fv), ctypes.addressof(lv), ctypes.addressof(mv),
+                                        local.pos.data_ptr(), local.normal.data_ptr(), local.min_dist.data_ptr(),
+                                        local.max_dist.data_ptr(), None if lr is None else lr.data_ptr(),
+                                        ctypes.addressof(ff), cur.mvInvLevelSigma2.ctypes.data,
+                                        (ctypes.c_double * 7)(*np.asarray(pose7, np.float64).reshape(7)))
+            last_cap, n_local = max(last_cap, last.cap), max(n_local, local.n)
+        need = int(lib.orb_tracking_chain_batch_scratch_bytes(self.B, self.cap, last_cap, n_local))
+        if need > self._scratch.numel():
+            self._retired.append(self._scratch)
+            self._scratch = torch.empty(need, dtype=torch.uint8, device=self.device)
+            self._bufs.scratch = self._scratch.data_ptr()
+        self._params.th_motion = self.th_motion * (2 if wide else 1)
+        check(lib.orb_tracking_chain_batch_device(self._h_motion, self._h_local, nb, arr, ctypes.byref(self._params),
+                                                  ctypes.byref(self._bufs), ctypes.c_void_p(st.cuda_stream)),
+              "orb_tracking_chain_batch_device")
+        return BatchTrackResult(self, st, nb)

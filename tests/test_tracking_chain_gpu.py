@@ -15,7 +15,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _device(pkg, sc, C, L):
+def _device(pkg, sc, C, L, cap=None):
     import torch
     dev = torch.device("cuda")
 
@@ -25,13 +25,15 @@ def _device(pkg, sc, C, L):
     def dframe(F, pad=37):
         # capacity past the count, filled with junk keypoints the chain must not read
         rng = np.random.default_rng(F.N)
-        cap = F.N + pad
+        if cap is not None:
+            pad = cap - F.N
+        cap_f = F.N + pad
         k = np.concatenate([F.mvKeysUn, F.mvKeysUn[rng.integers(0, F.N, pad)]])
         d = np.concatenate([F.mDescriptors, rng.integers(0, 256, (pad, 32), dtype=np.uint8)])
-        kps = up(k.view(np.float32).reshape(1, cap, 7), np.float32)
-        desc = up(d.reshape(1, cap, 32), np.uint8)
+        kps = up(k.view(np.float32).reshape(1, cap_f, 7), np.float32)
+        desc = up(d.reshape(1, cap_f, 32), np.uint8)
         counts = up(np.array([[F.N, 0]]), np.int32)
-        ur = None if F.mvuRight is None else up(np.concatenate([F.mvuRight, np.full(pad, 100, np.float32)]).reshape(1, cap),
+        ur = None if F.mvuRight is None else up(np.concatenate([F.mvuRight, np.full(pad, 100, np.float32)]).reshape(1, cap_f),
                                                 np.float32)
         return pkg.DeviceFrame(kps, desc, counts, 0, F.Tcw, sc["cur"]["camera"], F.mvScaleFactors, sc["level_sigma2"],
                                int(F.mnMaxX), int(F.mnMaxY), F.mbf, ur)
@@ -124,3 +126,33 @@ def test_tracking_chain_reuse_and_no_local_map(pkg, oracle, synth):
     r = chain.track(cur, last, empty, sc["pose7_pred"]).sync()
     assert r["n2"] == 0 and (r["m2"][:cur.cap] == -1).all()
     assert r["n1"] > 100 and len(r["edges2"]) == r["n_kept"]
+
+
+@pytest.mark.parametrize("stereo,seeds", [(True, (81, 82, 84)), (False, (83, 86))])
+def test_tracking_chain_batch_equals_single(pkg, synth, stereo, seeds):
+    """orb_tracking_chain_batch_device: one launch per stage over the frames (a batch with a free slot);
+    every frame's outputs equal the single chain's on the same inputs, bit for bit (poses included)."""
+    scenes = [synth.tracking_chain_scene(seed=s, stereo=stereo) for s in seeds]
+    fr = [_frames(pkg, sc) for sc in scenes]
+    cap = max(max(C.N, L.N) for C, L in fr) + 37
+    devs = [_device(pkg, sc, C, L, cap=cap) for sc, (C, L) in zip(scenes, fr)]
+    th = 7 if stereo else 15
+    single = []
+    for sc, (cur, last, local) in zip(scenes, devs):
+        ch = pkg.TrackingChain(cap, th_motion=th, th_local=1)
+        single.append(ch.track(cur, last, local, sc["pose7_pred"]).sync())
+    batch = pkg.TrackingChainBatch(cap, len(seeds) + 1, th_motion=th, th_local=1)
+    res = batch.track([(cur, last, local, sc["pose7_pred"]) for sc, (cur, last, local) in zip(scenes, devs)]).sync()
+    assert len(res) == len(seeds)
+    for r, o in zip(res, single):
+        for k in ("n1", "n2", "n_kept", "n_map"):
+            assert r[k] == o[k], k
+        for k in ("m1", "m2", "edge_kp1", "edge_kp2", "outlier1", "outlier2", "inliers"):
+            assert np.array_equal(np.asarray(r[k]), np.asarray(o[k])), k
+        for k in ("edges1", "edges2"):
+            assert np.array_equal(r[k].view(np.uint8), o[k].view(np.uint8)), k
+        assert np.array_equal(r["pose1"], o["pose1"]) and np.array_equal(r["pose2"], o["pose2"])
+        for k in (0, 1):  # the graphs' frame records, but for the batch's edge offset
+            for f in ("pose", "n_edges"):
+                assert np.array_equal(r["frames"][k][f], o["frames"][k][f]), f
+        assert o["n1"] > 100 and o["n2"] > 0

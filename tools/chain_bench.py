@@ -11,7 +11,10 @@ import torch  # noqa: E402
 from orbslam3_amd import synth  # noqa: E402
 
 cpu = "--cpu" in sys.argv
-out = bench.bench_tracking_chain(pkg, synth, torch.device("cuda:0"), 20, cpu)
+import os  # noqa: E402
+ns = int(os.environ.get("ORB_CHAIN_STREAMS", "4"))
+nb = int(os.environ.get("ORB_CHAIN_BATCH", "32"))
+out = bench.bench_tracking_chain(pkg, synth, torch.device("cuda:0"), 20, cpu, batch=nb, n_streams=ns)
 print(json.dumps(out, indent=1))
 if "--pose" in sys.argv:
     print(json.dumps(bench.bench_pose(pkg, synth, torch.device("cuda:0"), 20, cpu), indent=1))
