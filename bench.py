@@ -680,9 +680,10 @@ def bench_matchers(pkg, synth, dev, steps, cpu_baseline_on):
     return out
 
 
-def _chain_inputs(pkg, synth, dev, seed):
+def _chain_inputs(pkg, synth, dev, seed, cap=None):
     """One tracking-chain frame (synth.tracking_chain_scene) as device tables: the current frame, the
-    last frame's map points and the local map; plus the host Frames for the oracle."""
+    last frame's map points and the local map; plus the host Frames for the oracle.  cap: the frames'
+    capacity (rows past N zero, never read), default N."""
     import numpy as np
     import torch
     sc = synth.tracking_chain_scene(seed=seed)
@@ -691,16 +692,21 @@ def _chain_inputs(pkg, synth, dev, seed):
     def up(a, dt):
         return torch.from_numpy(np.ascontiguousarray(a, dt)).to(dev)
 
+    def pad(a, c):
+        return np.concatenate([a, np.zeros((c - len(a),) + a.shape[1:], a.dtype)])
+
     def dframe(F):
-        ur = None if F.mvuRight is None else up(F.mvuRight.reshape(1, F.N), np.float32)
-        return pkg.DeviceFrame(up(F.mvKeysUn.view(np.float32).reshape(1, F.N, 7), np.float32),
-                               up(F.mDescriptors.reshape(1, F.N, 32), np.uint8), up(np.array([[F.N, 0]]), np.int32), 0,
+        c = F.N if cap is None else cap
+        ur = None if F.mvuRight is None else up(pad(F.mvuRight, c).reshape(1, c), np.float32)
+        return pkg.DeviceFrame(up(pad(F.mvKeysUn, c).view(np.float32).reshape(1, c, 7), np.float32),
+                               up(pad(F.mDescriptors, c).reshape(1, c, 32), np.uint8), up(np.array([[F.N, 0]]), np.int32), 0,
                                F.Tcw, sc["cur"]["camera"], F.mvScaleFactors, sc["level_sigma2"], int(F.mnMaxX),
                                int(F.mnMaxY), F.mbf, ur)
     cur, lastf = dframe(C), dframe(L)
     mp = L.map_points
-    last = pkg.DeviceLastPoints(lastf, up(mp["valid"], np.uint8), up(mp["observed"], np.uint8),
-                                up(mp["xyz"], np.float32), up(mp["desc"], np.uint8))
+    cl = L.N if cap is None else cap
+    last = pkg.DeviceLastPoints(lastf, up(pad(mp["valid"], cl), np.uint8), up(pad(mp["observed"], cl), np.uint8),
+                                up(pad(mp["xyz"], cl), np.float32), up(pad(mp["desc"], cl), np.uint8))
     local = pkg.DeviceLocalMap.from_host(dev, **sc["local"])
     return sc, C, L, cur, last, local
 
@@ -753,12 +759,32 @@ def bench_tracking_chain(pkg, synth, dev, steps, cpu_baseline_on, n_scenes=8, ba
         batched()
     torch.cuda.synchronize(dev)
     bdt = (time.perf_counter() - t0) * 1e3
+    # the batch API (orb_tracking_chain_batch_device): nb frames per call, one launch per stage for the
+    # whole batch; every slot its own local map (the chain writes its tracking fields), frames shared
+    nb, capb = 128, 2048
+    sb = [_chain_inputs(pkg, synth, dev, 4400 + s, cap=capb) for s in range(n_scenes)]
+    locs = [pkg.DeviceLocalMap.from_host(dev, **sb[b % n_scenes][0]["local"]) for b in range(nb)]
+    items = [(sb[b % n_scenes][3], sb[b % n_scenes][4], locs[b], sb[b % n_scenes][0]["pose7_pred"]) for b in range(nb)]
+    chb = pkg.TrackingChainBatch(capb, nb, device=dev, th_motion=7, th_local=1)
+    for _ in range(2):
+        chb.track(items, stream=st)
+    st.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(brep):
+        chb.track(items, stream=st)
+    st.synchronize()
+    bat_ms = (time.perf_counter() - t0) * 1e3 / brep
+    res0 = chb.track(items[:1], stream=st).sync()[0]  # slot 0 is scene 0: the single chain's answer
+    assert res0["n1"] == n1 and res0["n2"] == n2, "batch API disagrees with the single chain"
     out = {"config": f"TrackWithMotionModel -> TrackLocalMap on one frame: {C.N} keypoints (stereo), last frame "
                      f"{L.N} keypoints / {int(L.map_points['valid'].sum())} map points, {len(sc['local']['pos'])} local "
                      f"map points; th 7 / 1, ORBmatcher(0.9, true) / (0.8); device-resident, one GPU",
            "single_frame_ms": round(float(np.median(lat)), 4), "single_frame_gpu_ms": round(float(np.median(gpu)), 4),
            "single_frame_enqueue_ms": round(float(np.median(enq)), 4),
            "batched_frames_per_ms": round(batch * brep / bdt, 4), "batch": batch, "streams": n_streams,
+           "batch_api": {"frames_per_call": nb, "ms_per_call": round(bat_ms, 4), "frames_per_ms": round(nb / bat_ms, 3),
+                         "note": "orb_tracking_chain_batch_device: one launch per stage for the whole batch, one "
+                                 "stream; frames padded to cap 2048; 8 scenes repeated, a local map per slot"},
            "matches_last_frame": n1, "matches_local_map": n2, "dtype": "u8 / f32 / f64"}
     if cpu_baseline_on:
         from oracle import tracking_chain as oracle_chain
