@@ -761,7 +761,7 @@ def bench_tracking_chain(pkg, synth, dev, steps, cpu_baseline_on, n_scenes=8, ba
     bdt = (time.perf_counter() - t0) * 1e3
     # the batch API (orb_tracking_chain_batch_device): nb frames per call, one launch per stage for the
     # whole batch; every slot its own local map (the chain writes its tracking fields), frames shared
-    nb, capb = 128, 2048
+    nb, capb = int(os.environ.get("ORB_CHAIN_NB", "256")), 2048
     sb = [_chain_inputs(pkg, synth, dev, 4400 + s, cap=capb) for s in range(n_scenes)]
     locs = [pkg.DeviceLocalMap.from_host(dev, **sb[b % n_scenes][0]["local"]) for b in range(nb)]
     items = [(sb[b % n_scenes][3], sb[b % n_scenes][4], locs[b], sb[b % n_scenes][0]["pose7_pred"]) for b in range(nb)]
