@@ -15,14 +15,14 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _device(pkg, sc, C, L, cap=None):
+def _device(pkg, sc, C, L, cap=None, last_cap=None, local=None):
     import torch
     dev = torch.device("cuda")
 
     def up(a, dt):
         return torch.from_numpy(np.ascontiguousarray(a, dt)).to(dev)
 
-    def dframe(F, pad=37):
+    def dframe(F, pad=37, cap=None):
         # capacity past the count, filled with junk keypoints the chain must not read
         rng = np.random.default_rng(F.N)
         if cap is not None:
@@ -38,7 +38,7 @@ def _device(pkg, sc, C, L, cap=None):
         return pkg.DeviceFrame(kps, desc, counts, 0, F.Tcw, sc["cur"]["camera"], F.mvScaleFactors, sc["level_sigma2"],
                                int(F.mnMaxX), int(F.mnMaxY), F.mbf, ur)
 
-    cur, last = dframe(C), dframe(L)
+    cur, last = dframe(C, cap=cap), dframe(L, cap=last_cap if last_cap is not None else cap)
     mp = L.map_points
     pad = last.cap - L.N
 
@@ -46,7 +46,7 @@ def _device(pkg, sc, C, L, cap=None):
         return np.concatenate([a, np.full((pad,) + a.shape[1:], v, a.dtype)])
     lastp = pkg.DeviceLastPoints(last, up(padded(mp["valid"], 1), np.uint8), up(padded(mp["observed"], 1), np.uint8),
                                  up(padded(mp["xyz"], 1.0), np.float32), up(padded(mp["desc"], 0), np.uint8))
-    local = pkg.DeviceLocalMap.from_host(dev, **sc["local"])
+    local = pkg.DeviceLocalMap.from_host(dev, **(sc["local"] if local is None else local))
     return cur, lastp, local
 
 
@@ -156,3 +156,30 @@ def test_tracking_chain_batch_equals_single(pkg, synth, stereo, seeds):
             for f in ("pose", "n_edges"):
                 assert np.array_equal(r["frames"][k][f], o["frames"][k][f]), f
         assert o["n1"] > 100 and o["n2"] > 0
+
+
+def test_tracking_chain_batch_ragged(pkg, synth):
+    """A batch whose frames differ in everything but cap: last-frame capacities, local map sizes (full,
+    truncated, empty) and a local map without the last-frame links; grids sized for the largest frame
+    must leave the others' results as their single chains give them."""
+    specs = [(81, None, 5, True), (82, 700, 60, True), (84, 0, 0, True), (85, 1200, 17, False)]
+    scenes = [synth.tracking_chain_scene(seed=s) for s, _, _, _ in specs]
+    fr = [_frames(pkg, sc) for sc in scenes]
+    cap = max(C.N for C, _ in fr) + 11
+    devs = []
+    for (seed, nloc, lpad, links), sc, (C, L) in zip(specs, scenes, fr):
+        loc = {k: (v if nloc is None else v[:nloc]) for k, v in sc["local"].items() if links or k != "last_row"}
+        devs.append(_device(pkg, sc, C, L, cap=cap, last_cap=L.N + lpad, local=loc))
+    single = []
+    for sc, (cur, last, local) in zip(scenes, devs):
+        single.append(pkg.TrackingChain(cap).track(cur, last, local, sc["pose7_pred"]).sync())
+    res = pkg.TrackingChainBatch(cap, len(specs)).track(
+        [(cur, last, local, sc["pose7_pred"]) for sc, (cur, last, local) in zip(scenes, devs)]).sync()
+    for (seed, nloc, _, _), r, o in zip(specs, res, single):
+        for k in ("n1", "n2", "n_kept", "n_map"):
+            assert r[k] == o[k], (seed, k)
+        for k in ("m1", "m2", "edge_kp1", "edge_kp2", "outlier1", "outlier2", "inliers"):
+            assert np.array_equal(np.asarray(r[k]), np.asarray(o[k])), (seed, k)
+        assert np.array_equal(r["pose1"], o["pose1"]) and np.array_equal(r["pose2"], o["pose2"]), seed
+        if nloc == 0:
+            assert r["n2"] == 0
