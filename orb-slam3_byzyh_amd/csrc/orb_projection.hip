@@ -21,6 +21,7 @@
 #include <cstdint>
 #include <cstring>
 #include <vector>
+#include <cstdlib>
 
 #include "orbgpu.h"
 #include "orbgpu_internal.h"
@@ -222,6 +223,111 @@ __global__ __launch_bounds__(64 * kCandWaves) void k_proj_candidates_b(const k_p
     k_proj_candidates_body(A.P, A.n_dev, A.valid, A.xyz, A.mp_desc, A.last_octave, A.cur_kp, A.cur_ur, A.cur_desc, A.cell_off, A.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.lister);
 }
 
+// The same candidate lists with one THREAD per point (round 5): a window holds a handful of cells and
+// keypoints, so a wave per point spent most of its time on the 64-lane prefix and compaction machinery;
+// a thread walks its window's cells (ix outer, iy inner) and their keypoints in index order, which is
+// window_candidates' order, and writes the same list.
+template <class Test>
+__device__ __forceinline__ int window_candidates_serial(const int32_t* __restrict__ cell_off,
+                                                        const int32_t* __restrict__ cell_idx, int x0, int x1, int y0,
+                                                        int y1, Cand* __restrict__ out, int cap, Test test) {
+    int n = 0;
+    for (int ix = x0; ix <= x1; ++ix)
+        for (int iy = y0; iy <= y1; ++iy) {
+            const int cell = ix * kGridRows + iy;
+            const int b = cell_off[cell], e = cell_off[cell + 1];
+            for (int k = b; k < e; ++k) {
+                const int j = cell_idx[k];
+                const int dist = test(j);
+                if (dist >= 0) {
+                    if (n < cap) out[n] = Cand{j, dist};
+                    ++n;
+                }
+            }
+        }
+    return n;
+}
+__device__ __forceinline__ void record_listers_serial(int i, int n, int cap, const Cand* __restrict__ c_i,
+                                                      const uint8_t* __restrict__ taken0, int32_t* __restrict__ lister) {
+    if (n > cap) return;  // overflow: the call is redone with a larger capacity
+    for (int k = 0; k < n; ++k) {
+        const Cand c = c_i[k];
+        if (c.dist < 256 && !(taken0 && taken0[c.i2])) atomicMin(&lister[c.i2], i);
+    }
+}
+
+constexpr int kCandThreads = 256;
+
+__device__ __forceinline__ void k_proj_candidates_t_body(const ProjParams P, const int32_t* __restrict__ n_dev,
+                                                         const uint8_t* __restrict__ valid,
+                                                         const float* __restrict__ xyz, const uint4* __restrict__ mp_desc,
+                                                         const int32_t* __restrict__ last_octave,
+                                                         const float4* __restrict__ cur_kp,
+                                                         const float* __restrict__ cur_ur, const uint4* __restrict__ cur_desc,
+                                                         const int32_t* __restrict__ cell_off, const int32_t* __restrict__ cell_idx,
+                                                         Cand* __restrict__ cands, int32_t* __restrict__ ncand,
+                                                         int32_t* __restrict__ overflow, const uint8_t* __restrict__ observed,
+                                                         int32_t* __restrict__ lister) {
+    const int i = blockIdx.x * kCandThreads + threadIdx.x;
+    if (i >= (n_dev ? *n_dev : P.n_last)) return;
+    int n = 0;
+    Cand* const out = cands + (size_t)i * P.cap;
+    if (valid[i]) {
+        const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+        float c[3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+            c[r] = __fmaf_rn(P.Tcw[4 * r + 2], z, __fmaf_rn(P.Tcw[4 * r], x, P.Tcw[4 * r + 1] * y)) + P.Tcw[4 * r + 3];
+        const float invzc = (float)(1.0 / (double)c[2]);
+        const float u = P.fx * c[0] / c[2] + P.cx;
+        const float v = P.fy * c[1] / c[2] + P.cy;
+        if (!(invzc < 0) && !(u < P.min_x || u > P.max_x || v < P.min_y || v > P.max_y)) {
+            const int oct = last_octave[i];
+            const float radius = P.th * P.scale[oct];
+            int minLevel, maxLevel;
+            if (P.bForward) { minLevel = oct; maxLevel = -1; }
+            else if (P.bBackward) { minLevel = 0; maxLevel = oct; }
+            else { minLevel = oct - 1; maxLevel = oct + 1; }
+            const int x0 = max(0, (int)floorf((u - P.min_x - radius) * P.inv_w));
+            const int x1 = min(kGridCols - 1, (int)ceilf((u - P.min_x + radius) * P.inv_w));
+            const int y0 = max(0, (int)floorf((v - P.min_y - radius) * P.inv_h));
+            const int y1 = min(kGridRows - 1, (int)ceilf((v - P.min_y + radius) * P.inv_h));
+            if (x0 < kGridCols && x1 >= 0 && y0 < kGridRows && y1 >= 0) {
+                const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+                const uint4 d0 = mp_desc[2 * (size_t)i], d1 = mp_desc[2 * (size_t)i + 1];
+                const float ur = __fmaf_rn(-P.bf, invzc, u);
+                n = window_candidates_serial(cell_off, cell_idx, x0, x1, y0, y1, out, P.cap, [&](int j) -> int {
+                    const float4 kp = cur_kp[j];
+                    const int koct = __float_as_int(kp.w);
+                    if (bCheckLevels) {
+                        if (koct < minLevel) return -1;
+                        if (maxLevel >= 0 && koct > maxLevel) return -1;
+                    }
+                    const float distx = kp.x - u, disty = kp.y - v;
+                    if (!(fabsf(distx) < radius && fabsf(disty) < radius)) return -1;
+                    if (P.has_ur && cur_ur[j] > 0) {
+                        const float er = fabsf(ur - cur_ur[j]);
+                        if (er > radius) return -1;
+                    }
+                    return hamming(d0, d1, cur_desc[2 * (size_t)j], cur_desc[2 * (size_t)j + 1]);
+                });
+            }
+        }
+    }
+    ncand[i] = n;
+    if (n > P.cap) atomicMax(overflow, n);
+    if (observed[i]) record_listers_serial(i, n, P.cap, out, nullptr, lister);
+}
+__global__ __launch_bounds__(kCandThreads) void k_proj_candidates_t(const k_proj_candidates_args A) {
+    k_proj_candidates_t_body(A.P, A.n_dev, A.valid, A.xyz, A.mp_desc, A.last_octave, A.cur_kp, A.cur_ur, A.cur_desc,
+                             A.cell_off, A.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.lister);
+}
+__global__ __launch_bounds__(kCandThreads) void k_proj_candidates_t_b(const k_proj_candidates_args* __restrict__ a) {
+    const k_proj_candidates_args& A = a[blockIdx.y];
+    k_proj_candidates_t_body(A.P, A.n_dev, A.valid, A.xyz, A.mp_desc, A.last_octave, A.cur_kp, A.cur_ur, A.cur_desc,
+                             A.cell_off, A.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.lister);
+}
+
 __device__ __forceinline__ int rot_bin(float a1, float a2) {
     float rot = a1 - a2;
     if ((double)rot < 0.0) rot += 360.0f;
@@ -330,6 +436,66 @@ struct k_lmp_candidates_args {
 __global__ __launch_bounds__(64 * kCandWaves) void k_lmp_candidates_b(const k_lmp_candidates_args* __restrict__ a) {
     const k_lmp_candidates_args& A = a[blockIdx.y];
     k_lmp_candidates_body(A.P, A.in_view, A.bad, A.proj, A.view_cos, A.depth, A.level, A.mp_desc, A.cur_kp, A.cur_ur, A.cur_desc, A.cell_off, A.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.taken0, A.lister);
+}
+
+__device__ __forceinline__ void k_lmp_candidates_t_body(const LocalParams P, const uint8_t* __restrict__ in_view,
+                                                        const uint8_t* __restrict__ bad, const float* __restrict__ proj,
+                                                        const float* __restrict__ view_cos, const float* __restrict__ depth,
+                                                        const int32_t* __restrict__ level, const uint4* __restrict__ mp_desc,
+                                                        const float4* __restrict__ cur_kp, const float* __restrict__ cur_ur,
+                                                        const uint4* __restrict__ cur_desc, const int32_t* __restrict__ cell_off,
+                                                        const int32_t* __restrict__ cell_idx, Cand* __restrict__ cands,
+                                                        int32_t* __restrict__ ncand, int32_t* __restrict__ overflow,
+                                                        const uint8_t* __restrict__ observed, const uint8_t* __restrict__ taken0,
+                                                        int32_t* __restrict__ lister) {
+    const int i = blockIdx.x * kCandThreads + threadIdx.x;
+    if (i >= P.n_pts) return;
+    int n = 0;
+    Cand* const out = cands + (size_t)i * P.cap;
+    if (in_view[i] && !(P.far && depth[i] > P.th_far) && !bad[i]) {
+        const int lvl = level[i];
+        float r = ((double)view_cos[i] > 0.998) ? 2.5f : 4.0f;  // RadiusByViewingCos (src:243-250)
+        if (P.th != 1.0f) r *= P.th;
+        const float radius = r * P.scale[lvl];
+        const float x = proj[3 * i], y = proj[3 * i + 1], xr = proj[3 * i + 2];
+        const int minLevel = lvl - 1, maxLevel = lvl;
+        const int x0 = max(0, (int)floorf((x - P.min_x - radius) * P.inv_w));
+        const int x1 = min(kGridCols - 1, (int)ceilf((x - P.min_x + radius) * P.inv_w));
+        const int y0 = max(0, (int)floorf((y - P.min_y - radius) * P.inv_h));
+        const int y1 = min(kGridRows - 1, (int)ceilf((y - P.min_y + radius) * P.inv_h));
+        if (x0 < kGridCols && x1 >= 0 && y0 < kGridRows && y1 >= 0) {
+            const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+            const uint4 d0 = mp_desc[2 * (size_t)i], d1 = mp_desc[2 * (size_t)i + 1];
+            n = window_candidates_serial(cell_off, cell_idx, x0, x1, y0, y1, out, P.cap, [&](int j) -> int {
+                const float4 kp = cur_kp[j];
+                const int koct = __float_as_int(kp.w);
+                if (bCheckLevels) {
+                    if (koct < minLevel) return -1;
+                    if (maxLevel >= 0 && koct > maxLevel) return -1;
+                }
+                if (!(fabsf(kp.x - x) < radius && fabsf(kp.y - y) < radius)) return -1;
+                if (P.has_ur && cur_ur[j] > 0) {
+                    const float er = fabsf(xr - cur_ur[j]);
+                    if (er > r * P.scale[lvl]) return -1;
+                }
+                return hamming(d0, d1, cur_desc[2 * (size_t)j], cur_desc[2 * (size_t)j + 1]);
+            });
+        }
+    }
+    ncand[i] = n;
+    if (n > P.cap) atomicMax(overflow, n);
+    if (observed[i]) record_listers_serial(i, n, P.cap, out, taken0, lister);
+}
+__global__ __launch_bounds__(kCandThreads) void k_lmp_candidates_t(const k_lmp_candidates_args A) {
+    k_lmp_candidates_t_body(A.P, A.in_view, A.bad, A.proj, A.view_cos, A.depth, A.level, A.mp_desc, A.cur_kp, A.cur_ur,
+                            A.cur_desc, A.cell_off, A.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.taken0,
+                            A.lister);
+}
+__global__ __launch_bounds__(kCandThreads) void k_lmp_candidates_t_b(const k_lmp_candidates_args* __restrict__ a) {
+    const k_lmp_candidates_args& A = a[blockIdx.y];
+    k_lmp_candidates_t_body(A.P, A.in_view, A.bad, A.proj, A.view_cos, A.depth, A.level, A.mp_desc, A.cur_kp, A.cur_ur,
+                            A.cur_desc, A.cell_off, A.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.taken0,
+                            A.lister);
 }
 
 // ---- the in-order assignment, resolved by parallel fixed-point rounds ----------------------------
@@ -922,6 +1088,19 @@ bool resolve_lds_ready() {
     return ok;
 }
 
+// Device forms' candidate pass: one wave per point or one thread per point; both write the same lists.
+// A single frame's few thousand points leave the chip mostly idle, and a wave's parallel window scan
+// has the shorter latency (0.51 vs 0.65 ms per tracked frame); a batch fills the chip, and threads
+// carry far less per-point machinery (256 frames: 3.2 -> 1.5 ms per call).  ORBGPU_CAND_MODE=wave /
+// thread forces one form everywhere (A/B).
+bool cand_thread_mode(bool batch) {
+    static const int forced = [] {
+        const char* c = getenv("ORBGPU_CAND_MODE");
+        return !c ? -1 : strcmp(c, "thread") == 0 ? 1 : strcmp(c, "wave") == 0 ? 0 : -1;
+    }();
+    return forced >= 0 ? forced == 1 : batch;
+}
+
 }  // namespace
 
 // Defined in orb_triangulation.hip: the matcher handle's staging buffers and ratio.
@@ -1374,9 +1553,12 @@ int orbgpu_sbp_frame_device_scratch(orb_matcher_t m, const orb_frame_device_t* c
         hipLaunchKernelGGL(k_last_prep, dim3((NL + 255) / 256), dim3(256), 0, s, lp.kps, lp.valid, lp.n_ptr, lp.cap,
                            lp.nlevels, lp.valid2, lp.octave, lp.angle, lp.n_out0, lp.n_out1);
         const k_proj_candidates_args& c = pl.cand;
-        hipLaunchKernelGGL(k_proj_candidates, dim3((NL + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s,
-                           c.P, c.n_dev, c.valid, c.xyz, c.mp_desc, c.last_octave, c.cur_kp, c.cur_ur, c.cur_desc,
-                           c.cell_off, c.cell_idx, c.cands, c.ncand, c.overflow, c.observed, c.lister);
+        if (cand_thread_mode(false))
+            hipLaunchKernelGGL(k_proj_candidates_t, dim3((NL + kCandThreads - 1) / kCandThreads), dim3(kCandThreads), 0, s, c);
+        else
+            hipLaunchKernelGGL(k_proj_candidates, dim3((NL + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s,
+                               c.P, c.n_dev, c.valid, c.xyz, c.mp_desc, c.last_octave, c.cur_kp, c.cur_ur, c.cur_desc,
+                               c.cell_off, c.cell_idx, c.cands, c.ncand, c.overflow, c.observed, c.lister);
         hipLaunchKernelGGL(k_resolve_init, dim3((NL + 255) / 256), dim3(256), 0, s, pl.init.a);
     }
     hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), pl.rounds.a.lds_keypoints ? 8 * (size_t)C : 0, s,
@@ -1418,8 +1600,12 @@ int orbgpu_sbp_frame_batch(orb_matcher_t m, int B, const orb_frame_device_t* con
     hipLaunchKernelGGL(k_frame_prep_b, dim3(1, B), dim3(kPrepThreads), 0, s, (const k_frame_prep_args*)(d + o_fp));
     if (maxNL > 0) {  // grids sized for the largest frame; the kernels bound themselves by their own counts
         hipLaunchKernelGGL(k_last_prep_b, dim3((maxNL + 255) / 256, B), dim3(256), 0, s, (const k_last_prep_args*)(d + o_lp));
-        hipLaunchKernelGGL(k_proj_candidates_b, dim3((maxNL + kCandWaves - 1) / kCandWaves, B), dim3(64 * kCandWaves), 0, s,
-                           (const k_proj_candidates_args*)(d + o_ca));
+        if (cand_thread_mode(true))
+            hipLaunchKernelGGL(k_proj_candidates_t_b, dim3((maxNL + kCandThreads - 1) / kCandThreads, B), dim3(kCandThreads), 0,
+                               s, (const k_proj_candidates_args*)(d + o_ca));
+        else
+            hipLaunchKernelGGL(k_proj_candidates_b, dim3((maxNL + kCandWaves - 1) / kCandWaves, B), dim3(64 * kCandWaves), 0, s,
+                               (const k_proj_candidates_args*)(d + o_ca));
         hipLaunchKernelGGL(k_resolve_init_b, dim3((maxNL + 255) / 256, B), dim3(256), 0, s, (const k_resolve_init_args*)(d + o_ri));
     }
     hipLaunchKernelGGL(k_resolve_rounds_b, dim3(1, B), dim3(kResolveThreads), rr[0].a.lds_keypoints ? 8 * (size_t)C : 0, s,
@@ -1534,9 +1720,13 @@ int orbgpu_sbp_local_device_scratch(orb_matcher_t m, const orb_frame_device_t* F
         hipLaunchKernelGGL(k_local_prep, dim3((np + 255) / 256), dim3(256), 0, s, lp.in_view, lp.level, lp.n, lp.nlevels,
                            lp.in_view2);
         const k_lmp_candidates_args& c = pl.cand;
-        hipLaunchKernelGGL(k_lmp_candidates, dim3((np + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s,
-                           c.P, c.in_view, c.bad, c.proj, c.view_cos, c.depth, c.level, c.mp_desc, c.cur_kp, c.cur_ur,
-                           c.cur_desc, c.cell_off, c.cell_idx, c.cands, c.ncand, c.overflow, c.observed, c.taken0, c.lister);
+        if (cand_thread_mode(false))
+            hipLaunchKernelGGL(k_lmp_candidates_t, dim3((np + kCandThreads - 1) / kCandThreads), dim3(kCandThreads), 0, s, c);
+        else
+            hipLaunchKernelGGL(k_lmp_candidates, dim3((np + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s,
+                               c.P, c.in_view, c.bad, c.proj, c.view_cos, c.depth, c.level, c.mp_desc, c.cur_kp, c.cur_ur,
+                               c.cur_desc, c.cell_off, c.cell_idx, c.cands, c.ncand, c.overflow, c.observed, c.taken0,
+                               c.lister);
         hipLaunchKernelGGL(k_resolve_init, dim3((np + 255) / 256), dim3(256), 0, s, pl.init.a);
     }
     hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), pl.rounds.a.lds_keypoints ? 8 * (size_t)C : 0, s,
@@ -1580,8 +1770,12 @@ int orbgpu_sbp_local_batch(orb_matcher_t m, int B, const orb_frame_device_t* con
     hipLaunchKernelGGL(k_frame_prep_b, dim3(1, B), dim3(kPrepThreads), 0, s, (const k_frame_prep_args*)(d + o_fp));
     if (maxNp > 0) {
         hipLaunchKernelGGL(k_local_prep_b, dim3((maxNp + 255) / 256, B), dim3(256), 0, s, (const k_local_prep_args*)(d + o_lp));
-        hipLaunchKernelGGL(k_lmp_candidates_b, dim3((maxNp + kCandWaves - 1) / kCandWaves, B), dim3(64 * kCandWaves), 0, s,
-                           (const k_lmp_candidates_args*)(d + o_ca));
+        if (cand_thread_mode(true))
+            hipLaunchKernelGGL(k_lmp_candidates_t_b, dim3((maxNp + kCandThreads - 1) / kCandThreads, B), dim3(kCandThreads), 0,
+                               s, (const k_lmp_candidates_args*)(d + o_ca));
+        else
+            hipLaunchKernelGGL(k_lmp_candidates_b, dim3((maxNp + kCandWaves - 1) / kCandWaves, B), dim3(64 * kCandWaves), 0, s,
+                               (const k_lmp_candidates_args*)(d + o_ca));
         hipLaunchKernelGGL(k_resolve_init_b, dim3((maxNp + 255) / 256, B), dim3(256), 0, s, (const k_resolve_init_args*)(d + o_ri));
     }
     hipLaunchKernelGGL(k_resolve_rounds_b, dim3(1, B), dim3(kResolveThreads), rr[0].a.lds_keypoints ? 8 * (size_t)C : 0, s,
