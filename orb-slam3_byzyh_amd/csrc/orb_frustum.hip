@@ -94,7 +94,8 @@ __global__ __launch_bounds__(256) void k_is_in_frustum(orb_frustum_frame_t F, co
                                                        ScaleSteps steps, uint8_t* __restrict__ in_view, float* __restrict__ proj,
                                                        float* __restrict__ depth, int32_t* __restrict__ level,
                                                        float* __restrict__ view_cos) {
-    k_is_in_frustum_body(F, pose7, n, pos, normal, min_dist, max_dist, viewingCosLimit, steps, in_view, proj, depth, level, view_cos);
+    k_is_in_frustum_body(F, pose7, n, pos, normal, min_dist, max_dist, viewingCosLimit, steps, in_view, proj, depth,
+                         level, view_cos);
 }
 struct k_is_in_frustum_args {
     orb_frustum_frame_t F;
@@ -115,7 +116,8 @@ struct k_is_in_frustum_args {
 // the same on frame blockIdx.y of a batch (one argument block per frame)
 __global__ __launch_bounds__(256) void k_is_in_frustum_b(const k_is_in_frustum_args* __restrict__ a) {
     const k_is_in_frustum_args& A = a[blockIdx.y];
-    k_is_in_frustum_body(A.F, A.pose7, A.n, A.pos, A.normal, A.min_dist, A.max_dist, A.viewingCosLimit, A.steps, A.in_view, A.proj, A.depth, A.level, A.view_cos);
+    k_is_in_frustum_body(A.F, A.pose7, A.n, A.pos, A.normal, A.min_dist, A.max_dist, A.viewingCosLimit, A.steps,
+                         A.in_view, A.proj, A.depth, A.level, A.view_cos);
 }
 
 }  // namespace
@@ -166,7 +168,8 @@ int orbgpu_frustum_chain_batch(int B, const orb_tracking_chain_frame_t* fr, cons
         maxn = std::max(maxn, L->n);
     }
     if (maxn == 0) return ORB_OK;
-    if (a.size() * sizeof(k_is_in_frustum_args) > args_cap) return orbgpu_fail(ORB_ERR_ARG, "frustum batch: argument area too small");
+    if (a.size() * sizeof(k_is_in_frustum_args) > args_cap)
+        return orbgpu_fail(ORB_ERR_ARG, "frustum batch: argument area too small");
     hipStream_t s = (hipStream_t)stream;
     memcpy(h_args, a.data(), a.size() * sizeof(k_is_in_frustum_args));  // pinned staging
     if (hipMemcpyAsync(d_args, h_args, a.size() * sizeof(k_is_in_frustum_args), hipMemcpyHostToDevice, s) != hipSuccess)
@@ -214,7 +217,8 @@ int orb_is_in_frustum(const orb_frustum_frame_t* frame, int n, const float* pos,
         hipMemcpy(dmax, max_dist, 4 * N, hipMemcpyHostToDevice) != hipSuccess)
         rc = orbgpu_fail(ORB_ERR_DEVICE, "frustum upload failed");
     if (rc == ORB_OK)
-        rc = orb_is_in_frustum_device(frame, n, dp, dn, dmin, dmax, viewing_cos_limit, din, dproj, ddep, dlev, dcos, nullptr);
+        rc = orb_is_in_frustum_device(frame, n, dp, dn, dmin, dmax, viewing_cos_limit, din, dproj, ddep, dlev, dcos,
+                                      nullptr);
     if (rc == ORB_OK &&
         (hipMemcpy(in_view, din, N, hipMemcpyDeviceToHost) != hipSuccess ||
          hipMemcpy(proj, dproj, 12 * N, hipMemcpyDeviceToHost) != hipSuccess ||

@@ -197,7 +197,8 @@ __global__ __launch_bounds__(64 * kCandWaves) void k_proj_candidates(const ProjP
                                                          Cand* __restrict__ cands, int32_t* __restrict__ ncand,
                                                          int32_t* __restrict__ overflow, const uint8_t* __restrict__ observed,
                                                          int32_t* __restrict__ lister) {
-    k_proj_candidates_body(P, n_dev, valid, xyz, mp_desc, last_octave, cur_kp, cur_ur, cur_desc, cell_off, cell_idx, cands, ncand, overflow, observed, lister);
+    k_proj_candidates_body(P, n_dev, valid, xyz, mp_desc, last_octave, cur_kp, cur_ur, cur_desc, cell_off, cell_idx,
+                           cands, ncand, overflow, observed, lister);
 }
 struct k_proj_candidates_args {
     ProjParams P;
@@ -220,7 +221,8 @@ struct k_proj_candidates_args {
 // the same on frame blockIdx.y of a batch (one argument block per frame)
 __global__ __launch_bounds__(64 * kCandWaves) void k_proj_candidates_b(const k_proj_candidates_args* __restrict__ a) {
     const k_proj_candidates_args& A = a[blockIdx.y];
-    k_proj_candidates_body(A.P, A.n_dev, A.valid, A.xyz, A.mp_desc, A.last_octave, A.cur_kp, A.cur_ur, A.cur_desc, A.cell_off, A.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.lister);
+    k_proj_candidates_body(A.P, A.n_dev, A.valid, A.xyz, A.mp_desc, A.last_octave, A.cur_kp, A.cur_ur, A.cur_desc,
+                           A.cell_off, A.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.lister);
 }
 
 // The same candidate lists with one THREAD per point (round 5): a window holds a handful of cells and
@@ -409,7 +411,8 @@ __global__ __launch_bounds__(64 * kCandWaves) void k_lmp_candidates(const LocalP
                                                         int32_t* __restrict__ ncand, int32_t* __restrict__ overflow,
                                                         const uint8_t* __restrict__ observed, const uint8_t* __restrict__ taken0,
                                                         int32_t* __restrict__ lister) {
-    k_lmp_candidates_body(P, in_view, bad, proj, view_cos, depth, level, mp_desc, cur_kp, cur_ur, cur_desc, cell_off, cell_idx, cands, ncand, overflow, observed, taken0, lister);
+    k_lmp_candidates_body(P, in_view, bad, proj, view_cos, depth, level, mp_desc, cur_kp, cur_ur, cur_desc, cell_off,
+                          cell_idx, cands, ncand, overflow, observed, taken0, lister);
 }
 struct k_lmp_candidates_args {
     LocalParams P;
@@ -435,7 +438,9 @@ struct k_lmp_candidates_args {
 // the same on frame blockIdx.y of a batch (one argument block per frame)
 __global__ __launch_bounds__(64 * kCandWaves) void k_lmp_candidates_b(const k_lmp_candidates_args* __restrict__ a) {
     const k_lmp_candidates_args& A = a[blockIdx.y];
-    k_lmp_candidates_body(A.P, A.in_view, A.bad, A.proj, A.view_cos, A.depth, A.level, A.mp_desc, A.cur_kp, A.cur_ur, A.cur_desc, A.cell_off, A.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.taken0, A.lister);
+    k_lmp_candidates_body(A.P, A.in_view, A.bad, A.proj, A.view_cos, A.depth, A.level, A.mp_desc, A.cur_kp, A.cur_ur,
+                          A.cur_desc, A.cell_off, A.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.taken0,
+                          A.lister);
 }
 
 __device__ __forceinline__ void k_lmp_candidates_t_body(const LocalParams P, const uint8_t* __restrict__ in_view,
@@ -1011,7 +1016,8 @@ struct k_frame_prep_args {
 // the same on frame blockIdx.y of a batch (one argument block per frame)
 __global__ __launch_bounds__(kPrepThreads) void k_frame_prep_b(const k_frame_prep_args* __restrict__ a) {
     const k_frame_prep_args& A = a[blockIdx.y];
-    k_frame_prep_body(A.kps, A.n_ptr, A.cap, A.min_x, A.min_y, A.inv_w, A.inv_h, A.kp4, A.cell_off, A.cell_idx, A.cell_of, A.n_out0, A.n_out1, A.z);
+    k_frame_prep_body(A.kps, A.n_ptr, A.cap, A.min_x, A.min_y, A.inv_w, A.inv_h, A.kp4, A.cell_off, A.cell_idx,
+                      A.cell_of, A.n_out0, A.n_out1, A.z);
 }
 
 // the last frame's per-point inputs of k_proj_candidates / the rotation bins: a point whose octave is
@@ -1243,7 +1249,8 @@ extern "C" int orb_search_by_projection_frame(orb_matcher_t m, const orb_frame_v
         // (a point with more candidates than the capacity) makes the resolve a no-op and is re-run
         if (ok) {
             if (ra.n_pts > 0) hipLaunchKernelGGL(k_resolve_init, dim3((ra.n_pts + 255) / 256), dim3(256), 0, s, ra);
-            hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 8 * (size_t)n : 0, s, ra);
+            hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 8 * (size_t)n : 0,
+                               s, ra);
         }
         ok = ok && hipGetLastError() == hipSuccess &&
              hipMemcpyAsync(h + o_ovf, d + o_ovf, o_mp - o_ovf + (size_t)std::max(n, 1) * 4, hipMemcpyDeviceToHost, s) ==
@@ -1378,7 +1385,8 @@ extern "C" int orb_search_by_projection_local(orb_matcher_t m, const orb_frame_v
         ra.mp = (int32_t*)(d + o_m); ra.out_n = (int32_t*)(d + o_ovf) + 1;
         if (ok) {
             if (ra.n_pts > 0) hipLaunchKernelGGL(k_resolve_init, dim3((ra.n_pts + 255) / 256), dim3(256), 0, s, ra);
-            hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 8 * (size_t)n : 0, s, ra);
+            hipLaunchKernelGGL(k_resolve_rounds, dim3(1), dim3(kResolveThreads), ra.lds_keypoints ? 8 * (size_t)n : 0,
+                               s, ra);
         }
         ok = ok && hipGetLastError() == hipSuccess &&
              hipMemcpyAsync(h + o_ovf, d + o_ovf, o_m - o_ovf + (size_t)std::max(n, 1) * 4, hipMemcpyDeviceToHost, s) ==
@@ -1554,7 +1562,8 @@ int orbgpu_sbp_frame_device_scratch(orb_matcher_t m, const orb_frame_device_t* c
                            lp.nlevels, lp.valid2, lp.octave, lp.angle, lp.n_out0, lp.n_out1);
         const k_proj_candidates_args& c = pl.cand;
         if (cand_thread_mode(false))
-            hipLaunchKernelGGL(k_proj_candidates_t, dim3((NL + kCandThreads - 1) / kCandThreads), dim3(kCandThreads), 0, s, c);
+            hipLaunchKernelGGL(k_proj_candidates_t, dim3((NL + kCandThreads - 1) / kCandThreads), dim3(kCandThreads), 0,
+                               s, c);
         else
             hipLaunchKernelGGL(k_proj_candidates, dim3((NL + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s,
                                c.P, c.n_dev, c.valid, c.xyz, c.mp_desc, c.last_octave, c.cur_kp, c.cur_ur, c.cur_desc,
@@ -1599,14 +1608,16 @@ int orbgpu_sbp_frame_batch(orb_matcher_t m, int B, const orb_frame_device_t* con
         return orbgpu_fail(ORB_ERR_DEVICE, "batch argument upload failed");
     hipLaunchKernelGGL(k_frame_prep_b, dim3(1, B), dim3(kPrepThreads), 0, s, (const k_frame_prep_args*)(d + o_fp));
     if (maxNL > 0) {  // grids sized for the largest frame; the kernels bound themselves by their own counts
-        hipLaunchKernelGGL(k_last_prep_b, dim3((maxNL + 255) / 256, B), dim3(256), 0, s, (const k_last_prep_args*)(d + o_lp));
+        hipLaunchKernelGGL(k_last_prep_b, dim3((maxNL + 255) / 256, B), dim3(256), 0, s,
+                           (const k_last_prep_args*)(d + o_lp));
         if (cand_thread_mode(true))
             hipLaunchKernelGGL(k_proj_candidates_t_b, dim3((maxNL + kCandThreads - 1) / kCandThreads, B), dim3(kCandThreads), 0,
                                s, (const k_proj_candidates_args*)(d + o_ca));
         else
             hipLaunchKernelGGL(k_proj_candidates_b, dim3((maxNL + kCandWaves - 1) / kCandWaves, B), dim3(64 * kCandWaves), 0, s,
                                (const k_proj_candidates_args*)(d + o_ca));
-        hipLaunchKernelGGL(k_resolve_init_b, dim3((maxNL + 255) / 256, B), dim3(256), 0, s, (const k_resolve_init_args*)(d + o_ri));
+        hipLaunchKernelGGL(k_resolve_init_b, dim3((maxNL + 255) / 256, B), dim3(256), 0, s,
+                           (const k_resolve_init_args*)(d + o_ri));
     }
     hipLaunchKernelGGL(k_resolve_rounds_b, dim3(1, B), dim3(kResolveThreads), rr[0].a.lds_keypoints ? 8 * (size_t)C : 0, s,
                        (const k_resolve_rounds_args*)(d + o_rr));
@@ -1721,7 +1732,8 @@ int orbgpu_sbp_local_device_scratch(orb_matcher_t m, const orb_frame_device_t* F
                            lp.in_view2);
         const k_lmp_candidates_args& c = pl.cand;
         if (cand_thread_mode(false))
-            hipLaunchKernelGGL(k_lmp_candidates_t, dim3((np + kCandThreads - 1) / kCandThreads), dim3(kCandThreads), 0, s, c);
+            hipLaunchKernelGGL(k_lmp_candidates_t, dim3((np + kCandThreads - 1) / kCandThreads), dim3(kCandThreads), 0,
+                               s, c);
         else
             hipLaunchKernelGGL(k_lmp_candidates, dim3((np + kCandWaves - 1) / kCandWaves), dim3(64 * kCandWaves), 0, s,
                                c.P, c.in_view, c.bad, c.proj, c.view_cos, c.depth, c.level, c.mp_desc, c.cur_kp, c.cur_ur,
@@ -1762,23 +1774,27 @@ int orbgpu_sbp_local_batch(orb_matcher_t m, int B, const orb_frame_device_t* con
     }
     ArgPacker pk;
     const size_t o_fp = pk.add(fp), o_lp = pk.add(lp), o_ca = pk.add(ca), o_ri = pk.add(ri), o_rr = pk.add(rr);
-    if (pk.host.size() > args_cap) return orbgpu_fail(ORB_ERR_ARG, "SearchByProjection(local) batch: argument area too small");
+    if (pk.host.size() > args_cap)
+        return orbgpu_fail(ORB_ERR_ARG, "SearchByProjection(local) batch: argument area too small");
     char* d = static_cast<char*>(d_args);
     memcpy(h_args, pk.host.data(), pk.host.size());  // pinned staging: the copy reads it when the stream runs it
     if (hipMemcpyAsync(d, h_args, pk.host.size(), hipMemcpyHostToDevice, s) != hipSuccess)
         return orbgpu_fail(ORB_ERR_DEVICE, "batch argument upload failed");
     hipLaunchKernelGGL(k_frame_prep_b, dim3(1, B), dim3(kPrepThreads), 0, s, (const k_frame_prep_args*)(d + o_fp));
     if (maxNp > 0) {
-        hipLaunchKernelGGL(k_local_prep_b, dim3((maxNp + 255) / 256, B), dim3(256), 0, s, (const k_local_prep_args*)(d + o_lp));
+        hipLaunchKernelGGL(k_local_prep_b, dim3((maxNp + 255) / 256, B), dim3(256), 0, s,
+                           (const k_local_prep_args*)(d + o_lp));
         if (cand_thread_mode(true))
             hipLaunchKernelGGL(k_lmp_candidates_t_b, dim3((maxNp + kCandThreads - 1) / kCandThreads, B), dim3(kCandThreads), 0,
                                s, (const k_lmp_candidates_args*)(d + o_ca));
         else
             hipLaunchKernelGGL(k_lmp_candidates_b, dim3((maxNp + kCandWaves - 1) / kCandWaves, B), dim3(64 * kCandWaves), 0, s,
                                (const k_lmp_candidates_args*)(d + o_ca));
-        hipLaunchKernelGGL(k_resolve_init_b, dim3((maxNp + 255) / 256, B), dim3(256), 0, s, (const k_resolve_init_args*)(d + o_ri));
+        hipLaunchKernelGGL(k_resolve_init_b, dim3((maxNp + 255) / 256, B), dim3(256), 0, s,
+                           (const k_resolve_init_args*)(d + o_ri));
     }
     hipLaunchKernelGGL(k_resolve_rounds_b, dim3(1, B), dim3(kResolveThreads), rr[0].a.lds_keypoints ? 8 * (size_t)C : 0, s,
                        (const k_resolve_rounds_args*)(d + o_rr));
-    return hipGetLastError() == hipSuccess ? ORB_OK : orbgpu_fail(ORB_ERR_DEVICE, "SearchByProjection(local) batch launch failed");
+    return hipGetLastError() == hipSuccess ? ORB_OK
+                                           : orbgpu_fail(ORB_ERR_DEVICE, "SearchByProjection(local) batch launch failed");
 }

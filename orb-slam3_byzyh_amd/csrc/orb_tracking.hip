@@ -140,7 +140,8 @@ struct k_track_pose_edges_args {
 // the same on frame blockIdx.y of a batch (one argument block per frame)
 __global__ __launch_bounds__(kThreads) void k_track_pose_edges_b(const k_track_pose_edges_args* __restrict__ a) {
     const k_track_pose_edges_args& A = a[blockIdx.y];
-    k_track_pose_edges_body(A.P, A.kps, A.u_right, A.n_ptr, A.match_a, A.xyz_a, A.match_b, A.xyz_b, A.pose_dev, A.frame, A.edges, A.edge_kp);
+    k_track_pose_edges_body(A.P, A.kps, A.u_right, A.n_ptr, A.match_a, A.xyz_a, A.match_b, A.xyz_b, A.pose_dev, A.frame,
+                            A.edges, A.edge_kp);
 }
 
 // outliers lose their map point; n_out[0] = the edges kept, n_out[1] = those whose map point has
@@ -216,7 +217,8 @@ struct k_track_discard_args {
 // the same on frame blockIdx.y of a batch (one argument block per frame)
 __global__ __launch_bounds__(kThreads) void k_track_discard_b(const k_track_discard_args* __restrict__ a) {
     const k_track_discard_args& A = a[blockIdx.y];
-    k_track_discard_body(A.frame, A.edge_kp, A.outlier, A.match_a, A.observed_a, A.match_b, A.observed_b, A.n_out, A.cap, A.taken);
+    k_track_discard_body(A.frame, A.edge_kp, A.outlier, A.match_a, A.observed_a, A.match_b, A.observed_b, A.n_out,
+                         A.cap, A.taken);
 }
 
 // SearchLocalPoints' first loop (src/Tracking.cc:4250-4266): a local map point the frame already holds
