@@ -2016,6 +2016,9 @@ struct orb_ba_s {
     DevBuf<unsigned> counters;  // last-block counters of the fused unit kernels
     uint8_t* h_stage = nullptr;  // pinned staging of the per-solve inputs
     size_t h_stage_cap = 0;
+    uint8_t* h_stage0 = nullptr;  // one rank: the raw inputs, uploaded before the structure is built
+    size_t h_stage0_cap = 0;
+    DevBuf<uint8_t> d_stage0;
     uint8_t* h_dl = nullptr;     // pinned download of the per-solve results
     size_t h_dl_cap = 0;
     DevBuf<uint8_t> d_stage;
@@ -2121,6 +2124,7 @@ int orb_ba_destroy(orb_ba_t h) {
     h->counters.release();
     h->d_stage.release();
     if (h->h_stage) hipHostFree(h->h_stage);
+    if (h->h_stage0) hipHostFree(h->h_stage0);
     if (h->h_dl) hipHostFree(h->h_dl);
     if (h->h_prog) hipHostFree(h->h_prog);
     if (h->h_stop) hipHostFree(h->h_stop);
@@ -2361,27 +2365,27 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         return h->h_scal[6] != 0.0;
     };
 
-    // ---- structure (initializeOptimization + BlockSolver::buildStructure), csrc/ba_structure.h
-    orbgpu_ba::BaStructure& T = h->st;
-    if (!orbgpu_ba::ba_build_structure(pr, h->world, h->rank, T)) {  // SparseOptimizer::optimize returns -1: nothing to do
-        for (int e = 0; e < ne_all; ++e) {
-            if (edge_chi2) edge_chi2[e] = 0;
-            if (edge_depth_ok) edge_depth_ok[e] = 0;
+    // [items table | data] of a Stager in one pinned buffer, one copy, one scatter launch
+    auto upload_stage = [&](const Stager& sg, uint8_t*& hbuf, size_t& hcap, DevBuf<uint8_t>& dbuf) -> bool {
+        if (sg.items.empty()) return true;
+        const size_t data_off = sg.table_bytes(), total = data_off + sg.data_bytes;
+        if (total > hcap) {
+            if (hbuf) hipHostFree(hbuf);
+            hbuf = nullptr;
+            hcap = 0;
+            if (hipHostMalloc(&hbuf, total, hipHostMallocDefault) != hipSuccess) return false;
+            hcap = total;
         }
-        return ORB_OK;
-    }
-    t_order = t_csr = clk::now();
-    if (stop()) { res->stopped = 1; return ORB_ERR_ABORTED; }
-    if (agree_fail(T.dup_edge)) return orbgpu_fail(ORB_ERR_ARG, "two edges between one keyframe and one map point");
-    if (agree_fail(T.n_products > INT32_MAX)) return orbgpu_fail(ORB_ERR_ARG, "BA window too large");
-    static_assert(sizeof(EdgeDev) == sizeof(orb_ba_edge_t), "EdgeDev mirrors orb_ba_edge_t");
-    const EdgeDev* ledges = reinterpret_cast<const EdgeDev*>(T.ledges);
-    const int nf = T.nf, ne = T.ne, nl = T.nl, nfe = T.nfe, nblk = T.nblk;
-    const int n = 6 * nf, m = 3 * nl;
-    const std::vector<int32_t>& point_l = T.point_l;
-    const std::vector<int32_t>& qdeg = T.qdeg;
-    const std::vector<int32_t>& lmap = T.lmap;
-    t_pairs = clk::now();
+        if (!dbuf.grow(total)) return false;
+        sg.pack(hbuf);
+        if (hipMemcpyAsync(dbuf.p, hbuf, total, hipMemcpyHostToDevice, s) != hipSuccess) return false;
+        size_t maxb = 0;
+        for (const ScatterItem& it : sg.items) maxb = std::max<size_t>(maxb, it.bytes);
+        const unsigned gx = (unsigned)std::min<size_t>(64, std::max<size_t>(1, (maxb / 16 + 255) / 256));
+        hipLaunchKernelGGL(k_ba_scatter, dim3(gx, (unsigned)sg.items.size()), dim3(256), 0, s, dbuf.p + data_off,
+                           (const ScatterItem*)dbuf.p);
+        return hipGetLastError() == hipSuccess;
+    };
     // poses normalised as SE3Quat(q, t) does
     std::vector<double> pose(pr->pose, pr->pose + 7 * (size_t)np);
     for (int i = 0; i < np; ++i) {
@@ -2390,6 +2394,48 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         const double nn = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
         if (nn > 0) for (int k = 0; k < 4; ++k) q[k] /= nn;
     }
+    // One rank uses the problem's edges in place: the raw inputs (poses, points, edges, cameras) go up
+    // now, and the copy runs while the host builds the structure below (it does not need them on the
+    // device).  Sharded solves upload their rank's edge copy with the structure.
+    const bool early = !dist && ne_all > 0;
+    if (early) {
+        Stager s0;
+        const bool ok0 = s0.add(h->pose, pose) && s0.add(h->point, pr->point, 3 * (size_t)nq) &&
+                         s0.add(h->edges, reinterpret_cast<const EdgeDev*>(pr->edges), (size_t)ne_all) &&
+                         s0.add(h->cams, pr->pose_camera, np) &&
+                         upload_stage(s0, h->h_stage0, h->h_stage0_cap, h->d_stage0);
+        if (!ok0) return orbgpu_fail(ORB_ERR_DEVICE, "BA device allocation / upload");
+    }
+
+    // ---- structure (initializeOptimization + BlockSolver::buildStructure), csrc/ba_structure.h
+    orbgpu_ba::BaStructure& T = h->st;
+    if (!orbgpu_ba::ba_build_structure(pr, h->world, h->rank, T)) {  // SparseOptimizer::optimize returns -1: nothing to do
+        if (early) (void)hipStreamSynchronize(s);  // the raw upload reads the pinned staging the next call rewrites
+        for (int e = 0; e < ne_all; ++e) {
+            if (edge_chi2) edge_chi2[e] = 0;
+            if (edge_depth_ok) edge_depth_ok[e] = 0;
+        }
+        return ORB_OK;
+    }
+    t_order = t_csr = clk::now();
+    if (stop()) {
+        if (early) (void)hipStreamSynchronize(s);
+        res->stopped = 1;
+        return ORB_ERR_ABORTED;
+    }
+    if (agree_fail(T.dup_edge) || agree_fail(T.n_products > INT32_MAX)) {
+        if (early) (void)hipStreamSynchronize(s);
+        return orbgpu_fail(ORB_ERR_ARG, T.dup_edge ? "two edges between one keyframe and one map point"
+                                                   : "BA window too large");
+    }
+    static_assert(sizeof(EdgeDev) == sizeof(orb_ba_edge_t), "EdgeDev mirrors orb_ba_edge_t");
+    const EdgeDev* ledges = reinterpret_cast<const EdgeDev*>(T.ledges);
+    const int nf = T.nf, ne = T.ne, nl = T.nl, nfe = T.nfe, nblk = T.nblk;
+    const int n = 6 * nf, m = 3 * nl;
+    const std::vector<int32_t>& point_l = T.point_l;
+    const std::vector<int32_t>& qdeg = T.qdeg;
+    const std::vector<int32_t>& lmap = T.lmap;
+    t_pairs = clk::now();
 
     const double tau = 1e-5;
     LmState lm_init{};  // the device-driven loop's start (g2o's Levenberg state before iteration 0)
@@ -2402,9 +2448,9 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     t_struct = clk::now();
     const size_t ne1 = std::max(ne, 1);
     Stager st;
-    bool ok = st.add(h->pose, pose) && h->pose_bak.grow(7 * (size_t)np) && st.add(h->point, pr->point, 3 * (size_t)nq) &&
-              h->point_bak.grow(3 * (size_t)nq) && st.add(h->edges, ledges, (size_t)ne) && st.add(h->cams, pr->pose_camera, np) &&
-              st.add(h->pose_h, T.pose_h) && st.add(h->free_pose, T.free_pose) && st.add(h->land_point, T.land_point) &&
+    bool ok = (early || (st.add(h->pose, pose) && st.add(h->point, pr->point, 3 * (size_t)nq) &&
+                         st.add(h->edges, ledges, (size_t)ne) && st.add(h->cams, pr->pose_camera, np))) &&
+              h->pose_bak.grow(7 * (size_t)np) && h->point_bak.grow(3 * (size_t)nq) && st.add(h->pose_h, T.pose_h) && st.add(h->free_pose, T.free_pose) && st.add(h->land_point, T.land_point) &&
               st.add(h->land_off, T.land_off) && st.add(h->land_edge, T.land_edge) &&
               st.add(h->landf_off, T.landf_off) && st.add(h->landf_edge, T.landf_edge) && st.add(h->fland, T.fland) &&
               st.add(h->landf_row, T.landf_row) && st.add(h->pose_off, T.pose_off) && st.add(h->pose_fl, T.pose_fl) &&
@@ -2419,29 +2465,11 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
               st.zero(h->x, n + m) && st.zero(h->scal, 8) && st.zero(h->status, 1) && st.zero(h->counters, 2) &&
               st.add(h->lm, &lm_init, 1);
     if (ok && !st.items.empty()) {
-        // [items table | data], one pinned buffer, one copy, one scatter launch
-        const size_t data_off = st.table_bytes(), total = data_off + st.data_bytes;
-        if (total > h->h_stage_cap) {
-            if (h->h_stage) hipHostFree(h->h_stage);
-            h->h_stage = nullptr;
-            h->h_stage_cap = 0;
-            ok = hipHostMalloc(&h->h_stage, total, hipHostMallocDefault) == hipSuccess;
-            if (ok) h->h_stage_cap = total;
-        }
-        ok = ok && h->d_stage.grow(total);
-        if (ok) {
-            st.pack(h->h_stage);
-            t_pack = clk::now();
-            ok = hipMemcpyAsync(h->d_stage.p, h->h_stage, total, hipMemcpyHostToDevice, s) == hipSuccess;
-            size_t maxb = 0;
-            for (const ScatterItem& it : st.items) maxb = std::max<size_t>(maxb, it.bytes);
-            const unsigned gx = (unsigned)std::min<size_t>(64, std::max<size_t>(1, (maxb / 16 + 255) / 256));
-            hipLaunchKernelGGL(k_ba_scatter, dim3(gx, (unsigned)st.items.size()), dim3(256), 0, s,
-                               h->d_stage.p + data_off, (const ScatterItem*)h->d_stage.p);
-            if (nblk)  // the Schur blocks' product lists, for every trial of the solve
-                hipLaunchKernelGGL(k_ba_schur_pairs, dim3(nblk), dim3(64), 0, s, nf, h->pose_off.p, h->pose_fl.p,
-                                   h->blk_off.p, h->pairs.p, h->blk_cnt.p);
-        }
+        ok = upload_stage(st, h->h_stage, h->h_stage_cap, h->d_stage);
+        t_pack = clk::now();
+        if (ok && nblk)  // the Schur blocks' product lists, for every trial of the solve
+            hipLaunchKernelGGL(k_ba_schur_pairs, dim3(nblk), dim3(64), 0, s, nf, h->pose_off.p, h->pose_fl.p,
+                               h->blk_off.p, h->pairs.p, h->blk_cnt.p);
     }
     // the pinned result buffer too, before the solve: [poses | points | edge chi2 | depth flags]
     const size_t dl_bytes = sizeof(double) * (7 * (size_t)np + 3 * (size_t)nq + ne1) + ne1;
