@@ -104,3 +104,20 @@ def test_sincos_exception_table_exhaustive():
     exe = _compile(ROOT / "tools" / "gen_sincos_exceptions.cpp", BUILD / "sincos_check", ("-DORB_CHECK_TABLE",))
     r = subprocess.run([str(exe), "--check"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and "\nOK: " in "\n" + r.stdout, r.stdout + r.stderr
+
+
+def test_tracking_chain_abi_host_side(pkg):
+    """The tracking chain entry points' host side, no device work: scratch sizes (the batch's grow with
+    the frame count and cover one chain's per frame) and argument rejection with ORB_ERR_ARG."""
+    from orbslam3_amd import _lib
+    _ensure_lib()
+    lib = _lib.load()
+    one = lib.orb_tracking_chain_scratch_bytes(1850, 1855, 1800)
+    b1 = lib.orb_tracking_chain_batch_scratch_bytes(1, 1850, 1855, 1800)
+    b8 = lib.orb_tracking_chain_batch_scratch_bytes(8, 1850, 1855, 1800)
+    assert one > 0 and b1 >= one and b8 >= 8 * one
+    assert lib.orb_tracking_chain_scratch_bytes(0, 10, 10) == 0
+    assert lib.orb_tracking_chain_batch_scratch_bytes(0, 1850, 10, 10) == 0
+    assert lib.orb_tracking_chain_batch_device(None, None, 0, None, None, None, None) == _lib.ORB_ERR_ARG
+    assert lib.orb_tracking_chain_device(None, None, None, None, None, None, None, None, None, None, None, None, None,
+                                         None, None, None) == _lib.ORB_ERR_ARG
