@@ -51,7 +51,13 @@
 
 namespace {
 
-constexpr int kT = 256;
+#ifndef ORB_BA_KT
+#define ORB_BA_KT 64
+#endif
+// threads per block of the edge / landmark kernels: 64 (round 5) spreads a unit kernel over 4x the CUs,
+// and the FP64 per-edge work runs faster one wave per CU than four (C5 0.169 -> 0.161 ms per added
+// LM iteration; tools/ba_var_ab.sh)
+constexpr int kT = ORB_BA_KT;
 
 // The host structure's list entries (csrc/ba_structure.h): a free pose's (landmark, edge) observations
 // and the Schur blocks' (Z edge, Hpl edge) products.
