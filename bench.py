@@ -1158,7 +1158,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--frames", type=int, default=FRAMES)
-    ap.add_argument("--in-flight", type=int, default=3,
+    ap.add_argument("--in-flight", type=int, default=4,
                     help="extractor handles with a batch in flight, each on its own stream (consecutive steps "
                          "overlap: one batch's latency-bound quad-tree/describe tail runs beside the next "
                          "batch's pyramid/FAST); 1 = one batch at a time")
