@@ -226,6 +226,7 @@ struct PyrArgs {
     int xtab_off, ytab_off, simd_end;
     int tiles_per_frame, share;    // share: tiles of a frame per XCD (blockIdx.x -> tile, pyr_tile)
     int tab_off;                   // this level's tile table (tile_tables)
+    int frame_affine;              // 1: every tile of frame f on XCD f % 8 (frames a multiple of 8)
 };
 
 template <bool kLevel0, int kBH = kSmallBoxH, int kBW = kSmallBoxW>
@@ -238,10 +239,22 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
                                                           int* __restrict__ status_reset) {
     // level 0 clears the batch's error status (read after the quad-tree), instead of a memset launch
     if (kLevel0 && status_reset && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *status_reset = 0;
-    // blockIdx.y = frame; blockIdx.x -> tile of the frame, XCD-chunked (xcd_tile)
-    const int t = xcd_tile(blockIdx.x, A.share);
-    if (t >= A.tiles_per_frame) return;
-    const int f = blockIdx.y;
+    // blockIdx.y = frame; blockIdx.x -> tile of the frame, XCD-chunked (xcd_tile).  Frame-affine
+    // (round 5): the dispatch deals linear block L to XCD L % 8, so XCD j runs its blocks in the order
+    // L >> 3 over all tiles of its frames j, j + 8, ...: a frame's halo re-reads and the next level's
+    // reads of this one stay in one L2.
+    int t, f;
+    if (A.frame_affine) {
+        const int L = blockIdx.y * gridDim.x + blockIdx.x, s8 = L >> 3;
+        const int q = s8 / A.tiles_per_frame;
+        t = s8 - q * A.tiles_per_frame;
+        f = (L & 7) + 8 * q;
+        if (f >= (int)gridDim.y) return;
+    } else {
+        t = xcd_tile(blockIdx.x, A.share);
+        if (t >= A.tiles_per_frame) return;
+        f = blockIdx.y;
+    }
     // debug (ORBGPU_PYR_STAMPS): per-block phase clocks, thread 0 of each block
     unsigned long long* stp = stamps ? stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 : nullptr;
     if (stp && threadIdx.x == 0) { stp[6] = wall_clock64(); stp[0] = __builtin_amdgcn_s_memtime(); }
@@ -743,7 +756,8 @@ __global__ __launch_bounds__(256) void k_fast_cells(const KernelGeom* __restrict
     const KernelGeom& g = *gp;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    // XCD-chunked block order (xcd_tile): neighbouring cells, whose windows overlap, share an L2
+    // XCD-chunked block order (xcd_tile): neighbouring cells, whose windows overlap, share an L2 (the
+    // pyramid's frame-affine order measured no fetch change here: the windows miss L2 either way)
     const int tb = xcd_tile(blockIdx.x, share);
     if (tb >= nblocks) return;
     const int f = tb / groups;
@@ -1952,6 +1966,7 @@ struct Extractor {
     int fast_split_cfg = 3;             // the configured split (orb_extractor_set_overlap(h, 0) sets fast_split 0)
     int chain_fast_split = 1;           // one-chain FAST launches (see launch_chunk; ORBGPU_CHAIN_FAST)
     int qt_key_room = 4;                // KB of quad-tree LDS for keys beyond the node tables (ORBGPU_QT_KEYROOM)
+    int pyr_affine = 1;                 // pyramid tiles of a frame on one XCD (ORBGPU_PYR_AFFINE=0: spread, for the A/B)
     int fast_per_level = 0;             // 1: FAST of each later level right after its pyramid level (side2); measured slower
     int desc_split = 1;                 // 1: quad-tree + descriptors of levels [0, fast_split) on the side stream (ORBGPU_DESC_SPLIT)
     orb_keypoint_t* d_st_kp = nullptr; size_t st_kp_cap = 0;   // their staging records (desc_split)
@@ -2266,6 +2281,7 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
         A.tab_off = e->tile_off[l];
         A.tiles_per_frame = pyr_tiles_x(L) * pyr_tiles_y(L);
         A.share = (A.tiles_per_frame + 7) / 8;  // tiles of a frame per XCD (xcd_tile)
+        A.frame_affine = e->pyr_affine && n % 8 == 0;
         const dim3 grid(8 * A.share, n);
         unsigned long long* stamps = nullptr;
         const size_t nblk = (size_t)grid.x * grid.y;
@@ -2417,6 +2433,7 @@ int orb_extractor_create(const orb_params_t* p, int max_width, int max_height, i
     e->fast_split_cfg = e->fast_split;
     if (const char* c = getenv("ORBGPU_CHAIN_FAST")) e->chain_fast_split = atoi(c);
     if (const char* c = getenv("ORBGPU_QT_KEYROOM")) e->qt_key_room = std::max(0, atoi(c));
+    if (const char* c = getenv("ORBGPU_PYR_AFFINE")) e->pyr_affine = atoi(c);
     bool ok = hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) == hipSuccess &&
               hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&e->side2, hipStreamNonBlocking) == hipSuccess;
