@@ -715,6 +715,9 @@ typedef struct orb_tracking_chain_batch_buffers {
 } orb_tracking_chain_batch_buffers_t;
 
 size_t orb_tracking_chain_batch_scratch_bytes(int n_frames, int cap, int last_cap, int n_local);
+/* Release the pinned host staging the batch calls keep for `scratch` (after its last call completed,
+ * before the scratch is freed or reused for something else).  A NULL or unknown scratch is a no-op. */
+int orb_tracking_chain_batch_release(void* scratch);
 int orb_tracking_chain_batch_device(orb_matcher_t m_motion, orb_matcher_t m_local, int n_frames,
                                     const orb_tracking_chain_frame_t* frames, const orb_tracking_chain_params_t* params,
                                     const orb_tracking_chain_batch_buffers_t* bufs, void* stream);

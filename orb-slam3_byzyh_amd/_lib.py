@@ -124,6 +124,7 @@ PROTOTYPES = {
     "orb_tracking_local_seen_device": (_i, [_vp, _i, _i, _vp, _i, _vp, _vp]),
     "orb_tracking_chain_scratch_bytes": (_sz, [_i, _i, _i]),
     "orb_tracking_chain_batch_scratch_bytes": (_sz, [_i, _i, _i, _i]),
+    "orb_tracking_chain_batch_release": (_i, [_vp]),
     "orb_tracking_chain_batch_device": (_i, [_vp, _vp, _i, _vp, _vp, _vp, _vp]),
     "orb_tracking_chain_device": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                         _vp]),

@@ -392,6 +392,20 @@ size_t orb_tracking_chain_batch_scratch_bytes(int n_frames, int cap, int last_ca
     return args + (size_t)n_frames * stride + (size_t)n_frames * cap * sizeof(double) + 256;
 }
 
+int orb_tracking_chain_batch_release(void* scratch) {
+    std::lock_guard<std::mutex> lock(g_staging_mu);
+    auto it = g_staging.find(scratch);
+    if (it == g_staging.end()) return ORB_OK;
+    BatchStaging& stg = it->second;
+    if (stg.copied) {
+        (void)hipEventSynchronize(stg.copied);
+        (void)hipEventDestroy(stg.copied);
+    }
+    if (stg.host) (void)hipHostFree(stg.host);
+    g_staging.erase(it);
+    return ORB_OK;
+}
+
 int orb_tracking_chain_batch_device(orb_matcher_t m_motion, orb_matcher_t m_local, int B,
                                     const orb_tracking_chain_frame_t* fr, const orb_tracking_chain_params_t* P,
                                     const orb_tracking_chain_batch_buffers_t* Bf, void* stream) {

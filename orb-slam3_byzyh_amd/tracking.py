@@ -396,6 +396,8 @@ class TrackingChainBatch:
             last_cap, n_local = max(last_cap, last.cap), max(n_local, local.n)
         need = int(lib.orb_tracking_chain_batch_scratch_bytes(self.B, self.cap, last_cap, n_local))
         if need > self._scratch.numel():
+            if self._scratch.numel():
+                lib.orb_tracking_chain_batch_release(ctypes.c_void_p(self._scratch.data_ptr()))
             self._retired.append(self._scratch)
             self._scratch = torch.empty(need, dtype=torch.uint8, device=self.device)
             self._bufs.scratch = self._scratch.data_ptr()
@@ -404,3 +406,15 @@ class TrackingChainBatch:
                                                   ctypes.byref(self._bufs), ctypes.c_void_p(st.cuda_stream)),
               "orb_tracking_chain_batch_device")
         return BatchTrackResult(self, st, nb)
+
+    def release(self) -> None:
+        """Free the library's pinned staging for this batch's scratch (waits for its last call)."""
+        if self._scratch.numel():
+            _lib.load().orb_tracking_chain_batch_release(ctypes.c_void_p(self._scratch.data_ptr()))
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:  # interpreter shutdown: the library may be gone
+            pass
+
