@@ -681,7 +681,7 @@ int orb_tracking_chain_device(orb_matcher_t m_motion, orb_matcher_t m_local, con
  * grid row per frame), so B frames cost one host crossing and ~20 launches instead of B of each, and
  * the frames' single-workgroup stages (the resolve, PoseOptimization) run side by side over the CUs.
  * Frame b's results are the single call's on the same inputs, bit for bit.  All frames share `cap`
- * (their frame views' cap); a last frame and a local map per frame. */
+ * (their frame views' cap); a last frame and a local map per frame; at most 65535 frames per call. */
 typedef struct orb_tracking_chain_frame {
     const orb_frame_device_t* frame;
     const orb_last_points_device_t* last;

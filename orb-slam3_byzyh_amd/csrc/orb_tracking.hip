@@ -409,7 +409,7 @@ int orb_tracking_chain_batch_release(void* scratch) {
 int orb_tracking_chain_batch_device(orb_matcher_t m_motion, orb_matcher_t m_local, int B,
                                     const orb_tracking_chain_frame_t* fr, const orb_tracking_chain_params_t* P,
                                     const orb_tracking_chain_batch_buffers_t* Bf, void* stream) {
-    if (!m_motion || !m_local || B <= 0 || !fr || !P || !Bf || !Bf->m1 || !Bf->m2 || !Bf->n_match || !Bf->frames ||
+    if (!m_motion || !m_local || B <= 0 || B > 65535 /* one grid row per frame */ || !fr || !P || !Bf || !Bf->m1 || !Bf->m2 || !Bf->n_match || !Bf->frames ||
         !Bf->edges1 || !Bf->edges2 || !Bf->edge_kp1 || !Bf->edge_kp2 || !Bf->outlier1 || !Bf->outlier2 || !Bf->poses ||
         !Bf->inliers || !Bf->n_out || !Bf->taken || !Bf->scratch)
         return orbgpu_fail(ORB_ERR_ARG, "bad tracking chain batch arguments");
