@@ -115,14 +115,35 @@ inline bool ba_build_structure(const orb_ba_problem_t* pr, int world, int rank, 
     S.pose_off.assign(nf + 1, 0);
     S.eland.resize(ne);
     S.erow.resize(ne);
-    for (int e = 0; e < ne; ++e) {
-        const int l = S.point_l[L[e].point], r = S.pose_h[L[e].pose];
-        S.eland[e] = l;
-        S.erow[e] = r;
-        S.land_off[l + 1]++;
-        if (r >= 0) {
-            S.landf_off[l + 1]++;
-            S.pose_off[r + 1]++;
+    // Edges come grouped by map point (LocalBundleAdjustment adds each point's observations in turn,
+    // src/Optimizer.cc:1965-2090), so a landmark's counts accumulate in registers over its run of edges
+    // instead of a read-modify-write chain through memory per edge.
+    {
+        const int32_t *pl = S.point_l.data(), *ph = S.pose_h.data();
+        int32_t *el = S.eland.data(), *er = S.erow.data(), *lo = S.land_off.data() + 1, *lf = S.landf_off.data() + 1,
+                *po = S.pose_off.data() + 1;
+        int cur = -1, n_all = 0, n_free = 0;
+        for (int e = 0; e < ne; ++e) {
+            const int l = pl[L[e].point], r = ph[L[e].pose];
+            el[e] = l;
+            er[e] = r;
+            if (l != cur) {
+                if (cur >= 0) {
+                    lo[cur] += n_all;
+                    lf[cur] += n_free;
+                }
+                cur = l;
+                n_all = n_free = 0;
+            }
+            ++n_all;
+            if (r >= 0) {
+                ++n_free;
+                po[r]++;
+            }
+        }
+        if (cur >= 0) {
+            lo[cur] += n_all;
+            lf[cur] += n_free;
         }
     }
     for (int l = 0; l < nl; ++l) {
@@ -136,10 +157,28 @@ inline bool ba_build_structure(const orb_ba_problem_t* pr, int world, int rank, 
     S.landf_edge.resize(nfe);
     S.c1.assign(S.land_off.begin(), S.land_off.end() - 1);
     S.c2.assign(S.landf_off.begin(), S.landf_off.end() - 1);
-    for (int e = 0; e < ne; ++e) {
-        const int l = S.eland[e];
-        S.land_edge[S.c1[l]++] = e;
-        if (S.erow[e] >= 0) S.landf_edge[S.c2[l]++] = e;
+    {  // the cursors of the current landmark's run in registers, as above
+        const int32_t *el = S.eland.data(), *er = S.erow.data();
+        int32_t *c1 = S.c1.data(), *c2 = S.c2.data(), *le = S.land_edge.data(), *lfe = S.landf_edge.data();
+        int cur = -1, k1 = 0, k2 = 0;
+        for (int e = 0; e < ne; ++e) {
+            const int l = el[e];
+            if (l != cur) {
+                if (cur >= 0) {
+                    c1[cur] = k1;
+                    c2[cur] = k2;
+                }
+                cur = l;
+                k1 = c1[l];
+                k2 = c2[l];
+            }
+            le[k1++] = e;
+            if (er[e] >= 0) lfe[k2++] = e;
+        }
+        if (cur >= 0) {
+            c1[cur] = k1;
+            c2[cur] = k2;
+        }
     }
     // each landmark's free edges by pose row, stable (an insertion sort: a landmark has a handful of
     // edges), with their rows and landmarks; then the pose lists in landmark order
@@ -148,11 +187,16 @@ inline bool ba_build_structure(const orb_ba_problem_t* pr, int world, int rank, 
     S.pose_fl.resize(nfe);
     S.c1.assign(S.pose_off.begin(), S.pose_off.end() - 1);
     S.dup_edge = false;
+    const int32_t* lfo = S.landf_off.data();
+    const int32_t* erw = S.erow.data();
+    int32_t* fl = S.fland.data();
+    int32_t* pc = S.c1.data();
+    LandEdge* pfl = S.pose_fl.data();
     for (int l = 0; l < nl; ++l) {
-        const int b0 = S.landf_off[l], d = S.landf_off[l + 1] - b0;
+        const int b0 = lfo[l], d = lfo[l + 1] - b0;
         int32_t* e0 = S.landf_edge.data() + b0;
         int32_t* r0 = S.landf_row.data() + b0;
-        for (int k = 0; k < d; ++k) r0[k] = S.erow[e0[k]];
+        for (int k = 0; k < d; ++k) r0[k] = erw[e0[k]];
         for (int a = 1; a < d; ++a) {
             const int32_t v = e0[a], key = r0[a];
             int b = a;
@@ -163,11 +207,13 @@ inline bool ba_build_structure(const orb_ba_problem_t* pr, int world, int rank, 
             e0[b] = v;
             r0[b] = key;
         }
+        bool dup = false;
         for (int k = 0; k < d; ++k) {
-            S.fland[b0 + k] = l;
-            S.pose_fl[S.c1[r0[k]]++] = LandEdge{l, e0[k]};
-            if (k && r0[k] == r0[k - 1]) S.dup_edge = true;
+            fl[b0 + k] = l;
+            pfl[pc[r0[k]]++] = LandEdge{l, e0[k]};
+            dup |= k && r0[k] == r0[k - 1];
         }
+        S.dup_edge |= dup;
     }
     // every upper-triangle block of S, row-major (k_ba_schur_pairs / schur_block_ij)
     S.nblk = nf * (nf + 1) / 2;
