@@ -183,3 +183,31 @@ def test_tracking_chain_batch_ragged(pkg, synth):
         assert np.array_equal(r["pose1"], o["pose1"]) and np.array_equal(r["pose2"], o["pose2"]), seed
         if nloc == 0:
             assert r["n2"] == 0
+
+
+def test_tracking_chain_batch_many_slots(pkg, synth):
+    """A batch of 48 frames (three scenes dealt round-robin, each slot with its own local map, as the
+    bench's 256-frame batches run): every slot's outputs equal its scene's single chain, so the grid
+    rows, the per-frame argument blocks and the scratch strides hold past a handful of frames."""
+    scenes = [synth.tracking_chain_scene(seed=s) for s in (81, 82, 84)]
+    fr = [_frames(pkg, sc) for sc in scenes]
+    cap = max(max(C.N, L.N) for C, L in fr) + 5
+    devs = [_device(pkg, sc, C, L, cap=cap) for sc, (C, L) in zip(scenes, fr)]
+    single = [pkg.TrackingChain(cap).track(cur, last, local, sc["pose7_pred"]).sync()
+              for sc, (cur, last, local) in zip(scenes, devs)]
+    n = 48
+    items = []
+    for i in range(n):
+        k = i % 3
+        sc, (cur, last, _) = scenes[k], devs[k]
+        local = _device(pkg, sc, *fr[k], cap=cap)[2]  # a local map per slot: isInFrustum writes its fields
+        items.append((cur, last, local, sc["pose7_pred"]))
+    res = pkg.TrackingChainBatch(cap, n).track(items).sync()
+    assert len(res) == n
+    for i, r in enumerate(res):
+        o = single[i % 3]
+        for k in ("n1", "n2", "n_kept", "n_map"):
+            assert r[k] == o[k], (i, k)
+        for k in ("m1", "m2", "edge_kp1", "edge_kp2", "outlier1", "outlier2", "inliers"):
+            assert np.array_equal(np.asarray(r[k]), np.asarray(o[k])), (i, k)
+        assert np.array_equal(r["pose1"], o["pose1"]) and np.array_equal(r["pose2"], o["pose2"]), i
