@@ -833,7 +833,7 @@ def bench_single_frame(pkg, synth, cpu_baseline_on, reps=50):
     return out
 
 
-def bench_c2_pcie(pkg, synth, dev, steps, n_frames=64, in_flight=3):
+def bench_c2_pcie(pkg, synth, dev, steps, n_frames=64, in_flight=16):
     """SURVEY.md 8(d)'s wording of the metric, H2D -> extract -> D2H: the C2 batch starts in pinned
     host memory and the keypoints, descriptors and counts end there, every step.  `in_flight` handles
     take the steps in turn.  The uploads run by DMA on one upload stream; each handle's extraction
@@ -847,6 +847,9 @@ def bench_c2_pcie(pkg, synth, dev, steps, n_frames=64, in_flight=3):
     import torch
     frames = np.stack([synth.polygon_frame(640, 480, seed=100 + i) for i in range(n_frames)])
     host = torch.from_numpy(frames).pin_memory()
+    # 16 handles: the upload of batch i + H waits for batch i's extraction to have read its buffer, so
+    # the handle count is how far the upload stream runs ahead (tools/pcie_h_sweep.sh, round 5: H = 3
+    # 129k, 4 135-139k, 8 142k, 12 145-148k, 16 150-151k features/ms; 0.83 of the link bound)
     H = int(os.environ.get("ORB_PCIE_H", max(1, in_flight)))
     exs = [pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=640, max_height=480, max_batch=n_frames)
            for _ in range(H)]
@@ -955,7 +958,7 @@ def bench_c2_pcie(pkg, synth, dev, steps, n_frames=64, in_flight=3):
         exs[0].extract_batch_device(dimg[0], (0, 1000), cap=cap, out=outs[0], stream=sts[0])
     up_ms, down_ms, both_ms, ext_ms = timed(upload), timed(download), timed(both), timed(extract)
     bound = max(up_ms, ext_ms) if mode in ("up_zc_out", "zc_out", "zc_all") else max(up_ms, down_ms, ext_ms)
-    return {"config": f"C2 ({n_frames} x 640x480) from pinned host memory to pinned host outputs, {H} batches in flight "
+    return {"config": f"C2 ({n_frames} x 640x480) from pinned host memory to pinned host outputs, {H} handles taking the batches in turn "
                       f"(mode {mode}: uploads on one upload stream, each extraction on its handle's stream writing "
                       f"its outputs into pinned host memory)",
             "features_per_ms": round(nfeat * reps / dt, 3), "ms_per_step": round(dt / reps, 4),
@@ -979,8 +982,8 @@ def throughput_mode(exs):
 
 def run_pcie_child(steps):
     """bench_c2_pcie in a process of its own.  HIP maps a process's streams onto 4 hardware queues
-    by use count; after the other measurements have created their handles' streams, the three
-    PCIe handles' streams can share a queue and serialise (0.73 ms per step in-process vs 0.41 in a
+    by use count; after the other measurements have created their handles' streams, the PCIe
+    handles' streams can share a queue and serialise (0.73 ms per step in-process vs 0.41 in a
     fresh process, tools/pcie_probe.py).  The child is started as a child (no exec of this process)."""
     import subprocess
     r = subprocess.run([sys.executable, os.path.abspath(__file__), "--pcie-only", "--steps", str(steps)],
@@ -1196,7 +1199,7 @@ def main():
     pkg = load_package()
     from orbslam3_amd import synth
     if args.pcie_only:
-        print(json.dumps(bench_c2_pcie(pkg, synth, dev, args.steps, in_flight=3)), flush=True)
+        print(json.dumps(bench_c2_pcie(pkg, synth, dev, args.steps)), flush=True)
         return
 
     nfr = args.frames
