@@ -761,17 +761,21 @@ def bench_tracking_chain(pkg, synth, dev, steps, cpu_baseline_on, n_scenes=8, ba
     bdt = (time.perf_counter() - t0) * 1e3
     # the batch API (orb_tracking_chain_batch_device): nb frames per call, one launch per stage for the
     # whole batch; every slot its own local map (the chain writes its tracking fields), frames shared
-    nb, capb = int(os.environ.get("ORB_CHAIN_NB", "256")), 2048
+    nb, capb = int(os.environ.get("ORB_CHAIN_NB", "512")), 2048  # 256: 171, 512: 183, 1024: 173-179 frames/ms
     sb = [_chain_inputs(pkg, synth, dev, 4400 + s, cap=capb) for s in range(n_scenes)]
     locs = [pkg.DeviceLocalMap.from_host(dev, **sb[b % n_scenes][0]["local"]) for b in range(nb)]
     items = [(sb[b % n_scenes][3], sb[b % n_scenes][4], locs[b], sb[b % n_scenes][0]["pose7_pred"]) for b in range(nb)]
-    chb = pkg.TrackingChainBatch(capb, nb, device=dev, th_motion=7, th_local=1)
-    for _ in range(2):
-        chb.track(items, stream=st)
+    # ORB_CHAIN_NBUF batch objects (scratch + pinned argument staging each) take the calls in turn: a
+    # call waits on the host until the previous call on its scratch has copied its arguments up
+    nbuf = max(1, int(os.environ.get("ORB_CHAIN_NBUF", "1")))
+    chbs = [pkg.TrackingChainBatch(capb, nb, device=dev, th_motion=7, th_local=1) for _ in range(nbuf)]
+    chb = chbs[0]
+    for i in range(2 * nbuf):
+        chbs[i % nbuf].track(items, stream=st)
     st.synchronize()
     t0 = time.perf_counter()
-    for _ in range(brep):
-        chb.track(items, stream=st)
+    for i in range(brep):
+        chbs[i % nbuf].track(items, stream=st)
     st.synchronize()
     bat_ms = (time.perf_counter() - t0) * 1e3 / brep
     res0 = chb.track(items[:1], stream=st).sync()[0]  # slot 0 is scene 0: the single chain's answer
@@ -782,7 +786,8 @@ def bench_tracking_chain(pkg, synth, dev, steps, cpu_baseline_on, n_scenes=8, ba
            "single_frame_ms": round(float(np.median(lat)), 4), "single_frame_gpu_ms": round(float(np.median(gpu)), 4),
            "single_frame_enqueue_ms": round(float(np.median(enq)), 4),
            "batched_frames_per_ms": round(batch * brep / bdt, 4), "batch": batch, "streams": n_streams,
-           "batch_api": {"frames_per_call": nb, "ms_per_call": round(bat_ms, 4), "frames_per_ms": round(nb / bat_ms, 3),
+           "batch_api": {"frames_per_call": nb, "batch_objects": nbuf, "ms_per_call": round(bat_ms, 4),
+                         "frames_per_ms": round(nb / bat_ms, 3),
                          "note": "orb_tracking_chain_batch_device: one launch per stage for the whole batch, one "
                                  "stream; frames padded to cap 2048; 8 scenes repeated, a local map per slot"},
            "matches_last_frame": n1, "matches_local_map": n2, "dtype": "u8 / f32 / f64"}
