@@ -322,8 +322,11 @@ def bench_c3_chain(pkg, synth, dev, steps, cpu_baseline_on, n_kf=32, n_nb=10):
     vocab = pkg.ORBVocabulary(voc)
     scale, sigma2 = synth.scale_tables()
     cap = 1200 + 16 * 8
+    # n_new buffer sets of new keyframes take the steps in turn (a step's extraction overlaps the
+    # previous step's matching), plus one set of predecessors (the previous step's keyframes)
+    n_new = max(1, int(os.environ.get("ORB_C3_INFLIGHT", "3")))
     sets = []
-    for _ in range(2):
+    for _ in range(n_new + 1):
         S = {"exl": pkg.ORBextractor(1200, 1.2, 8, 20, 7, max_width=752, max_height=480, max_batch=n_kf),
              "exr": pkg.ORBextractor(1200, 1.2, 8, 20, 7, max_width=752, max_height=480, max_batch=n_kf),
              "s_l": torch.cuda.Stream(dev), "s_r": torch.cuda.Stream(dev), "s_m": torch.cuda.Stream(dev)}
@@ -342,20 +345,25 @@ def bench_c3_chain(pkg, synth, dev, steps, cpu_baseline_on, n_kf=32, n_nb=10):
                     torch.empty((n_kf, cap), dtype=torch.int32, device=dev),
                     torch.empty((n_kf, 2), dtype=torch.int32, device=dev))
         sets.append(S)
-    kfs = []  # kfs[set][f]: frame f of that set's buffers, at stream index n_nb + f (set 0) or f (set 1)
+    # kfs[set][f]: frame f of that set's buffers, at stream index n_nb + f (new sets) or f (predecessors)
+    kfs = []
     for si, S in enumerate(sets):
-        base = n_nb if si == 0 else 0
+        base = n_nb if si < n_new else 0
         kfs.append([pkg.DeviceKeyFrame(S["out_l"], S["bow"], f, Tcw[base + f], synth.EUROC_K, scale, sigma2,
                                        u_right=S["u"]) for f in range(n_kf)])
     matcher = pkg.ORBmatcher(0.6, False)  # LocalMapping's ORBmatcher(0.6, false) (src/LocalMapping.cc:536)
-    # the new keyframes of set 0 against their predecessors: in set 0 before them, then the end of set 1
-    groups = []
-    for f in range(n_kf):
-        nb = [kfs[0][f - j] if f - j >= 0 else kfs[1][n_kf + f - j] for j in range(1, n_nb + 1)]
-        groups.append((kfs[0][f], nb))
-    prepared = matcher.prepare_device_batch(groups)
-    m_out = (torch.empty((n_kf * n_nb, cap), dtype=torch.int32, device=dev),
-             torch.empty(n_kf * n_nb, dtype=torch.int32, device=dev))
+    # the new keyframes of a set against their predecessors: in that set before them, then the end of
+    # the predecessor set
+    for k in range(n_new):
+        groups = []
+        for f in range(n_kf):
+            nb = [kfs[k][f - j] if f - j >= 0 else kfs[n_new][n_kf + f - j] for j in range(1, n_nb + 1)]
+            groups.append((kfs[k][f], nb))
+        sets[k]["groups"] = groups
+        sets[k]["prepared"] = matcher.prepare_device_batch(groups)
+        sets[k]["m_out"] = (torch.empty((n_kf * n_nb, cap), dtype=torch.int32, device=dev),
+                            torch.empty(n_kf * n_nb, dtype=torch.int32, device=dev))
+    m_out = sets[0]["m_out"]
 
     def extract(S, stream_done=None):
         S["s_l"].wait_stream(S["s_m"])
@@ -368,26 +376,28 @@ def bench_c3_chain(pkg, synth, dev, steps, cpu_baseline_on, n_kf=32, n_nb=10):
                                                 out=S["st_out"])
         vocab.transform_frames_device(S["out_l"][1], S["out_l"][2], 4, stream=S["s_m"], out=S["bow"])
 
-    # set 1 holds the previous step once; every timed step rebuilds set 0 and matches it
-    extract(sets[1])
-    S0 = sets[0]
+    # the predecessor set holds the previous step once; every timed step rebuilds one new set and
+    # matches it
+    extract(sets[n_new])
 
-    def step(ev=None):
-        extract(S0)
+    def step(i, ev=None):
+        S = sets[i % n_new]
+        extract(S)
         if ev is not None:
-            ev[0].record(S0["s_m"])
-        matcher.SearchForTriangulationDeviceBatch(groups, False, False, stream=S0["s_m"], out=m_out, prepared=prepared)
+            ev[0].record(S["s_m"])
+        matcher.SearchForTriangulationDeviceBatch(S["groups"], False, False, stream=S["s_m"], out=S["m_out"],
+                                                  prepared=S["prepared"])
         if ev is not None:
-            ev[1].record(S0["s_m"])
+            ev[1].record(S["s_m"])
 
-    for _ in range(3):
-        step()
+    for i in range(3 * n_new):
+        step(i)
     torch.cuda.synchronize(dev)
     reps = max(6, min(steps, 20))
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     t0 = time.perf_counter()
     for i in range(reps):
-        step(ev[i])
+        step(i, ev[i])
     torch.cuda.synchronize(dev)
     dt = (time.perf_counter() - t0) * 1e3
     sft_ms = sum(a.elapsed_time(z) for a, z in ev) / reps
@@ -424,7 +434,7 @@ def bench_c3_chain(pkg, synth, dev, steps, cpu_baseline_on, n_kf=32, n_nb=10):
                      "translating along x), nFeatures 1200, extract left || right + ComputeStereoMatches + ComputeBoW "
                      f"(k=10 L=6) + SearchForTriangulation of each against its {n_nb} predecessors, device-resident, "
                      "one GPU",
-           "keyframes_per_ms": round(n_kf * reps / dt, 4), "ms_per_step": round(dt / reps, 4),
+           "keyframes_per_ms": round(n_kf * reps / dt, 4), "ms_per_step": round(dt / reps, 4), "step_buffers": n_new,
            "sft_ms_per_step": round(sft_ms, 4), "sft_pairs_per_step": n_kf * n_nb,
            "matches_per_pair": round(float(cnt.mean()), 1), "single_keyframe_ms": round(lat, 4)}
     if cpu_baseline_on:
