@@ -1441,7 +1441,8 @@ def main():
     stereo = None
     if not args.no_stereo and world == 1:
         try:
-            stereo = bench_stereo(pkg, synth, dev, args.steps, not args.no_cpu_baseline)
+            stereo = bench_stereo(pkg, synth, dev, args.steps, not args.no_cpu_baseline,
+                                  n_sets=int(os.environ.get("ORB_STEREO_SETS", "2")))
         except Exception as e:  # noqa: BLE001
             stereo = {"error": repr(e)}
     pose = None

@@ -1,7 +1,7 @@
 """The benched workloads themselves, checked frame by frame against the oracle.
 
-bench.py times C2 as 64 frames (seeds 100..163) with three extractor handles taking the steps in
-turn on their own streams, so one batch's quad-tree/describe tail runs beside the next batch's
+bench.py times C2 as 64 frames (seeds 100..163) with four extractor handles taking the steps in
+turn on their own streams, each batch one chain on its handle's stream (set_overlap(False)), so one batch's quad-tree/describe tail runs beside the next batch's
 pyramid/FAST, with the pyramid launch stamps on (profile "pyramid_launches").  The C4 line runs
 32 frames of 1280x720 per GPU the same way.  Both are reproduced here at full size and every frame
 of every handle is compared with the CPU oracle: keypoints bitwise, descriptors, monoIndex.
@@ -17,7 +17,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _run_in_flight(pkg, imgs, nf, w, h, lap, steps=6, handles=3, stamps=True):
+def _run_in_flight(pkg, imgs, nf, w, h, lap, steps=8, handles=4, stamps=True):
     """bench.py's timed loop: `handles` extractors on their own streams, step i on handle i % handles."""
     import torch
     b = imgs.shape[0]
@@ -27,6 +27,9 @@ def _run_in_flight(pkg, imgs, nf, w, h, lap, steps=6, handles=3, stamps=True):
              torch.empty((b, cap, 32), dtype=torch.uint8, device=imgs.device),
              torch.empty((b, 2), dtype=torch.int32, device=imgs.device)) for _ in range(handles)]
     streams = [torch.cuda.Stream() for _ in range(handles)]
+    if handles > 1:  # bench.throughput_mode: one chain per batch on its handle's stream
+        for e in exs:
+            e.set_overlap(False)
     if stamps:
         for e in exs:
             e.profile("pyramid_launches")
@@ -59,7 +62,7 @@ def _check_against_oracle(pkg, oracle, frames, outs, nf, lap):
 
 
 def test_c2_as_benched(pkg, oracle, synth):
-    """C2 exactly as bench.py runs it: 64 frames (seeds 100..163), 3 handles in flight, 6 steps."""
+    """C2 exactly as bench.py runs it: 64 frames (seeds 100..163), 4 handles in flight, 8 steps."""
     import torch
     frames = np.stack([synth.polygon_frame(640, 480, seed=100 + i) for i in range(64)])
     outs = _run_in_flight(pkg, torch.from_numpy(frames).cuda(), 1000, 640, 480, (0, 1000))
@@ -68,7 +71,7 @@ def test_c2_as_benched(pkg, oracle, synth):
 
 
 def test_c4_shard_as_benched(pkg, oracle, synth):
-    """C4's per-GPU shard: 32 frames of 1280x720 (seeds 1000..1031), 3 handles in flight."""
+    """C4's per-GPU shard: 32 frames of 1280x720 (seeds 1000..1031), 4 handles in flight."""
     import torch
     frames = np.stack([synth.polygon_frame(1280, 720, seed=1000 + i) for i in range(32)])
     outs = _run_in_flight(pkg, torch.from_numpy(frames).cuda(), 1000, 1280, 720, (0, 1000), stamps=False)
