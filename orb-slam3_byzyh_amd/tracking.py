@@ -185,6 +185,17 @@ class DeviceLocalMap:
     def view(self) -> LocalPointsDeviceView:
         return self._view
 
+    def chain_pointers(self) -> tuple:
+        """(view address, pos, normal, min_dist, max_dist, last_row or 0) for a tracking-chain frame record
+        (the arrays are fixed at construction)."""
+        cp = getattr(self, "_chain_ptrs", None)
+        if cp is None:
+            lr = self.last_row
+            cp = self._chain_ptrs = (ctypes.addressof(self._view), self.pos.data_ptr(), self.normal.data_ptr(),
+                                     self.min_dist.data_ptr(), self.max_dist.data_ptr(),
+                                     0 if lr is None else lr.data_ptr())
+        return cp
+
 
 class TrackResult:
     """Device outputs of one TrackingChain.track call (valid once the stream reaches them)."""
@@ -296,6 +307,12 @@ class TrackingChainFrame(ctypes.Structure):  # orb_tracking_chain_frame_t
                 ("inv_level_sigma2", ctypes.c_void_p), ("pose7", ctypes.c_double * 7)]
 
 
+# The same record as a numpy dtype: track() fills a whole batch's records column-wise (the per-frame
+# ctypes constructions were half of a 512-frame call's host time)
+_CHAIN_FRAME_DTYPE = np.dtype([("p", "<u8", (10,)), ("pose7", "<f8", (7,))])
+assert _CHAIN_FRAME_DTYPE.itemsize == ctypes.sizeof(TrackingChainFrame)
+
+
 class TrackingChainBatchBuffers(ctypes.Structure):  # orb_tracking_chain_batch_buffers_t
     _fields_ = TrackingChainBuffers._fields_
 
@@ -371,6 +388,32 @@ class TrackingChainBatch:
             self.edge_kp[1].data_ptr(), self.outlier[0].data_ptr(), self.outlier[1].data_ptr(),
             self.poses.data_ptr(), self.inliers.data_ptr(), self.n_out.data_ptr(), self.taken.data_ptr(), None)
 
+    def _records(self, items):
+        """The batch's orb_tracking_chain_frame_t records (a numpy buffer of _CHAIN_FRAME_DTYPE), the
+        objects they point into, and the largest last-frame capacity and local map."""
+        nb = len(items)
+        rows, poses, keep = [], [], []
+        last_cap = n_local = 0
+        sf = self.scale_factor
+        for cur, last, local, pose7 in items:
+            if cur.cap != self.cap:
+                raise ValueError(f"frame capacity {cur.cap} differs from the batch's {self.cap}")
+            ff = cur.frustum_frame(sf)
+            lv = last.view()  # (refreshes the last frame's pose in its view)
+            mp = local.chain_pointers()
+            keep.append(ff)
+            rows.append((ctypes.addressof(cur.view()), ctypes.addressof(lv), mp[0], mp[1], mp[2], mp[3], mp[4], mp[5],
+                         ctypes.addressof(ff), cur.mvInvLevelSigma2.ctypes.data))
+            poses.append(pose7)
+            if last.cap > last_cap:
+                last_cap = last.cap
+            if local.n > n_local:
+                n_local = local.n
+        arr = np.empty(nb, _CHAIN_FRAME_DTYPE)
+        arr["p"] = np.array(rows, dtype=np.uint64)
+        arr["pose7"] = np.asarray(poses, dtype=np.float64).reshape(nb, 7)
+        return arr, keep, last_cap, n_local
+
     def track(self, items, stream=None, wide: bool = False) -> BatchTrackResult:
         """items: up to B tuples (cur DeviceFrame, DeviceLastPoints, DeviceLocalMap, pose7)."""
         import torch
@@ -379,21 +422,7 @@ class TrackingChainBatch:
             raise ValueError(f"{nb} frames for a batch of {self.B}")
         lib = _lib.load()
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
-        arr = (TrackingChainFrame * nb)()
-        keep = []
-        last_cap = n_local = 0
-        for b, (cur, last, local, pose7) in enumerate(items):
-            if cur.cap != self.cap:
-                raise ValueError(f"frame capacity {cur.cap} differs from the batch's {self.cap}")
-            fv, lv, mv, ff = cur.view(), last.view(), local.view(), cur.frustum_frame(self.scale_factor)
-            keep += [fv, lv, mv, ff]
-            lr = local.last_row
-            arr[b] = TrackingChainFrame(ctypes.addressof(fv), ctypes.addressof(lv), ctypes.addressof(mv),
-                                        local.pos.data_ptr(), local.normal.data_ptr(), local.min_dist.data_ptr(),
-                                        local.max_dist.data_ptr(), None if lr is None else lr.data_ptr(),
-                                        ctypes.addressof(ff), cur.mvInvLevelSigma2.ctypes.data,
-                                        (ctypes.c_double * 7)(*np.asarray(pose7, np.float64).reshape(7)))
-            last_cap, n_local = max(last_cap, last.cap), max(n_local, local.n)
+        arr, keep, last_cap, n_local = self._records(items)
         need = int(lib.orb_tracking_chain_batch_scratch_bytes(self.B, self.cap, last_cap, n_local))
         if need > self._scratch.numel():
             if self._scratch.numel():
@@ -402,8 +431,9 @@ class TrackingChainBatch:
             self._scratch = torch.empty(need, dtype=torch.uint8, device=self.device)
             self._bufs.scratch = self._scratch.data_ptr()
         self._params.th_motion = self.th_motion * (2 if wide else 1)
-        check(lib.orb_tracking_chain_batch_device(self._h_motion, self._h_local, nb, arr, ctypes.byref(self._params),
-                                                  ctypes.byref(self._bufs), ctypes.c_void_p(st.cuda_stream)),
+        check(lib.orb_tracking_chain_batch_device(self._h_motion, self._h_local, nb, arr.ctypes.data,
+                                                  ctypes.byref(self._params), ctypes.byref(self._bufs),
+                                                  ctypes.c_void_p(st.cuda_stream)),
               "orb_tracking_chain_batch_device")
         return BatchTrackResult(self, st, nb)
 
