@@ -422,7 +422,7 @@ class TrackingChainBatch:
             raise ValueError(f"{nb} frames for a batch of {self.B}")
         lib = _lib.load()
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
-        arr, keep, last_cap, n_local = self._records(items)
+        arr, keep, last_cap, n_local = self._records(items)  # keep: what the records point into, alive over the call
         need = int(lib.orb_tracking_chain_batch_scratch_bytes(self.B, self.cap, last_cap, n_local))
         if need > self._scratch.numel():
             if self._scratch.numel():
