@@ -1,6 +1,6 @@
 // ============================================================================================
 // ORACLE -- TEST INFRASTRUCTURE ONLY.  Never linked into, loaded by, or called from the product
-// path (orb-slam3_byzyh_amd/).  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+// product path (the HIP package).  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
 // leg may load liborb_oracle.so, and only as the checker / the timed CPU baseline.
 //
 // CPU restatement of ORB_SLAM3::ORBextractor (reference: src/ORBextractor.cc, include/ORBextractor.h)
