@@ -7,6 +7,8 @@ for stereo edges.  The erase decisions must be identical.
 """
 from __future__ import annotations
 
+import json
+
 import numpy as np
 import pytest
 
@@ -51,6 +53,17 @@ def test_local_ba_c5_parity(pkg, oracle, synth, solver, stereo_frac, seed):
           f"max |d chi2| {d.max():.3g} iterations {res['iterations']} trials {res['trials']}")
     # the final state improves on the initial one
     assert res["final_chi2"] < res["initial_chi2"]
+    # and against the committed record of the oracle's solution (tests/golden/ba_c5.npz)
+    from golden import fixtures as fx
+    name = {7: "c5_mono_seed7", 8: "c5_mixed_seed8"}.get(seed)
+    if name is not None:
+        g = fx.load_npz("ba_c5.npz")
+        assert fx.problem_sha(prob) == json.loads(g["meta_json"].tobytes())[name]["problem_sha256"]
+        assert np.array_equal(fx.ba_path(res), g[f"{name}__path"])
+        assert _rmse(pose[:, :3], g[f"{name}__pose"][:, :3]) < 1e-6
+        assert _rmse(_quat_aligned(pose[:, 3:], g[f"{name}__pose"][:, 3:]), g[f"{name}__pose"][:, 3:]) < 1e-6
+        assert _rmse(point, g[f"{name}__point"]) < 1e-6
+        assert np.array_equal(np.asarray(depth, np.uint8), g[f"{name}__depth"])
 
 
 def test_local_ba_small_and_edge_cases(pkg, oracle, synth, solver):

@@ -49,7 +49,20 @@ def chain(pkg, synth, oracle):
         ref.append((pkg.KeyFrame(keys_un=kl, descriptors=dl, Tcw=Tcw[f], camera=synth.EUROC_K, scale_factors=scale,
                                  level_sigma2=sigma2, u_right=ur, has_mappoint=has_mp[f, :len(kl)], feat_vec=fv), rbow))
     torch.cuda.synchronize()
-    return dict(dev=dev, ref=ref, bow=[t.cpu().numpy() for t in bow], counts=out_l[2].cpu().numpy(), n=n)
+    sides = {"left": (L, [t.cpu().numpy() for t in out_l]), "right": (R, [t.cpu().numpy() for t in out_r])}
+    return dict(dev=dev, ref=ref, bow=[t.cpu().numpy() for t in bow], counts=out_l[2].cpu().numpy(), n=n, sides=sides)
+
+
+def test_chain_extraction_golden(pkg, chain):
+    """The chain's device extraction of both sides of every stereo keyframe against the committed
+    records (tests/golden/extract.json, c3_left* / c3_right*)."""
+    from golden import fixtures as fx
+    golden = fx.load_json("extract.json")
+    for side, (imgs, (kps, desc, counts)) in chain["sides"].items():
+        for f in range(chain["n"]):
+            n = int(counts[f, 0])
+            k = np.ascontiguousarray(kps[f, :n]).view(np.uint8).reshape(n, 28).view(pkg.KEYPOINT_DTYPE).reshape(n)
+            fx.check_extract(golden[f"c3_{side}{f}"], imgs[f], k, desc[f, :n], int(counts[f, 1]), f"c3_{side}{f}")
 
 
 def test_chain_bow_stage(chain):
@@ -68,6 +81,8 @@ def test_chain_bow_stage(chain):
 def test_chain_search_for_triangulation(pkg, oracle, chain, only_stereo, coarse, check_ori):
     import torch
     n = chain["n"]
+    from golden import fixtures as fx
+    golden = fx.load_json("sft_c3.json")
     m = pkg.ORBmatcher(0.6, bool(check_ori))
     for k1 in (n - 1, 0):  # the newest keyframe against its predecessors, and the oldest against the rest
         nbrs = [f for f in range(n) if f != k1]
@@ -82,6 +97,8 @@ def test_chain_search_for_triangulation(pkg, oracle, chain, only_stereo, coarse,
             assert cnt[p] == rn, (k1, f, cnt[p], rn)
             assert np.array_equal(m12[p, :r1.N], rm), (k1, f, int((m12[p, :r1.N] != rm).sum()))
             assert (m12[p, r1.N:] == -1).all()
+            rec = golden[fx.sft_key(k1, f, (only_stereo, coarse, check_ori))]
+            assert rec == {"n": int(cnt[p]), "matches_sha256": fx.sha(np.asarray(m12[p, :r1.N], np.int32))}, (k1, f)
             total += rn
         assert total > 0
 

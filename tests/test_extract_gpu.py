@@ -48,6 +48,18 @@ def _first_diff(a, b):
     return f"{len(idx)} diffs, first at {idx[0].tolist()}: {a[tuple(idx[0])]} vs {b[tuple(idx[0])]}" if len(idx) else ""
 
 
+def test_c1_frame_against_golden(pkg, synth):
+    """C1 (seed 1, 640x480, N 1000, mono placement) on the device against the committed full dump
+    (tests/golden/c1_seed1.npz): keypoint records, descriptors and monoIndex byte for byte."""
+    from golden import fixtures as fx
+    g = fx.load_npz("c1_seed1.npz")
+    img = synth.polygon_frame(640, 480, seed=1)
+    kps, desc, mono = pkg.ORBextractor(1000, 1.2, 8, 20, 7, max_width=640, max_height=480)(img, None, (0, 1000))
+    assert np.array_equal(kps.view(np.uint8).reshape(-1, 28), g["kps"])
+    assert np.array_equal(desc, g["desc"]) and mono == int(g["mono"])
+    fx.check_extract(fx.load_json("extract.json")["c1_seed1"], img, kps, desc, mono, "c1_seed1")
+
+
 @pytest.mark.parametrize("case", CASES)
 def test_extract_parity(pkg, oracle, frames, case):
     img, nf, lap = frames[case]

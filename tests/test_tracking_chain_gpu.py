@@ -98,6 +98,14 @@ def test_tracking_chain_vs_oracle(pkg, oracle, synth, seed, stereo):
     for k in ("m1", "m2", "O1", "O2"):
         assert np.array_equal(e[k], o[k]), k
     assert np.abs(e["pose2"] - r["pose2"]).max() < 1e-6
+    # and against the committed record of the oracle chain (tests/golden/tracking.json)
+    from golden import fixtures as fx
+    g = fx.load_json("tracking.json")[f"scene{seed}"]
+    dev = fx.tracking_record(dict(n1=r["n1"], n2=r["n2"], I1=r["inliers"][0], I2=r["inliers"][1], n_kept=r["n_kept"],
+                                  n_map=r["n_map"], m1=r["m1"][:C.N], m2=r["m2"][:C.N], O1=r["outlier1"],
+                                  O2=r["outlier2"], pose2=g["pose2"]))
+    assert dev == g, seed
+    assert np.abs(r["pose2"] - np.asarray(g["pose2"])).max() < 1e-6
     # and the chain tracked: the final pose is closer to the truth than the prediction
     t = sc["pose7_true"]
     assert np.linalg.norm(r["pose2"][:3] - t[:3]) < 0.5 * np.linalg.norm(sc["pose7_pred"][:3] - t[:3])

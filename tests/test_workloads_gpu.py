@@ -45,7 +45,11 @@ def _run_in_flight(pkg, imgs, nf, w, h, lap, steps=8, handles=4, stamps=True):
     return outs
 
 
-def _check_against_oracle(pkg, oracle, frames, outs, nf, lap):
+def _check_against_oracle(pkg, oracle, frames, outs, nf, lap, golden_names=()):
+    """Every frame of every handle against the live oracle, and the frames named in golden_names against
+    the committed records (tests/golden/extract.json) as well."""
+    from golden import fixtures as fx
+    golden = fx.load_json("extract.json")
     ref = oracle.OracleExtractor(nf, 1.2, 8, 20, 7)
     counts = [o[2].cpu().numpy() for o in outs]
     total = 0
@@ -55,8 +59,12 @@ def _check_against_oracle(pkg, oracle, frames, outs, nf, lap):
             n = int(counts[hnd][f, 0])
             assert n == len(rk) and int(counts[hnd][f, 1]) == rm, f"handle {hnd} frame {f}: count/monoIndex"
             gk = pkg.keypoints_to_structured(kps[f], n)
+            gd = desc[f, :n].cpu().numpy()
             assert np.array_equal(gk.view(np.uint8), rk.view(np.uint8)), f"handle {hnd} frame {f} keypoints"
-            assert np.array_equal(desc[f, :n].cpu().numpy(), rd), f"handle {hnd} frame {f} descriptors"
+            assert np.array_equal(gd, rd), f"handle {hnd} frame {f} descriptors"
+            if f < len(golden_names):
+                fx.check_extract(golden[golden_names[f]], frames[f], gk, gd, int(counts[hnd][f, 1]),
+                                 f"handle {hnd} {golden_names[f]}")
         total += len(rk)
     return total
 
@@ -66,7 +74,7 @@ def test_c2_as_benched(pkg, oracle, synth):
     import torch
     frames = np.stack([synth.polygon_frame(640, 480, seed=100 + i) for i in range(64)])
     outs = _run_in_flight(pkg, torch.from_numpy(frames).cuda(), 1000, 640, 480, (0, 1000))
-    total = _check_against_oracle(pkg, oracle, frames, outs, 1000, (0, 1000))
+    total = _check_against_oracle(pkg, oracle, frames, outs, 1000, (0, 1000), [f"c2_seed{100 + i}" for i in range(64)])
     assert total > 60000
 
 
@@ -75,7 +83,7 @@ def test_c4_shard_as_benched(pkg, oracle, synth):
     import torch
     frames = np.stack([synth.polygon_frame(1280, 720, seed=1000 + i) for i in range(32)])
     outs = _run_in_flight(pkg, torch.from_numpy(frames).cuda(), 1000, 1280, 720, (0, 1000), stamps=False)
-    _check_against_oracle(pkg, oracle, frames, outs, 1000, (0, 1000))
+    _check_against_oracle(pkg, oracle, frames, outs, 1000, (0, 1000), [f"c4_seed{1000 + i}" for i in range(4)])
 
 
 def _rmse(a, b):
