@@ -16,17 +16,23 @@
  * (orb_extractor_level_download) fills the rest of the 19-pixel ring on the host by the REFLECT_101
  * rule of the reference's copyMakeBorder (:1712-1716, 1734-1736), so every byte reachable through the
  * view's ROI equals the reference's padded plane.
+ *
+ * Failures (orbgpu_status.hpp): nothing here throws on a library failure.  A handle that cannot be
+ * created leaves the scale getters on the host's restatement of the reference's tables
+ * (src/ORBextractor.cc:474-500) and every extraction failing; a failed extraction returns what the
+ * reference returns for an image without corners (no keypoints, descriptors released, monoIndex 0); a
+ * failed pyramid download leaves empty levels.  orbgpu::LastShimError() reports each.
  */
 #ifndef ORBGPU_CV_HPP
 #define ORBGPU_CV_HPP
 
-#include <stdexcept>
 #include <string>
 #include <vector>
 
 #include <opencv2/core/core.hpp>
 
 #include "orbgpu.h"
+#include "orbgpu_status.hpp"
 
 namespace orbgpu {
 
@@ -59,20 +65,24 @@ public:
                  int maxWidth = 1280, int maxHeight = 720)
         : nfeatures_(nfeatures), scaleFactor_(scaleFactor), nlevels_(nlevels) {
         orb_params_t p{nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST};
-        if (orb_extractor_create(&p, maxWidth, maxHeight, 1, &h_) != ORB_OK)
-            throw std::runtime_error(std::string("orb_extractor_create: ") + orb_last_error());
-        mvScaleFactor_.resize(nlevels);
-        mvInvScaleFactor_.resize(nlevels);
-        mvLevelSigma2_.resize(nlevels);
-        mvInvLevelSigma2_.resize(nlevels);
-        std::vector<int32_t> per(nlevels);
-        orb_extractor_scales(h_, mvScaleFactor_.data(), mvInvScaleFactor_.data(), mvLevelSigma2_.data(),
-                             mvInvLevelSigma2_.data(), per.data());
-        mvImagePyramid.resize(nlevels);
+        if (detail::Failed(orb_extractor_create(&p, maxWidth, maxHeight, 1, &h_), "orb_extractor_create")) h_ = nullptr;
+        const int nl = nlevels > 0 ? nlevels : 0;
+        mvScaleFactor_.resize(nl);
+        mvInvScaleFactor_.resize(nl);
+        mvLevelSigma2_.resize(nl);
+        mvInvLevelSigma2_.resize(nl);
+        std::vector<int32_t> per(nl);
+        if (!h_ || detail::Failed(orb_extractor_scales(h_, mvScaleFactor_.data(), mvInvScaleFactor_.data(),
+                                                       mvLevelSigma2_.data(), mvInvLevelSigma2_.data(), per.data()),
+                                  "orb_extractor_scales"))
+            HostScales();
+        mvImagePyramid.resize(nl);
     }
     // mvImagePyramid refers back to this object
     ORBextractor(ORBextractor&&) = delete;
-    ~ORBextractor() { orb_extractor_destroy(h_); }
+    ~ORBextractor() {
+        if (h_) orb_extractor_destroy(h_);
+    }
     ORBextractor(const ORBextractor&) = delete;
     ORBextractor& operator=(const ORBextractor&) = delete;
 
@@ -83,15 +93,17 @@ public:
         if (_image.empty()) return -1;
         cv::Mat image = _image.getMat();
         CV_Assert(image.type() == CV_8UC1);
+        pyramidStale_ = true;
         int cap = 2 * nfeatures_ + 64 * nlevels_;
         for (int attempt = 0; attempt < 2; ++attempt) {
             kps_.resize(cap);
             desc_.create(cap, 32, CV_8U);
             int n = 0;
-            int rc = orb_extract(h_, image.data, image.cols, image.rows, (int)image.step, vLappingArea[0],
-                                 vLappingArea[1], kps_.data(), desc_.data, cap, &n);
-            if (rc == ORB_ERR_CAPACITY) { cap = n; continue; }
-            if (rc < 0) throw std::runtime_error(std::string("orb_extract: ") + orb_last_error());
+            int rc = h_ ? orb_extract(h_, image.data, image.cols, image.rows, (int)image.step, vLappingArea[0],
+                                      vLappingArea[1], kps_.data(), desc_.data, cap, &n)
+                        : ORB_ERR_ARG;
+            if (rc == ORB_ERR_CAPACITY && attempt == 0 && n > cap) { cap = n; continue; }
+            if (detail::Failed(rc, h_ ? "orb_extract" : "orb_extract (no extractor handle)")) break;
             _keypoints.resize(n);
             for (int i = 0; i < n; ++i) {
                 const orb_keypoint_t& k = kps_[i];
@@ -99,10 +111,12 @@ public:
             }
             if (n == 0) _descriptors.release();
             else desc_.rowRange(0, n).copyTo(_descriptors);
-            pyramidStale_ = true;
             return rc;
         }
-        throw std::runtime_error("orb_extract: capacity retry failed");
+        // the reference's result for an image without corners
+        _keypoints.clear();
+        _descriptors.release();
+        return 0;
     }
 
     int inline GetLevels() { return nlevels_; }
@@ -116,15 +130,21 @@ public:
     // itself; an explicit call only moves the copy to a chosen point.
     void SyncPyramid() {
         if (!pyramidStale_) return;
-        for (int l = 0; l < nlevels_; ++l) {
+        pyramidStale_ = false;
+        for (int l = 0; l < nlevels_ && l < 12; ++l) {
             int w = 0, h = 0, pitch = 0;
-            if (orb_extractor_level(h_, 0, l, nullptr, &w, &h, &pitch) != ORB_OK)
-                throw std::runtime_error(std::string("orb_extractor_level: ") + orb_last_error());
-            padded_[l].create(h + 38, w + 38, CV_8U);
-            orb_extractor_level_download(h_, 0, l, padded_[l].data);
+            bool ok = !detail::Failed(h_ ? orb_extractor_level(h_, 0, l, nullptr, &w, &h, &pitch) : ORB_ERR_ARG,
+                                      "orb_extractor_level");
+            if (ok) {
+                padded_[l].create(h + 38, w + 38, CV_8U);
+                ok = !detail::Failed(orb_extractor_level_download(h_, 0, l, padded_[l].data), "orb_extractor_level_download");
+            }
+            if (!ok) {
+                for (auto& m : mvImagePyramid.levels_) m = cv::Mat();  // no pyramid: empty levels
+                return;
+            }
             mvImagePyramid.levels_[l] = padded_[l](cv::Rect(19, 19, w, h));
         }
-        pyramidStale_ = false;
     }
 
     LazyPyramid mvImagePyramid{this};
@@ -133,6 +153,19 @@ public:
     orb_extractor_t handle() const { return h_; }
 
 private:
+    // src/ORBextractor.cc:474-500 (scaleFactor is a double member; the tables are float)
+    void HostScales() {
+        const int nl = (int)mvScaleFactor_.size();
+        for (int i = 0; i < nl; ++i) {
+            mvScaleFactor_[i] = i == 0 ? 1.0f : (float)(mvScaleFactor_[i - 1] * scaleFactor_);
+            mvLevelSigma2_[i] = i == 0 ? 1.0f : mvScaleFactor_[i] * mvScaleFactor_[i];
+        }
+        for (int i = 0; i < nl; ++i) {
+            mvInvScaleFactor_[i] = 1.0f / mvScaleFactor_[i];
+            mvInvLevelSigma2_[i] = 1.0f / mvLevelSigma2_[i];
+        }
+    }
+
     orb_extractor_t h_ = nullptr;
     int nfeatures_;
     double scaleFactor_;

@@ -43,7 +43,11 @@
  *
  * Scope: pinhole single-camera frames and keyframes (the configuration the ABI covers).  For the
  * two-camera fisheye rig (mpCamera2 / Nleft != -1) Supports() is false and the caller keeps the
- * reference's CPU body.  Library failures throw std::runtime_error.
+ * reference's CPU body.
+ *
+ * Failures (orbgpu_status.hpp): nothing here throws.  A library failure returns the reference's result
+ * for a search that matches nothing -- 0, vMatchedPairs empty, no map point written -- and a failed
+ * ComputeDistinctiveDescriptors leaves every descriptor as it was; orbgpu::LastShimError() reports it.
  */
 #ifndef ORBGPU_MATCHER_HPP
 #define ORBGPU_MATCHER_HPP
@@ -52,13 +56,13 @@
 #include <map>
 #include <memory>
 #include <mutex>
-#include <stdexcept>
 #include <string>
 #include <tuple>
 #include <utility>
 #include <vector>
 
 #include "orbgpu.h"
+#include "orbgpu_status.hpp"
 
 namespace orbgpu {
 
@@ -72,9 +76,6 @@ struct TrackFields {
 };
 
 namespace detail {
-inline void Check(int rc, const char* what) {
-    if (rc < 0) throw std::runtime_error(std::string(what) + ": " + orb_last_error());
-}
 
 // One device matcher handle per (thread, nnratio, checkOri): the reference constructs ORBmatcher
 // objects on the stack per call site (e.g. src/LocalMapping.cc:536, src/Tracking.cc:4120), and a
@@ -86,7 +87,8 @@ public:
         auto it = handles_.find(key);
         if (it != handles_.end()) return it->second;
         orb_matcher_t h = nullptr;
-        Check(orb_matcher_create(nnratio, check_ori ? 1 : 0, &h), "orb_matcher_create");
+        if (Failed(orb_matcher_create(nnratio, check_ori ? 1 : 0, &h), "orb_matcher_create"))
+            return nullptr;  // not cached: the next call tries again
         handles_[key] = h;
         return h;
     }
@@ -200,9 +202,10 @@ public:
         }
         const int n1 = v1.view.n;
         std::vector<int32_t> m12((size_t)p * (n1 > 0 ? n1 : 1), -1), cnt(p, 0);
-        detail::Check(orb_search_for_triangulation(Handle(), &v1.view, views.data(), geoms.data(), (int)p,
-                                                   bOnlyStereo ? 1 : 0, bCoarse ? 1 : 0, m12.data(), cnt.data()),
-                      "orb_search_for_triangulation");
+        if (Failed(orb_search_for_triangulation(Handle(), &v1.view, views.data(), geoms.data(), (int)p,
+                                                bOnlyStereo ? 1 : 0, bCoarse ? 1 : 0, m12.data(), cnt.data()),
+                   "orb_search_for_triangulation"))
+            return counts;  // no pairs, 0 matches
         for (size_t k = 0; k < p; ++k) {
             auto& out = vvMatchedPairs[k];
             out.reserve(cnt[k]);
@@ -215,15 +218,22 @@ public:
         return counts;
     }
 
-    // src/ORBmatcher.cc:1951-2185.  Tracking clears CurrentFrame.mvpMapPoints before every call
-    // (src/Tracking.cc:4137,4156); the matches are written into it as the reference does
-    // (CurrentFrame.mvpMapPoints[i2] = LastFrame.mvpMapPoints[i]).
+    // src/ORBmatcher.cc:1951-2185.  The matches are written into CurrentFrame.mvpMapPoints as the
+    // reference does (CurrentFrame.mvpMapPoints[i2] = LastFrame.mvpMapPoints[i]); entries it does not
+    // match keep what they held.  Tracking clears the vector before every call (src/Tracking.cc:4137,
+    // 4156); a keypoint that already holds a map point with observations is skipped by every candidate
+    // search (:2038-2041), so the shim hides it from the grid (its copy of the keypoint is moved out of
+    // the frame bounds), which is the same skip for every last-frame point.
     int SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, const float th, const bool bMono) {
         auto& cur_mps = A::MapPoints(CurrentFrame);
-        for (MapPoint* m : cur_mps)
-            if (m) throw std::logic_error("orbgpu::ORBmatcher::SearchByProjection(Frame, Frame): CurrentFrame.mvpMapPoints "
-                                          "must be cleared first (as src/Tracking.cc:4137 does)");
-        const orb_frame_view_t cur = A::View(CurrentFrame);
+        orb_frame_view_t cur = A::View(CurrentFrame);
+        std::vector<orb_keypoint_t> hidden;
+        for (int i2 = 0; i2 < cur.n && i2 < (int)cur_mps.size(); ++i2) {
+            if (!cur_mps[i2] || A::Observations(cur_mps[i2]) <= 0) continue;
+            if (hidden.empty()) hidden.assign(cur.kps_un, cur.kps_un + cur.n);
+            hidden[i2].x = cur.min_x - 1e6f;  // outside every grid cell (Frame::PosInGrid fails)
+        }
+        if (!hidden.empty()) cur.kps_un = hidden.data();
         const orb_frame_view_t lastv = A::View(LastFrame);
         const auto& last_mps = A::MapPoints(LastFrame);
         const int nl = lastv.n;
@@ -247,8 +257,9 @@ public:
         for (int k = 0; k < 12; ++k) last.Tcw[k] = lastv.Tcw[k];
         std::vector<int32_t> match(cur.n > 0 ? cur.n : 1, -1);
         int32_t n = 0;
-        detail::Check(orb_search_by_projection_frame(Handle(), &cur, &last, th, bMono ? 1 : 0, match.data(), &n),
-                      "orb_search_by_projection_frame");
+        if (Failed(orb_search_by_projection_frame(Handle(), &cur, &last, th, bMono ? 1 : 0, match.data(), &n),
+                   "orb_search_by_projection_frame"))
+            return 0;
         for (int i2 = 0; i2 < cur.n; ++i2)
             if (match[i2] >= 0) cur_mps[i2] = last_mps[match[i2]];
         return n;
@@ -292,9 +303,10 @@ public:
         pts.desc = desc.data();
         std::vector<int32_t> match(fv.n > 0 ? fv.n : 1, -1);
         int32_t n = 0;
-        detail::Check(orb_search_by_projection_local(Handle(), &fv, taken.data(), &pts, th, bFarPoints ? 1 : 0,
-                                                     thFarPoints, match.data(), &n),
-                      "orb_search_by_projection_local");
+        if (Failed(orb_search_by_projection_local(Handle(), &fv, taken.data(), &pts, th, bFarPoints ? 1 : 0,
+                                                  thFarPoints, match.data(), &n),
+                   "orb_search_by_projection_local"))
+            return 0;
         for (int i = 0; i < fv.n; ++i)
             if (match[i] >= 0) fmps[i] = vpMapPoints[match[i]];  // F.mvpMapPoints[bestIdx] = pMP (:156)
         return n;
@@ -305,6 +317,7 @@ public:
 
 private:
     orb_matcher_t Handle() const { return detail::ThreadHandle(mfNNratio, mbCheckOrientation); }
+    static bool Failed(int rc, const char* what) { return detail::Failed(rc, what); }
 };
 
 // MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:438-529) for a batch of map points in one
@@ -341,9 +354,10 @@ void ComputeDistinctiveDescriptors(const std::vector<typename A::MapPoint*>& poi
     if (todo.empty()) return;
     std::vector<int32_t> best(todo.size());
     std::vector<uint8_t> out(32 * todo.size());
-    detail::Check(orb_compute_distinctive_descriptors(detail::ThreadHandle(0.6f, false), rows.data(), offsets.data(),
-                                                      (int)todo.size(), best.data(), out.data()),
-                  "orb_compute_distinctive_descriptors");
+    if (detail::Failed(orb_compute_distinctive_descriptors(detail::ThreadHandle(0.6f, false), rows.data(), offsets.data(),
+                                                           (int)todo.size(), best.data(), out.data()),
+                       "orb_compute_distinctive_descriptors"))
+        return;  // descriptors left as they were
     for (size_t p = 0; p < todo.size(); ++p) A::SetDescriptor(todo[p], &out[32 * p]);
 }
 

@@ -4,7 +4,11 @@
 //   * constructor: the orb_params_t it passes, the scale getters (include/ORBextractor.h:61-83);
 //   * operator() (src/ORBextractor.cc:1557-1682): the lapping area forwarded, keypoints converted
 //     field by field, descriptors as an n x 32 matrix, monoIndex returned, the ORB_ERR_CAPACITY retry
-//     with the needed count, an empty image returning -1, a library error as std::runtime_error;
+//     with the needed count, an empty image returning -1;
+//   * failures never throw (orbgpu_status.hpp): a library error, a second capacity shortfall, a handle
+//     that cannot be created (scale getters from the host restatement of src/ORBextractor.cc:474-500)
+//     and a failed pyramid download each give the reference's result for a frame without corners
+//     (no keypoints, descriptors released, monoIndex 0) or empty levels, with the code reported;
 //   * mvImagePyramid (read by Frame::ComputeStereoMatches as mvImagePyramid[octave],
 //     src/Frame.cc:1126,1249,1268,1275): downloaded on the first operator[] after an extraction and
 //     not again until the next one; each level a view at (19, 19) inside its padded plane, so the
@@ -27,7 +31,7 @@ static int g_fail = 0;
 // ---- ABI test doubles ---------------------------------------------------------------------------------
 static orb_params_t g_params;
 static int g_nfound = 37, g_extract_calls = 0, g_downloads = 0, g_last_cap = 0, g_lap[2];
-static bool g_fail_next = false;
+static bool g_fail_next = false, g_fail_create = false, g_fail_level = false, g_grow = false;
 static int g_handle_obj;
 
 static int level_w(int l) { return (int)std::lround(640 / std::pow(1.2, l)); }
@@ -36,6 +40,7 @@ static int level_h(int l) { return (int)std::lround(480 / std::pow(1.2, l)); }
 extern "C" {
 const char* orb_last_error(void) { return "mock failure"; }
 int orb_extractor_create(const orb_params_t* p, int, int, int, orb_extractor_t* out) {
+    if (g_fail_create) return ORB_ERR_DEVICE;
     g_params = *p;
     *out = (orb_extractor_t)&g_handle_obj;
     return ORB_OK;
@@ -54,6 +59,7 @@ int orb_extract(orb_extractor_t, const uint8_t* image, int w, int h, int stride,
     g_last_cap = cap, g_lap[0] = lx0, g_lap[1] = lx1;
     if (g_fail_next) { g_fail_next = false; return ORB_ERR_DEVICE; }
     if (!image || w != 640 || h != 480 || stride != 640) return ORB_ERR_ARG;
+    if (g_grow) g_nfound = cap + 1;  // never enough room
     *n = g_nfound;
     if (cap < g_nfound) return ORB_ERR_CAPACITY;
     for (int i = 0; i < g_nfound; ++i) {
@@ -63,7 +69,7 @@ int orb_extract(orb_extractor_t, const uint8_t* image, int w, int h, int stride,
     return g_nfound > 5 ? g_nfound - 5 : 0;  // monoIndex
 }
 int orb_extractor_level(orb_extractor_t, int frame, int l, const uint8_t**, int* w, int* h, int* pitch) {
-    if (frame != 0 || l < 0 || l >= g_params.nlevels) return ORB_ERR_ARG;
+    if (g_fail_level || frame != 0 || l < 0 || l >= g_params.nlevels) return ORB_ERR_ARG;
     *w = level_w(l), *h = level_h(l), *pitch = *w + 38;
     return ORB_OK;
 }
@@ -135,14 +141,51 @@ int main() {
 
     // empty image and library errors
     CHECK(ex(cv::Mat(), cv::Mat(), kps, desc, lap) == -1);
-    g_fail_next = true;
+    g_nfound = 37;
+    ex(img, cv::Mat(), kps, desc, lap);
+    CHECK(kps.size() == 37 && orbgpu::LastShimError() == ORB_OK);
+    const long fails0 = orbgpu::ShimFailureCount();
     bool threw = false;
     try {
-        ex(img, cv::Mat(), kps, desc, lap);
-    } catch (const std::runtime_error& e) {
-        threw = std::string(e.what()).find("mock failure") != std::string::npos;
+        g_fail_next = true;
+        CHECK(ex(img, cv::Mat(), kps, desc, lap) == 0 && kps.empty() && desc.empty());
+        CHECK(orbgpu::LastShimError() == ORB_ERR_DEVICE &&
+              orbgpu::LastShimMessage().find("mock failure") != std::string::npos);
+        orbgpu::ClearShimError();
+        g_grow = true;  // the capacity retry falls short again
+        CHECK(ex(img, cv::Mat(), kps, desc, lap) == 0 && kps.empty() && desc.empty());
+        CHECK(orbgpu::LastShimError() == ORB_ERR_CAPACITY);
+        g_grow = false;
+        g_nfound = 37;
+        orbgpu::ClearShimError();
+        CHECK(ex(img, cv::Mat(), kps, desc, lap) == 32 && kps.size() == 37 && orbgpu::LastShimError() == ORB_OK);
+        g_fail_level = true;  // pyramid download fails: empty levels
+        CHECK(ex.mvImagePyramid[2].empty() && ex.mvImagePyramid.size() == 8);
+        CHECK(orbgpu::LastShimError() == ORB_ERR_ARG);
+        g_fail_level = false;
+        // a handle that cannot be created
+        g_fail_create = true;
+        orbgpu::ClearShimError();
+        orbgpu::ORBextractor bad(1200, 1.2f, 8, 20, 7);
+        CHECK(orbgpu::LastShimError() == ORB_ERR_DEVICE);
+        float s = 1.0f;
+        const double sf = 1.2f;
+        for (int l = 0; l < 8; ++l) {  // src/ORBextractor.cc:474-500
+            if (l) s = (float)(s * sf);
+            CHECK(bad.GetScaleFactors()[l] == s && bad.GetScaleSigmaSquares()[l] == (l ? s * s : 1.0f));
+            CHECK(bad.GetInverseScaleFactors()[l] == 1.0f / s);
+        }
+        const int calls = g_extract_calls;
+        orbgpu::ClearShimError();
+        CHECK(bad(img, cv::Mat(), kps, desc, lap) == 0 && kps.empty() && desc.empty());
+        CHECK(g_extract_calls == calls && orbgpu::LastShimError() != ORB_OK);
+        CHECK(bad.mvImagePyramid[0].empty());
+        g_fail_create = false;
+    } catch (...) {
+        threw = true;
     }
-    CHECK(threw);
+    CHECK(!threw);
+    CHECK(orbgpu::ShimFailureCount() >= fails0 + 5);
 
     if (g_fail) return 1;
     std::printf("OK cv_shim_check\n");

@@ -117,6 +117,10 @@ int main(int argc, char** argv) {
         std::printf("FAIL exception: %s\n", e.what());
         return 1;
     }
+    if (orbgpu::LastShimError() != ORB_OK) {  // failures do not throw: every call must have succeeded
+        std::printf("FAIL shim error %d: %s\n", orbgpu::LastShimError(), orbgpu::LastShimMessage().c_str());
+        return 1;
+    }
     if (g_fail) {
         std::printf("%d checks failed\n", g_fail);
         return 1;

@@ -8,15 +8,18 @@
 //     form over several neighbours;
 //   * SearchByProjection(Frame, Frame) (:1951-2185): last-frame points valid only when non-NULL and
 //     not outliers (:1980-1984), their Observations() > 0, world positions, descriptors; the write of
-//     CurrentFrame.mvpMapPoints; the cleared-frame precondition (src/Tracking.cc:4137);
+//     CurrentFrame.mvpMapPoints; a frame that still holds map points: the ones with observations
+//     hidden from every candidate search (:2038-2041), the unmatched entries kept;
 //   * SearchByProjection(Frame, vector<MapPoint*>) (:46-240): keypoints already holding a map point
 //     with observations (:103-105), the tracking fields, the write of F.mvpMapPoints;
-//   * a library error surfaces as std::runtime_error; one device handle per (thread, nnratio, checkOri).
+//   * a library error never throws (orbgpu_status.hpp): every entry point returns the reference's
+//     empty result, leaves its outputs untouched and reports the ORB_ERR_* code through
+//     orbgpu::LastShimError(); a handle that cannot be created is retried on the next call; one
+//     device handle per (thread, nnratio, checkOri).
 #include <cstdio>
 #include <cstring>
 #include <map>
 #include <tuple>
-#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -127,7 +130,7 @@ struct FakeHandle {
     float nnratio;
     int check_ori;
 };
-static int g_creates = 0, g_rc = 0;
+static int g_creates = 0, g_rc = 0, g_create_rc = 0;
 static std::string g_err;
 // what the last call saw
 static struct {
@@ -141,7 +144,7 @@ static struct {
     FakeHandle* h = nullptr;
     orb_frame_view_t cur{};
     std::vector<uint8_t> valid, observed, taken, in_view, bad, desc;
-    std::vector<float> xyz, proj;
+    std::vector<float> xyz, proj, cur_x;
     std::vector<int32_t> level;
     float th = 0, th_far = 0;
     int mono = -1, far = -1;
@@ -160,6 +163,10 @@ static std::vector<uint8_t> g_dd_rows;
 static std::vector<int32_t> g_dd_off;
 int orb_compute_distinctive_descriptors(orb_matcher_t, const uint8_t* desc, const int32_t* offsets, int n_points,
                                         int32_t* best, uint8_t* out) {
+    if (g_rc) {
+        g_err = "fake failure";
+        return g_rc;
+    }
     g_dd_off.assign(offsets, offsets + n_points + 1);
     g_dd_rows.assign(desc, desc + 32 * (size_t)offsets[n_points]);
     for (int p = 0; p < n_points; ++p) {  // the double picks each point's last row
@@ -169,6 +176,10 @@ int orb_compute_distinctive_descriptors(orb_matcher_t, const uint8_t* desc, cons
     return ORB_OK;
 }
 int orb_matcher_create(float nnratio, int check_orientation, orb_matcher_t* out) {
+    if (g_create_rc) {
+        g_err = "fake create failure";
+        return g_create_rc;
+    }
     ++g_creates;
     *out = reinterpret_cast<orb_matcher_t>(new FakeHandle{nnratio, check_orientation});
     return ORB_OK;
@@ -202,8 +213,14 @@ int orb_search_for_triangulation(orb_matcher_t m, const orb_kf_view_t* kf1, cons
 }
 int orb_search_by_projection_frame(orb_matcher_t m, const orb_frame_view_t* cur, const orb_last_points_t* last,
                                    float th, int mono, int32_t* match, int32_t* n_matches) {
+    if (g_rc || !m) {
+        g_err = "fake failure";
+        return g_rc ? g_rc : ORB_ERR_ARG;
+    }
     g_seen.h = reinterpret_cast<FakeHandle*>(m);
     g_seen.cur = *cur;
+    g_seen.cur_x.clear();
+    for (int i = 0; i < cur->n; ++i) g_seen.cur_x.push_back(cur->kps_un[i].x);
     g_seen.th = th;
     g_seen.mono = mono;
     g_seen.valid.assign(last->valid, last->valid + last->n);
@@ -217,6 +234,10 @@ int orb_search_by_projection_frame(orb_matcher_t m, const orb_frame_view_t* cur,
 int orb_search_by_projection_local(orb_matcher_t m, const orb_frame_view_t* F, const uint8_t* frame_taken,
                                    const orb_local_points_t* pts, float th, int far_points, float th_far_points,
                                    int32_t* match, int32_t* n_matches) {
+    if (g_rc) {
+        g_err = "fake failure";
+        return g_rc;
+    }
     g_seen.h = reinterpret_cast<FakeHandle*>(m);
     g_seen.cur = *F;
     g_seen.taken.assign(frame_taken, frame_taken + F->n);
@@ -324,14 +345,22 @@ static void test_search_by_projection_frame() {
     CHECK(g_seen.th == 15.f && g_seen.mono == 1 && g_seen.cur.n == 5 && g_seen.cur.Tcw[3] == 0.5f);
     CHECK((cur.mps == std::vector<MockMP*>{nullptr, &b, nullptr, &a, nullptr}));
     CHECK(g_seen.h->nnratio == 0.9f && g_seen.h->check_ori == 1);
-    // a frame that still holds map points: the precondition Tracking guarantees
-    bool threw = false;
-    try {
-        matcher.SearchByProjection(cur, last, 15.f, true);
-    } catch (const std::logic_error&) {
-        threw = true;
-    }
-    CHECK(threw);
+    CHECK(g_seen.cur.kps_un == cur.kps.data());  // a cleared frame is passed as it is
+    // a frame that still holds map points (the reference has no precondition, src/ORBmatcher.cc:1951-2185):
+    // keypoint 3 holds a (observations 2): hidden from the candidate search; keypoint 1 holds b
+    // (no observations): still a candidate, and overwritten when matched
+    for (int i = 0; i < 5; ++i) cur.kps[i].x = 10.f * i;
+    MockMP d;
+    d.obs = 0;  // keypoint 2 holds d, also without observations: a candidate, kept when not matched
+    cur.mps = {nullptr, &b, &d, &a, nullptr};
+    g_match = {2, -1, -1, -1, 0};
+    g_counts = {2};
+    CHECK(matcher.SearchByProjection(cur, last, 15.f, true) == 2);
+    CHECK(g_seen.cur_x.size() == 5 && g_seen.cur_x[3] < -1e5f && g_seen.cur_x[1] == 10.f && g_seen.cur_x[2] == 20.f &&
+          g_seen.cur_x[4] == 40.f);
+    CHECK(g_seen.cur.kps_un != cur.kps.data() && cur.kps[3].x == 30.f);  // the frame's own keypoints untouched
+    CHECK((cur.mps == std::vector<MockMP*>{&b, &b, &d, &a, &a}));       // matched entries written, others kept
+    CHECK(orbgpu::LastShimError() == ORB_OK);
 }
 
 static void test_search_by_projection_local() {
@@ -372,16 +401,68 @@ static void test_errors_and_handles() {
     MockKF k1 = make_kf(3, 1), k2 = make_kf(3, 2);
     k1.fv[1] = {0, 1, 2};
     Matcher matcher(0.75f, true);
-    g_rc = ORB_ERR_ARG;
-    bool threw = false;
-    std::vector<std::pair<size_t, size_t>> pairs;
-    try {
-        matcher.SearchForTriangulation(&k1, &k2, pairs, false);
-    } catch (const std::runtime_error& e) {
-        threw = std::string(e.what()).find("fake failure") != std::string::npos;
+    std::vector<std::pair<size_t, size_t>> pairs{{7, 7}};
+    // every entry point on a library failure: no throw, the reference's empty result, the code reported
+    orbgpu::ClearShimError();
+    const long fails0 = orbgpu::ShimFailureCount();
+    for (int rc : {ORB_ERR_ARG, ORB_ERR_DEVICE, ORB_ERR_CAPACITY}) {
+        g_rc = rc;
+        bool threw = false;
+        try {
+            CHECK(matcher.SearchForTriangulation(&k1, &k2, pairs, false) == 0 && pairs.empty());
+            CHECK(orbgpu::LastShimError() == rc);
+            CHECK(orbgpu::LastShimMessage().find("fake failure") != std::string::npos);
+            MockMP held, lp;
+            lp.obs = 3;
+            MockFrame cur, last;
+            cur.kps.resize(3), cur.desc.resize(96), cur.ur.assign(3, -1.f), cur.outlier.assign(3, false);
+            cur.mps = {nullptr, &held, nullptr};
+            last.kps.resize(2), last.desc.resize(64), last.ur.assign(2, -1.f), last.outlier.assign(2, false);
+            last.mps = {&lp, &lp};
+            orbgpu::ClearShimError();
+            CHECK(matcher.SearchByProjection(cur, last, 7.f, false) == 0);
+            CHECK((cur.mps == std::vector<MockMP*>{nullptr, &held, nullptr}) && orbgpu::LastShimError() == rc);
+            const std::vector<MockMP*> pts{&lp};
+            orbgpu::ClearShimError();
+            CHECK(matcher.SearchByProjection(cur, pts, 3.f) == 0);
+            CHECK((cur.mps == std::vector<MockMP*>{nullptr, &held, nullptr}) && orbgpu::LastShimError() == rc);
+            MockKF K = make_kf(2, 9);
+            MockMP q;
+            q.obsmap[&K] = std::make_tuple(1, -1);
+            q.desc[0] = 0x5A;
+            orbgpu::ClearShimError();
+            orbgpu::ComputeDistinctiveDescriptors<Access>(std::vector<MockMP*>{&q});
+            CHECK(!q.desc_set && q.desc[0] == 0x5A && orbgpu::LastShimError() == rc);
+        } catch (...) {
+            threw = true;
+        }
+        CHECK(!threw);
     }
     g_rc = 0;
-    CHECK(threw);
+    CHECK(orbgpu::ShimFailureCount() == fails0 + 12);
+    // a handle that cannot be created: the search fails softly, and the next call creates it
+    g_create_rc = ORB_ERR_DEVICE;
+    orbgpu::ClearShimError();
+    {
+        MockFrame cur, last;
+        cur.kps.resize(2), cur.desc.resize(64), cur.ur.assign(2, -1.f), cur.mps.assign(2, nullptr);
+        last.kps.resize(1), last.desc.resize(32), last.ur.assign(1, -1.f), last.outlier.assign(1, false);
+        last.mps = {nullptr};
+        bool threw = false;
+        try {
+            CHECK(Matcher(0.31f, true).SearchByProjection(cur, last, 7.f, true) == 0);
+        } catch (...) {
+            threw = true;
+        }
+        CHECK(!threw && orbgpu::LastShimError() == ORB_ERR_ARG);  // the null handle, after the create failure
+        g_create_rc = 0;
+        const int c0 = g_creates;
+        g_match = {-1, -1};
+        g_counts = {0};
+        orbgpu::ClearShimError();
+        CHECK(Matcher(0.31f, true).SearchByProjection(cur, last, 7.f, true) == 0);
+        CHECK(g_creates == c0 + 1 && orbgpu::LastShimError() == ORB_OK);
+    }
     // handles: one per (thread, nnratio, checkOri), reused across ORBmatcher objects
     const int before = g_creates;
     g_match = {-1, -1, -1};
