@@ -629,15 +629,31 @@ int orb_tracking_local_seen_device(const int32_t* d_match_a, int cap, int last_c
  * -> PoseOptimization -> isInFrustum at the new pose + the seen skip -> discard -> SearchByProjection(F,
  * local points) -> PoseOptimization, every stage async on `stream`.  The caller owns the per-frame
  * device buffers (sized for frame->cap; m1 / m2 and the pose outputs are the results) and the local
- * map's tracking-field arrays (local->track_* are written by the frustum stage). */
+ * map's tracking-field arrays (local->track_* are written by the frustum stage).
+ *
+ * With params->motion_gate, TrackWithMotionModel's decisions run on the device with no host sync
+ * (src/Tracking.cc:4149-4217): fewer than 20 matches -> the search again with 2 th; still fewer than 20
+ * -> TrackWithMotionModel returns false: no PoseOptimization, no local-map stages; after the first
+ * PoseOptimization and the discard, nmatchesMap < 10 -> it returns false too and the local-map stages
+ * are skipped (the reference's Track() then runs TrackReferenceKeyFrame, the caller's).  The per-frame
+ * status word says which (ORB_TRACK_*).  For a frame that fails: m1 holds the last search's matches
+ * (status FAIL_SEARCH: not discarded, no graph: n_edges 0, pose1 = the motion model's pose) or the
+ * discarded ones (FAIL_MAP); m2 is all -1 and n_match[1] 0; the second graph is empty and pose2 is the
+ * pose the Frame keeps after TrackWithMotionModel (pose1 through Frame::SetPose's float round trip);
+ * the local map's track_* fields hold the frustum test at pose1 (no reference step reads them before
+ * recomputing them). */
+#define ORB_TRACK_RETRIED 1      /* the first search found < 20: the 2 th search ran */
+#define ORB_TRACK_FAIL_SEARCH 2  /* < 20 matches after the retry: TrackWithMotionModel false */
+#define ORB_TRACK_FAIL_MAP 4     /* nmatchesMap < 10 after PoseOptimization: TrackWithMotionModel false */
 typedef struct orb_tracking_chain_params {
-    float th_motion;            /* TrackWithMotionModel's th: 7 stereo, 15 otherwise (src/Tracking.cc:4141-4146);
-                                   the caller's nmatches < 20 retry passes 2 th */
+    float th_motion;            /* TrackWithMotionModel's th: 7 stereo, 15 otherwise (src/Tracking.cc:4141-4146) */
     int32_t mono;               /* bMono of SearchByProjection(F, LastFrame) */
     float th_local;             /* SearchLocalPoints' th (src/Tracking.cc:4801-4823) */
     int32_t far_points;         /* mpLocalMapper->mbFarPoints */
     float th_far_points;        /* mpLocalMapper->mThFarPoints */
     float viewing_cos_limit;    /* isInFrustum's 0.5 */
+    int32_t motion_gate;        /* 1: TrackWithMotionModel's retry / failure decisions on the device (above);
+                                   0: every stage runs on every frame with th_motion as given */
 } orb_tracking_chain_params_t;
 
 typedef struct orb_tracking_chain_buffers {
@@ -656,7 +672,8 @@ typedef struct orb_tracking_chain_buffers {
     int32_t* n_out;             /* 2: nmatches after the discard, nmatchesMap */
     uint8_t* taken;             /* cap: SearchLocalPoints' skip set */
     void* scratch;              /* orb_tracking_chain_scratch_bytes(cap, last cap, local points), reused stage
-                                   after stage on the stream; NULL: each stage allocates its own (stream-ordered) */
+                                   after stage on the stream (required) */
+    int32_t* status;            /* 1: ORB_TRACK_* bits (0: tracked by the motion model); NULL: not reported */
 } orb_tracking_chain_buffers_t;
 
 /* Scratch bytes of one chain call for frames of `cap` keypoints, a last frame of `last_cap` and `n_local`
@@ -712,11 +729,17 @@ typedef struct orb_tracking_chain_batch_buffers {
     int32_t* n_out;             /* B x 2 */
     uint8_t* taken;             /* B x cap */
     void* scratch;              /* orb_tracking_chain_batch_scratch_bytes(B, cap, max last cap, max local points) */
+    int32_t* status;            /* B: ORB_TRACK_* bits per frame; NULL: not reported */
 } orb_tracking_chain_batch_buffers_t;
 
 size_t orb_tracking_chain_batch_scratch_bytes(int n_frames, int cap, int last_cap, int n_local);
-/* Release the pinned host staging the batch calls keep for `scratch` (after its last call completed,
- * before the scratch is freed or reused for something else).  A NULL or unknown scratch is a no-op. */
+/* Release the pinned host staging the batch calls keep for `scratch`: waits until the last call made
+ * with it has finished on the device (every kernel, not only its argument copies), then frees the
+ * staging; call it before the scratch or the call's output buffers are freed or reused for something
+ * else.  A NULL or unknown scratch is a no-op.
+ * Memory: the scratch holds, per frame, the SearchByProjection candidate lists (8 B per (point,
+ * keypoint) pair: cap x max(last cap, local points) x 8 B) -- e.g. cap 2048 and 2048 points: 32 MiB per
+ * frame, 16 GiB for 512 frames; orb_tracking_chain_batch_scratch_bytes gives the exact size. */
 int orb_tracking_chain_batch_release(void* scratch);
 int orb_tracking_chain_batch_device(orb_matcher_t m_motion, orb_matcher_t m_local, int n_frames,
                                     const orb_tracking_chain_frame_t* frames, const orb_tracking_chain_params_t* params,

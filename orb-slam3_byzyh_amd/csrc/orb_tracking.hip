@@ -10,6 +10,14 @@
 //                         the start pose is the frame's (host) or the previous optimisation's (device).
 //   k_track_discard       TrackWithMotionModel's outlier discard (src/Tracking.cc:4180-4203): a keypoint
 //                         whose edge came back an outlier loses its map point; counts nmatchesMap.
+//   k_track_gate_*        TrackWithMotionModel's decisions (src/Tracking.cc:4149-4217) on the device: the
+//                         2 th retry of the search, and the frame's failure (< 20 matches after it, or
+//                         nmatchesMap < 10 after PoseOptimization).  They write per-frame gated counts --
+//                         the frame's keypoint count, or 0 -- that the later stages read in place of the
+//                         frame's own count: a stage on a 0-keypoint frame builds no grid, finds no
+//                         match and no edge, so a failed frame's remaining launches do no work and
+//                         write the "not run" outputs, with no host round trip and no change to the
+//                         stage kernels.
 // Map points are referenced by index into a device table of world positions (float xyz, as
 // MapPoint::GetWorldPos returns them); a keypoint's map point comes from the second match array when it
 // has one there (SearchByProjection(F, local points) overwrites, src/ORBmatcher.cc:156), else the first.
@@ -262,18 +270,130 @@ __global__ __launch_bounds__(kThreads) void k_track_local_seen_b(const k_track_l
     k_track_local_seen_body(A.match_a, A.cap, A.last_cap, A.last_row, A.n_local, A.in_view);
 }
 
+// ---- TrackWithMotionModel's decisions (src/Tracking.cc:4149-4217)
+constexpr int kMinMotionMatches = 20;  // nmatches < 20: the 2 th search, then failure (:4153, :4163)
+constexpr int kMinMapMatches = 10;     // return nmatchesMap >= 10 (:4216)
+
+// Per frame: the counts the gated stages read as their frame's (or last frame's) keypoint count, the
+// 2 th search's count, and its matches at m1w (cap entries) in the scratch.
+struct ChainGate {
+    int32_t n_wide;    // the 2 th search's current-frame count: N when it runs, else 0
+    int32_t nl_wide;   // its last-frame count
+    int32_t n_alive1;  // PoseOptimization's graph / the discard: N unless the search failed
+    int32_t n_alive2;  // the local-map stages: N unless TrackWithMotionModel failed
+    int32_t n1w;       // the 2 th search's match count
+    int32_t status;    // ORB_TRACK_* bits (copied to the caller's status word)
+    int32_t pad[2];
+};
+static_assert(sizeof(ChainGate) == 32, "gate record");
+
+struct GateArgs {
+    ChainGate* g;
+    const int32_t* cur_n;     // the frame's keypoint count (device)
+    const int32_t* last_n;    // the last frame's
+    int32_t* n1;              // SearchByProjection(LastFrame)'s count (n_match[0])
+    int32_t* m1;              // its matches (cap)
+    const int32_t* m1w;       // the 2 th search's matches (cap)
+    const orb_pose_frame_t* frame1;
+    const int32_t* edge_kp1;
+    const uint8_t* outlier1;
+    const uint8_t* observed;  // the last frame's map points' Observations() > 0 (NULL: all)
+    int32_t* status;          // the caller's status word, or NULL
+    int cap;
+};
+
+// after the first search: < 20 matches -> the 2 th search runs (its counts are the frame's)
+__device__ __forceinline__ void k_track_gate_retry_body(const GateArgs& a) {
+    if (threadIdx.x) return;
+    const bool retry = *a.n1 < kMinMotionMatches;
+    a.g->n_wide = retry ? *a.cur_n : 0;
+    a.g->nl_wide = retry ? *a.last_n : 0;
+    a.g->status = retry ? ORB_TRACK_RETRIED : 0;
+}
+__global__ __launch_bounds__(64) void k_track_gate_retry(GateArgs a) { k_track_gate_retry_body(a); }
+__global__ __launch_bounds__(64) void k_track_gate_retry_b(const GateArgs* __restrict__ a) {
+    k_track_gate_retry_body(a[blockIdx.y]);
+}
+
+// after the 2 th search: its matches replace the first ones (Tracking.cc:4156-4158 clears and searches
+// again); still < 20 -> TrackWithMotionModel returns false (:4161-4168): no graph, no local-map stages
+__device__ __forceinline__ void k_track_gate_search_body(const GateArgs& a) {
+    const int st = a.g->status;
+    if (st & ORB_TRACK_RETRIED)
+        for (int i = threadIdx.x; i < a.cap; i += kThreads) a.m1[i] = a.m1w[i];
+    __syncthreads();
+    if (threadIdx.x) return;
+    int n = *a.n1;
+    if (st & ORB_TRACK_RETRIED) *a.n1 = n = a.g->n1w;
+    const bool ok = n >= kMinMotionMatches;
+    a.g->n_alive1 = a.g->n_alive2 = ok ? *a.cur_n : 0;
+    a.g->status = ok ? st : (st | ORB_TRACK_FAIL_SEARCH);
+    if (a.status) *a.status = a.g->status;
+}
+__global__ __launch_bounds__(kThreads) void k_track_gate_search(GateArgs a) { k_track_gate_search_body(a); }
+__global__ __launch_bounds__(kThreads) void k_track_gate_search_b(const GateArgs* __restrict__ a) {
+    k_track_gate_search_body(a[blockIdx.y]);
+}
+
+// after the first PoseOptimization: nmatchesMap (the kept edges whose map point has observations,
+// :4176-4203, as the discard counts it) < 10 -> TrackWithMotionModel returns false (:4216)
+__device__ __forceinline__ void k_track_gate_map_body(const GateArgs& a) {
+    __shared__ int obs;
+    const int st = a.g->status;
+    if (st & ORB_TRACK_FAIL_SEARCH) return;  // (uniform: the whole block leaves)
+    if (threadIdx.x == 0) obs = 0;
+    __syncthreads();
+    const int ne = a.frame1->n_edges;
+    int o = 0;
+    for (int e = threadIdx.x; e < ne; e += kThreads)
+        if (!a.outlier1[e]) o += a.observed ? a.observed[a.m1[a.edge_kp1[e]]] != 0 : 1;
+    for (int off = 32; off > 0; off >>= 1) o += __shfl_xor(o, off, 64);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&obs, o);
+    __syncthreads();
+    if (threadIdx.x) return;
+    if (obs < kMinMapMatches) {
+        a.g->n_alive2 = 0;
+        a.g->status = st | ORB_TRACK_FAIL_MAP;
+    }
+    if (a.status) *a.status = a.g->status;
+}
+__global__ __launch_bounds__(kThreads) void k_track_gate_map(GateArgs a) { k_track_gate_map_body(a); }
+__global__ __launch_bounds__(kThreads) void k_track_gate_map_b(const GateArgs* __restrict__ a) {
+    k_track_gate_map_body(a[blockIdx.y]);
+}
+
+// A frame view whose keypoint count is read from `n` (a gate word) instead of the frame's own
+__host__ orb_frame_device_t gated(const orb_frame_device_t* F, const int32_t* n) {
+    orb_frame_device_t G = *F;
+    G.n = n;
+    return G;
+}
+__host__ orb_last_points_device_t gated(const orb_last_points_device_t* L, const int32_t* n) {
+    orb_last_points_device_t G = *L;
+    G.n = n;
+    return G;
+}
+
+// Tracking-chain scratch: the stages' region, then the gate record and the 2 th search's matches
+size_t stage_bytes(int cap, int last_cap, int n_local) {
+    return (std::max({orbgpu_sbp_frame_scratch_bytes(cap, last_cap), orbgpu_sbp_local_scratch_bytes(cap, n_local),
+                      (size_t)cap * sizeof(double)}) + 255) & ~(size_t)255;
+}
+
 // the batch's argument areas: one per stage, each room for B frames' largest argument blocks (the
-// SearchByProjection stages pack five kernels' blocks, 256-B aligned)
-constexpr int kBatchArgStages = 7;
+// SearchByProjection stages pack five kernels' blocks, 256-B aligned); 7-10: the 2 th search and the gates
+constexpr int kBatchArgStages = 11;
 size_t batch_args_bytes(int B) { return ((size_t)B * 4096 + 8 * 256 + 255) & ~(size_t)255; }
 
 // The pinned host side of a batch's argument areas, one per batch scratch (the caller's batch object),
-// and an event after the call's last copy: the next call on that scratch writes the staging only once
-// the previous call's copies have read it (stream-ordered copies read pinned memory when they run).
+// and events after the call's copies and after its last launch: the next call on that scratch writes the
+// staging only once the previous call's copies have read it (stream-ordered copies read pinned memory
+// when they run); release waits for the whole call.
 struct BatchStaging {
     void* host = nullptr;
     size_t bytes = 0;
-    hipEvent_t copied = nullptr;
+    hipEvent_t copied = nullptr;  // after the call's last argument copy
+    hipEvent_t done = nullptr;    // after the call's last launch
 };
 std::mutex g_staging_mu;
 std::unordered_map<const void*, BatchStaging> g_staging;
@@ -329,8 +449,7 @@ int orb_tracking_discard_outliers_device(const orb_pose_frame_t* d_frame, const 
 
 size_t orb_tracking_chain_scratch_bytes(int cap, int last_cap, int n_local) {
     if (cap <= 0 || last_cap < 0 || n_local < 0) return 0;
-    return std::max({orbgpu_sbp_frame_scratch_bytes(cap, last_cap), orbgpu_sbp_local_scratch_bytes(cap, n_local),
-                     (size_t)cap * sizeof(double)});
+    return stage_bytes(cap, last_cap, n_local) + 256 + (((size_t)cap * sizeof(int32_t) + 255) & ~(size_t)255);
 }
 
 int orb_tracking_chain_device(orb_matcher_t m_motion, orb_matcher_t m_local, const orb_frame_device_t* F,
@@ -342,19 +461,40 @@ int orb_tracking_chain_device(orb_matcher_t m_motion, orb_matcher_t m_local, con
                               void* stream) {
     if (!m_motion || !m_local || !F || !last || !local || !frustum || !inv_level_sigma2 || !pose7 || !P || !B ||
         !B->m1 || !B->m2 || !B->n_match || !B->frames || !B->edges1 || !B->edges2 || !B->edge_kp1 || !B->edge_kp2 ||
-        !B->outlier1 || !B->outlier2 || !B->poses || !B->inliers || !B->n_out || !B->taken ||
+        !B->outlier1 || !B->outlier2 || !B->poses || !B->inliers || !B->n_out || !B->taken || !B->scratch ||
+        F->cap <= 0 || last->cap < 0 || last->cap > kSeenBits || local->n < 0 || !last->n ||
         (local->n > 0 && (!d_pos || !d_normal || !d_min_dist || !d_max_dist)))
         return orbgpu_fail(ORB_ERR_ARG, "bad tracking chain arguments");
+    hipStream_t s = (hipStream_t)stream;
     int rc;
     void* const z = B->scratch;  // stream order: each stage's scratch is free again when the next one runs
+    char* const tail = static_cast<char*>(z) + stage_bytes(F->cap, last->cap, local->n);
+    ChainGate* const g = reinterpret_cast<ChainGate*>(tail);
+    int32_t* const m1w = reinterpret_cast<int32_t*>(tail + 256);
+    const bool gate = P->motion_gate != 0;
+    GateArgs ga{g, F->n, last->n, B->n_match, B->m1, m1w, B->frames, B->edge_kp1, B->outlier1, last->observed,
+                B->status, F->cap};
+    // the stages after a gate read the gated counts (the frame's own count when gating is off)
+    const orb_frame_device_t F1 = gate ? gated(F, &g->n_alive1) : *F, F2 = gate ? gated(F, &g->n_alive2) : *F;
     if ((rc = orbgpu_sbp_frame_device_scratch(m_motion, F, last, P->th_motion, P->mono, B->m1, B->n_match, stream, z)))
         return rc;
-    if ((rc = orb_tracking_pose_edges_device(F, B->m1, last->xyz, nullptr, nullptr, inv_level_sigma2, nullptr, pose7,
+    if (gate) {  // TrackWithMotionModel's retry (src/Tracking.cc:4153-4160)
+        hipLaunchKernelGGL(k_track_gate_retry, dim3(1), dim3(64), 0, s, ga);
+        const orb_frame_device_t Fw = gated(F, &g->n_wide);
+        const orb_last_points_device_t Lw = gated(last, &g->nl_wide);
+        if ((rc = orbgpu_sbp_frame_device_scratch(m_motion, &Fw, &Lw, 2 * P->th_motion, P->mono, m1w, &g->n1w, stream, z)))
+            return rc;
+        hipLaunchKernelGGL(k_track_gate_search, dim3(1), dim3(kThreads), 0, s, ga);
+    } else if (B->status && hipMemsetAsync(B->status, 0, sizeof(int32_t), s) != hipSuccess) {
+        return orbgpu_fail(ORB_ERR_DEVICE, "tracking chain status reset failed");
+    }
+    if ((rc = orb_tracking_pose_edges_device(&F1, B->m1, last->xyz, nullptr, nullptr, inv_level_sigma2, nullptr, pose7,
                                              B->frames, B->edges1, B->edge_kp1, stream)))
         return rc;
     if ((rc = orbgpu_pose_optimization_device_scratch(1, B->frames, F->cap, B->edges1, B->poses, B->outlier1, B->inliers,
                                                       stream, static_cast<double*>(z))))
         return rc;
+    if (gate) hipLaunchKernelGGL(k_track_gate_map, dim3(1), dim3(kThreads), 0, s, ga);  // (:4216)
     // isInFrustum at the first pose and the seen skip read the first search's assignments, which the
     // discard does not change (the reference marks its discarded outliers seen too, Tracking.cc:4195)
     if (local->n > 0) {
@@ -372,11 +512,11 @@ int orb_tracking_chain_device(orb_matcher_t m_motion, orb_matcher_t m_local, con
     if ((rc = orb_tracking_discard_outliers_device(B->frames, B->edge_kp1, B->outlier1, B->m1, last->observed, nullptr,
                                                    nullptr, B->n_out, F->cap, B->taken, stream)))
         return rc;
-    if ((rc = orbgpu_sbp_local_device_scratch(m_local, F, B->taken, local, P->th_local, P->far_points, P->th_far_points,
+    if ((rc = orbgpu_sbp_local_device_scratch(m_local, &F2, B->taken, local, P->th_local, P->far_points, P->th_far_points,
                                               B->m2, B->n_match + 1, stream, z)))
         return rc;
     const bool has_local = local->n > 0;  // an empty local map: the second search assigned nothing
-    if ((rc = orb_tracking_pose_edges_device(F, B->m1, last->xyz, has_local ? B->m2 : nullptr, has_local ? d_pos : nullptr,
+    if ((rc = orb_tracking_pose_edges_device(&F2, B->m1, last->xyz, has_local ? B->m2 : nullptr, has_local ? d_pos : nullptr,
                                              inv_level_sigma2, B->poses, nullptr, B->frames + 1, B->edges2, B->edge_kp2,
                                              stream)))
         return rc;
@@ -389,7 +529,9 @@ size_t orb_tracking_chain_batch_scratch_bytes(int n_frames, int cap, int last_ca
     const size_t stride = (std::max(orbgpu_sbp_frame_scratch_bytes(cap, last_cap),
                                     orbgpu_sbp_local_scratch_bytes(cap, n_local)) + 255) & ~(size_t)255;
     const size_t args = (size_t)kBatchArgStages * batch_args_bytes(n_frames);
-    return args + (size_t)n_frames * stride + (size_t)n_frames * cap * sizeof(double) + 256;
+    const size_t chi = ((size_t)n_frames * cap * sizeof(double) + 255) & ~(size_t)255;
+    const size_t gates = ((size_t)n_frames * sizeof(ChainGate) + 255) & ~(size_t)255;
+    return args + (size_t)n_frames * stride + chi + gates + (size_t)n_frames * cap * sizeof(int32_t) + 256;
 }
 
 int orb_tracking_chain_batch_release(void* scratch) {
@@ -397,6 +539,10 @@ int orb_tracking_chain_batch_release(void* scratch) {
     auto it = g_staging.find(scratch);
     if (it == g_staging.end()) return ORB_OK;
     BatchStaging& stg = it->second;
+    if (stg.done) {  // the last call's every kernel (its outputs and the scratch are free afterwards)
+        (void)hipEventSynchronize(stg.done);
+        (void)hipEventDestroy(stg.done);
+    }
     if (stg.copied) {
         (void)hipEventSynchronize(stg.copied);
         (void)hipEventDestroy(stg.copied);
@@ -413,22 +559,38 @@ int orb_tracking_chain_batch_device(orb_matcher_t m_motion, orb_matcher_t m_loca
         !Bf->edges1 || !Bf->edges2 || !Bf->edge_kp1 || !Bf->edge_kp2 || !Bf->outlier1 || !Bf->outlier2 || !Bf->poses ||
         !Bf->inliers || !Bf->n_out || !Bf->taken || !Bf->scratch)
         return orbgpu_fail(ORB_ERR_ARG, "bad tracking chain batch arguments");
+    // every per-frame check before the first copy or launch: a refused call enqueues nothing
     int C = 0, NL = 0, NP = 0;
     for (int b = 0; b < B; ++b) {
         const orb_tracking_chain_frame_t& f = fr[b];
         if (!f.frame || !f.last || !f.local || !f.frustum || !f.inv_level_sigma2 || f.frame->cap <= 0 ||
-            (b && f.frame->cap != C) || f.frame->nlevels <= 0 || f.frame->nlevels > kMaxLevels || f.last->cap > kSeenBits ||
-            (f.local->n > 0 && (!f.pos || !f.normal || !f.min_dist || !f.max_dist)))
+            (b && f.frame->cap != C) || f.frame->nlevels <= 0 || f.frame->nlevels > kMaxLevels || !f.frame->n ||
+            !f.frame->kps_un || !f.last->n || f.last->cap < 0 || f.last->cap > kSeenBits || f.local->n < 0 ||
+            f.frustum->n_levels <= 0 ||
+            (f.local->n > 0 && (!f.pos || !f.normal || !f.min_dist || !f.max_dist || !f.local->track_in_view ||
+                                !f.local->track_proj || !f.local->track_depth || !f.local->track_level ||
+                                !f.local->track_view_cos || !f.local->is_bad || !f.local->observed || !f.local->desc ||
+                                (reinterpret_cast<uintptr_t>(f.local->desc) & 15))))
             return orbgpu_fail(ORB_ERR_ARG, "bad tracking chain batch frame (every frame the same cap)");
         C = f.frame->cap;
         NL = std::max(NL, f.last->cap);
         NP = std::max(NP, f.local->n);
     }
     hipStream_t s = (hipStream_t)stream;
-    // scratch: argument areas (one per stage) | the frames' SearchByProjection scratch | PoseOptimization chi2
+    const bool gate = P->motion_gate != 0;
+    // scratch: argument areas (one per stage) | the frames' SearchByProjection scratch | PoseOptimization chi2 |
+    // gate records | the 2 th search's matches
     const size_t abytes = batch_args_bytes(B);
     char* base = static_cast<char*>(Bf->scratch);
     auto args = [&](int stage) { return static_cast<void*>(base + (size_t)stage * abytes); };
+    const size_t stride = (std::max(orbgpu_sbp_frame_scratch_bytes(C, NL), orbgpu_sbp_local_scratch_bytes(C, NP)) + 255) &
+                          ~(size_t)255;
+    char* sbp = base + (size_t)kBatchArgStages * abytes;
+    double* chi = reinterpret_cast<double*>(sbp + (size_t)B * stride);
+    ChainGate* gates = reinterpret_cast<ChainGate*>(reinterpret_cast<char*>(chi) +
+                                                    (((size_t)B * C * sizeof(double) + 255) & ~(size_t)255));
+    int32_t* m1w = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(gates) +
+                                              (((size_t)B * sizeof(ChainGate) + 255) & ~(size_t)255));
     std::lock_guard<std::mutex> lock(g_staging_mu);
     BatchStaging& stg = g_staging[Bf->scratch];
     if (stg.copied && hipEventSynchronize(stg.copied) != hipSuccess)
@@ -441,18 +603,32 @@ int orb_tracking_chain_batch_device(orb_matcher_t m_motion, orb_matcher_t m_loca
             return orbgpu_fail(ORB_ERR_DEVICE, "hipHostMalloc failed");
         stg.bytes = (size_t)kBatchArgStages * abytes;
     }
-    if (!stg.copied && hipEventCreateWithFlags(&stg.copied, hipEventDisableTiming) != hipSuccess)
+    if ((!stg.copied && hipEventCreateWithFlags(&stg.copied, hipEventDisableTiming) != hipSuccess) ||
+        (!stg.done && hipEventCreateWithFlags(&stg.done, hipEventDisableTiming) != hipSuccess))
         return orbgpu_fail(ORB_ERR_DEVICE, "hipEventCreate failed");
+    // from here on every exit marks the staging's copies (the next call waits for them before it
+    // rewrites the staging) and the call's end (release waits for it)
+    struct Marks {
+        BatchStaging& stg;
+        hipStream_t s;
+        bool copied = false;
+        void Copied() {
+            copied = hipEventRecord(stg.copied, s) == hipSuccess;
+        }
+        ~Marks() {
+            if (!copied) (void)hipEventRecord(stg.copied, s);
+            (void)hipEventRecord(stg.done, s);
+        }
+    } marks{stg, s};
     auto hargs = [&](int stage) { return static_cast<void*>(static_cast<char*>(stg.host) + (size_t)stage * abytes); };
-    const size_t stride = (std::max(orbgpu_sbp_frame_scratch_bytes(C, NL), orbgpu_sbp_local_scratch_bytes(C, NP)) + 255) &
-                          ~(size_t)255;
-    char* sbp = base + (size_t)kBatchArgStages * abytes;
-    double* chi = reinterpret_cast<double*>(sbp + (size_t)B * stride);
-    std::vector<const orb_frame_device_t*> cur(B);
-    std::vector<const orb_last_points_device_t*> last(B);
+    std::vector<const orb_frame_device_t*> cur(B), cur1(B), cur2(B), curw(B);
+    std::vector<const orb_last_points_device_t*> last(B), lastw(B);
+    std::vector<orb_frame_device_t> g1(B), g2(B), gw(B);
+    std::vector<orb_last_points_device_t> glw(B);
     std::vector<const orb_local_points_device_t*> loc(B);
-    std::vector<int32_t*> m1(B), m2(B), n1(B), n2(B);
+    std::vector<int32_t*> m1(B), m2(B), n1(B), n2(B), mw(B), nw(B);
     std::vector<const uint8_t*> taken(B);
+    std::vector<GateArgs> ga(B);
     for (int b = 0; b < B; ++b) {
         cur[b] = fr[b].frame;
         last[b] = fr[b].last;
@@ -461,20 +637,48 @@ int orb_tracking_chain_batch_device(orb_matcher_t m_motion, orb_matcher_t m_loca
         m2[b] = Bf->m2 + (size_t)b * C;
         n1[b] = Bf->n_match + 2 * (size_t)b;
         n2[b] = n1[b] + 1;
+        mw[b] = m1w + (size_t)b * C;
+        nw[b] = &gates[b].n1w;
         taken[b] = Bf->taken + (size_t)b * C;
+        g1[b] = gate ? gated(cur[b], &gates[b].n_alive1) : *cur[b];
+        g2[b] = gate ? gated(cur[b], &gates[b].n_alive2) : *cur[b];
+        gw[b] = gated(cur[b], &gates[b].n_wide);
+        glw[b] = gated(last[b], &gates[b].nl_wide);
+        cur1[b] = &g1[b];
+        cur2[b] = &g2[b];
+        curw[b] = &gw[b];
+        lastw[b] = &glw[b];
+        ga[b] = GateArgs{&gates[b], cur[b]->n, last[b]->n, n1[b], m1[b], mw[b], Bf->frames + b, Bf->edge_kp1 + (size_t)b * C,
+                         Bf->outlier1 + (size_t)b * C, last[b]->observed, Bf->status ? Bf->status + b : nullptr, C};
     }
     orb_pose_frame_t* fr1 = Bf->frames;
     orb_pose_frame_t* fr2 = Bf->frames + B;
     double* pose1 = Bf->poses;
     double* pose2 = Bf->poses + 7 * (size_t)B;
+    auto upload = [&](int stage, const void* h, size_t n) {
+        if (n > abytes) return false;
+        memcpy(hargs(stage), h, n);
+        return hipMemcpyAsync(args(stage), hargs(stage), n, hipMemcpyHostToDevice, s) == hipSuccess;
+    };
     int rc;
     if ((rc = orbgpu_sbp_frame_batch(m_motion, B, cur.data(), last.data(), P->th_motion, P->mono, m1.data(), n1.data(),
                                      sbp, stride, args(0), hargs(0), abytes, s)))
         return rc;
+    if (gate) {  // TrackWithMotionModel's retry and failure (src/Tracking.cc:4153-4168)
+        if (!upload(7, ga.data(), B * sizeof(ga[0]))) return orbgpu_fail(ORB_ERR_DEVICE, "batch argument upload failed");
+        const GateArgs* dga = static_cast<const GateArgs*>(args(7));
+        hipLaunchKernelGGL(k_track_gate_retry_b, dim3(1, B), dim3(64), 0, s, dga);
+        if ((rc = orbgpu_sbp_frame_batch(m_motion, B, curw.data(), lastw.data(), 2 * P->th_motion, P->mono, mw.data(),
+                                         nw.data(), sbp, stride, args(8), hargs(8), abytes, s)))
+            return rc;
+        hipLaunchKernelGGL(k_track_gate_search_b, dim3(1, B), dim3(kThreads), 0, s, dga);
+    } else if (Bf->status && hipMemsetAsync(Bf->status, 0, sizeof(int32_t) * B, s) != hipSuccess) {
+        return orbgpu_fail(ORB_ERR_DEVICE, "tracking chain status reset failed");
+    }
     // the first graphs: the last frame's points, the motion model's pose
     auto edges_args = [&](int b, bool second) {
         const orb_tracking_chain_frame_t& f = fr[b];
-        const orb_frame_device_t* F = f.frame;
+        const orb_frame_device_t* F = second ? cur2[b] : cur1[b];
         EdgeParams E{};
         for (int l = 0; l < F->nlevels; ++l) E.inv_sigma2[l] = f.inv_level_sigma2[l];
         E.nlevels = F->nlevels;
@@ -490,17 +694,16 @@ int orb_tracking_chain_batch_device(orb_matcher_t m_motion, orb_matcher_t m_loca
                                        second ? fr2 + b : fr1 + b, (second ? Bf->edges2 : Bf->edges1) + o,
                                        (second ? Bf->edge_kp2 : Bf->edge_kp1) + o};
     };
-    auto upload = [&](int stage, const void* h, size_t n) {
-        if (n > abytes) return false;
-        memcpy(hargs(stage), h, n);
-        return hipMemcpyAsync(args(stage), hargs(stage), n, hipMemcpyHostToDevice, s) == hipSuccess;
-    };
     std::vector<k_track_pose_edges_args> ea(B);
     for (int b = 0; b < B; ++b) ea[b] = edges_args(b, false);
     if (!upload(1, ea.data(), B * sizeof(ea[0]))) return orbgpu_fail(ORB_ERR_DEVICE, "batch argument upload failed");
     hipLaunchKernelGGL(k_track_pose_edges_b, dim3(1, B), dim3(kThreads), 0, s, (const k_track_pose_edges_args*)args(1));
     if ((rc = orbgpu_pose_optimization_device_scratch(B, fr1, B * C, Bf->edges1, pose1, Bf->outlier1, Bf->inliers, stream, chi)))
         return rc;
+    if (gate) {  // nmatchesMap < 10: TrackWithMotionModel false (:4216)
+        if (!upload(9, ga.data(), B * sizeof(ga[0]))) return orbgpu_fail(ORB_ERR_DEVICE, "batch argument upload failed");
+        hipLaunchKernelGGL(k_track_gate_map_b, dim3(1, B), dim3(kThreads), 0, s, static_cast<const GateArgs*>(args(9)));
+    }
     // isInFrustum at the first poses, the seen skip, the discard
     if ((rc = orbgpu_frustum_chain_batch(B, fr, pose1, P->viewing_cos_limit, args(2), hargs(2), abytes, stream))) return rc;
     std::vector<k_track_local_seen_args> sa(B);
@@ -522,15 +725,15 @@ int orb_tracking_chain_batch_device(orb_matcher_t m_motion, orb_matcher_t m_loca
                                      Bf->taken + (size_t)b * C};
     if (!upload(4, da.data(), B * sizeof(da[0]))) return orbgpu_fail(ORB_ERR_DEVICE, "batch argument upload failed");
     hipLaunchKernelGGL(k_track_discard_b, dim3(1, B), dim3(kThreads), 0, s, (const k_track_discard_args*)args(4));
-    if ((rc = orbgpu_sbp_local_batch(m_local, B, cur.data(), taken.data(), loc.data(), P->th_local, P->far_points,
+    if ((rc = orbgpu_sbp_local_batch(m_local, B, cur2.data(), taken.data(), loc.data(), P->th_local, P->far_points,
                                      P->th_far_points, m2.data(), n2.data(), sbp, stride, args(5), hargs(5), abytes, s)))
         return rc;
     // the second graphs: both searches, the first poses
     for (int b = 0; b < B; ++b) ea[b] = edges_args(b, true);
     if (!upload(6, ea.data(), B * sizeof(ea[0]))) return orbgpu_fail(ORB_ERR_DEVICE, "batch argument upload failed");
+    marks.Copied();  // the call's last copy from the staging
     hipLaunchKernelGGL(k_track_pose_edges_b, dim3(1, B), dim3(kThreads), 0, s, (const k_track_pose_edges_args*)args(6));
-    if (hipGetLastError() != hipSuccess || hipEventRecord(stg.copied, s) != hipSuccess)
-        return orbgpu_fail(ORB_ERR_DEVICE, "tracking chain batch launch failed");
+    if (hipGetLastError() != hipSuccess) return orbgpu_fail(ORB_ERR_DEVICE, "tracking chain batch launch failed");
     return orbgpu_pose_optimization_device_scratch(B, fr2, B * C, Bf->edges2, pose2, Bf->outlier2, Bf->inliers + B, stream,
                                                    chi);
 }

@@ -16,6 +16,12 @@ isInFrustum and the seen marks run before the discard here: they read the first 
 search's assignments, which the discard does not change (the reference marks its discarded outliers
 seen too, src/Tracking.cc:4195), so the order gives the reference's result.
 
+TrackWithMotionModel's decisions run on the device too (gate=True, src/Tracking.cc:4149-4217): fewer
+than 20 matches -> the search again with 2 th; still fewer -> the frame fails (no PoseOptimization,
+no local-map stages); nmatchesMap < 10 after the first PoseOptimization -> it fails as well.  The
+result's `status` holds the ORB_TRACK_* bits (RETRIED 1, FAIL_SEARCH 2, FAIL_MAP 4); a failed frame is
+the caller's to hand to TrackReferenceKeyFrame, as Tracking::Track does.
+
 The current frame is frame `f` of device arrays (ORBextractor.extract_batch_device, optionally
 undistort_keypoints_device, compute_stereo_matches_batch_device).  The last frame's tracked map points
 are a table indexed by its keypoints (Frame::mvpMapPoints with MapPoint::GetWorldPos / GetDescriptor /
@@ -61,13 +67,28 @@ class LocalPointsDeviceView(ctypes.Structure):  # orb_local_points_device_t
 class TrackingChainParams(ctypes.Structure):  # orb_tracking_chain_params_t
     _fields_ = [("th_motion", ctypes.c_float), ("mono", ctypes.c_int32), ("th_local", ctypes.c_float),
                 ("far_points", ctypes.c_int32), ("th_far_points", ctypes.c_float),
-                ("viewing_cos_limit", ctypes.c_float)]
+                ("viewing_cos_limit", ctypes.c_float), ("motion_gate", ctypes.c_int32)]
 
 
 class TrackingChainBuffers(ctypes.Structure):  # orb_tracking_chain_buffers_t
     _fields_ = [(k, ctypes.c_void_p) for k in ("m1", "m2", "n_match", "frames", "edges1", "edges2", "edge_kp1",
                                                "edge_kp2", "outlier1", "outlier2", "poses", "inliers", "n_out",
-                                               "taken", "scratch")]
+                                               "taken", "scratch", "status")]
+
+ORB_TRACK_RETRIED, ORB_TRACK_FAIL_SEARCH, ORB_TRACK_FAIL_MAP = 1, 2, 4
+
+
+def _alloc_scratch(need: int, have, device):
+    """A uint8 device buffer of at least `need` bytes, grown geometrically (1.5x) past `have`'s size so a
+    slowly growing workload reallocates O(log) times.  The size is the SearchByProjection candidate lists'
+    (orb_tracking_chain_*scratch_bytes: cap x points x 8 B per frame)."""
+    import torch
+    size = max(need, int(1.5 * have.numel())) if have.numel() else need
+    try:
+        return torch.empty(size, dtype=torch.uint8, device=device)
+    except torch.cuda.OutOfMemoryError as e:
+        raise MemoryError(f"tracking chain scratch of {size} bytes (cap x max(last-frame cap, local points) x 8 B "
+                          f"per frame) does not fit in device memory: lower cap or the local map size") from e
 
 
 def _stream_handle(stream, device):
@@ -208,14 +229,16 @@ class TrackResult:
         m2 (per keypoint: the last-frame row / local map point assigned, m1 after the discard), pose1 /
         pose2 (SE3Quat vectors), edges1 / edges2 (the PoseOptimization graphs), edge_kp1 / edge_kp2,
         outlier1 / outlier2 (per edge), inliers (the PoseOptimization returns), n_kept (nmatches after
-        the discard), n_map (nmatchesMap), n2 (SearchByProjection(local) matches)."""
+        the discard), n_map (nmatchesMap), n2 (SearchByProjection(local) matches), status (ORB_TRACK_*
+        bits: the 2 th retry ran / the frame failed after the search / after PoseOptimization)."""
         c = self.chain
         self.stream.synchronize()
         fr = c.frames.cpu().numpy().view(POSE_FRAME_DTYPE).reshape(2)
         ne = [int(fr[0]["n_edges"]), int(fr[1]["n_edges"])]
         out = dict(frames=fr, n1=int(c.n_match[0]), n2=int(c.n_match[1]), m1=c.m1.cpu().numpy(),
                    m2=c.m2.cpu().numpy(), pose1=c.poses[0].cpu().numpy(), pose2=c.poses[1].cpu().numpy(),
-                   inliers=c.inliers.cpu().numpy(), n_kept=int(c.n_out[0]), n_map=int(c.n_out[1]))
+                   inliers=c.inliers.cpu().numpy(), n_kept=int(c.n_out[0]), n_map=int(c.n_out[1]),
+                   status=int(c.status[0]))
         for k in (0, 1):
             out[f"edges{k + 1}"] = c.edges[k][:ne[k]].cpu().numpy().view(POSE_EDGE_DTYPE).reshape(-1)
             out[f"edge_kp{k + 1}"] = c.edge_kp[k][:ne[k]].cpu().numpy()
@@ -227,11 +250,12 @@ class TrackingChain:
     """Buffers and launch sequence for TrackWithMotionModel -> TrackLocalMap on frames of up to `cap`
     keypoints (one chain object per concurrently tracked frame).  th_motion: 7 for stereo, 15
     otherwise (src/Tracking.cc:4141-4146); th_local: SearchLocalPoints' th (1 for stereo / mono
-    without IMU, 3 for RGB-D, src/Tracking.cc:4801-4823); mono: bMono of the last-frame search."""
+    without IMU, 3 for RGB-D, src/Tracking.cc:4801-4823); mono: bMono of the last-frame search; gate:
+    TrackWithMotionModel's retry / failure decisions on the device (False: every stage always runs)."""
 
     def __init__(self, cap: int, device=None, th_motion: float = 7, th_local: float = 1, mono: bool = False,
                  far_points: bool = False, th_far_points: float = 20.0, viewing_cos_limit: float = 0.5,
-                 scale_factor: float = 1.2):
+                 scale_factor: float = 1.2, gate: bool = True):
         import torch
         self.device = torch.device(device if device is not None else "cuda")
         self.cap = int(cap)
@@ -252,42 +276,48 @@ class TrackingChain:
         self.inliers = torch.zeros(2, dtype=torch.int32, device=d)
         self.n_out = torch.zeros(2, dtype=torch.int32, device=d)
         self.taken = torch.empty(c, dtype=torch.uint8, device=d)
+        self.status = torch.zeros(1, dtype=torch.int32, device=d)
         self._h_motion, self._h_local = self.m_motion._handle(), self.m_local._handle()
         self._params = TrackingChainParams(self.th_motion, int(self.mono), self.th_local, int(self.far_points),
-                                           self.th_far_points, self.viewing_cos_limit)
+                                           self.th_far_points, self.viewing_cos_limit, int(bool(gate)))
         fsz = POSE_FRAME_DTYPE.itemsize
         self._bufs = TrackingChainBuffers(
             self.m1.data_ptr(), self.m2.data_ptr(), self.n_match.data_ptr(), self.frames.data_ptr(),
             self.edges[0].data_ptr(), self.edges[1].data_ptr(), self.edge_kp[0].data_ptr(),
             self.edge_kp[1].data_ptr(), self.outlier[0].data_ptr(), self.outlier[1].data_ptr(),
-            self.poses.data_ptr(), self.inliers.data_ptr(), self.n_out.data_ptr(), self.taken.data_ptr())
+            self.poses.data_ptr(), self.inliers.data_ptr(), self.n_out.data_ptr(), self.taken.data_ptr(), None,
+            self.status.data_ptr())
         assert self.frames.numel() == 2 * fsz
         self._scratch = torch.empty(0, dtype=torch.uint8, device=d)
         self._scratch_key = None
-        self._retired = []
+        self._scratch_streams = {}  # the streams that used the current scratch (its retirement waits for them)
 
-    def track(self, cur: DeviceFrame, last: DeviceLastPoints, local: DeviceLocalMap, pose7, stream=None,
-              wide: bool = False) -> TrackResult:
+    def track(self, cur: DeviceFrame, last: DeviceLastPoints, local: DeviceLocalMap, pose7, stream=None) -> TrackResult:
         """Enqueue the chain for `cur` on `stream` (default: torch's current stream).  pose7: the motion
         model's prediction as the SE3Quat vector PoseOptimization starts from (tx ty tz qx qy qz qw of
-        the frame's float pose); cur's Tcw must be the same pose.  wide: the 2 th retry of
-        TrackWithMotionModel (src/Tracking.cc:4153-4160); TrackResult's caller decides it from n1."""
+        the frame's float pose); cur's Tcw must be the same pose.  TrackWithMotionModel's 2 th retry and
+        failure are decided on the device (the result's status)."""
         import torch
         if cur.cap > self.cap:
             raise ValueError(f"frame capacity {cur.cap} exceeds the chain's {self.cap}")
         lib = _lib.load()
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         p0 = np.ascontiguousarray(pose7, np.float64).reshape(7)
-        self._params.th_motion = self.th_motion * (2 if wide else 1)
         lr = local.last_row
         key = (cur.cap, last.cap, local.n)
         if key != self._scratch_key:  # one scratch for every stage of the call, grown as the sizes need
             need = int(lib.orb_tracking_chain_scratch_bytes(*key))
             if need > self._scratch.numel():
-                self._retired.append(self._scratch)  # earlier calls' stages may still be reading it
-                self._scratch = torch.empty(need, dtype=torch.uint8, device=self.device)
+                old = self._scratch
+                self._scratch = _alloc_scratch(need, old, self.device)
+                # the old scratch goes back to torch's allocator once every stream that used it has
+                # passed this point (record_stream), not while an earlier call's stages still read it
+                for s_ in self._scratch_streams.values():
+                    old.record_stream(s_)
+                self._scratch_streams = {}
                 self._bufs.scratch = self._scratch.data_ptr()
             self._scratch_key = key
+        self._scratch_streams[st.cuda_stream] = st
         check(lib.orb_tracking_chain_device(self._h_motion, self._h_local, ctypes.byref(cur.view()),
                                             ctypes.byref(last.view()), ctypes.byref(local.view()),
                                             local.pos.data_ptr(), local.normal.data_ptr(), local.min_dist.data_ptr(),
@@ -330,7 +360,7 @@ class BatchTrackResult:
         # the per-graph arrays are laid out 2 x (frames of the call)
         fr = c.frames.cpu().numpy().view(POSE_FRAME_DTYPE)[:2 * B].reshape(2, B)
         m1, m2 = c.m1.cpu().numpy(), c.m2.cpu().numpy()
-        nm, no = c.n_match.cpu().numpy(), c.n_out.cpu().numpy()
+        nm, no, stat = c.n_match.cpu().numpy(), c.n_out.cpu().numpy(), c.status.cpu().numpy()
         poses = c.poses.cpu().numpy().reshape(-1)[:14 * B].reshape(2, B, 7)
         inl = c.inliers.cpu().numpy().reshape(-1)[:2 * B].reshape(2, B)
         edges = [c.edges[k].cpu().numpy() for k in (0, 1)]
@@ -339,7 +369,8 @@ class BatchTrackResult:
         out = []
         for b in range(B):
             d = dict(frames=fr[:, b].copy(), n1=int(nm[b, 0]), n2=int(nm[b, 1]), m1=m1[b], m2=m2[b], pose1=poses[0, b],
-                     pose2=poses[1, b], inliers=inl[:, b].copy(), n_kept=int(no[b, 0]), n_map=int(no[b, 1]))
+                     pose2=poses[1, b], inliers=inl[:, b].copy(), n_kept=int(no[b, 0]), n_map=int(no[b, 1]),
+                     status=int(stat[b]))
             for k in (0, 1):
                 ne = int(fr[k, b]["n_edges"])
                 d[f"edges{k + 1}"] = edges[k][b, :ne].view(POSE_EDGE_DTYPE).reshape(-1)
@@ -357,7 +388,7 @@ class TrackingChainBatch:
 
     def __init__(self, cap: int, B: int, device=None, th_motion: float = 7, th_local: float = 1, mono: bool = False,
                  far_points: bool = False, th_far_points: float = 20.0, viewing_cos_limit: float = 0.5,
-                 scale_factor: float = 1.2):
+                 scale_factor: float = 1.2, gate: bool = True):
         import torch
         self.device = torch.device(device if device is not None else "cuda")
         self.cap, self.B = int(cap), int(B)
@@ -377,16 +408,17 @@ class TrackingChainBatch:
         self.inliers = torch.zeros((2, B), dtype=torch.int32, device=d)
         self.n_out = torch.zeros((B, 2), dtype=torch.int32, device=d)
         self.taken = torch.empty((B, c), dtype=torch.uint8, device=d)
+        self.status = torch.zeros(B, dtype=torch.int32, device=d)
         self._scratch = torch.empty(0, dtype=torch.uint8, device=d)
-        self._retired = []
         self._h_motion, self._h_local = self.m_motion._handle(), self.m_local._handle()
         self._params = TrackingChainParams(self.th_motion, int(self.mono), self.th_local, int(far_points),
-                                           float(th_far_points), float(viewing_cos_limit))
+                                           float(th_far_points), float(viewing_cos_limit), int(bool(gate)))
         self._bufs = TrackingChainBatchBuffers(
             self.m1.data_ptr(), self.m2.data_ptr(), self.n_match.data_ptr(), self.frames.data_ptr(),
             self.edges[0].data_ptr(), self.edges[1].data_ptr(), self.edge_kp[0].data_ptr(),
             self.edge_kp[1].data_ptr(), self.outlier[0].data_ptr(), self.outlier[1].data_ptr(),
-            self.poses.data_ptr(), self.inliers.data_ptr(), self.n_out.data_ptr(), self.taken.data_ptr(), None)
+            self.poses.data_ptr(), self.inliers.data_ptr(), self.n_out.data_ptr(), self.taken.data_ptr(), None,
+            self.status.data_ptr())
 
     def _records(self, items):
         """The batch's orb_tracking_chain_frame_t records (a numpy buffer of _CHAIN_FRAME_DTYPE), the
@@ -395,9 +427,14 @@ class TrackingChainBatch:
         rows, poses, keep = [], [], []
         last_cap = n_local = 0
         sf = self.scale_factor
+        seen_maps = set()
         for cur, last, local, pose7 in items:
             if cur.cap != self.cap:
                 raise ValueError(f"frame capacity {cur.cap} differs from the batch's {self.cap}")
+            # isInFrustum writes the local map's tracking fields: one map in two slots of a call would race
+            if id(local) in seen_maps:
+                raise ValueError("a DeviceLocalMap appears in two slots of one batch call (each slot needs its own)")
+            seen_maps.add(id(local))
             ff = cur.frustum_frame(sf)
             lv = last.view()  # (refreshes the last frame's pose in its view)
             mp = local.chain_pointers()
@@ -414,8 +451,9 @@ class TrackingChainBatch:
         arr["pose7"] = np.asarray(poses, dtype=np.float64).reshape(nb, 7)
         return arr, keep, last_cap, n_local
 
-    def track(self, items, stream=None, wide: bool = False) -> BatchTrackResult:
-        """items: up to B tuples (cur DeviceFrame, DeviceLastPoints, DeviceLocalMap, pose7)."""
+    def track(self, items, stream=None) -> BatchTrackResult:
+        """items: up to B tuples (cur DeviceFrame, DeviceLastPoints, DeviceLocalMap, pose7), each slot
+        with its own DeviceLocalMap."""
         import torch
         nb = len(items)
         if not 0 < nb <= self.B:
@@ -425,12 +463,10 @@ class TrackingChainBatch:
         arr, keep, last_cap, n_local = self._records(items)  # keep: what the records point into, alive over the call
         need = int(lib.orb_tracking_chain_batch_scratch_bytes(self.B, self.cap, last_cap, n_local))
         if need > self._scratch.numel():
-            if self._scratch.numel():
+            if self._scratch.numel():  # waits for the last call on the old scratch, then frees its staging
                 lib.orb_tracking_chain_batch_release(ctypes.c_void_p(self._scratch.data_ptr()))
-            self._retired.append(self._scratch)
-            self._scratch = torch.empty(need, dtype=torch.uint8, device=self.device)
+            self._scratch = _alloc_scratch(need, self._scratch, self.device)  # (the old one is free: released)
             self._bufs.scratch = self._scratch.data_ptr()
-        self._params.th_motion = self.th_motion * (2 if wide else 1)
         check(lib.orb_tracking_chain_batch_device(self._h_motion, self._h_local, nb, arr.ctypes.data,
                                                   ctypes.byref(self._params), ctypes.byref(self._bufs),
                                                   ctypes.c_void_p(st.cuda_stream)),
@@ -438,7 +474,8 @@ class TrackingChainBatch:
         return BatchTrackResult(self, st, nb)
 
     def release(self) -> None:
-        """Free the library's pinned staging for this batch's scratch (waits for its last call)."""
+        """Free the library's pinned staging for this batch's scratch; waits until the last call's every
+        kernel has finished, so the scratch and the output tensors may be dropped afterwards."""
         if self._scratch.numel():
             _lib.load().orb_tracking_chain_batch_release(ctypes.c_void_p(self._scratch.data_ptr()))
 

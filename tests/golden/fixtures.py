@@ -19,8 +19,9 @@ Records (tests/golden/*.json, *.npz), written by tests/golden/gen_golden.py:
   ba_c5.npz        LocalBA C5 (mono seed 7, 50/50 seed 8): the problem's SHA-256 and the oracle's
                    solution (poses, points, edge chi2, depth flags, LM path); the full small problem
                    (6 keyframes, 150 points) with its solution
-  tracking.json    the oracle tracking chain on scenes 81 / 82 (stereo) / 83 (mono): match counts,
-                   SHA-256 of the matches and outlier flags, the final pose
+  tracking.json    the oracle tracking chain on scenes 81 / 82 (stereo) / 83 (mono) and on the
+                   TrackWithMotionModel gate scenes: status, match counts, SHA-256 of the matches and
+                   outlier flags, the final pose
 """
 from __future__ import annotations
 
@@ -139,8 +140,17 @@ def ba_path(res: dict) -> np.ndarray:
     return np.array([res["iterations"], res["trials"], res["terminated"], res["stopped"]], np.int64)
 
 
-# ---- tracking chain
-TRACK_SCENES = [(81, True), (82, True), (83, False)]
+# ---- tracking chain: the parity scenes, and scenes for TrackWithMotionModel's decisions (the 2 th
+# retry recovering, exactly 20 after it, failing twice, nmatchesMap < 10)
+TRACK_SCENES = {"scene81": dict(seed=81), "scene82": dict(seed=82), "scene83": dict(seed=83, stereo=False),
+                "gate_retry": dict(seed=81, pred_rot=0.05, pred_trans=0.3),
+                "gate_exactly_20": dict(seed=81, pred_rot=0.1, pred_trans=0.5),
+                "gate_fails_twice": dict(seed=83, pred_rot=0.1, pred_trans=0.5),
+                "gate_few_map_points": dict(seed=84, unobserved_frac=0.99)}
+
+
+def track_th(kw: dict) -> int:
+    return 7 if kw.get("stereo", True) else 15
 
 
 def tracking_record(o: dict) -> dict:
@@ -148,4 +158,4 @@ def tracking_record(o: dict) -> dict:
             "n_kept": int(o["n_kept"]), "n_map": int(o["n_map"]),
             "m1_sha256": sha(np.asarray(o["m1"], np.int32)), "m2_sha256": sha(np.asarray(o["m2"], np.int32)),
             "O1_sha256": sha(np.asarray(o["O1"], np.uint8)), "O2_sha256": sha(np.asarray(o["O2"], np.uint8)),
-            "pose2": [float(v) for v in np.asarray(o["pose2"], np.float64)]}
+            "pose2": [float(v) for v in np.asarray(o["pose2"], np.float64)], "status": int(o["status"])}

@@ -72,11 +72,11 @@ def main() -> int:
 
     # tracking chain
     tr = {}
-    for seed, stereo in fx.TRACK_SCENES:
-        sc = synth.tracking_chain_scene(seed=seed, stereo=stereo)
+    for name, kw in fx.TRACK_SCENES.items():
+        sc = synth.tracking_chain_scene(**kw)
         C, L = pkg.Frame(**sc["cur"]), pkg.Frame(**sc["last"])
-        o = tracking_chain.track(pkg, C, L, sc["local"], sc["pose7_pred"], sc["level_sigma2"], 7 if stereo else 15, 1)
-        tr[f"scene{seed}"] = fx.tracking_record(o)
+        o = tracking_chain.track(pkg, C, L, sc["local"], sc["pose7_pred"], sc["level_sigma2"], fx.track_th(kw), 1)
+        tr[name] = fx.tracking_record(o)
     (out / "tracking.json").write_text(json.dumps(tr, indent=1, sort_keys=True) + "\n")
     for f in sorted(out.glob("*")):
         if f.suffix in (".json", ".npz"):

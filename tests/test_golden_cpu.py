@@ -90,8 +90,11 @@ def test_small_ba_problem_round_trip(oracle, synth):
 def test_oracle_tracking_chain_matches_golden(pkg, synth):
     from oracle import tracking_chain
     golden = fx.load_json("tracking.json")
-    for seed, stereo in fx.TRACK_SCENES:
-        sc = synth.tracking_chain_scene(seed=seed, stereo=stereo)
+    assert golden.keys() == fx.TRACK_SCENES.keys()
+    for name, kw in fx.TRACK_SCENES.items():
+        sc = synth.tracking_chain_scene(**kw)
         C, L = pkg.Frame(**sc["cur"]), pkg.Frame(**sc["last"])
-        o = tracking_chain.track(pkg, C, L, sc["local"], sc["pose7_pred"], sc["level_sigma2"], 7 if stereo else 15, 1)
-        assert fx.tracking_record(o) == golden[f"scene{seed}"], seed
+        o = tracking_chain.track(pkg, C, L, sc["local"], sc["pose7_pred"], sc["level_sigma2"], fx.track_th(kw), 1)
+        assert fx.tracking_record(o) == golden[name], name
+    # every TrackWithMotionModel outcome is recorded
+    assert {golden[n]["status"] for n in golden} == {0, 1, 3, 4}

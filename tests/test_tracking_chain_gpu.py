@@ -100,10 +100,10 @@ def test_tracking_chain_vs_oracle(pkg, oracle, synth, seed, stereo):
     assert np.abs(e["pose2"] - r["pose2"]).max() < 1e-6
     # and against the committed record of the oracle chain (tests/golden/tracking.json)
     from golden import fixtures as fx
-    g = fx.load_json("tracking.json")[f"scene{seed}"]
+    g = fx.load_json("tracking.json")[f"scene{seed}"]  # (scene83 is the mono one)
     dev = fx.tracking_record(dict(n1=r["n1"], n2=r["n2"], I1=r["inliers"][0], I2=r["inliers"][1], n_kept=r["n_kept"],
                                   n_map=r["n_map"], m1=r["m1"][:C.N], m2=r["m2"][:C.N], O1=r["outlier1"],
-                                  O2=r["outlier2"], pose2=g["pose2"]))
+                                  O2=r["outlier2"], pose2=g["pose2"], status=r["status"]))
     assert dev == g, seed
     assert np.abs(r["pose2"] - np.asarray(g["pose2"])).max() < 1e-6
     # and the chain tracked: the final pose is closer to the truth than the prediction
@@ -219,3 +219,100 @@ def test_tracking_chain_batch_many_slots(pkg, synth):
         for k in ("m1", "m2", "edge_kp1", "edge_kp2", "outlier1", "outlier2", "inliers"):
             assert np.array_equal(np.asarray(r[k]), np.asarray(o[k])), (i, k)
         assert np.array_equal(r["pose1"], o["pose1"]) and np.array_equal(r["pose2"], o["pose2"]), i
+
+
+# TrackWithMotionModel's decisions on the device (src/Tracking.cc:4149-4217): scenes whose motion-model
+# prediction is off by enough that the th search finds < 20 matches (the 2 th search recovers; exactly 20
+# passes), fails twice, or passes the search with too few observed map points (nmatchesMap < 10)
+# (the scene parameters are tests/golden/fixtures.py's TRACK_SCENES, whose oracle records the
+# status of each)
+GATE_SCENES = {
+    "retry_recovers": ("gate_retry", 1),
+    "retry_exactly_20": ("gate_exactly_20", 1),
+    "fails_twice": ("gate_fails_twice", 3),
+    "few_map_points": ("gate_few_map_points", 4),
+    "tracked": ("scene82", 0),
+}
+
+
+def _gate_scene(synth, name):
+    from golden import fixtures as fx
+    key, status = GATE_SCENES[name]
+    return synth.tracking_chain_scene(**fx.TRACK_SCENES[key]), key, status
+
+
+def _check_gate(r, o, C, what):
+    assert r["status"] == o["status"], (what, r["status"], o["status"])
+    for k in ("n1", "n2", "n_kept", "n_map"):
+        assert r[k] == o[k], (what, k, r[k], o[k])
+    for k in ("m1", "m2"):
+        assert np.array_equal(np.asarray(r[k])[:C.N], o[k]), (what, k)
+    assert np.array_equal(np.asarray(r["outlier1"]), o["O1"]) and np.array_equal(np.asarray(r["outlier2"]), o["O2"]), what
+    assert list(np.asarray(r["inliers"])) == [o["I1"], o["I2"]], what
+    assert np.abs(r["pose1"] - o["pose1"]).max() < 1e-6 and np.abs(r["pose2"] - o["pose2"]).max() < 1e-6, what
+
+
+@pytest.mark.parametrize("name", list(GATE_SCENES))
+def test_tracking_chain_motion_gate(pkg, synth, name):
+    """Single chain: the status word, the matches of the search that counted (the 2 th one after a retry),
+    no graph / no local-map stage after a failure, poses as documented -- equal to the oracle chain's
+    TrackWithMotionModel decisions (oracle/tracking_chain.py, gate=True)."""
+    from golden import fixtures as fx
+    sc, key, status = _gate_scene(synth, name)
+    C, L = _frames(pkg, sc)
+    cur, last, local = _device(pkg, sc, C, L)
+    r = pkg.TrackingChain(cur.cap).track(cur, last, local, sc["pose7_pred"]).sync()
+    o = _oracle_stages(pkg, sc, C, L, 7, 1)
+    assert o["status"] == status, (name, o["status"])
+    _check_gate(r, o, C, name)
+    g = fx.load_json("tracking.json")[key]
+    assert g["status"] == r["status"] and g["n1"] == r["n1"] and g["n2"] == r["n2"]
+    assert g["m1_sha256"] == fx.sha(np.asarray(r["m1"][:C.N], np.int32))
+    if status & 6:  # a failed frame: nothing after the search / the first PoseOptimization
+        assert r["n2"] == 0 and (r["m2"][:cur.cap] == -1).all() and int(r["frames"][1]["n_edges"]) == 0
+    if status == 3:
+        assert int(r["frames"][0]["n_edges"]) == 0 and np.array_equal(r["pose1"], np.asarray(sc["pose7_pred"]))
+
+
+def test_tracking_chain_motion_gate_off(pkg, synth):
+    """gate=False: every stage runs with th as given, as the oracle chain with its gate off."""
+    sc, _, _ = _gate_scene(synth, "fails_twice")
+    C, L = _frames(pkg, sc)
+    cur, last, local = _device(pkg, sc, C, L)
+    r = pkg.TrackingChain(cur.cap, gate=False).track(cur, last, local, sc["pose7_pred"]).sync()
+    from oracle import tracking_chain
+    o = tracking_chain.track(pkg, C, L, sc["local"], sc["pose7_pred"], sc["level_sigma2"], 7, 1, gate=False)
+    assert r["status"] == 0 and o["status"] == 0 and r["n1"] == o["n1"] < 20
+    assert np.array_equal(r["m1"][:C.N], o["m1"]) and np.array_equal(r["m2"][:C.N], o["m2"])
+    assert np.abs(r["pose2"] - o["pose2"]).max() < 1e-6
+
+
+def test_tracking_chain_batch_motion_gate(pkg, synth):
+    """Batch: every gate case in one call (slots in mixed order, each with its own local map), each slot
+    equal to the single chain bit for bit (status included)."""
+    names = ["fails_twice", "tracked", "retry_recovers", "few_map_points", "retry_exactly_20", "fails_twice"]
+    scenes = [_gate_scene(synth, n)[0] for n in names]
+    fr = [_frames(pkg, sc) for sc in scenes]
+    cap = max(max(C.N, L.N) for C, L in fr) + 3
+    devs = [_device(pkg, sc, C, L, cap=cap) for sc, (C, L) in zip(scenes, fr)]
+    single = [pkg.TrackingChain(cap).track(cur, last, local, sc["pose7_pred"]).sync()
+              for sc, (cur, last, local) in zip(scenes, devs)]
+    batch = pkg.TrackingChainBatch(cap, len(names))
+    res = batch.track([(cur, last, local, sc["pose7_pred"]) for sc, (cur, last, local) in zip(scenes, devs)]).sync()
+    for n, r, o in zip(names, res, single):
+        assert r["status"] == o["status"] == GATE_SCENES[n][1], n
+        for k in ("n1", "n2", "n_kept", "n_map"):
+            assert r[k] == o[k], (n, k)
+        for k in ("m1", "m2", "edge_kp1", "edge_kp2", "outlier1", "outlier2", "inliers"):
+            assert np.array_equal(np.asarray(r[k]), np.asarray(o[k])), (n, k)
+        assert np.array_equal(r["pose1"], o["pose1"]) and np.array_equal(r["pose2"], o["pose2"]), n
+    batch.release()
+
+
+def test_tracking_chain_batch_rejects_shared_local_map(pkg, synth):
+    """isInFrustum writes each slot's local map, so one map in two slots of a call is refused."""
+    sc = synth.tracking_chain_scene(seed=82)
+    C, L = _frames(pkg, sc)
+    cur, last, local = _device(pkg, sc, C, L)
+    with pytest.raises(ValueError, match="two slots"):
+        pkg.TrackingChainBatch(cur.cap, 2).track([(cur, last, local, sc["pose7_pred"])] * 2)
