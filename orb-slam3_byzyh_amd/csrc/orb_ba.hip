@@ -2640,7 +2640,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         memset(h->h_prog, 0, sizeof(LmProgress));
         *h->h_stop = 0;
         if (dist) {  // the partial buffers; the scalar slots must start at zero (the ranks' max diag slots)
-            const size_t nd = 36 * (size_t)nf + n + (size_t)n * n + n + 2 * (size_t)(4 + h->world + 4);
+            const size_t nd = 2 * (36 * (size_t)nf + n + 4 + h->world) + (size_t)n * n + n + 2 * 4;
             const bool okp = h->dpart.grow(nd) && hipMemsetAsync(h->dpart.p, 0, nd * sizeof(double), s) == hipSuccess;
             if (agree_fail(!okp)) return orbgpu_fail(ORB_ERR_DEVICE, "BA sharded buffers");
         }
@@ -2660,15 +2660,18 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                                h->part.p, (const LmState*)L);
         };
         if (trial_lin) launch_edges_build();
-        // sharded: the partials [Hpp | b_p], [S | b_S], the build scalars (chi2, slots of the ranks'
-        // max diag at 4 + r) and the trial scalars (chi2, computeScale, stop), then their sums
+        // sharded: the partials [Hpp | b_p | build scalars] (chi2, slots of the ranks' max diag at
+        // 4 + r: one payload, one collective), their sums, [S | b_S], the trial scalars (chi2,
+        // computeScale, stop) and their sums
         const int nsb = 4 + h->world;
+        const size_t nhb = 36 * (size_t)nf + n;
         double* const p_hb = dist ? h->dpart.p : nullptr;
-        double* const p_sb = dist ? p_hb + 36 * (size_t)nf + n : nullptr;
-        double* const p_scb = dist ? p_sb + (size_t)n * n + n : nullptr;
-        double* const p_sct = dist ? p_scb + nsb : nullptr;
-        double* const r_scb = dist ? p_sct + 4 : nullptr;
-        double* const r_sct = dist ? r_scb + nsb : nullptr;
+        double* const p_scb = dist ? p_hb + nhb : nullptr;
+        double* const r_hb = dist ? p_scb + nsb : nullptr;
+        double* const r_scb = dist ? r_hb + nhb : nullptr;
+        double* const p_sb = dist ? r_scb + nsb : nullptr;
+        double* const p_sct = dist ? p_sb + (size_t)n * n + n : nullptr;
+        double* const r_sct = dist ? p_sct + 4 : nullptr;
         bool coll_ok = true;
         auto unit_launches = [&]() {
             if (!trial_lin) launch_edges_build();
@@ -2676,9 +2679,9 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                                h->pose_fl.p, h->ecp.p, dist ? p_hb : HPP, dist ? p_hb + 36 * (size_t)nf : BV,
                                h->land_off.p, h->land_edge.p, h->ecl.p, h->hll.p, bl, h->part.p, nparts, h->counters.p,
                                h->scal.p, L, dist ? 1 : 0, p_scb, h->rank);
-            if (dist) {
-                coll_ok = coll_ok && dev_reduce2(h, p_hb, HPP, 36 * (size_t)nf + n, ORB_BA_SUM) &&
-                          dev_reduce2(h, p_scb, r_scb, nsb, ORB_BA_SUM);
+            if (dist) {  // one collective for [Hpp | b_p | build scalars], then the sums into place
+                coll_ok = coll_ok && dev_reduce2(h, p_hb, r_hb, nhb + nsb, ORB_BA_SUM) &&
+                          hipMemcpyAsync(HPP, r_hb, nhb * sizeof(double), hipMemcpyDeviceToDevice, s) == hipSuccess;
                 hipLaunchKernelGGL(k_lm_build_ctl, dim3(1), dim3(64), 0, s, nf, (const double*)HPP, (const double*)r_scb,
                                    h->world, h->scal.p, L);
             }
