@@ -784,8 +784,11 @@ def bench_tracking_chain(pkg, synth, dev, steps, cpu_baseline_on, n_scenes=8, ba
         chbs[i % nbuf].track(items, stream=st)
     st.synchronize()
     t0 = time.perf_counter()
+    enq_b = []
     for i in range(brep):
+        t1 = time.perf_counter()
         chbs[i % nbuf].track(items, stream=st)
+        enq_b.append((time.perf_counter() - t1) * 1e3)
     st.synchronize()
     bat_ms = (time.perf_counter() - t0) * 1e3 / brep
     res0 = chb.track(items[:1], stream=st).sync()[0]  # slot 0 is scene 0: the single chain's answer
@@ -798,6 +801,8 @@ def bench_tracking_chain(pkg, synth, dev, steps, cpu_baseline_on, n_scenes=8, ba
            "batched_frames_per_ms": round(batch * brep / bdt, 4), "batch": batch, "streams": n_streams,
            "batch_api": {"frames_per_call": nb, "batch_objects": nbuf, "ms_per_call": round(bat_ms, 4),
                          "frames_per_ms": round(nb / bat_ms, 3),
+                         "host_enqueue_ms": {"median": round(float(np.median(enq_b)), 4),
+                                             "max": round(float(np.max(enq_b)), 4)},
                          "note": "orb_tracking_chain_batch_device: one launch per stage for the whole batch, one "
                                  "stream; frames padded to cap 2048; 8 scenes repeated, a local map per slot"},
            "matches_last_frame": n1, "matches_local_map": n2, "dtype": "u8 / f32 / f64"}

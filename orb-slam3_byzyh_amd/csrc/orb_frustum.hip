@@ -20,6 +20,23 @@
 
 namespace {
 
+// PredictScale's thresholds for (log scale factor, levels), memoised per thread: a binary search of
+// ~31 logf per level, which a batch of frames with one camera would otherwise repeat per frame (the
+// tracking-chain batch's host enqueue, round 6)
+bool scale_thresholds(float lsf, int n_levels, float* T) {
+    thread_local float m_lsf = -1.0f;
+    thread_local int m_n = -1;
+    thread_local float m_T[orbgpu::kPredictMaxLevels];
+    if (n_levels != m_n || std::memcmp(&lsf, &m_lsf, sizeof(float)) != 0) {
+        if (!orbgpu::predict_scale_thresholds(lsf, n_levels, m_T)) return false;
+        m_lsf = lsf;
+        m_n = n_levels;
+    }
+    std::memcpy(T, m_T, sizeof(float) * (n_levels > 1 ? n_levels - 1 : 0));
+    return true;
+}
+
+
 struct ScaleSteps {  // MapPoint::PredictScale level thresholds (orb_predict_scale.h)
     float t[orbgpu::kPredictMaxLevels];
 };
@@ -132,7 +149,7 @@ int orb_is_in_frustum_pose_device(const orb_frustum_frame_t* frame, const double
                                   !d_depth || !d_level || !d_view_cos)) || frame->n_levels <= 0)
         return orbgpu_fail(ORB_ERR_ARG, "invalid frustum arguments");
     ScaleSteps steps{};
-    if (!orbgpu::predict_scale_thresholds(frame->log_scale_factor, frame->n_levels, steps.t))
+    if (!scale_thresholds(frame->log_scale_factor, frame->n_levels, steps.t))
         return orbgpu_fail(ORB_ERR_ARG, "log_scale_factor must be > 0 and n_levels <= 32");
     if (n == 0) return ORB_OK;
     hipLaunchKernelGGL(k_is_in_frustum, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, *frame, d_pose7, n, d_pos,
@@ -159,7 +176,7 @@ int orbgpu_frustum_chain_batch(int B, const orb_tracking_chain_frame_t* fr, cons
                       !L->track_proj || !L->track_depth || !L->track_level || !L->track_view_cos)))
             return orbgpu_fail(ORB_ERR_ARG, "invalid frustum batch frame");
         ScaleSteps steps{};
-        if (!orbgpu::predict_scale_thresholds(F->log_scale_factor, F->n_levels, steps.t))
+        if (!scale_thresholds(F->log_scale_factor, F->n_levels, steps.t))
             return orbgpu_fail(ORB_ERR_ARG, "log_scale_factor must be > 0 and n_levels <= 32");
         a[b] = k_is_in_frustum_args{*F, d_poses + 7 * (size_t)b, L->n, fr[b].pos, fr[b].normal, fr[b].min_dist,
                                     fr[b].max_dist, viewing_cos_limit, steps, const_cast<uint8_t*>(L->track_in_view),

@@ -381,19 +381,23 @@ size_t stage_bytes(int cap, int last_cap, int n_local) {
 }
 
 // the batch's argument areas: one per stage, each room for B frames' largest argument blocks (the
-// SearchByProjection stages pack five kernels' blocks, 256-B aligned); 7-10: the 2 th search and the gates
-constexpr int kBatchArgStages = 11;
+// SearchByProjection stages pack five kernels' blocks, 256-B aligned); 7: the gates, 8: the 2 th search
+constexpr int kBatchArgStages = 9;
 size_t batch_args_bytes(int B) { return ((size_t)B * 4096 + 8 * 256 + 255) & ~(size_t)255; }
 
-// The pinned host side of a batch's argument areas, one per batch scratch (the caller's batch object),
-// and events after the call's copies and after its last launch: the next call on that scratch writes the
-// staging only once the previous call's copies have read it (stream-ordered copies read pinned memory
-// when they run); release waits for the whole call.
+// The pinned host side of a batch's argument areas, per batch scratch (the caller's batch object): a
+// ring of two, taken by the calls in turn, each with an event after its call's last copy -- a call
+// rewrites an area only once the copies of the call two back have read it (stream-ordered copies read
+// pinned memory when they run), so in steady state the host does not wait on the call just queued
+// (round 6: with one area every call blocked the host thread on the previous call's event).  An event
+// after each call's last launch is what release waits for.
+constexpr int kStagingRing = 2;
 struct BatchStaging {
-    void* host = nullptr;
+    void* host[kStagingRing] = {};         // the calls take the areas in turn
     size_t bytes = 0;
-    hipEvent_t copied = nullptr;  // after the call's last argument copy
-    hipEvent_t done = nullptr;    // after the call's last launch
+    hipEvent_t copied[kStagingRing] = {};  // after that area's call's last argument copy
+    hipEvent_t done = nullptr;             // after the last call's last launch
+    int next = 0;
 };
 std::mutex g_staging_mu;
 std::unordered_map<const void*, BatchStaging> g_staging;
@@ -543,11 +547,13 @@ int orb_tracking_chain_batch_release(void* scratch) {
         (void)hipEventSynchronize(stg.done);
         (void)hipEventDestroy(stg.done);
     }
-    if (stg.copied) {
-        (void)hipEventSynchronize(stg.copied);
-        (void)hipEventDestroy(stg.copied);
+    for (int r = 0; r < kStagingRing; ++r) {
+        if (stg.copied[r]) {
+            (void)hipEventSynchronize(stg.copied[r]);
+            (void)hipEventDestroy(stg.copied[r]);
+        }
+        if (stg.host[r]) (void)hipHostFree(stg.host[r]);
     }
-    if (stg.host) (void)hipHostFree(stg.host);
     g_staging.erase(it);
     return ORB_OK;
 }
@@ -593,34 +599,42 @@ int orb_tracking_chain_batch_device(orb_matcher_t m_motion, orb_matcher_t m_loca
                                               (((size_t)B * sizeof(ChainGate) + 255) & ~(size_t)255));
     std::lock_guard<std::mutex> lock(g_staging_mu);
     BatchStaging& stg = g_staging[Bf->scratch];
-    if (stg.copied && hipEventSynchronize(stg.copied) != hipSuccess)
+    const int ring = stg.next;
+    if (stg.copied[ring] && hipEventSynchronize(stg.copied[ring]) != hipSuccess)
         return orbgpu_fail(ORB_ERR_DEVICE, "batch staging wait failed");
-    if (stg.bytes < (size_t)kBatchArgStages * abytes) {
-        if (stg.host) (void)hipHostFree(stg.host);
-        stg.host = nullptr;
+    if (stg.bytes < (size_t)kBatchArgStages * abytes) {  // (re)size every area: the others' calls are done
+        for (int r = 0; r < kStagingRing; ++r) {
+            if (stg.copied[r] && hipEventSynchronize(stg.copied[r]) != hipSuccess)
+                return orbgpu_fail(ORB_ERR_DEVICE, "batch staging wait failed");
+            if (stg.host[r]) (void)hipHostFree(stg.host[r]);
+            stg.host[r] = nullptr;
+        }
         stg.bytes = 0;
-        if (hipHostMalloc(&stg.host, (size_t)kBatchArgStages * abytes, hipHostMallocDefault) != hipSuccess)
-            return orbgpu_fail(ORB_ERR_DEVICE, "hipHostMalloc failed");
+        for (int r = 0; r < kStagingRing; ++r)
+            if (hipHostMalloc(&stg.host[r], (size_t)kBatchArgStages * abytes, hipHostMallocDefault) != hipSuccess)
+                return orbgpu_fail(ORB_ERR_DEVICE, "hipHostMalloc failed");
         stg.bytes = (size_t)kBatchArgStages * abytes;
     }
-    if ((!stg.copied && hipEventCreateWithFlags(&stg.copied, hipEventDisableTiming) != hipSuccess) ||
+    if ((!stg.copied[ring] && hipEventCreateWithFlags(&stg.copied[ring], hipEventDisableTiming) != hipSuccess) ||
         (!stg.done && hipEventCreateWithFlags(&stg.done, hipEventDisableTiming) != hipSuccess))
         return orbgpu_fail(ORB_ERR_DEVICE, "hipEventCreate failed");
+    stg.next = (ring + 1) % kStagingRing;
     // from here on every exit marks the staging's copies (the next call waits for them before it
     // rewrites the staging) and the call's end (release waits for it)
     struct Marks {
         BatchStaging& stg;
+        int ring;
         hipStream_t s;
         bool copied = false;
         void Copied() {
-            copied = hipEventRecord(stg.copied, s) == hipSuccess;
+            copied = hipEventRecord(stg.copied[ring], s) == hipSuccess;
         }
         ~Marks() {
-            if (!copied) (void)hipEventRecord(stg.copied, s);
+            if (!copied) (void)hipEventRecord(stg.copied[ring], s);
             (void)hipEventRecord(stg.done, s);
         }
-    } marks{stg, s};
-    auto hargs = [&](int stage) { return static_cast<void*>(static_cast<char*>(stg.host) + (size_t)stage * abytes); };
+    } marks{stg, ring, s};
+    auto hargs = [&](int stage) { return static_cast<void*>(static_cast<char*>(stg.host[ring]) + (size_t)stage * abytes); };
     std::vector<const orb_frame_device_t*> cur(B), cur1(B), cur2(B), curw(B);
     std::vector<const orb_last_points_device_t*> last(B), lastw(B);
     std::vector<orb_frame_device_t> g1(B), g2(B), gw(B);
@@ -700,10 +714,8 @@ int orb_tracking_chain_batch_device(orb_matcher_t m_motion, orb_matcher_t m_loca
     hipLaunchKernelGGL(k_track_pose_edges_b, dim3(1, B), dim3(kThreads), 0, s, (const k_track_pose_edges_args*)args(1));
     if ((rc = orbgpu_pose_optimization_device_scratch(B, fr1, B * C, Bf->edges1, pose1, Bf->outlier1, Bf->inliers, stream, chi)))
         return rc;
-    if (gate) {  // nmatchesMap < 10: TrackWithMotionModel false (:4216)
-        if (!upload(9, ga.data(), B * sizeof(ga[0]))) return orbgpu_fail(ORB_ERR_DEVICE, "batch argument upload failed");
-        hipLaunchKernelGGL(k_track_gate_map_b, dim3(1, B), dim3(kThreads), 0, s, static_cast<const GateArgs*>(args(9)));
-    }
+    if (gate)  // nmatchesMap < 10: TrackWithMotionModel false (:4216); the gate blocks uploaded for the retry
+        hipLaunchKernelGGL(k_track_gate_map_b, dim3(1, B), dim3(kThreads), 0, s, static_cast<const GateArgs*>(args(7)));
     // isInFrustum at the first poses, the seen skip, the discard
     if ((rc = orbgpu_frustum_chain_batch(B, fr, pose1, P->viewing_cos_limit, args(2), hargs(2), abytes, stream))) return rc;
     std::vector<k_track_local_seen_args> sa(B);

@@ -114,6 +114,7 @@ class DeviceFrame:
         self.mvScaleFactors = np.ascontiguousarray(scale_factors, np.float32)
         self.mvLevelSigma2 = np.ascontiguousarray(level_sigma2, np.float32)
         self.mvInvLevelSigma2 = (np.float32(1.0) / self.mvLevelSigma2).astype(np.float32)  # src/Frame.cc:124
+        self._inv_sigma2_ptr = self.mvInvLevelSigma2.ctypes.data  # (a batch record per call reads it)
         self.mbf = float(np.float32(bf))
         self.mb = float(np.float32(np.float32(bf) / np.float32(self.fx))) if bf else 0.0
         b = (0.0, float(width), 0.0, float(height)) if bounds is None else tuple(float(v) for v in bounds)
@@ -132,6 +133,7 @@ class DeviceFrame:
         self.Tcw = np.ascontiguousarray(Tcw, np.float32).reshape(3, 4)
         self._view.Tcw[:] = [float(x) for x in self.Tcw.reshape(-1)]
         self._ff = None
+        self._pose_version = getattr(self, "_pose_version", 0) + 1  # (DeviceLastPoints copies it on change)
 
     def view(self) -> FrameDeviceView:
         return self._view
@@ -164,9 +166,12 @@ class DeviceLastPoints:
         self._view = LastPointsDeviceView(fv.n, frame.cap, valid.data_ptr(), observed.data_ptr(), xyz.data_ptr(),
                                           desc.data_ptr(), fv.kps_un)
         self._view.Tcw[:] = list(fv.Tcw)
+        self._pose_version = frame._pose_version
 
     def view(self) -> LastPointsDeviceView:
-        self._view.Tcw[:] = list(self.frame.view().Tcw)
+        if self._pose_version != self.frame._pose_version:  # the last frame's pose changed since
+            self._view.Tcw[:] = list(self.frame.view().Tcw)
+            self._pose_version = self.frame._pose_version
         return self._view
 
 
@@ -440,7 +445,7 @@ class TrackingChainBatch:
             mp = local.chain_pointers()
             keep.append(ff)
             rows.append((ctypes.addressof(cur.view()), ctypes.addressof(lv), mp[0], mp[1], mp[2], mp[3], mp[4], mp[5],
-                         ctypes.addressof(ff), cur.mvInvLevelSigma2.ctypes.data))
+                         ctypes.addressof(ff), cur._inv_sigma2_ptr))
             poses.append(pose7)
             if last.cap > last_cap:
                 last_cap = last.cap
