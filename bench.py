@@ -62,16 +62,18 @@ def survey_bytes_per_frame(w, h, nkp):
     return w * h + 2 * sum(a * b for a, b in sizes[1:]) + nkp * 60
 
 
-def algorithmic_bytes_per_frame(w, h, nkp):
+def algorithmic_bytes_per_frame(w, h, nkp, pairs=False):
     """Per-frame bytes each stage of THIS implementation moves (a traffic model, not the roofline's
     algorithmic figure, which is survey_bytes_per_frame)."""
     sizes = level_sizes(w, h)
     px = [a * b for a, b in sizes]
     written = [(a + 6) * (b + 6) for a, b in sizes]  # each view + its 3-px REFLECT_101 border
+    # level passes read the input and levels 0..6; two-level passes (k_pyramid_pair) the input and
+    # levels 1, 3, 5 (level l + 1 is resized from level l while it is in LDS)
+    reads = sum(px[1:-1:2]) if pairs else sum(px[:-1])
     return {
-        # read L0 + read levels 0..6 to resize; write every level's view + border (no blurred levels:
-        # k_describe blurs its own samples)
-        "pyramid": w * h + sum(px[:-1]) + sum(written),
+        # write every level's view + border (no blurred levels: k_describe blurs its own samples)
+        "pyramid": w * h + reads + sum(written),
         # read every level once; candidates are ~1% of pixels (not counted)
         "fast": sum(px),
         # candidates in, selected keys out (small); counted as one level read equivalent of 4 B/cand
@@ -1340,8 +1342,14 @@ def main():
                      "launch_ms: the timed region's steps again, all in-flight handles (shared chip); "
                      "exclusive_ms: the same steps one batch at a time on handle 0 (the roofline's)",
              "launch_ms": launch_ms, "exclusive_ms": excl_ms}))
-    launches_per_step = NLEVELS  # one k_pyramid_level launch per level per batch
-    pyr_launch_avg_ms = sum(excl_ms["k_pyramid_level"]) / max(1, len(excl_ms["k_pyramid_level"]))
+    # pyramid launches per batch: 4 two-level passes (k_pyramid_pair), or 8 level passes
+    # (k_pyramid_level, ORBGPU_PYR_PAIR=0 or a geometry outside the pair kernel's boxes); both are
+    # recorded under the pyramid tag
+    launches_per_step = max(1, round(len(excl_ms["k_pyramid_level"]) / max(1, args.steps)))
+    pyr_kernel = "k_pyramid_pair" if launches_per_step < NLEVELS else "k_pyramid_level"
+    excl_ms = {(pyr_kernel if k == "k_pyramid_level" else k): v for k, v in excl_ms.items()}
+    launch_ms = {(pyr_kernel if k == "k_pyramid_level" else k): v for k, v in launch_ms.items()}
+    pyr_launch_avg_ms = sum(excl_ms[pyr_kernel]) / max(1, len(excl_ms[pyr_kernel]))
 
     total_feats = feats_per_step * args.steps
     if world > 1:
@@ -1363,7 +1371,7 @@ def main():
         dom = "pyramid"
         nkp_frame = feats_per_step / nfr
         dom_bytes = survey_bytes_per_frame(WIDTH, HEIGHT, nkp_frame) * nfr / launches_per_step
-        model_bytes = algorithmic_bytes_per_frame(WIDTH, HEIGHT, nkp_frame)[dom] * nfr / launches_per_step
+        model_bytes = algorithmic_bytes_per_frame(WIDTH, HEIGHT, nkp_frame, pairs=pyr_kernel == "k_pyramid_pair")[dom] * nfr / launches_per_step
         achieved = dom_bytes / (pyr_launch_avg_ms * 1e-3) / 1e9 if pyr_launch_avg_ms > 0 else 0.0
         pmc = pmc_traffic()
         traffic = None
@@ -1374,9 +1382,9 @@ def main():
         # step (one batch alone on the chip), and against the integer-VALU bound (PMC counters,
         # profiles/pmc_latest.json).  Beside it the step-level attribution: the kernel's share of the
         # summed shared-pass launch time x ms_per_step (what the kernel costs the overlapped step).
-        alg = algorithmic_bytes_per_frame(WIDTH, HEIGHT, nkp_frame)
-        stage_of = {"k_pyramid_level": "pyramid", "k_fast_cells": "fast", "k_quadtree_kp": "quadtree",
-                    "k_describe": "describe"}
+        alg = algorithmic_bytes_per_frame(WIDTH, HEIGHT, nkp_frame, pairs=pyr_kernel == "k_pyramid_pair")
+        stage_of = {"k_pyramid_level": "pyramid", "k_pyramid_pair": "pyramid", "k_fast_cells": "fast",
+                    "k_quadtree_kp": "quadtree", "k_describe": "describe"}
         step_ms = elapsed_ms / args.steps
         shared_total = sum(sum(v) for v in launch_ms.values()) / args.steps
         kern = {}
@@ -1404,7 +1412,7 @@ def main():
             if ps.get("lds_conflict_cycles_per_lds_inst") is not None:
                 ent["lds_conflict_cycles_per_lds_inst"] = round(ps["lds_conflict_cycles_per_lds_inst"], 3)
             kern[k] = ent
-        dom_k = max(kern, key=lambda k: kern[k]["ms_per_step"]) if kern else "k_pyramid_level"
+        dom_k = max(kern, key=lambda k: kern[k]["ms_per_step"]) if kern else pyr_kernel
         dk = kern.get(dom_k, {})
         dom_ach = dk.get("algorithmic_bytes_per_step", 0) / (dk.get("ms_per_step", 1) * 1e-3) / 1e9 if dk else 0.0
         # cross-check: the dominant kernel's exclusive time per step fits inside the step,
@@ -1452,7 +1460,7 @@ def main():
                          "durations": "exclusive: one batch alone on the chip (handle 0, synchronize after each batch); "
                                       "shared_*: the timed region's steps with every in-flight handle; attributed = "
                                       "share of the summed shared launch time x ms_per_step",
-                         "pyramid": {"kernel": "k_pyramid_level", "achieved": round(achieved, 2),
+                         "pyramid": {"kernel": pyr_kernel, "achieved": round(achieved, 2),
                                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                                      "algorithmic_bytes_per_launch": int(dom_bytes),
                                      "traffic_over_algorithmic": round(traffic / dom_bytes, 3) if traffic else None,

@@ -452,6 +452,227 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
 #undef PYR_STAMP
 }
 
+// One lane's output column over kN rows out of an LDS source box: k_pyramid_level's resize in its two
+// forms (the SIMD-path form when every lane of the wave is on the 128-bit vertical path, else the mixed
+// form).  yr: per output row the two source-row byte offsets into `box` and the row weights << 8;
+// sx / sx1: the column's taps relative to a box row, a0 / a1 its weights.  Stores where `ok`.
+template <int kN>
+__device__ __forceinline__ void pyr_resize_col(const uint8_t* __restrict__ box, const int4* __restrict__ yr, int sx,
+                                               int sx1, unsigned a0, unsigned a1, bool simd, bool ok,
+                                               uint8_t* __restrict__ out, int ostride) {
+    if (__ballot(!simd) == 0) {
+        const int sxa = sx & ~3;
+        const uint32_t sel = (uint32_t)(sx & 3) | 0x0c00u | (uint32_t)((sx & 3) + 1) << 16 | 0x0c000000u;
+        const u16x2 A16 = w16(a0 << 4, a1 << 4);
+        auto H = [&](int row_off) -> uint32_t {
+            const uint32_t* p = reinterpret_cast<const uint32_t*>(box + row_off + sxa);
+            const uint32_t pair = __builtin_amdgcn_perm(p[1], p[0], sel);  // s0 | s1 << 16
+            return __builtin_amdgcn_udot2(as_u16x2(pair), A16, 0u, false) & 0xffffff00u;
+        };
+#pragma unroll
+        for (int k = 0; k < kN; ++k) {
+            const int4 Y = yr[k];  // LDS broadcast
+            const uint32_t HA = H(Y.x), HB = H(Y.y);
+            uint32_t m0, m1;
+            asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(m0) : "v"(HA), "v"(Y.z));
+            asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(m1) : "v"(HB), "v"(Y.w));
+            if (ok) out[k * ostride] = (uint8_t)((m0 + m1 + 2) >> 2);
+        }
+    } else {
+        const int hs = simd ? 4 : 0;
+        auto hrow = [&](int off) { return (int)(__umul24(box[off + sx], a0) + __umul24(box[off + sx1], a1)) >> hs; };
+#pragma unroll
+        for (int k = 0; k < kN; ++k) {
+            const int4 Y = yr[k];
+            const int p0 = (int)__umul24((unsigned)hrow(Y.x), (unsigned)Y.z >> 8);
+            const int p1 = (int)__umul24((unsigned)hrow(Y.y), (unsigned)Y.w >> 8);
+            int v = ((p0 >> 16) + (p1 >> 16) + 2) >> 2;
+            if (!simd) v = min((p0 + p1 + (1 << 21)) >> 22, 255);
+            if (ok) out[k * ostride] = (uint8_t)v;
+        }
+    }
+}
+
+// Two levels per pass (round 6).  One workgroup makes a 128 x kTileH tile of level l + 1 -- the tile grid
+// and tile records of k_pyramid_level -- and, on the way, the box U of level l that the tile reads:
+// INTER_LINEAR from an LDS box C of level l - 1, or for l = 0 the input rows themselves.  It also writes
+// the level-l pixels it owns: the level-(l+1) tiles' columns and rows cut level l's written region (view
+// + 3-px border) into disjoint shares, each inside its tile's U together with its REFLECT_101 sources.
+// Level l is therefore never read back from memory by level l + 1, and a batch's pyramid takes 4
+// launches instead of 8.  The arithmetic is k_pyramid_level's; where two tiles' U overlap, both compute
+// the same values.
+constexpr int kPairUP = 164, kPairUH = 32;  // U: row pitch (>= U width + 8: dword over-read), rows
+constexpr int kPairCW = 200, kPairCH = 40;  // C: row pitch (>= C width + 3 alignment + 8), rows (x4)
+static_assert(kPairCH * kPairCW >= kTileH * (kTileW + 8), "the tile reuses C's LDS");
+static_assert(kPairUH == 4 * 8, "U rows: 8 per wave");
+
+struct PairArgs {
+    long long frame_bytes;
+    long long plane_l, plane_n;  // padded planes of level l and l + 1
+    long long src_off;           // level l - 1 view origin (l > 0)
+    int wl, hl, pitch_l, xtab_l, ytab_l, simd_l;  // level l (its tables: the resize from level l - 1)
+    int wn, hn, pitch_n, xtab_n, ytab_n, simd_n;  // level l + 1
+    int spitch;                                   // level l - 1 row pitch
+    int tiles_per_frame, share, tab_off, frame_affine;
+};
+
+template <bool kFirst>
+__global__ __launch_bounds__(256, 8) void k_pyramid_pair(const PairArgs A, const uint8_t* __restrict__ in,
+                                                         long long in_frame_stride, int in_stride,
+                                                         uint8_t* __restrict__ pyr, const int2* __restrict__ xtab,
+                                                         const int4* __restrict__ ytab,
+                                                         const int4* __restrict__ tiletab,
+                                                         const int4* __restrict__ pairtab,
+                                                         int* __restrict__ status_reset) {
+    if (kFirst && status_reset && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *status_reset = 0;
+    int t, f;  // tile of level l + 1 and frame, as k_pyramid_level
+    if (A.frame_affine) {
+        const int L = blockIdx.y * gridDim.x + blockIdx.x, s8 = L >> 3;
+        const int q = s8 / A.tiles_per_frame;
+        t = s8 - q * A.tiles_per_frame;
+        f = (L & 7) + 8 * q;
+        if (f >= (int)gridDim.y) return;
+    } else {
+        t = xcd_tile(blockIdx.x, A.share);
+        if (t >= A.tiles_per_frame) return;
+        f = blockIdx.y;
+    }
+    const int4 T = tiletab[A.tab_off + t];
+    const int4 P = pairtab[2 * (A.tab_off + t)], O = pairtab[2 * (A.tab_off + t) + 1];
+    const int X0 = T.x & 0xffff, Y0 = T.x >> 16;
+    const int ux0 = P.x & 0xffff, uw = P.x >> 16, uy0 = P.y & 0xffff, uh = P.y >> 16;
+    const int cx0 = P.z & 0xffff, cw = P.z >> 16, cy0 = P.w & 0xffff, ch = P.w >> 16;
+    const int ox0 = (int)(int16_t)(O.x & 0xffff), ox1 = O.x >> 16, oy0 = (int)(int16_t)(O.y & 0xffff), oy1 = O.y >> 16;
+    // C, then (once U is made) the level-(l+1) tile: one LDS area
+    __shared__ __attribute__((aligned(16))) uint8_t cbox[kFirst ? kTileH * (kTileW + 8) : kPairCH * kPairCW];
+    __shared__ __attribute__((aligned(16))) uint8_t ubuf[kPairUH * kPairUP];
+    uint8_t (*tile)[kTileW + 8] = reinterpret_cast<uint8_t (*)[kTileW + 8]>(cbox);  // +8: lds_bytes8 over-read
+    __shared__ int4 yrowU[kPairUH];
+    __shared__ int4 yrowT[kTileH];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = uniform(tid >> 6);
+    uint8_t* plane_l = pyr + (size_t)f * A.frame_bytes + A.plane_l;
+    uint8_t* plane_n = pyr + (size_t)f * A.frame_bytes + A.plane_n;
+    // the level-(l+1) tile: written region, this lane's column (view coordinates) and its taps in U
+    const int ex = kEdge + A.wn + kBorder, ey = kEdge + A.hn + kBorder;
+    const int tx = (wave & 1) * 64 + lane, r0 = (wave >> 1) * (kTileH / 2);
+    const int vxn = reflect101(min(X0 + tx, ex - 1) - kEdge, A.wn);
+    // 1. every global load of the block before the first LDS store
+    int2 XU[3] = {make_int2(0, 0), make_int2(0, 0), make_int2(0, 0)};
+    int4 yu = make_int4(0, 0, 0, 0);
+    int shift = 0;
+    if (kFirst) {
+        // U = input pixels [ux0, ux0 + uw) x [uy0, uy0 + uh): per row (wave-uniform) the aligned dwords
+        // from the row's first byte, realigned by v_alignbyte (buffer loads over the frame rounded up to
+        // whole dwords; 0 past it)
+        const uint8_t* fbase = in + (size_t)f * in_frame_stride;
+        const uintptr_t fb = reinterpret_cast<uintptr_t>(fbase);
+        const int fmis = uniform((int)(fb & 3));
+        const uint64_t fal = (uint64_t)(uint32_t)uniform((int)(uint32_t)(fb - fmis)) |
+                             (uint64_t)(uint32_t)uniform((int)(uint32_t)((fb - fmis) >> 32)) << 32;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<void*>(fal), (short)0, uniform((fmis + (A.hl - 1) * in_stride + A.wl + 3) & ~3), kBufDword3);
+        uint32_t w0[8], w1[8];
+        int sh[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int y = uy0 + min(wave + 4 * q, uh - 1);
+            const int off = uniform(fmis + y * in_stride + ux0), oa = off & ~3;
+            sh[q] = off & 3;
+            w0[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, oa + 4 * lane, 0, 0);
+            w1[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, oa + 4 * lane + 4, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (4 * lane < kPairUP)
+                reinterpret_cast<uint32_t*>(ubuf + (wave + 4 * q) * kPairUP)[lane] = __builtin_amdgcn_alignbyte(w1[q], w0[q], sh[q]);
+    } else {
+        // C = level l - 1 view box [cx0, cx0 + cw) x [cy0, cy0 + ch) as aligned dwords (k_pyramid_level's
+        // box load, bounded to the rows and words the resize reads)
+        shift = (int)((A.src_off + cx0) & 3);
+        const long long box_off = A.src_off + (long long)cy0 * A.spitch + (cx0 - shift);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            pyr + (size_t)f * A.frame_bytes + box_off, (short)0, (int)(A.frame_bytes - box_off), kBufDword3);
+        const int cwords = min((cw + shift + 3) / 4 + 1, kPairCW / 4), rg = tid >> 6;
+        constexpr int kRowPass = kPairCH / 4;
+        uint32_t v[kRowPass];
+#pragma unroll
+        for (int q = 0; q < kRowPass; ++q)
+            v[q] = (4 * q + rg < ch && lane < cwords)
+                       ? __builtin_amdgcn_raw_buffer_load_b32(rs, rg * A.spitch + 4 * lane, 4 * q * A.spitch, 0) : 0u;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) XU[c] = xtab[A.xtab_l + ux0 + min(64 * c + lane, uw - 1)];
+        if (tid < kPairUH) yu = ytab[A.ytab_l + uy0 + min(tid, uh - 1)];
+#pragma unroll
+        for (int q = 0; q < kRowPass; ++q)
+            if (lane < kPairCW / 4) reinterpret_cast<uint32_t*>(cbox + (4 * q + rg) * kPairCW)[lane] = v[q];
+        if (tid < kPairUH)
+            yrowU[tid] = make_int4((yu.x - cy0) * kPairCW, (yu.y - cy0) * kPairCW, yu.z << 8, yu.w << 8);
+    }
+    int4 yv = make_int4(0, 0, 0, 0);
+    if (tid < kTileH) yv = ytab[A.ytab_n + reflect101(min(Y0 + tid, ey - 1) - kEdge, A.hn)];
+    const int2 XN = xtab[A.xtab_n + vxn];
+    if (tid < kTileH) yrowT[tid] = make_int4((yv.x - uy0) * kPairUP, (yv.y - uy0) * kPairUP, yv.z << 8, yv.w << 8);
+    __syncthreads();
+    // 2. U from C (l > 0): lane per U column (three 64-column passes), wave per 8 rows; rows past uh
+    //    repeat the last one (never read), columns past uw are not stored
+    if (!kFirst) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            if (64 * c >= uw) break;
+            const int col = 64 * c + lane, vx = ux0 + min(col, uw - 1);
+            const int sx = XU[c].x - cx0 + shift, sx1 = min(XU[c].x + 1, cx0 + cw - 1) - cx0 + shift;
+            pyr_resize_col<8>(cbox, &yrowU[8 * wave], sx, sx1, (unsigned)XU[c].y & 0xffffu, (unsigned)XU[c].y >> 16,
+                              vx < A.simd_l, col < uw, &ubuf[8 * wave * kPairUP + col], kPairUP);
+        }
+        __syncthreads();
+    }
+    // 3a. the owned share of level l: [ox0, ox1) x [oy0, oy1) in view coordinates (border included), a
+    //     plane dword per lane (interior dwords as two aligned LDS reads + v_alignbyte), a row per wave
+    {
+        const int pc0 = (ox0 + kEdge) & ~3;
+        const int ndw = ((ox1 + kEdge - 1) >> 2) - (pc0 >> 2) + 1;
+        for (int r = wave; r < oy1 - oy0; r += 4) {
+            const int y = oy0 + r;
+            const uint8_t* urow = ubuf + (reflect101(y, A.hl) - uy0) * kPairUP;
+            uint8_t* dst = plane_l + (size_t)(y + kEdge) * A.pitch_l;
+            if (lane < ndw) {
+                const int pc = pc0 + 4 * lane, x = pc - kEdge;
+                if (x >= ox0 && x + 4 <= ox1 && x >= 0 && x + 4 <= A.wl) {
+                    const int o = x - ux0;
+                    const uint32_t* w = reinterpret_cast<const uint32_t*>(urow) + (o >> 2);
+                    *reinterpret_cast<uint32_t*>(dst + pc) = __builtin_amdgcn_alignbyte(w[1], w[0], o & 3);
+                } else {
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        if (x + b >= ox0 && x + b < ox1) dst[pc + b] = urow[reflect101(x + b, A.wl) - ux0];
+                }
+            }
+        }
+    }
+    // 3b. the level-(l+1) tile from U
+    {
+        const int sx = XN.x - ux0, sx1 = min(XN.x + 1, ux0 + uw - 1) - ux0;
+        pyr_resize_col<kTileH / 2>(ubuf, &yrowT[r0], sx, sx1, (unsigned)XN.y & 0xffffu, (unsigned)XN.y >> 16,
+                                   vxn < A.simd_n, true, &tile[r0][tx], kTileW + 8);
+    }
+    __syncthreads();
+    // 4. store the tile: 8 consecutive pixels per thread, 16 rows per pass, clipped to the written region
+#pragma unroll
+    for (int r = tid >> 4; r < kTileH; r += 16) {
+        const int c = (tid & 15) * 8;
+        const int py = Y0 + r, px = X0 + c;
+        if (py < ey && px < ex) {
+            uint8_t* dst = plane_n + (size_t)py * A.pitch_n + px;
+            if (px + 7 < ex) {
+                *reinterpret_cast<unsigned long long*>(dst) = lds_bytes8(tile[r], c);
+            } else {
+                for (int k = 0; k < 8 && px + k < ex; ++k) dst[k] = tile[r][c + k];
+            }
+        }
+    }
+}
+
 // Debug (orb_debug_level_blurred): the reference's GaussianBlur(level.clone(), 7x7, 2, 2,
 // BORDER_REFLECT_101) of a whole level view, one thread per pixel, from the stored view (the
 // descriptor kernel blurs only its own samples; this is the test hook for that arithmetic).
@@ -1931,6 +2152,10 @@ struct Extractor {
     CellDesc* d_cells = nullptr; size_t cells_cap = 0;
     int2* d_xtab = nullptr; size_t xtab_cap = 0;
     int4* d_tiletab = nullptr; size_t tiletab_cap = 0;  // pyramid tile records (tile_tables)
+    int4* d_pairtab = nullptr; size_t pairtab_cap = 0;  // their two-level records (pair_tables)
+    bool pair_ok = false;                               // the geometry fits k_pyramid_pair's boxes
+    int pyr_pair = 0;                                   // ORBGPU_PYR_PAIR=1: two levels per pyramid pass (measured
+                                                        // slower with batches in flight; off by default)
     int tile_off[orbgpu::kMaxLevels] = {};
     int4* d_ytab = nullptr; size_t ytab_cap = 0;
     uint8_t* d_pyr = nullptr; size_t pyr_cap = 0;
@@ -1967,6 +2192,9 @@ struct Extractor {
     int chain_fast_split = 1;           // one-chain FAST launches (see launch_chunk; ORBGPU_CHAIN_FAST)
     int qt_key_room = 4;                // KB of quad-tree LDS for keys beyond the node tables (ORBGPU_QT_KEYROOM)
     int pyr_affine = 1;                 // pyramid tiles of a frame on one XCD (ORBGPU_PYR_AFFINE=0: spread, for the A/B)
+    int ablate = 0;                     // timing study only (ORBGPU_ABLATE): skip stage launches, outputs stale --
+                                        // 1 pyramid levels > 0, 2 level 0, 4 FAST, 8 quad-tree, 16 describe,
+                                        // 32 levels >= 4, 64 levels 1-3
     int fast_per_level = 0;             // 1: FAST of each later level right after its pyramid level (side2); measured slower
     int desc_split = 1;                 // 1: quad-tree + descriptors of levels [0, fast_split) on the side stream (ORBGPU_DESC_SPLIT)
     orb_keypoint_t* d_st_kp = nullptr; size_t st_kp_cap = 0;   // their staging records (desc_split)
@@ -2053,6 +2281,62 @@ void tile_tables(const orbgpu::KernelGeom& k, std::vector<int4>& tab, int* off) 
     }
 }
 
+// Two-level records (k_pyramid_pair), two int4 per tile of each level n = l + 1 with l even, at twice the
+// tile's index in the tile table (other entries unused):
+//   {ux0 | uw << 16, uy0 | uh << 16, cx0 | cw << 16, cy0 | ch << 16}: U, the level-l view box the workgroup
+//     computes, and C, the level-(l-1) view box U's taps read (l > 0; the kernel's double expressions, as
+//     tile_tables);
+//   {ox0 | ox1 << 16, oy0 | oy1 << 16} (16-bit signed): the level-l range it writes, border included.
+// The tile columns cut level l's written columns at their first source column (tile_tables' bx0), the
+// tile rows its rows likewise.  U is the hull of the tile's own box and the owned range's REFLECT_101
+// sources.  Returns false if a box exceeds the kernel's LDS boxes (the level-by-level path runs then).
+bool pair_tables(const orbgpu::KernelGeom& k, const std::vector<int4>& tiles, const int* off, std::vector<int4>& tab) {
+    auto src = [](int d, double scale, int slen) {
+        const float f = (float)((d + 0.5) * scale - 0.5);
+        int s2 = (int)f;
+        s2 -= (s2 > f);
+        return std::min(std::max(s2, 0), slen - 1);
+    };
+    auto refl = [](int p, int len) { p = p < 0 ? -p : p; return p >= len ? 2 * len - 2 - p : p; };
+    tab.assign(2 * tiles.size(), make_int4(0, 0, 0, 0));
+    for (int nl = 1; nl < k.nlevels; nl += 2) {
+        const orbgpu::LevelGeom &N = k.lv[nl], &L = k.lv[nl - 1];
+        const int ntx = pyr_tiles_x(N), nty = pyr_tiles_y(N);
+        std::vector<int> cx(ntx + 1), cy(nty + 1);
+        cx[0] = -kBorder; cx[ntx] = L.w + kBorder;
+        cy[0] = -kBorder; cy[nty] = L.h + kBorder;
+        for (int i = 1; i < ntx; ++i) cx[i] = tiles[off[nl] + i].y & 0xffff;
+        for (int j = 1; j < nty; ++j) cy[j] = tiles[off[nl] + j * ntx].z & 0xffff;
+        for (int i = 0; i < ntx; ++i) if (cx[i] >= cx[i + 1]) return false;
+        for (int j = 0; j < nty; ++j) if (cy[j] >= cy[j + 1]) return false;
+        for (int ty = 0; ty < nty; ++ty)
+            for (int tx = 0; tx < ntx; ++tx) {
+                const int idx = off[nl] + ty * ntx + tx;
+                const int4 T = tiles[idx];
+                int ux0 = T.y & 0xffff, ux1 = ux0 + (T.y >> 16), uy0 = T.z & 0xffff, uy1 = uy0 + (T.z >> 16);
+                const int ox0 = cx[tx], ox1 = cx[tx + 1], oy0 = cy[ty], oy1 = cy[ty + 1];
+                for (int x = ox0; x < ox1; ++x) { const int v = refl(x, L.w); ux0 = std::min(ux0, v); ux1 = std::max(ux1, v + 1); }
+                for (int y = oy0; y < oy1; ++y) { const int v = refl(y, L.h); uy0 = std::min(uy0, v); uy1 = std::max(uy1, v + 1); }
+                const int uw = ux1 - ux0, uh = uy1 - uy0;
+                const int ndw = ((ox1 + kEdge - 1) >> 2) - ((ox0 + kEdge) >> 2) + 1;
+                if (uw + 8 > kPairUP || uh > kPairUH || ndw > 64 || ox0 < -32768 || ox1 > 32767) return false;
+                int cx0 = 0, cw = 0, cy0 = 0, chh = 0;
+                if (nl > 1) {
+                    const orbgpu::LevelGeom& Pv = k.lv[nl - 2];
+                    const double scx = 1. / ((double)L.w / Pv.w), scy = 1. / ((double)L.h / Pv.h);
+                    cx0 = src(ux0, scx, Pv.w);
+                    cw = std::min(src(ux1 - 1, scx, Pv.w) + 1, Pv.w - 1) - cx0 + 1;
+                    cy0 = src(uy0, scy, Pv.h);
+                    chh = std::min(src(uy1 - 1, scy, Pv.h) + 1, Pv.h - 1) - cy0 + 1;
+                    if (cw + 3 + 8 > kPairCW || chh > kPairCH) return false;
+                }
+                tab[2 * idx] = make_int4(ux0 | uw << 16, uy0 | uh << 16, cx0 | cw << 16, cy0 | chh << 16);
+                tab[2 * idx + 1] = make_int4((ox0 & 0xffff) | ox1 << 16, (oy0 & 0xffff) | oy1 << 16, 0, 0);
+            }
+    }
+    return true;
+}
+
 int prepare(Extractor* e, int w, int h, int n) {
     if (w != e->cur_w || h != e->cur_h) {
         // the tables below are read by in-flight launches of the previous frame size
@@ -2094,6 +2378,13 @@ int prepare(Extractor* e, int w, int h, int n) {
         if ((rc = grow(e->d_tiletab, e->tiletab_cap, tt.size())) != ORB_OK) return rc;
         if (hipMemcpy(e->d_tiletab, tt.data(), tt.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess)
             return orbgpu_fail(ORB_ERR_DEVICE, "table upload failed");
+        std::vector<int4> pt;
+        e->pair_ok = pair_tables(g.k, tt, e->tile_off, pt);
+        if (e->pair_ok) {
+            if ((rc = grow(e->d_pairtab, e->pairtab_cap, pt.size())) != ORB_OK) return rc;
+            if (hipMemcpy(e->d_pairtab, pt.data(), pt.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess)
+                return orbgpu_fail(ORB_ERR_DEVICE, "table upload failed");
+        }
         e->geo_ok = true;
         // quad-tree LDS: node metadata of the largest level (larger feature budgets, e.g. the 5x
         // monocular-init extractor, need more) + key room
@@ -2182,6 +2473,7 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
         return pe;
     };
     auto launch_fast = [&](int l0, int l1, hipStream_t s2) {
+        if (e->ablate & 4) return;
         const int c0 = k.lv[l0].cell_begin, c1 = k.lv[l1 - 1].cell_begin + k.lv[l1 - 1].cell_count;
         if (c1 <= c0) return;
         unsigned long long* stamps = nullptr;
@@ -2231,7 +2523,7 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     };
     // quad-tree of levels [l0, l1): one wave per (level, frame)
     auto launch_qt = [&](int l0, int l1, hipStream_t s2) {
-        if (l1 <= l0) return;
+        if (l1 <= l0 || (e->ablate & 8)) return;
         unsigned long long* qst = e->d_stamps ? e->d_stamps + (size_t)f0 * k.nlevels * kQtStamps : nullptr;
         if (hipEvent_t* pe = launch_events(kLaunchQuadtree))
             hipExtLaunchKernelGGL(k_quadtree_kp, dim3(l1 - l0, n), dim3(kQtThreads), e->qt_lds, s2, pe[0], pe[1], 0,
@@ -2245,6 +2537,7 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     // `split` from their staging records; 0: all levels computed here)
     bool desc_split = false;  // set once the pyramid path is known (below)
     auto launch_desc = [&](int mode, int lim, hipStream_t s2) {
+        if (e->ablate & 16) return;
         int chunks = 0;  // blocks per frame: ceil(sel_cap_l / 8) per level (see k_describe)
         for (int l = 0; l < lim; ++l) chunks += (k.lv[l].sel_cap + kDescKpPerBlock - 1) / kDescKpPerBlock;
         const int total = chunks * n, share = (total + 7) / 8;
@@ -2266,7 +2559,64 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     desc_split = e->desc_split && split > 0 && !e->fast_per_level && e->d_st_kp;
     const bool qts = (e->qt_split || desc_split) && split > 0 && !e->fast_per_level;
     const bool pyr_stamps = e->pyr_stamps;
+    // what follows pyramid level l on the streams (FAST of the early levels once they exist)
+    auto level_done = [&](int l) {
+        if (!split && chain_lds_split == 2 && l == chain_s - 1) {
+            launch_fast(0, chain_s, st);  // one chain: the early levels' FAST right after their pyramid levels
+        } else if (split && l == split - 1) {
+            hipEventRecord(e->split_ev[0], st);
+            hipStreamWaitEvent(e->side, e->split_ev[0], 0);
+            launch_fast(0, split, e->side);
+            if (qts) launch_qt(0, split, e->side);
+            if (desc_split) launch_desc(1, split, e->side);
+            hipEventRecord(e->split_ev[1], e->side);
+        } else if (split && l >= split && e->fast_per_level) {
+            // later (small) levels: FAST as soon as the level exists, on a second side stream
+            hipEventRecord(e->lvl_ev[l], st);
+            hipStreamWaitEvent(e->side2, e->lvl_ev[l], 0);
+            launch_fast(l, l + 1, e->side2);
+        }
+    };
+    // two levels per pass (k_pyramid_pair) when the geometry fits its boxes; the phase-clock debug
+    // mode (ORBGPU_PYR_STAMPS) times the level kernel
+    const bool pairs = e->pyr_pair && e->pair_ok && !pyr_stamps;
     for (int l = 0; l < k.nlevels; ++l) {
+        if (pairs && (l & 1) == 0 && l + 1 < k.nlevels) {
+            const orbgpu::LevelGeom &Ll = k.lv[l], &Ln = k.lv[l + 1];
+            PairArgs A{};
+            A.frame_bytes = k.pyr_frame_bytes;
+            A.plane_l = Ll.plane_off;
+            A.plane_n = Ln.plane_off;
+            if (l > 0) {
+                const orbgpu::LevelGeom& P = k.lv[l - 1];
+                A.src_off = P.plane_off + (long long)kEdge * P.pitch + kEdge;
+                A.spitch = P.pitch;
+            }
+            A.wl = Ll.w; A.hl = Ll.h; A.pitch_l = Ll.pitch; A.xtab_l = Ll.xtab_off; A.ytab_l = Ll.ytab_off; A.simd_l = Ll.simd_end;
+            A.wn = Ln.w; A.hn = Ln.h; A.pitch_n = Ln.pitch; A.xtab_n = Ln.xtab_off; A.ytab_n = Ln.ytab_off; A.simd_n = Ln.simd_end;
+            A.tab_off = e->tile_off[l + 1];
+            A.tiles_per_frame = pyr_tiles_x(Ln) * pyr_tiles_y(Ln);
+            A.share = (A.tiles_per_frame + 7) / 8;
+            A.frame_affine = e->pyr_affine && n % 8 == 0;
+            const dim3 grid(8 * A.share, n);
+            hipEvent_t* pe = launch_events(kLaunchPyramid);
+            auto go = [&](auto kern, auto... args) {
+                if (e->ablate & (l == 0 ? 3 : 1)) return;
+                if (pe) hipExtLaunchKernelGGL(kern, grid, dim3(256), 0, st, pe[0], pe[1], 0, args...);
+                else hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, args...);
+            };
+            if (l == 0)
+                go(k_pyramid_pair<true>, A, imgs, (long long)frame_stride, stride, pyr, (const int2*)e->d_xtab,
+                   (const int4*)e->d_ytab, (const int4*)e->d_tiletab, (const int4*)e->d_pairtab,
+                   e->clear_status_l0 && f0 == 0 ? e->d_status : (int*)nullptr);
+            else
+                go(k_pyramid_pair<false>, A, (const uint8_t*)nullptr, 0LL, 0, pyr, (const int2*)e->d_xtab,
+                   (const int4*)e->d_ytab, (const int4*)e->d_tiletab, (const int4*)e->d_pairtab, (int*)nullptr);
+            level_done(l);
+            level_done(l + 1);
+            ++l;
+            continue;
+        }
         const orbgpu::LevelGeom& L = k.lv[l];
         PyrArgs A{};
         A.frame_bytes = k.pyr_frame_bytes;
@@ -2291,6 +2641,9 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
         // begin / end timestamps -- the interval rocprofv3's kernel trace reports for it
         hipEvent_t* pe = launch_events(kLaunchPyramid);
         auto go = [&](auto kern, auto... args) {
+            if (e->ablate & (l == 0 ? 2 : 1)) return;
+            if ((e->ablate & 32) && l >= 4) return;
+            if ((e->ablate & 64) && l >= 1 && l < 4) return;
             if (pe) hipExtLaunchKernelGGL(kern, grid, dim3(256), 0, st, pe[0], pe[1], 0, args...);
             else hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, args...);
         };
@@ -2327,21 +2680,7 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
                     l, cnt, (t1 - t0) * 0.01, life / cnt * 0.01, life / (double)(t1 - t0), ph[1] / cnt, ph[2] / cnt,
                     ph[3] / cnt);
         }
-        if (!split && chain_lds_split == 2 && l == chain_s - 1) {
-            launch_fast(0, chain_s, st);  // one chain: the early levels' FAST right after their pyramid levels
-        } else if (split && l == split - 1) {
-            hipEventRecord(e->split_ev[0], st);
-            hipStreamWaitEvent(e->side, e->split_ev[0], 0);
-            launch_fast(0, split, e->side);
-            if (qts) launch_qt(0, split, e->side);
-            if (desc_split) launch_desc(1, split, e->side);
-            hipEventRecord(e->split_ev[1], e->side);
-        } else if (split && l >= split && e->fast_per_level) {
-            // later (small) levels: FAST as soon as the level exists, on a second side stream
-            hipEventRecord(e->lvl_ev[l], st);
-            hipStreamWaitEvent(e->side2, e->lvl_ev[l], 0);
-            launch_fast(l, l + 1, e->side2);
-        }
+        level_done(l);
     }
     mark(1);
     if (split && e->fast_per_level) {
@@ -2376,6 +2715,10 @@ int launch_batch(Extractor* e, const uint8_t* d_images, int n, int w, int h, int
                  int lap0, int lap1, orb_keypoint_t* d_kps, uint8_t* d_desc, int cap, int32_t* d_counts,
                  hipStream_t st) {
     (void)w; (void)h;
+    {   // timing study only: re-read per call, so a handle warmed with every stage can then skip some
+        const char* c = getenv("ORBGPU_ABLATE");
+        e->ablate = c ? atoi(c) : 0;
+    }
     // the level-0 pyramid launch of the first (sub-)batch clears the status; sub-batches on several
     // streams need it cleared before the fork
     e->clear_status_l0 = !(e->nstreams > 1 && (n + e->chunk - 1) / e->chunk > 1);
@@ -2434,6 +2777,7 @@ int orb_extractor_create(const orb_params_t* p, int max_width, int max_height, i
     if (const char* c = getenv("ORBGPU_CHAIN_FAST")) e->chain_fast_split = atoi(c);
     if (const char* c = getenv("ORBGPU_QT_KEYROOM")) e->qt_key_room = std::max(0, atoi(c));
     if (const char* c = getenv("ORBGPU_PYR_AFFINE")) e->pyr_affine = atoi(c);
+    if (const char* c = getenv("ORBGPU_PYR_PAIR")) e->pyr_pair = atoi(c);
     bool ok = hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) == hipSuccess &&
               hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&e->side2, hipStreamNonBlocking) == hipSuccess;
@@ -2482,7 +2826,7 @@ int orb_extractor_destroy(orb_extractor_t h) {
     Extractor* e = reinterpret_cast<Extractor*>(h);
     if (!e) return ORB_ERR_ARG;
     if (e->stream) hipStreamSynchronize(e->stream);
-    void* bufs[] = {e->d_st_kp, e->d_st_desc, e->d_stamps, e->d_geom, e->d_cells, e->d_xtab, e->d_tiletab, e->d_ytab, e->d_pyr, e->d_cand, e->d_scratch,
+    void* bufs[] = {e->d_st_kp, e->d_st_desc, e->d_stamps, e->d_geom, e->d_cells, e->d_xtab, e->d_tiletab, e->d_pairtab, e->d_ytab, e->d_pyr, e->d_cand, e->d_scratch,
                     e->d_cell_count, e->d_cell_thr, e->d_sel, e->d_dst, e->d_sel_count, e->d_lap_count, e->d_status_own,
                     e->d_img, e->d_out};
     for (void* b : bufs)
@@ -2599,7 +2943,8 @@ int orb_extract(orb_extractor_t h, const uint8_t* image, int width, int height, 
             (uintptr_t)e->d_scratch, (uintptr_t)e->d_cell_count, (uintptr_t)e->d_cell_thr, (uintptr_t)e->d_sel,
             (uintptr_t)e->d_dst, (uintptr_t)e->d_sel_count, (uintptr_t)e->d_lap_count, (uintptr_t)e->d_st_kp,
             (uintptr_t)e->d_st_desc, (uintptr_t)e->d_geom, (uintptr_t)e->d_cells, (uintptr_t)e->d_xtab,
-            (uintptr_t)e->d_ytab, (uintptr_t)e->d_tiletab, (uintptr_t)e->qt_lds, (uintptr_t)e->d_stamps};
+            (uintptr_t)e->d_ytab, (uintptr_t)e->d_tiletab, (uintptr_t)e->d_pairtab, (uintptr_t)(e->pyr_pair && e->pair_ok),
+            (uintptr_t)e->qt_lds, (uintptr_t)e->d_stamps};
         if (!e->g1_exec || key != e->g1_key) {
             if (e->g1_exec) { (void)hipGraphExecDestroy(e->g1_exec); e->g1_exec = nullptr; }
             if (e->g1_graph) { (void)hipGraphDestroy(e->g1_graph); e->g1_graph = nullptr; }

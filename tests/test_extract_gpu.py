@@ -275,8 +275,9 @@ def test_sparse_corners_parity(pkg, oracle):
 
 @pytest.mark.parametrize("env", [{"ORBGPU_CHUNK": "2"}, {"ORBGPU_STREAMS": "2", "ORBGPU_CHUNK": "3"},
                                  {"ORBGPU_FAST_SPLIT": "3"}, {"ORBGPU_FAST_PER_LEVEL": "1"}, {"ORBGPU_QT_SPLIT": "1"},
-                                 {"ORBGPU_FAST_STAMPS": "1", "ORBGPU_PYR_STAMPS": "1"}],
-                         ids=["chunk2", "streams2_chunk3", "fast_split3", "fast_per_level", "qt_split", "phase_stamps"])
+                                 {"ORBGPU_FAST_STAMPS": "1", "ORBGPU_PYR_STAMPS": "1"}, {"ORBGPU_PYR_PAIR": "1"}],
+                         ids=["chunk2", "streams2_chunk3", "fast_split3", "fast_per_level", "qt_split", "phase_stamps",
+                              "two_level_pyramid"])
 def test_schedule_switches_parity(pkg, oracle, synth, monkeypatch, env):
     """Every per-handle schedule switch (read when the handle is created; orb_extract.hip
     orb_extractor_create) changes only how the batch is cut into launches and streams: a 7-frame batch
@@ -353,11 +354,15 @@ def test_set_overlap_parity(pkg, oracle, synth):
     (1280, 720, "noise", 800, 2.0, 4, 20, 7),    # ratio 2, few levels
     (752, 480, "poly", 1000, 1.1, 12, 15, 5),    # 12 levels (kMaxLevels), low thresholds
     (104, 110, "noise", 200, 1.2, 2, 20, 7),     # one cell column per level: 72- and 55-px FAST windows
+    (640, 480, "poly", 1000, 1.2, 7, 20, 7),     # odd level count (with ORBGPU_PYR_PAIR=1: three two-level passes, then one)
 ])
-def test_extract_parity_other_parameters(pkg, oracle, synth, w, h, kind, nf, scale, nlevels, ini, mn):
+@pytest.mark.parametrize("pair", ["0", "1"], ids=["level_passes", "two_level_passes"])
+def test_extract_parity_other_parameters(pkg, oracle, synth, monkeypatch, w, h, kind, nf, scale, nlevels, ini, mn, pair):
     """ORBextractor parameters other than the 1.2 / 8 / 20 / 7 of the bench configs (the reference
     reads them from the settings file, src/Tracking.cc:1346-1362): pyramid levels, keypoints (bitwise)
-    and descriptors against the oracle."""
+    and descriptors against the oracle, with the level-by-level pyramid and with the two-level passes
+    (ORBGPU_PYR_PAIR=1; level ratios above ~1.25 do not fit its boxes and keep the level passes)."""
+    monkeypatch.setenv("ORBGPU_PYR_PAIR", pair)
     img = synth.polygon_frame(w, h, seed=21) if kind == "poly" else synth.blurred_noise_frame(w, h, seed=22)
     ex = pkg.ORBextractor(nf, scale, nlevels, ini, mn, max_width=w, max_height=h)
     ref = oracle.OracleExtractor(nf, scale, nlevels, ini, mn)

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Critical path of the C2 step from a rocprofv3 kernel trace (csv) of bench.py: the extraction
-kernels grouped into batches per stream (k_pyramid_level x levels -> k_fast_cells -> k_quadtree_kp ->
+kernels grouped into batches per stream (k_pyramid_pair / k_pyramid_level passes -> k_fast_cells -> k_quadtree_kp ->
 k_describe on one handle's stream), then per batch its span (first start to last end), the kernel time
 inside it, and the gaps between its kernels (the batch waiting for the device: other batches' kernels
 hold the CUs, or the host had not enqueued the next launch).  With H batches in flight the step time
@@ -18,6 +18,9 @@ STAGES = ("k_pyramid_level", "k_fast_cells", "k_quadtree_kp", "k_describe")
 
 
 def short(name):
+    """Stage of a kernel (the two-level k_pyramid_pair passes count as the pyramid stage)."""
+    if "k_pyramid_pair" in name:
+        return "k_pyramid_level"
     for s in STAGES:
         if s in name:
             return s

@@ -12,11 +12,11 @@ import json
 import re
 import sys
 
-STAGE_KERNELS = {"pyramid": ["k_pyramid_level"], "fast": ["k_fast_cells"], "quadtree": ["k_quadtree_kp"],
+STAGE_KERNELS = {"pyramid": ["k_pyramid_pair", "k_pyramid_level"], "fast": ["k_fast_cells"], "quadtree": ["k_quadtree_kp"],
                  "describe": ["k_describe"]}
-# launches per step: 8 pyramid levels; FAST two (levels 0-2, 3-7), quad-tree and describe one each (the bench's handles
+# launches per step: 4 two-level pyramid passes (8 level passes with ORBGPU_PYR_PAIR=0); FAST two (levels 0-2, 3-7), quad-tree and describe one each (the bench's handles
 # run one chain per batch, orb_extractor_set_overlap(h, 0); with the side-stream overlap they are two)
-LAUNCHES = {"k_pyramid_level": 8, "k_fast_cells": 2, "k_quadtree_kp": 1, "k_describe": 1}
+LAUNCHES = {"k_pyramid_pair": 4, "k_pyramid_level": 8, "k_fast_cells": 2, "k_quadtree_kp": 1, "k_describe": 1}
 
 
 def main(d, out, frames=64):
@@ -43,9 +43,10 @@ def main(d, out, frames=64):
             fetch += 2 * 1024 * sum(fd.values()) / len(fd) * nper
             if wd:
                 write += 1024 * sum(wd.values()) / len(wd) * nper
-            launches = nper
+            launches += nper
         if launches:
-            res["stages"][stage] = {"fetch_bytes": fetch, "write_bytes": write, "hbm_bytes": fetch + write}
+            res["stages"][stage] = {"fetch_bytes": fetch, "write_bytes": write, "hbm_bytes": fetch + write,
+                                    "launches_per_step": launches}
             # integer-VALU bound: a wave64 VALU instruction issues over 2 cycles
             # (MI355X_MICROARCH.md), 1024 SIMDs, GRBM_GUI_ACTIVE summed over the 8 XCDs:
             # frac = SQ_INSTS_VALU x 2 / (1024 x GRBM_GUI_ACTIVE / 8), over the stage's dispatches
@@ -66,7 +67,7 @@ def main(d, out, frames=64):
     dom = max(res["stages"], key=lambda s: res["stages"][s]["hbm_bytes"]) if res["stages"] else None
     res["kernel_stage"] = "pyramid" if "pyramid" in res["stages"] else dom
     if res["kernel_stage"]:
-        n = LAUNCHES.get(STAGE_KERNELS[res["kernel_stage"]][0], 1)
+        n = res["stages"][res["kernel_stage"]]["launches_per_step"]
         res["hbm_bytes_per_step"] = res["stages"][res["kernel_stage"]]["hbm_bytes"]
         res["launches_per_step"] = n
         res["hbm_bytes_per_launch"] = res["hbm_bytes_per_step"] / n
