@@ -456,7 +456,7 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_level(const PyrArgs A, const
 // forms (the SIMD-path form when every lane of the wave is on the 128-bit vertical path, else the mixed
 // form).  yr: per output row the two source-row byte offsets into `box` and the row weights << 8;
 // sx / sx1: the column's taps relative to a box row, a0 / a1 its weights.  Stores where `ok`.
-template <int kN>
+template <int kN, int kYS = 1>
 __device__ __forceinline__ void pyr_resize_col(const uint8_t* __restrict__ box, const int4* __restrict__ yr, int sx,
                                                int sx1, unsigned a0, unsigned a1, bool simd, bool ok,
                                                uint8_t* __restrict__ out, int ostride) {
@@ -471,7 +471,7 @@ __device__ __forceinline__ void pyr_resize_col(const uint8_t* __restrict__ box, 
         };
 #pragma unroll
         for (int k = 0; k < kN; ++k) {
-            const int4 Y = yr[k];  // LDS broadcast
+            const int4 Y = yr[k * kYS];  // LDS broadcast
             const uint32_t HA = H(Y.x), HB = H(Y.y);
             uint32_t m0, m1;
             asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(m0) : "v"(HA), "v"(Y.z));
@@ -483,7 +483,7 @@ __device__ __forceinline__ void pyr_resize_col(const uint8_t* __restrict__ box, 
         auto hrow = [&](int off) { return (int)(__umul24(box[off + sx], a0) + __umul24(box[off + sx1], a1)) >> hs; };
 #pragma unroll
         for (int k = 0; k < kN; ++k) {
-            const int4 Y = yr[k];
+            const int4 Y = yr[k * kYS];
             const int p0 = (int)__umul24((unsigned)hrow(Y.x), (unsigned)Y.z >> 8);
             const int p1 = (int)__umul24((unsigned)hrow(Y.y), (unsigned)Y.w >> 8);
             int v = ((p0 >> 16) + (p1 >> 16) + 2) >> 2;
@@ -601,7 +601,8 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_pair(const PairArgs A, const
             v[q] = (4 * q + rg < ch && lane < cwords)
                        ? __builtin_amdgcn_raw_buffer_load_b32(rs, rg * A.spitch + 4 * lane, 4 * q * A.spitch, 0) : 0u;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) XU[c] = xtab[A.xtab_l + ux0 + min(64 * c + lane, uw - 1)];
+        for (int c = 0; c < 2; ++c) XU[c] = xtab[A.xtab_l + ux0 + min(64 * c + lane, uw - 1)];
+        XU[2] = xtab[A.xtab_l + ux0 + min(128 + (lane & 31), uw - 1)];
         if (tid < kPairUH) yu = ytab[A.ytab_l + uy0 + min(tid, uh - 1)];
 #pragma unroll
         for (int q = 0; q < kRowPass; ++q)
@@ -614,37 +615,47 @@ __global__ __launch_bounds__(256, 8) void k_pyramid_pair(const PairArgs A, const
     const int2 XN = xtab[A.xtab_n + vxn];
     if (tid < kTileH) yrowT[tid] = make_int4((yv.x - uy0) * kPairUP, (yv.y - uy0) * kPairUP, yv.z << 8, yv.w << 8);
     __syncthreads();
-    // 2. U from C (l > 0): lane per U column (three 64-column passes), wave per 8 rows; rows past uh
-    //    repeat the last one (never read), columns past uw are not stored
+    // 2. U from C (l > 0): lane per U column, wave per 8 rows -- columns 0-127 in two 64-lane passes,
+    //    columns 128.. (at most 28: U is at most kPairUP - 8 wide) as two rows per pass, half-waves on
+    //    alternate rows; rows past uh repeat the last one (never read), columns past uw are not stored
     if (!kFirst) {
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
+        for (int c = 0; c < 2; ++c) {
             if (64 * c >= uw) break;
             const int col = 64 * c + lane, vx = ux0 + min(col, uw - 1);
             const int sx = XU[c].x - cx0 + shift, sx1 = min(XU[c].x + 1, cx0 + cw - 1) - cx0 + shift;
             pyr_resize_col<8>(cbox, &yrowU[8 * wave], sx, sx1, (unsigned)XU[c].y & 0xffffu, (unsigned)XU[c].y >> 16,
                               vx < A.simd_l, col < uw, &ubuf[8 * wave * kPairUP + col], kPairUP);
         }
+        if (uw > 128) {
+            const int col = 128 + (lane & 31), half = lane >> 5, vx = ux0 + min(col, uw - 1);
+            const int sx = XU[2].x - cx0 + shift, sx1 = min(XU[2].x + 1, cx0 + cw - 1) - cx0 + shift;
+            pyr_resize_col<4, 2>(cbox, &yrowU[8 * wave + half], sx, sx1, (unsigned)XU[2].y & 0xffffu,
+                                 (unsigned)XU[2].y >> 16, vx < A.simd_l, col < uw,
+                                 &ubuf[(8 * wave + half) * kPairUP + col], 2 * kPairUP);
+        }
         __syncthreads();
     }
-    // 3a. the owned share of level l: [ox0, ox1) x [oy0, oy1) in view coordinates (border included), a
-    //     plane dword per lane (interior dwords as two aligned LDS reads + v_alignbyte), a row per wave
+    // 3a. the owned share of level l: [ox0, ox1) x [oy0, oy1) in view coordinates (border included), 8
+    //     plane bytes per lane (interior chunks by lds_bytes8), nch chunks per row, 64 / nch rows per
+    //     wave pass (nch <= 21: the share is at most ~157 bytes wide)
     {
-        const int pc0 = (ox0 + kEdge) & ~3;
-        const int ndw = ((ox1 + kEdge - 1) >> 2) - (pc0 >> 2) + 1;
-        for (int r = wave; r < oy1 - oy0; r += 4) {
-            const int y = oy0 + r;
-            const uint8_t* urow = ubuf + (reflect101(y, A.hl) - uy0) * kPairUP;
-            uint8_t* dst = plane_l + (size_t)(y + kEdge) * A.pitch_l;
-            if (lane < ndw) {
-                const int pc = pc0 + 4 * lane, x = pc - kEdge;
-                if (x >= ox0 && x + 4 <= ox1 && x >= 0 && x + 4 <= A.wl) {
-                    const int o = x - ux0;
-                    const uint32_t* w = reinterpret_cast<const uint32_t*>(urow) + (o >> 2);
-                    *reinterpret_cast<uint32_t*>(dst + pc) = __builtin_amdgcn_alignbyte(w[1], w[0], o & 3);
+        const int pc0 = (ox0 + kEdge) & ~7;
+        const int nch = ((ox1 + kEdge - 1) >> 3) - (pc0 >> 3) + 1;
+        const int rpp = 64 / nch, lr = lane / nch, ch = lane - lr * nch;
+        const int nrow = oy1 - oy0;
+        for (int r0o = rpp * wave; r0o < nrow; r0o += 4 * rpp) {
+            const int r = r0o + lr;
+            if (lr < rpp && r < nrow) {
+                const int y = oy0 + r;
+                const uint8_t* urow = ubuf + (reflect101(y, A.hl) - uy0) * kPairUP;
+                uint8_t* dst = plane_l + (size_t)(y + kEdge) * A.pitch_l;
+                const int pc = pc0 + 8 * ch, x = pc - kEdge;
+                if (x >= ox0 && x + 8 <= ox1 && x >= 0 && x + 8 <= A.wl) {
+                    *reinterpret_cast<unsigned long long*>(dst + pc) = lds_bytes8(urow, x - ux0);
                 } else {
 #pragma unroll
-                    for (int b = 0; b < 4; ++b)
+                    for (int b = 0; b < 8; ++b)
                         if (x + b >= ox0 && x + b < ox1) dst[pc + b] = urow[reflect101(x + b, A.wl) - ux0];
                 }
             }
@@ -2318,8 +2329,8 @@ bool pair_tables(const orbgpu::KernelGeom& k, const std::vector<int4>& tiles, co
                 for (int x = ox0; x < ox1; ++x) { const int v = refl(x, L.w); ux0 = std::min(ux0, v); ux1 = std::max(ux1, v + 1); }
                 for (int y = oy0; y < oy1; ++y) { const int v = refl(y, L.h); uy0 = std::min(uy0, v); uy1 = std::max(uy1, v + 1); }
                 const int uw = ux1 - ux0, uh = uy1 - uy0;
-                const int ndw = ((ox1 + kEdge - 1) >> 2) - ((ox0 + kEdge) >> 2) + 1;
-                if (uw + 8 > kPairUP || uh > kPairUH || ndw > 64 || ox0 < -32768 || ox1 > 32767) return false;
+                const int nch = ((ox1 + kEdge - 1) >> 3) - ((ox0 + kEdge) >> 3) + 1;  // 8-byte chunks of a row
+                if (uw + 8 > kPairUP || uw > 128 + 32 || uh > kPairUH || nch > 21 || ox0 < -32768 || ox1 > 32767) return false;
                 int cx0 = 0, cw = 0, cy0 = 0, chh = 0;
                 if (nl > 1) {
                     const orbgpu::LevelGeom& Pv = k.lv[nl - 2];
