@@ -2165,8 +2165,8 @@ struct Extractor {
     int4* d_tiletab = nullptr; size_t tiletab_cap = 0;  // pyramid tile records (tile_tables)
     int4* d_pairtab = nullptr; size_t pairtab_cap = 0;  // their two-level records (pair_tables)
     bool pair_ok = false;                               // the geometry fits k_pyramid_pair's boxes
-    int pyr_pair = 0;                                   // ORBGPU_PYR_PAIR=1: two levels per pyramid pass (measured
-                                                        // slower with batches in flight; off by default)
+    int pyr_pair = 0;                                   // ORBGPU_PYR_PAIR=1: two levels per pyramid pass, 2: only
+                                                        // levels 0 + 1 (level passes by default)
     int tile_off[orbgpu::kMaxLevels] = {};
     int4* d_ytab = nullptr; size_t ytab_cap = 0;
     uint8_t* d_pyr = nullptr; size_t pyr_cap = 0;
@@ -2592,7 +2592,7 @@ int launch_chunk(Extractor* e, int f0, const uint8_t* d_images, int n, int strid
     // mode (ORBGPU_PYR_STAMPS) times the level kernel
     const bool pairs = e->pyr_pair && e->pair_ok && !pyr_stamps;
     for (int l = 0; l < k.nlevels; ++l) {
-        if (pairs && (l & 1) == 0 && l + 1 < k.nlevels) {
+        if (pairs && (l & 1) == 0 && l + 1 < k.nlevels && (e->pyr_pair == 1 || l == 0)) {
             const orbgpu::LevelGeom &Ll = k.lv[l], &Ln = k.lv[l + 1];
             PairArgs A{};
             A.frame_bytes = k.pyr_frame_bytes;

@@ -356,7 +356,7 @@ def test_set_overlap_parity(pkg, oracle, synth):
     (104, 110, "noise", 200, 1.2, 2, 20, 7),     # one cell column per level: 72- and 55-px FAST windows
     (640, 480, "poly", 1000, 1.2, 7, 20, 7),     # odd level count (with ORBGPU_PYR_PAIR=1: three two-level passes, then one)
 ])
-@pytest.mark.parametrize("pair", ["0", "1"], ids=["level_passes", "two_level_passes"])
+@pytest.mark.parametrize("pair", ["0", "1", "2"], ids=["level_passes", "two_level_passes", "first_two_levels"])
 def test_extract_parity_other_parameters(pkg, oracle, synth, monkeypatch, w, h, kind, nf, scale, nlevels, ini, mn, pair):
     """ORBextractor parameters other than the 1.2 / 8 / 20 / 7 of the bench configs (the reference
     reads them from the settings file, src/Tracking.cc:1346-1362): pyramid levels, keypoints (bitwise)

@@ -43,7 +43,7 @@ def _run_in_flight(pkg, imgs, nf, w, h, lap, steps=8, handles=4, stamps=True):
         if stamps:
             ms, n = e.pyramid_launch_ms()
             # 8 levels: 8 level passes, or 4 two-level passes (k_pyramid_pair) with ORBGPU_PYR_PAIR=1
-            per_batch = 4 if os.environ.get("ORBGPU_PYR_PAIR", "0") == "1" else 8
+            per_batch = {"1": 4, "2": 7}.get(os.environ.get("ORBGPU_PYR_PAIR", "0"), 8)
             assert n == per_batch * (steps // handles) and ms > 0
             e.profile(False)
     return outs

@@ -3,7 +3,7 @@
 # step time (tools/c2_ablate.py, no stage skipped), alternated.
 set -u
 for r in 1 2; do
-  for v in 1 0; do
+  for v in ${MODES:-1 0}; do
     echo "PYR_PAIR=$v: $(ORBGPU_PYR_PAIR=$v timeout -k 10 200 python3 tools/c2_ablate.py 0 | tr '\n' ' ')" || exit 1
   done
 done
