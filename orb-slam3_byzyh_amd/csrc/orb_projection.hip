@@ -229,9 +229,8 @@ __global__ __launch_bounds__(64 * kCandWaves) void k_proj_candidates_b(const k_p
 // keypoints, so a wave per point spent most of its time on the 64-lane prefix and compaction machinery;
 // a thread walks its window's cells (ix outer, iy inner) and their keypoints in index order, which is
 // window_candidates' order, and writes the same list.
-template <class Test>
-__device__ __forceinline__ int window_candidates_serial(const int32_t* __restrict__ cell_off,
-                                                        const int32_t* __restrict__ cell_idx, int x0, int x1, int y0,
+template <class Test, class CO = const int32_t*, class CI = const int32_t*>
+__device__ __forceinline__ int window_candidates_serial(CO cell_off, CI cell_idx, int x0, int x1, int y0,
                                                         int y1, Cand* __restrict__ out, int cap, Test test) {
     int n = 0;
     for (int ix = x0; ix <= x1; ++ix)
@@ -260,17 +259,17 @@ __device__ __forceinline__ void record_listers_serial(int i, int n, int cap, con
 
 constexpr int kCandThreads = 256;
 
-__device__ __forceinline__ void k_proj_candidates_t_body(const ProjParams P, const int32_t* __restrict__ n_dev,
+// (KP / UR / DS / CO / CI: the current frame's records, global pointers or, in the LDS-staged form, LDS ones)
+template <class KP = const float4*, class UR = const float*, class DS = const uint4*, class CO = const int32_t*,
+          class CI = const int32_t*>
+__device__ __forceinline__ void k_proj_candidates_t_body(int i, const ProjParams P, const int32_t* __restrict__ n_dev,
                                                          const uint8_t* __restrict__ valid,
                                                          const float* __restrict__ xyz, const uint4* __restrict__ mp_desc,
                                                          const int32_t* __restrict__ last_octave,
-                                                         const float4* __restrict__ cur_kp,
-                                                         const float* __restrict__ cur_ur, const uint4* __restrict__ cur_desc,
-                                                         const int32_t* __restrict__ cell_off, const int32_t* __restrict__ cell_idx,
+                                                         KP cur_kp, UR cur_ur, DS cur_desc, CO cell_off, CI cell_idx,
                                                          Cand* __restrict__ cands, int32_t* __restrict__ ncand,
                                                          int32_t* __restrict__ overflow, const uint8_t* __restrict__ observed,
                                                          int32_t* __restrict__ lister) {
-    const int i = blockIdx.x * kCandThreads + threadIdx.x;
     if (i >= (n_dev ? *n_dev : P.n_last)) return;
     int n = 0;
     Cand* const out = cands + (size_t)i * P.cap;
@@ -321,12 +320,12 @@ __device__ __forceinline__ void k_proj_candidates_t_body(const ProjParams P, con
     if (observed[i]) record_listers_serial(i, n, P.cap, out, nullptr, lister);
 }
 __global__ __launch_bounds__(kCandThreads) void k_proj_candidates_t(const k_proj_candidates_args A) {
-    k_proj_candidates_t_body(A.P, A.n_dev, A.valid, A.xyz, A.mp_desc, A.last_octave, A.cur_kp, A.cur_ur, A.cur_desc,
+    k_proj_candidates_t_body(blockIdx.x * kCandThreads + threadIdx.x, A.P, A.n_dev, A.valid, A.xyz, A.mp_desc, A.last_octave, A.cur_kp, A.cur_ur, A.cur_desc,
                              A.cell_off, A.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.lister);
 }
 __global__ __launch_bounds__(kCandThreads) void k_proj_candidates_t_b(const k_proj_candidates_args* __restrict__ a) {
     const k_proj_candidates_args& A = a[blockIdx.y];
-    k_proj_candidates_t_body(A.P, A.n_dev, A.valid, A.xyz, A.mp_desc, A.last_octave, A.cur_kp, A.cur_ur, A.cur_desc,
+    k_proj_candidates_t_body(blockIdx.x * kCandThreads + threadIdx.x, A.P, A.n_dev, A.valid, A.xyz, A.mp_desc, A.last_octave, A.cur_kp, A.cur_ur, A.cur_desc,
                              A.cell_off, A.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.lister);
 }
 
@@ -443,17 +442,17 @@ __global__ __launch_bounds__(64 * kCandWaves) void k_lmp_candidates_b(const k_lm
                           A.lister);
 }
 
-__device__ __forceinline__ void k_lmp_candidates_t_body(const LocalParams P, const uint8_t* __restrict__ in_view,
+template <class KP = const float4*, class UR = const float*, class DS = const uint4*, class CO = const int32_t*,
+          class CI = const int32_t*>
+__device__ __forceinline__ void k_lmp_candidates_t_body(int i, const LocalParams P, const uint8_t* __restrict__ in_view,
                                                         const uint8_t* __restrict__ bad, const float* __restrict__ proj,
                                                         const float* __restrict__ view_cos, const float* __restrict__ depth,
                                                         const int32_t* __restrict__ level, const uint4* __restrict__ mp_desc,
-                                                        const float4* __restrict__ cur_kp, const float* __restrict__ cur_ur,
-                                                        const uint4* __restrict__ cur_desc, const int32_t* __restrict__ cell_off,
-                                                        const int32_t* __restrict__ cell_idx, Cand* __restrict__ cands,
+                                                        KP cur_kp, UR cur_ur, DS cur_desc, CO cell_off, CI cell_idx,
+                                                        Cand* __restrict__ cands,
                                                         int32_t* __restrict__ ncand, int32_t* __restrict__ overflow,
                                                         const uint8_t* __restrict__ observed, const uint8_t* __restrict__ taken0,
                                                         int32_t* __restrict__ lister) {
-    const int i = blockIdx.x * kCandThreads + threadIdx.x;
     if (i >= P.n_pts) return;
     int n = 0;
     Cand* const out = cands + (size_t)i * P.cap;
@@ -492,15 +491,91 @@ __device__ __forceinline__ void k_lmp_candidates_t_body(const LocalParams P, con
     if (observed[i]) record_listers_serial(i, n, P.cap, out, taken0, lister);
 }
 __global__ __launch_bounds__(kCandThreads) void k_lmp_candidates_t(const k_lmp_candidates_args A) {
-    k_lmp_candidates_t_body(A.P, A.in_view, A.bad, A.proj, A.view_cos, A.depth, A.level, A.mp_desc, A.cur_kp, A.cur_ur,
+    k_lmp_candidates_t_body(blockIdx.x * kCandThreads + threadIdx.x, A.P, A.in_view, A.bad, A.proj, A.view_cos, A.depth, A.level, A.mp_desc, A.cur_kp, A.cur_ur,
                             A.cur_desc, A.cell_off, A.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.taken0,
                             A.lister);
 }
 __global__ __launch_bounds__(kCandThreads) void k_lmp_candidates_t_b(const k_lmp_candidates_args* __restrict__ a) {
     const k_lmp_candidates_args& A = a[blockIdx.y];
-    k_lmp_candidates_t_body(A.P, A.in_view, A.bad, A.proj, A.view_cos, A.depth, A.level, A.mp_desc, A.cur_kp, A.cur_ur,
+    k_lmp_candidates_t_body(blockIdx.x * kCandThreads + threadIdx.x, A.P, A.in_view, A.bad, A.proj, A.view_cos, A.depth, A.level, A.mp_desc, A.cur_kp, A.cur_ur,
                             A.cur_desc, A.cell_off, A.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.taken0,
                             A.lister);
+}
+
+// LDS-staged batch forms (round 6).  The thread forms above walk a window as a chain of dependent
+// global loads per candidate (cell offsets -> keypoint index -> keypoint record -> descriptor); with a
+// batch those records are spread over hundreds of frames and miss the caches.  Here one 1024-thread
+// workgroup per frame first copies the frame's grid (cell offsets, cell index list) and its keypoint
+// records (x, y, angle, octave; u_R; descriptors: all `cap` rows, the frame's padding included) into
+// LDS, then every thread walks its points' windows with the same code -- the same lists in the same
+// order, the chain now on LDS.  LDS: 56 B per keypoint + the 3,073 cell offsets (cap <= kCandLdsCap).
+constexpr int kCandLdsThreads = 1024;
+constexpr int kCandLdsCap = (160 * 1024 - 4 * (kGridCols * kGridRows + 1)) / 56;
+__host__ __device__ constexpr size_t cand_lds_bytes(int cap) {
+    return (size_t)cap * (32 + 16 + 4 + 4) + 4 * (size_t)(kGridCols * kGridRows + 1);
+}
+// Readers of the staged records through address-space-3 pointers, so that the walk issues ds_read
+// (the compiler does not infer the address space through the generic pointers otherwise: flat loads)
+#define ORB_LDS __attribute__((address_space(3)))
+struct LdsF4 {
+    const ORB_LDS float* p;
+    __device__ float4 operator[](int j) const { const ORB_LDS float* q = p + 4 * j; return make_float4(q[0], q[1], q[2], q[3]); }
+};
+struct LdsU4 {
+    const ORB_LDS uint32_t* p;
+    __device__ uint4 operator[](size_t j) const { const ORB_LDS uint32_t* q = p + 4 * j; return make_uint4(q[0], q[1], q[2], q[3]); }
+};
+template <class T>
+struct LdsArr {
+    const ORB_LDS T* p;
+    __device__ T operator[](int k) const { return p[k]; }
+};
+struct CandLds {
+    LdsU4 desc;
+    LdsF4 kp;
+    LdsArr<float> ur;
+    LdsArr<int32_t> cell_idx;
+    LdsArr<int32_t> cell_off;
+};
+// descriptors | keypoint records | u_R | cell index list | cell offsets (16-B aligned sections)
+__device__ __forceinline__ CandLds stage_frame_lds(uint8_t* smem, int cap, const float4* __restrict__ kp,
+                                                   const float* __restrict__ ur, const uint4* __restrict__ desc,
+                                                   const int32_t* __restrict__ cell_off, const int32_t* __restrict__ cell_idx) {
+    uint4* s_desc = reinterpret_cast<uint4*>(smem);
+    float4* s_kp = reinterpret_cast<float4*>(smem + 32 * (size_t)cap);
+    float* s_ur = reinterpret_cast<float*>(smem + 48 * (size_t)cap);
+    int32_t* s_idx = reinterpret_cast<int32_t*>(smem + 52 * (size_t)cap);
+    int32_t* s_off = reinterpret_cast<int32_t*>(smem + 56 * (size_t)cap);
+    const int t = threadIdx.x;
+    for (int k = t; k < 2 * cap; k += kCandLdsThreads) s_desc[k] = desc[k];
+    for (int k = t; k < cap; k += kCandLdsThreads) {
+        s_kp[k] = kp[k];
+        s_idx[k] = cell_idx[k];
+        if (ur) s_ur[k] = ur[k];
+    }
+    for (int k = t; k <= kGridCols * kGridRows; k += kCandLdsThreads) s_off[k] = cell_off[k];
+    __syncthreads();
+    // (u_R is read only when the frame has it, ProjParams / LocalParams has_ur)
+    return CandLds{LdsU4{(const ORB_LDS uint32_t*)s_desc}, LdsF4{(const ORB_LDS float*)s_kp}, LdsArr<float>{(const ORB_LDS float*)s_ur},
+                   LdsArr<int32_t>{(const ORB_LDS int32_t*)s_idx}, LdsArr<int32_t>{(const ORB_LDS int32_t*)s_off}};
+}
+__global__ __launch_bounds__(kCandLdsThreads) void k_proj_candidates_l_b(const k_proj_candidates_args* __restrict__ a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t cand_smem[];
+    const k_proj_candidates_args& A = a[blockIdx.x];
+    const CandLds S = stage_frame_lds(cand_smem, A.P.cap, A.cur_kp, A.cur_ur, A.cur_desc, A.cell_off, A.cell_idx);
+    const int np = A.n_dev ? *A.n_dev : A.P.n_last;
+    for (int i = threadIdx.x; i < np; i += kCandLdsThreads)
+        k_proj_candidates_t_body(i, A.P, A.n_dev, A.valid, A.xyz, A.mp_desc, A.last_octave, S.kp, S.ur, S.desc, S.cell_off,
+                                 S.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.lister);
+}
+__global__ __launch_bounds__(kCandLdsThreads) void k_lmp_candidates_l_b(const k_lmp_candidates_args* __restrict__ a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t cand_smem[];
+    const k_lmp_candidates_args& A = a[blockIdx.x];
+    const CandLds S = stage_frame_lds(cand_smem, A.P.cap, A.cur_kp, A.cur_ur, A.cur_desc, A.cell_off, A.cell_idx);
+    for (int i = threadIdx.x; i < A.P.n_pts; i += kCandLdsThreads)
+        k_lmp_candidates_t_body(i, A.P, A.in_view, A.bad, A.proj, A.view_cos, A.depth, A.level, A.mp_desc, S.kp, S.ur,
+                                S.desc, S.cell_off, S.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.taken0,
+                                A.lister);
 }
 
 // ---- the in-order assignment, resolved by parallel fixed-point rounds ----------------------------
@@ -1099,12 +1174,29 @@ bool resolve_lds_ready() {
 // has the shorter latency (0.51 vs 0.65 ms per tracked frame); a batch fills the chip, and threads
 // carry far less per-point machinery (256 frames: 3.2 -> 1.5 ms per call).  ORBGPU_CAND_MODE=wave /
 // thread forces one form everywhere (A/B).
-bool cand_thread_mode(bool batch) {
+int cand_forced_mode() {
     static const int forced = [] {
         const char* c = getenv("ORBGPU_CAND_MODE");
-        return !c ? -1 : strcmp(c, "thread") == 0 ? 1 : strcmp(c, "wave") == 0 ? 0 : -1;
+        return !c ? -1 : strcmp(c, "lds") == 0 ? 2 : strcmp(c, "thread") == 0 ? 1 : strcmp(c, "wave") == 0 ? 0 : -1;
     }();
-    return forced >= 0 ? forced == 1 : batch;
+    return forced;
+}
+bool cand_thread_mode(bool batch) {
+    const int forced = cand_forced_mode();
+    return forced >= 0 ? forced >= 1 : batch;
+}
+// A batch's candidate pass in the LDS-staged form (k_*_candidates_l_b) unless a form is forced
+// (ORBGPU_CAND_MODE=thread / wave) or the frame's records do not fit one workgroup's LDS.
+bool cand_lds_mode(int cap) {
+    const int forced = cand_forced_mode();
+    if (!(forced == -1 || forced == 2) || cap > kCandLdsCap) return false;
+    static const bool ready = [] {
+        return hipFuncSetAttribute((const void*)k_proj_candidates_l_b, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)cand_lds_bytes(kCandLdsCap)) == hipSuccess &&
+               hipFuncSetAttribute((const void*)k_lmp_candidates_l_b, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)cand_lds_bytes(kCandLdsCap)) == hipSuccess;
+    }();
+    return ready;
 }
 
 }  // namespace
@@ -1610,7 +1702,10 @@ int orbgpu_sbp_frame_batch(orb_matcher_t m, int B, const orb_frame_device_t* con
     if (maxNL > 0) {  // grids sized for the largest frame; the kernels bound themselves by their own counts
         hipLaunchKernelGGL(k_last_prep_b, dim3((maxNL + 255) / 256, B), dim3(256), 0, s,
                            (const k_last_prep_args*)(d + o_lp));
-        if (cand_thread_mode(true))
+        if (cand_lds_mode(C))
+            hipLaunchKernelGGL(k_proj_candidates_l_b, dim3(B), dim3(kCandLdsThreads), cand_lds_bytes(C), s,
+                               (const k_proj_candidates_args*)(d + o_ca));
+        else if (cand_thread_mode(true))
             hipLaunchKernelGGL(k_proj_candidates_t_b, dim3((maxNL + kCandThreads - 1) / kCandThreads, B), dim3(kCandThreads), 0,
                                s, (const k_proj_candidates_args*)(d + o_ca));
         else
@@ -1784,7 +1879,10 @@ int orbgpu_sbp_local_batch(orb_matcher_t m, int B, const orb_frame_device_t* con
     if (maxNp > 0) {
         hipLaunchKernelGGL(k_local_prep_b, dim3((maxNp + 255) / 256, B), dim3(256), 0, s,
                            (const k_local_prep_args*)(d + o_lp));
-        if (cand_thread_mode(true))
+        if (cand_lds_mode(C))
+            hipLaunchKernelGGL(k_lmp_candidates_l_b, dim3(B), dim3(kCandLdsThreads), cand_lds_bytes(C), s,
+                               (const k_lmp_candidates_args*)(d + o_ca));
+        else if (cand_thread_mode(true))
             hipLaunchKernelGGL(k_lmp_candidates_t_b, dim3((maxNp + kCandThreads - 1) / kCandThreads, B), dim3(kCandThreads), 0,
                                s, (const k_lmp_candidates_args*)(d + o_ca));
         else
