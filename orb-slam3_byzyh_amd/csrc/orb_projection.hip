@@ -537,18 +537,20 @@ struct CandLds {
     LdsArr<int32_t> cell_idx;
     LdsArr<int32_t> cell_off;
 };
-// descriptors | keypoint records | u_R | cell index list | cell offsets (16-B aligned sections)
+// descriptors | keypoint records | u_R | cell index list | cell offsets (16-B aligned sections); the
+// first `rows` keypoint rows are staged (the cell offsets always)
 __device__ __forceinline__ CandLds stage_frame_lds(uint8_t* smem, int cap, const float4* __restrict__ kp,
                                                    const float* __restrict__ ur, const uint4* __restrict__ desc,
-                                                   const int32_t* __restrict__ cell_off, const int32_t* __restrict__ cell_idx) {
+                                                   const int32_t* __restrict__ cell_off, const int32_t* __restrict__ cell_idx,
+                                                   int rows) {
     uint4* s_desc = reinterpret_cast<uint4*>(smem);
     float4* s_kp = reinterpret_cast<float4*>(smem + 32 * (size_t)cap);
     float* s_ur = reinterpret_cast<float*>(smem + 48 * (size_t)cap);
     int32_t* s_idx = reinterpret_cast<int32_t*>(smem + 52 * (size_t)cap);
     int32_t* s_off = reinterpret_cast<int32_t*>(smem + 56 * (size_t)cap);
     const int t = threadIdx.x;
-    for (int k = t; k < 2 * cap; k += kCandLdsThreads) s_desc[k] = desc[k];
-    for (int k = t; k < cap; k += kCandLdsThreads) {
+    for (int k = t; k < 2 * rows; k += kCandLdsThreads) s_desc[k] = desc[k];
+    for (int k = t; k < rows; k += kCandLdsThreads) {
         s_kp[k] = kp[k];
         s_idx[k] = cell_idx[k];
         if (ur) s_ur[k] = ur[k];
@@ -559,25 +561,6 @@ __device__ __forceinline__ CandLds stage_frame_lds(uint8_t* smem, int cap, const
     return CandLds{LdsU4{(const ORB_LDS uint32_t*)s_desc}, LdsF4{(const ORB_LDS float*)s_kp}, LdsArr<float>{(const ORB_LDS float*)s_ur},
                    LdsArr<int32_t>{(const ORB_LDS int32_t*)s_idx}, LdsArr<int32_t>{(const ORB_LDS int32_t*)s_off}};
 }
-__global__ __launch_bounds__(kCandLdsThreads) void k_proj_candidates_l_b(const k_proj_candidates_args* __restrict__ a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t cand_smem[];
-    const k_proj_candidates_args& A = a[blockIdx.x];
-    const CandLds S = stage_frame_lds(cand_smem, A.P.cap, A.cur_kp, A.cur_ur, A.cur_desc, A.cell_off, A.cell_idx);
-    const int np = A.n_dev ? *A.n_dev : A.P.n_last;
-    for (int i = threadIdx.x; i < np; i += kCandLdsThreads)
-        k_proj_candidates_t_body(i, A.P, A.n_dev, A.valid, A.xyz, A.mp_desc, A.last_octave, S.kp, S.ur, S.desc, S.cell_off,
-                                 S.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.lister);
-}
-__global__ __launch_bounds__(kCandLdsThreads) void k_lmp_candidates_l_b(const k_lmp_candidates_args* __restrict__ a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t cand_smem[];
-    const k_lmp_candidates_args& A = a[blockIdx.x];
-    const CandLds S = stage_frame_lds(cand_smem, A.P.cap, A.cur_kp, A.cur_ur, A.cur_desc, A.cell_off, A.cell_idx);
-    for (int i = threadIdx.x; i < A.P.n_pts; i += kCandLdsThreads)
-        k_lmp_candidates_t_body(i, A.P, A.in_view, A.bad, A.proj, A.view_cos, A.depth, A.level, A.mp_desc, S.kp, S.ur,
-                                S.desc, S.cell_off, S.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.taken0,
-                                A.lister);
-}
-
 // ---- the in-order assignment, resolved by parallel fixed-point rounds ----------------------------
 // Both SearchByProjection loops visit the points in index order, and point i only sees the state the
 // earlier points left: a current keypoint that holds a map point with observations is skipped
@@ -700,13 +683,7 @@ __device__ __forceinline__ int decide(const ResolveArgs& a, int d1, int j1, int 
 // kTop best usable candidates in (distance, order), the classification, the work list and the fixed
 // claims.  k_resolve_rounds (one workgroup) then iterates only the work list, each point re-deciding
 // from its kTop best (a full scan only when too many of them are claimed).
-__device__ __forceinline__ void k_resolve_init_body(ResolveArgs a) {
-    if (a.dims) {
-        a.n_pts = a.dims[0];
-        a.n_cur = a.dims[1];
-    }
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= a.n_pts || *a.overflow > a.cap) return;
+__device__ __forceinline__ void resolve_init_point(const ResolveArgs& a, int i) {
     unsigned long long t[kTop];
     int ti[kTop];
 #pragma unroll
@@ -738,6 +715,15 @@ __device__ __forceinline__ void k_resolve_init_body(ResolveArgs a) {
     if (affected) a.work[atomicAdd(&a.out_n[2], 1)] = i;
     else if (st >= 0 && a.observed[i]) atomicMin(&a.fixed[st], i);
 }
+__device__ __forceinline__ void k_resolve_init_body(ResolveArgs a) {
+    if (a.dims) {
+        a.n_pts = a.dims[0];
+        a.n_cur = a.dims[1];
+    }
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n_pts || *a.overflow > a.cap) return;
+    resolve_init_point(a, i);
+}
 __global__ __launch_bounds__(256) void k_resolve_init(ResolveArgs a) {
     k_resolve_init_body(a);
 }
@@ -748,6 +734,34 @@ struct k_resolve_init_args {
 __global__ __launch_bounds__(256) void k_resolve_init_b(const k_resolve_init_args* __restrict__ a) {
     const k_resolve_init_args& A = a[blockIdx.y];
     k_resolve_init_body(A.a);
+}
+
+// The LDS-staged candidate passes of a batch (one workgroup per frame).  (Running k_resolve_init's
+// per-point pass in the same launch, after the frame's listers are final, was measured slower: 2.14 ->
+// 2.62 ms per 512-frame call -- one CU per frame instead of the whole chip.)
+__global__ __launch_bounds__(kCandLdsThreads) void k_proj_candidates_l_b(const k_proj_candidates_args* __restrict__ a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t cand_smem[];
+    const k_proj_candidates_args& A = a[blockIdx.x];
+    const int np = A.n_dev ? *A.n_dev : A.P.n_last;
+    if (np == 0) return;  // (a frame the motion gate turned off: nothing to stage)
+    const CandLds S = stage_frame_lds(cand_smem, A.P.cap, A.cur_kp, A.cur_ur, A.cur_desc, A.cell_off, A.cell_idx, A.P.cap);
+    for (int i = threadIdx.x; i < np; i += kCandLdsThreads)
+        k_proj_candidates_t_body(i, A.P, A.n_dev, A.valid, A.xyz, A.mp_desc, A.last_octave, S.kp, S.ur, S.desc, S.cell_off,
+                                 S.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.lister);
+}
+__global__ __launch_bounds__(kCandLdsThreads) void k_lmp_candidates_l_b(const k_lmp_candidates_args* __restrict__ a,
+                                                                        const k_resolve_init_args* __restrict__ ri) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t cand_smem[];
+    const k_lmp_candidates_args& A = a[blockIdx.x];
+    const ResolveArgs& R = ri[blockIdx.x].a;
+    if (A.P.n_pts == 0) return;
+    // a frame without keypoints (the motion gate's failed frames) stages only its (empty) grid
+    const CandLds S = stage_frame_lds(cand_smem, A.P.cap, A.cur_kp, A.cur_ur, A.cur_desc, A.cell_off, A.cell_idx,
+                                      R.dims && R.dims[1] == 0 ? 0 : A.P.cap);
+    for (int i = threadIdx.x; i < A.P.n_pts; i += kCandLdsThreads)
+        k_lmp_candidates_t_body(i, A.P, A.in_view, A.bad, A.proj, A.view_cos, A.depth, A.level, A.mp_desc, S.kp, S.ur,
+                                S.desc, S.cell_off, S.cell_idx, A.cands, A.ncand, A.overflow, A.observed, A.taken0,
+                                A.lister);
 }
 
 // point i's answer in a round, from its kTop best (claims by earlier points excluded)
@@ -1879,9 +1893,9 @@ int orbgpu_sbp_local_batch(orb_matcher_t m, int B, const orb_frame_device_t* con
     if (maxNp > 0) {
         hipLaunchKernelGGL(k_local_prep_b, dim3((maxNp + 255) / 256, B), dim3(256), 0, s,
                            (const k_local_prep_args*)(d + o_lp));
-        if (cand_lds_mode(C))
+        if (cand_lds_mode(C))  // (the frame's keypoint count, for the gated frames: the init block's dims)
             hipLaunchKernelGGL(k_lmp_candidates_l_b, dim3(B), dim3(kCandLdsThreads), cand_lds_bytes(C), s,
-                               (const k_lmp_candidates_args*)(d + o_ca));
+                               (const k_lmp_candidates_args*)(d + o_ca), (const k_resolve_init_args*)(d + o_ri));
         else if (cand_thread_mode(true))
             hipLaunchKernelGGL(k_lmp_candidates_t_b, dim3((maxNp + kCandThreads - 1) / kCandThreads, B), dim3(kCandThreads), 0,
                                s, (const k_lmp_candidates_args*)(d + o_ca));
