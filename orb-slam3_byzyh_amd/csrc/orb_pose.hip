@@ -22,6 +22,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -42,6 +43,7 @@ constexpr int kPT = ORB_POSE_THREADS;  // threads per frame
 constexpr int kPW = kPT / 64;          // waves
 constexpr int kCap = 2048;             // edges per frame held in LDS (beyond: read from memory every pass)
 constexpr int kPair = 2 * kPT;         // edge positions per pair step of the pass
+constexpr int kDualMinFrames = 512;    // batches from this size run two frames per CU (launch site)
 static_assert(kPT % 64 == 0 && kCap % kPair == 0 && kPW <= 32, "pose workgroup shape");
 
 static_assert(sizeof(orb_pose_edge_t) == 56, "pose edge layout");
@@ -577,20 +579,21 @@ struct LmState {
 // a rejected trial keeps the old linearisation, so the next iteration's build is this pass's sums.
 // Thread 0 holds the LM state; per trial it takes the totals, decides, and solves the next trial,
 // between two barriers.
-__global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __restrict__ frames,
+template <int kCapT, int kOcc>
+__global__ __launch_bounds__(kPT, kOcc) void k_pose_opt_t(const orb_pose_frame_t* __restrict__ frames,
                                                   const orb_pose_edge_t* __restrict__ edges,
                                                   double* __restrict__ pose_out, uint8_t* __restrict__ level,
                                                   int32_t* __restrict__ inliers, double* __restrict__ echi2, Huber2 hub) {
     __shared__ double part[kPW * 32];
     __shared__ double T[7];
     __shared__ int s_state;  // 1: evaluate the trial pose in T, 2: the round's optimize() is done
-    constexpr int kA = kCap / kPT;  // edges ranked per thread by the type sort
-    __shared__ int perm[kCap];      // position -> edge index
+    constexpr int kA = kCapT / kPT;  // edges ranked per thread by the type sort
+    __shared__ int perm[kCapT];      // position -> edge index
     __shared__ int scan[kPT];
-    __shared__ double lxw[3][kCap], lob[3][kCap];  // xw, obs by position
-    __shared__ float lis[kCap];                    // inv_sigma2
-    __shared__ double lch[kCap];                   // last chi2
-    __shared__ uint8_t llv[kCap];                  // level (1: outlier)
+    __shared__ double lxw[3][kCapT], lob[3][kCapT];  // xw, obs by position
+    __shared__ float lis[kCapT];                    // inv_sigma2
+    __shared__ double lch[kCapT];                   // last chi2
+    __shared__ uint8_t llv[kCapT];                  // level (1: outlier)
     const int tid = threadIdx.x, f = blockIdx.x;
     long long* const tr = f == 0 ? g_pose_trace : nullptr;
     const int tr_cap = g_pose_trace_cap;
@@ -612,7 +615,7 @@ __global__ __launch_bounds__(kPT) void k_pose_opt(const orb_pose_frame_t* __rest
     // ---- the LDS edges sorted by type: thread t ranks edges [kA t, kA t + kA).  The monocular edges
     // take positions [0, nmono), the stereo ones start at s0 (nmono rounded up to a wave's 128 positions
     // of a pair step, the gap filled with dummies), so every wave of a pair step runs one edge type.
-    const int nr = min(n, kCap - 128);
+    const int nr = min(n, kCapT - 128);
     int nmono, s0, npos;
     {
         int mono = 0;
@@ -970,8 +973,17 @@ int orbgpu_pose_optimization_device_scratch(int n_frames, const orb_pose_frame_t
     if (!chi && hipMallocAsync(reinterpret_cast<void**>(&chi), std::max<size_t>(1, (size_t)n_edges) * sizeof(double),
                                (hipStream_t)stream) != hipSuccess)
         return orbgpu_fail(ORB_ERR_DEVICE, "hipMallocAsync failed");
-    hipLaunchKernelGGL(k_pose_opt, dim3(n_frames), dim3(kPT), 0, (hipStream_t)stream, d_frames, d_edges,
-                       d_pose_out, d_outlier, d_inliers, chi, make_huber());
+    // Large batches (the batched tracking chain: 2 x 512 frames per call) run two frames per CU: the
+    // kernel with a 1024-edge LDS room (69 KB) at two waves per SIMD (its registers spill more); a frame
+    // beyond ~900 edges reads the rest from memory every pass.  ORBGPU_POSE_DUAL=0 / 1 forces one form.
+    const char* fc = getenv("ORBGPU_POSE_DUAL");
+    const int forced = fc ? atoi(fc) : -1;
+    if (forced == 1 || (forced < 0 && n_frames >= kDualMinFrames))
+        hipLaunchKernelGGL((k_pose_opt_t<1024, 2>), dim3(n_frames), dim3(kPT), 0, (hipStream_t)stream, d_frames, d_edges,
+                           d_pose_out, d_outlier, d_inliers, chi, make_huber());
+    else
+        hipLaunchKernelGGL((k_pose_opt_t<kCap, 1>), dim3(n_frames), dim3(kPT), 0, (hipStream_t)stream, d_frames, d_edges,
+                           d_pose_out, d_outlier, d_inliers, chi, make_huber());
     const bool launched = hipGetLastError() == hipSuccess;
     if ((!d_chi && hipFreeAsync(chi, (hipStream_t)stream) != hipSuccess) || !launched)
         return orbgpu_fail(ORB_ERR_DEVICE, "pose kernel launch failed");

@@ -38,3 +38,18 @@ def test_pose_optimization_ragged_and_edge_cases(pkg, oracle, synth):
     # empty batch
     P, O, I = pkg.pose_optimization(frames[:0], edges[:0])
     assert len(P) == 0 and len(I) == 0
+
+
+@pytest.mark.parametrize("stereo_frac,seed", [(0.0, 44), (0.5, 45)])
+def test_pose_optimization_two_frames_per_cu(pkg, oracle, synth, monkeypatch, stereo_frac, seed):
+    """The batch form (two frames per CU: a 1024-edge LDS room, frames beyond ~900 edges read the rest
+    from memory each pass), forced on small batches incl. the ragged frames, and taken by itself at 512
+    frames: the oracle's poses, outlier flags and inlier counts."""
+    monkeypatch.setenv("ORBGPU_POSE_DUAL", "1")
+    counts = [0, 2, 3, 9, 10, 64, 256, 895, 896, 897, 1023, 1024, 1025, 1500, 3000]
+    frames, edges, _ = synth.pose_opt_batch(len(counts), 0, seed=seed, points_per_frame=counts, outlier_frac=0.3,
+                                            rot_err=0.03, trans_err=0.1, stereo_frac=stereo_frac)
+    _check(pkg, oracle, frames, edges)
+    monkeypatch.delenv("ORBGPU_POSE_DUAL")
+    frames, edges, _ = synth.pose_opt_batch(512, 300, stereo_frac=stereo_frac, seed=seed + 10)
+    _check(pkg, oracle, frames, edges)
