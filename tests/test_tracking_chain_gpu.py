@@ -316,3 +316,33 @@ def test_tracking_chain_batch_rejects_shared_local_map(pkg, synth):
     cur, last, local = _device(pkg, sc, C, L)
     with pytest.raises(ValueError, match="two slots"):
         pkg.TrackingChainBatch(cur.cap, 2).track([(cur, last, local, sc["pose7_pred"])] * 2)
+
+
+def test_tracking_chain_batch_forms(pkg, synth, monkeypatch):
+    """The batch's alternative forms against the single chain: a cap above the LDS-staged candidate
+    passes' limit (the frame's records no longer fit one workgroup: the thread form runs) and the
+    two-frames-per-CU PoseOptimization (forced; batches of >= 512 frames take it by themselves)."""
+    scenes = [synth.tracking_chain_scene(seed=s) for s in (81, 83)]
+    fr = [_frames(pkg, sc) for sc in scenes]
+    for cap, dual in ((3000, None), (max(max(C.N, L.N) for C, L in fr) + 3, "1")):
+        devs = [_device(pkg, sc, C, L, cap=cap) for sc, (C, L) in zip(scenes, fr)]
+        single = [pkg.TrackingChain(cap).track(cur, last, local, sc["pose7_pred"]).sync()
+                  for sc, (cur, last, local) in zip(scenes, devs)]
+        if dual:
+            monkeypatch.setenv("ORBGPU_POSE_DUAL", dual)
+        res = pkg.TrackingChainBatch(cap, len(scenes)).track(
+            [(cur, last, local, sc["pose7_pred"]) for sc, (cur, last, local) in zip(scenes, devs)]).sync()
+        monkeypatch.delenv("ORBGPU_POSE_DUAL", raising=False)
+        for r, o in zip(res, single):
+            for k in ("n1", "n2", "n_kept", "n_map"):
+                assert r[k] == o[k], (cap, k)
+            for k in ("m1", "m2", "edge_kp1", "edge_kp2"):
+                assert np.array_equal(np.asarray(r[k]), np.asarray(o[k])), (cap, k)
+            if dual:  # another kernel build: the 1e-6 PoseOptimization bar, identical outlier flags
+                for k in ("outlier1", "outlier2", "inliers"):
+                    assert np.array_equal(np.asarray(r[k]), np.asarray(o[k])), (cap, k)
+                for k in ("pose1", "pose2"):
+                    assert np.sqrt(np.mean((np.asarray(r[k]) - np.asarray(o[k])) ** 2)) < 1e-6, (cap, k)
+            else:
+                for k in ("outlier1", "outlier2", "inliers", "pose1", "pose2"):
+                    assert np.array_equal(np.asarray(r[k]), np.asarray(o[k])), (cap, k)
