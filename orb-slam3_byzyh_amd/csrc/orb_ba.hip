@@ -102,7 +102,72 @@ __device__ __forceinline__ bool lm_skip(const LmState* st, int kind) {
     return false;
 }
 
+// The trial's pose update (push + VertexSE3Expmap::oplusImpl per free pose) for the landmark-major
+// trial kernel (k_u_land_trial), which does it in LDS for up to kT free poses, and for
+// k_u_pose_update, which moves more of them (tile-row Cholesky sizes) before it.  pose == nullptr: no
+// pose kernel (launch_chol).  pscale: k_u_pose_update's computeScale part of the poses,
+// sum_t x_t (lambda x_t + b_p) (rank 0 only when sharded: primary).
+struct PoseTail {
+    const int32_t* free_pose;
+    double* pose;
+    double* pose_bak;
+    const double* bp;
+    const double* lam;
+    double* pscale;
+    int nf, primary;
+};
+
+// pose t of the tail: from the backup when the previous trial was rejected (and not restored), the
+// backup refreshed, exp(x_t) applied.  Returns pose t's computeScale part.
+__device__ __forceinline__ double pose_tail_one(const PoseTail& pt, int t, int fp, const double* __restrict__ xt,
+                                                bool rej) {
+    double* T = pt.pose + 7 * (size_t)fp;
+    double* Tb = pt.pose_bak + 7 * (size_t)fp;
+    double v[7], u[6];
+    for (int i = 0; i < 7; ++i) {
+        v[i] = rej ? Tb[i] : T[i];
+        Tb[i] = v[i];
+    }
+    for (int i = 0; i < 6; ++i) u[i] = xt[i];
+    double c = 0.0;
+    if (pt.primary) {
+        const double lambda = *pt.lam;
+        for (int i = 0; i < 6; ++i) c += u[i] * (lambda * u[i] + pt.bp[6 * (size_t)t + i]);
+    }
+    se3_oplus(v, u);
+    for (int i = 0; i < 7; ++i) T[i] = v[i];
+    return c;
+}
+
 // ---- per-edge error / linearisation ------------------------------------------------------------
+
+// Error and robust chi2 of edge E at pose T and point X (computeError + the Huber kernel); Xc: the
+// point in the camera frame.  Returns rho0.
+__device__ __forceinline__ double ba_edge_err(const EdgeDev& E, const orb_ba_camera_t& cam, const double T[7],
+                                              const double X[3], Huber2 hub, double Xc[3], double er[3], double& rho1) {
+    const double q[4] = {T[3], T[4], T[5], T[6]};
+    qrotate(q, X, Xc);
+    Xc[0] += T[0]; Xc[1] += T[1]; Xc[2] += T[2];
+    if (!E.stereo) {  // obs - Pinhole::project (src/CameraModels/Pinhole.cpp:47-54)
+        er[0] = E.obs[0] - ((double)cam.fx * Xc[0] / Xc[2] + (double)cam.cx);
+        er[1] = E.obs[1] - ((double)cam.fy * Xc[1] / Xc[2] + (double)cam.cy);
+        er[2] = 0.0;
+    } else {  // EdgeStereoSE3ProjectXYZ::cam_project: float invz and bf (types_six_dof_expmap.cpp:190-197)
+        const float invz = (float)(1.0f / Xc[2]);
+        const double u = Xc[0] * invz * (double)cam.fx + (double)cam.cx;
+        const double v = Xc[1] * invz * (double)cam.fy + (double)cam.cy;
+        er[0] = E.obs[0] - u;
+        er[1] = E.obs[1] - v;
+        er[2] = E.obs[2] - (u - (double)(cam.bf * invz));
+    }
+    const double info = (double)E.inv_sigma2;
+    double chi2 = er[0] * info * er[0] + er[1] * info * er[1];
+    if (E.stereo) chi2 += er[2] * info * er[2];
+    double rho0;
+    if (E.stereo) huber(chi2, hub.delta_stereo, hub.dsqr_stereo, rho0, rho1);
+    else huber(chi2, hub.delta_mono, hub.dsqr_mono, rho0, rho1);
+    return rho0;
+}
 
 template <bool kBuild>
 __device__ __forceinline__ double ba_edge(int e, const EdgeDev* __restrict__ edges,
@@ -119,27 +184,9 @@ __device__ __forceinline__ double ba_edge(int e, const EdgeDev* __restrict__ edg
     for (int i = 0; i < 7; ++i) T[i] = pose[7 * (size_t)E.pose + i];
     for (int i = 0; i < 3; ++i) X[i] = point[3 * (size_t)E.point + i];
     const double q[4] = {T[3], T[4], T[5], T[6]};
-    qrotate(q, X, Xc);
-    Xc[0] += T[0]; Xc[1] += T[1]; Xc[2] += T[2];
-    double er[3];
-    if (!E.stereo) {  // obs - Pinhole::project (src/CameraModels/Pinhole.cpp:47-54)
-        er[0] = E.obs[0] - ((double)cam.fx * Xc[0] / Xc[2] + (double)cam.cx);
-        er[1] = E.obs[1] - ((double)cam.fy * Xc[1] / Xc[2] + (double)cam.cy);
-        er[2] = 0.0;
-    } else {  // EdgeStereoSE3ProjectXYZ::cam_project: float invz and bf (types_six_dof_expmap.cpp:190-197)
-        const float invz = (float)(1.0f / Xc[2]);
-        const double u = Xc[0] * invz * (double)cam.fx + (double)cam.cx;
-        const double v = Xc[1] * invz * (double)cam.fy + (double)cam.cy;
-        er[0] = E.obs[0] - u;
-        er[1] = E.obs[1] - v;
-        er[2] = E.obs[2] - (u - (double)(cam.bf * invz));
-    }
+    double er[3], rho1;
+    const double rho0 = ba_edge_err(E, cam, T, X, hub, Xc, er, rho1);
     const double info = (double)E.inv_sigma2;
-    double chi2 = er[0] * info * er[0] + er[1] * info * er[1];
-    if (E.stereo) chi2 += er[2] * info * er[2];
-    double rho0, rho1;
-    if (E.stereo) huber(chi2, hub.delta_stereo, hub.dsqr_stereo, rho0, rho1);
-    else huber(chi2, hub.delta_mono, hub.dsqr_mono, rho0, rho1);
     err[3 * (size_t)e] = er[0];
     err[3 * (size_t)e + 1] = er[1];
     err[3 * (size_t)e + 2] = er[2];
@@ -1186,6 +1233,23 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
     if (trace && threadIdx.x == 0) trace[kTrEnd] = clock64();
 }
 
+// The pose update after the tile-row Cholesky (PoseTail): one workgroup, poses in strides
+__global__ __launch_bounds__(256) void k_u_pose_update(PoseTail pt, const double* __restrict__ x,
+                                                       const LmState* __restrict__ st) {
+    if (lm_skip(st, kGateTrial)) return;
+    __shared__ double cs[256];
+    const bool rej = st && st->reject;
+    double c = 0.0;  // thread t: poses t, t + 256, ... in order
+    for (int t = threadIdx.x; t < pt.nf; t += 256) c += pose_tail_one(pt, t, pt.free_pose[t], x + 6 * (size_t)t, rej);
+    cs[threadIdx.x] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s = 0.0;
+        for (int i = 0; i < 256; ++i) s += cs[i];
+        *pt.pscale = s;
+    }
+}
+
 // ---- tile-row Cholesky + solve over many workgroups (any n up to 16 x 256) ----------------------
 // Workgroup i owns tile row i of S (tiles (i, j), j <= i, in the operand layout O of the kernels
 // above) and runs the whole row left to right, eagerly:
@@ -1901,6 +1965,157 @@ __global__ __launch_bounds__(kT) void k_u_edges_trial(int ne, const EdgeDev* __r
     }
 }
 
+// unit steps 6 + 7 in one launch, landmark-major: thread l computes x_l (back-substitution), pushes
+// and moves landmark l, and evaluates the errors of the landmark's edges (all of them, in edge order)
+// at the new estimate, with the new point from registers.  A block is two waves: wave 0 takes kT
+// landmarks; wave 1 the poses (pose_mode 1, nf <= kT): every block computes the whole pose update into
+// LDS (lane t: pose t from its base -- the backup when the previous trial was rejected -- and
+// exp(x_t)) while wave 0 runs the back-substitution, so that no block waits for another; only the last
+// block, once every other block has read the bases, writes the poses and their backups.  pose_mode 2:
+// k_u_pose_update moved them before this launch (and left their computeScale part in *pscale); 0: no
+// free pose.  Per block: the chi2 partial into part[block], the landmarks' computeScale partial into
+// part2[block]; the last block sums both in block order, adds the poses' part (in pose order) and runs
+// the trial controller, as k_u_edges_trial<false> does.  The sums are grouped by landmark instead of
+// by edge block: the same terms, another rounding order.
+constexpr int kLandEdgeBatch = 8;  // a landmark's edges evaluated 8 at a time (loads issued together; the
+                                   // first batch's before the back-substitution)
+constexpr int kLT = 2 * kT;        // k_u_land_trial's block: landmark wave + pose wave
+static_assert(kT == 64, "k_u_land_trial: one wave of landmarks, one of poses");
+__global__ __launch_bounds__(kLT) void k_u_land_trial(int nl, int n, const double* __restrict__ lam,
+                                                     const int32_t* __restrict__ landf_off, const int32_t* __restrict__ landf_edge,
+                                                     const int32_t* __restrict__ landf_row, const double* __restrict__ hpl,
+                                                     size_t hpl_alt, const double* __restrict__ bl,
+                                                     const double* __restrict__ hll, double* __restrict__ x,
+                                                     const int32_t* __restrict__ land_point, double* __restrict__ point,
+                                                     double* __restrict__ point_bak, const int32_t* __restrict__ land_off,
+                                                     const int32_t* __restrict__ land_edge, const EdgeDev* __restrict__ edges,
+                                                     const orb_ba_camera_t* __restrict__ cams, double* __restrict__ pose,
+                                                     const int32_t* __restrict__ pose_h, PoseTail pt, int pose_mode,
+                                                     Huber2 hub, double* __restrict__ err, double* __restrict__ rho0_out,
+                                                     double* __restrict__ part, double* __restrict__ part2,
+                                                     unsigned* counter, const int32_t* __restrict__ status,
+                                                     double* __restrict__ scal, LmState* st, LmProgress* prog, int dist,
+                                                     double* __restrict__ sc_part, const volatile int32_t* h_stop) {
+    if (lm_skip(st, kGateTrial)) return;
+    __shared__ double s_new[kT][7], s_base[kT][7], s_pc[kT];
+    hpl += hpl_cur(st, hpl_alt);
+    const bool rej = st->reject != 0;
+    const double lambda = *lam;
+    const int tid = threadIdx.x, pw = tid - kT;  // pw: the pose wave's lane (wave 1)
+    const int l = tid < kT ? blockIdx.x * kT + tid : nl;
+    if (pose_mode == 1 && pw >= 0 && pw < pt.nf) {  // pose pw's trial update, into LDS only
+        const int fp = pt.free_pose[pw];
+        const double* src = (rej ? pt.pose_bak : pose) + 7 * (size_t)fp;
+        double v[7], u[6];
+        for (int i = 0; i < 7; ++i) v[i] = src[i];
+        for (int i = 0; i < 6; ++i) u[i] = x[6 * (size_t)pw + i];
+        double c = 0.0;
+        if (pt.primary)
+            for (int i = 0; i < 6; ++i) c += u[i] * (lambda * u[i] + pt.bp[6 * (size_t)pw + i]);
+        for (int i = 0; i < 7; ++i) s_base[pw][i] = v[i];
+        se3_oplus(v, u);
+        for (int i = 0; i < 7; ++i) s_new[pw][i] = v[i];
+        s_pc[pw] = c;
+    }
+    // the first edge batch's records (independent of the solve) are requested before the back-substitution
+    int k0 = 0, k1 = 0;
+    int e[kLandEdgeBatch], pr[kLandEdgeBatch];
+    EdgeDev E[kLandEdgeBatch];
+    orb_ba_camera_t cam[kLandEdgeBatch];
+    auto load_batch = [&](int kb) {
+#pragma unroll
+        for (int u = 0; u < kLandEdgeBatch; ++u) {
+            e[u] = land_edge[min(kb + u, k1 - 1)];
+            E[u] = edges[e[u]];
+            cam[u] = cams[E[u].pose];
+            pr[u] = pose_mode == 1 ? pose_h[E[u].pose] : -1;
+        }
+    };
+    if (l < nl) {
+        k0 = land_off[l];
+        k1 = land_off[l + 1];
+        load_batch(k0);
+    }
+    double c = 0.0, r = 0.0;
+    double Xn[3] = {0.0, 0.0, 0.0};
+    if (l < nl) {
+        double xl[3];
+        ba_backsub(l, n, lambda, landf_off, landf_edge, landf_row, hpl, bl, hll, x, xl);
+        for (int i = 0; i < 3; ++i) c += xl[i] * (lambda * xl[i] + bl[3 * (size_t)l + i]);
+        double* X = point + 3 * (size_t)land_point[l];
+        double* Xb = point_bak + 3 * (size_t)land_point[l];
+        for (int i = 0; i < 3; ++i) {
+            const double v = rej ? Xb[i] : X[i];
+            Xb[i] = v;
+            Xn[i] = v + xl[i];
+            X[i] = Xn[i];
+        }
+    }
+    if (pose_mode == 1) __syncthreads();  // s_new complete
+    if (l < nl) {
+        for (int kb = k0; kb < k1; kb += kLandEdgeBatch) {
+            if (kb != k0) load_batch(kb);
+            double T[kLandEdgeBatch][7];
+#pragma unroll
+            for (int u = 0; u < kLandEdgeBatch; ++u) {
+                const double* ts = pr[u] >= 0 ? &s_new[pr[u]][0] : pose + 7 * (size_t)E[u].pose;
+#pragma unroll
+                for (int i = 0; i < 7; ++i) T[u][i] = ts[i];
+            }
+#pragma unroll
+            for (int u = 0; u < kLandEdgeBatch; ++u) {
+                if (kb + u >= k1) break;
+                double Xc[3], er[3], rho1;
+                const double rho0 = ba_edge_err(E[u], cam[u], T[u], Xn, hub, Xc, er, rho1);
+                err[3 * (size_t)e[u]] = er[0];
+                err[3 * (size_t)e[u] + 1] = er[1];
+                err[3 * (size_t)e[u] + 2] = er[2];
+                rho0_out[e[u]] = rho0;
+                r += rho0;
+            }
+        }
+    }
+    const double rsum = block_sum<kLT>(r);
+    const double csum = block_sum<kLT>(c);
+    if (tid == 0) {
+        part[blockIdx.x] = rsum;
+        part2[blockIdx.x] = csum;
+    }
+    if (!last_block(counter)) return;
+    if (pose_mode == 1 && pw >= 0 && pw < pt.nf) {  // every other block has read the bases: commit the poses
+        const int fp = pt.free_pose[pw];
+        for (int i = 0; i < 7; ++i) {
+            pt.pose_bak[7 * (size_t)fp + i] = s_base[pw][i];
+            pose[7 * (size_t)fp + i] = s_new[pw][i];
+        }
+    }
+    double a = 0.0, d = 0.0;
+    for (int i = tid; i < (int)gridDim.x; i += kLT) {
+        a += part[i];
+        d += part2[i];
+    }
+    const double chi = block_sum<kLT>(a);
+    double scale = block_sum<kLT>(d);
+    if (tid == 0) {
+        if (pose_mode == 1)
+            for (int p = 0; p < pt.nf; ++p) scale += s_pc[p];
+        else if (pose_mode == 2)
+            scale += *pt.pscale;
+        if (dist) {  // this rank's parts and its stop flag, for k_lm_trial_ctl after the all-reduce
+            sc_part[0] = chi;
+            sc_part[1] = scale;
+            sc_part[2] = (h_stop && *h_stop) ? 1.0 : 0.0;
+        } else {
+            const bool failed = *status != 0;
+            scal[0] = chi;
+            scal[1] = scale;
+            scal[2] = failed ? 1.0 : 0.0;
+            lm_trial_done(st, chi, scale, failed, prog, false);
+        }
+        *counter = 0;
+    }
+}
+
 // sharded trial controller, after the all-reduce of the trial partials (sc_red: chi2, computeScale,
 // the number of ranks whose stop flag is raised): every rank takes the same decision; a raised flag
 // on any rank ends the solve after this trial (g2o's force-stop flag, tested between iterations)
@@ -2346,7 +2561,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     const bool dist = h->world > 1 || h->force_dist;
     const bool primary = h->rank == 0;
     hipStream_t s = h->stream;
-    if (!h->scal.grow(8)) return orbgpu_fail(ORB_ERR_DEVICE, "BA scalar buffer");
+    if (!h->scal.grow(16)) return orbgpu_fail(ORB_ERR_DEVICE, "BA scalar buffer");
     // the stop flag, agreed across the ranks (MAX) so that every rank takes the same path
     auto stop = [&]() -> bool {
         double f = stop_requested(opt) ? 1.0 : 0.0;
@@ -2529,7 +2744,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     }
     // ORBGPU_BA_TRACE: the first Cholesky of the process records its phase stamps (dump_chol_trace)
     static int trace_left = getenv("ORBGPU_BA_TRACE") ? 1 : 0;
-    auto launch_chol = [&](const LmState* g) {
+    auto launch_chol = [&](const LmState* g, const PoseTail& pt) {
         if (use_rows) {
             if (rows_lds)
                 hipLaunchKernelGGL(k_ba_chol_rows<true>, dim3(NT), dim3(kRowThreads), rows_lds_bytes, s, n, SS,
@@ -2539,6 +2754,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                 hipLaunchKernelGGL(k_ba_chol_rows<false>, dim3(NT), dim3(kRowThreads), rows_lds_bytes, s, n, SS,
                                    BSV, h->x.p, h->status.p, h->lpub.p, h->ypub.p, h->cflag.p, h->racc.p, g,
                                    (int)kGateTrial);
+            if (pt.pose) hipLaunchKernelGGL(k_u_pose_update, dim3(1), dim3(256), 0, s, pt, (const double*)h->x.p, g);
             return;
         }
         int64_t* tr = nullptr;
@@ -2598,7 +2814,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                                primary ? 1 : 0, BSV, G, (int)kGateTrial);
             if (!dev_reduce(h, SS, (size_t)n * n, ORB_BA_SUM) || !dev_reduce(h, BSV, n, ORB_BA_SUM))
                 return false;
-            launch_chol(G);
+            launch_chol(G, PoseTail{});
         } else if (!dev_lm) {
             hipMemsetAsync(h->status.p, 0, sizeof(int32_t), s);
         }
@@ -2654,6 +2870,16 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         // the build launch saves, C5 1.590 vs 1.582 ms per solve)
         static const char* tl_env = getenv("ORBGPU_BA_TRIAL_LIN");
         const bool trial_lin = tl_env && !strcmp(tl_env, "1");
+        // The trial's back-substitution, update and error pass in one launch instead of two (round 6):
+        // k_u_land_trial moves the poses (each block in LDS, the last one in memory) and the landmarks,
+        // then evaluates the landmarks' edges.  Beyond kT free poses (tile-row Cholesky sizes)
+        // k_u_pose_update moves the poses first.  ORBGPU_BA_FUSED_TRIAL=0: k_u_backsub_update +
+        // k_u_edges_trial.
+        static const char* ft_env = getenv("ORBGPU_BA_FUSED_TRIAL");
+        const bool fused = !trial_lin && !(ft_env && !strcmp(ft_env, "0"));
+        const int pose_mode = nf == 0 ? 0 : nf <= kT ? 1 : 2;
+        const PoseTail pt_unit = PoseTail{h->free_pose.p, h->pose.p, h->pose_bak.p, BV, lam, h->scal.p + 8, nf,
+                                          primary ? 1 : 0};
         auto launch_edges_build = [&]() {
             hipLaunchKernelGGL(k_u_edges_build, dim3(nparts), dim3(kT), 0, s, ne, h->edges.p, h->cams.p, h->pose.p,
                                h->point.p, h->pose_h.p, hub, h->err.p, h->rho0.p, h->ecl.p, h->hpl.p, h->ecp.p,
@@ -2695,8 +2921,17 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                                    dist ? p_sb : SS, h->cb.p, BV, dist ? p_sb + (size_t)n * n : BSV, (const LmState*)L,
                                    primary ? 1 : 0);
                 if (dist) coll_ok = coll_ok && dev_reduce2(h, p_sb, SS, (size_t)n * n + n, ORB_BA_SUM);
-                launch_chol((const LmState*)L);
+                launch_chol((const LmState*)L, fused && pose_mode == 2 ? pt_unit : PoseTail{});
             }
+            if (fused) {
+                hipLaunchKernelGGL(k_u_land_trial, dim3(grid(nl)), dim3(kLT), 0, s, nl, n, lam, h->landf_off.p,
+                                   h->landf_edge.p, h->landf_row.p, h->hpl.p, hpl_alt, bl, h->hll.p, h->x.p,
+                                   h->land_point.p, h->point.p, h->point_bak.p, h->land_off.p, h->land_edge.p,
+                                   h->edges.p, h->cams.p, h->pose.p, h->pose_h.p, pt_unit, pose_mode, hub, h->err.p,
+                                   h->rho0.p, h->part.p, h->part.p + nparts, h->counters.p + 1, h->status.p, h->scal.p,
+                                   L, h->h_prog, dist ? 1 : 0, p_sct,
+                                   (const volatile int32_t*)h->h_stop);
+            } else {
             hipLaunchKernelGGL(k_u_backsub_update, dim3(nparts2), dim3(kT), 0, s, nl, nf, n, lam, h->landf_off.p,
                                h->landf_edge.p, h->landf_row.p, h->hpl.p, hpl_alt, bl, h->hll.p, h->x.p, BV,
                                h->free_pose.p, h->land_point.p, h->pose.p, h->pose_bak.p, h->point.p, h->point_bak.p,
@@ -2706,6 +2941,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                                h->ecl.p, h->hpl.p, hpl_alt, h->ecp.p, h->part.p, h->counters.p + 1, h->part.p + nparts,
                                nparts2, h->status.p, h->scal.p, L, h->h_prog, dist ? 1 : 0, p_sct,
                                (const volatile int32_t*)h->h_stop);
+            }
             if (dist) {
                 coll_ok = coll_ok && dev_reduce2(h, p_sct, r_sct, 4, ORB_BA_SUM);
                 hipLaunchKernelGGL(trial_lin ? k_lm_trial_ctl<true> : k_lm_trial_ctl<false>, dim3(1), dim3(64), 0, s,
@@ -2737,7 +2973,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                 (uintptr_t)h->blk_cnt.p, (uintptr_t)BSV,
                 (uintptr_t)h->x.p, (uintptr_t)h->status.p, (uintptr_t)h->landf_off.p, (uintptr_t)h->landf_row.p, (uintptr_t)h->free_pose.p,
                 (uintptr_t)h->land_point.p, (uintptr_t)h->pose_bak.p, (uintptr_t)h->point_bak.p, (uintptr_t)h->h_prog,
-                (uintptr_t)use_rows, (uintptr_t)trial_lin, (uintptr_t)h->lpub.p, (uintptr_t)h->ypub.p, (uintptr_t)h->cflag.p,
+                (uintptr_t)use_rows, (uintptr_t)trial_lin, (uintptr_t)fused, (uintptr_t)h->lpub.p, (uintptr_t)h->ypub.p, (uintptr_t)h->cflag.p,
                 (uintptr_t)h->racc.p};
             if (!h->unit_exec || key != h->unit_key) {
                 if (h->unit_exec) { hipGraphExecDestroy(h->unit_exec); h->unit_exec = nullptr; }
