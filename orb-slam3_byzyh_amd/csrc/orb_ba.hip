@@ -169,7 +169,13 @@ __device__ __forceinline__ double ba_edge_err(const EdgeDev& E, const orb_ba_cam
     return rho0;
 }
 
-template <bool kBuild>
+// kReg (k_u_land_build): the landmark part (Hll, b_l) and the edge's Hpl kept in registers (lo) instead
+// of the ecl record; Hpl and the pose part still go to memory
+struct LinOut {
+    double pl[12], hx[18];
+    bool free;
+};
+template <bool kBuild, bool kReg = false>
 __device__ __forceinline__ double ba_edge(int e, const EdgeDev* __restrict__ edges,
                                                  const orb_ba_camera_t* __restrict__ cams,
                                                  const double* __restrict__ pose, const double* __restrict__ point,
@@ -177,7 +183,7 @@ __device__ __forceinline__ double ba_edge(int e, const EdgeDev* __restrict__ edg
                                                  double* __restrict__ err, double* __restrict__ rho0_out,
                                                  double* __restrict__ ecl, double* __restrict__ hpl,
                                                  double* __restrict__ ecp,
-        int) {
+        int, LinOut* lo = nullptr) {
     const EdgeDev E = edges[e];
     const orb_ba_camera_t cam = cams[E.pose];
     double T[7], X[3], Xc[3];
@@ -229,7 +235,7 @@ __device__ __forceinline__ double ba_edge(int e, const EdgeDev* __restrict__ edg
     const double w = rho1 * info;
     double omr[3];
     for (int r = 0; r < 3; ++r) omr[r] = -info * er[r] * rho1;
-    double* pl = ecl + 12 * (size_t)e;  // Hll part (3x3) + b_l part (3)
+    double* pl = kReg ? lo->pl : ecl + 12 * (size_t)e;  // Hll part (3x3) + b_l part (3)
     for (int i = 0; i < 3; ++i) {
         for (int j = 0; j < 3; ++j) {
             double s = 0;
@@ -240,6 +246,7 @@ __device__ __forceinline__ double ba_edge(int e, const EdgeDev* __restrict__ edg
         for (int r = 0; r < D; ++r) bs += A[3 * r + i] * omr[r];
         pl[9 + i] = bs;
     }
+    if (kReg) lo->free = pose_h[E.pose] >= 0;
     if (pose_h[E.pose] < 0) return rho0;
     double* hx = hpl + 18 * (size_t)e;  // B^T W A (6 x 3)
     for (int i = 0; i < 6; ++i)
@@ -247,6 +254,7 @@ __device__ __forceinline__ double ba_edge(int e, const EdgeDev* __restrict__ edg
             double s = 0;
             for (int r = 0; r < D; ++r) s += B[6 * r + i] * w * A[3 * r + j];
             hx[3 * i + j] = s;
+            if (kReg) lo->hx[3 * i + j] = s;
         }
     double* pp = ecp + 42 * (size_t)e;  // Hpp part (6x6) + b_p part (6)
     for (int i = 0; i < 6; ++i) {
@@ -316,8 +324,7 @@ __global__ __launch_bounds__(kT) void k_ba_reduce_land(int nl, const int32_t* __
 // Sum of 64 lanes' partials of NC values, lane c < NC adding value c's partials in lane order
 // (LDS transpose; one pass, no barrier-separated tree).  Returns value `lane`'s sum in lanes < NC.
 template <int NC>
-__device__ __forceinline__ double wave_sum_cols(const double (&v)[NC], int lane) {
-    __shared__ double red[NC][65];
+__device__ __forceinline__ double wave_sum_cols_in(const double (&v)[NC], int lane, double (*red)[65]) {
 #pragma unroll
     for (int i = 0; i < NC; ++i) red[i][lane] = v[i];
     __syncthreads();
@@ -326,13 +333,25 @@ __device__ __forceinline__ double wave_sum_cols(const double (&v)[NC], int lane)
         for (int q = 0; q < 64; ++q) t += red[lane][q];
     return t;
 }
+template <int NC>
+__device__ __forceinline__ double wave_sum_cols(const double (&v)[NC], int lane) {
+    __shared__ double red[NC][65];
+    return wave_sum_cols_in<NC>(v, lane, red);
+}
+// the caller's LDS buffer (kernels whose branches would otherwise each hold their own)
+template <int NC, bool kExt>
+__device__ __forceinline__ double wave_sum_cols_x(const double (&v)[NC], int lane, double (*red)[65]) {
+    if constexpr (kExt) return wave_sum_cols_in<NC>(v, lane, red);
+    else return wave_sum_cols<NC>(v, lane);
+}
 
 // Hpp and b_p per free pose: one wave; lane l sums the pose's edges l, l + 64, ... in order.  The
 // indices of up to 8 edges per lane are loaded first, then two edges' 42 values at a time, so the
 // usual pose (a few hundred edges) takes three rounds of loads instead of two per edge.
+template <bool kExt = false>
 __device__ __forceinline__ void ba_reduce_pose(int p, int lane, const int32_t* __restrict__ off,
                                                const LandEdge* __restrict__ eidx, const double* __restrict__ ecp,
-                                               double* __restrict__ hpp, double* __restrict__ bp) {
+                                               double* __restrict__ hpp, double* __restrict__ bp, double (*red)[65] = nullptr) {
     double s[42];
 #pragma unroll
     for (int i = 0; i < 42; ++i) s[i] = 0;
@@ -361,7 +380,7 @@ __device__ __forceinline__ void ba_reduce_pose(int p, int lane, const int32_t* _
 #pragma unroll
         for (int i = 0; i < 42; ++i) s[i] += q[i];
     }
-    const double t = wave_sum_cols<42>(s, lane);
+    const double t = wave_sum_cols_x<42, kExt>(s, lane, red);
     if (lane < 36) hpp[36 * (size_t)p + lane] = t;
     else if (lane < 42) bp[6 * (size_t)p + lane - 36] = t;
 }
@@ -515,11 +534,12 @@ __device__ __forceinline__ void schur_acc(double (&acc)[36], const double* __res
             acc[6 * r + c] += Z[3 * r] * H[3 * c] + Z[3 * r + 1] * H[3 * c + 1] + Z[3 * r + 2] * H[3 * c + 2];
 }
 
+template <bool kExt = false>
 __device__ __forceinline__ void ba_schur_block(int blk, int lane, int n, int nf, double lambda, int add_diag,
                                                const int32_t* __restrict__ blk_off, const EdgePair* __restrict__ pairs,
                                                const int32_t* __restrict__ cnt, const double* __restrict__ z,
                                                const double* __restrict__ hpl, const double* __restrict__ hpp,
-                                               double* __restrict__ S) {
+                                               double* __restrict__ S, double (*red)[65] = nullptr) {
     int i, j;
     schur_block_ij(blk, nf, i, j);
     double acc[36];
@@ -551,7 +571,7 @@ __device__ __forceinline__ void ba_schur_block(int blk, int lane, int n, int nf,
         for (int q = 0; q < 18; ++q) { zr[q] = z[18 * (size_t)p2.a + q]; hr[q] = hpl[18 * (size_t)p2.b + q]; }
         schur_acc(acc, zr, hr);
     }
-    const double sum = wave_sum_cols<36>(acc, lane);
+    const double sum = wave_sum_cols_x<36, kExt>(acc, lane, red);
     if (lane >= 36) return;
     const int r = lane / 6, c = lane % 6;
     double v = 0.0 - sum;
@@ -942,9 +962,20 @@ template <int W>
 __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const double* __restrict__ S,
                                                               const double* __restrict__ b, double* __restrict__ x,
                                                               int32_t* __restrict__ status, int64_t* __restrict__ trace,
-                                                              const LmState* __restrict__ lm_st, int lm_gk) {
+                                                              const LmState* __restrict__ lm_st, int lm_gk,
+                                                              const double* __restrict__ hpp_add, const double* __restrict__ lam_add) {
     if (lm_skip(lm_st, lm_gk)) return;
     constexpr int SL = (kMfMaxNT * (kMfMaxNT + 1) / 2 + W - 1) / W;
+    // hpp_add (the fast unit, k_u_schur2): S holds -sum Z Hpl^T only; element (row, col) of a diagonal 6x6
+    // block gains Hpp + lambda I here, in the value k_ba_schur_block would have stored there (its mirror
+    // store, lane (col % 6, row % 6), is the one that lands): (0 - sum) + (Hpp + lambda) = (Hpp + lambda) - sum
+    const double lam_d = hpp_add ? *lam_add : 0.0;
+    auto s_at = [&](int row, int col) {
+        double v = S[(size_t)row * n + col];
+        if (hpp_add && row / 6 == col / 6)
+            v += hpp_add[36 * (size_t)(row / 6) + 6 * (col % 6) + row % 6] + (row == col ? lam_d : 0.0);
+        return v;
+    };
     static_assert(SL <= 32, "slot dispatch covers 32 slots");
     extern __shared__ double lds[];
     double* pan = lds;                        // [2][NT][256] panel tiles O(L_ik), by step parity
@@ -981,7 +1012,7 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
         __builtin_amdgcn_s_setprio(3);
         for (int t = lane; t < 256; t += 64) {
             const int r = t >> 4, c = t & 15;
-            dk[r * 17 + c] = (r < n && c < n) ? S[(size_t)r * n + c] : (r == c ? 1.0 : 0.0);
+            dk[r * 17 + c] = (r < n && c < n) ? s_at(r, c) : (r == c ? 1.0 : 0.0);
         }
         mf_wave_sync();
         mf_diag<true>(dk, linv, yv, lane, &fail);
@@ -1071,7 +1102,7 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {  // S symmetric: read as S[col block][row block], coalesced
                     const int row = 16 * j + g4 + 4 * q, col = 16 * i + r16;
-                    const double v = S[(size_t)min(row, n - 1) * n + min(col, n - 1)];
+                    const double v = s_at(min(row, n - 1), min(col, n - 1));
                     e[q] = (row < n && col < n) ? v : (row == col ? 1.0 : 0.0);
                 }
                 T[s] = f64x4{e[0], e[1], e[2], e[3]};
@@ -1653,8 +1684,11 @@ __device__ void lm_build_done(LmState* st, double chi, double maxdiag) {
 // after a trial: accept (lambda shrinks) or reject (lambda grows; the next update starts from the
 // backup, and a final restore launch undoes a rejected last trial); at the end of the trial loop
 // the termination tests
+// fast (the fast unit, no build controller): the trial loop's next unit skips the build (phase 1); at
+// an iteration's end the next iteration's start is recorded here (ini_chi = the accepted chi2, qmax 0)
+// and its unit builds (phase 0)
 __device__ void lm_trial_done(LmState* st, double chi, double scale_part, bool failed, LmProgress* prog,
-                              bool flip_lin = false) {
+                              bool flip_lin = false, bool fast = false) {
     double tempChi = chi;
     if (failed) tempChi = DBL_MAX;
     double rho = st->current_chi - tempChi;
@@ -1675,6 +1709,7 @@ __device__ void lm_trial_done(LmState* st, double chi, double scale_part, bool f
     }
     st->qmax++;
     st->trials++;
+    if (fast) st->phase = 1;
     if (!(rho < 0 && st->qmax < 10)) {  // the trial loop is over
         st->final_chi = st->current_chi;
         if (st->qmax == 10 || rho == 0) {
@@ -1690,6 +1725,10 @@ __device__ void lm_trial_done(LmState* st, double chi, double scale_part, bool f
                 st->done = 1;
             } else {
                 st->phase = 0;
+                if (fast) {
+                    st->ini_chi = st->current_chi;
+                    st->qmax = 0;
+                }
                 if (st->it >= st->iterations) st->done = 1;
             }
         }
@@ -1965,6 +2004,137 @@ __global__ __launch_bounds__(kT) void k_u_edges_trial(int ne, const EdgeDev* __r
     }
 }
 
+// Fast unit (round 6; one process, the single-workgroup Cholesky): steps 1-3 in one landmark-major
+// launch.  kLB lanes per landmark: at the start of an iteration (phase 0) lane j linearises the
+// landmark's edges j, j + kLB, ... (ba_edge: error, Jacobians, Hpl and the pose part to memory) and
+// keeps their landmark parts; the lanes' sums (a fixed xor tree) are the landmark's Hll and b_l.  A
+// re-trial after a rejection (phase 1) reads Hll and b_l back.  Then every lane forms
+// Dinv = (Hll + lambda I)^-1 and, for its free edges, Z_e = Hpl_e Dinv and cb_e = Hpl_e (Dinv b_l),
+// as k_ba_schur_edges does.  The pose sums (Hpp, b_p) follow in k_u_schur2, lambda I and Hpp join S in
+// the Cholesky's tile loads, and the iteration's current chi2 is the accepted trial's (the same
+// estimate; g2o's build recomputes the same value).
+constexpr int kLB = 8;
+__global__ __launch_bounds__(kT) void k_u_land_build(int nl, const double* __restrict__ lam,
+                                                     const int32_t* __restrict__ land_off,
+                                                     const int32_t* __restrict__ land_edge, const EdgeDev* __restrict__ edges,
+                                                     const orb_ba_camera_t* __restrict__ cams,
+                                                     const double* __restrict__ pose, const double* __restrict__ point,
+                                                     const int32_t* __restrict__ pose_h, Huber2 hub,
+                                                     double* __restrict__ err, double* __restrict__ rho0_out,
+                                                     double* __restrict__ hpl, double* __restrict__ ecp,
+                                                     double* __restrict__ hll, double* __restrict__ bl,
+                                                     double* __restrict__ z, double* __restrict__ cb,
+                                                     const LmState* __restrict__ st) {
+    if (lm_skip(st, kGateTrial)) return;
+    static_assert(kT % kLB == 0, "landmark groups inside a block");
+    const bool build = st->phase == 0;
+    const double lambda = *lam;
+    const int g = (blockIdx.x * kT + threadIdx.x) / kLB, j = threadIdx.x % kLB;
+    const bool live = g < nl;
+    const int k0 = live ? land_off[g] : 0, k1 = live ? land_off[g + 1] : 0;
+    double H[12];  // Hll (9) and b_l (3)
+    LinOut lo;
+    lo.free = false;
+    if (build) {
+#pragma unroll
+        for (int i = 0; i < 12; ++i) H[i] = 0.0;
+        for (int k = k0 + j; k < k1; k += kLB) {
+            ba_edge<true, true>(land_edge[k], edges, cams, pose, point, pose_h, hub, err, rho0_out, nullptr, hpl, ecp,
+                                0, &lo);
+#pragma unroll
+            for (int i = 0; i < 12; ++i) H[i] += lo.pl[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {  // the group's sum, the same bits in its kLB lanes
+            H[i] += __shfl_xor(H[i], 1);
+            H[i] += __shfl_xor(H[i], 2);
+            H[i] += __shfl_xor(H[i], 4);
+        }
+        if (live && j == 0) {
+#pragma unroll
+            for (int i = 0; i < 9; ++i) hll[9 * (size_t)g + i] = H[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) bl[3 * (size_t)g + i] = H[9 + i];
+        }
+    } else if (live) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) H[i] = hll[9 * (size_t)g + i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) H[9 + i] = bl[3 * (size_t)g + i];
+    }
+    if (!live || k0 + j >= k1) return;
+    double D[9], Di[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) D[i] = H[i] + (i % 4 == 0 ? lambda : 0.0);
+    inverse3(D, Di);
+    double db[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) db[r] = Di[3 * r] * H[9] + Di[3 * r + 1] * H[10] + Di[3 * r + 2] * H[11];
+    for (int k = k0 + j; k < k1; k += kLB) {
+        const int e = land_edge[k];
+        double h[18];
+        bool fr;
+        if (build && k + kLB >= k1) {  // the lane's last edge: its Hpl is still in registers
+            fr = lo.free;
+#pragma unroll
+            for (int q = 0; q < 18; ++q) h[q] = lo.hx[q];
+        } else {  // (this lane wrote it, or an earlier build did)
+            fr = pose_h[edges[e].pose] >= 0;
+#pragma unroll
+            for (int q = 0; q < 18; ++q) h[q] = fr ? hpl[18 * (size_t)e + q] : 0.0;
+        }
+        if (!fr) continue;
+        double* Z = z + 18 * (size_t)e;
+        double* C = cb + 6 * (size_t)e;
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+            const double h0 = h[3 * r], h1 = h[3 * r + 1], h2 = h[3 * r + 2];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) Z[3 * r + c] = h0 * Di[c] + h1 * Di[3 + c] + h2 * Di[6 + c];
+            C[r] = h0 * db[0] + h1 * db[1] + h2 * db[2];
+        }
+    }
+}
+
+// Fast unit, step 4: the S blocks without Hpp + lambda I (the Cholesky adds them), b_S = b_p - sum cb per
+// free pose with b_p summed here from the pose parts (ba_reduce_pose's order for its b_p), and per free
+// pose Hpp and b_p (ba_reduce_pose) for the Cholesky and the trial.  Blocks: [0, nblk) S, then nf b_S,
+// then nf Hpp.
+__global__ __launch_bounds__(64) void k_u_schur2(int n, int nf, int nblk, const double* __restrict__ lam,
+                                                 const int32_t* __restrict__ blk_off, const EdgePair* __restrict__ pairs,
+                                                 const int32_t* __restrict__ cnt, const int32_t* __restrict__ pose_off,
+                                                 const LandEdge* __restrict__ pose_fl, const double* __restrict__ z,
+                                                 const double* __restrict__ hpl, const double* __restrict__ ecp,
+                                                 double* __restrict__ hpp, double* __restrict__ bp, double* __restrict__ S,
+                                                 const double* __restrict__ cb, double* __restrict__ bs,
+                                                 const LmState* __restrict__ st) {
+    if (lm_skip(st, kGateTrial)) return;
+    __shared__ double red[42][65];  // the branches' column sums share one buffer
+    const int b = blockIdx.x, lane = threadIdx.x;
+    if (b < nblk) {
+        ba_schur_block<true>(b, lane, n, nf, *lam, 0, blk_off, pairs, cnt, z, hpl, hpp, S, red);
+    } else if (b < nblk + nf) {
+        const int p = b - nblk;
+        double s[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // b_p part sums, then cb sums
+        const int k0 = pose_off[p] + lane, k1 = pose_off[p + 1];
+        for (int k = k0; k < k1; k += 64) {
+            const int e = pose_fl[k].e;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                s[i] += ecp[42 * (size_t)e + 36 + i];
+                s[6 + i] += cb[6 * (size_t)e + i];
+            }
+        }
+        const double t = wave_sum_cols_in<12>(s, lane, red);
+        __shared__ double bpv[6];
+        if (lane < 6) bpv[lane] = t;
+        __syncthreads();
+        if (lane >= 6 && lane < 12) bs[6 * (size_t)p + lane - 6] = bpv[lane - 6] - t;
+    } else if (b < nblk + 2 * nf) {
+        ba_reduce_pose<true>(b - nblk - nf, lane, pose_off, pose_fl, ecp, hpp, bp, red);
+    }
+}
+
 // unit steps 6 + 7 in one launch, landmark-major: thread l computes x_l (back-substitution), pushes
 // and moves landmark l, and evaluates the errors of the landmark's edges (all of them, in edge order)
 // at the new estimate, with the new point from registers.  A block is two waves: wave 0 takes kT
@@ -1995,7 +2165,8 @@ __global__ __launch_bounds__(kLT) void k_u_land_trial(int nl, int n, const doubl
                                                      double* __restrict__ part, double* __restrict__ part2,
                                                      unsigned* counter, const int32_t* __restrict__ status,
                                                      double* __restrict__ scal, LmState* st, LmProgress* prog, int dist,
-                                                     double* __restrict__ sc_part, const volatile int32_t* h_stop) {
+                                                     double* __restrict__ sc_part, const volatile int32_t* h_stop,
+                                                     int fast) {
     if (lm_skip(st, kGateTrial)) return;
     __shared__ double s_new[kT][7], s_base[kT][7], s_pc[kT];
     hpl += hpl_cur(st, hpl_alt);
@@ -2110,7 +2281,7 @@ __global__ __launch_bounds__(kLT) void k_u_land_trial(int nl, int n, const doubl
             scal[0] = chi;
             scal[1] = scale;
             scal[2] = failed ? 1.0 : 0.0;
-            lm_trial_done(st, chi, scale, failed, prog, false);
+            lm_trial_done(st, chi, scale, failed, prog, false, fast != 0);
         }
         *counter = 0;
     }
@@ -2744,7 +2915,8 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
     }
     // ORBGPU_BA_TRACE: the first Cholesky of the process records its phase stamps (dump_chol_trace)
     static int trace_left = getenv("ORBGPU_BA_TRACE") ? 1 : 0;
-    auto launch_chol = [&](const LmState* g, const PoseTail& pt) {
+    auto launch_chol = [&](const LmState* g, const PoseTail& pt, const double* hpp_add = nullptr,
+                           const double* lam_add = nullptr) {
         if (use_rows) {
             if (rows_lds)
                 hipLaunchKernelGGL(k_ba_chol_rows<true>, dim3(NT), dim3(kRowThreads), rows_lds_bytes, s, n, SS,
@@ -2763,7 +2935,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
             tr = h->trace.p;
         }
         hipLaunchKernelGGL((k_ba_chol_mf2<kMf2TileWaves>), dim3(1), dim3((kMf2TileWaves + 1) * 64), kMf2Lds, s, n,
-                           SS, BSV, h->x.p, h->status.p, tr, g, (int)kGateTrial);
+                           SS, BSV, h->x.p, h->status.p, tr, g, (int)kGateTrial, hpp_add, lam_add);
         if (tr) {
             trace_left = 0;
             dump_chol_trace(tr, n, s);
@@ -2899,7 +3071,42 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         double* const p_sct = dist ? p_sb + (size_t)n * n + n : nullptr;
         double* const r_sct = dist ? p_sct + 4 : nullptr;
         bool coll_ok = true;
+        // The fast unit (one process, the single-workgroup Cholesky, the fused trial): 4 launches per trial
+        // instead of 6 -- k_u_land_build (linearisation, Hll / b_l, Z and cb), k_u_schur2 (S without its
+        // diagonal Hpp + lambda I, b_S, Hpp / b_p), the Cholesky (adding Hpp + lambda I as it loads S),
+        // k_u_land_trial.  The solve's first build (lambda from max diag) runs once before the units,
+        // with the build controller.  ORBGPU_BA_FAST_UNIT=0: the 6-launch unit.
+        static const char* fu_env = getenv("ORBGPU_BA_FAST_UNIT");
+        const bool fast = fused && !dist && !use_rows && !(fu_env && !strcmp(fu_env, "0"));
+        auto launch_reduce_build = [&]() {
+            hipLaunchKernelGGL(k_u_reduce_build, dim3(nf + grid(nl, 64)), dim3(64), 0, s, nf, nl, h->pose_off.p,
+                               h->pose_fl.p, h->ecp.p, HPP, BV, h->land_off.p, h->land_edge.p, h->ecl.p, h->hll.p, bl,
+                               h->part.p, nparts, h->counters.p, h->scal.p, L, 0, (double*)nullptr, h->rank);
+        };
+        if (fast) {  // the solve's first build (gated to phase 0, i.e. before any unit has run)
+            launch_edges_build();
+            launch_reduce_build();
+        }
         auto unit_launches = [&]() {
+            if (fast) {
+                hipLaunchKernelGGL(k_u_land_build, dim3(grid((size_t)nl * kLB)), dim3(kT), 0, s, nl, lam, h->land_off.p,
+                                   h->land_edge.p, h->edges.p, h->cams.p, h->pose.p, h->point.p, h->pose_h.p, hub,
+                                   h->err.p, h->rho0.p, h->hpl.p, h->ecp.p, h->hll.p, bl, h->z.p, h->cb.p,
+                                   (const LmState*)L);
+                if (nf) {
+                    hipLaunchKernelGGL(k_u_schur2, dim3(nblk + 2 * nf), dim3(64), 0, s, n, nf, nblk, lam, h->blk_off.p,
+                                       h->pairs.p, h->blk_cnt.p, h->pose_off.p, h->pose_fl.p, h->z.p, h->hpl.p, h->ecp.p,
+                                       HPP, BV, SS, h->cb.p, BSV, (const LmState*)L);
+                    launch_chol((const LmState*)L, PoseTail{}, HPP, lam);
+                }
+                hipLaunchKernelGGL(k_u_land_trial, dim3(grid(nl)), dim3(kLT), 0, s, nl, n, lam, h->landf_off.p,
+                                   h->landf_edge.p, h->landf_row.p, h->hpl.p, hpl_alt, bl, h->hll.p, h->x.p,
+                                   h->land_point.p, h->point.p, h->point_bak.p, h->land_off.p, h->land_edge.p,
+                                   h->edges.p, h->cams.p, h->pose.p, h->pose_h.p, pt_unit, pose_mode, hub, h->err.p,
+                                   h->rho0.p, h->part.p, h->part.p + nparts, h->counters.p + 1, h->status.p, h->scal.p,
+                                   L, h->h_prog, 0, (double*)nullptr, (const volatile int32_t*)h->h_stop, 1);
+                return;
+            }
             if (!trial_lin) launch_edges_build();
             hipLaunchKernelGGL(k_u_reduce_build, dim3(nf + grid(nl, 64)), dim3(64), 0, s, nf, nl, h->pose_off.p,
                                h->pose_fl.p, h->ecp.p, dist ? p_hb : HPP, dist ? p_hb + 36 * (size_t)nf : BV,
@@ -2930,7 +3137,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                                    h->edges.p, h->cams.p, h->pose.p, h->pose_h.p, pt_unit, pose_mode, hub, h->err.p,
                                    h->rho0.p, h->part.p, h->part.p + nparts, h->counters.p + 1, h->status.p, h->scal.p,
                                    L, h->h_prog, dist ? 1 : 0, p_sct,
-                                   (const volatile int32_t*)h->h_stop);
+                                   (const volatile int32_t*)h->h_stop, 0);
             } else {
             hipLaunchKernelGGL(k_u_backsub_update, dim3(nparts2), dim3(kT), 0, s, nl, nf, n, lam, h->landf_off.p,
                                h->landf_edge.p, h->landf_row.p, h->hpl.p, hpl_alt, bl, h->hll.p, h->x.p, BV,
@@ -2973,7 +3180,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
                 (uintptr_t)h->blk_cnt.p, (uintptr_t)BSV,
                 (uintptr_t)h->x.p, (uintptr_t)h->status.p, (uintptr_t)h->landf_off.p, (uintptr_t)h->landf_row.p, (uintptr_t)h->free_pose.p,
                 (uintptr_t)h->land_point.p, (uintptr_t)h->pose_bak.p, (uintptr_t)h->point_bak.p, (uintptr_t)h->h_prog,
-                (uintptr_t)use_rows, (uintptr_t)trial_lin, (uintptr_t)fused, (uintptr_t)h->lpub.p, (uintptr_t)h->ypub.p, (uintptr_t)h->cflag.p,
+                (uintptr_t)use_rows, (uintptr_t)trial_lin, (uintptr_t)fused, (uintptr_t)fast, (uintptr_t)h->lpub.p, (uintptr_t)h->ypub.p, (uintptr_t)h->cflag.p,
                 (uintptr_t)h->racc.p};
             if (!h->unit_exec || key != h->unit_key) {
                 if (h->unit_exec) { hipGraphExecDestroy(h->unit_exec); h->unit_exec = nullptr; }

@@ -86,10 +86,13 @@ def test_sharded_local_ba_matches_oracle(oracle, synth, world, stereo_frac, seed
 
 def _rccl_one_rank_worker(port, kw, q):
     """One rank with an RCCL communicator forced onto the sharded path (ORBGPU_BA_DIST_FORCE=1): the
-    device LM loop with its all-reduces as real RCCL calls, next to a plain single-GPU handle."""
+    device LM loop with its all-reduces as real RCCL calls, next to a plain single-GPU handle running the
+    6-launch unit the sharded loop shares its arithmetic with (ORBGPU_BA_FAST_UNIT=0; the default fast
+    unit sums in another order and is checked against the oracle by tests/test_ba_gpu.py)."""
     import torch
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ORBGPU_BA_DIST_FORCE="1")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ORBGPU_BA_DIST_FORCE="1",
+                      ORBGPU_BA_FAST_UNIT="0")
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1)
     try:

@@ -6,8 +6,9 @@ import re
 import statistics
 import sys
 
-UNIT = ("k_u_edges_build", "k_u_reduce_build", "k_ba_schur_edges", "k_u_schur", "k_ba_chol_mf2",
-        "k_u_pose_update", "k_u_backsub_update", "k_u_edges_trial", "k_u_land_trial")
+UNIT = ("k_u_land_build", "k_u_schur2", "k_u_edges_build", "k_u_reduce_build", "k_ba_schur_edges", "k_u_schur",
+        "k_ba_chol_mf2", "k_u_pose_update", "k_u_backsub_update", "k_u_edges_trial", "k_u_land_trial")
+START = ("k_u_edges_build", "k_u_land_build")  # the first launch of a unit (6-launch / fast unit)
 
 
 def short(name):
@@ -23,7 +24,7 @@ live = False
 for i, (k, s, e) in enumerate(ev):
     if k not in UNIT:
         continue
-    if k == "k_u_edges_build":  # a unit starts: live if its Cholesky (next mf2 launch) ran
+    if k in START:  # a unit starts: live if its Cholesky (next mf2 launch) ran
         nxt = next((x for x in ev[i:] if x[0] == "k_ba_chol_mf2"), None)
         live = nxt is not None and nxt[2] - nxt[1] > 3000
         if i and ev[i - 1][0] in UNIT and live:
