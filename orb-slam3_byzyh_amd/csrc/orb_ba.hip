@@ -3161,11 +3161,15 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         auto dbits = [](double v) { uintptr_t u; memcpy(&u, &v, sizeof(u)); return u; };
         bool use_graph = !trace_left && !dist;  // (the trace dump synchronises the stream: not capturable;
                                                 // sharded, the collectives stay direct calls)
-        // two units per graph launch: each launch boundary costs ~13 us on the device, a gated no-op
-        // unit behind the last trial less (C5 solve 1.89 -> 1.87 ms against one unit; three: 1.89)
+        // four units per graph launch: each launch boundary costs ~13 us on the device, a gated no-op
+        // unit behind the last trial about as much (round 6, the 4-launch fast unit, C5 mono solve:
+        // 2 units 1.410 / 1.436 ms, 3: 1.397 / 1.377, 4: 1.368 / 1.381, 8: 1.356 / 1.360; 4 keeps the
+        // waste of a 9-12-trial solve small, profiles/r06/ba_units_ab_r06.txt)
         // With a stop flag, one unit per launch: the host polls the flag after every launch, so at
         // most two trials (the running and the queued unit) follow a raised flag, as before.
-        const int units_per_launch = (opt->stop_flag || opt->stop_flag_bool) ? 1 : 2;
+        static const char* upl_env = getenv("ORBGPU_BA_UNITS");  // (A/B of the units per graph launch)
+        const int upl_default = upl_env ? std::max(1, std::min(16, atoi(upl_env))) : 4;
+        const int units_per_launch = (opt->stop_flag || opt->stop_flag_bool) ? 1 : upl_default;
         if (use_graph) {
             const std::vector<uintptr_t> key = {
                 (uintptr_t)s, (uintptr_t)n, (uintptr_t)m, (uintptr_t)ne, (uintptr_t)nf, (uintptr_t)nl, (uintptr_t)nfe,
