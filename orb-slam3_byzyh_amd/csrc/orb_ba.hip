@@ -700,11 +700,14 @@ __device__ __forceinline__ void mf_wave_sync() {
 }
 
 // 1/sqrt(x): v_rsq_f64 and two Newton steps (about 1 ulp; the factor need not be correctly rounded)
+#ifndef ORB_BA_RSQ_NEWTON
+#define ORB_BA_RSQ_NEWTON 2
+#endif
 __device__ __forceinline__ double rsqrt_nr(double x) {
     double y = __builtin_amdgcn_rsq(x);
     const double h = 0.5 * x;
-    y = y * __builtin_fma(-h, y * y, 1.5);
-    y = y * __builtin_fma(-h, y * y, 1.5);
+#pragma unroll
+    for (int i = 0; i < ORB_BA_RSQ_NEWTON; ++i) y = y * __builtin_fma(-h, y * y, 1.5);
     return y;
 }
 
