@@ -2,7 +2,11 @@
   * ORBGPU_BA_CHOL=rows: the tile-row multi-workgroup Cholesky (k_ba_chol_rows), which windows above
     48 free keyframes use, here at n = 288;
   * ORBGPU_BA_HOST_LM=1: the host-driven LM loop the sharded (multi-GPU) solve uses, on one process;
-  * both together.
+  * both together;
+  * ORBGPU_BA_FAST_UNIT=0: the 6-launch LM unit (the sharded solve's) on one process;
+  * ORBGPU_BA_FUSED_TRIAL=0: the round-5 back-substitution + error launches (k_u_backsub_update +
+    k_u_edges_trial) instead of k_u_land_trial;
+  * ORBGPU_BA_UNITS=1 / 8: one and eight LM trials per graph launch.
 The switches are read once per process, so each variant solves in a child process (tools/ba_dump.py:
 the C5 problem, mono and 50 % stereo) and the saved results are compared here."""
 import os
@@ -19,7 +23,8 @@ ROOT = pathlib.Path(__file__).resolve().parents[1]
 def _solve(tmp_path, name, env_extra):
     out = tmp_path / f"{name}.npz"
     env = dict(os.environ)
-    for k in ("ORBGPU_BA_CHOL", "ORBGPU_BA_HOST_LM", "ORBGPU_BA_TRACE"):
+    for k in ("ORBGPU_BA_CHOL", "ORBGPU_BA_HOST_LM", "ORBGPU_BA_TRACE", "ORBGPU_BA_FAST_UNIT", "ORBGPU_BA_FUSED_TRIAL",
+              "ORBGPU_BA_UNITS"):
         env.pop(k, None)
     env.update(env_extra)
     subprocess.run([sys.executable, str(ROOT / "tools" / "ba_dump.py"), str(out)], env=env, check=True,
@@ -33,7 +38,10 @@ def _rmse(a, b):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,env", [("rows", {"ORBGPU_BA_CHOL": "rows"}), ("host_lm", {"ORBGPU_BA_HOST_LM": "1"}),
-                                      ("rows_host_lm", {"ORBGPU_BA_CHOL": "rows", "ORBGPU_BA_HOST_LM": "1"})])
+                                      ("rows_host_lm", {"ORBGPU_BA_CHOL": "rows", "ORBGPU_BA_HOST_LM": "1"}),
+                                      ("unit6", {"ORBGPU_BA_FAST_UNIT": "0"}),
+                                      ("unfused", {"ORBGPU_BA_FUSED_TRIAL": "0"}),
+                                      ("units1", {"ORBGPU_BA_UNITS": "1"}), ("units8", {"ORBGPU_BA_UNITS": "8"})])
 def test_ba_variant_against_oracle(tmp_path, oracle, synth, name, env):
     got = _solve(tmp_path, name, env)
     for st in (0.0, 0.5):
