@@ -284,7 +284,7 @@ __global__ __launch_bounds__(kT) void k_ba_edges(int ne, const EdgeDev* __restri
 }
 
 // Hll and b_l per landmark: sum of its edges in edge order (g2o accumulates in edge id order)
-__device__ __forceinline__ void ba_reduce_land(int l, const int32_t* __restrict__ off, const int32_t* __restrict__ eidx,
+__device__ __forceinline__ double ba_reduce_land(int l, const int32_t* __restrict__ off, const int32_t* __restrict__ eidx,
                                                const double* __restrict__ ecl, double* __restrict__ hll,
                                                double* __restrict__ bl) {
     double s[12] = {0};
@@ -310,6 +310,7 @@ __device__ __forceinline__ void ba_reduce_land(int l, const int32_t* __restrict_
     }
     for (int i = 0; i < 9; ++i) hll[9 * (size_t)l + i] = s[i];
     for (int i = 0; i < 3; ++i) bl[3 * (size_t)l + i] = s[9 + i];
+    return fmax(fmax(fabs(s[0]), fabs(s[4])), fabs(s[8]));  // computeLambdaInit's part of this landmark
 }
 
 __global__ __launch_bounds__(kT) void k_ba_reduce_land(int nl, const int32_t* __restrict__ off,
@@ -318,7 +319,7 @@ __global__ __launch_bounds__(kT) void k_ba_reduce_land(int nl, const int32_t* __
                                                        const LmState* __restrict__ lm_st, int lm_gk) {
     if (lm_skip(lm_st, lm_gk)) return;
     const int l = blockIdx.x * kT + threadIdx.x;
-    if (l < nl) ba_reduce_land(l, off, eidx, ecl, hll, bl);
+    if (l < nl) (void)ba_reduce_land(l, off, eidx, ecl, hll, bl);
 }
 
 // Sum of 64 lanes' partials of NC values, lane c < NC adding value c's partials in lane order
@@ -349,7 +350,7 @@ __device__ __forceinline__ double wave_sum_cols_x(const double (&v)[NC], int lan
 // indices of up to 8 edges per lane are loaded first, then two edges' 42 values at a time, so the
 // usual pose (a few hundred edges) takes three rounds of loads instead of two per edge.
 template <bool kExt = false>
-__device__ __forceinline__ void ba_reduce_pose(int p, int lane, const int32_t* __restrict__ off,
+__device__ __forceinline__ double ba_reduce_pose(int p, int lane, const int32_t* __restrict__ off,
                                                const LandEdge* __restrict__ eidx, const double* __restrict__ ecp,
                                                double* __restrict__ hpp, double* __restrict__ bp, double (*red)[65] = nullptr) {
     double s[42];
@@ -383,6 +384,7 @@ __device__ __forceinline__ void ba_reduce_pose(int p, int lane, const int32_t* _
     const double t = wave_sum_cols_x<42, kExt>(s, lane, red);
     if (lane < 36) hpp[36 * (size_t)p + lane] = t;
     else if (lane < 42) bp[6 * (size_t)p + lane - 36] = t;
+    return t;  // value `lane`'s total (lanes < 42)
 }
 
 __global__ __launch_bounds__(64) void k_ba_reduce_pose(const int32_t* __restrict__ off, const LandEdge* __restrict__ eidx,
@@ -1806,50 +1808,38 @@ __global__ __launch_bounds__(64) void k_u_reduce_build(int nf, int nl, const int
                                                        const double* __restrict__ ecl, double* __restrict__ hll,
                                                        double* __restrict__ bl, const double* __restrict__ part,
                                                        int nparts, unsigned* counter, double* __restrict__ scal,
-                                                       LmState* st, int dist, double* __restrict__ sc_part, int rank) {
+                                                       LmState* st, int dist, double* __restrict__ sc_part, int rank,
+                                                       double* __restrict__ pmax) {
     if (lm_skip(st, kGateBuild)) return;
     const int b = blockIdx.x, lane = threadIdx.x;
+    // computeLambdaInit (iteration 0): each block's max |diag| of what it reduced, to pmax[block], so
+    // the last block takes one max over the blocks instead of a pass over every Hpp / Hll (sharded:
+    // the poses' part comes from the reduced Hpp, k_lm_build_ctl)
+    double m = 0.0;
     if (b < nf) {
-        ba_reduce_pose(b, lane, pose_off, pose_edge, ecp, hpp, bp);
+        const double t = ba_reduce_pose(b, lane, pose_off, pose_edge, ecp, hpp, bp);
+        if (!dist && lane < 36 && lane % 7 == 0) m = fabs(t);
     } else {
         const int l = (b - nf) * 64 + lane;
-        if (l < nl) ba_reduce_land(l, land_off, land_edge, ecl, hll, bl);
+        if (l < nl) m = ba_reduce_land(l, land_off, land_edge, ecl, hll, bl);
+    }
+    const bool first = st->it == 0;
+    if (first) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o));
+        if (lane == 0) pmax[b] = m;
     }
     if (!last_block(counter)) return;
     double c = 0.0;
     for (int i = lane; i < nparts; i += 64) c += part[i];
     const double chi = block_sum<64>(c);
     double md = 0.0;
-    if (st->it == 0) {
-        double m = 0;  // (max is order-independent: loads batched 8 per lane)
-        for (int i0 = lane; !dist && i0 < 6 * nf; i0 += 8 * 64) {  // (sharded: from the reduced Hpp later)
-            double v[8];
+    if (first) {  // (max is order-independent)
+        double mm = 0.0;
+        for (int i = lane; i < (int)gridDim.x; i += 64) mm = fmax(mm, pmax[i]);
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int i = min(i0 + 64 * u, 6 * nf - 1);
-                v[u] = fabs(hpp[36 * (size_t)(i / 6) + 7 * (i % 6)]);
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) m = fmax(m, v[u]);
-        }
-        for (int i0 = lane; i0 < 3 * nl; i0 += 8 * 64) {
-            double v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int i = min(i0 + 64 * u, 3 * nl - 1);
-                v[u] = fabs(hll[9 * (size_t)(i / 3) + 4 * (i % 3)]);
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) m = fmax(m, v[u]);
-        }
-        __shared__ double mx[64];
-        mx[lane] = m;
-        __syncthreads();
-        for (int w = 32; w >= 1; w >>= 1) {
-            if (lane < w) mx[lane] = fmax(mx[lane], mx[lane + w]);
-            __syncthreads();
-        }
-        md = mx[0];
+        for (int o = 32; o >= 1; o >>= 1) mm = fmax(mm, __shfl_xor(mm, o));
+        md = mm;
     }
     if (lane == 0) {
         if (dist) {
@@ -2134,7 +2124,7 @@ __global__ __launch_bounds__(64) void k_u_schur2(int n, int nf, int nblk, const 
         __syncthreads();
         if (lane >= 6 && lane < 12) bs[6 * (size_t)p + lane - 6] = bpv[lane - 6] - t;
     } else if (b < nblk + 2 * nf) {
-        ba_reduce_pose<true>(b - nblk - nf, lane, pose_off, pose_fl, ecp, hpp, bp, red);
+        (void)ba_reduce_pose<true>(b - nblk - nf, lane, pose_off, pose_fl, ecp, hpp, bp, red);
     }
 }
 
@@ -2854,7 +2844,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
               h->err.grow(3 * ne1) && h->rho0.grow(ne1) && h->ecl.grow(12 * ne1) && h->hpl.grow(36 * ne1) &&
               h->ecp.grow(42 * ne1) && h->hpp.grow(36 * (size_t)nf + n + m) && h->hll.grow(9 * (size_t)nl) &&
               h->z.grow(18 * ne1) && h->cb.grow(6 * ne1) && h->S.grow((size_t)n * n + n) &&
-              h->depth.grow(ne1) && h->part.grow(grid(ne) + grid(nl + nf)) &&
+              h->depth.grow(ne1) && h->part.grow(grid(ne) + grid(nl + nf) + nf + grid(nl, 64)) &&
               // cleared by the scatter launch: g2o's _x starts zeroed, the scalars, the factorisation
               // status, the last-block counters of the unit kernels; and the device LM state's start
               st.zero(h->x, n + m) && st.zero(h->scal, 8) && st.zero(h->status, 1) && st.zero(h->counters, 2) &&
@@ -3036,6 +3026,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
             if (agree_fail(!okp)) return orbgpu_fail(ORB_ERR_DEVICE, "BA sharded buffers");
         }
         const int nparts = (int)grid(ne), nparts2 = (int)grid(nl + nf);  // partials: edge blocks, vertex blocks
+        double* const pmax = h->part.p + nparts + nparts2;  // k_u_reduce_build's per-block max |diag|
         LmState* L = h->lm.p;
         // one unit = 6 launches: reductions (+ chi2, max diag, build controller), Schur edges, Schur
         // blocks + rhs, Cholesky + solves, back-substitution + update, errors and linearisation at the
@@ -3084,7 +3075,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
         auto launch_reduce_build = [&]() {
             hipLaunchKernelGGL(k_u_reduce_build, dim3(nf + grid(nl, 64)), dim3(64), 0, s, nf, nl, h->pose_off.p,
                                h->pose_fl.p, h->ecp.p, HPP, BV, h->land_off.p, h->land_edge.p, h->ecl.p, h->hll.p, bl,
-                               h->part.p, nparts, h->counters.p, h->scal.p, L, 0, (double*)nullptr, h->rank);
+                               h->part.p, nparts, h->counters.p, h->scal.p, L, 0, (double*)nullptr, h->rank, pmax);
         };
         if (fast) {  // the solve's first build (gated to phase 0, i.e. before any unit has run)
             launch_edges_build();
@@ -3114,7 +3105,7 @@ int orb_ba_optimize(orb_ba_t h, orb_ba_problem_t* pr, const orb_ba_options_t* op
             hipLaunchKernelGGL(k_u_reduce_build, dim3(nf + grid(nl, 64)), dim3(64), 0, s, nf, nl, h->pose_off.p,
                                h->pose_fl.p, h->ecp.p, dist ? p_hb : HPP, dist ? p_hb + 36 * (size_t)nf : BV,
                                h->land_off.p, h->land_edge.p, h->ecl.p, h->hll.p, bl, h->part.p, nparts, h->counters.p,
-                               h->scal.p, L, dist ? 1 : 0, p_scb, h->rank);
+                               h->scal.p, L, dist ? 1 : 0, p_scb, h->rank, pmax);
             if (dist) {  // one collective for [Hpp | b_p | build scalars], then the sums into place
                 coll_ok = coll_ok && dev_reduce2(h, p_hb, r_hb, nhb + nsb, ORB_BA_SUM) &&
                           hipMemcpyAsync(HPP, r_hb, nhb * sizeof(double), hipMemcpyDeviceToDevice, s) == hipSuccess;
