@@ -975,11 +975,14 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
     // block gains Hpp + lambda I here, in the value k_ba_schur_block would have stored there (its mirror
     // store, lane (col % 6, row % 6), is the one that lands): (0 - sum) + (Hpp + lambda) = (Hpp + lambda) - sum
     const double lam_d = hpp_add ? *lam_add : 0.0;
+    // (the Hpp load is unconditional, from an in-range index, and the sum a select: the loads of a tile
+    // stay one batch; a conditional load had cost ~8k cycles before the first step)
     auto s_at = [&](int row, int col) {
-        double v = S[(size_t)row * n + col];
-        if (hpp_add && row / 6 == col / 6)
-            v += hpp_add[36 * (size_t)(row / 6) + 6 * (col % 6) + row % 6] + (row == col ? lam_d : 0.0);
-        return v;
+        const double v = S[(size_t)row * n + col];
+        if (!hpp_add) return v;
+        const bool dg = row / 6 == col / 6;
+        const double h = hpp_add[36 * (size_t)(row / 6) + (dg ? 6 * (col % 6) : 0) + row % 6];
+        return dg ? v + (h + (row == col ? lam_d : 0.0)) : v;
     };
     static_assert(SL <= 32, "slot dispatch covers 32 slots");
     extern __shared__ double lds[];
