@@ -1506,6 +1506,9 @@ __device__ __forceinline__ void ba_backsub(int l, int n, double lambda, const in
                                            const double* __restrict__ hll, double* __restrict__ x, double xl[3]) {
     double cl[3] = {bl[3 * (size_t)l], bl[3 * (size_t)l + 1], bl[3 * (size_t)l + 2]};
     const int k0 = off[l], k1 = off[l + 1];
+    // Dinv first: its loads and the 3x3 inverse overlap the rounds of the loop below
+    double Di[9];
+    land_dinv(hll, l, lambda, Di);
     for (int kb = k0; kb < k1; kb += 8) {
         int e[8], ph[8];
 #pragma unroll
@@ -1534,8 +1537,6 @@ __device__ __forceinline__ void ba_backsub(int l, int n, double lambda, const in
                         for (int r = 0; r < 6; ++r) cl[c] += H[u][3 * r + c] * -xp[u][r];
         }
     }
-    double Di[9];
-    land_dinv(hll, l, lambda, Di);
     for (int r = 0; r < 3; ++r) {
         xl[r] = Di[3 * r] * cl[0] + Di[3 * r + 1] * cl[1] + Di[3 * r + 2] * cl[2];
         x[n + 3 * (size_t)l + r] = xl[r];
@@ -2206,15 +2207,17 @@ __global__ __launch_bounds__(kLT) void k_u_land_trial(int nl, int n, const doubl
     double c = 0.0, r = 0.0;
     double Xn[3] = {0.0, 0.0, 0.0};
     if (l < nl) {
+        // the landmark's base estimate is requested before the back-substitution (independent of it)
+        double* X = point + 3 * (size_t)land_point[l];
+        double* Xb = point_bak + 3 * (size_t)land_point[l];
+        double v[3];
+        for (int i = 0; i < 3; ++i) v[i] = rej ? Xb[i] : X[i];
         double xl[3];
         ba_backsub(l, n, lambda, landf_off, landf_edge, landf_row, hpl, bl, hll, x, xl);
         for (int i = 0; i < 3; ++i) c += xl[i] * (lambda * xl[i] + bl[3 * (size_t)l + i]);
-        double* X = point + 3 * (size_t)land_point[l];
-        double* Xb = point_bak + 3 * (size_t)land_point[l];
         for (int i = 0; i < 3; ++i) {
-            const double v = rej ? Xb[i] : X[i];
-            Xb[i] = v;
-            Xn[i] = v + xl[i];
+            Xb[i] = v[i];
+            Xn[i] = v[i] + xl[i];
             X[i] = Xn[i];
         }
     }

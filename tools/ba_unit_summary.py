@@ -1,6 +1,6 @@
 """Median duration of each LocalBA unit kernel over its live launches, from a rocprofv3 kernel trace
 (csv).  A launch is live when the Cholesky of its unit ran (the gated no-op units after a solve's end
-return at once: their Cholesky takes a few microseconds); the graph boundary gap is reported too."""
+return at once: their Cholesky takes a few microseconds, a live one ~100); the graph boundary gap is reported too."""
 import csv
 import re
 import statistics
@@ -26,7 +26,7 @@ for i, (k, s, e) in enumerate(ev):
         continue
     if k in START:  # a unit starts: live if its Cholesky (next mf2 launch) ran
         nxt = next((x for x in ev[i:] if x[0] == "k_ba_chol_mf2"), None)
-        live = nxt is not None and nxt[2] - nxt[1] > 3000
+        live = nxt is not None and nxt[2] - nxt[1] > 30000  # a gated-off Cholesky launch is a few us
         if i and ev[i - 1][0] in UNIT and live:
             gaps.append((s - ev[i - 1][2]) / 1e3)
     if live:
