@@ -975,11 +975,13 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
     // block gains Hpp + lambda I here, in the value k_ba_schur_block would have stored there (its mirror
     // store, lane (col % 6, row % 6), is the one that lands): (0 - sum) + (Hpp + lambda) = (Hpp + lambda) - sum
     const double lam_d = hpp_add ? *lam_add : 0.0;
-    // (the Hpp load is unconditional, from an in-range index, and the sum a select: the loads of a tile
-    // stay one batch; a conditional load had cost ~8k cycles before the first step)
-    auto s_at = [&](int row, int col) {
+    // Only tiles (i, j) with i - j <= 1 hold diagonal 6x6 blocks (6 < 16), so only they read Hpp (a
+    // wave-uniform choice per tile): S streams into the one CU at ~64 B per clock, and an Hpp load beside
+    // every S element had doubled the load instructions before the first step (+8k cycles).  Within such
+    // a tile the Hpp load is unconditional (an in-range index) and the sum a select.
+    auto s_at = [&](int row, int col, bool near) {
         const double v = S[(size_t)row * n + col];
-        if (!hpp_add) return v;
+        if (!hpp_add || !near) return v;
         const bool dg = row / 6 == col / 6;
         const double h = hpp_add[36 * (size_t)(row / 6) + (dg ? 6 * (col % 6) : 0) + row % 6];
         return dg ? v + (h + (row == col ? lam_d : 0.0)) : v;
@@ -1020,7 +1022,7 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
         __builtin_amdgcn_s_setprio(3);
         for (int t = lane; t < 256; t += 64) {
             const int r = t >> 4, c = t & 15;
-            dk[r * 17 + c] = (r < n && c < n) ? s_at(r, c) : (r == c ? 1.0 : 0.0);
+            dk[r * 17 + c] = (r < n && c < n) ? s_at(r, c, true) : (r == c ? 1.0 : 0.0);
         }
         mf_wave_sync();
         mf_diag<true>(dk, linv, yv, lane, &fail);
@@ -1107,10 +1109,11 @@ __global__ __launch_bounds__((W + 1) * 64) void k_ba_chol_mf2(int n, const doubl
                 const int j = NT - 1 - c, i = j + (t - c * (c + 1) / 2);
                 tij[s] = i | (j << 8);
                 double e[4];
+                const bool near = i - j <= 1;  // (wave-uniform: the slot's tile)
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {  // S symmetric: read as S[col block][row block], coalesced
                     const int row = 16 * j + g4 + 4 * q, col = 16 * i + r16;
-                    const double v = s_at(min(row, n - 1), min(col, n - 1));
+                    const double v = s_at(min(row, n - 1), min(col, n - 1), near);
                     e[q] = (row < n && col < n) ? v : (row == col ? 1.0 : 0.0);
                 }
                 T[s] = f64x4{e[0], e[1], e[2], e[3]};
