@@ -7,7 +7,7 @@ import statistics
 import sys
 
 UNIT = ("k_u_land_build", "k_u_schur2", "k_u_edges_build", "k_u_reduce_build", "k_ba_schur_edges", "k_u_schur",
-        "k_ba_chol_mf2", "k_u_pose_update", "k_u_backsub_update", "k_u_edges_trial", "k_u_land_trial")
+        "k_ba_chol_mf2", "k_u_pose_update", "k_u_backsub_update", "k_u_edges_trial", "k_u_land_trial", "k_u_land_trial8")
 START = ("k_u_edges_build", "k_u_land_build")  # the first launch of a unit (6-launch / fast unit)
 
 
